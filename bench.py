@@ -1,0 +1,286 @@
+#!/usr/bin/env python3
+"""Headline benchmark: differentiable 3DGS rasterizer fwd+bwd on MI355X.
+
+BASELINE.json metric: "Mpixels/s fwd+bwd and train iters/s, 1M Gaussians @ 1080^2".
+
+A step = one view per GPU: project -> SH (deg 3) -> bin/sort -> rasterize forward ->
+loss -> backward through rasterize / SH / project, plus (N > 1) the RCCL all-reduce of the
+flat Gaussian-gradient bucket -- the multi-view exchange of the data-parallel train step
+(SURVEY.md §8e).  `value` = all ranks' rendered pixels / max-over-ranks step time.  The
+full train step (splatfacto 0.8 L1 + 0.2 SSIM loss + Adam) is timed separately and
+reported as `train_iters_per_s`.  Inputs are synthetic (SURVEY.md §8d scene: random
+Gaussians in [-1.5,1.5]^3 seen from (0,0,4), fov 50 deg) and resident in HBM before timing.
+
+Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--config headline|c2|c3|c5]
+(N > 1 under torch.distributed.run, one process per GPU, backend nccl = RCCL.)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from gaussctrl_exp_amd import timing  # noqa: E402
+from gaussctrl_exp_amd.camera import gc_camera, look_at_c2w  # noqa: E402
+from gaussctrl_exp_amd.rasterize import bin_gaussians  # noqa: E402
+from gaussctrl_exp_amd.scene import render, synthetic_scene  # noqa: E402
+from gaussctrl_exp_amd.sh import num_sh_bases  # noqa: E402
+from gaussctrl_exp_amd.train import TrainStep  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
+
+CONFIGS = {
+    # name: (N, W, H, sh_degree, scale_lo, scale_hi, seed, description)
+    "headline": (1_000_000, 1080, 1080, 3, 0.005, 0.02, 10,
+                 "1M synthetic Gaussians @ 1080x1080, SH deg 3, fwd+bwd"),
+    "c2": (100_000, 512, 512, 0, 0.005, 0.03, 2,
+           "100k synthetic Gaussians @ 512x512, SH deg 0, fwd+bwd"),
+    "c3": (300_000, 512, 512, 3, 0.004, 0.02, 3,
+           "300k synthetic Gaussians @ 512x512, SH deg 3, fwd+bwd"),
+    "c5": (5_000_000, 2048, 2048, 3, 0.01, 0.016, 5,
+           "5M synthetic Gaussians @ 2048x2048, SH deg 3, heavy overlap, fwd+bwd"),
+}
+
+
+def view_camera(W, H, view: int):
+    """Camera `view` of an orbit at radius 4 around the origin (view 0 = (0,0,4))."""
+    ang = 2 * math.pi * view / 8.0
+    eye = (4.0 * math.sin(ang), 0.3 * math.sin(3 * ang), 4.0 * math.cos(ang))
+    fx = 0.5 * W / math.tan(math.radians(25.0))
+    return gc_camera(look_at_c2w(eye, up=(0.0, 1.0, 0.0)), fx, fx, W / 2.0, H / 2.0, W, H)
+
+
+def algorithmic_bytes(N, I, P, T, K, nvis):
+    """Per-view algorithmic HBM bytes of each C-ABI entry point (SURVEY.md §8d model)."""
+    return {
+        "gsplat_project_gaussians_forward": 96 * N,
+        "gsplat_compute_sh_forward": (24 + 12 * K) * N,
+        "gsplat_bin_count": 8 * N,
+        "gsplat_bin_emit": 20 * N + 44 * I + 8 * T,
+        "gsplat_rasterize_forward": 40 * I + 20 * P,
+        "gsplat_rasterize_backward": 40 * I + 24 * P + 36 * N,
+        "gsplat_compute_sh_backward": (24 + 12 * K) * N,
+        "gsplat_project_gaussians_backward": 180 * N,
+    }
+
+
+def cpu_baseline(scene, cam, sh_degree, budget_tiles=64, seed=0):
+    """C oracle (single-threaded restatement of gsplat) on a bounded sample: the full
+    per-Gaussian stages (project, SH, map+stable sort+bins) plus rasterize fwd+bwd on
+    `budget_tiles` random tiles, extrapolated to all tiles."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    O.build()
+    rng = np.random.default_rng(seed)
+    sc = scene.to("cpu")
+    means = sc.means.numpy()
+    scales = torch.exp(sc.scales).numpy()
+    quats = (sc.quats / sc.quats.norm(dim=-1, keepdim=True)).numpy()
+    opac = torch.sigmoid(sc.opacities).numpy()
+    coeffs = torch.cat([sc.features_dc[:, None], sc.features_rest], 1).numpy()
+    H, W = cam.height, cam.width
+    t0 = time.perf_counter()
+    xys, depths, radii, conics, nth, cov3d = O.project_forward(
+        means, scales, 1.0, quats, cam.viewmat.numpy(), cam.projmat.numpy(), cam.fx, cam.fy,
+        cam.cx, cam.cy, H, W, cam.tile_bounds)
+    dirs = means - cam.c2w[:3, 3].numpy()
+    dirs = dirs / np.linalg.norm(dirs, axis=1, keepdims=True)
+    colors = np.maximum(O.sh_forward(sh_degree, dirs, coeffs) + 0.5, 0.0).astype(np.float32)
+    b = O.bin_and_sort(xys, depths, radii, nth, cam.tile_bounds)
+    t_gauss_fwd = time.perf_counter() - t0
+    T = cam.tile_bounds[0] * cam.tile_bounds[1]
+    tiles = rng.choice(T, size=min(budget_tiles, T), replace=False).astype(np.int32)
+    bg = np.zeros(3, np.float32)
+    t0 = time.perf_counter()
+    img, fT, fi = O.rasterize_forward(cam.tile_bounds, H, W, b["gaussian_ids_sorted"],
+                                      b["tile_bins"], xys, conics, colors, opac, bg,
+                                      tile_list=tiles)
+    v_img = np.ones((H, W, 3), np.float32)
+    v_a = np.zeros((H, W), np.float32)
+    gr = O.rasterize_backward(cam.tile_bounds, H, W, b["gaussian_ids_sorted"], b["tile_bins"],
+                              xys, conics, colors, opac, bg, fT, fi, v_img, v_a,
+                              tile_list=tiles)
+    t_tiles = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    vc = O.sh_backward(sh_degree, dirs, gr[2], coeffs.shape[1])
+    O.project_backward(means, scales, 1.0, quats, cam.viewmat.numpy(), cam.projmat.numpy(),
+                       cam.fx, cam.fy, cam.cx, cam.cy, H, W, cov3d, radii, conics, gr[0],
+                       np.zeros_like(depths), gr[1])
+    t_gauss_bwd = time.perf_counter() - t0
+    total = t_gauss_fwd + t_gauss_bwd + t_tiles * T / len(tiles)
+    return {
+        "value": round(H * W / total / 1e6, 4),
+        "unit": "Mpixels/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": (f"C oracle, 1 thread: full project+SH+bin/sort+SH-bwd+project-bwd over "
+                   f"{means.shape[0]} Gaussians ({t_gauss_fwd + t_gauss_bwd:.2f}s) + rasterize "
+                   f"fwd+bwd on {len(tiles)} of {T} random tiles ({t_tiles:.2f}s) "
+                   f"extrapolated x{T / len(tiles):.1f}; est {total:.1f}s per view; "
+                   f"host cpu_count={os.cpu_count()}"),
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="headline", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--train-steps", type=int, default=None)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    N, W, H, deg, lo, hi, seed, desc = CONFIGS[args.config]
+    K = num_sh_bases(deg)
+    scene = synthetic_scene(N, deg, seed=seed, scale_lo=lo, scale_hi=hi, device=dev)
+    cam = view_camera(W, H, rank).to(dev)
+    g = torch.Generator().manual_seed(1000 + rank)
+    gt = torch.rand(H, W, 3, generator=g).to(dev)
+    bg = torch.zeros(3, device=dev)
+    trainer = TrainStep(scene, sh_degree=deg, world_size=world, loss="l1")
+
+    def step():
+        trainer.bucket.zero_()
+        trainer.forward_backward(cam, gt, bg)
+        if world > 1:
+            trainer.bucket.all_reduce_()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    ms_per_step = dt / args.steps * 1e3
+    value = world * H * W * args.steps / dt / 1e6
+
+    # per-entry-point device time (HIP events on the launch stream), same step, K steps
+    with timing.timed_calls() as tm:
+        for _ in range(args.steps):
+            step()
+        per_call = tm.summary()
+    with torch.no_grad():
+        from gaussctrl_exp_amd.project_gaussians import project_gaussians
+        xys, depths, radii, conics, nth, _ = project_gaussians(
+            scene.means, torch.exp(scene.scales), 1,
+            scene.quats / scene.quats.norm(dim=-1, keepdim=True), *cam.project_args())
+        I, _, _ = bin_gaussians(xys, depths, radii, nth, H, W)
+        nvis = int((radii > 0).sum().item())
+    T = cam.tile_bounds[0] * cam.tile_bounds[1]
+    P = H * W
+    ab = algorithmic_bytes(N, I, P, T, K, nvis)
+    kernels = {}
+    for name, (calls, mean_ms, tot_ms) in per_call.items():
+        per_step = calls / args.steps
+        b = ab.get(name)
+        kernels[name] = {
+            "ms_per_call": round(mean_ms, 4),
+            "calls_per_step": per_step,
+            "GBps": round(b / (mean_ms * 1e-3) / 1e9, 1) if b else None,
+        }
+    dom = max(per_call, key=lambda k: per_call[k][2])
+    dom_ms = per_call[dom][1]
+    dom_bytes = ab.get(dom)
+    step_bytes = sum(ab.values())
+    roofline = {
+        "kernel": dom,
+        "bound": "hbm",
+        "achieved": round(dom_bytes / (dom_ms * 1e-3) / 1e9, 1) if dom_bytes else None,
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(dom_bytes / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if dom_bytes else None,
+        "traffic": None,
+        "step_algorithmic_bytes": step_bytes,
+        "step_frac": round(step_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+        "roofline_mpix_s": round(P / (step_bytes / (HBM_PEAK_GBS * 1e9)) / 1e6, 1),
+    }
+
+    # full train step: splatfacto loss + backward + all-reduce + Adam
+    tsteps = args.train_steps if args.train_steps is not None else args.steps
+    trainer.loss_kind = "splatfacto"
+    for _ in range(2):
+        trainer.step(cam, gt)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(tsteps):
+        trainer.step(cam, gt)
+    barrier()
+    tdt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([tdt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        tdt = float(t.item())
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(scene, view_camera(W, H, 0), deg)
+
+    if rank == 0:
+        line = {
+            "metric": "Mpixels/s fwd+bwd and train iters/s, 1M Gaussians @ 1080^2",
+            "value": round(value, 2),
+            "unit": "Mpixels/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic (random-Gaussian scene per SURVEY.md §8d; random-init params)",
+            "config": {
+                "workload": desc,
+                "num_gaussians": N,
+                "num_visible": nvis,
+                "num_intersects": I,
+                "tiles": T,
+                "image": [H, W],
+                "sh_degree": deg,
+                "views_per_gpu_per_step": 1,
+                "parallelism": f"dp{world} (1 view/GPU, RCCL all-reduce of {N * 59 * 4} B "
+                               f"grad bucket)" if world > 1 else "dp1",
+            },
+            "train_iters_per_s": round(tsteps / tdt, 2),
+            "train_views_per_s": round(world * tsteps / tdt, 2),
+            "roofline": roofline,
+            "kernels": kernels,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

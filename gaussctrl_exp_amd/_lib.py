@@ -1,0 +1,117 @@
+"""ctypes binding of the C-ABI library libgsplat_mi355x.so (include/gsplat_mi355x.h).
+
+The library is the only compute path: there is no CPU or eager-PyTorch fallback.  If it
+is missing, or a tensor is not on a ROCm device, calls raise instead of silently running
+something else.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libgsplat_mi355x.so")
+CSRC = os.path.join(_HERE, "csrc")
+
+_c = ctypes
+_P = _c.c_void_p
+_F = _c.c_float
+_I = _c.c_int
+_I64 = _c.c_int64
+_SZ = _c.c_size_t
+
+# name -> (restype, argtypes); must match include/gsplat_mi355x.h exactly.
+SIGNATURES = {
+    "gsplat_abi_version": (_I, []),
+    "gsplat_last_error": (_c.c_char_p, []),
+    "gsplat_project_gaussians_forward": (_I, [
+        _I, _P, _P, _F, _P, _P, _P, _F, _F, _F, _F, _I, _I, _I, _I, _F,
+        _P, _P, _P, _P, _P, _P, _P]),
+    "gsplat_project_gaussians_backward": (_I, [
+        _I, _P, _P, _F, _P, _P, _P, _F, _F, _F, _F, _I, _I, _P, _P, _P, _P, _P, _P,
+        _P, _P, _P, _P, _P, _P]),
+    "gsplat_compute_sh_forward": (_I, [_I, _I, _I, _P, _P, _P, _P]),
+    "gsplat_compute_sh_backward": (_I, [_I, _I, _I, _P, _P, _P, _P]),
+    "gsplat_compute_cov2d_bounds": (_I, [_I, _P, _P, _P, _P]),
+    "gsplat_map_gaussian_to_intersects": (_I, [_I, _P, _P, _P, _P, _I, _I, _P, _P, _P]),
+    "gsplat_sort_isect_pairs_workspace_size": (_SZ, [_I64]),
+    "gsplat_sort_isect_pairs": (_I, [_I64, _I, _P, _P, _P, _P, _P, _SZ, _P]),
+    "gsplat_get_tile_bin_edges": (_I, [_I64, _P, _P, _I64, _P]),
+    "gsplat_bin_count_workspace_size": (_SZ, [_I]),
+    "gsplat_bin_emit_workspace_size": (_SZ, [_I64]),
+    "gsplat_bin_count": (_I, [_I, _P, _P, _P, _P, _P, _SZ, _P]),
+    "gsplat_bin_emit": (_I, [_I, _I64, _P, _P, _I, _I, _P, _P, _P, _SZ, _P, _SZ, _P]),
+    "gsplat_rasterize_forward": (_I, [_I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P,
+                                      _P, _P]),
+    "gsplat_rasterize_backward": (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P,
+                                       _P, _P, _P, _F, _P, _P, _P, _P, _P]),
+}
+
+_lib = None
+
+
+def build(jobs: int = 8) -> str:
+    """Compile the HIP sources for gfx950 (hipcc cross-compiles without a GPU)."""
+    subprocess.run(["make", "-s", "-C", CSRC, f"-j{jobs}"], check=True)
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"gsplat MI355X library not built: {LIB_PATH} is missing "
+                "(run `python -c 'import __graft_entry__ as g; g.build()'`)")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        if L.gsplat_abi_version() != 1:
+            raise RuntimeError("libgsplat_mi355x.so ABI version mismatch")
+        _lib = L
+    return _lib
+
+
+def call(name: str, *args) -> int:
+    """Call a status-returning entry point; non-zero status -> RuntimeError."""
+    rc = getattr(lib(), name)(*args)
+    if rc != 0:
+        msg = lib().gsplat_last_error().decode(errors="replace")
+        raise RuntimeError(f"{name} failed: {msg}")
+    return rc
+
+
+def query(name: str, *args) -> int:
+    """Call a size query (`*_workspace_size`)."""
+    return int(getattr(lib(), name)(*args))
+
+
+def ptr(t):
+    return None if t is None else _c.c_void_p(t.data_ptr())
+
+
+def stream(device) -> _c.c_void_p:
+    return _c.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def check_device(name: str, *tensors):
+    """gsplat's CHECK_INPUT: ROCm-device, contiguous tensors only."""
+    dev = None
+    for t in tensors:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise RuntimeError(f"{name}: expected a ROCm device tensor, got {t.device} "
+                               "(this rasterizer has no CPU path)")
+        if not t.is_contiguous():
+            raise RuntimeError(f"{name}: tensor must be contiguous")
+        if dev is None:
+            dev = t.device
+        elif t.device != dev:
+            raise RuntimeError(f"{name}: tensors on different devices ({dev} vs {t.device})")
+    return dev

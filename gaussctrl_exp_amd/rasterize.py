@@ -1,0 +1,189 @@
+"""Differentiable tile rasterizer (gsplat 0.1.2.1 `gsplat/rasterize.py`).
+
+`rasterize_gaussians` is called by /root/reference/gaussctrl/gc_model.py:208-220 (RGB with
+return_alpha=True, random background during training) and :225-236 (depth, eval).  The
+binning (cumsum -> intersect map -> sort -> tile bins) runs fused on the GPU
+(csrc/binning.hip) with one host read of the intersection count, exactly where gsplat
+reads `cum_tiles_hit[-1].item()`; blending runs in csrc/raster.hip.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+from torch import Tensor
+from torch.autograd import Function
+
+from . import _lib
+
+BLOCK_X, BLOCK_Y = 16, 16
+
+# gsplat 0.1.x clamps alpha at 0.999 in the forward but at 0.99 in the backward
+# (SURVEY.md Appendix A10).  Kept for parity; set to 0.999 for the consistent gradient.
+BACKWARD_ALPHA_CLAMP = 0.99
+
+
+def rasterize_gaussians(
+    xys: Tensor,
+    depths: Tensor,
+    radii: Tensor,
+    conics: Tensor,
+    num_tiles_hit: Tensor,
+    colors: Tensor,
+    opacity: Tensor,
+    img_height: int,
+    img_width: int,
+    background: Optional[Tensor] = None,
+    return_alpha: Optional[bool] = False,
+):
+    """Rasterize 2D Gaussians by front-to-back alpha blending per 16x16 tile.
+
+    Args: xys [N,2], depths [N], radii [N] int, conics [N,3], num_tiles_hit [N] int (all
+    from project_gaussians), colors [N,C] (float, or uint8 -> /255), opacity [N,1],
+    img_height, img_width, background [C] (default ones), return_alpha.
+
+    Returns out_img [H,W,C], plus out_alpha [H,W] = 1 - final transmittance when
+    return_alpha.  Gradients flow to xys, conics, colors and opacity.
+    """
+    if colors.dtype == torch.uint8:
+        # make sure colors are float [0,1]
+        colors = colors.float() / 255
+
+    if background is not None:
+        assert background.shape[0] == colors.shape[-1], (
+            f"incorrect shape of background color tensor, expected shape {colors.shape[-1]}")
+    else:
+        background = torch.ones(colors.shape[-1], dtype=torch.float32, device=colors.device)
+
+    if xys.ndimension() != 2 or xys.size(1) != 2:
+        raise ValueError("xys must have dimensions (N, 2)")
+
+    if colors.ndimension() != 2:
+        raise ValueError("colors must have dimensions (N, D)")
+
+    return _RasterizeGaussians.apply(
+        xys.contiguous(), depths.contiguous(), radii.contiguous(), conics.contiguous(),
+        num_tiles_hit.contiguous(), colors.contiguous(), opacity.contiguous(), img_height,
+        img_width, background.contiguous(), return_alpha)
+
+
+def bin_gaussians(xys: Tensor, depths: Tensor, radii: Tensor, num_tiles_hit: Tensor,
+                  img_height: int, img_width: int):
+    """Fused on-device binning: (num_intersects, gaussian_ids_sorted [I] int32,
+    tile_bins [tiles, 2] int32).  Same order as gsplat's stable-sorted isect_ids."""
+    n = xys.shape[0]
+    tbx = (img_width + BLOCK_X - 1) // BLOCK_X
+    tby = (img_height + BLOCK_Y - 1) // BLOCK_Y
+    dev = xys.device
+    radii = radii.to(torch.int32).contiguous()
+    num_tiles_hit = num_tiles_hit.to(torch.int32).contiguous()
+    depths = depths.float().contiguous()
+    ws1 = torch.empty((_lib.query("gsplat_bin_count_workspace_size", n),), device=dev,
+                      dtype=torch.uint8)
+    counts = torch.empty((2,), device=dev, dtype=torch.int32)
+    P, st = _lib.ptr, _lib.stream(dev)
+    _lib.call("gsplat_bin_count", n, P(depths), P(radii), P(num_tiles_hit), P(counts), P(ws1),
+              ws1.numel(), st)
+    num_intersects = int(counts[1].item())  # the single host sync (gsplat: .item())
+    tile_bins = torch.empty((tbx * tby, 2), device=dev, dtype=torch.int32)
+    gaussian_ids_sorted = torch.empty((max(num_intersects, 0),), device=dev, dtype=torch.int32)
+    ws2 = torch.empty((_lib.query("gsplat_bin_emit_workspace_size", num_intersects),),
+                      device=dev, dtype=torch.uint8)
+    _lib.call("gsplat_bin_emit", n, num_intersects, P(xys), P(radii), tbx, tby,
+              P(gaussian_ids_sorted), P(tile_bins), P(ws1), ws1.numel(), P(ws2), ws2.numel(), st)
+    return num_intersects, gaussian_ids_sorted, tile_bins
+
+
+class _RasterizeGaussians(Function):
+    """Rasterizes 2D gaussians (autograd wrapper of the C-ABI binning/raster kernels)."""
+
+    @staticmethod
+    def forward(ctx, xys, depths, radii, conics, num_tiles_hit, colors, opacity, img_height,
+                img_width, background=None, return_alpha=False):
+        num_points = xys.size(0)
+        H, W = int(img_height), int(img_width)
+        tbx = (W + BLOCK_X - 1) // BLOCK_X
+        tby = (H + BLOCK_Y - 1) // BLOCK_Y
+        C = colors.shape[-1]
+        xys, conics = xys.float().contiguous(), conics.float().contiguous()
+        colors, opacity = colors.float().contiguous(), opacity.float().contiguous()
+        background = background.float().contiguous()
+        dev = _lib.check_device("rasterize_gaussians", xys, depths, radii, conics,
+                                num_tiles_hit, colors, opacity, background)
+        if opacity.numel() != num_points or conics.shape != (num_points, 3) or \
+                colors.shape[0] != num_points:
+            raise ValueError("rasterize_gaussians: inconsistent per-Gaussian tensor shapes")
+
+        num_intersects, gaussian_ids_sorted, tile_bins = bin_gaussians(
+            xys, depths, radii, num_tiles_hit, H, W)
+
+        if num_intersects < 1:
+            # gsplat 0.1.x: background image, final_Ts zero (so alpha = 1)
+            out_img = torch.ones(H, W, C, device=dev) * background
+            final_Ts = torch.zeros(H, W, device=dev)
+            final_idx = torch.zeros(H, W, device=dev, dtype=torch.int32)
+        else:
+            out_img = torch.empty((H, W, C), device=dev, dtype=torch.float32)
+            final_Ts = torch.empty((H, W), device=dev, dtype=torch.float32)
+            final_idx = torch.empty((H, W), device=dev, dtype=torch.int32)
+            P = _lib.ptr
+            _lib.call("gsplat_rasterize_forward", tbx, tby, H, W, C, P(gaussian_ids_sorted),
+                      P(tile_bins), P(xys), P(conics), P(colors), P(opacity), P(background),
+                      P(out_img), P(final_Ts), P(final_idx), _lib.stream(dev))
+
+        ctx.img_width = W
+        ctx.img_height = H
+        ctx.num_intersects = num_intersects
+        ctx.opacity_shape = opacity.shape
+        ctx.save_for_backward(gaussian_ids_sorted, tile_bins, xys, conics, colors, opacity,
+                              background, final_Ts, final_idx)
+
+        if return_alpha:
+            out_alpha = 1 - final_Ts
+            return out_img, out_alpha
+        return out_img
+
+    @staticmethod
+    def backward(ctx, v_out_img, v_out_alpha=None):
+        H, W = ctx.img_height, ctx.img_width
+        (gaussian_ids_sorted, tile_bins, xys, conics, colors, opacity, background, final_Ts,
+         final_idx) = ctx.saved_tensors
+        num_points, C = colors.shape
+        dev = xys.device
+        if v_out_alpha is None:
+            v_out_alpha = torch.zeros_like(v_out_img[..., 0])
+
+        if ctx.num_intersects < 1:
+            v_xy = torch.zeros_like(xys)
+            v_conic = torch.zeros_like(conics)
+            v_colors = torch.zeros_like(colors)
+            v_opacity = torch.zeros_like(opacity)
+        else:
+            v_out_img = v_out_img.float().contiguous()
+            v_out_alpha = v_out_alpha.float().contiguous()
+            v_xy = torch.empty((num_points, 2), device=dev, dtype=torch.float32)
+            v_conic = torch.empty((num_points, 3), device=dev, dtype=torch.float32)
+            v_colors = torch.empty((num_points, C), device=dev, dtype=torch.float32)
+            v_opacity = torch.empty(ctx.opacity_shape, device=dev, dtype=torch.float32)
+            P = _lib.ptr
+            tbx = (W + BLOCK_X - 1) // BLOCK_X
+            tby = (H + BLOCK_Y - 1) // BLOCK_Y
+            _lib.call("gsplat_rasterize_backward", tbx, tby, H, W, C, num_points,
+                      P(gaussian_ids_sorted), P(tile_bins), P(xys), P(conics), P(colors),
+                      P(opacity), P(background), P(final_Ts), P(final_idx), P(v_out_img),
+                      P(v_out_alpha), float(BACKWARD_ALPHA_CLAMP), P(v_xy), P(v_conic),
+                      P(v_colors), P(v_opacity), _lib.stream(dev))
+
+        return (
+            v_xy,  # xys
+            None,  # depths
+            None,  # radii
+            v_conic,  # conics
+            None,  # num_tiles_hit
+            v_colors,  # colors
+            v_opacity,  # opacity
+            None,  # img_height
+            None,  # img_width
+            None,  # background
+            None,  # return_alpha
+        )

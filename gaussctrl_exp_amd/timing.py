@@ -1,0 +1,49 @@
+"""Per-entry-point HIP-event timing of the C-ABI calls (used by bench.py).
+
+When enabled, every `_lib.call` is bracketed by two events recorded on the stream the
+kernels are launched on (torch's current stream, which is what the wrappers pass to the
+C ABI), so per-call device durations are measured live without a profiler.
+"""
+from __future__ import annotations
+
+import collections
+import contextlib
+
+import torch
+
+from . import _lib
+
+_orig_call = _lib.call
+
+
+class CallTimer:
+    def __init__(self):
+        self.events = collections.defaultdict(list)
+
+    def _call(self, name, *args):
+        s = torch.cuda.Event(enable_timing=True)
+        e = torch.cuda.Event(enable_timing=True)
+        s.record()
+        rc = _orig_call(name, *args)
+        e.record()
+        self.events[name].append((s, e))
+        return rc
+
+    def summary(self):
+        """{name: (calls, mean_ms, total_ms)} -- synchronises the device."""
+        torch.cuda.synchronize()
+        out = {}
+        for name, evs in self.events.items():
+            ms = [s.elapsed_time(e) for s, e in evs]
+            out[name] = (len(ms), sum(ms) / len(ms), sum(ms))
+        return out
+
+
+@contextlib.contextmanager
+def timed_calls():
+    t = CallTimer()
+    _lib.call = t._call
+    try:
+        yield t
+    finally:
+        _lib.call = _orig_call

@@ -1,0 +1,130 @@
+"""Multi-view data-parallel training step (one camera per GPU, RCCL gradient all-reduce).
+
+The reference trains one camera per iteration on one device
+(gaussctrl/gc_datamanager.py:213-235 -> gc_pipeline.py:469-480 -> gc_trainer.py:258-301):
+render (gc_model.get_outputs) -> splatfacto loss 0.8*L1 + 0.2*(1-SSIM) -> backward ->
+Adam over the six Gaussian parameter groups (gc_config.py:58-87).  Here each rank renders
+its own camera of a multi-view batch against a replica of the parameters; the per-view
+losses sum, so the gradients are summed across ranks with one all-reduce of a single flat
+fp32 bucket ([N x 59], 236 B/Gaussian) over RCCL/xGMI, after which every rank takes the
+identical Adam step.  Gradients are accumulated by autograd directly into views of the
+flat bucket, so the all-reduce needs no pack/unpack copies.
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+import torch.nn.functional as F
+
+from .camera import GCCamera
+from .scene import PARAM_NAMES, GaussianScene, render
+
+# gc_config.py:58-87 (Adam, eps 1e-15); xyz decays 1.6e-4 -> 1.6e-6 over 30k steps.
+GROUP_LR = {"means": 1.6e-4, "features_dc": 0.0025, "features_rest": 0.0025 / 20,
+            "opacities": 0.05, "scales": 0.005, "quats": 0.001}
+XYZ_LR_FINAL, XYZ_MAX_STEPS = 1.6e-6, 30000
+SSIM_LAMBDA = 0.2  # splatfacto SplatfactoModelConfig.ssim_lambda
+
+
+def _gauss_window(size=11, sigma=1.5, device="cpu"):
+    coords = torch.arange(size, dtype=torch.float32, device=device) - size // 2
+    g = torch.exp(-(coords ** 2) / (2 * sigma ** 2))
+    return g / g.sum()
+
+
+def ssim(x, y, data_range=1.0, win_size=11, sigma=1.5, k1=0.01, k2=0.03):
+    """pytorch_msssim.ssim semantics (separable Gaussian window, 'valid' convolution,
+    size_average): x, y [B,C,H,W]."""
+    C = x.shape[1]
+    w = _gauss_window(win_size, sigma, x.device)
+
+    def filt(t):
+        t = F.conv2d(t, w.view(1, 1, 1, -1).expand(C, 1, 1, -1), groups=C)
+        return F.conv2d(t, w.view(1, 1, -1, 1).expand(C, 1, -1, 1), groups=C)
+
+    c1, c2 = (k1 * data_range) ** 2, (k2 * data_range) ** 2
+    mu1, mu2 = filt(x), filt(y)
+    s11 = filt(x * x) - mu1 * mu1
+    s22 = filt(y * y) - mu2 * mu2
+    s12 = filt(x * y) - mu1 * mu2
+    cs = (2 * s12 + c2) / (s11 + s22 + c2)
+    m = ((2 * mu1 * mu2 + c1) / (mu1 * mu1 + mu2 * mu2 + c1)) * cs
+    return m.flatten(2).mean(-1).mean()
+
+
+def splatfacto_loss(pred, gt):
+    """0.8 * L1 + 0.2 * (1 - SSIM) on [H,W,3] images (nerfstudio splatfacto get_loss_dict)."""
+    l1 = torch.abs(gt - pred).mean()
+    sim = 1 - ssim(gt.permute(2, 0, 1)[None], pred.permute(2, 0, 1)[None])
+    return (1 - SSIM_LAMBDA) * l1 + SSIM_LAMBDA * sim
+
+
+class FlatGradBucket:
+    """One contiguous fp32 buffer holding every parameter's .grad as a view."""
+
+    def __init__(self, params: List[torch.Tensor]):
+        numel = sum(p.numel() for p in params)
+        self.buffer = torch.zeros(numel, device=params[0].device, dtype=torch.float32)
+        off = 0
+        for p in params:
+            p.grad = self.buffer[off:off + p.numel()].view_as(p)
+            off += p.numel()
+        self.params = params
+
+    def zero_(self):
+        self.buffer.zero_()
+
+    def all_reduce_(self, group=None):
+        dist.all_reduce(self.buffer, op=dist.ReduceOp.SUM, group=group)
+
+
+class TrainStep:
+    """render -> loss -> backward -> [all-reduce] -> Adam, on this rank's camera."""
+
+    def __init__(self, scene: GaussianScene, sh_degree: int = 3, world_size: int = 1,
+                 loss: str = "splatfacto", group=None):
+        self.scene = scene.requires_grad_()
+        self.params = scene.params()
+        self.bucket = FlatGradBucket(self.params)
+        self.world_size = world_size
+        self.group = group
+        self.sh_degree = sh_degree
+        self.loss_kind = loss
+        self.opt = torch.optim.Adam(
+            [{"params": [getattr(scene, k)], "lr": GROUP_LR[k], "name": k}
+             for k in PARAM_NAMES], eps=1e-15, foreach=True)
+        self.step_count = 0
+
+    def _xyz_lr(self):
+        t = min(self.step_count / XYZ_MAX_STEPS, 1.0)
+        return math.exp(math.log(GROUP_LR["means"]) * (1 - t) + math.log(XYZ_LR_FINAL) * t)
+
+    def loss(self, pred, gt):
+        if self.loss_kind == "l1":
+            return torch.abs(gt - pred).mean()
+        return splatfacto_loss(pred, gt)
+
+    def forward_backward(self, cam: GCCamera, gt: torch.Tensor, background: torch.Tensor):
+        out = render(self.scene, cam, self.sh_degree, background)
+        loss = self.loss(out["rgb"], gt)
+        loss.backward()
+        return loss, out
+
+    def step(self, cam: GCCamera, gt: torch.Tensor, background: Optional[torch.Tensor] = None,
+             optimizer: bool = True):
+        if background is None:
+            background = torch.rand(3, device=gt.device)
+        self.bucket.zero_()
+        loss, out = self.forward_backward(cam, gt, background)
+        if self.world_size > 1:
+            self.bucket.all_reduce_(self.group)
+        if optimizer:
+            for g in self.opt.param_groups:
+                if g["name"] == "means":
+                    g["lr"] = self._xyz_lr()
+            self.opt.step()
+            self.step_count += 1
+        return loss

@@ -1,0 +1,147 @@
+/*
+ * gsplat_mi355x.h -- C ABI of the MI355X (gfx950) 3D Gaussian splatting rasterizer.
+ *
+ * Drop-in boundary: these entry points are what gsplat 0.1.2.1's Python autograd
+ * wrappers bind through `gsplat._C` (un-vendored dependency pinned at
+ * /root/reference/README.md:58, called from /root/reference/gaussctrl/gc_model.py:174-236).
+ * One entry point per `_C` function, with the same argument meaning; plain pointers,
+ * sizes and a hipStream_t passed as void*.  All tensor pointers are DEVICE pointers to
+ * contiguous row-major storage (float32 unless named *_i32 / int).  No entry point
+ * allocates, frees or synchronises: scratch comes from a caller-provided workspace whose
+ * size is reported by the matching *_workspace_size() query, so every call is
+ * hipGraph-capturable.
+ *
+ * Return value: 0 on success, non-zero on error (gsplat_last_error() describes it);
+ * argument errors are reported before anything is launched.
+ *
+ * Reference interfaces replaced (gsplat 0.1.2.1, [ext] = not vendored in the reference):
+ *   gsplat_project_gaussians_forward   <- _C.project_gaussians_forward  (gc_model.py:174-188)
+ *   gsplat_project_gaussians_backward  <- _C.project_gaussians_backward (autograd of :174)
+ *   gsplat_compute_sh_forward          <- _C.compute_sh_forward         (gc_model.py:200)
+ *   gsplat_compute_sh_backward         <- _C.compute_sh_backward        (autograd of :200)
+ *   gsplat_compute_cov2d_bounds        <- _C.compute_cov2d_bounds       (gsplat.utils)
+ *   gsplat_map_gaussian_to_intersects  <- _C.map_gaussian_to_intersects (gsplat.utils)
+ *   gsplat_sort_isect_pairs            <- torch.sort + torch.gather in utils.bin_and_sort_gaussians
+ *   gsplat_get_tile_bin_edges          <- _C.get_tile_bin_edges         (gsplat.utils)
+ *   gsplat_bin_count / gsplat_bin_emit <- the cumsum/map/sort/bin sequence inside
+ *                                         rasterize.py _RasterizeGaussians.forward
+ *                                         (gc_model.py:208-220, :225-236), fused
+ *   gsplat_rasterize_forward           <- _C.rasterize_forward / _C.nd_rasterize_forward
+ *   gsplat_rasterize_backward          <- _C.rasterize_backward / _C.nd_rasterize_backward
+ */
+#ifndef GSPLAT_MI355X_H
+#define GSPLAT_MI355X_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GSPLAT_MI355X_ABI_VERSION 1
+
+int gsplat_abi_version(void);
+const char *gsplat_last_error(void);
+
+/* ---- projection (forward.cu / backward.cu project_gaussians_*) ----------------------
+ * means3d [N,3], scales [N,3], quats [N,4] (w,x,y,z), viewmat >= 12 floats (row-major
+ * [3,4] or [4,4]; first 12 read), projmat [4,4].  Outputs are fully written (culled
+ * Gaussians get zeros, except conics/cov3d which follow gsplat's write order). */
+int gsplat_project_gaussians_forward(
+    int num_points, const float *means3d, const float *scales, float glob_scale,
+    const float *quats, const float *viewmat, const float *projmat, float fx, float fy,
+    float cx, float cy, int img_height, int img_width, int tile_bounds_x, int tile_bounds_y,
+    float clip_thresh, float *cov3d, float *xys, float *depths, int32_t *radii,
+    float *conics, int32_t *num_tiles_hit, void *stream);
+
+/* Outputs v_cov2d [N,3], v_cov3d [N,6], v_mean3d [N,3], v_scale [N,3], v_quat [N,4] are
+ * fully written (zeros where radii <= 0). */
+int gsplat_project_gaussians_backward(
+    int num_points, const float *means3d, const float *scales, float glob_scale,
+    const float *quats, const float *viewmat, const float *projmat, float fx, float fy,
+    float cx, float cy, int img_height, int img_width, const float *cov3d,
+    const int32_t *radii, const float *conics, const float *v_xy, const float *v_depth,
+    const float *v_conic, float *v_cov2d, float *v_cov3d, float *v_mean3d, float *v_scale,
+    float *v_quat, void *stream);
+
+/* ---- spherical harmonics (sh.cuh) ----------------------------------------------------
+ * coeffs [N, num_sh_bases(degree), 3]; colors [N,3]; v_coeffs fully written. */
+int gsplat_compute_sh_forward(int num_points, int degree, int degrees_to_use,
+                              const float *viewdirs, const float *coeffs, float *colors,
+                              void *stream);
+int gsplat_compute_sh_backward(int num_points, int degree, int degrees_to_use,
+                               const float *viewdirs, const float *v_colors, float *v_coeffs,
+                               void *stream);
+
+/* covs2d [N,3] -> conics [N,3], radii [N] (float).  det == 0 rows get zeros. */
+int gsplat_compute_cov2d_bounds(int num_points, const float *covs2d, float *conics,
+                                float *radii, void *stream);
+
+/* ---- gsplat-layout binning (utils.py) -------------------------------------------------
+ * isect_ids [I] int64 = (tile_id << 32) | float_bits(depth), gaussian_ids [I] int32,
+ * written at cum_tiles_hit[i-1] for Gaussian i (cum_tiles_hit = inclusive cumsum). */
+int gsplat_map_gaussian_to_intersects(int num_points, const float *xys, const float *depths,
+                                      const int32_t *radii, const int32_t *cum_tiles_hit,
+                                      int tile_bounds_x, int tile_bounds_y, int64_t *isect_ids,
+                                      int32_t *gaussian_ids, void *stream);
+
+/* Stable LSD radix sort of (isect_ids, gaussian_ids) pairs by key bits [0, key_bits).
+ * Keys must be non-negative.  Outputs may not alias inputs. */
+size_t gsplat_sort_isect_pairs_workspace_size(int64_t num_items);
+int gsplat_sort_isect_pairs(int64_t num_items, int key_bits, const int64_t *keys_in,
+                            const int32_t *vals_in, int64_t *keys_out, int32_t *vals_out,
+                            void *workspace, size_t workspace_bytes, void *stream);
+
+/* tile_bins [num_rows,2] int32: zero-filled here, then [first,last+1) per tile id. Tile
+ * ids >= num_rows are dropped (gsplat 0.1.x sizes the table by num_intersects). */
+int gsplat_get_tile_bin_edges(int64_t num_intersects, const int64_t *isect_ids_sorted,
+                              int32_t *tile_bins, int64_t num_rows, void *stream);
+
+/* ---- fused binning for rasterize (cumsum -> map -> sort -> bins) ------------------------
+ * Phase 1 (gsplat_bin_count) orders the visible Gaussians (radii > 0) front to back
+ * (stable on the depth bits, ties by Gaussian id) and writes d_counts[0] = visible count,
+ * d_counts[1] = total intersections I (device int32[2]).  The caller reads d_counts -- the
+ * one host sync, like gsplat's cum_tiles_hit[-1].item() -- sizes phase 2's workspace from
+ * I, and calls gsplat_bin_emit with BOTH workspaces (phase 1's must be left untouched in
+ * between).  Phase 2 writes gaussian_ids_sorted [I] and tile_bins [tbx*tby, 2]; the order is
+ * identical to a stable sort of gsplat's 64-bit isect_ids. */
+size_t gsplat_bin_count_workspace_size(int num_points);
+size_t gsplat_bin_emit_workspace_size(int64_t num_intersects);
+int gsplat_bin_count(int num_points, const float *depths, const int32_t *radii,
+                     const int32_t *num_tiles_hit, int32_t *d_counts, void *workspace1,
+                     size_t workspace1_bytes, void *stream);
+int gsplat_bin_emit(int num_points, int64_t num_intersects, const float *xys,
+                    const int32_t *radii, int tile_bounds_x, int tile_bounds_y,
+                    int32_t *gaussian_ids_sorted, int32_t *tile_bins, const void *workspace1,
+                    size_t workspace1_bytes, void *workspace2, size_t workspace2_bytes,
+                    void *stream);
+
+/* ---- rasterization (forward.cu rasterize_forward, backward.cu rasterize_backward) -----
+ * colors [N,C], opacity [N] (or [N,1]), background [C]; out_img [H,W,C], final_Ts [H,W],
+ * final_idx [H,W] int32.  C == 3 takes the specialised kernel; 1 <= C <= 64 otherwise. */
+int gsplat_rasterize_forward(int tile_bounds_x, int tile_bounds_y, int img_height,
+                             int img_width, int channels, const int32_t *gaussian_ids_sorted,
+                             const int32_t *tile_bins, const float *xys, const float *conics,
+                             const float *colors, const float *opacity,
+                             const float *background, float *out_img, float *final_Ts,
+                             int32_t *final_idx, void *stream);
+
+/* v_output [H,W,C], v_output_alpha [H,W]; gradients v_xy [N,2], v_conic [N,3],
+ * v_colors [N,C], v_opacity [N] are fully written.  alpha_max is the backward alpha clamp
+ * (gsplat 0.1.x uses 0.99f). */
+int gsplat_rasterize_backward(int tile_bounds_x, int tile_bounds_y, int img_height,
+                              int img_width, int channels, int num_points,
+                              const int32_t *gaussian_ids_sorted, const int32_t *tile_bins,
+                              const float *xys, const float *conics, const float *colors,
+                              const float *opacity, const float *background,
+                              const float *final_Ts, const int32_t *final_idx,
+                              const float *v_output, const float *v_output_alpha,
+                              float alpha_max, float *v_xy, float *v_conic, float *v_colors,
+                              float *v_opacity, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GSPLAT_MI355X_H */

@@ -1,0 +1,238 @@
+"""ctypes/numpy front-end of the C oracle (oracle/gsplat_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg, never by the product path.  Parity status vs real gsplat 0.1.2.1:
+"parity unpinned" (no gsplat source/fixtures exist offline; see gsplat_oracle.c header
+and DESIGN.md §Oracle).
+
+Every function mirrors one gsplat 0.1.2.1 `_C` entry point; `render_forward` /
+`render_backward` chain them exactly as gsplat's Python wrappers do
+(rasterize.py `_RasterizeGaussians`, utils.py `bin_and_sort_gaussians`), which is how
+gaussctrl/gc_model.py:174-236 drives them.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "liboracle.so")
+_lib = None
+
+f32p = ctypes.POINTER(ctypes.c_float)
+i32p = ctypes.POINTER(ctypes.c_int)
+i64p = ctypes.POINTER(ctypes.c_int64)
+
+
+def build(force: bool = False) -> str:
+    """Compile the oracle with its Makefile (gcc, -ffp-contract=off)."""
+    if force or not os.path.exists(_LIB_PATH):
+        subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        _lib = ctypes.CDLL(_LIB_PATH)
+    return _lib
+
+
+def _f(a):
+    return np.ascontiguousarray(a, dtype=np.float32)
+
+
+def _p(a):
+    if a is None:
+        return None
+    if a.dtype == np.float32:
+        return a.ctypes.data_as(f32p)
+    if a.dtype == np.int32:
+        return a.ctypes.data_as(i32p)
+    if a.dtype == np.int64:
+        return a.ctypes.data_as(i64p)
+    raise TypeError(a.dtype)
+
+
+def num_sh_bases(degree: int) -> int:
+    return {0: 1, 1: 4, 2: 9, 3: 16}.get(degree, 25)
+
+
+def project_forward(means, scales, glob_scale, quats, viewmat, projmat, fx, fy, cx, cy,
+                    H, W, tile_bounds, clip_thresh=0.01):
+    means, scales, quats = _f(means), _f(scales), _f(quats)
+    vm = _f(viewmat).reshape(-1)[:12].copy()
+    pm = _f(projmat).reshape(-1)
+    n = means.shape[0]
+    cov3d = np.zeros((n, 6), np.float32)
+    xys = np.zeros((n, 2), np.float32)
+    depths = np.zeros((n,), np.float32)
+    radii = np.zeros((n,), np.int32)
+    conics = np.zeros((n, 3), np.float32)
+    nth = np.zeros((n,), np.int32)
+    lib().oracle_project_forward(
+        n, _p(means), _p(scales), ctypes.c_float(glob_scale), _p(quats), _p(vm), _p(pm),
+        ctypes.c_float(fx), ctypes.c_float(fy), ctypes.c_float(cx), ctypes.c_float(cy),
+        int(H), int(W), int(tile_bounds[0]), int(tile_bounds[1]),
+        ctypes.c_float(clip_thresh), _p(cov3d), _p(xys), _p(depths), _p(radii), _p(conics),
+        _p(nth))
+    return xys, depths, radii, conics, nth, cov3d
+
+
+def project_backward(means, scales, glob_scale, quats, viewmat, projmat, fx, fy, cx, cy,
+                     H, W, cov3d, radii, conics, v_xys, v_depths, v_conics):
+    means, scales, quats = _f(means), _f(scales), _f(quats)
+    vm = _f(viewmat).reshape(-1)[:12].copy()
+    pm = _f(projmat).reshape(-1)
+    n = means.shape[0]
+    out = [np.zeros((n, k), np.float32) for k in (3, 6, 3, 3, 4)]
+    lib().oracle_project_backward(
+        n, _p(means), _p(scales), ctypes.c_float(glob_scale), _p(quats), _p(vm), _p(pm),
+        ctypes.c_float(fx), ctypes.c_float(fy), ctypes.c_float(cx), ctypes.c_float(cy),
+        int(H), int(W), _p(_f(cov3d)), _p(np.ascontiguousarray(radii, np.int32)),
+        _p(_f(conics)), _p(_f(v_xys)), _p(_f(v_depths)), _p(_f(v_conics)),
+        *[_p(o) for o in out])
+    v_cov2d, v_cov3d, v_mean, v_scale, v_quat = out
+    return v_cov2d, v_cov3d, v_mean, v_scale, v_quat
+
+
+def sh_forward(degrees_to_use, viewdirs, coeffs):
+    coeffs = _f(coeffs)
+    n, K = coeffs.shape[0], coeffs.shape[1]
+    degree = {1: 0, 4: 1, 9: 2, 16: 3, 25: 4}[K]
+    out = np.zeros((n, 3), np.float32)
+    lib().oracle_sh_forward(n, degree, int(degrees_to_use), _p(_f(viewdirs)), _p(coeffs),
+                            _p(out))
+    return out
+
+
+def sh_backward(degrees_to_use, viewdirs, v_colors, K):
+    n = v_colors.shape[0]
+    degree = {1: 0, 4: 1, 9: 2, 16: 3, 25: 4}[K]
+    out = np.zeros((n, K, 3), np.float32)
+    lib().oracle_sh_backward(n, degree, int(degrees_to_use), _p(_f(viewdirs)),
+                             _p(_f(v_colors)), _p(out))
+    return out
+
+
+def cov2d_bounds(cov2d):
+    cov2d = _f(cov2d)
+    n = cov2d.shape[0]
+    conics = np.zeros((n, 3), np.float32)
+    radii = np.zeros((n, 1), np.float32)
+    lib().oracle_cov2d_bounds(n, _p(cov2d), _p(conics), _p(radii))
+    return conics, radii
+
+
+def map_intersects(xys, depths, radii, cum_tiles_hit, tile_bounds, num_intersects):
+    n = xys.shape[0]
+    isect = np.zeros((num_intersects,), np.int64)
+    gids = np.zeros((num_intersects,), np.int32)
+    lib().oracle_map_intersects(n, _p(_f(xys)), _p(_f(depths)),
+                                _p(np.ascontiguousarray(radii, np.int32)),
+                                _p(np.ascontiguousarray(cum_tiles_hit, np.int32)),
+                                int(tile_bounds[0]), int(tile_bounds[1]), _p(isect), _p(gids))
+    return isect, gids
+
+
+def sort_pairs(keys, vals):
+    keys = np.ascontiguousarray(keys, np.int64).copy()
+    vals = np.ascontiguousarray(vals, np.int32).copy()
+    lib().oracle_sort_pairs(ctypes.c_int64(keys.shape[0]), _p(keys), _p(vals))
+    return keys, vals
+
+
+def tile_bin_edges(isect_sorted, rows):
+    bins = np.zeros((rows, 2), np.int32)
+    lib().oracle_tile_bin_edges(ctypes.c_int64(isect_sorted.shape[0]),
+                                _p(np.ascontiguousarray(isect_sorted, np.int64)), _p(bins),
+                                ctypes.c_int64(rows))
+    return bins
+
+
+def bin_and_sort(xys, depths, radii, num_tiles_hit, tile_bounds):
+    """utils.bin_and_sort_gaussians with tile_bins sized [num_tiles, 2]."""
+    cum = np.cumsum(np.asarray(num_tiles_hit, np.int64)).astype(np.int32)
+    I = int(cum[-1]) if cum.size else 0
+    isect, gids = map_intersects(xys, depths, radii, cum, tile_bounds, I)
+    isect_s, gids_s = sort_pairs(isect, gids)
+    T = int(tile_bounds[0]) * int(tile_bounds[1])
+    bins = tile_bin_edges(isect_s, T)
+    return dict(num_intersects=I, cum_tiles_hit=cum, isect_ids=isect, gaussian_ids=gids,
+                isect_ids_sorted=isect_s, gaussian_ids_sorted=gids_s, tile_bins=bins)
+
+
+def rasterize_forward(tile_bounds, H, W, gids_sorted, tile_bins, xys, conics, colors,
+                      opacity, background, tile_list=None):
+    colors = _f(colors)
+    C = colors.shape[1]
+    out = np.zeros((H, W, C), np.float32)
+    final_Ts = np.zeros((H, W), np.float32)
+    final_idx = np.zeros((H, W), np.int32)
+    tl = None if tile_list is None else np.ascontiguousarray(tile_list, np.int32)
+    lib().oracle_rasterize_forward(
+        int(tile_bounds[0]), int(tile_bounds[1]), int(H), int(W), C,
+        _p(np.ascontiguousarray(gids_sorted, np.int32)),
+        _p(np.ascontiguousarray(tile_bins, np.int32)), _p(_f(xys)), _p(_f(conics)),
+        _p(colors), _p(_f(opacity).reshape(-1)), _p(_f(background)), _p(tl),
+        0 if tl is None else tl.shape[0], _p(out), _p(final_Ts), _p(final_idx))
+    return out, final_Ts, final_idx
+
+
+def rasterize_backward(tile_bounds, H, W, gids_sorted, tile_bins, xys, conics, colors,
+                       opacity, background, final_Ts, final_idx, v_out, v_out_alpha,
+                       alpha_max=0.99, tile_list=None):
+    colors = _f(colors)
+    n, C = colors.shape
+    v_xy = np.zeros((n, 2), np.float32)
+    v_conic = np.zeros((n, 3), np.float32)
+    v_colors = np.zeros((n, C), np.float32)
+    v_opac = np.zeros((n, 1), np.float32)
+    tl = None if tile_list is None else np.ascontiguousarray(tile_list, np.int32)
+    lib().oracle_rasterize_backward(
+        int(tile_bounds[0]), int(tile_bounds[1]), int(H), int(W), C, n,
+        _p(np.ascontiguousarray(gids_sorted, np.int32)),
+        _p(np.ascontiguousarray(tile_bins, np.int32)), _p(_f(xys)), _p(_f(conics)),
+        _p(colors), _p(_f(opacity).reshape(-1)), _p(_f(background)), _p(_f(final_Ts)),
+        _p(np.ascontiguousarray(final_idx, np.int32)), _p(_f(v_out)), _p(_f(v_out_alpha)),
+        ctypes.c_float(alpha_max), _p(tl), 0 if tl is None else tl.shape[0], _p(v_xy),
+        _p(v_conic), _p(v_colors), _p(v_opac))
+    return v_xy, v_conic, v_colors, v_opac
+
+
+def render_forward(xys, depths, radii, conics, num_tiles_hit, colors, opacity, H, W,
+                   background):
+    """gsplat 0.1.2.1 `_RasterizeGaussians.forward` (rasterize.py), numpy edition.
+
+    Returns dict(img, alpha, final_Ts, final_idx, gaussian_ids_sorted, tile_bins, ...)."""
+    tb = ((W + 15) // 16, (H + 15) // 16, 1)
+    b = bin_and_sort(xys, depths, radii, num_tiles_hit, tb)
+    C = np.asarray(colors).shape[1]
+    if b["num_intersects"] < 1:  # image = background, alpha = 1
+        img = np.ones((H, W, C), np.float32) * _f(background)
+        final_Ts = np.zeros((H, W), np.float32)
+        final_idx = np.zeros((H, W), np.int32)
+    else:
+        img, final_Ts, final_idx = rasterize_forward(
+            tb, H, W, b["gaussian_ids_sorted"], b["tile_bins"], xys, conics, colors, opacity,
+            background)
+    b.update(img=img, alpha=1.0 - final_Ts, final_Ts=final_Ts, final_idx=final_idx,
+             tile_bounds=tb)
+    return b
+
+
+def render_backward(fwd, xys, conics, colors, opacity, background, v_img, v_alpha,
+                    alpha_max=0.99):
+    H, W = fwd["final_Ts"].shape
+    n, C = np.asarray(colors).shape
+    if fwd["num_intersects"] < 1:
+        return (np.zeros((n, 2), np.float32), np.zeros((n, 3), np.float32),
+                np.zeros((n, C), np.float32), np.zeros((n, 1), np.float32))
+    return rasterize_backward(fwd["tile_bounds"], H, W, fwd["gaussian_ids_sorted"],
+                              fwd["tile_bins"], xys, conics, colors, opacity, background,
+                              fwd["final_Ts"], fwd["final_idx"], v_img, v_alpha,
+                              alpha_max=alpha_max)

@@ -1,0 +1,209 @@
+"""Pure-PyTorch differentiable restatement of the gsplat 0.1.2.1 forward pass.
+
+TEST INFRASTRUCTURE ONLY (tests/ and bench.py cpu_baseline).  Parity vs real gsplat:
+"parity unpinned" (see oracle/gsplat_oracle.c header).
+
+Purpose: the C oracle's backward is a restatement of gsplat's *hand-written* VJPs
+(backward.cu / helpers.cuh).  This module re-derives those gradients with torch
+autograd from the forward math alone, so the hand VJPs are checked against calculus.
+gsplat 0.1.x's VJPs deviate from the exact derivative in three documented places
+(SURVEY.md Appendix A); `quirks=True` reproduces each deviation with a
+straight-through construction so autograd yields exactly what gsplat's VJP computes:
+
+  A5  project_pix_vjp drops the derivative of the perspective divide 1/(w+1e-6)
+      -> rw is detached.
+  A6  project_cov3d_ewa_vjp recomputes t WITHOUT the 1.3*tan_fov clamp
+      -> T = T_unclamped + (T_clamped - T_unclamped).detach().
+  A8  quat_to_rotmat_vjp ignores the normalisation Jacobian -> the norm is detached.
+
+The remaining quirk, the 0.99 alpha clamp in rasterize backward (A10), is not the
+gradient of any forward; tests keep opacity*exp(-sigma) < 0.99 where they compare
+against autograd.  `rasterize` is the naive per-pixel CPU rasterizer (loop over
+depth-ordered Gaussians, vectorised over pixels).
+"""
+from __future__ import annotations
+
+import torch
+
+BLOCK = 16
+
+
+def quat_to_rotmat(q, quirks=True):
+    n = q.norm(dim=-1, keepdim=True)
+    if quirks:
+        n = n.detach()
+    q = q / n
+    w, x, y, z = q.unbind(-1)
+    R = torch.stack([
+        1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y),
+        2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x),
+        2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y),
+    ], dim=-1)
+    return R.reshape(q.shape[:-1] + (3, 3))
+
+
+def cov3d_full(scales, glob_scale, quats, quirks=True):
+    R = quat_to_rotmat(quats, quirks)
+    M = R * (glob_scale * scales)[..., None, :]
+    return M @ M.transpose(-1, -2)
+
+
+def project(means, scales, glob_scale, quats, viewmat, projmat, fx, fy, cx, cy, H, W,
+            tile_bounds, clip_thresh=0.01, quirks=True):
+    """Returns xys, depths, radii, conics, num_tiles_hit, cov3d (gsplat layout) plus the
+    visibility mask.  Culled entries are zero, like gsplat's zero-initialised outputs."""
+    dt = means.dtype
+    vm = viewmat.reshape(-1)[:12].reshape(3, 4).to(dt)
+    Pm = projmat.reshape(4, 4).to(dt)
+    Wr, tv = vm[:, :3], vm[:, 3]
+    t = means @ Wr.T + tv
+    V = cov3d_full(scales, glob_scale, quats, quirks)
+    tan_fovx = 0.5 * W / fx
+    tan_fovy = 0.5 * H / fy
+    lim_x, lim_y = 1.3 * tan_fovx, 1.3 * tan_fovy
+    tz = t[:, 2]
+    txc = tz * torch.clamp(t[:, 0] / tz, -lim_x, lim_x)
+    tyc = tz * torch.clamp(t[:, 1] / tz, -lim_y, lim_y)
+
+    def jac(tx, ty):
+        z0 = torch.zeros_like(tz)
+        return torch.stack([
+            torch.stack([fx / tz, z0, -fx * tx / tz ** 2], -1),
+            torch.stack([z0, fy / tz, -fy * ty / tz ** 2], -1)], -2)
+
+    Jc = jac(txc, tyc)
+    if quirks:
+        Ju = jac(t[:, 0], t[:, 1])
+        J = Ju + (Jc - Ju).detach()
+    else:
+        J = Jc
+    T = J @ Wr
+    cov2 = T @ V @ T.transpose(-1, -2)
+    a = cov2[:, 0, 0] + 0.3
+    b = cov2[:, 1, 0]
+    c = cov2[:, 1, 1] + 0.3
+    det = a * c - b * b
+    conic = torch.stack([c / det, -b / det, a / det], -1)
+    with torch.no_grad():
+        bb = 0.5 * (a + c)
+        v1 = bb + torch.sqrt(torch.clamp(bb * bb - det, min=0.1))
+        v2 = bb - torch.sqrt(torch.clamp(bb * bb - det, min=0.1))
+        radius = torch.ceil(3 * torch.sqrt(torch.maximum(v1, v2)))
+    ph = torch.cat([means, torch.ones_like(means[:, :1])], -1) @ Pm.T
+    rw = 1.0 / (ph[:, 3] + 1e-6)
+    if quirks:
+        rw = rw.detach()
+    xy = torch.stack([0.5 * W * ph[:, 0] * rw + cx - 0.5, 0.5 * H * ph[:, 1] * rw + cy - 0.5],
+                     -1)
+    with torch.no_grad():
+        tcx, tcy = xy[:, 0] / BLOCK, xy[:, 1] / BLOCK
+        tr = radius / BLOCK
+        tbx, tby = tile_bounds[0], tile_bounds[1]
+        tminx = torch.clamp(torch.trunc(tcx - tr), 0, tbx)
+        tmaxx = torch.clamp(torch.trunc(tcx + tr + 1), 0, tbx)
+        tminy = torch.clamp(torch.trunc(tcy - tr), 0, tby)
+        tmaxy = torch.clamp(torch.trunc(tcy + tr + 1), 0, tby)
+        area = (tmaxx - tminx) * (tmaxy - tminy)
+        vis = (tz > clip_thresh) & (det != 0) & (area > 0)
+    m = vis.to(dt)[:, None]
+    cov3d = torch.stack([V[:, 0, 0], V[:, 1, 0], V[:, 2, 0], V[:, 1, 1], V[:, 2, 1], V[:, 2, 2]],
+                        -1)
+    radii = torch.where(vis, radius, torch.zeros_like(radius)).to(torch.int32)
+    nth = torch.where(vis, area, torch.zeros_like(area)).to(torch.int32)
+    depths = tz * m[:, 0]
+    return dict(xys=xy * m, depths=depths, radii=radii, conics=conic * m, num_tiles_hit=nth,
+                cov3d=cov3d * (tz > clip_thresh).to(dt)[:, None], visible=vis,
+                tile_min=(tminx, tminy), tile_max=(tmaxx, tmaxy))
+
+
+SH_C0 = 0.28209479177387814
+SH_C1 = 0.4886025119029199
+SH_C2 = [1.0925484305920792, -1.0925484305920792, 0.31539156525252005, -1.0925484305920792,
+         0.5462742152960396]
+SH_C3 = [-0.5900435899266435, 2.890611442640554, -0.4570457994644658, 0.3731763325901154,
+         -0.4570457994644658, 1.445305721320277, -0.5900435899266435]
+SH_C4 = [2.5033429417967046, -1.7701307697799304, 0.9461746957575601, -0.6690465435572892,
+         0.10578554691520431, -0.6690465435572892, 0.47308734787878004, -1.7701307697799304,
+         0.6258357354491761]
+
+
+def sh_basis(degree, dirs):
+    out = [torch.full_like(dirs[:, 0], SH_C0)]
+    if degree >= 1:
+        d = dirs / dirs.norm(dim=-1, keepdim=True)
+        x, y, z = d.unbind(-1)
+        xx, xy, xz, yy, yz, zz = x * x, x * y, x * z, y * y, y * z, z * z
+        out += [-SH_C1 * y, SH_C1 * z, -SH_C1 * x]
+        if degree >= 2:
+            out += [SH_C2[0] * xy, SH_C2[1] * yz, SH_C2[2] * (2 * zz - xx - yy), SH_C2[3] * xz,
+                    SH_C2[4] * (xx - yy)]
+        if degree >= 3:
+            out += [SH_C3[0] * y * (3 * xx - yy), SH_C3[1] * xy * z,
+                    SH_C3[2] * y * (4 * zz - xx - yy), SH_C3[3] * z * (2 * zz - 3 * xx - 3 * yy),
+                    SH_C3[4] * x * (4 * zz - xx - yy), SH_C3[5] * z * (xx - yy),
+                    SH_C3[6] * x * (xx - 3 * yy)]
+        if degree >= 4:
+            out += [SH_C4[0] * xy * (xx - yy), SH_C4[1] * yz * (3 * xx - yy),
+                    SH_C4[2] * xy * (7 * zz - 1), SH_C4[3] * yz * (7 * zz - 3),
+                    SH_C4[4] * (zz * (35 * zz - 30) + 3), SH_C4[5] * xz * (7 * zz - 3),
+                    SH_C4[6] * (xx - yy) * (7 * zz - 1), SH_C4[7] * xz * (xx - 3 * yy),
+                    SH_C4[8] * (xx * (xx - 3 * yy) - yy * (3 * xx - yy))]
+    return torch.stack(out, -1)
+
+
+def spherical_harmonics(degrees_to_use, viewdirs, coeffs):
+    """Viewdirs carry no gradient in gsplat (sh.py backward returns None for them)."""
+    b = sh_basis(degrees_to_use, viewdirs.detach())
+    nb = b.shape[-1]
+    return (b[:, :, None] * coeffs[:, :nb, :]).sum(1)
+
+
+def rasterize(xys, depths, radii, conics, num_tiles_hit, colors, opacity, H, W, background,
+              tile_min=None, tile_max=None):
+    """Naive per-pixel front-to-back compositing with gsplat 0.1.x rules.
+
+    Returns (img [H,W,C], alpha [H,W]).  Gaussians are visited in (depth, id) order,
+    which is each tile's sorted order; a pixel sees a Gaussian only if its tile lies in
+    the Gaussian's tile bbox (recomputed from xys/radii like map_gaussian_to_intersects).
+    """
+    dt = colors.dtype
+    C = colors.shape[1]
+    tbx, tby = (W + BLOCK - 1) // BLOCK, (H + BLOCK - 1) // BLOCK
+    iy, ix = torch.meshgrid(torch.arange(H), torch.arange(W), indexing="ij")
+    px, py = ix.reshape(-1).to(dt), iy.reshape(-1).to(dt)
+    ptx, pty = ix.reshape(-1) // BLOCK, iy.reshape(-1) // BLOCK
+    with torch.no_grad():
+        vis = radii > 0
+        ids = torch.nonzero(vis).reshape(-1)
+        order = torch.argsort(depths.detach()[ids].float(), stable=True)
+        ids = ids[order]
+        x32 = xys.detach().float()
+        r32 = radii.float()
+        tminx = torch.clamp(torch.trunc(x32[:, 0] / BLOCK - r32 / BLOCK), 0, tbx).long()
+        tmaxx = torch.clamp(torch.trunc(x32[:, 0] / BLOCK + r32 / BLOCK + 1), 0, tbx).long()
+        tminy = torch.clamp(torch.trunc(x32[:, 1] / BLOCK - r32 / BLOCK), 0, tby).long()
+        tmaxy = torch.clamp(torch.trunc(x32[:, 1] / BLOCK + r32 / BLOCK + 1), 0, tby).long()
+    P = H * W
+    T = torch.ones(P, dtype=dt)
+    done = torch.zeros(P, dtype=torch.bool)
+    acc = torch.zeros(P, C, dtype=dt)
+    for g in ids.tolist():
+        inb = ((ptx >= tminx[g]) & (ptx < tmaxx[g]) & (pty >= tminy[g]) & (pty < tmaxy[g])
+               & ~done)
+        if not bool(inb.any()):
+            continue
+        dx = xys[g, 0] - px
+        dy = xys[g, 1] - py
+        cn = conics[g]
+        sigma = 0.5 * (cn[0] * dx * dx + cn[2] * dy * dy) + cn[1] * dx * dy
+        alpha = torch.clamp(opacity.reshape(-1)[g] * torch.exp(-sigma), max=0.999)
+        ok = inb & ~(sigma < 0) & ~(alpha < 1.0 / 255.0)
+        next_T = T * (1 - alpha)
+        term = ok & (next_T <= 1e-4)
+        done = done | term
+        ok = ok & ~term
+        okf = ok.to(dt)
+        acc = acc + (colors[g][None, :] * (alpha * T)[:, None]) * okf[:, None]
+        T = torch.where(ok, next_T, T)
+    img = acc + T[:, None] * background.to(dt)[None, :]
+    return img.reshape(H, W, C), (1 - T).reshape(H, W)

@@ -1,0 +1,346 @@
+"""MI355X kernels (through the C ABI via the gsplat API) vs the CPU oracle.
+
+Bar (north_star): projection outputs, tile counts, intersection keys, sort order and tile
+bins bit-exact; images/alpha and every gradient within 1e-5 abs / 1e-4 rel (per element:
+|gpu - ref| <= 1e-5 + 1e-4 |ref|).  The forward blend uses the hardware exp on the GPU and
+libm expf on the CPU, so a pixel whose alpha lands within an ulp of a threshold (1/255,
+T <= 1e-4) may take the other branch; such pixels are counted and must stay rare
+(<= 0.1 %), everything else must meet the tolerance.
+"""
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+from gaussctrl_exp_amd import _lib
+from gaussctrl_exp_amd.camera import synthetic_camera
+from gaussctrl_exp_amd.project_gaussians import project_gaussians
+from gaussctrl_exp_amd.rasterize import bin_gaussians, rasterize_gaussians
+from gaussctrl_exp_amd.scene import render, synthetic_scene
+from gaussctrl_exp_amd.sh import spherical_harmonics
+from gaussctrl_exp_amd.utils import bin_and_sort_gaussians, compute_cov2d_bounds
+
+pytestmark = pytest.mark.gpu
+
+ATOL, RTOL = 1e-5, 1e-4
+
+
+def _close_frac(a, b, atol=ATOL, rtol=RTOL):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    bad = np.abs(a - b) > atol + rtol * np.abs(b)
+    return bad.mean() if bad.size else 0.0, (np.abs(a - b).max() if a.size else 0.0)
+
+
+def _np(t):
+    return t.detach().cpu().numpy()
+
+
+CASES = [
+    # (n, W, H, seed, scale_lo, scale_hi, extent)
+    (2000, 64, 48, 0, 0.01, 0.08, 1.5),       # ragged image (48 not a tile multiple)
+    (5000, 256, 256, 1, 0.005, 0.05, 1.5),
+    (20000, 512, 512, 2, 0.003, 0.03, 1.5),
+    (3000, 100, 75, 3, 0.02, 0.3, 4.0),       # large Gaussians, some behind the camera
+]
+
+
+def _inputs(n, W, H, seed, lo, hi, ext):
+    sc = synthetic_scene(n, 3, seed=seed, scale_lo=lo, scale_hi=hi, extent=ext)
+    cam = synthetic_camera(W, H)
+    scales = torch.exp(sc.scales)
+    quats = sc.quats / sc.quats.norm(dim=-1, keepdim=True)
+    return sc, cam, scales, quats
+
+
+def _project_both(gpu, sc, cam, scales, quats):
+    args = (cam.fx, cam.fy, cam.cx, cam.cy, cam.height, cam.width, cam.tile_bounds)
+    g = project_gaussians(sc.means.to(gpu), scales.to(gpu), 1, quats.to(gpu),
+                          cam.viewmat.to(gpu), cam.projmat.to(gpu), *args)
+    o = O.project_forward(sc.means.numpy(), scales.numpy(), 1.0, quats.numpy(),
+                          cam.viewmat.numpy(), cam.projmat.numpy(), *args)
+    return g, o
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_project_forward_bitexact(gpu, case):
+    sc, cam, scales, quats = _inputs(*case)
+    g, o = _project_both(gpu, sc, cam, scales, quats)
+    names = ["xys", "depths", "radii", "conics", "num_tiles_hit", "cov3d"]
+    for name, gt, ot in zip(names, g, o):
+        np.testing.assert_array_equal(_np(gt), ot, err_msg=name)
+    assert (o[2] > 0).sum() > 0
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_project_backward(gpu, case):
+    sc, cam, scales, quats = _inputs(*case)
+    n = sc.num_points
+    gen = torch.Generator().manual_seed(11)
+    v_xy, v_d, v_c = torch.randn(n, 2, generator=gen), torch.randn(n, generator=gen), \
+        torch.randn(n, 3, generator=gen)
+    m, s, q = [t.to(gpu).requires_grad_() for t in (sc.means, scales, quats)]
+    args = (cam.fx, cam.fy, cam.cx, cam.cy, cam.height, cam.width, cam.tile_bounds)
+    xys, depths, radii, conics, nth, cov3d = project_gaussians(
+        m, s, 1, q, cam.viewmat.to(gpu), cam.projmat.to(gpu), *args)
+    ((xys * v_xy.to(gpu)).sum() + (depths * v_d.to(gpu)).sum() +
+     (conics * v_c.to(gpu)).sum()).backward()
+    o = O.project_forward(sc.means.numpy(), scales.numpy(), 1.0, quats.numpy(),
+                          cam.viewmat.numpy(), cam.projmat.numpy(), *args)
+    ob = O.project_backward(sc.means.numpy(), scales.numpy(), 1.0, quats.numpy(),
+                            cam.viewmat.numpy(), cam.projmat.numpy(), cam.fx, cam.fy, cam.cx,
+                            cam.cy, cam.height, cam.width, o[5], o[2], o[3], v_xy.numpy(),
+                            v_d.numpy(), v_c.numpy())
+    for name, gt, ot in (("means", m.grad, ob[2]), ("scales", s.grad, ob[3]),
+                         ("quats", q.grad, ob[4])):
+        frac, mx = _close_frac(_np(gt), ot)
+        assert frac == 0.0, f"{name}: {frac:.2e} of elements out of tolerance (max {mx:.3e})"
+
+
+@pytest.mark.parametrize("degree,use", [(0, 0), (1, 1), (2, 2), (3, 3), (3, 0), (3, 2),
+                                        (4, 4)])
+def test_sh(gpu, degree, use):
+    gen = torch.Generator().manual_seed(degree * 7 + use)
+    for n in (1, 255, 1000, 4097):
+        K = (degree + 1) ** 2
+        dirs, coeffs = torch.randn(n, 3, generator=gen), torch.randn(n, K, 3, generator=gen)
+        v = torch.randn(n, 3, generator=gen)
+        c = coeffs.to(gpu).requires_grad_()
+        out = spherical_harmonics(use, dirs.to(gpu), c)
+        (out * v.to(gpu)).sum().backward()
+        ref = O.sh_forward(use, dirs.numpy(), coeffs.numpy())
+        vref = O.sh_backward(use, dirs.numpy(), v.numpy(), K)
+        frac, mx = _close_frac(_np(out), ref)
+        assert frac == 0.0, f"sh fwd n={n}: max err {mx}"
+        frac, mx = _close_frac(_np(c.grad), vref)
+        assert frac == 0.0, f"sh bwd n={n}: max err {mx}"
+
+
+def test_sh_unaligned_slab(gpu):
+    """Coefficient slabs that do not start 16-byte aligned take the dword copy path."""
+    gen = torch.Generator().manual_seed(5)
+    base = torch.randn(1 + 300 * 9 * 3, generator=gen)
+    coeffs = base[1:].reshape(300, 9, 3)
+    dirs = torch.randn(300, 3, generator=gen)
+    cg = base.to(gpu)[1:].reshape(300, 9, 3)
+    out = spherical_harmonics(2, dirs.to(gpu), cg)
+    np.testing.assert_allclose(_np(out), O.sh_forward(2, dirs.numpy(), coeffs.numpy()),
+                               rtol=RTOL, atol=ATOL)
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_binning_fused_bitexact(gpu, case):
+    sc, cam, scales, quats = _inputs(*case)
+    g, o = _project_both(gpu, sc, cam, scales, quats)
+    xys, depths, radii, conics, nth, cov3d = g
+    I, gids, bins = bin_gaussians(xys, depths, radii, nth, cam.height, cam.width)
+    ref = O.bin_and_sort(o[0], o[1], o[2], o[4], cam.tile_bounds)
+    assert I == ref["num_intersects"]
+    np.testing.assert_array_equal(_np(gids), ref["gaussian_ids_sorted"])
+    np.testing.assert_array_equal(_np(bins), ref["tile_bins"])
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_binning_utils_bitexact(gpu, case):
+    sc, cam, scales, quats = _inputs(*case)
+    g, o = _project_both(gpu, sc, cam, scales, quats)
+    xys, depths, radii, conics, nth, cov3d = g
+    cum = torch.cumsum(nth, 0, dtype=torch.int32)
+    I = int(cum[-1].item())
+    isect, gid, isect_s, gid_s, bins = bin_and_sort_gaussians(
+        sc.num_points, I, xys, depths, radii, cum, cam.tile_bounds)
+    ref = O.bin_and_sort(o[0], o[1], o[2], o[4], cam.tile_bounds)
+    np.testing.assert_array_equal(_np(isect), ref["isect_ids"])
+    np.testing.assert_array_equal(_np(gid), ref["gaussian_ids"])
+    np.testing.assert_array_equal(_np(isect_s), ref["isect_ids_sorted"])
+    np.testing.assert_array_equal(_np(gid_s), ref["gaussian_ids_sorted"])
+    T = cam.tile_bounds[0] * cam.tile_bounds[1]
+    np.testing.assert_array_equal(_np(bins)[:T], ref["tile_bins"])
+    assert not _np(bins)[T:].any()
+
+
+def test_cov2d_bounds(gpu):
+    gen = torch.Generator().manual_seed(3)
+    a = torch.rand(1000, generator=gen) * 10 + 0.1
+    c = torch.rand(1000, generator=gen) * 10 + 0.1
+    b = (torch.rand(1000, generator=gen) * 2 - 1) * torch.sqrt(a * c) * 0.9
+    cov = torch.stack([a, b, c], 1)
+    cov[0] = torch.tensor([1.0, 1.0, 1.0])  # det == 0
+    conics, radii = compute_cov2d_bounds(cov.to(gpu))
+    rc, rr = O.cov2d_bounds(cov.numpy())
+    np.testing.assert_array_equal(_np(conics), rc)
+    np.testing.assert_array_equal(_np(radii), rr)
+
+
+def _raster_case(gpu, case, C=3, colors_u8=False):
+    sc, cam, scales, quats = _inputs(*case)
+    g, o = _project_both(gpu, sc, cam, scales, quats)
+    n = sc.num_points
+    gen = torch.Generator().manual_seed(case[3] + 50)
+    colors = torch.rand(n, C, generator=gen)
+    if colors_u8:
+        colors = (colors * 255).to(torch.uint8)
+    opac = torch.sigmoid(sc.opacities)
+    bg = torch.rand(C, generator=gen)
+    return sc, cam, g, o, colors, opac, bg
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_raster_forward(gpu, case):
+    sc, cam, g, o, colors, opac, bg = _raster_case(gpu, case)
+    xys, depths, radii, conics, nth, cov3d = g
+    img, alpha = rasterize_gaussians(xys, depths, radii, conics, nth, colors.to(gpu),
+                                     opac.to(gpu), cam.height, cam.width, bg.to(gpu),
+                                     return_alpha=True)
+    f = O.render_forward(o[0], o[1], o[2], o[3], o[4], colors.numpy(), opac.numpy(),
+                         cam.height, cam.width, bg.numpy())
+    fi, mi = _close_frac(_np(img), f["img"])
+    fa, ma = _close_frac(_np(alpha), f["alpha"])
+    assert fi <= 1e-3 and fa <= 1e-3, (fi, mi, fa, ma)
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_raster_backward(gpu, case):
+    """Backward kernel parity, fed the GPU forward state (final_Ts / final_idx) so a forward
+    threshold flip cannot leak into the gradient comparison."""
+    sc, cam, g, o, colors, opac, bg = _raster_case(gpu, case)
+    xys, depths, radii, conics, nth, cov3d = [t.detach() for t in g]
+    H, W = cam.height, cam.width
+    gen = torch.Generator().manual_seed(77)
+    v_img = torch.randn(H, W, 3, generator=gen)
+    v_alpha = torch.randn(H, W, generator=gen)
+    xy = xys.clone().requires_grad_()
+    cn = conics.clone().requires_grad_()
+    col = colors.to(gpu).requires_grad_()
+    op = opac.to(gpu).requires_grad_()
+    img, alpha = rasterize_gaussians(xy, depths, radii, cn, nth, col, op, H, W, bg.to(gpu),
+                                     return_alpha=True)
+    ((img * v_img.to(gpu)).sum() + (alpha * v_alpha.to(gpu)).sum()).backward()
+    # oracle backward on the GPU's forward state
+    I, gids, bins = bin_gaussians(xys, depths, radii, nth, H, W)
+    from gaussctrl_exp_amd import rasterize as R
+    tb = cam.tile_bounds
+    out = torch.empty(H, W, 3, device=gpu)
+    fT = torch.empty(H, W, device=gpu)
+    fi = torch.empty(H, W, device=gpu, dtype=torch.int32)
+    P = _lib.ptr
+    _lib.call("gsplat_rasterize_forward", tb[0], tb[1], H, W, 3, P(gids), P(bins), P(xys),
+              P(conics), P(col.detach()), P(op.detach()), P(bg.to(gpu)), P(out), P(fT), P(fi),
+              _lib.stream(gpu))
+    ref = O.rasterize_backward(tb, H, W, _np(gids), _np(bins), _np(xys), _np(conics),
+                               colors.numpy(), opac.numpy(), bg.numpy(), _np(fT), _np(fi),
+                               v_img.numpy(), v_alpha.numpy(), alpha_max=R.BACKWARD_ALPHA_CLAMP)
+    for name, gt, rt in (("xys", xy.grad, ref[0]), ("conics", cn.grad, ref[1]),
+                         ("colors", col.grad, ref[2]), ("opacity", op.grad, ref[3])):
+        frac, mx = _close_frac(_np(gt), rt.reshape(gt.shape))
+        assert frac == 0.0, f"{name}: {frac:.2e} out of tolerance (max {mx:.3e})"
+
+
+@pytest.mark.parametrize("C", [1, 4, 7])
+def test_nd_rasterize(gpu, C):
+    case = CASES[1]
+    sc, cam, g, o, colors, opac, bg = _raster_case(gpu, case, C=C)
+    xys, depths, radii, conics, nth, cov3d = [t.detach() for t in g]
+    H, W = cam.height, cam.width
+    col = colors.to(gpu).requires_grad_()
+    op = opac.to(gpu).requires_grad_()
+    img, alpha = rasterize_gaussians(xys, depths, radii, conics, nth, col, op, H, W,
+                                     bg.to(gpu), return_alpha=True)
+    f = O.render_forward(o[0], o[1], o[2], o[3], o[4], colors.numpy(), opac.numpy(), H, W,
+                         bg.numpy())
+    fr, mx = _close_frac(_np(img), f["img"])
+    assert fr <= 1e-3, (fr, mx)
+    gen = torch.Generator().manual_seed(8)
+    v_img = torch.randn(H, W, C, generator=gen)
+    (img * v_img.to(gpu)).sum().backward()
+    ref = O.render_backward(f, o[0], o[3], colors.numpy(), opac.numpy(), bg.numpy(),
+                            v_img.numpy(), np.zeros((H, W), np.float32))
+    frac, mx = _close_frac(_np(col.grad), ref[2])
+    assert frac <= 1e-3, (frac, mx)
+
+
+def test_uint8_colors(gpu):
+    sc, cam, g, o, colors, opac, bg = _raster_case(gpu, CASES[0], colors_u8=True)
+    xys, depths, radii, conics, nth, cov3d = g
+    img = rasterize_gaussians(xys, depths, radii, conics, nth, colors.to(gpu), opac.to(gpu),
+                              cam.height, cam.width, bg.to(gpu))
+    f = O.render_forward(o[0], o[1], o[2], o[3], o[4], colors.numpy().astype(np.float32) / 255,
+                         opac.numpy(), cam.height, cam.width, bg.numpy())
+    assert _close_frac(_np(img), f["img"])[0] <= 1e-3
+
+
+def test_empty_scene(gpu):
+    """All Gaussians behind the camera: I = 0 -> background image, alpha = 1,
+    zero gradients."""
+    sc, cam, scales, quats = _inputs(500, 64, 64, 0, 0.01, 0.05, 1.0)
+    means = sc.means.clone()
+    means[:, 2] += 10.0  # camera at z=4 looking down -z: everything behind it
+    xys, depths, radii, conics, nth, cov3d = project_gaussians(
+        means.to(gpu), scales.to(gpu), 1, quats.to(gpu), cam.viewmat.to(gpu),
+        cam.projmat.to(gpu), cam.fx, cam.fy, cam.cx, cam.cy, 64, 64, cam.tile_bounds)
+    assert int(radii.sum()) == 0
+    col = torch.rand(500, 3, device=gpu, requires_grad=True)
+    op = torch.rand(500, 1, device=gpu, requires_grad=True)
+    bg = torch.tensor([0.1, 0.2, 0.3], device=gpu)
+    img, alpha = rasterize_gaussians(xys, depths, radii, conics, nth, col, op, 64, 64, bg,
+                                     return_alpha=True)
+    assert torch.allclose(img, bg.expand(64, 64, 3))
+    assert torch.all(alpha == 1)
+    (img.sum() + alpha.sum()).backward()
+    assert float(col.grad.abs().sum()) == 0 and float(op.grad.abs().sum()) == 0
+
+
+def test_single_gaussian_ragged(gpu):
+    means = torch.tensor([[0.05, -0.02, 0.0]])
+    scales = torch.tensor([[0.05, 0.03, 0.02]])
+    quats = torch.tensor([[0.9, 0.1, 0.2, 0.3]])
+    quats = quats / quats.norm()
+    cam = synthetic_camera(37, 29)
+    args = (cam.fx, cam.fy, cam.cx, cam.cy, cam.height, cam.width, cam.tile_bounds)
+    g = project_gaussians(means.to(gpu), scales.to(gpu), 1, quats.to(gpu), cam.viewmat.to(gpu),
+                          cam.projmat.to(gpu), *args)
+    o = O.project_forward(means.numpy(), scales.numpy(), 1.0, quats.numpy(),
+                          cam.viewmat.numpy(), cam.projmat.numpy(), *args)
+    for gt, ot in zip(g, o):
+        np.testing.assert_array_equal(_np(gt), ot)
+    col = torch.tensor([[0.2, 0.5, 0.9]])
+    op = torch.tensor([[0.8]])
+    img = rasterize_gaussians(*g[:5], col.to(gpu), op.to(gpu), 29, 37)
+    f = O.render_forward(o[0], o[1], o[2], o[3], o[4], col.numpy(), op.numpy(), 29, 37,
+                         np.ones(3, np.float32))
+    assert _close_frac(_np(img), f["img"])[0] <= 1e-3
+
+
+def test_end_to_end_render_grads(gpu):
+    """scene.render (gc_model.get_outputs restated) on the GPU vs the same caller code on
+    the oracle-backed gsplat emulation: image, alpha, depth and all 6 parameter grads."""
+    from oracle_gsplat import API
+    sc = synthetic_scene(3000, 3, seed=21, scale_lo=0.01, scale_hi=0.06)
+    cam = synthetic_camera(128, 96)
+    bg = torch.tensor([0.3, 0.6, 0.9])
+    gen = torch.Generator().manual_seed(4)
+    gt = torch.rand(96, 128, 3, generator=gen)
+    results = {}
+    for name, dev, api in (("gpu", gpu, None), ("ref", torch.device("cpu"), API)):
+        s = sc.to(dev).requires_grad_()
+        c = cam.to(dev)
+        out = render(s, c, 3, bg.to(dev), api=api)
+        loss = (out["rgb"] - gt.to(dev)).abs().mean() + 0.1 * out["accumulation"].mean()
+        loss.backward()
+        with torch.no_grad():
+            dep = render(s, c, 3, bg.to(dev), return_depth=True, api=api)["depth"]
+        results[name] = [_np(out["rgb"]), _np(out["accumulation"]), _np(dep)] + \
+                        [_np(p.grad) for p in s.params()]
+    names = ["rgb", "alpha", "depth", "means", "scales", "quats", "opacities", "features_dc",
+             "features_rest"]
+    for i, name in enumerate(names):
+        frac, mx = _close_frac(results["gpu"][i], results["ref"][i])
+        assert frac <= 2e-3, f"{name}: {frac:.2e} out of tolerance (max {mx:.3e})"
+
+
+def test_c_abi_rejects_cpu_tensors():
+    sc = synthetic_scene(10)
+    cam = synthetic_camera(32, 32)
+    with pytest.raises(RuntimeError, match="ROCm device"):
+        project_gaussians(sc.means, torch.exp(sc.scales), 1, sc.quats, cam.viewmat,
+                          cam.projmat, cam.fx, cam.fy, cam.cx, cam.cy, 32, 32,
+                          cam.tile_bounds)
