@@ -82,7 +82,7 @@ def cpu_baseline(scene, cam, sh_degree, budget_tiles=64, seed=0):
     import oracle as O
     O.build()
     rng = np.random.default_rng(seed)
-    sc = scene.to("cpu")
+    sc = scene.detach().to("cpu")
     means = sc.means.numpy()
     scales = torch.exp(sc.scales).numpy()
     quats = (sc.quats / sc.quats.norm(dim=-1, keepdim=True)).numpy()

@@ -609,8 +609,15 @@ void oracle_rasterize_backward(int tbx, int tby, int H, int W, int C, int num_po
                                const float *bg, const float *final_Ts, const int *final_idx,
                                const float *v_out, const float *v_out_alpha, float alpha_max,
                                const int *tile_list, int num_tile_list, float *v_xy,
-                               float *v_conic, float *v_colors, float *v_opacity) {
+                               float *v_conic, float *v_colors, float *v_opacity,
+                               float *abs_sum) {
+    /* abs_sum (optional, [num_points, 6+C] in the order xy0 xy1 con0 con1 con2 opac colors):
+     * the sum of |term| over the per-pixel contributions of each gradient element -- the
+     * scale of the fp32 summation error any implementation accumulating in fp32 incurs. */
     double *acc = (double *)calloc((size_t)num_points * (9 + (size_t)C), sizeof(double));
+    double *aacc = abs_sum ? (double *)calloc((size_t)num_points * (9 + (size_t)C),
+                                              sizeof(double))
+                           : NULL;
     /* per Gaussian: [xy0 xy1 con0 con1 con2 opac | C colors] */
     const int S = 6 + C;
     int ntiles = tile_list ? num_tile_list : tbx * tby;
@@ -647,8 +654,10 @@ void oracle_rasterize_backward(int tbx, int tby, int H, int W, int C, int num_po
                     float v_alpha = 0.f;
                     const float *rgb = colors + (size_t)C * g;
                     double *a = acc + (size_t)g * S;
+                    double *aa = aacc ? aacc + (size_t)g * S : NULL;
                     for (int c = 0; c < C; ++c) {
                         a[6 + c] += (double)(fac * vo[c]);
+                        if (aa) aa[6 + c] += fabs((double)(fac * vo[c]));
                         v_alpha += (rgb[c] * T - buf[c] * ra) * vo[c];
                     }
                     v_alpha += T_final * ra * va_out;
@@ -661,6 +670,14 @@ void oracle_rasterize_backward(int tbx, int tby, int H, int W, int C, int num_po
                     a[3] += (double)(0.5f * v_sigma * dx * dy);
                     a[4] += (double)(0.5f * v_sigma * dy * dy);
                     a[5] += (double)(vis * v_alpha);
+                    if (aa) {
+                        aa[0] += fabs((double)(v_sigma * (cn[0] * dx + cn[1] * dy)));
+                        aa[1] += fabs((double)(v_sigma * (cn[1] * dx + cn[2] * dy)));
+                        aa[2] += fabs((double)(0.5f * v_sigma * dx * dx));
+                        aa[3] += fabs((double)(0.5f * v_sigma * dx * dy));
+                        aa[4] += fabs((double)(0.5f * v_sigma * dy * dy));
+                        aa[5] += fabs((double)(vis * v_alpha));
+                    }
                 }
             }
     }
@@ -673,6 +690,9 @@ void oracle_rasterize_backward(int tbx, int tby, int H, int W, int C, int num_po
         v_conic[3 * g + 2] = (float)a[4];
         v_opacity[g] = (float)a[5];
         for (int c = 0; c < C; ++c) v_colors[(size_t)C * g + c] = (float)a[6 + c];
+        if (aacc)
+            for (int k = 0; k < S; ++k) abs_sum[(size_t)g * S + k] = (float)aacc[(size_t)g * S + k];
     }
     free(acc);
+    free(aacc);
 }

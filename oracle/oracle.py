@@ -185,7 +185,9 @@ def rasterize_forward(tile_bounds, H, W, gids_sorted, tile_bins, xys, conics, co
 
 def rasterize_backward(tile_bounds, H, W, gids_sorted, tile_bins, xys, conics, colors,
                        opacity, background, final_Ts, final_idx, v_out, v_out_alpha,
-                       alpha_max=0.99, tile_list=None):
+                       alpha_max=0.99, tile_list=None, return_abs=False):
+    """Returns (v_xy, v_conic, v_colors, v_opacity) [+ abs-sum tuple of the same shapes:
+    sum over pixels of |contribution|, the fp32 accumulation-error scale]."""
     colors = _f(colors)
     n, C = colors.shape
     v_xy = np.zeros((n, 2), np.float32)
@@ -193,6 +195,7 @@ def rasterize_backward(tile_bounds, H, W, gids_sorted, tile_bins, xys, conics, c
     v_colors = np.zeros((n, C), np.float32)
     v_opac = np.zeros((n, 1), np.float32)
     tl = None if tile_list is None else np.ascontiguousarray(tile_list, np.int32)
+    absum = np.zeros((n, 6 + C), np.float32) if return_abs else None
     lib().oracle_rasterize_backward(
         int(tile_bounds[0]), int(tile_bounds[1]), int(H), int(W), C, n,
         _p(np.ascontiguousarray(gids_sorted, np.int32)),
@@ -200,7 +203,10 @@ def rasterize_backward(tile_bounds, H, W, gids_sorted, tile_bins, xys, conics, c
         _p(colors), _p(_f(opacity).reshape(-1)), _p(_f(background)), _p(_f(final_Ts)),
         _p(np.ascontiguousarray(final_idx, np.int32)), _p(_f(v_out)), _p(_f(v_out_alpha)),
         ctypes.c_float(alpha_max), _p(tl), 0 if tl is None else tl.shape[0], _p(v_xy),
-        _p(v_conic), _p(v_colors), _p(v_opac))
+        _p(v_conic), _p(v_colors), _p(v_opac), _p(absum))
+    if return_abs:
+        return (v_xy, v_conic, v_colors, v_opac), (absum[:, 0:2], absum[:, 2:5], absum[:, 6:],
+                                                    absum[:, 5:6])
     return v_xy, v_conic, v_colors, v_opac
 
 
