@@ -1,5 +1,6 @@
-// binning.hip -- tile binning for gfx950: device scan, stable LSD radix sort, fused
-// depth-ordered intersection emission, tile bin edges, and the gsplat-layout utilities.
+// binning.hip -- tile binning for gfx950: device scan, stable one-sweep LSD radix sort,
+// fused depth-ordered intersection emission, tile bin edges, and the gsplat-layout
+// utilities.
 //
 // Replaces, inside rasterize.py _RasterizeGaussians.forward (gsplat 0.1.2.1, reached from
 // /root/reference/gaussctrl/gc_model.py:208-220 and :225-236):
@@ -9,26 +10,35 @@
 //     tile_bins = _C.get_tile_bin_edges(I, isect_ids_sorted)
 //
 // MI355X design (integer work, HBM-bound -- no MFMA):
-//   The 64-bit key (tile << 32 | depth_bits) sort of gsplat moves 12 B per intersection
-//   through ~6 eight-bit LSD passes.  Sorting by depth first -- N keys of 32 bits, N << I
-//   -- and then stably by tile id -- ceil(log2(T+1)) <= 16 bits, two passes over I --
-//   yields the identical order (ties by Gaussian id, as a stable sort of gsplat's keys)
-//   while moving ~3.5x fewer bytes.  The emission of (tile, id) pairs happens directly in
-//   depth order, and tile_bins falls out of the tile-sorted keys.
-//
-//   Radix pass = per-workgroup digit histogram (LDS atomics) -> device exclusive scan of
-//   the [256][nblocks] histogram -> stable scatter whose in-wave rank comes from eight
-//   wave64 ballots (a 64-lane match of the 8-bit digit).
+//   * gsplat sorts I 64-bit keys (tile << 32 | depth_bits).  Sorting the N visible depths
+//     first (32-bit keys, N << I) and then the I intersections stably by tile id
+//     (ceil(log2(T+1)) <= 16 bits, two passes) gives the identical order -- ties by Gaussian
+//     id, as a stable sort of gsplat's keys -- while moving ~3.5x fewer bytes.
+//   * Radix sort = one histogram kernel for all digit passes (one read of the keys), then
+//     ONE kernel per pass: each workgroup takes a 4096-key tile by ticket, ranks it stably in
+//     LDS (wave64 ballot match of the digit, per-wave LDS counters), publishes its digit
+//     counts, obtains its global offsets by decoupled look-back over the preceding tiles'
+//     tagged status words (agent-scope relaxed atomics, bounded spins), and writes the
+//     tile out from LDS in digit order so each digit's run is written by consecutive lanes.
+//     Digit width is ceil(bits / passes), so a 13-bit tile key takes two 7-bit passes.
+//   * Emission: one wave per 64 depth-ordered Gaussians fills their combined slot range
+//     with lanes striding over it (owner found by a 6-step shuffle search), so the
+//     (tile, id) stores are coalesced.
 #include "common.h"
 
 namespace gs {
 namespace {
 
 constexpr int TPB = 256;
-constexpr int RS_ITEMS = 16;
-constexpr int RS_TILE = TPB * RS_ITEMS;  // keys per radix workgroup
 constexpr int SC_ITEMS = 16;
 constexpr int SC_TILE = TPB * SC_ITEMS;  // elements per scan workgroup
+constexpr int OS_ITEMS = 16;
+constexpr int OS_TILE = TPB * OS_ITEMS;  // keys per sort workgroup
+constexpr int OS_MAX_PASSES = 8;
+constexpr uint32_t ST_AGG = 1u << 30;    // status word: aggregate of this tile only
+constexpr uint32_t ST_PRE = 2u << 30;    // status word: inclusive prefix up to this tile
+constexpr uint32_t ST_VAL = (1u << 30) - 1u;
+constexpr uint32_t SPIN_LIMIT = 1u << 24;
 
 // ------------------------------------------------------------------ block scan helpers
 
@@ -113,10 +123,6 @@ __global__ __launch_bounds__(TPB) void scan_downsweep_kernel(const uint32_t *in,
   }
 }
 
-struct ScanWs {
-  uint32_t *partial;  // cdiv(m, SC_TILE) entries
-};
-
 size_t scan_ws_bytes(long long m) { return (size_t)(cdiv(m, SC_TILE) + 1) * sizeof(uint32_t); }
 
 // Exclusive scan of in[0..m) into out (in place allowed); total (device) optional.
@@ -132,114 +138,217 @@ void device_exclusive_scan(const uint32_t *in, uint32_t *out, long long m, uint3
   hipLaunchKernelGGL(scan_downsweep_kernel, dim3(nb), dim3(TPB), 0, st, in, m, partial, out);
 }
 
-// ------------------------------------------------------------------------ radix sort
+// ------------------------------------------------------------ one-sweep radix sort
 
-template <typename K>
-__global__ __launch_bounds__(TPB) void rs_upsweep_kernel(const K *__restrict__ keys, long long n,
-                                                         int shift, int nblocks,
-                                                         uint32_t *__restrict__ hist) {
-  __shared__ uint32_t cnt[4][256];
-  const int tid = threadIdx.x, wave = tid >> 6;
-#pragma unroll
-  for (int w = 0; w < 4; ++w) cnt[w][tid] = 0;
-  __syncthreads();
-  const long long base = (long long)blockIdx.x * RS_TILE;
-#pragma unroll 4
-  for (int r = 0; r < RS_ITEMS; ++r) {
-    long long i = base + r * TPB + tid;
-    if (i < n) {
-      uint32_t d = (uint32_t)(keys[i] >> shift) & 255u;
-      atomicAdd(&cnt[wave][d], 1u);
-    }
-  }
-  __syncthreads();
-  hist[(size_t)tid * nblocks + blockIdx.x] = cnt[0][tid] + cnt[1][tid] + cnt[2][tid] + cnt[3][tid];
+struct SortPlan {
+  int passes, width, radix;
+  long long nblocks;
+};
+
+SortPlan sort_plan(long long n, int begin_bit, int end_bit) {
+  SortPlan p;
+  int bits = end_bit - begin_bit;
+  p.passes = bits <= 0 ? 0 : (bits + 7) / 8;
+  p.width = p.passes ? (bits + p.passes - 1) / p.passes : 0;
+  p.radix = 1 << p.width;
+  p.nblocks = n > 0 ? cdiv(n, OS_TILE) : 0;
+  return p;
+}
+
+// Workspace: [hist: MAX_PASSES x 256][tickets: MAX_PASSES][error][pad] | status[passes][nblocks][radix]
+constexpr size_t OS_HEAD_WORDS = OS_MAX_PASSES * 256 + OS_MAX_PASSES + 8;
+
+size_t radix_ws_bytes(long long n, int begin_bit, int end_bit) {
+  SortPlan p = sort_plan(n, begin_bit, end_bit);
+  return (OS_HEAD_WORDS + (size_t)p.passes * p.nblocks * p.radix) * sizeof(uint32_t);
 }
 
 template <typename K>
-__global__ __launch_bounds__(TPB) void rs_downsweep_kernel(
-    const K *__restrict__ kin, const uint32_t *__restrict__ vin, K *__restrict__ kout,
-    uint32_t *__restrict__ vout, long long n, int shift, int nblocks,
-    const uint32_t *__restrict__ hist_scanned) {
-  __shared__ uint32_t digit_base[256];
-  __shared__ uint32_t wcnt[4][256];
-  __shared__ uint32_t woff[4][256];
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  digit_base[tid] = hist_scanned[(size_t)tid * nblocks + blockIdx.x];
-#pragma unroll
-  for (int w = 0; w < 4; ++w) wcnt[w][tid] = 0;
+__global__ __launch_bounds__(TPB) void os_hist_kernel(const K *__restrict__ keys, long long n,
+                                                      int begin_bit, int width, int passes,
+                                                      uint32_t *__restrict__ hist) {
+  __shared__ uint32_t lh[OS_MAX_PASSES * 256];
+  const int R = 1 << width;
+  for (int i = threadIdx.x; i < passes * 256; i += TPB) lh[i] = 0;
   __syncthreads();
-  const unsigned long long lt = (1ull << lane) - 1ull;
-  const long long base = (long long)blockIdx.x * RS_TILE;
-  for (int r = 0; r < RS_ITEMS; ++r) {
-    const long long i = base + r * TPB + tid;
-    const bool valid = i < n;
-    K key = valid ? kin[i] : (K)0;
-    uint32_t val = valid ? vin[i] : 0u;
-    const uint32_t d = (uint32_t)(key >> shift) & 255u;
-    unsigned long long peers = __ballot(valid);
+  for (long long i = (long long)blockIdx.x * TPB + threadIdx.x; i < n;
+       i += (long long)gridDim.x * TPB) {
+    const K k = keys[i];
+    for (int p = 0; p < passes; ++p) {
+      const uint32_t d = (uint32_t)(k >> (begin_bit + p * width)) & (uint32_t)(R - 1);
+      atomicAdd(&lh[p * 256 + d], 1u);
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < passes * 256; i += TPB)
+    if (lh[i]) atomicAdd(&hist[i], lh[i]);
+}
+
+template <typename K>
+struct OsSmem {
+  K keys[OS_TILE];
+  uint32_t vals[OS_TILE];
+  uint32_t wcnt[4][256];   // per-wave digit counters, then per-wave digit offsets
+  uint32_t loc_off[256];   // tile-local exclusive offset of each digit
+  uint32_t gofs[256];      // global output offset of each digit, minus loc_off
+  uint32_t hscan[256];     // exclusive scan of this pass's global histogram
+  uint32_t scan_tmp[4];
+  uint32_t ticket;
+};
+
+template <typename K>
+__global__ __launch_bounds__(TPB) void os_pass_kernel(
+    const K *__restrict__ kin, const uint32_t *__restrict__ vin, K *__restrict__ kout,
+    uint32_t *__restrict__ vout, long long n, int shift, int width,
+    const uint32_t *__restrict__ hist, uint32_t *__restrict__ ticket_ctr,
+    uint32_t *__restrict__ status, uint32_t *__restrict__ err) {
+  __shared__ OsSmem<K> sm;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int R = 1 << width;
+  const uint32_t dmask = (uint32_t)(R - 1);
+  if (tid == 0) sm.ticket = atomicAdd(ticket_ctr, 1u);
 #pragma unroll
-    for (int b = 0; b < 8; ++b) {
+  for (int w = 0; w < 4; ++w) sm.wcnt[w][tid] = 0;
+  {
+    uint32_t h = tid < R ? hist[tid] : 0u, tot;
+    sm.hscan[tid] = block_exclusive_scan<TPB>(h, tot, sm.scan_tmp);  // contains barriers
+  }
+  const uint32_t t = sm.ticket;
+  const long long base = (long long)t * OS_TILE;
+  const long long seg = base + (long long)wave * (OS_ITEMS * 64);
+  const unsigned long long lt = (1ull << lane) - 1ull;
+
+  K key[OS_ITEMS];
+  uint32_t val[OS_ITEMS], rank[OS_ITEMS];
+#pragma unroll
+  for (int r = 0; r < OS_ITEMS; ++r) {
+    const long long i = seg + r * 64 + lane;
+    const bool valid = i < n;
+    key[r] = valid ? kin[i] : (K)0;
+    val[r] = valid ? vin[i] : 0u;
+  }
+#pragma unroll
+  for (int r = 0; r < OS_ITEMS; ++r) {
+    const bool valid = seg + r * 64 + lane < n;
+    const uint32_t d = (uint32_t)(key[r] >> shift) & dmask;
+    unsigned long long peers = __ballot(valid);
+    for (int b = 0; b < width; ++b) {
       const bool bit = (d >> b) & 1u;
       const unsigned long long m = __ballot(bit);
       peers &= bit ? m : ~m;
     }
-    const uint32_t rank = (uint32_t)__popcll(peers & lt);
-    if (valid && rank == 0) wcnt[wave][d] = (uint32_t)__popcll(peers);
-    __syncthreads();
-    {
-      uint32_t s = digit_base[tid];
+    const uint32_t old = sm.wcnt[wave][d];
+    rank[r] = old + (uint32_t)__popcll(peers & lt);
+    __builtin_amdgcn_wave_barrier();
+    if (valid && (peers & lt) == 0) sm.wcnt[wave][d] = old + (uint32_t)__popcll(peers);
+    __builtin_amdgcn_wave_barrier();
+  }
+  __syncthreads();
+  uint32_t local_count = 0;
+  {
+    uint32_t s = 0;
 #pragma unroll
-      for (int w = 0; w < 4; ++w) {
-        uint32_t c = wcnt[w][tid];
-        woff[w][tid] = s;
-        s += c;
-        wcnt[w][tid] = 0;
-      }
-      digit_base[tid] = s;
+    for (int w = 0; w < 4; ++w) {
+      uint32_t c = sm.wcnt[w][tid];
+      sm.wcnt[w][tid] = s;
+      s += c;
     }
-    __syncthreads();
+    local_count = s;  // digit tid's count in this tile (0 for tid >= R)
+  }
+  // publish this tile's aggregate as early as possible (tile 0 publishes its prefix)
+  if (tid < R) {
+    uint32_t word = (t == 0 ? ST_PRE : ST_AGG) | local_count;
+    __hip_atomic_store(&status[(size_t)t * R + tid], word, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+  {
+    uint32_t tot;
+    sm.loc_off[tid] = block_exclusive_scan<TPB>(local_count, tot, sm.scan_tmp);
+  }
+  __syncthreads();  // loc_off[d] is read by every thread below
+  // stable local sort into LDS
+#pragma unroll
+  for (int r = 0; r < OS_ITEMS; ++r) {
+    const bool valid = seg + r * 64 + lane < n;
     if (valid) {
-      const uint32_t pos = woff[wave][d] + rank;
-      kout[pos] = key;
-      vout[pos] = val;
+      const uint32_t d = (uint32_t)(key[r] >> shift) & dmask;
+      const uint32_t lp = sm.loc_off[d] + sm.wcnt[wave][d] + rank[r];
+      sm.keys[lp] = key[r];
+      sm.vals[lp] = val[r];
+    }
+  }
+  // decoupled look-back for this digit's exclusive prefix over the preceding tiles
+  if (tid < R) {
+    uint32_t excl = 0;
+    if (t > 0) {
+      long long j = (long long)t - 1;
+      uint32_t spins = 0;
+      while (true) {
+        const uint32_t s = __hip_atomic_load(&status[(size_t)j * R + tid], __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+        if ((s & ~ST_VAL) == 0) {
+          if (++spins > SPIN_LIMIT) {  // bounded: report instead of hanging
+            atomicOr(err, 1u);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        excl += s & ST_VAL;
+        if ((s & ST_PRE) || j == 0) break;
+        --j;
+      }
+      __hip_atomic_store(&status[(size_t)t * R + tid], ST_PRE | (excl + local_count),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    sm.gofs[tid] = sm.hscan[tid] + excl - sm.loc_off[tid];
+  }
+  __syncthreads();
+  const long long cnt = min((long long)OS_TILE, n - base);
+#pragma unroll
+  for (int r = 0; r < OS_ITEMS; ++r) {
+    const int i = r * TPB + tid;
+    if (i < cnt) {
+      const K k = sm.keys[i];
+      const uint32_t d = (uint32_t)(k >> shift) & dmask;
+      const uint32_t pos = sm.gofs[d] + (uint32_t)i;
+      kout[pos] = k;
+      vout[pos] = sm.vals[i];
     }
   }
 }
 
-size_t radix_ws_bytes(long long n) {
-  long long nb = cdiv(n > 0 ? n : 1, RS_TILE);
-  return (size_t)(256 * nb) * sizeof(uint32_t) + scan_ws_bytes(256 * nb);
-}
-
 // Stable LSD sort of (keys, vals) by bits [begin_bit, end_bit).  Ping-pongs between
-// (ka, va) and (kb, vb); the final pass writes (kout, vout).  Inputs (ka, va) are clobbered
-// unless there is exactly one pass.
+// (ka, va) and (kb, vb); the last pass writes (kout, vout).  (ka, va) are clobbered when
+// there are more than two passes.  ws must hold radix_ws_bytes(n, begin_bit, end_bit).
 template <typename K>
 int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t *vout,
                      long long n, int begin_bit, int end_bit, void *ws, hipStream_t st) {
   if (n <= 0) return 0;
-  const int nb = (int)cdiv(n, RS_TILE);
-  uint32_t *hist = (uint32_t *)ws;
-  uint32_t *partial = hist + 256 * (size_t)nb;
-  int passes = (end_bit - begin_bit + 7) / 8;
-  if (passes <= 0) {
+  const SortPlan p = sort_plan(n, begin_bit, end_bit);
+  if (p.passes == 0) {
     note(hipMemcpyAsync(kout, ka, n * sizeof(K), hipMemcpyDeviceToDevice, st), "hipMemcpyAsync");
-    note(hipMemcpyAsync(vout, va, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, st), "hipMemcpyAsync");
+    note(hipMemcpyAsync(vout, va, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, st),
+         "hipMemcpyAsync");
     return 0;
   }
+  uint32_t *hist = (uint32_t *)ws;
+  uint32_t *tickets = hist + OS_MAX_PASSES * 256;
+  uint32_t *err = tickets + OS_MAX_PASSES;
+  uint32_t *status = (uint32_t *)ws + OS_HEAD_WORDS;
+  note(hipMemsetAsync(ws, 0, radix_ws_bytes(n, begin_bit, end_bit), st), "hipMemsetAsync");
+  const int hist_blocks = (int)min((long long)cdiv(n, TPB * 8), 2048LL);
+  hipLaunchKernelGGL(os_hist_kernel<K>, dim3(hist_blocks), dim3(TPB), 0, st, ka, n, begin_bit,
+                     p.width, p.passes, hist);
   K *kin = ka, *kalt = kb;
   uint32_t *vin = va, *valt = vb;
-  for (int p = 0; p < passes; ++p) {
-    const int shift = begin_bit + 8 * p;
-    const bool last = p == passes - 1;
+  for (int q = 0; q < p.passes; ++q) {
+    const bool last = q == p.passes - 1;
     K *ko = last ? kout : kalt;
     uint32_t *vo = last ? vout : valt;
-    hipLaunchKernelGGL(rs_upsweep_kernel<K>, dim3(nb), dim3(TPB), 0, st, kin, n, shift, nb, hist);
-    device_exclusive_scan(hist, hist, 256LL * nb, nullptr, partial, st);
-    hipLaunchKernelGGL(rs_downsweep_kernel<K>, dim3(nb), dim3(TPB), 0, st, kin, vin, ko, vo, n,
-                       shift, nb, hist);
-    // next pass reads what this one wrote; its scratch is whatever it did not write
+    hipLaunchKernelGGL(os_pass_kernel<K>, dim3((unsigned)p.nblocks), dim3(TPB), 0, st, kin, vin,
+                       ko, vo, n, begin_bit + q * p.width, p.width, hist + q * 256, tickets + q,
+                       status + (size_t)q * p.nblocks * p.radix, err);
     K *kfree = (kin == ka || kin == kb) ? kin : kalt;
     uint32_t *vfree = (vin == va || vin == vb) ? vin : valt;
     kin = ko;
@@ -264,37 +373,39 @@ __device__ __forceinline__ void tile_bbox(float x, float y, float radius, int tb
 }
 
 // Depth keys: visible -> float bits of depth (positive floats order as uints), culled ->
-// 0xFFFFFFFF (sorted last).  Also counts the visible Gaussians (wave ballot + one atomic).
+// 0xFFFFFFFF (sorted last).
 __global__ __launch_bounds__(TPB) void depth_keys_kernel(int n, const float *__restrict__ depths,
                                                          const int *__restrict__ radii,
                                                          uint32_t *__restrict__ keys,
-                                                         uint32_t *__restrict__ vals,
-                                                         int *__restrict__ num_visible) {
+                                                         uint32_t *__restrict__ vals) {
   int i = blockIdx.x * TPB + threadIdx.x;
-  bool vis = false;
-  if (i < n) {
-    vis = radii[i] > 0;
-    keys[i] = vis ? __float_as_uint(depths[i]) : 0xFFFFFFFFu;
-    vals[i] = (uint32_t)i;
-  }
-  unsigned long long b = __ballot(vis);
-  if ((threadIdx.x & 63) == 0 && b) atomicAdd(num_visible, (int)__popcll(b));
+  if (i >= n) return;
+  keys[i] = radii[i] > 0 ? __float_as_uint(depths[i]) : 0xFFFFFFFFu;
+  vals[i] = (uint32_t)i;
 }
 
+// cnt[p] = tiles hit by the p-th Gaussian in depth order; the visible count is the index
+// where the depth-sorted keys reach the culled sentinel.
 __global__ __launch_bounds__(TPB) void gather_counts_kernel(int n, const uint32_t *__restrict__ order,
+                                                            const uint32_t *__restrict__ skeys,
                                                             const int *__restrict__ radii,
                                                             const int *__restrict__ num_tiles_hit,
-                                                            uint32_t *__restrict__ cnt) {
+                                                            uint32_t *__restrict__ cnt,
+                                                            int *__restrict__ num_visible) {
   int p = blockIdx.x * TPB + threadIdx.x;
   if (p >= n) return;
   uint32_t g = order[p];
   int c = radii[g] > 0 ? num_tiles_hit[g] : 0;
   cnt[p] = c > 0 ? (uint32_t)c : 0u;
+  const bool vis = skeys[p] != 0xFFFFFFFFu;
+  if (vis && (p == n - 1 || skeys[p + 1] == 0xFFFFFFFFu)) *num_visible = p + 1;
 }
 
-// One lane per depth-ordered Gaussian writes its allotted cnt[p] (tile, id) pairs at
-// off[p]; a bbox smaller than the allotment (inconsistent caller inputs) is padded with the
-// sentinel tile id T, which sorts past every real tile and is ignored by the bins.
+// One wave per 64 depth-ordered Gaussians: the wave fills their combined slot range
+// [off[p0], off[p0] + total) with lanes striding over it, so stores are coalesced.  Slot j
+// belongs to the lane q with start[q] <= j < start[q+1] (6-step shuffle search); its tile
+// is the (j - start[q])-th tile of q's bbox in row-major order.  An allotment larger than
+// the bbox (inconsistent caller inputs) is padded with the sentinel tile id T.
 __global__ __launch_bounds__(TPB) void emit_kernel(int n, const uint32_t *__restrict__ order,
                                                    const uint32_t *__restrict__ cnt,
                                                    const uint32_t *__restrict__ off,
@@ -302,23 +413,53 @@ __global__ __launch_bounds__(TPB) void emit_kernel(int n, const uint32_t *__rest
                                                    const int *__restrict__ radii, int tbx, int tby,
                                                    uint32_t *__restrict__ tkeys,
                                                    uint32_t *__restrict__ tvals) {
-  int p = blockIdx.x * TPB + threadIdx.x;
-  if (p >= n) return;
-  uint32_t c = cnt[p];
-  if (c == 0) return;
-  uint32_t g = order[p];
-  uint32_t o = off[p];
-  int x0, x1, y0, y1;
-  tile_bbox(xys[2 * g], xys[2 * g + 1], (float)radii[g], tbx, tby, x0, x1, y0, y1);
-  uint32_t j = 0;
-  for (int y = y0; y < y1 && j < c; ++y)
-    for (int x = x0; x < x1 && j < c; ++x, ++j) {
-      tkeys[o + j] = (uint32_t)(y * tbx + x);
-      tvals[o + j] = g;
+  const int lane = threadIdx.x & 63;
+  const long long p0 = ((long long)blockIdx.x * TPB + threadIdx.x) - lane;
+  if (p0 >= n) return;  // wave-uniform
+  const long long p = p0 + lane;
+  const bool in = p < n;
+  uint32_t c = 0, g = 0, start = 0;
+  int x0 = 0, y0 = 0, bw = 1, area = 0;
+  if (in) {
+    c = cnt[p];
+    start = off[p];
+    if (c) {
+      g = order[p];
+      int x1, y1;
+      tile_bbox(xys[2 * g], xys[2 * g + 1], (float)radii[g], tbx, tby, x0, x1, y0, y1);
+      bw = max(x1 - x0, 1);
+      area = max(x1 - x0, 0) * max(y1 - y0, 0);
     }
-  for (; j < c; ++j) {
-    tkeys[o + j] = (uint32_t)(tbx * tby);
-    tvals[o + j] = g;
+  }
+  const uint32_t base = __shfl(start, 0, 64);
+  const int last_lane = (int)min(63LL, (long long)n - 1 - p0);
+  const uint32_t total = __shfl(start + c, last_lane, 64) - base;
+  const uint32_t rel = in ? start - base : total;  // lanes past n are never chosen
+  // wave-uniform trip count: every lane stays active for the shuffles (a shuffle reading an
+  // inactive lane is undefined); only the stores are predicated.
+  for (uint32_t j0 = 0; j0 < total; j0 += 64) {
+    const uint32_t j = j0 + lane;
+    int q = 0;  // largest q with rel[q] <= j
+#pragma unroll
+    for (int step = 32; step >= 1; step >>= 1) {
+      const uint32_t rq = __shfl(rel, (q + step) & 63, 64);
+      if (q + step <= 63 && rq <= j) q += step;
+    }
+    const uint32_t li = j - __shfl(rel, q, 64);
+    const int qx0 = __shfl(x0, q, 64), qy0 = __shfl(y0, q, 64), qbw = __shfl(bw, q, 64);
+    const int qarea = __shfl(area, q, 64);
+    const uint32_t qg = __shfl(g, q, 64);
+    uint32_t tile;
+    if ((int)li < qarea) {
+      const int ly = (int)li / qbw;
+      tile = (uint32_t)((qy0 + ly) * tbx + qx0 + ((int)li - ly * qbw));
+    } else {
+      tile = (uint32_t)(tbx * tby);
+    }
+    if (j < total) {
+      tkeys[base + j] = tile;
+      tvals[base + j] = qg;
+    }
   }
 }
 
@@ -359,40 +500,51 @@ __global__ __launch_bounds__(TPB) void map_intersects_kernel(
     }
 }
 
-// ---- workspace layout of the fused binning (phase-1 region first, phase-2 after it) ----
+// ---- workspace layouts of the fused binning (phase 1 and phase 2 are separate buffers) ----
 constexpr size_t ALIGN = 256;
 inline size_t al(size_t x) { return (x + ALIGN - 1) / ALIGN * ALIGN; }
 
+struct Carver {
+  char *base;
+  size_t off = 0;
+  explicit Carver(void *b) : base((char *)b) {}
+  template <typename T>
+  T *take(size_t bytes) {
+    T *r = (T *)(base + off);
+    off += al(bytes);
+    return r;
+  }
+};
+
 struct Phase1 {
-  uint32_t *dkeys_a, *dvals_a, *dkeys_b, *dvals_b, *dkeys_s, *order, *cnt, *off, *total;
+  uint32_t *dkeys_a, *dvals_a, *dkeys_b, *dvals_b, *dkeys_s, *order, *cnt, *off;
   void *rs_ws;
   size_t bytes;
 };
 
 Phase1 carve_phase1(void *base, int n) {
   Phase1 p;
-  char *c = (char *)base;
-  size_t o = 0;
-  auto take = [&](size_t b) {
-    char *r = c + o;
-    o += al(b);
-    return r;
-  };
+  Carver c(base);
   size_t nn = (size_t)(n > 0 ? n : 1) * 4;
-  p.dkeys_a = (uint32_t *)take(nn);
-  p.dvals_a = (uint32_t *)take(nn);
-  p.dkeys_b = (uint32_t *)take(nn);
-  p.dvals_b = (uint32_t *)take(nn);
-  p.dkeys_s = (uint32_t *)take(nn);
-  p.order = (uint32_t *)take(nn);
-  p.cnt = (uint32_t *)take(nn);
-  p.off = (uint32_t *)take(nn);
-  p.total = (uint32_t *)take(16);
-  size_t rs = radix_ws_bytes(n);
+  p.dkeys_a = c.take<uint32_t>(nn);
+  p.dvals_a = c.take<uint32_t>(nn);
+  p.dkeys_b = c.take<uint32_t>(nn);
+  p.dvals_b = c.take<uint32_t>(nn);
+  p.dkeys_s = c.take<uint32_t>(nn);
+  p.order = c.take<uint32_t>(nn);
+  p.cnt = c.take<uint32_t>(nn);
+  p.off = c.take<uint32_t>(nn);
+  size_t rs = radix_ws_bytes(n, 0, 32);
   size_t sc = scan_ws_bytes(n);
-  p.rs_ws = take(rs > sc ? rs : sc);
-  p.bytes = o;
+  p.rs_ws = c.take<char>(rs > sc ? rs : sc);
+  p.bytes = c.off;
   return p;
+}
+
+int bits_for(long long v) {  // smallest b with (1 << b) > v
+  int b = 0;
+  while (b < 62 && (1LL << b) <= v) ++b;
+  return b;
 }
 
 struct Phase2 {
@@ -403,28 +555,16 @@ struct Phase2 {
 
 Phase2 carve_phase2(void *base, long long I) {
   Phase2 p;
-  char *c = (char *)base;
-  size_t o = 0;
-  auto take = [&](size_t b) {
-    char *r = c + o;
-    o += al(b);
-    return r;
-  };
+  Carver c(base);
   size_t ii = (size_t)(I > 0 ? I : 1) * 4;
-  p.tk_a = (uint32_t *)take(ii);
-  p.tv_a = (uint32_t *)take(ii);
-  p.tk_b = (uint32_t *)take(ii);
-  p.tv_b = (uint32_t *)take(ii);
-  p.tk_s = (uint32_t *)take(ii);
-  p.rs_ws = take(radix_ws_bytes(I));
-  p.bytes = o;
+  p.tk_a = c.take<uint32_t>(ii);
+  p.tv_a = c.take<uint32_t>(ii);
+  p.tk_b = c.take<uint32_t>(ii);
+  p.tv_b = c.take<uint32_t>(ii);
+  p.tk_s = c.take<uint32_t>(ii);
+  p.rs_ws = c.take<char>(radix_ws_bytes(I, 0, 16));  // >= any tile-key width (T < 65536)
+  p.bytes = c.off;
   return p;
-}
-
-int bits_for(long long v) {  // smallest b with (1 << b) > v
-  int b = 0;
-  while (b < 62 && (1LL << b) <= v) ++b;
-  return b;
 }
 
 }  // namespace
@@ -457,11 +597,11 @@ extern "C" int gsplat_bin_count(int num_points, const float *depths, const int32
   if (num_points == 0) return check_launch("bin_count");
   const int n = num_points;
   hipLaunchKernelGGL(depth_keys_kernel, dim3(cdiv(n, TPB)), dim3(TPB), 0, st, n, depths, radii,
-                     p.dkeys_a, p.dvals_a, d_counts);
+                     p.dkeys_a, p.dvals_a);
   radix_sort_pairs<uint32_t>(p.dkeys_a, p.dvals_a, p.dkeys_b, p.dvals_b, p.dkeys_s, p.order, n, 0,
                              32, p.rs_ws, st);
   hipLaunchKernelGGL(gather_counts_kernel, dim3(cdiv(n, TPB)), dim3(TPB), 0, st, n, p.order,
-                     radii, num_tiles_hit, p.cnt);
+                     p.dkeys_s, radii, num_tiles_hit, p.cnt, d_counts);
   device_exclusive_scan(p.cnt, p.off, n, (uint32_t *)(d_counts + 1), (uint32_t *)p.rs_ws, st);
   return check_launch("bin_count");
 }
@@ -472,8 +612,9 @@ extern "C" int gsplat_bin_emit(int num_points, int64_t num_intersects, const flo
                                const void *workspace1, size_t workspace1_bytes,
                                void *workspace2, size_t workspace2_bytes, void *stream) {
   hipStream_t st = (hipStream_t)stream;
-  if (num_points < 0 || num_intersects < 0 || num_intersects > 0x7FFFFFFFLL ||
-      tile_bounds_x <= 0 || tile_bounds_y <= 0) {
+  const long long T = (long long)tile_bounds_x * tile_bounds_y;
+  if (num_points < 0 || num_intersects < 0 || num_intersects > 0x3FFFFFFFLL ||
+      tile_bounds_x <= 0 || tile_bounds_y <= 0 || T >= 65536) {
     set_error("bin_emit: bad sizes (N=%d I=%lld tiles=%dx%d)", num_points,
               (long long)num_intersects, tile_bounds_x, tile_bounds_y);
     return 1;
@@ -485,7 +626,6 @@ extern "C" int gsplat_bin_emit(int num_points, int64_t num_intersects, const flo
               workspace2_bytes, p1.bytes, p2.bytes);
     return 1;
   }
-  const long long T = (long long)tile_bounds_x * tile_bounds_y;
   note(hipMemsetAsync(tile_bins, 0, (size_t)T * 2 * sizeof(int32_t), st), "hipMemsetAsync");
   if (num_intersects == 0 || num_points == 0) return check_launch("bin_emit");
   const int n = num_points;
@@ -518,7 +658,7 @@ extern "C" int gsplat_map_gaussian_to_intersects(int num_points, const float *xy
 extern "C" size_t gsplat_sort_isect_pairs_workspace_size(int64_t num_items) {
   size_t kk = al((size_t)(num_items > 0 ? num_items : 1) * 8);
   size_t vv = al((size_t)(num_items > 0 ? num_items : 1) * 4);
-  return 2 * kk + 2 * vv + radix_ws_bytes(num_items);
+  return 2 * kk + 2 * vv + radix_ws_bytes(num_items, 0, 64);
 }
 
 extern "C" int gsplat_sort_isect_pairs(int64_t num_items, int key_bits, const int64_t *keys_in,
@@ -526,7 +666,7 @@ extern "C" int gsplat_sort_isect_pairs(int64_t num_items, int key_bits, const in
                                        int32_t *vals_out, void *workspace,
                                        size_t workspace_bytes, void *stream) {
   hipStream_t st = (hipStream_t)stream;
-  if (num_items < 0 || key_bits < 0 || key_bits > 64) {
+  if (num_items < 0 || num_items > 0x3FFFFFFFLL || key_bits < 0 || key_bits > 64) {
     set_error("sort_isect_pairs: bad args");
     return 1;
   }
@@ -554,7 +694,9 @@ extern "C" int gsplat_get_tile_bin_edges(int64_t num_intersects, const int64_t *
     set_error("get_tile_bin_edges: bad sizes");
     return 1;
   }
-  if (num_rows > 0) note(hipMemsetAsync(tile_bins, 0, (size_t)num_rows * 2 * sizeof(int32_t), st), "hipMemsetAsync");
+  if (num_rows > 0)
+    note(hipMemsetAsync(tile_bins, 0, (size_t)num_rows * 2 * sizeof(int32_t), st),
+         "hipMemsetAsync");
   if (num_intersects == 0) return check_launch("get_tile_bin_edges");
   hipLaunchKernelGGL((bin_edges_kernel<uint64_t, 32>), dim3(cdiv(num_intersects, TPB)), dim3(TPB),
                      0, st, (long long)num_intersects, (const uint64_t *)isect_ids_sorted,
