@@ -85,7 +85,7 @@ class TrainStep:
     """render -> loss -> backward -> [all-reduce] -> Adam, on this rank's camera."""
 
     def __init__(self, scene: GaussianScene, sh_degree: int = 3, world_size: int = 1,
-                 loss: str = "splatfacto", group=None):
+                 loss: str = "splatfacto", group=None, api=None):
         self.scene = scene.requires_grad_()
         self.params = scene.params()
         self.bucket = FlatGradBucket(self.params)
@@ -93,6 +93,7 @@ class TrainStep:
         self.group = group
         self.sh_degree = sh_degree
         self.loss_kind = loss
+        self.api = api  # gsplat implementation override (tests: CPU-oracle emulation)
         self.opt = torch.optim.Adam(
             [{"params": [getattr(scene, k)], "lr": GROUP_LR[k], "name": k}
              for k in PARAM_NAMES], eps=1e-15, foreach=True)
@@ -108,7 +109,7 @@ class TrainStep:
         return splatfacto_loss(pred, gt)
 
     def forward_backward(self, cam: GCCamera, gt: torch.Tensor, background: torch.Tensor):
-        out = render(self.scene, cam, self.sh_degree, background)
+        out = render(self.scene, cam, self.sh_degree, background, api=self.api)
         loss = self.loss(out["rgb"], gt)
         loss.backward()
         return loss, out
