@@ -46,8 +46,10 @@ SIGNATURES = {
     "gsplat_bin_emit": (_I, [_I, _I64, _P, _P, _I, _I, _P, _P, _P, _SZ, _P, _SZ, _P]),
     "gsplat_rasterize_forward": (_I, [_I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                                       _P, _P]),
+    "gsplat_rasterize_backward_workspace_size": (_SZ, [_I, _I]),
+    "gsplat_debug_set_raster_variant": (_I, [_I, _I, _I]),
     "gsplat_rasterize_backward": (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P,
-                                       _P, _P, _P, _F, _P, _P, _P, _P, _P]),
+                                       _P, _P, _P, _F, _P, _P, _P, _P, _P, _SZ, _P]),
 }
 
 _lib = None
@@ -71,7 +73,7 @@ def lib():
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
-        if L.gsplat_abi_version() != 1:
+        if L.gsplat_abi_version() != 2:
             raise RuntimeError("libgsplat_mi355x.so ABI version mismatch")
         _lib = L
     return _lib

@@ -5,19 +5,24 @@
 // backward.cu; semantics SURVEY.md Appendix A9/A10), reached from
 // /root/reference/gaussctrl/gc_model.py:208-220 (RGB + alpha) and :225-236 (depth).
 //
-// MI355X mapping (the path is per-pixel serial compositing: no MFMA):
-//  * One wave64 owns one 16x16 tile; each lane owns 4 pixels of a column (rows
-//    r, r+4, r+8, r+12).  No workgroup barrier is ever needed: a wave stages its own
-//    tile's Gaussians in its own LDS slice, 64 at a time (one Gaussian per lane, loaded
-//    coalesced from the sorted id list), then every lane reads each staged Gaussian as an
-//    LDS broadcast and applies it to its 4 pixels -- one LDS read per 4 pixel-evaluations.
-//  * Early termination is per wave (__all over 256 pixels) and is tested after every
-//    Gaussian, not per 256-Gaussian batch as in gsplat.
-//  * Backward: the per-pixel contributions to one Gaussian are summed in registers over the
-//    lane's 4 pixels, then across the wave with DPP row operations (6 VALU ops per value,
-//    no LDS), and one lane issues the 9 float atomics of the (tile, Gaussian) pair.  Waves
-//    with no valid pixel for a Gaussian skip the reduction entirely.
-//  * 4 tiles (4 independent waves) per 256-thread workgroup.
+// MI355X mapping (per-pixel serial compositing: VALU/latency-bound, no MFMA):
+//  * A 16x16 tile is split into 4/PXL horizontal strips, one wave64 each; a lane owns PXL
+//    pixels of one column of its strip.  The waves of a tile are independent -- each stages
+//    its own copy of the tile's sorted Gaussians in its own LDS slice, 64 at a time (one
+//    Gaussian per lane, coalesced id loads; colour loaded only if kept) -- so a wave whose
+//    pixels have all terminated leaves early and no workgroup barrier is ever executed.
+//    (One wave per tile would serialise a 2.8k-Gaussian tile on one wave: the headline
+//    forward was bound by exactly that critical path.)
+//  * While staging, each lane culls its Gaussian against the wave's pixel rectangle with a
+//    conservative bound (touches_rect) and the survivors are compacted in order with a
+//    ballot + mbcnt prefix, so the per-pixel loop only visits Gaussians that can pass
+//    gsplat's alpha >= 1/255 test somewhere in the strip.  The bound never drops a Gaussian
+//    that could contribute, so results are unchanged bit for bit.
+//  * Backward: per Gaussian, the lane sums its PXL pixels' contributions in registers, the
+//    wave reduces the 9 partial sums with DPP row operations, and ONE 9-lane atomic
+//    instruction adds them to the Gaussian's 64-byte-aligned gradient record (one memory
+//    request instead of nine single-lane atomics); a split kernel then writes gsplat's
+//    v_xy / v_conic / v_colors / v_opacity tensors.
 //  * C != 3 (gsplat nd_rasterize): one pixel per lane, 4 waves per tile, register
 //    accumulators sized by a compile-time channel bound.
 #include "common.h"
@@ -25,38 +30,73 @@
 namespace gs {
 namespace {
 
-constexpr int WPB = 4;             // tiles (waves) per workgroup
-constexpr int PXL = 4;             // pixels per lane
 constexpr float ALPHA_MIN = 1.f / 255.f;
+constexpr int REC = 16;  // floats per gradient record: x y a b c r g b o + pad = 64 B
+constexpr int FWD_PXL = 1;
+constexpr int BWD_PXL = 2;
+// Tuning / ablation knobs (gsplat_debug_set_raster_variant); defaults are the shipped ones.
+int g_fwd_pxl = FWD_PXL, g_bwd_pxl = BWD_PXL, g_bwd_flags = 0;
 
-struct __attribute__((aligned(16))) GFwd {
-  float x, y, a, b;
-  float c, o, r, g;
-  float bl, p0, p1, p2;
-};
-
-struct __attribute__((aligned(16))) GBwd {
+struct __attribute__((aligned(16))) GStage {
   float x, y, a, b;
   float c, o, r, g;
   float bl;
-  int id;
-  float p0, p1;
+  int idx;  // position in the tile's sorted list
+  int id;   // Gaussian id
+  float pad;
 };
 
-__global__ __launch_bounds__(64 * WPB) void raster_fwd3_kernel(
+// Conservative, exactness-preserving cull of one Gaussian against the pixel-centre
+// rectangle [rx0,rx1] x [ry0,ry1].  For every pixel p in it, with d = xy - p,
+//   sigma(p) = 0.5 d^T Q d >= 0.5 lmin(Q) |d|^2 >= 0.5 lmin dist(xy, rect)^2,
+// so when even half of that lower bound (float-safety margin) makes o*exp(-sigma) < 1/255,
+// gsplat's per-pixel test rejects the Gaussian at every pixel of the rectangle.  A Gaussian
+// with o < 1/255 is never composited (alpha <= o).  Non-positive-definite conics and NaNs
+// are kept.
+__device__ __forceinline__ bool touches_rect(float gx, float gy, float a, float b, float c,
+                                             float o, float rx0, float rx1, float ry0,
+                                             float ry1) {
+  if (!(o >= ALPHA_MIN)) return false;
+  const float dx = gx - fminf(fmaxf(gx, rx0), rx1);
+  const float dy = gy - fminf(fmaxf(gy, ry0), ry1);
+  const float d2 = dx * dx + dy * dy;
+  const float hm = 0.5f * (a + c), hd = 0.5f * (a - c);
+  const float lmax = hm + sqrtf(hd * hd + b * b);
+  const float det = a * c - b * b;
+  if (!(det > 0.f) || !(lmax > 0.f)) return true;
+  const float lmin = det / lmax;
+  const float bound = 0.25f * lmin * d2;
+  return !(bound > __logf(255.f * o) + 0.01f);
+}
+
+__device__ __forceinline__ uint32_t lanes_below(unsigned long long mask) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                   __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+template <int PXL>
+__global__ __launch_bounds__(256) void raster_fwd3_kernel(
     int tbx, int tby, int H, int W, const int *__restrict__ gids, const int2 *__restrict__ bins,
     const float2 *__restrict__ xys, const float *__restrict__ conics,
     const float *__restrict__ colors, const float *__restrict__ opacity,
     const float *__restrict__ background, float *__restrict__ out_img,
     float *__restrict__ final_Ts, int *__restrict__ final_idx) {
-  __shared__ GFwd lds[WPB][64];
+  constexpr int WPT = 4 / PXL;    // waves per tile
+  constexpr int TPBLK = 4 / WPT;  // tiles per workgroup
+  constexpr int ROWS = 4 * PXL;   // rows per strip
+  __shared__ GStage lds[4][64];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int tile = blockIdx.x * WPB + wave;
+  const int tile = blockIdx.x * TPBLK + wave / WPT;
+  const int strip = wave % WPT;
   if (tile >= tbx * tby) return;  // wave-uniform
   const int tx = tile % tbx, ty = tile / tbx;
+  const int r0 = ty * GS_BLOCK + strip * ROWS;
+  if (r0 >= H) return;  // strip entirely below the image
   const int j = tx * GS_BLOCK + (lane & 15);
-  const int i0 = ty * GS_BLOCK + (lane >> 4);
+  const int i0 = r0 + (lane >> 4);
   const float px = (float)j;
+  const float rx0 = (float)(tx * GS_BLOCK), rx1 = (float)min(tx * GS_BLOCK + 15, W - 1);
+  const float ry0 = (float)r0, ry1 = (float)min(r0 + ROWS - 1, H - 1);
   float py[PXL], T[PXL], cr[PXL], cg[PXL], cb[PXL];
   int cur[PXL];
   bool done[PXL];
@@ -70,30 +110,39 @@ __global__ __launch_bounds__(64 * WPB) void raster_fwd3_kernel(
     done[k] = !(i < H && j < W);
   }
   const int2 range = bins[tile];
-  GFwd *slot = lds[wave];
+  GStage *slot = lds[wave];
   for (int b = range.x; b < range.y; b += 64) {
-    if (__all(done[0] && done[1] && done[2] && done[3])) break;
+    bool all_done = true;
+#pragma unroll
+    for (int k = 0; k < PXL; ++k) all_done = all_done && done[k];
+    if (__all(all_done)) break;
     const int idx = b + lane;
+    bool keep = false;
+    GStage s;
     if (idx < range.y) {
       const int g = gids[idx];
       const float2 xy = xys[g];
-      GFwd s;
       s.x = xy.x;
       s.y = xy.y;
       s.a = conics[3 * g];
       s.b = conics[3 * g + 1];
       s.c = conics[3 * g + 2];
       s.o = opacity[g];
-      s.r = colors[3 * g];
-      s.g = colors[3 * g + 1];
-      s.bl = colors[3 * g + 2];
-      slot[lane] = s;
+      keep = touches_rect(s.x, s.y, s.a, s.b, s.c, s.o, rx0, rx1, ry0, ry1);
+      if (keep) {
+        s.r = colors[3 * g];
+        s.g = colors[3 * g + 1];
+        s.bl = colors[3 * g + 2];
+        s.idx = idx;
+      }
     }
+    const unsigned long long kmask = __ballot(keep);
+    if (keep) slot[lanes_below(kmask)] = s;
+    const int n = __popcll(kmask);
     wave_lds_sync();
-    const int n = min(64, range.y - b);
     for (int t = 0; t < n; ++t) {
-      const GFwd G = slot[t];
-      bool all_done = true;
+      const GStage G = slot[t];
+      bool fin = true;
 #pragma unroll
       for (int k = 0; k < PXL; ++k) {
         if (!done[k]) {
@@ -110,13 +159,13 @@ __global__ __launch_bounds__(64 * WPB) void raster_fwd3_kernel(
               cg[k] += G.g * vis;
               cb[k] += G.bl * vis;
               T[k] = nT;
-              cur[k] = b + t;
+              cur[k] = G.idx;
             }
           }
         }
-        all_done = all_done && done[k];
+        fin = fin && done[k];
       }
-      if (__all(all_done)) break;
+      if (__all(fin)) break;
     }
     wave_lds_sync();
   }
@@ -135,22 +184,30 @@ __global__ __launch_bounds__(64 * WPB) void raster_fwd3_kernel(
   }
 }
 
-__global__ __launch_bounds__(64 * WPB) void raster_bwd3_kernel(
+template <int PXL, bool ATOMICS>
+__global__ __launch_bounds__(256) void raster_bwd3_kernel(
     int tbx, int tby, int H, int W, const int *__restrict__ gids, const int2 *__restrict__ bins,
     const float2 *__restrict__ xys, const float *__restrict__ conics,
     const float *__restrict__ colors, const float *__restrict__ opacity,
     const float *__restrict__ background, const float *__restrict__ final_Ts,
     const int *__restrict__ final_idx, const float *__restrict__ v_out,
-    const float *__restrict__ v_out_alpha, float alpha_max, float *__restrict__ v_xy,
-    float *__restrict__ v_conic, float *__restrict__ v_rgb, float *__restrict__ v_opacity) {
-  __shared__ GBwd lds[WPB][64];
+    const float *__restrict__ v_out_alpha, float alpha_max, float *__restrict__ rec) {
+  constexpr int WPT = 4 / PXL;
+  constexpr int TPBLK = 4 / WPT;
+  constexpr int ROWS = 4 * PXL;
+  __shared__ GStage lds[4][64];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int tile = blockIdx.x * WPB + wave;
+  const int tile = blockIdx.x * TPBLK + wave / WPT;
+  const int strip = wave % WPT;
   if (tile >= tbx * tby) return;
   const int tx = tile % tbx, ty = tile / tbx;
+  const int r0 = ty * GS_BLOCK + strip * ROWS;
+  if (r0 >= H) return;
   const int j = tx * GS_BLOCK + (lane & 15);
-  const int i0 = ty * GS_BLOCK + (lane >> 4);
+  const int i0 = r0 + (lane >> 4);
   const float px = (float)j;
+  const float rx0 = (float)(tx * GS_BLOCK), rx1 = (float)min(tx * GS_BLOCK + 15, W - 1);
+  const float ry0 = (float)r0, ry1 = (float)min(r0 + ROWS - 1, H - 1);
   const float bg0 = background[0], bg1 = background[1], bg2 = background[2];
   float py[PXL], T[PXL], Tf[PXL], vr[PXL], vg[PXL], vb[PXL], va[PXL], bgdot[PXL];
   float br[PXL], bgr[PXL], bb[PXL];
@@ -181,30 +238,35 @@ __global__ __launch_bounds__(64 * WPB) void raster_bwd3_kernel(
   maxbin = wave_max_int(maxbin);
   const int2 range = bins[tile];
   const int last = min(maxbin, range.y - 1);
-  GBwd *slot = lds[wave];
+  GStage *slot = lds[wave];
   for (int b = last; b >= range.x; b -= 64) {
     const int idx = b - lane;
+    bool keep = false;
+    GStage s;
     if (idx >= range.x) {
       const int g = gids[idx];
       const float2 xy = xys[g];
-      GBwd s;
       s.x = xy.x;
       s.y = xy.y;
       s.a = conics[3 * g];
       s.b = conics[3 * g + 1];
       s.c = conics[3 * g + 2];
       s.o = opacity[g];
-      s.r = colors[3 * g];
-      s.g = colors[3 * g + 1];
-      s.bl = colors[3 * g + 2];
-      s.id = g;
-      slot[lane] = s;
+      keep = touches_rect(s.x, s.y, s.a, s.b, s.c, s.o, rx0, rx1, ry0, ry1);
+      if (keep) {
+        s.r = colors[3 * g];
+        s.g = colors[3 * g + 1];
+        s.bl = colors[3 * g + 2];
+        s.idx = idx;
+        s.id = g;
+      }
     }
+    const unsigned long long kmask = __ballot(keep);
+    if (keep) slot[lanes_below(kmask)] = s;
+    const int n = __popcll(kmask);
     wave_lds_sync();
-    const int n = min(64, b - range.x + 1);
     for (int t = 0; t < n; ++t) {
-      const int k_idx = b - t;
-      const GBwd G = slot[t];
+      const GStage G = slot[t];
       float s_x = 0.f, s_y = 0.f, s_a = 0.f, s_b = 0.f, s_c = 0.f, s_r = 0.f, s_g = 0.f,
             s_bl = 0.f, s_o = 0.f;
       bool anyv = false;
@@ -214,7 +276,7 @@ __global__ __launch_bounds__(64 * WPB) void raster_bwd3_kernel(
         const float sigma = 0.5f * (G.a * dx * dx + G.c * dy * dy) + G.b * dx * dy;
         const float vis = __expf(-sigma);
         const float alpha = fminf(alpha_max, G.o * vis);
-        const bool valid = k_idx <= binf[k] && sigma >= 0.f && alpha >= ALPHA_MIN;
+        const bool valid = G.idx <= binf[k] && sigma >= 0.f && alpha >= ALPHA_MIN;
         if (valid) {
           anyv = true;
           const float ra = __builtin_amdgcn_rcpf(1.f - alpha);
@@ -249,22 +311,45 @@ __global__ __launch_bounds__(64 * WPB) void raster_bwd3_kernel(
         s_g = wave_sum(s_g);
         s_bl = wave_sum(s_bl);
         s_o = wave_sum(s_o);
-        if (lane == 0) {
-          const int g = G.id;
-          atomicAdd(v_xy + 2 * g, s_x);
-          atomicAdd(v_xy + 2 * g + 1, s_y);
-          atomicAdd(v_conic + 3 * g, s_a);
-          atomicAdd(v_conic + 3 * g + 1, s_b);
-          atomicAdd(v_conic + 3 * g + 2, s_c);
-          atomicAdd(v_rgb + 3 * g, s_r);
-          atomicAdd(v_rgb + 3 * g + 1, s_g);
-          atomicAdd(v_rgb + 3 * g + 2, s_bl);
-          atomicAdd(v_opacity + g, s_o);
+        float v = s_x;
+        v = lane == 1 ? s_y : v;
+        v = lane == 2 ? s_a : v;
+        v = lane == 3 ? s_b : v;
+        v = lane == 4 ? s_c : v;
+        v = lane == 5 ? s_r : v;
+        v = lane == 6 ? s_g : v;
+        v = lane == 7 ? s_bl : v;
+        v = lane == 8 ? s_o : v;
+        if constexpr (ATOMICS) {
+          if (lane < 9) atomicAdd(rec + (size_t)G.id * REC + lane, v);
+        } else {
+          asm volatile("" ::"v"(v));  // ablation build: keep the reduction, drop the atomic
         }
       }
     }
     wave_lds_sync();
   }
+}
+
+// Gradient records -> gsplat's v_xy [N,2], v_conic [N,3], v_colors [N,3], v_opacity [N].
+__global__ __launch_bounds__(256) void split_grads_kernel(int n, const float4 *__restrict__ rec,
+                                                          float *__restrict__ v_xy,
+                                                          float *__restrict__ v_conic,
+                                                          float *__restrict__ v_rgb,
+                                                          float *__restrict__ v_opacity) {
+  const int g = blockIdx.x * 256 + threadIdx.x;
+  if (g >= n) return;
+  const float4 r0 = rec[(size_t)g * (REC / 4)], r1 = rec[(size_t)g * (REC / 4) + 1],
+               r2 = rec[(size_t)g * (REC / 4) + 2];
+  v_xy[2 * g] = r0.x;
+  v_xy[2 * g + 1] = r0.y;
+  v_conic[3 * g] = r0.z;
+  v_conic[3 * g + 1] = r0.w;
+  v_conic[3 * g + 2] = r1.x;
+  v_rgb[3 * g] = r1.y;
+  v_rgb[3 * g + 1] = r1.z;
+  v_rgb[3 * g + 2] = r1.w;
+  v_opacity[g] = r2.x;
 }
 
 // ---------------------------------------------------------------- N-channel variants
@@ -502,16 +587,37 @@ extern "C" int gsplat_rasterize_forward(int tile_bounds_x, int tile_bounds_y, in
   }
   const int T = tile_bounds_x * tile_bounds_y;
   if (channels == 3) {
-    hipLaunchKernelGGL(raster_fwd3_kernel, dim3(cdiv(T, WPB)), dim3(64 * WPB), 0, st,
-                       tile_bounds_x, tile_bounds_y, img_height, img_width, gaussian_ids_sorted,
-                       (const int2 *)tile_bins, (const float2 *)xys, conics, colors, opacity,
-                       background, out_img, final_Ts, final_idx);
+#define FWD3(P)                                                                            \
+  hipLaunchKernelGGL(raster_fwd3_kernel<P>, dim3(cdiv(T, P)), dim3(256), 0, st, tile_bounds_x, \
+                     tile_bounds_y, img_height, img_width, gaussian_ids_sorted,                \
+                     (const int2 *)tile_bins, (const float2 *)xys, conics, colors, opacity,    \
+                     background, out_img, final_Ts, final_idx)
+    if (g_fwd_pxl == 4) FWD3(4);
+    else if (g_fwd_pxl == 2) FWD3(2);
+    else FWD3(1);
+#undef FWD3
   } else {
     ND_DISPATCH(raster_fwdn_kernel, tile_bounds_x, tile_bounds_y, img_height, img_width,
                 channels, gaussian_ids_sorted, (const int2 *)tile_bins, (const float2 *)xys,
                 conics, colors, opacity, background, out_img, final_Ts, final_idx);
   }
   return check_launch("rasterize_forward");
+}
+
+extern "C" int gsplat_debug_set_raster_variant(int fwd_pxl, int bwd_pxl, int bwd_flags) {
+  auto ok = [](int p) { return p == 1 || p == 2 || p == 4; };
+  if (!ok(fwd_pxl) || !ok(bwd_pxl)) {
+    set_error("debug_set_raster_variant: pixels per lane must be 1, 2 or 4");
+    return 1;
+  }
+  g_fwd_pxl = fwd_pxl;
+  g_bwd_pxl = bwd_pxl;
+  g_bwd_flags = bwd_flags;
+  return 0;
+}
+
+extern "C" size_t gsplat_rasterize_backward_workspace_size(int num_points, int channels) {
+  return channels == 3 && num_points > 0 ? (size_t)num_points * REC * sizeof(float) : 0;
 }
 
 extern "C" int gsplat_rasterize_backward(int tile_bounds_x, int tile_bounds_y, int img_height,
@@ -523,7 +629,8 @@ extern "C" int gsplat_rasterize_backward(int tile_bounds_x, int tile_bounds_y, i
                                          const float *final_Ts, const int32_t *final_idx,
                                          const float *v_output, const float *v_output_alpha,
                                          float alpha_max, float *v_xy, float *v_conic,
-                                         float *v_colors, float *v_opacity, void *stream) {
+                                         float *v_colors, float *v_opacity, void *workspace,
+                                         size_t workspace_bytes, void *stream) {
   hipStream_t st = (hipStream_t)stream;
   if (tile_bounds_x <= 0 || tile_bounds_y <= 0 || img_height <= 0 || img_width <= 0 ||
       channels < 1 || channels > 64 || num_points < 0 ||
@@ -533,20 +640,38 @@ extern "C" int gsplat_rasterize_backward(int tile_bounds_x, int tile_bounds_y, i
               tile_bounds_y, img_height, img_width, channels, num_points);
     return 1;
   }
-  if (num_points > 0) {
-    note(hipMemsetAsync(v_xy, 0, (size_t)num_points * 2 * sizeof(float), st), "hipMemsetAsync");
-    note(hipMemsetAsync(v_conic, 0, (size_t)num_points * 3 * sizeof(float), st), "hipMemsetAsync");
-    note(hipMemsetAsync(v_colors, 0, (size_t)num_points * channels * sizeof(float), st), "hipMemsetAsync");
-    note(hipMemsetAsync(v_opacity, 0, (size_t)num_points * sizeof(float), st), "hipMemsetAsync");
-  }
   const int T = tile_bounds_x * tile_bounds_y;
   if (channels == 3) {
-    hipLaunchKernelGGL(raster_bwd3_kernel, dim3(cdiv(T, WPB)), dim3(64 * WPB), 0, st,
-                       tile_bounds_x, tile_bounds_y, img_height, img_width, gaussian_ids_sorted,
-                       (const int2 *)tile_bins, (const float2 *)xys, conics, colors, opacity,
-                       background, final_Ts, final_idx, v_output, v_output_alpha, alpha_max,
-                       v_xy, v_conic, v_colors, v_opacity);
+    const size_t need = gsplat_rasterize_backward_workspace_size(num_points, channels);
+    if (workspace_bytes < need || (need && !workspace)) {
+      set_error("rasterize_backward: workspace %zu < %zu bytes", workspace_bytes, need);
+      return 1;
+    }
+    if (num_points == 0) return check_launch("rasterize_backward");
+    float *rec = (float *)workspace;
+    note(hipMemsetAsync(rec, 0, need, st), "hipMemsetAsync");
+#define BWD3(P, A)                                                                         \
+  hipLaunchKernelGGL((raster_bwd3_kernel<P, A>), dim3(cdiv(T, P)), dim3(256), 0, st,          \
+                     tile_bounds_x, tile_bounds_y, img_height, img_width, gaussian_ids_sorted,  \
+                     (const int2 *)tile_bins, (const float2 *)xys, conics, colors, opacity,     \
+                     background, final_Ts, final_idx, v_output, v_output_alpha, alpha_max, rec)
+    const bool atomics = !(g_bwd_flags & 1);
+    if (g_bwd_pxl == 4) { if (atomics) BWD3(4, true); else BWD3(4, false); }
+    else if (g_bwd_pxl == 1) { if (atomics) BWD3(1, true); else BWD3(1, false); }
+    else { if (atomics) BWD3(2, true); else BWD3(2, false); }
+#undef BWD3
+    hipLaunchKernelGGL(split_grads_kernel, dim3(cdiv(num_points, 256)), dim3(256), 0, st,
+                       num_points, (const float4 *)rec, v_xy, v_conic, v_colors, v_opacity);
   } else {
+    if (num_points > 0) {
+      note(hipMemsetAsync(v_xy, 0, (size_t)num_points * 2 * sizeof(float), st), "hipMemsetAsync");
+      note(hipMemsetAsync(v_conic, 0, (size_t)num_points * 3 * sizeof(float), st),
+           "hipMemsetAsync");
+      note(hipMemsetAsync(v_colors, 0, (size_t)num_points * channels * sizeof(float), st),
+           "hipMemsetAsync");
+      note(hipMemsetAsync(v_opacity, 0, (size_t)num_points * sizeof(float), st),
+           "hipMemsetAsync");
+    }
     ND_DISPATCH(raster_bwdn_kernel, tile_bounds_x, tile_bounds_y, img_height, img_width,
                 channels, gaussian_ids_sorted, (const int2 *)tile_bins, (const float2 *)xys,
                 conics, colors, opacity, background, final_Ts, final_idx, v_output,

@@ -168,11 +168,13 @@ class _RasterizeGaussians(Function):
             P = _lib.ptr
             tbx = (W + BLOCK_X - 1) // BLOCK_X
             tby = (H + BLOCK_Y - 1) // BLOCK_Y
+            wsz = _lib.query("gsplat_rasterize_backward_workspace_size", num_points, C)
+            ws = torch.empty((max(wsz, 1),), device=dev, dtype=torch.uint8)
             _lib.call("gsplat_rasterize_backward", tbx, tby, H, W, C, num_points,
                       P(gaussian_ids_sorted), P(tile_bins), P(xys), P(conics), P(colors),
                       P(opacity), P(background), P(final_Ts), P(final_idx), P(v_out_img),
                       P(v_out_alpha), float(BACKWARD_ALPHA_CLAMP), P(v_xy), P(v_conic),
-                      P(v_colors), P(v_opacity), _lib.stream(dev))
+                      P(v_colors), P(v_opacity), P(ws), wsz, _lib.stream(dev))
 
         return (
             v_xy,  # xys

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define GSPLAT_MI355X_ABI_VERSION 1
+#define GSPLAT_MI355X_ABI_VERSION 2
 
 int gsplat_abi_version(void);
 const char *gsplat_last_error(void);
@@ -129,7 +129,10 @@ int gsplat_rasterize_forward(int tile_bounds_x, int tile_bounds_y, int img_heigh
 
 /* v_output [H,W,C], v_output_alpha [H,W]; gradients v_xy [N,2], v_conic [N,3],
  * v_colors [N,C], v_opacity [N] are fully written.  alpha_max is the backward alpha clamp
- * (gsplat 0.1.x uses 0.99f). */
+ * (gsplat 0.1.x uses 0.99f).  workspace holds the per-Gaussian gradient
+ * records the kernel accumulates into (gsplat_rasterize_backward_workspace_size bytes;
+ * may be 0 / NULL when that size is 0). */
+size_t gsplat_rasterize_backward_workspace_size(int num_points, int channels);
 int gsplat_rasterize_backward(int tile_bounds_x, int tile_bounds_y, int img_height,
                               int img_width, int channels, int num_points,
                               const int32_t *gaussian_ids_sorted, const int32_t *tile_bins,
@@ -138,7 +141,14 @@ int gsplat_rasterize_backward(int tile_bounds_x, int tile_bounds_y, int img_heig
                               const float *final_Ts, const int32_t *final_idx,
                               const float *v_output, const float *v_output_alpha,
                               float alpha_max, float *v_xy, float *v_conic, float *v_colors,
-                              float *v_opacity, void *stream);
+                              float *v_opacity, void *workspace, size_t workspace_bytes,
+                              void *stream);
+
+/* Tuning / ablation hook (not part of the gsplat surface): pixels per lane of the 3-channel
+ * forward and backward kernels (1, 2 or 4; a 16x16 tile is covered by 4/pxl waves), and
+ * backward flags (bit 0: drop the gradient atomics -- timing ablation only, results wrong).
+ * Process-wide; defaults are the shipped configuration. */
+int gsplat_debug_set_raster_variant(int fwd_pxl, int bwd_pxl, int bwd_flags);
 
 #ifdef __cplusplus
 }

@@ -23,7 +23,7 @@ def test_library_exports_every_declared_symbol():
     from gaussctrl_exp_amd import _lib
     lib = ctypes.CDLL(_lib.LIB_PATH)
     names = _declared()
-    assert len(names) >= 17
+    assert len(names) >= 18
     missing = [n for n in names if not hasattr(lib, n)]
     assert not missing, missing
     # every declared symbol has a binding signature and vice versa
@@ -32,7 +32,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_host_queries_without_gpu():
     from gaussctrl_exp_amd import _lib
-    assert _lib.lib().gsplat_abi_version() == 1
+    assert _lib.lib().gsplat_abi_version() == 2
     assert _lib.query("gsplat_bin_count_workspace_size", 1000) > 1000 * 16
     assert _lib.query("gsplat_bin_emit_workspace_size", 10 ** 6) >= 5 * 4 * 10 ** 6
     assert _lib.query("gsplat_sort_isect_pairs_workspace_size", 0) > 0
