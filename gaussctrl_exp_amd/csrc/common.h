@@ -64,6 +64,69 @@ __device__ __forceinline__ float wave_sum(float v) {
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, r), 63));
 }
 
+// ---- wave64 reduce-scatter of nine values --------------------------------------------
+// Summing nine per-lane values with nine independent wave_sum()s costs ~9x18 serialised
+// DPP slots.  Instead every exchange step halves the number of live slots per lane:
+// lanes l / l^32 (v_permlane32_swap), l / l^16 (v_permlane16_swap), l / l^8 (row_ror:8),
+// l / 7-l within 8 (row_half_mirror), then a quad sum.  Afterwards each quad of lanes holds
+// the full wave sum of ONE of the nine values (27 VALU ops, no serial chain).  Which value
+// a lane holds is learned once per wave with reduce9_slot().
+
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __builtin_bit_cast(float,
+                            __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF,
+                                                        0xF, false));
+}
+
+// Pair exchange over lanes l / l^32 (or l^16): one half of the wave keeps x summed with the
+// partner's x, the other half keeps y summed with the partner's y.
+__device__ __forceinline__ float swap32_sum(float x, float y) {
+  auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, x),
+                                            __builtin_bit_cast(unsigned, y), false, false);
+  return __builtin_bit_cast(float, (unsigned)r[0]) + __builtin_bit_cast(float, (unsigned)r[1]);
+}
+__device__ __forceinline__ float swap16_sum(float x, float y) {
+  auto r = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, x),
+                                            __builtin_bit_cast(unsigned, y), false, false);
+  return __builtin_bit_cast(float, (unsigned)r[0]) + __builtin_bit_cast(float, (unsigned)r[1]);
+}
+// Same through a DPP pairing `ctrl` whose partner lane has the opposite `hi` bit.
+template <int CTRL>
+__device__ __forceinline__ float dpp_pair_sum(float x, float y, bool hi) {
+  const float keep = hi ? y : x, send = hi ? x : y;
+  return keep + dpp_f<CTRL>(send);
+}
+
+__device__ __forceinline__ float reduce9(const float (&v)[9]) {
+  const int lane = __lane_id();
+  // 9 slots -> 5 (lanes l, l^32)
+  const float a0 = swap32_sum(v[0], v[5]), a1 = swap32_sum(v[1], v[6]),
+              a2 = swap32_sum(v[2], v[7]), a3 = swap32_sum(v[3], v[8]),
+              a4 = swap32_sum(v[4], 0.f);
+  // 5 -> 3 (lanes l, l^16)
+  const float b0 = swap16_sum(a0, a2), b1 = swap16_sum(a1, a3), b2 = swap16_sum(a4, 0.f);
+  // 3 -> 2 (lanes l, l^8: row_ror:8)
+  const bool h8 = lane & 8, h4 = lane & 4;
+  const float c0 = dpp_pair_sum<0x128>(b0, b1, h8), c1 = dpp_pair_sum<0x128>(b2, 0.f, h8);
+  // 2 -> 1 (lanes l, 7-l within eight: row_half_mirror pairs opposite bit-2 halves)
+  float d = dpp_pair_sum<0x141>(c0, c1, h4);
+  d += dpp_f<0xB1>(d);  // quad_perm [1,0,3,2]
+  d += dpp_f<0x4E>(d);  // quad_perm [2,3,0,1]
+  return d;
+}
+
+// Which of the nine values reduce9() leaves in this lane: 0..8 for one lane per quad
+// (lane % 4 == 0), -1 elsewhere.  Found by reducing a probe where lane 0 holds k+1.
+__device__ __forceinline__ int reduce9_slot() {
+  const int lane = __lane_id();
+  float p[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) p[k] = lane == 0 ? (float)(k + 1) : 0.f;
+  const int s = (int)reduce9(p) - 1;
+  return (lane & 3) == 0 ? s : -1;
+}
+
 __device__ __forceinline__ int wave_max_int(int v) {
   for (int off = 32; off >= 1; off >>= 1) {
     int o = __shfl_xor(v, off, 64);

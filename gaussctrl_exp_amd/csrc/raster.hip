@@ -110,7 +110,7 @@ __global__ __launch_bounds__(256) void raster_fwd3_kernel(
     done[k] = !(i < H && j < W);
   }
   const int2 range = bins[tile];
-  GStage *slot = lds[wave];
+  GStage *stage = lds[wave];
   for (int b = range.x; b < range.y; b += 64) {
     bool all_done = true;
 #pragma unroll
@@ -137,11 +137,11 @@ __global__ __launch_bounds__(256) void raster_fwd3_kernel(
       }
     }
     const unsigned long long kmask = __ballot(keep);
-    if (keep) slot[lanes_below(kmask)] = s;
+    if (keep) stage[lanes_below(kmask)] = s;
     const int n = __popcll(kmask);
     wave_lds_sync();
     for (int t = 0; t < n; ++t) {
-      const GStage G = slot[t];
+      const GStage G = stage[t];
       bool fin = true;
 #pragma unroll
       for (int k = 0; k < PXL; ++k) {
@@ -236,9 +236,10 @@ __global__ __launch_bounds__(256) void raster_bwd3_kernel(
     maxbin = max(maxbin, binf[k]);
   }
   maxbin = wave_max_int(maxbin);
+  const int slot = reduce9_slot();  // record field this lane adds (reduce9), or -1
   const int2 range = bins[tile];
   const int last = min(maxbin, range.y - 1);
-  GStage *slot = lds[wave];
+  GStage *stage = lds[wave];
   for (int b = last; b >= range.x; b -= 64) {
     const int idx = b - lane;
     bool keep = false;
@@ -262,11 +263,11 @@ __global__ __launch_bounds__(256) void raster_bwd3_kernel(
       }
     }
     const unsigned long long kmask = __ballot(keep);
-    if (keep) slot[lanes_below(kmask)] = s;
+    if (keep) stage[lanes_below(kmask)] = s;
     const int n = __popcll(kmask);
     wave_lds_sync();
     for (int t = 0; t < n; ++t) {
-      const GStage G = slot[t];
+      const GStage G = stage[t];
       float s_x = 0.f, s_y = 0.f, s_a = 0.f, s_b = 0.f, s_c = 0.f, s_r = 0.f, s_g = 0.f,
             s_bl = 0.f, s_o = 0.f;
       bool anyv = false;
@@ -302,26 +303,10 @@ __global__ __launch_bounds__(256) void raster_bwd3_kernel(
         }
       }
       if (__any(anyv)) {
-        s_x = wave_sum(s_x);
-        s_y = wave_sum(s_y);
-        s_a = wave_sum(s_a);
-        s_b = wave_sum(s_b);
-        s_c = wave_sum(s_c);
-        s_r = wave_sum(s_r);
-        s_g = wave_sum(s_g);
-        s_bl = wave_sum(s_bl);
-        s_o = wave_sum(s_o);
-        float v = s_x;
-        v = lane == 1 ? s_y : v;
-        v = lane == 2 ? s_a : v;
-        v = lane == 3 ? s_b : v;
-        v = lane == 4 ? s_c : v;
-        v = lane == 5 ? s_r : v;
-        v = lane == 6 ? s_g : v;
-        v = lane == 7 ? s_bl : v;
-        v = lane == 8 ? s_o : v;
+        const float parts[9] = {s_x, s_y, s_a, s_b, s_c, s_r, s_g, s_bl, s_o};
+        const float v = reduce9(parts);
         if constexpr (ATOMICS) {
-          if (lane < 9) atomicAdd(rec + (size_t)G.id * REC + lane, v);
+          if (slot >= 0) atomicAdd(rec + (size_t)G.id * REC + slot, v);
         } else {
           asm volatile("" ::"v"(v));  // ablation build: keep the reduction, drop the atomic
         }

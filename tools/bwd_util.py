@@ -1,0 +1,86 @@
+"""Backward lane utilisation on the headline raster: for sampled tiles, wave iterations after
+the strip cull (touches_rect, restated in torch) vs pixel-Gaussian pairs that are valid
+(idx <= final_idx, sigma >= 0, alpha >= 1/255).  Also the forward's iterations."""
+import os, sys
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+import numpy as np
+import torch
+import bench
+from gaussctrl_exp_amd import _lib
+from gaussctrl_exp_amd.project_gaussians import project_gaussians
+from gaussctrl_exp_amd.rasterize import bin_gaussians
+from gaussctrl_exp_amd.scene import synthetic_scene
+
+cfg = sys.argv[1] if len(sys.argv) > 1 else "headline"
+N, W, H, deg, lo, hi, seed, desc = bench.CONFIGS[cfg]
+dev = torch.device("cuda:0")
+sc = synthetic_scene(N, deg, seed=seed, scale_lo=lo, scale_hi=hi, device=dev)
+cam = bench.view_camera(W, H, 0).to(dev)
+with torch.no_grad():
+    xys, depths, radii, conics, nth, _ = project_gaussians(
+        sc.means, torch.exp(sc.scales), 1, sc.quats / sc.quats.norm(dim=-1, keepdim=True),
+        *cam.project_args())
+    I, gids, bins = bin_gaussians(xys, depths, radii, nth, H, W)
+    tb = cam.tile_bounds
+    colors = torch.rand(N, 3, device=dev)
+    opac = torch.sigmoid(sc.opacities).contiguous()
+    out = torch.empty(H, W, 3, device=dev); fT = torch.empty(H, W, device=dev)
+    fi = torch.empty(H, W, device=dev, dtype=torch.int32)
+    P = _lib.ptr
+    _lib.call("gsplat_rasterize_forward", tb[0], tb[1], H, W, 3, P(gids), P(bins), P(xys),
+              P(conics), P(colors), P(opac), P(torch.zeros(3, device=dev)), P(out), P(fT), P(fi),
+              _lib.stream(dev))
+    torch.cuda.synchronize()
+
+    def touches(gx, gy, a, b, c, o, rx0, rx1, ry0, ry1):
+        dx = gx - torch.clamp(gx, rx0, rx1); dy = gy - torch.clamp(gy, ry0, ry1)
+        d2 = dx * dx + dy * dy
+        hm, hd = 0.5 * (a + c), 0.5 * (a - c)
+        lmax = hm + torch.sqrt(hd * hd + b * b); det = a * c - b * b
+        lmin = det / lmax
+        keep = ~(0.25 * lmin * d2 > torch.log(255 * o) + 0.01)
+        keep |= ~((det > 0) & (lmax > 0))
+        return keep & (o >= 1 / 255)
+
+    rng = np.random.default_rng(0)
+    T = tb[0] * tb[1]
+    sample = rng.choice(T, 256, replace=False)
+    tot = {k: 0.0 for k in ("pairs_valid", "iters_s8", "iters_s4", "iters_s16", "fwd_pairs",
+                            "fwd_iters_s4", "list")}
+    b = bins.cpu().numpy()
+    for t in sample:
+        s, e = int(b[t, 0]), int(b[t, 1])
+        if e <= s:
+            continue
+        tx, ty = t % tb[0], t // tb[0]
+        g = gids[s:e].long()
+        idx = torch.arange(s, e, device=dev)
+        gx, gy = xys[g, 0], xys[g, 1]
+        a, bb, c = conics[g, 0], conics[g, 1], conics[g, 2]
+        o = opac[g, 0]
+        ys = torch.arange(ty * 16, min(ty * 16 + 16, H), device=dev)
+        xs = torch.arange(tx * 16, min(tx * 16 + 16, W), device=dev)
+        py, px = torch.meshgrid(ys.float(), xs.float(), indexing="ij")
+        dx = gx[:, None, None] - px; dy = gy[:, None, None] - py
+        sig = 0.5 * (a[:, None, None] * dx * dx + c[:, None, None] * dy * dy) + bb[:, None, None] * dx * dy
+        al = torch.clamp(o[:, None, None] * torch.exp(-sig), max=0.999)
+        fin = fi[ty * 16: ty * 16 + len(ys), tx * 16: tx * 16 + len(xs)]
+        v = (sig >= 0) & (al >= 1 / 255)
+        tot["fwd_pairs"] += (v & (idx[:, None, None] <= fin + 1)).sum().item()
+        tot["pairs_valid"] += (v & (idx[:, None, None] <= fin)).sum().item()
+        tot["list"] += e - s
+        for rows, key in ((8, "iters_s8"), (4, "iters_s4"), (16, "iters_s16")):
+            for r0 in range(ty * 16, min(ty * 16 + 16, H), rows):
+                r1 = min(r0 + rows - 1, H - 1)
+                k = touches(gx, gy, a, bb, c, o, float(tx * 16), float(min(tx * 16 + 15, W - 1)),
+                            float(r0), float(r1))
+                mf = fin[r0 - ty * 16: r1 - ty * 16 + 1].max().item()
+                tot[key] += (k & (idx <= mf)).sum().item()
+                if key == "iters_s4":
+                    tot["fwd_iters_s4"] += (k & (idx <= mf + 64)).sum().item()
+    n = len(sample)
+    print({k: v / n for k, v in tot.items()})
+    for rows, key in ((8, "iters_s8"), (4, "iters_s4"), (16, "iters_s16")):
+        pix = 16 * rows
+        print(f"strip {rows} rows: iters/tile {tot[key]/n:.0f}; lane util "
+              f"{tot['pairs_valid'] / (tot[key] * pix):.3f}")
