@@ -18,11 +18,15 @@
 //    ballot + mbcnt prefix, so the per-pixel loop only visits Gaussians that can pass
 //    gsplat's alpha >= 1/255 test somewhere in the strip.  The bound never drops a Gaussian
 //    that could contribute, so results are unchanged bit for bit.
-//  * Backward: per Gaussian, the lane sums its PXL pixels' contributions in registers, the
-//    wave reduces the 9 partial sums with DPP row operations, and ONE 9-lane atomic
-//    instruction adds them to the Gaussian's 64-byte-aligned gradient record (one memory
-//    request instead of nine single-lane atomics); a split kernel then writes gsplat's
+//  * Backward (shipped: raster_bwd3p_kernel<1>, 16x8 strips, 2 pixels per lane): the lane's
+//    two pixels are a float2 pair blended branch-free; per Gaussian the lane folds them into
+//    9 partial sums (sigma-gradient moments, colour and opacity terms), the wave
+//    reduce-scatters the 9 sums (common.h reduce9: permlane32/16 swaps + 3 DPP steps) so
+//    that 9 lanes each hold one total, and ONE 9-lane atomic instruction adds them to the
+//    Gaussian's 64-byte gradient record; a split kernel then writes gsplat's
 //    v_xy / v_conic / v_colors / v_opacity tensors.
+//  * Every variant evaluates sigma and exp(-sigma) through the same helpers (gs_sigma*,
+//    gs_vis*), so forward and backward take identical per-pixel decisions.
 //  * C != 3 (gsplat nd_rasterize): one pixel per lane, 4 waves per tile, register
 //    accumulators sized by a compile-time channel bound.
 #include "common.h"
@@ -32,19 +36,42 @@ namespace {
 
 constexpr float ALPHA_MIN = 1.f / 255.f;
 constexpr int REC = 16;  // floats per gradient record: x y a b c r g b o + pad = 64 B
-constexpr int FWD_PXL = 1;
-constexpr int BWD_PXL = 2;
+constexpr int FWD_PXL = 1;  // scalar forward, 16x4 strips (4 waves per tile)
+constexpr int BWD_PXL = 2;  // packed backward, 16x8 strips (2 waves per tile)
 // Tuning / ablation knobs (gsplat_debug_set_raster_variant); defaults are the shipped ones.
 int g_fwd_pxl = FWD_PXL, g_bwd_pxl = BWD_PXL, g_bwd_flags = 0;
 
 struct __attribute__((aligned(16))) GStage {
-  float x, y, a, b;
-  float c, o, r, g;
+  float x, y, ha, b;  // mean, 0.5*conic.a, conic.b
+  float hc, o, r, g;  // 0.5*conic.c, opacity, colour
   float bl;
   int idx;  // position in the tile's sorted list
   int id;   // Gaussian id
   float pad;
 };
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+// sigma = 0.5 (a dx^2 + c dy^2) + b dx dy, evaluated as fma(fma(c/2, dy, b dx), dy, a/2 dx^2)
+// with explicit fmas.  EVERY blend kernel below (scalar or packed, forward or backward) uses
+// exactly this rounding, so the backward re-derives the forward's per-pixel decisions
+// (sigma >= 0, alpha >= 1/255) bit for bit.  hA = (ha*dx)*dx and bdx = b*dx are per
+// (Gaussian, lane): a lane's pixels share one column.
+__device__ __forceinline__ float gs_sigma(float hc, float bdx, float hA, float dy) {
+  return fmaf(fmaf(hc, dy, bdx), dy, hA);
+}
+__device__ __forceinline__ f2 gs_sigma2(float hc, float bdx, float hA, f2 dy) {
+  return __builtin_elementwise_fma(__builtin_elementwise_fma((f2)hc, dy, (f2)bdx), dy, (f2)hA);
+}
+// exp(-sigma) with the hardware exp2 (gsplat: __expf).
+constexpr float NEG_LOG2E = -0x1.715476p+0f;
+__device__ __forceinline__ float gs_vis(float sigma) {
+  return __builtin_amdgcn_exp2f(sigma * NEG_LOG2E);
+}
+__device__ __forceinline__ f2 gs_vis2(f2 sigma) {
+  const f2 e = sigma * NEG_LOG2E;
+  return (f2){__builtin_amdgcn_exp2f(e.x), __builtin_amdgcn_exp2f(e.y)};
+}
 
 // Conservative, exactness-preserving cull of one Gaussian against the pixel-centre
 // rectangle [rx0,rx1] x [ry0,ry1].  For every pixel p in it, with d = xy - p,
@@ -74,6 +101,37 @@ __device__ __forceinline__ uint32_t lanes_below(unsigned long long mask) {
                                    __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
+// Stage this lane's Gaussian (list position idx) if it can touch the wave's rectangle.
+// Returns keep; fills s (colour and ids only when kept).
+__device__ __forceinline__ bool stage_gaussian(int idx, const int *__restrict__ gids,
+                                               const float2 *__restrict__ xys,
+                                               const float *__restrict__ conics,
+                                               const float *__restrict__ colors,
+                                               const float *__restrict__ opacity, float rx0,
+                                               float rx1, float ry0, float ry1, GStage &s) {
+  const int g = gids[idx];
+  const float2 xy = xys[g];
+  const float a = conics[3 * g], b = conics[3 * g + 1], c = conics[3 * g + 2];
+  const float o = opacity[g];
+  const bool keep = touches_rect(xy.x, xy.y, a, b, c, o, rx0, rx1, ry0, ry1);
+  if (keep) {
+    s.x = xy.x;
+    s.y = xy.y;
+    s.ha = 0.5f * a;
+    s.b = b;
+    s.hc = 0.5f * c;
+    s.o = o;
+    s.r = colors[3 * g];
+    s.g = colors[3 * g + 1];
+    s.bl = colors[3 * g + 2];
+    s.idx = idx;
+    s.id = g;
+  }
+  return keep;
+}
+
+// ---------------------------------------------------------------- forward, C = 3
+// Scalar variant: PXL pixels per lane (rows i0 + 4k of one column).
 template <int PXL>
 __global__ __launch_bounds__(256) void raster_fwd3_kernel(
     int tbx, int tby, int H, int W, const int *__restrict__ gids, const int2 *__restrict__ bins,
@@ -117,38 +175,24 @@ __global__ __launch_bounds__(256) void raster_fwd3_kernel(
     for (int k = 0; k < PXL; ++k) all_done = all_done && done[k];
     if (__all(all_done)) break;
     const int idx = b + lane;
-    bool keep = false;
     GStage s;
-    if (idx < range.y) {
-      const int g = gids[idx];
-      const float2 xy = xys[g];
-      s.x = xy.x;
-      s.y = xy.y;
-      s.a = conics[3 * g];
-      s.b = conics[3 * g + 1];
-      s.c = conics[3 * g + 2];
-      s.o = opacity[g];
-      keep = touches_rect(s.x, s.y, s.a, s.b, s.c, s.o, rx0, rx1, ry0, ry1);
-      if (keep) {
-        s.r = colors[3 * g];
-        s.g = colors[3 * g + 1];
-        s.bl = colors[3 * g + 2];
-        s.idx = idx;
-      }
-    }
+    const bool keep = idx < range.y &&
+                      stage_gaussian(idx, gids, xys, conics, colors, opacity, rx0, rx1, ry0,
+                                     ry1, s);
     const unsigned long long kmask = __ballot(keep);
     if (keep) stage[lanes_below(kmask)] = s;
     const int n = __popcll(kmask);
     wave_lds_sync();
     for (int t = 0; t < n; ++t) {
       const GStage G = stage[t];
+      const float dx = G.x - px;
+      const float hA = G.ha * dx * dx, bdx = G.b * dx;
       bool fin = true;
 #pragma unroll
       for (int k = 0; k < PXL; ++k) {
         if (!done[k]) {
-          const float dx = G.x - px, dy = G.y - py[k];
-          const float sigma = 0.5f * (G.a * dx * dx + G.c * dy * dy) + G.b * dx * dy;
-          const float alpha = fminf(0.999f, G.o * __expf(-sigma));
+          const float sigma = gs_sigma(G.hc, bdx, hA, G.y - py[k]);
+          const float alpha = fminf(0.999f, G.o * gs_vis(sigma));
           if (sigma >= 0.f && alpha >= ALPHA_MIN) {
             const float nT = T[k] * (1.f - alpha);
             if (nT <= 1e-4f) {
@@ -184,6 +228,113 @@ __global__ __launch_bounds__(256) void raster_fwd3_kernel(
   }
 }
 
+// Packed variant: 2*NP pixels per lane held as NP float2 pairs and blended branch-free
+// with v_pk_{fma,mul,add}_f32 (two fp32 lanes per VALU op).  A pixel that is not composited
+// this step gets alpha 0, which leaves T and the colour sums exactly unchanged.
+template <int NP>
+__global__ __launch_bounds__(256) void raster_fwd3p_kernel(
+    int tbx, int tby, int H, int W, const int *__restrict__ gids, const int2 *__restrict__ bins,
+    const float2 *__restrict__ xys, const float *__restrict__ conics,
+    const float *__restrict__ colors, const float *__restrict__ opacity,
+    const float *__restrict__ background, float *__restrict__ out_img,
+    float *__restrict__ final_Ts, int *__restrict__ final_idx) {
+  constexpr int PXL = 2 * NP;
+  constexpr int WPT = 4 / PXL;
+  constexpr int TPBLK = 4 / WPT;
+  constexpr int ROWS = 4 * PXL;
+  __shared__ GStage lds[4][64];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int tile = blockIdx.x * TPBLK + wave / WPT;
+  const int strip = wave % WPT;
+  if (tile >= tbx * tby) return;
+  const int tx = tile % tbx, ty = tile / tbx;
+  const int r0 = ty * GS_BLOCK + strip * ROWS;
+  if (r0 >= H) return;
+  const int j = tx * GS_BLOCK + (lane & 15);
+  const int i0 = r0 + (lane >> 4);
+  const float px = (float)j;
+  const float rx0 = (float)(tx * GS_BLOCK), rx1 = (float)min(tx * GS_BLOCK + 15, W - 1);
+  const float ry0 = (float)r0, ry1 = (float)min(r0 + ROWS - 1, H - 1);
+  f2 py[NP], T[NP], cr[NP], cg[NP], cb[NP];
+  int cur[PXL];
+  bool done[PXL];
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const int ia = i0 + 8 * p, ib = ia + 4;
+    py[p] = (f2){(float)ia, (float)ib};
+    T[p] = (f2)1.f;
+    cr[p] = cg[p] = cb[p] = (f2)0.f;
+    cur[2 * p] = cur[2 * p + 1] = 0;
+    done[2 * p] = !(ia < H && j < W);
+    done[2 * p + 1] = !(ib < H && j < W);
+  }
+  const int2 range = bins[tile];
+  GStage *stage = lds[wave];
+  for (int b = range.x; b < range.y; b += 64) {
+    bool all_done = true;
+#pragma unroll
+    for (int k = 0; k < PXL; ++k) all_done = all_done && done[k];
+    if (__all(all_done)) break;
+    const int idx = b + lane;
+    GStage s;
+    const bool keep = idx < range.y &&
+                      stage_gaussian(idx, gids, xys, conics, colors, opacity, rx0, rx1, ry0,
+                                     ry1, s);
+    const unsigned long long kmask = __ballot(keep);
+    if (keep) stage[lanes_below(kmask)] = s;
+    const int n = __popcll(kmask);
+    wave_lds_sync();
+    for (int t = 0; t < n; ++t) {
+      const GStage G = stage[t];
+      const float dx = G.x - px;
+      const float hA = G.ha * dx * dx, bdx = G.b * dx;
+      bool fin = true;
+#pragma unroll
+      for (int p = 0; p < NP; ++p) {
+        const f2 sg = gs_sigma2(G.hc, bdx, hA, G.y - py[p]);
+        const f2 ov = G.o * gs_vis2(sg);
+        const f2 al = {fminf(0.999f, ov.x), fminf(0.999f, ov.y)};
+        const f2 nT = T[p] * (1.f - al);
+        const bool v0 = !done[2 * p] && sg.x >= 0.f && al.x >= ALPHA_MIN;
+        const bool v1 = !done[2 * p + 1] && sg.y >= 0.f && al.y >= ALPHA_MIN;
+        const bool t0 = v0 && nT.x <= 1e-4f, t1 = v1 && nT.y <= 1e-4f;
+        const bool c0 = v0 && !t0, c1 = v1 && !t1;
+        done[2 * p] = done[2 * p] || t0;
+        done[2 * p + 1] = done[2 * p + 1] || t1;
+        const f2 w = (f2){c0 ? al.x : 0.f, c1 ? al.y : 0.f} * T[p];
+        cr[p] = __builtin_elementwise_fma((f2)G.r, w, cr[p]);
+        cg[p] = __builtin_elementwise_fma((f2)G.g, w, cg[p]);
+        cb[p] = __builtin_elementwise_fma((f2)G.bl, w, cb[p]);
+        T[p] = (f2){c0 ? nT.x : T[p].x, c1 ? nT.y : T[p].y};
+        cur[2 * p] = c0 ? G.idx : cur[2 * p];
+        cur[2 * p + 1] = c1 ? G.idx : cur[2 * p + 1];
+        fin = fin && done[2 * p] && done[2 * p + 1];
+      }
+      if (__all(fin)) break;
+    }
+    wave_lds_sync();
+  }
+  const float bg0 = background[0], bg1 = background[1], bg2 = background[2];
+#pragma unroll
+  for (int k = 0; k < PXL; ++k) {
+    const int i = i0 + 4 * k;
+    const int p = k >> 1;
+    const float Tk = (k & 1) ? T[p].y : T[p].x;
+    if (i < H && j < W) {
+      const int pix = i * W + j;
+      final_Ts[pix] = Tk;
+      final_idx[pix] = cur[k];
+      out_img[3 * pix] = ((k & 1) ? cr[p].y : cr[p].x) + Tk * bg0;
+      out_img[3 * pix + 1] = ((k & 1) ? cg[p].y : cg[p].x) + Tk * bg1;
+      out_img[3 * pix + 2] = ((k & 1) ? cb[p].y : cb[p].x) + Tk * bg2;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- backward, C = 3
+// Record fields: 0 v_x, 1 v_y, 2..4 v_conic (a, b, c) * CONIC_SCALE^-1, 5..7 v_rgb,
+// 8 v_opacity.  The scalar kernel stores v_conic itself (scale 1); the packed kernel stores
+// 2*v_conic (the 0.5 is applied once in split_grads_kernel, exact).
 template <int PXL, bool ATOMICS>
 __global__ __launch_bounds__(256) void raster_bwd3_kernel(
     int tbx, int tby, int H, int W, const int *__restrict__ gids, const int2 *__restrict__ bins,
@@ -242,40 +393,27 @@ __global__ __launch_bounds__(256) void raster_bwd3_kernel(
   GStage *stage = lds[wave];
   for (int b = last; b >= range.x; b -= 64) {
     const int idx = b - lane;
-    bool keep = false;
     GStage s;
-    if (idx >= range.x) {
-      const int g = gids[idx];
-      const float2 xy = xys[g];
-      s.x = xy.x;
-      s.y = xy.y;
-      s.a = conics[3 * g];
-      s.b = conics[3 * g + 1];
-      s.c = conics[3 * g + 2];
-      s.o = opacity[g];
-      keep = touches_rect(s.x, s.y, s.a, s.b, s.c, s.o, rx0, rx1, ry0, ry1);
-      if (keep) {
-        s.r = colors[3 * g];
-        s.g = colors[3 * g + 1];
-        s.bl = colors[3 * g + 2];
-        s.idx = idx;
-        s.id = g;
-      }
-    }
+    const bool keep = idx >= range.x &&
+                      stage_gaussian(idx, gids, xys, conics, colors, opacity, rx0, rx1, ry0,
+                                     ry1, s);
     const unsigned long long kmask = __ballot(keep);
     if (keep) stage[lanes_below(kmask)] = s;
     const int n = __popcll(kmask);
     wave_lds_sync();
     for (int t = 0; t < n; ++t) {
       const GStage G = stage[t];
+      const float dx = G.x - px;
+      const float hA = G.ha * dx * dx, bdx = G.b * dx;
+      const float a2 = 2.f * G.ha, c2 = 2.f * G.hc;
       float s_x = 0.f, s_y = 0.f, s_a = 0.f, s_b = 0.f, s_c = 0.f, s_r = 0.f, s_g = 0.f,
             s_bl = 0.f, s_o = 0.f;
       bool anyv = false;
 #pragma unroll
       for (int k = 0; k < PXL; ++k) {
-        const float dx = G.x - px, dy = G.y - py[k];
-        const float sigma = 0.5f * (G.a * dx * dx + G.c * dy * dy) + G.b * dx * dy;
-        const float vis = __expf(-sigma);
+        const float dy = G.y - py[k];
+        const float sigma = gs_sigma(G.hc, bdx, hA, dy);
+        const float vis = gs_vis(sigma);
         const float alpha = fminf(alpha_max, G.o * vis);
         const bool valid = G.idx <= binf[k] && sigma >= 0.f && alpha >= ALPHA_MIN;
         if (valid) {
@@ -297,8 +435,8 @@ __global__ __launch_bounds__(256) void raster_bwd3_kernel(
           s_a += 0.5f * v_sigma * dx * dx;
           s_b += 0.5f * v_sigma * dx * dy;
           s_c += 0.5f * v_sigma * dy * dy;
-          s_x += v_sigma * (G.a * dx + G.b * dy);
-          s_y += v_sigma * (G.b * dx + G.c * dy);
+          s_x += v_sigma * (a2 * dx + G.b * dy);
+          s_y += v_sigma * (G.b * dx + c2 * dy);
           s_o += vis * v_alpha;
         }
       }
@@ -316,8 +454,145 @@ __global__ __launch_bounds__(256) void raster_bwd3_kernel(
   }
 }
 
+// Packed backward: 2*NP pixels per lane as float2 pairs, branch-free (an invalid pixel gets
+// alpha = vis = 0: T, the colour buffer and every partial sum are unchanged exactly).
+// Per pixel the colour buffer is carried as one dot product Sb = sum_c buf_c * v_c, and the
+// sigma gradient as moments V = sum v_sigma, Vy = sum v_sigma dy, Vyy = sum v_sigma dy^2
+// (dx is constant along the lane's column), from which
+//   v_conic = 0.5 (dx^2 V, dx Vy, Vyy),  v_xy = (a dx V + b Vy, b dx V + c Vy).
+template <int NP, bool ATOMICS>
+__global__ __launch_bounds__(256) void raster_bwd3p_kernel(
+    int tbx, int tby, int H, int W, const int *__restrict__ gids, const int2 *__restrict__ bins,
+    const float2 *__restrict__ xys, const float *__restrict__ conics,
+    const float *__restrict__ colors, const float *__restrict__ opacity,
+    const float *__restrict__ background, const float *__restrict__ final_Ts,
+    const int *__restrict__ final_idx, const float *__restrict__ v_out,
+    const float *__restrict__ v_out_alpha, float alpha_max, float *__restrict__ rec) {
+  constexpr int PXL = 2 * NP;
+  constexpr int WPT = 4 / PXL;
+  constexpr int TPBLK = 4 / WPT;
+  constexpr int ROWS = 4 * PXL;
+  __shared__ GStage lds[4][64];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int tile = blockIdx.x * TPBLK + wave / WPT;
+  const int strip = wave % WPT;
+  if (tile >= tbx * tby) return;
+  const int tx = tile % tbx, ty = tile / tbx;
+  const int r0 = ty * GS_BLOCK + strip * ROWS;
+  if (r0 >= H) return;
+  const int j = tx * GS_BLOCK + (lane & 15);
+  const int i0 = r0 + (lane >> 4);
+  const float px = (float)j;
+  const float rx0 = (float)(tx * GS_BLOCK), rx1 = (float)min(tx * GS_BLOCK + 15, W - 1);
+  const float ry0 = (float)r0, ry1 = (float)min(r0 + ROWS - 1, H - 1);
+  const float bg0 = background[0], bg1 = background[1], bg2 = background[2];
+  f2 py[NP], T[NP], vr[NP], vg[NP], vb[NP], q[NP], Sb[NP];
+  int binf[PXL];
+  int maxbin = -1;
+#pragma unroll
+  for (int k = 0; k < PXL; ++k) {
+    const int i = i0 + 4 * k, p = k >> 1;
+    float Tf = 0.f, r = 0.f, g = 0.f, bl = 0.f, a = 0.f;
+    int bf = -1;
+    if (i < H && j < W) {
+      const int pix = i * W + j;
+      Tf = final_Ts[pix];
+      bf = final_idx[pix];
+      r = v_out[3 * pix];
+      g = v_out[3 * pix + 1];
+      bl = v_out[3 * pix + 2];
+      a = v_out_alpha[pix];
+    }
+    // v_alpha's background/alpha terms: Tf/(1-alpha) * (v_alpha_out - bg . v_out)
+    const float qk = Tf * (a - (bg0 * r + bg1 * g + bg2 * bl));
+    if (k & 1) {
+      py[p].y = (float)i; T[p].y = Tf; vr[p].y = r; vg[p].y = g; vb[p].y = bl; q[p].y = qk;
+    } else {
+      py[p].x = (float)i; T[p].x = Tf; vr[p].x = r; vg[p].x = g; vb[p].x = bl; q[p].x = qk;
+    }
+    Sb[p] = (f2)0.f;
+    binf[k] = bf;
+    maxbin = max(maxbin, bf);
+  }
+  maxbin = wave_max_int(maxbin);
+  const int slot = reduce9_slot();
+  const int2 range = bins[tile];
+  const int last = min(maxbin, range.y - 1);
+  GStage *stage = lds[wave];
+  for (int b = last; b >= range.x; b -= 64) {
+    const int idx = b - lane;
+    GStage s;
+    const bool keep = idx >= range.x &&
+                      stage_gaussian(idx, gids, xys, conics, colors, opacity, rx0, rx1, ry0,
+                                     ry1, s);
+    const unsigned long long kmask = __ballot(keep);
+    if (keep) stage[lanes_below(kmask)] = s;
+    const int n = __popcll(kmask);
+    wave_lds_sync();
+    for (int t = 0; t < n; ++t) {
+      const GStage G = stage[t];
+      const float dx = G.x - px;
+      const float hA = G.ha * dx * dx, bdx = G.b * dx;
+      f2 sr = 0.f, sg = 0.f, sb = 0.f, so = 0.f, V = 0.f, Vy = 0.f, Vyy = 0.f;
+      bool anyv = false;
+#pragma unroll
+      for (int p = 0; p < NP; ++p) {
+        const f2 dy = G.y - py[p];
+        const f2 sig = gs_sigma2(G.hc, bdx, hA, dy);
+        const f2 vis = gs_vis2(sig);
+        const f2 ov = G.o * vis;
+        const f2 al = {fminf(alpha_max, ov.x), fminf(alpha_max, ov.y)};
+        const bool v0 = G.idx <= binf[2 * p] && sig.x >= 0.f && al.x >= ALPHA_MIN;
+        const bool v1 = G.idx <= binf[2 * p + 1] && sig.y >= 0.f && al.y >= ALPHA_MIN;
+        anyv = anyv || v0 || v1;
+        const f2 am = {v0 ? al.x : 0.f, v1 ? al.y : 0.f};
+        const f2 vm = {v0 ? vis.x : 0.f, v1 ? vis.y : 0.f};
+        const f2 om = 1.f - am;
+        const f2 ra = {__builtin_amdgcn_rcpf(om.x), __builtin_amdgcn_rcpf(om.y)};
+        T[p] = T[p] * ra;
+        const f2 fac = am * T[p];
+        sr = __builtin_elementwise_fma(fac, vr[p], sr);
+        sg = __builtin_elementwise_fma(fac, vg[p], sg);
+        sb = __builtin_elementwise_fma(fac, vb[p], sb);
+        const f2 gv = __builtin_elementwise_fma(
+            (f2)G.r, vr[p], __builtin_elementwise_fma((f2)G.g, vg[p], G.bl * vb[p]));
+        const f2 v_alpha = __builtin_elementwise_fma(gv, T[p], ra * (q[p] - Sb[p]));
+        Sb[p] = __builtin_elementwise_fma(fac, gv, Sb[p]);
+        const f2 vva = vm * v_alpha;
+        so += vva;
+        const f2 vs = vva * (-G.o);
+        const f2 vsdy = vs * dy;
+        V += vs;
+        Vy += vsdy;
+        Vyy = __builtin_elementwise_fma(vsdy, dy, Vyy);
+      }
+      if (__any(anyv)) {
+        const float Vs = V.x + V.y, Vys = Vy.x + Vy.y;
+        const float dxV = dx * Vs;
+        const float parts[9] = {fmaf(2.f * G.ha, dxV, G.b * Vys),  // v_x
+                                fmaf(G.b, dxV, 2.f * G.hc * Vys),  // v_y
+                                dx * dxV,                          // 2 v_conic.a
+                                dx * Vys,                          // 2 v_conic.b
+                                Vyy.x + Vyy.y,                     // 2 v_conic.c
+                                sr.x + sr.y,
+                                sg.x + sg.y,
+                                sb.x + sb.y,
+                                so.x + so.y};
+        const float v = reduce9(parts);
+        if constexpr (ATOMICS) {
+          if (slot >= 0) atomicAdd(rec + (size_t)G.id * REC + slot, v);
+        } else {
+          asm volatile("" ::"v"(v));
+        }
+      }
+    }
+    wave_lds_sync();
+  }
+}
+
 // Gradient records -> gsplat's v_xy [N,2], v_conic [N,3], v_colors [N,3], v_opacity [N].
 __global__ __launch_bounds__(256) void split_grads_kernel(int n, const float4 *__restrict__ rec,
+                                                          float conic_scale,
                                                           float *__restrict__ v_xy,
                                                           float *__restrict__ v_conic,
                                                           float *__restrict__ v_rgb,
@@ -328,9 +603,9 @@ __global__ __launch_bounds__(256) void split_grads_kernel(int n, const float4 *_
                r2 = rec[(size_t)g * (REC / 4) + 2];
   v_xy[2 * g] = r0.x;
   v_xy[2 * g + 1] = r0.y;
-  v_conic[3 * g] = r0.z;
-  v_conic[3 * g + 1] = r0.w;
-  v_conic[3 * g + 2] = r1.x;
+  v_conic[3 * g] = conic_scale * r0.z;
+  v_conic[3 * g + 1] = conic_scale * r0.w;
+  v_conic[3 * g + 2] = conic_scale * r1.x;
   v_rgb[3 * g] = r1.y;
   v_rgb[3 * g + 1] = r1.z;
   v_rgb[3 * g + 2] = r1.w;
@@ -577,10 +852,17 @@ extern "C" int gsplat_rasterize_forward(int tile_bounds_x, int tile_bounds_y, in
                      tile_bounds_y, img_height, img_width, gaussian_ids_sorted,                \
                      (const int2 *)tile_bins, (const float2 *)xys, conics, colors, opacity,    \
                      background, out_img, final_Ts, final_idx)
-    if (g_fwd_pxl == 4) FWD3(4);
-    else if (g_fwd_pxl == 2) FWD3(2);
+#define FWD3P(NP)                                                                          \
+  hipLaunchKernelGGL(raster_fwd3p_kernel<NP>, dim3(cdiv(T, 2 * NP)), dim3(256), 0, st,          \
+                     tile_bounds_x, tile_bounds_y, img_height, img_width, gaussian_ids_sorted,  \
+                     (const int2 *)tile_bins, (const float2 *)xys, conics, colors, opacity,     \
+                     background, out_img, final_Ts, final_idx)
+    const bool scalar = g_bwd_flags & 4;
+    if (g_fwd_pxl == 4) { if (scalar) FWD3(4); else FWD3P(2); }
+    else if (g_fwd_pxl == 2) { if (scalar) FWD3(2); else FWD3P(1); }
     else FWD3(1);
 #undef FWD3
+#undef FWD3P
   } else {
     ND_DISPATCH(raster_fwdn_kernel, tile_bounds_x, tile_bounds_y, img_height, img_width,
                 channels, gaussian_ids_sorted, (const int2 *)tile_bins, (const float2 *)xys,
@@ -640,13 +922,24 @@ extern "C" int gsplat_rasterize_backward(int tile_bounds_x, int tile_bounds_y, i
                      tile_bounds_x, tile_bounds_y, img_height, img_width, gaussian_ids_sorted,  \
                      (const int2 *)tile_bins, (const float2 *)xys, conics, colors, opacity,     \
                      background, final_Ts, final_idx, v_output, v_output_alpha, alpha_max, rec)
+#define BWD3P(NP, A)                                                                       \
+  hipLaunchKernelGGL((raster_bwd3p_kernel<NP, A>), dim3(cdiv(T, 2 * NP)), dim3(256), 0, st,     \
+                     tile_bounds_x, tile_bounds_y, img_height, img_width, gaussian_ids_sorted,  \
+                     (const int2 *)tile_bins, (const float2 *)xys, conics, colors, opacity,     \
+                     background, final_Ts, final_idx, v_output, v_output_alpha, alpha_max, rec)
     const bool atomics = !(g_bwd_flags & 1);
-    if (g_bwd_pxl == 4) { if (atomics) BWD3(4, true); else BWD3(4, false); }
+    const bool packed = g_bwd_pxl >= 2 && !(g_bwd_flags & 2);
+    if (packed) {
+      if (g_bwd_pxl == 4) { if (atomics) BWD3P(2, true); else BWD3P(2, false); }
+      else { if (atomics) BWD3P(1, true); else BWD3P(1, false); }
+    } else if (g_bwd_pxl == 4) { if (atomics) BWD3(4, true); else BWD3(4, false); }
     else if (g_bwd_pxl == 1) { if (atomics) BWD3(1, true); else BWD3(1, false); }
     else { if (atomics) BWD3(2, true); else BWD3(2, false); }
 #undef BWD3
+#undef BWD3P
     hipLaunchKernelGGL(split_grads_kernel, dim3(cdiv(num_points, 256)), dim3(256), 0, st,
-                       num_points, (const float4 *)rec, v_xy, v_conic, v_colors, v_opacity);
+                       num_points, (const float4 *)rec, packed ? 0.5f : 1.f, v_xy, v_conic,
+                       v_colors, v_opacity);
   } else {
     if (num_points > 0) {
       note(hipMemsetAsync(v_xy, 0, (size_t)num_points * 2 * sizeof(float), st), "hipMemsetAsync");

@@ -192,6 +192,10 @@ def _raster_case(gpu, case, C=3, colors_u8=False):
 
 @pytest.mark.parametrize("case", CASES)
 def test_raster_forward(gpu, case):
+    _check_raster_forward(gpu, case)
+
+
+def _check_raster_forward(gpu, case):
     sc, cam, g, o, colors, opac, bg = _raster_case(gpu, case)
     xys, depths, radii, conics, nth, cov3d = g
     img, alpha = rasterize_gaussians(xys, depths, radii, conics, nth, colors.to(gpu),
@@ -208,6 +212,28 @@ def test_raster_forward(gpu, case):
 def test_raster_backward(gpu, case):
     """Backward kernel parity, fed the GPU forward state (final_Ts / final_idx) so a forward
     threshold flip cannot leak into the gradient comparison."""
+    _check_raster_backward(gpu, case)
+
+
+# (fwd pixels/lane, bwd pixels/lane, flags): flags 1 = no atomics (timing only), 2 = scalar
+# backward, 4 = scalar forward; pixels/lane >= 2 default to the packed float2 kernels.
+RASTER_VARIANTS = [(1, 2, 0), (2, 2, 0), (4, 4, 0), (2, 2, 6), (4, 4, 6), (1, 1, 0)]
+
+
+@pytest.mark.parametrize("variant", RASTER_VARIANTS)
+@pytest.mark.parametrize("case", [CASES[0], CASES[1], CASES[3]])
+def test_raster_variants(gpu, case, variant):
+    """Every blend-kernel variant reachable through gsplat_debug_set_raster_variant meets the
+    same bar as the shipped one."""
+    _lib.call("gsplat_debug_set_raster_variant", *variant)
+    try:
+        _check_raster_forward(gpu, case)
+        _check_raster_backward(gpu, case)
+    finally:
+        _lib.call("gsplat_debug_set_raster_variant", 1, 2, 0)
+
+
+def _check_raster_backward(gpu, case):
     sc, cam, g, o, colors, opac, bg = _raster_case(gpu, case)
     xys, depths, radii, conics, nth, cov3d = [t.detach() for t in g]
     H, W = cam.height, cam.width

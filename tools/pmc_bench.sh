@@ -1,0 +1,16 @@
+#!/bin/bash
+# PMC passes over a short bench run (one counter group per rocprofv3 run, kernel-trace only).
+# Output: gpurun_out/pmc_<name>/... counter_collection.csv per pass.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+ARGS=${BENCH_ARGS:---steps 3 --warmup 1 --no-cpu-baseline}
+run() {  # run <name> <counters...>
+  local name=$1; shift
+  timeout -k 10 300 rocprofv3 --pmc "$@" --output-format csv -d gpurun_out/pmc_$name -o run \
+    -- python3 bench.py $ARGS > gpurun_out/pmc_$name.log 2>&1
+}
+run fetch FETCH_SIZE && run write WRITE_SIZE && \
+run sq SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAIT_INST_ANY \
+  SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU_TRANS_F32 && \
+run sq2 SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_WAVES SQ_INSTS_VMEM_RD \
+  SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS

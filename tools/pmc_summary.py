@@ -1,0 +1,31 @@
+"""Per-kernel averages of rocprofv3 --pmc CSV passes (tools/pmc_bench.sh output).
+Usage: pmc_summary.py gpurun_out [out.csv]"""
+import collections
+import csv
+import glob
+import os
+import re
+import sys
+
+root = sys.argv[1]
+acc = collections.defaultdict(lambda: collections.defaultdict(list))
+for f in glob.glob(os.path.join(root, "pmc_*", "*counter_collection.csv")):
+    for r in csv.DictReader(open(f)):
+        name = r["Kernel_Name"].replace("(anonymous namespace)::", "")
+        if name.startswith("void gs::") or name.startswith("gs::"):
+            name = re.sub(r"\(.*$", "", name)
+        else:
+            continue
+        acc[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
+rows = []
+for k, d in sorted(acc.items()):
+    row = {"kernel": k}
+    for c, v in sorted(d.items()):
+        row[c] = sum(v) / len(v)
+    rows.append(row)
+cols = sorted({c for r in rows for c in r if c != "kernel"})
+out = sys.argv[2] if len(sys.argv) > 2 else None
+w = csv.writer(open(out, "w", newline="") if out else sys.stdout)
+w.writerow(["kernel"] + cols)
+for r in rows:
+    w.writerow([r["kernel"]] + [f"{r.get(c, float('nan')):.4g}" for c in cols])
