@@ -5,7 +5,7 @@ BASELINE.json metric: "Mpixels/s fwd+bwd and train iters/s, 1M Gaussians @ 1080^
 
 A step = one view per GPU: project -> SH (deg 3) -> bin/sort -> rasterize forward ->
 loss -> backward through rasterize / SH / project, plus (N > 1) the RCCL all-reduce of the
-flat Gaussian-gradient bucket -- the multi-view exchange of the data-parallel train step
+Gaussian gradients -- the multi-view exchange of the data-parallel train step
 (SURVEY.md §8e).  `value` = all ranks' rendered pixels / max-over-ranks step time.  The
 full train step (splatfacto 0.8 L1 + 0.2 SSIM loss + Adam) is timed separately and
 reported as `train_iters_per_s`.  Inputs are synthetic (SURVEY.md §8d scene: random
@@ -159,10 +159,9 @@ def main():
     trainer = TrainStep(scene, sh_degree=deg, world_size=world, loss="l1")
 
     def step():
-        trainer.bucket.zero_()
+        trainer.zero_grad()
         trainer.forward_backward(cam, gt, bg)
-        if world > 1:
-            trainer.bucket.all_reduce_()
+        trainer.sync_grads()
 
     def barrier():
         if world > 1:
@@ -269,7 +268,7 @@ def main():
                 "sh_degree": deg,
                 "views_per_gpu_per_step": 1,
                 "parallelism": f"dp{world} (1 view/GPU, RCCL all-reduce of {N * 59 * 4} B "
-                               f"grad bucket)" if world > 1 else "dp1",
+                               f"of gradients per step)" if world > 1 else "dp1",
             },
             "train_iters_per_s": round(tsteps / tdt, 2),
             "train_views_per_s": round(world * tsteps / tdt, 2),

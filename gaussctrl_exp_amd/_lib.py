@@ -42,8 +42,8 @@ SIGNATURES = {
     "gsplat_get_tile_bin_edges": (_I, [_I64, _P, _P, _I64, _P]),
     "gsplat_bin_count_workspace_size": (_SZ, [_I]),
     "gsplat_bin_emit_workspace_size": (_SZ, [_I64]),
-    "gsplat_bin_count": (_I, [_I, _P, _P, _P, _P, _P, _SZ, _P]),
-    "gsplat_bin_emit": (_I, [_I, _I64, _P, _P, _I, _I, _P, _P, _P, _SZ, _P, _SZ, _P]),
+    "gsplat_bin_count": (_I, [_I, _P, _P, _P, _P, _I, _I, _P, _P, _SZ, _P]),
+    "gsplat_bin_emit": (_I, [_I, _I64, _I, _I, _P, _P, _P, _SZ, _P, _SZ, _P]),
     "gsplat_rasterize_forward": (_I, [_I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                                       _P, _P]),
     "gsplat_rasterize_backward_workspace_size": (_SZ, [_I, _I]),
@@ -51,6 +51,8 @@ SIGNATURES = {
     "gsplat_rasterize_backward": (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P,
                                        _P, _P, _P, _F, _P, _P, _P, _P, _P, _SZ, _P]),
 }
+
+ABI_VERSION = 3  # include/gsplat_mi355x.h GSPLAT_MI355X_ABI_VERSION
 
 _lib = None
 
@@ -73,7 +75,7 @@ def lib():
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
-        if L.gsplat_abi_version() != 2:
+        if L.gsplat_abi_version() != ABI_VERSION:
             raise RuntimeError("libgsplat_mi355x.so ABI version mismatch")
         _lib = L
     return _lib

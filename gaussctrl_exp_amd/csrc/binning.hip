@@ -171,8 +171,21 @@ __global__ __launch_bounds__(TPB) void os_hist_kernel(const K *__restrict__ keys
   const int R = 1 << width;
   for (int i = threadIdx.x; i < passes * 256; i += TPB) lh[i] = 0;
   __syncthreads();
-  for (long long i = (long long)blockIdx.x * TPB + threadIdx.x; i < n;
-       i += (long long)gridDim.x * TPB) {
+  const long long stride = (long long)gridDim.x * TPB;
+  long long i = (long long)blockIdx.x * TPB + threadIdx.x;
+  for (; i + 3 * stride < n; i += 4 * stride) {  // four independent loads in flight
+    K k[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) k[u] = keys[i + u * stride];
+    for (int p = 0; p < passes; ++p) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t d = (uint32_t)(k[u] >> (begin_bit + p * width)) & (uint32_t)(R - 1);
+        atomicAdd(&lh[p * 256 + d], 1u);
+      }
+    }
+  }
+  for (; i < n; i += stride) {
     const K k = keys[i];
     for (int p = 0; p < passes; ++p) {
       const uint32_t d = (uint32_t)(k >> (begin_bit + p * width)) & (uint32_t)(R - 1);
@@ -337,7 +350,9 @@ int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t
   uint32_t *err = tickets + OS_MAX_PASSES;
   uint32_t *status = (uint32_t *)ws + OS_HEAD_WORDS;
   note(hipMemsetAsync(ws, 0, radix_ws_bytes(n, begin_bit, end_bit), st), "hipMemsetAsync");
-  const int hist_blocks = (int)min((long long)cdiv(n, TPB * 8), 2048LL);
+  // Few, fat histogram blocks: every block flushes passes x 256 counters with global
+  // atomics onto the SAME addresses, which the L2 serialises -- 2048 blocks cost ~35 us.
+  const int hist_blocks = (int)min((long long)cdiv(n, TPB * 64), 256LL);
   hipLaunchKernelGGL(os_hist_kernel<K>, dim3(hist_blocks), dim3(TPB), 0, st, ka, n, begin_bit,
                      p.width, p.passes, hist);
   K *kin = ka, *kalt = kb;
@@ -373,30 +388,48 @@ __device__ __forceinline__ void tile_bbox(float x, float y, float radius, int tb
 }
 
 // Depth keys: visible -> float bits of depth (positive floats order as uints), culled ->
-// 0xFFFFFFFF (sorted last).
-__global__ __launch_bounds__(TPB) void depth_keys_kernel(int n, const float *__restrict__ depths,
+// 0xFFFFFFFF (sorted last).  Also writes the Gaussian's binning record, read by coalesced
+// loads here so that the depth-ordered passes need ONE gather per Gaussian:
+// rec[g] = {tile allotment, x0 | y0 << 16, x1 | y1 << 16, 0} (tile bbox, T < 65536).
+__global__ __launch_bounds__(TPB) void depth_keys_kernel(int n, const float *__restrict__ xys,
+                                                         const float *__restrict__ depths,
                                                          const int *__restrict__ radii,
+                                                         const int *__restrict__ num_tiles_hit,
+                                                         int tbx, int tby,
                                                          uint32_t *__restrict__ keys,
-                                                         uint32_t *__restrict__ vals) {
+                                                         uint32_t *__restrict__ vals,
+                                                         uint4 *__restrict__ rec) {
   int i = blockIdx.x * TPB + threadIdx.x;
   if (i >= n) return;
-  keys[i] = radii[i] > 0 ? __float_as_uint(depths[i]) : 0xFFFFFFFFu;
+  const int r = radii[i];
+  const bool vis = r > 0;
+  keys[i] = vis ? __float_as_uint(depths[i]) : 0xFFFFFFFFu;
   vals[i] = (uint32_t)i;
+  const int c = vis ? num_tiles_hit[i] : 0;
+  uint4 q = {c > 0 ? (uint32_t)c : 0u, 0u, 0u, 0u};
+  if (c > 0) {
+    int x0, x1, y0, y1;
+    tile_bbox(xys[2 * i], xys[2 * i + 1], (float)r, tbx, tby, x0, x1, y0, y1);
+    q.y = (uint32_t)x0 | ((uint32_t)y0 << 16);
+    q.z = (uint32_t)x1 | ((uint32_t)y1 << 16);
+  }
+  rec[i] = q;
 }
 
-// cnt[p] = tiles hit by the p-th Gaussian in depth order; the visible count is the index
-// where the depth-sorted keys reach the culled sentinel.
+// Depth-ordered allotments and boxes: cnt[p], box[p] from the p-th Gaussian's record (the
+// one random gather of the binning); the visible count is the index where the depth-sorted
+// keys reach the culled sentinel.
 __global__ __launch_bounds__(TPB) void gather_counts_kernel(int n, const uint32_t *__restrict__ order,
                                                             const uint32_t *__restrict__ skeys,
-                                                            const int *__restrict__ radii,
-                                                            const int *__restrict__ num_tiles_hit,
+                                                            const uint4 *__restrict__ rec,
                                                             uint32_t *__restrict__ cnt,
+                                                            uint2 *__restrict__ box,
                                                             int *__restrict__ num_visible) {
   int p = blockIdx.x * TPB + threadIdx.x;
   if (p >= n) return;
-  uint32_t g = order[p];
-  int c = radii[g] > 0 ? num_tiles_hit[g] : 0;
-  cnt[p] = c > 0 ? (uint32_t)c : 0u;
+  const uint4 q = rec[order[p]];
+  cnt[p] = q.x;
+  box[p] = make_uint2(q.y, q.z);
   const bool vis = skeys[p] != 0xFFFFFFFFu;
   if (vis && (p == n - 1 || skeys[p + 1] == 0xFFFFFFFFu)) *num_visible = p + 1;
 }
@@ -409,9 +442,8 @@ __global__ __launch_bounds__(TPB) void gather_counts_kernel(int n, const uint32_
 __global__ __launch_bounds__(TPB) void emit_kernel(int n, const uint32_t *__restrict__ order,
                                                    const uint32_t *__restrict__ cnt,
                                                    const uint32_t *__restrict__ off,
-                                                   const float *__restrict__ xys,
-                                                   const int *__restrict__ radii, int tbx, int tby,
-                                                   uint32_t *__restrict__ tkeys,
+                                                   const uint2 *__restrict__ box, int tbx,
+                                                   int tby, uint32_t *__restrict__ tkeys,
                                                    uint32_t *__restrict__ tvals) {
   const int lane = threadIdx.x & 63;
   const long long p0 = ((long long)blockIdx.x * TPB + threadIdx.x) - lane;
@@ -425,8 +457,10 @@ __global__ __launch_bounds__(TPB) void emit_kernel(int n, const uint32_t *__rest
     start = off[p];
     if (c) {
       g = order[p];
-      int x1, y1;
-      tile_bbox(xys[2 * g], xys[2 * g + 1], (float)radii[g], tbx, tby, x0, x1, y0, y1);
+      const uint2 b = box[p];
+      x0 = (int)(b.x & 0xFFFFu);
+      y0 = (int)(b.x >> 16);
+      const int x1 = (int)(b.y & 0xFFFFu), y1 = (int)(b.y >> 16);
       bw = max(x1 - x0, 1);
       area = max(x1 - x0, 0) * max(y1 - y0, 0);
     }
@@ -518,6 +552,8 @@ struct Carver {
 
 struct Phase1 {
   uint32_t *dkeys_a, *dvals_a, *dkeys_b, *dvals_b, *dkeys_s, *order, *cnt, *off;
+  uint4 *rec;  // per-Gaussian binning record (Gaussian order)
+  uint2 *box;  // tile bbox in depth order
   void *rs_ws;
   size_t bytes;
 };
@@ -534,6 +570,8 @@ Phase1 carve_phase1(void *base, int n) {
   p.order = c.take<uint32_t>(nn);
   p.cnt = c.take<uint32_t>(nn);
   p.off = c.take<uint32_t>(nn);
+  p.rec = c.take<uint4>(nn * 4);
+  p.box = c.take<uint2>(nn * 2);
   size_t rs = radix_ws_bytes(n, 0, 32);
   size_t sc = scan_ws_bytes(n);
   p.rs_ws = c.take<char>(rs > sc ? rs : sc);
@@ -580,12 +618,15 @@ extern "C" size_t gsplat_bin_emit_workspace_size(int64_t num_intersects) {
   return carve_phase2(nullptr, num_intersects).bytes;
 }
 
-extern "C" int gsplat_bin_count(int num_points, const float *depths, const int32_t *radii,
-                                const int32_t *num_tiles_hit, int32_t *d_counts,
+extern "C" int gsplat_bin_count(int num_points, const float *xys, const float *depths,
+                                const int32_t *radii, const int32_t *num_tiles_hit,
+                                int tile_bounds_x, int tile_bounds_y, int32_t *d_counts,
                                 void *workspace1, size_t workspace1_bytes, void *stream) {
   hipStream_t st = (hipStream_t)stream;
-  if (num_points < 0) {
-    set_error("bin_count: bad size");
+  const long long T = (long long)tile_bounds_x * tile_bounds_y;
+  if (num_points < 0 || tile_bounds_x <= 0 || tile_bounds_y <= 0 || T >= 65536) {
+    set_error("bin_count: bad sizes (N=%d tiles=%dx%d)", num_points, tile_bounds_x,
+              tile_bounds_y);
     return 1;
   }
   Phase1 p = carve_phase1(workspace1, num_points);
@@ -596,21 +637,22 @@ extern "C" int gsplat_bin_count(int num_points, const float *depths, const int32
   note(hipMemsetAsync(d_counts, 0, 2 * sizeof(int32_t), st), "hipMemsetAsync");
   if (num_points == 0) return check_launch("bin_count");
   const int n = num_points;
-  hipLaunchKernelGGL(depth_keys_kernel, dim3(cdiv(n, TPB)), dim3(TPB), 0, st, n, depths, radii,
-                     p.dkeys_a, p.dvals_a);
+  hipLaunchKernelGGL(depth_keys_kernel, dim3(cdiv(n, TPB)), dim3(TPB), 0, st, n, xys, depths,
+                     radii, num_tiles_hit, tile_bounds_x, tile_bounds_y, p.dkeys_a, p.dvals_a,
+                     p.rec);
   radix_sort_pairs<uint32_t>(p.dkeys_a, p.dvals_a, p.dkeys_b, p.dvals_b, p.dkeys_s, p.order, n, 0,
                              32, p.rs_ws, st);
   hipLaunchKernelGGL(gather_counts_kernel, dim3(cdiv(n, TPB)), dim3(TPB), 0, st, n, p.order,
-                     p.dkeys_s, radii, num_tiles_hit, p.cnt, d_counts);
+                     p.dkeys_s, p.rec, p.cnt, p.box, d_counts);
   device_exclusive_scan(p.cnt, p.off, n, (uint32_t *)(d_counts + 1), (uint32_t *)p.rs_ws, st);
   return check_launch("bin_count");
 }
 
-extern "C" int gsplat_bin_emit(int num_points, int64_t num_intersects, const float *xys,
-                               const int32_t *radii, int tile_bounds_x, int tile_bounds_y,
-                               int32_t *gaussian_ids_sorted, int32_t *tile_bins,
-                               const void *workspace1, size_t workspace1_bytes,
-                               void *workspace2, size_t workspace2_bytes, void *stream) {
+extern "C" int gsplat_bin_emit(int num_points, int64_t num_intersects, int tile_bounds_x,
+                               int tile_bounds_y, int32_t *gaussian_ids_sorted,
+                               int32_t *tile_bins, const void *workspace1,
+                               size_t workspace1_bytes, void *workspace2,
+                               size_t workspace2_bytes, void *stream) {
   hipStream_t st = (hipStream_t)stream;
   const long long T = (long long)tile_bounds_x * tile_bounds_y;
   if (num_points < 0 || num_intersects < 0 || num_intersects > 0x3FFFFFFFLL ||
@@ -631,7 +673,7 @@ extern "C" int gsplat_bin_emit(int num_points, int64_t num_intersects, const flo
   const int n = num_points;
   const long long I = num_intersects;
   hipLaunchKernelGGL(emit_kernel, dim3(cdiv(n, TPB)), dim3(TPB), 0, st, n, p1.order, p1.cnt,
-                     p1.off, xys, radii, tile_bounds_x, tile_bounds_y, p2.tk_a, p2.tv_a);
+                     p1.off, p1.box, tile_bounds_x, tile_bounds_y, p2.tk_a, p2.tv_a);
   radix_sort_pairs<uint32_t>(p2.tk_a, p2.tv_a, p2.tk_b, p2.tv_b, p2.tk_s,
                              (uint32_t *)gaussian_ids_sorted, I, 0, bits_for(T), p2.rs_ws, st);
   hipLaunchKernelGGL((bin_edges_kernel<uint32_t, 0>), dim3(cdiv(I, TPB)), dim3(TPB), 0, st, I,

@@ -68,8 +68,18 @@ __device__ __forceinline__ int sh_basis(int degree, float dx, float dy, float dz
   return 25;
 }
 
-// 256 Gaussians per workgroup (48 KiB of LDS at degree 3); 128 at degree 4.
+// 256 Gaussians per workgroup (49 KiB of LDS at degree 3); 128 at degree 4.
 __host__ __device__ constexpr int sh_threads(int K) { return K > 16 ? 128 : 256; }
+
+// LDS row pitch: each thread reads/writes its own row, so an even pitch (48 floats at
+// degree 3) puts a wave's 64 rows on 4 of the 64 banks (16-way conflicts); an odd pitch
+// spreads them over all banks.
+__host__ __device__ constexpr int sh_row_pitch(int K) { return (K * 3) | 1; }
+template <int ROW, int ROWP>
+__device__ __forceinline__ int sh_lds_index(int k) {
+  const int r = k / ROW;
+  return r * ROWP + (k - r * ROW);
+}
 
 // Coefficient rows are K*3 floats; the block's slab [256*K*3] is copied with 16-byte
 // vector loads when the slab start is 16-byte aligned, else with dword loads.
@@ -80,19 +90,41 @@ __global__ __launch_bounds__(256) void sh_fwd_kernel(int n, int degrees_to_use,
                                                              float *__restrict__ colors) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int ROW = K * 3;
+  constexpr int ROWP = sh_row_pitch(K);
   constexpr int SH_THREADS = sh_threads(K);
   const long long g0 = (long long)blockIdx.x * SH_THREADS;
   const int cnt = (int)min((long long)SH_THREADS, (long long)n - g0);
   const int total = cnt * ROW;
   const float *src = coeffs + g0 * ROW;
-  if ((((uintptr_t)src) & 15) == 0) {
+  if (ROW % 4 == 0 && cnt == SH_THREADS && (((uintptr_t)src) & 15) == 0) {
+    // full block: all of this thread's ROW/4 16-byte loads are issued before any LDS write
+    constexpr int PER = ROW % 4 == 0 ? ROW / 4 : 1;
+    const float4 *s4 = reinterpret_cast<const float4 *>(src);
+    float4 v[PER];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) v[u] = s4[u * SH_THREADS + threadIdx.x];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int k = 4 * (u * SH_THREADS + threadIdx.x);
+      smem[sh_lds_index<ROW, ROWP>(k)] = v[u].x;
+      smem[sh_lds_index<ROW, ROWP>(k + 1)] = v[u].y;
+      smem[sh_lds_index<ROW, ROWP>(k + 2)] = v[u].z;
+      smem[sh_lds_index<ROW, ROWP>(k + 3)] = v[u].w;
+    }
+  } else if ((((uintptr_t)src) & 15) == 0) {
     const int nv = total >> 2;
     const float4 *s4 = reinterpret_cast<const float4 *>(src);
-    float4 *d4 = reinterpret_cast<float4 *>(smem);
-    for (int k = threadIdx.x; k < nv; k += SH_THREADS) d4[k] = s4[k];
-    for (int k = (nv << 2) + threadIdx.x; k < total; k += SH_THREADS) smem[k] = src[k];
+    for (int k = threadIdx.x; k < nv; k += SH_THREADS) {
+      const float4 v = s4[k];
+      const float e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int u = 0; u < 4; ++u) smem[sh_lds_index<ROW, ROWP>(4 * k + u)] = e[u];
+    }
+    for (int k = (nv << 2) + threadIdx.x; k < total; k += SH_THREADS)
+      smem[sh_lds_index<ROW, ROWP>(k)] = src[k];
   } else {
-    for (int k = threadIdx.x; k < total; k += SH_THREADS) smem[k] = src[k];
+    for (int k = threadIdx.x; k < total; k += SH_THREADS)
+      smem[sh_lds_index<ROW, ROWP>(k)] = src[k];
   }
   __syncthreads();
   const int t = threadIdx.x;
@@ -101,7 +133,7 @@ __global__ __launch_bounds__(256) void sh_fwd_kernel(int n, int degrees_to_use,
   float b[25];
   int nb = sh_basis(degrees_to_use, viewdirs[3 * g], viewdirs[3 * g + 1], viewdirs[3 * g + 2],
                     b);
-  const float *co = smem + t * ROW;
+  const float *co = smem + t * ROWP;
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
     float acc = b[0] * co[c];
@@ -124,6 +156,7 @@ __global__ __launch_bounds__(256) void sh_bwd_kernel(int n, int degrees_to_use,
                                                              float *__restrict__ v_coeffs) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int ROW = K * 3;
+  constexpr int ROWP = sh_row_pitch(K);
   constexpr int SH_THREADS = sh_threads(K);
   const long long g0 = (long long)blockIdx.x * SH_THREADS;
   const int cnt = (int)min((long long)SH_THREADS, (long long)n - g0);
@@ -134,7 +167,7 @@ __global__ __launch_bounds__(256) void sh_bwd_kernel(int n, int degrees_to_use,
     int nb = sh_basis(degrees_to_use, viewdirs[3 * g], viewdirs[3 * g + 1],
                       viewdirs[3 * g + 2], b);
     float vc0 = v_colors[3 * g], vc1 = v_colors[3 * g + 1], vc2 = v_colors[3 * g + 2];
-    float *row = smem + t * ROW;
+    float *row = smem + t * ROWP;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       float bk = k < nb ? b[k] : 0.f;
@@ -149,11 +182,19 @@ __global__ __launch_bounds__(256) void sh_bwd_kernel(int n, int degrees_to_use,
   if ((((uintptr_t)dst) & 15) == 0) {
     const int nv = total >> 2;
     float4 *d4 = reinterpret_cast<float4 *>(dst);
-    const float4 *s4 = reinterpret_cast<const float4 *>(smem);
-    for (int k = threadIdx.x; k < nv; k += SH_THREADS) d4[k] = s4[k];
-    for (int k = (nv << 2) + threadIdx.x; k < total; k += SH_THREADS) dst[k] = smem[k];
+    for (int k = threadIdx.x; k < nv; k += SH_THREADS) {
+      float4 v;
+      v.x = smem[sh_lds_index<ROW, ROWP>(4 * k)];
+      v.y = smem[sh_lds_index<ROW, ROWP>(4 * k + 1)];
+      v.z = smem[sh_lds_index<ROW, ROWP>(4 * k + 2)];
+      v.w = smem[sh_lds_index<ROW, ROWP>(4 * k + 3)];
+      d4[k] = v;
+    }
+    for (int k = (nv << 2) + threadIdx.x; k < total; k += SH_THREADS)
+      dst[k] = smem[sh_lds_index<ROW, ROWP>(k)];
   } else {
-    for (int k = threadIdx.x; k < total; k += SH_THREADS) dst[k] = smem[k];
+    for (int k = threadIdx.x; k < total; k += SH_THREADS)
+      dst[k] = smem[sh_lds_index<ROW, ROWP>(k)];
   }
 }
 
@@ -184,7 +225,7 @@ extern "C" int gsplat_compute_sh_forward(int num_points, int degree, int degrees
   const int K = num_bases(degree);
   const int thr = sh_threads(K);
   dim3 grid(cdiv(num_points, thr)), block(thr);
-  size_t smem = (size_t)thr * K * 3 * sizeof(float);
+  size_t smem = (size_t)thr * sh_row_pitch(K) * sizeof(float);
   hipStream_t st = (hipStream_t)stream;
   SH_DISPATCH(sh_fwd_kernel, num_points, degrees_to_use, viewdirs, coeffs, colors);
   return check_launch("compute_sh_forward");
@@ -203,7 +244,7 @@ extern "C" int gsplat_compute_sh_backward(int num_points, int degree, int degree
   const int K = num_bases(degree);
   const int thr = sh_threads(K);
   dim3 grid(cdiv(num_points, thr)), block(thr);
-  size_t smem = (size_t)thr * K * 3 * sizeof(float);
+  size_t smem = (size_t)thr * sh_row_pitch(K) * sizeof(float);
   hipStream_t st = (hipStream_t)stream;
   SH_DISPATCH(sh_bwd_kernel, num_points, degrees_to_use, viewdirs, v_colors, v_coeffs);
   return check_launch("compute_sh_backward");

@@ -82,15 +82,16 @@ def bin_gaussians(xys: Tensor, depths: Tensor, radii: Tensor, num_tiles_hit: Ten
                       dtype=torch.uint8)
     counts = torch.empty((2,), device=dev, dtype=torch.int32)
     P, st = _lib.ptr, _lib.stream(dev)
-    _lib.call("gsplat_bin_count", n, P(depths), P(radii), P(num_tiles_hit), P(counts), P(ws1),
-              ws1.numel(), st)
+    xys = xys.float().contiguous()
+    _lib.call("gsplat_bin_count", n, P(xys), P(depths), P(radii), P(num_tiles_hit), tbx, tby,
+              P(counts), P(ws1), ws1.numel(), st)
     num_intersects = int(counts[1].item())  # the single host sync (gsplat: .item())
     tile_bins = torch.empty((tbx * tby, 2), device=dev, dtype=torch.int32)
     gaussian_ids_sorted = torch.empty((max(num_intersects, 0),), device=dev, dtype=torch.int32)
     ws2 = torch.empty((_lib.query("gsplat_bin_emit_workspace_size", num_intersects),),
                       device=dev, dtype=torch.uint8)
-    _lib.call("gsplat_bin_emit", n, num_intersects, P(xys), P(radii), tbx, tby,
-              P(gaussian_ids_sorted), P(tile_bins), P(ws1), ws1.numel(), P(ws2), ws2.numel(), st)
+    _lib.call("gsplat_bin_emit", n, num_intersects, tbx, tby, P(gaussian_ids_sorted),
+              P(tile_bins), P(ws1), ws1.numel(), P(ws2), ws2.numel(), st)
     return num_intersects, gaussian_ids_sorted, tile_bins
 
 

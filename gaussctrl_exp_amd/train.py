@@ -5,10 +5,9 @@ The reference trains one camera per iteration on one device
 render (gc_model.get_outputs) -> splatfacto loss 0.8*L1 + 0.2*(1-SSIM) -> backward ->
 Adam over the six Gaussian parameter groups (gc_config.py:58-87).  Here each rank renders
 its own camera of a multi-view batch against a replica of the parameters; the per-view
-losses sum, so the gradients are summed across ranks with one all-reduce of a single flat
-fp32 bucket ([N x 59], 236 B/Gaussian) over RCCL/xGMI, after which every rank takes the
-identical Adam step.  Gradients are accumulated by autograd directly into views of the
-flat bucket, so the all-reduce needs no pack/unpack copies.
+losses sum, so the gradients ([N x 59] fp32, 236 B/Gaussian) are summed across ranks over
+RCCL/xGMI -- one async all-reduce per parameter tensor, issued as soon as autograd
+finishes it (GradAllReduce) -- after which every rank takes the identical Adam step.
 """
 from __future__ import annotations
 
@@ -62,23 +61,29 @@ def splatfacto_loss(pred, gt):
     return (1 - SSIM_LAMBDA) * l1 + SSIM_LAMBDA * sim
 
 
-class FlatGradBucket:
-    """One contiguous fp32 buffer holding every parameter's .grad as a view."""
+class GradAllReduce:
+    """Sums every parameter's gradient over the data-parallel ranks (RCCL over xGMI).
 
-    def __init__(self, params: List[torch.Tensor]):
-        numel = sum(p.numel() for p in params)
-        self.buffer = torch.zeros(numel, device=params[0].device, dtype=torch.float32)
-        off = 0
-        for p in params:
-            p.grad = self.buffer[off:off + p.numel()].view_as(p)
-            off += p.numel()
-        self.params = params
+    One async all-reduce per parameter, launched from a post-accumulate-grad hook the moment
+    autograd has produced that gradient: the SH-feature gradients (81 % of the 236 B per
+    Gaussian) are issued right after the SH backward and overlap the projection backward.
+    Gradients stay the tensors autograd produced (no flat bucket to zero-fill and accumulate
+    into, no pack/unpack copies); hooks fire in the same order on every rank because every
+    rank runs the same graph."""
 
-    def zero_(self):
-        self.buffer.zero_()
+    def __init__(self, params: List[torch.Tensor], group=None):
+        self.group = group
+        self.works = []
+        self.handles = [p.register_post_accumulate_grad_hook(self._hook) for p in params]
 
-    def all_reduce_(self, group=None):
-        dist.all_reduce(self.buffer, op=dist.ReduceOp.SUM, group=group)
+    def _hook(self, p: torch.Tensor):
+        self.works.append(dist.all_reduce(p.grad, op=dist.ReduceOp.SUM, group=self.group,
+                                          async_op=True))
+
+    def wait(self):
+        for w in self.works:
+            w.wait()
+        self.works.clear()
 
 
 class TrainStep:
@@ -88,8 +93,8 @@ class TrainStep:
                  loss: str = "splatfacto", group=None, api=None):
         self.scene = scene.requires_grad_()
         self.params = scene.params()
-        self.bucket = FlatGradBucket(self.params)
         self.world_size = world_size
+        self.grad_sync = GradAllReduce(self.params, group) if world_size > 1 else None
         self.group = group
         self.sh_degree = sh_degree
         self.loss_kind = loss
@@ -108,6 +113,18 @@ class TrainStep:
             return torch.abs(gt - pred).mean()
         return splatfacto_loss(pred, gt)
 
+    def zero_grad(self):
+        for p in self.params:
+            p.grad = None
+
+    def sync_grads(self):
+        """Wait for this step's gradient all-reduces (no-op on one rank)."""
+        if self.grad_sync is not None:
+            self.grad_sync.wait()
+
+    def flat_grad(self) -> torch.Tensor:
+        return torch.cat([p.grad.reshape(-1) for p in self.params])
+
     def forward_backward(self, cam: GCCamera, gt: torch.Tensor, background: torch.Tensor):
         out = render(self.scene, cam, self.sh_degree, background, api=self.api)
         loss = self.loss(out["rgb"], gt)
@@ -118,10 +135,9 @@ class TrainStep:
              optimizer: bool = True):
         if background is None:
             background = torch.rand(3, device=gt.device)
-        self.bucket.zero_()
+        self.zero_grad()
         loss, out = self.forward_backward(cam, gt, background)
-        if self.world_size > 1:
-            self.bucket.all_reduce_(self.group)
+        self.sync_grads()
         if optimizer:
             for g in self.opt.param_groups:
                 if g["name"] == "means":

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define GSPLAT_MI355X_ABI_VERSION 2
+#define GSPLAT_MI355X_ABI_VERSION 3
 
 int gsplat_abi_version(void);
 const char *gsplat_last_error(void);
@@ -108,14 +108,14 @@ int gsplat_get_tile_bin_edges(int64_t num_intersects, const int64_t *isect_ids_s
  * identical to a stable sort of gsplat's 64-bit isect_ids. */
 size_t gsplat_bin_count_workspace_size(int num_points);
 size_t gsplat_bin_emit_workspace_size(int64_t num_intersects);
-int gsplat_bin_count(int num_points, const float *depths, const int32_t *radii,
-                     const int32_t *num_tiles_hit, int32_t *d_counts, void *workspace1,
+int gsplat_bin_count(int num_points, const float *xys, const float *depths,
+                     const int32_t *radii, const int32_t *num_tiles_hit, int tile_bounds_x,
+                     int tile_bounds_y, int32_t *d_counts, void *workspace1,
                      size_t workspace1_bytes, void *stream);
-int gsplat_bin_emit(int num_points, int64_t num_intersects, const float *xys,
-                    const int32_t *radii, int tile_bounds_x, int tile_bounds_y,
-                    int32_t *gaussian_ids_sorted, int32_t *tile_bins, const void *workspace1,
-                    size_t workspace1_bytes, void *workspace2, size_t workspace2_bytes,
-                    void *stream);
+int gsplat_bin_emit(int num_points, int64_t num_intersects, int tile_bounds_x,
+                    int tile_bounds_y, int32_t *gaussian_ids_sorted, int32_t *tile_bins,
+                    const void *workspace1, size_t workspace1_bytes, void *workspace2,
+                    size_t workspace2_bytes, void *stream);
 
 /* ---- rasterization (forward.cu rasterize_forward, backward.cu rasterize_backward) -----
  * colors [N,C], opacity [N] (or [N,1]), background [C]; out_img [H,W,C], final_Ts [H,W],

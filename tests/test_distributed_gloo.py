@@ -1,5 +1,5 @@
 """World-size-2 data-parallel train step on CPU (gloo): each rank renders its own camera
-(oracle-backed gsplat emulation), gradients land in the flat bucket and are all-reduced;
+(oracle-backed gsplat emulation), gradients are all-reduced per parameter as autograd finishes them;
 the result must equal the sum of the two single-view gradients (SURVEY.md §8e parity
 check), and after the identical Adam step both ranks hold identical parameters."""
 import os
@@ -43,7 +43,7 @@ def _worker(rank, world, port, out_dir):
     gt = torch.rand(48, 64, 3, generator=torch.Generator().manual_seed(rank))
     t = TrainStep(_scene(), sh_degree=3, world_size=world, loss="l1", api=API)
     t.step(cam, gt, background=torch.tensor([0.5, 0.5, 0.5]), optimizer=False)
-    np.save(os.path.join(out_dir, f"grad{rank}.npy"), t.bucket.buffer.numpy())
+    np.save(os.path.join(out_dir, f"grad{rank}.npy"), t.flat_grad().numpy())
     t.opt.step()
     np.save(os.path.join(out_dir, f"means{rank}.npy"), t.scene.means.detach().numpy())
     dist.destroy_process_group()
@@ -55,13 +55,13 @@ def test_two_rank_allreduce_equals_sum_of_views(tmp_path):
     port = _free_port()
     mp.spawn(_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
     g0, g1 = np.load(tmp_path / "grad0.npy"), np.load(tmp_path / "grad1.npy")
-    np.testing.assert_array_equal(g0, g1)  # every rank holds the same reduced bucket
+    np.testing.assert_array_equal(g0, g1)  # every rank holds the same reduced gradients
     ref = 0
     for r in range(2):
         t = TrainStep(_scene(), sh_degree=3, world_size=1, loss="l1", api=API)
         gt = torch.rand(48, 64, 3, generator=torch.Generator().manual_seed(r))
         t.step(_views()[r], gt, background=torch.tensor([0.5, 0.5, 0.5]), optimizer=False)
-        ref = ref + t.bucket.buffer.numpy()
+        ref = ref + t.flat_grad().numpy()
     assert np.abs(ref).max() > 0
     np.testing.assert_allclose(g0, ref, rtol=1e-5, atol=1e-7)
     np.testing.assert_array_equal(np.load(tmp_path / "means0.npy"),
