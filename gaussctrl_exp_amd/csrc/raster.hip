@@ -5,19 +5,20 @@
 // backward.cu; semantics SURVEY.md Appendix A9/A10), reached from
 // /root/reference/gaussctrl/gc_model.py:208-220 (RGB + alpha) and :225-236 (depth).
 //
-// MI355X mapping (per-pixel serial compositing: VALU/latency-bound, no MFMA):
-//  * A 16x16 tile is split into 4/PXL horizontal strips, one wave64 each; a lane owns PXL
-//    pixels of one column of its strip.  The waves of a tile are independent -- each stages
-//    its own copy of the tile's sorted Gaussians in its own LDS slice, 64 at a time (one
-//    Gaussian per lane, coalesced id loads; colour loaded only if kept) -- so a wave whose
-//    pixels have all terminated leaves early and no workgroup barrier is ever executed.
-//    (One wave per tile would serialise a 2.8k-Gaussian tile on one wave: the headline
-//    forward was bound by exactly that critical path.)
-//  * While staging, each lane culls its Gaussian against the wave's pixel rectangle with a
-//    conservative bound (touches_rect) and the survivors are compacted in order with a
-//    ballot + mbcnt prefix, so the per-pixel loop only visits Gaussians that can pass
-//    gsplat's alpha >= 1/255 test somewhere in the strip.  The bound never drops a Gaussian
-//    that could contribute, so results are unchanged bit for bit.
+// MI355X mapping (per-pixel serial compositing: VALU-issue bound, no MFMA):
+//  * A 16x16 tile is split into independent wave rectangles (wave_rect): the forward uses
+//    four 8x8 blocks, the backward two 16x8 strips with two pixels per lane.  Each wave
+//    stages its own copy of the tile's sorted Gaussians in its own LDS slice, 64 at a time
+//    (one Gaussian per lane, coalesced id loads; colour loaded only if kept), so a wave
+//    whose pixels have all terminated leaves early and no workgroup barrier is executed.
+//    (One wave per tile would serialise a 2.8k-Gaussian tile on one wave.)
+//  * While staging, each lane culls its Gaussian against the wave's rectangle with the
+//    exact minimum of sigma over the rectangle (touches_rect) and the survivors are
+//    compacted in order with a ballot + mbcnt prefix, so the per-pixel loop only visits
+//    Gaussians that can pass gsplat's alpha >= 1/255 test somewhere in the rectangle.  The
+//    cull keeps a rounding margin, so results are unchanged bit for bit.
+//  * Forward (raster_fwd3u_kernel): two staged Gaussians per iteration -- their sigma /
+//    exp / alpha are independent; the blend is applied in list order, branch-free.
 //  * Backward (shipped: raster_bwd3p_kernel<1>, 16x8 strips, 2 pixels per lane): the lane's
 //    two pixels are a float2 pair blended branch-free; per Gaussian the lane folds them into
 //    9 partial sums (sigma-gradient moments, colour and opacity terms), the wave
@@ -36,7 +37,7 @@ namespace {
 
 constexpr float ALPHA_MIN = 1.f / 255.f;
 constexpr int REC = 16;  // floats per gradient record: x y a b c r g b o + pad = 64 B
-constexpr int FWD_PXL = 1;  // scalar forward, 16x4 strips (4 waves per tile)
+constexpr int FWD_PXL = 1;  // forward: 8x8 blocks, two Gaussians per iteration (4 waves/tile)
 constexpr int BWD_PXL = 2;  // packed backward, 16x8 strips (2 waves per tile)
 // Tuning / ablation knobs (gsplat_debug_set_raster_variant); defaults are the shipped ones.
 int g_fwd_pxl = FWD_PXL, g_bwd_pxl = BWD_PXL, g_bwd_flags = 0;
@@ -73,27 +74,41 @@ __device__ __forceinline__ f2 gs_vis2(f2 sigma) {
   return (f2){__builtin_amdgcn_exp2f(e.x), __builtin_amdgcn_exp2f(e.y)};
 }
 
-// Conservative, exactness-preserving cull of one Gaussian against the pixel-centre
-// rectangle [rx0,rx1] x [ry0,ry1].  For every pixel p in it, with d = xy - p,
-//   sigma(p) = 0.5 d^T Q d >= 0.5 lmin(Q) |d|^2 >= 0.5 lmin dist(xy, rect)^2,
-// so when even half of that lower bound (float-safety margin) makes o*exp(-sigma) < 1/255,
-// gsplat's per-pixel test rejects the Gaussian at every pixel of the rectangle.  A Gaussian
-// with o < 1/255 is never composited (alpha <= o).  Non-positive-definite conics and NaNs
-// are kept.
+// Exactness-preserving cull of one Gaussian against the wave's pixel-centre rectangle
+// [rx0,rx1] x [ry0,ry1].  With d = xy - p ranging over the box [dx0,dx1] x [dy0,dy1],
+// sigma(p) = 0.5 q(d), q = a dx^2 + 2 b dx dy + c dy^2, is convex for a positive-definite
+// conic, so its minimum over the box is 0 when the mean lies inside, else the smallest of the
+// four edge minima (each a clamped 1-D minimisation).  The Gaussian is dropped only when that
+// minimum, lowered by a rounding margin proportional to the magnitude of q's terms plus an
+// absolute 1e-3, still makes o * exp(-sigma) < 1/255 -- i.e. when gsplat's per-pixel test
+// rejects it at every pixel of the rectangle.  A Gaussian with o < 1/255 is never composited
+// (alpha <= o).  Non-positive-definite conics and NaNs are kept.  Compared with an isotropic
+// (smallest-eigenvalue) bound this removes ~42 % of the per-wave iterations at the headline
+// size: elongated Gaussians no longer count as touching rectangles they only pass near.
+__device__ __forceinline__ float q_edge(float e, float lo, float hi, float diag_e, float diag_f,
+                                        float b, float &mag) {
+  // min over f in [lo, hi] of diag_e e^2 + 2 b e f + diag_f f^2 (diag_f > 0)
+  const float f = fminf(fmaxf(-b * e / diag_f, lo), hi);
+  const float t0 = diag_e * e * e, t1 = 2.f * b * e * f, t2 = diag_f * f * f;
+  mag = t0 + fabsf(t1) + t2;
+  return t0 + t1 + t2;
+}
 __device__ __forceinline__ bool touches_rect(float gx, float gy, float a, float b, float c,
                                              float o, float rx0, float rx1, float ry0,
                                              float ry1) {
   if (!(o >= ALPHA_MIN)) return false;
-  const float dx = gx - fminf(fmaxf(gx, rx0), rx1);
-  const float dy = gy - fminf(fmaxf(gy, ry0), ry1);
-  const float d2 = dx * dx + dy * dy;
-  const float hm = 0.5f * (a + c), hd = 0.5f * (a - c);
-  const float lmax = hm + sqrtf(hd * hd + b * b);
-  const float det = a * c - b * b;
-  if (!(det > 0.f) || !(lmax > 0.f)) return true;
-  const float lmin = det / lmax;
-  const float bound = 0.25f * lmin * d2;
-  return !(bound > __logf(255.f * o) + 0.01f);
+  if (!(a > 0.f) || !(a * c - b * b > 0.f)) return true;  // not positive definite (or NaN)
+  const float dx0 = gx - rx1, dx1 = gx - rx0, dy0 = gy - ry1, dy1 = gy - ry0;
+  if (dx0 <= 0.f && dx1 >= 0.f && dy0 <= 0.f && dy1 >= 0.f) return true;  // mean inside
+  float m0, m1, m2, m3;
+  const float q0 = q_edge(dx0, dy0, dy1, a, c, b, m0), q1 = q_edge(dx1, dy0, dy1, a, c, b, m1);
+  const float q2 = q_edge(dy0, dx0, dx1, c, a, b, m2), q3 = q_edge(dy1, dx0, dx1, c, a, b, m3);
+  float q = q0, m = m0;
+  if (q1 < q) { q = q1; m = m1; }
+  if (q2 < q) { q = q2; m = m2; }
+  if (q3 < q) { q = q3; m = m3; }
+  const float sigma_lb = 0.5f * (q - 1e-5f * m) - 1e-3f;
+  return !(sigma_lb > __logf(255.f * o));
 }
 
 __device__ __forceinline__ uint32_t lanes_below(unsigned long long mask) {
@@ -128,6 +143,43 @@ __device__ __forceinline__ bool stage_gaussian(int idx, const int *__restrict__ 
     s.id = g;
   }
   return keep;
+}
+
+// A workgroup of 4 waves covers 4 / (waves per tile) tiles.  A wave owns a COLS-wide
+// rectangle of its tile: lanes map to (column lane % COLS, row lane / COLS), and each lane
+// holds PXL pixels spaced 64 / COLS rows apart.  COLS = 16 gives full-width strips, COLS = 8
+// gives more compact blocks (fewer Gaussians touch an 8x8 block than a 16x4 strip).
+struct WaveRect {
+  bool live;
+  int tile, j, i0;
+  float rx0, rx1, ry0, ry1;
+};
+template <int PXL, int COLS>
+__device__ __forceinline__ WaveRect wave_rect(int tbx, int tby, int H, int W) {
+  constexpr int LROWS = 64 / COLS;      // rows per lane pass
+  constexpr int WROWS = LROWS * PXL;    // rows per wave
+  constexpr int WX = GS_BLOCK / COLS, WY = GS_BLOCK / WROWS;
+  constexpr int WPT = WX * WY;          // waves per tile
+  static_assert(WPT >= 1 && WPT <= 4 && 4 % WPT == 0, "wave footprint must tile 16x16");
+  constexpr int TPBLK = 4 / WPT;        // tiles per workgroup
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  WaveRect r;
+  r.tile = blockIdx.x * TPBLK + wave / WPT;
+  const int wt = wave % WPT;
+  const int tx = r.tile % tbx, ty = r.tile / tbx;
+  const int c0 = tx * GS_BLOCK + (wt % WX) * COLS, r0 = ty * GS_BLOCK + (wt / WX) * WROWS;
+  r.live = r.tile < tbx * tby && c0 < W && r0 < H;
+  r.j = c0 + lane % COLS;
+  r.i0 = r0 + lane / COLS;
+  r.rx0 = (float)c0;
+  r.rx1 = (float)min(c0 + COLS - 1, W - 1);
+  r.ry0 = (float)r0;
+  r.ry1 = (float)min(r0 + WROWS - 1, H - 1);
+  return r;
+}
+template <int PXL, int COLS>
+constexpr int tiles_per_block() {
+  return 4 / ((GS_BLOCK / COLS) * (GS_BLOCK / ((64 / COLS) * PXL)));
 }
 
 // ---------------------------------------------------------------- forward, C = 3
@@ -217,6 +269,108 @@ __global__ __launch_bounds__(256) void raster_fwd3_kernel(
 #pragma unroll
   for (int k = 0; k < PXL; ++k) {
     const int i = i0 + 4 * k;
+    if (i < H && j < W) {
+      const int pix = i * W + j;
+      final_Ts[pix] = T[k];
+      final_idx[pix] = cur[k];
+      out_img[3 * pix] = cr[k] + T[k] * bg0;
+      out_img[3 * pix + 1] = cg[k] + T[k] * bg1;
+      out_img[3 * pix + 2] = cb[k] + T[k] * bg2;
+    }
+  }
+}
+
+// Two staged Gaussians per iteration (PXL pixels per lane, branch-free): both Gaussians'
+// sigma / exp / alpha are independent and evaluated together; only the transmittance
+// update is applied in list order, so every pixel sees exactly the scalar kernel's
+// sequence of operations.
+template <int PXL, int COLS>
+__global__ __launch_bounds__(256) void raster_fwd3u_kernel(
+    int tbx, int tby, int H, int W, const int *__restrict__ gids, const int2 *__restrict__ bins,
+    const float2 *__restrict__ xys, const float *__restrict__ conics,
+    const float *__restrict__ colors, const float *__restrict__ opacity,
+    const float *__restrict__ background, float *__restrict__ out_img,
+    float *__restrict__ final_Ts, int *__restrict__ final_idx) {
+  const WaveRect R = wave_rect<PXL, COLS>(tbx, tby, H, W);
+  if (!R.live) return;  // wave-uniform
+  __shared__ GStage lds[4][64];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int tile = R.tile, j = R.j, i0 = R.i0;
+  const float px = (float)j;
+  const float rx0 = R.rx0, rx1 = R.rx1, ry0 = R.ry0, ry1 = R.ry1;
+  constexpr int LROWS = 64 / COLS;
+  float py[PXL], T[PXL], cr[PXL], cg[PXL], cb[PXL];
+  int cur[PXL];
+  bool done[PXL];
+#pragma unroll
+  for (int k = 0; k < PXL; ++k) {
+    const int i = i0 + LROWS * k;
+    py[k] = (float)i;
+    T[k] = 1.f;
+    cr[k] = cg[k] = cb[k] = 0.f;
+    cur[k] = 0;
+    done[k] = !(i < H && j < W);
+  }
+  const int2 range = bins[tile];
+  GStage *stage = lds[wave];
+  for (int b = range.x; b < range.y; b += 64) {
+    bool all_done = true;
+#pragma unroll
+    for (int k = 0; k < PXL; ++k) all_done = all_done && done[k];
+    if (__all(all_done)) break;
+    const int idx = b + lane;
+    GStage s;
+    const bool keep = idx < range.y &&
+                      stage_gaussian(idx, gids, xys, conics, colors, opacity, rx0, rx1, ry0,
+                                     ry1, s);
+    const unsigned long long kmask = __ballot(keep);
+    if (keep) stage[lanes_below(kmask)] = s;
+    const int n = __popcll(kmask);
+    wave_lds_sync();
+    for (int t = 0; t < n; t += 2) {
+      GStage G[2];
+      G[0] = stage[t];
+      G[1] = stage[min(t + 1, 63)];
+      const bool live1 = t + 1 < n;
+      if (!live1) G[1].r = G[1].g = G[1].bl = 0.f;  // stale slot: keep 0 * colour finite
+      float sg[2][PXL], al[2][PXL];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const float dx = G[u].x - px;
+        const float hA = G[u].ha * dx * dx, bdx = G[u].b * dx;
+#pragma unroll
+        for (int k = 0; k < PXL; ++k) {
+          sg[u][k] = gs_sigma(G[u].hc, bdx, hA, G[u].y - py[k]);
+          al[u][k] = fminf(0.999f, G[u].o * gs_vis(sg[u][k]));
+        }
+      }
+      bool fin = true;
+#pragma unroll
+      for (int k = 0; k < PXL; ++k) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const bool v = !done[k] && (u == 0 || live1) && sg[u][k] >= 0.f &&
+                         al[u][k] >= ALPHA_MIN;
+          const float nT = T[k] * (1.f - al[u][k]);
+          const bool term = v && nT <= 1e-4f, comp = v && !term;
+          done[k] = done[k] || term;
+          const float w = comp ? al[u][k] * T[k] : 0.f;
+          cr[k] += G[u].r * w;
+          cg[k] += G[u].g * w;
+          cb[k] += G[u].bl * w;
+          T[k] = comp ? nT : T[k];
+          cur[k] = comp ? G[u].idx : cur[k];
+        }
+        fin = fin && done[k];
+      }
+      if (__all(fin)) break;
+    }
+    wave_lds_sync();
+  }
+  const float bg0 = background[0], bg1 = background[1], bg2 = background[2];
+#pragma unroll
+  for (int k = 0; k < PXL; ++k) {
+    const int i = i0 + LROWS * k;
     if (i < H && j < W) {
       const int pix = i * W + j;
       final_Ts[pix] = T[k];
@@ -460,7 +614,7 @@ __global__ __launch_bounds__(256) void raster_bwd3_kernel(
 // sigma gradient as moments V = sum v_sigma, Vy = sum v_sigma dy, Vyy = sum v_sigma dy^2
 // (dx is constant along the lane's column), from which
 //   v_conic = 0.5 (dx^2 V, dx Vy, Vyy),  v_xy = (a dx V + b Vy, b dx V + c Vy).
-template <int NP, bool ATOMICS>
+template <int NP, bool ATOMICS, int COLS>
 __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
     int tbx, int tby, int H, int W, const int *__restrict__ gids, const int2 *__restrict__ bins,
     const float2 *__restrict__ xys, const float *__restrict__ conics,
@@ -469,29 +623,21 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
     const int *__restrict__ final_idx, const float *__restrict__ v_out,
     const float *__restrict__ v_out_alpha, float alpha_max, float *__restrict__ rec) {
   constexpr int PXL = 2 * NP;
-  constexpr int WPT = 4 / PXL;
-  constexpr int TPBLK = 4 / WPT;
-  constexpr int ROWS = 4 * PXL;
+  constexpr int LROWS = 64 / COLS;
+  const WaveRect R = wave_rect<PXL, COLS>(tbx, tby, H, W);
+  if (!R.live) return;  // wave-uniform
   __shared__ GStage lds[4][64];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int tile = blockIdx.x * TPBLK + wave / WPT;
-  const int strip = wave % WPT;
-  if (tile >= tbx * tby) return;
-  const int tx = tile % tbx, ty = tile / tbx;
-  const int r0 = ty * GS_BLOCK + strip * ROWS;
-  if (r0 >= H) return;
-  const int j = tx * GS_BLOCK + (lane & 15);
-  const int i0 = r0 + (lane >> 4);
+  const int tile = R.tile, j = R.j, i0 = R.i0;
   const float px = (float)j;
-  const float rx0 = (float)(tx * GS_BLOCK), rx1 = (float)min(tx * GS_BLOCK + 15, W - 1);
-  const float ry0 = (float)r0, ry1 = (float)min(r0 + ROWS - 1, H - 1);
+  const float rx0 = R.rx0, rx1 = R.rx1, ry0 = R.ry0, ry1 = R.ry1;
   const float bg0 = background[0], bg1 = background[1], bg2 = background[2];
   f2 py[NP], T[NP], vr[NP], vg[NP], vb[NP], q[NP], Sb[NP];
   int binf[PXL];
   int maxbin = -1;
 #pragma unroll
   for (int k = 0; k < PXL; ++k) {
-    const int i = i0 + 4 * k, p = k >> 1;
+    const int i = i0 + LROWS * k, p = k >> 1;
     float Tf = 0.f, r = 0.f, g = 0.f, bl = 0.f, a = 0.f;
     int bf = -1;
     if (i < H && j < W) {
@@ -529,60 +675,80 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
     if (keep) stage[lanes_below(kmask)] = s;
     const int n = __popcll(kmask);
     wave_lds_sync();
-    for (int t = 0; t < n; ++t) {
-      const GStage G = stage[t];
-      const float dx = G.x - px;
-      const float hA = G.ha * dx * dx, bdx = G.b * dx;
-      f2 sr = 0.f, sg = 0.f, sb = 0.f, so = 0.f, V = 0.f, Vy = 0.f, Vyy = 0.f;
-      bool anyv = false;
+    constexpr int U = 1;  // (two per iteration measured slower: register pressure)
+    for (int t = 0; t < n; t += U) {
+      float parts[U][9];
+      bool anyv[U];
+      int gid[U];
 #pragma unroll
-      for (int p = 0; p < NP; ++p) {
-        const f2 dy = G.y - py[p];
-        const f2 sig = gs_sigma2(G.hc, bdx, hA, dy);
-        const f2 vis = gs_vis2(sig);
-        const f2 ov = G.o * vis;
-        const f2 al = {fminf(alpha_max, ov.x), fminf(alpha_max, ov.y)};
-        const bool v0 = G.idx <= binf[2 * p] && sig.x >= 0.f && al.x >= ALPHA_MIN;
-        const bool v1 = G.idx <= binf[2 * p + 1] && sig.y >= 0.f && al.y >= ALPHA_MIN;
-        anyv = anyv || v0 || v1;
-        const f2 am = {v0 ? al.x : 0.f, v1 ? al.y : 0.f};
-        const f2 vm = {v0 ? vis.x : 0.f, v1 ? vis.y : 0.f};
-        const f2 om = 1.f - am;
-        const f2 ra = {__builtin_amdgcn_rcpf(om.x), __builtin_amdgcn_rcpf(om.y)};
-        T[p] = T[p] * ra;
-        const f2 fac = am * T[p];
-        sr = __builtin_elementwise_fma(fac, vr[p], sr);
-        sg = __builtin_elementwise_fma(fac, vg[p], sg);
-        sb = __builtin_elementwise_fma(fac, vb[p], sb);
-        const f2 gv = __builtin_elementwise_fma(
-            (f2)G.r, vr[p], __builtin_elementwise_fma((f2)G.g, vg[p], G.bl * vb[p]));
-        const f2 v_alpha = __builtin_elementwise_fma(gv, T[p], ra * (q[p] - Sb[p]));
-        Sb[p] = __builtin_elementwise_fma(fac, gv, Sb[p]);
-        const f2 vva = vm * v_alpha;
-        so += vva;
-        const f2 vs = vva * (-G.o);
-        const f2 vsdy = vs * dy;
-        V += vs;
-        Vy += vsdy;
-        Vyy = __builtin_elementwise_fma(vsdy, dy, Vyy);
-      }
-      if (__any(anyv)) {
+      for (int u = 0; u < U; ++u) {
+        GStage G = stage[min(t + u, 63)];
+        const bool live = t + u < n;
+        if (!live) G.r = G.g = G.bl = G.o = 0.f;  // stale slot: keep T / Sb finite
+        gid[u] = G.id;
+        const float dx = G.x - px;
+        const float hA = G.ha * dx * dx, bdx = G.b * dx;
+        f2 sr = 0.f, sg = 0.f, sb = 0.f, so = 0.f, V = 0.f, Vy = 0.f, Vyy = 0.f;
+        bool any = false;
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+          const f2 dy = G.y - py[p];
+          const f2 sig = gs_sigma2(G.hc, bdx, hA, dy);
+          const f2 vis = gs_vis2(sig);
+          const f2 ov = G.o * vis;
+          const f2 al = {fminf(alpha_max, ov.x), fminf(alpha_max, ov.y)};
+          const bool v0 = live && G.idx <= binf[2 * p] && sig.x >= 0.f && al.x >= ALPHA_MIN;
+          const bool v1 =
+              live && G.idx <= binf[2 * p + 1] && sig.y >= 0.f && al.y >= ALPHA_MIN;
+          any = any || v0 || v1;
+          const f2 am = {v0 ? al.x : 0.f, v1 ? al.y : 0.f};
+          const f2 vm = {v0 ? vis.x : 0.f, v1 ? vis.y : 0.f};
+          const f2 om = 1.f - am;
+          const f2 ra = {__builtin_amdgcn_rcpf(om.x), __builtin_amdgcn_rcpf(om.y)};
+          T[p] = T[p] * ra;
+          const f2 fac = am * T[p];
+          sr = __builtin_elementwise_fma(fac, vr[p], sr);
+          sg = __builtin_elementwise_fma(fac, vg[p], sg);
+          sb = __builtin_elementwise_fma(fac, vb[p], sb);
+          const f2 gv = __builtin_elementwise_fma(
+              (f2)G.r, vr[p], __builtin_elementwise_fma((f2)G.g, vg[p], G.bl * vb[p]));
+          const f2 v_alpha = __builtin_elementwise_fma(gv, T[p], ra * (q[p] - Sb[p]));
+          Sb[p] = __builtin_elementwise_fma(fac, gv, Sb[p]);
+          const f2 vva = vm * v_alpha;
+          so += vva;
+          const f2 vs = vva * (-G.o);
+          const f2 vsdy = vs * dy;
+          V += vs;
+          Vy += vsdy;
+          Vyy = __builtin_elementwise_fma(vsdy, dy, Vyy);
+        }
+        anyv[u] = any;
         const float Vs = V.x + V.y, Vys = Vy.x + Vy.y;
         const float dxV = dx * Vs;
-        const float parts[9] = {fmaf(2.f * G.ha, dxV, G.b * Vys),  // v_x
-                                fmaf(G.b, dxV, 2.f * G.hc * Vys),  // v_y
-                                dx * dxV,                          // 2 v_conic.a
-                                dx * Vys,                          // 2 v_conic.b
-                                Vyy.x + Vyy.y,                     // 2 v_conic.c
-                                sr.x + sr.y,
-                                sg.x + sg.y,
-                                sb.x + sb.y,
-                                so.x + so.y};
-        const float v = reduce9(parts);
-        if constexpr (ATOMICS) {
-          if (slot >= 0) atomicAdd(rec + (size_t)G.id * REC + slot, v);
-        } else {
-          asm volatile("" ::"v"(v));
+        parts[u][0] = fmaf(2.f * G.ha, dxV, G.b * Vys);  // v_x
+        parts[u][1] = fmaf(G.b, dxV, 2.f * G.hc * Vys);  // v_y
+        parts[u][2] = dx * dxV;                          // 2 v_conic.a
+        parts[u][3] = dx * Vys;                          // 2 v_conic.b
+        parts[u][4] = Vyy.x + Vyy.y;                     // 2 v_conic.c
+        parts[u][5] = sr.x + sr.y;
+        parts[u][6] = sg.x + sg.y;
+        parts[u][7] = sb.x + sb.y;
+        parts[u][8] = so.x + so.y;
+      }
+      bool any_all = false;
+#pragma unroll
+      for (int u = 0; u < U; ++u) any_all = any_all || anyv[u];
+      if (__any(any_all)) {
+        float v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = reduce9(parts[u]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if constexpr (ATOMICS) {
+            if (__any(anyv[u]) && slot >= 0) atomicAdd(rec + (size_t)gid[u] * REC + slot, v[u]);
+          } else {
+            asm volatile("" ::"v"(v[u]));
+          }
         }
       }
     }
@@ -857,10 +1023,22 @@ extern "C" int gsplat_rasterize_forward(int tile_bounds_x, int tile_bounds_y, in
                      tile_bounds_x, tile_bounds_y, img_height, img_width, gaussian_ids_sorted,  \
                      (const int2 *)tile_bins, (const float2 *)xys, conics, colors, opacity,     \
                      background, out_img, final_Ts, final_idx)
-    const bool scalar = g_bwd_flags & 4;
-    if (g_fwd_pxl == 4) { if (scalar) FWD3(4); else FWD3P(2); }
-    else if (g_fwd_pxl == 2) { if (scalar) FWD3(2); else FWD3P(1); }
-    else FWD3(1);
+#define FWD3U(P, C)                                                                        \
+  hipLaunchKernelGGL((raster_fwd3u_kernel<P, C>), dim3(cdiv(T, (tiles_per_block<P, C>()))),    \
+                     dim3(256), 0, st, tile_bounds_x, tile_bounds_y, img_height, img_width,     \
+                     gaussian_ids_sorted, (const int2 *)tile_bins, (const float2 *)xys, conics, \
+                     colors, opacity, background, out_img, final_Ts, final_idx)
+    // flags: 4 scalar one-Gaussian-per-iteration kernel, 8 packed float2 kernel, 16 full-width
+    // (16-column) rectangles; default: two Gaussians per iteration on 8-column rectangles.
+    const bool scalar = g_bwd_flags & 4, packed = g_bwd_flags & 8, wide = g_bwd_flags & 16;
+    if (g_fwd_pxl == 4) {
+      if (scalar) FWD3(4); else if (packed) FWD3P(2); else FWD3U(4, 16);
+    } else if (g_fwd_pxl == 2) {
+      if (scalar) FWD3(2); else if (packed) FWD3P(1); else if (wide) FWD3U(2, 16); else FWD3U(2, 8);
+    } else {
+      if (scalar) FWD3(1); else if (wide) FWD3U(1, 16); else FWD3U(1, 8);
+    }
+#undef FWD3U
 #undef FWD3
 #undef FWD3P
   } else {
@@ -922,16 +1100,22 @@ extern "C" int gsplat_rasterize_backward(int tile_bounds_x, int tile_bounds_y, i
                      tile_bounds_x, tile_bounds_y, img_height, img_width, gaussian_ids_sorted,  \
                      (const int2 *)tile_bins, (const float2 *)xys, conics, colors, opacity,     \
                      background, final_Ts, final_idx, v_output, v_output_alpha, alpha_max, rec)
-#define BWD3P(NP, A)                                                                       \
-  hipLaunchKernelGGL((raster_bwd3p_kernel<NP, A>), dim3(cdiv(T, 2 * NP)), dim3(256), 0, st,     \
+#define BWD3P(NP, A, C)                                                                    \
+  hipLaunchKernelGGL((raster_bwd3p_kernel<NP, A, C>),                                       \
+                     dim3(cdiv(T, (tiles_per_block<2 * NP, C>()))), dim3(256), 0, st,         \
                      tile_bounds_x, tile_bounds_y, img_height, img_width, gaussian_ids_sorted,  \
                      (const int2 *)tile_bins, (const float2 *)xys, conics, colors, opacity,     \
                      background, final_Ts, final_idx, v_output, v_output_alpha, alpha_max, rec)
     const bool atomics = !(g_bwd_flags & 1);
     const bool packed = g_bwd_pxl >= 2 && !(g_bwd_flags & 2);
+    const bool narrow = g_bwd_flags & 32;  // 8-column wave rectangles
     if (packed) {
-      if (g_bwd_pxl == 4) { if (atomics) BWD3P(2, true); else BWD3P(2, false); }
-      else { if (atomics) BWD3P(1, true); else BWD3P(1, false); }
+      if (g_bwd_pxl == 4) {
+        if (atomics) BWD3P(2, true, 16); else BWD3P(2, false, 16);  // 16x16: one wave
+      } else {
+        if (narrow) { if (atomics) BWD3P(1, true, 8); else BWD3P(1, false, 8); }
+        else { if (atomics) BWD3P(1, true, 16); else BWD3P(1, false, 16); }
+      }
     } else if (g_bwd_pxl == 4) { if (atomics) BWD3(4, true); else BWD3(4, false); }
     else if (g_bwd_pxl == 1) { if (atomics) BWD3(1, true); else BWD3(1, false); }
     else { if (atomics) BWD3(2, true); else BWD3(2, false); }

@@ -145,10 +145,12 @@ int gsplat_rasterize_backward(int tile_bounds_x, int tile_bounds_y, int img_heig
                               void *stream);
 
 /* Tuning / ablation hook (not part of the gsplat surface): pixels per lane of the 3-channel
- * forward and backward kernels (1, 2 or 4; a 16x16 tile is covered by 4/pxl waves; 2 and 4
- * select the packed float2 kernels), and flags (bit 0: drop the gradient atomics -- timing
- * ablation only, results wrong; bit 1: scalar backward; bit 2: scalar forward).
- * Process-wide; defaults (1, 2, 0) are the shipped configuration. */
+ * forward and backward kernels (1, 2 or 4; a 16x16 tile is covered by 4/pxl waves), and
+ * flags: bit 0 drops the gradient atomics (timing ablation only, results wrong); bit 1
+ * scalar backward; bit 2 scalar forward (one Gaussian per iteration, 16-column strips);
+ * bit 3 packed float2 forward; bit 4 16-column forward rectangles; bit 5 8-column backward
+ * rectangles.  Every variant produces results within the same parity bar.  Process-wide;
+ * defaults (1, 2, 0) are the shipped configuration. */
 int gsplat_debug_set_raster_variant(int fwd_pxl, int bwd_pxl, int bwd_flags);
 
 #ifdef __cplusplus

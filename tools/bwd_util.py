@@ -42,11 +42,29 @@ with torch.no_grad():
         keep |= ~((det > 0) & (lmax > 0))
         return keep & (o >= 1 / 255)
 
+    def touches_exact(gx, gy, a, b, c, o, rx0, rx1, ry0, ry1):
+        """min over the rectangle of sigma (exact for a PSD conic), culled with a margin."""
+        dx0, dx1 = gx - rx1, gx - rx0
+        dy0, dy1 = gy - ry1, gy - ry0
+        inside = (dx0 <= 0) & (dx1 >= 0) & (dy0 <= 0) & (dy1 >= 0)
+        def q(dx, dy):
+            return a * dx * dx + 2 * b * dx * dy + c * dy * dy
+        best = torch.full_like(gx, float("inf"))
+        for dxe in (dx0, dx1):
+            dys = torch.clamp(-b * dxe / c, dy0, dy1)
+            best = torch.minimum(best, q(dxe, dys))
+        for dye in (dy0, dy1):
+            dxs = torch.clamp(-b * dye / a, dx0, dx1)
+            best = torch.minimum(best, q(dxs, dye))
+        smin = torch.where(inside, torch.zeros_like(best), 0.5 * best)
+        keep = ~(smin * 0.999 - 1e-3 > torch.log(255 * o))
+        keep |= ~((a * c - b * b > 0) & (a > 0))
+        return keep & (o >= 1 / 255)
+
     rng = np.random.default_rng(0)
     T = tb[0] * tb[1]
     sample = rng.choice(T, 256, replace=False)
-    tot = {k: 0.0 for k in ("pairs_valid", "iters_s8", "iters_s4", "iters_s16", "fwd_pairs",
-                            "fwd_iters_s4", "list")}
+    tot = {k: 0.0 for k in ("pairs_valid", "fwd_pairs", "list")}
     b = bins.cpu().numpy()
     for t in sample:
         s, e = int(b[t, 0]), int(b[t, 1])
@@ -69,18 +87,22 @@ with torch.no_grad():
         tot["fwd_pairs"] += (v & (idx[:, None, None] <= fin + 1)).sum().item()
         tot["pairs_valid"] += (v & (idx[:, None, None] <= fin)).sum().item()
         tot["list"] += e - s
-        for rows, key in ((8, "iters_s8"), (4, "iters_s4"), (16, "iters_s16")):
-            for r0 in range(ty * 16, min(ty * 16 + 16, H), rows):
-                r1 = min(r0 + rows - 1, H - 1)
-                k = touches(gx, gy, a, bb, c, o, float(tx * 16), float(min(tx * 16 + 15, W - 1)),
-                            float(r0), float(r1))
-                mf = fin[r0 - ty * 16: r1 - ty * 16 + 1].max().item()
-                tot[key] += (k & (idx <= mf)).sum().item()
-                if key == "iters_s4":
-                    tot["fwd_iters_s4"] += (k & (idx <= mf + 64)).sum().item()
+        # wave footprints (cols, rows): strips of the full tile width and 8x8 blocks
+        for cols, rows in ((16, 8), (16, 4), (16, 16), (8, 8), (8, 16)):
+            for c0 in range(tx * 16, min(tx * 16 + 16, W), cols):
+                c1 = min(c0 + cols - 1, W - 1)
+                for r0 in range(ty * 16, min(ty * 16 + 16, H), rows):
+                    r1 = min(r0 + rows - 1, H - 1)
+                    mf = fin[r0 - ty * 16: r1 - ty * 16 + 1, c0 - tx * 16: c1 - tx * 16 + 1].max().item()
+                    for name, fn in (("cons", touches), ("exact", touches_exact)):
+                        k = fn(gx, gy, a, bb, c, o, float(c0), float(c1), float(r0), float(r1))
+                        key = f"{name}_{cols}x{rows}"
+                        tot[key] = tot.get(key, 0) + (k & (idx <= mf)).sum().item()
     n = len(sample)
-    print({k: v / n for k, v in tot.items()})
-    for rows, key in ((8, "iters_s8"), (4, "iters_s4"), (16, "iters_s16")):
-        pix = 16 * rows
-        print(f"strip {rows} rows: iters/tile {tot[key]/n:.0f}; lane util "
-              f"{tot['pairs_valid'] / (tot[key] * pix):.3f}")
+    print({k: round(v / n, 1) for k, v in tot.items()})
+    for cols, rows in ((16, 8), (16, 4), (16, 16), (8, 8), (8, 16)):
+        for name in ("cons", "exact"):
+            key = f"{name}_{cols}x{rows}"
+            pix = cols * rows
+            print(f"{name:5s} {cols}x{rows}: wave iters/tile {tot[key]/n:7.1f}; lane util "
+                  f"{tot['pairs_valid'] / (tot[key] * pix):.3f}")

@@ -50,8 +50,8 @@ def timeit(fn, reps=10):
     return s.elapsed_time(e) / reps
 
 variants = [(f, b, fl) for f, b, fl in
-            [(1, 2, 0), (2, 2, 0), (4, 4, 0), (2, 2, 6), (4, 4, 6), (1, 2, 1), (1, 4, 1),
-             (1, 1, 0)]]
+            [(1, 2, 0), (1, 2, 4), (1, 2, 16), (2, 2, 0), (2, 2, 8), (4, 4, 0), (1, 2, 32),
+             (1, 2, 1)]]
 res = {v: {"fwd": [], "bwd": []} for v in variants}
 for rnd in range(5):
     for v in variants:
