@@ -621,7 +621,8 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
     const float *__restrict__ colors, const float *__restrict__ opacity,
     const float *__restrict__ background, const float *__restrict__ final_Ts,
     const int *__restrict__ final_idx, const float *__restrict__ v_out,
-    const float *__restrict__ v_out_alpha, float alpha_max, float *__restrict__ rec) {
+    const float *__restrict__ v_out_alpha, float alpha_max, float *__restrict__ rec,
+    bool stage_only) {
   constexpr int PXL = 2 * NP;
   constexpr int LROWS = 64 / COLS;
   const WaveRect R = wave_rect<PXL, COLS>(tbx, tby, H, W);
@@ -676,7 +677,7 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
     const int n = __popcll(kmask);
     wave_lds_sync();
     constexpr int U = 1;  // (two per iteration measured slower: register pressure)
-    for (int t = 0; t < n; t += U) {
+    for (int t = 0; t < (stage_only ? 0 : n); t += U) {
       float parts[U][9];
       bool anyv[U];
       int gid[U];
@@ -1105,7 +1106,8 @@ extern "C" int gsplat_rasterize_backward(int tile_bounds_x, int tile_bounds_y, i
                      dim3(cdiv(T, (tiles_per_block<2 * NP, C>()))), dim3(256), 0, st,         \
                      tile_bounds_x, tile_bounds_y, img_height, img_width, gaussian_ids_sorted,  \
                      (const int2 *)tile_bins, (const float2 *)xys, conics, colors, opacity,     \
-                     background, final_Ts, final_idx, v_output, v_output_alpha, alpha_max, rec)
+                     background, final_Ts, final_idx, v_output, v_output_alpha, alpha_max, rec, \
+                     (g_bwd_flags & 64) != 0)
     const bool atomics = !(g_bwd_flags & 1);
     const bool packed = g_bwd_pxl >= 2 && !(g_bwd_flags & 2);
     const bool narrow = g_bwd_flags & 32;  // 8-column wave rectangles
