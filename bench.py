@@ -73,6 +73,37 @@ def algorithmic_bytes(N, I, P, T, K, nvis):
     }
 
 
+# Device kernels behind each C-ABI entry (for the PMC traffic of the dominant entry).
+ENTRY_KERNELS = {
+    "gsplat_rasterize_backward": ("raster_bwd", "split_grads_kernel"),
+    "gsplat_rasterize_forward": ("raster_fwd",),
+    "gsplat_compute_sh_forward": ("sh_fwd_kernel",),
+}
+PMC_TRAFFIC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
+                           "pmc_traffic.json")
+
+
+def pmc_traffic(entry):
+    """HBM bytes per call of a C-ABI entry from the committed rocprofv3 PMC summary
+    (profiles/pmc_traffic.json, tools/pmc_bench.sh + tools/pmc_summary.py): FETCH_SIZE is
+    doubled (gfx950 counts half the bytes of wide reads, MI355X_MICROARCH.md HBM section),
+    WRITE_SIZE taken as is; None when no summary covers the entry."""
+    try:
+        with open(PMC_TRAFFIC) as f:
+            kern = json.load(f)["kernels"]
+    except (OSError, ValueError, KeyError):
+        return None
+    pats = ENTRY_KERNELS.get(entry)
+    if not pats:
+        return None
+    tot, hit = 0.0, False
+    for name, v in kern.items():
+        if any(p in name for p in pats) and v.get("fetch_kb") is not None:
+            tot += (2.0 * v["fetch_kb"] + (v.get("write_kb") or 0.0)) * 1024.0
+            hit = True
+    return int(tot) if hit else None
+
+
 def cpu_baseline(scene, cam, sh_degree, budget_tiles=64, seed=0):
     """C oracle (single-threaded restatement of gsplat) on a bounded sample: the full
     per-Gaussian stages (project, SH, map+stable sort+bins) plus rasterize fwd+bwd on
@@ -218,7 +249,7 @@ def main():
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
         "frac": round(dom_bytes / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if dom_bytes else None,
-        "traffic": None,
+        "traffic": pmc_traffic(dom),
         "step_algorithmic_bytes": step_bytes,
         "step_frac": round(step_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
         "roofline_mpix_s": round(P / (step_bytes / (HBM_PEAK_GBS * 1e9)) / 1e6, 1),

@@ -1,5 +1,9 @@
 """Per-kernel averages of rocprofv3 --pmc CSV passes (tools/pmc_bench.sh output).
-Usage: pmc_summary.py gpurun_out [out.csv]"""
+Usage: pmc_summary.py gpurun_out [out.csv] [traffic.json]
+
+traffic.json (read by bench.py for roofline.traffic): per device kernel, the mean per-dispatch
+FETCH_SIZE and WRITE_SIZE in KiB as rocprofv3 reports them (uncorrected)."""
+import json
 import collections
 import csv
 import glob
@@ -24,6 +28,12 @@ for k, d in sorted(acc.items()):
         row[c] = sum(v) / len(v)
     rows.append(row)
 cols = sorted({c for r in rows for c in r if c != "kernel"})
+if len(sys.argv) > 3:
+    tj = {r["kernel"]: {"fetch_kb": r.get("FETCH_SIZE"), "write_kb": r.get("WRITE_SIZE")}
+          for r in rows if "FETCH_SIZE" in r and "WRITE_SIZE" in r}
+    with open(sys.argv[3], "w") as f:
+        json.dump({"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, "
+                             "tools/pmc_bench.sh", "kernels": tj}, f, indent=1)
 out = sys.argv[2] if len(sys.argv) > 2 else None
 w = csv.writer(open(out, "w", newline="") if out else sys.stdout)
 w.writerow(["kernel"] + cols)
