@@ -1,0 +1,74 @@
+"""Fused splatfacto photometric loss on MI355X.
+
+nerfstudio 1.0 splatfacto's get_loss_dict (reached from the reference's training step,
+/root/reference/gaussctrl/gc_pipeline.py:477-478) computes
+
+    main_loss = (1 - ssim_lambda) * |gt - pred|.mean()
+                + ssim_lambda * (1 - SSIM(gt.permute(2,0,1)[None], pred.permute(2,0,1)[None]))
+
+with pytorch_msssim's SSIM (11x11 Gaussian window sigma 1.5, 'valid' filtering, data range 1,
+K = (0.01, 0.03)).  `fused_splatfacto_loss` evaluates it with two HIP kernels (csrc/loss.hip)
+instead of ~20 torch ops and 10 MIOpen convolutions; gradients flow to `pred` only.  The torch
+restatement it is tested against is train.splatfacto_loss.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+from torch import Tensor
+from torch.autograd import Function
+
+from . import _lib
+
+SSIM_WIN, SSIM_SIGMA = 11, 1.5
+
+
+def _window_host():
+    coords = torch.arange(SSIM_WIN, dtype=torch.float32) - SSIM_WIN // 2
+    g = torch.exp(-(coords ** 2) / (2 * SSIM_SIGMA ** 2))
+    g = g / g.sum()
+    return (ctypes.c_float * SSIM_WIN)(*g.tolist())
+
+
+_WINDOW = _window_host()
+
+
+class _FusedL1SSIM(Function):
+    @staticmethod
+    def forward(ctx, pred: Tensor, gt: Tensor, ssim_lambda: float):
+        if pred.dim() != 3 or pred.shape != gt.shape:
+            raise ValueError("fused_splatfacto_loss: pred and gt must both be [H, W, C]")
+        pred = pred.float().contiguous()
+        gt = gt.float().contiguous()
+        dev = _lib.check_device("fused_splatfacto_loss", pred, gt)
+        H, W, C = pred.shape
+        nb = _lib.lib().gsplat_l1_ssim_num_blocks(H, W)
+        partials = torch.empty((max(2 * nb, 1),), device=dev, dtype=torch.float32)
+        dmaps = torch.empty((3 * C * max(H - SSIM_WIN + 1, 0) * max(W - SSIM_WIN + 1, 0),),
+                            device=dev, dtype=torch.float32)
+        loss = torch.empty((), device=dev, dtype=torch.float32)
+        P = _lib.ptr
+        _lib.call("gsplat_l1_ssim_forward", H, W, C, P(pred), P(gt), ctypes.cast(_WINDOW,
+                  ctypes.c_void_p), float(ssim_lambda), P(partials), P(dmaps), P(loss),
+                  _lib.stream(dev))
+        ctx.save_for_backward(pred, gt, dmaps)
+        ctx.ssim_lambda = float(ssim_lambda)
+        return loss
+
+    @staticmethod
+    def backward(ctx, grad_loss):
+        pred, gt, dmaps = ctx.saved_tensors
+        H, W, C = pred.shape
+        g = grad_loss.float().contiguous()
+        v_pred = torch.empty_like(pred)
+        P = _lib.ptr
+        _lib.call("gsplat_l1_ssim_backward", H, W, C, P(pred), P(gt), ctypes.cast(_WINDOW,
+                  ctypes.c_void_p), ctx.ssim_lambda, P(dmaps), P(g), P(v_pred),
+                  _lib.stream(pred.device))
+        return v_pred, None, None
+
+
+def fused_splatfacto_loss(pred: Tensor, gt: Tensor, ssim_lambda: float = 0.2) -> Tensor:
+    """(1 - ssim_lambda) * L1 + ssim_lambda * (1 - SSIM) on [H, W, C] images, on the GPU."""
+    return _FusedL1SSIM.apply(pred, gt, ssim_lambda)

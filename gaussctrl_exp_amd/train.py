@@ -38,7 +38,7 @@ def ssim(x, y, data_range=1.0, win_size=11, sigma=1.5, k1=0.01, k2=0.03):
     """pytorch_msssim.ssim semantics (separable Gaussian window, 'valid' convolution,
     size_average): x, y [B,C,H,W]."""
     C = x.shape[1]
-    w = _gauss_window(win_size, sigma, x.device)
+    w = _gauss_window(win_size, sigma, x.device).to(x.dtype)  # pytorch_msssim: win.to(X.dtype)
 
     def filt(t):
         t = F.conv2d(t, w.view(1, 1, 1, -1).expand(C, 1, 1, -1), groups=C)
@@ -111,7 +111,10 @@ class TrainStep:
     def loss(self, pred, gt):
         if self.loss_kind == "l1":
             return torch.abs(gt - pred).mean()
-        return splatfacto_loss(pred, gt)
+        if self.loss_kind == "splatfacto_torch" or self.api is not None or not pred.is_cuda:
+            return splatfacto_loss(pred, gt)  # torch restatement (CPU-emulation tests)
+        from .loss import fused_splatfacto_loss
+        return fused_splatfacto_loss(pred, gt, SSIM_LAMBDA)
 
     def zero_grad(self):
         for p in self.params:

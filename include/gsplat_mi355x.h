@@ -153,6 +153,25 @@ int gsplat_rasterize_backward(int tile_bounds_x, int tile_bounds_y, int img_heig
  * defaults (1, 2, 0) are the shipped configuration. */
 int gsplat_debug_set_raster_variant(int fwd_pxl, int bwd_pxl, int bwd_flags);
 
+/* ---- training-step photometric loss -------------------------------------
+ * nerfstudio 1.0 splatfacto get_loss_dict's main loss, which the reference's training step
+ * computes on every iteration (gc_pipeline.py:477-478):
+ *     loss = (1 - lambda) * mean|gt - pred| + lambda * (1 - SSIM(gt, pred))
+ * with pytorch_msssim's SSIM (11x11 Gaussian window, 'valid' filtering, data range 1,
+ * K = (0.01, 0.03)).  pred / gt: [H, W, C] fp32 (the caller's rgb and gt images, H, W >= 11);
+ * window11: HOST pointer to the 11 normalised window weights.  Forward writes partials
+ * [2 * gsplat_l1_ssim_num_blocks(H, W)] (scratch), dmaps [3 * C * (H-10) * (W-10)] (kept for
+ * the backward) and the loss scalar (device).  Backward reads the upstream gradient scalar
+ * from device memory (no host sync) and writes v_pred [H, W, C] (gt gets no gradient). */
+int gsplat_l1_ssim_num_blocks(int img_height, int img_width);
+int gsplat_l1_ssim_forward(int img_height, int img_width, int channels, const float *pred,
+                           const float *gt, const float *window11, float ssim_lambda,
+                           float *partials, float *dmaps, float *loss, void *stream);
+int gsplat_l1_ssim_backward(int img_height, int img_width, int channels, const float *pred,
+                            const float *gt, const float *window11, float ssim_lambda,
+                            const float *dmaps, const float *grad_loss, float *v_pred,
+                            void *stream);
+
 #ifdef __cplusplus
 }
 #endif
