@@ -99,9 +99,13 @@ class TrainStep:
         self.sh_degree = sh_degree
         self.loss_kind = loss
         self.api = api  # gsplat implementation override (tests: CPU-oracle emulation)
-        self.opt = torch.optim.Adam(
-            [{"params": [getattr(scene, k)], "lr": GROUP_LR[k], "name": k}
-             for k in PARAM_NAMES], eps=1e-15, foreach=True)
+        groups = [{"params": [getattr(scene, k)], "lr": GROUP_LR[k], "name": k}
+                  for k in PARAM_NAMES]
+        if api is None and scene.means.is_cuda:
+            from .optim import FusedAdam
+            self.opt = FusedAdam(groups, eps=1e-15)  # csrc/adam.hip, one launch per step
+        else:  # CPU-oracle emulation (tests): torch's Adam, same semantics
+            self.opt = torch.optim.Adam(groups, eps=1e-15, foreach=True)
         self.step_count = 0
 
     def _xyz_lr(self):

@@ -172,6 +172,18 @@ int gsplat_l1_ssim_backward(int img_height, int img_width, int channels, const f
                             const float *dmaps, const float *grad_loss, float *v_pred,
                             void *stream);
 
+/* ---- optimizer step -----------------------------------------------------
+ * One torch.optim.Adam step (non-capturable foreach semantics, no weight decay / amsgrad) over
+ * up to 8 parameter tensors in ONE launch, as the reference's trainer takes it for the six
+ * splatfacto groups (gc_trainer.py:281,298; gc_config.py:58-87).  params / grads / exp_avgs /
+ * exp_avg_sqs: HOST arrays of device pointers (fp32, contiguous); numels, lrs: HOST arrays;
+ * step: the step number after increment (>= 1); beta1 must lie in (0.5, 1) (torch's lerp
+ * formula changes below).  Updates params, exp_avgs, exp_avg_sqs in place. */
+int gsplat_adam_step(int num_tensors, float *const *params, const float *const *grads,
+                     float *const *exp_avgs, float *const *exp_avg_sqs, const int64_t *numels,
+                     const float *lrs, int step, float beta1, float beta2, float eps,
+                     void *stream);
+
 #ifdef __cplusplus
 }
 #endif
