@@ -145,6 +145,20 @@ def test_binning_fused_bitexact(gpu, case):
     np.testing.assert_array_equal(_np(bins), ref["tile_bins"])
 
 
+def test_binning_large_tile_grid_bitexact(gpu):
+    """A 4096x2400 image (38,400 tiles: 16-bit tile keys, three 6-bit sort passes)."""
+    case = (3000, 4096, 2400, 5, 0.01, 0.2, 1.5)
+    sc, cam, scales, quats = _inputs(*case)
+    assert cam.tile_bounds[0] * cam.tile_bounds[1] >= 36 * 1024
+    g, o = _project_both(gpu, sc, cam, scales, quats)
+    xys, depths, radii, conics, nth, cov3d = g
+    I, gids, bins = bin_gaussians(xys, depths, radii, nth, cam.height, cam.width)
+    ref = O.bin_and_sort(o[0], o[1], o[2], o[4], cam.tile_bounds)
+    assert I == ref["num_intersects"] and I > 0
+    np.testing.assert_array_equal(_np(gids), ref["gaussian_ids_sorted"])
+    np.testing.assert_array_equal(_np(bins), ref["tile_bins"])
+
+
 @pytest.mark.parametrize("case", CASES)
 def test_binning_utils_bitexact(gpu, case):
     sc, cam, scales, quats = _inputs(*case)
