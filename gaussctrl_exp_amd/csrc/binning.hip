@@ -32,8 +32,9 @@ namespace {
 constexpr int TPB = 256;
 constexpr int SC_ITEMS = 16;
 constexpr int SC_TILE = TPB * SC_ITEMS;  // elements per scan workgroup
-constexpr int OS_ITEMS = 16;
-constexpr int OS_TILE = TPB * OS_ITEMS;  // keys per sort workgroup
+// keys per thread of a sort pass (workgroup tile = TPB * items): small sorts use short tiles
+// so that more, shorter workgroups run at once (a pass is a chain of latencies per workgroup)
+int os_items_for(long long n) { return n >= (16LL << 20) ? 16 : (n >= (4LL << 20) ? 8 : 4); }
 constexpr int OS_MAX_PASSES = 8;
 constexpr uint32_t ST_AGG = 1u << 30;    // status word: aggregate of this tile only
 constexpr uint32_t ST_PRE = 2u << 30;    // status word: inclusive prefix up to this tile
@@ -141,7 +142,7 @@ void device_exclusive_scan(const uint32_t *in, uint32_t *out, long long m, uint3
 // ------------------------------------------------------------ one-sweep radix sort
 
 struct SortPlan {
-  int passes, width, radix;
+  int passes, width, radix, items;
   long long nblocks;
 };
 
@@ -151,16 +152,22 @@ SortPlan sort_plan(long long n, int begin_bit, int end_bit) {
   p.passes = bits <= 0 ? 0 : (bits + 7) / 8;
   p.width = p.passes ? (bits + p.passes - 1) / p.passes : 0;
   p.radix = 1 << p.width;
-  p.nblocks = n > 0 ? cdiv(n, OS_TILE) : 0;
+  p.items = os_items_for(n);
+  p.nblocks = n > 0 ? cdiv(n, (long long)TPB * p.items) : 0;
   return p;
 }
 
 // Workspace: [hist: MAX_PASSES x 256][tickets: MAX_PASSES][error][pad] | status[passes][nblocks][radix]
 constexpr size_t OS_HEAD_WORDS = OS_MAX_PASSES * 256 + OS_MAX_PASSES + 8;
 
+// [head words][one-sweep status: passes x nblocks x radix | reduce-then-scan tile counts
+// nblocks x radix + scan scratch]
 size_t radix_ws_bytes(long long n, int begin_bit, int end_bit) {
   SortPlan p = sort_plan(n, begin_bit, end_bit);
-  return (OS_HEAD_WORDS + (size_t)p.passes * p.nblocks * p.radix) * sizeof(uint32_t);
+  const size_t onesweep = (size_t)p.passes * p.nblocks * p.radix * sizeof(uint32_t);
+  const size_t rts = (size_t)p.nblocks * p.radix * sizeof(uint32_t) +
+                     scan_ws_bytes((long long)p.nblocks * p.radix);
+  return OS_HEAD_WORDS * sizeof(uint32_t) + (onesweep > rts ? onesweep : rts);
 }
 
 template <typename K>
@@ -197,10 +204,57 @@ __global__ __launch_bounds__(TPB) void os_hist_kernel(const K *__restrict__ keys
     if (lh[i]) atomicAdd(&hist[i], lh[i]);
 }
 
-template <typename K>
+// Reduce-then-scan pass, part 1: the digit histogram of every tile of TPB*ITEMS keys, stored
+// digit-major (counts[d * nblocks + tile]) so one exclusive scan yields every tile's global
+// offset for every digit.
+template <typename K, int ITEMS>
+__global__ __launch_bounds__(TPB) void rts_count_kernel(const K *__restrict__ keys, long long n,
+                                                        int shift, int width, long long nblocks,
+                                                        uint32_t *__restrict__ counts) {
+  __shared__ uint32_t h[256];
+  const int tid = threadIdx.x;
+  const int R = 1 << width;
+  const uint32_t dmask = (uint32_t)(R - 1);
+  h[tid] = 0;
+  __syncthreads();
+  const long long base = (long long)blockIdx.x * TPB * ITEMS;
+  K k[ITEMS];
+#pragma unroll
+  for (int r = 0; r < ITEMS; ++r) {
+    const long long i = base + r * TPB + tid;
+    k[r] = i < n ? keys[i] : (K)0;
+  }
+#pragma unroll
+  for (int r = 0; r < ITEMS; ++r)
+    if (base + r * TPB + tid < n) atomicAdd(&h[(uint32_t)(k[r] >> shift) & dmask], 1u);
+  __syncthreads();
+  if (tid < R) counts[(size_t)tid * nblocks + blockIdx.x] = h[tid];
+}
+
+// Reduce-then-scan pass, part 2: one workgroup per digit scans that digit's row of tile
+// counts in place (exclusive) and writes the row total; the pass kernel turns the <= 256 row
+// totals into digit bases itself.  (One launch instead of a three-kernel device scan.)
+__global__ __launch_bounds__(1024) void rts_rowscan_kernel(uint32_t *__restrict__ counts,
+                                                           long long nblocks,
+                                                           uint32_t *__restrict__ rowtot) {
+  __shared__ uint32_t lds[16];
+  uint32_t *row = counts + (size_t)blockIdx.x * nblocks;
+  uint32_t running = 0;
+  for (long long c0 = 0; c0 < nblocks; c0 += 1024) {
+    const long long i = c0 + threadIdx.x;
+    const uint32_t v = i < nblocks ? row[i] : 0u;
+    uint32_t tot;
+    const uint32_t ex = block_exclusive_scan<1024>(v, tot, lds);
+    if (i < nblocks) row[i] = running + ex;
+    running += tot;
+  }
+  if (threadIdx.x == 0) rowtot[blockIdx.x] = running;
+}
+
+template <typename K, int ITEMS>
 struct OsSmem {
-  K keys[OS_TILE];
-  uint32_t vals[OS_TILE];
+  K keys[TPB * ITEMS];
+  uint32_t vals[TPB * ITEMS];
   uint32_t wcnt[4][256];   // per-wave digit counters, then per-wave digit offsets
   uint32_t loc_off[256];   // tile-local exclusive offset of each digit
   uint32_t gofs[256];      // global output offset of each digit, minus loc_off
@@ -209,52 +263,83 @@ struct OsSmem {
   uint32_t ticket;
 };
 
-template <typename K>
+template <typename K, int WIDTH, int ITEMS>
 __global__ __launch_bounds__(TPB) void os_pass_kernel(
     const K *__restrict__ kin, const uint32_t *__restrict__ vin, K *__restrict__ kout,
     uint32_t *__restrict__ vout, long long n, int shift, int width,
     const uint32_t *__restrict__ hist, uint32_t *__restrict__ ticket_ctr,
-    uint32_t *__restrict__ status, uint32_t *__restrict__ err) {
-  __shared__ OsSmem<K> sm;
+    uint32_t *__restrict__ status, uint32_t *__restrict__ err,
+    unsigned long long *__restrict__ tbuf, bool use_ticket, const uint32_t *__restrict__ offs,
+    long long nblocks) {
+  __shared__ OsSmem<K, ITEMS> sm;
+  // optional phase timestamps (debug hook gsplat_debug_sort_timing): [ticket][6]
+  unsigned long long ts0 = tbuf ? __builtin_amdgcn_s_memrealtime() : 0ull;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int R = 1 << width;
   const uint32_t dmask = (uint32_t)(R - 1);
-  if (tid == 0) sm.ticket = atomicAdd(ticket_ctr, 1u);
+  // Tile index = dispatch order: workgroups are dispatched in increasing ID order, so every
+  // tile a workgroup looks back at has already been dispatched and makes progress without it.
+  // (An atomic ticket serialised ~1k workgroups on one counter: 9 us per pass.)
+  if (tid == 0) sm.ticket = use_ticket ? atomicAdd(ticket_ctr, 1u) : blockIdx.x;
 #pragma unroll
   for (int w = 0; w < 4; ++w) sm.wcnt[w][tid] = 0;
-  {
+  {  // digit bases: exclusive scan of the pass histogram (one-sweep) or of the digit row
+     // totals (reduce-then-scan)
     uint32_t h = tid < R ? hist[tid] : 0u, tot;
     sm.hscan[tid] = block_exclusive_scan<TPB>(h, tot, sm.scan_tmp);  // contains barriers
   }
   const uint32_t t = sm.ticket;
-  const long long base = (long long)t * OS_TILE;
-  const long long seg = base + (long long)wave * (OS_ITEMS * 64);
+  unsigned long long ts1 = tbuf ? __builtin_amdgcn_s_memrealtime() : 0ull;
+  const long long base = (long long)t * TPB * ITEMS;
+  const long long seg = base + (long long)wave * (ITEMS * 64);
   const unsigned long long lt = (1ull << lane) - 1ull;
 
-  K key[OS_ITEMS];
-  uint32_t val[OS_ITEMS], rank[OS_ITEMS];
+  K key[ITEMS];
+  uint32_t val[ITEMS], rank[ITEMS];
 #pragma unroll
-  for (int r = 0; r < OS_ITEMS; ++r) {
+  for (int r = 0; r < ITEMS; ++r) {
     const long long i = seg + r * 64 + lane;
     const bool valid = i < n;
     key[r] = valid ? kin[i] : (K)0;
     val[r] = valid ? vin[i] : 0u;
   }
+  unsigned long long ts2 = 0ull;
+  if (tbuf) {
+    // the loads are consumed by the ranking below; force them complete for the timestamp
+    uint32_t acc = 0;
 #pragma unroll
-  for (int r = 0; r < OS_ITEMS; ++r) {
+    for (int r = 0; r < ITEMS; ++r) acc ^= (uint32_t)key[r] ^ val[r];
+    asm volatile("" ::"v"(acc));
+    ts2 = __builtin_amdgcn_s_memrealtime();
+  }
+  // Stable rank within the wave: a ballot match finds the lanes sharing this key's digit
+  // (peers); the group's lowest lane reserves popc(peers) slots of the wave's LDS counter for
+  // that digit with ONE returning LDS atomic and the others read the old value from it
+  // (a wave's LDS atomics execute in issue order, so the rounds stay ordered).
+#pragma unroll
+  for (int r = 0; r < ITEMS; ++r) {
     const bool valid = seg + r * 64 + lane < n;
     const uint32_t d = (uint32_t)(key[r] >> shift) & dmask;
     unsigned long long peers = __ballot(valid);
-    for (int b = 0; b < width; ++b) {
+#pragma unroll
+    for (int b = 0; b < WIDTH; ++b) {
       const bool bit = (d >> b) & 1u;
       const unsigned long long m = __ballot(bit);
       peers &= bit ? m : ~m;
     }
-    const uint32_t old = sm.wcnt[wave][d];
+    const int leader = valid ? (int)__builtin_ctzll(peers) : lane;
+    uint32_t old = 0;
+    if (valid && leader == lane) old = atomicAdd(&sm.wcnt[wave][d], (uint32_t)__popcll(peers));
+    old = __shfl(old, leader, 64);
     rank[r] = old + (uint32_t)__popcll(peers & lt);
-    __builtin_amdgcn_wave_barrier();
-    if (valid && (peers & lt) == 0) sm.wcnt[wave][d] = old + (uint32_t)__popcll(peers);
-    __builtin_amdgcn_wave_barrier();
+  }
+  unsigned long long ts2a = 0ull;
+  if (tbuf) {
+    uint32_t acc = 0;
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) acc ^= rank[r];
+    asm volatile("" ::"v"(acc));
+    ts2a = __builtin_amdgcn_s_memrealtime();
   }
   __syncthreads();
   uint32_t local_count = 0;
@@ -269,7 +354,7 @@ __global__ __launch_bounds__(TPB) void os_pass_kernel(
     local_count = s;  // digit tid's count in this tile (0 for tid >= R)
   }
   // publish this tile's aggregate as early as possible (tile 0 publishes its prefix)
-  if (tid < R) {
+  if (!offs && tid < R) {
     uint32_t word = (t == 0 ? ST_PRE : ST_AGG) | local_count;
     __hip_atomic_store(&status[(size_t)t * R + tid], word, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
@@ -279,9 +364,10 @@ __global__ __launch_bounds__(TPB) void os_pass_kernel(
     sm.loc_off[tid] = block_exclusive_scan<TPB>(local_count, tot, sm.scan_tmp);
   }
   __syncthreads();  // loc_off[d] is read by every thread below
+  unsigned long long ts2b = tbuf ? __builtin_amdgcn_s_memrealtime() : 0ull;
   // stable local sort into LDS
 #pragma unroll
-  for (int r = 0; r < OS_ITEMS; ++r) {
+  for (int r = 0; r < ITEMS; ++r) {
     const bool valid = seg + r * 64 + lane < n;
     if (valid) {
       const uint32_t d = (uint32_t)(key[r] >> shift) & dmask;
@@ -290,26 +376,53 @@ __global__ __launch_bounds__(TPB) void os_pass_kernel(
       sm.vals[lp] = val[r];
     }
   }
-  // decoupled look-back for this digit's exclusive prefix over the preceding tiles
-  if (tid < R) {
+  unsigned long long ts3 = tbuf ? __builtin_amdgcn_s_memrealtime() : 0ull;
+  // decoupled look-back for this digit's exclusive prefix over the preceding tiles.  The
+  // status words are agent-scope (they cross XCDs, so every read misses the per-XCD L2): the
+  // walk reads LB_WIN predecessors per round trip and consumes them nearest first until it
+  // meets an inclusive prefix; a not-yet-published word ends the round.
+  if (offs && tid < R) {  // reduce-then-scan: offsets come from the scanned tile counts
+    sm.gofs[tid] = sm.hscan[tid] + offs[(size_t)tid * nblocks + t] - sm.loc_off[tid];
+  } else if (tid < R) {
     uint32_t excl = 0;
     if (t > 0) {
+      constexpr int LB_WIN = 16;
       long long j = (long long)t - 1;
       uint32_t spins = 0;
-      while (true) {
-        const uint32_t s = __hip_atomic_load(&status[(size_t)j * R + tid], __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT);
-        if ((s & ~ST_VAL) == 0) {
+      bool done = false;
+      while (!done) {
+        uint32_t st[LB_WIN];
+#pragma unroll
+        for (int k = 0; k < LB_WIN; ++k)
+          st[k] = j - k >= 0 ? __hip_atomic_load(&status[(size_t)(j - k) * R + tid],
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                             : 0u;
+        int used = 0;
+        bool stop = false;
+#pragma unroll
+        for (int k = 0; k < LB_WIN; ++k) {
+          if (stop) continue;
+          const uint32_t sv = st[k];
+          if (j - k < 0 || (sv & ~ST_VAL) == 0) {  // not published yet: next round
+            stop = true;
+            continue;
+          }
+          excl += sv & ST_VAL;
+          used = k + 1;
+          if ((sv & ST_PRE) || j - k == 0) {
+            done = true;
+            stop = true;
+          }
+        }
+        if (done) break;
+        if (used == 0) {
           if (++spins > SPIN_LIMIT) {  // bounded: report instead of hanging
             atomicOr(err, 1u);
             break;
           }
           __builtin_amdgcn_s_sleep(1);
-          continue;
         }
-        excl += s & ST_VAL;
-        if ((s & ST_PRE) || j == 0) break;
-        --j;
+        j -= used;
       }
       __hip_atomic_store(&status[(size_t)t * R + tid], ST_PRE | (excl + local_count),
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -317,9 +430,10 @@ __global__ __launch_bounds__(TPB) void os_pass_kernel(
     sm.gofs[tid] = sm.hscan[tid] + excl - sm.loc_off[tid];
   }
   __syncthreads();
-  const long long cnt = min((long long)OS_TILE, n - base);
+  unsigned long long ts4 = tbuf ? __builtin_amdgcn_s_memrealtime() : 0ull;
+  const long long cnt = min((long long)TPB * ITEMS, n - base);
 #pragma unroll
-  for (int r = 0; r < OS_ITEMS; ++r) {
+  for (int r = 0; r < ITEMS; ++r) {
     const int i = r * TPB + tid;
     if (i < cnt) {
       const K k = sm.keys[i];
@@ -329,7 +443,24 @@ __global__ __launch_bounds__(TPB) void os_pass_kernel(
       vout[pos] = sm.vals[i];
     }
   }
+  if (tbuf && tid == 0) {
+    __builtin_amdgcn_s_waitcnt(0);
+    const unsigned long long ts5 = __builtin_amdgcn_s_memrealtime();
+    unsigned long long *o = tbuf + (size_t)t * 8;
+    o[0] = ts0; o[1] = ts1; o[2] = ts2; o[3] = ts2a; o[4] = ts2b; o[5] = ts3; o[6] = ts4;
+    o[7] = ts5;
+  }
 }
+
+// Debug hook (gsplat_debug_sort_timing): the next `calls` sort passes record per-workgroup
+// phase timestamps into consecutive [nblocks][6] slabs of this buffer.
+unsigned long long *g_sort_timing = nullptr;
+int g_sort_timing_calls = 0;
+bool g_sort_ticket = false;  // debug: atomic tickets instead of dispatch order
+// Pass scheme: reduce-then-scan (tile digit counts -> device scan -> scatter; no cross-
+// workgroup waiting) or one-sweep decoupled look-back.  Per-workgroup phase timing showed the
+// look-back chain dominating one-sweep passes on MI355X (status words cross XCDs).
+bool g_sort_rts = true;
 
 // Stable LSD sort of (keys, vals) by bits [begin_bit, end_bit).  Ping-pongs between
 // (ka, va) and (kb, vb); the last pass writes (kout, vout).  (ka, va) are clobbered when
@@ -349,21 +480,70 @@ int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t
   uint32_t *tickets = hist + OS_MAX_PASSES * 256;
   uint32_t *err = tickets + OS_MAX_PASSES;
   uint32_t *status = (uint32_t *)ws + OS_HEAD_WORDS;
-  note(hipMemsetAsync(ws, 0, radix_ws_bytes(n, begin_bit, end_bit), st), "hipMemsetAsync");
-  // Few, fat histogram blocks: every block flushes passes x 256 counters with global
-  // atomics onto the SAME addresses, which the L2 serialises -- 2048 blocks cost ~35 us.
-  const int hist_blocks = (int)min((long long)cdiv(n, TPB * 64), 256LL);
-  hipLaunchKernelGGL(os_hist_kernel<K>, dim3(hist_blocks), dim3(TPB), 0, st, ka, n, begin_bit,
-                     p.width, p.passes, hist);
+  const bool rts = g_sort_rts;
+  uint32_t *rts_counts = status;
+  uint32_t *rts_partial = status + (size_t)p.nblocks * p.radix;
+  if (rts) {
+    note(hipMemsetAsync(ws, 0, OS_HEAD_WORDS * sizeof(uint32_t), st), "hipMemsetAsync");
+  } else {
+    note(hipMemsetAsync(ws, 0, radix_ws_bytes(n, begin_bit, end_bit), st), "hipMemsetAsync");
+    // Few, fat histogram blocks: every block flushes passes x 256 counters with global
+    // atomics onto the SAME addresses, which the L2 serialises -- 2048 blocks cost ~35 us.
+    const int hist_blocks = (int)min((long long)cdiv(n, TPB * 64), 256LL);
+    hipLaunchKernelGGL(os_hist_kernel<K>, dim3(hist_blocks), dim3(TPB), 0, st, ka, n, begin_bit,
+                       p.width, p.passes, hist);
+  }
   K *kin = ka, *kalt = kb;
   uint32_t *vin = va, *valt = vb;
   for (int q = 0; q < p.passes; ++q) {
     const bool last = q == p.passes - 1;
     K *ko = last ? kout : kalt;
     uint32_t *vo = last ? vout : valt;
-    hipLaunchKernelGGL(os_pass_kernel<K>, dim3((unsigned)p.nblocks), dim3(TPB), 0, st, kin, vin,
-                       ko, vo, n, begin_bit + q * p.width, p.width, hist + q * 256, tickets + q,
-                       status + (size_t)q * p.nblocks * p.radix, err);
+    unsigned long long *tb = nullptr;
+    if (g_sort_timing && g_sort_timing_calls > 0) {  // debug hook: time this pass
+      tb = g_sort_timing;
+      --g_sort_timing_calls;
+      g_sort_timing += (size_t)p.nblocks * 8;
+    }
+    uint32_t *offs = nullptr;
+    if (rts) {  // reduce-then-scan: tile digit counts -> one exclusive scan -> offsets
+      offs = rts_counts;
+      const int sh = begin_bit + q * p.width;
+      if (p.items == 16)
+        hipLaunchKernelGGL((rts_count_kernel<K, 16>), dim3((unsigned)p.nblocks), dim3(TPB), 0, st,
+                           kin, n, sh, p.width, p.nblocks, offs);
+      else if (p.items == 8)
+        hipLaunchKernelGGL((rts_count_kernel<K, 8>), dim3((unsigned)p.nblocks), dim3(TPB), 0, st,
+                           kin, n, sh, p.width, p.nblocks, offs);
+      else
+        hipLaunchKernelGGL((rts_count_kernel<K, 4>), dim3((unsigned)p.nblocks), dim3(TPB), 0, st,
+                           kin, n, sh, p.width, p.nblocks, offs);
+      hipLaunchKernelGGL(rts_rowscan_kernel, dim3((unsigned)p.radix), dim3(1024), 0, st, offs,
+                         p.nblocks, rts_partial);
+    }
+#define OS_PASS(Wd, It)                                                                     \
+  hipLaunchKernelGGL((os_pass_kernel<K, Wd, It>), dim3((unsigned)p.nblocks), dim3(TPB), 0, st,   \
+                     kin, vin, ko, vo, n, begin_bit + q * p.width, p.width,                    \
+                     rts ? rts_partial : hist + q * 256,                                       \
+                     tickets + q, status + (size_t)q * p.nblocks * p.radix, err, tb,       \
+                     g_sort_ticket, offs, p.nblocks)
+#define OS_PASS_W(Wd)                                                                       \
+  do {                                                                                      \
+    if (p.items == 16) OS_PASS(Wd, 16); else if (p.items == 8) OS_PASS(Wd, 8);             \
+    else OS_PASS(Wd, 4);                                                                    \
+  } while (0)
+    switch (p.width) {
+      case 1: OS_PASS_W(1); break;
+      case 2: OS_PASS_W(2); break;
+      case 3: OS_PASS_W(3); break;
+      case 4: OS_PASS_W(4); break;
+      case 5: OS_PASS_W(5); break;
+      case 6: OS_PASS_W(6); break;
+      case 7: OS_PASS_W(7); break;
+      default: OS_PASS_W(8); break;
+    }
+#undef OS_PASS_W
+#undef OS_PASS
     K *kfree = (kin == ka || kin == kb) ? kin : kalt;
     uint32_t *vfree = (vin == va || vin == vb) ? vin : valt;
     kin = ko;
@@ -609,6 +789,17 @@ Phase2 carve_phase2(void *base, long long I) {
 }  // namespace gs
 
 using namespace gs;
+
+extern "C" int gsplat_debug_sort_scheme(int reduce_then_scan) {
+  g_sort_rts = reduce_then_scan != 0;
+  return 0;
+}
+
+extern "C" int gsplat_debug_sort_timing(void *buffer, int calls) {
+  g_sort_timing = (unsigned long long *)buffer;
+  g_sort_timing_calls = buffer ? calls : 0;
+  return 0;
+}
 
 extern "C" size_t gsplat_bin_count_workspace_size(int num_points) {
   return carve_phase1(nullptr, num_points).bytes;

@@ -153,6 +153,14 @@ int gsplat_rasterize_backward(int tile_bounds_x, int tile_bounds_y, int img_heig
  * defaults (1, 2, 0) are the shipped configuration. */
 int gsplat_debug_set_raster_variant(int fwd_pxl, int bwd_pxl, int bwd_flags);
 
+/* Profiling hook (not part of the gsplat surface): the next `calls` radix-sort passes write
+ * per-workgroup phase timestamps (s_memrealtime, 100 MHz: start, ticket, keys loaded, ranked,
+ * tile counts scanned, scattered to LDS, offsets resolved, end) as consecutive
+ * [workgroups][8] uint64 slabs into the device buffer (NULL disables). */
+int gsplat_debug_sort_timing(void *buffer, int calls);
+/* Radix-sort pass scheme: 1 = reduce-then-scan (default), 0 = one-sweep decoupled look-back. */
+int gsplat_debug_sort_scheme(int reduce_then_scan);
+
 /* ---- training-step photometric loss -------------------------------------
  * nerfstudio 1.0 splatfacto get_loss_dict's main loss, which the reference's training step
  * computes on every iteration (gc_pipeline.py:477-478):
