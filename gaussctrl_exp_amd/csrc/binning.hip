@@ -34,7 +34,7 @@ constexpr int SC_ITEMS = 16;
 constexpr int SC_TILE = TPB * SC_ITEMS;  // elements per scan workgroup
 // keys per thread of a sort pass (workgroup tile = TPB * items): small sorts use short tiles
 // so that more, shorter workgroups run at once (a pass is a chain of latencies per workgroup)
-int os_items_for(long long n) { return n >= (16LL << 20) ? 16 : (n >= (4LL << 20) ? 8 : 4); }
+int os_items_for(long long n) { return n >= (4LL << 20) ? 16 : 4; }
 constexpr int OS_MAX_PASSES = 8;
 constexpr uint32_t ST_AGG = 1u << 30;    // status word: aggregate of this tile only
 constexpr uint32_t ST_PRE = 2u << 30;    // status word: inclusive prefix up to this tile
@@ -210,9 +210,11 @@ __global__ __launch_bounds__(TPB) void os_hist_kernel(const K *__restrict__ keys
 template <typename K, int ITEMS>
 __global__ __launch_bounds__(TPB) void rts_count_kernel(const K *__restrict__ keys, long long n,
                                                         int shift, int width, long long nblocks,
-                                                        uint32_t *__restrict__ counts) {
+                                                        uint32_t *__restrict__ counts,
+                                                        uint32_t *__restrict__ err) {
   __shared__ uint32_t h[256];
   const int tid = threadIdx.x;
+  if (err && blockIdx.x == 0 && tid == 0) *err = 0;  // the look-back error word stays clear
   const int R = 1 << width;
   const uint32_t dmask = (uint32_t)(R - 1);
   h[tid] = 0;
@@ -452,6 +454,9 @@ __global__ __launch_bounds__(TPB) void os_pass_kernel(
   }
 }
 
+uint32_t *rts_tile_counts(void *ws) { return (uint32_t *)ws + OS_HEAD_WORDS; }
+uint32_t *sort_err_word(void *ws) { return (uint32_t *)ws + OS_MAX_PASSES * 256 + OS_MAX_PASSES; }
+
 // Debug hook (gsplat_debug_sort_timing): the next `calls` sort passes record per-workgroup
 // phase timestamps into consecutive [nblocks][6] slabs of this buffer.
 unsigned long long *g_sort_timing = nullptr;
@@ -465,9 +470,12 @@ bool g_sort_rts = true;
 // Stable LSD sort of (keys, vals) by bits [begin_bit, end_bit).  Ping-pongs between
 // (ka, va) and (kb, vb); the last pass writes (kout, vout).  (ka, va) are clobbered when
 // there are more than two passes.  ws must hold radix_ws_bytes(n, begin_bit, end_bit).
+// first_counts_ready (reduce-then-scan only): the caller's key kernel already wrote pass 0's
+// tile digit counts to rts_tile_counts(ws) and cleared the error word.
 template <typename K>
 int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t *vout,
-                     long long n, int begin_bit, int end_bit, void *ws, hipStream_t st) {
+                     long long n, int begin_bit, int end_bit, void *ws, hipStream_t st,
+                     bool first_counts_ready = false) {
   if (n <= 0) return 0;
   const SortPlan p = sort_plan(n, begin_bit, end_bit);
   if (p.passes == 0) {
@@ -483,9 +491,7 @@ int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t
   const bool rts = g_sort_rts;
   uint32_t *rts_counts = status;
   uint32_t *rts_partial = status + (size_t)p.nblocks * p.radix;
-  if (rts) {
-    note(hipMemsetAsync(ws, 0, OS_HEAD_WORDS * sizeof(uint32_t), st), "hipMemsetAsync");
-  } else {
+  if (!rts) {
     note(hipMemsetAsync(ws, 0, radix_ws_bytes(n, begin_bit, end_bit), st), "hipMemsetAsync");
     // Few, fat histogram blocks: every block flushes passes x 256 counters with global
     // atomics onto the SAME addresses, which the L2 serialises -- 2048 blocks cost ~35 us.
@@ -509,15 +515,17 @@ int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t
     if (rts) {  // reduce-then-scan: tile digit counts -> one exclusive scan -> offsets
       offs = rts_counts;
       const int sh = begin_bit + q * p.width;
-      if (p.items == 16)
+      if (q == 0 && first_counts_ready) {
+        // the key producer already wrote pass 0's tile digit counts (and cleared err)
+      } else if (p.items == 16)
         hipLaunchKernelGGL((rts_count_kernel<K, 16>), dim3((unsigned)p.nblocks), dim3(TPB), 0, st,
-                           kin, n, sh, p.width, p.nblocks, offs);
+                           kin, n, sh, p.width, p.nblocks, offs, q == 0 ? err : nullptr);
       else if (p.items == 8)
         hipLaunchKernelGGL((rts_count_kernel<K, 8>), dim3((unsigned)p.nblocks), dim3(TPB), 0, st,
-                           kin, n, sh, p.width, p.nblocks, offs);
+                           kin, n, sh, p.width, p.nblocks, offs, q == 0 ? err : nullptr);
       else
         hipLaunchKernelGGL((rts_count_kernel<K, 4>), dim3((unsigned)p.nblocks), dim3(TPB), 0, st,
-                           kin, n, sh, p.width, p.nblocks, offs);
+                           kin, n, sh, p.width, p.nblocks, offs, q == 0 ? err : nullptr);
       hipLaunchKernelGGL(rts_rowscan_kernel, dim3((unsigned)p.radix), dim3(1024), 0, st, offs,
                          p.nblocks, rts_partial);
     }
@@ -571,6 +579,10 @@ __device__ __forceinline__ void tile_bbox(float x, float y, float radius, int tb
 // 0xFFFFFFFF (sorted last).  Also writes the Gaussian's binning record, read by coalesced
 // loads here so that the depth-ordered passes need ONE gather per Gaussian:
 // rec[g] = {tile allotment, x0 | y0 << 16, x1 | y1 << 16, 0} (tile bbox, T < 65536).
+// One workgroup per depth-sort tile (TPB * ITEMS keys): with counts != null it also writes the
+// tile's histogram of the first sort digit (reduce-then-scan pass 0) and clears the sort's
+// error word, saving the sort its first count launch.
+template <int ITEMS>
 __global__ __launch_bounds__(TPB) void depth_keys_kernel(int n, const float *__restrict__ xys,
                                                          const float *__restrict__ depths,
                                                          const int *__restrict__ radii,
@@ -578,40 +590,74 @@ __global__ __launch_bounds__(TPB) void depth_keys_kernel(int n, const float *__r
                                                          int tbx, int tby,
                                                          uint32_t *__restrict__ keys,
                                                          uint32_t *__restrict__ vals,
-                                                         uint4 *__restrict__ rec) {
-  int i = blockIdx.x * TPB + threadIdx.x;
-  if (i >= n) return;
-  const int r = radii[i];
-  const bool vis = r > 0;
-  keys[i] = vis ? __float_as_uint(depths[i]) : 0xFFFFFFFFu;
-  vals[i] = (uint32_t)i;
-  const int c = vis ? num_tiles_hit[i] : 0;
-  uint4 q = {c > 0 ? (uint32_t)c : 0u, 0u, 0u, 0u};
-  if (c > 0) {
-    int x0, x1, y0, y1;
-    tile_bbox(xys[2 * i], xys[2 * i + 1], (float)r, tbx, tby, x0, x1, y0, y1);
-    q.y = (uint32_t)x0 | ((uint32_t)y0 << 16);
-    q.z = (uint32_t)x1 | ((uint32_t)y1 << 16);
+                                                         uint4 *__restrict__ rec,
+                                                         uint32_t *__restrict__ counts,
+                                                         long long nblocks,
+                                                         uint32_t *__restrict__ err) {
+  __shared__ uint32_t h[256];
+  const int tid = threadIdx.x;
+  if (counts) {
+    h[tid] = 0;
+    if (blockIdx.x == 0 && tid == 0) *err = 0;
+    __syncthreads();
   }
-  rec[i] = q;
+  const long long base = (long long)blockIdx.x * TPB * ITEMS;
+#pragma unroll
+  for (int k = 0; k < ITEMS; ++k) {
+    const long long i = base + k * TPB + tid;
+    if (i >= n) break;
+    const int r = radii[i];
+    const bool vis = r > 0;
+    const uint32_t key = vis ? __float_as_uint(depths[i]) : 0xFFFFFFFFu;
+    keys[i] = key;
+    vals[i] = (uint32_t)i;
+    if (counts) atomicAdd(&h[key & 0xFFu], 1u);
+    const int c = vis ? num_tiles_hit[i] : 0;
+    uint4 q = {c > 0 ? (uint32_t)c : 0u, 0u, 0u, 0u};
+    if (c > 0) {
+      int x0, x1, y0, y1;
+      tile_bbox(xys[2 * i], xys[2 * i + 1], (float)r, tbx, tby, x0, x1, y0, y1);
+      q.y = (uint32_t)x0 | ((uint32_t)y0 << 16);
+      q.z = (uint32_t)x1 | ((uint32_t)y1 << 16);
+    }
+    rec[i] = q;
+  }
+  if (counts) {
+    __syncthreads();
+    counts[(size_t)tid * nblocks + blockIdx.x] = h[tid];
+  }
 }
 
 // Depth-ordered allotments and boxes: cnt[p], box[p] from the p-th Gaussian's record (the
 // one random gather of the binning); the visible count is the index where the depth-sorted
-// keys reach the culled sentinel.
+// keys reach the culled sentinel.  One workgroup per scan tile (SC_TILE entries): it also
+// writes the tile's allotment sum, the first step of the device scan of cnt.
 __global__ __launch_bounds__(TPB) void gather_counts_kernel(int n, const uint32_t *__restrict__ order,
                                                             const uint32_t *__restrict__ skeys,
                                                             const uint4 *__restrict__ rec,
                                                             uint32_t *__restrict__ cnt,
                                                             uint2 *__restrict__ box,
-                                                            int *__restrict__ num_visible) {
-  int p = blockIdx.x * TPB + threadIdx.x;
-  if (p >= n) return;
-  const uint4 q = rec[order[p]];
-  cnt[p] = q.x;
-  box[p] = make_uint2(q.y, q.z);
-  const bool vis = skeys[p] != 0xFFFFFFFFu;
-  if (vis && (p == n - 1 || skeys[p + 1] == 0xFFFFFFFFu)) *num_visible = p + 1;
+                                                            int *__restrict__ num_visible,
+                                                            uint32_t *__restrict__ partial) {
+  __shared__ uint32_t lds[TPB / 64];
+  const long long base = (long long)blockIdx.x * SC_TILE;
+  uint32_t sum = 0;
+#pragma unroll
+  for (int k = 0; k < SC_ITEMS; ++k) {
+    const long long p = base + k * TPB + threadIdx.x;
+    if (p < n) {
+      const uint4 q = rec[order[p]];
+      cnt[p] = q.x;
+      box[p] = make_uint2(q.y, q.z);
+      sum += q.x;
+      const bool vis = skeys[p] != 0xFFFFFFFFu;
+      if (vis && (p == n - 1 || skeys[p + 1] == 0xFFFFFFFFu)) *num_visible = (int)(p + 1);
+      if (p == 0 && !vis) *num_visible = 0;  // nothing visible
+    }
+  }
+  uint32_t total;
+  block_exclusive_scan<TPB>(sum, total, lds);
+  if (threadIdx.x == 0) partial[blockIdx.x] = total;
 }
 
 // One wave per 64 depth-ordered Gaussians: the wave fills their combined slot range
@@ -624,7 +670,13 @@ __global__ __launch_bounds__(TPB) void emit_kernel(int n, const uint32_t *__rest
                                                    const uint32_t *__restrict__ off,
                                                    const uint2 *__restrict__ box, int tbx,
                                                    int tby, uint32_t *__restrict__ tkeys,
-                                                   uint32_t *__restrict__ tvals) {
+                                                   uint32_t *__restrict__ tvals,
+                                                   int *__restrict__ tile_bins) {
+  // tile_bins starts zeroed for bin_edges_kernel (empty tiles stay (0, 0)): cleared here
+  // instead of by a separate fill launch
+  for (long long i = (long long)blockIdx.x * TPB + threadIdx.x; i < 2LL * tbx * tby;
+       i += (long long)gridDim.x * TPB)
+    tile_bins[i] = 0;
   const int lane = threadIdx.x & 63;
   const long long p0 = ((long long)blockIdx.x * TPB + threadIdx.x) - lane;
   if (p0 >= n) return;  // wave-uniform
@@ -825,17 +877,34 @@ extern "C" int gsplat_bin_count(int num_points, const float *xys, const float *d
     set_error("bin_count: workspace %zu < %zu bytes", workspace1_bytes, p.bytes);
     return 1;
   }
-  note(hipMemsetAsync(d_counts, 0, 2 * sizeof(int32_t), st), "hipMemsetAsync");
-  if (num_points == 0) return check_launch("bin_count");
+  if (num_points == 0) {
+    note(hipMemsetAsync(d_counts, 0, 2 * sizeof(int32_t), st), "hipMemsetAsync");
+    return check_launch("bin_count");
+  }
   const int n = num_points;
-  hipLaunchKernelGGL(depth_keys_kernel, dim3(cdiv(n, TPB)), dim3(TPB), 0, st, n, xys, depths,
-                     radii, num_tiles_hit, tile_bounds_x, tile_bounds_y, p.dkeys_a, p.dvals_a,
-                     p.rec);
+  // depth keys + records; in reduce-then-scan mode also the sort's pass-0 tile counts
+  const SortPlan sp = sort_plan(n, 0, 32);
+  const bool pre = g_sort_rts;
+  uint32_t *c0 = pre ? rts_tile_counts(p.rs_ws) : nullptr;
+#define DEPTH_KEYS(It)                                                                      \
+  hipLaunchKernelGGL(depth_keys_kernel<It>, dim3((unsigned)sp.nblocks), dim3(TPB), 0, st, n, xys, \
+                     depths, radii, num_tiles_hit, tile_bounds_x, tile_bounds_y, p.dkeys_a,    \
+                     p.dvals_a, p.rec, c0, sp.nblocks, sort_err_word(p.rs_ws))
+  if (sp.items == 16) DEPTH_KEYS(16);
+  else if (sp.items == 8) DEPTH_KEYS(8);
+  else DEPTH_KEYS(4);
+#undef DEPTH_KEYS
   radix_sort_pairs<uint32_t>(p.dkeys_a, p.dvals_a, p.dkeys_b, p.dvals_b, p.dkeys_s, p.order, n, 0,
-                             32, p.rs_ws, st);
-  hipLaunchKernelGGL(gather_counts_kernel, dim3(cdiv(n, TPB)), dim3(TPB), 0, st, n, p.order,
-                     p.dkeys_s, p.rec, p.cnt, p.box, d_counts);
-  device_exclusive_scan(p.cnt, p.off, n, (uint32_t *)(d_counts + 1), (uint32_t *)p.rs_ws, st);
+                             32, p.rs_ws, st, pre);
+  // depth-ordered allotments (+ per-tile sums) -> scan -> offsets and I = d_counts[1]
+  const int nb = (int)cdiv(n, SC_TILE);
+  uint32_t *partial = (uint32_t *)p.rs_ws;  // the sort is done with its workspace
+  hipLaunchKernelGGL(gather_counts_kernel, dim3(nb), dim3(TPB), 0, st, n, p.order, p.dkeys_s,
+                     p.rec, p.cnt, p.box, d_counts, partial);
+  hipLaunchKernelGGL(scan_partials_kernel, dim3(1), dim3(1024), 0, st, partial, nb,
+                     (uint32_t *)(d_counts + 1));
+  hipLaunchKernelGGL(scan_downsweep_kernel, dim3(nb), dim3(TPB), 0, st, p.cnt, (long long)n,
+                     partial, p.off);
   return check_launch("bin_count");
 }
 
@@ -859,12 +928,14 @@ extern "C" int gsplat_bin_emit(int num_points, int64_t num_intersects, int tile_
               workspace2_bytes, p1.bytes, p2.bytes);
     return 1;
   }
-  note(hipMemsetAsync(tile_bins, 0, (size_t)T * 2 * sizeof(int32_t), st), "hipMemsetAsync");
-  if (num_intersects == 0 || num_points == 0) return check_launch("bin_emit");
+  if (num_intersects == 0 || num_points == 0) {
+    note(hipMemsetAsync(tile_bins, 0, (size_t)T * 2 * sizeof(int32_t), st), "hipMemsetAsync");
+    return check_launch("bin_emit");
+  }
   const int n = num_points;
   const long long I = num_intersects;
   hipLaunchKernelGGL(emit_kernel, dim3(cdiv(n, TPB)), dim3(TPB), 0, st, n, p1.order, p1.cnt,
-                     p1.off, p1.box, tile_bounds_x, tile_bounds_y, p2.tk_a, p2.tv_a);
+                     p1.off, p1.box, tile_bounds_x, tile_bounds_y, p2.tk_a, p2.tv_a, tile_bins);
   radix_sort_pairs<uint32_t>(p2.tk_a, p2.tv_a, p2.tk_b, p2.tv_b, p2.tk_s,
                              (uint32_t *)gaussian_ids_sorted, I, 0, bits_for(T), p2.rs_ws, st);
   hipLaunchKernelGGL((bin_edges_kernel<uint32_t, 0>), dim3(cdiv(I, TPB)), dim3(TPB), 0, st, I,

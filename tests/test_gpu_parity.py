@@ -146,7 +146,7 @@ def test_binning_fused_bitexact(gpu, case):
 
 
 def test_binning_large_tile_grid_bitexact(gpu):
-    """A 4096x2400 image (38,400 tiles: 16-bit tile keys, three 6-bit sort passes)."""
+    """A 4096x2400 image (38,400 tiles: 16-bit tile keys, two 8-bit sort passes)."""
     case = (3000, 4096, 2400, 5, 0.01, 0.2, 1.5)
     sc, cam, scales, quats = _inputs(*case)
     assert cam.tile_bounds[0] * cam.tile_bounds[1] >= 36 * 1024

@@ -22,7 +22,7 @@ with torch.no_grad():
     for _ in range(5):
         I, gids, bins = bin_gaussians(xys, depths, radii, nth, H, W)
     def nblk(n):
-        items = 16 if n >= (16 << 20) else (8 if n >= (4 << 20) else 4)
+        items = 16 if n >= (4 << 20) else 4
         return (n + 256 * items - 1) // (256 * items)
     nb_d = nblk(N)
     nb_t = nblk(I)
