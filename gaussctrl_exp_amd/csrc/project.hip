@@ -219,7 +219,7 @@ __global__ __launch_bounds__(256) void project_bwd_kernel(
       vmean[1] = P[1] * vpx + P[5] * vpy + P[9] * vpz;
       vmean[2] = P[2] * vpx + P[6] * vpy + P[10] * vpz;
     }
-    float vz = v_depth[i];
+    float vz = v_depth ? v_depth[i] : 0.f;
     vmean[0] += vm[8] * vz;
     vmean[1] += vm[9] * vz;
     vmean[2] += vm[10] * vz;

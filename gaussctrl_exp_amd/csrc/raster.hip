@@ -530,7 +530,7 @@ __global__ __launch_bounds__(256) void raster_bwd3_kernel(
       vr[k] = v_out[3 * pix];
       vg[k] = v_out[3 * pix + 1];
       vb[k] = v_out[3 * pix + 2];
-      va[k] = v_out_alpha[pix];
+      va[k] = v_out_alpha ? v_out_alpha[pix] : 0.f;
     } else {
       Tf[k] = 0.f;
       binf[k] = -1;
@@ -648,7 +648,7 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
       r = v_out[3 * pix];
       g = v_out[3 * pix + 1];
       bl = v_out[3 * pix + 2];
-      a = v_out_alpha[pix];
+      a = v_out_alpha ? v_out_alpha[pix] : 0.f;
     }
     // v_alpha's background/alpha terms: Tf/(1-alpha) * (v_alpha_out - bg . v_out)
     const float qk = Tf * (a - (bg0 * r + bg1 * g + bg2 * bl));
@@ -881,7 +881,7 @@ __global__ __launch_bounds__(256) void raster_bwdn_kernel(
   const float Tf = inside ? final_Ts[pix] : 0.f;
   float T = Tf;
   const int binf = inside ? final_idx[pix] : -1;
-  const float va = inside ? v_out_alpha[pix] : 0.f;
+  const float va = inside && v_out_alpha ? v_out_alpha[pix] : 0.f;
   float vo[CMAX], buf[CMAX];
   float bgdot = 0.f;
 #pragma unroll

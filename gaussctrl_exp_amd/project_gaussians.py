@@ -86,6 +86,9 @@ class _ProjectGaussians(Function):
         ctx.fx, ctx.fy, ctx.cx, ctx.cy = fx, fy, cx, cy
         ctx.save_for_backward(means3d, scales, quats, viewmat, projmat, cov3d, radii, conics)
         ctx.mark_non_differentiable(radii, num_tiles_hit)
+        # Outputs nothing consumed (depths, cov3d in the splatfacto caller) reach backward as
+        # None instead of autograd-materialised zero tensors (one fill kernel each).
+        ctx.set_materialize_grads(False)
         return (xys, depths, radii, conics, num_tiles_hit, cov3d)
 
     @staticmethod
@@ -93,9 +96,12 @@ class _ProjectGaussians(Function):
         means3d, scales, quats, viewmat, projmat, cov3d, radii, conics = ctx.saved_tensors
         n = ctx.num_points
         dev = means3d.device
-        v_xys = _as_f32(v_xys).contiguous()
-        v_depths = _as_f32(v_depths).contiguous()
-        v_conics = _as_f32(v_conics).contiguous()
+        v_xys = _as_f32(v_xys).contiguous() if v_xys is not None else \
+            torch.zeros((n, 2), device=dev, dtype=torch.float32)
+        v_conics = _as_f32(v_conics).contiguous() if v_conics is not None else \
+            torch.zeros((n, 3), device=dev, dtype=torch.float32)
+        if v_depths is not None:  # NULL = zero depth gradient
+            v_depths = _as_f32(v_depths).contiguous()
         v_cov2d = torch.empty((n, 3), device=dev, dtype=torch.float32)
         v_cov3d_out = torch.empty((n, 6), device=dev, dtype=torch.float32)
         v_mean3d = torch.empty((n, 3), device=dev, dtype=torch.float32)

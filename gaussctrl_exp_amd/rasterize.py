@@ -138,6 +138,7 @@ class _RasterizeGaussians(Function):
         ctx.opacity_shape = opacity.shape
         ctx.save_for_backward(gaussian_ids_sorted, tile_bins, xys, conics, colors, opacity,
                               background, final_Ts, final_idx)
+        ctx.set_materialize_grads(False)  # an unused alpha output costs no zero fill
 
         if return_alpha:
             out_alpha = 1 - final_Ts
@@ -151,8 +152,8 @@ class _RasterizeGaussians(Function):
          final_idx) = ctx.saved_tensors
         num_points, C = colors.shape
         dev = xys.device
-        if v_out_alpha is None:
-            v_out_alpha = torch.zeros_like(v_out_img[..., 0])
+        if v_out_img is None:
+            v_out_img = torch.zeros((H, W, C), device=dev, dtype=torch.float32)
 
         if ctx.num_intersects < 1:
             v_xy = torch.zeros_like(xys)
@@ -161,7 +162,8 @@ class _RasterizeGaussians(Function):
             v_opacity = torch.zeros_like(opacity)
         else:
             v_out_img = v_out_img.float().contiguous()
-            v_out_alpha = v_out_alpha.float().contiguous()
+            if v_out_alpha is not None:  # NULL = zero alpha gradient
+                v_out_alpha = v_out_alpha.float().contiguous()
             v_xy = torch.empty((num_points, 2), device=dev, dtype=torch.float32)
             v_conic = torch.empty((num_points, 3), device=dev, dtype=torch.float32)
             v_colors = torch.empty((num_points, C), device=dev, dtype=torch.float32)

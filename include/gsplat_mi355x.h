@@ -56,7 +56,8 @@ int gsplat_project_gaussians_forward(
     float *conics, int32_t *num_tiles_hit, void *stream);
 
 /* Outputs v_cov2d [N,3], v_cov3d [N,6], v_mean3d [N,3], v_scale [N,3], v_quat [N,4] are
- * fully written (zeros where radii <= 0). */
+ * fully written (zeros where radii <= 0).  v_depth may be NULL (an all-zero depth gradient,
+ * which is what the gsplat autograd wrapper passes when nothing consumed depths). */
 int gsplat_project_gaussians_backward(
     int num_points, const float *means3d, const float *scales, float glob_scale,
     const float *quats, const float *viewmat, const float *projmat, float fx, float fy,
@@ -127,7 +128,7 @@ int gsplat_rasterize_forward(int tile_bounds_x, int tile_bounds_y, int img_heigh
                              const float *background, float *out_img, float *final_Ts,
                              int32_t *final_idx, void *stream);
 
-/* v_output [H,W,C], v_output_alpha [H,W]; gradients v_xy [N,2], v_conic [N,3],
+/* v_output [H,W,C], v_output_alpha [H,W] (may be NULL: an all-zero alpha gradient); gradients v_xy [N,2], v_conic [N,3],
  * v_colors [N,C], v_opacity [N] are fully written.  alpha_max is the backward alpha clamp
  * (gsplat 0.1.x uses 0.99f).  workspace holds the per-Gaussian gradient
  * records the kernel accumulates into (gsplat_rasterize_backward_workspace_size bytes;

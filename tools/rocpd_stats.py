@@ -1,5 +1,5 @@
 """Summarise a rocprofv3 rocpd database (--kernel-trace) into the --stats CSV shape:
-name, calls, total_ns, average_ns, percentage.  Usage: rocpd_stats.py run_results.db out.csv"""
+name, calls, total_us, average_us, percentage (rocpd top_kernels reports microseconds).  Usage: rocpd_stats.py run_results.db out.csv"""
 import csv
 import re
 import sqlite3
@@ -10,7 +10,7 @@ rows = db.execute("select name, total_calls, total_duration, average, percentage
                   "from top_kernels").fetchall()
 with open(sys.argv[2], "w", newline="") as f:
     w = csv.writer(f)
-    w.writerow(["Name", "Calls", "TotalDurationNs", "AverageNs", "Percentage"])
+    w.writerow(["Name", "Calls", "TotalDurationUs", "AverageUs", "Percentage"])
     for name, calls, tot, avg, pct in rows:
         short = name.replace("(anonymous namespace)::", "")
         if short.startswith("void gs::") or short.startswith("gs::"):
