@@ -298,8 +298,10 @@ def main():
                 "image": [H, W],
                 "sh_degree": deg,
                 "views_per_gpu_per_step": 1,
-                "parallelism": f"dp{world} (1 view/GPU, RCCL all-reduce of {N * 59 * 4} B "
-                               f"of gradients per step)" if world > 1 else "dp1",
+                "parallelism": f"dp{world} (1 view/GPU; SH-coefficient grads by RCCL all-gather "
+                               f"of {N * 12 + 16} B/rank + multi-view SH backward, other "
+                               f"{N * 11 * 4} B of grads RCCL all-reduced)" if world > 1
+                               else "dp1",
             },
             "train_iters_per_s": round(tsteps / tdt, 2),
             "train_views_per_s": round(world * tsteps / tdt, 2),

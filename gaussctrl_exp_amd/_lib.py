@@ -35,6 +35,7 @@ SIGNATURES = {
         _P, _P, _P, _P, _P, _P]),
     "gsplat_compute_sh_forward": (_I, [_I, _I, _I, _P, _P, _P, _P]),
     "gsplat_compute_sh_backward": (_I, [_I, _I, _I, _P, _P, _P, _P]),
+    "gsplat_compute_sh_backward_views": (_I, [_I, _I, _I, _I, _P, _P, _I64, _P, _P]),
     "gsplat_compute_cov2d_bounds": (_I, [_I, _P, _P, _P, _P]),
     "gsplat_map_gaussian_to_intersects": (_I, [_I, _P, _P, _P, _P, _I, _I, _P, _P, _P]),
     "gsplat_sort_isect_pairs_workspace_size": (_SZ, [_I64]),
@@ -58,7 +59,7 @@ SIGNATURES = {
                                        _P, _P, _P, _F, _P, _P, _P, _P, _P, _SZ, _P]),
 }
 
-ABI_VERSION = 3  # include/gsplat_mi355x.h GSPLAT_MI355X_ABI_VERSION
+ABI_VERSION = 4  # include/gsplat_mi355x.h GSPLAT_MI355X_ABI_VERSION
 
 _lib = None
 

@@ -81,6 +81,33 @@ __device__ __forceinline__ int sh_lds_index(int k) {
   return r * ROWP + (k - r * ROW);
 }
 
+// Writes the block's cnt staged rows (LDS, pitch sh_row_pitch) to dst [cnt * K * 3] with
+// 16-byte coalesced stores when dst is 16-byte aligned.
+template <int K>
+__device__ __forceinline__ void store_rows(const float *smem, int cnt, float *dst) {
+  constexpr int ROW = K * 3;
+  constexpr int ROWP = sh_row_pitch(K);
+  constexpr int SH_THREADS = sh_threads(K);
+  const int total = cnt * ROW;
+  if ((((uintptr_t)dst) & 15) == 0) {
+    const int nv = total >> 2;
+    float4 *d4 = reinterpret_cast<float4 *>(dst);
+    for (int k = threadIdx.x; k < nv; k += SH_THREADS) {
+      float4 v;
+      v.x = smem[sh_lds_index<ROW, ROWP>(4 * k)];
+      v.y = smem[sh_lds_index<ROW, ROWP>(4 * k + 1)];
+      v.z = smem[sh_lds_index<ROW, ROWP>(4 * k + 2)];
+      v.w = smem[sh_lds_index<ROW, ROWP>(4 * k + 3)];
+      d4[k] = v;
+    }
+    for (int k = (nv << 2) + threadIdx.x; k < total; k += SH_THREADS)
+      dst[k] = smem[sh_lds_index<ROW, ROWP>(k)];
+  } else {
+    for (int k = threadIdx.x; k < total; k += SH_THREADS)
+      dst[k] = smem[sh_lds_index<ROW, ROWP>(k)];
+  }
+}
+
 // Coefficient rows are K*3 floats; the block's slab [256*K*3] is copied with 16-byte
 // vector loads when the slab start is 16-byte aligned, else with dword loads.
 template <int K>
@@ -177,25 +204,57 @@ __global__ __launch_bounds__(256) void sh_bwd_kernel(int n, int degrees_to_use,
     }
   }
   __syncthreads();
-  const int total = cnt * ROW;
-  float *dst = v_coeffs + g0 * ROW;
-  if ((((uintptr_t)dst) & 15) == 0) {
-    const int nv = total >> 2;
-    float4 *d4 = reinterpret_cast<float4 *>(dst);
-    for (int k = threadIdx.x; k < nv; k += SH_THREADS) {
-      float4 v;
-      v.x = smem[sh_lds_index<ROW, ROWP>(4 * k)];
-      v.y = smem[sh_lds_index<ROW, ROWP>(4 * k + 1)];
-      v.z = smem[sh_lds_index<ROW, ROWP>(4 * k + 2)];
-      v.w = smem[sh_lds_index<ROW, ROWP>(4 * k + 3)];
-      d4[k] = v;
+  store_rows<K>(smem, cnt, v_coeffs + g0 * ROW);
+}
+
+// Multi-view SH backward for data-parallel training: the coefficient
+// gradient of one view is the rank-1 product Y(dir) (x) v_colors, and the direction is the
+// (replicated) mean minus that view's camera centre, so the ranks exchange only v_colors
+// (12 B per Gaussian) plus their camera centre, and every rank evaluates
+//   v_coeffs[i] = sum_r Y(means[i] - campos_r) (x) v_colors_r[i]
+// itself -- in view order, so every rank produces bit-identical gradients.
+// views[r * view_stride + 3 i + c] = v_colors of view r; views[r * view_stride + 3 n + c] =
+// camera centre of view r.
+template <int K>
+__global__ __launch_bounds__(256) void sh_bwd_views_kernel(int n, int degrees_to_use,
+                                                           int num_views,
+                                                           const float *__restrict__ means,
+                                                           const float *__restrict__ views,
+                                                           long long view_stride,
+                                                           float *__restrict__ v_coeffs) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int ROW = K * 3;
+  constexpr int ROWP = sh_row_pitch(K);
+  constexpr int SH_THREADS = sh_threads(K);
+  const long long g0 = (long long)blockIdx.x * SH_THREADS;
+  const int cnt = (int)min((long long)SH_THREADS, (long long)n - g0);
+  const int t = threadIdx.x;
+  if (t < cnt) {
+    const long long g = g0 + t;
+    const float mx = means[3 * g], my = means[3 * g + 1], mz = means[3 * g + 2];
+    float acc[ROW];
+#pragma unroll
+    for (int k = 0; k < ROW; ++k) acc[k] = 0.f;
+    for (int r = 0; r < num_views; ++r) {
+      const float *view = views + r * view_stride;
+      const float *cam = view + 3LL * n;  // uniform address: scalar loads
+      float b[25];
+      const int nb = sh_basis(degrees_to_use, mx - cam[0], my - cam[1], mz - cam[2], b);
+      const float vc0 = view[3 * g], vc1 = view[3 * g + 1], vc2 = view[3 * g + 2];
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const float bk = k < nb ? b[k] : 0.f;
+        acc[k * 3 + 0] += bk * vc0;
+        acc[k * 3 + 1] += bk * vc1;
+        acc[k * 3 + 2] += bk * vc2;
+      }
     }
-    for (int k = (nv << 2) + threadIdx.x; k < total; k += SH_THREADS)
-      dst[k] = smem[sh_lds_index<ROW, ROWP>(k)];
-  } else {
-    for (int k = threadIdx.x; k < total; k += SH_THREADS)
-      dst[k] = smem[sh_lds_index<ROW, ROWP>(k)];
+    float *row = smem + t * ROWP;
+#pragma unroll
+    for (int k = 0; k < ROW; ++k) row[k] = acc[k];
   }
+  __syncthreads();
+  store_rows<K>(smem, cnt, v_coeffs + g0 * ROW);
 }
 
 }  // namespace
@@ -248,4 +307,25 @@ extern "C" int gsplat_compute_sh_backward(int num_points, int degree, int degree
   hipStream_t st = (hipStream_t)stream;
   SH_DISPATCH(sh_bwd_kernel, num_points, degrees_to_use, viewdirs, v_colors, v_coeffs);
   return check_launch("compute_sh_backward");
+}
+
+extern "C" int gsplat_compute_sh_backward_views(int num_points, int degree, int degrees_to_use,
+                                                int num_views, const float *means3d,
+                                                const float *views, long long view_stride,
+                                                float *v_coeffs, void *stream) {
+  if (num_points < 0 || degree < 0 || degree > 4 || degrees_to_use < 0 ||
+      degrees_to_use > degree || num_views < 1 || view_stride < 3LL * num_points + 3) {
+    set_error("compute_sh_backward_views: bad args (N=%d degree=%d degrees_to_use=%d views=%d "
+              "stride=%lld)", num_points, degree, degrees_to_use, num_views, view_stride);
+    return 1;
+  }
+  if (num_points == 0) return 0;
+  const int K = num_bases(degree);
+  const int thr = sh_threads(K);
+  dim3 grid(cdiv(num_points, thr)), block(thr);
+  size_t smem = (size_t)thr * sh_row_pitch(K) * sizeof(float);
+  hipStream_t st = (hipStream_t)stream;
+  SH_DISPATCH(sh_bwd_views_kernel, num_points, degrees_to_use, num_views, means3d, views,
+              view_stride, v_coeffs);
+  return check_launch("compute_sh_backward_views");
 }

@@ -9,7 +9,7 @@ import torch
 from torch import Tensor
 from torch.autograd import Function
 
-from . import _lib
+from . import _lib, exchange
 
 
 def num_sh_bases(degree: int) -> int:
@@ -62,6 +62,7 @@ class _SphericalHarmonics(Function):
         ctx.degree = degree
         ctx.degrees_to_use = degrees_to_use
         ctx.save_for_backward(viewdirs)
+        ctx.exchange = exchange.active()  # data-parallel SH-gradient exchange, if any
         colors = torch.empty((num_points, 3), device=dev, dtype=torch.float32)
         _lib.call("gsplat_compute_sh_forward", num_points, degree, int(degrees_to_use),
                   _lib.ptr(viewdirs), _lib.ptr(coeffs), _lib.ptr(colors), _lib.stream(dev))
@@ -74,7 +75,26 @@ class _SphericalHarmonics(Function):
         K = num_sh_bases(ctx.degree)
         dev = viewdirs.device
         v_colors = v_colors.float().contiguous()
+        if ctx.exchange is not None:
+            degree, dtu = ctx.degree, int(ctx.degrees_to_use)
+            return None, None, ctx.exchange.reduce(
+                v_colors, lambda means, views: sh_backward_views(degree, dtu, means, views))
         v_coeffs = torch.empty((num_points, K, 3), device=dev, dtype=torch.float32)
         _lib.call("gsplat_compute_sh_backward", num_points, ctx.degree, int(ctx.degrees_to_use),
                   _lib.ptr(viewdirs), _lib.ptr(v_colors), _lib.ptr(v_coeffs), _lib.stream(dev))
         return None, None, v_coeffs
+
+
+def sh_backward_views(degree: int, degrees_to_use: int, means: Tensor, views: Tensor) -> Tensor:
+    """sum_r Y(means - campos_r) (x) v_colors_r over the gathered view records
+    views [R, >= 3N + 3] = [v_colors_r (3N) | campos_r (3) | ...]  (exchange.ShViewExchange)."""
+    n = means.shape[0]
+    means = means.float().contiguous()
+    views = views.float().contiguous()
+    dev = _lib.check_device("sh_backward_views", means, views)
+    K = num_sh_bases(degree)
+    v_coeffs = torch.empty((n, K, 3), device=dev, dtype=torch.float32)
+    _lib.call("gsplat_compute_sh_backward_views", n, degree, int(degrees_to_use), views.shape[0],
+              _lib.ptr(means), _lib.ptr(views), views.shape[1], _lib.ptr(v_coeffs),
+              _lib.stream(dev))
+    return v_coeffs

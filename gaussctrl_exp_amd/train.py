@@ -6,8 +6,12 @@ render (gc_model.get_outputs) -> splatfacto loss 0.8*L1 + 0.2*(1-SSIM) -> backwa
 Adam over the six Gaussian parameter groups (gc_config.py:58-87).  Here each rank renders
 its own camera of a multi-view batch against a replica of the parameters; the per-view
 losses sum, so the gradients ([N x 59] fp32, 236 B/Gaussian) are summed across ranks over
-RCCL/xGMI -- one async all-reduce per parameter tensor, issued as soon as autograd
-finishes it (GradAllReduce) -- after which every rank takes the identical Adam step.
+RCCL/xGMI, after which every rank takes the identical Adam step.  GradExchange does the
+summing: the 192 B/Gaussian SH-coefficient gradient through exchange.ShViewExchange
+(all-gather of each view's 12 B/Gaussian colour gradient + camera centre, summed by one HIP
+kernel on every rank), the other 44 B/Gaussian by one async all-reduce per parameter
+tensor, issued as soon as autograd finishes it.  grad_exchange="allreduce" all-reduces
+every tensor instead.
 """
 from __future__ import annotations
 
@@ -19,6 +23,7 @@ import torch.distributed as dist
 import torch.nn.functional as F
 
 from .camera import GCCamera
+from .exchange import ShViewExchange
 from .scene import PARAM_NAMES, GaussianScene, render
 
 # gc_config.py:58-87 (Adam, eps 1e-15); xyz decays 1.6e-4 -> 1.6e-6 over 30k steps.
@@ -61,22 +66,27 @@ def splatfacto_loss(pred, gt):
     return (1 - SSIM_LAMBDA) * l1 + SSIM_LAMBDA * sim
 
 
-class GradAllReduce:
+class GradExchange:
     """Sums every parameter's gradient over the data-parallel ranks (RCCL over xGMI).
 
     One async all-reduce per parameter, launched from a post-accumulate-grad hook the moment
-    autograd has produced that gradient: the SH-feature gradients (81 % of the 236 B per
-    Gaussian) are issued right after the SH backward and overlap the projection backward.
-    Gradients stay the tensors autograd produced (no flat bucket to zero-fill and accumulate
-    into, no pack/unpack copies); hooks fire in the same order on every rank because every
-    rank runs the same graph."""
+    autograd has produced that gradient (gradients stay the tensors autograd produced: no
+    flat bucket to zero-fill and accumulate into, no pack/unpack copies; hooks fire in the
+    same order on every rank because every rank runs the same graph).  With an
+    ShViewExchange (`sh`), the SH-coefficient parameters (`sh_params`) are skipped in any
+    step whose SH backward already produced the all-rank sum through the exchange."""
 
-    def __init__(self, params: List[torch.Tensor], group=None):
+    def __init__(self, params: List[torch.Tensor], group=None,
+                 sh: Optional[ShViewExchange] = None, sh_params=()):
         self.group = group
+        self.sh = sh
+        self.sh_ids = {id(p) for p in sh_params}
         self.works = []
         self.handles = [p.register_post_accumulate_grad_hook(self._hook) for p in params]
 
     def _hook(self, p: torch.Tensor):
+        if self.sh is not None and self.sh.handled and id(p) in self.sh_ids:
+            return  # already summed over the ranks by the SH view exchange
         self.works.append(dist.all_reduce(p.grad, op=dist.ReduceOp.SUM, group=self.group,
                                           async_op=True))
 
@@ -84,17 +94,26 @@ class GradAllReduce:
         for w in self.works:
             w.wait()
         self.works.clear()
+        if self.sh is not None:
+            self.sh.reset()
 
 
 class TrainStep:
     """render -> loss -> backward -> [all-reduce] -> Adam, on this rank's camera."""
 
     def __init__(self, scene: GaussianScene, sh_degree: int = 3, world_size: int = 1,
-                 loss: str = "splatfacto", group=None, api=None):
+                 loss: str = "splatfacto", group=None, api=None,
+                 grad_exchange: str = "sh_views"):
         self.scene = scene.requires_grad_()
         self.params = scene.params()
         self.world_size = world_size
-        self.grad_sync = GradAllReduce(self.params, group) if world_size > 1 else None
+        if grad_exchange not in ("sh_views", "allreduce"):
+            raise ValueError(f"grad_exchange must be 'sh_views' or 'allreduce', not {grad_exchange}")
+        self.sh_exchange = ShViewExchange(group) if world_size > 1 and \
+            grad_exchange == "sh_views" else None
+        self.grad_sync = GradExchange(
+            self.params, group, sh=self.sh_exchange,
+            sh_params=(scene.features_dc, scene.features_rest)) if world_size > 1 else None
         self.group = group
         self.sh_degree = sh_degree
         self.loss_kind = loss
@@ -123,6 +142,8 @@ class TrainStep:
     def zero_grad(self):
         for p in self.params:
             p.grad = None
+        if self.sh_exchange is not None:
+            self.sh_exchange.reset()
 
     def sync_grads(self):
         """Wait for this step's gradient all-reduces (no-op on one rank)."""
@@ -133,7 +154,11 @@ class TrainStep:
         return torch.cat([p.grad.reshape(-1) for p in self.params])
 
     def forward_backward(self, cam: GCCamera, gt: torch.Tensor, background: torch.Tensor):
-        out = render(self.scene, cam, self.sh_degree, background, api=self.api)
+        if self.sh_exchange is not None:
+            with self.sh_exchange.view(self.scene.means, cam.c2w[..., :3, 3]):
+                out = render(self.scene, cam, self.sh_degree, background, api=self.api)
+        else:
+            out = render(self.scene, cam, self.sh_degree, background, api=self.api)
         loss = self.loss(out["rgb"], gt)
         loss.backward()
         return loss, out

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define GSPLAT_MI355X_ABI_VERSION 3
+#define GSPLAT_MI355X_ABI_VERSION 4
 
 int gsplat_abi_version(void);
 const char *gsplat_last_error(void);
@@ -74,6 +74,16 @@ int gsplat_compute_sh_forward(int num_points, int degree, int degrees_to_use,
 int gsplat_compute_sh_backward(int num_points, int degree, int degrees_to_use,
                                const float *viewdirs, const float *v_colors, float *v_coeffs,
                                void *stream);
+
+/* Data-parallel extension (no gsplat counterpart): the sum over num_views
+ * cameras of the SH coefficient gradient, v_coeffs[i] = sum_r Y(means3d[i] - campos_r) (x)
+ * v_colors_r[i], summed in view order (bit-identical on every rank).  views holds one
+ * record per view, view_stride (>= 3 N + 3) floats apart: v_colors_r [N,3] followed by
+ * campos_r [3] -- exactly what an all-gather of each rank's [v_colors | campos] produces.
+ * v_coeffs [N, num_sh_bases(degree), 3] fully written. */
+int gsplat_compute_sh_backward_views(int num_points, int degree, int degrees_to_use,
+                                     int num_views, const float *means3d, const float *views,
+                                     long long view_stride, float *v_coeffs, void *stream);
 
 /* covs2d [N,3] -> conics [N,3], radii [N] (float).  det == 0 rows get zeros. */
 int gsplat_compute_cov2d_bounds(int num_points, const float *covs2d, float *conics,

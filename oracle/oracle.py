@@ -119,6 +119,21 @@ def sh_backward(degrees_to_use, viewdirs, v_colors, K):
     return out
 
 
+def sh_backward_views(degrees_to_use, means, views, K):
+    """Multi-view SH backward (data-parallel exchange, include/gsplat_mi355x.h
+    gsplat_compute_sh_backward_views): sum over view records r, in order, of
+    sh_backward(means - campos_r, v_colors_r); views [R, >= 3N + 3] = [v_colors_r | campos_r]."""
+    means = _f(means)
+    views = np.asarray(views, np.float32)
+    n = means.shape[0]
+    out = np.zeros((n, K, 3), np.float32)
+    for r in range(views.shape[0]):
+        campos = views[r, 3 * n:3 * n + 3]
+        out += sh_backward(degrees_to_use, means - campos[None, :],
+                           views[r, :3 * n].reshape(n, 3), K)
+    return out
+
+
 def cov2d_bounds(cov2d):
     cov2d = _f(cov2d)
     n = cov2d.shape[0]

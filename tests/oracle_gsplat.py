@@ -15,6 +15,8 @@ import torch
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "oracle"))
 import oracle as O  # noqa: E402
 
+from gaussctrl_exp_amd import exchange  # noqa: E402
+
 BACKWARD_ALPHA_CLAMP = 0.99
 
 
@@ -53,12 +55,17 @@ class _SH(torch.autograd.Function):
     @staticmethod
     def forward(ctx, deg, viewdirs, coeffs):
         ctx.deg, ctx.K = deg, coeffs.shape[1]
+        ctx.exchange = exchange.active()
         ctx.save_for_backward(viewdirs)
         return torch.from_numpy(O.sh_forward(deg, _np(viewdirs), _np(coeffs)))
 
     @staticmethod
     def backward(ctx, v):
         (viewdirs,) = ctx.saved_tensors
+        if ctx.exchange is not None:  # data-parallel SH-gradient exchange (gloo tests)
+            deg, K = ctx.deg, ctx.K
+            return None, None, ctx.exchange.reduce(v.contiguous(), lambda means, views: (
+                torch.from_numpy(O.sh_backward_views(deg, _np(means), _np(views), K))))
         return None, None, torch.from_numpy(O.sh_backward(ctx.deg, _np(viewdirs), _np(v), ctx.K))
 
 

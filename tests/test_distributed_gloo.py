@@ -1,11 +1,15 @@
 """World-size-2 data-parallel train step on CPU (gloo): each rank renders its own camera
-(oracle-backed gsplat emulation), gradients are all-reduced per parameter as autograd finishes them;
-the result must equal the sum of the two single-view gradients (SURVEY.md §8e parity
-check), and after the identical Adam step both ranks hold identical parameters."""
+(oracle-backed gsplat emulation) and the gradients are summed over the ranks -- either every
+tensor all-reduced as autograd finishes it ("allreduce"), or the SH-coefficient gradient
+through the view exchange (all-gather of v_colors + camera centre, exchange.ShViewExchange)
+and the rest all-reduced ("sh_views").  Either way the result must equal the sum of the two
+single-view gradients (SURVEY.md §8e parity check), be identical on both ranks, and give
+identical parameters after the Adam step."""
 import os
 import socket
 
 import numpy as np
+import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -33,7 +37,7 @@ def _scene():
     return synthetic_scene(400, 3, seed=3, scale_lo=0.02, scale_hi=0.08, extent=1.0)
 
 
-def _worker(rank, world, port, out_dir):
+def _worker(rank, world, port, out_dir, mode):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from oracle_gsplat import API
@@ -41,7 +45,8 @@ def _worker(rank, world, port, out_dir):
     torch.manual_seed(0)
     cam = _views()[rank]
     gt = torch.rand(48, 64, 3, generator=torch.Generator().manual_seed(rank))
-    t = TrainStep(_scene(), sh_degree=3, world_size=world, loss="l1", api=API)
+    t = TrainStep(_scene(), sh_degree=3, world_size=world, loss="l1", api=API,
+                  grad_exchange=mode)
     t.step(cam, gt, background=torch.tensor([0.5, 0.5, 0.5]), optimizer=False)
     np.save(os.path.join(out_dir, f"grad{rank}.npy"), t.flat_grad().numpy())
     t.opt.step()
@@ -49,11 +54,12 @@ def _worker(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
-def test_two_rank_allreduce_equals_sum_of_views(tmp_path):
+@pytest.mark.parametrize("mode", ["allreduce", "sh_views"])
+def test_two_rank_gradients_equal_sum_of_views(tmp_path, mode):
     from oracle_gsplat import API
     from gaussctrl_exp_amd.train import TrainStep
     port = _free_port()
-    mp.spawn(_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    mp.spawn(_worker, args=(2, port, str(tmp_path), mode), nprocs=2, join=True)
     g0, g1 = np.load(tmp_path / "grad0.npy"), np.load(tmp_path / "grad1.npy")
     np.testing.assert_array_equal(g0, g1)  # every rank holds the same reduced gradients
     ref = 0
