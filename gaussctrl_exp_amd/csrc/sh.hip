@@ -235,18 +235,31 @@ __global__ __launch_bounds__(256) void sh_bwd_views_kernel(int n, int degrees_to
     float acc[ROW];
 #pragma unroll
     for (int k = 0; k < ROW; ++k) acc[k] = 0.f;
+    // software-pipelined over views: view r+1's colour gradient and camera centre are in
+    // flight while view r's basis and outer product are computed
+    const float *cam = views + 3LL * n;  // uniform addresses: scalar loads
+    float c0 = cam[0], c1 = cam[1], c2 = cam[2];
+    float vc0 = views[3 * g], vc1 = views[3 * g + 1], vc2 = views[3 * g + 2];
     for (int r = 0; r < num_views; ++r) {
-      const float *view = views + r * view_stride;
-      const float *cam = view + 3LL * n;  // uniform address: scalar loads
+      const float dx = mx - c0, dy = my - c1, dz = mz - c2;
+      const float u0 = vc0, u1 = vc1, u2 = vc2;
+      if (r + 1 < num_views) {
+        const float *view = views + (r + 1) * view_stride;
+        c0 = view[3LL * n];
+        c1 = view[3LL * n + 1];
+        c2 = view[3LL * n + 2];
+        vc0 = view[3 * g];
+        vc1 = view[3 * g + 1];
+        vc2 = view[3 * g + 2];
+      }
       float b[25];
-      const int nb = sh_basis(degrees_to_use, mx - cam[0], my - cam[1], mz - cam[2], b);
-      const float vc0 = view[3 * g], vc1 = view[3 * g + 1], vc2 = view[3 * g + 2];
+      const int nb = sh_basis(degrees_to_use, dx, dy, dz, b);
 #pragma unroll
       for (int k = 0; k < K; ++k) {
         const float bk = k < nb ? b[k] : 0.f;
-        acc[k * 3 + 0] += bk * vc0;
-        acc[k * 3 + 1] += bk * vc1;
-        acc[k * 3 + 2] += bk * vc2;
+        acc[k * 3 + 0] += bk * u0;
+        acc[k * 3 + 1] += bk * u1;
+        acc[k * 3 + 2] += bk * u2;
       }
     }
     float *row = smem + t * ROWP;
