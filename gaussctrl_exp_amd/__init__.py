@@ -13,7 +13,7 @@ Layout:
 `import gsplat` (the top-level shim package) resolves to this implementation.
 """
 from .project_gaussians import project_gaussians
-from .rasterize import rasterize_gaussians
+from .rasterize import rasterize_gaussians, rasterize_gaussians_rgbd
 from .sh import num_sh_bases, spherical_harmonics
 from .utils import (bin_and_sort_gaussians, compute_cov2d_bounds,
                     compute_cumulative_intersects, get_tile_bin_edges,
@@ -24,6 +24,7 @@ __version__ = "0.1.2.1+mi355x"
 __all__ = [
     "project_gaussians",
     "rasterize_gaussians",
+    "rasterize_gaussians_rgbd",
     "spherical_harmonics",
     "num_sh_bases",
     "map_gaussian_to_intersects",

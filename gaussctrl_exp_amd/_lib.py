@@ -47,6 +47,7 @@ SIGNATURES = {
     "gsplat_bin_emit": (_I, [_I, _I64, _I, _I, _P, _P, _P, _SZ, _P, _SZ, _P]),
     "gsplat_rasterize_forward": (_I, [_I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                                       _P, _P]),
+    "gsplat_rasterize_forward_rgbd": (_I, [_I, _I, _I, _I] + [_P] * 13),
     "gsplat_rasterize_backward_workspace_size": (_SZ, [_I, _I]),
     "gsplat_debug_set_raster_variant": (_I, [_I, _I, _I]),
     "gsplat_debug_sort_timing": (_I, [_P, _I]),

@@ -48,7 +48,7 @@ struct __attribute__((aligned(16))) GStage {
   float bl;
   int idx;  // position in the tile's sorted list
   int id;   // Gaussian id
-  float pad;
+  float d;  // depth (fused RGB+depth forward only)
 };
 
 typedef float f2 __attribute__((ext_vector_type(2)));
@@ -284,13 +284,19 @@ __global__ __launch_bounds__(256) void raster_fwd3_kernel(
 // sigma / exp / alpha are independent and evaluated together; only the transmittance
 // update is applied in list order, so every pixel sees exactly the scalar kernel's
 // sequence of operations.
-template <int PXL, int COLS>
+//
+// DEPTH (fused RGB+depth eval render): each staged Gaussian also carries its
+// depth, accumulated with the same weight as the colour channels into out_depth -- exactly
+// channel 0 of a second render with colours = depth and a zero background (gc_model.py:
+// 225-238), without the second binning and traversal.
+template <int PXL, int COLS, bool DEPTH = false>
 __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
     int tbx, int tby, int H, int W, const int *__restrict__ gids, const int2 *__restrict__ bins,
     const float2 *__restrict__ xys, const float *__restrict__ conics,
     const float *__restrict__ colors, const float *__restrict__ opacity,
     const float *__restrict__ background, float *__restrict__ out_img,
-    float *__restrict__ final_Ts, int *__restrict__ final_idx) {
+    float *__restrict__ final_Ts, int *__restrict__ final_idx,
+    const float *__restrict__ depths = nullptr, float *__restrict__ out_depth = nullptr) {
   const WaveRect R = wave_rect<PXL, COLS>(tbx, tby, H, W);
   if (!R.live) return;  // wave-uniform
   __shared__ GStage lds[4][64];
@@ -299,7 +305,7 @@ __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
   const float px = (float)j;
   const float rx0 = R.rx0, rx1 = R.rx1, ry0 = R.ry0, ry1 = R.ry1;
   constexpr int LROWS = 64 / COLS;
-  float py[PXL], T[PXL], cr[PXL], cg[PXL], cb[PXL];
+  float py[PXL], T[PXL], cr[PXL], cg[PXL], cb[PXL], cd[PXL];
   int cur[PXL];
   bool done[PXL];
 #pragma unroll
@@ -307,7 +313,7 @@ __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
     const int i = i0 + LROWS * k;
     py[k] = (float)i;
     T[k] = 1.f;
-    cr[k] = cg[k] = cb[k] = 0.f;
+    cr[k] = cg[k] = cb[k] = cd[k] = 0.f;
     cur[k] = 0;
     done[k] = !(i < H && j < W);
   }
@@ -323,6 +329,7 @@ __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
     const bool keep = idx < range.y &&
                       stage_gaussian(idx, gids, xys, conics, colors, opacity, rx0, rx1, ry0,
                                      ry1, s);
+    if (DEPTH && keep) s.d = depths[s.id];
     const unsigned long long kmask = __ballot(keep);
     if (keep) stage[lanes_below(kmask)] = s;
     const int n = __popcll(kmask);
@@ -332,7 +339,7 @@ __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
       G[0] = stage[t];
       G[1] = stage[min(t + 1, 63)];
       const bool live1 = t + 1 < n;
-      if (!live1) G[1].r = G[1].g = G[1].bl = 0.f;  // stale slot: keep 0 * colour finite
+      if (!live1) G[1].r = G[1].g = G[1].bl = G[1].d = 0.f;  // stale slot: keep 0 * x finite
       float sg[2][PXL], al[2][PXL];
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
@@ -358,6 +365,7 @@ __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
           cr[k] += G[u].r * w;
           cg[k] += G[u].g * w;
           cb[k] += G[u].bl * w;
+          if (DEPTH) cd[k] += G[u].d * w;
           T[k] = comp ? nT : T[k];
           cur[k] = comp ? G[u].idx : cur[k];
         }
@@ -378,6 +386,7 @@ __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
       out_img[3 * pix] = cr[k] + T[k] * bg0;
       out_img[3 * pix + 1] = cg[k] + T[k] * bg1;
       out_img[3 * pix + 2] = cb[k] + T[k] * bg2;
+      if (DEPTH) out_depth[pix] = cd[k] + T[k] * 0.f;  // the depth render's zero background
     }
   }
 }
@@ -1048,6 +1057,32 @@ extern "C" int gsplat_rasterize_forward(int tile_bounds_x, int tile_bounds_y, in
                 conics, colors, opacity, background, out_img, final_Ts, final_idx);
   }
   return check_launch("rasterize_forward");
+}
+
+extern "C" int gsplat_rasterize_forward_rgbd(int tile_bounds_x, int tile_bounds_y,
+                                             int img_height, int img_width,
+                                             const int32_t *gaussian_ids_sorted,
+                                             const int32_t *tile_bins, const float *xys,
+                                             const float *conics, const float *colors,
+                                             const float *depths, const float *opacity,
+                                             const float *background, float *out_img,
+                                             float *out_depth, float *final_Ts,
+                                             int32_t *final_idx, void *stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (tile_bounds_x <= 0 || tile_bounds_y <= 0 || img_height <= 0 || img_width <= 0 ||
+      (long long)tile_bounds_x * GS_BLOCK < img_width ||
+      (long long)tile_bounds_y * GS_BLOCK < img_height || !depths || !out_depth) {
+    set_error("rasterize_forward_rgbd: bad sizes or NULL depth buffers (tiles=%dx%d H=%d W=%d)",
+              tile_bounds_x, tile_bounds_y, img_height, img_width);
+    return 1;
+  }
+  const int T = tile_bounds_x * tile_bounds_y;
+  hipLaunchKernelGGL((raster_fwd3u_kernel<1, 8, true>), dim3(cdiv(T, (tiles_per_block<1, 8>()))),
+                     dim3(256), 0, st, tile_bounds_x, tile_bounds_y, img_height, img_width,
+                     gaussian_ids_sorted, (const int2 *)tile_bins, (const float2 *)xys, conics,
+                     colors, opacity, background, out_img, final_Ts, final_idx, depths,
+                     out_depth);
+  return check_launch("rasterize_forward_rgbd");
 }
 
 extern "C" int gsplat_debug_set_raster_variant(int fwd_pxl, int bwd_pxl, int bwd_flags) {

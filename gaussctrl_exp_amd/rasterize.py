@@ -5,9 +5,16 @@ return_alpha=True, random background during training) and :225-236 (depth, eval)
 binning (cumsum -> intersect map -> sort -> tile bins) runs fused on the GPU
 (csrc/binning.hip) with one host read of the intersection count, exactly where gsplat
 reads `cum_tiles_hit[-1].item()`; blending runs in csrc/raster.hip.
+
+The eval render calls rasterize_gaussians twice on the same projected Gaussians (RGB, then
+depth as colours).  The binning depends only on (xys, depths, radii, num_tiles_hit, H, W),
+so the second call reuses the first call's binning (`_BinCache`) when those are the very
+same live tensors, unmodified, on the same stream.  `rasterize_gaussians_rgbd` goes further:
+RGB, depth and alpha from one binning and one traversal.
 """
 from __future__ import annotations
 
+import weakref
 from typing import Optional
 
 import torch
@@ -95,6 +102,100 @@ def bin_gaussians(xys: Tensor, depths: Tensor, radii: Tensor, num_tiles_hit: Ten
     return num_intersects, gaussian_ids_sorted, tile_bins
 
 
+class _BinCache:
+    """The last rasterize call's binning, reused while its inputs are the same tensor
+    objects (weak references: a freed tensor whose address is recycled never matches),
+    at the same version counter (an in-place edit invalidates), size and stream."""
+
+    def __init__(self):
+        self.refs = None
+        self.key = None
+        self.value = None
+        self.hits = 0
+
+    @staticmethod
+    def _key(tensors, H, W, stream):
+        return (tuple((t._version, tuple(t.shape), t.dtype) for t in tensors), H, W,
+                stream.value)
+
+    def get(self, tensors, H, W, stream):
+        if self.refs is None or len(self.refs) != len(tensors):
+            return None
+        if any(r() is not t for r, t in zip(self.refs, tensors)):
+            return None
+        if self.key != self._key(tensors, H, W, stream):
+            return None
+        self.hits += 1
+        return self.value
+
+    def put(self, tensors, H, W, stream, value):
+        self.refs = [weakref.ref(t) for t in tensors]
+        self.key = self._key(tensors, H, W, stream)
+        self.value = value
+
+    def clear(self):
+        self.refs = self.key = self.value = None
+
+
+_BIN_CACHE = _BinCache()
+
+
+def _binning(xys, depths, radii, num_tiles_hit, H, W):
+    """bin_gaussians through the one-entry cache (see module docstring)."""
+    key_tensors = (xys, depths, radii, num_tiles_hit)
+    st = _lib.stream(xys.device)
+    hit = _BIN_CACHE.get(key_tensors, H, W, st)
+    if hit is not None:
+        return hit
+    res = bin_gaussians(xys, depths, radii, num_tiles_hit, H, W)
+    _BIN_CACHE.put(key_tensors, H, W, st, res)
+    return res
+
+
+def rasterize_gaussians_rgbd(xys: Tensor, depths: Tensor, radii: Tensor, conics: Tensor,
+                             num_tiles_hit: Tensor, colors: Tensor, opacity: Tensor,
+                             img_height: int, img_width: int,
+                             background: Optional[Tensor] = None):
+    """Fused eval render: (rgb [H,W,3], depth [H,W,1], alpha [H,W]) from one
+    binning and one traversal.  rgb and alpha equal rasterize_gaussians(..., return_alpha=True);
+    depth equals channel 0 of rasterize_gaussians(..., colors=depths[:, None].repeat(1, 3),
+    background=zeros(3)) -- gc_model.py:225-236's second call -- before the caller's division
+    by alpha.  Forward only (no autograd): the eval path runs without gradients."""
+    H, W = int(img_height), int(img_width)
+    if colors.dim() != 2 or colors.shape[-1] != 3:
+        raise ValueError("rasterize_gaussians_rgbd: colors must be [N, 3]")
+    num_points = xys.size(0)
+    tbx = (W + BLOCK_X - 1) // BLOCK_X
+    tby = (H + BLOCK_Y - 1) // BLOCK_Y
+    with torch.no_grad():
+        xys, conics = xys.float().contiguous(), conics.float().contiguous()
+        colors, opacity = colors.float().contiguous(), opacity.float().contiguous()
+        depths_f = depths.float().contiguous()
+        if background is None:
+            background = torch.ones(3, dtype=torch.float32, device=colors.device)
+        background = background.float().contiguous()
+        dev = _lib.check_device("rasterize_gaussians_rgbd", xys, depths_f, radii, conics,
+                                num_tiles_hit, colors, opacity, background)
+        if opacity.numel() != num_points or conics.shape != (num_points, 3) or \
+                colors.shape[0] != num_points or depths_f.numel() != num_points:
+            raise ValueError("rasterize_gaussians_rgbd: inconsistent per-Gaussian tensor shapes")
+        num_intersects, gaussian_ids_sorted, tile_bins = _binning(xys, depths, radii,
+                                                                  num_tiles_hit, H, W)
+        if num_intersects < 1:
+            return (torch.ones(H, W, 3, device=dev) * background,
+                    torch.zeros(H, W, 1, device=dev), torch.ones(H, W, device=dev))
+        out_img = torch.empty((H, W, 3), device=dev, dtype=torch.float32)
+        out_depth = torch.empty((H, W, 1), device=dev, dtype=torch.float32)
+        final_Ts = torch.empty((H, W), device=dev, dtype=torch.float32)
+        final_idx = torch.empty((H, W), device=dev, dtype=torch.int32)
+        P = _lib.ptr
+        _lib.call("gsplat_rasterize_forward_rgbd", tbx, tby, H, W, P(gaussian_ids_sorted),
+                  P(tile_bins), P(xys), P(conics), P(colors), P(depths_f), P(opacity),
+                  P(background), P(out_img), P(out_depth), P(final_Ts), P(final_idx),
+                  _lib.stream(dev))
+        return out_img, out_depth, 1 - final_Ts
+
+
 class _RasterizeGaussians(Function):
     """Rasterizes 2D gaussians (autograd wrapper of the C-ABI binning/raster kernels)."""
 
@@ -115,7 +216,7 @@ class _RasterizeGaussians(Function):
                 colors.shape[0] != num_points:
             raise ValueError("rasterize_gaussians: inconsistent per-Gaussian tensor shapes")
 
-        num_intersects, gaussian_ids_sorted, tile_bins = bin_gaussians(
+        num_intersects, gaussian_ids_sorted, tile_bins = _binning(
             xys, depths, radii, num_tiles_hit, H, W)
 
         if num_intersects < 1:

@@ -17,7 +17,7 @@ import torch
 
 from .camera import GCCamera
 from .project_gaussians import project_gaussians
-from .rasterize import rasterize_gaussians
+from .rasterize import rasterize_gaussians, rasterize_gaussians_rgbd
 from .sh import num_sh_bases, spherical_harmonics
 
 PARAM_NAMES = ("means", "scales", "quats", "opacities", "features_dc", "features_rest")
@@ -118,11 +118,13 @@ def scene_from_points(xyz: torch.Tensor, rgb: Optional[torch.Tensor], n: int,
 
 
 def render(scene: GaussianScene, cam: GCCamera, sh_degree_to_use: int, background: torch.Tensor,
-           return_depth: bool = False, api=None):
+           return_depth: bool = False, api=None, fused_depth: bool = False):
     """GaussCtrlModel.get_outputs' hot path (gc_model.py:158-238) on a GCCamera.
 
     `api` swaps the gsplat implementation (tests pass the CPU-oracle emulation); by default
-    the MI355X kernels are used.  Returns dict(rgb [H,W,3], accumulation [H,W,1],
+    the MI355X kernels are used.  With return_depth, the depth image comes from a second
+    rasterize call as in gc_model.py:225-236, or -- fused_depth=True, MI355X kernels, no
+    autograd -- from the single fused RGB+depth pass (rasterize_gaussians_rgbd).  Returns dict(rgb [H,W,3], accumulation [H,W,1],
     depth [H,W,1] or None, xys, radii)."""
     project = api.project_gaussians if api is not None else project_gaussians
     sh_eval = api.spherical_harmonics if api is not None else spherical_harmonics
@@ -144,6 +146,17 @@ def render(scene: GaussianScene, cam: GCCamera, sh_degree_to_use: int, backgroun
         rgbs = torch.clamp(rgbs + 0.5, min=0.0)
     else:
         rgbs = torch.sigmoid(colors_crop[:, 0, :])
+    if return_depth and fused_depth:
+        if api is not None:
+            raise ValueError("fused_depth renders with the MI355X kernels only")
+        rgb, depth_im, alpha = rasterize_gaussians_rgbd(
+            xys, depths, radii, conics, num_tiles_hit, rgbs, torch.sigmoid(scene.opacities),
+            cam.height, cam.width, background=background)
+        alpha = alpha[..., None]
+        rgb = torch.clamp(rgb, max=1.0)
+        depth_im[alpha > 0] = depth_im[alpha > 0] / alpha[alpha > 0]
+        depth_im[alpha == 0] = 1000
+        return {"rgb": rgb, "depth": depth_im, "accumulation": alpha, "xys": xys, "radii": radii}
     rgb, alpha = raster(xys, depths, radii, conics, num_tiles_hit, rgbs,
                                      torch.sigmoid(scene.opacities), cam.height, cam.width,
                                      background=background, return_alpha=True)

@@ -138,6 +138,18 @@ int gsplat_rasterize_forward(int tile_bounds_x, int tile_bounds_y, int img_heigh
                              const float *background, float *out_img, float *final_Ts,
                              int32_t *final_idx, void *stream);
 
+/* Fused RGB+depth eval forward (no gsplat counterpart): out_img [H,W,3],
+ * final_Ts, final_idx exactly as gsplat_rasterize_forward with C = 3, plus out_depth [H,W] =
+ * sum of depth * alpha * T -- channel 0 of a second forward with colours = depths and a zero
+ * background (gc_model.py:225-236), from the same binning and traversal.  depths [N]. */
+int gsplat_rasterize_forward_rgbd(int tile_bounds_x, int tile_bounds_y, int img_height,
+                                  int img_width, const int32_t *gaussian_ids_sorted,
+                                  const int32_t *tile_bins, const float *xys,
+                                  const float *conics, const float *colors,
+                                  const float *depths, const float *opacity,
+                                  const float *background, float *out_img, float *out_depth,
+                                  float *final_Ts, int32_t *final_idx, void *stream);
+
 /* v_output [H,W,C], v_output_alpha [H,W] (may be NULL: an all-zero alpha gradient); gradients v_xy [N,2], v_conic [N,3],
  * v_colors [N,C], v_opacity [N] are fully written.  alpha_max is the backward alpha clamp
  * (gsplat 0.1.x uses 0.99f).  workspace holds the per-Gaussian gradient
