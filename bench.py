@@ -11,7 +11,7 @@ full train step (splatfacto 0.8 L1 + 0.2 SSIM loss + Adam) is timed separately a
 reported as `train_iters_per_s`.  Inputs are synthetic (SURVEY.md §8d scene: random
 Gaussians in [-1.5,1.5]^3 seen from (0,0,4), fov 50 deg) and resident in HBM before timing.
 
-Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--config headline|c2|c3|c5]
+Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--config headline|c2|c3|c4|c5]
 (N > 1 under torch.distributed.run, one process per GPU, backend nccl = RCCL.)
 """
 from __future__ import annotations
@@ -39,16 +39,45 @@ from gaussctrl_exp_amd.train import TrainStep  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 
 CONFIGS = {
-    # name: (N, W, H, sh_degree, scale_lo, scale_hi, seed, description)
-    "headline": (1_000_000, 1080, 1080, 3, 0.005, 0.02, 10,
+    # name: (N, W, H, sh_degree, scale_lo, scale_hi, seed, real scene or None, description)
+    "headline": (1_000_000, 1080, 1080, 3, 0.005, 0.02, 10, None,
                  "1M synthetic Gaussians @ 1080x1080, SH deg 3, fwd+bwd"),
-    "c2": (100_000, 512, 512, 0, 0.005, 0.03, 2,
+    "c2": (100_000, 512, 512, 0, 0.005, 0.03, 2, None,
            "100k synthetic Gaussians @ 512x512, SH deg 0, fwd+bwd"),
-    "c3": (300_000, 512, 512, 3, 0.004, 0.02, 3,
-           "300k synthetic Gaussians @ 512x512, SH deg 3, fwd+bwd"),
-    "c5": (5_000_000, 2048, 2048, 3, 0.01, 0.016, 5,
+    "c3": (300_000, 512, 512, 3, 0.0025, 0.012, 3, "bear",
+           "bear: 300k Gaussians seeded around data/bear/sparse_pc.ply (34,174 points), "
+           "bear cameras (transforms.json, 512x512), SH deg 3, fwd+bwd"),
+    "c4": (2_000_000, 1080, 1080, 3, 0.0016, 0.006, 4, "garden",
+           "garden: 2M Gaussians seeded around data/garden/sparse_pc.ply (27,046 points), "
+           "garden cameras rescaled x1080/512, 1 view/GPU (first sorted frames), SH deg 3, "
+           "fwd+bwd"),
+    "c5": (5_000_000, 2048, 2048, 3, 0.01, 0.016, 5, None,
            "5M synthetic Gaussians @ 2048x2048, SH deg 3, heavy overlap, fwd+bwd"),
 }
+
+
+def make_workload(config: str, rank: int, dev):
+    """(scene, camera) of one rank.  Synthetic configs: SURVEY.md §8d scene, camera `rank`
+    of an orbit.  Real configs: Gaussians seeded around the scene's sparse point cloud and
+    the scene's own camera `rank` (dataparser coordinates; tests/golden fixtures written by
+    tools/make_scene_fixtures.py, so the GPU box needs no reference checkout)."""
+    N, W, H, deg, lo, hi, seed, real, _ = CONFIGS[config]
+    if real is None:
+        return synthetic_scene(N, deg, seed=seed, scale_lo=lo, scale_hi=hi, device=dev), \
+            view_camera(W, H, rank)
+    import numpy as np
+    from gaussctrl_exp_amd.formats import load_transforms, rescale_cameras, transform_points
+    from gaussctrl_exp_amd.scene import scene_from_points
+    golden = os.path.join(ROOT, "tests", "golden")
+    d = load_transforms(os.path.join(golden, f"{real}_transforms.json"))
+    pc = np.load(os.path.join(golden, f"{real}_sparse_pc.npz"))
+    pts = transform_points(torch.from_numpy(pc["xyz"]), d.transform_matrix, d.points_scale)
+    scene = scene_from_points(pts, torch.from_numpy(pc["rgb"]), N, deg, seed=seed,
+                              scale_lo=lo, scale_hi=hi, device=dev)
+    cam = d.cameras[rank % len(d.cameras)]
+    if cam.width != W:
+        cam = rescale_cameras([cam], W / cam.width)[0]
+    return scene, cam
 
 
 def view_camera(W, H, view: int):
@@ -180,10 +209,11 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    N, W, H, deg, lo, hi, seed, desc = CONFIGS[args.config]
+    N, W, H, deg, lo, hi, seed, real, desc = CONFIGS[args.config]
     K = num_sh_bases(deg)
-    scene = synthetic_scene(N, deg, seed=seed, scale_lo=lo, scale_hi=hi, device=dev)
-    cam = view_camera(W, H, rank).to(dev)
+    scene, cam_cpu = make_workload(args.config, rank, dev)
+    cam = cam_cpu.to(dev)
+    H, W = cam.height, cam.width
     g = torch.Generator().manual_seed(1000 + rank)
     gt = torch.rand(H, W, 3, generator=g).to(dev)
     bg = torch.zeros(3, device=dev)
@@ -273,7 +303,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(scene, view_camera(W, H, 0), deg)
+        cpu = cpu_baseline(scene, cam_cpu, deg)
 
     if rank == 0:
         line = {
@@ -288,7 +318,9 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "fp32",
-            "data": "synthetic (random-Gaussian scene per SURVEY.md §8d; random-init params)",
+            "data": ("synthetic (random-Gaussian scene per SURVEY.md §8d; random-init params)"
+                     if real is None else f"{real} cameras + seed cloud (tests/golden); "
+                     "random-init Gaussians around the seeds; synthetic GT"),
             "config": {
                 "workload": desc,
                 "num_gaussians": N,
