@@ -7,8 +7,11 @@ Layout:
   _lib.py               ctypes binding (no CPU fallback)
   project_gaussians.py  sh.py  rasterize.py  utils.py   gsplat 0.1.2.1 surface
   camera.py             gc_model.py camera conventions (viewmat flip, projmat, tiles)
-  scene.py              synthetic / on-disk scene inputs for tests and benchmarks
-  train.py              multi-view data-parallel train step (RCCL gradient all-reduce)
+  scene.py              synthetic scenes + the gc_model render restatement
+  formats.py            transforms.json / sparse_pc.ply / splatfacto ckpt loaders
+  train.py              multi-view data-parallel train step (fused loss, fused Adam)
+  exchange.py           data-parallel SH-gradient view exchange (RCCL all-gather)
+  loss.py  optim.py     fused L1+SSIM loss, fused multi-tensor Adam
 
 `import gsplat` (the top-level shim package) resolves to this implementation.
 """
