@@ -43,7 +43,7 @@ CONFIGS = {
     "headline": (1_000_000, 1080, 1080, 3, 0.005, 0.02, 10, None,
                  "1M synthetic Gaussians @ 1080x1080, SH deg 3, fwd+bwd"),
     "c2": (100_000, 512, 512, 0, 0.005, 0.03, 2, None,
-           "100k synthetic Gaussians @ 512x512, SH deg 0, fwd+bwd"),
+           "100k synthetic Gaussians @ 512x512, SH deg 0, forward rasterize only"),
     "c3": (300_000, 512, 512, 3, 0.0025, 0.012, 3, "bear",
            "bear: 300k Gaussians seeded around data/bear/sparse_pc.ply (34,174 points), "
            "bear cameras (transforms.json, 512x512), SH deg 3, fwd+bwd"),
@@ -54,6 +54,9 @@ CONFIGS = {
     "c5": (5_000_000, 2048, 2048, 3, 0.01, 0.016, 5, None,
            "5M synthetic Gaussians @ 2048x2048, SH deg 3, heavy overlap, fwd+bwd"),
 }
+
+
+FORWARD_ONLY = {"c2"}  # BASELINE.json configs[1]: "forward rasterize only"
 
 
 def make_workload(config: str, rank: int, dev):
@@ -199,6 +202,8 @@ def main():
     ap.add_argument("--config", default="headline", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--train-steps", type=int, default=None)
+    ap.add_argument("--forward-only", action="store_true",
+                    help="time the render without backward (default for config c2)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -219,7 +224,13 @@ def main():
     bg = torch.zeros(3, device=dev)
     trainer = TrainStep(scene, sh_degree=deg, world_size=world, loss="l1")
 
+    fwd_only = args.forward_only or args.config in FORWARD_ONLY
+
     def step():
+        if fwd_only:
+            with torch.no_grad():
+                render(scene, cam, deg, bg)
+            return
         trainer.zero_grad()
         trainer.forward_backward(cam, gt, bg)
         trainer.sync_grads()
@@ -271,7 +282,7 @@ def main():
     dom = max(per_call, key=lambda k: per_call[k][2])
     dom_ms = per_call[dom][1]
     dom_bytes = ab.get(dom)
-    step_bytes = sum(ab.values())
+    step_bytes = sum(b for k, b in ab.items() if k in per_call)  # entries this step ran
     roofline = {
         "kernel": dom,
         "bound": "hbm",
@@ -307,7 +318,8 @@ def main():
 
     if rank == 0:
         line = {
-            "metric": "Mpixels/s fwd+bwd and train iters/s, 1M Gaussians @ 1080^2",
+            "metric": ("Mpixels/s fwd+bwd and train iters/s, 1M Gaussians @ 1080^2"
+                       if not fwd_only else "Mpixels/s forward and train iters/s"),
             "value": round(value, 2),
             "unit": "Mpixels/s",
             "n_gpus": world,
