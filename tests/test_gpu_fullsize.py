@@ -1,0 +1,128 @@
+"""The headline workload at full size (1M Gaussians @ 1080², ~7.7M intersections) on the
+MI355X -- the sizes where the sort switches to 16 keys per thread and the blend kernels see
+~1,700 Gaussians per tile -- against the CPU oracle:
+
+* binning (fused depth + tile radix sorts) bit-exact against the oracle's map + numpy stable
+  sort of the 64-bit keys, under both sort schemes (reduce-then-scan, one-sweep);
+* forward blend on 48 random tiles within the parity tolerance, and bit-identical when run
+  twice (no atomics in the forward);
+* backward on the same tiles (upstream gradient zero elsewhere, so only those tiles
+  contribute) within the tolerance plus the fp32 accumulation bound, as in
+  test_gpu_parity.
+"""
+import numpy as np
+import pytest
+import torch
+
+import bench
+import oracle as O
+from gaussctrl_exp_amd import _lib
+from gaussctrl_exp_amd import rasterize as R
+from gaussctrl_exp_amd.project_gaussians import project_gaussians
+from gaussctrl_exp_amd.rasterize import bin_gaussians
+
+pytestmark = pytest.mark.gpu
+
+ATOL, RTOL = 1e-5, 1e-4
+
+
+def _np(t):
+    return t.detach().cpu().numpy()
+
+
+@pytest.fixture(scope="module")
+def headline(gpu, oracle_lib):
+    sc, cam = bench.make_workload("headline", 0, gpu)
+    cam = cam.to(gpu)
+    with torch.no_grad():
+        g = project_gaussians(sc.means, torch.exp(sc.scales), 1,
+                              sc.quats / sc.quats.norm(dim=-1, keepdim=True),
+                              *cam.project_args())
+    xys, depths, radii, conics, nth, _ = [t.detach() for t in g]
+    ref = O.bin_and_sort(_np(xys), _np(depths), _np(radii), _np(nth), cam.tile_bounds)
+    gen = torch.Generator().manual_seed(5)
+    colors = torch.rand(xys.shape[0], 3, generator=gen)
+    opac = torch.sigmoid(sc.opacities.detach().cpu())
+    return dict(cam=cam, xys=xys, depths=depths, radii=radii, conics=conics, nth=nth, ref=ref,
+                colors=colors, opac=opac)
+
+
+@pytest.mark.parametrize("scheme", [1, 0])
+def test_headline_binning_bitexact(gpu, headline, scheme):
+    h, cam = headline, headline["cam"]
+    assert h["ref"]["num_intersects"] > 4 << 20  # the 16-keys-per-thread tile sort
+    _lib.call("gsplat_debug_sort_scheme", scheme)
+    try:
+        I, gids, bins = bin_gaussians(h["xys"], h["depths"], h["radii"], h["nth"], cam.height,
+                                      cam.width)
+    finally:
+        _lib.call("gsplat_debug_sort_scheme", 1)
+    assert I == h["ref"]["num_intersects"]
+    np.testing.assert_array_equal(_np(gids), h["ref"]["gaussian_ids_sorted"])
+    np.testing.assert_array_equal(_np(bins), h["ref"]["tile_bins"])
+
+
+def _tile_pixel_mask(cam, tiles):
+    H, W = cam.height, cam.width
+    m = np.zeros((H, W), bool)
+    tx = cam.tile_bounds[0]
+    for t in tiles:
+        y0, x0 = (t // tx) * 16, (t % tx) * 16
+        m[y0:y0 + 16, x0:x0 + 16] = True
+    return m
+
+
+def test_headline_raster_on_sampled_tiles(gpu, headline):
+    h, cam = headline, headline["cam"]
+    H, W, tb = cam.height, cam.width, cam.tile_bounds
+    T = tb[0] * tb[1]
+    tiles = np.random.default_rng(3).choice(T, size=48, replace=False).astype(np.int32)
+    mask = _tile_pixel_mask(cam, tiles)
+    bg = torch.tensor([0.3, 0.2, 0.1])
+    xy = h["xys"].clone().requires_grad_()
+    cn = h["conics"].clone().requires_grad_()
+    col = h["colors"].to(gpu).requires_grad_()
+    op = h["opac"].to(gpu).requires_grad_()
+    img, alpha = R.rasterize_gaussians(xy, h["depths"], h["radii"], cn, h["nth"], col, op, H, W,
+                                       bg.to(gpu), return_alpha=True)
+    img2 = R.rasterize_gaussians(h["xys"], h["depths"], h["radii"], h["conics"], h["nth"],
+                                 h["colors"].to(gpu), h["opac"].to(gpu), H, W, bg.to(gpu))
+    np.testing.assert_array_equal(_np(img), _np(img2))  # deterministic forward
+    ref = h["ref"]
+    rimg, rT, ridx = O.rasterize_forward(tb, H, W, ref["gaussian_ids_sorted"], ref["tile_bins"],
+                                         _np(h["xys"]), _np(h["conics"]), h["colors"].numpy(),
+                                         h["opac"].numpy(), bg.numpy(), tile_list=tiles)
+    got = _np(img)[mask]
+    want = rimg[mask]
+    bad = np.abs(got - want) > ATOL + RTOL * np.abs(want)
+    assert bad.mean() <= 1e-3, f"{bad.mean():.2e} of sampled pixels out of tolerance"
+    assert np.abs(_np(alpha)[mask] - (1 - rT[mask])).max() < 1e-4
+    # backward: upstream gradient only on the sampled tiles
+    gen = torch.Generator().manual_seed(9)
+    v_img = torch.randn(H, W, 3, generator=gen) * torch.from_numpy(mask)[..., None]
+    v_alpha = torch.randn(H, W, generator=gen) * torch.from_numpy(mask)
+    ((img * v_img.to(gpu)).sum() + (alpha * v_alpha.to(gpu)).sum()).backward()
+    # the oracle backward on the GPU's own forward state (final T / index), as test_gpu_parity
+    out = torch.empty(H, W, 3, device=gpu)
+    fT2 = torch.empty(H, W, device=gpu)
+    fi = torch.empty(H, W, device=gpu, dtype=torch.int32)
+    I, gids, bins = bin_gaussians(h["xys"], h["depths"], h["radii"], h["nth"], H, W)
+    P = _lib.ptr
+    _lib.call("gsplat_rasterize_forward", tb[0], tb[1], H, W, 3, P(gids), P(bins), P(h["xys"]),
+              P(h["conics"]), P(col.detach()), P(op.detach()), P(bg.to(gpu)), P(out), P(fT2),
+              P(fi), _lib.stream(gpu))
+    grads, absum = O.rasterize_backward(tb, H, W, ref["gaussian_ids_sorted"], ref["tile_bins"],
+                                        _np(h["xys"]), _np(h["conics"]), h["colors"].numpy(),
+                                        h["opac"].numpy(), bg.numpy(), _np(fT2), _np(fi),
+                                        v_img.numpy(), v_alpha.numpy(),
+                                        alpha_max=R.BACKWARD_ALPHA_CLAMP, tile_list=tiles,
+                                        return_abs=True)
+    for k, (name, g) in enumerate((("xys", xy.grad), ("conics", cn.grad), ("colors", col.grad),
+                                   ("opacity", op.grad))):
+        a = _np(g).astype(np.float64)
+        b = grads[k].reshape(a.shape).astype(np.float64)
+        tol = ATOL + RTOL * np.abs(b) + absum[k].reshape(a.shape) * 2.0 ** -20
+        bad = np.abs(a - b) > tol
+        assert np.abs(b).max() > 0
+        assert not bad.any(), f"{name}: {bad.mean():.2e} out of tolerance " \
+                              f"(max {np.abs(a - b).max():.3e})"

@@ -11,7 +11,7 @@ from gaussctrl_exp_amd.project_gaussians import project_gaussians
 from gaussctrl_exp_amd.rasterize import bin_gaussians
 from gaussctrl_exp_amd.scene import synthetic_scene
 
-N, W, H, deg, lo, hi, seed, desc = bench.CONFIGS[os.environ.get("CFG", "headline")]
+N, W, H, deg, lo, hi, seed, _real, desc = bench.CONFIGS[os.environ.get("CFG", "headline")]
 dev = torch.device("cuda:0")
 sc = synthetic_scene(N, deg, seed=seed, scale_lo=lo, scale_hi=hi, device=dev)
 cam = bench.view_camera(W, H, 0).to(dev)
