@@ -305,10 +305,14 @@ __global__ __launch_bounds__(256) void project_bwd_kernel(
 #undef GR
     }
   }
+  if (v_cov2d_out) {  // intermediate gradients: optional (the autograd wrapper drops them)
 #pragma unroll
-  for (int k = 0; k < 3; ++k) v_cov2d_out[3 * i + k] = vc2[k];
+    for (int k = 0; k < 3; ++k) v_cov2d_out[3 * i + k] = vc2[k];
+  }
+  if (v_cov3d_out) {
 #pragma unroll
-  for (int k = 0; k < 6; ++k) v_cov3d_out[6 * i + k] = vc3[k];
+    for (int k = 0; k < 6; ++k) v_cov3d_out[6 * i + k] = vc3[k];
+  }
 #pragma unroll
   for (int k = 0; k < 3; ++k) v_mean_out[3 * i + k] = vmean[k];
 #pragma unroll

@@ -102,8 +102,6 @@ class _ProjectGaussians(Function):
             torch.zeros((n, 3), device=dev, dtype=torch.float32)
         if v_depths is not None:  # NULL = zero depth gradient
             v_depths = _as_f32(v_depths).contiguous()
-        v_cov2d = torch.empty((n, 3), device=dev, dtype=torch.float32)
-        v_cov3d_out = torch.empty((n, 6), device=dev, dtype=torch.float32)
         v_mean3d = torch.empty((n, 3), device=dev, dtype=torch.float32)
         v_scale = torch.empty((n, 3), device=dev, dtype=torch.float32)
         v_quat = torch.empty((n, 4), device=dev, dtype=torch.float32)
@@ -112,7 +110,7 @@ class _ProjectGaussians(Function):
                   float(ctx.glob_scale), P(quats), P(viewmat), P(projmat), float(ctx.fx),
                   float(ctx.fy), float(ctx.cx), float(ctx.cy), int(ctx.img_height),
                   int(ctx.img_width), P(cov3d), P(radii), P(conics), P(v_xys), P(v_depths),
-                  P(v_conics), P(v_cov2d), P(v_cov3d_out), P(v_mean3d), P(v_scale), P(v_quat),
+                  P(v_conics), None, None, P(v_mean3d), P(v_scale), P(v_quat),
                   _lib.stream(dev))
         # one gradient per input of forward (gsplat 0.1.2.1 returns None for the rest)
         return (v_mean3d, v_scale, None, v_quat, None, None, None, None, None, None, None,

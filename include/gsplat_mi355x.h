@@ -56,7 +56,8 @@ int gsplat_project_gaussians_forward(
     float *conics, int32_t *num_tiles_hit, void *stream);
 
 /* Outputs v_cov2d [N,3], v_cov3d [N,6], v_mean3d [N,3], v_scale [N,3], v_quat [N,4] are
- * fully written (zeros where radii <= 0).  v_depth may be NULL (an all-zero depth gradient,
+ * fully written (zeros where radii <= 0); v_cov2d / v_cov3d (gsplat's intermediate
+ * gradients, which its autograd wrapper discards) may be NULL.  v_depth may be NULL (an all-zero depth gradient,
  * which is what the gsplat autograd wrapper passes when nothing consumed depths). */
 int gsplat_project_gaussians_backward(
     int num_points, const float *means3d, const float *scales, float glob_scale,

@@ -45,9 +45,9 @@ def test_sh_backward_views_vs_oracle(gpu, oracle_lib, degree, dtu, n, R, pad):
         d = (means - campos[r]).to(gpu)
         d = d / d.norm(dim=-1, keepdim=True)
         out = torch.empty(n, K, 3, device=gpu)
-        _lib.call("gsplat_compute_sh_backward", n, degree, dtu, _lib.ptr(d),
-                  _lib.ptr(vcol[r].contiguous().to(gpu)), _lib.ptr(out),
-                  _lib.stream(gpu))
+        vc = vcol[r].contiguous().to(gpu)  # held: a pointer to a temporary would dangle
+        _lib.call("gsplat_compute_sh_backward", n, degree, dtu, _lib.ptr(d), _lib.ptr(vc),
+                  _lib.ptr(out), _lib.stream(gpu))
         acc += out
     np.testing.assert_allclose(got, acc.cpu().numpy(), rtol=1e-5, atol=1e-6)
     if dtu < degree:  # bases above degrees_to_use get zero gradient

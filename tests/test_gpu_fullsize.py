@@ -107,9 +107,10 @@ def test_headline_raster_on_sampled_tiles(gpu, headline):
     fT2 = torch.empty(H, W, device=gpu)
     fi = torch.empty(H, W, device=gpu, dtype=torch.int32)
     I, gids, bins = bin_gaussians(h["xys"], h["depths"], h["radii"], h["nth"], H, W)
+    bg_d = bg.to(gpu)  # held: a pointer to a temporary would dangle
     P = _lib.ptr
     _lib.call("gsplat_rasterize_forward", tb[0], tb[1], H, W, 3, P(gids), P(bins), P(h["xys"]),
-              P(h["conics"]), P(col.detach()), P(op.detach()), P(bg.to(gpu)), P(out), P(fT2),
+              P(h["conics"]), P(col.detach()), P(op.detach()), P(bg_d), P(out), P(fT2),
               P(fi), _lib.stream(gpu))
     grads, absum = O.rasterize_backward(tb, H, W, ref["gaussian_ids_sorted"], ref["tile_bins"],
                                         _np(h["xys"]), _np(h["conics"]), h["colors"].numpy(),

@@ -100,6 +100,21 @@ def test_project_backward(gpu, case):
                          ("quats", q.grad, ob[4])):
         frac, mx = _close_frac(_np(gt), ot)
         assert frac == 0.0, f"{name}: {frac:.2e} of elements out of tolerance (max {mx:.3e})"
+    # the C ABI's optional intermediate outputs (v_cov2d, v_cov3d; the wrapper passes NULL)
+    # (device copies held in locals: a pointer to a temporary would dangle)
+    P = _lib.ptr
+    dv = lambda *shape: torch.empty(*shape, device=gpu)
+    v_cov2d, v_cov3d, vm, vs, vq = dv(n, 3), dv(n, 6), dv(n, 3), dv(n, 3), dv(n, 4)
+    d_view, d_proj = cam.viewmat.to(gpu), cam.projmat.to(gpu)
+    d_vxy, d_vd, d_vc = v_xy.to(gpu), v_d.to(gpu), v_c.to(gpu)
+    _lib.call("gsplat_project_gaussians_backward", n, P(m.detach()), P(s.detach()), 1.0,
+              P(q.detach()), P(d_view), P(d_proj), *args[:6], P(cov3d.detach()), P(radii),
+              P(conics.detach()), P(d_vxy), P(d_vd), P(d_vc), P(v_cov2d), P(v_cov3d), P(vm),
+              P(vs), P(vq), _lib.stream(gpu))
+    for name, gt, ot in (("v_cov2d", v_cov2d, ob[0]), ("v_cov3d", v_cov3d, ob[1]),
+                         ("means (C ABI)", vm, ob[2])):
+        frac, mx = _close_frac(_np(gt), ot)
+        assert frac == 0.0, f"{name}: {frac:.2e} of elements out of tolerance (max {mx:.3e})"
 
 
 @pytest.mark.parametrize("degree,use", [(0, 0), (1, 1), (2, 2), (3, 3), (3, 0), (3, 2),
@@ -270,9 +285,10 @@ def _check_raster_backward(gpu, case):
     out = torch.empty(H, W, 3, device=gpu)
     fT = torch.empty(H, W, device=gpu)
     fi = torch.empty(H, W, device=gpu, dtype=torch.int32)
+    bg_d = bg.to(gpu)
     P = _lib.ptr
     _lib.call("gsplat_rasterize_forward", tb[0], tb[1], H, W, 3, P(gids), P(bins), P(xys),
-              P(conics), P(col.detach()), P(op.detach()), P(bg.to(gpu)), P(out), P(fT), P(fi),
+              P(conics), P(col.detach()), P(op.detach()), P(bg_d), P(out), P(fT), P(fi),
               _lib.stream(gpu))
     ref = O.rasterize_backward(tb, H, W, _np(gids), _np(bins), _np(xys), _np(conics),
                                colors.numpy(), opac.numpy(), bg.numpy(), _np(fT), _np(fi),
