@@ -49,6 +49,8 @@ class ShViewExchange:
 
     @contextlib.contextmanager
     def view(self, means: torch.Tensor, campos: torch.Tensor):
+        # (set before the render, so a rank whose render never reaches spherical_harmonics
+        #  can still take part in the step's exchange: TrainStep._null_sh_exchange)
         """Scope of one rank's render: SH calls inside it exchange their gradients."""
         global _ACTIVE
         prev = _ACTIVE

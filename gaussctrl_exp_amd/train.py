@@ -69,31 +69,33 @@ def splatfacto_loss(pred, gt):
 class GradExchange:
     """Sums every parameter's gradient over the data-parallel ranks (RCCL over xGMI).
 
-    One async all-reduce per parameter, launched from a post-accumulate-grad hook the moment
-    autograd has produced that gradient (gradients stay the tensors autograd produced: no
-    flat bucket to zero-fill and accumulate into, no pack/unpack copies; hooks fire in the
-    same order on every rank because every rank runs the same graph).  With an
-    ShViewExchange (`sh`), the SH-coefficient parameters (`sh_params`) are skipped in any
-    step whose SH backward already produced the all-rank sum through the exchange."""
+    After backward, one async all-reduce per parameter tensor in a fixed (parameter) order,
+    then one wait: every rank issues the same collective sequence whatever its own graph
+    looked like -- a rank whose view saw no Gaussians (the caller's early background return,
+    gc_model.py:189-190) contributes zero gradients instead of skipping collectives and
+    hanging the others.  The gradients are reduced in place (the tensors autograd produced:
+    no flat bucket to zero-fill and accumulate into).  With an ShViewExchange (`sh`), the
+    SH-coefficient parameters (`sh_params`) are skipped in a step whose SH backward already
+    produced the all-rank sum through the exchange."""
 
     def __init__(self, params: List[torch.Tensor], group=None,
                  sh: Optional[ShViewExchange] = None, sh_params=()):
+        self.params = list(params)
         self.group = group
         self.sh = sh
         self.sh_ids = {id(p) for p in sh_params}
-        self.works = []
-        self.handles = [p.register_post_accumulate_grad_hook(self._hook) for p in params]
-
-    def _hook(self, p: torch.Tensor):
-        if self.sh is not None and self.sh.handled and id(p) in self.sh_ids:
-            return  # already summed over the ranks by the SH view exchange
-        self.works.append(dist.all_reduce(p.grad, op=dist.ReduceOp.SUM, group=self.group,
-                                          async_op=True))
 
     def wait(self):
-        for w in self.works:
+        works = []
+        for p in self.params:
+            if self.sh is not None and self.sh.handled and id(p) in self.sh_ids:
+                continue  # already summed over the ranks by the SH view exchange
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+            works.append(dist.all_reduce(p.grad, op=dist.ReduceOp.SUM, group=self.group,
+                                         async_op=True))
+        for w in works:
             w.wait()
-        self.works.clear()
         if self.sh is not None:
             self.sh.reset()
 
@@ -160,8 +162,28 @@ class TrainStep:
         else:
             out = render(self.scene, cam, self.sh_degree, background, api=self.api)
         loss = self.loss(out["rgb"], gt)
-        loss.backward()
+        if loss.requires_grad:
+            loss.backward()
+        elif self.sh_exchange is not None and self.scene.features_rest.shape[1] > 0:
+            # no Gaussian in view (the caller returned the background): no local gradient,
+            # but the other ranks' SH exchange still needs this rank's (zero) record
+            self._null_sh_exchange()
         return loss, out
+
+    def _null_sh_exchange(self):
+        sc = self.scene
+        n, K = sc.num_points, sc.features_rest.shape[1] + 1
+        degree = {1: 0, 4: 1, 9: 2, 16: 3, 25: 4}[K]
+        zeros = torch.zeros(n, 3, device=sc.means.device)
+        if self.api is None:
+            from .sh import sh_backward_views
+            fn = lambda means, views: sh_backward_views(degree, self.sh_degree, means, views)
+        else:
+            fn = lambda means, views: self.api.sh_backward_views(degree, self.sh_degree, means,
+                                                                 views)
+        v = self.sh_exchange.reduce(zeros, fn)
+        sc.features_dc.grad = v[:, 0, :].contiguous()
+        sc.features_rest.grad = v[:, 1:, :].contiguous()
 
     def step(self, cam: GCCamera, gt: torch.Tensor, background: Optional[torch.Tensor] = None,
              optimizer: bool = True):

@@ -108,7 +108,13 @@ def rasterize_gaussians(xys, depths, radii, conics, nth, colors, opacity, H, W,
                          return_alpha)
 
 
+def sh_backward_views(degree, degrees_to_use, means, views):
+    K = {0: 1, 1: 4, 2: 9, 3: 16, 4: 25}[degree]
+    return torch.from_numpy(O.sh_backward_views(degrees_to_use, _np(means), _np(views), K))
+
+
 class API:
+    sh_backward_views = staticmethod(sh_backward_views)
     project_gaussians = staticmethod(project_gaussians)
     spherical_harmonics = staticmethod(spherical_harmonics)
     rasterize_gaussians = staticmethod(rasterize_gaussians)

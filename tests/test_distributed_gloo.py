@@ -32,6 +32,49 @@ def _views():
     return cams
 
 
+def _away_camera():
+    """Looks away from the scene: every Gaussian is behind it, so the caller's render takes
+    its early background return (gc_model.py:189-190) and the rank has no local graph."""
+    from gaussctrl_exp_amd.camera import gc_camera, look_at_c2w
+    return gc_camera(look_at_c2w((0.0, 0.0, 4.0), target=(0.0, 0.0, 8.0), up=(0.0, 1.0, 0.0)),
+                     80.0, 80.0, 32.0, 24.0, 64, 48)
+
+
+def _empty_worker(rank, world, port, out_dir, mode):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle_gsplat import API
+    from gaussctrl_exp_amd.train import TrainStep
+    cam = _views()[0] if rank == 0 else _away_camera()
+    gt = torch.rand(48, 64, 3, generator=torch.Generator().manual_seed(rank))
+    t = TrainStep(_scene(), sh_degree=3, world_size=world, loss="l1", api=API,
+                  grad_exchange=mode)
+    t.step(cam, gt, background=torch.tensor([0.5, 0.5, 0.5]), optimizer=False)
+    np.save(os.path.join(out_dir, f"grad{rank}.npy"), t.flat_grad().numpy())
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["allreduce", "sh_views"])
+def test_rank_with_empty_view_contributes_zero(tmp_path, mode):
+    """A rank that sees no Gaussian still takes part in every collective (no hang) and
+    contributes nothing: both ranks end with rank 0's single-view gradient."""
+    from oracle_gsplat import API
+    from gaussctrl_exp_amd.scene import render
+    from gaussctrl_exp_amd.train import TrainStep
+    out = render(_scene(), _away_camera(), 3, torch.zeros(3), api=API)
+    assert out["accumulation"] is None  # really the early-return path
+    port = _free_port()
+    mp.spawn(_empty_worker, args=(2, port, str(tmp_path), mode), nprocs=2, join=True)
+    g0, g1 = np.load(tmp_path / "grad0.npy"), np.load(tmp_path / "grad1.npy")
+    np.testing.assert_array_equal(g0, g1)
+    t = TrainStep(_scene(), sh_degree=3, world_size=1, loss="l1", api=API)
+    gt = torch.rand(48, 64, 3, generator=torch.Generator().manual_seed(0))
+    t.step(_views()[0], gt, background=torch.tensor([0.5, 0.5, 0.5]), optimizer=False)
+    ref = t.flat_grad().numpy()
+    assert np.abs(ref).max() > 0
+    np.testing.assert_allclose(g0, ref, rtol=1e-5, atol=1e-7)
+
+
 def _scene():
     from gaussctrl_exp_amd.scene import synthetic_scene
     return synthetic_scene(400, 3, seed=3, scale_lo=0.02, scale_hi=0.08, extent=1.0)

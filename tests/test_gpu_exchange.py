@@ -103,3 +103,38 @@ def test_exchange_over_rccl_world1_matches_plain(gpu):
             np.testing.assert_allclose(a, b, rtol=1e-5, atol=1e-6)
     finally:
         dist.destroy_process_group()
+
+
+def test_trainstep_multirank_path_over_rccl_world1(gpu):
+    """TrainStep's multi-rank configuration (SH view exchange + canonical-order all-reduces,
+    what bench.py runs at N > 1) driven over RCCL at world size 1 equals the single-rank
+    step, and an empty view (the caller's early background return) goes through every
+    collective without a hang and leaves zero gradients."""
+    import torch.distributed as dist
+    from gaussctrl_exp_amd.camera import gc_camera, look_at_c2w, synthetic_camera
+    from gaussctrl_exp_amd.scene import synthetic_scene
+    from gaussctrl_exp_amd.train import TrainStep
+
+    store = dist.TCPStore("127.0.0.1", _free_port(), 1, True)
+    dist.init_process_group("nccl", store=store, rank=0, world_size=1, device_id=gpu)
+    try:
+        cam = synthetic_camera(256, 192).to(gpu)
+        gt = torch.rand(192, 256, 3, generator=torch.Generator().manual_seed(2)).to(gpu)
+        bg = torch.tensor([0.2, 0.3, 0.4], device=gpu)
+        flats = []
+        for ws in (1, 2):  # 2: build the multi-rank exchange objects (the group has 1 rank)
+            t = TrainStep(synthetic_scene(20000, 3, seed=6, device=gpu), sh_degree=3,
+                          world_size=ws, loss="splatfacto")
+            t.step(cam, gt, background=bg, optimizer=False)
+            flats.append(t.flat_grad().cpu().numpy())
+        assert np.abs(flats[0]).max() > 0
+        np.testing.assert_allclose(flats[1], flats[0], rtol=1e-5, atol=1e-6)
+        away = gc_camera(look_at_c2w((0.0, 0.0, 4.0), target=(0.0, 0.0, 8.0),
+                                     up=(0.0, 1.0, 0.0)), 200.0, 200.0, 128.0, 96.0, 256,
+                         192).to(gpu)
+        t = TrainStep(synthetic_scene(20000, 3, seed=6, device=gpu), sh_degree=3,
+                      world_size=2, loss="splatfacto")
+        t.step(away, gt, background=bg, optimizer=True)
+        assert all(p.grad is not None and not p.grad.any() for p in t.params)
+    finally:
+        dist.destroy_process_group()
