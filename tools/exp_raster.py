@@ -11,10 +11,10 @@ from gaussctrl_exp_amd.rasterize import bin_gaussians
 from gaussctrl_exp_amd.scene import synthetic_scene
 
 cfg = os.environ.get("CFG", "headline")
-N, W, H, deg, lo, hi, seed, desc = bench.CONFIGS[cfg]
 dev = torch.device("cuda:0")
-sc = synthetic_scene(N, deg, seed=seed, scale_lo=lo, scale_hi=hi, device=dev)
-cam = bench.view_camera(W, H, 0).to(dev)
+sc, cam = bench.make_workload(cfg, 0, dev)
+cam = cam.to(dev)
+N, H, W = sc.num_points, cam.height, cam.width
 P, st = _lib.ptr, _lib.stream(dev)
 with torch.no_grad():
     xys, depths, radii, conics, nth, _ = project_gaussians(
@@ -50,7 +50,7 @@ def timeit(fn, reps=10):
     return s.elapsed_time(e) / reps
 
 variants = [(f, b, fl) for f, b, fl in
-            [(1, 2, 0), (1, 2, 4), (1, 2, 16), (2, 2, 0), (2, 2, 8), (4, 4, 0), (1, 2, 32),
+            [(1, 2, 0), (1, 2, 4), (1, 2, 16), (2, 2, 0), (1, 1, 0), (1, 2, 2), (1, 2, 32),
              (1, 2, 1)]]
 res = {v: {"fwd": [], "bwd": []} for v in variants}
 for rnd in range(5):
