@@ -7,16 +7,16 @@
 // gaussctrl_exp_amd/train.py ssim() / splatfacto_loss().
 //
 // MI355X design (stencil work, HBM/LDS-bound; no MFMA):
-//  * Forward: one 256-thread workgroup per 16x16 block of SSIM outputs (block origin (bx, by)).
-//    Per channel it stages the 26x26 input patches of gt and pred in LDS, runs the separable
+//  * Forward: one 256-thread workgroup per 32x16 block of SSIM outputs (block origin (bx, by)).
+//    Per channel it stages the 42x26 input patches of gt and pred in LDS, runs the separable
 //    filter horizontally (5 moments: x, y, x^2, y^2, xy) then vertically, and evaluates the
 //    SSIM map m and its partial derivatives with respect to the filtered pred statistics
 //    (mu_y, E[y^2], E[xy]); those three maps are written for the backward.  The same
-//    workgroup sums |gt - pred| over its 16x16 input block (the blocks tile the image) and
+//    workgroup sums |gt - pred| over its 32x16 input block (the blocks tile the image) and
 //    the SSIM values of its outputs; per-block partial sums are reduced by one tiny kernel
 //    into the loss scalar (deterministic, no host sync).
-//  * Backward: one workgroup per 16x16 block of input pixels correlates the three derivative
-//    maps (26x26 halo patch in LDS, separable) back to input resolution and adds the L1 sign
+//  * Backward: one workgroup per 32x16 block of input pixels correlates the three derivative
+//    maps (42x26 halo patch in LDS, separable) back to input resolution and adds the L1 sign
 //    term; the upstream gradient is read from device memory (no host sync).
 #include "common.h"
 
@@ -24,8 +24,9 @@ namespace gs {
 namespace {
 
 constexpr int WIN = 11;
-constexpr int TB = 16;              // block edge
-constexpr int PATCH = TB + WIN - 1;  // 26
+constexpr int TW = 32, TH = 16;      // block: 32 columns x 16 rows
+constexpr int PW = TW + WIN - 1;     // 42-column halo patch
+constexpr int PH = TH + WIN - 1;     // 26-row halo patch
 constexpr float K1 = 0.01f, K2 = 0.03f;
 
 struct Win {
@@ -42,6 +43,11 @@ __device__ __forceinline__ float block_sum(float v, float *red) {
   return t;
 }
 
+// LDS layout rule (MI355X_MICROARCH.md §LDS): ds_read_b32 / ds_write_b32 bank by dword
+// address mod 32 within each 32-lane half-wave.  Every pass below maps a half-wave to 32
+// consecutive columns of ONE row, so all its LDS accesses are conflict-free; thread t works
+// on column t % 32 and rows 2 (t / 32) and 2 (t / 32) + 1 of its block.
+
 // partials[block] = {sum |gt - pred| over the block's input pixels (all channels),
 //                    sum of SSIM map values over the block's valid outputs (all channels)}
 __global__ __launch_bounds__(256) void l1_ssim_fwd_kernel(int H, int W, int C,
@@ -49,40 +55,57 @@ __global__ __launch_bounds__(256) void l1_ssim_fwd_kernel(int H, int W, int C,
                                                           const float *__restrict__ gt, Win win,
                                                           float *__restrict__ partials,
                                                           float *__restrict__ dmaps) {
-  __shared__ float sx[PATCH][PATCH + 1], sy[PATCH][PATCH + 1];
-  __shared__ float hm[5][PATCH][TB + 1];
+  __shared__ float sx[PH * PW], sy[PH * PW];
+  __shared__ float hm[5][PH][TW];
   __shared__ float red[4];
   const int Ho = H - WIN + 1, Wo = W - WIN + 1;
-  const int nbx = (W + TB - 1) / TB;
-  const int bx = (blockIdx.x % nbx) * TB, by = (blockIdx.x / nbx) * TB;
-  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const int nbx = (W + TW - 1) / TW;
+  const int bx = (blockIdx.x % nbx) * TW, by = (blockIdx.x / nbx) * TH;
+  const int tx = threadIdx.x & 31, ty = (threadIdx.x >> 5) * 2;
   const float c1 = K1 * K1, c2 = K2 * K2;
   float l1 = 0.f, ssum = 0.f;
   const size_t plane = (size_t)Ho * Wo;
-  for (int c = 0; c < C; ++c) {
-    for (int k = threadIdx.x; k < PATCH * PATCH; k += 256) {
-      const int r = k / PATCH, q = k % PATCH;
+  // the patch is staged with the next channel's values prefetched into registers while the
+  // current channel is filtered (SLOTS = ceil(26 * 42 / 256) elements per thread)
+  constexpr int SLOTS = (PH * PW + 255) / 256;
+  float px[SLOTS], py[SLOTS];
+  auto fetch = [&](int c) {
+#pragma unroll
+    for (int u = 0; u < SLOTS; ++u) {
+      const int k = threadIdx.x + 256 * u;
+      const int r = k / PW, q = k - r * PW;
       const int i = by + r, j = bx + q;
-      float xv = 0.f, yv = 0.f;
-      if (i < H && j < W) {
-        xv = gt[((size_t)i * W + j) * C + c];
-        yv = pred[((size_t)i * W + j) * C + c];
+      px[u] = py[u] = 0.f;
+      if (k < PH * PW && i < H && j < W) {
+        px[u] = gt[((size_t)i * W + j) * C + c];
+        py[u] = pred[((size_t)i * W + j) * C + c];
       }
-      sx[r][q] = xv;
-      sy[r][q] = yv;
     }
+  };
+  fetch(0);
+  for (int c = 0; c < C; ++c) {
+#pragma unroll
+    for (int u = 0; u < SLOTS; ++u) {
+      const int k = threadIdx.x + 256 * u;
+      if (k < PH * PW) {
+        sx[k] = px[u];
+        sy[k] = py[u];
+      }
+    }
+    if (c + 1 < C) fetch(c + 1);
     __syncthreads();
-    {  // L1 over this block's own input pixels
-      const int i = by + ty, j = bx + tx;
-      if (i < H && j < W) l1 += fabsf(sx[ty][tx] - sy[ty][tx]);
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr) {  // L1 over this block's own input pixels
+      const int i = by + ty + rr, j = bx + tx;
+      if (i < H && j < W) l1 += fabsf(sx[(ty + rr) * PW + tx] - sy[(ty + rr) * PW + tx]);
     }
-    // horizontal pass: rows 0..25, output columns 0..15
-    for (int k = threadIdx.x; k < PATCH * TB; k += 256) {
-      const int r = k / TB, q = k % TB;
+    // horizontal pass: patch rows 0..25, output columns 0..31 (one row per half-wave)
+    for (int k = threadIdx.x; k < PH * TW; k += 256) {
+      const int r = k >> 5, q = k & 31;
       float m0 = 0.f, m1 = 0.f, m2 = 0.f, m3 = 0.f, m4 = 0.f;
 #pragma unroll
       for (int t = 0; t < WIN; ++t) {
-        const float w = win.w[t], xv = sx[r][q + t], yv = sy[r][q + t];
+        const float w = win.w[t], xv = sx[r * PW + q + t], yv = sy[r * PW + q + t];
         m0 += w * xv;
         m1 += w * yv;
         m2 += w * xv * xv;
@@ -96,31 +119,40 @@ __global__ __launch_bounds__(256) void l1_ssim_fwd_kernel(int H, int W, int C,
       hm[4][r][q] = m4;
     }
     __syncthreads();
-    {
-      const int oi = by + ty, oj = bx + tx;
-      if (oi < Ho && oj < Wo) {
-        float mu1 = 0.f, mu2 = 0.f, exx = 0.f, eyy = 0.f, exy = 0.f;
+    // vertical pass: output rows ty and ty + 1 share 10 of their 11 taps (12 rows loaded)
+    float a[2][5];
 #pragma unroll
-        for (int t = 0; t < WIN; ++t) {
-          const float w = win.w[t];
-          mu1 += w * hm[0][ty + t][tx];
-          mu2 += w * hm[1][ty + t][tx];
-          exx += w * hm[2][ty + t][tx];
-          eyy += w * hm[3][ty + t][tx];
-          exy += w * hm[4][ty + t][tx];
-        }
+    for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+      for (int m = 0; m < 5; ++m) a[rr][m] = 0.f;
+#pragma unroll
+    for (int u = 0; u <= WIN; ++u) {
+#pragma unroll
+      for (int m = 0; m < 5; ++m) {
+        const float h = hm[m][ty + u][tx];
+        if (u < WIN) a[0][m] += win.w[u] * h;
+        if (u >= 1) a[1][m] += win.w[u - 1] * h;
+      }
+    }
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr) {
+      const int oi = by + ty + rr, oj = bx + tx;
+      if (oi < Ho && oj < Wo) {
+        const float mu1 = a[rr][0], mu2 = a[rr][1], exx = a[rr][2], eyy = a[rr][3],
+                    exy = a[rr][4];
         const float s11 = exx - mu1 * mu1, s22 = eyy - mu2 * mu2, s12 = exy - mu1 * mu2;
         const float A = 2.f * mu1 * mu2 + c1, B = mu1 * mu1 + mu2 * mu2 + c1;
         const float Cn = 2.f * s12 + c2, D = s11 + s22 + c2;
-        const float l = A / B, cs = Cn / D;
+        const float rB = 1.f / B, rD = 1.f / D;  // two divisions; the rest are products
+        const float l = A * rB, cs = Cn * rD;
         ssum += l * cs;
         // d m / d mu2, d m / d E[y^2], d m / d E[xy]  (mu1, E[x^2] belong to gt: constant)
-        const float dl = (2.f * mu1 * B - 2.f * mu2 * A) / (B * B);
-        const float dcs = (-2.f * mu1 * D + 2.f * mu2 * Cn) / (D * D);
+        const float dl = (2.f * mu1 * B - 2.f * mu2 * A) * (rB * rB);
+        const float dcs = (-2.f * mu1 * D + 2.f * mu2 * Cn) * (rD * rD);
         const size_t o = (size_t)oi * Wo + oj;
         dmaps[(size_t)(0 * C + c) * plane + o] = dl * cs + l * dcs;
-        dmaps[(size_t)(1 * C + c) * plane + o] = -l * Cn / (D * D);
-        dmaps[(size_t)(2 * C + c) * plane + o] = 2.f * l / D;
+        dmaps[(size_t)(1 * C + c) * plane + o] = -l * cs * rD;
+        dmaps[(size_t)(2 * C + c) * plane + o] = 2.f * l * rD;
       }
     }
     __syncthreads();
@@ -162,58 +194,86 @@ __global__ __launch_bounds__(256) void l1_ssim_bwd_kernel(
     int H, int W, int C, const float *__restrict__ pred, const float *__restrict__ gt, Win win,
     const float *__restrict__ dmaps, const float *__restrict__ grad_out, float ssim_scale,
     float l1_scale, float *__restrict__ v_pred) {
-  __shared__ float sd[3][PATCH][PATCH + 1];
-  __shared__ float hd[3][PATCH][TB + 1];
+  __shared__ float sd[3][PH * PW];
+  __shared__ float hd[3][PH][TW];
   const int Ho = H - WIN + 1, Wo = W - WIN + 1;
-  const int nbx = (W + TB - 1) / TB;
-  const int bx = (blockIdx.x % nbx) * TB, by = (blockIdx.x / nbx) * TB;
-  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const int nbx = (W + TW - 1) / TW;
+  const int bx = (blockIdx.x % nbx) * TW, by = (blockIdx.x / nbx) * TH;
+  const int tx = threadIdx.x & 31, ty = (threadIdx.x >> 5) * 2;
   const float g = grad_out[0];
   const float gs = g * ssim_scale, gl = g * l1_scale;
   const size_t plane = (size_t)Ho * Wo;
   // input q receives from outputs p = q - t, t in [0, 10]: patch rows/cols start at b - 10
   const int oy0 = by - (WIN - 1), ox0 = bx - (WIN - 1);
-  for (int c = 0; c < C; ++c) {
-    for (int k = threadIdx.x; k < PATCH * PATCH; k += 256) {
-      const int r = k / PATCH, q = k % PATCH;
+  constexpr int SLOTS = (PH * PW + 255) / 256;
+  float pd[3][SLOTS];
+  auto fetch = [&](int c) {
+#pragma unroll
+    for (int u = 0; u < SLOTS; ++u) {
+      const int k = threadIdx.x + 256 * u;
+      const int r = k / PW, q = k - r * PW;
       const int oi = oy0 + r, oj = ox0 + q;
-      const bool ok = oi >= 0 && oj >= 0 && oi < Ho && oj < Wo;
+      const bool ok = k < PH * PW && oi >= 0 && oj >= 0 && oi < Ho && oj < Wo;
       const size_t o = ok ? (size_t)oi * Wo + oj : 0;
 #pragma unroll
-      for (int m = 0; m < 3; ++m) sd[m][r][q] = ok ? dmaps[(size_t)(m * C + c) * plane + o] : 0.f;
+      for (int m = 0; m < 3; ++m) pd[m][u] = ok ? dmaps[(size_t)(m * C + c) * plane + o] : 0.f;
     }
+  };
+  fetch(0);
+  for (int c = 0; c < C; ++c) {
+#pragma unroll
+    for (int u = 0; u < SLOTS; ++u) {
+      const int k = threadIdx.x + 256 * u;
+      if (k < PH * PW) {
+#pragma unroll
+        for (int m = 0; m < 3; ++m) sd[m][k] = pd[m][u];
+      }
+    }
+    if (c + 1 < C) fetch(c + 1);
     __syncthreads();
     // horizontal: input column q gathers output columns q - t -> patch column (q + 10 - t)
-    for (int k = threadIdx.x; k < PATCH * TB; k += 256) {
-      const int r = k / TB, q = k % TB;
+    for (int k = threadIdx.x; k < PH * TW; k += 256) {
+      const int r = k >> 5, q = k & 31;
       float a0 = 0.f, a1 = 0.f, a2 = 0.f;
 #pragma unroll
       for (int t = 0; t < WIN; ++t) {
         const float w = win.w[t];
-        a0 += w * sd[0][r][q + WIN - 1 - t];
-        a1 += w * sd[1][r][q + WIN - 1 - t];
-        a2 += w * sd[2][r][q + WIN - 1 - t];
+        const int e = r * PW + q + WIN - 1 - t;
+        a0 += w * sd[0][e];
+        a1 += w * sd[1][e];
+        a2 += w * sd[2][e];
       }
       hd[0][r][q] = a0;
       hd[1][r][q] = a1;
       hd[2][r][q] = a2;
     }
     __syncthreads();
-    const int i = by + ty, j = bx + tx;
-    if (i < H && j < W) {
-      float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+    // vertical: input row ty gathers patch rows ty + 10 - t (t ascending = u descending);
+    // rows ty and ty + 1 share 10 of their 11 taps
+    float s[2][3];
 #pragma unroll
-      for (int t = 0; t < WIN; ++t) {
-        const float w = win.w[t];
-        s0 += w * hd[0][ty + WIN - 1 - t][tx];
-        s1 += w * hd[1][ty + WIN - 1 - t][tx];
-        s2 += w * hd[2][ty + WIN - 1 - t][tx];
+    for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+      for (int m = 0; m < 3; ++m) s[rr][m] = 0.f;
+#pragma unroll
+    for (int u = WIN; u >= 0; --u) {
+#pragma unroll
+      for (int m = 0; m < 3; ++m) {
+        const float h = hd[m][ty + u][tx];
+        if (u < WIN) s[0][m] += win.w[WIN - 1 - u] * h;
+        if (u >= 1) s[1][m] += win.w[WIN - u] * h;
       }
-      const size_t e = ((size_t)i * W + j) * C + c;
-      const float xv = gt[e], yv = pred[e];
-      const float d = yv - xv;
-      const float sgn = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
-      v_pred[e] = gs * (s0 + 2.f * yv * s1 + xv * s2) + gl * sgn;
+    }
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr) {
+      const int i = by + ty + rr, j = bx + tx;
+      if (i < H && j < W) {
+        const size_t e = ((size_t)i * W + j) * C + c;
+        const float xv = gt[e], yv = pred[e];
+        const float d = yv - xv;
+        const float sgn = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
+        v_pred[e] = gs * (s[rr][0] + 2.f * yv * s[rr][1] + xv * s[rr][2]) + gl * sgn;
+      }
     }
     __syncthreads();
   }
@@ -226,7 +286,7 @@ using namespace gs;
 
 extern "C" int gsplat_l1_ssim_num_blocks(int img_height, int img_width) {
   if (img_height <= 0 || img_width <= 0) return 0;
-  return (int)(cdiv(img_width, TB) * cdiv(img_height, TB));
+  return (int)(cdiv(img_width, TW) * cdiv(img_height, TH));
 }
 
 static bool l1_ssim_args_ok(int H, int W, int C, const char *what) {

@@ -12,7 +12,7 @@ from gaussctrl_exp_amd.train import splatfacto_loss
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("H,W,C,seed", [(11, 11, 3, 0), (48, 64, 3, 1), (75, 100, 3, 2),
-                                         (128, 96, 1, 3), (33, 17, 4, 4)])
+                                         (128, 96, 1, 3), (33, 17, 4, 4), (270, 481, 3, 5)])
 def test_fused_loss_matches_torch(gpu, H, W, C, seed):
     g = torch.Generator().manual_seed(seed)
     gt = torch.rand(H, W, C, generator=g)
