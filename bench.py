@@ -136,6 +136,28 @@ def pmc_traffic(entry):
     return int(tot) if hit else None
 
 
+def pmc_valu_busy(entry, ms_per_call, n_simd=256 * 4, clock_hz=2.4e9):
+    """Fraction of the chip's VALU issue slots the entry's kernels used: rocprofv3
+    SQ_ACTIVE_INST_VALU (quad-cycles, one fp32 wave64 VALU instruction each;
+    MI355X_MICROARCH.md) per call / (SIMDs x call duration in quad-cycles at the peak engine
+    clock).  The blend kernels are VALU-issue bound, so this -- not the HBM fraction -- is the
+    roofline that binds them.  None without a PMC summary."""
+    try:
+        with open(PMC_TRAFFIC) as f:
+            kern = json.load(f)["kernels"]
+    except (OSError, ValueError, KeyError):
+        return None
+    pats = ENTRY_KERNELS.get(entry)
+    tot, hit = 0.0, False
+    for name, v in kern.items():
+        if pats and any(p in name for p in pats) and v.get("valu_quad_cycles") is not None:
+            tot += v["valu_quad_cycles"]
+            hit = True
+    if not hit or not ms_per_call:
+        return None
+    return round(tot / (n_simd * ms_per_call * 1e-3 * clock_hz / 4.0), 3)
+
+
 def cpu_baseline(scene, cam, sh_degree, budget_tiles=64, seed=0):
     """C oracle (single-threaded restatement of gsplat) on a bounded sample: the full
     per-Gaussian stages (project, SH, map+stable sort+bins) plus rasterize fwd+bwd on
@@ -291,6 +313,7 @@ def main():
         "unit": "GB/s",
         "frac": round(dom_bytes / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if dom_bytes else None,
         "traffic": pmc_traffic(dom),
+        "valu_busy": pmc_valu_busy(dom, dom_ms),
         "step_algorithmic_bytes": step_bytes,
         "step_frac": round(step_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
         "roofline_mpix_s": round(P / (step_bytes / (HBM_PEAK_GBS * 1e9)) / 1e6, 1),

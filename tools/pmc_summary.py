@@ -29,11 +29,13 @@ for k, d in sorted(acc.items()):
     rows.append(row)
 cols = sorted({c for r in rows for c in r if c != "kernel"})
 if len(sys.argv) > 3:
-    tj = {r["kernel"]: {"fetch_kb": r.get("FETCH_SIZE"), "write_kb": r.get("WRITE_SIZE")}
+    tj = {r["kernel"]: {"fetch_kb": r.get("FETCH_SIZE"), "write_kb": r.get("WRITE_SIZE"),
+                        "valu_quad_cycles": r.get("SQ_ACTIVE_INST_VALU")}
           for r in rows if "FETCH_SIZE" in r and "WRITE_SIZE" in r}
     with open(sys.argv[3], "w") as f:
-        json.dump({"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, "
-                             "tools/pmc_bench.sh", "kernels": tj}, f, indent=1)
+        json.dump({"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE / SQ_ACTIVE_INST_VALU "
+                             "(quad-cycles), separate passes, tools/pmc_bench.sh",
+                   "kernels": tj}, f, indent=1)
 out = sys.argv[2] if len(sys.argv) > 2 else None
 w = csv.writer(open(out, "w", newline="") if out else sys.stdout)
 w.writerow(["kernel"] + cols)
