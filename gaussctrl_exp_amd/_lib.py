@@ -49,6 +49,13 @@ SIGNATURES = {
                                       _P, _P]),
     "gsplat_rasterize_forward_rgbd": (_I, [_I, _I, _I, _I] + [_P] * 13),
     "gsplat_rasterize_backward_workspace_size": (_SZ, [_I, _I]),
+    "gsplat_rasterize_chunk_size": (_I, [_I, _I, _I64]),
+    "gsplat_rasterize_checkpoint_bytes": (_SZ, [_I, _I, _I64, _I]),
+    "gsplat_rasterize_forward_chunked": (_I, [_I, _I, _I, _I] + [_P] * 10 + [_I64, _I, _P, _SZ,
+                                                                             _P]),
+    "gsplat_rasterize_backward_chunked": (_I, [_I, _I, _I, _I, _I] + [_P] * 11 + [_F] +
+                                          [_P] * 4 + [_I64, _I, _P, _SZ, _P, _SZ, _P]),
+    "gsplat_debug_set_chunk": (_I, [_I]),
     "gsplat_debug_set_raster_variant": (_I, [_I, _I, _I]),
     "gsplat_debug_sort_timing": (_I, [_P, _I]),
     "gsplat_debug_sort_scheme": (_I, [_I]),
@@ -60,7 +67,7 @@ SIGNATURES = {
                                        _P, _P, _P, _F, _P, _P, _P, _P, _P, _SZ, _P]),
 }
 
-ABI_VERSION = 4  # include/gsplat_mi355x.h GSPLAT_MI355X_ABI_VERSION
+ABI_VERSION = 5  # include/gsplat_mi355x.h GSPLAT_MI355X_ABI_VERSION
 
 _lib = None
 

@@ -32,6 +32,8 @@
 //    accumulators sized by a compile-time channel bound.
 #include "common.h"
 
+#include <algorithm>
+
 namespace gs {
 namespace {
 
@@ -154,17 +156,22 @@ struct WaveRect {
   int tile, j, i0;
   float rx0, rx1, ry0, ry1;
 };
+// Work slot of this wave: blockIdx.x * (tiles per workgroup) + wave / (waves per tile).
 template <int PXL, int COLS>
-__device__ __forceinline__ WaveRect wave_rect(int tbx, int tby, int H, int W) {
+__device__ __forceinline__ int wave_slot() {
+  constexpr int WPT = (GS_BLOCK / COLS) * (GS_BLOCK / ((64 / COLS) * PXL));
+  return blockIdx.x * (4 / WPT) + (threadIdx.x >> 6) / WPT;
+}
+template <int PXL, int COLS>
+__device__ __forceinline__ WaveRect wave_rect(int tbx, int tby, int H, int W, int tile = -1) {
   constexpr int LROWS = 64 / COLS;      // rows per lane pass
   constexpr int WROWS = LROWS * PXL;    // rows per wave
   constexpr int WX = GS_BLOCK / COLS, WY = GS_BLOCK / WROWS;
   constexpr int WPT = WX * WY;          // waves per tile
   static_assert(WPT >= 1 && WPT <= 4 && 4 % WPT == 0, "wave footprint must tile 16x16");
-  constexpr int TPBLK = 4 / WPT;        // tiles per workgroup
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   WaveRect r;
-  r.tile = blockIdx.x * TPBLK + wave / WPT;
+  r.tile = tile >= 0 ? tile : wave_slot<PXL, COLS>();
   const int wt = wave % WPT;
   const int tx = r.tile % tbx, ty = r.tile / tbx;
   const int c0 = tx * GS_BLOCK + (wt % WX) * COLS, r0 = ty * GS_BLOCK + (wt / WX) * WROWS;
@@ -289,14 +296,20 @@ __global__ __launch_bounds__(256) void raster_fwd3_kernel(
 // depth, accumulated with the same weight as the colour channels into out_depth -- exactly
 // channel 0 of a second render with colours = depth and a zero background (gc_model.py:
 // 225-238), without the second binning and traversal.
-template <int PXL, int COLS, bool DEPTH = false>
+//
+// CKPT (list-split backward, see chunk_plan_kernel): for a tile whose list is longer than
+// `chunk`, each pixel's state (T, accumulated colour) is recorded after every `chunk` list
+// positions and at the end, so the backward can start each chunk from it.
+template <int PXL, int COLS, bool DEPTH = false, bool CKPT = false>
 __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
     int tbx, int tby, int H, int W, const int *__restrict__ gids, const int2 *__restrict__ bins,
     const float2 *__restrict__ xys, const float *__restrict__ conics,
     const float *__restrict__ colors, const float *__restrict__ opacity,
     const float *__restrict__ background, float *__restrict__ out_img,
     float *__restrict__ final_Ts, int *__restrict__ final_idx,
-    const float *__restrict__ depths = nullptr, float *__restrict__ out_depth = nullptr) {
+    const float *__restrict__ depths = nullptr, float *__restrict__ out_depth = nullptr,
+    int chunk = 0, const int *__restrict__ ckpt_off = nullptr,
+    float4 *__restrict__ ckpt = nullptr) {
   const WaveRect R = wave_rect<PXL, COLS>(tbx, tby, H, W);
   if (!R.live) return;  // wave-uniform
   __shared__ GStage lds[4][64];
@@ -319,7 +332,25 @@ __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
   }
   const int2 range = bins[tile];
   GStage *stage = lds[wave];
+  // checkpoints (CKPT): m states per chunked tile, state k after list position
+  // range.x + (k + 1) * chunk (k = m - 1: the final state)
+  int m = 0, nextk = 0;
+  if (CKPT) {
+    const int len = range.y - range.x;
+    if (len > chunk) m = (len + chunk - 1) / chunk;
+  }
+  auto write_ckpt = [&](int kk) {  // (addresses recomputed here: fewer live registers)
+    const size_t base = ((size_t)ckpt_off[tile] + kk) * (GS_BLOCK * GS_BLOCK);
+    const int ly0 = i0 - (tile / tbx) * GS_BLOCK, lx = j - (tile % tbx) * GS_BLOCK;
+#pragma unroll
+    for (int k = 0; k < PXL; ++k)
+      if (i0 + LROWS * k < H && j < W)
+        ckpt[base + (ly0 + LROWS * k) * GS_BLOCK + lx] = make_float4(T[k], cr[k], cg[k], cb[k]);
+  };
   for (int b = range.x; b < range.y; b += 64) {
+    if (CKPT && m) {
+      if (nextk < m - 1 && b - range.x == (nextk + 1) * chunk) write_ckpt(nextk++);
+    }
     bool all_done = true;
 #pragma unroll
     for (int k = 0; k < PXL; ++k) all_done = all_done && done[k];
@@ -374,6 +405,9 @@ __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
       if (__all(fin)) break;
     }
     wave_lds_sync();
+  }
+  if (CKPT) {  // boundaries after an early exit, and the final state
+    for (int kk = nextk; kk < m; ++kk) write_ckpt(kk);
   }
   const float bg0 = background[0], bg1 = background[1], bg2 = background[2];
 #pragma unroll
@@ -623,7 +657,13 @@ __global__ __launch_bounds__(256) void raster_bwd3_kernel(
 // sigma gradient as moments V = sum v_sigma, Vy = sum v_sigma dy, Vyy = sum v_sigma dy^2
 // (dx is constant along the lane's column), from which
 //   v_conic = 0.5 (dx^2 V, dx Vy, Vyy),  v_xy = (a dx V + b Vy, b dx V + c Vy).
-template <int NP, bool ATOMICS, int COLS>
+//
+// CHUNKED (list-split backward): the work slots are (tile, chunk) items of chunk_plan_kernel's
+// table instead of tiles.  Chunk j of a tile covers list positions
+// [range.x + j * chunk, range.x + (j + 1) * chunk) and starts from the forward's checkpoint
+// after its last position: T = checkpoint T, and the colour behind it, Sb = (C_final - C_j) . v,
+// instead of T_final and 0 -- so long lists and small images (few tiles) still fill the GPU.
+template <int NP, bool ATOMICS, int COLS, bool CHUNKED = false>
 __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
     int tbx, int tby, int H, int W, const int *__restrict__ gids, const int2 *__restrict__ bins,
     const float2 *__restrict__ xys, const float *__restrict__ conics,
@@ -631,10 +671,19 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
     const float *__restrict__ background, const float *__restrict__ final_Ts,
     const int *__restrict__ final_idx, const float *__restrict__ v_out,
     const float *__restrict__ v_out_alpha, float alpha_max, float *__restrict__ rec,
-    bool stage_only) {
+    bool stage_only, int chunk = 0, const int *__restrict__ item_off = nullptr,
+    const int *__restrict__ item_tile = nullptr, const int *__restrict__ ckpt_off = nullptr,
+    const float4 *__restrict__ ckpt = nullptr) {
   constexpr int PXL = 2 * NP;
   constexpr int LROWS = 64 / COLS;
-  const WaveRect R = wave_rect<PXL, COLS>(tbx, tby, H, W);
+  int ctile = -1, cj = 0;
+  if (CHUNKED) {
+    const int slot = wave_slot<PXL, COLS>();
+    if (slot >= item_off[tbx * tby]) return;  // wave-uniform: past the last item
+    ctile = item_tile[slot];
+    cj = slot - item_off[ctile];
+  }
+  const WaveRect R = wave_rect<PXL, COLS>(tbx, tby, H, W, ctile);
   if (!R.live) return;  // wave-uniform
   __shared__ GStage lds[4][64];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -670,15 +719,41 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
     binf[k] = bf;
     maxbin = max(maxbin, bf);
   }
+  const int2 range = bins[tile];
+  int lo = range.x, hi = range.y;
+  if (CHUNKED) {
+    const int len = range.y - range.x;
+    const int m = len > chunk ? (len + chunk - 1) / chunk : 1;
+    if (m > 1) {
+      lo = range.x + cj * chunk;
+      hi = min(lo + chunk, range.y);
+      if (cj < m - 1) {  // start from the checkpoint after this chunk
+        const size_t cb = (size_t)ckpt_off[tile] * (GS_BLOCK * GS_BLOCK);
+        const int oy = (tile / tbx) * GS_BLOCK, ox = (tile % tbx) * GS_BLOCK;
+#pragma unroll
+        for (int k = 0; k < PXL; ++k) {
+          const int i = i0 + LROWS * k, p = k >> 1;
+          if (i < H && j < W) {
+            const int lpix = (i - oy) * GS_BLOCK + (j - ox);
+            const float4 cj4 = ckpt[cb + (size_t)cj * (GS_BLOCK * GS_BLOCK) + lpix];
+            const float4 cf4 = ckpt[cb + (size_t)(m - 1) * (GS_BLOCK * GS_BLOCK) + lpix];
+            const float vr_ = (k & 1) ? vr[p].y : vr[p].x, vg_ = (k & 1) ? vg[p].y : vg[p].x,
+                        vb_ = (k & 1) ? vb[p].y : vb[p].x;
+            const float sb = (cf4.y - cj4.y) * vr_ + (cf4.z - cj4.z) * vg_ + (cf4.w - cj4.w) * vb_;
+            if (k & 1) { T[p].y = cj4.x; Sb[p].y = sb; } else { T[p].x = cj4.x; Sb[p].x = sb; }
+          }
+        }
+      }
+    }
+  }
   maxbin = wave_max_int(maxbin);
   const int slot = reduce9_slot();
-  const int2 range = bins[tile];
-  const int last = min(maxbin, range.y - 1);
+  const int last = min(maxbin, hi - 1);
   GStage *stage = lds[wave];
-  for (int b = last; b >= range.x; b -= 64) {
+  for (int b = last; b >= lo; b -= 64) {
     const int idx = b - lane;
     GStage s;
-    const bool keep = idx >= range.x &&
+    const bool keep = idx >= lo &&
                       stage_gaussian(idx, gids, xys, conics, colors, opacity, rx0, rx1, ry0,
                                      ry1, s);
     const unsigned long long kmask = __ballot(keep);
@@ -763,6 +838,57 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
       }
     }
     wave_lds_sync();
+  }
+}
+
+// List-split plan (one workgroup): per tile, the number of backward items (chunks of the
+// depth-sorted list, 1 for a tile no longer than `chunk`, 0 for an empty one) and of forward
+// checkpoints (as many as chunks for a split tile, else 0); exclusive scans of both give
+// item_off[T + 1] / ckpt_off[T + 1], and item_tile[] maps each item back to its tile.
+__global__ __launch_bounds__(1024) void chunk_plan_kernel(int T, const int2 *__restrict__ bins,
+                                                          int chunk, int *__restrict__ item_off,
+                                                          int *__restrict__ ckpt_off,
+                                                          int *__restrict__ item_tile) {
+  __shared__ int sa[1024], sc[1024];
+  const int tid = threadIdx.x;
+  const int per = (T + 1023) / 1024;
+  const int t0 = min(T, tid * per), t1 = min(T, t0 + per);
+  auto items = [&](int t, int &mi, int &mc) {
+    const int2 r = bins[t];
+    const int len = r.y - r.x;
+    mi = len <= 0 ? 0 : (len > chunk ? (len + chunk - 1) / chunk : 1);
+    mc = len > chunk ? mi : 0;
+  };
+  int a = 0, c = 0;
+  for (int t = t0; t < t1; ++t) {
+    int mi, mc;
+    items(t, mi, mc);
+    a += mi;
+    c += mc;
+  }
+  sa[tid] = a;
+  sc[tid] = c;
+  __syncthreads();
+  for (int d = 1; d < 1024; d <<= 1) {  // inclusive Hillis-Steele scan
+    const int va = tid >= d ? sa[tid - d] : 0, vc = tid >= d ? sc[tid - d] : 0;
+    __syncthreads();
+    sa[tid] += va;
+    sc[tid] += vc;
+    __syncthreads();
+  }
+  int ra = sa[tid] - a, rc = sc[tid] - c;
+  for (int t = t0; t < t1; ++t) {
+    int mi, mc;
+    items(t, mi, mc);
+    item_off[t] = ra;
+    ckpt_off[t] = rc;
+    for (int k = 0; k < mi; ++k) item_tile[ra + k] = t;
+    ra += mi;
+    rc += mc;
+  }
+  if (tid == 1023) {
+    item_off[T] = sa[1023];
+    ckpt_off[T] = sc[1023];
   }
 }
 
@@ -1004,6 +1130,65 @@ using namespace gs;
       hipLaunchKernelGGL(KERNEL<64>, dim3(T), dim3(256), 0, st, __VA_ARGS__);             \
   } while (0)
 
+// ---- list-split backward (checkpointed forward) ----------------------------------------
+// Workspace layout (gsplat_rasterize_checkpoint_bytes): item_off[T+1], ckpt_off[T+1],
+// item_tile[T + ceil(I/chunk)], 16-B aligned float4 ckpt[(2 ceil(I/chunk) + 1) * 256].
+int g_chunk_override = 0;  // gsplat_debug_set_chunk: 0 auto, > 0 forced, < 0 off
+struct ChunkWs {
+  int *item_off, *ckpt_off, *item_tile;
+  float4 *ckpt;
+  long long items_bound, ckpt_bound;
+  size_t bytes;
+};
+static ChunkWs carve_chunk_ws(void *base, long long T, long long I, int chunk) {
+  ChunkWs w{};
+  const long long per = (I + chunk - 1) / chunk;
+  w.items_bound = T + per;
+  w.ckpt_bound = 2 * per + 1;
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    const size_t o = off;
+    off += (bytes + 255) & ~(size_t)255;
+    return (char *)base + o;
+  };
+  w.item_off = (int *)take((size_t)(T + 1) * sizeof(int));
+  w.ckpt_off = (int *)take((size_t)(T + 1) * sizeof(int));
+  w.item_tile = (int *)take((size_t)w.items_bound * sizeof(int));
+  w.ckpt = (float4 *)take((size_t)w.ckpt_bound * GS_BLOCK * GS_BLOCK * sizeof(float4));
+  w.bytes = off;
+  return w;
+}
+static bool default_variants() {
+  return g_fwd_pxl == FWD_PXL && g_bwd_pxl == BWD_PXL && g_bwd_flags == 0;
+}
+
+extern "C" int gsplat_rasterize_chunk_size(int tile_bounds_x, int tile_bounds_y,
+                                           int64_t num_intersects) {
+  if (g_chunk_override < 0 || !default_variants() || num_intersects <= 0) return 0;
+  if (g_chunk_override > 0) return (g_chunk_override + 63) / 64 * 64;
+  // Split only frames with too few tiles to occupy the chip: the backward runs 2 waves per
+  // tile and ~7 fit per SIMD (7,168 on 256 CUs), so below ~3,584 tiles (e.g. 512x512 =
+  // 1,024) CUs sit idle and splitting lists into 256-position chunks pays (bear c3: backward
+  // 0.269 -> 0.195 ms).  At 1080x1080 (4,624 tiles) the tile count already fills the chip
+  // and splitting measured 12-30 % slower (pixels saturate early, so the front chunk keeps
+  // the critical path while checkpoints cost traffic) -- see DESIGN.md.
+  const long long T = (long long)tile_bounds_x * tile_bounds_y;
+  return T < 3584 ? 256 : 0;
+}
+
+extern "C" size_t gsplat_rasterize_checkpoint_bytes(int tile_bounds_x, int tile_bounds_y,
+                                                    int64_t num_intersects, int chunk) {
+  if (chunk <= 0 || chunk % 64 || tile_bounds_x <= 0 || tile_bounds_y <= 0 || num_intersects < 0)
+    return 0;
+  return carve_chunk_ws(nullptr, (long long)tile_bounds_x * tile_bounds_y, num_intersects, chunk)
+      .bytes;
+}
+
+extern "C" int gsplat_debug_set_chunk(int chunk) {
+  g_chunk_override = chunk;
+  return 0;
+}
+
 extern "C" int gsplat_rasterize_forward(int tile_bounds_x, int tile_bounds_y, int img_height,
                                         int img_width, int channels,
                                         const int32_t *gaussian_ids_sorted,
@@ -1177,4 +1362,87 @@ extern "C" int gsplat_rasterize_backward(int tile_bounds_x, int tile_bounds_y, i
                 v_output_alpha, alpha_max, v_xy, v_conic, v_colors, v_opacity);
   }
   return check_launch("rasterize_backward");
+}
+
+extern "C" int gsplat_rasterize_forward_chunked(
+    int tile_bounds_x, int tile_bounds_y, int img_height, int img_width,
+    const int32_t *gaussian_ids_sorted, const int32_t *tile_bins, const float *xys,
+    const float *conics, const float *colors, const float *opacity, const float *background,
+    float *out_img, float *final_Ts, int32_t *final_idx, int64_t num_intersects, int chunk,
+    void *checkpoints, size_t checkpoint_bytes, void *stream) {
+  if (chunk <= 0)
+    return gsplat_rasterize_forward(tile_bounds_x, tile_bounds_y, img_height, img_width, 3,
+                                    gaussian_ids_sorted, tile_bins, xys, conics, colors, opacity,
+                                    background, out_img, final_Ts, final_idx, stream);
+  hipStream_t st = (hipStream_t)stream;
+  if (tile_bounds_x <= 0 || tile_bounds_y <= 0 || img_height <= 0 || img_width <= 0 ||
+      (long long)tile_bounds_x * GS_BLOCK < img_width ||
+      (long long)tile_bounds_y * GS_BLOCK < img_height || chunk % 64 || num_intersects < 0) {
+    set_error("rasterize_forward_chunked: bad sizes (tiles=%dx%d H=%d W=%d chunk=%d)",
+              tile_bounds_x, tile_bounds_y, img_height, img_width, chunk);
+    return 1;
+  }
+  const int T = tile_bounds_x * tile_bounds_y;
+  const ChunkWs w = carve_chunk_ws(checkpoints, T, num_intersects, chunk);
+  if (!checkpoints || checkpoint_bytes < w.bytes || !default_variants()) {
+    set_error("rasterize_forward_chunked: checkpoint buffer %zu < %zu bytes (or non-default "
+              "raster variant)", checkpoint_bytes, w.bytes);
+    return 1;
+  }
+  hipLaunchKernelGGL(chunk_plan_kernel, dim3(1), dim3(1024), 0, st, T, (const int2 *)tile_bins,
+                     chunk, w.item_off, w.ckpt_off, w.item_tile);
+  hipLaunchKernelGGL((raster_fwd3u_kernel<1, 8, false, true>),
+                     dim3(cdiv(T, (tiles_per_block<1, 8>()))), dim3(256), 0, st, tile_bounds_x,
+                     tile_bounds_y, img_height, img_width, gaussian_ids_sorted,
+                     (const int2 *)tile_bins, (const float2 *)xys, conics, colors, opacity,
+                     background, out_img, final_Ts, final_idx, nullptr, nullptr, chunk,
+                     w.ckpt_off, w.ckpt);
+  return check_launch("rasterize_forward_chunked");
+}
+
+extern "C" int gsplat_rasterize_backward_chunked(
+    int tile_bounds_x, int tile_bounds_y, int img_height, int img_width, int num_points,
+    const int32_t *gaussian_ids_sorted, const int32_t *tile_bins, const float *xys,
+    const float *conics, const float *colors, const float *opacity, const float *background,
+    const float *final_Ts, const int32_t *final_idx, const float *v_output,
+    const float *v_output_alpha, float alpha_max, float *v_xy, float *v_conic, float *v_colors,
+    float *v_opacity, int64_t num_intersects, int chunk, const void *checkpoints,
+    size_t checkpoint_bytes, void *workspace, size_t workspace_bytes, void *stream) {
+  if (chunk <= 0)
+    return gsplat_rasterize_backward(tile_bounds_x, tile_bounds_y, img_height, img_width, 3,
+                                     num_points, gaussian_ids_sorted, tile_bins, xys, conics,
+                                     colors, opacity, background, final_Ts, final_idx, v_output,
+                                     v_output_alpha, alpha_max, v_xy, v_conic, v_colors,
+                                     v_opacity, workspace, workspace_bytes, stream);
+  hipStream_t st = (hipStream_t)stream;
+  if (tile_bounds_x <= 0 || tile_bounds_y <= 0 || img_height <= 0 || img_width <= 0 ||
+      num_points < 0 || (long long)tile_bounds_x * GS_BLOCK < img_width ||
+      (long long)tile_bounds_y * GS_BLOCK < img_height || chunk % 64 || num_intersects < 0) {
+    set_error("rasterize_backward_chunked: bad sizes (tiles=%dx%d H=%d W=%d N=%d chunk=%d)",
+              tile_bounds_x, tile_bounds_y, img_height, img_width, num_points, chunk);
+    return 1;
+  }
+  const int T = tile_bounds_x * tile_bounds_y;
+  const ChunkWs w =
+      carve_chunk_ws(const_cast<void *>(checkpoints), T, num_intersects, chunk);
+  const size_t need = gsplat_rasterize_backward_workspace_size(num_points, 3);
+  if (!checkpoints || checkpoint_bytes < w.bytes || workspace_bytes < need ||
+      (need && !workspace) || !default_variants()) {
+    set_error("rasterize_backward_chunked: buffers too small (checkpoints %zu < %zu or "
+              "workspace %zu < %zu) or non-default raster variant",
+              checkpoint_bytes, w.bytes, workspace_bytes, need);
+    return 1;
+  }
+  if (num_points == 0) return check_launch("rasterize_backward_chunked");
+  float *rec = (float *)workspace;
+  note(hipMemsetAsync(rec, 0, need, st), "hipMemsetAsync");
+  hipLaunchKernelGGL((raster_bwd3p_kernel<1, true, 16, true>),
+                     dim3((unsigned)cdiv(w.items_bound, (long long)(tiles_per_block<2, 16>()))),
+                     dim3(256), 0, st, tile_bounds_x, tile_bounds_y, img_height, img_width,
+                     gaussian_ids_sorted, (const int2 *)tile_bins, (const float2 *)xys, conics,
+                     colors, opacity, background, final_Ts, final_idx, v_output, v_output_alpha,
+                     alpha_max, rec, false, chunk, w.item_off, w.item_tile, w.ckpt_off, w.ckpt);
+  hipLaunchKernelGGL(split_grads_kernel, dim3(cdiv(num_points, 256)), dim3(256), 0, st,
+                     num_points, (const float4 *)rec, 0.5f, v_xy, v_conic, v_colors, v_opacity);
+  return check_launch("rasterize_backward_chunked");
 }

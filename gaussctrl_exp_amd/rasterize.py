@@ -229,9 +229,24 @@ class _RasterizeGaussians(Function):
             final_Ts = torch.empty((H, W), device=dev, dtype=torch.float32)
             final_idx = torch.empty((H, W), device=dev, dtype=torch.int32)
             P = _lib.ptr
-            _lib.call("gsplat_rasterize_forward", tbx, tby, H, W, C, P(gaussian_ids_sorted),
-                      P(tile_bins), P(xys), P(conics), P(colors), P(opacity), P(background),
-                      P(out_img), P(final_Ts), P(final_idx), _lib.stream(dev))
+            # list-split backward (C = 3, gradients wanted): the forward records checkpoints
+            chunk = _lib.query("gsplat_rasterize_chunk_size", tbx, tby, num_intersects) \
+                if C == 3 and any(ctx.needs_input_grad) else 0
+            if chunk > 0:
+                ckpt = torch.empty((_lib.query("gsplat_rasterize_checkpoint_bytes", tbx, tby,
+                                               num_intersects, chunk),),
+                                   device=dev, dtype=torch.uint8)
+                _lib.call("gsplat_rasterize_forward_chunked", tbx, tby, H, W,
+                          P(gaussian_ids_sorted), P(tile_bins), P(xys), P(conics), P(colors),
+                          P(opacity), P(background), P(out_img), P(final_Ts), P(final_idx),
+                          num_intersects, chunk, P(ckpt), ckpt.numel(), _lib.stream(dev))
+                ctx.chunk, ctx.ckpt = chunk, ckpt
+            else:
+                _lib.call("gsplat_rasterize_forward", tbx, tby, H, W, C, P(gaussian_ids_sorted),
+                          P(tile_bins), P(xys), P(conics), P(colors), P(opacity), P(background),
+                          P(out_img), P(final_Ts), P(final_idx), _lib.stream(dev))
+        if not hasattr(ctx, "chunk"):
+            ctx.chunk, ctx.ckpt = 0, None
 
         ctx.img_width = W
         ctx.img_height = H
@@ -274,11 +289,19 @@ class _RasterizeGaussians(Function):
             tby = (H + BLOCK_Y - 1) // BLOCK_Y
             wsz = _lib.query("gsplat_rasterize_backward_workspace_size", num_points, C)
             ws = torch.empty((max(wsz, 1),), device=dev, dtype=torch.uint8)
-            _lib.call("gsplat_rasterize_backward", tbx, tby, H, W, C, num_points,
-                      P(gaussian_ids_sorted), P(tile_bins), P(xys), P(conics), P(colors),
-                      P(opacity), P(background), P(final_Ts), P(final_idx), P(v_out_img),
-                      P(v_out_alpha), float(BACKWARD_ALPHA_CLAMP), P(v_xy), P(v_conic),
-                      P(v_colors), P(v_opacity), P(ws), wsz, _lib.stream(dev))
+            if ctx.chunk > 0:
+                _lib.call("gsplat_rasterize_backward_chunked", tbx, tby, H, W, num_points,
+                          P(gaussian_ids_sorted), P(tile_bins), P(xys), P(conics), P(colors),
+                          P(opacity), P(background), P(final_Ts), P(final_idx), P(v_out_img),
+                          P(v_out_alpha), float(BACKWARD_ALPHA_CLAMP), P(v_xy), P(v_conic),
+                          P(v_colors), P(v_opacity), ctx.num_intersects, ctx.chunk,
+                          P(ctx.ckpt), ctx.ckpt.numel(), P(ws), wsz, _lib.stream(dev))
+            else:
+                _lib.call("gsplat_rasterize_backward", tbx, tby, H, W, C, num_points,
+                          P(gaussian_ids_sorted), P(tile_bins), P(xys), P(conics), P(colors),
+                          P(opacity), P(background), P(final_Ts), P(final_idx), P(v_out_img),
+                          P(v_out_alpha), float(BACKWARD_ALPHA_CLAMP), P(v_xy), P(v_conic),
+                          P(v_colors), P(v_opacity), P(ws), wsz, _lib.stream(dev))
 
         return (
             v_xy,  # xys

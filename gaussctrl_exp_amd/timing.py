@@ -26,7 +26,9 @@ class CallTimer:
         s.record()
         rc = _orig_call(name, *args)
         e.record()
-        self.events[name].append((s, e))
+        # the list-split variants are the same entry (gsplat_rasterize_forward/_backward)
+        key = name[:-len("_chunked")] if name.endswith("_chunked") else name
+        self.events[key].append((s, e))
         return rc
 
     def summary(self):

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define GSPLAT_MI355X_ABI_VERSION 4
+#define GSPLAT_MI355X_ABI_VERSION 5
 
 int gsplat_abi_version(void);
 const char *gsplat_last_error(void);
@@ -156,6 +156,37 @@ int gsplat_rasterize_forward_rgbd(int tile_bounds_x, int tile_bounds_y, int img_
  * (gsplat 0.1.x uses 0.99f).  workspace holds the per-Gaussian gradient
  * records the kernel accumulates into (gsplat_rasterize_backward_workspace_size bytes;
  * may be 0 / NULL when that size is 0). */
+/* List-split backward (C = 3; no gsplat counterpart).  gsplat's backward walks each tile's
+ * whole depth-sorted list from the back; with few tiles (small images) or a few very long
+ * lists (real scenes) that leaves the GPU idle.  The chunked forward records, for every tile
+ * whose list is longer than `chunk` (a multiple of 64), each pixel's (T, accumulated RGB)
+ * after every `chunk` list positions and at the end; the chunked backward then processes
+ * every (tile, chunk) pair independently, starting from those states.  Outputs equal the
+ * unchunked entry points' (forward: identical; gradients: within fp32 rounding).
+ * gsplat_rasterize_chunk_size picks `chunk` (0 = do not split) for a frame's intersection
+ * count; gsplat_rasterize_checkpoint_bytes sizes the buffer the forward fills and the
+ * backward reads.  chunk <= 0 makes both entries the plain ones. */
+int gsplat_rasterize_chunk_size(int tile_bounds_x, int tile_bounds_y, int64_t num_intersects);
+size_t gsplat_rasterize_checkpoint_bytes(int tile_bounds_x, int tile_bounds_y,
+                                         int64_t num_intersects, int chunk);
+int gsplat_rasterize_forward_chunked(
+    int tile_bounds_x, int tile_bounds_y, int img_height, int img_width,
+    const int32_t *gaussian_ids_sorted, const int32_t *tile_bins, const float *xys,
+    const float *conics, const float *colors, const float *opacity, const float *background,
+    float *out_img, float *final_Ts, int32_t *final_idx, int64_t num_intersects, int chunk,
+    void *checkpoints, size_t checkpoint_bytes, void *stream);
+int gsplat_rasterize_backward_chunked(
+    int tile_bounds_x, int tile_bounds_y, int img_height, int img_width, int num_points,
+    const int32_t *gaussian_ids_sorted, const int32_t *tile_bins, const float *xys,
+    const float *conics, const float *colors, const float *opacity, const float *background,
+    const float *final_Ts, const int32_t *final_idx, const float *v_output,
+    const float *v_output_alpha, float alpha_max, float *v_xy, float *v_conic, float *v_colors,
+    float *v_opacity, int64_t num_intersects, int chunk, const void *checkpoints,
+    size_t checkpoint_bytes, void *workspace, size_t workspace_bytes, void *stream);
+/* Debug: force the list-split chunk (> 0, rounded up to 64), disable it (< 0) or restore
+ * the automatic choice (0). */
+int gsplat_debug_set_chunk(int chunk);
+
 size_t gsplat_rasterize_backward_workspace_size(int num_points, int channels);
 int gsplat_rasterize_backward(int tile_bounds_x, int tile_bounds_y, int img_height,
                               int img_width, int channels, int num_points,

@@ -32,7 +32,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_host_queries_without_gpu():
     from gaussctrl_exp_amd import _lib
-    assert _lib.lib().gsplat_abi_version() == _lib.ABI_VERSION == 4
+    assert _lib.lib().gsplat_abi_version() == _lib.ABI_VERSION == 5
     assert _lib.query("gsplat_bin_count_workspace_size", 1000) > 1000 * 16
     assert _lib.query("gsplat_bin_emit_workspace_size", 10 ** 6) >= 5 * 4 * 10 ** 6
     assert _lib.query("gsplat_sort_isect_pairs_workspace_size", 0) > 0

@@ -30,9 +30,11 @@ def _np(t):
     return t.detach().cpu().numpy()
 
 
-@pytest.fixture(scope="module")
-def headline(gpu, oracle_lib):
-    sc, cam = bench.make_workload("headline", 0, gpu)
+@pytest.fixture(scope="module", params=["headline", "c3"])
+def headline(request, gpu, oracle_lib):
+    """The headline scene, and the bear scene at 512x512 (c3: few tiles, imbalanced lists --
+    the list-split backward is on there)."""
+    sc, cam = bench.make_workload(request.param, 0, gpu)
     cam = cam.to(gpu)
     with torch.no_grad():
         g = project_gaussians(sc.means, torch.exp(sc.scales), 1,
@@ -50,7 +52,7 @@ def headline(gpu, oracle_lib):
 @pytest.mark.parametrize("scheme", [1, 0])
 def test_headline_binning_bitexact(gpu, headline, scheme):
     h, cam = headline, headline["cam"]
-    assert h["ref"]["num_intersects"] > 4 << 20  # the 16-keys-per-thread tile sort
+    assert h["ref"]["num_intersects"] > 1 << 20
     _lib.call("gsplat_debug_sort_scheme", scheme)
     try:
         I, gids, bins = bin_gaussians(h["xys"], h["depths"], h["radii"], h["nth"], cam.height,
@@ -118,11 +120,18 @@ def test_headline_raster_on_sampled_tiles(gpu, headline):
                                         v_img.numpy(), v_alpha.numpy(),
                                         alpha_max=R.BACKWARD_ALPHA_CLAMP, tile_list=tiles,
                                         return_abs=True)
+    # gsplat (and the oracle) recover each Gaussian's T by dividing T_final back through
+    # every later Gaussian of the tile: fp32 drift up to ~L 2^-24 relative for a list of L.
+    # The list-split backward (on for 512x512 frames) starts each 256-position chunk from
+    # the forward's recorded T instead, so it may differ from the oracle by that drift.
+    split = _lib.query("gsplat_rasterize_chunk_size", tb[0], tb[1], I) > 0
+    lmax = int((ref["tile_bins"][:, 1] - ref["tile_bins"][:, 0]).max())
+    drift = lmax * 2.0 ** -24 if split else 0.0
     for k, (name, g) in enumerate((("xys", xy.grad), ("conics", cn.grad), ("colors", col.grad),
                                    ("opacity", op.grad))):
         a = _np(g).astype(np.float64)
         b = grads[k].reshape(a.shape).astype(np.float64)
-        tol = ATOL + RTOL * np.abs(b) + absum[k].reshape(a.shape) * 2.0 ** -20
+        tol = ATOL + RTOL * np.abs(b) + absum[k].reshape(a.shape) * (2.0 ** -20 + drift)
         bad = np.abs(a - b) > tol
         assert np.abs(b).max() > 0
         assert not bad.any(), f"{name}: {bad.mean():.2e} out of tolerance " \

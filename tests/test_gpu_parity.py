@@ -301,6 +301,19 @@ def _check_raster_backward(gpu, case):
         assert frac == 0.0, f"{name}: {frac:.2e} out of tolerance (max {mx:.3e})"
 
 
+@pytest.mark.parametrize("chunk", [64, 128, 256])
+@pytest.mark.parametrize("case", CASES[1:3])
+def test_raster_backward_list_split(gpu, case, chunk):
+    """The list-split backward (checkpointed forward + per-chunk backward, forced chunk
+    size): identical forward, gradients within the same bar vs the oracle."""
+    _lib.call("gsplat_debug_set_chunk", chunk)
+    try:
+        _check_raster_forward(gpu, case)
+        _check_raster_backward(gpu, case)
+    finally:
+        _lib.call("gsplat_debug_set_chunk", 0)
+
+
 @pytest.mark.parametrize("C", [1, 4, 7])
 def test_nd_rasterize(gpu, C):
     case = CASES[1]
