@@ -46,11 +46,18 @@ class FusedAdam:
         return st
 
     @torch.no_grad()
-    def step(self):
-        live = [(g, g["params"][0]) for g in self.param_groups if g["params"][0].grad is not None]
+    def step(self, names=None, advance: bool = True):
+        """One Adam update of every group with a gradient -- or only of the groups named in
+        `names`, so that a caller can update some groups while other gradients are still
+        being reduced (TrainStep).  `advance=False` reuses the current step count: the
+        groups of one optimisation step split over several calls share their bias
+        correction, exactly as one call would."""
+        live = [(g, g["params"][0]) for g in self.param_groups if g["params"][0].grad is not None
+                and (names is None or g.get("name") in names)]
+        if advance:
+            self.step_count += 1
         if not live:
             return
-        self.step_count += 1
         n = len(live)
         P, G, M, V = (ctypes.c_void_p * n)(), (ctypes.c_void_p * n)(), (ctypes.c_void_p * n)(), \
             (ctypes.c_void_p * n)()

@@ -66,6 +66,14 @@ def splatfacto_loss(pred, gt):
     return (1 - SSIM_LAMBDA) * l1 + SSIM_LAMBDA * sim
 
 
+SH_GROUPS = ("features_dc", "features_rest")
+
+
+def FusedAdamType():
+    from .optim import FusedAdam
+    return FusedAdam
+
+
 class GradExchange:
     """Sums every parameter's gradient over the data-parallel ranks (RCCL over xGMI).
 
@@ -85,7 +93,8 @@ class GradExchange:
         self.sh = sh
         self.sh_ids = {id(p) for p in sh_params}
 
-    def wait(self):
+    def start(self):
+        """Issue this step's all-reduces (async); returns the handles for finish()."""
         works = []
         for p in self.params:
             if self.sh is not None and self.sh.handled and id(p) in self.sh_ids:
@@ -94,10 +103,20 @@ class GradExchange:
                 p.grad = torch.zeros_like(p)
             works.append(dist.all_reduce(p.grad, op=dist.ReduceOp.SUM, group=self.group,
                                          async_op=True))
+        return works
+
+    def finish(self, works):
         for w in works:
             w.wait()
         if self.sh is not None:
             self.sh.reset()
+
+    def sh_done(self) -> bool:
+        """True when the SH-coefficient gradients are already the all-rank sums."""
+        return self.sh is not None and self.sh.handled
+
+    def wait(self):
+        self.finish(self.start())
 
 
 class TrainStep:
@@ -191,11 +210,22 @@ class TrainStep:
             background = torch.rand(3, device=gt.device)
         self.zero_grad()
         loss, out = self.forward_backward(cam, gt, background)
-        self.sync_grads()
-        if optimizer:
-            for g in self.opt.param_groups:
-                if g["name"] == "means":
-                    g["lr"] = self._xyz_lr()
+        if not optimizer:
+            self.sync_grads()
+            return loss
+        for g in self.opt.param_groups:
+            if g["name"] == "means":
+                g["lr"] = self._xyz_lr()
+        gs = self.grad_sync
+        if gs is not None and gs.sh_done() and isinstance(self.opt, FusedAdamType()):
+            # the SH-feature gradients (81 % of the update's bytes) are final: update them
+            # while the other groups' all-reduces are in flight, then the rest
+            works = gs.start()
+            self.opt.step(names=SH_GROUPS)
+            gs.finish(works)
+            self.opt.step(names=[n for n in PARAM_NAMES if n not in SH_GROUPS], advance=False)
+        else:
+            self.sync_grads()
             self.opt.step()
-            self.step_count += 1
+        self.step_count += 1
         return loss

@@ -129,6 +129,18 @@ def test_trainstep_multirank_path_over_rccl_world1(gpu):
             flats.append(t.flat_grad().cpu().numpy())
         assert np.abs(flats[0]).max() > 0
         np.testing.assert_allclose(flats[1], flats[0], rtol=1e-5, atol=1e-6)
+        # optimiser steps: the multi-rank path updates the SH-feature groups while the other
+        # groups' all-reduces are in flight, then the rest (one shared step count)
+        params = []
+        for ws in (1, 2):
+            t = TrainStep(synthetic_scene(20000, 3, seed=6, device=gpu), sh_degree=3,
+                          world_size=ws, loss="splatfacto")
+            for _ in range(3):
+                t.step(cam, gt, background=bg, optimizer=True)
+            assert t.opt.step_count == 3
+            params.append([p.detach().cpu().numpy() for p in t.params])
+        for a, b in zip(*params):
+            np.testing.assert_allclose(b, a, rtol=1e-5, atol=1e-6)
         away = gc_camera(look_at_c2w((0.0, 0.0, 4.0), target=(0.0, 0.0, 8.0),
                                      up=(0.0, 1.0, 0.0)), 200.0, 200.0, 128.0, 96.0, 256,
                          192).to(gpu)
