@@ -59,6 +59,7 @@ SIGNATURES = {
     "gsplat_debug_set_raster_variant": (_I, [_I, _I, _I]),
     "gsplat_debug_sort_timing": (_I, [_P, _I]),
     "gsplat_debug_sort_scheme": (_I, [_I]),
+    "gsplat_debug_sort_items": (_I, [_I]),
     "gsplat_l1_ssim_num_blocks": (_I, [_I, _I]),
     "gsplat_l1_ssim_forward": (_I, [_I, _I, _I, _P, _P, _P, _F, _P, _P, _P, _P]),
     "gsplat_l1_ssim_backward": (_I, [_I, _I, _I, _P, _P, _P, _F, _P, _P, _P, _P]),

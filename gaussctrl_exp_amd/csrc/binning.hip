@@ -34,7 +34,11 @@ constexpr int SC_ITEMS = 16;
 constexpr int SC_TILE = TPB * SC_ITEMS;  // elements per scan workgroup
 // keys per thread of a sort pass (workgroup tile = TPB * items): small sorts use short tiles
 // so that more, shorter workgroups run at once (a pass is a chain of latencies per workgroup)
-int os_items_for(long long n) { return n >= (4LL << 20) ? 16 : 4; }
+int g_items_override = 0;  // experiment hook (gsplat_debug_sort_items)
+int os_items_for(long long n) {
+  if (g_items_override) return g_items_override;
+  return n >= (4LL << 20) ? 16 : 4;
+}
 constexpr int OS_MAX_PASSES = 8;
 constexpr uint32_t ST_AGG = 1u << 30;    // status word: aggregate of this tile only
 constexpr uint32_t ST_PRE = 2u << 30;    // status word: inclusive prefix up to this tile
@@ -841,6 +845,11 @@ Phase2 carve_phase2(void *base, long long I) {
 }  // namespace gs
 
 using namespace gs;
+
+extern "C" int gsplat_debug_sort_items(int items) {
+  g_items_override = (items == 4 || items == 8 || items == 16) ? items : 0;
+  return 0;
+}
 
 extern "C" int gsplat_debug_sort_scheme(int reduce_then_scan) {
   g_sort_rts = reduce_then_scan != 0;

@@ -215,6 +215,8 @@ int gsplat_debug_set_raster_variant(int fwd_pxl, int bwd_pxl, int bwd_flags);
 int gsplat_debug_sort_timing(void *buffer, int calls);
 /* Radix-sort pass scheme: 1 = reduce-then-scan (default), 0 = one-sweep decoupled look-back. */
 int gsplat_debug_sort_scheme(int reduce_then_scan);
+/* Debug: force 4, 8 or 16 keys per thread in every radix-sort pass (0 = automatic). */
+int gsplat_debug_sort_items(int items);
 
 /* ---- training-step photometric loss -------------------------------------
  * nerfstudio 1.0 splatfacto get_loss_dict's main loss, which the reference's training step
