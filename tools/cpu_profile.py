@@ -7,7 +7,7 @@ import bench
 from gaussctrl_exp_amd.scene import synthetic_scene
 from gaussctrl_exp_amd.train import TrainStep
 
-N, W, H, deg, lo, hi, seed, desc = bench.CONFIGS["headline"]
+N, W, H, deg, lo, hi, seed, _real, desc = bench.CONFIGS["headline"]
 dev = torch.device("cuda:0")
 scene = synthetic_scene(N, deg, seed=seed, scale_lo=lo, scale_hi=hi, device=dev)
 cam = bench.view_camera(W, H, 0).to(dev)

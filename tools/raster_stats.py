@@ -10,7 +10,7 @@ from gaussctrl_exp_amd.rasterize import bin_gaussians
 from gaussctrl_exp_amd.scene import synthetic_scene
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "headline"
-N, W, H, deg, lo, hi, seed, desc = bench.CONFIGS[cfg]
+N, W, H, deg, lo, hi, seed, _real, desc = bench.CONFIGS[cfg]
 dev = torch.device("cuda:0")
 sc = synthetic_scene(N, deg, seed=seed, scale_lo=lo, scale_hi=hi, device=dev)
 cam = bench.view_camera(W, H, 0).to(dev)
