@@ -582,7 +582,7 @@ __device__ __forceinline__ void tile_bbox(float x, float y, float radius, int tb
 // Depth keys: visible -> float bits of depth (positive floats order as uints), culled ->
 // 0xFFFFFFFF (sorted last).  Also writes the Gaussian's binning record, read by coalesced
 // loads here so that the depth-ordered passes need ONE gather per Gaussian:
-// rec[g] = {tile allotment, x0 | y0 << 16, x1 | y1 << 16, 0} (tile bbox, T < 65536).
+// rec[g] = {tile allotment, x0 | y0 << 16, x1 | y1 << 16, 0} (tile bbox; < 65536 tiles per axis).
 // One workgroup per depth-sort tile (TPB * ITEMS keys): with counts != null it also writes the
 // tile's histogram of the first sort digit (reduce-then-scan pass 0) and clears the sort's
 // error word, saving the sort its first count launch.
@@ -836,7 +836,7 @@ Phase2 carve_phase2(void *base, long long I) {
   p.tk_b = c.take<uint32_t>(ii);
   p.tv_b = c.take<uint32_t>(ii);
   p.tk_s = c.take<uint32_t>(ii);
-  p.rs_ws = c.take<char>(radix_ws_bytes(I, 0, 16));  // >= any tile-key width (T < 65536)
+  p.rs_ws = c.take<char>(radix_ws_bytes(I, 0, 32));  // >= any tile-key width
   p.bytes = c.off;
   return p;
 }
@@ -876,7 +876,8 @@ extern "C" int gsplat_bin_count(int num_points, const float *xys, const float *d
                                 void *workspace1, size_t workspace1_bytes, void *stream) {
   hipStream_t st = (hipStream_t)stream;
   const long long T = (long long)tile_bounds_x * tile_bounds_y;
-  if (num_points < 0 || tile_bounds_x <= 0 || tile_bounds_y <= 0 || T >= 65536) {
+  if (num_points < 0 || tile_bounds_x <= 0 || tile_bounds_y <= 0 || tile_bounds_x > 65535 ||
+      tile_bounds_y > 65535 || T >= (1LL << 31)) {
     set_error("bin_count: bad sizes (N=%d tiles=%dx%d)", num_points, tile_bounds_x,
               tile_bounds_y);
     return 1;
@@ -925,7 +926,8 @@ extern "C" int gsplat_bin_emit(int num_points, int64_t num_intersects, int tile_
   hipStream_t st = (hipStream_t)stream;
   const long long T = (long long)tile_bounds_x * tile_bounds_y;
   if (num_points < 0 || num_intersects < 0 || num_intersects > 0x3FFFFFFFLL ||
-      tile_bounds_x <= 0 || tile_bounds_y <= 0 || T >= 65536) {
+      tile_bounds_x <= 0 || tile_bounds_y <= 0 || tile_bounds_x > 65535 ||
+      tile_bounds_y > 65535 || T >= (1LL << 31)) {
     set_error("bin_emit: bad sizes (N=%d I=%lld tiles=%dx%d)", num_points,
               (long long)num_intersects, tile_bounds_x, tile_bounds_y);
     return 1;

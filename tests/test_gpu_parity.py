@@ -160,11 +160,13 @@ def test_binning_fused_bitexact(gpu, case):
     np.testing.assert_array_equal(_np(bins), ref["tile_bins"])
 
 
-def test_binning_large_tile_grid_bitexact(gpu):
-    """A 4096x2400 image (38,400 tiles: 16-bit tile keys, two 8-bit sort passes)."""
-    case = (3000, 4096, 2400, 5, 0.01, 0.2, 1.5)
+@pytest.mark.parametrize("W,H,tiles", [(4096, 2400, 38400), (4112, 4096, 65792)])
+def test_binning_large_tile_grid_bitexact(gpu, W, H, tiles):
+    """Large tile grids: 38,400 tiles (16-bit tile keys, two 8-bit sort passes) and 65,792
+    (17-bit keys, three passes) -- gsplat takes any image size."""
+    case = (3000, W, H, 5, 0.01, 0.2, 1.5)
     sc, cam, scales, quats = _inputs(*case)
-    assert cam.tile_bounds[0] * cam.tile_bounds[1] >= 36 * 1024
+    assert cam.tile_bounds[0] * cam.tile_bounds[1] == tiles
     g, o = _project_both(gpu, sc, cam, scales, quats)
     xys, depths, radii, conics, nth, cov3d = g
     I, gids, bins = bin_gaussians(xys, depths, radii, nth, cam.height, cam.width)
