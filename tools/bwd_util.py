@@ -98,6 +98,12 @@ with torch.no_grad():
                         k = fn(gx, gy, a, bb, c, o, float(c0), float(c1), float(r0), float(r1))
                         key = f"{name}_{cols}x{rows}"
                         tot[key] = tot.get(key, 0) + (k & (idx <= mf)).sum().item()
+                        if name == "exact":  # iterations with >= 1 valid pair in the wave
+                            sub = v[:, r0 - ty * 16: r1 - ty * 16 + 1, c0 - tx * 16: c1 - tx * 16 + 1]
+                            fsub = fin[r0 - ty * 16: r1 - ty * 16 + 1, c0 - tx * 16: c1 - tx * 16 + 1]
+                            live = (sub & (idx[:, None, None] <= fsub)).flatten(1).any(1)
+                            lk = f"live_{cols}x{rows}"
+                            tot[lk] = tot.get(lk, 0) + (k & (idx <= mf) & live).sum().item()
     n = len(sample)
     print({k: round(v / n, 1) for k, v in tot.items()})
     for cols, rows in ((16, 8), (16, 4), (16, 16), (8, 8), (8, 16)):
@@ -106,3 +112,6 @@ with torch.no_grad():
             pix = cols * rows
             print(f"{name:5s} {cols}x{rows}: wave iters/tile {tot[key]/n:7.1f}; lane util "
                   f"{tot['pairs_valid'] / (tot[key] * pix):.3f}")
+        lk = f"live_{cols}x{rows}"
+        print(f"      {cols}x{rows}: iterations with a valid pair: "
+              f"{tot[lk] / tot[f'exact_{cols}x{rows}']:.3f} of the exact-cull iterations")
