@@ -165,6 +165,36 @@ __global__ __launch_bounds__(256) void l1_ssim_fwd_kernel(int H, int W, int C,
   }
 }
 
+// ssim_lambda == 0: plain L1 (the SSIM term has weight zero) -- one streaming pass.
+// partials[2 b] = sum |gt - pred| over this block's grid-stride share, partials[2 b + 1] = 0.
+__global__ __launch_bounds__(256) void l1_only_fwd_kernel(long long n, const float *__restrict__ pred,
+                                                          const float *__restrict__ gt,
+                                                          float *__restrict__ partials) {
+  __shared__ float red[4];
+  float acc = 0.f;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n;
+       i += (long long)gridDim.x * 256)
+    acc += fabsf(gt[i] - pred[i]);
+  acc = block_sum(acc, red);
+  if (threadIdx.x == 0) {
+    partials[2 * blockIdx.x] = acc;
+    partials[2 * blockIdx.x + 1] = 0.f;
+  }
+}
+
+__global__ __launch_bounds__(256) void l1_only_bwd_kernel(long long n, const float *__restrict__ pred,
+                                                          const float *__restrict__ gt,
+                                                          const float *__restrict__ grad_out,
+                                                          float l1_scale,
+                                                          float *__restrict__ v_pred) {
+  const float gl = grad_out[0] * l1_scale;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n;
+       i += (long long)gridDim.x * 256) {
+    const float d = pred[i] - gt[i];
+    v_pred[i] = gl * (d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f));
+  }
+}
+
 // loss = (1 - lambda) * L1 / (C H W) + lambda * (1 - SSIM_sum / (C Ho Wo)); one workgroup,
 // double accumulation in a fixed order (deterministic).
 __global__ __launch_bounds__(256) void l1_ssim_finalize_kernel(int nblocks, const float *partials,
@@ -289,8 +319,9 @@ extern "C" int gsplat_l1_ssim_num_blocks(int img_height, int img_width) {
   return (int)(cdiv(img_width, TW) * cdiv(img_height, TH));
 }
 
-static bool l1_ssim_args_ok(int H, int W, int C, const char *what) {
-  if (H < WIN || W < WIN || C < 1 || C > 64) {
+static bool l1_ssim_args_ok(int H, int W, int C, const char *what, float lambda = 1.f) {
+  const int min_hw = lambda == 0.f ? 1 : WIN;  // the L1-only path has no SSIM window
+  if (H < min_hw || W < min_hw || C < 1 || C > 64) {
     set_error("%s: need H, W >= %d and 1 <= C <= 64 (H=%d W=%d C=%d)", what, WIN, H, W, C);
     return false;
   }
@@ -307,12 +338,17 @@ extern "C" int gsplat_l1_ssim_forward(int img_height, int img_width, int channel
                                       const float *pred, const float *gt, const float *window11,
                                       float ssim_lambda, float *partials, float *dmaps,
                                       float *loss, void *stream) {
-  if (!l1_ssim_args_ok(img_height, img_width, channels, "l1_ssim_forward")) return 1;
+  if (!l1_ssim_args_ok(img_height, img_width, channels, "l1_ssim_forward", ssim_lambda)) return 1;
   hipStream_t st = (hipStream_t)stream;
   const int nb = gsplat_l1_ssim_num_blocks(img_height, img_width);
-  const Win w = load_win(window11);
-  hipLaunchKernelGGL(l1_ssim_fwd_kernel, dim3(nb), dim3(256), 0, st, img_height, img_width,
-                     channels, pred, gt, w, partials, dmaps);
+  if (ssim_lambda == 0.f) {  // L1 only: no SSIM statistics, dmaps untouched
+    hipLaunchKernelGGL(l1_only_fwd_kernel, dim3(nb), dim3(256), 0, st,
+                       (long long)img_height * img_width * channels, pred, gt, partials);
+  } else {
+    const Win w = load_win(window11);
+    hipLaunchKernelGGL(l1_ssim_fwd_kernel, dim3(nb), dim3(256), 0, st, img_height, img_width,
+                       channels, pred, gt, w, partials, dmaps);
+  }
   const double n1 = (double)channels * img_height * img_width;
   const double n2 = (double)channels * (img_height - WIN + 1) * (img_width - WIN + 1);
   hipLaunchKernelGGL(l1_ssim_finalize_kernel, dim3(1), dim3(256), 0, st, nb, partials,
@@ -324,12 +360,17 @@ extern "C" int gsplat_l1_ssim_backward(int img_height, int img_width, int channe
                                        const float *pred, const float *gt, const float *window11,
                                        float ssim_lambda, const float *dmaps,
                                        const float *grad_loss, float *v_pred, void *stream) {
-  if (!l1_ssim_args_ok(img_height, img_width, channels, "l1_ssim_backward")) return 1;
+  if (!l1_ssim_args_ok(img_height, img_width, channels, "l1_ssim_backward", ssim_lambda)) return 1;
   hipStream_t st = (hipStream_t)stream;
   const int nb = gsplat_l1_ssim_num_blocks(img_height, img_width);
-  const Win w = load_win(window11);
   const double n1 = (double)channels * img_height * img_width;
   const double n2 = (double)channels * (img_height - WIN + 1) * (img_width - WIN + 1);
+  if (ssim_lambda == 0.f) {
+    hipLaunchKernelGGL(l1_only_bwd_kernel, dim3(nb), dim3(256), 0, st, (long long)n1, pred, gt,
+                       grad_loss, (float)(1.0 / n1), v_pred);
+    return check_launch("l1_ssim_backward");
+  }
+  const Win w = load_win(window11);
   hipLaunchKernelGGL(l1_ssim_bwd_kernel, dim3(nb), dim3(256), 0, st, img_height, img_width,
                      channels, pred, gt, w, dmaps, grad_loss, (float)(-ssim_lambda / n2),
                      (float)((1.0 - ssim_lambda) / n1), v_pred);

@@ -45,8 +45,9 @@ class _FusedL1SSIM(Function):
         H, W, C = pred.shape
         nb = _lib.lib().gsplat_l1_ssim_num_blocks(H, W)
         partials = torch.empty((max(2 * nb, 1),), device=dev, dtype=torch.float32)
-        dmaps = torch.empty((3 * C * max(H - SSIM_WIN + 1, 0) * max(W - SSIM_WIN + 1, 0),),
-                            device=dev, dtype=torch.float32)
+        n_maps = 3 * C * max(H - SSIM_WIN + 1, 0) * max(W - SSIM_WIN + 1, 0)
+        dmaps = torch.empty((n_maps if ssim_lambda != 0 else 1,), device=dev,
+                            dtype=torch.float32)  # (lambda 0: L1 only, no SSIM maps)
         loss = torch.empty((), device=dev, dtype=torch.float32)
         P = _lib.ptr
         _lib.call("gsplat_l1_ssim_forward", H, W, C, P(pred), P(gt), ctypes.cast(_WINDOW,

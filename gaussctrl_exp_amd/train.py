@@ -154,6 +154,9 @@ class TrainStep:
 
     def loss(self, pred, gt):
         if self.loss_kind == "l1":
+            if self.api is None and pred.is_cuda:  # csrc/loss.hip, ssim_lambda = 0 fast path
+                from .loss import fused_splatfacto_loss
+                return fused_splatfacto_loss(pred, gt, 0.0)
             return torch.abs(gt - pred).mean()
         if self.loss_kind == "splatfacto_torch" or self.api is not None or not pred.is_cuda:
             return splatfacto_loss(pred, gt)  # torch restatement (CPU-emulation tests)

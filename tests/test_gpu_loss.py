@@ -52,3 +52,22 @@ def test_fused_loss_has_no_cpu_path():
 def test_fused_loss_rejects_small_images(gpu):
     with pytest.raises(RuntimeError, match="H, W >= 11"):
         fused_splatfacto_loss(torch.rand(10, 20, 3, device=gpu), torch.rand(10, 20, 3, device=gpu))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("H,W,C", [(48, 64, 3), (5, 7, 3), (1080, 1080, 3)])
+def test_l1_only_fast_path(gpu, H, W, C):
+    """ssim_lambda = 0 takes the L1-only kernels (any image size): loss and gradient equal
+    torch's |gt - pred|.mean() (gradient sign(pred - gt) / n, sign(0) = 0)."""
+    g = torch.Generator().manual_seed(H)
+    gt = torch.rand(H, W, C, generator=g)
+    pred = gt.clone()
+    pred[: H // 2] += 0.1 * torch.randn(H // 2, W, C, generator=g)  # exact ties elsewhere
+    p = pred.to(gpu).requires_grad_()
+    loss = fused_splatfacto_loss(p, gt.to(gpu), 0.0)
+    loss.backward()
+    p64 = pred.double().requires_grad_()
+    ref = torch.abs(gt.double() - p64).mean()
+    ref.backward()
+    assert abs(loss.item() - ref.item()) <= 1e-6 * max(1.0, ref.item())
+    torch.testing.assert_close(p.grad.double().cpu(), p64.grad, rtol=1e-6, atol=1e-12)
