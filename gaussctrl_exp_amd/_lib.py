@@ -13,7 +13,7 @@ import subprocess
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libgsplat_mi355x.so")
+LIB_PATH = os.environ.get("GSPLAT_MI355X_LIB") or os.path.join(_HERE, "libgsplat_mi355x.so")
 CSRC = os.path.join(_HERE, "csrc")
 
 _c = ctypes

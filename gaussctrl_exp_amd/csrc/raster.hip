@@ -76,6 +76,37 @@ __device__ __forceinline__ f2 gs_vis2(f2 sigma) {
   return (f2){__builtin_amdgcn_exp2f(e.x), __builtin_amdgcn_exp2f(e.y)};
 }
 
+// A pixel pair as two scalars (s2) or one packed register pair (f2): the same arithmetic,
+// rounding and decisions either way; s2 compiles to scalar v_fma/v_mul (gfx950 issues packed
+// fp32 ops no faster than two scalar ones), f2 to v_pk_*.
+struct s2 {
+  float x, y;
+  __device__ __forceinline__ s2() {}
+  __device__ __forceinline__ s2(float v) : x(v), y(v) {}
+  __device__ __forceinline__ s2(float a, float b) : x(a), y(b) {}
+};
+__device__ __forceinline__ s2 operator+(s2 a, s2 b) { return s2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ s2 operator-(s2 a, s2 b) { return s2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ s2 operator*(s2 a, s2 b) { return s2(a.x * b.x, a.y * b.y); }
+__device__ __forceinline__ s2 operator+(float a, s2 b) { return s2(a) + b; }
+__device__ __forceinline__ s2 operator-(float a, s2 b) { return s2(a) - b; }
+__device__ __forceinline__ s2 operator*(float a, s2 b) { return s2(a) * b; }
+__device__ __forceinline__ s2 operator*(s2 a, float b) { return a * s2(b); }
+__device__ __forceinline__ s2 &operator+=(s2 &a, s2 b) { a = a + b; return a; }
+__device__ __forceinline__ s2 vfma(s2 a, s2 b, s2 c) {
+  return s2(fmaf(a.x, b.x, c.x), fmaf(a.y, b.y, c.y));
+}
+__device__ __forceinline__ f2 vfma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+template <typename V>
+__device__ __forceinline__ V gs_sigma2v(float hc, float bdx, float hA, V dy) {
+  return vfma(vfma(V(hc), dy, V(bdx)), dy, V(hA));
+}
+template <typename V>
+__device__ __forceinline__ V gs_vis2v(V sigma) {
+  const V e = sigma * NEG_LOG2E;
+  return V{__builtin_amdgcn_exp2f(e.x), __builtin_amdgcn_exp2f(e.y)};
+}
+
 // Exactness-preserving cull of one Gaussian against the wave's pixel-centre rectangle
 // [rx0,rx1] x [ry0,ry1].  With d = xy - p ranging over the box [dx0,dx1] x [dy0,dy1],
 // sigma(p) = 0.5 q(d), q = a dx^2 + 2 b dx dy + c dy^2, is convex for a positive-definite
@@ -663,7 +694,7 @@ __global__ __launch_bounds__(256) void raster_bwd3_kernel(
 // [range.x + j * chunk, range.x + (j + 1) * chunk) and starts from the forward's checkpoint
 // after its last position: T = checkpoint T, and the colour behind it, Sb = (C_final - C_j) . v,
 // instead of T_final and 0 -- so long lists and small images (few tiles) still fill the GPU.
-template <int NP, bool ATOMICS, int COLS, bool CHUNKED = false>
+template <int NP, bool ATOMICS, int COLS, bool CHUNKED = false, typename PV = f2>
 __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
     int tbx, int tby, int H, int W, const int *__restrict__ gids, const int2 *__restrict__ bins,
     const float2 *__restrict__ xys, const float *__restrict__ conics,
@@ -691,7 +722,7 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
   const float px = (float)j;
   const float rx0 = R.rx0, rx1 = R.rx1, ry0 = R.ry0, ry1 = R.ry1;
   const float bg0 = background[0], bg1 = background[1], bg2 = background[2];
-  f2 py[NP], T[NP], vr[NP], vg[NP], vb[NP], q[NP], Sb[NP];
+  PV py[NP], T[NP], vr[NP], vg[NP], vb[NP], q[NP], Sb[NP];
   int binf[PXL];
   int maxbin = -1;
 #pragma unroll
@@ -715,7 +746,7 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
     } else {
       py[p].x = (float)i; T[p].x = Tf; vr[p].x = r; vg[p].x = g; vb[p].x = bl; q[p].x = qk;
     }
-    Sb[p] = (f2)0.f;
+    Sb[p] = PV(0.f);
     binf[k] = bf;
     maxbin = max(maxbin, bf);
   }
@@ -773,39 +804,39 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
         gid[u] = G.id;
         const float dx = G.x - px;
         const float hA = G.ha * dx * dx, bdx = G.b * dx;
-        f2 sr = 0.f, sg = 0.f, sb = 0.f, so = 0.f, V = 0.f, Vy = 0.f, Vyy = 0.f;
+        PV sr = 0.f, sg = 0.f, sb = 0.f, so = 0.f, V = 0.f, Vy = 0.f, Vyy = 0.f;
         bool any = false;
 #pragma unroll
         for (int p = 0; p < NP; ++p) {
-          const f2 dy = G.y - py[p];
-          const f2 sig = gs_sigma2(G.hc, bdx, hA, dy);
-          const f2 vis = gs_vis2(sig);
-          const f2 ov = G.o * vis;
-          const f2 al = {fminf(alpha_max, ov.x), fminf(alpha_max, ov.y)};
+          const PV dy = G.y - py[p];
+          const PV sig = gs_sigma2v<PV>(G.hc, bdx, hA, dy);
+          const PV vis = gs_vis2v<PV>(sig);
+          const PV ov = G.o * vis;
+          const PV al = {fminf(alpha_max, ov.x), fminf(alpha_max, ov.y)};
           const bool v0 = live && G.idx <= binf[2 * p] && sig.x >= 0.f && al.x >= ALPHA_MIN;
           const bool v1 =
               live && G.idx <= binf[2 * p + 1] && sig.y >= 0.f && al.y >= ALPHA_MIN;
           any = any || v0 || v1;
-          const f2 am = {v0 ? al.x : 0.f, v1 ? al.y : 0.f};
-          const f2 vm = {v0 ? vis.x : 0.f, v1 ? vis.y : 0.f};
-          const f2 om = 1.f - am;
-          const f2 ra = {__builtin_amdgcn_rcpf(om.x), __builtin_amdgcn_rcpf(om.y)};
+          const PV am = {v0 ? al.x : 0.f, v1 ? al.y : 0.f};
+          const PV vm = {v0 ? vis.x : 0.f, v1 ? vis.y : 0.f};
+          const PV om = 1.f - am;
+          const PV ra = {__builtin_amdgcn_rcpf(om.x), __builtin_amdgcn_rcpf(om.y)};
           T[p] = T[p] * ra;
-          const f2 fac = am * T[p];
-          sr = __builtin_elementwise_fma(fac, vr[p], sr);
-          sg = __builtin_elementwise_fma(fac, vg[p], sg);
-          sb = __builtin_elementwise_fma(fac, vb[p], sb);
-          const f2 gv = __builtin_elementwise_fma(
-              (f2)G.r, vr[p], __builtin_elementwise_fma((f2)G.g, vg[p], G.bl * vb[p]));
-          const f2 v_alpha = __builtin_elementwise_fma(gv, T[p], ra * (q[p] - Sb[p]));
-          Sb[p] = __builtin_elementwise_fma(fac, gv, Sb[p]);
-          const f2 vva = vm * v_alpha;
+          const PV fac = am * T[p];
+          sr = vfma(fac, vr[p], sr);
+          sg = vfma(fac, vg[p], sg);
+          sb = vfma(fac, vb[p], sb);
+          const PV gv = vfma(
+              PV(G.r), vr[p], vfma(PV(G.g), vg[p], G.bl * vb[p]));
+          const PV v_alpha = vfma(gv, T[p], ra * (q[p] - Sb[p]));
+          Sb[p] = vfma(fac, gv, Sb[p]);
+          const PV vva = vm * v_alpha;
           so += vva;
-          const f2 vs = vva * (-G.o);
-          const f2 vsdy = vs * dy;
+          const PV vs = vva * (-G.o);
+          const PV vsdy = vs * dy;
           V += vs;
           Vy += vsdy;
-          Vyy = __builtin_elementwise_fma(vsdy, dy, Vyy);
+          Vyy = vfma(vsdy, dy, Vyy);
         }
         anyv[u] = any;
         const float Vs = V.x + V.y, Vys = Vy.x + Vy.y;
@@ -1231,7 +1262,8 @@ extern "C" int gsplat_rasterize_forward(int tile_bounds_x, int tile_bounds_y, in
     } else if (g_fwd_pxl == 2) {
       if (scalar) FWD3(2); else if (packed) FWD3P(1); else if (wide) FWD3U(2, 16); else FWD3U(2, 8);
     } else {
-      if (scalar) FWD3(1); else if (wide) FWD3U(1, 16); else FWD3U(1, 8);
+      if (scalar) FWD3(1); else if (wide) FWD3U(1, 16);
+      else FWD3U(1, 8);
     }
 #undef FWD3U
 #undef FWD3
@@ -1336,7 +1368,14 @@ extern "C" int gsplat_rasterize_backward(int tile_bounds_x, int tile_bounds_y, i
         if (atomics) BWD3P(2, true, 16); else BWD3P(2, false, 16);  // 16x16: one wave
       } else {
         if (narrow) { if (atomics) BWD3P(1, true, 8); else BWD3P(1, false, 8); }
-        else { if (atomics) BWD3P(1, true, 16); else BWD3P(1, false, 16); }
+        else if (atomics && (g_bwd_flags & 512)) {  // ablation: scalar pixel pairs
+          hipLaunchKernelGGL((raster_bwd3p_kernel<1, true, 16, false, s2>),
+                             dim3(cdiv(T, (tiles_per_block<2, 16>()))), dim3(256), 0, st,
+                             tile_bounds_x, tile_bounds_y, img_height, img_width,
+                             gaussian_ids_sorted, (const int2 *)tile_bins, (const float2 *)xys,
+                             conics, colors, opacity, background, final_Ts, final_idx, v_output,
+                             v_output_alpha, alpha_max, rec, (g_bwd_flags & 64) != 0);
+        } else { if (atomics) BWD3P(1, true, 16); else BWD3P(1, false, 16); }
       }
     } else if (g_bwd_pxl == 4) { if (atomics) BWD3(4, true); else BWD3(4, false); }
     else if (g_bwd_pxl == 1) { if (atomics) BWD3(1, true); else BWD3(1, false); }

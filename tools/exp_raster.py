@@ -49,9 +49,9 @@ def timeit(fn, reps=10):
     e.record(); torch.cuda.synchronize()
     return s.elapsed_time(e) / reps
 
-variants = [(f, b, fl) for f, b, fl in
-            [(1, 2, 0), (1, 2, 4), (1, 2, 16), (2, 2, 0), (1, 1, 0), (1, 2, 2), (1, 2, 32),
-             (1, 2, 1)]]
+# VARIANTS="fwd_pxl,bwd_pxl,flags;..." (default: the shipped one and a few ablations)
+variants = [tuple(int(x) for x in v.split(",")) for v in os.environ.get(
+    "VARIANTS", "1,2,0;1,2,1;1,2,64;1,4,0;1,2,32;2,2,0").split(";")]
 res = {v: {"fwd": [], "bwd": []} for v in variants}
 for rnd in range(5):
     for v in variants:
