@@ -31,6 +31,7 @@ sys.path.insert(0, ROOT)
 
 from gaussctrl_exp_amd import timing  # noqa: E402
 from gaussctrl_exp_amd.camera import gc_camera, look_at_c2w  # noqa: E402
+from gaussctrl_exp_amd.fused import render_fused  # noqa: E402
 from gaussctrl_exp_amd.rasterize import bin_gaussians  # noqa: E402
 from gaussctrl_exp_amd.scene import render, synthetic_scene  # noqa: E402
 from gaussctrl_exp_amd.sh import num_sh_bases  # noqa: E402
@@ -102,12 +103,21 @@ def algorithmic_bytes(N, I, P, T, K, nvis):
         "gsplat_rasterize_backward": 40 * I + 24 * P + 36 * N,
         "gsplat_compute_sh_backward": (24 + 12 * K) * N,
         "gsplat_project_gaussians_backward": 180 * N,
+        # fused training render (csrc/preprocess.hip): raw params (56 + 12 (K-1) B) in,
+        # projection + colour + opacity (48 B) out, 48 B record zeroed per visible Gaussian
+        "gsplat_fused_preprocess_forward": (92 + 12 * K) * N + 48 * nvis,
+        "gsplat_rasterize_backward_records": 40 * I + 24 * P,
+        # params + saved forward outputs (72 B) and the 48 B record in, 6 gradients out
+        "gsplat_fused_preprocess_backward": (116 + 12 * K) * N + 48 * nvis,
     }
 
 
 # Device kernels behind each C-ABI entry (for the PMC traffic of the dominant entry).
 ENTRY_KERNELS = {
     "gsplat_rasterize_backward": ("raster_bwd", "split_grads_kernel"),
+    "gsplat_rasterize_backward_records": ("raster_bwd",),
+    "gsplat_fused_preprocess_forward": ("fused_fwd_kernel",),
+    "gsplat_fused_preprocess_backward": ("fused_bwd_kernel",),
     "gsplat_rasterize_forward": ("raster_fwd",),
     "gsplat_compute_sh_forward": ("sh_fwd_kernel",),
 }
@@ -226,6 +236,9 @@ def main():
     ap.add_argument("--train-steps", type=int, default=None)
     ap.add_argument("--forward-only", action="store_true",
                     help="time the render without backward (default for config c2)")
+    ap.add_argument("--render", default="fused", choices=("fused", "caller"),
+                    help="fused: the caller's activations inside the HIP kernels (default); "
+                         "caller: gc_model.py's torch glue around the gsplat API")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -244,18 +257,36 @@ def main():
     g = torch.Generator().manual_seed(1000 + rank)
     gt = torch.rand(H, W, 3, generator=g).to(dev)
     bg = torch.zeros(3, device=dev)
-    trainer = TrainStep(scene, sh_degree=deg, world_size=world, loss="l1")
+    trainer = TrainStep(scene, sh_degree=deg, world_size=world, loss="l1",
+                        render_mode=args.render)
+    caller = TrainStep(scene, sh_degree=deg, world_size=world, loss="l1", render_mode="caller")
 
     fwd_only = args.forward_only or args.config in FORWARD_ONLY
 
-    def step():
+    def step(t=trainer):
         if fwd_only:
             with torch.no_grad():
-                render(scene, cam, deg, bg)
+                if t.render_mode == "fused":
+                    render_fused(scene, cam, deg, bg)
+                else:
+                    render(scene, cam, deg, bg)
             return
-        trainer.zero_grad()
-        trainer.forward_backward(cam, gt, bg)
-        trainer.sync_grads()
+        t.zero_grad()
+        t.forward_backward(cam, gt, bg)
+        t.sync_grads()
+
+    def timed(fn, steps):
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            fn()
+        barrier()
+        dt = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([dt], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+        return dt
 
     def barrier():
         if world > 1:
@@ -276,6 +307,11 @@ def main():
         dt = float(t.item())
     ms_per_step = dt / args.steps * 1e3
     value = world * H * W * args.steps / dt / 1e6
+    # the same step through the unchanged caller's torch glue (gc_model.py as it runs on the
+    # gsplat drop-in), for comparison
+    for _ in range(max(args.warmup // 2, 1)):
+        step(caller)
+    caller_value = world * H * W * args.steps / timed(lambda: step(caller), args.steps) / 1e6
 
     # per-entry-point device time (HIP events on the launch stream), same step, K steps
     with timing.timed_calls() as tm:
@@ -370,6 +406,8 @@ def main():
                                f"{N * 11 * 4} B of grads RCCL all-reduced)" if world > 1
                                else "dp1",
             },
+            "render": args.render,
+            "value_unchanged_caller": round(caller_value, 2),
             "train_iters_per_s": round(tsteps / tdt, 2),
             "train_views_per_s": round(world * tsteps / tdt, 2),
             "roofline": roofline,

@@ -36,6 +36,7 @@ SIGNATURES = {
     "gsplat_compute_sh_forward": (_I, [_I, _I, _I, _P, _P, _P, _P]),
     "gsplat_compute_sh_backward": (_I, [_I, _I, _I, _P, _P, _P, _P]),
     "gsplat_compute_sh_backward_views": (_I, [_I, _I, _I, _I, _P, _P, _I64, _P, _P]),
+    "gsplat_compute_sh_backward_views_split": (_I, [_I, _I, _I, _I, _P, _P, _I64, _P, _P, _P]),
     "gsplat_compute_cov2d_bounds": (_I, [_I, _P, _P, _P, _P]),
     "gsplat_map_gaussian_to_intersects": (_I, [_I, _P, _P, _P, _P, _I, _I, _P, _P, _P]),
     "gsplat_sort_isect_pairs_workspace_size": (_SZ, [_I64]),
@@ -66,9 +67,16 @@ SIGNATURES = {
     "gsplat_adam_step": (_I, [_I, _P, _P, _P, _P, _P, _P, _I, _F, _F, _F, _P]),
     "gsplat_rasterize_backward": (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P,
                                        _P, _P, _P, _F, _P, _P, _P, _P, _P, _SZ, _P]),
+    "gsplat_fused_preprocess_forward": (_I, [_I, _I, _I] + [_P] * 9 + [_F] * 4 +
+                                        [_I] * 4 + [_F] + [_P] * 11),
+    "gsplat_fused_preprocess_backward": (_I, [_I, _I, _I] + [_P] * 6 + [_F] * 4 + [_I, _I] +
+                                         [_P] * 13),
+    "gsplat_grad_records_bytes": (_SZ, [_I]),
+    "gsplat_rasterize_backward_records": (_I, [_I] * 5 + [_P] * 11 + [_F, _I64, _I, _P, _SZ,
+                                                                       _P, _SZ, _P]),
 }
 
-ABI_VERSION = 5  # include/gsplat_mi355x.h GSPLAT_MI355X_ABI_VERSION
+ABI_VERSION = 6  # include/gsplat_mi355x.h GSPLAT_MI355X_ABI_VERSION
 
 _lib = None
 

@@ -1,0 +1,343 @@
+// preprocess.hip -- the reference caller's per-Gaussian glue fused into the projection and
+// SH kernels: the fused training render (no gsplat counterpart; SURVEY.md §8a rows a1-a3,
+// a10 plus their caller).
+//
+// GaussCtrlModel.get_outputs (/root/reference/gaussctrl/gc_model.py:158-215) prepares
+// gsplat's inputs with ~10 torch ops per step -- cat(features_dc, features_rest) (:172),
+// exp(scales) (:177), quats / |quats| (:178), viewdirs = normalise(means - campos)
+// (:197-198), SH -> clamp(rgb + 0.5, min=0) (:200-201) or sigmoid(dc) (:203),
+// sigmoid(opacities) (:215) -- and autograd runs their backwards and copies the SH-feature
+// gradients out of cat's strided views.  At 1M Gaussians that glue cost more device time
+// than the projection, SH and raster-forward kernels together.  The fused path evaluates all
+// of it per Gaussian, in registers:
+//  * fused_fwd_kernel: raw parameters -> activations (torch's formulas) -> gsplat projection
+//    (project_math.h: the same arithmetic as project.hip) -> SH colour straight from the two
+//    feature tensors (features_rest staged through LDS with 16-byte loads) -> clamp; writes
+//    exactly what binning and rasterization consume, and zeroes the Gaussian's
+//    rasterize-backward gradient record when it is visible (no separate memset).
+//  * fused_bwd_kernel: gradient record -> projection VJP (project_math.h) -> chain rule
+//    through the activations with torch's own backward formulas (exp' = result, sigmoid' =
+//    (1 - y) y, the division and vector-norm backwards of the quaternion normalisation, the
+//    clamp mask) -> the six raw-parameter gradients, the SH-feature ones written straight
+//    into their own contiguous tensors (LDS-staged 16-byte stores).
+// Built with -ffp-contract=off (projection bit-identical to project.hip given the same
+// activated inputs); the SH helpers carry their own contract pragma (sh_math.h).
+#include "project_math.h"
+#include "sh_math.h"
+
+namespace gs {
+namespace {
+
+constexpr int RECF = 16;  // floats per gradient record (raster.hip REC)
+
+// clamp(x, min=0) that keeps the clamp's backward mask in the sign bit: x < 0 -> -0.0f,
+// otherwise x (NaN stays NaN, as torch.clamp).  A -0 colour leaves every rasterizer sum
+// unchanged, and the backward passes the gradient exactly where torch's clamp_min backward
+// does (x >= 0): non-negative value with a clear sign bit.
+__device__ __forceinline__ float clamp0_signed(float x) { return x < 0.f ? -0.f : x; }
+__device__ __forceinline__ bool clamp0_passes(float stored) {
+  return stored >= 0.f && !__builtin_signbit(stored);
+}
+
+// torch.sigmoid on ROCm: 1 / (1 + exp(-x)) in fp32.
+__device__ __forceinline__ float sigmoidf(float x) { return 1.f / (1.f + expf(-x)); }
+
+struct FusedFwdArgs {
+  int n, degrees_to_use;
+  const float *means, *log_scales, *quats, *opacity_logits, *features_dc, *features_rest;
+  const float *viewmat, *projmat, *campos;
+  float *xys, *depths;
+  int *radii;
+  float *conics;
+  int *num_tiles_hit;
+  float *colors, *opacity;
+  float *records;                // NULL: no backward planned
+  float *scales_out, *quats_out;  // debug (activated inputs), NULL normally
+};
+
+struct FusedBwdArgs {
+  int n, degrees_to_use;
+  const float *means, *log_scales, *quats, *viewmat, *projmat, *campos;
+  const int *radii;
+  const float *conics, *colors, *opacity, *records;
+  float conic_scale;
+  float *v_means, *v_log_scales, *v_quats, *v_opacity_logits, *v_dc, *v_rest;
+  float *v_colors;  // non-NULL: write the SH-output gradient here instead of v_dc / v_rest
+};
+
+// The caller's activations (gc_model.py:177-178): exp(scales), quats / |quats|.
+__device__ __forceinline__ void activate(const float *__restrict__ ls, const float *__restrict__ q,
+                                         long long g, float s[3], float qr[4], float qn[4],
+                                         float &norm) {
+#pragma unroll
+  for (int k = 0; k < 3; ++k) s[k] = expf(ls[3 * g + k]);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) qr[k] = q[4 * g + k];
+  // torch's vector-norm reduction order for a 4-vector (measured bit-identical on MI355X:
+  // tests/test_gpu_fused.py records it), so qn equals the caller's quats / |quats| exactly
+  norm = sqrtf((qr[0] * qr[0] + qr[1] * qr[1]) + (qr[2] * qr[2] + qr[3] * qr[3]));
+#pragma unroll
+  for (int k = 0; k < 4; ++k) qn[k] = qr[k] / norm;
+}
+
+// SH basis along the caller's view direction: viewdirs = (means - campos) / |means - campos|
+// (gc_model.py:197-198), which gsplat renormalises in-kernel (sh.cuh).
+__device__ __forceinline__ int view_basis(int degrees_to_use, float p0, float p1, float p2,
+                                          const float *__restrict__ campos, float *b) {
+  float dx = p0 - campos[0], dy = p1 - campos[1], dz = p2 - campos[2];
+  const float dn = sqrtf(dx * dx + dy * dy + dz * dz);
+  dx = dx / dn;
+  dy = dy / dn;
+  dz = dz / dn;
+  return sh_basis(degrees_to_use, dx, dy, dz, b);
+}
+
+template <int K>
+__global__ __launch_bounds__(sh_threads(K)) void fused_fwd_kernel(FusedFwdArgs a, ProjParams pp) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int RROW = (K - 1) * 3;  // features_rest floats per Gaussian
+  constexpr int RP = RROW | 1;       // odd LDS pitch: conflict-free per-thread rows
+  constexpr int THR = sh_threads(K);
+  const long long g0 = (long long)blockIdx.x * THR;
+  const int cnt = (int)min((long long)THR, (long long)a.n - g0);
+  // the features_rest slab's loads go out first and land in LDS after the projection: the
+  // per-Gaussian math hides their latency (LDS caps the block count per CU)
+  const float *rest_src = K > 1 ? a.features_rest + g0 * RROW : nullptr;
+  RowStager<RROW, RP, THR> rs;
+  if constexpr (K > 1) rs.issue(rest_src, cnt);
+  const int t = threadIdx.x;
+  const bool live = t < cnt;
+  const long long g = g0 + (live ? t : 0);
+  float p0 = 0.f, p1 = 0.f, p2 = 0.f, dc[3] = {0.f, 0.f, 0.f};
+  if (live) {
+    p0 = a.means[3 * g];
+    p1 = a.means[3 * g + 1];
+    p2 = a.means[3 * g + 2];
+    float s[3], qr[4], qn[4], norm;
+    activate(a.log_scales, a.quats, g, s, qr, qn, norm);
+    Cam cam;
+    load_cam(cam, a.viewmat, a.projmat);
+    ProjOut o;
+    project_one(cam, pp, p0, p1, p2, s[0], s[1], s[2], qn[0], qn[1], qn[2], qn[3], o);
+    a.xys[2 * g] = o.xy[0];
+    a.xys[2 * g + 1] = o.xy[1];
+    a.depths[g] = o.depth;
+    a.radii[g] = o.radius;
+    a.conics[3 * g] = o.con[0];
+    a.conics[3 * g + 1] = o.con[1];
+    a.conics[3 * g + 2] = o.con[2];
+    a.num_tiles_hit[g] = o.tiles;
+    if (a.records && o.radius > 0) {  // only visible Gaussians receive raster atomics
+      float4 *r = reinterpret_cast<float4 *>(a.records + g * RECF);
+      const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+      r[0] = z;
+      r[1] = z;
+      r[2] = z;
+    }
+    a.opacity[g] = sigmoidf(a.opacity_logits[g]);  // gc_model.py:215
+#pragma unroll
+    for (int c = 0; c < 3; ++c) dc[c] = a.features_dc[3 * g + c];
+    if (a.scales_out) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) a.scales_out[3 * g + k] = s[k];
+    }
+    if (a.quats_out) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) a.quats_out[4 * g + k] = qn[k];
+    }
+  }
+  if constexpr (K == 1) {  // sh_degree 0: sigmoid(features_dc) (gc_model.py:203)
+    if (live) {
+#pragma unroll
+      for (int c = 0; c < 3; ++c) a.colors[3 * g + c] = sigmoidf(dc[c]);
+    }
+  } else {
+    rs.land(rest_src, cnt, smem);
+    __syncthreads();
+    if (live) {
+      float b[25];
+      const int nb = view_basis(a.degrees_to_use, p0, p1, p2, a.campos, b);
+      const float *row = smem + t * RP;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const float v =
+            sh_channel<K>(b, nb, [&](int k) { return k == 0 ? dc[c] : row[(k - 1) * 3 + c]; });
+        a.colors[3 * g + c] = clamp0_signed(v + 0.5f);  // gc_model.py:201
+      }
+    }
+  }
+}
+
+template <int K>
+__global__ __launch_bounds__(sh_threads(K)) void fused_bwd_kernel(FusedBwdArgs a, ProjParams pp) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int RROW = (K - 1) * 3;
+  constexpr int RP = RROW | 1;
+  constexpr int THR = sh_threads(K);
+  const long long g0 = (long long)blockIdx.x * THR;
+  const int cnt = (int)min((long long)THR, (long long)a.n - g0);
+  const bool rest_out = K > 1 && a.v_colors == nullptr;
+  const int t = threadIdx.x;
+  if (t < cnt) {
+    const long long g = g0 + t;
+    float vmean[3] = {0.f, 0.f, 0.f}, vls[3] = {0.f, 0.f, 0.f}, vq[4] = {0.f, 0.f, 0.f, 0.f};
+    float vlogit = 0.f, vc[3] = {0.f, 0.f, 0.f};
+    const bool vis = a.radii[g] > 0;
+    const float p0 = a.means[3 * g], p1 = a.means[3 * g + 1], p2 = a.means[3 * g + 2];
+    if (vis) {
+      const float4 *rec = reinterpret_cast<const float4 *>(a.records + g * RECF);
+      const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2];
+      float s[3], qr[4], qn[4], norm;
+      activate(a.log_scales, a.quats, g, s, qr, qn, norm);
+      Cam cam;
+      load_cam(cam, a.viewmat, a.projmat);
+      float cv[6];
+      cov3d_one(pp.glob_scale, s[0], s[1], s[2], qn[0], qn[1], qn[2], qn[3], cv);
+      ProjGrad pg;
+      const float cs = a.conic_scale;
+      project_backward_one(cam, pp, p0, p1, p2, s[0], s[1], s[2], qn[0], qn[1], qn[2], qn[3],
+                           cv, a.conics[3 * g], a.conics[3 * g + 1], a.conics[3 * g + 2], r0.x,
+                           r0.y, 0.f, cs * r0.z, cs * r0.w, cs * r1.x, pg);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) vmean[k] = pg.vmean[k];
+      // exp backward: grad * result
+#pragma unroll
+      for (int k = 0; k < 3; ++k) vls[k] = pg.vscale[k] * s[k];
+      // quats / norm: div backward (grad / other; -grad * ((self / other) / other), summed
+      // over the broadcast dim) + linalg_vector_norm backward (self * (grad / norm))
+      float gn = 0.f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) gn += -pg.vquat[k] * ((qr[k] / norm) / norm);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) vq[k] = pg.vquat[k] / norm + qr[k] * (gn / norm);
+      // sigmoid backward: grad * (1 - y) * y
+      const float y = a.opacity[g];
+      vlogit = r2.x * (1.f - y) * y;
+      const float vrgb[3] = {r1.y, r1.z, r1.w};
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const float col = a.colors[3 * g + c];
+        vc[c] = K == 1 ? vrgb[c] * (1.f - col) * col : (clamp0_passes(col) ? vrgb[c] : 0.f);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) a.v_means[3 * g + k] = vmean[k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) a.v_log_scales[3 * g + k] = vls[k];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) a.v_quats[4 * g + k] = vq[k];
+    a.v_opacity_logits[g] = vlogit;
+    if constexpr (K == 1) {
+#pragma unroll
+      for (int c = 0; c < 3; ++c) a.v_dc[3 * g + c] = vc[c];
+    } else if (a.v_colors) {  // data-parallel view exchange sums the SH gradient later
+#pragma unroll
+      for (int c = 0; c < 3; ++c) a.v_colors[3 * g + c] = vc[c];
+    } else {
+      float b[25];
+      b[0] = 0.f;
+      int nb = 0;  // culled: every coefficient gradient is 0
+      if (vis) nb = view_basis(a.degrees_to_use, p0, p1, p2, a.campos, b);
+      // gsplat compute_sh_backward: v_coeffs[k][c] = basis_k * v_rgb[c] for k < nb, else 0
+#pragma unroll
+      for (int c = 0; c < 3; ++c) a.v_dc[3 * g + c] = b[0] * vc[c];
+      float *row = smem + t * RP;
+#pragma unroll
+      for (int k = 1; k < K; ++k) {
+        const float bk = k < nb ? b[k] : 0.f;
+        row[(k - 1) * 3 + 0] = bk * vc[0];
+        row[(k - 1) * 3 + 1] = bk * vc[1];
+        row[(k - 1) * 3 + 2] = bk * vc[2];
+      }
+    }
+  }
+  if constexpr (K > 1) {
+    if (rest_out) {
+      __syncthreads();
+      store_cols<RROW, 0, RP, THR>(smem, cnt, a.v_rest + g0 * RROW);
+    }
+  }
+}
+
+bool valid_bases(int K) { return K == 1 || K == 4 || K == 9 || K == 16 || K == 25; }
+int degree_of(int K) { return K == 1 ? 0 : K == 4 ? 1 : K == 9 ? 2 : K == 16 ? 3 : 4; }
+
+}  // namespace
+}  // namespace gs
+
+using namespace gs;
+
+#define FUSED_DISPATCH(KERNEL, ARGS)                                                       \
+  switch (K) {                                                                            \
+    case 1: hipLaunchKernelGGL(KERNEL<1>, grid, dim3(thr), smem, st, ARGS, pp); break;    \
+    case 4: hipLaunchKernelGGL(KERNEL<4>, grid, dim3(thr), smem, st, ARGS, pp); break;    \
+    case 9: hipLaunchKernelGGL(KERNEL<9>, grid, dim3(thr), smem, st, ARGS, pp); break;    \
+    case 16: hipLaunchKernelGGL(KERNEL<16>, grid, dim3(thr), smem, st, ARGS, pp); break;  \
+    default: hipLaunchKernelGGL(KERNEL<25>, grid, dim3(thr), smem, st, ARGS, pp); break;  \
+  }
+
+extern "C" int gsplat_fused_preprocess_forward(
+    int num_points, int sh_bases, int degrees_to_use, const float *means3d,
+    const float *log_scales, const float *quats, const float *opacity_logits,
+    const float *features_dc, const float *features_rest, const float *viewmat,
+    const float *projmat, const float *campos, float fx, float fy, float cx, float cy,
+    int img_height, int img_width, int tile_bounds_x, int tile_bounds_y, float clip_thresh,
+    float *xys, float *depths, int32_t *radii, float *conics, int32_t *num_tiles_hit,
+    float *colors, float *opacity, void *grad_records, float *scales_out, float *quats_out,
+    void *stream) {
+  const int K = sh_bases;
+  if (num_points < 0 || !valid_bases(K) || degrees_to_use < 0 || degrees_to_use > degree_of(K) ||
+      img_height <= 0 || img_width <= 0 || tile_bounds_x <= 0 || tile_bounds_y <= 0 ||
+      (num_points > 0 && K > 1 && (!features_rest || !campos))) {
+    set_error("fused_preprocess_forward: bad args (N=%d sh_bases=%d degrees_to_use=%d H=%d W=%d "
+              "tiles=%dx%d)", num_points, sh_bases, degrees_to_use, img_height, img_width,
+              tile_bounds_x, tile_bounds_y);
+    return 1;
+  }
+  if (num_points == 0) return 0;
+  FusedFwdArgs args{num_points, degrees_to_use, means3d, log_scales, quats, opacity_logits,
+                    features_dc, features_rest, viewmat, projmat, campos, xys, depths, radii,
+                    conics, num_tiles_hit, colors, opacity, (float *)grad_records, scales_out,
+                    quats_out};
+  const ProjParams pp = make_proj_params(fx, fy, cx, cy, 1.f, clip_thresh, img_height,
+                                         img_width, tile_bounds_x, tile_bounds_y);
+  const int thr = sh_threads(K);
+  const dim3 grid(cdiv(num_points, thr));
+  const size_t smem = K > 1 ? (size_t)thr * (((K - 1) * 3) | 1) * sizeof(float) : 0;
+  hipStream_t st = (hipStream_t)stream;
+  FUSED_DISPATCH(fused_fwd_kernel, args);
+  return check_launch("fused_preprocess_forward");
+}
+
+extern "C" int gsplat_fused_preprocess_backward(
+    int num_points, int sh_bases, int degrees_to_use, const float *means3d,
+    const float *log_scales, const float *quats, const float *viewmat, const float *projmat,
+    const float *campos, float fx, float fy, float cx, float cy, int img_height, int img_width,
+    const int32_t *radii, const float *conics, const float *colors, const float *opacity,
+    const void *grad_records, float *v_means3d, float *v_log_scales, float *v_quats,
+    float *v_opacity_logits, float *v_features_dc, float *v_features_rest, float *v_colors,
+    void *stream) {
+  const int K = sh_bases;
+  if (num_points < 0 || !valid_bases(K) || degrees_to_use < 0 || degrees_to_use > degree_of(K) ||
+      img_height <= 0 || img_width <= 0 ||
+      (num_points > 0 && (!grad_records || (K > 1 && !campos) ||
+                          (K > 1 && !v_colors && !v_features_rest)))) {
+    set_error("fused_preprocess_backward: bad args (N=%d sh_bases=%d degrees_to_use=%d H=%d W=%d)",
+              num_points, sh_bases, degrees_to_use, img_height, img_width);
+    return 1;
+  }
+  if (num_points == 0) return 0;
+  // 0.5: the shipped packed backward accumulates 2 v_conic (raster.hip split_grads_kernel)
+  FusedBwdArgs args{num_points, degrees_to_use, means3d, log_scales, quats, viewmat, projmat,
+                    campos, radii, conics, colors, opacity, (const float *)grad_records, 0.5f,
+                    v_means3d, v_log_scales, v_quats, v_opacity_logits, v_features_dc,
+                    v_features_rest, K > 1 ? v_colors : nullptr};
+  const ProjParams pp = make_proj_params(fx, fy, cx, cy, 1.f, 0.f, img_height, img_width, 1, 1);
+  const int thr = sh_threads(K);
+  const dim3 grid(cdiv(num_points, thr));
+  const size_t smem = (K > 1 && !args.v_colors) ? (size_t)thr * (((K - 1) * 3) | 1) * sizeof(float)
+                                                : 0;
+  hipStream_t st = (hipStream_t)stream;
+  FUSED_DISPATCH(fused_bwd_kernel, args);
+  return check_launch("fused_preprocess_backward");
+}

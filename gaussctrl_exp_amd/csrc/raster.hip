@@ -1485,3 +1485,58 @@ extern "C" int gsplat_rasterize_backward_chunked(
                      num_points, (const float4 *)rec, 0.5f, v_xy, v_conic, v_colors, v_opacity);
   return check_launch("rasterize_backward_chunked");
 }
+
+extern "C" size_t gsplat_grad_records_bytes(int num_points) {
+  return num_points > 0 ? (size_t)num_points * REC * sizeof(float) : 0;
+}
+
+extern "C" int gsplat_rasterize_backward_records(
+    int tile_bounds_x, int tile_bounds_y, int img_height, int img_width, int num_points,
+    const int32_t *gaussian_ids_sorted, const int32_t *tile_bins, const float *xys,
+    const float *conics, const float *colors, const float *opacity, const float *background,
+    const float *final_Ts, const int32_t *final_idx, const float *v_output,
+    const float *v_output_alpha, float alpha_max, int64_t num_intersects, int chunk,
+    const void *checkpoints, size_t checkpoint_bytes, void *records, size_t records_bytes,
+    void *stream) {
+  hipStream_t st = (hipStream_t)stream;
+  const size_t need = gsplat_grad_records_bytes(num_points);
+  if (tile_bounds_x <= 0 || tile_bounds_y <= 0 || img_height <= 0 || img_width <= 0 ||
+      num_points < 0 || (long long)tile_bounds_x * GS_BLOCK < img_width ||
+      (long long)tile_bounds_y * GS_BLOCK < img_height || num_intersects < 0 ||
+      (chunk > 0 && chunk % 64) || records_bytes < need || (need && !records)) {
+    set_error("rasterize_backward_records: bad sizes (tiles=%dx%d H=%d W=%d N=%d chunk=%d "
+              "records %zu < %zu bytes)", tile_bounds_x, tile_bounds_y, img_height, img_width,
+              num_points, chunk, records_bytes, need);
+    return 1;
+  }
+  if (!default_variants()) {
+    set_error("rasterize_backward_records: needs the default raster variant");
+    return 1;
+  }
+  if (num_points == 0 || num_intersects == 0) return check_launch("rasterize_backward_records");
+  const int T = tile_bounds_x * tile_bounds_y;
+  float *rec = (float *)records;
+  if (chunk > 0) {
+    const ChunkWs w = carve_chunk_ws(const_cast<void *>(checkpoints), T, num_intersects, chunk);
+    if (!checkpoints || checkpoint_bytes < w.bytes) {
+      set_error("rasterize_backward_records: checkpoint buffer %zu < %zu bytes", checkpoint_bytes,
+                w.bytes);
+      return 1;
+    }
+    hipLaunchKernelGGL((raster_bwd3p_kernel<1, true, 16, true>),
+                       dim3((unsigned)cdiv(w.items_bound, (long long)(tiles_per_block<2, 16>()))),
+                       dim3(256), 0, st, tile_bounds_x, tile_bounds_y, img_height, img_width,
+                       gaussian_ids_sorted, (const int2 *)tile_bins, (const float2 *)xys, conics,
+                       colors, opacity, background, final_Ts, final_idx, v_output,
+                       v_output_alpha, alpha_max, rec, false, chunk, w.item_off, w.item_tile,
+                       w.ckpt_off, w.ckpt);
+  } else {
+    hipLaunchKernelGGL((raster_bwd3p_kernel<1, true, 16>),
+                       dim3(cdiv(T, (tiles_per_block<2, 16>()))), dim3(256), 0, st,
+                       tile_bounds_x, tile_bounds_y, img_height, img_width, gaussian_ids_sorted,
+                       (const int2 *)tile_bins, (const float2 *)xys, conics, colors, opacity,
+                       background, final_Ts, final_idx, v_output, v_output_alpha, alpha_max, rec,
+                       false);
+  }
+  return check_launch("rasterize_backward_records");
+}

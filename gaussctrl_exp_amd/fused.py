@@ -1,0 +1,198 @@
+"""Fused training render: the reference caller's glue and gsplat's three calls in four HIP
+kernel groups (csrc/preprocess.hip, binning.hip, raster.hip).
+
+GaussCtrlModel.get_outputs (/root/reference/gaussctrl/gc_model.py:158-222) turns the raw
+splatfacto parameters into gsplat's inputs with ~10 torch ops -- cat of the SH features
+(:172), exp(scales) (:177), quats / |quats| (:178), viewdirs (:197-198), SH + clamp (:200-201)
+or sigmoid(dc) (:203), sigmoid(opacities) (:215) -- then calls project_gaussians (:174),
+spherical_harmonics (:200) and rasterize_gaussians (:208) and clamps the image (:222).
+`render_fused` computes the same image and the same six parameter gradients with
+
+  forward:  gsplat_fused_preprocess_forward (activations + projection + SH + clamp, one
+            kernel) -> gsplat_bin_count / gsplat_bin_emit -> gsplat_rasterize_forward
+  backward: gsplat_rasterize_backward_records -> gsplat_fused_preprocess_backward (projection
+            VJP + SH backward + the activations' chain rule, one kernel)
+
+so none of the glue's elementwise kernels, reductions, the cat, its backward's strided copies
+or the caller's `radii.sum() == 0` host sync remain.  Results equal the unchanged-caller path
+(scene.render) within fp32 rounding of the activations; tests/test_gpu_fused.py holds both
+against the CPU oracle.  The unchanged caller (gc_model.py through the gsplat shim) is still
+the drop-in; this is the framework's own training step (TrainStep(render_mode="fused")).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+from torch import Tensor
+from torch.autograd import Function
+
+from . import _lib, exchange
+from .camera import GCCamera
+from .rasterize import BACKWARD_ALPHA_CLAMP, BLOCK_X, BLOCK_Y, bin_gaussians
+
+_DEG_OF_BASES = {1: 0, 4: 1, 9: 2, 16: 3, 25: 4}
+
+
+class _FusedRender(Function):
+    @staticmethod
+    def forward(ctx, means, scales, quats, opacities, features_dc, features_rest, viewmat,
+                projmat, campos, fx, fy, cx, cy, H, W, degrees_to_use, background,
+                return_alpha, aux):
+        n = means.shape[0]
+        K = 1 + features_rest.shape[1]
+        if K not in _DEG_OF_BASES or features_dc.shape != (n, 3) or \
+                features_rest.shape[-1] != 3 or means.shape != (n, 3):
+            raise ValueError("render_fused: bad parameter shapes")
+        if not 0 <= degrees_to_use <= _DEG_OF_BASES[K]:
+            raise ValueError(f"render_fused: degrees_to_use {degrees_to_use} > layout degree")
+        dev = _lib.check_device("render_fused", means, scales, quats, opacities, features_dc,
+                                features_rest, viewmat, projmat, campos, background)
+        H, W = int(H), int(W)
+        tbx, tby = (W + BLOCK_X - 1) // BLOCK_X, (H + BLOCK_Y - 1) // BLOCK_Y
+        f32 = dict(device=dev, dtype=torch.float32)
+        xys = torch.empty((n, 2), **f32)
+        depths = torch.empty((n,), **f32)
+        radii = torch.empty((n,), device=dev, dtype=torch.int32)
+        conics = torch.empty((n, 3), **f32)
+        nth = torch.empty((n,), device=dev, dtype=torch.int32)
+        colors = torch.empty((n, 3), **f32)
+        opac = torch.empty((n,), **f32)
+        need_grad = any(ctx.needs_input_grad[:6])
+        rec = torch.empty((max(_lib.query("gsplat_grad_records_bytes", n), 1),), device=dev,
+                          dtype=torch.uint8) if need_grad else None
+        P, st = _lib.ptr, _lib.stream(dev)
+        _lib.call("gsplat_fused_preprocess_forward", n, K, int(degrees_to_use), P(means),
+                  P(scales), P(quats), P(opacities), P(features_dc),
+                  P(features_rest) if K > 1 else None, P(viewmat), P(projmat), P(campos),
+                  float(fx), float(fy), float(cx), float(cy), H, W, tbx, tby, 0.01, P(xys),
+                  P(depths), P(radii), P(conics), P(nth), P(colors), P(opac), P(rec), None, None,
+                  st)
+        num_intersects, gids, bins = bin_gaussians(xys, depths, radii, nth, H, W)
+        chunk, ckpt = 0, None
+        if num_intersects < 1:
+            # nothing visible: the background (the caller returns it at gc_model.py:189-190),
+            # and every gradient is zero
+            out_img = torch.ones(H, W, 3, **f32) * background
+            final_Ts = torch.ones(H, W, **f32)
+            final_idx = torch.zeros(H, W, device=dev, dtype=torch.int32)
+        else:
+            out_img = torch.empty((H, W, 3), **f32)
+            final_Ts = torch.empty((H, W), **f32)
+            final_idx = torch.empty((H, W), device=dev, dtype=torch.int32)
+            chunk = _lib.query("gsplat_rasterize_chunk_size", tbx, tby, num_intersects) \
+                if need_grad else 0
+            if chunk > 0:
+                ckpt = torch.empty((_lib.query("gsplat_rasterize_checkpoint_bytes", tbx, tby,
+                                               num_intersects, chunk),),
+                                   device=dev, dtype=torch.uint8)
+                _lib.call("gsplat_rasterize_forward_chunked", tbx, tby, H, W, P(gids), P(bins),
+                          P(xys), P(conics), P(colors), P(opac), P(background), P(out_img),
+                          P(final_Ts), P(final_idx), num_intersects, chunk, P(ckpt),
+                          ckpt.numel(), st)
+            else:
+                _lib.call("gsplat_rasterize_forward", tbx, tby, H, W, 3, P(gids), P(bins),
+                          P(xys), P(conics), P(colors), P(opac), P(background), P(out_img),
+                          P(final_Ts), P(final_idx), st)
+        ctx.meta = (n, K, int(degrees_to_use), float(fx), float(fy), float(cx), float(cy), H, W,
+                    tbx, tby, num_intersects, chunk)
+        ctx.ckpt, ctx.rec = ckpt, rec
+        ctx.opac_shape = opacities.shape
+        ctx.exchange = exchange.active() if K > 1 else None
+        ctx.save_for_backward(means, scales, quats, features_rest, viewmat, projmat, campos,
+                              background, xys, radii, conics, colors, opac, gids, bins, final_Ts,
+                              final_idx)
+        ctx.set_materialize_grads(False)
+        aux.update(xys=xys, radii=radii, depths=depths, num_intersects=num_intersects,
+                   records=rec, num_points=n)
+        if return_alpha:
+            return out_img, 1 - final_Ts
+        return out_img
+
+    @staticmethod
+    def backward(ctx, v_img, v_alpha=None):
+        (means, scales, quats, features_rest, viewmat, projmat, campos, background, xys, radii,
+         conics, colors, opac, gids, bins, final_Ts, final_idx) = ctx.saved_tensors
+        n, K, dtu, fx, fy, cx, cy, H, W, tbx, tby, I, chunk = ctx.meta
+        dev = means.device
+        P, st = _lib.ptr, _lib.stream(dev)
+        rec = ctx.rec
+        if I >= 1 and (v_img is not None or v_alpha is not None):
+            v_img = v_img.float().contiguous() if v_img is not None else \
+                torch.zeros((H, W, 3), device=dev, dtype=torch.float32)
+            if v_alpha is not None:
+                v_alpha = v_alpha.float().contiguous()
+            _lib.call("gsplat_rasterize_backward_records", tbx, tby, H, W, n, P(gids), P(bins),
+                      P(xys), P(conics), P(colors), P(opac), P(background), P(final_Ts),
+                      P(final_idx), P(v_img), P(v_alpha), float(BACKWARD_ALPHA_CLAMP), I, chunk,
+                      P(ctx.ckpt), ctx.ckpt.numel() if ctx.ckpt is not None else 0, P(rec),
+                      rec.numel(), st)
+        f32 = dict(device=dev, dtype=torch.float32)
+        v_means = torch.empty((n, 3), **f32)
+        v_scales = torch.empty((n, 3), **f32)
+        v_quats = torch.empty((n, 4), **f32)
+        v_opac = torch.empty((n, 1), **f32)
+        v_dc = torch.empty((n, 3), **f32)
+        v_rest = torch.empty((n, K - 1, 3), **f32)
+        xchg = ctx.exchange
+        v_colors = torch.empty((n, 3), **f32) if xchg is not None else None
+        _lib.call("gsplat_fused_preprocess_backward", n, K, dtu, P(means), P(scales), P(quats),
+                  P(viewmat), P(projmat), P(campos), fx, fy, cx, cy, H, W, P(radii), P(conics),
+                  P(colors), P(opac), P(rec), P(v_means), P(v_scales), P(v_quats), P(v_opac),
+                  P(v_dc), P(v_rest) if K > 1 else None, P(v_colors), st)
+        if xchg is not None:
+            v_dc, v_rest = xchg.reduce(
+                v_colors, lambda m, views: sh_backward_views_split(_DEG_OF_BASES[K], dtu, m,
+                                                                   views))
+        return (v_means, v_scales, v_quats, v_opac.view(ctx.opac_shape), v_dc, v_rest) + \
+            (None,) * 13
+
+
+def sh_backward_views_split(degree: int, degrees_to_use: int, means: Tensor, views: Tensor):
+    """(v_features_dc [N,3], v_features_rest [N,K-1,3]) = sum_r Y(means - campos_r) (x)
+    v_colors_r over the gathered view records (exchange.ShViewExchange)."""
+    n = means.shape[0]
+    means = means.float().contiguous()
+    views = views.float().contiguous()
+    dev = _lib.check_device("sh_backward_views_split", means, views)
+    K = {0: 1, 1: 4, 2: 9, 3: 16, 4: 25}[degree]
+    v_dc = torch.empty((n, 3), device=dev, dtype=torch.float32)
+    v_rest = torch.empty((n, K - 1, 3), device=dev, dtype=torch.float32)
+    _lib.call("gsplat_compute_sh_backward_views_split", n, degree, int(degrees_to_use),
+              views.shape[0], _lib.ptr(means), _lib.ptr(views), views.shape[1], _lib.ptr(v_dc),
+              _lib.ptr(v_rest) if K > 1 else None, _lib.stream(dev))
+    return v_dc, v_rest
+
+
+def _contig_f32(t: Tensor) -> Tensor:
+    return t if (t.dtype == torch.float32 and t.is_contiguous()) else t.float().contiguous()
+
+
+def render_fused(scene, cam: GCCamera, sh_degree_to_use: int, background: Tensor,
+                 return_alpha: bool = False):
+    """scene.render's training output (gc_model.py:158-222) through the fused kernels.
+
+    Returns dict(rgb [H,W,3] (clamped at 1, gc_model.py:222), accumulation [H,W,1] or None,
+    xys [N,2] and radii [N] (detached), xys_grad: callable returning v_xy [N,2] after
+    backward -- what splatfacto's densification reads from `xys.grad`)."""
+    aux = {}
+    campos = cam.c2w[..., :3, 3].reshape(3)
+    args = [_contig_f32(scene.means), _contig_f32(scene.scales), _contig_f32(scene.quats),
+            _contig_f32(scene.opacities), _contig_f32(scene.features_dc),
+            _contig_f32(scene.features_rest), _contig_f32(cam.viewmat), _contig_f32(cam.projmat),
+            _contig_f32(campos), cam.fx, cam.fy, cam.cx, cam.cy, cam.height, cam.width,
+            int(sh_degree_to_use), _contig_f32(background), bool(return_alpha), aux]
+    out = _FusedRender.apply(*args)
+    img, alpha = (out if return_alpha else (out, None))
+    rgb = torch.clamp(img, max=1.0)
+
+    def xys_grad() -> Optional[Tensor]:
+        rec = aux.get("records")
+        if rec is None:
+            return None
+        v = rec[:aux["num_points"] * 64].view(torch.float32).view(-1, 16)[:, :2]
+        return torch.where(aux["radii"][:, None] > 0, v, torch.zeros_like(v))  # culled: 0
+
+    return {"rgb": rgb, "accumulation": alpha[..., None] if alpha is not None else None,
+            "xys": aux["xys"], "radii": aux["radii"], "xys_grad": xys_grad,
+            "num_intersects": aux["num_intersects"]}

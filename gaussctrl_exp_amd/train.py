@@ -24,6 +24,7 @@ import torch.nn.functional as F
 
 from .camera import GCCamera
 from .exchange import ShViewExchange
+from .fused import render_fused
 from .scene import PARAM_NAMES, GaussianScene, render
 
 # gc_config.py:58-87 (Adam, eps 1e-15); xyz decays 1.6e-4 -> 1.6e-6 over 30k steps.
@@ -124,7 +125,16 @@ class TrainStep:
 
     def __init__(self, scene: GaussianScene, sh_degree: int = 3, world_size: int = 1,
                  loss: str = "splatfacto", group=None, api=None,
-                 grad_exchange: str = "sh_views"):
+                 grad_exchange: str = "sh_views", render_mode: str = "caller"):
+        if render_mode not in ("caller", "fused"):
+            raise ValueError(f"render_mode must be 'caller' or 'fused', not {render_mode}")
+        if render_mode == "fused" and (api is not None or not scene.means.is_cuda):
+            raise ValueError("render_mode='fused' runs the MI355X kernels only (no api override, "
+                             "ROCm tensors)")
+        # "caller": scene.render, the reference caller's torch glue around the gsplat API
+        # (gc_model.py:158-238, what gc_model.py runs through the drop-in); "fused": the same
+        # step with that glue inside the HIP kernels (fused.render_fused)
+        self.render_mode = render_mode
         self.scene = scene.requires_grad_()
         self.params = scene.params()
         self.world_size = world_size
@@ -177,12 +187,17 @@ class TrainStep:
     def flat_grad(self) -> torch.Tensor:
         return torch.cat([p.grad.reshape(-1) for p in self.params])
 
+    def _render(self, cam: GCCamera, background: torch.Tensor):
+        if self.render_mode == "fused":
+            return render_fused(self.scene, cam, self.sh_degree, background)
+        return render(self.scene, cam, self.sh_degree, background, api=self.api)
+
     def forward_backward(self, cam: GCCamera, gt: torch.Tensor, background: torch.Tensor):
         if self.sh_exchange is not None:
             with self.sh_exchange.view(self.scene.means, cam.c2w[..., :3, 3]):
-                out = render(self.scene, cam, self.sh_degree, background, api=self.api)
+                out = self._render(cam, background)
         else:
-            out = render(self.scene, cam, self.sh_degree, background, api=self.api)
+            out = self._render(cam, background)
         loss = self.loss(out["rgb"], gt)
         if loss.requires_grad:
             loss.backward()

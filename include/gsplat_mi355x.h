@@ -28,6 +28,8 @@
  *                                         (gc_model.py:208-220, :225-236), fused
  *   gsplat_rasterize_forward           <- _C.rasterize_forward / _C.nd_rasterize_forward
  *   gsplat_rasterize_backward          <- _C.rasterize_backward / _C.nd_rasterize_backward
+ *   gsplat_fused_preprocess_forward /  <- gc_model.py:158-215's activations + project_gaussians
+ *   gsplat_fused_preprocess_backward      + spherical_harmonics (fused training render)
  */
 #ifndef GSPLAT_MI355X_H
 #define GSPLAT_MI355X_H
@@ -39,7 +41,7 @@
 extern "C" {
 #endif
 
-#define GSPLAT_MI355X_ABI_VERSION 5
+#define GSPLAT_MI355X_ABI_VERSION 6
 
 int gsplat_abi_version(void);
 const char *gsplat_last_error(void);
@@ -85,6 +87,14 @@ int gsplat_compute_sh_backward(int num_points, int degree, int degrees_to_use,
 int gsplat_compute_sh_backward_views(int num_points, int degree, int degrees_to_use,
                                      int num_views, const float *means3d, const float *views,
                                      long long view_stride, float *v_coeffs, void *stream);
+
+/* Split-output variant for the fused training path: v_dc [N,3] gets basis 0, v_rest
+ * [N, num_sh_bases(degree) - 1, 3] the rest (may be NULL when degree == 0) -- splatfacto's
+ * separate features_dc / features_rest gradients, without a combined tensor. */
+int gsplat_compute_sh_backward_views_split(int num_points, int degree, int degrees_to_use,
+                                           int num_views, const float *means3d,
+                                           const float *views, long long view_stride,
+                                           float *v_dc, float *v_rest, void *stream);
 
 /* covs2d [N,3] -> conics [N,3], radii [N] (float).  det == 0 rows get zeros. */
 int gsplat_compute_cov2d_bounds(int num_points, const float *covs2d, float *conics,
@@ -198,6 +208,58 @@ int gsplat_rasterize_backward(int tile_bounds_x, int tile_bounds_y, int img_heig
                               float alpha_max, float *v_xy, float *v_conic, float *v_colors,
                               float *v_opacity, void *workspace, size_t workspace_bytes,
                               void *stream);
+
+/* ---- fused training render (no gsplat counterpart; SURVEY.md §8a a1-a3, a10 + caller) ----
+ * The reference caller's per-Gaussian glue (gc_model.py:158-215: exp(scales), quats/|quats|,
+ * cat(features_dc, features_rest), viewdirs, SH -> clamp(rgb + 0.5, min 0) or sigmoid(dc),
+ * sigmoid(opacities)) evaluated inside the projection + SH kernel, and its chain rule inside
+ * the backward.  Raw splatfacto parameters in: means3d [N,3], log_scales [N,3], quats [N,4]
+ * (unnormalised), opacity_logits [N], features_dc [N,3], features_rest [N, sh_bases-1, 3]
+ * (NULL when sh_bases == 1), campos [3] (DEVICE; the camera centre, c2w[:3,3]).
+ * Forward writes xys, depths, radii, conics, num_tiles_hit (as gsplat_project_gaussians_forward
+ * on the activated inputs), colors [N,3] (clamped SH colour; a colour the clamp raised from
+ * below zero is stored as -0.0f so the backward knows it) and opacity [N] (sigmoid).  With
+ * grad_records != NULL (gsplat_grad_records_bytes) it zeroes the record of every visible
+ * Gaussian for gsplat_rasterize_backward_records.  scales_out [N,3] / quats_out [N,4]
+ * (optional, testing) receive the activated scales and normalised quaternions.
+ * Backward reads the records and writes v_means3d [N,3], v_log_scales [N,3], v_quats [N,4],
+ * v_opacity_logits [N] and either v_features_dc [N,3] + v_features_rest [N, sh_bases-1, 3],
+ * or -- v_colors != NULL, sh_bases > 1, data-parallel view exchange -- the gradient of the SH
+ * colour v_colors [N,3] instead of the two feature gradients (sum them with
+ * gsplat_compute_sh_backward_views_split).  Every output is fully written. */
+int gsplat_fused_preprocess_forward(
+    int num_points, int sh_bases, int degrees_to_use, const float *means3d,
+    const float *log_scales, const float *quats, const float *opacity_logits,
+    const float *features_dc, const float *features_rest, const float *viewmat,
+    const float *projmat, const float *campos, float fx, float fy, float cx, float cy,
+    int img_height, int img_width, int tile_bounds_x, int tile_bounds_y, float clip_thresh,
+    float *xys, float *depths, int32_t *radii, float *conics, int32_t *num_tiles_hit,
+    float *colors, float *opacity, void *grad_records, float *scales_out, float *quats_out,
+    void *stream);
+int gsplat_fused_preprocess_backward(
+    int num_points, int sh_bases, int degrees_to_use, const float *means3d,
+    const float *log_scales, const float *quats, const float *viewmat, const float *projmat,
+    const float *campos, float fx, float fy, float cx, float cy, int img_height, int img_width,
+    const int32_t *radii, const float *conics, const float *colors, const float *opacity,
+    const void *grad_records, float *v_means3d, float *v_log_scales, float *v_quats,
+    float *v_opacity_logits, float *v_features_dc, float *v_features_rest, float *v_colors,
+    void *stream);
+
+/* Per-Gaussian gradient records (64 B each) the fused path's rasterize backward accumulates
+ * into: gsplat_rasterize_backward_records is gsplat_rasterize_backward (C = 3, default
+ * variant, list-split when chunk > 0 as in the _chunked entry) without the zero fill and
+ * without the split into v_xy / v_conic / v_colors / v_opacity -- the records must be zeroed
+ * by the caller (gsplat_fused_preprocess_forward does it for visible Gaussians) and are read
+ * by gsplat_fused_preprocess_backward. */
+size_t gsplat_grad_records_bytes(int num_points);
+int gsplat_rasterize_backward_records(
+    int tile_bounds_x, int tile_bounds_y, int img_height, int img_width, int num_points,
+    const int32_t *gaussian_ids_sorted, const int32_t *tile_bins, const float *xys,
+    const float *conics, const float *colors, const float *opacity, const float *background,
+    const float *final_Ts, const int32_t *final_idx, const float *v_output,
+    const float *v_output_alpha, float alpha_max, int64_t num_intersects, int chunk,
+    const void *checkpoints, size_t checkpoint_bytes, void *records, size_t records_bytes,
+    void *stream);
 
 /* Tuning / ablation hook (not part of the gsplat surface): pixels per lane of the 3-channel
  * forward and backward kernels (1, 2 or 4; a 16x16 tile is covered by 4/pxl waves), and

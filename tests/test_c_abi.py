@@ -30,9 +30,29 @@ def test_library_exports_every_declared_symbol():
     assert set(names) == set(_lib.SIGNATURES)
 
 
+def _prototypes():
+    """{name: parameter count} of every prototype in the header."""
+    src = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    out = {}
+    for m in re.finditer(r"\b(gsplat_[a-z0-9_]+)\s*\(([^;]*?)\)\s*;", src, flags=re.S):
+        params = m.group(2).strip()
+        out[m.group(1)] = 0 if params in ("", "void") else params.count(",") + 1
+    return out
+
+
+def test_binding_arities_match_the_header():
+    """ctypes argtypes have exactly as many entries as the C prototypes have parameters."""
+    from gaussctrl_exp_amd import _lib
+    protos = _prototypes()
+    assert set(protos) == set(_lib.SIGNATURES)
+    wrong = {n: (len(_lib.SIGNATURES[n][1]), k) for n, k in protos.items()
+             if len(_lib.SIGNATURES[n][1]) != k}
+    assert not wrong, wrong
+
+
 def test_host_queries_without_gpu():
     from gaussctrl_exp_amd import _lib
-    assert _lib.lib().gsplat_abi_version() == _lib.ABI_VERSION == 5
+    assert _lib.lib().gsplat_abi_version() == _lib.ABI_VERSION == 6
     assert _lib.query("gsplat_bin_count_workspace_size", 1000) > 1000 * 16
     assert _lib.query("gsplat_bin_emit_workspace_size", 10 ** 6) >= 5 * 4 * 10 ** 6
     assert _lib.query("gsplat_sort_isect_pairs_workspace_size", 0) > 0

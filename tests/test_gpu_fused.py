@@ -1,0 +1,217 @@
+"""The fused training render (csrc/preprocess.hip via fused.render_fused) against the CPU
+oracle and against the unchanged-caller path (scene.render: gc_model.py's torch glue around
+the gsplat API).
+
+Bars: given the activated inputs the fused kernel computed (its optional scales_out /
+quats_out), the projection outputs, tile counts and therefore the binning are bit-exact with
+the oracle; the activations themselves are torch's formulas in fp32 (within 1 ulp of torch's
+kernels); images, alpha and all six parameter gradients meet the end-to-end bar of
+test_gpu_parity.test_end_to_end_render_grads (per element 1e-5 + 1e-4 |ref|, <= 0.2 % of
+elements outside).
+"""
+import json
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+from gaussctrl_exp_amd import _lib
+from gaussctrl_exp_amd.camera import gc_camera, look_at_c2w, synthetic_camera
+from gaussctrl_exp_amd.fused import render_fused
+from gaussctrl_exp_amd.scene import render, synthetic_scene
+
+pytestmark = pytest.mark.gpu
+
+ATOL, RTOL = 1e-5, 1e-4
+NAMES = ["means", "scales", "quats", "opacities", "features_dc", "features_rest"]
+STATS = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out",
+                     "fused_activation_stats.json")
+
+
+def _np(t):
+    return t.detach().cpu().numpy()
+
+
+def _bad_frac(a, b, atol=ATOL, rtol=RTOL):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    bad = ~(np.abs(a - b) <= atol + rtol * np.abs(b))  # NaN counts as out of tolerance
+    return (bad.mean() if bad.size else 0.0), (np.abs(a - b).max() if a.size else 0.0)
+
+
+# (n, W, H, sh_degree, degrees_to_use, seed, scale_lo, scale_hi, extent)
+CASES = [
+    (3000, 128, 96, 3, 3, 21, 0.01, 0.06, 1.5),
+    (2000, 64, 48, 3, 1, 0, 0.01, 0.08, 1.5),     # ragged image, fewer bands than stored
+    (3000, 100, 75, 3, 3, 3, 0.02, 0.3, 4.0),     # large Gaussians, some behind the camera
+    (2500, 96, 64, 0, 0, 5, 0.01, 0.05, 1.5),     # one SH band: sigmoid colours (gc_model:203)
+    (2500, 96, 64, 2, 0, 6, 0.01, 0.05, 1.5),     # SH path evaluated at degree 0
+    (2500, 80, 64, 4, 4, 7, 0.01, 0.05, 1.5),     # degree 4 (128-thread blocks)
+    (20000, 512, 512, 3, 3, 2, 0.003, 0.03, 1.5),  # 1,024 tiles: list-split backward
+]
+
+
+def _scene_cam(case):
+    n, W, H, deg, dtu, seed, lo, hi, ext = case
+    return synthetic_scene(n, deg, seed=seed, scale_lo=lo, scale_hi=hi, extent=ext), \
+        synthetic_camera(W, H)
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_fused_forward_bitexact_given_activations(gpu, case):
+    sc, cam = _scene_cam(case)
+    n, W, H, deg, dtu = case[:5]
+    d = sc.to(gpu)
+    c = cam.to(gpu)
+    K = d.features_rest.shape[1] + 1
+    f = lambda *s: torch.empty(*s, device=gpu)
+    xys, depths, conics, colors, opac = f(n, 2), f(n), f(n, 3), f(n, 3), f(n)
+    radii = torch.empty(n, device=gpu, dtype=torch.int32)
+    nth = torch.empty(n, device=gpu, dtype=torch.int32)
+    s_out, q_out = f(n, 3), f(n, 4)
+    campos = c.c2w[:3, 3].contiguous()
+    P = _lib.ptr
+    tb = cam.tile_bounds
+    _lib.call("gsplat_fused_preprocess_forward", n, K, dtu, P(d.means), P(d.scales), P(d.quats),
+              P(d.opacities), P(d.features_dc), P(d.features_rest) if K > 1 else None,
+              P(c.viewmat), P(c.projmat), P(campos), cam.fx, cam.fy, cam.cx, cam.cy, H, W,
+              tb[0], tb[1], 0.01, P(xys), P(depths), P(radii), P(conics), P(nth), P(colors),
+              P(opac), None, P(s_out), P(q_out), _lib.stream(gpu))
+    # activations: torch's formulas in fp32 (record how often they equal torch's kernels)
+    t_s = torch.exp(d.scales)
+    t_q = d.quats / d.quats.norm(dim=-1, keepdim=True)
+    t_o = torch.sigmoid(d.opacities).reshape(-1)
+    stats = {}
+    for name, mine, ref in (("scales", s_out, t_s), ("quats", q_out, t_q), ("opacity", opac, t_o)):
+        a, b = _np(mine).astype(np.float64), _np(ref).astype(np.float64)
+        rel = np.abs(a - b) / np.maximum(np.abs(b), 1e-30)
+        stats[name] = {"equal_frac": float((a == b).mean()), "max_rel": float(rel.max())}
+        # bit-identical to torch's own kernels (exp, the 4-vector norm order, sigmoid)
+        assert (a == b).all(), f"{name}: {1 - (a == b).mean():.2e} differ from torch"
+    os.makedirs(os.path.dirname(STATS), exist_ok=True)
+    if case == CASES[0]:  # torch's 3-vector norms (view directions), to study offline
+        vd = d.means - c.c2w[:3, 3]
+        np.savez(os.path.join(os.path.dirname(STATS), "norm3_probe.npz"), v=_np(vd),
+                 torch_norm=_np(vd.norm(dim=-1)))
+    with open(STATS, "a") as fh:
+        fh.write(json.dumps({"case": list(case), **stats}) + "\n")
+    # projection: bit-exact with the oracle on the kernel's own activated inputs
+    o = O.project_forward(_np(d.means), _np(s_out), 1.0, _np(q_out), cam.viewmat.numpy(),
+                          cam.projmat.numpy(), cam.fx, cam.fy, cam.cx, cam.cy, H, W, tb)
+    for name, g, r in zip(["xys", "depths", "radii", "conics", "num_tiles_hit"],
+                          [xys, depths, radii, conics, nth], o[:5]):
+        np.testing.assert_array_equal(_np(g), r, err_msg=name)
+    assert (o[2] > 0).sum() > 0
+    # colours: the caller's SH + clamp (or sigmoid) on the oracle
+    if K > 1:
+        vd = d.means - c.c2w[:3, 3]
+        vd = vd / vd.norm(dim=-1, keepdim=True)
+        coeffs = torch.cat([d.features_dc[:, None], d.features_rest], 1)
+        ref = np.maximum(O.sh_forward(dtu, _np(vd), _np(coeffs)) + 0.5, 0.0)
+    else:
+        ref = _np(torch.sigmoid(d.features_dc))
+    frac, mx = _bad_frac(_np(colors), ref, atol=1e-6, rtol=1e-5)
+    assert frac == 0.0, f"colors: {frac:.2e} out of tolerance (max {mx:.3e})"
+
+
+def _run(sc, cam, deg, bg, gt, dev, mode, api=None):
+    s = sc.to(dev).requires_grad_()
+    c = cam.to(dev)
+    if mode == "fused":
+        out = render_fused(s, c, deg, bg.to(dev), return_alpha=True)
+    else:
+        out = render(s, c, deg, bg.to(dev), api=api)
+    # sums, not means: O(1) gradients, so the absolute tolerance cannot hide a wrong one
+    loss = (out["rgb"] - gt.to(dev)).abs().sum() + 0.1 * out["accumulation"].sum()
+    loss.backward()
+    return [_np(out["rgb"]), _np(out["accumulation"])] + [_np(p.grad) for p in s.params()]
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_fused_render_grads_match_caller_and_oracle(gpu, case):
+    from oracle_gsplat import API
+    sc, cam = _scene_cam(case)
+    deg = case[4]
+    bg = torch.tensor([0.3, 0.6, 0.9])
+    gt = torch.rand(cam.height, cam.width, 3, generator=torch.Generator().manual_seed(4))
+    fused = _run(sc, cam, deg, bg, gt, gpu, "fused")
+    caller = _run(sc, cam, deg, bg, gt, gpu, "caller")
+    ref = _run(sc, cam, deg, bg, gt, torch.device("cpu"), "caller", api=API)
+    for i, name in enumerate(["rgb", "alpha"] + NAMES):
+        assert np.isfinite(fused[i]).all(), f"{name}: non-finite values"
+        if fused[i].size and i >= 2 and not (name == "features_rest" and deg == 0):
+            assert np.abs(ref[i]).max() > 1e-3, f"{name}: degenerate reference gradient"
+        for other, label in ((ref, "oracle"), (caller, "gpu caller path")):
+            frac, mx = _bad_frac(fused[i], other[i])
+            assert frac <= 2e-3, f"{name} vs {label}: {frac:.2e} out of tolerance (max {mx:.3e})"
+
+
+def test_fused_xys_grad_matches_retain_grad(gpu):
+    sc, cam = _scene_cam(CASES[0])
+    bg = torch.zeros(3)
+    gt = torch.rand(cam.height, cam.width, 3, generator=torch.Generator().manual_seed(1))
+    s = sc.to(gpu).requires_grad_()
+    out = render_fused(s, cam.to(gpu), 3, bg.to(gpu))
+    (out["rgb"] - gt.to(gpu)).abs().sum().backward()
+    s2 = sc.to(gpu).requires_grad_()
+    ref = render(s2, cam.to(gpu), 3, bg.to(gpu))
+    (ref["rgb"] - gt.to(gpu)).abs().sum().backward()
+    frac, mx = _bad_frac(_np(out["xys_grad"]()), _np(ref["xys"].grad))
+    assert frac <= 2e-3, f"xys.grad: {frac:.2e} out of tolerance (max {mx:.3e})"
+
+
+def test_fused_empty_view_gives_background_and_zero_grads(gpu):
+    sc = synthetic_scene(2000, 3, seed=1).to(gpu).requires_grad_()
+    away = gc_camera(look_at_c2w((0.0, 0.0, 4.0), target=(0.0, 0.0, 8.0), up=(0.0, 1.0, 0.0)),
+                     200.0, 200.0, 64.0, 48.0, 128, 96).to(gpu)
+    bg = torch.tensor([0.2, 0.4, 0.6], device=gpu)
+    out = render_fused(sc, away, 3, bg, return_alpha=True)
+    assert out["num_intersects"] == 0
+    assert torch.equal(out["rgb"], bg.expand(96, 128, 3))
+    assert not out["accumulation"].any()
+    out["rgb"].sum().backward()
+    assert all(p.grad is not None and not p.grad.any() for p in sc.params())
+
+
+def test_fused_rejects_cpu_tensors():
+    sc = synthetic_scene(10)
+    with pytest.raises(RuntimeError, match="ROCm device"):
+        render_fused(sc, synthetic_camera(32, 32), 3, torch.zeros(3))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def test_fused_trainstep_exchange_over_rccl_world1(gpu):
+    """TrainStep(render_mode="fused") single-rank vs its multi-rank configuration (SH view
+    exchange through gsplat_compute_sh_backward_views_split + all-reduces) over RCCL at world
+    size 1, and vs the caller-glue TrainStep."""
+    import torch.distributed as dist
+    from gaussctrl_exp_amd.train import TrainStep
+
+    store = dist.TCPStore("127.0.0.1", _free_port(), 1, True)
+    dist.init_process_group("nccl", store=store, rank=0, world_size=1, device_id=gpu)
+    try:
+        cam = synthetic_camera(256, 192).to(gpu)
+        gt = torch.rand(192, 256, 3, generator=torch.Generator().manual_seed(2)).to(gpu)
+        bg = torch.tensor([0.2, 0.3, 0.4], device=gpu)
+        flats = {}
+        for ws, mode in ((1, "fused"), (2, "fused"), (1, "caller")):
+            t = TrainStep(synthetic_scene(20000, 3, seed=6, device=gpu), sh_degree=3,
+                          world_size=ws, loss="splatfacto", render_mode=mode)
+            t.step(cam, gt, background=bg, optimizer=False)
+            flats[(ws, mode)] = t.flat_grad().cpu().numpy()
+        base = flats[(1, "fused")]
+        assert np.abs(base).max() > 0
+        np.testing.assert_allclose(flats[(2, "fused")], base, rtol=1e-5, atol=1e-6)
+        frac, mx = _bad_frac(base, flats[(1, "caller")])
+        assert frac <= 2e-3, f"fused vs caller train step: {frac:.2e} (max {mx:.3e})"
+    finally:
+        dist.destroy_process_group()

@@ -33,7 +33,7 @@ def _close_frac(a, b, atol=ATOL, rtol=RTOL, abs_sum=None):
     tol = atol + rtol * np.abs(b)
     if abs_sum is not None:
         tol = tol + np.asarray(abs_sum, np.float64).reshape(b.shape) * 2.0 ** -20
-    bad = np.abs(a - b) > tol
+    bad = ~(np.abs(a - b) <= tol)  # NaN counts as out of tolerance
     return bad.mean() if bad.size else 0.0, (np.abs(a - b).max() if a.size else 0.0)
 
 
@@ -405,7 +405,8 @@ def test_end_to_end_render_grads(gpu):
         s = sc.to(dev).requires_grad_()
         c = cam.to(dev)
         out = render(s, c, 3, bg.to(dev), api=api)
-        loss = (out["rgb"] - gt.to(dev)).abs().mean() + 0.1 * out["accumulation"].mean()
+        # sums, not means: O(1) gradients, so the absolute tolerance cannot hide a wrong one
+        loss = (out["rgb"] - gt.to(dev)).abs().sum() + 0.1 * out["accumulation"].sum()
         loss.backward()
         with torch.no_grad():
             dep = render(s, c, 3, bg.to(dev), return_depth=True, api=api)["depth"]
