@@ -220,7 +220,7 @@ int gsplat_rasterize_backward(int tile_bounds_x, int tile_bounds_y, int img_heig
  * on the activated inputs), colors [N,3] (clamped SH colour; a colour the clamp raised from
  * below zero is stored as -0.0f so the backward knows it) and opacity [N] (sigmoid).  With
  * grad_records != NULL (gsplat_grad_records_bytes) it zeroes the record of every visible
- * Gaussian for gsplat_rasterize_backward_records.  scales_out [N,3] / quats_out [N,4]
+ * Gaussian (radii > 0) for gsplat_rasterize_backward_records.  scales_out [N,3] / quats_out [N,4]
  * (optional, testing) receive the activated scales and normalised quaternions.
  * Backward reads the records and writes v_means3d [N,3], v_log_scales [N,3], v_quats [N,4],
  * v_opacity_logits [N] and either v_features_dc [N,3] + v_features_rest [N, sh_bases-1, 3],
@@ -249,7 +249,8 @@ int gsplat_fused_preprocess_backward(
  * into: gsplat_rasterize_backward_records is gsplat_rasterize_backward (C = 3, default
  * variant, list-split when chunk > 0 as in the _chunked entry) without the zero fill and
  * without the split into v_xy / v_conic / v_colors / v_opacity -- the records must be zeroed
- * by the caller (gsplat_fused_preprocess_forward does it for visible Gaussians) and are read
+ * by the caller (gsplat_fused_preprocess_forward does it for the visible Gaussians, the
+ * only ones the kernel touches) and are read
  * by gsplat_fused_preprocess_backward. */
 size_t gsplat_grad_records_bytes(int num_points);
 int gsplat_rasterize_backward_records(

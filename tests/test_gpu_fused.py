@@ -91,10 +91,6 @@ def test_fused_forward_bitexact_given_activations(gpu, case):
         # bit-identical to torch's own kernels (exp, the 4-vector norm order, sigmoid)
         assert (a == b).all(), f"{name}: {1 - (a == b).mean():.2e} differ from torch"
     os.makedirs(os.path.dirname(STATS), exist_ok=True)
-    if case == CASES[0]:  # torch's 3-vector norms (view directions), to study offline
-        vd = d.means - c.c2w[:3, 3]
-        np.savez(os.path.join(os.path.dirname(STATS), "norm3_probe.npz"), v=_np(vd),
-                 torch_norm=_np(vd.norm(dim=-1)))
     with open(STATS, "a") as fh:
         fh.write(json.dumps({"case": list(case), **stats}) + "\n")
     # projection: bit-exact with the oracle on the kernel's own activated inputs
@@ -114,6 +110,23 @@ def test_fused_forward_bitexact_given_activations(gpu, case):
         ref = _np(torch.sigmoid(d.features_dc))
     frac, mx = _bad_frac(_np(colors), ref, atol=1e-6, rtol=1e-5)
     assert frac == 0.0, f"colors: {frac:.2e} out of tolerance (max {mx:.3e})"
+    # and bit-identical to the unchanged caller's path on the GPU (torch glue + gsplat API)
+    from gaussctrl_exp_amd.project_gaussians import project_gaussians
+    from gaussctrl_exp_amd.sh import spherical_harmonics
+    with torch.no_grad():
+        g = project_gaussians(d.means, t_s, 1, t_q, c.viewmat, c.projmat, cam.fx, cam.fy,
+                              cam.cx, cam.cy, H, W, tb)
+        if K > 1:
+            vd = d.means - c.c2w[:3, 3]
+            vd = vd / vd.norm(dim=-1, keepdim=True)
+            cc = torch.clamp(spherical_harmonics(dtu, vd, torch.cat(
+                [d.features_dc[:, None], d.features_rest], 1)) + 0.5, min=0.0)
+        else:
+            cc = torch.sigmoid(d.features_dc)
+    for name, mine, theirs in zip(["xys", "depths", "radii", "conics", "num_tiles_hit",
+                                   "colors"], [xys, depths, radii, conics, nth, colors],
+                                  list(g[:5]) + [cc]):
+        assert torch.equal(mine, theirs), f"{name}: fused != caller path"
 
 
 def _run(sc, cam, deg, bg, gt, dev, mode, api=None):
