@@ -1,7 +1,8 @@
 // sh_math.h -- real spherical-harmonics basis (degrees 0-4) and the LDS row staging shared by
 // sh.hip (gsplat compute_sh_forward / backward) and preprocess.hip (the fused caller glue).
 // Restates gsplat 0.1.2.1 sh.cuh.  The arithmetic carries its own
-// `fp contract(fast)` pragma, so it rounds the same in the -ffp-contract=off translation
+// `fp contract(on)` pragma (a*b+c fused within one expression, never across statements), so
+// it rounds the same in the -ffp-contract=off translation
 // units (preprocess.hip) as in the default ones (sh.hip).
 #pragma once
 
@@ -31,7 +32,7 @@ __host__ __device__ __forceinline__ int num_bases(int degree) {
 
 // Basis values in sh_coeffs_to_color's consumption order (same expressions as the oracle).
 __device__ __forceinline__ int sh_basis(int degree, float dx, float dy, float dz, float *b) {
-#pragma clang fp contract(fast)
+#pragma clang fp contract(on)
   b[0] = SH_C0;
   if (degree < 1) return 1;
   float norm = sqrtf(dx * dx + dy * dy + dz * dz);
@@ -196,7 +197,7 @@ __device__ __forceinline__ void store_rows(const float *smem, int cnt, float *ds
 // gsplat's sh_coeffs_to_color does; co(k) returns basis k's coefficient of this channel.
 template <int K, typename Co>
 __device__ __forceinline__ float sh_channel(const float *b, int nb, Co co) {
-#pragma clang fp contract(fast)
+#pragma clang fp contract(on)
   float acc = b[0] * co(0);
 #pragma unroll
   for (int band = 1; band <= 4; ++band) {
