@@ -62,8 +62,8 @@ SIGNATURES = {
     "gsplat_debug_sort_scheme": (_I, [_I]),
     "gsplat_debug_sort_items": (_I, [_I]),
     "gsplat_l1_ssim_num_blocks": (_I, [_I, _I]),
-    "gsplat_l1_ssim_forward": (_I, [_I, _I, _I, _P, _P, _P, _F, _P, _P, _P, _P]),
-    "gsplat_l1_ssim_backward": (_I, [_I, _I, _I, _P, _P, _P, _F, _P, _P, _P, _P]),
+    "gsplat_l1_ssim_forward": (_I, [_I, _I, _I, _P, _P, _P, _F, _I, _P, _P, _P, _P]),
+    "gsplat_l1_ssim_backward": (_I, [_I, _I, _I, _P, _P, _P, _F, _I, _P, _P, _P, _P]),
     "gsplat_adam_step": (_I, [_I, _P, _P, _P, _P, _P, _P, _I, _F, _F, _F, _P]),
     "gsplat_rasterize_backward": (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P,
                                        _P, _P, _P, _F, _P, _P, _P, _P, _P, _SZ, _P]),

@@ -50,6 +50,19 @@ __device__ __forceinline__ float block_sum(float v, float *red) {
 
 // partials[block] = {sum |gt - pred| over the block's input pixels (all channels),
 //                    sum of SSIM map values over the block's valid outputs (all channels)}
+// The caller's image clamp (gc_model.py:222: torch.clamp(rgb, max=1.0)) folded into the loss:
+// CLAMP kernels read min(pred, 1) (NaN stays NaN, as torch.clamp) and mask the gradient where
+// torch's clamp backward does (pass where pred <= 1).
+template <bool CLAMP>
+__device__ __forceinline__ float clamp_pred(float x) {
+  return CLAMP ? (x > 1.f ? 1.f : x) : x;
+}
+template <bool CLAMP>
+__device__ __forceinline__ float clamp_mask(float x) {
+  return CLAMP ? (x <= 1.f ? 1.f : 0.f) : 1.f;
+}
+
+template <bool CLAMP>
 __global__ __launch_bounds__(256) void l1_ssim_fwd_kernel(int H, int W, int C,
                                                           const float *__restrict__ pred,
                                                           const float *__restrict__ gt, Win win,
@@ -78,7 +91,7 @@ __global__ __launch_bounds__(256) void l1_ssim_fwd_kernel(int H, int W, int C,
       px[u] = py[u] = 0.f;
       if (k < PH * PW && i < H && j < W) {
         px[u] = gt[((size_t)i * W + j) * C + c];
-        py[u] = pred[((size_t)i * W + j) * C + c];
+        py[u] = clamp_pred<CLAMP>(pred[((size_t)i * W + j) * C + c]);
       }
     }
   };
@@ -167,6 +180,7 @@ __global__ __launch_bounds__(256) void l1_ssim_fwd_kernel(int H, int W, int C,
 
 // ssim_lambda == 0: plain L1 (the SSIM term has weight zero) -- one streaming pass.
 // partials[2 b] = sum |gt - pred| over this block's grid-stride share, partials[2 b + 1] = 0.
+template <bool CLAMP>
 __global__ __launch_bounds__(256) void l1_only_fwd_kernel(long long n, const float *__restrict__ pred,
                                                           const float *__restrict__ gt,
                                                           float *__restrict__ partials) {
@@ -174,7 +188,7 @@ __global__ __launch_bounds__(256) void l1_only_fwd_kernel(long long n, const flo
   float acc = 0.f;
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n;
        i += (long long)gridDim.x * 256)
-    acc += fabsf(gt[i] - pred[i]);
+    acc += fabsf(gt[i] - clamp_pred<CLAMP>(pred[i]));
   acc = block_sum(acc, red);
   if (threadIdx.x == 0) {
     partials[2 * blockIdx.x] = acc;
@@ -182,6 +196,7 @@ __global__ __launch_bounds__(256) void l1_only_fwd_kernel(long long n, const flo
   }
 }
 
+template <bool CLAMP>
 __global__ __launch_bounds__(256) void l1_only_bwd_kernel(long long n, const float *__restrict__ pred,
                                                           const float *__restrict__ gt,
                                                           const float *__restrict__ grad_out,
@@ -190,8 +205,9 @@ __global__ __launch_bounds__(256) void l1_only_bwd_kernel(long long n, const flo
   const float gl = grad_out[0] * l1_scale;
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n;
        i += (long long)gridDim.x * 256) {
-    const float d = pred[i] - gt[i];
-    v_pred[i] = gl * (d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f));
+    const float p = pred[i];
+    const float d = clamp_pred<CLAMP>(p) - gt[i];
+    v_pred[i] = gl * (d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f)) * clamp_mask<CLAMP>(p);
   }
 }
 
@@ -220,6 +236,7 @@ __global__ __launch_bounds__(256) void l1_ssim_finalize_kernel(int nblocks, cons
     loss[0] = (float)((1.0 - lambda) * ra[0] * inv_l1 + lambda * (1.0 - rb[0] * inv_ssim));
 }
 
+template <bool CLAMP>
 __global__ __launch_bounds__(256) void l1_ssim_bwd_kernel(
     int H, int W, int C, const float *__restrict__ pred, const float *__restrict__ gt, Win win,
     const float *__restrict__ dmaps, const float *__restrict__ grad_out, float ssim_scale,
@@ -299,10 +316,12 @@ __global__ __launch_bounds__(256) void l1_ssim_bwd_kernel(
       const int i = by + ty + rr, j = bx + tx;
       if (i < H && j < W) {
         const size_t e = ((size_t)i * W + j) * C + c;
-        const float xv = gt[e], yv = pred[e];
+        const float p = pred[e];
+        const float xv = gt[e], yv = clamp_pred<CLAMP>(p);
         const float d = yv - xv;
         const float sgn = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
-        v_pred[e] = gs * (s[rr][0] + 2.f * yv * s[rr][1] + xv * s[rr][2]) + gl * sgn;
+        v_pred[e] = (gs * (s[rr][0] + 2.f * yv * s[rr][1] + xv * s[rr][2]) + gl * sgn) *
+                    clamp_mask<CLAMP>(p);
       }
     }
     __syncthreads();
@@ -336,18 +355,26 @@ static Win load_win(const float *window) {
 
 extern "C" int gsplat_l1_ssim_forward(int img_height, int img_width, int channels,
                                       const float *pred, const float *gt, const float *window11,
-                                      float ssim_lambda, float *partials, float *dmaps,
-                                      float *loss, void *stream) {
+                                      float ssim_lambda, int clamp_pred, float *partials,
+                                      float *dmaps, float *loss, void *stream) {
   if (!l1_ssim_args_ok(img_height, img_width, channels, "l1_ssim_forward", ssim_lambda)) return 1;
   hipStream_t st = (hipStream_t)stream;
   const int nb = gsplat_l1_ssim_num_blocks(img_height, img_width);
   if (ssim_lambda == 0.f) {  // L1 only: no SSIM statistics, dmaps untouched
-    hipLaunchKernelGGL(l1_only_fwd_kernel, dim3(nb), dim3(256), 0, st,
-                       (long long)img_height * img_width * channels, pred, gt, partials);
+    if (clamp_pred)
+      hipLaunchKernelGGL(l1_only_fwd_kernel<true>, dim3(nb), dim3(256), 0, st,
+                         (long long)img_height * img_width * channels, pred, gt, partials);
+    else
+      hipLaunchKernelGGL(l1_only_fwd_kernel<false>, dim3(nb), dim3(256), 0, st,
+                         (long long)img_height * img_width * channels, pred, gt, partials);
   } else {
     const Win w = load_win(window11);
-    hipLaunchKernelGGL(l1_ssim_fwd_kernel, dim3(nb), dim3(256), 0, st, img_height, img_width,
-                       channels, pred, gt, w, partials, dmaps);
+    if (clamp_pred)
+      hipLaunchKernelGGL(l1_ssim_fwd_kernel<true>, dim3(nb), dim3(256), 0, st, img_height,
+                         img_width, channels, pred, gt, w, partials, dmaps);
+    else
+      hipLaunchKernelGGL(l1_ssim_fwd_kernel<false>, dim3(nb), dim3(256), 0, st, img_height,
+                         img_width, channels, pred, gt, w, partials, dmaps);
   }
   const double n1 = (double)channels * img_height * img_width;
   const double n2 = (double)channels * (img_height - WIN + 1) * (img_width - WIN + 1);
@@ -358,7 +385,7 @@ extern "C" int gsplat_l1_ssim_forward(int img_height, int img_width, int channel
 
 extern "C" int gsplat_l1_ssim_backward(int img_height, int img_width, int channels,
                                        const float *pred, const float *gt, const float *window11,
-                                       float ssim_lambda, const float *dmaps,
+                                       float ssim_lambda, int clamp_pred, const float *dmaps,
                                        const float *grad_loss, float *v_pred, void *stream) {
   if (!l1_ssim_args_ok(img_height, img_width, channels, "l1_ssim_backward", ssim_lambda)) return 1;
   hipStream_t st = (hipStream_t)stream;
@@ -366,13 +393,22 @@ extern "C" int gsplat_l1_ssim_backward(int img_height, int img_width, int channe
   const double n1 = (double)channels * img_height * img_width;
   const double n2 = (double)channels * (img_height - WIN + 1) * (img_width - WIN + 1);
   if (ssim_lambda == 0.f) {
-    hipLaunchKernelGGL(l1_only_bwd_kernel, dim3(nb), dim3(256), 0, st, (long long)n1, pred, gt,
-                       grad_loss, (float)(1.0 / n1), v_pred);
+    if (clamp_pred)
+      hipLaunchKernelGGL(l1_only_bwd_kernel<true>, dim3(nb), dim3(256), 0, st, (long long)n1, pred,
+                         gt, grad_loss, (float)(1.0 / n1), v_pred);
+    else
+      hipLaunchKernelGGL(l1_only_bwd_kernel<false>, dim3(nb), dim3(256), 0, st, (long long)n1,
+                         pred, gt, grad_loss, (float)(1.0 / n1), v_pred);
     return check_launch("l1_ssim_backward");
   }
   const Win w = load_win(window11);
-  hipLaunchKernelGGL(l1_ssim_bwd_kernel, dim3(nb), dim3(256), 0, st, img_height, img_width,
-                     channels, pred, gt, w, dmaps, grad_loss, (float)(-ssim_lambda / n2),
-                     (float)((1.0 - ssim_lambda) / n1), v_pred);
+  if (clamp_pred)
+    hipLaunchKernelGGL(l1_ssim_bwd_kernel<true>, dim3(nb), dim3(256), 0, st, img_height,
+                       img_width, channels, pred, gt, w, dmaps, grad_loss,
+                       (float)(-ssim_lambda / n2), (float)((1.0 - ssim_lambda) / n1), v_pred);
+  else
+    hipLaunchKernelGGL(l1_ssim_bwd_kernel<false>, dim3(nb), dim3(256), 0, st, img_height,
+                       img_width, channels, pred, gt, w, dmaps, grad_loss,
+                       (float)(-ssim_lambda / n2), (float)((1.0 - ssim_lambda) / n1), v_pred);
   return check_launch("l1_ssim_backward");
 }

@@ -169,10 +169,12 @@ def _contig_f32(t: Tensor) -> Tensor:
 
 
 def render_fused(scene, cam: GCCamera, sh_degree_to_use: int, background: Tensor,
-                 return_alpha: bool = False):
+                 return_alpha: bool = False, clamp: bool = True):
     """scene.render's training output (gc_model.py:158-222) through the fused kernels.
 
-    Returns dict(rgb [H,W,3] (clamped at 1, gc_model.py:222), accumulation [H,W,1] or None,
+    Returns dict(rgb [H,W,3] (clamped at 1 as gc_model.py:222 -- or, clamp=False, the raw
+    image for a loss that applies the clamp itself: loss.fused_splatfacto_loss(clamp_pred=True)),
+    accumulation [H,W,1] or None,
     xys [N,2] and radii [N] (detached), xys_grad: callable returning v_xy [N,2] after
     backward -- what splatfacto's densification reads from `xys.grad`)."""
     aux = {}
@@ -184,7 +186,7 @@ def render_fused(scene, cam: GCCamera, sh_degree_to_use: int, background: Tensor
             int(sh_degree_to_use), _contig_f32(background), bool(return_alpha), aux]
     out = _FusedRender.apply(*args)
     img, alpha = (out if return_alpha else (out, None))
-    rgb = torch.clamp(img, max=1.0)
+    rgb = torch.clamp(img, max=1.0) if clamp else img
 
     def xys_grad() -> Optional[Tensor]:
         rec = aux.get("records")
@@ -193,6 +195,7 @@ def render_fused(scene, cam: GCCamera, sh_degree_to_use: int, background: Tensor
         v = rec[:aux["num_points"] * 64].view(torch.float32).view(-1, 16)[:, :2]
         return torch.where(aux["radii"][:, None] > 0, v, torch.zeros_like(v))  # culled: 0
 
-    return {"rgb": rgb, "accumulation": alpha[..., None] if alpha is not None else None,
+    return {"rgb": rgb, "clamped": bool(clamp),
+            "accumulation": alpha[..., None] if alpha is not None else None,
             "xys": aux["xys"], "radii": aux["radii"], "xys_grad": xys_grad,
             "num_intersects": aux["num_intersects"]}

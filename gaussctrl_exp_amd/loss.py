@@ -36,7 +36,7 @@ _WINDOW = _window_host()
 
 class _FusedL1SSIM(Function):
     @staticmethod
-    def forward(ctx, pred: Tensor, gt: Tensor, ssim_lambda: float):
+    def forward(ctx, pred: Tensor, gt: Tensor, ssim_lambda: float, clamp_pred: bool = False):
         if pred.dim() != 3 or pred.shape != gt.shape:
             raise ValueError("fused_splatfacto_loss: pred and gt must both be [H, W, C]")
         pred = pred.float().contiguous()
@@ -51,10 +51,11 @@ class _FusedL1SSIM(Function):
         loss = torch.empty((), device=dev, dtype=torch.float32)
         P = _lib.ptr
         _lib.call("gsplat_l1_ssim_forward", H, W, C, P(pred), P(gt), ctypes.cast(_WINDOW,
-                  ctypes.c_void_p), float(ssim_lambda), P(partials), P(dmaps), P(loss),
-                  _lib.stream(dev))
+                  ctypes.c_void_p), float(ssim_lambda), int(bool(clamp_pred)), P(partials),
+                  P(dmaps), P(loss), _lib.stream(dev))
         ctx.save_for_backward(pred, gt, dmaps)
         ctx.ssim_lambda = float(ssim_lambda)
+        ctx.clamp_pred = int(bool(clamp_pred))
         return loss
 
     @staticmethod
@@ -65,11 +66,14 @@ class _FusedL1SSIM(Function):
         v_pred = torch.empty_like(pred)
         P = _lib.ptr
         _lib.call("gsplat_l1_ssim_backward", H, W, C, P(pred), P(gt), ctypes.cast(_WINDOW,
-                  ctypes.c_void_p), ctx.ssim_lambda, P(dmaps), P(g), P(v_pred),
+                  ctypes.c_void_p), ctx.ssim_lambda, ctx.clamp_pred, P(dmaps), P(g), P(v_pred),
                   _lib.stream(pred.device))
-        return v_pred, None, None
+        return v_pred, None, None, None
 
 
-def fused_splatfacto_loss(pred: Tensor, gt: Tensor, ssim_lambda: float = 0.2) -> Tensor:
-    """(1 - ssim_lambda) * L1 + ssim_lambda * (1 - SSIM) on [H, W, C] images, on the GPU."""
-    return _FusedL1SSIM.apply(pred, gt, ssim_lambda)
+def fused_splatfacto_loss(pred: Tensor, gt: Tensor, ssim_lambda: float = 0.2,
+                          clamp_pred: bool = False) -> Tensor:
+    """(1 - ssim_lambda) * L1 + ssim_lambda * (1 - SSIM) on [H, W, C] images, on the GPU.
+    clamp_pred: the loss of torch.clamp(pred, max=1.0) (gc_model.py:222) without materialising
+    the clamped image (its forward and backward kernels fold into the loss kernels)."""
+    return _FusedL1SSIM.apply(pred, gt, ssim_lambda, clamp_pred)

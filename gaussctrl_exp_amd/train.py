@@ -162,16 +162,22 @@ class TrainStep:
         t = min(self.step_count / XYZ_MAX_STEPS, 1.0)
         return math.exp(math.log(GROUP_LR["means"]) * (1 - t) + math.log(XYZ_LR_FINAL) * t)
 
-    def loss(self, pred, gt):
+    def loss(self, pred, gt, clamp_pred: bool = False):
+        """Photometric loss of the rendered image.  clamp_pred: `pred` is the raw render and the
+        loss applies the caller's clamp(max=1) itself (gc_model.py:222) -- folded into the HIP
+        loss kernels, so the clamped image is never materialised."""
+        fused = self.api is None and pred.is_cuda
+        if clamp_pred and not (fused and self.loss_kind in ("l1", "splatfacto")):
+            pred, clamp_pred = torch.clamp(pred, max=1.0), False
         if self.loss_kind == "l1":
-            if self.api is None and pred.is_cuda:  # csrc/loss.hip, ssim_lambda = 0 fast path
+            if fused:  # csrc/loss.hip, ssim_lambda = 0 fast path
                 from .loss import fused_splatfacto_loss
-                return fused_splatfacto_loss(pred, gt, 0.0)
+                return fused_splatfacto_loss(pred, gt, 0.0, clamp_pred)
             return torch.abs(gt - pred).mean()
-        if self.loss_kind == "splatfacto_torch" or self.api is not None or not pred.is_cuda:
+        if self.loss_kind == "splatfacto_torch" or not fused:
             return splatfacto_loss(pred, gt)  # torch restatement (CPU-emulation tests)
         from .loss import fused_splatfacto_loss
-        return fused_splatfacto_loss(pred, gt, SSIM_LAMBDA)
+        return fused_splatfacto_loss(pred, gt, SSIM_LAMBDA, clamp_pred)
 
     def zero_grad(self):
         for p in self.params:
@@ -188,8 +194,8 @@ class TrainStep:
         return torch.cat([p.grad.reshape(-1) for p in self.params])
 
     def _render(self, cam: GCCamera, background: torch.Tensor):
-        if self.render_mode == "fused":
-            return render_fused(self.scene, cam, self.sh_degree, background)
+        if self.render_mode == "fused":  # raw image: the loss applies the clamp
+            return render_fused(self.scene, cam, self.sh_degree, background, clamp=False)
         return render(self.scene, cam, self.sh_degree, background, api=self.api)
 
     def forward_backward(self, cam: GCCamera, gt: torch.Tensor, background: torch.Tensor):
@@ -198,7 +204,7 @@ class TrainStep:
                 out = self._render(cam, background)
         else:
             out = self._render(cam, background)
-        loss = self.loss(out["rgb"], gt)
+        loss = self.loss(out["rgb"], gt, clamp_pred=not out.get("clamped", True))
         if loss.requires_grad:
             loss.backward()
         elif self.sh_exchange is not None and self.scene.features_rest.shape[1] > 0:

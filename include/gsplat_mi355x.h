@@ -290,15 +290,18 @@ int gsplat_debug_sort_items(int items);
  * window11: HOST pointer to the 11 normalised window weights.  Forward writes partials
  * [2 * gsplat_l1_ssim_num_blocks(H, W)] (scratch), dmaps [3 * C * (H-10) * (W-10)] (kept for
  * the backward) and the loss scalar (device).  Backward reads the upstream gradient scalar
- * from device memory (no host sync) and writes v_pred [H, W, C] (gt gets no gradient). */
+ * from device memory (no host sync) and writes v_pred [H, W, C] (gt gets no gradient).
+ * clamp_pred != 0 folds the caller's torch.clamp(rgb, max=1.0) (gc_model.py:222) in: the loss
+ * of min(pred, 1), with the gradient masked where pred > 1 (torch's clamp backward). */
 int gsplat_l1_ssim_num_blocks(int img_height, int img_width);
 int gsplat_l1_ssim_forward(int img_height, int img_width, int channels, const float *pred,
                            const float *gt, const float *window11, float ssim_lambda,
-                           float *partials, float *dmaps, float *loss, void *stream);
+                           int clamp_pred, float *partials, float *dmaps, float *loss,
+                           void *stream);
 int gsplat_l1_ssim_backward(int img_height, int img_width, int channels, const float *pred,
                             const float *gt, const float *window11, float ssim_lambda,
-                            const float *dmaps, const float *grad_loss, float *v_pred,
-                            void *stream);
+                            int clamp_pred, const float *dmaps, const float *grad_loss,
+                            float *v_pred, void *stream);
 
 /* ---- optimizer step -----------------------------------------------------
  * One torch.optim.Adam step (non-capturable foreach semantics, no weight decay / amsgrad) over

@@ -71,3 +71,27 @@ def test_l1_only_fast_path(gpu, H, W, C):
     ref.backward()
     assert abs(loss.item() - ref.item()) <= 1e-6 * max(1.0, ref.item())
     torch.testing.assert_close(p.grad.double().cpu(), p64.grad, rtol=1e-6, atol=1e-12)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("lam", [0.2, 0.0])
+@pytest.mark.parametrize("H,W,C,seed", [(48, 64, 3, 1), (270, 481, 3, 5)])
+def test_fused_loss_with_folded_clamp(gpu, lam, H, W, C, seed):
+    """clamp_pred=True == the loss of torch.clamp(pred, max=1.0) (gc_model.py:222), gradient
+    masked exactly where torch's clamp backward masks it (pred > 1)."""
+    g = torch.Generator().manual_seed(seed)
+    gt = torch.rand(H, W, C, generator=g)
+    pred = gt + 0.4 * torch.randn(H, W, C, generator=g)  # ~30 % of values above 1
+    pred[0, 0, 0] = 1.0                                   # the boundary passes the gradient
+    p = pred.to(gpu).requires_grad_()
+    loss = fused_splatfacto_loss(p, gt.to(gpu), lam, clamp_pred=True)
+    loss.backward()
+    p64 = pred.double().requires_grad_()
+    c64 = torch.clamp(p64, max=1.0)
+    ref = splatfacto_loss(c64, gt.double()) if lam else torch.abs(gt.double() - c64).mean()
+    ref.backward()
+    assert abs(loss.item() - ref.item()) <= 2e-6, (loss.item(), ref.item())
+    err = (p.grad.double().cpu() - p64.grad).abs().max().item()
+    scale = p64.grad.abs().max().item()
+    assert err <= 1e-4 * scale, (err, scale)
+    assert not p.grad.cpu()[pred > 1].any()
