@@ -187,11 +187,23 @@ struct WaveRect {
   int tile, j, i0;
   float rx0, rx1, ry0, ry1;
 };
-// Work slot of this wave: blockIdx.x * (tiles per workgroup) + wave / (waves per tile).
+// XCD-aware block order (gsplat_debug_set_raster_variant flag 1024): the dispatcher deals
+// workgroups to the 8 XCDs round-robin, so consecutive blocks -- neighbouring tiles, which
+// stage largely the same Gaussians -- land on different L2s.  With the remap each XCD takes a
+// contiguous run of blocks (bijective for any grid size).
+__device__ int g_xcd_remap = 0;
+__device__ __forceinline__ int block_slot() {
+  const int b = blockIdx.x;
+  if (!g_xcd_remap) return b;
+  const int n = gridDim.x, q = n >> 3, r = n & 7, x = b & 7, k = b >> 3;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
+}
+
+// Work slot of this wave: block slot * (tiles per workgroup) + wave / (waves per tile).
 template <int PXL, int COLS>
 __device__ __forceinline__ int wave_slot() {
   constexpr int WPT = (GS_BLOCK / COLS) * (GS_BLOCK / ((64 / COLS) * PXL));
-  return blockIdx.x * (4 / WPT) + (threadIdx.x >> 6) / WPT;
+  return block_slot() * (4 / WPT) + (threadIdx.x >> 6) / WPT;
 }
 template <int PXL, int COLS>
 __device__ __forceinline__ WaveRect wave_rect(int tbx, int tby, int H, int W, int tile = -1) {
@@ -1310,7 +1322,12 @@ extern "C" int gsplat_debug_set_raster_variant(int fwd_pxl, int bwd_pxl, int bwd
   }
   g_fwd_pxl = fwd_pxl;
   g_bwd_pxl = bwd_pxl;
-  g_bwd_flags = bwd_flags;
+  g_bwd_flags = bwd_flags & ~1024;
+  const int remap = (bwd_flags & 1024) ? 1 : 0;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_xcd_remap), &remap, sizeof(int)) != hipSuccess) {
+    set_error("debug_set_raster_variant: hipMemcpyToSymbol failed");
+    return 1;
+  }
   return 0;
 }
 

@@ -267,7 +267,8 @@ int gsplat_rasterize_backward_records(
  * flags: bit 0 drops the gradient atomics (timing ablation only, results wrong); bit 1
  * scalar backward; bit 2 scalar forward (one Gaussian per iteration, 16-column strips);
  * bit 3 packed float2 forward; bit 4 16-column forward rectangles; bit 5 8-column backward
- * rectangles; bit 6 backward stages and culls but skips the blend (timing ablation only).  Every variant produces results within the same parity bar.  Process-wide;
+ * rectangles; bit 6 backward stages and culls but skips the blend (timing ablation only); bit 10
+ * XCD-contiguous block order in the shipped forward and backward kernels.  Every variant produces results within the same parity bar.  Process-wide;
  * defaults (1, 2, 0) are the shipped configuration. */
 int gsplat_debug_set_raster_variant(int fwd_pxl, int bwd_pxl, int bwd_flags);
 
