@@ -71,6 +71,8 @@ SIGNATURES = {
                                         [_I] * 4 + [_F] + [_P] * 11),
     "gsplat_fused_preprocess_backward": (_I, [_I, _I, _I] + [_P] * 6 + [_F] * 4 + [_I, _I] +
                                          [_P] * 13),
+    "gsplat_fused_preprocess_backward_adam": (_I, [_I, _I, _I] + [_P] * 9 + [_F] * 4 +
+                                              [_I, _I] + [_P] * 8 + [_I, _F, _F, _F, _P]),
     "gsplat_grad_records_bytes": (_SZ, [_I]),
     "gsplat_rasterize_backward_records": (_I, [_I] * 5 + [_P] * 11 + [_F, _I64, _I, _P, _SZ,
                                                                        _P, _SZ, _P]),

@@ -14,7 +14,7 @@
 //   p = p - step_size * m / (sqrt(v) / bias_correction2_sqrt + eps)
 // with step_size = lr / (1 - beta1^t) and bias_correction2_sqrt = sqrt(1 - beta2^t) computed
 // on the host in double (as torch does for non-capturable Adam).
-#include "common.h"
+#include "adam_math.h"
 
 namespace gs {
 namespace {
@@ -36,14 +36,6 @@ struct AdamTable {
   int nseg;
 };
 
-__device__ __forceinline__ void adam_elem(float &p, float g, float &m, float &v, float w1,
-                                          float beta2, float w2, float ss, float bc2s,
-                                          float eps) {
-  m = fmaf(w1, g - m, m);  // torch lerp, weight < 0.5 branch
-  v = fmaf(w2 * g, g, v * beta2);
-  const float denom = sqrtf(v) / bc2s + eps;
-  p = fmaf(-ss, m / denom, p);
-}
 
 __global__ __launch_bounds__(ADAM_TPB) void adam_kernel(AdamTable t, float beta1, float beta2,
                                                         float eps) {

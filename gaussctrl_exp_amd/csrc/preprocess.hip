@@ -22,6 +22,7 @@
 //    into their own contiguous tensors (LDS-staged 16-byte stores).
 // Built with -ffp-contract=off (projection bit-identical to project.hip given the same
 // activated inputs); the SH helpers carry their own contract pragma (sh_math.h).
+#include "adam_math.h"
 #include "project_math.h"
 #include "sh_math.h"
 
@@ -63,6 +64,15 @@ struct FusedBwdArgs {
   float conic_scale;
   float *v_means, *v_log_scales, *v_quats, *v_opacity_logits, *v_dc, *v_rest;
   float *v_colors;  // non-NULL: write the SH-output gradient here instead of v_dc / v_rest
+};
+
+// Adam fused into the backward (single-GPU training step): the six parameter tensors are
+// updated in place from the gradients in registers, which are never written to memory.
+// Group order = splatfacto's (means, scales, quats, opacities, features_dc, features_rest).
+struct FusedAdamArgs {
+  float *p[6], *m[6], *v[6];
+  float ss[6], bc2s[6];  // lr / (1 - beta1^t), sqrt(1 - beta2^t) (host, double -> float)
+  float beta1, beta2, eps;
 };
 
 // The caller's activations (gc_model.py:177-178): exp(scales), quats / |quats|.
@@ -171,8 +181,9 @@ __global__ __launch_bounds__(sh_threads(K)) void fused_fwd_kernel(FusedFwdArgs a
   }
 }
 
-template <int K>
-__global__ __launch_bounds__(sh_threads(K)) void fused_bwd_kernel(FusedBwdArgs a, ProjParams pp) {
+template <int K, bool ADAM = false>
+__global__ __launch_bounds__(sh_threads(K)) void fused_bwd_kernel(FusedBwdArgs a, ProjParams pp,
+                                                                  FusedAdamArgs o = {}) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int RROW = (K - 1) * 3;
   constexpr int RP = RROW | 1;
@@ -223,27 +234,54 @@ __global__ __launch_bounds__(sh_threads(K)) void fused_bwd_kernel(FusedBwdArgs a
         vc[c] = K == 1 ? vrgb[c] * (1.f - col) * col : (clamp0_passes(col) ? vrgb[c] : 0.f);
       }
     }
+    float vdc[3] = {vc[0], vc[1], vc[2]};  // K == 1: sigmoid backward already applied
+    float b[25];
+    b[0] = 0.f;
+    int nb = 0;  // culled: every coefficient gradient is 0
+    if constexpr (K > 1) {
+      if (!a.v_colors) {
+        if (vis) nb = view_basis(a.degrees_to_use, p0, p1, p2, a.campos, b);
+        // gsplat compute_sh_backward: v_coeffs[k][c] = basis_k * v_rgb[c] for k < nb, else 0
 #pragma unroll
-    for (int k = 0; k < 3; ++k) a.v_means[3 * g + k] = vmean[k];
+        for (int c = 0; c < 3; ++c) vdc[c] = b[0] * vc[c];
+      }
+    }
+    if constexpr (ADAM) {
+      const float w1 = 1.f - o.beta1, w2 = 1.f - o.beta2;
+      auto upd = [&](int grp, long long idx, float gv) {
+        float pv = o.p[grp][idx], mv = o.m[grp][idx], vv = o.v[grp][idx];
+        adam_elem(pv, gv, mv, vv, w1, o.beta2, w2, o.ss[grp], o.bc2s[grp], o.eps);
+        o.p[grp][idx] = pv;
+        o.m[grp][idx] = mv;
+        o.v[grp][idx] = vv;
+      };
 #pragma unroll
-    for (int k = 0; k < 3; ++k) a.v_log_scales[3 * g + k] = vls[k];
+      for (int k = 0; k < 3; ++k) upd(0, 3 * g + k, vmean[k]);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) a.v_quats[4 * g + k] = vq[k];
-    a.v_opacity_logits[g] = vlogit;
-    if constexpr (K == 1) {
+      for (int k = 0; k < 3; ++k) upd(1, 3 * g + k, vls[k]);
 #pragma unroll
-      for (int c = 0; c < 3; ++c) a.v_dc[3 * g + c] = vc[c];
-    } else if (a.v_colors) {  // data-parallel view exchange sums the SH gradient later
+      for (int k = 0; k < 4; ++k) upd(2, 4 * g + k, vq[k]);
+      upd(3, g, vlogit);
 #pragma unroll
-      for (int c = 0; c < 3; ++c) a.v_colors[3 * g + c] = vc[c];
+      for (int c = 0; c < 3; ++c) upd(4, 3 * g + c, vdc[c]);
     } else {
-      float b[25];
-      b[0] = 0.f;
-      int nb = 0;  // culled: every coefficient gradient is 0
-      if (vis) nb = view_basis(a.degrees_to_use, p0, p1, p2, a.campos, b);
-      // gsplat compute_sh_backward: v_coeffs[k][c] = basis_k * v_rgb[c] for k < nb, else 0
 #pragma unroll
-      for (int c = 0; c < 3; ++c) a.v_dc[3 * g + c] = b[0] * vc[c];
+      for (int k = 0; k < 3; ++k) a.v_means[3 * g + k] = vmean[k];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) a.v_log_scales[3 * g + k] = vls[k];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) a.v_quats[4 * g + k] = vq[k];
+      a.v_opacity_logits[g] = vlogit;
+      if (K == 1 || !a.v_colors) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) a.v_dc[3 * g + c] = vdc[c];
+      }
+    }
+    if constexpr (K > 1) {
+      if (a.v_colors) {  // data-parallel view exchange sums the SH gradient later
+#pragma unroll
+        for (int c = 0; c < 3; ++c) a.v_colors[3 * g + c] = vc[c];
+      } else {
       float *row = smem + t * RP;
 #pragma unroll
       for (int k = 1; k < K; ++k) {
@@ -252,12 +290,28 @@ __global__ __launch_bounds__(sh_threads(K)) void fused_bwd_kernel(FusedBwdArgs a
         row[(k - 1) * 3 + 1] = bk * vc[1];
         row[(k - 1) * 3 + 2] = bk * vc[2];
       }
+      }
     }
   }
   if constexpr (K > 1) {
     if (rest_out) {
       __syncthreads();
-      store_cols<RROW, 0, RP, THR>(smem, cnt, a.v_rest + g0 * RROW);
+      if constexpr (ADAM) {  // features_rest: coalesced slab update from the LDS gradient rows
+        const int total = cnt * RROW;
+        const long long off = g0 * RROW;
+        const float w1 = 1.f - o.beta1, w2 = 1.f - o.beta2;
+        for (int k = threadIdx.x; k < total; k += THR) {
+          const int r = k / RROW;
+          const float gv = smem[r * RP + (k - r * RROW)];
+          float pv = o.p[5][off + k], mv = o.m[5][off + k], vv = o.v[5][off + k];
+          adam_elem(pv, gv, mv, vv, w1, o.beta2, w2, o.ss[5], o.bc2s[5], o.eps);
+          o.p[5][off + k] = pv;
+          o.m[5][off + k] = mv;
+          o.v[5][off + k] = vv;
+        }
+      } else {
+        store_cols<RROW, 0, RP, THR>(smem, cnt, a.v_rest + g0 * RROW);
+      }
     }
   }
 }
@@ -343,4 +397,59 @@ extern "C" int gsplat_fused_preprocess_backward(
   hipStream_t st = (hipStream_t)stream;
   FUSED_DISPATCH(fused_bwd_kernel, args);
   return check_launch("fused_preprocess_backward");
+}
+
+extern "C" int gsplat_fused_preprocess_backward_adam(
+    int num_points, int sh_bases, int degrees_to_use, float *means3d, float *log_scales,
+    float *quats, float *opacity_logits, float *features_dc, float *features_rest,
+    const float *viewmat, const float *projmat, const float *campos, float fx, float fy,
+    float cx, float cy, int img_height, int img_width, const int32_t *radii, const float *conics,
+    const float *colors, const float *opacity, const void *grad_records, float *const *exp_avgs,
+    float *const *exp_avg_sqs, const float *lrs, int step, float beta1, float beta2, float eps,
+    void *stream) {
+  const int K = sh_bases;
+  if (num_points < 0 || !valid_bases(K) || degrees_to_use < 0 || degrees_to_use > degree_of(K) ||
+      img_height <= 0 || img_width <= 0 || step < 1 || !(beta1 > 0.5f && beta1 < 1.f) ||
+      !(beta2 >= 0.f && beta2 < 1.f) || !exp_avgs || !exp_avg_sqs || !lrs ||
+      (num_points > 0 && (!grad_records || (K > 1 && (!campos || !features_rest))))) {
+    set_error("fused_preprocess_backward_adam: bad args (N=%d sh_bases=%d degrees_to_use=%d "
+              "step=%d)", num_points, sh_bases, degrees_to_use, step);
+    return 1;
+  }
+  if (num_points == 0) return 0;
+  FusedBwdArgs args{num_points, degrees_to_use, means3d, log_scales, quats, viewmat, projmat,
+                    campos, radii, conics, colors, opacity, (const float *)grad_records, 0.5f,
+                    nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  FusedAdamArgs o{};
+  float *params[6] = {means3d, log_scales, quats, opacity_logits, features_dc, features_rest};
+  // torch non-capturable Adam: bias corrections in double on the host (as gsplat_adam_step)
+  const double bc1 = 1.0 - pow((double)beta1, step), bc2 = 1.0 - pow((double)beta2, step);
+  for (int k = 0; k < 6; ++k) {
+    o.p[k] = params[k];
+    o.m[k] = exp_avgs[k];
+    o.v[k] = exp_avg_sqs[k];
+    o.ss[k] = (float)(lrs[k] / bc1);
+    o.bc2s[k] = (float)sqrt(bc2);
+  }
+  o.beta1 = beta1;
+  o.beta2 = beta2;
+  o.eps = eps;
+  const ProjParams pp = make_proj_params(fx, fy, cx, cy, 1.f, 0.f, img_height, img_width, 1, 1);
+  const int thr = sh_threads(K);
+  const dim3 grid(cdiv(num_points, thr));
+  const size_t smem = K > 1 ? (size_t)thr * (((K - 1) * 3) | 1) * sizeof(float) : 0;
+  hipStream_t st = (hipStream_t)stream;
+  switch (K) {
+#define ADAM_CASE(KK)                                                                      \
+  case KK:                                                                                 \
+    hipLaunchKernelGGL((fused_bwd_kernel<KK, true>), grid, dim3(thr), smem, st, args, pp, o); \
+    break;
+    ADAM_CASE(1)
+    ADAM_CASE(4)
+    ADAM_CASE(9)
+    ADAM_CASE(16)
+    ADAM_CASE(25)
+#undef ADAM_CASE
+  }
+  return check_launch("fused_preprocess_backward_adam");
 }

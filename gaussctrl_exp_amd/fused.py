@@ -21,6 +21,7 @@ the drop-in; this is the framework's own training step (TrainStep(render_mode="f
 """
 from __future__ import annotations
 
+import ctypes
 from typing import Optional
 
 import torch
@@ -38,7 +39,7 @@ class _FusedRender(Function):
     @staticmethod
     def forward(ctx, means, scales, quats, opacities, features_dc, features_rest, viewmat,
                 projmat, campos, fx, fy, cx, cy, H, W, degrees_to_use, background,
-                return_alpha, aux):
+                return_alpha, aux, adam=None):
         n = means.shape[0]
         K = 1 + features_rest.shape[1]
         if K not in _DEG_OF_BASES or features_dc.shape != (n, 3) or \
@@ -99,7 +100,17 @@ class _FusedRender(Function):
         ctx.ckpt, ctx.rec = ckpt, rec
         ctx.opac_shape = opacities.shape
         ctx.exchange = exchange.active() if K > 1 else None
-        ctx.save_for_backward(means, scales, quats, features_rest, viewmat, projmat, campos,
+        if adam is not None:
+            if ctx.exchange is not None:
+                raise ValueError("render_fused: the in-backward Adam step is single-GPU only")
+            for p, q in zip(adam["params"], (means, scales, quats, opacities, features_dc,
+                                             features_rest)):
+                if p.data_ptr() != q.data_ptr():
+                    raise ValueError("render_fused: in-backward Adam needs the parameters "
+                                     "themselves (contiguous fp32), not copies")
+        ctx.adam = adam
+        ctx.save_for_backward(means, scales, quats, opacities, features_dc, features_rest,
+                              viewmat, projmat, campos,
                               background, xys, radii, conics, colors, opac, gids, bins, final_Ts,
                               final_idx)
         ctx.set_materialize_grads(False)
@@ -111,8 +122,9 @@ class _FusedRender(Function):
 
     @staticmethod
     def backward(ctx, v_img, v_alpha=None):
-        (means, scales, quats, features_rest, viewmat, projmat, campos, background, xys, radii,
-         conics, colors, opac, gids, bins, final_Ts, final_idx) = ctx.saved_tensors
+        (means, scales, quats, opacities, features_dc, features_rest, viewmat, projmat, campos,
+         background, xys, radii, conics, colors, opac, gids, bins, final_Ts,
+         final_idx) = ctx.saved_tensors
         n, K, dtu, fx, fy, cx, cy, H, W, tbx, tby, I, chunk = ctx.meta
         dev = means.device
         P, st = _lib.ptr, _lib.stream(dev)
@@ -127,6 +139,18 @@ class _FusedRender(Function):
                       P(final_idx), P(v_img), P(v_alpha), float(BACKWARD_ALPHA_CLAMP), I, chunk,
                       P(ctx.ckpt), ctx.ckpt.numel() if ctx.ckpt is not None else 0, P(rec),
                       rec.numel(), st)
+        if ctx.adam is not None:
+            # Adam inside the backward: parameters (and moments) updated in place, no gradients
+            a = ctx.adam
+            cast = ctypes.cast
+            _lib.call("gsplat_fused_preprocess_backward_adam", n, K, dtu, P(means), P(scales),
+                      P(quats), P(opacities), P(features_dc),
+                      P(features_rest) if K > 1 else None, P(viewmat), P(projmat), P(campos),
+                      fx, fy, cx, cy, H, W, P(radii), P(conics), P(colors), P(opac), P(rec),
+                      cast(a["exp_avgs"], ctypes.c_void_p), cast(a["exp_avg_sqs"], ctypes.c_void_p),
+                      cast(a["lrs"], ctypes.c_void_p), int(a["step"]), float(a["betas"][0]),
+                      float(a["betas"][1]), float(a["eps"]), st)
+            return (None,) * 20
         f32 = dict(device=dev, dtype=torch.float32)
         v_means = torch.empty((n, 3), **f32)
         v_scales = torch.empty((n, 3), **f32)
@@ -145,7 +169,7 @@ class _FusedRender(Function):
                 v_colors, lambda m, views: sh_backward_views_split(_DEG_OF_BASES[K], dtu, m,
                                                                    views))
         return (v_means, v_scales, v_quats, v_opac.view(ctx.opac_shape), v_dc, v_rest) + \
-            (None,) * 13
+            (None,) * 14
 
 
 def sh_backward_views_split(degree: int, degrees_to_use: int, means: Tensor, views: Tensor):
@@ -169,21 +193,24 @@ def _contig_f32(t: Tensor) -> Tensor:
 
 
 def render_fused(scene, cam: GCCamera, sh_degree_to_use: int, background: Tensor,
-                 return_alpha: bool = False, clamp: bool = True):
+                 return_alpha: bool = False, clamp: bool = True, adam=None):
     """scene.render's training output (gc_model.py:158-222) through the fused kernels.
 
     Returns dict(rgb [H,W,3] (clamped at 1 as gc_model.py:222 -- or, clamp=False, the raw
     image for a loss that applies the clamp itself: loss.fused_splatfacto_loss(clamp_pred=True)),
     accumulation [H,W,1] or None,
     xys [N,2] and radii [N] (detached), xys_grad: callable returning v_xy [N,2] after
-    backward -- what splatfacto's densification reads from `xys.grad`)."""
+    backward -- what splatfacto's densification reads from `xys.grad`).
+    adam: optim.FusedAdam.fused_spec(params) of the six parameters -- the backward then takes
+    that Adam step itself (gsplat_fused_preprocess_backward_adam: parameters updated in place,
+    no .grad); single-GPU only."""
     aux = {}
     campos = cam.c2w[..., :3, 3].reshape(3)
     args = [_contig_f32(scene.means), _contig_f32(scene.scales), _contig_f32(scene.quats),
             _contig_f32(scene.opacities), _contig_f32(scene.features_dc),
             _contig_f32(scene.features_rest), _contig_f32(cam.viewmat), _contig_f32(cam.projmat),
             _contig_f32(campos), cam.fx, cam.fy, cam.cx, cam.cy, cam.height, cam.width,
-            int(sh_degree_to_use), _contig_f32(background), bool(return_alpha), aux]
+            int(sh_degree_to_use), _contig_f32(background), bool(return_alpha), aux, adam]
     out = _FusedRender.apply(*args)
     img, alpha = (out if return_alpha else (out, None))
     rgb = torch.clamp(img, max=1.0) if clamp else img

@@ -76,6 +76,27 @@ class FusedAdam:
                   cast(numel, ctypes.c_void_p), cast(lrs, ctypes.c_void_p), self.step_count,
                   self.betas[0], self.betas[1], self.eps, _lib.stream(live[0][1].device))
 
+    def fused_spec(self, params):
+        """The state a kernel needs to take this optimiser's next step itself
+        (gsplat_fused_preprocess_backward_adam): host arrays of the exp_avg / exp_avg_sq
+        pointers and learning rates of `params` (in that order, each the only parameter of its
+        group), the step number after increment, betas and eps.  Advances the step count --
+        the caller must run the kernel exactly once."""
+        by_param = {id(g["params"][0]): g for g in self.param_groups}
+        n = len(params)
+        M, V = (ctypes.c_void_p * n)(), (ctypes.c_void_p * n)()
+        lrs = (ctypes.c_float * n)()
+        for k, p in enumerate(params):
+            g = by_param.get(id(p))
+            if g is None:
+                raise ValueError("fused_spec: parameter not managed by this optimiser")
+            st = self._buffers(p)
+            M[k], V[k] = st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr()
+            lrs[k] = float(g["lr"])
+        self.step_count += 1
+        return {"exp_avgs": M, "exp_avg_sqs": V, "lrs": lrs, "step": self.step_count,
+                "betas": self.betas, "eps": self.eps, "params": list(params)}
+
     def zero_grad(self, set_to_none: bool = True):
         for g in self.param_groups:
             p = g["params"][0]

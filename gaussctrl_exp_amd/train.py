@@ -125,7 +125,8 @@ class TrainStep:
 
     def __init__(self, scene: GaussianScene, sh_degree: int = 3, world_size: int = 1,
                  loss: str = "splatfacto", group=None, api=None,
-                 grad_exchange: str = "sh_views", render_mode: str = "caller"):
+                 grad_exchange: str = "sh_views", render_mode: str = "caller",
+                 fuse_adam: bool = True):
         if render_mode not in ("caller", "fused"):
             raise ValueError(f"render_mode must be 'caller' or 'fused', not {render_mode}")
         if render_mode == "fused" and (api is not None or not scene.means.is_cuda):
@@ -135,6 +136,9 @@ class TrainStep:
         # (gc_model.py:158-238, what gc_model.py runs through the drop-in); "fused": the same
         # step with that glue inside the HIP kernels (fused.render_fused)
         self.render_mode = render_mode
+        # single-GPU fused steps take the Adam update inside the backward kernel
+        # (gsplat_fused_preprocess_backward_adam): no gradient tensors are written or re-read
+        self.fuse_adam = bool(fuse_adam) and render_mode == "fused" and world_size == 1
         self.scene = scene.requires_grad_()
         self.params = scene.params()
         self.world_size = world_size
@@ -193,17 +197,19 @@ class TrainStep:
     def flat_grad(self) -> torch.Tensor:
         return torch.cat([p.grad.reshape(-1) for p in self.params])
 
-    def _render(self, cam: GCCamera, background: torch.Tensor):
+    def _render(self, cam: GCCamera, background: torch.Tensor, adam=None):
         if self.render_mode == "fused":  # raw image: the loss applies the clamp
-            return render_fused(self.scene, cam, self.sh_degree, background, clamp=False)
+            return render_fused(self.scene, cam, self.sh_degree, background, clamp=False,
+                                adam=adam)
         return render(self.scene, cam, self.sh_degree, background, api=self.api)
 
-    def forward_backward(self, cam: GCCamera, gt: torch.Tensor, background: torch.Tensor):
+    def forward_backward(self, cam: GCCamera, gt: torch.Tensor, background: torch.Tensor,
+                         adam=None):
         if self.sh_exchange is not None:
             with self.sh_exchange.view(self.scene.means, cam.c2w[..., :3, 3]):
                 out = self._render(cam, background)
         else:
-            out = self._render(cam, background)
+            out = self._render(cam, background, adam=adam)
         loss = self.loss(out["rgb"], gt, clamp_pred=not out.get("clamped", True))
         if loss.requires_grad:
             loss.backward()
@@ -232,14 +238,23 @@ class TrainStep:
              optimizer: bool = True):
         if background is None:
             background = torch.rand(3, device=gt.device)
+        if optimizer:
+            for g in self.opt.param_groups:
+                if g["name"] == "means":
+                    g["lr"] = self._xyz_lr()
+        if optimizer and self.fuse_adam and isinstance(self.opt, FusedAdamType()) and \
+                all(p.dtype == torch.float32 and p.is_contiguous() for p in self.params):
+            # the backward takes the Adam step (one kernel instead of gradient tensors + step)
+            self.zero_grad()
+            loss, out = self.forward_backward(cam, gt, background,
+                                              adam=self.opt.fused_spec(self.params))
+            self.step_count += 1
+            return loss
         self.zero_grad()
         loss, out = self.forward_backward(cam, gt, background)
         if not optimizer:
             self.sync_grads()
             return loss
-        for g in self.opt.param_groups:
-            if g["name"] == "means":
-                g["lr"] = self._xyz_lr()
         gs = self.grad_sync
         if gs is not None and gs.sh_done() and isinstance(self.opt, FusedAdamType()):
             # the SH-feature gradients (81 % of the update's bytes) are final: update them

@@ -245,6 +245,22 @@ int gsplat_fused_preprocess_backward(
     float *v_opacity_logits, float *v_features_dc, float *v_features_rest, float *v_colors,
     void *stream);
 
+/* Single-GPU training step: gsplat_fused_preprocess_backward with the Adam step of the six
+ * parameter groups fused in (torch.optim.Adam foreach semantics, exactly gsplat_adam_step's
+ * arithmetic).  The gradients stay in registers; means3d, log_scales, quats, opacity_logits,
+ * features_dc, features_rest are updated IN PLACE, together with their exp_avgs /
+ * exp_avg_sqs (HOST arrays of 6 device pointers, group order as listed); lrs: HOST array of
+ * the 6 learning rates; step >= 1 after increment; 0.5 < beta1 < 1.  Every Gaussian is
+ * updated (culled ones with a zero gradient, as torch does). */
+int gsplat_fused_preprocess_backward_adam(
+    int num_points, int sh_bases, int degrees_to_use, float *means3d, float *log_scales,
+    float *quats, float *opacity_logits, float *features_dc, float *features_rest,
+    const float *viewmat, const float *projmat, const float *campos, float fx, float fy,
+    float cx, float cy, int img_height, int img_width, const int32_t *radii, const float *conics,
+    const float *colors, const float *opacity, const void *grad_records, float *const *exp_avgs,
+    float *const *exp_avg_sqs, const float *lrs, int step, float beta1, float beta2, float eps,
+    void *stream);
+
 /* Per-Gaussian gradient records (64 B each) the fused path's rasterize backward accumulates
  * into: gsplat_rasterize_backward_records is gsplat_rasterize_backward (C = 3, default
  * variant, list-split when chunk > 0 as in the _chunked entry) without the zero fill and

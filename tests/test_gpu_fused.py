@@ -228,3 +228,27 @@ def test_fused_trainstep_exchange_over_rccl_world1(gpu):
         assert frac <= 2e-3, f"fused vs caller train step: {frac:.2e} (max {mx:.3e})"
     finally:
         dist.destroy_process_group()
+
+
+def test_fused_adam_in_backward_matches_separate_step(gpu):
+    """TrainStep(render_mode="fused") on one GPU takes the Adam step inside the backward
+    kernel; three steps equal the same step with gradient tensors + FusedAdam (same formulas;
+    only the rasterizer's atomic summation order differs run to run)."""
+    from gaussctrl_exp_amd.train import TrainStep
+    cam = synthetic_camera(256, 192).to(gpu)
+    gt = torch.rand(192, 256, 3, generator=torch.Generator().manual_seed(3)).to(gpu)
+    bg = torch.tensor([0.2, 0.3, 0.4], device=gpu)
+    params = {}
+    for fuse in (True, False):
+        t = TrainStep(synthetic_scene(20000, 3, seed=8, device=gpu), sh_degree=3,
+                      loss="splatfacto", render_mode="fused", fuse_adam=fuse)
+        for _ in range(3):
+            t.step(cam, gt, background=bg)
+        assert t.opt.step_count == 3 and t.step_count == 3
+        if fuse:
+            assert all(p.grad is None for p in t.params)  # gradients never materialised
+        params[fuse] = [p.detach().cpu().numpy() for p in t.params]
+    for name, a, b in zip(NAMES, params[True], params[False]):
+        bad = ~np.isclose(a, b, rtol=1e-5, atol=1e-6)
+        assert bad.mean() <= 1e-4, f"{name}: {bad.mean():.2e} differ (max {np.abs(a - b).max():.3e})"
+        assert not np.array_equal(b, _np(getattr(synthetic_scene(20000, 3, seed=8), name)))
