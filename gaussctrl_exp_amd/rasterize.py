@@ -74,6 +74,18 @@ def rasterize_gaussians(
         img_width, background.contiguous(), return_alpha)
 
 
+_PINNED = {}
+
+
+def _pinned_counts(dev) -> Tensor:
+    """A 2-int32 pinned host buffer per device, written by gsplat_bin_count (pinned host
+    memory is device-addressable on ROCm) and read by the host after a stream sync."""
+    t = _PINNED.get(dev)
+    if t is None:
+        t = _PINNED[dev] = torch.zeros(2, dtype=torch.int32, pin_memory=True)
+    return t
+
+
 def bin_gaussians(xys: Tensor, depths: Tensor, radii: Tensor, num_tiles_hit: Tensor,
                   img_height: int, img_width: int):
     """Fused on-device binning: (num_intersects, gaussian_ids_sorted [I] int32,
@@ -85,15 +97,22 @@ def bin_gaussians(xys: Tensor, depths: Tensor, radii: Tensor, num_tiles_hit: Ten
     radii = radii.to(torch.int32).contiguous()
     num_tiles_hit = num_tiles_hit.to(torch.int32).contiguous()
     depths = depths.float().contiguous()
+    _lib.check_device("bin_gaussians", xys, depths, radii, num_tiles_hit)
+    if n == 0:
+        return 0, torch.empty((0,), device=dev, dtype=torch.int32), \
+            torch.zeros((tbx * tby, 2), device=dev, dtype=torch.int32)
     ws1 = torch.empty((_lib.query("gsplat_bin_count_workspace_size", n),), device=dev,
                       dtype=torch.uint8)
-    counts = torch.empty((2,), device=dev, dtype=torch.int32)
+    counts = _pinned_counts(dev)
     P, st = _lib.ptr, _lib.stream(dev)
     xys = xys.float().contiguous()
+    tile_bins = torch.empty((tbx * tby, 2), device=dev, dtype=torch.int32)
     _lib.call("gsplat_bin_count", n, P(xys), P(depths), P(radii), P(num_tiles_hit), tbx, tby,
               P(counts), P(ws1), ws1.numel(), st)
-    num_intersects = int(counts[1].item())  # the single host sync (gsplat: .item())
-    tile_bins = torch.empty((tbx * tby, 2), device=dev, dtype=torch.int32)
+    # the single host sync (gsplat: cum_tiles_hit[-1].item()): the kernels write the counts
+    # straight into pinned host memory, so the host only waits for the stream -- no copy
+    torch.cuda.current_stream(dev).synchronize()
+    num_intersects = int(counts[1])
     gaussian_ids_sorted = torch.empty((max(num_intersects, 0),), device=dev, dtype=torch.int32)
     ws2 = torch.empty((_lib.query("gsplat_bin_emit_workspace_size", num_intersects),),
                       device=dev, dtype=torch.uint8)

@@ -37,7 +37,13 @@ def test_sh_backward_views_vs_oracle(gpu, oracle_lib, degree, dtu, n, R, pad):
     got = sh_backward_views(degree, dtu, means.to(gpu), views.to(gpu)).cpu().numpy()
     ref = O.sh_backward_views(dtu, means.numpy(), views.numpy(), K)
     assert got.shape == (n, K, 3)
-    np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-6)
+    # the parity bar (1e-5 abs / 1e-4 rel): a degree-4 basis near cancellation rounds ~1e-6
+    np.testing.assert_allclose(got, ref, rtol=1e-4, atol=1e-5)
+    # the split-output variant (fused training path) writes the same values into two tensors
+    from gaussctrl_exp_amd.fused import sh_backward_views_split
+    v_dc, v_rest = sh_backward_views_split(degree, dtu, means.to(gpu), views.to(gpu))
+    np.testing.assert_array_equal(v_dc.cpu().numpy(), got[:, 0])
+    np.testing.assert_array_equal(v_rest.cpu().numpy(), got[:, 1:])
     # == the sum of the single-view HIP backward on each view's (normalised) directions
     from gaussctrl_exp_amd import _lib
     acc = torch.zeros(n, K, 3, device=gpu)
@@ -49,7 +55,7 @@ def test_sh_backward_views_vs_oracle(gpu, oracle_lib, degree, dtu, n, R, pad):
         _lib.call("gsplat_compute_sh_backward", n, degree, dtu, _lib.ptr(d), _lib.ptr(vc),
                   _lib.ptr(out), _lib.stream(gpu))
         acc += out
-    np.testing.assert_allclose(got, acc.cpu().numpy(), rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(got, acc.cpu().numpy(), rtol=1e-4, atol=1e-5)
     if dtu < degree:  # bases above degrees_to_use get zero gradient
         assert not got[:, num_sh_bases(dtu):].any()
 
