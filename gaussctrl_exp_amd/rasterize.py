@@ -97,6 +97,7 @@ def bin_gaussians(xys: Tensor, depths: Tensor, radii: Tensor, num_tiles_hit: Ten
     radii = radii.to(torch.int32).contiguous()
     num_tiles_hit = num_tiles_hit.to(torch.int32).contiguous()
     depths = depths.float().contiguous()
+    xys = xys.float().contiguous()
     _lib.check_device("bin_gaussians", xys, depths, radii, num_tiles_hit)
     if n == 0:
         return 0, torch.empty((0,), device=dev, dtype=torch.int32), \
@@ -105,7 +106,6 @@ def bin_gaussians(xys: Tensor, depths: Tensor, radii: Tensor, num_tiles_hit: Ten
                       dtype=torch.uint8)
     counts = _pinned_counts(dev)
     P, st = _lib.ptr, _lib.stream(dev)
-    xys = xys.float().contiguous()
     tile_bins = torch.empty((tbx * tby, 2), device=dev, dtype=torch.int32)
     _lib.call("gsplat_bin_count", n, P(xys), P(depths), P(radii), P(num_tiles_hit), tbx, tby,
               P(counts), P(ws1), ws1.numel(), st)
