@@ -1,0 +1,84 @@
+"""The fused training step's data-parallel path with two ranks on one GPU (gloo carries the
+collectives here: RCCL needs one GPU per rank, and the box has one).  Each rank renders its
+own view through the fused kernels; the SH-feature gradients go through the view exchange
+(gsplat_compute_sh_backward_views_split on the all-gathered colour gradients) or plain
+all-reduces, the rest through all-reduces.  The result must equal the sum of the two
+single-view fused gradients on both ranks, and the ranks must hold identical parameters after
+Adam -- the path bench.py runs at N > 1 under RCCL."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _views(dev):
+    from gaussctrl_exp_amd.camera import gc_camera, look_at_c2w
+    return [gc_camera(look_at_c2w(eye, up=(0.0, 1.0, 0.0)), 220.0, 220.0, 96.0, 64.0, 192, 128)
+            .to(dev) for eye in ((0.0, 0.0, 4.0), (1.5, 0.5, 3.6))]
+
+
+def _scene(dev):
+    from gaussctrl_exp_amd.scene import synthetic_scene
+    return synthetic_scene(6000, 3, seed=12, scale_lo=0.01, scale_hi=0.05, device=dev)
+
+
+def _gt(rank, dev):
+    return torch.rand(128, 192, 3, generator=torch.Generator().manual_seed(rank)).to(dev)
+
+
+BG = (0.3, 0.5, 0.7)
+
+
+def _worker(rank, world, port, out_dir, mode):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from gaussctrl_exp_amd.train import TrainStep
+    bg = torch.tensor(BG, device=dev)
+    t = TrainStep(_scene(dev), sh_degree=3, world_size=world, loss="l1", render_mode="fused",
+                  grad_exchange=mode)
+    assert not t.fuse_adam  # multi-rank: the gradients must be summed before Adam
+    t.step(_views(dev)[rank], _gt(rank, dev), background=bg, optimizer=False)
+    np.save(os.path.join(out_dir, f"grad{rank}.npy"), t.flat_grad().cpu().numpy())
+    for _ in range(2):
+        t.step(_views(dev)[rank], _gt(rank, dev), background=bg)
+    np.save(os.path.join(out_dir, f"params{rank}.npy"),
+            torch.cat([p.detach().reshape(-1) for p in t.params]).cpu().numpy())
+    torch.cuda.synchronize()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["sh_views", "allreduce"])
+def test_fused_two_ranks_sum_the_view_gradients(tmp_path, mode):
+    port = _free_port()
+    mp.spawn(_worker, args=(2, port, str(tmp_path), mode), nprocs=2, join=True)
+    g0, g1 = np.load(tmp_path / "grad0.npy"), np.load(tmp_path / "grad1.npy")
+    np.testing.assert_array_equal(g0, g1)  # every rank holds the same summed gradients
+    np.testing.assert_array_equal(np.load(tmp_path / "params0.npy"),
+                                  np.load(tmp_path / "params1.npy"))
+    from gaussctrl_exp_amd.train import TrainStep
+    dev = torch.device("cuda:0")
+    ref = 0
+    for r in range(2):
+        t = TrainStep(_scene(dev), sh_degree=3, world_size=1, loss="l1", render_mode="fused")
+        t.step(_views(dev)[r], _gt(r, dev), background=torch.tensor(BG, device=dev),
+               optimizer=False)
+        ref = ref + t.flat_grad().cpu().numpy()
+    assert np.abs(ref).max() > 0
+    bad = ~np.isclose(g0, ref, rtol=1e-4, atol=1e-6)
+    assert bad.mean() <= 1e-4, f"{bad.mean():.2e} differ (max {np.abs(g0 - ref).max():.3e})"
