@@ -226,3 +226,52 @@ def render_fused(scene, cam: GCCamera, sh_degree_to_use: int, background: Tensor
             "accumulation": alpha[..., None] if alpha is not None else None,
             "xys": aux["xys"], "radii": aux["radii"], "xys_grad": xys_grad,
             "num_intersects": aux["num_intersects"]}
+
+
+@torch.no_grad()
+def render_fused_eval(scene, cam: GCCamera, sh_degree_to_use: int, background: Tensor):
+    """The eval render of gc_model.get_outputs (gc_model.py:158-238: RGB, alpha and the depth
+    image of the second rasterize call, depth / alpha with 1000 where alpha == 0) from one
+    fused preprocess kernel, one binning and one RGB+depth traversal
+    (gsplat_rasterize_forward_rgbd).  Bit-identical to scene.render(..., return_depth=True,
+    fused_depth=True), whose inputs the caller's torch glue prepares.  Used by the eval /
+    render_reverse path (gc_pipeline.py:228, gc_render.py:196-203)."""
+    n = scene.means.shape[0]
+    params = [_contig_f32(t) for t in (scene.means, scene.scales, scene.quats, scene.opacities,
+                                       scene.features_dc, scene.features_rest)]
+    K = 1 + params[5].shape[1]
+    if K not in _DEG_OF_BASES or not 0 <= sh_degree_to_use <= _DEG_OF_BASES[K]:
+        raise ValueError("render_fused_eval: bad SH layout / degree")
+    viewmat, projmat = _contig_f32(cam.viewmat), _contig_f32(cam.projmat)
+    campos, background = _contig_f32(cam.c2w[..., :3, 3].reshape(3)), _contig_f32(background)
+    dev = _lib.check_device("render_fused_eval", *params, viewmat, projmat, campos, background)
+    H, W = cam.height, cam.width
+    tbx, tby = (W + BLOCK_X - 1) // BLOCK_X, (H + BLOCK_Y - 1) // BLOCK_Y
+    f32 = dict(device=dev, dtype=torch.float32)
+    xys, depths, conics = torch.empty((n, 2), **f32), torch.empty((n,), **f32), \
+        torch.empty((n, 3), **f32)
+    colors, opac = torch.empty((n, 3), **f32), torch.empty((n,), **f32)
+    radii = torch.empty((n,), device=dev, dtype=torch.int32)
+    nth = torch.empty((n,), device=dev, dtype=torch.int32)
+    P, st = _lib.ptr, _lib.stream(dev)
+    _lib.call("gsplat_fused_preprocess_forward", n, K, int(sh_degree_to_use), *[P(t) for t in
+              params[:5]], P(params[5]) if K > 1 else None, P(viewmat), P(projmat), P(campos),
+              float(cam.fx), float(cam.fy), float(cam.cx), float(cam.cy), H, W, tbx, tby, 0.01,
+              P(xys), P(depths), P(radii), P(conics), P(nth), P(colors), P(opac), None, None,
+              None, st)
+    num_intersects, gids, bins = bin_gaussians(xys, depths, radii, nth, H, W)
+    if num_intersects < 1:  # nothing visible: the caller's early return (gc_model.py:189-190)
+        return {"rgb": background.repeat(H, W, 1), "depth": None, "accumulation": None,
+                "xys": xys, "radii": radii}
+    out_img = torch.empty((H, W, 3), **f32)
+    depth_im = torch.empty((H, W, 1), **f32)
+    final_Ts = torch.empty((H, W), **f32)
+    final_idx = torch.empty((H, W), device=dev, dtype=torch.int32)
+    _lib.call("gsplat_rasterize_forward_rgbd", tbx, tby, H, W, P(gids), P(bins), P(xys),
+              P(conics), P(colors), P(depths), P(opac), P(background), P(out_img), P(depth_im),
+              P(final_Ts), P(final_idx), st)
+    alpha = (1 - final_Ts)[..., None]
+    rgb = torch.clamp(out_img, max=1.0)
+    depth_im[alpha > 0] = depth_im[alpha > 0] / alpha[alpha > 0]
+    depth_im[alpha == 0] = 1000
+    return {"rgb": rgb, "depth": depth_im, "accumulation": alpha, "xys": xys, "radii": radii}

@@ -252,3 +252,18 @@ def test_fused_adam_in_backward_matches_separate_step(gpu):
         bad = ~np.isclose(a, b, rtol=1e-5, atol=1e-6)
         assert bad.mean() <= 1e-4, f"{name}: {bad.mean():.2e} differ (max {np.abs(a - b).max():.3e})"
         assert not np.array_equal(b, _np(getattr(synthetic_scene(20000, 3, seed=8), name)))
+
+
+@pytest.mark.parametrize("case", [CASES[0], CASES[2], CASES[3], CASES[6]])
+def test_fused_eval_render_bitexact_with_caller(gpu, case):
+    """render_fused_eval == scene.render(return_depth=True, fused_depth=True) bit for bit (the
+    forward of the fused preprocess is bit-identical to the caller's glue + gsplat calls)."""
+    from gaussctrl_exp_amd.fused import render_fused_eval
+    sc, cam = _scene_cam(case)
+    d, c = sc.to(gpu), cam.to(gpu)
+    bg = torch.tensor([0.1, 0.2, 0.3], device=gpu)
+    a = render_fused_eval(d, c, case[4], bg)
+    with torch.no_grad():
+        b = render(d, c, case[4], bg, return_depth=True, fused_depth=True)
+    for k in ("rgb", "depth", "accumulation", "xys", "radii"):
+        assert torch.equal(a[k], b[k]), k
