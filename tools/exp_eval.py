@@ -1,5 +1,6 @@
 """Eval render (gc_model.get_outputs with return_depth) at the headline size: the reference
-caller's two rasterize calls (with and without the binning reuse) vs the fused RGB+depth pass."""
+caller's two rasterize calls (with and without the binning reuse) vs the fused RGB+depth pass, and
+the fused preprocess + RGB+depth pass (fused.render_fused_eval)."""
 import os
 import sys
 import time
@@ -39,3 +40,19 @@ def run(label, fused, cache=True, reps=30):
 run("two rasterize calls, no binning reuse", False, cache=False)
 run("two rasterize calls, binning reused", False)
 run("fused RGB+depth pass", True)
+
+
+def run_fused_eval(reps=30):
+    from gaussctrl_exp_amd.fused import render_fused_eval
+    for _ in range(5):
+        render_fused_eval(sc, cam, 3, bg)
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(reps):
+        render_fused_eval(sc, cam, 3, bg)
+    torch.cuda.synchronize()
+    print(f"fused preprocess + RGB+depth pass (render_fused_eval): "
+          f"{(time.perf_counter() - t) / reps * 1e3:.3f} ms per eval render")
+
+
+run_fused_eval()
