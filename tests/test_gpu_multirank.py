@@ -1,4 +1,4 @@
-"""The fused training step's data-parallel path with two ranks on one GPU (gloo carries the
+"""The fused training step's data-parallel path with two (four) ranks on one GPU (gloo carries the
 collectives here: RCCL needs one GPU per rank, and the box has one).  Each rank renders its
 own view through the fused kernels; the SH-feature gradients go through the view exchange
 (gsplat_compute_sh_backward_views_split on the all-gathered colour gradients) or plain
@@ -25,10 +25,13 @@ def _free_port():
     return port
 
 
+EYES = ((0.0, 0.0, 4.0), (1.5, 0.5, 3.6), (-1.2, -0.4, 3.7), (0.4, 1.3, 3.7))
+
+
 def _views(dev):
     from gaussctrl_exp_amd.camera import gc_camera, look_at_c2w
     return [gc_camera(look_at_c2w(eye, up=(0.0, 1.0, 0.0)), 220.0, 220.0, 96.0, 64.0, 192, 128)
-            .to(dev) for eye in ((0.0, 0.0, 4.0), (1.5, 0.5, 3.6))]
+            .to(dev) for eye in EYES]
 
 
 def _scene(dev):
@@ -63,18 +66,19 @@ def _worker(rank, world, port, out_dir, mode):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", ["sh_views", "allreduce"])
-def test_fused_two_ranks_sum_the_view_gradients(tmp_path, mode):
+@pytest.mark.parametrize("mode,world", [("sh_views", 2), ("allreduce", 2), ("sh_views", 4)])
+def test_fused_ranks_sum_the_view_gradients(tmp_path, mode, world):
     port = _free_port()
-    mp.spawn(_worker, args=(2, port, str(tmp_path), mode), nprocs=2, join=True)
-    g0, g1 = np.load(tmp_path / "grad0.npy"), np.load(tmp_path / "grad1.npy")
-    np.testing.assert_array_equal(g0, g1)  # every rank holds the same summed gradients
-    np.testing.assert_array_equal(np.load(tmp_path / "params0.npy"),
-                                  np.load(tmp_path / "params1.npy"))
+    mp.spawn(_worker, args=(world, port, str(tmp_path), mode), nprocs=world, join=True)
+    g0 = np.load(tmp_path / "grad0.npy")
+    for r in range(1, world):  # every rank holds the same summed gradients and parameters
+        np.testing.assert_array_equal(np.load(tmp_path / f"grad{r}.npy"), g0)
+        np.testing.assert_array_equal(np.load(tmp_path / f"params{r}.npy"),
+                                      np.load(tmp_path / "params0.npy"))
     from gaussctrl_exp_amd.train import TrainStep
     dev = torch.device("cuda:0")
     ref = 0
-    for r in range(2):
+    for r in range(world):
         t = TrainStep(_scene(dev), sh_degree=3, world_size=1, loss="l1", render_mode="fused")
         t.step(_views(dev)[r], _gt(r, dev), background=torch.tensor(BG, device=dev),
                optimizer=False)
