@@ -300,14 +300,40 @@ __global__ __launch_bounds__(sh_threads(K)) void fused_bwd_kernel(FusedBwdArgs a
         const int total = cnt * RROW;
         const long long off = g0 * RROW;
         const float w1 = 1.f - o.beta1, w2 = 1.f - o.beta2;
-        for (int k = threadIdx.x; k < total; k += THR) {
+        float *P = o.p[5] + off, *M = o.m[5] + off, *V = o.v[5] + off;
+        auto grad_at = [&](int k) {
           const int r = k / RROW;
-          const float gv = smem[r * RP + (k - r * RROW)];
-          float pv = o.p[5][off + k], mv = o.m[5][off + k], vv = o.v[5][off + k];
-          adam_elem(pv, gv, mv, vv, w1, o.beta2, w2, o.ss[5], o.bc2s[5], o.eps);
-          o.p[5][off + k] = pv;
-          o.m[5][off + k] = mv;
-          o.v[5][off + k] = vv;
+          return smem[r * RP + (k - r * RROW)];
+        };
+        int k0 = 0;
+        if (((((uintptr_t)P) | ((uintptr_t)M) | ((uintptr_t)V)) & 15) == 0) {
+          // 16-byte vectors: the slab of a block starts 16-byte aligned (256 x 180 B)
+          typedef float f4 __attribute__((ext_vector_type(4)));
+          const int nv = total >> 2;
+          for (int q = threadIdx.x; q < nv; q += THR) {
+            f4 pv = reinterpret_cast<f4 *>(P)[q], mv = reinterpret_cast<f4 *>(M)[q],
+               vv = reinterpret_cast<f4 *>(V)[q];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              float pj = pv[j], mj = mv[j], vj = vv[j];
+              adam_elem(pj, grad_at(4 * q + j), mj, vj, w1, o.beta2, w2, o.ss[5], o.bc2s[5],
+                        o.eps);
+              pv[j] = pj;
+              mv[j] = mj;
+              vv[j] = vj;
+            }
+            reinterpret_cast<f4 *>(P)[q] = pv;
+            reinterpret_cast<f4 *>(M)[q] = mv;
+            reinterpret_cast<f4 *>(V)[q] = vv;
+          }
+          k0 = nv << 2;
+        }
+        for (int k = k0 + threadIdx.x; k < total; k += THR) {
+          float pv = P[k], mv = M[k], vv = V[k];
+          adam_elem(pv, grad_at(k), mv, vv, w1, o.beta2, w2, o.ss[5], o.bc2s[5], o.eps);
+          P[k] = pv;
+          M[k] = mv;
+          V[k] = vv;
         }
       } else {
         store_cols<RROW, 0, RP, THR>(smem, cnt, a.v_rest + g0 * RROW);
