@@ -48,6 +48,34 @@ def fused_bwd():
               None, st)
 
 
+import ctypes
+mv = [(torch.zeros_like(t), torch.zeros_like(t)) for t in
+      (sc.means, sc.scales, sc.quats, sc.opacities, sc.features_dc, sc.features_rest)]
+M = (ctypes.c_void_p * 6)(*[m.data_ptr() for m, _ in mv])
+V = (ctypes.c_void_p * 6)(*[v.data_ptr() for _, v in mv])
+LR = (ctypes.c_float * 6)(1e-9, 1e-9, 1e-9, 1e-9, 1e-9, 1e-9)  # keep the scene ~fixed
+pc = [t.clone() for t in (sc.means, sc.scales, sc.quats, sc.opacities, sc.features_dc,
+                          sc.features_rest)]
+
+
+def fused_bwd_adam():
+    _lib.call("gsplat_fused_preprocess_backward_adam", N, 16, 3, *[P(t) for t in pc],
+              P(cam.viewmat), P(cam.projmat), P(campos), cam.fx, cam.fy, cam.cx, cam.cy, H, W,
+              P(radii), P(conics), P(colors), P(opac), P(rec), ctypes.cast(M, ctypes.c_void_p),
+              ctypes.cast(V, ctypes.c_void_p), ctypes.cast(LR, ctypes.c_void_p), 1, 0.9, 0.999,
+              1e-15, st)
+
+
+def adam_sep():
+    Pp = (ctypes.c_void_p * 6)(*[t.data_ptr() for t in pc])
+    G = (ctypes.c_void_p * 6)(*[x.data_ptr() for x in v])
+    n = (ctypes.c_int64 * 6)(*[t.numel() for t in pc])
+    _lib.call("gsplat_adam_step", 6, ctypes.cast(Pp, ctypes.c_void_p),
+              ctypes.cast(G, ctypes.c_void_p), ctypes.cast(M, ctypes.c_void_p),
+              ctypes.cast(V, ctypes.c_void_p), ctypes.cast(n, ctypes.c_void_p),
+              ctypes.cast(LR, ctypes.c_void_p), 1, 0.9, 0.999, 1e-15, st)
+
+
 scales = torch.exp(sc.scales)
 quats = sc.quats / sc.quats.norm(dim=-1, keepdim=True)
 cov3d = f(N, 6)
@@ -78,13 +106,14 @@ def timeit(fn, reps=20):
 
 cases = {"fused_fwd K16": fused_fwd, "fused_fwd K16 no records": lambda: fused_fwd(records=False),
          "fused_fwd K1 (projection + activations)": lambda: fused_fwd(sc1),
-         "fused_bwd K16": fused_bwd, "project_fwd": proj_fwd, "sh_fwd": sh_fwd}
+         "fused_bwd K16": fused_bwd, "fused_bwd+adam K16": fused_bwd_adam,
+         "adam_step (separate)": adam_sep, "project_fwd": proj_fwd, "sh_fwd": sh_fwd}
 res = {k: [] for k in cases}
 for _ in range(5):
     for k, fn in cases.items():
         fn()
         torch.cuda.synchronize()
         res[k].append(timeit(fn))
-print(f"{cfg}: N={N}")
+print(f"{cfg}: N={N} lib={_lib.LIB_PATH}")
 for k in cases:
     print(f"{k:45s} {np.median(res[k]):8.1f} us")
