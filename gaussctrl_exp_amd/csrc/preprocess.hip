@@ -103,39 +103,6 @@ __device__ __forceinline__ int view_basis(int degrees_to_use, float p0, float p1
   return sh_basis(degrees_to_use, dx, dy, dz, b);
 }
 
-// Backward LDS rows: [basis_1 .. basis_{K-1}, v_rgb0, v_rgb1, v_rgb2] per Gaussian (72 B at
-// degree 3 instead of the 180 B of formed gradients: more blocks per CU).
-__host__ __device__ constexpr int bwd_row_pitch(int K) { return (K + 2) | 1; }
-// Element k of the block's features_rest gradient slab (gsplat compute_sh_backward:
-// basis_j * v_rgb[c] for coefficient j + 1, channel c) -- the same single product as before.
-template <int K, int RP>
-__device__ __forceinline__ float rest_grad(const float *smem, int k) {
-  constexpr int RROW = (K - 1) * 3;
-  const int r = k / RROW, e = k - r * RROW, j = e / 3, c = e - 3 * j;
-  return smem[r * RP + j] * smem[r * RP + (K - 1) + c];
-}
-// Writes the block's cnt gradient rows to dst [cnt * (K-1) * 3] (16-byte stores if aligned).
-template <int K, int RP, int THR>
-__device__ __forceinline__ void store_rest_grads(const float *smem, int cnt, float *dst) {
-  constexpr int RROW = (K - 1) * 3;
-  const int total = cnt * RROW;
-  int k0 = 0;
-  if ((((uintptr_t)dst) & 15) == 0) {
-    const int nv = total >> 2;
-    float4 *d4 = reinterpret_cast<float4 *>(dst);
-    for (int q = threadIdx.x; q < nv; q += THR) {
-      float4 v;
-      v.x = rest_grad<K, RP>(smem, 4 * q);
-      v.y = rest_grad<K, RP>(smem, 4 * q + 1);
-      v.z = rest_grad<K, RP>(smem, 4 * q + 2);
-      v.w = rest_grad<K, RP>(smem, 4 * q + 3);
-      d4[q] = v;
-    }
-    k0 = nv << 2;
-  }
-  for (int k = k0 + threadIdx.x; k < total; k += THR) dst[k] = rest_grad<K, RP>(smem, k);
-}
-
 template <int K>
 __global__ __launch_bounds__(sh_threads(K)) void fused_fwd_kernel(FusedFwdArgs a, ProjParams pp) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -219,9 +186,7 @@ __global__ __launch_bounds__(sh_threads(K)) void fused_bwd_kernel(FusedBwdArgs a
                                                                   FusedAdamArgs o = {}) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int RROW = (K - 1) * 3;
-  // LDS row per Gaussian: the K-1 basis values and the 3 colour gradients (odd pitch); the
-  // features_rest gradient element (k, c) = basis_k * v_rgb[c] is formed when it is stored
-  constexpr int RP = bwd_row_pitch(K);
+  constexpr int RP = RROW | 1;
   constexpr int THR = sh_threads(K);
   const long long g0 = (long long)blockIdx.x * THR;
   const int cnt = (int)min((long long)THR, (long long)a.n - g0);
@@ -319,10 +284,12 @@ __global__ __launch_bounds__(sh_threads(K)) void fused_bwd_kernel(FusedBwdArgs a
       } else {
       float *row = smem + t * RP;
 #pragma unroll
-      for (int k = 1; k < K; ++k) row[k - 1] = k < nb ? b[k] : 0.f;
-      row[K - 1] = vc[0];
-      row[K] = vc[1];
-      row[K + 1] = vc[2];
+      for (int k = 1; k < K; ++k) {
+        const float bk = k < nb ? b[k] : 0.f;
+        row[(k - 1) * 3 + 0] = bk * vc[0];
+        row[(k - 1) * 3 + 1] = bk * vc[1];
+        row[(k - 1) * 3 + 2] = bk * vc[2];
+      }
       }
     }
   }
@@ -334,7 +301,10 @@ __global__ __launch_bounds__(sh_threads(K)) void fused_bwd_kernel(FusedBwdArgs a
         const long long off = g0 * RROW;
         const float w1 = 1.f - o.beta1, w2 = 1.f - o.beta2;
         float *P = o.p[5] + off, *M = o.m[5] + off, *V = o.v[5] + off;
-        auto grad_at = [&](int k) { return rest_grad<K, RP>(smem, k); };
+        auto grad_at = [&](int k) {
+          const int r = k / RROW;
+          return smem[r * RP + (k - r * RROW)];
+        };
         int k0 = 0;
         if (((((uintptr_t)P) | ((uintptr_t)M) | ((uintptr_t)V)) & 15) == 0) {
           // 16-byte vectors: the slab of a block starts 16-byte aligned (256 x 180 B)
@@ -366,7 +336,7 @@ __global__ __launch_bounds__(sh_threads(K)) void fused_bwd_kernel(FusedBwdArgs a
           V[k] = vv;
         }
       } else {
-        store_rest_grads<K, RP, THR>(smem, cnt, a.v_rest + g0 * RROW);
+        store_cols<RROW, 0, RP, THR>(smem, cnt, a.v_rest + g0 * RROW);
       }
     }
   }
@@ -448,7 +418,7 @@ extern "C" int gsplat_fused_preprocess_backward(
   const ProjParams pp = make_proj_params(fx, fy, cx, cy, 1.f, 0.f, img_height, img_width, 1, 1);
   const int thr = sh_threads(K);
   const dim3 grid(cdiv(num_points, thr));
-  const size_t smem = (K > 1 && !args.v_colors) ? (size_t)thr * bwd_row_pitch(K) * sizeof(float)
+  const size_t smem = (K > 1 && !args.v_colors) ? (size_t)thr * (((K - 1) * 3) | 1) * sizeof(float)
                                                 : 0;
   hipStream_t st = (hipStream_t)stream;
   FUSED_DISPATCH(fused_bwd_kernel, args);
@@ -493,7 +463,7 @@ extern "C" int gsplat_fused_preprocess_backward_adam(
   const ProjParams pp = make_proj_params(fx, fy, cx, cy, 1.f, 0.f, img_height, img_width, 1, 1);
   const int thr = sh_threads(K);
   const dim3 grid(cdiv(num_points, thr));
-  const size_t smem = K > 1 ? (size_t)thr * bwd_row_pitch(K) * sizeof(float) : 0;
+  const size_t smem = K > 1 ? (size_t)thr * (((K - 1) * 3) | 1) * sizeof(float) : 0;
   hipStream_t st = (hipStream_t)stream;
   switch (K) {
 #define ADAM_CASE(KK)                                                                      \
