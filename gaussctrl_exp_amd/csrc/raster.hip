@@ -884,6 +884,235 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
   }
 }
 
+// ---------------------------------------------------------------- grouped backward
+// Row-local reduce-scatter of nine values over each 16-lane DPP row (row_ror:8,
+// row_half_mirror, quad perms): afterwards nine lanes of every row each hold the row sum of
+// one value (reduce9_row_slot() says which) -- four independent reductions per instruction.
+__device__ __forceinline__ float reduce9_row(const float (&v)[9]) {
+  const int lane = __lane_id();
+  const bool h8 = lane & 8, h4 = lane & 4, h2 = lane & 2, h1 = lane & 1;
+  const float a0 = dpp_pair_sum<0x128>(v[0], v[5], h8), a1 = dpp_pair_sum<0x128>(v[1], v[6], h8),
+              a2 = dpp_pair_sum<0x128>(v[2], v[7], h8), a3 = dpp_pair_sum<0x128>(v[3], v[8], h8),
+              a4 = dpp_pair_sum<0x128>(v[4], 0.f, h8);
+  const float b0 = dpp_pair_sum<0x141>(a0, a2, h4), b1 = dpp_pair_sum<0x141>(a1, a3, h4),
+              b2 = dpp_pair_sum<0x141>(a4, 0.f, h4);
+  const float c0 = dpp_pair_sum<0x4E>(b0, b1, h2), c1 = dpp_pair_sum<0x4E>(b2, 0.f, h2);
+  return dpp_pair_sum<0xB1>(c0, c1, h1);
+}
+__device__ __forceinline__ int reduce9_row_slot() {
+  float p[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) p[k] = (__lane_id() & 15) == 0 ? (float)(k + 1) : 0.f;
+  return (int)reduce9_row(p) - 1;
+}
+__device__ __forceinline__ int row_max_int(int v) {  // max over the lane's 16-lane row
+  for (int off = 8; off >= 1; off >>= 1) {
+    const int o = __shfl_xor(v, off, 64);
+    v = v > o ? v : o;
+  }
+  return v;
+}
+
+// Backward with sub-wave lists (gsplat_debug_set_raster_variant flag 2048): the wave's 16x8
+// strip is split into four 8x4 rectangles, one per 16-lane row (two vertically adjacent
+// pixels per lane), and each row walks its own culled list of the staged Gaussians -- a
+// Gaussian is visited only by the rows whose rectangle it can touch (exact min-sigma cull per
+// rectangle, and idx <= the rectangle's largest final_idx), so a wave iteration carries up to
+// four different Gaussians.  Per iteration each row reduce-scatters its nine partial sums
+// with row-local DPP and one atomic instruction adds all four rows' records.
+template <bool CHUNKED = false>
+__global__ __launch_bounds__(256) void raster_bwd3g_kernel(
+    int tbx, int tby, int H, int W, const int *__restrict__ gids, const int2 *__restrict__ bins,
+    const float2 *__restrict__ xys, const float *__restrict__ conics,
+    const float *__restrict__ colors, const float *__restrict__ opacity,
+    const float *__restrict__ background, const float *__restrict__ final_Ts,
+    const int *__restrict__ final_idx, const float *__restrict__ v_out,
+    const float *__restrict__ v_out_alpha, float alpha_max, float *__restrict__ rec,
+    int chunk = 0, const int *__restrict__ item_off = nullptr,
+    const int *__restrict__ item_tile = nullptr, const int *__restrict__ ckpt_off = nullptr,
+    const float4 *__restrict__ ckpt = nullptr) {
+  constexpr int PXL = 2, COLS = 16;
+  typedef f2 PV;
+  int ctile = -1, cj = 0;
+  if (CHUNKED) {
+    const int slot = wave_slot<PXL, COLS>();
+    if (slot >= item_off[tbx * tby]) return;  // wave-uniform: past the last item
+    ctile = item_tile[slot];
+    cj = slot - item_off[ctile];
+  }
+  const WaveRect R = wave_rect<PXL, COLS>(tbx, tby, H, W, ctile);
+  if (!R.live) return;  // wave-uniform
+  __shared__ GStage lds[4][64];
+  __shared__ unsigned char lists[4][4][64];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int grp = lane >> 4, m = lane & 15;
+  const int tile = R.tile;
+  const int c0 = (int)R.rx0, r0 = (int)R.ry0;
+  const int j = c0 + (grp & 1) * 8 + (m & 7);
+  const int i0 = r0 + (grp >> 1) * 4 + (m >> 3) * 2;
+  const float px = (float)j;
+  const float bg0 = background[0], bg1 = background[1], bg2 = background[2];
+  PV py, T, vr, vg, vb, q, Sb;
+  int binf[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int i = i0 + k;
+    float Tf = 0.f, r = 0.f, g = 0.f, bl = 0.f, a = 0.f;
+    int bf = -1;
+    if (i < H && j < W) {
+      const int pix = i * W + j;
+      Tf = final_Ts[pix];
+      bf = final_idx[pix];
+      r = v_out[3 * pix];
+      g = v_out[3 * pix + 1];
+      bl = v_out[3 * pix + 2];
+      a = v_out_alpha ? v_out_alpha[pix] : 0.f;
+    }
+    const float qk = Tf * (a - (bg0 * r + bg1 * g + bg2 * bl));
+    if (k) {
+      py.y = (float)i; T.y = Tf; vr.y = r; vg.y = g; vb.y = bl; q.y = qk;
+    } else {
+      py.x = (float)i; T.x = Tf; vr.x = r; vg.x = g; vb.x = bl; q.x = qk;
+    }
+    binf[k] = bf;
+  }
+  Sb = PV(0.f);
+  const int2 range = bins[tile];
+  int lo = range.x, hi = range.y;
+  if (CHUNKED) {
+    const int len = range.y - range.x;
+    const int nch = len > chunk ? (len + chunk - 1) / chunk : 1;
+    if (nch > 1) {
+      lo = range.x + cj * chunk;
+      hi = min(lo + chunk, range.y);
+      if (cj < nch - 1) {  // start from the checkpoint after this chunk
+        const size_t cb = (size_t)ckpt_off[tile] * (GS_BLOCK * GS_BLOCK);
+        const int oy = (tile / tbx) * GS_BLOCK, ox = (tile % tbx) * GS_BLOCK;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const int i = i0 + k;
+          if (i < H && j < W) {
+            const int lpix = (i - oy) * GS_BLOCK + (j - ox);
+            const float4 cj4 = ckpt[cb + (size_t)cj * (GS_BLOCK * GS_BLOCK) + lpix];
+            const float4 cf4 = ckpt[cb + (size_t)(nch - 1) * (GS_BLOCK * GS_BLOCK) + lpix];
+            const float vr_ = k ? vr.y : vr.x, vg_ = k ? vg.y : vg.x, vb_ = k ? vb.y : vb.x;
+            const float sb = (cf4.y - cj4.y) * vr_ + (cf4.z - cj4.z) * vg_ + (cf4.w - cj4.w) * vb_;
+            if (k) { T.y = cj4.x; Sb.y = sb; } else { T.x = cj4.x; Sb.x = sb; }
+          }
+        }
+      }
+    }
+  }
+  // per-row (8x4 rectangle) largest final_idx, and the rectangles (wave-uniform)
+  const int rmax = row_max_int(max(binf[0], binf[1]));
+  int gmax[4];
+  float gx0[4], gx1[4], gy0[4], gy1[4];
+  bool gok[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    gmax[g] = __builtin_amdgcn_readlane(rmax, 16 * g);
+    const int sx0 = c0 + (g & 1) * 8, sy0 = r0 + (g >> 1) * 4;
+    gok[g] = sx0 < W && sy0 < H && gmax[g] >= 0;
+    gx0[g] = (float)sx0;
+    gx1[g] = (float)min(sx0 + 7, W - 1);
+    gy0[g] = (float)sy0;
+    gy1[g] = (float)min(sy0 + 3, H - 1);
+  }
+  const int maxbin = max(max(gmax[0], gmax[1]), max(gmax[2], gmax[3]));
+  const int slot = reduce9_row_slot();
+  const int last = min(maxbin, hi - 1);
+  GStage *stage = lds[wave];
+  for (int b = last; b >= lo; b -= 64) {
+    const int idx = b - lane;
+    GStage s;
+    bool kg[4] = {false, false, false, false};
+    if (idx >= lo) {
+      const int gid = gids[idx];
+      const float2 xy = xys[gid];
+      const float a = conics[3 * gid], bb = conics[3 * gid + 1], c = conics[3 * gid + 2];
+      const float o = opacity[gid];
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        kg[g] = gok[g] && idx <= gmax[g] &&
+                touches_rect(xy.x, xy.y, a, bb, c, o, gx0[g], gx1[g], gy0[g], gy1[g]);
+      if (kg[0] || kg[1] || kg[2] || kg[3]) {
+        s.x = xy.x;
+        s.y = xy.y;
+        s.ha = 0.5f * a;
+        s.b = bb;
+        s.hc = 0.5f * c;
+        s.o = o;
+        s.r = colors[3 * gid];
+        s.g = colors[3 * gid + 1];
+        s.bl = colors[3 * gid + 2];
+        s.idx = idx;
+        s.id = gid;
+      }
+    }
+    const bool keep = kg[0] || kg[1] || kg[2] || kg[3];
+    const unsigned long long kmask = __ballot(keep);
+    const int my_slot = (int)lanes_below(kmask);
+    if (keep) stage[my_slot] = s;
+    int ng[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const unsigned long long gm = __ballot(kg[g]);
+      ng[g] = __popcll(gm);
+      if (kg[g]) lists[wave][g][lanes_below(gm)] = (unsigned char)my_slot;
+    }
+    wave_lds_sync();
+    const int nmax = max(max(ng[0], ng[1]), max(ng[2], ng[3]));
+    const int myn = grp == 0 ? ng[0] : grp == 1 ? ng[1] : grp == 2 ? ng[2] : ng[3];
+    for (int t = 0; t < nmax; ++t) {
+      const bool live = t < myn;
+      GStage G = stage[lists[wave][grp][live ? t : 0] & 63];
+      if (!live) G.r = G.g = G.bl = G.o = 0.f;  // keep T / Sb finite; no contribution
+      const float dx = G.x - px;
+      const float hA = G.ha * dx * dx, bdx = G.b * dx;
+      const PV dy = G.y - py;
+      const PV sig = gs_sigma2v<PV>(G.hc, bdx, hA, dy);
+      const PV vis = gs_vis2v<PV>(sig);
+      const PV ov = G.o * vis;
+      const PV al = {fminf(alpha_max, ov.x), fminf(alpha_max, ov.y)};
+      const bool v0 = live && G.idx <= binf[0] && sig.x >= 0.f && al.x >= ALPHA_MIN;
+      const bool v1 = live && G.idx <= binf[1] && sig.y >= 0.f && al.y >= ALPHA_MIN;
+      const PV am = {v0 ? al.x : 0.f, v1 ? al.y : 0.f};
+      const PV vm = {v0 ? vis.x : 0.f, v1 ? vis.y : 0.f};
+      const PV om = 1.f - am;
+      const PV ra = {__builtin_amdgcn_rcpf(om.x), __builtin_amdgcn_rcpf(om.y)};
+      T = T * ra;
+      const PV fac = am * T;
+      const PV gv = vfma(PV(G.r), vr, vfma(PV(G.g), vg, G.bl * vb));
+      const PV v_alpha = vfma(gv, T, ra * (q - Sb));
+      Sb = vfma(fac, gv, Sb);
+      const unsigned long long amask = __ballot(v0 || v1);
+      if (amask) {
+        const PV vva = vm * v_alpha;
+        const PV vs = vva * (-G.o);
+        const PV vsdy = vs * dy;
+        const float Vs = vs.x + vs.y, Vys = vsdy.x + vsdy.y;
+        const float dxV = dx * Vs;
+        float parts[9];
+        parts[0] = fmaf(2.f * G.ha, dxV, G.b * Vys);  // v_x
+        parts[1] = fmaf(G.b, dxV, 2.f * G.hc * Vys);  // v_y
+        parts[2] = dx * dxV;                          // 2 v_conic.a
+        parts[3] = dx * Vys;                          // 2 v_conic.b
+        const PV vsdy2 = vsdy * dy;
+        parts[4] = vsdy2.x + vsdy2.y;                 // 2 v_conic.c
+        const PV fr = fac * vr, fg = fac * vg, fb = fac * vb;
+        parts[5] = fr.x + fr.y;
+        parts[6] = fg.x + fg.y;
+        parts[7] = fb.x + fb.y;
+        parts[8] = vva.x + vva.y;
+        const float v = reduce9_row(parts);
+        const bool row_any = ((amask >> (16 * grp)) & 0xFFFFull) != 0;
+        if (row_any && slot >= 0) atomicAdd(rec + (size_t)G.id * REC + slot, v);
+      }
+    }
+    wave_lds_sync();
+  }
+}
+
 // List-split plan (one workgroup): per tile, the number of backward items (chunks of the
 // depth-sorted list, 1 for a tile no longer than `chunk`, 0 for an empty one) and of forward
 // checkpoints (as many as chunks for a split tile, else 0); exclusive scans of both give
@@ -1385,6 +1614,14 @@ extern "C" int gsplat_rasterize_backward(int tile_bounds_x, int tile_bounds_y, i
         if (atomics) BWD3P(2, true, 16); else BWD3P(2, false, 16);  // 16x16: one wave
       } else {
         if (narrow) { if (atomics) BWD3P(1, true, 8); else BWD3P(1, false, 8); }
+        else if (atomics && (g_bwd_flags & 2048)) {  // sub-wave lists (8x4 rectangles per row)
+          hipLaunchKernelGGL((raster_bwd3g_kernel<false>),
+                             dim3(cdiv(T, (tiles_per_block<2, 16>()))), dim3(256), 0, st,
+                             tile_bounds_x, tile_bounds_y, img_height, img_width,
+                             gaussian_ids_sorted, (const int2 *)tile_bins, (const float2 *)xys,
+                             conics, colors, opacity, background, final_Ts, final_idx, v_output,
+                             v_output_alpha, alpha_max, rec);
+        }
         else if (atomics && (g_bwd_flags & 512)) {  // ablation: scalar pixel pairs
           hipLaunchKernelGGL((raster_bwd3p_kernel<1, true, 16, false, s2>),
                              dim3(cdiv(T, (tiles_per_block<2, 16>()))), dim3(256), 0, st,

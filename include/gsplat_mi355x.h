@@ -284,7 +284,8 @@ int gsplat_rasterize_backward_records(
  * scalar backward; bit 2 scalar forward (one Gaussian per iteration, 16-column strips);
  * bit 3 packed float2 forward; bit 4 16-column forward rectangles; bit 5 8-column backward
  * rectangles; bit 6 backward stages and culls but skips the blend (timing ablation only); bit 10
- * XCD-contiguous block order in the shipped forward and backward kernels.  Every variant produces results within the same parity bar.  Process-wide;
+ * XCD-contiguous block order in the shipped forward and backward kernels; bit 11 backward with
+ * sub-wave lists (each 16-lane row of a wave walks its own 8x4 rectangle's culled list).  Every variant produces results within the same parity bar.  Process-wide;
  * defaults (1, 2, 0) are the shipped configuration. */
 int gsplat_debug_set_raster_variant(int fwd_pxl, int bwd_pxl, int bwd_flags);
 

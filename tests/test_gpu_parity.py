@@ -248,9 +248,11 @@ def test_raster_backward(gpu, case):
 
 # (fwd pixels/lane, bwd pixels/lane, flags): see gsplat_debug_set_raster_variant in
 # include/gsplat_mi355x.h (1 no atomics, 2 scalar bwd, 4 scalar fwd, 8 packed fwd, 16 wide
-# fwd, 32 narrow bwd, 1024 XCD-contiguous block order).
+# fwd, 32 narrow bwd, 1024 XCD-contiguous block order, 2048
+# sub-wave-list backward).
 RASTER_VARIANTS = [(1, 2, 0), (1, 2, 4), (1, 2, 16), (2, 2, 0), (2, 2, 8), (2, 2, 6), (4, 4, 0),
-                   (4, 4, 8), (4, 4, 6), (1, 1, 0), (1, 2, 32), (1, 2, 1024)]
+                   (4, 4, 8), (4, 4, 6), (1, 1, 0), (1, 2, 32), (1, 2, 1024),
+                   (1, 2, 2048)]
 
 
 @pytest.mark.parametrize("variant", RASTER_VARIANTS)

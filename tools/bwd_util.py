@@ -87,6 +87,23 @@ with torch.no_grad():
         tot["fwd_pairs"] += (v & (idx[:, None, None] <= fin + 1)).sum().item()
         tot["pairs_valid"] += (v & (idx[:, None, None] <= fin)).sum().item()
         tot["list"] += e - s
+        # sub-wave groups: a wave footprint (W x R) split into 4 groups of 16 lanes that each
+        # walk their own culled list (iterations per wave = the longest of the 4 lists)
+        for (wc, wr), (gc, gr) in (((16, 8), (8, 4)), ((8, 8), (4, 4)), ((16, 8), (16, 2))):
+            key = f"grouped_{wc}x{wr}_by_{gc}x{gr}"
+            for c0 in range(tx * 16, min(tx * 16 + 16, W), wc):
+                for r0 in range(ty * 16, min(ty * 16 + 16, H), wr):
+                    longest = 0
+                    for sc0 in range(c0, min(c0 + wc, W), gc):
+                        sc1 = min(sc0 + gc - 1, W - 1)
+                        for sr0 in range(r0, min(r0 + wr, H), gr):
+                            sr1 = min(sr0 + gr - 1, H - 1)
+                            mf = fin[sr0 - ty * 16: sr1 - ty * 16 + 1,
+                                     sc0 - tx * 16: sc1 - tx * 16 + 1].max().item()
+                            k = touches_exact(gx, gy, a, bb, c, o, float(sc0), float(sc1),
+                                              float(sr0), float(sr1))
+                            longest = max(longest, (k & (idx <= mf)).sum().item())
+                    tot[key] = tot.get(key, 0) + longest
         # wave footprints (cols, rows): strips of the full tile width and 8x8 blocks
         for cols, rows in ((16, 8), (16, 4), (16, 16), (8, 8), (8, 16)):
             for c0 in range(tx * 16, min(tx * 16 + 16, W), cols):
@@ -106,6 +123,8 @@ with torch.no_grad():
                             tot[lk] = tot.get(lk, 0) + (k & (idx <= mf) & live).sum().item()
     n = len(sample)
     print({k: round(v / n, 1) for k, v in tot.items()})
+    for k in sorted(t for t in tot if t.startswith("grouped")):
+        print(f"{k}: wave iters/tile {tot[k] / n:7.1f}")
     for cols, rows in ((16, 8), (16, 4), (16, 16), (8, 8), (8, 16)):
         for name in ("cons", "exact"):
             key = f"{name}_{cols}x{rows}"
