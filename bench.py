@@ -104,8 +104,10 @@ def algorithmic_bytes(N, I, P, T, K, nvis):
         "gsplat_compute_sh_backward": (24 + 12 * K) * N,
         "gsplat_project_gaussians_backward": 180 * N,
         # fused training render (csrc/preprocess.hip): raw params (56 + 12 (K-1) B) in,
-        # projection + colour + opacity (48 B) out, 48 B record zeroed per visible Gaussian
-        "gsplat_fused_preprocess_forward": (92 + 12 * K) * N + 48 * nvis,
+        # projection + colour + opacity (48 B) out
+        "gsplat_fused_preprocess_forward": (92 + 12 * K) * N,
+        # its blend also zeroes the 48-B gradient record of every visible Gaussian
+        "gsplat_rasterize_forward_clearing": 40 * I + 20 * P + 48 * nvis,
         "gsplat_rasterize_backward_records": 40 * I + 24 * P,
         # params + saved forward outputs (72 B) and the 48 B record in, 6 gradients out
         "gsplat_fused_preprocess_backward": (116 + 12 * K) * N + 48 * nvis,
@@ -119,6 +121,7 @@ ENTRY_KERNELS = {
     "gsplat_fused_preprocess_forward": ("fused_fwd_kernel",),
     "gsplat_fused_preprocess_backward": ("fused_bwd_kernel",),
     "gsplat_rasterize_forward": ("raster_fwd",),
+    "gsplat_rasterize_forward_clearing": ("raster_fwd",),
     "gsplat_compute_sh_forward": ("sh_fwd_kernel",),
 }
 PMC_TRAFFIC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",

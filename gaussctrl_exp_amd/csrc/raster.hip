@@ -352,9 +352,22 @@ __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
     float *__restrict__ final_Ts, int *__restrict__ final_idx,
     const float *__restrict__ depths = nullptr, float *__restrict__ out_depth = nullptr,
     int chunk = 0, const int *__restrict__ ckpt_off = nullptr,
-    float4 *__restrict__ ckpt = nullptr) {
+    float4 *__restrict__ ckpt = nullptr, float4 *__restrict__ zero = nullptr,
+    long long zero_n = 0) {
+  // Side job: clear a buffer (the fused path's gradient records) with the memory bandwidth the
+  // VALU-bound blend leaves idle -- a grid-stride sweep of coalesced 16-B stores, issued by each
+  // wave as it finishes (issued first, the blend's first load wait would also wait for them:
+  // gfx9's vmcnt counts stores).
+  auto clear_side_job = [&]() {
+    for (long long k = (long long)blockIdx.x * 256 + threadIdx.x; k < zero_n;
+         k += (long long)gridDim.x * 256)
+      zero[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+  };
   const WaveRect R = wave_rect<PXL, COLS>(tbx, tby, H, W);
-  if (!R.live) return;  // wave-uniform
+  if (!R.live) {  // wave-uniform
+    clear_side_job();
+    return;
+  }
   __shared__ GStage lds[4][64];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int tile = R.tile, j = R.j, i0 = R.i0;
@@ -466,6 +479,7 @@ __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
       if (DEPTH) out_depth[pix] = cd[k] + T[k] * 0.f;  // the depth render's zero background
     }
   }
+  clear_side_job();
 }
 
 // Packed variant: 2*NP pixels per lane held as NP float2 pairs and blended branch-free
@@ -1657,6 +1671,59 @@ extern "C" int gsplat_rasterize_backward(int tile_bounds_x, int tile_bounds_y, i
   return check_launch("rasterize_backward");
 }
 
+static int rasterize_forward_impl(int tile_bounds_x, int tile_bounds_y, int img_height,
+                                  int img_width, const int32_t *gaussian_ids_sorted,
+                                  const int32_t *tile_bins, const float *xys, const float *conics,
+                                  const float *colors, const float *opacity,
+                                  const float *background, float *out_img, float *final_Ts,
+                                  int32_t *final_idx, int64_t num_intersects, int chunk,
+                                  void *checkpoints, size_t checkpoint_bytes, void *zero,
+                                  size_t zero_bytes, void *stream, const char *who) {
+  hipStream_t st = (hipStream_t)stream;
+  if (tile_bounds_x <= 0 || tile_bounds_y <= 0 || img_height <= 0 || img_width <= 0 ||
+      (long long)tile_bounds_x * GS_BLOCK < img_width ||
+      (long long)tile_bounds_y * GS_BLOCK < img_height || (chunk > 0 && chunk % 64) ||
+      num_intersects < 0 || zero_bytes % 16 || (zero_bytes && !zero)) {
+    set_error("%s: bad sizes (tiles=%dx%d H=%d W=%d chunk=%d zero=%zu)", who, tile_bounds_x,
+              tile_bounds_y, img_height, img_width, chunk, zero_bytes);
+    return 1;
+  }
+  const int T = tile_bounds_x * tile_bounds_y;
+  const long long zn = (long long)(zero_bytes / 16);
+  if (chunk <= 0) {
+    if (!default_variants()) {  // debug variants: clear up front, then the variant's launch
+      if (zn && hipMemsetAsync(zero, 0, zero_bytes, st) != hipSuccess) {
+        set_error("%s: memset failed", who);
+        return 1;
+      }
+      return gsplat_rasterize_forward(tile_bounds_x, tile_bounds_y, img_height, img_width, 3,
+                                      gaussian_ids_sorted, tile_bins, xys, conics, colors,
+                                      opacity, background, out_img, final_Ts, final_idx, stream);
+    }
+    hipLaunchKernelGGL((raster_fwd3u_kernel<1, 8>), dim3(cdiv(T, (tiles_per_block<1, 8>()))),
+                       dim3(256), 0, st, tile_bounds_x, tile_bounds_y, img_height, img_width,
+                       gaussian_ids_sorted, (const int2 *)tile_bins, (const float2 *)xys,
+                       conics, colors, opacity, background, out_img, final_Ts, final_idx,
+                       nullptr, nullptr, 0, nullptr, nullptr, (float4 *)zero, zn);
+    return check_launch(who);
+  }
+  const ChunkWs w = carve_chunk_ws(checkpoints, T, num_intersects, chunk);
+  if (!checkpoints || checkpoint_bytes < w.bytes || !default_variants()) {
+    set_error("%s: checkpoint buffer %zu < %zu bytes (or non-default raster variant)", who,
+              checkpoint_bytes, w.bytes);
+    return 1;
+  }
+  hipLaunchKernelGGL(chunk_plan_kernel, dim3(1), dim3(1024), 0, st, T, (const int2 *)tile_bins,
+                     chunk, w.item_off, w.ckpt_off, w.item_tile);
+  hipLaunchKernelGGL((raster_fwd3u_kernel<1, 8, false, true>),
+                     dim3(cdiv(T, (tiles_per_block<1, 8>()))), dim3(256), 0, st, tile_bounds_x,
+                     tile_bounds_y, img_height, img_width, gaussian_ids_sorted,
+                     (const int2 *)tile_bins, (const float2 *)xys, conics, colors, opacity,
+                     background, out_img, final_Ts, final_idx, nullptr, nullptr, chunk,
+                     w.ckpt_off, w.ckpt, (float4 *)zero, zn);
+  return check_launch(who);
+}
+
 extern "C" int gsplat_rasterize_forward_chunked(
     int tile_bounds_x, int tile_bounds_y, int img_height, int img_width,
     const int32_t *gaussian_ids_sorted, const int32_t *tile_bins, const float *xys,
@@ -1667,30 +1734,24 @@ extern "C" int gsplat_rasterize_forward_chunked(
     return gsplat_rasterize_forward(tile_bounds_x, tile_bounds_y, img_height, img_width, 3,
                                     gaussian_ids_sorted, tile_bins, xys, conics, colors, opacity,
                                     background, out_img, final_Ts, final_idx, stream);
-  hipStream_t st = (hipStream_t)stream;
-  if (tile_bounds_x <= 0 || tile_bounds_y <= 0 || img_height <= 0 || img_width <= 0 ||
-      (long long)tile_bounds_x * GS_BLOCK < img_width ||
-      (long long)tile_bounds_y * GS_BLOCK < img_height || chunk % 64 || num_intersects < 0) {
-    set_error("rasterize_forward_chunked: bad sizes (tiles=%dx%d H=%d W=%d chunk=%d)",
-              tile_bounds_x, tile_bounds_y, img_height, img_width, chunk);
-    return 1;
-  }
-  const int T = tile_bounds_x * tile_bounds_y;
-  const ChunkWs w = carve_chunk_ws(checkpoints, T, num_intersects, chunk);
-  if (!checkpoints || checkpoint_bytes < w.bytes || !default_variants()) {
-    set_error("rasterize_forward_chunked: checkpoint buffer %zu < %zu bytes (or non-default "
-              "raster variant)", checkpoint_bytes, w.bytes);
-    return 1;
-  }
-  hipLaunchKernelGGL(chunk_plan_kernel, dim3(1), dim3(1024), 0, st, T, (const int2 *)tile_bins,
-                     chunk, w.item_off, w.ckpt_off, w.item_tile);
-  hipLaunchKernelGGL((raster_fwd3u_kernel<1, 8, false, true>),
-                     dim3(cdiv(T, (tiles_per_block<1, 8>()))), dim3(256), 0, st, tile_bounds_x,
-                     tile_bounds_y, img_height, img_width, gaussian_ids_sorted,
-                     (const int2 *)tile_bins, (const float2 *)xys, conics, colors, opacity,
-                     background, out_img, final_Ts, final_idx, nullptr, nullptr, chunk,
-                     w.ckpt_off, w.ckpt);
-  return check_launch("rasterize_forward_chunked");
+  return rasterize_forward_impl(tile_bounds_x, tile_bounds_y, img_height, img_width,
+                                gaussian_ids_sorted, tile_bins, xys, conics, colors, opacity,
+                                background, out_img, final_Ts, final_idx, num_intersects, chunk,
+                                checkpoints, checkpoint_bytes, nullptr, 0, stream,
+                                "rasterize_forward_chunked");
+}
+
+extern "C" int gsplat_rasterize_forward_clearing(
+    int tile_bounds_x, int tile_bounds_y, int img_height, int img_width,
+    const int32_t *gaussian_ids_sorted, const int32_t *tile_bins, const float *xys,
+    const float *conics, const float *colors, const float *opacity, const float *background,
+    float *out_img, float *final_Ts, int32_t *final_idx, int64_t num_intersects, int chunk,
+    void *checkpoints, size_t checkpoint_bytes, void *clear, size_t clear_bytes, void *stream) {
+  return rasterize_forward_impl(tile_bounds_x, tile_bounds_y, img_height, img_width,
+                                gaussian_ids_sorted, tile_bins, xys, conics, colors, opacity,
+                                background, out_img, final_Ts, final_idx, num_intersects, chunk,
+                                checkpoints, checkpoint_bytes, clear, clear_bytes, stream,
+                                "rasterize_forward_clearing");
 }
 
 extern "C" int gsplat_rasterize_backward_chunked(

@@ -9,7 +9,8 @@ spherical_harmonics (:200) and rasterize_gaussians (:208) and clamps the image (
 `render_fused` computes the same image and the same six parameter gradients with
 
   forward:  gsplat_fused_preprocess_forward (activations + projection + SH + clamp, one
-            kernel) -> gsplat_bin_count / gsplat_bin_emit -> gsplat_rasterize_forward
+            kernel) -> gsplat_bin_count / gsplat_bin_emit -> gsplat_rasterize_forward_clearing
+            (the blend, which also zeroes the backward's per-Gaussian gradient records)
   backward: gsplat_rasterize_backward_records -> gsplat_fused_preprocess_backward (projection
             VJP + SH backward + the activations' chain rule, one kernel)
 
@@ -67,7 +68,7 @@ class _FusedRender(Function):
                   P(scales), P(quats), P(opacities), P(features_dc),
                   P(features_rest) if K > 1 else None, P(viewmat), P(projmat), P(campos),
                   float(fx), float(fy), float(cx), float(cy), H, W, tbx, tby, 0.01, P(xys),
-                  P(depths), P(radii), P(conics), P(nth), P(colors), P(opac), P(rec), None, None,
+                  P(depths), P(radii), P(conics), P(nth), P(colors), P(opac), None, None, None,
                   st)
         num_intersects, gids, bins = bin_gaussians(xys, depths, radii, nth, H, W)
         chunk, ckpt = 0, None
@@ -77,6 +78,8 @@ class _FusedRender(Function):
             out_img = torch.ones(H, W, 3, **f32) * background
             final_Ts = torch.ones(H, W, **f32)
             final_idx = torch.zeros(H, W, device=dev, dtype=torch.int32)
+            if rec is not None:
+                rec.zero_()
         else:
             out_img = torch.empty((H, W, 3), **f32)
             final_Ts = torch.empty((H, W), **f32)
@@ -87,14 +90,12 @@ class _FusedRender(Function):
                 ckpt = torch.empty((_lib.query("gsplat_rasterize_checkpoint_bytes", tbx, tby,
                                                num_intersects, chunk),),
                                    device=dev, dtype=torch.uint8)
-                _lib.call("gsplat_rasterize_forward_chunked", tbx, tby, H, W, P(gids), P(bins),
-                          P(xys), P(conics), P(colors), P(opac), P(background), P(out_img),
-                          P(final_Ts), P(final_idx), num_intersects, chunk, P(ckpt),
-                          ckpt.numel(), st)
-            else:
-                _lib.call("gsplat_rasterize_forward", tbx, tby, H, W, 3, P(gids), P(bins),
-                          P(xys), P(conics), P(colors), P(opac), P(background), P(out_img),
-                          P(final_Ts), P(final_idx), st)
+            # the blend kernel also clears the gradient records the backward accumulates into
+            _lib.call("gsplat_rasterize_forward_clearing", tbx, tby, H, W, P(gids), P(bins),
+                      P(xys), P(conics), P(colors), P(opac), P(background), P(out_img),
+                      P(final_Ts), P(final_idx), num_intersects, chunk, P(ckpt),
+                      ckpt.numel() if ckpt is not None else 0, P(rec),
+                      rec.numel() if rec is not None else 0, st)
         ctx.meta = (n, K, int(degrees_to_use), float(fx), float(fy), float(cx), float(cy), H, W,
                     tbx, tby, num_intersects, chunk)
         ctx.ckpt, ctx.rec = ckpt, rec

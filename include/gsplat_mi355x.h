@@ -193,6 +193,17 @@ int gsplat_rasterize_backward_chunked(
     const float *v_output_alpha, float alpha_max, float *v_xy, float *v_conic, float *v_colors,
     float *v_opacity, int64_t num_intersects, int chunk, const void *checkpoints,
     size_t checkpoint_bytes, void *workspace, size_t workspace_bytes, void *stream);
+/* The RGB forward (plain when chunk <= 0, chunked otherwise) that also clears
+ * `clear_bytes` (a multiple of 16) at `clear`: the fused training render hands it the
+ * per-Gaussian gradient records, which the blend kernel zeroes with the memory bandwidth its
+ * VALU-bound loop leaves idle (instead of the preprocess kernel spending ~18 us on it).
+ * Outputs equal gsplat_rasterize_forward(_chunked)'s. */
+int gsplat_rasterize_forward_clearing(
+    int tile_bounds_x, int tile_bounds_y, int img_height, int img_width,
+    const int32_t *gaussian_ids_sorted, const int32_t *tile_bins, const float *xys,
+    const float *conics, const float *colors, const float *opacity, const float *background,
+    float *out_img, float *final_Ts, int32_t *final_idx, int64_t num_intersects, int chunk,
+    void *checkpoints, size_t checkpoint_bytes, void *clear, size_t clear_bytes, void *stream);
 /* Debug: force the list-split chunk (> 0, rounded up to 64), disable it (< 0) or restore
  * the automatic choice (0). */
 int gsplat_debug_set_chunk(int chunk);
@@ -220,7 +231,8 @@ int gsplat_rasterize_backward(int tile_bounds_x, int tile_bounds_y, int img_heig
  * on the activated inputs), colors [N,3] (clamped SH colour; a colour the clamp raised from
  * below zero is stored as -0.0f so the backward knows it) and opacity [N] (sigmoid).  With
  * grad_records != NULL (gsplat_grad_records_bytes) it zeroes the record of every visible
- * Gaussian (radii > 0) for gsplat_rasterize_backward_records.  scales_out [N,3] / quats_out [N,4]
+ * Gaussian (radii > 0) for gsplat_rasterize_backward_records (the fused render passes NULL
+ * and lets gsplat_rasterize_forward_clearing clear them instead).  scales_out [N,3] / quats_out [N,4]
  * (optional, testing) receive the activated scales and normalised quaternions.
  * Backward reads the records and writes v_means3d [N,3], v_log_scales [N,3], v_quats [N,4],
  * v_opacity_logits [N] and either v_features_dc [N,3] + v_features_rest [N, sh_bases-1, 3],

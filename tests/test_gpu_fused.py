@@ -129,6 +129,56 @@ def test_fused_forward_bitexact_given_activations(gpu, case):
         assert torch.equal(mine, theirs), f"{name}: fused != caller path"
 
 
+@pytest.mark.parametrize("case", [CASES[0], CASES[1], CASES[6]])
+@pytest.mark.parametrize("chunked", [False, True])
+def test_forward_clearing_equals_forward_and_clears_records(gpu, case, chunked):
+    """gsplat_rasterize_forward_clearing: the blend's outputs are those of the plain (chunked)
+    forward, and the record buffer is all zero afterwards whatever it held."""
+    from gaussctrl_exp_amd.project_gaussians import project_gaussians
+    from gaussctrl_exp_amd.rasterize import bin_gaussians
+    sc, cam = _scene_cam(case)
+    n, W, H = case[:3]
+    d, c = sc.to(gpu), cam.to(gpu)
+    tb = cam.tile_bounds
+    with torch.no_grad():
+        xys, depths, radii, conics, nth, _ = project_gaussians(
+            d.means, torch.exp(d.scales), 1, d.quats / d.quats.norm(dim=-1, keepdim=True),
+            *c.project_args())
+    I, gids, bins = bin_gaussians(xys, depths, radii, nth, H, W)
+    assert I > 0
+    colors = torch.rand(n, 3, device=gpu)
+    opac = torch.rand(n, device=gpu)
+    bg = torch.tensor([0.2, 0.4, 0.6], device=gpu)
+    P, st = _lib.ptr, _lib.stream(gpu)
+    chunk = 64 if chunked else 0
+    ckpt = torch.empty(max(_lib.query("gsplat_rasterize_checkpoint_bytes", tb[0], tb[1], I,
+                                      chunk), 1), device=gpu, dtype=torch.uint8)
+    outs = []
+    for clear in (False, True):
+        img = torch.full((H, W, 3), float("nan"), device=gpu)
+        fT = torch.full((H, W), float("nan"), device=gpu)
+        fi = torch.full((H, W), -7, device=gpu, dtype=torch.int32)
+        if clear:
+            rec = torch.full((_lib.query("gsplat_grad_records_bytes", n),), 255, device=gpu,
+                             dtype=torch.uint8)
+            _lib.call("gsplat_rasterize_forward_clearing", tb[0], tb[1], H, W, P(gids), P(bins),
+                      P(xys), P(conics), P(colors), P(opac), P(bg), P(img), P(fT), P(fi), I,
+                      chunk, P(ckpt), ckpt.numel(), P(rec), rec.numel(), st)
+            torch.cuda.synchronize()
+            assert int(rec.count_nonzero()) == 0
+        else:
+            _lib.call("gsplat_rasterize_forward_chunked", tb[0], tb[1], H, W, P(gids), P(bins),
+                      P(xys), P(conics), P(colors), P(opac), P(bg), P(img), P(fT), P(fi), I,
+                      chunk, P(ckpt), ckpt.numel(), st)
+        outs.append((img, fT, fi))
+    for name, a, b in zip(("img", "final_Ts", "final_idx"), *outs):
+        assert torch.equal(a, b), name
+    with pytest.raises(RuntimeError):  # clear size must be a multiple of 16 bytes
+        _lib.call("gsplat_rasterize_forward_clearing", tb[0], tb[1], H, W, P(gids), P(bins),
+                  P(xys), P(conics), P(colors), P(opac), P(bg), P(img), P(fT), P(fi), I,
+                  chunk, P(ckpt), ckpt.numel(), P(rec), 24, st)
+
+
 def _run(sc, cam, deg, bg, gt, dev, mode, api=None):
     s = sc.to(dev).requires_grad_()
     c = cam.to(dev)
