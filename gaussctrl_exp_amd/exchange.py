@@ -46,6 +46,10 @@ class ShViewExchange:
         self.means: Optional[torch.Tensor] = None
         self.campos: Optional[torch.Tensor] = None
         self.handled = False  # set when this step's SH gradient went through the exchange
+        # the fused render's early all-reduce of the other four gradients (one flat buffer):
+        # (async work, {param data_ptr: expected grad data_ptr})
+        self.early = None
+        self.early_steps = 0  # steps that took the early all-reduce (tests)
 
     @contextlib.contextmanager
     def view(self, means: torch.Tensor, campos: torch.Tensor):
@@ -64,6 +68,7 @@ class ShViewExchange:
 
     def reset(self):
         self.handled = False
+        self.early = None
 
     def gather(self, v_colors: torch.Tensor) -> torch.Tensor:
         """All ranks' [v_colors (3N floats) | campos (3) | pad] records, [world, 3N + 4]."""
@@ -76,9 +81,20 @@ class ShViewExchange:
         return out.view(world, 3 * n + 4)
 
     def reduce(self, v_colors: torch.Tensor,
-               views_backward: Callable[[torch.Tensor, torch.Tensor], torch.Tensor]):
+               views_backward: Callable[[torch.Tensor, torch.Tensor], torch.Tensor],
+               early_flat: Optional[torch.Tensor] = None, early_map=None):
         """Summed coefficient gradient of all ranks' views.  `views_backward(means, views)`
-        evaluates sum_r Y(means - campos_r) (x) v_colors_r from the gathered records."""
+        evaluates sum_r Y(means - campos_r) (x) v_colors_r from the gathered records.
+
+        early_flat: the fused render's means/scales/quats/opacity gradients in one buffer.
+        Its all-reduce is issued (async) between the all-gather and the views kernel, so the
+        kernel runs while RCCL moves those 44 B per Gaussian; train.GradExchange then skips
+        the four parameters (early_map: which gradient storage each parameter must hold) and
+        waits for it."""
         views = self.gather(v_colors)
         self.handled = True
+        if early_flat is not None:
+            self.early = (dist.all_reduce(early_flat, op=dist.ReduceOp.SUM, group=self.group,
+                                          async_op=True), dict(early_map))
+            self.early_steps += 1
         return views_backward(self.means, views)

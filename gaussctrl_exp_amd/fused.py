@@ -101,6 +101,11 @@ class _FusedRender(Function):
         ctx.ckpt, ctx.rec = ckpt, rec
         ctx.opac_shape = opacities.shape
         ctx.exchange = exchange.active() if K > 1 else None
+        # data-parallel: all-reduce the four non-SH gradients from inside the backward (one flat
+        # buffer, overlapping the SH views kernel) when autograd will hand them over as the
+        # parameters' .grad (no gradient to accumulate into)
+        ctx.early = ctx.exchange is not None and all(
+            t.is_leaf and t.grad is None for t in (means, scales, quats, opacities))
         if adam is not None:
             if ctx.exchange is not None:
                 raise ValueError("render_fused: the in-backward Adam step is single-GPU only")
@@ -153,13 +158,21 @@ class _FusedRender(Function):
                       float(a["betas"][1]), float(a["eps"]), st)
             return (None,) * 20
         f32 = dict(device=dev, dtype=torch.float32)
-        v_means = torch.empty((n, 3), **f32)
-        v_scales = torch.empty((n, 3), **f32)
-        v_quats = torch.empty((n, 4), **f32)
-        v_opac = torch.empty((n, 1), **f32)
+        xchg = ctx.exchange
+        if xchg is not None and ctx.early:
+            flat = torch.empty((11 * n,), **f32)
+            v_means, v_scales = flat[:3 * n].view(n, 3), flat[3 * n:6 * n].view(n, 3)
+            v_quats, v_opac = flat[6 * n:10 * n].view(n, 4), flat[10 * n:].view(n, 1)
+            early = dict(flat=flat, map={p.data_ptr(): g.data_ptr() for p, g in zip(
+                (means, scales, quats, opacities), (v_means, v_scales, v_quats, v_opac))})
+        else:
+            v_means = torch.empty((n, 3), **f32)
+            v_scales = torch.empty((n, 3), **f32)
+            v_quats = torch.empty((n, 4), **f32)
+            v_opac = torch.empty((n, 1), **f32)
+            early = dict(flat=None, map=None)
         v_dc = torch.empty((n, 3), **f32)
         v_rest = torch.empty((n, K - 1, 3), **f32)
-        xchg = ctx.exchange
         v_colors = torch.empty((n, 3), **f32) if xchg is not None else None
         _lib.call("gsplat_fused_preprocess_backward", n, K, dtu, P(means), P(scales), P(quats),
                   P(viewmat), P(projmat), P(campos), fx, fy, cx, cy, H, W, P(radii), P(conics),
@@ -168,7 +181,8 @@ class _FusedRender(Function):
         if xchg is not None:
             v_dc, v_rest = xchg.reduce(
                 v_colors, lambda m, views: sh_backward_views_split(_DEG_OF_BASES[K], dtu, m,
-                                                                   views))
+                                                                   views),
+                early_flat=early["flat"], early_map=early["map"])
         return (v_means, v_scales, v_quats, v_opac.view(ctx.opac_shape), v_dc, v_rest) + \
             (None,) * 14
 

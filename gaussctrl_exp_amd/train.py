@@ -97,9 +97,20 @@ class GradExchange:
     def start(self):
         """Issue this step's all-reduces (async); returns the handles for finish()."""
         works = []
+        early = self.sh.early if self.sh is not None else None
+        if early is not None:
+            works.append(early[0])
         for p in self.params:
             if self.sh is not None and self.sh.handled and id(p) in self.sh_ids:
                 continue  # already summed over the ranks by the SH view exchange
+            if early is not None and p.data_ptr() in early[1]:
+                # all-reduced in place by the fused backward (exchange.ShViewExchange.reduce):
+                # autograd must have kept that buffer as the gradient
+                if p.grad is None or p.grad.data_ptr() != early[1][p.data_ptr()]:
+                    raise RuntimeError("GradExchange: a gradient the fused backward all-reduced "
+                                       "early is not the parameter's .grad (was it accumulated "
+                                       "into an existing gradient?)")
+                continue
             if p.grad is None:
                 p.grad = torch.zeros_like(p)
             works.append(dist.all_reduce(p.grad, op=dist.ReduceOp.SUM, group=self.group,

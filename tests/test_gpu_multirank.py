@@ -58,6 +58,8 @@ def _worker(rank, world, port, out_dir, mode):
     assert not t.fuse_adam  # multi-rank: the gradients must be summed before Adam
     t.step(_views(dev)[rank], _gt(rank, dev), background=bg, optimizer=False)
     np.save(os.path.join(out_dir, f"grad{rank}.npy"), t.flat_grad().cpu().numpy())
+    if mode == "sh_views":  # the four non-SH gradients went out early, from the fused backward
+        assert t.sh_exchange.early_steps == 1
     for _ in range(2):
         t.step(_views(dev)[rank], _gt(rank, dev), background=bg)
     np.save(os.path.join(out_dir, f"params{rank}.npy"),
