@@ -750,6 +750,40 @@ __global__ __launch_bounds__(TPB) void bin_edges_kernel(long long n, const K *__
   }
 }
 
+// The same for the fused binning's 32-bit tile keys, four keys per thread: one 16-B load,
+// the predecessor of the first from the neighbouring lane (lane 0 loads it).
+__global__ __launch_bounds__(TPB) void bin_edges4_kernel(long long n, const uint32_t *__restrict__ keys,
+                                                         int *__restrict__ bins, long long rows) {
+  const long long q = (long long)blockIdx.x * TPB + threadIdx.x;  // keys [4q, 4q + 4)
+  const long long k0 = 4 * q;
+  uint32_t v[4];
+  if (k0 + 3 < n) {
+    const uint4 w = *reinterpret_cast<const uint4 *>(keys + k0);
+    v[0] = w.x; v[1] = w.y; v[2] = w.z; v[3] = w.w;
+  } else {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = k0 + r < n ? keys[k0 + r] : 0u;
+  }
+  uint32_t prev = __shfl_up(v[3], 1, 64);
+  if ((threadIdx.x & 63) == 0 && k0 > 0 && k0 - 1 < n) prev = keys[k0 - 1];
+  if (k0 >= n) return;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const long long k = k0 + r;
+    if (k >= n) break;
+    const long long cur = (long long)(int32_t)v[r];
+    if (k == 0 && cur >= 0 && cur < rows) bins[2 * cur] = 0;
+    if (k == n - 1 && cur >= 0 && cur < rows) bins[2 * cur + 1] = (int)n;
+    if (k > 0) {
+      const long long pv = (long long)(int32_t)(r == 0 ? prev : v[r - 1]);
+      if (pv != cur) {
+        if (pv >= 0 && pv < rows) bins[2 * pv + 1] = (int)k;
+        if (cur >= 0 && cur < rows) bins[2 * cur] = (int)k;
+      }
+    }
+  }
+}
+
 // map_gaussian_to_intersects (gsplat layout: Gaussian-major, bbox row-major).
 __global__ __launch_bounds__(TPB) void map_intersects_kernel(
     int n, const float *__restrict__ xys, const float *__restrict__ depths,
@@ -949,7 +983,7 @@ extern "C" int gsplat_bin_emit(int num_points, int64_t num_intersects, int tile_
                      p1.off, p1.box, tile_bounds_x, tile_bounds_y, p2.tk_a, p2.tv_a, tile_bins);
   radix_sort_pairs<uint32_t>(p2.tk_a, p2.tv_a, p2.tk_b, p2.tv_b, p2.tk_s,
                              (uint32_t *)gaussian_ids_sorted, I, 0, bits_for(T), p2.rs_ws, st);
-  hipLaunchKernelGGL((bin_edges_kernel<uint32_t, 0>), dim3(cdiv(I, TPB)), dim3(TPB), 0, st, I,
+  hipLaunchKernelGGL(bin_edges4_kernel, dim3(cdiv(cdiv(I, 4), TPB)), dim3(TPB), 0, st, I,
                      p2.tk_s, tile_bins, T);
   return check_launch("bin_emit");
 }
