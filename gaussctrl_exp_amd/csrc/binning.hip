@@ -687,18 +687,13 @@ __global__ __launch_bounds__(TPB) void emit_kernel(int n, const uint32_t *__rest
   const long long p = p0 + lane;
   const bool in = p < n;
   uint32_t c = 0, g = 0, start = 0;
-  int x0 = 0, y0 = 0, bw = 1, area = 0;
+  uint2 b = make_uint2(0u, 0u);  // {x0 | y0 << 16, x1 | y1 << 16}: an empty box
   if (in) {
     c = cnt[p];
     start = off[p];
     if (c) {
       g = order[p];
-      const uint2 b = box[p];
-      x0 = (int)(b.x & 0xFFFFu);
-      y0 = (int)(b.x >> 16);
-      const int x1 = (int)(b.y & 0xFFFFu), y1 = (int)(b.y >> 16);
-      bw = max(x1 - x0, 1);
-      area = max(x1 - x0, 0) * max(y1 - y0, 0);
+      b = box[p];
     }
   }
   const uint32_t base = __shfl(start, 0, 64);
@@ -716,12 +711,20 @@ __global__ __launch_bounds__(TPB) void emit_kernel(int n, const uint32_t *__rest
       if (q + step <= 63 && rq <= j) q += step;
     }
     const uint32_t li = j - __shfl(rel, q, 64);
-    const int qx0 = __shfl(x0, q, 64), qy0 = __shfl(y0, q, 64), qbw = __shfl(bw, q, 64);
-    const int qarea = __shfl(area, q, 64);
+    // the owner's box (two shuffles of the packed corners) and id
+    const uint32_t b0 = __shfl(b.x, q, 64), b1 = __shfl(b.y, q, 64);
     const uint32_t qg = __shfl(g, q, 64);
+    const int qx0 = (int)(b0 & 0xFFFFu), qy0 = (int)(b0 >> 16);
+    const int qx1 = (int)(b1 & 0xFFFFu), qy1 = (int)(b1 >> 16);
+    const int qbw = max(qx1 - qx0, 1);
+    const int qarea = max(qx1 - qx0, 0) * max(qy1 - qy0, 0);
     uint32_t tile;
     if ((int)li < qarea) {
-      const int ly = (int)li / qbw;
+      // row = li / bw: (li + 0.5) / bw is at least 0.5 / bw from an integer, far more than
+      // the float quotient's error while li < 2^20; exact integer division beyond
+      const int ly = li < (1u << 20)
+                         ? (int)(((float)li + 0.5f) * __builtin_amdgcn_rcpf((float)qbw))
+                         : (int)li / qbw;
       tile = (uint32_t)((qy0 + ly) * tbx + qx0 + ((int)li - ly * qbw));
     } else {
       tile = (uint32_t)(tbx * tby);
