@@ -106,6 +106,9 @@ def algorithmic_bytes(N, I, P, T, K, nvis):
         # fused training render (csrc/preprocess.hip): raw params (56 + 12 (K-1) B) in,
         # projection + colour + opacity (48 B) out
         "gsplat_fused_preprocess_forward": (92 + 12 * K) * N,
+        # + the binning's depth key, id and 16-B record per Gaussian
+        "gsplat_fused_preprocess_forward_binned": (116 + 12 * K) * N,
+        "gsplat_bin_count_keyed": 8 * N,
         # its blend also zeroes the 48-B gradient record of every visible Gaussian
         "gsplat_rasterize_forward_clearing": 40 * I + 20 * P + 48 * nvis,
         "gsplat_rasterize_backward_records": 40 * I + 24 * P,
@@ -119,6 +122,7 @@ ENTRY_KERNELS = {
     "gsplat_rasterize_backward": ("raster_bwd", "split_grads_kernel"),
     "gsplat_rasterize_backward_records": ("raster_bwd",),
     "gsplat_fused_preprocess_forward": ("fused_fwd_kernel",),
+    "gsplat_fused_preprocess_forward_binned": ("fused_fwd_kernel",),
     "gsplat_fused_preprocess_backward": ("fused_bwd_kernel",),
     "gsplat_rasterize_forward": ("raster_fwd",),
     "gsplat_rasterize_forward_clearing": ("raster_fwd",),

@@ -71,6 +71,9 @@ SIGNATURES = {
                                        _P, _P, _P, _F, _P, _P, _P, _P, _P, _SZ, _P]),
     "gsplat_fused_preprocess_forward": (_I, [_I, _I, _I] + [_P] * 9 + [_F] * 4 +
                                         [_I] * 4 + [_F] + [_P] * 11),
+    "gsplat_fused_preprocess_forward_binned": (_I, [_I, _I, _I] + [_P] * 9 + [_F] * 4 +
+                                               [_I] * 4 + [_F] + [_P] * 8 + [_SZ, _P]),
+    "gsplat_bin_count_keyed": (_I, [_I, _I, _I, _P, _P, _SZ, _P]),
     "gsplat_fused_preprocess_backward": (_I, [_I, _I, _I] + [_P] * 6 + [_F] * 4 + [_I, _I] +
                                          [_P] * 13),
     "gsplat_fused_preprocess_backward_adam": (_I, [_I, _I, _I] + [_P] * 9 + [_F] * 4 +

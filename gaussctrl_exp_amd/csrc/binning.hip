@@ -879,6 +879,12 @@ Phase2 carve_phase2(void *base, long long I) {
 }
 
 }  // namespace
+
+BinKeys bin_keys_view(void *workspace1, int n) {
+  const Phase1 p = carve_phase1(workspace1, n);
+  return BinKeys{p.dkeys_a, p.dvals_a, p.rec, p.bytes};
+}
+
 }  // namespace gs
 
 using namespace gs;
@@ -907,10 +913,10 @@ extern "C" size_t gsplat_bin_emit_workspace_size(int64_t num_intersects) {
   return carve_phase2(nullptr, num_intersects).bytes;
 }
 
-extern "C" int gsplat_bin_count(int num_points, const float *xys, const float *depths,
-                                const int32_t *radii, const int32_t *num_tiles_hit,
-                                int tile_bounds_x, int tile_bounds_y, int32_t *d_counts,
-                                void *workspace1, size_t workspace1_bytes, void *stream) {
+static int bin_count_impl(int num_points, const float *xys, const float *depths,
+                          const int32_t *radii, const int32_t *num_tiles_hit, int tile_bounds_x,
+                          int tile_bounds_y, int32_t *d_counts, void *workspace1,
+                          size_t workspace1_bytes, bool keyed, void *stream) {
   hipStream_t st = (hipStream_t)stream;
   const long long T = (long long)tile_bounds_x * tile_bounds_y;
   if (num_points < 0 || tile_bounds_x <= 0 || tile_bounds_y <= 0 || tile_bounds_x > 65535 ||
@@ -931,13 +937,15 @@ extern "C" int gsplat_bin_count(int num_points, const float *xys, const float *d
   const int n = num_points;
   // depth keys + records; in reduce-then-scan mode also the sort's pass-0 tile counts
   const SortPlan sp = sort_plan(n, 0, 32);
-  const bool pre = g_sort_rts;
+  const bool pre = g_sort_rts && !keyed;  // keyed: the sort counts its first digit itself
   uint32_t *c0 = pre ? rts_tile_counts(p.rs_ws) : nullptr;
 #define DEPTH_KEYS(It)                                                                      \
   hipLaunchKernelGGL(depth_keys_kernel<It>, dim3((unsigned)sp.nblocks), dim3(TPB), 0, st, n, xys, \
                      depths, radii, num_tiles_hit, tile_bounds_x, tile_bounds_y, p.dkeys_a,    \
                      p.dvals_a, p.rec, c0, sp.nblocks, sort_err_word(p.rs_ws))
-  if (sp.items == 16) DEPTH_KEYS(16);
+  if (keyed) {
+    // keys, ids and records already written (gsplat_fused_preprocess_forward_binned)
+  } else if (sp.items == 16) DEPTH_KEYS(16);
   else if (sp.items == 8) DEPTH_KEYS(8);
   else DEPTH_KEYS(4);
 #undef DEPTH_KEYS
@@ -953,6 +961,21 @@ extern "C" int gsplat_bin_count(int num_points, const float *xys, const float *d
   hipLaunchKernelGGL(scan_downsweep_kernel, dim3(nb), dim3(TPB), 0, st, p.cnt, (long long)n,
                      partial, p.off);
   return check_launch("bin_count");
+}
+
+extern "C" int gsplat_bin_count(int num_points, const float *xys, const float *depths,
+                                const int32_t *radii, const int32_t *num_tiles_hit,
+                                int tile_bounds_x, int tile_bounds_y, int32_t *d_counts,
+                                void *workspace1, size_t workspace1_bytes, void *stream) {
+  return bin_count_impl(num_points, xys, depths, radii, num_tiles_hit, tile_bounds_x,
+                        tile_bounds_y, d_counts, workspace1, workspace1_bytes, false, stream);
+}
+
+extern "C" int gsplat_bin_count_keyed(int num_points, int tile_bounds_x, int tile_bounds_y,
+                                      int32_t *d_counts, void *workspace1,
+                                      size_t workspace1_bytes, void *stream) {
+  return bin_count_impl(num_points, nullptr, nullptr, nullptr, nullptr, tile_bounds_x,
+                        tile_bounds_y, d_counts, workspace1, workspace1_bytes, true, stream);
 }
 
 extern "C" int gsplat_bin_emit(int num_points, int64_t num_intersects, int tile_bounds_x,

@@ -135,4 +135,14 @@ __device__ __forceinline__ int wave_max_int(int v) {
   return v;
 }
 
+// The depth-sort inputs inside a gsplat_bin_count workspace (binning.hip): keys [n] (depth
+// bits, 0xFFFFFFFF culled), vals [n] (Gaussian ids) and the per-Gaussian binning record
+// {tile allotment, x0 | y0 << 16, x1 | y1 << 16, 0} [n].  `bytes` = the workspace size.
+struct BinKeys {
+  uint32_t *keys, *vals;
+  uint4 *rec;
+  size_t bytes;
+};
+BinKeys bin_keys_view(void *workspace1, int n);
+
 }  // namespace gs

@@ -54,6 +54,7 @@ struct FusedFwdArgs {
   float *colors, *opacity;
   float *records;                // NULL: no backward planned
   float *scales_out, *quats_out;  // debug (activated inputs), NULL normally
+  BinKeys bin;                    // bin.keys != NULL: also write the binning's sort inputs
 };
 
 struct FusedBwdArgs {
@@ -138,6 +139,20 @@ __global__ __launch_bounds__(sh_threads(K)) void fused_fwd_kernel(FusedFwdArgs a
     a.conics[3 * g + 1] = o.con[1];
     a.conics[3 * g + 2] = o.con[2];
     a.num_tiles_hit[g] = o.tiles;
+    if (a.bin.keys) {  // binning.hip depth_keys_kernel's outputs, from the registers
+      const bool vis = o.radius > 0;
+      a.bin.keys[g] = vis ? __float_as_uint(o.depth) : 0xFFFFFFFFu;
+      a.bin.vals[g] = (uint32_t)g;
+      const int c = vis ? o.tiles : 0;
+      uint4 q = {c > 0 ? (uint32_t)c : 0u, 0u, 0u, 0u};
+      if (c > 0) {
+        int x0, x1, y0, y1;
+        tile_bbox(o.xy[0], o.xy[1], (float)o.radius, pp.tbx, pp.tby, x0, x1, y0, y1);
+        q.y = (uint32_t)x0 | ((uint32_t)y0 << 16);
+        q.z = (uint32_t)x1 | ((uint32_t)y1 << 16);
+      }
+      a.bin.rec[g] = q;
+    }
     if (a.records && o.radius > 0) {  // only visible Gaussians receive raster atomics
       // the whole 64-B record (one full line: no partial-line read-modify-write)
       float4 *r = reinterpret_cast<float4 *>(a.records + g * RECF);
@@ -359,7 +374,7 @@ using namespace gs;
     default: hipLaunchKernelGGL(KERNEL<25>, grid, dim3(thr), smem, st, ARGS, pp); break;  \
   }
 
-extern "C" int gsplat_fused_preprocess_forward(
+static int fused_forward_impl(
     int num_points, int sh_bases, int degrees_to_use, const float *means3d,
     const float *log_scales, const float *quats, const float *opacity_logits,
     const float *features_dc, const float *features_rest, const float *viewmat,
@@ -367,7 +382,7 @@ extern "C" int gsplat_fused_preprocess_forward(
     int img_height, int img_width, int tile_bounds_x, int tile_bounds_y, float clip_thresh,
     float *xys, float *depths, int32_t *radii, float *conics, int32_t *num_tiles_hit,
     float *colors, float *opacity, void *grad_records, float *scales_out, float *quats_out,
-    void *stream) {
+    void *bin_workspace, size_t bin_workspace_bytes, void *stream) {
   const int K = sh_bases;
   if (num_points < 0 || !valid_bases(K) || degrees_to_use < 0 || degrees_to_use > degree_of(K) ||
       img_height <= 0 || img_width <= 0 || tile_bounds_x <= 0 || tile_bounds_y <= 0 ||
@@ -381,7 +396,15 @@ extern "C" int gsplat_fused_preprocess_forward(
   FusedFwdArgs args{num_points, degrees_to_use, means3d, log_scales, quats, opacity_logits,
                     features_dc, features_rest, viewmat, projmat, campos, xys, depths, radii,
                     conics, num_tiles_hit, colors, opacity, (float *)grad_records, scales_out,
-                    quats_out};
+                    quats_out, BinKeys{nullptr, nullptr, nullptr, 0}};
+  if (bin_workspace) {
+    args.bin = bin_keys_view(bin_workspace, num_points);
+    if (bin_workspace_bytes < args.bin.bytes || tile_bounds_x > 65535 || tile_bounds_y > 65535) {
+      set_error("fused_preprocess_forward_binned: binning workspace %zu < %zu bytes (or tiles "
+                "%dx%d)", bin_workspace_bytes, args.bin.bytes, tile_bounds_x, tile_bounds_y);
+      return 1;
+    }
+  }
   const ProjParams pp = make_proj_params(fx, fy, cx, cy, 1.f, clip_thresh, img_height,
                                          img_width, tile_bounds_x, tile_bounds_y);
   const int thr = sh_threads(K);
@@ -390,6 +413,43 @@ extern "C" int gsplat_fused_preprocess_forward(
   hipStream_t st = (hipStream_t)stream;
   FUSED_DISPATCH(fused_fwd_kernel, args);
   return check_launch("fused_preprocess_forward");
+}
+
+extern "C" int gsplat_fused_preprocess_forward(
+    int num_points, int sh_bases, int degrees_to_use, const float *means3d,
+    const float *log_scales, const float *quats, const float *opacity_logits,
+    const float *features_dc, const float *features_rest, const float *viewmat,
+    const float *projmat, const float *campos, float fx, float fy, float cx, float cy,
+    int img_height, int img_width, int tile_bounds_x, int tile_bounds_y, float clip_thresh,
+    float *xys, float *depths, int32_t *radii, float *conics, int32_t *num_tiles_hit,
+    float *colors, float *opacity, void *grad_records, float *scales_out, float *quats_out,
+    void *stream) {
+  return fused_forward_impl(num_points, sh_bases, degrees_to_use, means3d, log_scales, quats,
+                            opacity_logits, features_dc, features_rest, viewmat, projmat, campos,
+                            fx, fy, cx, cy, img_height, img_width, tile_bounds_x, tile_bounds_y,
+                            clip_thresh, xys, depths, radii, conics, num_tiles_hit, colors,
+                            opacity, grad_records, scales_out, quats_out, nullptr, 0, stream);
+}
+
+extern "C" int gsplat_fused_preprocess_forward_binned(
+    int num_points, int sh_bases, int degrees_to_use, const float *means3d,
+    const float *log_scales, const float *quats, const float *opacity_logits,
+    const float *features_dc, const float *features_rest, const float *viewmat,
+    const float *projmat, const float *campos, float fx, float fy, float cx, float cy,
+    int img_height, int img_width, int tile_bounds_x, int tile_bounds_y, float clip_thresh,
+    float *xys, float *depths, int32_t *radii, float *conics, int32_t *num_tiles_hit,
+    float *colors, float *opacity, void *bin_workspace, size_t bin_workspace_bytes,
+    void *stream) {
+  if (!bin_workspace) {
+    set_error("fused_preprocess_forward_binned: no binning workspace");
+    return 1;
+  }
+  return fused_forward_impl(num_points, sh_bases, degrees_to_use, means3d, log_scales, quats,
+                            opacity_logits, features_dc, features_rest, viewmat, projmat, campos,
+                            fx, fy, cx, cy, img_height, img_width, tile_bounds_x, tile_bounds_y,
+                            clip_thresh, xys, depths, radii, conics, num_tiles_hit, colors,
+                            opacity, nullptr, nullptr, nullptr, bin_workspace,
+                            bin_workspace_bytes, stream);
 }
 
 extern "C" int gsplat_fused_preprocess_backward(

@@ -8,8 +8,9 @@ or sigmoid(dc) (:203), sigmoid(opacities) (:215) -- then calls project_gaussians
 spherical_harmonics (:200) and rasterize_gaussians (:208) and clamps the image (:222).
 `render_fused` computes the same image and the same six parameter gradients with
 
-  forward:  gsplat_fused_preprocess_forward (activations + projection + SH + clamp, one
-            kernel) -> gsplat_bin_count / gsplat_bin_emit -> gsplat_rasterize_forward_clearing
+  forward:  gsplat_fused_preprocess_forward_binned (activations + projection + SH + clamp
+            + the binning's depth keys, one kernel) -> gsplat_bin_count_keyed /
+            gsplat_bin_emit -> gsplat_rasterize_forward_clearing
             (the blend, which also zeroes the backward's per-Gaussian gradient records)
   backward: gsplat_rasterize_backward_records -> gsplat_fused_preprocess_backward (projection
             VJP + SH backward + the activations' chain rule, one kernel)
@@ -64,13 +65,17 @@ class _FusedRender(Function):
         rec = torch.empty((max(_lib.query("gsplat_grad_records_bytes", n), 1),), device=dev,
                           dtype=torch.uint8) if need_grad else None
         P, st = _lib.ptr, _lib.stream(dev)
-        _lib.call("gsplat_fused_preprocess_forward", n, K, int(degrees_to_use), P(means),
+        # the preprocess kernel also writes the binning's depth-sort inputs into its workspace
+        ws1 = torch.empty((max(_lib.query("gsplat_bin_count_workspace_size", n), 1),),
+                          device=dev, dtype=torch.uint8)
+        _lib.call("gsplat_fused_preprocess_forward_binned", n, K, int(degrees_to_use), P(means),
                   P(scales), P(quats), P(opacities), P(features_dc),
                   P(features_rest) if K > 1 else None, P(viewmat), P(projmat), P(campos),
                   float(fx), float(fy), float(cx), float(cy), H, W, tbx, tby, 0.01, P(xys),
-                  P(depths), P(radii), P(conics), P(nth), P(colors), P(opac), None, None, None,
-                  st)
-        num_intersects, gids, bins = bin_gaussians(xys, depths, radii, nth, H, W)
+                  P(depths), P(radii), P(conics), P(nth), P(colors), P(opac), P(ws1),
+                  ws1.numel(), st)
+        num_intersects, gids, bins = bin_gaussians(xys, depths, radii, nth, H, W,
+                                                   keyed_workspace=ws1)
         chunk, ckpt = 0, None
         if num_intersects < 1:
             # nothing visible: the background (the caller returns it at gc_model.py:189-190),
@@ -269,12 +274,15 @@ def render_fused_eval(scene, cam: GCCamera, sh_degree_to_use: int, background: T
     radii = torch.empty((n,), device=dev, dtype=torch.int32)
     nth = torch.empty((n,), device=dev, dtype=torch.int32)
     P, st = _lib.ptr, _lib.stream(dev)
-    _lib.call("gsplat_fused_preprocess_forward", n, K, int(sh_degree_to_use), *[P(t) for t in
-              params[:5]], P(params[5]) if K > 1 else None, P(viewmat), P(projmat), P(campos),
-              float(cam.fx), float(cam.fy), float(cam.cx), float(cam.cy), H, W, tbx, tby, 0.01,
-              P(xys), P(depths), P(radii), P(conics), P(nth), P(colors), P(opac), None, None,
-              None, st)
-    num_intersects, gids, bins = bin_gaussians(xys, depths, radii, nth, H, W)
+    ws1 = torch.empty((max(_lib.query("gsplat_bin_count_workspace_size", n), 1),), device=dev,
+                      dtype=torch.uint8)
+    _lib.call("gsplat_fused_preprocess_forward_binned", n, K, int(sh_degree_to_use),
+              *[P(t) for t in params[:5]], P(params[5]) if K > 1 else None, P(viewmat),
+              P(projmat), P(campos), float(cam.fx), float(cam.fy), float(cam.cx), float(cam.cy),
+              H, W, tbx, tby, 0.01, P(xys), P(depths), P(radii), P(conics), P(nth), P(colors),
+              P(opac), P(ws1), ws1.numel(), st)
+    num_intersects, gids, bins = bin_gaussians(xys, depths, radii, nth, H, W,
+                                               keyed_workspace=ws1)
     if num_intersects < 1:  # nothing visible: the caller's early return (gc_model.py:189-190)
         return {"rgb": background.repeat(H, W, 1), "depth": None, "accumulation": None,
                 "xys": xys, "radii": radii}

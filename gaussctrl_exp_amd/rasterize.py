@@ -110,9 +110,11 @@ def _wait_count(host, dev, spin_s: float = 2.0) -> int:
 
 
 def bin_gaussians(xys: Tensor, depths: Tensor, radii: Tensor, num_tiles_hit: Tensor,
-                  img_height: int, img_width: int):
+                  img_height: int, img_width: int, keyed_workspace: Optional[Tensor] = None):
     """Fused on-device binning: (num_intersects, gaussian_ids_sorted [I] int32,
-    tile_bins [tiles, 2] int32).  Same order as gsplat's stable-sorted isect_ids."""
+    tile_bins [tiles, 2] int32).  Same order as gsplat's stable-sorted isect_ids.
+    keyed_workspace: a gsplat_bin_count workspace gsplat_fused_preprocess_forward_binned
+    already filled with the depth-sort inputs (the depth-key pass is skipped)."""
     n = xys.shape[0]
     tbx = (img_width + BLOCK_X - 1) // BLOCK_X
     tby = (img_height + BLOCK_Y - 1) // BLOCK_Y
@@ -125,14 +127,18 @@ def bin_gaussians(xys: Tensor, depths: Tensor, radii: Tensor, num_tiles_hit: Ten
     if n == 0:
         return 0, torch.empty((0,), device=dev, dtype=torch.int32), \
             torch.zeros((tbx * tby, 2), device=dev, dtype=torch.int32)
-    ws1 = torch.empty((_lib.query("gsplat_bin_count_workspace_size", n),), device=dev,
-                      dtype=torch.uint8)
     counts, host = _pinned_counts(dev)
     P, st = _lib.ptr, _lib.stream(dev)
     tile_bins = torch.empty((tbx * tby, 2), device=dev, dtype=torch.int32)
     host[1] = -1  # the previous call's value has been consumed (its wait completed)
-    _lib.call("gsplat_bin_count", n, P(xys), P(depths), P(radii), P(num_tiles_hit), tbx, tby,
-              P(counts), P(ws1), ws1.numel(), st)
+    if keyed_workspace is not None:
+        ws1 = keyed_workspace
+        _lib.call("gsplat_bin_count_keyed", n, tbx, tby, P(counts), P(ws1), ws1.numel(), st)
+    else:
+        ws1 = torch.empty((_lib.query("gsplat_bin_count_workspace_size", n),), device=dev,
+                          dtype=torch.uint8)
+        _lib.call("gsplat_bin_count", n, P(xys), P(depths), P(radii), P(num_tiles_hit), tbx,
+                  tby, P(counts), P(ws1), ws1.numel(), st)
     num_intersects = _wait_count(host, dev)
     gaussian_ids_sorted = torch.empty((max(num_intersects, 0),), device=dev, dtype=torch.int32)
     ws2 = torch.empty((_lib.query("gsplat_bin_emit_workspace_size", num_intersects),),

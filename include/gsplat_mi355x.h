@@ -134,6 +134,12 @@ int gsplat_bin_count(int num_points, const float *xys, const float *depths,
                      const int32_t *radii, const int32_t *num_tiles_hit, int tile_bounds_x,
                      int tile_bounds_y, int32_t *d_counts, void *workspace1,
                      size_t workspace1_bytes, void *stream);
+/* gsplat_bin_count for a workspace whose depth-sort inputs (depth keys, ids, per-Gaussian
+ * binning records) gsplat_fused_preprocess_forward_binned already wrote: the same outputs
+ * without reading xys/depths/radii/num_tiles_hit again. */
+int gsplat_bin_count_keyed(int num_points, int tile_bounds_x, int tile_bounds_y,
+                           int32_t *d_counts, void *workspace1, size_t workspace1_bytes,
+                           void *stream);
 int gsplat_bin_emit(int num_points, int64_t num_intersects, int tile_bounds_x,
                     int tile_bounds_y, int32_t *gaussian_ids_sorted, int32_t *tile_bins,
                     const void *workspace1, size_t workspace1_bytes, void *workspace2,
@@ -247,6 +253,19 @@ int gsplat_fused_preprocess_forward(
     int img_height, int img_width, int tile_bounds_x, int tile_bounds_y, float clip_thresh,
     float *xys, float *depths, int32_t *radii, float *conics, int32_t *num_tiles_hit,
     float *colors, float *opacity, void *grad_records, float *scales_out, float *quats_out,
+    void *stream);
+/* The forward above (no records, no debug outputs) that also writes the binning's depth-sort
+ * inputs into a gsplat_bin_count workspace (gsplat_bin_count_workspace_size(num_points)
+ * bytes), from the projection's registers; follow it with gsplat_bin_count_keyed on that
+ * workspace.  Saves the binning's depth-key pass over xys/depths/radii/num_tiles_hit. */
+int gsplat_fused_preprocess_forward_binned(
+    int num_points, int sh_bases, int degrees_to_use, const float *means3d,
+    const float *log_scales, const float *quats, const float *opacity_logits,
+    const float *features_dc, const float *features_rest, const float *viewmat,
+    const float *projmat, const float *campos, float fx, float fy, float cx, float cy,
+    int img_height, int img_width, int tile_bounds_x, int tile_bounds_y, float clip_thresh,
+    float *xys, float *depths, int32_t *radii, float *conics, int32_t *num_tiles_hit,
+    float *colors, float *opacity, void *bin_workspace, size_t bin_workspace_bytes,
     void *stream);
 int gsplat_fused_preprocess_backward(
     int num_points, int sh_bases, int degrees_to_use, const float *means3d,

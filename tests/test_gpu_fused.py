@@ -179,6 +179,49 @@ def test_forward_clearing_equals_forward_and_clears_records(gpu, case, chunked):
                   chunk, P(ckpt), ckpt.numel(), P(rec), 24, st)
 
 
+@pytest.mark.parametrize("case", [CASES[0], CASES[2], CASES[3], CASES[6]])
+def test_binned_forward_and_keyed_count_equal_the_separate_passes(gpu, case):
+    """gsplat_fused_preprocess_forward_binned + gsplat_bin_count_keyed: the same projection
+    outputs, intersection count, sorted ids and tile bins as the plain forward followed by the
+    binning's own depth-key pass (gsplat_bin_count)."""
+    from gaussctrl_exp_amd.rasterize import bin_gaussians
+    sc, cam = _scene_cam(case)
+    n, W, H, deg, dtu = case[:5]
+    d, c = sc.to(gpu), cam.to(gpu)
+    K = d.features_rest.shape[1] + 1
+    tb = cam.tile_bounds
+    campos = c.c2w[:3, 3].contiguous()
+    P, st = _lib.ptr, _lib.stream(gpu)
+    outs = []
+    for binned in (False, True):
+        f = lambda *s: torch.full(s, float("nan"), device=gpu)
+        o = dict(xys=f(n, 2), depths=f(n), conics=f(n, 3), colors=f(n, 3), opac=f(n),
+                 radii=torch.full((n,), -5, device=gpu, dtype=torch.int32),
+                 nth=torch.full((n,), -5, device=gpu, dtype=torch.int32))
+        head = (n, K, dtu, P(d.means), P(d.scales), P(d.quats), P(d.opacities),
+                P(d.features_dc), P(d.features_rest) if K > 1 else None, P(c.viewmat),
+                P(c.projmat), P(campos), cam.fx, cam.fy, cam.cx, cam.cy, H, W, tb[0], tb[1],
+                0.01, P(o["xys"]), P(o["depths"]), P(o["radii"]), P(o["conics"]), P(o["nth"]),
+                P(o["colors"]), P(o["opac"]))
+        if binned:
+            ws = torch.full((_lib.query("gsplat_bin_count_workspace_size", n),), 0xAB,
+                            device=gpu, dtype=torch.uint8)
+            _lib.call("gsplat_fused_preprocess_forward_binned", *head, P(ws), ws.numel(), st)
+            b = bin_gaussians(o["xys"], o["depths"], o["radii"], o["nth"], H, W,
+                              keyed_workspace=ws)
+        else:
+            _lib.call("gsplat_fused_preprocess_forward", *head, None, None, None, st)
+            b = bin_gaussians(o["xys"], o["depths"], o["radii"], o["nth"], H, W)
+        outs.append((o, b))
+    (o0, b0), (o1, b1) = outs
+    for k in o0:
+        assert torch.equal(o0[k], o1[k]), k
+    assert b0[0] == b1[0] > 0
+    assert torch.equal(b0[1], b1[1]) and torch.equal(b0[2], b1[2])
+    with pytest.raises(RuntimeError):  # a workspace too small for the depth-sort inputs
+        _lib.call("gsplat_fused_preprocess_forward_binned", *head, P(ws), 64, st)
+
+
 def _run(sc, cam, deg, bg, gt, dev, mode, api=None):
     s = sc.to(dev).requires_grad_()
     c = cam.to(dev)
