@@ -55,7 +55,7 @@ SIGNATURES = {
     "gsplat_rasterize_forward_chunked": (_I, [_I, _I, _I, _I] + [_P] * 10 + [_I64, _I, _P, _SZ,
                                                                              _P]),
     "gsplat_rasterize_forward_clearing": (_I, [_I, _I, _I, _I] + [_P] * 10 +
-                                          [_I64, _I, _P, _SZ, _P, _SZ, _P]),
+                                          [_I64, _I, _P, _SZ, _P, _SZ, _P, _P]),
     "gsplat_rasterize_backward_chunked": (_I, [_I, _I, _I, _I, _I] + [_P] * 11 + [_F] +
                                           [_P] * 4 + [_I64, _I, _P, _SZ, _P, _SZ, _P]),
     "gsplat_debug_set_chunk": (_I, [_I]),

@@ -353,7 +353,7 @@ __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
     const float *__restrict__ depths = nullptr, float *__restrict__ out_depth = nullptr,
     int chunk = 0, const int *__restrict__ ckpt_off = nullptr,
     float4 *__restrict__ ckpt = nullptr, float4 *__restrict__ zero = nullptr,
-    long long zero_n = 0) {
+    long long zero_n = 0, const int *__restrict__ zero_radii = nullptr) {
   // Side job: clear a buffer (the fused path's gradient records) with the memory bandwidth the
   // VALU-bound blend leaves idle -- a grid-stride sweep of coalesced 16-B stores, issued by each
   // wave as it finishes (issued first, the blend's first load wait would also wait for them:
@@ -361,7 +361,8 @@ __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
   auto clear_side_job = [&]() {
     for (long long k = (long long)blockIdx.x * 256 + threadIdx.x; k < zero_n;
          k += (long long)gridDim.x * 256)
-      zero[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (!zero_radii || zero_radii[k >> 2] > 0)  // 64-B records of visible Gaussians only
+        zero[k] = make_float4(0.f, 0.f, 0.f, 0.f);
   };
   const WaveRect R = wave_rect<PXL, COLS>(tbx, tby, H, W);
   if (!R.live) {  // wave-uniform
@@ -1678,12 +1679,14 @@ static int rasterize_forward_impl(int tile_bounds_x, int tile_bounds_y, int img_
                                   const float *background, float *out_img, float *final_Ts,
                                   int32_t *final_idx, int64_t num_intersects, int chunk,
                                   void *checkpoints, size_t checkpoint_bytes, void *zero,
-                                  size_t zero_bytes, void *stream, const char *who) {
+                                  size_t zero_bytes, const int32_t *zero_radii, void *stream,
+                                  const char *who) {
   hipStream_t st = (hipStream_t)stream;
   if (tile_bounds_x <= 0 || tile_bounds_y <= 0 || img_height <= 0 || img_width <= 0 ||
       (long long)tile_bounds_x * GS_BLOCK < img_width ||
       (long long)tile_bounds_y * GS_BLOCK < img_height || (chunk > 0 && chunk % 64) ||
-      num_intersects < 0 || zero_bytes % 16 || (zero_bytes && !zero)) {
+      num_intersects < 0 || zero_bytes % 16 || (zero_bytes && !zero) ||
+      (zero_radii && zero_bytes % 64)) {
     set_error("%s: bad sizes (tiles=%dx%d H=%d W=%d chunk=%d zero=%zu)", who, tile_bounds_x,
               tile_bounds_y, img_height, img_width, chunk, zero_bytes);
     return 1;
@@ -1704,7 +1707,7 @@ static int rasterize_forward_impl(int tile_bounds_x, int tile_bounds_y, int img_
                        dim3(256), 0, st, tile_bounds_x, tile_bounds_y, img_height, img_width,
                        gaussian_ids_sorted, (const int2 *)tile_bins, (const float2 *)xys,
                        conics, colors, opacity, background, out_img, final_Ts, final_idx,
-                       nullptr, nullptr, 0, nullptr, nullptr, (float4 *)zero, zn);
+                       nullptr, nullptr, 0, nullptr, nullptr, (float4 *)zero, zn, zero_radii);
     return check_launch(who);
   }
   const ChunkWs w = carve_chunk_ws(checkpoints, T, num_intersects, chunk);
@@ -1720,7 +1723,7 @@ static int rasterize_forward_impl(int tile_bounds_x, int tile_bounds_y, int img_
                      tile_bounds_y, img_height, img_width, gaussian_ids_sorted,
                      (const int2 *)tile_bins, (const float2 *)xys, conics, colors, opacity,
                      background, out_img, final_Ts, final_idx, nullptr, nullptr, chunk,
-                     w.ckpt_off, w.ckpt, (float4 *)zero, zn);
+                     w.ckpt_off, w.ckpt, (float4 *)zero, zn, zero_radii);
   return check_launch(who);
 }
 
@@ -1737,7 +1740,7 @@ extern "C" int gsplat_rasterize_forward_chunked(
   return rasterize_forward_impl(tile_bounds_x, tile_bounds_y, img_height, img_width,
                                 gaussian_ids_sorted, tile_bins, xys, conics, colors, opacity,
                                 background, out_img, final_Ts, final_idx, num_intersects, chunk,
-                                checkpoints, checkpoint_bytes, nullptr, 0, stream,
+                                checkpoints, checkpoint_bytes, nullptr, 0, nullptr, stream,
                                 "rasterize_forward_chunked");
 }
 
@@ -1746,12 +1749,13 @@ extern "C" int gsplat_rasterize_forward_clearing(
     const int32_t *gaussian_ids_sorted, const int32_t *tile_bins, const float *xys,
     const float *conics, const float *colors, const float *opacity, const float *background,
     float *out_img, float *final_Ts, int32_t *final_idx, int64_t num_intersects, int chunk,
-    void *checkpoints, size_t checkpoint_bytes, void *clear, size_t clear_bytes, void *stream) {
+    void *checkpoints, size_t checkpoint_bytes, void *clear, size_t clear_bytes,
+    const int32_t *clear_radii, void *stream) {
   return rasterize_forward_impl(tile_bounds_x, tile_bounds_y, img_height, img_width,
                                 gaussian_ids_sorted, tile_bins, xys, conics, colors, opacity,
                                 background, out_img, final_Ts, final_idx, num_intersects, chunk,
-                                checkpoints, checkpoint_bytes, clear, clear_bytes, stream,
-                                "rasterize_forward_clearing");
+                                checkpoints, checkpoint_bytes, clear, clear_bytes, clear_radii,
+                                stream, "rasterize_forward_clearing");
 }
 
 extern "C" int gsplat_rasterize_backward_chunked(

@@ -32,7 +32,7 @@ from torch.autograd import Function
 
 from . import _lib, exchange
 from .camera import GCCamera
-from .rasterize import BACKWARD_ALPHA_CLAMP, BLOCK_X, BLOCK_Y, bin_gaussians
+from .rasterize import BACKWARD_ALPHA_CLAMP, BLOCK_X, BLOCK_Y, bin_gaussians, last_num_visible
 
 _DEG_OF_BASES = {1: 0, 4: 1, 9: 2, 16: 3, 25: 4}
 
@@ -100,7 +100,11 @@ class _FusedRender(Function):
                       P(xys), P(conics), P(colors), P(opac), P(background), P(out_img),
                       P(final_Ts), P(final_idx), num_intersects, chunk, P(ckpt),
                       ckpt.numel() if ckpt is not None else 0, P(rec),
-                      rec.numel() if rec is not None else 0, st)
+                      rec.numel() if rec is not None else 0,
+                      # skip culled Gaussians' records when many are culled (real scenes);
+                      # at ~all visible the radii loads cost more than the stores they save
+                      P(radii) if rec is not None and last_num_visible(dev) < 0.9 * n else None,
+                      st)
         ctx.meta = (n, K, int(degrees_to_use), float(fx), float(fy), float(cx), float(cy), H, W,
                     tbx, tby, num_intersects, chunk)
         ctx.ckpt, ctx.rec = ckpt, rec

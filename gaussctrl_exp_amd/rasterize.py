@@ -88,6 +88,12 @@ def _pinned_counts(dev):
     return t
 
 
+def last_num_visible(dev) -> int:
+    """The visible-Gaussian count of this device's last bin_gaussians call (written by the
+    binning next to the intersection count; valid once that call has returned)."""
+    return int(_pinned_counts(dev)[1][0])
+
+
 def _wait_count(host, dev, spin_s: float = 2.0) -> int:
     """The single host sync of the binning (gsplat: cum_tiles_hit[-1].item()): the scan kernel
     writes the intersection count once, straight into pinned host memory, so the host polls

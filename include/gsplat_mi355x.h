@@ -203,13 +203,16 @@ int gsplat_rasterize_backward_chunked(
  * `clear_bytes` (a multiple of 16) at `clear`: the fused training render hands it the
  * per-Gaussian gradient records, which the blend kernel zeroes with the memory bandwidth its
  * VALU-bound loop leaves idle (instead of the preprocess kernel spending ~18 us on it).
- * Outputs equal gsplat_rasterize_forward(_chunked)'s. */
+ * With clear_radii != NULL the buffer is 64-B records and record g is cleared only when
+ * clear_radii[g] > 0 (the backward touches no other).  Outputs equal
+ * gsplat_rasterize_forward(_chunked)'s. */
 int gsplat_rasterize_forward_clearing(
     int tile_bounds_x, int tile_bounds_y, int img_height, int img_width,
     const int32_t *gaussian_ids_sorted, const int32_t *tile_bins, const float *xys,
     const float *conics, const float *colors, const float *opacity, const float *background,
     float *out_img, float *final_Ts, int32_t *final_idx, int64_t num_intersects, int chunk,
-    void *checkpoints, size_t checkpoint_bytes, void *clear, size_t clear_bytes, void *stream);
+    void *checkpoints, size_t checkpoint_bytes, void *clear, size_t clear_bytes,
+    const int32_t *clear_radii, void *stream);
 /* Debug: force the list-split chunk (> 0, rounded up to 64), disable it (< 0) or restore
  * the automatic choice (0). */
 int gsplat_debug_set_chunk(int chunk);

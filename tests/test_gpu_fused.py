@@ -163,9 +163,20 @@ def test_forward_clearing_equals_forward_and_clears_records(gpu, case, chunked):
                              dtype=torch.uint8)
             _lib.call("gsplat_rasterize_forward_clearing", tb[0], tb[1], H, W, P(gids), P(bins),
                       P(xys), P(conics), P(colors), P(opac), P(bg), P(img), P(fT), P(fi), I,
-                      chunk, P(ckpt), ckpt.numel(), P(rec), rec.numel(), st)
+                      chunk, P(ckpt), ckpt.numel(), P(rec), rec.numel(), None, st)
             torch.cuda.synchronize()
             assert int(rec.count_nonzero()) == 0
+            # visible-only clearing: culled Gaussians' records keep their bytes
+            rec.fill_(255)
+            img2 = torch.empty_like(img)
+            _lib.call("gsplat_rasterize_forward_clearing", tb[0], tb[1], H, W, P(gids), P(bins),
+                      P(xys), P(conics), P(colors), P(opac), P(bg), P(img2), P(fT), P(fi), I,
+                      chunk, P(ckpt), ckpt.numel(), P(rec), rec.numel(), P(radii), st)
+            r = rec.view(n, 64)
+            vis = radii > 0
+            assert (~vis).any() or n == int(vis.sum())
+            assert int(r[vis].count_nonzero()) == 0 and bool((r[~vis] == 255).all())
+            assert torch.equal(img2, img)
         else:
             _lib.call("gsplat_rasterize_forward_chunked", tb[0], tb[1], H, W, P(gids), P(bins),
                       P(xys), P(conics), P(colors), P(opac), P(bg), P(img), P(fT), P(fi), I,
@@ -176,7 +187,7 @@ def test_forward_clearing_equals_forward_and_clears_records(gpu, case, chunked):
     with pytest.raises(RuntimeError):  # clear size must be a multiple of 16 bytes
         _lib.call("gsplat_rasterize_forward_clearing", tb[0], tb[1], H, W, P(gids), P(bins),
                   P(xys), P(conics), P(colors), P(opac), P(bg), P(img), P(fT), P(fi), I,
-                  chunk, P(ckpt), ckpt.numel(), P(rec), 24, st)
+                  chunk, P(ckpt), ckpt.numel(), P(rec), 24, None, st)
 
 
 @pytest.mark.parametrize("case", [CASES[0], CASES[2], CASES[3], CASES[6]])
