@@ -44,6 +44,8 @@ SIGNATURES = {
     "gsplat_get_tile_bin_edges": (_I, [_I64, _P, _P, _I64, _P]),
     "gsplat_bin_count_workspace_size": (_SZ, [_I]),
     "gsplat_bin_emit_workspace_size": (_SZ, [_I64]),
+    "gsplat_bin_emit_workspace_size_for": (_SZ, [_I, _I64, _I, _I]),
+    "gsplat_debug_binning_scheme": (_I, [_I]),
     "gsplat_bin_count": (_I, [_I, _P, _P, _P, _P, _I, _I, _P, _P, _SZ, _P]),
     "gsplat_bin_emit": (_I, [_I, _I64, _I, _I, _P, _P, _P, _SZ, _P, _SZ, _P]),
     "gsplat_rasterize_forward": (_I, [_I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P,
@@ -63,6 +65,7 @@ SIGNATURES = {
     "gsplat_debug_sort_timing": (_I, [_P, _I]),
     "gsplat_debug_sort_scheme": (_I, [_I]),
     "gsplat_debug_sort_items": (_I, [_I]),
+    "gsplat_debug_wave_log": (_I, [_P]),
     "gsplat_l1_ssim_num_blocks": (_I, [_I, _I]),
     "gsplat_l1_ssim_forward": (_I, [_I, _I, _I, _P, _P, _P, _F, _I, _P, _P, _P, _P]),
     "gsplat_l1_ssim_backward": (_I, [_I, _I, _I, _P, _P, _P, _F, _I, _P, _P, _P, _P]),

@@ -807,6 +807,681 @@ __global__ __launch_bounds__(TPB) void map_intersects_kernel(
     }
 }
 
+// ------------------------------------------------------------------ bucket binning
+// The same output as the sorted scheme above (gsplat's order: by tile, then depth bits, then
+// Gaussian id) without any device-wide sort:
+//   phase 1  bk_totals / bk_finalize: I = sum of tile allotments, visible count (2 launches);
+//   phase 2  bk_count: per workgroup of BK_CHUNK Gaussians, an LDS histogram of the tile ids
+//              of their intersections (the emit kernel's coalesced expansion) -> M[w][tile];
+//            bk_scan: per tile, the exclusive prefix of M over workgroups; the last workgroup
+//              scans the tile totals -> tile starts and tile_bins;
+//            bk_place: the same expansion again, each intersection's Gaussian id stored at
+//              start[tile] + M[w][tile] + (LDS atomic rank) -- grouped by tile, unordered;
+//            bk_sort: one workgroup per tile sorts its list by (depth bits, id) with an LDS
+//              LSD radix sort (stable wave64 ballot-match ranking, digits whose value never
+//              changes inside the tile skipped); longer lists than LDS holds stream through
+//              a global ping-pong buffer.  Id ties (equal depth bits) are resolved by sorting
+//              the ids first (only when the tile has equal keys).
+// Replaces the N-key depth sort (4 passes), the emission and the I-key tile sort (2 passes):
+// 4 launches after the host read of I instead of 8, and 2 before it instead of 15.
+constexpr int BK_NT = 1024;               // threads of the bucket count / place / scan kernels
+constexpr int BK_CHUNK = 4096;            // Gaussians per bucket workgroup
+constexpr int BK_MAX_BUCKETS = 16448;     // tiles + 1 (sentinel bucket) held in LDS (~64 KB)
+constexpr int BS_ITEMS = 16;
+constexpr int BS_CAP = TPB * BS_ITEMS;    // list length sorted entirely in LDS
+
+// phase 1: per block, the sum of tile allotments and the number of visible Gaussians
+__global__ __launch_bounds__(TPB) void bk_totals_kernel(int n, const uint4 *__restrict__ rec,
+                                                        const uint32_t *__restrict__ dkeys,
+                                                        uint32_t *__restrict__ partial) {
+  __shared__ uint32_t lds[TPB / 64];
+  const long long base = (long long)blockIdx.x * SC_TILE;
+  uint32_t c = 0, v = 0;
+#pragma unroll
+  for (int k = 0; k < SC_ITEMS; ++k) {
+    const long long i = base + k * TPB + threadIdx.x;
+    if (i < n) {
+      c += rec[i].x;
+      v += dkeys[i] != 0xFFFFFFFFu;
+    }
+  }
+  uint32_t tc, tv;
+  block_exclusive_scan<TPB>(c, tc, lds);
+  block_exclusive_scan<TPB>(v, tv, lds);
+  if (threadIdx.x == 0) {
+    partial[2 * blockIdx.x] = tc;
+    partial[2 * blockIdx.x + 1] = tv;
+  }
+}
+
+// One workgroup: d_counts[0] = visible count, d_counts[1] = I (pinned host memory).
+__global__ __launch_bounds__(1024) void bk_finalize_kernel(int nb, const uint32_t *__restrict__ partial,
+                                                           int *__restrict__ d_counts) {
+  __shared__ uint32_t lds[16];
+  uint32_t c = 0, v = 0;
+  for (int i = threadIdx.x; i < nb; i += 1024) {
+    c += partial[2 * i];
+    v += partial[2 * i + 1];
+  }
+  uint32_t tc, tv;
+  block_exclusive_scan<1024>(c, tc, lds);
+  block_exclusive_scan<1024>(v, tv, lds);
+  if (threadIdx.x == 0) {
+    d_counts[0] = (int)tv;
+    __threadfence_system();
+    d_counts[1] = (int)tc;  // written last: the host polls this word
+  }
+}
+
+// The intersections of 64 consecutive Gaussians (one per lane), expanded cooperatively: the
+// wave's combined slot range is walked 64 slots at a time and f(tile, gaussian) is called for
+// each slot (tile = T for the padding of an allotment larger than its box, as emit_kernel).
+template <typename F>
+__device__ __forceinline__ void expand_wave(long long p, long long n, const uint4 *__restrict__ rec,
+                                            int tbx, int tby, F &&f) {
+  const int lane = threadIdx.x & 63;
+  uint32_t c = 0;
+  uint4 q = make_uint4(0u, 0u, 0u, 0u);
+  if (p < n) {
+    q = rec[p];
+    c = q.x;
+  }
+  // inclusive wave scan of the allotments
+  uint32_t inc = c;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t o = __shfl_up(inc, off, 64);
+    if (lane >= off) inc += o;
+  }
+  const uint32_t total = __shfl(inc, 63, 64);
+  const uint32_t rel = inc - c;  // exclusive start of this lane's slots
+  const uint32_t g = (uint32_t)p;
+  for (uint32_t j0 = 0; j0 < total; j0 += 64) {
+    const uint32_t j = j0 + lane;
+    // owner = the largest lane o with rel[o] <= j (a zero allotment after the owner starts past
+    // j; lanes past n start at total)
+    int o = 0;
+#pragma unroll
+    for (int step = 32; step >= 1; step >>= 1) {
+      const uint32_t ro = __shfl(rel, (o + step) & 63, 64);
+      if (o + step <= 63 && ro <= j) o += step;
+    }
+    const uint32_t li = j - __shfl(rel, o, 64);
+    const uint32_t b0 = __shfl(q.y, o, 64), b1 = __shfl(q.z, o, 64);
+    const uint32_t og = __shfl(g, o, 64);
+    const int qx0 = (int)(b0 & 0xFFFFu), qy0 = (int)(b0 >> 16);
+    const int qx1 = (int)(b1 & 0xFFFFu), qy1 = (int)(b1 >> 16);
+    const int qbw = max(qx1 - qx0, 1);
+    const int qarea = max(qx1 - qx0, 0) * max(qy1 - qy0, 0);
+    uint32_t tile;
+    if ((int)li < qarea) {
+      const int ly = li < (1u << 20)
+                         ? (int)(((float)li + 0.5f) * __builtin_amdgcn_rcpf((float)qbw))
+                         : (int)li / qbw;
+      tile = (uint32_t)((qy0 + ly) * tbx + qx0 + ((int)li - ly * qbw));
+    } else {
+      tile = (uint32_t)(tbx * tby);
+    }
+    if (j < total) f(tile, og);
+  }
+}
+
+__global__ __launch_bounds__(BK_NT) void bk_count_kernel(int n, const uint4 *__restrict__ rec, int tbx,
+                                                         int tby, int nbk, uint32_t *__restrict__ M,
+                                                         uint32_t *__restrict__ ctr) {
+  constexpr int NW = BK_NT / 64;
+  __shared__ uint32_t hist[BK_MAX_BUCKETS];
+  for (int i = threadIdx.x; i < nbk; i += BK_NT) hist[i] = 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *ctr = 0u;  // bk_scan's last-block counter
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const long long base = (long long)blockIdx.x * BK_CHUNK;
+  for (int r = 0; r < BK_CHUNK / (64 * NW); ++r) {
+    const long long p0 = base + (long long)(r * NW + wave) * 64;
+    if (p0 >= n) break;  // wave-uniform
+    expand_wave(p0 + lane, n, rec, tbx, tby,
+                [&](uint32_t tile, uint32_t) { atomicAdd(&hist[tile], 1u); });
+  }
+  __syncthreads();
+  uint32_t *col = M + (size_t)blockIdx.x * nbk;
+  for (int i = threadIdx.x; i < nbk; i += BK_NT) col[i] = hist[i];
+}
+
+// Bucket b = blockIdx.x * 64 + lane; wave v scans workgroup columns [v * cw, (v+1) * cw).
+__global__ __launch_bounds__(BK_NT) void bk_scan_kernel(int nbk, int nwg, uint32_t *__restrict__ M,
+                                                        uint32_t *__restrict__ tot,
+                                                        uint32_t *__restrict__ start,
+                                                        uint32_t *__restrict__ ctr, int T,
+                                                        int *__restrict__ tile_bins) {
+  constexpr int NW = BK_NT / 64;
+  __shared__ uint32_t seg[NW][64];
+  __shared__ uint32_t lds[NW];
+  __shared__ bool last;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int b = blockIdx.x * 64 + lane;
+  const int cw = (nwg + NW - 1) / NW;
+  const int w0 = min(wave * cw, nwg), w1 = min(w0 + cw, nwg);
+  uint32_t s = 0;
+  if (b < nbk) {
+    int w = w0;
+    for (; w + 8 <= w1; w += 8) {
+      uint32_t v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = M[(size_t)(w + u) * nbk + b];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; w < w1; ++w) s += M[(size_t)w * nbk + b];
+  }
+  seg[wave][lane] = s;
+  __syncthreads();
+  uint32_t run = 0, total = 0;
+#pragma unroll
+  for (int v = 0; v < NW; ++v) {
+    const uint32_t x = seg[v][lane];
+    if (v < wave) run += x;
+    total += x;
+  }
+  if (b < nbk) {
+    int w = w0;
+    for (; w + 8 <= w1; w += 8) {
+      uint32_t v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = M[(size_t)(w + u) * nbk + b];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        M[(size_t)(w + u) * nbk + b] = run;
+        run += v[u];
+      }
+    }
+    for (; w < w1; ++w) {
+      const uint32_t v = M[(size_t)w * nbk + b];
+      M[(size_t)w * nbk + b] = run;
+      run += v;
+    }
+    if (wave == 0) tot[b] = total;
+  }
+  // the last workgroup to finish scans the bucket totals (one device-scope fence per
+  // workgroup: on MI355X it writes back the XCD's L2, far too costly per wave)
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    last = atomicAdd(ctr, 1u) == gridDim.x - 1;
+    if (last) __threadfence();
+  }
+  __syncthreads();
+  if (!last) return;
+  uint32_t running = 0;
+  for (int c0 = 0; c0 < nbk; c0 += BK_NT) {
+    const int i = c0 + threadIdx.x;
+    const uint32_t v = i < nbk ? __hip_atomic_load(&tot[i], __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT)
+                               : 0u;
+    uint32_t t;
+    const uint32_t ex = running + block_exclusive_scan<BK_NT>(v, t, lds);
+    if (i < nbk) {
+      start[i] = ex;
+      if (i < T) {  // empty tiles stay (0, 0), as gsplat's zero-filled tile_bins
+        tile_bins[2 * i] = v ? (int)ex : 0;
+        tile_bins[2 * i + 1] = v ? (int)(ex + v) : 0;
+      }
+    }
+    running += t;
+  }
+}
+
+__global__ __launch_bounds__(BK_NT) void bk_place_kernel(int n, const uint4 *__restrict__ rec, int tbx,
+                                                         int tby, int nbk,
+                                                         const uint32_t *__restrict__ M,
+                                                         const uint32_t *__restrict__ start,
+                                                         uint32_t *__restrict__ ids) {
+  constexpr int NW = BK_NT / 64;
+  __shared__ uint32_t cur[BK_MAX_BUCKETS];
+  const uint32_t *col = M + (size_t)blockIdx.x * nbk;
+  for (int i = threadIdx.x; i < nbk; i += BK_NT) cur[i] = start[i] + col[i];
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const long long base = (long long)blockIdx.x * BK_CHUNK;
+  for (int r = 0; r < BK_CHUNK / (64 * NW); ++r) {
+    const long long p0 = base + (long long)(r * NW + wave) * 64;
+    if (p0 >= n) break;  // wave-uniform
+    expand_wave(p0 + lane, n, rec, tbx, tby, [&](uint32_t tile, uint32_t g) {
+      ids[atomicAdd(&cur[tile], 1u)] = g;
+    });
+  }
+}
+
+// ---- per-tile LSD radix sort (bk_sort_kernel) ----
+// ITEMS = 0: the MSD kernel's layout (key/val arrays of CAPX entries)
+template <int NT, int ITEMS>
+struct BsSmem {
+  static constexpr int MB = ITEMS ? 2 : 1024;  // MSD buckets (bs_msd_sort; unused by the LSD)
+  static constexpr int CAPX = ITEMS ? NT * ITEMS : 4096;
+  uint32_t key[CAPX];
+  uint32_t val[CAPX];
+  uint32_t wcnt[NT / 64][256];
+  uint32_t loc_off[256];
+  uint32_t base[256];
+  uint32_t scan_tmp[NT / 64];
+  uint32_t red, red2[3];
+  uint32_t mtab[2 * MB];  // MSD bucket counters / cursors and starts
+};
+
+// Stable rank, within the workgroup, of this thread's elements r < R (element index
+// wave * R * 64 + r * 64 + lane; the first nvalid elements are real) by their 8-bit digit
+// dg[r]: dst[r] = chunk-local destination.  Returns, in thread tid < 256, digit tid's count;
+// sm.loc_off holds the digits' exclusive scan.
+template <int NT, int ITEMS>
+__device__ __forceinline__ uint32_t bs_rank(const uint32_t (&dg)[ITEMS], int R, int nvalid,
+                                            uint32_t (&dst)[ITEMS], BsSmem<NT, ITEMS> &sm) {
+  constexpr int NW = NT / 64;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  for (int e = tid; e < NW * 256; e += NT) (&sm.wcnt[0][0])[e] = 0;
+  __syncthreads();
+  uint32_t rank[ITEMS];
+#pragma unroll
+  for (int r = 0; r < ITEMS; ++r) {
+    if (r >= R) break;  // wave-uniform
+    const int i = wave * R * 64 + r * 64 + lane;
+    const bool valid = i < nvalid;
+    const uint32_t d = dg[r];
+    unsigned long long peers = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const bool bit = (d >> b) & 1u;
+      const unsigned long long m = __ballot(bit);
+      peers &= bit ? m : ~m;
+    }
+    const int leader = valid ? (int)__builtin_ctzll(peers) : lane;
+    uint32_t old = 0;
+    if (valid && leader == lane) old = atomicAdd(&sm.wcnt[wave][d], (uint32_t)__popcll(peers));
+    old = __shfl(old, leader, 64);
+    rank[r] = old + (uint32_t)__popcll(peers & lt);
+  }
+  __syncthreads();
+  uint32_t cnt = 0;
+  if (tid < 256) {
+    uint32_t sacc = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      const uint32_t c = sm.wcnt[w][tid];
+      sm.wcnt[w][tid] = sacc;
+      sacc += c;
+    }
+    cnt = sacc;
+  }
+  {
+    uint32_t tot;
+    const uint32_t ex = block_exclusive_scan<NT>(cnt, tot, sm.scan_tmp);
+    if (tid < 256) sm.loc_off[tid] = ex;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < ITEMS; ++r) {
+    if (r >= R) break;
+    dst[r] = sm.loc_off[dg[r]] + sm.wcnt[wave][dg[r]] + rank[r];
+  }
+  return cnt;
+}
+
+template <int NT, int ITEMS>
+__device__ __forceinline__ uint32_t bs_block_reduce(uint32_t w, bool is_min, BsSmem<NT, ITEMS> &sm) {
+  const int tid = threadIdx.x, lane = tid & 63;
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const uint32_t o = __shfl_xor(w, off, 64);
+    w = is_min ? min(w, o) : (w | o);
+  }
+  __syncthreads();
+  if (tid == 0) sm.red = is_min ? 0xFFFFFFFFu : 0u;
+  __syncthreads();
+  if (lane == 0) {
+    if (is_min) atomicMin(&sm.red, w); else atomicOr(&sm.red, w);
+  }
+  __syncthreads();
+  return sm.red;
+}
+
+// Common case of the per-tile sort: one MSD step into MB buckets by the top bits of key - min
+// (unstable LDS scatter), then each element's rank inside its bucket by counting the smaller
+// (key, id) pairs there (equal pairs -- a Gaussian padded into the sentinel bucket more than
+// once -- ordered by scatter position).  Returns false, having written nothing to global memory,
+// when a bucket holds more than BS_MSD_MAXB elements (clustered depths): the LSD path then sorts.
+constexpr int BS_MSD_MAXB = 64;
+template <int NT, int ITEMS, int SI>
+__device__ bool bs_msd_sort(uint32_t s0, uint32_t L, const uint32_t *__restrict__ ids,
+                            const uint32_t *__restrict__ dkeys, uint32_t *__restrict__ out,
+                            BsSmem<NT, SI> &sm, unsigned long long *tl = nullptr) {
+  constexpr int MB = BsSmem<NT, SI>::MB;
+  auto stamp = [&](int k) {
+    if (tl && threadIdx.x == 0) tl[k] = __builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
+  constexpr int LOGMB = MB == 2048 ? 11 : MB == 1024 ? 10 : MB == 512 ? 9 : 8;
+  static_assert((1 << LOGMB) == MB, "MSD bucket count must be 256..2048");
+  const int tid = threadIdx.x;
+  uint32_t k[ITEMS], v[ITEMS], bk[ITEMS], pos[ITEMS];
+  uint32_t kmn = 0xFFFFFFFFu, kmx = 0u;
+#pragma unroll
+  for (int r = 0; r < ITEMS; ++r) {
+    const uint32_t i = tid + r * NT;
+    if (i < L) {
+      v[r] = ids[s0 + i];
+      k[r] = dkeys[v[r]];
+      kmn = min(kmn, k[r]);
+      kmx = max(kmx, k[r]);
+    }
+  }
+  if (tl) {  // force the loads for the timestamp
+    uint32_t acc = 0;
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) if (tid + r * NT < L) acc ^= k[r];
+    asm volatile("" ::"v"(acc));
+  }
+  stamp(1);
+  uint32_t *hist = sm.mtab, *bstart = sm.mtab + MB;
+  for (int e = tid; e < MB; e += NT) hist[e] = 0;
+  // min and max in one round: sm.red2 = {min k, min ~k}
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    kmn = min(kmn, (uint32_t)__shfl_xor(kmn, off, 64));
+    kmx = max(kmx, (uint32_t)__shfl_xor(kmx, off, 64));
+  }
+  if (tid == 0) {
+    sm.red2[0] = 0xFFFFFFFFu;
+    sm.red2[1] = 0u;
+  }
+  __syncthreads();
+  if ((tid & 63) == 0) {
+    atomicMin(&sm.red2[0], kmn);
+    atomicMax(&sm.red2[1], kmx);
+  }
+  __syncthreads();
+  const uint32_t kmin = sm.red2[0], kmax = sm.red2[1];
+  stamp(2);
+  const int bits = 32 - __builtin_clz((kmax - kmin) | 1u);
+  const int shift = bits > LOGMB ? bits - LOGMB : 0;
+#pragma unroll
+  for (int r = 0; r < ITEMS; ++r) {
+    if (tid + r * NT < L) {
+      bk[r] = (k[r] - kmin) >> shift;
+      atomicAdd(&hist[bk[r]], 1u);
+    }
+  }
+  __syncthreads();
+  stamp(3);
+  constexpr int PER = MB / NT;
+  uint32_t c[PER], sum = 0, mx = 0;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    c[j] = hist[tid * PER + j];
+    sum += c[j];
+    mx = max(mx, c[j]);
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) mx = max(mx, (uint32_t)__shfl_xor(mx, off, 64));
+  if (tid == 0) sm.red2[2] = 0u;
+  uint32_t tot;
+  uint32_t run = block_exclusive_scan<NT>(sum, tot, sm.scan_tmp);  // (barriers)
+  if ((tid & 63) == 0) atomicMax(&sm.red2[2], mx);
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    bstart[tid * PER + j] = run;
+    hist[tid * PER + j] = run;  // scatter cursor
+    run += c[j];
+  }
+  __syncthreads();
+  stamp(4);
+  if (sm.red2[2] > (uint32_t)BS_MSD_MAXB) return false;
+#pragma unroll
+  for (int r = 0; r < ITEMS; ++r) {
+    if (tid + r * NT < L) {
+      pos[r] = atomicAdd(&hist[bk[r]], 1u);
+      sm.key[pos[r]] = k[r];
+      sm.val[pos[r]] = v[r];
+    }
+  }
+  __syncthreads();
+  stamp(5);
+#pragma unroll
+  for (int r = 0; r < ITEMS; ++r) {
+    if (tid + r * NT < L) {
+      const uint32_t bs = bstart[bk[r]];
+      const uint32_t be = bk[r] + 1 < (uint32_t)MB ? bstart[bk[r] + 1] : L;
+      uint32_t rank = 0;
+      for (uint32_t j = bs; j < be; ++j) {
+        const uint32_t kj = sm.key[j], vj = sm.val[j];
+        rank += (kj < k[r]) || (kj == k[r] && (vj < v[r] || (vj == v[r] && j < pos[r])));
+      }
+      out[s0 + bs + rank] = v[r];
+    }
+  }
+  if (tl) {
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    stamp(6);
+  }
+  return true;
+}
+
+// The per-tile sort's common case (bs_msd_sort) for lists up to NT * ITEMS long; other lists
+// (longer, or with a crowded MSD bucket) are flagged in fail[] for bk_sort_kernel.
+template <int NT, int ITEMS>
+__global__ __launch_bounds__(NT) void bk_msd_kernel(int nbk, const uint32_t *__restrict__ start,
+                                                    const uint32_t *__restrict__ tot,
+                                                    const uint32_t *__restrict__ ids,
+                                                    const uint32_t *__restrict__ dkeys,
+                                                    uint32_t *__restrict__ out,
+                                                    uint32_t *__restrict__ fail,
+                                                    unsigned long long *__restrict__ tlog) {
+  __shared__ BsSmem<NT, 0> sm;
+  const int b = blockIdx.x;
+  const uint32_t s0 = start[b], L = tot[b];
+  bool ok = true;
+  if (L == 1) {
+    if (threadIdx.x == 0) out[s0] = ids[s0];
+  } else if (L > 1) {
+    ok = L <= (uint32_t)(NT * ITEMS) &&
+         bs_msd_sort<NT, ITEMS>(s0, L, ids, dkeys, out, sm, tlog ? tlog + 8 * b : nullptr);
+  }
+  if (threadIdx.x == 0) fail[b] = ok ? 0u : 1u;
+}
+
+// Sorts bucket b's list ids[start[b] .. start[b] + tot[b]) by (dkeys[id], id) into out, for
+// lists with lo <= length <= hi.  Digits are taken from key - (the list's smallest key), and
+// digits that never vary are skipped.  Up to NT * ITEMS elements stay in registers and LDS;
+// longer lists stream through (ka, va) / (kb, vb) at the list's offset in chunks of that size.
+// Equal keys: sorted by id first (LSD), then by key.
+template <int NT, int ITEMS>
+__global__ __launch_bounds__(NT) void bk_sort_kernel(int nbk, uint32_t lo, uint32_t hi,
+                                                     const uint32_t *__restrict__ start,
+                                                     const uint32_t *__restrict__ tot,
+                                                     const uint32_t *__restrict__ ids,
+                                                     const uint32_t *__restrict__ dkeys,
+                                                     uint32_t *__restrict__ out, uint32_t *ka,
+                                                     uint32_t *va, uint32_t *kb, uint32_t *vb,
+                                                     int dbg, const uint32_t *__restrict__ fail) {
+  constexpr int CAP = NT * ITEMS;
+  __shared__ BsSmem<NT, ITEMS> sm;
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  if (fail && !fail[b]) return;  // sorted by bk_msd_kernel
+  const uint32_t s0 = start[b], L = tot[b];
+  if (L < lo || L > hi || L == 0) return;
+  if (L == 1) {
+    if (tid == 0) out[s0] = ids[s0];
+    return;
+  }
+  if (L <= (uint32_t)CAP) {
+    const int R = (int)((L + NT - 1) / NT);  // rows per wave
+    if (dbg & 1) {  // timing ablation: copy only
+      for (uint32_t i = tid; i < L; i += NT) out[s0 + i] = ids[s0 + i];
+      return;
+    }
+    uint32_t k[ITEMS], v[ITEMS], dg[ITEMS], dst[ITEMS];
+    uint32_t kmn = 0xFFFFFFFFu;
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) {
+      if (r >= R) break;
+      const uint32_t i = wave * R * 64 + r * 64 + lane;
+      v[r] = i < L ? ids[s0 + i] : 0u;
+      k[r] = i < L ? dkeys[v[r]] : 0xFFFFFFFFu;
+      kmn = min(kmn, k[r]);
+    }
+    const uint32_t kmin = bs_block_reduce(kmn, true, sm);
+    uint32_t xv = 0;
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) {
+      if (r >= R) break;
+      if (wave * R * 64 + r * 64 + lane < (int)L) xv |= k[r] - kmin;
+    }
+    uint32_t keymask = 0, idmask = 0;
+    {
+      const uint32_t x = bs_block_reduce(xv, false, sm);
+      for (int d = 0; d < 4; ++d) keymask |= ((x >> (8 * d)) & 0xFFu) ? 1u << d : 0u;
+    }
+    if (dbg & 2) keymask = 0;  // timing ablation: loads, reductions and the tie check only
+    for (int phase = 0;; ++phase) {
+      // passes: id digits (idmask) then key digits (keymask), least significant first
+      for (int q = 0; q < 8; ++q) {
+        const bool by_id = q < 4;
+        const int d = q & 3;
+        if (!(((by_id ? idmask : keymask) >> d) & 1u)) continue;
+#pragma unroll
+        for (int r = 0; r < ITEMS; ++r) {
+          if (r >= R) break;
+          dg[r] = ((by_id ? v[r] : k[r] - kmin) >> (8 * d)) & 0xFFu;
+        }
+        bs_rank<NT, ITEMS>(dg, R, (int)L, dst, sm);
+#pragma unroll
+        for (int r = 0; r < ITEMS; ++r) {
+          if (r >= R) break;
+          if (wave * R * 64 + r * 64 + lane < (int)L) {
+            sm.key[dst[r]] = k[r];
+            sm.val[dst[r]] = v[r];
+          }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < ITEMS; ++r) {
+          if (r >= R) break;
+          const int i = wave * R * 64 + r * 64 + lane;
+          if (i < (int)L) {
+            k[r] = sm.key[i];
+            v[r] = sm.val[i];
+          }
+        }
+        __syncthreads();
+      }
+      if (phase == 1) break;
+      // in key order now: equal neighbours are id ties, which need the id digits first
+      uint32_t tie = 0;
+#pragma unroll
+      for (int r = 0; r < ITEMS; ++r) {
+        if (r >= R) break;
+        const int i = wave * R * 64 + r * 64 + lane;
+        if (i > 0 && i < (int)L && sm.key[i - 1] == k[r]) tie = 1;
+      }
+      if (!bs_block_reduce(tie, false, sm)) break;
+      uint32_t iv = 0;
+#pragma unroll
+      for (int r = 0; r < ITEMS; ++r) {
+        if (r >= R) break;
+        if (wave * R * 64 + r * 64 + lane < (int)L) iv |= v[r];
+      }
+      const uint32_t ix = bs_block_reduce(iv, false, sm);
+      for (int d = 0; d < 4; ++d) idmask |= ((ix >> (8 * d)) & 0xFFu) ? 1u << d : 0u;
+    }
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) {
+      if (r >= R) break;
+      const int i = wave * R * 64 + r * 64 + lane;
+      if (i < (int)L) out[s0 + i] = v[r];
+    }
+    return;
+  }
+  // long list: chunks of CAP through global memory, id digits always first
+  uint32_t kmn = 0xFFFFFFFFu, iv = 0;
+  for (uint32_t i = tid; i < L; i += NT) {
+    const uint32_t g = ids[s0 + i];
+    kmn = min(kmn, dkeys[g]);
+    iv |= g;
+  }
+  const uint32_t kmin = bs_block_reduce(kmn, true, sm);
+  uint32_t xv = 0;
+  for (uint32_t i = tid; i < L; i += NT) xv |= dkeys[ids[s0 + i]] - kmin;
+  const uint32_t x = bs_block_reduce(xv, false, sm);
+  const uint32_t ix = bs_block_reduce(iv, false, sm);
+  int npass = 0;
+  for (int d = 0; d < 4; ++d) npass += (((ix >> (8 * d)) & 0xFFu) != 0) + (((x >> (8 * d)) & 0xFFu) != 0);
+  if (npass == 0) {  // one Gaussian repeated (sentinel padding): already in order
+    for (uint32_t i = tid; i < L; i += NT) out[s0 + i] = ids[s0 + i];
+    return;
+  }
+  const uint32_t *srck = nullptr, *srcv = ids;  // the first pass gathers the keys
+  uint32_t *dk = ka, *dv = va;
+  int done = 0;
+  for (int q = 0; q < 8; ++q) {
+    const bool by_id = q < 4;
+    const int d = q & 3, shift = 8 * d;
+    if (!(((by_id ? ix : x) >> shift) & 0xFFu)) continue;
+    const bool final_pass = ++done == npass;
+    // digit histogram of the whole list -> digit bases
+    if (tid < 256) sm.base[tid] = 0;
+    __syncthreads();
+    for (uint32_t i = tid; i < L; i += NT) {
+      const uint32_t vv = srcv[s0 + i];
+      const uint32_t kk = srck ? srck[s0 + i] : dkeys[vv];
+      atomicAdd(&sm.base[((by_id ? vv : kk - kmin) >> shift) & 0xFFu], 1u);
+    }
+    __syncthreads();
+    {
+      const uint32_t c = tid < 256 ? sm.base[tid] : 0u;
+      uint32_t t;
+      const uint32_t ex = block_exclusive_scan<NT>(c, t, sm.scan_tmp);
+      if (tid < 256) sm.base[tid] = ex;
+    }
+    __syncthreads();
+    for (uint32_t c0 = 0; c0 < L; c0 += CAP) {
+      const int nv = (int)min((uint32_t)CAP, L - c0);
+      const int R = (nv + NT - 1) / NT;
+      uint32_t k[ITEMS], v[ITEMS], dg[ITEMS], dst[ITEMS];
+#pragma unroll
+      for (int r = 0; r < ITEMS; ++r) {
+        if (r >= R) break;
+        const int i = wave * R * 64 + r * 64 + lane;
+        v[r] = i < nv ? srcv[s0 + c0 + i] : 0u;
+        k[r] = i < nv ? (srck ? srck[s0 + c0 + i] : dkeys[v[r]]) : 0u;
+        dg[r] = ((by_id ? v[r] : k[r] - kmin) >> shift) & 0xFFu;
+      }
+      const uint32_t cnt = bs_rank<NT, ITEMS>(dg, R, nv, dst, sm);
+#pragma unroll
+      for (int r = 0; r < ITEMS; ++r) {
+        if (r >= R) break;
+        if (wave * R * 64 + r * 64 + lane < nv) {
+          const uint32_t pos = sm.base[dg[r]] + dst[r] - sm.loc_off[dg[r]];
+          if (final_pass) {
+            out[s0 + pos] = v[r];
+          } else {
+            dk[s0 + pos] = k[r];
+            dv[s0 + pos] = v[r];
+          }
+        }
+      }
+      __syncthreads();
+      if (tid < 256) sm.base[tid] += cnt;  // this chunk's count of digit tid
+      __syncthreads();
+    }
+    srck = dk;
+    srcv = dv;
+    dk = dk == ka ? kb : ka;
+    dv = dv == va ? vb : va;
+    __threadfence_block();
+    __syncthreads();
+  }
+}
+
 // ---- workspace layouts of the fused binning (phase 1 and phase 2 are separate buffers) ----
 constexpr size_t ALIGN = 256;
 inline size_t al(size_t x) { return (x + ALIGN - 1) / ALIGN * ALIGN; }
@@ -878,6 +1553,38 @@ Phase2 carve_phase2(void *base, long long I) {
   return p;
 }
 
+// bucket scheme, phase 2: M [nwg][nbk], tot/start [nbk], last-block counter, the grouped ids
+// and the long-list ping-pong buffers [I] each
+struct BkWs {
+  uint32_t *M, *tot, *start, *ctr, *fail, *ids, *ka, *va, *kb, *vb;
+  int nwg, nbk;
+  size_t bytes;
+};
+
+BkWs carve_bk(void *base, int n, long long I, long long T) {
+  BkWs w;
+  Carver c(base);
+  w.nwg = (int)cdiv(n > 0 ? n : 1, BK_CHUNK);
+  w.nbk = (int)(T + 1);
+  const size_t ii = (size_t)(I > 0 ? I : 1) * 4;
+  w.M = c.take<uint32_t>((size_t)w.nwg * w.nbk * 4);
+  w.tot = c.take<uint32_t>((size_t)w.nbk * 4);
+  w.start = c.take<uint32_t>((size_t)w.nbk * 4);
+  w.ctr = c.take<uint32_t>(4);
+  w.fail = c.take<uint32_t>((size_t)w.nbk * 4);
+  w.ids = c.take<uint32_t>(ii);
+  w.ka = c.take<uint32_t>(ii);
+  w.va = c.take<uint32_t>(ii);
+  w.kb = c.take<uint32_t>(ii);
+  w.vb = c.take<uint32_t>(ii);
+  w.bytes = c.off;
+  return w;
+}
+
+bool g_bucket = false;  // gsplat_debug_binning_scheme
+int g_bk_dbg = 0;      // gsplat_debug_binning_scheme(bucket | ablation bits << 1)
+bool use_bucket(long long T) { return g_bucket && T + 1 <= BK_MAX_BUCKETS; }
+
 }  // namespace
 
 BinKeys bin_keys_view(void *workspace1, int n) {
@@ -903,6 +1610,21 @@ extern "C" int gsplat_debug_sort_timing(void *buffer, int calls) {
   g_sort_timing = (unsigned long long *)buffer;
   g_sort_timing_calls = buffer ? calls : 0;
   return 0;
+}
+
+extern "C" int gsplat_debug_binning_scheme(int bucket) {
+  g_bucket = (bucket & 1) != 0;
+  g_bk_dbg = bucket >> 1;
+  return 0;
+}
+
+extern "C" size_t gsplat_bin_emit_workspace_size_for(int num_points, int64_t num_intersects,
+                                                     int tile_bounds_x, int tile_bounds_y) {
+  const size_t sorted = carve_phase2(nullptr, num_intersects).bytes;
+  const long long T = (long long)tile_bounds_x * tile_bounds_y;
+  if (num_points < 0 || num_intersects < 0 || T <= 0 || !use_bucket(T)) return sorted;
+  const size_t bk = carve_bk(nullptr, num_points, num_intersects, T).bytes;
+  return bk > sorted ? bk : sorted;
 }
 
 extern "C" size_t gsplat_bin_count_workspace_size(int num_points) {
@@ -935,6 +1657,23 @@ static int bin_count_impl(int num_points, const float *xys, const float *depths,
     return check_launch("bin_count");
   }
   const int n = num_points;
+  if (use_bucket(T)) {  // bucket scheme: depth keys + records, then I and the visible count
+    const SortPlan sp = sort_plan(n, 0, 32);
+#define DEPTH_KEYS0(It)                                                                     \
+  hipLaunchKernelGGL(depth_keys_kernel<It>, dim3((unsigned)sp.nblocks), dim3(TPB), 0, st, n, xys, \
+                     depths, radii, num_tiles_hit, tile_bounds_x, tile_bounds_y, p.dkeys_a,    \
+                     p.dvals_a, p.rec, nullptr, sp.nblocks, nullptr)
+    if (keyed) {
+    } else if (sp.items == 16) DEPTH_KEYS0(16);
+    else if (sp.items == 8) DEPTH_KEYS0(8);
+    else DEPTH_KEYS0(4);
+#undef DEPTH_KEYS0
+    const int nb = (int)cdiv(n, SC_TILE);
+    uint32_t *partial = (uint32_t *)p.rs_ws;
+    hipLaunchKernelGGL(bk_totals_kernel, dim3(nb), dim3(TPB), 0, st, n, p.rec, p.dkeys_a, partial);
+    hipLaunchKernelGGL(bk_finalize_kernel, dim3(1), dim3(1024), 0, st, nb, partial, d_counts);
+    return check_launch("bin_count");
+  }
   // depth keys + records; in reduce-then-scan mode also the sort's pass-0 tile counts
   const SortPlan sp = sort_plan(n, 0, 32);
   const bool pre = g_sort_rts && !keyed;  // keyed: the sort counts its first digit itself
@@ -993,6 +1732,39 @@ extern "C" int gsplat_bin_emit(int num_points, int64_t num_intersects, int tile_
     return 1;
   }
   Phase1 p1 = carve_phase1(const_cast<void *>(workspace1), num_points);
+  if (use_bucket(T)) {
+    const BkWs w = carve_bk(workspace2, num_points, num_intersects, T);
+    if (workspace1_bytes < p1.bytes || workspace2_bytes < w.bytes) {
+      set_error("bin_emit: workspaces %zu/%zu < %zu/%zu bytes (phase-2 size from "
+                "gsplat_bin_emit_workspace_size_for)", workspace1_bytes, workspace2_bytes,
+                p1.bytes, w.bytes);
+      return 1;
+    }
+    if (num_intersects == 0 || num_points == 0) {
+      note(hipMemsetAsync(tile_bins, 0, (size_t)T * 2 * sizeof(int32_t), st), "hipMemsetAsync");
+      return check_launch("bin_emit");
+    }
+    const int n = num_points;
+    hipLaunchKernelGGL(bk_count_kernel, dim3(w.nwg), dim3(BK_NT), 0, st, n, p1.rec, tile_bounds_x,
+                       tile_bounds_y, w.nbk, w.M, w.ctr);
+    hipLaunchKernelGGL(bk_scan_kernel, dim3(cdiv(w.nbk, 64)), dim3(BK_NT), 0, st, w.nbk, w.nwg, w.M,
+                       w.tot, w.start, w.ctr, (int)T, tile_bins);
+    hipLaunchKernelGGL(bk_place_kernel, dim3(w.nwg), dim3(BK_NT), 0, st, n, p1.rec, tile_bounds_x,
+                       tile_bounds_y, w.nbk, w.M, w.start, w.ids);
+    // MSD + bucket ranking for lists up to 4,096 long; then the LSD sort for the others (up to
+    // 4,096: 256 threads; longer: 1,024 threads, in LDS up to 14,336, then through the
+    // ping-pong buffers)
+    hipLaunchKernelGGL((bk_msd_kernel<TPB, 16>), dim3(w.nbk), dim3(TPB), 0, st, w.nbk, w.start,
+                       w.tot, w.ids, p1.dkeys_a, (uint32_t *)gaussian_ids_sorted, w.fail,
+                       g_sort_timing);
+    hipLaunchKernelGGL((bk_sort_kernel<TPB, 16>), dim3(w.nbk), dim3(TPB), 0, st, w.nbk, 0u,
+                       (uint32_t)(TPB * 16), w.start, w.tot, w.ids, p1.dkeys_a,
+                       (uint32_t *)gaussian_ids_sorted, w.ka, w.va, w.kb, w.vb, g_bk_dbg, w.fail);
+    hipLaunchKernelGGL((bk_sort_kernel<1024, 14>), dim3(w.nbk), dim3(1024), 0, st, w.nbk,
+                       (uint32_t)(TPB * 16 + 1), 0xFFFFFFFFu, w.start, w.tot, w.ids, p1.dkeys_a,
+                       (uint32_t *)gaussian_ids_sorted, w.ka, w.va, w.kb, w.vb, 0, w.fail);
+    return check_launch("bin_emit");
+  }
   Phase2 p2 = carve_phase2(workspace2, num_intersects);
   if (workspace1_bytes < p1.bytes || workspace2_bytes < p2.bytes) {
     set_error("bin_emit: workspaces %zu/%zu < %zu/%zu bytes", workspace1_bytes,

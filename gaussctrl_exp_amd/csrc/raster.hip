@@ -33,6 +33,7 @@
 #include "common.h"
 
 #include <algorithm>
+#include <type_traits>
 
 namespace gs {
 namespace {
@@ -187,6 +188,26 @@ struct WaveRect {
   int tile, j, i0;
   float rx0, rx1, ry0, ry1;
 };
+// Debug hook (gsplat_debug_wave_log): when set, the backward blend kernels record per wave
+// {start, end (s_memrealtime, 100 MHz), HW_ID, XCC_ID, work slot} into [waves][5] u64.
+__device__ unsigned long long *g_wave_log = nullptr;
+struct WaveLog {
+  unsigned long long t0;
+  __device__ __forceinline__ WaveLog() : t0(__builtin_amdgcn_s_memrealtime()) {}
+  __device__ __forceinline__ void done(int slot) const {
+    unsigned long long *log = g_wave_log;
+    if (log && (threadIdx.x & 63) == 0) {
+      const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+      const int w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+      log[5 * w + 0] = t0;
+      log[5 * w + 1] = t1;
+      log[5 * w + 2] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+      log[5 * w + 3] = (unsigned)__builtin_amdgcn_s_getreg((15 << 11) | 20);  // XCC_ID
+      log[5 * w + 4] = (unsigned)slot;
+    }
+  }
+};
+
 // XCD-aware block order (gsplat_debug_set_raster_variant flag 1024): the dispatcher deals
 // workgroups to the 8 XCDs round-robin, so consecutive blocks -- neighbouring tiles, which
 // stage largely the same Gaussians -- land on different L2s.  With the remap each XCD takes a
@@ -364,6 +385,7 @@ __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
       if (!zero_radii || zero_radii[k >> 2] > 0)  // 64-B records of visible Gaussians only
         zero[k] = make_float4(0.f, 0.f, 0.f, 0.f);
   };
+  const WaveLog wlog;
   const WaveRect R = wave_rect<PXL, COLS>(tbx, tby, H, W);
   if (!R.live) {  // wave-uniform
     clear_side_job();
@@ -480,6 +502,7 @@ __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
       if (DEPTH) out_depth[pix] = cd[k] + T[k] * 0.f;  // the depth render's zero background
     }
   }
+  wlog.done(tile);
   clear_side_job();
 }
 
@@ -741,6 +764,7 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
     ctile = item_tile[slot];
     cj = slot - item_off[ctile];
   }
+  const WaveLog wlog;
   const WaveRect R = wave_rect<PXL, COLS>(tbx, tby, H, W, ctile);
   if (!R.live) return;  // wave-uniform
   __shared__ GStage lds[4][64];
@@ -897,6 +921,241 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
     }
     wave_lds_sync();
   }
+  wlog.done(tile);
+}
+
+// ---------------------------------------------------------------- tile-wave backward
+// One wave per 16x16 tile.  Lane l holds column l & 15 and rows rg, rg+4 | rg+8, rg+12
+// (rg = l >> 4) as two float2 pixel pairs: pair 0 lies in the tile's top 16x8 half, pair 1 in
+// the bottom half.  Each staged Gaussian carries two cull bits (top / bottom half, each also
+// limited to that half's last contributing list position), and the blend of a pair runs only
+// when its half is touched (a wave-uniform branch).  The per-Gaussian fixed cost -- LDS read,
+// the nine partial sums, the reduce-scatter and the atomic -- is paid once per tile instead of
+// once per 16x8 strip, while the per-pixel work keeps the 16x8 cull (measured on the headline
+// scene: 191.5 staged Gaussians per tile against 293.2 strip iterations).
+//
+// Per pixel the blend drops two products and two selects of raster_bwd3p_kernel: for a
+// Gaussian with o <= alpha_max the alpha clamp cannot bind (vis <= 1 wherever sigma >= 0), so
+// alpha = o * vis and vis * v_alpha = (alpha * v_alpha) / o.  The lanes accumulate
+// alpha * v_alpha and its dy moments; the factors -o and 1/o are applied once per Gaussian
+// before the reduction.  A Gaussian with o > alpha_max takes the clamped form.
+struct __attribute__((aligned(16))) GStageB {
+  float x, y, ha, b;   // mean, 0.5*conic.a, conic.b
+  float hc, o, r, g;   // 0.5*conic.c, opacity, colour
+  float bl;
+  int idx;             // position in the tile's sorted list
+  int id;              // Gaussian id
+  int halves;          // bit 0: touches the top 16x8 half, bit 1: the bottom half
+};
+
+template <bool CHUNKED = false, int WPB = 4>
+__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(5, 8))) void
+raster_bwd4_kernel(
+    int tbx, int tby, int H, int W, const int *__restrict__ gids, const int2 *__restrict__ bins,
+    const float2 *__restrict__ xys, const float *__restrict__ conics,
+    const float *__restrict__ colors, const float *__restrict__ opacity,
+    const float *__restrict__ background, const float *__restrict__ final_Ts,
+    const int *__restrict__ final_idx, const float *__restrict__ v_out,
+    const float *__restrict__ v_out_alpha, float alpha_max, float *__restrict__ rec,
+    int chunk = 0, const int *__restrict__ item_off = nullptr,
+    const int *__restrict__ item_tile = nullptr, const int *__restrict__ ckpt_off = nullptr,
+    const float4 *__restrict__ ckpt = nullptr, const int *__restrict__ order = nullptr,
+    int *__restrict__ queue = nullptr) {
+  constexpr int PXL = 4, LROWS = 4;
+  const WaveLog wlog;
+  __shared__ GStageB lds[WPB][64];
+  const int nslots = CHUNKED ? item_off[tbx * tby] : tbx * tby;
+  // one work slot (tile, or list-split item) per wave; with a queue, waves are persistent and
+  // take further slots from it (first slots dealt in launch order, then queue + #waves)
+  int tile = -1;
+  auto run = [&](const int wslot) {
+  int ctile = wslot, cj = 0;
+  if (!CHUNKED && order && wslot < tbx * tby) ctile = order[wslot];
+  if (CHUNKED) {
+    ctile = item_tile[wslot];
+    cj = wslot - item_off[ctile];
+  }
+  const WaveRect R = wave_rect<PXL, 16>(tbx, tby, H, W, ctile);
+  if (!R.live) return;  // wave-uniform
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  tile = R.tile;
+  const int j = R.j, i0 = R.i0;
+  const float px = (float)j;
+  // the two halves' pixel-centre rectangles (the bottom one may lie below the image)
+  const float rx0 = R.rx0, rx1 = R.rx1;
+  const float ty0 = R.ry0, ty1 = fminf(R.ry0 + 7.f, R.ry1);
+  const float by0 = R.ry0 + 8.f, by1 = R.ry1;
+  const bool bottom_live = by0 <= by1;
+  const float bg0 = background[0], bg1 = background[1], bg2 = background[2];
+  f2 py[2], T[2], vr[2], vg[2], vb[2], q[2], Sb[2];
+  int binf[PXL];
+  int mb0 = -1, mb1 = -1;
+#pragma unroll
+  for (int k = 0; k < PXL; ++k) {
+    const int i = i0 + LROWS * k, p = k >> 1;
+    float Tf = 0.f, r = 0.f, g = 0.f, bl = 0.f, a = 0.f;
+    int bf = -1;
+    if (i < H && j < W) {
+      const int pix = i * W + j;
+      Tf = final_Ts[pix];
+      bf = final_idx[pix];
+      r = v_out[3 * pix];
+      g = v_out[3 * pix + 1];
+      bl = v_out[3 * pix + 2];
+      a = v_out_alpha ? v_out_alpha[pix] : 0.f;
+    }
+    const float qk = Tf * (a - (bg0 * r + bg1 * g + bg2 * bl));
+    if (k & 1) {
+      py[p].y = (float)i; T[p].y = Tf; vr[p].y = r; vg[p].y = g; vb[p].y = bl; q[p].y = qk;
+    } else {
+      py[p].x = (float)i; T[p].x = Tf; vr[p].x = r; vg[p].x = g; vb[p].x = bl; q[p].x = qk;
+    }
+    Sb[p] = (f2)0.f;
+    binf[k] = bf;
+    if (p == 0) mb0 = max(mb0, bf); else mb1 = max(mb1, bf);
+  }
+  const int2 range = bins[tile];
+  int lo = range.x, hi = range.y;
+  if (CHUNKED) {
+    const int len = range.y - range.x;
+    const int m = len > chunk ? (len + chunk - 1) / chunk : 1;
+    if (m > 1) {
+      lo = range.x + cj * chunk;
+      hi = min(lo + chunk, range.y);
+      if (cj < m - 1) {  // start from the checkpoint after this chunk
+        const size_t cb = (size_t)ckpt_off[tile] * (GS_BLOCK * GS_BLOCK);
+        const int oy = (tile / tbx) * GS_BLOCK, ox = (tile % tbx) * GS_BLOCK;
+#pragma unroll
+        for (int k = 0; k < PXL; ++k) {
+          const int i = i0 + LROWS * k, p = k >> 1;
+          if (i < H && j < W) {
+            const int lpix = (i - oy) * GS_BLOCK + (j - ox);
+            const float4 cj4 = ckpt[cb + (size_t)cj * (GS_BLOCK * GS_BLOCK) + lpix];
+            const float4 cf4 = ckpt[cb + (size_t)(m - 1) * (GS_BLOCK * GS_BLOCK) + lpix];
+            const float vr_ = (k & 1) ? vr[p].y : vr[p].x, vg_ = (k & 1) ? vg[p].y : vg[p].x,
+                        vb_ = (k & 1) ? vb[p].y : vb[p].x;
+            const float sb = (cf4.y - cj4.y) * vr_ + (cf4.z - cj4.z) * vg_ + (cf4.w - cj4.w) * vb_;
+            if (k & 1) { T[p].y = cj4.x; Sb[p].y = sb; } else { T[p].x = cj4.x; Sb[p].x = sb; }
+          }
+        }
+      }
+    }
+  }
+  mb0 = min(wave_max_int(mb0), hi - 1);
+  mb1 = min(wave_max_int(mb1), hi - 1);
+  const int slot = reduce9_slot();
+  const int last = max(mb0, mb1);
+  GStageB *stage = lds[wave];
+  for (int b = last; b >= lo; b -= 64) {
+    const int idx = b - lane;
+    int halves = 0;
+    GStageB s;
+    if (idx >= lo) {
+      const int g = gids[idx];
+      const float2 xy = xys[g];
+      const float a = conics[3 * g], bb = conics[3 * g + 1], c = conics[3 * g + 2];
+      const float o = opacity[g];
+      if (idx <= mb0 && touches_rect(xy.x, xy.y, a, bb, c, o, rx0, rx1, ty0, ty1)) halves = 1;
+      if (bottom_live && idx <= mb1 &&
+          touches_rect(xy.x, xy.y, a, bb, c, o, rx0, rx1, by0, by1))
+        halves |= 2;
+      if (halves) {
+        s.x = xy.x;
+        s.y = xy.y;
+        s.ha = 0.5f * a;
+        s.b = bb;
+        s.hc = 0.5f * c;
+        s.o = o;
+        s.r = colors[3 * g];
+        s.g = colors[3 * g + 1];
+        s.bl = colors[3 * g + 2];
+        s.idx = idx;
+        s.id = g;
+        s.halves = halves | (o <= alpha_max ? 0 : 4);
+      }
+    }
+    const unsigned long long kmask = __ballot(halves != 0);
+    if (halves) stage[lanes_below(kmask)] = s;
+    const int n = __popcll(kmask);
+    wave_lds_sync();
+    for (int t = 0; t < n; ++t) {
+      const GStageB G = stage[t];
+      // bits 0/1: halves touched; bit 2: o > alpha_max (the clamped form)
+      const int hv = __builtin_amdgcn_readfirstlane(G.halves);
+      const float dx = G.x - px;
+      const float hA = G.ha * dx * dx, bdx = G.b * dx;
+      f2 sr = 0.f, sg = 0.f, sb = 0.f, sa = 0.f, Vy = 0.f, Vyy = 0.f;
+      bool any = false;
+      // one pixel pair: sa accumulates o * vis * v_alpha (the unclamped alpha times v_alpha)
+      auto pair = [&](auto clamped, int p, int k0) {
+        constexpr bool CL = decltype(clamped)::value;
+        const f2 dy = G.y - py[p];
+        const f2 sig = gs_sigma2v<f2>(G.hc, bdx, hA, dy);
+        const f2 vis = gs_vis2v<f2>(sig);
+        const f2 ov = G.o * vis;
+        f2 al = ov;
+        if constexpr (CL) al = (f2){fminf(alpha_max, ov.x), fminf(alpha_max, ov.y)};
+        const bool v0 = G.idx <= binf[k0] && sig.x >= 0.f && al.x >= ALPHA_MIN;
+        const bool v1 = G.idx <= binf[k0 + 1] && sig.y >= 0.f && al.y >= ALPHA_MIN;
+        any = any || v0 || v1;
+        const f2 am = {v0 ? al.x : 0.f, v1 ? al.y : 0.f};
+        f2 ovm = am;
+        if constexpr (CL) ovm = (f2){v0 ? ov.x : 0.f, v1 ? ov.y : 0.f};
+        const f2 om = 1.f - am;
+        const f2 ra = {__builtin_amdgcn_rcpf(om.x), __builtin_amdgcn_rcpf(om.y)};
+        T[p] = T[p] * ra;
+        const f2 fac = am * T[p];
+        sr = vfma(fac, vr[p], sr);
+        sg = vfma(fac, vg[p], sg);
+        sb = vfma(fac, vb[p], sb);
+        const f2 gv = vfma((f2)G.r, vr[p], vfma((f2)G.g, vg[p], G.bl * vb[p]));
+        const f2 v_alpha = vfma(gv, T[p], ra * (q[p] - Sb[p]));
+        Sb[p] = vfma(fac, gv, Sb[p]);
+        const f2 va = ovm * v_alpha;
+        sa += va;
+        const f2 vady = va * dy;
+        Vy += vady;
+        Vyy = vfma(vady, dy, Vyy);
+      };
+      using F = std::integral_constant<bool, false>;
+      using Tr = std::integral_constant<bool, true>;
+      if (hv & 4) {
+        if (hv & 1) pair(Tr{}, 0, 0);
+        if (hv & 2) pair(Tr{}, 1, 2);
+      } else {
+        if (hv & 1) pair(F{}, 0, 0);
+        if (hv & 2) pair(F{}, 1, 2);
+      }
+      if (__any(any)) {
+        const float Sa = sa.x + sa.y;
+        const float Vs = -Sa, Vys = -(Vy.x + Vy.y);
+        const float dxV = dx * Vs;
+        float parts[9];
+        parts[0] = fmaf(2.f * G.ha, dxV, G.b * Vys);  // v_x
+        parts[1] = fmaf(G.b, dxV, 2.f * G.hc * Vys);  // v_y
+        parts[2] = dx * dxV;                          // 2 v_conic.a
+        parts[3] = dx * Vys;                          // 2 v_conic.b
+        parts[4] = -(Vyy.x + Vyy.y);                  // 2 v_conic.c
+        parts[5] = sr.x + sr.y;
+        parts[6] = sg.x + sg.y;
+        parts[7] = sb.x + sb.y;
+        parts[8] = Sa * __builtin_amdgcn_rcpf(G.o);  // v_opacity = sum vis * v_alpha
+        const float v = reduce9(parts);
+        if (slot >= 0) atomicAdd(rec + (size_t)G.id * REC + slot, v);
+      }
+    }
+    wave_lds_sync();
+  }
+  };
+  const int nw = gridDim.x * WPB;
+  for (int wslot = block_slot() * WPB + (threadIdx.x >> 6); wslot < nslots;) {
+    run(wslot);
+    if (!queue) break;
+    int v = 0;
+    if ((threadIdx.x & 63) == 0) v = atomicAdd(queue, 1);
+    wslot = nw + __builtin_amdgcn_readfirstlane(v);
+  }
+  wlog.done(tile);
 }
 
 // ---------------------------------------------------------------- grouped backward
@@ -1126,6 +1385,50 @@ __global__ __launch_bounds__(256) void raster_bwd3g_kernel(
     }
     wave_lds_sync();
   }
+}
+
+// Tile processing order (one workgroup): tiles by decreasing list length, ties by tile id.
+// The backward deals consecutive work slots to CUs round-robin, so each SIMD receives one tile
+// from every cost tier and the per-SIMD sums even out (longest-processing-time-first dealing).
+// Keys (log2-spaced length bucket, tile) are sorted by an LDS bitonic sort; frames with more
+// than 16,384 tiles keep the identity order.
+constexpr int ORDER_MAX = 16384;
+__global__ __launch_bounds__(1024) void tile_order_kernel(int T, const int2 *__restrict__ bins,
+                                                          int *__restrict__ order) {
+  __shared__ uint32_t key[ORDER_MAX];
+  const int tid = threadIdx.x;
+  if (T > ORDER_MAX) {
+    for (int t = tid; t < T; t += 1024) order[t] = t;
+    return;
+  }
+  int n = 1;
+  while (n < T) n <<= 1;
+  for (int t = tid; t < n; t += 1024) {
+    uint32_t k = 0xFFFFFFFFu;  // padding sorts last
+    if (t < T) {
+      const int2 r = bins[t];
+      const int len = max(r.y - r.x, 0);
+      const uint32_t b = min(1023u, (uint32_t)(log2f((float)len + 1.f) * 64.f));
+      k = ((1023u - b) << 18) | (uint32_t)t;  // descending length, ascending tile
+    }
+    key[t] = k;
+  }
+  __syncthreads();
+  for (int size = 2; size <= n; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = tid; i < (n >> 1); i += 1024) {
+        const int lo = 2 * i - (i & (stride - 1)), hi = lo + stride;
+        const bool up = (lo & size) == 0;
+        const uint32_t a = key[lo], b = key[hi];
+        if ((a > b) == up) {
+          key[lo] = b;
+          key[hi] = a;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int t = tid; t < T; t += 1024) order[t] = (int)(key[t] & 0x3FFFFu);
 }
 
 // List-split plan (one workgroup): per tile, the number of backward items (chunks of the
@@ -1445,8 +1748,8 @@ static ChunkWs carve_chunk_ws(void *base, long long T, long long I, int chunk) {
   w.bytes = off;
   return w;
 }
-static bool default_variants() {
-  return g_fwd_pxl == FWD_PXL && g_bwd_pxl == BWD_PXL && g_bwd_flags == 0;
+static bool default_variants() {  // (flag 4096, the tile-wave backward, keeps the layout)
+  return g_fwd_pxl == FWD_PXL && g_bwd_pxl == BWD_PXL && (g_bwd_flags & ~4096) == 0;
 }
 
 extern "C" int gsplat_rasterize_chunk_size(int tile_bounds_x, int tile_bounds_y,
@@ -1575,6 +1878,15 @@ extern "C" int gsplat_debug_set_raster_variant(int fwd_pxl, int bwd_pxl, int bwd
   return 0;
 }
 
+extern "C" int gsplat_debug_wave_log(void *buffer) {
+  unsigned long long *p = (unsigned long long *)buffer;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_wave_log), &p, sizeof(p)) != hipSuccess) {
+    set_error("debug_wave_log: hipMemcpyToSymbol failed");
+    return 1;
+  }
+  return 0;
+}
+
 extern "C" size_t gsplat_rasterize_backward_workspace_size(int num_points, int channels) {
   return channels == 3 && num_points > 0 ? (size_t)num_points * REC * sizeof(float) : 0;
 }
@@ -1644,7 +1956,45 @@ extern "C" int gsplat_rasterize_backward(int tile_bounds_x, int tile_bounds_y, i
                              gaussian_ids_sorted, (const int2 *)tile_bins, (const float2 *)xys,
                              conics, colors, opacity, background, final_Ts, final_idx, v_output,
                              v_output_alpha, alpha_max, rec, (g_bwd_flags & 64) != 0);
-        } else { if (atomics) BWD3P(1, true, 16); else BWD3P(1, false, 16); }
+        } else if (atomics && (g_bwd_flags & 4096)) {  // ablation: one wave per tile
+          if (g_bwd_flags & 8192)
+            hipLaunchKernelGGL((raster_bwd4_kernel<false, 1>), dim3(T), dim3(64), 0, st,
+                               tile_bounds_x, tile_bounds_y, img_height, img_width,
+                               gaussian_ids_sorted, (const int2 *)tile_bins, (const float2 *)xys,
+                               conics, colors, opacity, background, final_Ts, final_idx, v_output,
+                               v_output_alpha, alpha_max, rec);
+          else {
+            const int *ord = nullptr;
+            if (g_bwd_flags & 16384) {
+              static int *buf = nullptr;
+              static int cap = 0;
+              if (cap < T) {
+                if (buf) (void)hipFree(buf);
+                note(hipMalloc(&buf, (size_t)T * sizeof(int)), "hipMalloc");
+                cap = T;
+              }
+              hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, st, T,
+                                 (const int2 *)tile_bins, buf);
+              ord = buf;
+            }
+            int *queue = nullptr;
+            unsigned grid = cdiv(T, 4);
+            const int pw = (g_bwd_flags >> 15) & 7;  // persistent waves per SIMD (0: off)
+            if (pw && (unsigned)(256 * pw) < grid) {
+              static int *qbuf = nullptr;
+              if (!qbuf) note(hipMalloc(&qbuf, sizeof(int)), "hipMalloc");
+              note(hipMemsetAsync(qbuf, 0, sizeof(int), st), "hipMemsetAsync");
+              queue = qbuf;
+              grid = 256 * pw;
+            }
+            hipLaunchKernelGGL((raster_bwd4_kernel<false>), dim3(grid), dim3(256), 0, st,
+                               tile_bounds_x, tile_bounds_y, img_height, img_width,
+                               gaussian_ids_sorted, (const int2 *)tile_bins, (const float2 *)xys,
+                               conics, colors, opacity, background, final_Ts, final_idx, v_output,
+                               v_output_alpha, alpha_max, rec, 0, nullptr, nullptr, nullptr,
+                               nullptr, ord, queue);
+          }
+        } else { if (atomics) BWD3P(1, true, 16); else BWD3P(1, false, 16); }  // 16x8 strips
       }
     } else if (g_bwd_pxl == 4) { if (atomics) BWD3(4, true); else BWD3(4, false); }
     else if (g_bwd_pxl == 1) { if (atomics) BWD3(1, true); else BWD3(1, false); }
@@ -1758,6 +2108,30 @@ extern "C" int gsplat_rasterize_forward_clearing(
                                 stream, "rasterize_forward_clearing");
 }
 
+// List-split backward launch: two waves (16x8 strips) per (tile, chunk) item, or one wave per
+// item with the tile-wave kernel (ablation flag 4096).
+static void launch_bwd_chunked(hipStream_t st, int tbx, int tby, int H, int W, const int32_t *gids,
+                               const int32_t *bins, const float *xys, const float *conics,
+                               const float *colors, const float *opacity, const float *background,
+                               const float *final_Ts, const int32_t *final_idx,
+                               const float *v_output, const float *v_output_alpha,
+                               float alpha_max, float *rec, int chunk, const ChunkWs &w) {
+  if (!(g_bwd_flags & 4096)) {
+    hipLaunchKernelGGL((raster_bwd3p_kernel<1, true, 16, true>),
+                       dim3((unsigned)cdiv(w.items_bound, (long long)(tiles_per_block<2, 16>()))),
+                       dim3(256), 0, st, tbx, tby, H, W, gids, (const int2 *)bins,
+                       (const float2 *)xys, conics, colors, opacity, background, final_Ts,
+                       final_idx, v_output, v_output_alpha, alpha_max, rec, false, chunk,
+                       w.item_off, w.item_tile, w.ckpt_off, w.ckpt);
+    return;
+  }
+  hipLaunchKernelGGL((raster_bwd4_kernel<true>), dim3((unsigned)cdiv(w.items_bound, 4LL)),
+                     dim3(256), 0, st, tbx, tby, H, W, gids, (const int2 *)bins,
+                     (const float2 *)xys, conics, colors, opacity, background, final_Ts,
+                     final_idx, v_output, v_output_alpha, alpha_max, rec, chunk, w.item_off,
+                     w.item_tile, w.ckpt_off, w.ckpt);
+}
+
 extern "C" int gsplat_rasterize_backward_chunked(
     int tile_bounds_x, int tile_bounds_y, int img_height, int img_width, int num_points,
     const int32_t *gaussian_ids_sorted, const int32_t *tile_bins, const float *xys,
@@ -1794,12 +2168,9 @@ extern "C" int gsplat_rasterize_backward_chunked(
   if (num_points == 0) return check_launch("rasterize_backward_chunked");
   float *rec = (float *)workspace;
   note(hipMemsetAsync(rec, 0, need, st), "hipMemsetAsync");
-  hipLaunchKernelGGL((raster_bwd3p_kernel<1, true, 16, true>),
-                     dim3((unsigned)cdiv(w.items_bound, (long long)(tiles_per_block<2, 16>()))),
-                     dim3(256), 0, st, tile_bounds_x, tile_bounds_y, img_height, img_width,
-                     gaussian_ids_sorted, (const int2 *)tile_bins, (const float2 *)xys, conics,
-                     colors, opacity, background, final_Ts, final_idx, v_output, v_output_alpha,
-                     alpha_max, rec, false, chunk, w.item_off, w.item_tile, w.ckpt_off, w.ckpt);
+  launch_bwd_chunked(st, tile_bounds_x, tile_bounds_y, img_height, img_width,
+                     gaussian_ids_sorted, tile_bins, xys, conics, colors, opacity, background,
+                     final_Ts, final_idx, v_output, v_output_alpha, alpha_max, rec, chunk, w);
   hipLaunchKernelGGL(split_grads_kernel, dim3(cdiv(num_points, 256)), dim3(256), 0, st,
                      num_points, (const float4 *)rec, 0.5f, v_xy, v_conic, v_colors, v_opacity);
   return check_launch("rasterize_backward_chunked");
@@ -1842,13 +2213,14 @@ extern "C" int gsplat_rasterize_backward_records(
                 w.bytes);
       return 1;
     }
-    hipLaunchKernelGGL((raster_bwd3p_kernel<1, true, 16, true>),
-                       dim3((unsigned)cdiv(w.items_bound, (long long)(tiles_per_block<2, 16>()))),
-                       dim3(256), 0, st, tile_bounds_x, tile_bounds_y, img_height, img_width,
-                       gaussian_ids_sorted, (const int2 *)tile_bins, (const float2 *)xys, conics,
-                       colors, opacity, background, final_Ts, final_idx, v_output,
-                       v_output_alpha, alpha_max, rec, false, chunk, w.item_off, w.item_tile,
-                       w.ckpt_off, w.ckpt);
+    launch_bwd_chunked(st, tile_bounds_x, tile_bounds_y, img_height, img_width,
+                       gaussian_ids_sorted, tile_bins, xys, conics, colors, opacity, background,
+                       final_Ts, final_idx, v_output, v_output_alpha, alpha_max, rec, chunk, w);
+  } else if (g_bwd_flags & 4096) {
+    hipLaunchKernelGGL((raster_bwd4_kernel<false>), dim3(cdiv(T, 4)), dim3(256), 0, st,
+                       tile_bounds_x, tile_bounds_y, img_height, img_width, gaussian_ids_sorted,
+                       (const int2 *)tile_bins, (const float2 *)xys, conics, colors, opacity,
+                       background, final_Ts, final_idx, v_output, v_output_alpha, alpha_max, rec);
   } else {
     hipLaunchKernelGGL((raster_bwd3p_kernel<1, true, 16>),
                        dim3(cdiv(T, (tiles_per_block<2, 16>()))), dim3(256), 0, st,

@@ -147,8 +147,8 @@ def bin_gaussians(xys: Tensor, depths: Tensor, radii: Tensor, num_tiles_hit: Ten
                   tby, P(counts), P(ws1), ws1.numel(), st)
     num_intersects = _wait_count(host, dev)
     gaussian_ids_sorted = torch.empty((max(num_intersects, 0),), device=dev, dtype=torch.int32)
-    ws2 = torch.empty((_lib.query("gsplat_bin_emit_workspace_size", num_intersects),),
-                      device=dev, dtype=torch.uint8)
+    ws2 = torch.empty((_lib.query("gsplat_bin_emit_workspace_size_for", n, num_intersects, tbx,
+                                  tby),), device=dev, dtype=torch.uint8)
     _lib.call("gsplat_bin_emit", n, num_intersects, tbx, tby, P(gaussian_ids_sorted),
               P(tile_bins), P(ws1), ws1.numel(), P(ws2), ws2.numel(), st)
     return num_intersects, gaussian_ids_sorted, tile_bins

@@ -130,6 +130,10 @@ int gsplat_get_tile_bin_edges(int64_t num_intersects, const int64_t *isect_ids_s
  * identical to a stable sort of gsplat's 64-bit isect_ids. */
 size_t gsplat_bin_count_workspace_size(int num_points);
 size_t gsplat_bin_emit_workspace_size(int64_t num_intersects);
+/* Phase-2 workspace for the binning scheme in use (tile bucketing needs N and the tile
+ * count; callers should size gsplat_bin_emit's workspace2 with this query). */
+size_t gsplat_bin_emit_workspace_size_for(int num_points, int64_t num_intersects,
+                                          int tile_bounds_x, int tile_bounds_y);
 int gsplat_bin_count(int num_points, const float *xys, const float *depths,
                      const int32_t *radii, const int32_t *num_tiles_hit, int tile_bounds_x,
                      int tile_bounds_y, int32_t *d_counts, void *workspace1,
@@ -319,7 +323,11 @@ int gsplat_rasterize_backward_records(
  * bit 3 packed float2 forward; bit 4 16-column forward rectangles; bit 5 8-column backward
  * rectangles; bit 6 backward stages and culls but skips the blend (timing ablation only); bit 10
  * XCD-contiguous block order in the shipped forward and backward kernels; bit 11 backward with
- * sub-wave lists (each 16-lane row of a wave walks its own 8x4 rectangle's culled list).  Every variant produces results within the same parity bar.  Process-wide;
+ * sub-wave lists (each 16-lane row of a wave walks its own 8x4 rectangle's culled list); bit 12
+ * one backward wave per 16x16 tile (four pixels per lane as two float2 pairs, per-half cull
+ * bits; also used by the list-split backward), with bit 13 one-wave workgroups, bit 14 tiles
+ * dealt longest-list-first, bits 15-17 = p > 0: p persistent waves per SIMD taking tiles from a
+ * queue.  Every variant produces results within the same parity bar.  Process-wide;
  * defaults (1, 2, 0) are the shipped configuration. */
 int gsplat_debug_set_raster_variant(int fwd_pxl, int bwd_pxl, int bwd_flags);
 
@@ -332,6 +340,14 @@ int gsplat_debug_sort_timing(void *buffer, int calls);
 int gsplat_debug_sort_scheme(int reduce_then_scan);
 /* Debug: force 4, 8 or 16 keys per thread in every radix-sort pass (0 = automatic). */
 int gsplat_debug_sort_items(int items);
+/* Binning scheme: 1 = tile bucketing + per-tile LDS sort (frames up to 16,447
+ * tiles), 0 = depth sort + stable tile sort (default).  Same output either way.  Must not change between
+ * a gsplat_bin_count and its gsplat_bin_emit. */
+int gsplat_debug_binning_scheme(int bucket);
+/* Profiling hook: the backward blend kernels record per wave {start, end (s_memrealtime,
+ * 100 MHz), HW_ID, XCC_ID, work slot} as [waves][5] uint64 into the device buffer (NULL
+ * disables); the buffer needs 5 entries per launched wave. */
+int gsplat_debug_wave_log(void *buffer);
 
 /* ---- training-step photometric loss -------------------------------------
  * nerfstudio 1.0 splatfacto get_loss_dict's main loss, which the reference's training step

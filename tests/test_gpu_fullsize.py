@@ -49,16 +49,20 @@ def headline(request, gpu, oracle_lib):
                 colors=colors, opac=opac)
 
 
-@pytest.mark.parametrize("scheme", [1, 0])
+@pytest.mark.parametrize("scheme", ["rts", "onesweep", "bucket"])
 def test_headline_binning_bitexact(gpu, headline, scheme):
+    """Sorted binning under both radix-sort pass schemes (reduce-then-scan, one-sweep) and
+    the tile-bucketing scheme (per-tile LDS sort): all bit-exact."""
     h, cam = headline, headline["cam"]
     assert h["ref"]["num_intersects"] > 1 << 20
-    _lib.call("gsplat_debug_sort_scheme", scheme)
+    _lib.call("gsplat_debug_sort_scheme", 0 if scheme == "onesweep" else 1)
+    _lib.call("gsplat_debug_binning_scheme", 1 if scheme == "bucket" else 0)
     try:
         I, gids, bins = bin_gaussians(h["xys"], h["depths"], h["radii"], h["nth"], cam.height,
                                       cam.width)
     finally:
         _lib.call("gsplat_debug_sort_scheme", 1)
+        _lib.call("gsplat_debug_binning_scheme", 0)
     assert I == h["ref"]["num_intersects"]
     np.testing.assert_array_equal(_np(gids), h["ref"]["gaussian_ids_sorted"])
     np.testing.assert_array_equal(_np(bins), h["ref"]["tile_bins"])

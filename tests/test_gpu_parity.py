@@ -148,12 +148,17 @@ def test_sh_unaligned_slab(gpu):
                                rtol=RTOL, atol=ATOL)
 
 
+@pytest.mark.parametrize("bucket", [0, 1])
 @pytest.mark.parametrize("case", CASES)
-def test_binning_fused_bitexact(gpu, case):
+def test_binning_fused_bitexact(gpu, case, bucket):
     sc, cam, scales, quats = _inputs(*case)
     g, o = _project_both(gpu, sc, cam, scales, quats)
     xys, depths, radii, conics, nth, cov3d = g
-    I, gids, bins = bin_gaussians(xys, depths, radii, nth, cam.height, cam.width)
+    _lib.call("gsplat_debug_binning_scheme", bucket)
+    try:
+        I, gids, bins = bin_gaussians(xys, depths, radii, nth, cam.height, cam.width)
+    finally:
+        _lib.call("gsplat_debug_binning_scheme", 0)
     ref = O.bin_and_sort(o[0], o[1], o[2], o[4], cam.tile_bounds)
     assert I == ref["num_intersects"]
     np.testing.assert_array_equal(_np(gids), ref["gaussian_ids_sorted"])
@@ -249,10 +254,12 @@ def test_raster_backward(gpu, case):
 # (fwd pixels/lane, bwd pixels/lane, flags): see gsplat_debug_set_raster_variant in
 # include/gsplat_mi355x.h (1 no atomics, 2 scalar bwd, 4 scalar fwd, 8 packed fwd, 16 wide
 # fwd, 32 narrow bwd, 1024 XCD-contiguous block order, 2048
-# sub-wave-list backward).
+# sub-wave-list backward, 4096 one wave per tile (+8192 one-wave workgroups, +16384 tiles
+# longest-first, + 4 << 15 four persistent waves per SIMD pulling tiles from a queue)).
 RASTER_VARIANTS = [(1, 2, 0), (1, 2, 4), (1, 2, 16), (2, 2, 0), (2, 2, 8), (2, 2, 6), (4, 4, 0),
                    (4, 4, 8), (4, 4, 6), (1, 1, 0), (1, 2, 32), (1, 2, 1024),
-                   (1, 2, 2048)]
+                   (1, 2, 2048), (1, 2, 4096), (1, 2, 4096 | 8192), (1, 2, 4096 | 16384),
+                   (1, 2, 4096 | (4 << 15))]
 
 
 @pytest.mark.parametrize("variant", RASTER_VARIANTS)
@@ -305,17 +312,21 @@ def _check_raster_backward(gpu, case):
         assert frac == 0.0, f"{name}: {frac:.2e} out of tolerance (max {mx:.3e})"
 
 
+@pytest.mark.parametrize("flags", [0, 4096])
 @pytest.mark.parametrize("chunk", [64, 128, 256])
 @pytest.mark.parametrize("case", CASES[1:3])
-def test_raster_backward_list_split(gpu, case, chunk):
+def test_raster_backward_list_split(gpu, case, chunk, flags):
     """The list-split backward (checkpointed forward + per-chunk backward, forced chunk
-    size): identical forward, gradients within the same bar vs the oracle."""
+    size; strip waves or, flag 4096, one wave per item): identical forward, gradients within
+    the same bar vs the oracle."""
     _lib.call("gsplat_debug_set_chunk", chunk)
+    _lib.call("gsplat_debug_set_raster_variant", 1, 2, flags)
     try:
         _check_raster_forward(gpu, case)
         _check_raster_backward(gpu, case)
     finally:
         _lib.call("gsplat_debug_set_chunk", 0)
+        _lib.call("gsplat_debug_set_raster_variant", 1, 2, 0)
 
 
 @pytest.mark.parametrize("C", [1, 4, 7])
