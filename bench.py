@@ -93,12 +93,18 @@ def view_camera(W, H, view: int):
 
 
 def algorithmic_bytes(N, I, P, T, K, nvis):
-    """Per-view algorithmic HBM bytes of each C-ABI entry point (SURVEY.md §8d model)."""
+    """Per-view algorithmic HBM bytes of each C-ABI entry point (SURVEY.md §8d model; the
+    binning entries count every radix pass's key/value reads and writes)."""
+    tile_passes = max(1, -(-max(1, (T - 1).bit_length()) // 8))  # 8-bit digits of the tile id
     return {
         "gsplat_project_gaussians_forward": 96 * N,
         "gsplat_compute_sh_forward": (24 + 12 * K) * N,
-        "gsplat_bin_count": 8 * N,
-        "gsplat_bin_emit": 20 * N + 44 * I + 8 * T,
+        # depth keys (44 N) + 4 radix passes (count 4 N, scatter 16 N each) + the depth-ordered
+        # record gather (36 N) + the allotment scan (8 N)
+        "gsplat_bin_count": 168 * N,
+        "gsplat_bin_count_keyed": 124 * N,
+        # emission (records in, (tile, id) pairs out) + per tile-digit pass 20 I + bin edges
+        "gsplat_bin_emit": 20 * N + 8 * I + 20 * tile_passes * I + 4 * I + 8 * T,
         "gsplat_rasterize_forward": 40 * I + 20 * P,
         "gsplat_rasterize_backward": 40 * I + 24 * P + 36 * N,
         "gsplat_compute_sh_backward": (24 + 12 * K) * N,
@@ -108,7 +114,6 @@ def algorithmic_bytes(N, I, P, T, K, nvis):
         "gsplat_fused_preprocess_forward": (92 + 12 * K) * N,
         # + the binning's depth key, id and 16-B record per Gaussian
         "gsplat_fused_preprocess_forward_binned": (116 + 12 * K) * N,
-        "gsplat_bin_count_keyed": 8 * N,
         # its blend also zeroes the 48-B gradient record of every visible Gaussian
         "gsplat_rasterize_forward_clearing": 40 * I + 20 * P + 48 * nvis,
         "gsplat_rasterize_backward_records": 40 * I + 24 * P,
@@ -117,65 +122,119 @@ def algorithmic_bytes(N, I, P, T, K, nvis):
     }
 
 
-# Device kernels behind each C-ABI entry (for the PMC traffic of the dominant entry).
+# Device kernels behind each C-ABI entry (for the PMC counters of the dominant entry), and
+# whether their loads are 16-B-per-lane streaming reads -- the only access width for which
+# MI355X_MICROARCH.md calibrates gfx950's FETCH_SIZE (it reports half the bytes: x2).  The
+# blend kernels gather 4-8 B per lane; their FETCH_SIZE is reported raw (uncalibrated).
 ENTRY_KERNELS = {
-    "gsplat_rasterize_backward": ("raster_bwd", "split_grads_kernel"),
-    "gsplat_rasterize_backward_records": ("raster_bwd",),
-    "gsplat_fused_preprocess_forward": ("fused_fwd_kernel",),
-    "gsplat_fused_preprocess_forward_binned": ("fused_fwd_kernel",),
-    "gsplat_fused_preprocess_backward": ("fused_bwd_kernel",),
-    "gsplat_rasterize_forward": ("raster_fwd",),
-    "gsplat_rasterize_forward_clearing": ("raster_fwd",),
-    "gsplat_compute_sh_forward": ("sh_fwd_kernel",),
+    "gsplat_rasterize_backward": (("raster_bwd", "split_grads_kernel"), False),
+    "gsplat_rasterize_backward_records": (("raster_bwd",), False),
+    "gsplat_fused_preprocess_forward": (("fused_fwd_kernel",), True),
+    "gsplat_fused_preprocess_forward_binned": (("fused_fwd_kernel",), True),
+    "gsplat_fused_preprocess_backward": (("fused_bwd_kernel",), True),
+    "gsplat_rasterize_forward": (("raster_fwd",), False),
+    "gsplat_rasterize_forward_clearing": (("raster_fwd",), False),
+    "gsplat_compute_sh_forward": (("sh_fwd_kernel",), True),
 }
 PMC_TRAFFIC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
                            "pmc_traffic.json")
 
 
-def pmc_traffic(entry):
-    """HBM bytes per call of a C-ABI entry from the committed rocprofv3 PMC summary
-    (profiles/pmc_traffic.json, tools/pmc_bench.sh + tools/pmc_summary.py): FETCH_SIZE is
-    doubled (gfx950 counts half the bytes of wide reads, MI355X_MICROARCH.md HBM section),
-    WRITE_SIZE taken as is; None when no summary covers the entry."""
+def _pmc_kernels(config):
+    """The committed rocprofv3 PMC summary of `config` (profiles/pmc_traffic.json, written by
+    tools/pmc_bench.sh + tools/pmc_summary.py on that config), or None: counters collected on
+    another config are never used."""
     try:
         with open(PMC_TRAFFIC) as f:
-            kern = json.load(f)["kernels"]
+            return json.load(f)["configs"][config]["kernels"]
     except (OSError, ValueError, KeyError):
         return None
-    pats = ENTRY_KERNELS.get(entry)
-    if not pats:
+
+
+def pmc_traffic(entry, config):
+    """HBM bytes per call of a C-ABI entry on `config`: FETCH_SIZE (x2 only for streaming
+    16-B-per-lane kernels, see ENTRY_KERNELS) + WRITE_SIZE; None without counters."""
+    kern = _pmc_kernels(config)
+    pats, streaming = ENTRY_KERNELS.get(entry, ((), False))
+    if not kern or not pats:
         return None
     tot, hit = 0.0, False
     for name, v in kern.items():
         if any(p in name for p in pats) and v.get("fetch_kb") is not None:
-            tot += (2.0 * v["fetch_kb"] + (v.get("write_kb") or 0.0)) * 1024.0
+            tot += ((2.0 if streaming else 1.0) * v["fetch_kb"] + (v.get("write_kb") or 0.0)) \
+                * 1024.0
             hit = True
     return int(tot) if hit else None
 
 
-def pmc_valu_busy(entry, ms_per_call, n_simd=256 * 4, clock_hz=2.4e9):
-    """Fraction of the chip's VALU issue slots the entry's kernels used: rocprofv3
-    SQ_ACTIVE_INST_VALU (quad-cycles, one fp32 wave64 VALU instruction each;
-    MI355X_MICROARCH.md) per call / (SIMDs x call duration in quad-cycles at the peak engine
-    clock).  The blend kernels are VALU-issue bound, so this -- not the HBM fraction -- is the
-    roofline that binds them.  None without a PMC summary."""
-    try:
-        with open(PMC_TRAFFIC) as f:
-            kern = json.load(f)["kernels"]
-    except (OSError, ValueError, KeyError):
+def pmc_valu_busy(entry, config, ms_per_call, n_simd=256 * 4, clock_hz=2.4e9):
+    """Fraction of the chip's VALU issue slots the entry's kernels used on `config`: rocprofv3
+    SQ_ACTIVE_INST_VALU (quad-cycles) per call / (SIMDs x call duration in quad-cycles at the
+    peak engine clock).  The blend kernels are VALU-issue bound, so this -- not the HBM
+    fraction -- is the roofline that binds them.  None without that config's counters."""
+    kern = _pmc_kernels(config)
+    pats, _ = ENTRY_KERNELS.get(entry, ((), False))
+    if not kern or not pats or not ms_per_call:
         return None
-    pats = ENTRY_KERNELS.get(entry)
     tot, hit = 0.0, False
     for name, v in kern.items():
-        if pats and any(p in name for p in pats) and v.get("valu_quad_cycles") is not None:
+        if any(p in name for p in pats) and v.get("valu_quad_cycles") is not None:
             tot += v["valu_quad_cycles"]
             hit = True
-    if not hit or not ms_per_call:
-        return None
-    return round(tot / (n_simd * ms_per_call * 1e-3 * clock_hz / 4.0), 3)
+    return round(tot / (n_simd * ms_per_call * 1e-3 * clock_hz / 4.0), 3) if hit else None
 
 
-def cpu_baseline(scene, cam, sh_degree, budget_tiles=64, seed=0):
+def cpu_threads():
+    """Host threads the CPU baseline may use: the CPUs this process may run on, capped by
+    OMP_NUM_THREADS when the job sets it (the GPU box gives one GPU's job 16 of its CPUs
+    and says so there; os.cpu_count() reports the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        n = min(n, int(env))
+    return max(1, n)
+
+
+def cpu_baseline(scene, cam, sh_degree, n_tiles=256, seed=0, backward=True):
+    """The north-star CPU baseline: a naive pure-PyTorch per-pixel rasterizer
+    (oracle/torch_ref.render_fwd_bwd_sampled: gc_model's activations, projection, SH,
+    torch.sort binning, per-pixel compositing over each tile's whole list, autograd backward)
+    on all host threads, the compositing timed on `n_tiles` seeded random tiles and
+    extrapolated by the tile count.  The single-threaded C oracle (a hand-written port of
+    gsplat's kernels, a much stronger CPU program) is timed on 64 tiles beside it."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import torch_ref as TR
+    threads = cpu_threads()
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        sc = scene.detach().to("cpu")
+        H, W = cam.height, cam.width
+        T = cam.tile_bounds[0] * cam.tile_bounds[1]
+        total, d = TR.render_fwd_bwd_sampled(
+            sc.means, sc.scales, sc.quats, sc.opacities, sc.features_dc, sc.features_rest,
+            cam.viewmat, cam.projmat, cam.c2w[:3, 3], cam.fx, cam.fy, cam.cx, cam.cy, H, W,
+            sh_degree, n_tiles=min(n_tiles, T), seed=seed, backward=backward)
+    finally:
+        torch.set_num_threads(prev)
+    c_port = c_oracle_baseline(scene, cam, sh_degree, seed=seed) if backward else None
+    return {
+        "value": round(H * W / total / 1e6, 5),
+        "unit": "Mpixels/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": (f"pure-PyTorch per-pixel rasterizer (oracle/torch_ref.py), "
+                   f"{'fwd + autograd bwd' if backward else 'forward only'}, torch.set_num_threads({threads}) (host os.cpu_count()="
+                   f"{os.cpu_count()}): per-Gaussian stages over all {sc.means.shape[0]} "
+                   f"Gaussians + torch.sort binning of {d['intersects']} intersections "
+                   f"({d['t_gauss']:.2f}s) + compositing fwd+bwd on {d['tiles']} of {T} random "
+                   f"tiles ({d['t_tiles']:.2f}s) extrapolated x{d['scale']:.1f}; "
+                   f"est {total:.1f}s per view"),
+        "c_oracle_1thread": c_port,
+    }
+
+
+def c_oracle_baseline(scene, cam, sh_degree, budget_tiles=64, seed=0):
     """C oracle (single-threaded restatement of gsplat) on a bounded sample: the full
     per-Gaussian stages (project, SH, map+stable sort+bins) plus rasterize fwd+bwd on
     `budget_tiles` random tiles, extrapolated to all tiles."""
@@ -214,7 +273,7 @@ def cpu_baseline(scene, cam, sh_degree, budget_tiles=64, seed=0):
                               tile_list=tiles)
     t_tiles = time.perf_counter() - t0
     t0 = time.perf_counter()
-    vc = O.sh_backward(sh_degree, dirs, gr[2], coeffs.shape[1])
+    O.sh_backward(sh_degree, dirs, gr[2], coeffs.shape[1])
     O.project_backward(means, scales, 1.0, quats, cam.viewmat.numpy(), cam.projmat.numpy(),
                        cam.fx, cam.fy, cam.cx, cam.cy, H, W, cov3d, radii, conics, gr[0],
                        np.zeros_like(depths), gr[1])
@@ -228,8 +287,7 @@ def cpu_baseline(scene, cam, sh_degree, budget_tiles=64, seed=0):
         "sample": (f"C oracle, 1 thread: full project+SH+bin/sort+SH-bwd+project-bwd over "
                    f"{means.shape[0]} Gaussians ({t_gauss_fwd + t_gauss_bwd:.2f}s) + rasterize "
                    f"fwd+bwd on {len(tiles)} of {T} random tiles ({t_tiles:.2f}s) "
-                   f"extrapolated x{T / len(tiles):.1f}; est {total:.1f}s per view; "
-                   f"host cpu_count={os.cpu_count()}"),
+                   f"extrapolated x{T / len(tiles):.1f}; est {total:.1f}s per view"),
     }
 
 
@@ -355,8 +413,9 @@ def main():
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
         "frac": round(dom_bytes / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if dom_bytes else None,
-        "traffic": pmc_traffic(dom),
-        "valu_busy": pmc_valu_busy(dom, dom_ms),
+        "traffic": pmc_traffic(dom, args.config),
+        "traffic_fetch_scale": 2 if ENTRY_KERNELS.get(dom, ((), False))[1] else 1,
+        "valu_busy": pmc_valu_busy(dom, args.config, dom_ms),
         "step_algorithmic_bytes": step_bytes,
         "step_frac": round(step_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
         "roofline_mpix_s": round(P / (step_bytes / (HBM_PEAK_GBS * 1e9)) / 1e6, 1),
@@ -380,7 +439,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(scene, cam_cpu, deg)
+        cpu = cpu_baseline(scene, cam_cpu, deg, backward=not fwd_only)
 
     if rank == 0:
         line = {

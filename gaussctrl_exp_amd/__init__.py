@@ -12,9 +12,13 @@ Layout:
   train.py              multi-view data-parallel train step (fused loss, fused Adam)
   exchange.py           data-parallel SH-gradient view exchange (RCCL all-gather)
   loss.py  optim.py     fused L1+SSIM loss, fused multi-tensor Adam
+  quirks.py             the gsplat 0.1.2.1 [VERIFY] behaviour switch (GSPLAT_MI355X_QUIRKS)
+  set_deterministic     bit-reproducible rasterize backward (GSPLAT_MI355X_DETERMINISTIC=1)
 
 `import gsplat` (the top-level shim package) resolves to this implementation.
 """
+from . import quirks
+from ._lib import set_deterministic
 from .project_gaussians import project_gaussians
 from .rasterize import rasterize_gaussians, rasterize_gaussians_rgbd
 from .sh import num_sh_bases, spherical_harmonics
@@ -35,4 +39,6 @@ __all__ = [
     "compute_cumulative_intersects",
     "compute_cov2d_bounds",
     "get_tile_bin_edges",
+    "quirks",
+    "set_deterministic",
 ]

@@ -26,6 +26,10 @@ _SZ = _c.c_size_t
 # name -> (restype, argtypes); must match include/gsplat_mi355x.h exactly.
 SIGNATURES = {
     "gsplat_abi_version": (_I, []),
+    "gsplat_set_quirks": (_I, [_I]),
+    "gsplat_get_quirks": (_I, []),
+    "gsplat_set_deterministic": (_I, [_I]),
+    "gsplat_get_deterministic": (_I, []),
     "gsplat_last_error": (_c.c_char_p, []),
     "gsplat_project_gaussians_forward": (_I, [
         _I, _P, _P, _F, _P, _P, _P, _F, _F, _F, _F, _I, _I, _I, _I, _F,
@@ -86,9 +90,21 @@ SIGNATURES = {
                                                                        _P, _SZ, _P]),
 }
 
-ABI_VERSION = 6  # include/gsplat_mi355x.h GSPLAT_MI355X_ABI_VERSION
+ABI_VERSION = 7  # include/gsplat_mi355x.h GSPLAT_MI355X_ABI_VERSION
 
 _lib = None
+_DETERMINISTIC = os.environ.get("GSPLAT_MI355X_DETERMINISTIC", "0") not in ("", "0")
+
+
+def set_deterministic(on: bool) -> bool:
+    """Deterministic rasterize backward (integer accumulation; bit-identical gradients run to
+    run, slower -- a debugging mode).  Also GSPLAT_MI355X_DETERMINISTIC=1.  Returns the previous
+    setting."""
+    global _DETERMINISTIC
+    prev, _DETERMINISTIC = _DETERMINISTIC, bool(on)
+    if _lib is not None:
+        _lib.gsplat_set_deterministic(int(_DETERMINISTIC))
+    return prev
 
 
 def build(jobs: int = 8) -> str:
@@ -111,6 +127,10 @@ def lib():
             fn.argtypes = args
         if L.gsplat_abi_version() != ABI_VERSION:
             raise RuntimeError("libgsplat_mi355x.so ABI version mismatch")
+        from . import quirks
+        if L.gsplat_set_quirks(quirks.get()) != 0:
+            raise RuntimeError(L.gsplat_last_error().decode(errors="replace"))
+        L.gsplat_set_deterministic(int(_DETERMINISTIC))
         _lib = L
     return _lib
 

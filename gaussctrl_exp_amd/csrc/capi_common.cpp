@@ -7,6 +7,8 @@
 
 namespace gs {
 
+int g_quirks = GSPLAT_QUIRKS_ALL;
+
 static thread_local char g_err[512] = "";
 
 void set_error(const char *fmt, ...) {
@@ -44,3 +46,13 @@ int check_launch(const char *what) {
 
 extern "C" int gsplat_abi_version(void) { return GSPLAT_MI355X_ABI_VERSION; }
 extern "C" const char *gsplat_last_error(void) { return gs::g_err; }
+
+extern "C" int gsplat_set_quirks(int mask) {
+  if (mask & ~GSPLAT_QUIRKS_ALL) {
+    gs::set_error("gsplat_set_quirks: unknown bits 0x%x", mask & ~GSPLAT_QUIRKS_ALL);
+    return 1;
+  }
+  gs::g_quirks = mask;
+  return 0;
+}
+extern "C" int gsplat_get_quirks(void) { return gs::g_quirks; }

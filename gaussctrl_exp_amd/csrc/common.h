@@ -19,6 +19,18 @@ void set_error(const char *fmt, ...);
 void note(hipError_t e, const char *what);
 int check_launch(const char *what);
 
+// gsplat 0.1.2.1 behaviours recalled but unverified (SURVEY.md Appendix A [VERIFY]); each is a
+// bit of the process-wide quirk mask (gsplat_set_quirks, default GSPLAT_QUIRKS_ALL):
+//   GSPLAT_QUIRK_ALPHA_099       A10: the backward clamps alpha at 0.99 (the forward at 0.999);
+//                                off: 0.999 in both.  (Applied by the callers' alpha_max.)
+//   GSPLAT_QUIRK_CONIC_HALF      A7/A9: v_conic.y = 1/2 v_sigma dx dy, paired with a conic VJP
+//                                that takes it as the gradient of each symmetric off-diagonal;
+//                                off: v_conic.y = v_sigma dx dy (d sigma / d conic.y) and the VJP
+//                                halves it.  End-to-end gradients are identical either way.
+//   GSPLAT_QUIRK_EWA_UNCLAMPED   A6: the EWA VJP recomputes t without the 1.3 tan_fov clamp;
+//                                off: the Jacobian of the clamped forward (through the clamp).
+extern int g_quirks;
+
 static inline unsigned int cdiv(long long a, long long b) { return (unsigned int)((a + b - 1) / b); }
 
 // Saturating float->int truncation, NaN -> 0: the semantics of v_cvt_i32_f32 (and of

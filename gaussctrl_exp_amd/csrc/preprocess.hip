@@ -226,7 +226,9 @@ __global__ __launch_bounds__(sh_threads(K)) void fused_bwd_kernel(FusedBwdArgs a
       const float cs = a.conic_scale;
       project_backward_one(cam, pp, p0, p1, p2, s[0], s[1], s[2], qn[0], qn[1], qn[2], qn[3],
                            cv, a.conics[3 * g], a.conics[3 * g + 1], a.conics[3 * g + 2], r0.x,
-                           r0.y, 0.f, cs * r0.z, cs * r0.w, cs * r1.x, pg);
+                           r0.y, 0.f, cs * r0.z,
+                           (pp.quirks & GSPLAT_QUIRK_CONIC_HALF ? cs : 2.f * cs) * r0.w, cs * r1.x,
+                           pg);
 #pragma unroll
       for (int k = 0; k < 3; ++k) vmean[k] = pg.vmean[k];
       // exp backward: grad * result

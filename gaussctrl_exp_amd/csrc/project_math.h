@@ -92,6 +92,7 @@ __device__ __forceinline__ void tile_bbox(float x, float y, float radius, int tb
 struct ProjParams {
   float fx, fy, cx, cy, glob_scale, tan_fovx, tan_fovy, clip_thresh;
   int H, W, tbx, tby;
+  int quirks;  // GSPLAT_QUIRK_* bits (common.h), from gsplat_set_quirks at launch
 };
 
 // gsplat computes tan_fov = 0.5 * img_size / f with a double literal.
@@ -107,6 +108,7 @@ static inline ProjParams make_proj_params(float fx, float fy, float cx, float cy
   pp.tan_fovx = (float)(0.5 * (double)W / (double)fx);
   pp.tan_fovy = (float)(0.5 * (double)H / (double)fy);
   pp.clip_thresh = clip_thresh;
+  pp.quirks = g_quirks;
   pp.H = H;
   pp.W = W;
   pp.tbx = tbx;
@@ -233,7 +235,9 @@ __device__ __forceinline__ void project_backward_one(const Cam &cam, const ProjP
   g.vmean[0] += vm[8] * vz;
   g.vmean[1] += vm[9] * vz;
   g.vmean[2] += vm[10] * vz;
-  // cov2d_to_conic_vjp
+  // cov2d_to_conic_vjp: G = [[ga, gb], [gb, gc]] holds the gradient of each symmetric entry;
+  // without the conic-half convention the upstream gb is d/d(conic.y) of both entries at once
+  if (!(pp.quirks & GSPLAT_QUIRK_CONIC_HALF)) gb = 0.5f * gb;
   {
     float xg00 = a * ga + b * gb, xg01 = a * gb + b * gc;
     float xg10 = b * ga + c * gb, xg11 = b * gb + c * gc;
@@ -243,12 +247,23 @@ __device__ __forceinline__ void project_backward_one(const Cam &cam, const ProjP
     g.vc2[1] = -s10 + -s01;
     g.vc2[2] = -s11;
   }
-  // project_cov3d_ewa_vjp (no fov clamp)
+  // project_cov3d_ewa_vjp (gsplat: no fov clamp; without that quirk, the
+  // Jacobian of the clamped forward: t_x = t_z clamp(t_x / t_z) passes d/dt_x inside the
+  // clamp and +-lim * d/dt_z outside)
   {
     M3 Wm = {{vm[0], vm[1], vm[2], vm[4], vm[5], vm[6], vm[8], vm[9], vm[10]}};
     float tx = vm[0] * p0 + vm[1] * p1 + vm[2] * p2 + vm[3];
     float ty = vm[4] * p0 + vm[5] * p1 + vm[6] * p2 + vm[7];
     float tz = vm[8] * p0 + vm[9] * p1 + vm[10] * p2 + vm[11];
+    const bool clamped = !(pp.quirks & GSPLAT_QUIRK_EWA_UNCLAMPED);
+    float limx = 1.3f * pp.tan_fovx, limy = 1.3f * pp.tan_fovy, sx = 0.f, sy = 0.f;
+    if (clamped) {
+      const float ux = tx / tz, uy = ty / tz;
+      sx = ux < -limx ? -limx : (ux > limx ? limx : 0.f);  // 0: inside the clamp
+      sy = uy < -limy ? -limy : (uy > limy ? limy : 0.f);
+      tx = tz * fminf(limx, fmaxf(-limx, ux));
+      ty = tz * fminf(limy, fmaxf(-limy, uy));
+    }
     float rz = 1.f / tz;
     float rz2 = rz * rz;
     float rz3 = rz2 * rz;
@@ -275,6 +290,10 @@ __device__ __forceinline__ void project_backward_one(const Cam &cam, const ProjP
     float vt1 = -fy * rz2 * vJ21;
     float vt2 = -fx * rz2 * vJ00 + 2.f * fx * tx * rz3 * vJ20 - fy * rz2 * vJ11 +
                 2.f * fy * ty * rz3 * vJ21;
+    if (clamped) {
+      if (sx != 0.f) { vt2 += sx * vt0; vt0 = 0.f; }
+      if (sy != 0.f) { vt2 += sy * vt1; vt1 = 0.f; }
+    }
     g.vmean[0] += vt0 * Wm.m[0] + vt1 * Wm.m[3] + vt2 * Wm.m[6];
     g.vmean[1] += vt0 * Wm.m[1] + vt1 * Wm.m[4] + vt2 * Wm.m[7];
     g.vmean[2] += vt0 * Wm.m[2] + vt1 * Wm.m[5] + vt2 * Wm.m[8];

@@ -40,6 +40,45 @@ namespace {
 
 constexpr float ALPHA_MIN = 1.f / 255.f;
 constexpr int REC = 16;  // floats per gradient record: x y a b c r g b o + pad = 64 B
+
+// Deterministic backward (gsplat_set_deterministic): every wave's nine per-Gaussian totals
+// (reduce9: a fixed reduction order, so run-independent) are added as 64-bit fixed-point
+// integers (2^-32 units) instead of fp32 atomics.  Integer addition is associative, so the
+// sums -- and every gradient downstream -- are bit-identical from run to run whatever order
+// the waves finish in; det_finish_kernel converts them into the usual float records.  The
+// quantisation error (<= 2^-33 per wave total) is far below the fp32 atomics' own.
+constexpr int DET_REC = 9;
+constexpr float DET_SCALE = 4294967296.f;  // 2^32
+__device__ __forceinline__ unsigned long long det_quantize(float v) {
+  const float s = fminf(fmaxf(v * DET_SCALE, -9.2e18f), 9.2e18f);  // |v| < 2^31
+  return (unsigned long long)__float2ll_rn(s);
+}
+__global__ __launch_bounds__(256) void det_finish_kernel(int n,
+                                                         const unsigned long long *__restrict__ det,
+                                                         float *__restrict__ rec) {
+  const int g = blockIdx.x * 256 + threadIdx.x;
+  if (g >= n) return;
+#pragma unroll
+  for (int k = 0; k < DET_REC; ++k)
+    rec[(size_t)g * REC + k] =
+        (float)((double)(long long)det[(size_t)g * DET_REC + k] * (1.0 / 4294967296.0));
+}
+bool g_det = false;
+unsigned long long *g_det_buf = nullptr;
+size_t g_det_cap = 0;
+// The deterministic accumulators (debug mode only: allocated on first use, grown as needed,
+// then cleared on the call's stream).
+unsigned long long *det_buffer(int n, hipStream_t st) {
+  const size_t need = (size_t)n * DET_REC * sizeof(unsigned long long);
+  if (need > g_det_cap) {
+    if (g_det_buf) note(hipFree(g_det_buf), "hipFree");
+    g_det_buf = nullptr;
+    note(hipMalloc(&g_det_buf, need), "hipMalloc");
+    g_det_cap = g_det_buf ? need : 0;
+  }
+  if (g_det_buf) note(hipMemsetAsync(g_det_buf, 0, need, st), "hipMemsetAsync");
+  return g_det_buf;
+}
 constexpr int FWD_PXL = 1;  // forward: 8x8 blocks, two Gaussians per iteration (4 waves/tile)
 constexpr int BWD_PXL = 2;  // packed backward, 16x8 strips (2 waves per tile)
 // Tuning / ablation knobs (gsplat_debug_set_raster_variant); defaults are the shipped ones.
@@ -744,7 +783,8 @@ __global__ __launch_bounds__(256) void raster_bwd3_kernel(
 // [range.x + j * chunk, range.x + (j + 1) * chunk) and starts from the forward's checkpoint
 // after its last position: T = checkpoint T, and the colour behind it, Sb = (C_final - C_j) . v,
 // instead of T_final and 0 -- so long lists and small images (few tiles) still fill the GPU.
-template <int NP, bool ATOMICS, int COLS, bool CHUNKED = false, typename PV = f2>
+template <int NP, bool ATOMICS, int COLS, bool CHUNKED = false, typename PV = f2,
+          bool DET = false>
 __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
     int tbx, int tby, int H, int W, const int *__restrict__ gids, const int2 *__restrict__ bins,
     const float2 *__restrict__ xys, const float *__restrict__ conics,
@@ -754,7 +794,7 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
     const float *__restrict__ v_out_alpha, float alpha_max, float *__restrict__ rec,
     bool stage_only, int chunk = 0, const int *__restrict__ item_off = nullptr,
     const int *__restrict__ item_tile = nullptr, const int *__restrict__ ckpt_off = nullptr,
-    const float4 *__restrict__ ckpt = nullptr) {
+    const float4 *__restrict__ ckpt = nullptr, unsigned long long *__restrict__ det = nullptr) {
   constexpr int PXL = 2 * NP;
   constexpr int LROWS = 64 / COLS;
   int ctile = -1, cj = 0;
@@ -911,7 +951,10 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
         for (int u = 0; u < U; ++u) v[u] = reduce9(parts[u]);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          if constexpr (ATOMICS) {
+          if constexpr (DET) {  // deterministic mode: exact integer sums of the wave totals
+            if (__any(anyv[u]) && slot >= 0)
+              atomicAdd(det + (size_t)gid[u] * DET_REC + slot, det_quantize(v[u]));
+          } else if constexpr (ATOMICS) {
             if (__any(anyv[u]) && slot >= 0) atomicAdd(rec + (size_t)gid[u] * REC + slot, v[u]);
           } else {
             asm volatile("" ::"v"(v[u]));
@@ -1483,8 +1526,15 @@ __global__ __launch_bounds__(1024) void chunk_plan_kernel(int T, const int2 *__r
 }
 
 // Gradient records -> gsplat's v_xy [N,2], v_conic [N,3], v_colors [N,3], v_opacity [N].
+// Scale of a record's conic.y sum into gsplat's v_conic.y: the records hold the gradient of
+// each conic entry in gsplat's halved convention times 1/s; without the CONIC_HALF quirk
+// v_conic.y is d loss / d conic.y, twice that.
+static inline float conic_y_scale(float s) {
+  return (g_quirks & GSPLAT_QUIRK_CONIC_HALF) ? s : 2.f * s;
+}
+
 __global__ __launch_bounds__(256) void split_grads_kernel(int n, const float4 *__restrict__ rec,
-                                                          float conic_scale,
+                                                          float conic_scale, float conic_scale_b,
                                                           float *__restrict__ v_xy,
                                                           float *__restrict__ v_conic,
                                                           float *__restrict__ v_rgb,
@@ -1496,7 +1546,7 @@ __global__ __launch_bounds__(256) void split_grads_kernel(int n, const float4 *_
   v_xy[2 * g] = r0.x;
   v_xy[2 * g + 1] = r0.y;
   v_conic[3 * g] = conic_scale * r0.z;
-  v_conic[3 * g + 1] = conic_scale * r0.w;
+  v_conic[3 * g + 1] = conic_scale_b * r0.w;
   v_conic[3 * g + 2] = conic_scale * r1.x;
   v_rgb[3 * g] = r1.y;
   v_rgb[3 * g + 1] = r1.z;
@@ -1878,6 +1928,12 @@ extern "C" int gsplat_debug_set_raster_variant(int fwd_pxl, int bwd_pxl, int bwd
   return 0;
 }
 
+extern "C" int gsplat_set_deterministic(int on) {
+  g_det = on != 0;
+  return 0;
+}
+extern "C" int gsplat_get_deterministic(void) { return g_det ? 1 : 0; }
+
 extern "C" int gsplat_debug_wave_log(void *buffer) {
   unsigned long long *p = (unsigned long long *)buffer;
   if (hipMemcpyToSymbol(HIP_SYMBOL(g_wave_log), &p, sizeof(p)) != hipSuccess) {
@@ -1885,6 +1941,20 @@ extern "C" int gsplat_debug_wave_log(void *buffer) {
     return 1;
   }
   return 0;
+}
+
+// The shipped 16x8-strip backward in deterministic mode (integer accumulators in det).
+static void launch_bwd_det(hipStream_t st, int tbx, int tby, int H, int W, const int32_t *gids,
+                           const int32_t *bins, const float *xys, const float *conics,
+                           const float *colors, const float *opacity, const float *background,
+                           const float *final_Ts, const int32_t *final_idx,
+                           const float *v_output, const float *v_output_alpha, float alpha_max,
+                           float *rec, unsigned long long *det) {
+  hipLaunchKernelGGL((raster_bwd3p_kernel<1, true, 16, false, f2, true>),
+                     dim3(cdiv((long long)tbx * tby, (tiles_per_block<2, 16>()))), dim3(256), 0,
+                     st, tbx, tby, H, W, gids, (const int2 *)bins, (const float2 *)xys, conics,
+                     colors, opacity, background, final_Ts, final_idx, v_output, v_output_alpha,
+                     alpha_max, rec, false, 0, nullptr, nullptr, nullptr, nullptr, det);
 }
 
 extern "C" size_t gsplat_rasterize_backward_workspace_size(int num_points, int channels) {
@@ -1936,7 +2006,19 @@ extern "C" int gsplat_rasterize_backward(int tile_bounds_x, int tile_bounds_y, i
     const bool atomics = !(g_bwd_flags & 1);
     const bool packed = g_bwd_pxl >= 2 && !(g_bwd_flags & 2);
     const bool narrow = g_bwd_flags & 32;  // 8-column wave rectangles
-    if (packed) {
+    if (g_det) {
+      if (!default_variants() || (g_bwd_flags & 4096)) {
+        set_error("rasterize_backward: deterministic mode needs the default raster variant");
+        return 1;
+      }
+      unsigned long long *det = det_buffer(num_points, st);
+      if (!det) return check_launch("rasterize_backward");
+      launch_bwd_det(st, tile_bounds_x, tile_bounds_y, img_height, img_width, gaussian_ids_sorted,
+                     tile_bins, xys, conics, colors, opacity, background, final_Ts, final_idx,
+                     v_output, v_output_alpha, alpha_max, rec, det);
+      hipLaunchKernelGGL(det_finish_kernel, dim3(cdiv(num_points, 256)), dim3(256), 0, st,
+                         num_points, det, rec);
+    } else if (packed) {
       if (g_bwd_pxl == 4) {
         if (atomics) BWD3P(2, true, 16); else BWD3P(2, false, 16);  // 16x16: one wave
       } else {
@@ -2002,8 +2084,8 @@ extern "C" int gsplat_rasterize_backward(int tile_bounds_x, int tile_bounds_y, i
 #undef BWD3
 #undef BWD3P
     hipLaunchKernelGGL(split_grads_kernel, dim3(cdiv(num_points, 256)), dim3(256), 0, st,
-                       num_points, (const float4 *)rec, packed ? 0.5f : 1.f, v_xy, v_conic,
-                       v_colors, v_opacity);
+                       num_points, (const float4 *)rec, packed ? 0.5f : 1.f,
+                       conic_y_scale(packed ? 0.5f : 1.f), v_xy, v_conic, v_colors, v_opacity);
   } else {
     if (num_points > 0) {
       note(hipMemsetAsync(v_xy, 0, (size_t)num_points * 2 * sizeof(float), st), "hipMemsetAsync");
@@ -2115,7 +2197,17 @@ static void launch_bwd_chunked(hipStream_t st, int tbx, int tby, int H, int W, c
                                const float *colors, const float *opacity, const float *background,
                                const float *final_Ts, const int32_t *final_idx,
                                const float *v_output, const float *v_output_alpha,
-                               float alpha_max, float *rec, int chunk, const ChunkWs &w) {
+                               float alpha_max, float *rec, int chunk, const ChunkWs &w,
+                               unsigned long long *det = nullptr) {
+  if (g_det) {
+    hipLaunchKernelGGL((raster_bwd3p_kernel<1, true, 16, true, f2, true>),
+                       dim3((unsigned)cdiv(w.items_bound, (long long)(tiles_per_block<2, 16>()))),
+                       dim3(256), 0, st, tbx, tby, H, W, gids, (const int2 *)bins,
+                       (const float2 *)xys, conics, colors, opacity, background, final_Ts,
+                       final_idx, v_output, v_output_alpha, alpha_max, rec, false, chunk,
+                       w.item_off, w.item_tile, w.ckpt_off, w.ckpt, det);
+    return;
+  }
   if (!(g_bwd_flags & 4096)) {
     hipLaunchKernelGGL((raster_bwd3p_kernel<1, true, 16, true>),
                        dim3((unsigned)cdiv(w.items_bound, (long long)(tiles_per_block<2, 16>()))),
@@ -2168,11 +2260,17 @@ extern "C" int gsplat_rasterize_backward_chunked(
   if (num_points == 0) return check_launch("rasterize_backward_chunked");
   float *rec = (float *)workspace;
   note(hipMemsetAsync(rec, 0, need, st), "hipMemsetAsync");
+  unsigned long long *det = g_det ? det_buffer(num_points, st) : nullptr;
+  if (g_det && !det) return check_launch("rasterize_backward_chunked");
   launch_bwd_chunked(st, tile_bounds_x, tile_bounds_y, img_height, img_width,
                      gaussian_ids_sorted, tile_bins, xys, conics, colors, opacity, background,
-                     final_Ts, final_idx, v_output, v_output_alpha, alpha_max, rec, chunk, w);
+                     final_Ts, final_idx, v_output, v_output_alpha, alpha_max, rec, chunk, w, det);
+  if (det)
+    hipLaunchKernelGGL(det_finish_kernel, dim3(cdiv(num_points, 256)), dim3(256), 0, st,
+                       num_points, det, rec);
   hipLaunchKernelGGL(split_grads_kernel, dim3(cdiv(num_points, 256)), dim3(256), 0, st,
-                     num_points, (const float4 *)rec, 0.5f, v_xy, v_conic, v_colors, v_opacity);
+                     num_points, (const float4 *)rec, 0.5f, conic_y_scale(0.5f), v_xy, v_conic,
+                     v_colors, v_opacity);
   return check_launch("rasterize_backward_chunked");
 }
 
@@ -2206,6 +2304,13 @@ extern "C" int gsplat_rasterize_backward_records(
   if (num_points == 0 || num_intersects == 0) return check_launch("rasterize_backward_records");
   const int T = tile_bounds_x * tile_bounds_y;
   float *rec = (float *)records;
+  if (g_det && (g_bwd_flags & 4096)) {
+    set_error("rasterize_backward_records: deterministic mode needs the strip backward");
+    return 1;
+  }
+  // deterministic mode: the records' clear by the forward is superseded by the integer sums
+  unsigned long long *det = g_det ? det_buffer(num_points, st) : nullptr;
+  if (g_det && !det) return check_launch("rasterize_backward_records");
   if (chunk > 0) {
     const ChunkWs w = carve_chunk_ws(const_cast<void *>(checkpoints), T, num_intersects, chunk);
     if (!checkpoints || checkpoint_bytes < w.bytes) {
@@ -2215,7 +2320,12 @@ extern "C" int gsplat_rasterize_backward_records(
     }
     launch_bwd_chunked(st, tile_bounds_x, tile_bounds_y, img_height, img_width,
                        gaussian_ids_sorted, tile_bins, xys, conics, colors, opacity, background,
-                       final_Ts, final_idx, v_output, v_output_alpha, alpha_max, rec, chunk, w);
+                       final_Ts, final_idx, v_output, v_output_alpha, alpha_max, rec, chunk, w,
+                       det);
+  } else if (det) {
+    launch_bwd_det(st, tile_bounds_x, tile_bounds_y, img_height, img_width, gaussian_ids_sorted,
+                   tile_bins, xys, conics, colors, opacity, background, final_Ts, final_idx,
+                   v_output, v_output_alpha, alpha_max, rec, det);
   } else if (g_bwd_flags & 4096) {
     hipLaunchKernelGGL((raster_bwd4_kernel<false>), dim3(cdiv(T, 4)), dim3(256), 0, st,
                        tile_bounds_x, tile_bounds_y, img_height, img_width, gaussian_ids_sorted,
@@ -2229,5 +2339,8 @@ extern "C" int gsplat_rasterize_backward_records(
                        background, final_Ts, final_idx, v_output, v_output_alpha, alpha_max, rec,
                        false);
   }
+  if (det)
+    hipLaunchKernelGGL(det_finish_kernel, dim3(cdiv(num_points, 256)), dim3(256), 0, st,
+                       num_points, det, rec);
   return check_launch("rasterize_backward_records");
 }

@@ -30,9 +30,9 @@ import torch
 from torch import Tensor
 from torch.autograd import Function
 
-from . import _lib, exchange
+from . import _lib, exchange, quirks
 from .camera import GCCamera
-from .rasterize import BACKWARD_ALPHA_CLAMP, BLOCK_X, BLOCK_Y, bin_gaussians, last_num_visible
+from .rasterize import BLOCK_X, BLOCK_Y, bin_gaussians, last_num_visible
 
 _DEG_OF_BASES = {1: 0, 4: 1, 9: 2, 16: 3, 25: 4}
 
@@ -130,7 +130,8 @@ class _FusedRender(Function):
                               final_idx)
         ctx.set_materialize_grads(False)
         aux.update(xys=xys, radii=radii, depths=depths, num_intersects=num_intersects,
-                   records=rec, num_points=n)
+                   records=rec, num_points=n, conics=conics, colors=colors, opacity=opac,
+                   num_tiles_hit=nth)
         if return_alpha:
             return out_img, 1 - final_Ts
         return out_img
@@ -151,7 +152,7 @@ class _FusedRender(Function):
                 v_alpha = v_alpha.float().contiguous()
             _lib.call("gsplat_rasterize_backward_records", tbx, tby, H, W, n, P(gids), P(bins),
                       P(xys), P(conics), P(colors), P(opac), P(background), P(final_Ts),
-                      P(final_idx), P(v_img), P(v_alpha), float(BACKWARD_ALPHA_CLAMP), I, chunk,
+                      P(final_idx), P(v_img), P(v_alpha), quirks.backward_alpha_clamp(), I, chunk,
                       P(ctx.ckpt), ctx.ckpt.numel() if ctx.ckpt is not None else 0, P(rec),
                       rec.numel(), st)
         if ctx.adam is not None:
@@ -246,9 +247,28 @@ def render_fused(scene, cam: GCCamera, sh_degree_to_use: int, background: Tensor
         v = rec[:aux["num_points"] * 64].view(torch.float32).view(-1, 16)[:, :2]
         return torch.where(aux["radii"][:, None] > 0, v, torch.zeros_like(v))  # culled: 0
 
+    def raster_grads():
+        """After backward: the rasterizer-level gradients in gsplat's convention -- v_xy [N,2],
+        v_conic [N,3] (v_conic.y per the CONIC_HALF quirk), v_colors [N,3], v_opacity [N,1] --
+        i.e. what gsplat's rasterize_gaussians backward returns for this render; zero for
+        culled Gaussians.  None without records (no gradient requested)."""
+        rec = aux.get("records")
+        if rec is None:
+            return None
+        r = rec[:aux["num_points"] * 64].view(torch.float32).view(-1, 16)
+        cy = 0.5 if quirks.get() & quirks.CONIC_HALF else 1.0
+        scale = torch.tensor([1.0, 1.0, 0.5, cy, 0.5, 1.0, 1.0, 1.0, 1.0], device=r.device)
+        g = torch.where(aux["radii"][:, None] > 0, r[:, :9] * scale, torch.zeros_like(r[:, :9]))
+        return g[:, 0:2], g[:, 2:5], g[:, 5:8], g[:, 8:9]
+
     return {"rgb": rgb, "clamped": bool(clamp),
             "accumulation": alpha[..., None] if alpha is not None else None,
             "xys": aux["xys"], "radii": aux["radii"], "xys_grad": xys_grad,
+            "raster_grads": raster_grads,
+            # the rasterizer's inputs as the fused preprocess wrote them (the colours carry
+            # the clamp mask in their sign bit: -0.0, which no rasterizer sum can see)
+            "raster_inputs": {k: aux[k] for k in ("xys", "depths", "radii", "conics",
+                                                   "num_tiles_hit", "colors", "opacity")},
             "num_intersects": aux["num_intersects"]}
 
 

@@ -22,13 +22,9 @@ import torch
 from torch import Tensor
 from torch.autograd import Function
 
-from . import _lib
+from . import _lib, quirks
 
 BLOCK_X, BLOCK_Y = 16, 16
-
-# gsplat 0.1.x clamps alpha at 0.999 in the forward but at 0.99 in the backward
-# (SURVEY.md Appendix A10).  Kept for parity; set to 0.999 for the consistent gradient.
-BACKWARD_ALPHA_CLAMP = 0.99
 
 
 def rasterize_gaussians(
@@ -75,31 +71,59 @@ def rasterize_gaussians(
         img_width, background.contiguous(), return_alpha)
 
 
-_PINNED = {}
+class _CountSlots:
+    """Pinned host words the binning kernels write the (visible count, intersection count) of
+    one call into (pinned host memory is device-addressable on ROCm).  Every bin_gaussians
+    call takes a slot of its own for as long as it waits, so calls in flight on different
+    streams or threads never share a word: a queued scan of one call cannot overwrite the
+    count another call is polling."""
+
+    SLOTS = 64
+
+    def __init__(self):
+        import threading
+        self.lock = threading.Lock()
+        self.bufs = {}
+        self.busy = {}
+        self.last_visible = {}
+
+    def acquire(self, dev):
+        with self.lock:
+            if dev not in self.bufs:
+                buf = torch.zeros((self.SLOTS, 4), dtype=torch.int32, pin_memory=True)
+                self.bufs[dev] = (buf, buf.numpy())
+                self.busy[dev] = set()
+            busy = self.busy[dev]
+            free = next((k for k in range(self.SLOTS) if k not in busy), None)
+            if free is None:
+                raise RuntimeError(f"bin_gaussians: more than {self.SLOTS} calls in flight")
+            busy.add(free)
+            buf, host = self.bufs[dev]
+            host[free, :2] = -1
+            return free, buf[free], host[free]
+
+    def release(self, dev, slot, visible=None):
+        with self.lock:
+            self.busy[dev].discard(slot)
+            if visible is not None:
+                self.last_visible[dev] = visible
 
 
-def _pinned_counts(dev):
-    """A 2-int32 pinned host buffer per device (and its numpy view), written by the binning
-    kernels directly (pinned host memory is device-addressable on ROCm)."""
-    t = _PINNED.get(dev)
-    if t is None:
-        buf = torch.zeros(2, dtype=torch.int32, pin_memory=True)
-        t = _PINNED[dev] = (buf, buf.numpy())
-    return t
+_COUNTS = _CountSlots()
 
 
 def last_num_visible(dev) -> int:
-    """The visible-Gaussian count of this device's last bin_gaussians call (written by the
-    binning next to the intersection count; valid once that call has returned)."""
-    return int(_pinned_counts(dev)[1][0])
+    """The visible-Gaussian count of this device's last completed bin_gaussians call (written
+    by the binning next to the intersection count)."""
+    return int(_COUNTS.last_visible.get(dev, 0))
 
 
-def _wait_count(host, dev, spin_s: float = 2.0) -> int:
+def _wait_count(host, stream, spin_s: float = 2.0) -> int:
     """The single host sync of the binning (gsplat: cum_tiles_hit[-1].item()): the scan kernel
-    writes the intersection count once, straight into pinned host memory, so the host polls
-    that word (about a microsecond from the write to the read) instead of a copy kernel plus
-    a stream synchronisation (tens of microseconds of wake-up latency).  Falls back to a stream
-    synchronisation if nothing arrives within spin_s."""
+    writes the intersection count once, straight into this call's pinned slot, so the host
+    polls that word (about a microsecond from the write to the read) instead of a copy kernel
+    plus a stream synchronisation (tens of microseconds of wake-up latency).  Falls back to
+    synchronising the stream the binning was issued on if nothing arrives within spin_s."""
     t_end = None
     while True:
         v = int(host[1])
@@ -108,7 +132,7 @@ def _wait_count(host, dev, spin_s: float = 2.0) -> int:
         if t_end is None:
             t_end = time.perf_counter() + spin_s
         elif time.perf_counter() > t_end:
-            torch.cuda.current_stream(dev).synchronize()
+            stream.synchronize()
             v = int(host[1])
             if v == -1:
                 raise RuntimeError("bin_gaussians: the intersection count was never written")
@@ -133,19 +157,23 @@ def bin_gaussians(xys: Tensor, depths: Tensor, radii: Tensor, num_tiles_hit: Ten
     if n == 0:
         return 0, torch.empty((0,), device=dev, dtype=torch.int32), \
             torch.zeros((tbx * tby, 2), device=dev, dtype=torch.int32)
-    counts, host = _pinned_counts(dev)
     P, st = _lib.ptr, _lib.stream(dev)
     tile_bins = torch.empty((tbx * tby, 2), device=dev, dtype=torch.int32)
-    host[1] = -1  # the previous call's value has been consumed (its wait completed)
-    if keyed_workspace is not None:
-        ws1 = keyed_workspace
-        _lib.call("gsplat_bin_count_keyed", n, tbx, tby, P(counts), P(ws1), ws1.numel(), st)
-    else:
-        ws1 = torch.empty((_lib.query("gsplat_bin_count_workspace_size", n),), device=dev,
-                          dtype=torch.uint8)
-        _lib.call("gsplat_bin_count", n, P(xys), P(depths), P(radii), P(num_tiles_hit), tbx,
-                  tby, P(counts), P(ws1), ws1.numel(), st)
-    num_intersects = _wait_count(host, dev)
+    slot, counts, host = _COUNTS.acquire(dev)
+    visible = None
+    try:
+        if keyed_workspace is not None:
+            ws1 = keyed_workspace
+            _lib.call("gsplat_bin_count_keyed", n, tbx, tby, P(counts), P(ws1), ws1.numel(), st)
+        else:
+            ws1 = torch.empty((_lib.query("gsplat_bin_count_workspace_size", n),), device=dev,
+                              dtype=torch.uint8)
+            _lib.call("gsplat_bin_count", n, P(xys), P(depths), P(radii), P(num_tiles_hit), tbx,
+                      tby, P(counts), P(ws1), ws1.numel(), st)
+        num_intersects = _wait_count(host, torch.cuda.current_stream(dev))
+        visible = int(host[0])
+    finally:
+        _COUNTS.release(dev, slot, visible)
     gaussian_ids_sorted = torch.empty((max(num_intersects, 0),), device=dev, dtype=torch.int32)
     ws2 = torch.empty((_lib.query("gsplat_bin_emit_workspace_size_for", n, num_intersects, tbx,
                                   tby),), device=dev, dtype=torch.uint8)
@@ -345,14 +373,14 @@ class _RasterizeGaussians(Function):
                 _lib.call("gsplat_rasterize_backward_chunked", tbx, tby, H, W, num_points,
                           P(gaussian_ids_sorted), P(tile_bins), P(xys), P(conics), P(colors),
                           P(opacity), P(background), P(final_Ts), P(final_idx), P(v_out_img),
-                          P(v_out_alpha), float(BACKWARD_ALPHA_CLAMP), P(v_xy), P(v_conic),
+                          P(v_out_alpha), quirks.backward_alpha_clamp(), P(v_xy), P(v_conic),
                           P(v_colors), P(v_opacity), ctx.num_intersects, ctx.chunk,
                           P(ctx.ckpt), ctx.ckpt.numel(), P(ws), wsz, _lib.stream(dev))
             else:
                 _lib.call("gsplat_rasterize_backward", tbx, tby, H, W, C, num_points,
                           P(gaussian_ids_sorted), P(tile_bins), P(xys), P(conics), P(colors),
                           P(opacity), P(background), P(final_Ts), P(final_idx), P(v_out_img),
-                          P(v_out_alpha), float(BACKWARD_ALPHA_CLAMP), P(v_xy), P(v_conic),
+                          P(v_out_alpha), quirks.backward_alpha_clamp(), P(v_xy), P(v_conic),
                           P(v_colors), P(v_opacity), P(ws), wsz, _lib.stream(dev))
 
         return (

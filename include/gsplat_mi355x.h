@@ -41,10 +41,39 @@
 extern "C" {
 #endif
 
-#define GSPLAT_MI355X_ABI_VERSION 6
+#define GSPLAT_MI355X_ABI_VERSION 7
 
 int gsplat_abi_version(void);
 const char *gsplat_last_error(void);
+
+/* ---- gsplat 0.1.2.1 behaviours recalled but unverified (SURVEY.md Appendix A [VERIFY]) -
+ * One process-wide mask, read at each launch (default GSPLAT_QUIRKS_ALL = gsplat as recalled;
+ * the Python layer sets it from the GSPLAT_MI355X_QUIRKS environment variable).
+ *   ALPHA_099      A10: the rasterize backward clamps alpha at 0.99 (forward 0.999).  The
+ *                  callers pass that clamp as alpha_max; the bit records the choice.
+ *   CONIC_HALF     A7/A9: v_conic.y = 1/2 v_sigma dx dy, paired with a conic VJP taking it as
+ *                  the gradient of each symmetric entry; off: v_conic.y = d loss / d conic.y.
+ *                  Gradients of means/scales/quats are identical either way.
+ *   EWA_UNCLAMPED  A6: the EWA VJP recomputes t without the 1.3 tan_fov clamp; off: the
+ *                  derivative of the clamped forward.
+ * Replaces no gsplat entry point: gsplat has these behaviours hard-coded in
+ * gsplat/cuda/csrc/{backward.cu, helpers.cuh}. */
+#define GSPLAT_QUIRK_ALPHA_099 1
+#define GSPLAT_QUIRK_CONIC_HALF 2
+#define GSPLAT_QUIRK_EWA_UNCLAMPED 4
+#define GSPLAT_QUIRKS_ALL 7
+int gsplat_set_quirks(int mask);
+int gsplat_get_quirks(void);
+
+/* ---- deterministic backward (debugging) -------------------------------
+ * on != 0: the C = 3 rasterize backward entries (gsplat_rasterize_backward,
+ * _backward_chunked, _backward_records) add every wave's per-Gaussian totals as 64-bit
+ * fixed-point integers (2^-32 units) instead of fp32 atomics, then convert: gradients are
+ * bit-identical from run to run.  Slower (integer atomics, an extra pass over N); the
+ * accumulator buffer is allocated by the library on first use (debug mode only).  Replaces no
+ * gsplat entry point (gsplat's backward.cu atomics are order-nondeterministic). */
+int gsplat_set_deterministic(int on);
+int gsplat_get_deterministic(void);
 
 /* ---- projection (forward.cu / backward.cu project_gaussians_*) ----------------------
  * means3d [N,3], scales [N,3], quats [N,4] (w,x,y,z), viewmat >= 12 floats (row-major

@@ -45,6 +45,18 @@
 
 #define BLOCK 16
 
+/* gsplat 0.1.2.1 behaviours recalled but unverified (SURVEY.md Appendix A [VERIFY]), the same
+ * bits as include/gsplat_mi355x.h GSPLAT_QUIRK_* (the HIP library's gsplat_set_quirks):
+ *   1 ALPHA_099      A10 backward alpha clamp 0.99 -- applied by the callers' alpha_max
+ *   2 CONIC_HALF     A7/A9 v_conic.y = 1/2 v_sigma dx dy with the matching conic VJP
+ *   4 EWA_UNCLAMPED  A6 EWA VJP without the 1.3 tan_fov clamp
+ * Default: all (gsplat as recalled). */
+#define Q_CONIC_HALF 2
+#define Q_EWA_UNCLAMPED 4
+static int g_quirks = 7;
+void oracle_set_quirks(int mask) { g_quirks = mask; }
+int oracle_get_quirks(void) { return g_quirks; }
+
 /* ---------------------------------------------------------------- helpers */
 
 /* float->int conversion with the GPU's saturating semantics (v_cvt_i32_f32 / PTX
@@ -223,9 +235,12 @@ void oracle_project_forward(int n, const float *means, const float *scales, floa
 
 /* cov2d_to_conic_vjp (helpers.cuh) */
 static void cov2d_to_conic_vjp(const float *conic, const float *v_conic, float *v_cov2d) {
-    /* X = [[a,b],[b,c]], G = [[va,vb],[vb,vc]], v_Sigma = -X G X */
+    /* X = [[a,b],[b,c]], G = [[va,vb],[vb,vc]], v_Sigma = -X G X.  G holds the gradient of
+     * each symmetric entry: gsplat's halved v_conic.y as is (CONIC_HALF), else half of
+     * d loss / d conic.y. */
     float a = conic[0], b = conic[1], c = conic[2];
     float ga = v_conic[0], gb = v_conic[1], gc = v_conic[2];
+    if (!(g_quirks & Q_CONIC_HALF)) gb = 0.5f * gb;
     /* XG */
     float xg00 = a * ga + b * gb, xg01 = a * gb + b * gc;
     float xg10 = b * ga + c * gb, xg11 = b * gb + c * gc;
@@ -251,14 +266,25 @@ static void project_pix_vjp(const float *P, const float *p, int W, int H, const 
     v_mean[2] = P[2] * vpx + P[6] * vpy + P[10] * vpz;
 }
 
-/* project_cov3d_ewa_vjp (helpers.cuh): t is recomputed WITHOUT the fov clamp. */
+/* project_cov3d_ewa_vjp (helpers.cuh): t is recomputed WITHOUT the fov clamp
+ * (EWA_UNCLAMPED); otherwise the derivative of the clamped forward: t_x = t_z clamp(t_x/t_z)
+ * passes d/dt_x inside the clamp and +-lim d/dt_z outside it. */
 static void project_cov3d_ewa_vjp(const float *mean, const float *cov3d, const float *vm,
-                                  float fx, float fy, const float *v_cov2d, float *v_mean,
-                                  float *v_cov3d) {
+                                  float fx, float fy, float tan_fovx, float tan_fovy,
+                                  const float *v_cov2d, float *v_mean, float *v_cov3d) {
     float W[9] = {vm[0], vm[1], vm[2], vm[4], vm[5], vm[6], vm[8], vm[9], vm[10]};
     float tx = vm[0] * mean[0] + vm[1] * mean[1] + vm[2] * mean[2] + vm[3];
     float ty = vm[4] * mean[0] + vm[5] * mean[1] + vm[6] * mean[2] + vm[7];
     float tz = vm[8] * mean[0] + vm[9] * mean[1] + vm[10] * mean[2] + vm[11];
+    int clamped = !(g_quirks & Q_EWA_UNCLAMPED);
+    float limx = 1.3f * tan_fovx, limy = 1.3f * tan_fovy, sx = 0.f, sy = 0.f;
+    if (clamped) {
+        float ux = tx / tz, uy = ty / tz;
+        sx = ux < -limx ? -limx : (ux > limx ? limx : 0.f);
+        sy = uy < -limy ? -limy : (uy > limy ? limy : 0.f);
+        tx = tz * fminf(limx, fmaxf(-limx, ux));
+        ty = tz * fminf(limy, fmaxf(-limy, uy));
+    }
     float rz = 1.f / tz;
     float rz2 = rz * rz;
     float rz3 = rz2 * rz;
@@ -299,6 +325,10 @@ static void project_cov3d_ewa_vjp(const float *mean, const float *cov3d, const f
     float vt1 = -fy * rz2 * vJ21;
     float vt2 = -fx * rz2 * vJ00 + 2.f * fx * tx * rz3 * vJ20 - fy * rz2 * vJ11 +
                 2.f * fy * ty * rz3 * vJ21;
+    if (clamped) {
+        if (sx != 0.f) { vt2 += sx * vt0; vt0 = 0.f; }
+        if (sy != 0.f) { vt2 += sy * vt1; vt1 = 0.f; }
+    }
     /* v_mean += W^T v_t  (glm dot(v_t, W[c]) with W[c] = column c of W) */
     v_mean[0] += vt0 * W[0] + vt1 * W[3] + vt2 * W[6];
     v_mean[1] += vt0 * W[1] + vt1 * W[4] + vt2 * W[7];
@@ -354,6 +384,8 @@ void oracle_project_backward(int n, const float *means, const float *scales, flo
                              float *v_quat) {
     (void)cx;
     (void)cy;
+    float tan_fovx = (float)(0.5 * (double)W / (double)fx);
+    float tan_fovy = (float)(0.5 * (double)H / (double)fy);
     for (int i = 0; i < n; ++i) {
         if (radii[i] <= 0) continue;
         const float *p = means + 3 * i;
@@ -364,8 +396,8 @@ void oracle_project_backward(int n, const float *means, const float *scales, flo
         vm[1] += viewmat[9] * vz;
         vm[2] += viewmat[10] * vz;
         cov2d_to_conic_vjp(conics + 3 * i, v_conic + 3 * i, v_cov2d + 3 * i);
-        project_cov3d_ewa_vjp(p, cov3d + 6 * i, viewmat, fx, fy, v_cov2d + 3 * i, vm,
-                              v_cov3d + 6 * i);
+        project_cov3d_ewa_vjp(p, cov3d + 6 * i, viewmat, fx, fy, tan_fovx, tan_fovy,
+                              v_cov2d + 3 * i, vm, v_cov3d + 6 * i);
         scale_rot_to_cov3d_vjp(scales + 3 * i, glob_scale, quats + 4 * i, v_cov3d + 6 * i,
                                v_scale + 3 * i, v_quat + 4 * i);
     }
@@ -614,6 +646,8 @@ void oracle_rasterize_backward(int tbx, int tby, int H, int W, int C, int num_po
     /* abs_sum (optional, [num_points, 6+C] in the order xy0 xy1 con0 con1 con2 opac colors):
      * the sum of |term| over the per-pixel contributions of each gradient element -- the
      * scale of the fp32 summation error any implementation accumulating in fp32 incurs. */
+    /* gsplat's v_conic.y carries 1/2 (CONIC_HALF); else d sigma / d conic.y = dx dy */
+    const float hb = (g_quirks & Q_CONIC_HALF) ? 0.5f : 1.0f;
     double *acc = (double *)calloc((size_t)num_points * (9 + (size_t)C), sizeof(double));
     double *aacc = abs_sum ? (double *)calloc((size_t)num_points * (9 + (size_t)C),
                                               sizeof(double))
@@ -667,14 +701,14 @@ void oracle_rasterize_backward(int tbx, int tby, int H, int W, int C, int num_po
                     a[0] += (double)(v_sigma * (cn[0] * dx + cn[1] * dy));
                     a[1] += (double)(v_sigma * (cn[1] * dx + cn[2] * dy));
                     a[2] += (double)(0.5f * v_sigma * dx * dx);
-                    a[3] += (double)(0.5f * v_sigma * dx * dy);
+                    a[3] += (double)(hb * v_sigma * dx * dy);
                     a[4] += (double)(0.5f * v_sigma * dy * dy);
                     a[5] += (double)(vis * v_alpha);
                     if (aa) {
                         aa[0] += fabs((double)(v_sigma * (cn[0] * dx + cn[1] * dy)));
                         aa[1] += fabs((double)(v_sigma * (cn[1] * dx + cn[2] * dy)));
                         aa[2] += fabs((double)(0.5f * v_sigma * dx * dx));
-                        aa[3] += fabs((double)(0.5f * v_sigma * dx * dy));
+                        aa[3] += fabs((double)(hb * v_sigma * dx * dy));
                         aa[4] += fabs((double)(0.5f * v_sigma * dy * dy));
                         aa[5] += fabs((double)(vis * v_alpha));
                     }

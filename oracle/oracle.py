@@ -58,6 +58,24 @@ def _p(a):
     raise TypeError(a.dtype)
 
 
+# gsplat 0.1.2.1 [VERIFY] behaviours (include/gsplat_mi355x.h GSPLAT_QUIRK_*): same bits as the
+# HIP library's gsplat_set_quirks.  ALPHA_099 is applied through alpha_max by the callers.
+QUIRK_ALPHA_099, QUIRK_CONIC_HALF, QUIRK_EWA_UNCLAMPED, QUIRKS_ALL = 1, 2, 4, 7
+
+
+def set_quirks(mask: int) -> None:
+    lib().oracle_set_quirks(int(mask))
+
+
+def get_quirks() -> int:
+    return int(lib().oracle_get_quirks())
+
+
+def backward_alpha_clamp(mask=None) -> float:
+    mask = get_quirks() if mask is None else mask
+    return 0.99 if mask & QUIRK_ALPHA_099 else 0.999
+
+
 def num_sh_bases(degree: int) -> int:
     return {0: 1, 1: 4, 2: 9, 3: 16}.get(degree, 25)
 

@@ -28,6 +28,15 @@ import torch
 BLOCK = 16
 
 
+def _quirk_flags(quirks):
+    """(A5, A6, A8) straight-throughs from quirks: a bool switches all three; an int is the
+    library's GSPLAT_QUIRK_* mask, whose EWA_UNCLAMPED bit (4) selects A6 (A5 and A8 are not
+    switchable in the kernels and stay on)."""
+    if isinstance(quirks, bool):
+        return quirks, quirks, quirks
+    return True, bool(int(quirks) & 4), True
+
+
 def quat_to_rotmat(q, quirks=True):
     n = q.norm(dim=-1, keepdim=True)
     if quirks:
@@ -52,12 +61,13 @@ def project(means, scales, glob_scale, quats, viewmat, projmat, fx, fy, cx, cy, 
             tile_bounds, clip_thresh=0.01, quirks=True):
     """Returns xys, depths, radii, conics, num_tiles_hit, cov3d (gsplat layout) plus the
     visibility mask.  Culled entries are zero, like gsplat's zero-initialised outputs."""
+    q5, q6, q8 = _quirk_flags(quirks)
     dt = means.dtype
     vm = viewmat.reshape(-1)[:12].reshape(3, 4).to(dt)
     Pm = projmat.reshape(4, 4).to(dt)
     Wr, tv = vm[:, :3], vm[:, 3]
     t = means @ Wr.T + tv
-    V = cov3d_full(scales, glob_scale, quats, quirks)
+    V = cov3d_full(scales, glob_scale, quats, q8)
     tan_fovx = 0.5 * W / fx
     tan_fovy = 0.5 * H / fy
     lim_x, lim_y = 1.3 * tan_fovx, 1.3 * tan_fovy
@@ -72,7 +82,7 @@ def project(means, scales, glob_scale, quats, viewmat, projmat, fx, fy, cx, cy, 
             torch.stack([z0, fy / tz, -fy * ty / tz ** 2], -1)], -2)
 
     Jc = jac(txc, tyc)
-    if quirks:
+    if q6:
         Ju = jac(t[:, 0], t[:, 1])
         J = Ju + (Jc - Ju).detach()
     else:
@@ -91,7 +101,7 @@ def project(means, scales, glob_scale, quats, viewmat, projmat, fx, fy, cx, cy, 
         radius = torch.ceil(3 * torch.sqrt(torch.maximum(v1, v2)))
     ph = torch.cat([means, torch.ones_like(means[:, :1])], -1) @ Pm.T
     rw = 1.0 / (ph[:, 3] + 1e-6)
-    if quirks:
+    if q5:
         rw = rw.detach()
     xy = torch.stack([0.5 * W * ph[:, 0] * rw + cx - 0.5, 0.5 * H * ph[:, 1] * rw + cy - 0.5],
                      -1)
@@ -207,3 +217,133 @@ def rasterize(xys, depths, radii, conics, num_tiles_hit, colors, opacity, H, W, 
         T = torch.where(ok, next_T, T)
     img = acc + T[:, None] * background.to(dt)[None, :]
     return img.reshape(H, W, C), (1 - T).reshape(H, W)
+
+
+def bin_and_sort(xys, depths, radii, tile_bounds):
+    """gsplat's map_gaussian_to_intersects + sort + get_tile_bin_edges in plain torch (CPU
+    baseline; the C oracle is the parity checker).  Key = tile << 32 | depth bits, sorted
+    stably (ties by Gaussian id).  Returns (gaussian_ids_sorted [I] int64, tile_bins [T,2])."""
+    tbx, tby = int(tile_bounds[0]), int(tile_bounds[1])
+    vis = radii > 0
+    ids = torch.nonzero(vis).reshape(-1)
+    x = xys[ids].float()
+    r = radii[ids].float()
+    t0x = torch.clamp(torch.trunc(x[:, 0] / BLOCK - r / BLOCK), 0, tbx).long()
+    t1x = torch.clamp(torch.trunc(x[:, 0] / BLOCK + r / BLOCK + 1), 0, tbx).long()
+    t0y = torch.clamp(torch.trunc(x[:, 1] / BLOCK - r / BLOCK), 0, tby).long()
+    t1y = torch.clamp(torch.trunc(x[:, 1] / BLOCK + r / BLOCK + 1), 0, tby).long()
+    wx, wy = t1x - t0x, t1y - t0y
+    cnt = wx * wy
+    keep = cnt > 0
+    ids, t0x, t0y, wx, cnt = ids[keep], t0x[keep], t0y[keep], wx[keep], cnt[keep]
+    g = torch.repeat_interleave(torch.arange(ids.numel()), cnt)
+    start = torch.cumsum(cnt, 0) - cnt
+    k = torch.arange(g.numel()) - start[g]
+    tile = (t0y[g] + k // wx[g]) * tbx + t0x[g] + k % wx[g]
+    dbits = depths[ids].float().contiguous().view(torch.int32).long() & 0xFFFFFFFF
+    key = (tile << 32) | dbits[g]
+    key, order = torch.sort(key, stable=True)
+    gids = ids[g][order]
+    tiles_sorted = key >> 32
+    T = tbx * tby
+    first = torch.searchsorted(tiles_sorted, torch.arange(T))
+    last = torch.searchsorted(tiles_sorted, torch.arange(T), right=True)
+    return gids, torch.stack([first, last], -1)
+
+
+def rasterize_tiles(xys, conics, colors, opacity, background, gids_sorted, tile_bins, tiles,
+                    tile_bounds, H, W):
+    """Per-pixel front-to-back compositing of the listed tiles, vectorised over
+    each tile's [list, pixel] pairs: alpha for every pair, the transmittance as a running
+    product down the list, gsplat's termination (the first Gaussian with T(1 - alpha) <= 1e-4
+    and everything behind it dropped).  Differentiable in xys, conics, colors and opacity.
+    Returns [(flat pixel indices, img [p, C], alpha [p])] per tile."""
+    out = []
+    tbx = int(tile_bounds[0])
+    op_all = opacity.reshape(-1)
+    for t in tiles:
+        ty, tx = divmod(int(t), tbx)
+        iy, ix = torch.meshgrid(torch.arange(ty * BLOCK, min(ty * BLOCK + BLOCK, H)),
+                                torch.arange(tx * BLOCK, min(tx * BLOCK + BLOCK, W)),
+                                indexing="ij")
+        px, py = ix.reshape(-1).to(xys.dtype), iy.reshape(-1).to(xys.dtype)
+        lo, hi = int(tile_bins[t, 0]), int(tile_bins[t, 1])
+        C = colors.shape[1]
+        if hi <= lo:
+            T = torch.ones_like(px)
+            out.append((iy.reshape(-1) * W + ix.reshape(-1),
+                        T[:, None] * background[None, :].to(xys.dtype), 1 - T))
+            continue
+        ids = gids_sorted[lo:hi].long()
+        g = xys[ids]
+        cn = conics[ids]
+        dx = g[:, :1] - px[None, :]
+        dy = g[:, 1:2] - py[None, :]
+        sigma = 0.5 * (cn[:, :1] * dx * dx + cn[:, 2:3] * dy * dy) + cn[:, 1:2] * dx * dy
+        alpha = torch.clamp(op_all[ids][:, None] * torch.exp(-sigma), max=0.999)
+        ok = (sigma >= 0) & (alpha >= 1.0 / 255.0)
+        a = torch.where(ok, alpha, torch.zeros_like(alpha))
+        T_after = torch.cumprod(1 - a, 0)
+        T_before = torch.cat([torch.ones_like(T_after[:1]), T_after[:-1]], 0)
+        term = ok & (T_after <= 1e-4)
+        alive = torch.cumsum(term.to(torch.int32), 0) == 0
+        w = a * T_before * alive
+        T_fin = torch.prod(torch.where(alive, 1 - a, torch.ones_like(a)), 0)
+        img = w.t() @ colors[ids] + T_fin[:, None] * background[None, :].to(xys.dtype)
+        out.append((iy.reshape(-1) * W + ix.reshape(-1), img.reshape(-1, C), 1 - T_fin))
+    return out
+
+
+def render_fwd_bwd_sampled(means, scales, quats, opacities, features_dc, features_rest,
+                           viewmat, projmat, campos, fx, fy, cx, cy, H, W, sh_degree,
+                           n_tiles=64, seed=0, backward=True):
+    """The CPU baseline of BASELINE.json / north_star: the whole per-view fwd+bwd render in
+    plain PyTorch on the host cores -- gc_model.py's activations (:172-203), projection,
+    SH, binning (torch.sort), the naive per-pixel compositing above and the autograd
+    backward of all of it -- with the compositing timed on `n_tiles` seeded random tiles and
+    extrapolated by the tile count.  Returns (seconds per view, detail dict)."""
+    import time
+    tb = ((W + BLOCK - 1) // BLOCK, (H + BLOCK - 1) // BLOCK, 1)
+    T = tb[0] * tb[1]
+    params = [p.detach().clone().requires_grad_() for p in
+              (means, scales, quats, opacities, features_dc, features_rest)]
+    m, s, q, o, dc, rest = params
+    t0 = time.perf_counter()
+    pr = project(m, torch.exp(s), 1.0, q / q.norm(dim=-1, keepdim=True), viewmat, projmat,
+                 fx, fy, cx, cy, H, W, tb)
+    coeffs = torch.cat([dc[:, None], rest], 1)
+    if sh_degree > 0:
+        vd = m.detach() - campos
+        vd = vd / vd.norm(dim=-1, keepdim=True)
+        rgb = torch.clamp(spherical_harmonics(sh_degree, vd, coeffs) + 0.5, min=0.0)
+    else:
+        rgb = torch.sigmoid(dc)
+    opac = torch.sigmoid(o)
+    with torch.no_grad():
+        gids, bins = bin_and_sort(pr["xys"], pr["depths"], pr["radii"], tb)
+    t_gauss = time.perf_counter() - t0
+    tiles = torch.randperm(T, generator=torch.Generator().manual_seed(seed))[:n_tiles]
+    bg = torch.zeros(3, dtype=m.dtype)
+    # the compositing's inputs as leaves, so its backward is timed apart from the
+    # per-Gaussian VJPs (those run once over all N; the tiles' part is extrapolated)
+    mid = [pr["xys"], pr["conics"], rgb, opac]
+    leaf = [t.detach().requires_grad_() for t in mid]
+    t0 = time.perf_counter()
+    outs = rasterize_tiles(*leaf, bg, gids, bins, tiles.tolist(), tb, H, W)
+    gen = torch.Generator().manual_seed(seed + 1)
+    loss = sum((img * torch.rand(img.shape, generator=gen)).sum() + al.sum()
+               for _, img, al in outs)
+    t_fwd_tiles = time.perf_counter() - t0
+    t_bwd_tiles = t_bwd_gauss = 0.0
+    if backward:
+        t0 = time.perf_counter()
+        loss.backward()
+        t_bwd_tiles = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        torch.autograd.backward(mid, [t.grad for t in leaf])
+        t_bwd_gauss = time.perf_counter() - t0
+    scale = T / len(tiles)
+    total = t_gauss + t_bwd_gauss + (t_fwd_tiles + t_bwd_tiles) * scale
+    return total, dict(t_gauss=t_gauss + t_bwd_gauss, t_tiles=t_fwd_tiles + t_bwd_tiles,
+                       tiles=len(tiles), scale=scale, intersects=int(gids.numel()),
+                       grads=[p.grad for p in params])

@@ -17,7 +17,10 @@ import oracle as O  # noqa: E402
 
 from gaussctrl_exp_amd import exchange  # noqa: E402
 
-BACKWARD_ALPHA_CLAMP = 0.99
+
+def _alpha_max():
+    from gaussctrl_exp_amd import quirks
+    return quirks.backward_alpha_clamp()
 
 
 def _np(t):
@@ -94,7 +97,7 @@ class _Raster(torch.autograd.Function):
             v_alpha = torch.zeros_like(v_img[..., 0])
         v_xy, v_conic, v_colors, v_opac = O.render_backward(
             ctx.f, _np(xys), _np(conics), _np(colors), _np(opacity), _np(background),
-            _np(v_img), _np(v_alpha), alpha_max=BACKWARD_ALPHA_CLAMP)
+            _np(v_img), _np(v_alpha), alpha_max=_alpha_max())
         return (torch.from_numpy(v_xy), None, None, torch.from_numpy(v_conic), None,
                 torch.from_numpy(v_colors), torch.from_numpy(v_opac).reshape(ctx.opacity_shape),
                 None, None, None, None)

@@ -52,10 +52,32 @@ def test_binding_arities_match_the_header():
 
 def test_host_queries_without_gpu():
     from gaussctrl_exp_amd import _lib
-    assert _lib.lib().gsplat_abi_version() == _lib.ABI_VERSION == 6
+    assert _lib.lib().gsplat_abi_version() == _lib.ABI_VERSION == 7
     assert _lib.query("gsplat_bin_count_workspace_size", 1000) > 1000 * 16
     assert _lib.query("gsplat_bin_emit_workspace_size", 10 ** 6) >= 5 * 4 * 10 ** 6
     assert _lib.query("gsplat_sort_isect_pairs_workspace_size", 0) > 0
+
+
+def test_quirk_switch_reaches_the_library():
+    """GSPLAT_MI355X_QUIRKS / quirks.set select the [VERIFY] behaviours in the library."""
+    from gaussctrl_exp_amd import _lib, quirks
+    L = _lib.lib()
+    assert L.gsplat_get_quirks() == quirks.get()
+    prev = quirks.set("none")
+    try:
+        assert L.gsplat_get_quirks() == 0 and quirks.backward_alpha_clamp() == 0.999
+        quirks.set("-ewa_unclamped")
+        assert L.gsplat_get_quirks() == quirks.ALPHA_099 | quirks.CONIC_HALF
+        assert quirks.backward_alpha_clamp() == 0.99
+        quirks.set("conic_half,ewa_unclamped")
+        assert L.gsplat_get_quirks() == 6
+        with pytest.raises(ValueError):
+            quirks.set("no_such_quirk")
+        with pytest.raises(RuntimeError, match="unknown bits"):
+            _lib.call("gsplat_set_quirks", 8)
+    finally:
+        quirks.set(prev)
+    assert L.gsplat_get_quirks() == prev
 
 
 def test_bad_arguments_are_rejected_before_launch():

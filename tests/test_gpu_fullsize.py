@@ -16,7 +16,7 @@ import torch
 
 import bench
 import oracle as O
-from gaussctrl_exp_amd import _lib
+from gaussctrl_exp_amd import _lib, quirks
 from gaussctrl_exp_amd import rasterize as R
 from gaussctrl_exp_amd.project_gaussians import project_gaussians
 from gaussctrl_exp_amd.rasterize import bin_gaussians
@@ -30,10 +30,12 @@ def _np(t):
     return t.detach().cpu().numpy()
 
 
-@pytest.fixture(scope="module", params=["headline", "c3"])
+@pytest.fixture(scope="module", params=["headline", "c3", "c4", "c5"])
 def headline(request, gpu, oracle_lib):
-    """The headline scene, and the bear scene at 512x512 (c3: few tiles, imbalanced lists --
-    the list-split backward is on there)."""
+    """The headline scene; the bear scene at 512x512 (c3: few tiles, imbalanced lists -- the
+    list-split backward is on there); garden 2M at 1080^2 (c4: real-scene layout, ~45 % of the
+    Gaussians culled); 5M at 2048^2 (c5: 83M intersections, 16-key sort passes, the heaviest
+    atomic contention)."""
     sc, cam = bench.make_workload(request.param, 0, gpu)
     cam = cam.to(gpu)
     with torch.no_grad():
@@ -46,7 +48,7 @@ def headline(request, gpu, oracle_lib):
     colors = torch.rand(xys.shape[0], 3, generator=gen)
     opac = torch.sigmoid(sc.opacities.detach().cpu())
     return dict(cam=cam, xys=xys, depths=depths, radii=radii, conics=conics, nth=nth, ref=ref,
-                colors=colors, opac=opac)
+                colors=colors, opac=opac, config=request.param)
 
 
 @pytest.mark.parametrize("scheme", ["rts", "onesweep", "bucket"])
@@ -55,6 +57,8 @@ def test_headline_binning_bitexact(gpu, headline, scheme):
     the tile-bucketing scheme (per-tile LDS sort): all bit-exact."""
     h, cam = headline, headline["cam"]
     assert h["ref"]["num_intersects"] > 1 << 20
+    if scheme != "rts" and h["config"] in ("c4", "c5"):
+        pytest.skip("ablation schemes: headline and c3 only")
     _lib.call("gsplat_debug_sort_scheme", 0 if scheme == "onesweep" else 1)
     _lib.call("gsplat_debug_binning_scheme", 1 if scheme == "bucket" else 0)
     try:
@@ -82,7 +86,8 @@ def test_headline_raster_on_sampled_tiles(gpu, headline):
     h, cam = headline, headline["cam"]
     H, W, tb = cam.height, cam.width, cam.tile_bounds
     T = tb[0] * tb[1]
-    tiles = np.random.default_rng(3).choice(T, size=48, replace=False).astype(np.int32)
+    tiles = np.random.default_rng(3).choice(T, size=24 if h["config"] == "c5" else 48,
+                                            replace=False).astype(np.int32)
     mask = _tile_pixel_mask(cam, tiles)
     bg = torch.tensor([0.3, 0.2, 0.1])
     xy = h["xys"].clone().requires_grad_()
@@ -101,8 +106,10 @@ def test_headline_raster_on_sampled_tiles(gpu, headline):
     got = _np(img)[mask]
     want = rimg[mask]
     bad = np.abs(got - want) > ATOL + RTOL * np.abs(want)
-    assert bad.mean() <= 1e-3, f"{bad.mean():.2e} of sampled pixels out of tolerance"
-    assert np.abs(_np(alpha)[mask] - (1 - rT[mask])).max() < 1e-4
+    assert not bad.any(), f"{bad.mean():.2e} of sampled pixels out of tolerance " \
+                          f"(max {np.abs(got - want).max():.3e})"
+    da = np.abs(_np(alpha)[mask] - (1 - rT[mask]))
+    assert not (da > ATOL + RTOL * (1 - rT[mask])).any(), f"alpha: max {da.max():.3e}"
     # backward: upstream gradient only on the sampled tiles
     gen = torch.Generator().manual_seed(9)
     v_img = torch.randn(H, W, 3, generator=gen) * torch.from_numpy(mask)[..., None]
@@ -122,15 +129,11 @@ def test_headline_raster_on_sampled_tiles(gpu, headline):
                                         _np(h["xys"]), _np(h["conics"]), h["colors"].numpy(),
                                         h["opac"].numpy(), bg.numpy(), _np(fT2), _np(fi),
                                         v_img.numpy(), v_alpha.numpy(),
-                                        alpha_max=R.BACKWARD_ALPHA_CLAMP, tile_list=tiles,
+                                        alpha_max=quirks.backward_alpha_clamp(), tile_list=tiles,
                                         return_abs=True)
-    # gsplat (and the oracle) recover each Gaussian's T by dividing T_final back through
-    # every later Gaussian of the tile: fp32 drift up to ~L 2^-24 relative for a list of L.
-    # The list-split backward (on for 512x512 frames) starts each 256-position chunk from
-    # the forward's recorded T instead, so it may differ from the oracle by that drift.
-    split = _lib.query("gsplat_rasterize_chunk_size", tb[0], tb[1], I) > 0
-    lmax = int((ref["tile_bins"][:, 1] - ref["tile_bins"][:, 0]).max())
-    drift = lmax * 2.0 ** -24 if split else 0.0
+    # transmittance-recovery drift over the sampled tiles' lists (tests/parity.py)
+    from parity import recovery_drift
+    drift = recovery_drift(ref["tile_bins"], tiles)
     for k, (name, g) in enumerate((("xys", xy.grad), ("conics", cn.grad), ("colors", col.grad),
                                    ("opacity", op.grad))):
         a = _np(g).astype(np.float64)

@@ -70,8 +70,16 @@ def _worker(rank, world, port, out_dir, mode):
 
 @pytest.mark.parametrize("mode,world", [("sh_views", 2), ("allreduce", 2), ("sh_views", 4)])
 def test_fused_ranks_sum_the_view_gradients(tmp_path, mode, world):
+    from gaussctrl_exp_amd import _lib
+    from parity import assert_close
     port = _free_port()
-    mp.spawn(_worker, args=(world, port, str(tmp_path), mode), nprocs=world, join=True)
+    # deterministic rasterizer backward in every process: the per-view reference below then
+    # has the very raster gradients the ranks summed, and the bar needs no outlier allowance
+    os.environ["GSPLAT_MI355X_DETERMINISTIC"] = "1"
+    try:
+        mp.spawn(_worker, args=(world, port, str(tmp_path), mode), nprocs=world, join=True)
+    finally:
+        os.environ.pop("GSPLAT_MI355X_DETERMINISTIC", None)
     g0 = np.load(tmp_path / "grad0.npy")
     for r in range(1, world):  # every rank holds the same summed gradients and parameters
         np.testing.assert_array_equal(np.load(tmp_path / f"grad{r}.npy"), g0)
@@ -80,11 +88,14 @@ def test_fused_ranks_sum_the_view_gradients(tmp_path, mode, world):
     from gaussctrl_exp_amd.train import TrainStep
     dev = torch.device("cuda:0")
     ref = 0
-    for r in range(world):
-        t = TrainStep(_scene(dev), sh_degree=3, world_size=1, loss="l1", render_mode="fused")
-        t.step(_views(dev)[r], _gt(r, dev), background=torch.tensor(BG, device=dev),
-               optimizer=False)
-        ref = ref + t.flat_grad().cpu().numpy()
+    prev = _lib.set_deterministic(True)
+    try:
+        for r in range(world):
+            t = TrainStep(_scene(dev), sh_degree=3, world_size=1, loss="l1", render_mode="fused")
+            t.step(_views(dev)[r], _gt(r, dev), background=torch.tensor(BG, device=dev),
+                   optimizer=False)
+            ref = ref + t.flat_grad().cpu().numpy()
+    finally:
+        _lib.set_deterministic(prev)
     assert np.abs(ref).max() > 0
-    bad = ~np.isclose(g0, ref, rtol=1e-4, atol=1e-6)
-    assert bad.mean() <= 1e-4, f"{bad.mean():.2e} differ (max {np.abs(g0 - ref).max():.3e})"
+    assert_close("summed view gradients", g0, ref, atol=1e-6, rtol=1e-4)

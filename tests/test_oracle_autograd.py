@@ -47,10 +47,31 @@ def test_project_forward_matches_torch(oracle_lib):
                                atol=1e-8)
 
 
-@pytest.mark.parametrize("seed", [0, 1])
-def test_project_backward_matches_autograd(oracle_lib, seed):
+def _wide(sc, scales):
+    """x spread to [-3.6, 3.6] at depths 2.8-5.2 (|x/z| up to ~1.3, past the clamp at 0.61) and
+    4x larger Gaussians, so some beyond the clamp still reach into the image."""
+    sc.means = sc.means * torch.tensor([3.0, 1.0, 1.0])
+    return sc, scales * 4
+
+
+@pytest.fixture
+def quirk_mask(oracle_lib, request):
+    """Run the oracle under GSPLAT_QUIRK_* mask request.param, restoring the default after."""
+    prev = oracle_lib.get_quirks()
+    oracle_lib.set_quirks(request.param)
+    yield request.param
+    oracle_lib.set_quirks(prev)
+
+
+# all gsplat quirks, none, and each of the switchable VJP conventions alone
+@pytest.mark.parametrize("quirk_mask", [7, 0, 2, 4], indirect=True)
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_project_backward_matches_autograd(oracle_lib, seed, quirk_mask):
     O = oracle_lib
-    sc, cam, scales, quats, _ = _setup(seed=seed)
+    # seed 2: a scene spread sideways, so part of it lies beyond the 1.3 tan_fov clamp
+    sc, cam, scales, quats, _ = _setup(seed=seed, n=600 if seed == 2 else 300)
+    if seed == 2:
+        sc, scales = _wide(sc, scales)
     xys, depths, radii, conics, nth, cov3d = O.project_forward(
         sc.means.numpy(), scales.numpy(), 1.0, quats.numpy(), cam.viewmat.numpy(),
         cam.projmat.numpy(), cam.fx, cam.fy, cam.cx, cam.cy, cam.height, cam.width,
@@ -68,17 +89,56 @@ def test_project_backward_matches_autograd(oracle_lib, seed):
     s = scales.double().requires_grad_()
     q = quats.double().requires_grad_()
     r = TR.project(m, s, 1.0, q, cam.viewmat.double(), cam.projmat.double(), cam.fx, cam.fy,
-                   cam.cx, cam.cy, cam.height, cam.width, cam.tile_bounds, quirks=True)
+                   cam.cx, cam.cy, cam.height, cam.width, cam.tile_bounds, quirks=quirk_mask)
     # gsplat's v_conic.y is the gradient w.r.t. one off-diagonal of the symmetric conic
-    # (SURVEY A7/A10): the parameter gradient is twice it.
-    w = torch.tensor([1.0, 2.0, 1.0], dtype=torch.float64)
+    # (SURVEY A7/A10, quirk CONIC_HALF): the parameter gradient is twice it.
+    w = torch.tensor([1.0, 2.0 if quirk_mask & 2 else 1.0, 1.0], dtype=torch.float64)
     vis = torch.from_numpy(radii > 0)
     loss = ((v_xys.double() * r["xys"]).sum(1) + v_depths.double() * r["depths"] +
             (v_conics.double() * w * r["conics"]).sum(1))[vis].sum()
     loss.backward()
-    np.testing.assert_allclose(v_mean, m.grad.numpy(), rtol=2e-3, atol=2e-3)
-    np.testing.assert_allclose(v_scale, s.grad.numpy(), rtol=2e-3, atol=2e-3)
-    np.testing.assert_allclose(v_quat, q.grad.numpy(), rtol=2e-3, atol=2e-3)
+    rows = np.ones(n, bool)
+    if quirk_mask & 4:
+        # gsplat's A6 VJP recomputes the Jacobian VALUE without the clamp for every term (also
+        # v_cov3d), which is no straight-through of the clamped forward: beyond the clamp it is
+        # the gradient of nothing, so only the Gaussians inside are compared with calculus
+        t = sc.means.numpy() @ cam.viewmat.numpy()[:3, :3].T + cam.viewmat.numpy()[:3, 3]
+        lim = 1.3 * 0.5 * cam.width / cam.fx
+        rows = np.abs(t[:, 0] / t[:, 2]) <= lim
+        lim = 1.3 * 0.5 * cam.height / cam.fy
+        rows &= np.abs(t[:, 1] / t[:, 2]) <= lim
+    np.testing.assert_allclose(v_mean[rows], m.grad.numpy()[rows], rtol=2e-3, atol=2e-3)
+    np.testing.assert_allclose(v_scale[rows], s.grad.numpy()[rows], rtol=2e-3, atol=2e-3)
+    np.testing.assert_allclose(v_quat[rows], q.grad.numpy()[rows], rtol=2e-3, atol=2e-3)
+
+
+def test_project_quirk_A6_is_real(oracle_lib):
+    """The EWA_UNCLAMPED quirk changes the means gradient of Gaussians beyond the clamp (and
+    nothing else): both settings are live code paths."""
+    O = oracle_lib
+    sc, cam, scales, quats, _ = _setup(seed=2, n=600)
+    sc, scales = _wide(sc, scales)
+    args = (sc.means.numpy(), scales.numpy(), 1.0, quats.numpy(), cam.viewmat.numpy(),
+            cam.projmat.numpy(), cam.fx, cam.fy, cam.cx, cam.cy, cam.height, cam.width)
+    xys, depths, radii, conics, nth, cov3d = O.project_forward(*args, cam.tile_bounds)
+    n = sc.num_points
+    g = np.random.default_rng(0)
+    vc = (g.standard_normal((n, 3)) * 10).astype(np.float32)
+    zero1, zero2 = np.zeros(n, np.float32), np.zeros((n, 2), np.float32)
+    prev = O.get_quirks()
+    try:
+        outs = {}
+        for mask in (7, 3):
+            O.set_quirks(mask)
+            outs[mask] = O.project_backward(*args, cov3d, radii, conics, zero2, zero1, vc)[2]
+    finally:
+        O.set_quirks(prev)
+    t = sc.means.numpy() @ cam.viewmat.numpy()[:3, :3].T + cam.viewmat.numpy()[:3, 3]
+    lim = 1.3 * 0.5 * cam.width / cam.fx
+    outside = (np.abs(t[:, 0] / t[:, 2]) > lim) & (radii > 0)
+    assert outside.sum() >= 5
+    diff = np.abs(outs[7] - outs[3]).max(1) > 1e-6
+    assert diff[outside].all() and not diff[~outside & (radii > 0)].any()
 
 
 def test_project_quirk_A5_is_real(oracle_lib):

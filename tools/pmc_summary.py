@@ -1,8 +1,9 @@
 """Per-kernel averages of rocprofv3 --pmc CSV passes (tools/pmc_bench.sh output).
-Usage: pmc_summary.py gpurun_out [out.csv] [traffic.json]
+Usage: pmc_summary.py gpurun_out [out.csv] [traffic.json [config]]
 
 traffic.json (read by bench.py for roofline.traffic): per device kernel, the mean per-dispatch
-FETCH_SIZE and WRITE_SIZE in KiB as rocprofv3 reports them (uncorrected)."""
+FETCH_SIZE and WRITE_SIZE in KiB as rocprofv3 reports them (uncorrected), stored under the bench
+config the counters were collected on (default headline); other configs' entries are kept."""
 import json
 import collections
 import csv
@@ -13,7 +14,10 @@ import sys
 
 root = sys.argv[1]
 acc = collections.defaultdict(lambda: collections.defaultdict(list))
-for f in glob.glob(os.path.join(root, "pmc_*", "*counter_collection.csv")):
+cfg_arg = sys.argv[4] if len(sys.argv) > 4 else "headline"
+files = glob.glob(os.path.join(root, "pmc", cfg_arg + "_*", "**", "*counter_collection.csv"),
+                  recursive=True)
+for f in files:
     for r in csv.DictReader(open(f)):
         name = r["Kernel_Name"].replace("(anonymous namespace)::", "")
         if name.startswith("void gs::") or name.startswith("gs::"):
@@ -32,10 +36,17 @@ if len(sys.argv) > 3:
     tj = {r["kernel"]: {"fetch_kb": r.get("FETCH_SIZE"), "write_kb": r.get("WRITE_SIZE"),
                         "valu_quad_cycles": r.get("SQ_ACTIVE_INST_VALU")}
           for r in rows if "FETCH_SIZE" in r and "WRITE_SIZE" in r}
+    cfg = cfg_arg
+    try:
+        with open(sys.argv[3]) as f:
+            doc = json.load(f)
+    except (OSError, ValueError):
+        doc = {}
+    doc.setdefault("source", "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE / SQ_ACTIVE_INST_VALU "
+                             "(quad-cycles), separate passes, tools/pmc_bench.sh")
+    doc.setdefault("configs", {})[cfg] = {"kernels": tj}
     with open(sys.argv[3], "w") as f:
-        json.dump({"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE / SQ_ACTIVE_INST_VALU "
-                             "(quad-cycles), separate passes, tools/pmc_bench.sh",
-                   "kernels": tj}, f, indent=1)
+        json.dump(doc, f, indent=1)
 out = sys.argv[2] if len(sys.argv) > 2 else None
 w = csv.writer(open(out, "w", newline="") if out else sys.stdout)
 w.writerow(["kernel"] + cols)
