@@ -34,11 +34,15 @@ SIGNATURES = {
     "gsplat_project_gaussians_forward": (_I, [
         _I, _P, _P, _F, _P, _P, _P, _F, _F, _F, _F, _I, _I, _I, _I, _F,
         _P, _P, _P, _P, _P, _P, _P]),
+    "gsplat_project_gaussians_forward_binned": (_I, [
+        _I, _P, _P, _F, _P, _P, _P, _F, _F, _F, _F, _I, _I, _I, _I, _F,
+        _P, _P, _P, _P, _P, _P, _P, _SZ, _P]),
     "gsplat_project_gaussians_backward": (_I, [
         _I, _P, _P, _F, _P, _P, _P, _F, _F, _F, _F, _I, _I, _P, _P, _P, _P, _P, _P,
         _P, _P, _P, _P, _P, _P]),
     "gsplat_compute_sh_forward": (_I, [_I, _I, _I, _P, _P, _P, _P]),
     "gsplat_compute_sh_backward": (_I, [_I, _I, _I, _P, _P, _P, _P]),
+    "gsplat_compute_sh_backward_split": (_I, [_I, _I, _I, _P, _P, _P, _P, _P]),
     "gsplat_compute_sh_backward_views": (_I, [_I, _I, _I, _I, _P, _P, _I64, _P, _P]),
     "gsplat_compute_sh_backward_views_split": (_I, [_I, _I, _I, _I, _P, _P, _I64, _P, _P, _P]),
     "gsplat_compute_cov2d_bounds": (_I, [_I, _P, _P, _P, _P]),
@@ -66,6 +70,7 @@ SIGNATURES = {
                                           [_P] * 4 + [_I64, _I, _P, _SZ, _P, _SZ, _P]),
     "gsplat_debug_set_chunk": (_I, [_I]),
     "gsplat_debug_set_raster_variant": (_I, [_I, _I, _I]),
+    "gsplat_debug_raster_variant_is_default": (_I, []),
     "gsplat_debug_sort_timing": (_I, [_P, _I]),
     "gsplat_debug_sort_scheme": (_I, [_I]),
     "gsplat_debug_sort_items": (_I, [_I]),
@@ -86,6 +91,7 @@ SIGNATURES = {
     "gsplat_fused_preprocess_backward_adam": (_I, [_I, _I, _I] + [_P] * 9 + [_F] * 4 +
                                               [_I, _I] + [_P] * 8 + [_I, _F, _F, _F, _P]),
     "gsplat_grad_records_bytes": (_SZ, [_I]),
+    "gsplat_grad_records_split": (_I, [_I, _P, _SZ, _P, _P, _P, _P, _P]),
     "gsplat_rasterize_backward_records": (_I, [_I] * 5 + [_P] * 11 + [_F, _I64, _I, _P, _SZ,
                                                                        _P, _SZ, _P]),
 }

@@ -19,7 +19,7 @@ __global__ __launch_bounds__(256) void project_fwd_kernel(
     const float *__restrict__ quats, const float *__restrict__ viewmat,
     const float *__restrict__ projmat, ProjParams pp, float *__restrict__ cov3d,
     float *__restrict__ xys, float *__restrict__ depths, int *__restrict__ radii,
-    float *__restrict__ conics, int *__restrict__ num_tiles_hit) {
+    float *__restrict__ conics, int *__restrict__ num_tiles_hit, BinKeys bin) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   Cam cam;
@@ -40,6 +40,20 @@ __global__ __launch_bounds__(256) void project_fwd_kernel(
   depths[i] = o.depth;
   radii[i] = o.radius;
   num_tiles_hit[i] = o.tiles;
+  if (bin.keys) {  // the binning's depth-sort inputs (binning.hip depth_keys_kernel's outputs)
+    const bool vis = o.radius > 0;
+    bin.keys[i] = vis ? __float_as_uint(o.depth) : 0xFFFFFFFFu;
+    bin.vals[i] = (uint32_t)i;
+    const int c = vis ? o.tiles : 0;
+    uint4 q = {c > 0 ? (uint32_t)c : 0u, 0u, 0u, 0u};
+    if (c > 0) {
+      int x0, x1, y0, y1;
+      tile_bbox(o.xy[0], o.xy[1], (float)o.radius, pp.tbx, pp.tby, x0, x1, y0, y1);
+      q.y = (uint32_t)x0 | ((uint32_t)y0 << 16);
+      q.z = (uint32_t)x1 | ((uint32_t)y1 << 16);
+    }
+    bin.rec[i] = q;
+  }
 }
 
 __global__ __launch_bounds__(256) void project_bwd_kernel(
@@ -111,25 +125,65 @@ __global__ __launch_bounds__(256) void cov2d_bounds_kernel(int n, const float *_
 
 using namespace gs;
 
-extern "C" int gsplat_project_gaussians_forward(
+static int project_forward_impl(
     int num_points, const float *means3d, const float *scales, float glob_scale,
     const float *quats, const float *viewmat, const float *projmat, float fx, float fy,
     float cx, float cy, int img_height, int img_width, int tile_bounds_x, int tile_bounds_y,
     float clip_thresh, float *cov3d, float *xys, float *depths, int32_t *radii,
-    float *conics, int32_t *num_tiles_hit, void *stream) {
+    float *conics, int32_t *num_tiles_hit, void *workspace1, size_t workspace1_bytes,
+    void *stream, const char *who) {
   if (num_points < 0 || img_height <= 0 || img_width <= 0 || tile_bounds_x <= 0 ||
       tile_bounds_y <= 0) {
-    set_error("project_gaussians_forward: bad sizes (N=%d H=%d W=%d tiles=%dx%d)", num_points,
-              img_height, img_width, tile_bounds_x, tile_bounds_y);
+    set_error("%s: bad sizes (N=%d H=%d W=%d tiles=%dx%d)", who, num_points, img_height,
+              img_width, tile_bounds_x, tile_bounds_y);
     return 1;
+  }
+  BinKeys bin = {nullptr, nullptr, nullptr, 0};
+  if (workspace1) {
+    bin = bin_keys_view(workspace1, num_points);
+    if (workspace1_bytes < bin.bytes) {
+      set_error("%s: workspace %zu < %zu bytes (gsplat_bin_count_workspace_size)", who,
+                workspace1_bytes, bin.bytes);
+      return 1;
+    }
   }
   if (num_points == 0) return 0;
   const ProjParams pp = make_proj_params(fx, fy, cx, cy, glob_scale, clip_thresh, img_height,
                                          img_width, tile_bounds_x, tile_bounds_y);
   hipLaunchKernelGGL(project_fwd_kernel, dim3(cdiv(num_points, 256)), dim3(256), 0,
                      (hipStream_t)stream, num_points, means3d, scales, quats, viewmat, projmat,
-                     pp, cov3d, xys, depths, radii, conics, num_tiles_hit);
-  return check_launch("project_gaussians_forward");
+                     pp, cov3d, xys, depths, radii, conics, num_tiles_hit, bin);
+  return check_launch(who);
+}
+
+extern "C" int gsplat_project_gaussians_forward(
+    int num_points, const float *means3d, const float *scales, float glob_scale,
+    const float *quats, const float *viewmat, const float *projmat, float fx, float fy,
+    float cx, float cy, int img_height, int img_width, int tile_bounds_x, int tile_bounds_y,
+    float clip_thresh, float *cov3d, float *xys, float *depths, int32_t *radii,
+    float *conics, int32_t *num_tiles_hit, void *stream) {
+  return project_forward_impl(num_points, means3d, scales, glob_scale, quats, viewmat, projmat,
+                              fx, fy, cx, cy, img_height, img_width, tile_bounds_x,
+                              tile_bounds_y, clip_thresh, cov3d, xys, depths, radii, conics,
+                              num_tiles_hit, nullptr, 0, stream, "project_gaussians_forward");
+}
+
+extern "C" int gsplat_project_gaussians_forward_binned(
+    int num_points, const float *means3d, const float *scales, float glob_scale,
+    const float *quats, const float *viewmat, const float *projmat, float fx, float fy,
+    float cx, float cy, int img_height, int img_width, int tile_bounds_x, int tile_bounds_y,
+    float clip_thresh, float *cov3d, float *xys, float *depths, int32_t *radii,
+    float *conics, int32_t *num_tiles_hit, void *workspace1, size_t workspace1_bytes,
+    void *stream) {
+  if (!workspace1) {
+    set_error("project_gaussians_forward_binned: no workspace");
+    return 1;
+  }
+  return project_forward_impl(num_points, means3d, scales, glob_scale, quats, viewmat, projmat,
+                              fx, fy, cx, cy, img_height, img_width, tile_bounds_x,
+                              tile_bounds_y, clip_thresh, cov3d, xys, depths, radii, conics,
+                              num_tiles_hit, workspace1, workspace1_bytes, stream,
+                              "project_gaussians_forward_binned");
 }
 
 extern "C" int gsplat_project_gaussians_backward(

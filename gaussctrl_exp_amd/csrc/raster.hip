@@ -1928,6 +1928,8 @@ extern "C" int gsplat_debug_set_raster_variant(int fwd_pxl, int bwd_pxl, int bwd
   return 0;
 }
 
+extern "C" int gsplat_debug_raster_variant_is_default(void) { return default_variants() ? 1 : 0; }
+
 extern "C" int gsplat_set_deterministic(int on) {
   g_det = on != 0;
   return 0;
@@ -2272,6 +2274,22 @@ extern "C" int gsplat_rasterize_backward_chunked(
                      num_points, (const float4 *)rec, 0.5f, conic_y_scale(0.5f), v_xy, v_conic,
                      v_colors, v_opacity);
   return check_launch("rasterize_backward_chunked");
+}
+
+extern "C" int gsplat_grad_records_split(int num_points, const void *records,
+                                         size_t records_bytes, float *v_xy, float *v_conic,
+                                         float *v_colors, float *v_opacity, void *stream) {
+  const size_t need = num_points > 0 ? (size_t)num_points * REC * sizeof(float) : 0;
+  if (num_points < 0 || records_bytes < need || (need && !records)) {
+    set_error("grad_records_split: records %zu < %zu bytes (N=%d)", records_bytes, need,
+              num_points);
+    return 1;
+  }
+  if (num_points == 0) return 0;
+  hipLaunchKernelGGL(split_grads_kernel, dim3(cdiv(num_points, 256)), dim3(256), 0,
+                     (hipStream_t)stream, num_points, (const float4 *)records, 0.5f,
+                     conic_y_scale(0.5f), v_xy, v_conic, v_colors, v_opacity);
+  return check_launch("grad_records_split");
 }
 
 extern "C" size_t gsplat_grad_records_bytes(int num_points) {

@@ -39,11 +39,15 @@ __global__ __launch_bounds__(256) void sh_fwd_kernel(int n, int degrees_to_use,
     colors[3 * g + c] = sh_channel<K>(b, nb, [&](int k) { return co[k * 3 + c]; });
 }
 
-template <int K>
+// SPLIT: the gradient goes to v_coeffs = v_dc [N,3] (basis 0) and v_rest [N,K-1,3] -- the
+// caller's cat(features_dc[:, None], features_rest) undone (sh.py bypasses that cat in the
+// autograd graph, so the parameters receive contiguous gradients and need no layout copies).
+template <int K, bool SPLIT = false>
 __global__ __launch_bounds__(256) void sh_bwd_kernel(int n, int degrees_to_use,
                                                              const float *__restrict__ viewdirs,
                                                              const float *__restrict__ v_colors,
-                                                             float *__restrict__ v_coeffs) {
+                                                             float *__restrict__ v_coeffs,
+                                                             float *__restrict__ v_rest = nullptr) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int ROW = K * 3;
   constexpr int ROWP = sh_row_pitch(K);
@@ -67,7 +71,12 @@ __global__ __launch_bounds__(256) void sh_bwd_kernel(int n, int degrees_to_use,
     }
   }
   __syncthreads();
-  store_rows<K>(smem, cnt, v_coeffs + g0 * ROW);
+  if constexpr (SPLIT) {
+    store_cols<3, 0, ROWP, SH_THREADS>(smem, cnt, v_coeffs + g0 * 3);
+    if constexpr (K > 1) store_cols<ROW - 3, 3, ROWP, SH_THREADS>(smem, cnt, v_rest + g0 * (ROW - 3));
+  } else {
+    store_rows<K>(smem, cnt, v_coeffs + g0 * ROW);
+  }
 }
 
 // Multi-view SH backward for data-parallel training: the coefficient
@@ -247,4 +256,35 @@ extern "C" int gsplat_compute_sh_backward_views_split(int num_points, int degree
 #undef SPLIT_CASE
   }
   return check_launch("compute_sh_backward_views_split");
+}
+
+extern "C" int gsplat_compute_sh_backward_split(int num_points, int degree, int degrees_to_use,
+                                                const float *viewdirs, const float *v_colors,
+                                                float *v_dc, float *v_rest, void *stream) {
+  if (num_points < 0 || degree < 0 || degree > 4 || degrees_to_use < 0 ||
+      degrees_to_use > degree || (num_points > 0 && (!v_dc || (degree > 0 && !v_rest)))) {
+    set_error("compute_sh_backward_split: bad args (N=%d degree=%d degrees_to_use=%d)",
+              num_points, degree, degrees_to_use);
+    return 1;
+  }
+  if (num_points == 0) return 0;
+  const int K = num_bases(degree);
+  const int thr = sh_threads(K);
+  dim3 grid(cdiv(num_points, thr)), block(thr);
+  size_t smem = (size_t)thr * sh_row_pitch(K) * sizeof(float);
+  hipStream_t st = (hipStream_t)stream;
+  switch (K) {
+#define SPLIT_CASE(KK)                                                                     \
+  case KK:                                                                                 \
+    hipLaunchKernelGGL((sh_bwd_kernel<KK, true>), grid, block, smem, st, num_points,        \
+                       degrees_to_use, viewdirs, v_colors, v_dc, v_rest);                   \
+    break;
+    SPLIT_CASE(1)
+    SPLIT_CASE(4)
+    SPLIT_CASE(9)
+    SPLIT_CASE(16)
+    SPLIT_CASE(25)
+#undef SPLIT_CASE
+  }
+  return check_launch("compute_sh_backward_split");
 }

@@ -6,6 +6,8 @@ are the gfx950 ones in csrc/project.hip reached through the C ABI.
 """
 from __future__ import annotations
 
+import threading
+
 from typing import Tuple
 
 import torch
@@ -42,10 +44,22 @@ def project_gaussians(
     cov3d [N,6]); culled Gaussians have radii == 0.  Gradients flow to means3d, scales and
     quats (gsplat 0.1.x returns None for viewmat/projmat).
     """
-    return _ProjectGaussians.apply(
+    out = _ProjectGaussians.apply(
         means3d.contiguous(), scales.contiguous(), glob_scale, quats.contiguous(),
         viewmat.contiguous(), projmat.contiguous(), fx, fy, cx, cy, img_height, img_width,
         tile_bounds, clip_thresh)
+    ws1 = getattr(_LAST, "ws1", None)
+    if ws1 is not None:
+        # the binning's depth-sort inputs, written by the projection kernel: the rasterize call
+        # on exactly these (unmodified) outputs bins with gsplat_bin_count_keyed
+        _LAST.ws1 = None
+        from .rasterize import keyed_workspaces
+        keyed_workspaces.put((out[0], out[1], out[2], out[4]), int(tile_bounds[0]),
+                             int(tile_bounds[1]), ws1)
+    return out
+
+
+_LAST = threading.local()
 
 
 def _as_f32(t: Tensor) -> Tensor:
@@ -74,11 +88,14 @@ class _ProjectGaussians(Function):
         conics = torch.empty((n, 3), device=dev, dtype=torch.float32)
         num_tiles_hit = torch.empty((n,), device=dev, dtype=torch.int32)
         P = _lib.ptr
-        _lib.call("gsplat_project_gaussians_forward", n, P(means3d), P(scales),
+        ws1 = torch.empty((_lib.query("gsplat_bin_count_workspace_size", n),), device=dev,
+                          dtype=torch.uint8)
+        _lib.call("gsplat_project_gaussians_forward_binned", n, P(means3d), P(scales),
                   float(glob_scale), P(quats), P(viewmat), P(projmat), float(fx), float(fy),
                   float(cx), float(cy), int(img_height), int(img_width), int(tile_bounds[0]),
                   int(tile_bounds[1]), float(clip_thresh), P(cov3d), P(xys), P(depths),
-                  P(radii), P(conics), P(num_tiles_hit), _lib.stream(dev))
+                  P(radii), P(conics), P(num_tiles_hit), P(ws1), ws1.numel(), _lib.stream(dev))
+        _LAST.ws1 = ws1
         ctx.img_height = img_height
         ctx.img_width = img_width
         ctx.num_points = num_points

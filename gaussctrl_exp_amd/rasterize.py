@@ -220,14 +220,39 @@ class _BinCache:
 _BIN_CACHE = _BinCache()
 
 
+class _KeyedWorkspaces:
+    """The depth-sort inputs project_gaussians wrote for its latest outputs
+    (gsplat_project_gaussians_forward_binned), handed to the rasterize call that bins exactly
+    those outputs -- the same tensor objects (weak references), unmodified (version counters),
+    for the same tile grid, on the same stream.  Single use: the sort consumes the workspace."""
+
+    def __init__(self):
+        self.cache = _BinCache()
+
+    def put(self, tensors, tbx, tby, ws1):
+        self.cache.put(tensors, tbx, tby, _lib.stream(tensors[0].device), ws1)
+
+    def take(self, tensors, tbx, tby, stream):
+        ws1 = self.cache.get(tensors, tbx, tby, stream)
+        if ws1 is not None:
+            self.cache.clear()
+        return ws1
+
+
+keyed_workspaces = _KeyedWorkspaces()
+
+
 def _binning(xys, depths, radii, num_tiles_hit, H, W):
-    """bin_gaussians through the one-entry cache (see module docstring)."""
+    """bin_gaussians through the one-entry cache (see module docstring), with the depth-sort
+    inputs the projection kernel already wrote when these are its outputs."""
     key_tensors = (xys, depths, radii, num_tiles_hit)
     st = _lib.stream(xys.device)
     hit = _BIN_CACHE.get(key_tensors, H, W, st)
     if hit is not None:
         return hit
-    res = bin_gaussians(xys, depths, radii, num_tiles_hit, H, W)
+    tbx, tby = (W + BLOCK_X - 1) // BLOCK_X, (H + BLOCK_Y - 1) // BLOCK_Y
+    ws1 = keyed_workspaces.take(key_tensors, tbx, tby, st)
+    res = bin_gaussians(xys, depths, radii, num_tiles_hit, H, W, keyed_workspace=ws1)
     _BIN_CACHE.put(key_tensors, H, W, st, res)
     return res
 
@@ -309,10 +334,26 @@ class _RasterizeGaussians(Function):
             final_Ts = torch.empty((H, W), device=dev, dtype=torch.float32)
             final_idx = torch.empty((H, W), device=dev, dtype=torch.int32)
             P = _lib.ptr
+            grads = C == 3 and any(ctx.needs_input_grad)
             # list-split backward (C = 3, gradients wanted): the forward records checkpoints
             chunk = _lib.query("gsplat_rasterize_chunk_size", tbx, tby, num_intersects) \
-                if C == 3 and any(ctx.needs_input_grad) else 0
-            if chunk > 0:
+                if grads else 0
+            if grads and _lib.lib().gsplat_debug_raster_variant_is_default():
+                # the backward accumulates into per-Gaussian gradient records that this blend
+                # zeroes as its waves finish (no memset in the backward; every record, since
+                # gsplat_grad_records_split reads the culled Gaussians' zeros too)
+                ckpt = torch.empty((max(_lib.query("gsplat_rasterize_checkpoint_bytes", tbx,
+                                                   tby, num_intersects, chunk), 1),),
+                                   device=dev, dtype=torch.uint8) if chunk > 0 else None
+                rec = torch.empty((_lib.query("gsplat_grad_records_bytes", num_points),),
+                                  device=dev, dtype=torch.uint8)
+                _lib.call("gsplat_rasterize_forward_clearing", tbx, tby, H, W,
+                          P(gaussian_ids_sorted), P(tile_bins), P(xys), P(conics), P(colors),
+                          P(opacity), P(background), P(out_img), P(final_Ts), P(final_idx),
+                          num_intersects, chunk, P(ckpt), ckpt.numel() if chunk > 0 else 0,
+                          P(rec), rec.numel(), None, _lib.stream(dev))
+                ctx.chunk, ctx.ckpt, ctx.rec = chunk, ckpt, rec
+            elif chunk > 0:
                 ckpt = torch.empty((_lib.query("gsplat_rasterize_checkpoint_bytes", tbx, tby,
                                                num_intersects, chunk),),
                                    device=dev, dtype=torch.uint8)
@@ -327,6 +368,8 @@ class _RasterizeGaussians(Function):
                           P(out_img), P(final_Ts), P(final_idx), _lib.stream(dev))
         if not hasattr(ctx, "chunk"):
             ctx.chunk, ctx.ckpt = 0, None
+        if not hasattr(ctx, "rec"):
+            ctx.rec = None
 
         ctx.img_width = W
         ctx.img_height = H
@@ -367,6 +410,19 @@ class _RasterizeGaussians(Function):
             P = _lib.ptr
             tbx = (W + BLOCK_X - 1) // BLOCK_X
             tby = (H + BLOCK_Y - 1) // BLOCK_Y
+            if ctx.rec is not None:  # records cleared by the forward blend
+                rec, st = ctx.rec, _lib.stream(dev)
+                _lib.call("gsplat_rasterize_backward_records", tbx, tby, H, W, num_points,
+                          P(gaussian_ids_sorted), P(tile_bins), P(xys), P(conics), P(colors),
+                          P(opacity), P(background), P(final_Ts), P(final_idx), P(v_out_img),
+                          P(v_out_alpha), quirks.backward_alpha_clamp(), ctx.num_intersects,
+                          ctx.chunk, P(ctx.ckpt), ctx.ckpt.numel() if ctx.ckpt is not None
+                          else 0, P(rec), rec.numel(), st)
+                _lib.call("gsplat_grad_records_split", num_points, P(rec), rec.numel(), P(v_xy),
+                          P(v_conic), P(v_colors), P(v_opacity), st)
+                ctx.rec = None
+                return (v_xy, None, None, v_conic, None, v_colors, v_opacity, None, None, None,
+                        None)
             wsz = _lib.query("gsplat_rasterize_backward_workspace_size", num_points, C)
             ws = torch.empty((max(wsz, 1),), device=dev, dtype=torch.uint8)
             if ctx.chunk > 0:

@@ -86,6 +86,19 @@ int gsplat_project_gaussians_forward(
     float clip_thresh, float *cov3d, float *xys, float *depths, int32_t *radii,
     float *conics, int32_t *num_tiles_hit, void *stream);
 
+/* gsplat_project_gaussians_forward that also writes the binning's depth-sort inputs (depth
+ * keys, ids, per-Gaussian tile records) into a gsplat_bin_count workspace (>=
+ * gsplat_bin_count_workspace_size(num_points) bytes), so the rasterize call that follows bins
+ * with gsplat_bin_count_keyed instead of re-reading xys/depths/radii/num_tiles_hit
+ * (the drop-in project_gaussians does this; no gsplat counterpart). */
+int gsplat_project_gaussians_forward_binned(
+    int num_points, const float *means3d, const float *scales, float glob_scale,
+    const float *quats, const float *viewmat, const float *projmat, float fx, float fy,
+    float cx, float cy, int img_height, int img_width, int tile_bounds_x, int tile_bounds_y,
+    float clip_thresh, float *cov3d, float *xys, float *depths, int32_t *radii,
+    float *conics, int32_t *num_tiles_hit, void *workspace1, size_t workspace1_bytes,
+    void *stream);
+
 /* Outputs v_cov2d [N,3], v_cov3d [N,6], v_mean3d [N,3], v_scale [N,3], v_quat [N,4] are
  * fully written (zeros where radii <= 0); v_cov2d / v_cov3d (gsplat's intermediate
  * gradients, which its autograd wrapper discards) may be NULL.  v_depth may be NULL (an all-zero depth gradient,
@@ -106,6 +119,14 @@ int gsplat_compute_sh_forward(int num_points, int degree, int degrees_to_use,
 int gsplat_compute_sh_backward(int num_points, int degree, int degrees_to_use,
                                const float *viewdirs, const float *v_colors, float *v_coeffs,
                                void *stream);
+
+/* gsplat_compute_sh_backward with the coefficient gradient split into v_dc [N,3] (basis 0)
+ * and v_rest [N, K-1, 3] (may be NULL when degree == 0): the gradients of the caller's
+ * cat(features_dc[:, None], features_rest) inputs, so the drop-in spherical_harmonics can
+ * hand splatfacto's parameters contiguous gradients (no cat backward, no layout copies). */
+int gsplat_compute_sh_backward_split(int num_points, int degree, int degrees_to_use,
+                                     const float *viewdirs, const float *v_colors, float *v_dc,
+                                     float *v_rest, void *stream);
 
 /* Data-parallel extension (no gsplat counterpart): the sum over num_views
  * cameras of the SH coefficient gradient, v_coeffs[i] = sum_r Y(means3d[i] - campos_r) (x)
@@ -344,6 +365,14 @@ int gsplat_rasterize_backward_records(
     const float *v_output_alpha, float alpha_max, int64_t num_intersects, int chunk,
     const void *checkpoints, size_t checkpoint_bytes, void *records, size_t records_bytes,
     void *stream);
+/* The records -> gsplat's four rasterize gradients (v_xy [N,2], v_conic [N,3] in gsplat's
+ * convention (GSPLAT_QUIRK_CONIC_HALF), v_colors [N,3], v_opacity [N]) -- the tail of
+ * gsplat_rasterize_backward, for a caller that cleared the records in the forward blend
+ * (gsplat_rasterize_forward_clearing) and accumulated them with
+ * gsplat_rasterize_backward_records (the drop-in rasterize_gaussians does). */
+int gsplat_grad_records_split(int num_points, const void *records, size_t records_bytes,
+                              float *v_xy, float *v_conic, float *v_colors, float *v_opacity,
+                              void *stream);
 
 /* Tuning / ablation hook (not part of the gsplat surface): pixels per lane of the 3-channel
  * forward and backward kernels (1, 2 or 4; a 16x16 tile is covered by 4/pxl waves), and
@@ -359,6 +388,8 @@ int gsplat_rasterize_backward_records(
  * queue.  Every variant produces results within the same parity bar.  Process-wide;
  * defaults (1, 2, 0) are the shipped configuration. */
 int gsplat_debug_set_raster_variant(int fwd_pxl, int bwd_pxl, int bwd_flags);
+/* 1 while the shipped raster variants are selected (the record-based entries need them). */
+int gsplat_debug_raster_variant_is_default(void);
 
 /* Profiling hook (not part of the gsplat surface): the next `calls` radix-sort passes write
  * per-workgroup phase timestamps (s_memrealtime, 100 MHz: start, ticket, keys loaded, ranked,

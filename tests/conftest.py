@@ -27,3 +27,17 @@ def gpu():
     if not torch.cuda.is_available():
         pytest.skip("no ROCm device")
     return torch.device("cuda:0")
+
+
+@pytest.fixture
+def quirk_mask(request, oracle_lib):
+    """Run a test under GSPLAT_QUIRK_* mask request.param (default all) in both the HIP library
+    and the oracle, restoring the previous mask afterwards."""
+    from gaussctrl_exp_amd import quirks
+    mask = getattr(request, "param", quirks.ALL)
+    prev, prev_o = quirks.get(), oracle_lib.get_quirks()
+    quirks.set(mask)
+    oracle_lib.set_quirks(mask)
+    yield mask
+    quirks.set(prev)
+    oracle_lib.set_quirks(prev_o)

@@ -264,7 +264,7 @@ def _ref_run(sc, cam, deg, bg, raster_grads):
 
 
 @pytest.mark.parametrize("case", CASES)
-def test_fused_render_grads_match_oracle(gpu, case):
+def test_fused_render_grads_match_oracle(gpu, case, quirk_mask):
     """The fused training render (bench.py's step) vs the oracle with zero outliers: its
     rasterizer-level gradients (the backward's records) vs the oracle's rasterize backward on
     the same forward state, and image, alpha and all six parameter gradients vs the oracle
@@ -285,6 +285,14 @@ def test_fused_render_grads_match_oracle(gpu, case):
             assert np.abs(ref[i]).max() > 1e-3, f"{name}: degenerate reference gradient"
         mx = assert_close(name, fused[i], ref[i])
         print(f"{name}: max |diff| {mx:.3e}")
+
+
+@pytest.mark.parametrize("quirk_mask", [0], indirect=True)
+@pytest.mark.parametrize("case", [CASES[0], CASES[2]])
+def test_fused_render_grads_without_quirks(gpu, case, quirk_mask):
+    """The fused kernels under the consistent conventions (quirk mask 0: 0.999 backward clamp,
+    d loss / d conic.y, the clamped EWA Jacobian; CASES[2] has Gaussians beyond the clamp)."""
+    test_fused_render_grads_match_oracle(gpu, case, quirk_mask)
 
 
 def test_fused_xys_grad_is_the_raster_gradient(gpu):

@@ -49,11 +49,15 @@ def timeit(fn, reps=10):
     e.record(); torch.cuda.synchronize()
     return s.elapsed_time(e) / reps
 
-variants = [int(x) for x in os.environ.get("FLAGS", "0,4096").split(",")]
+# VARIANTS="fwd_pxl:bwd_pxl:flags,..." (gsplat_debug_set_raster_variant) or FLAGS (bwd_pxl 2)
+if os.environ.get("VARIANTS"):
+    variants = [tuple(int(v) for v in x.split(":")) for x in os.environ["VARIANTS"].split(",")]
+else:
+    variants = [(1, 2, int(x)) for x in os.environ.get("FLAGS", "0,4096").split(",")]
 fwd(); torch.cuda.synchronize()
 grads = {}
 for f in variants:
-    _lib.call("gsplat_debug_set_raster_variant", 1, 2, f)
+    _lib.call("gsplat_debug_set_raster_variant", *f)
     g = [torch.zeros(N, k, device=dev) for k in (2, 3, 3, 1)]
     bwd(g); torch.cuda.synchronize()
     grads[f] = g
@@ -68,10 +72,10 @@ for f in variants[:-1]:
 res = {f: [] for f in variants}
 for rnd in range(5):
     for f in variants:
-        _lib.call("gsplat_debug_set_raster_variant", 1, 2, f)
+        _lib.call("gsplat_debug_set_raster_variant", *f)
         g = grads[f]
         res[f].append(timeit(lambda: bwd(g)))
 _lib.call("gsplat_debug_set_raster_variant", 1, 2, 0)
 print(f"{cfg}: N={N} I={I} tiles={tb[0]*tb[1]}")
 for f in variants:
-    print(f"bwd flags={f}: {np.median(res[f]):.4f} ms  (rounds {np.round(res[f], 4).tolist()})")
+    print(f"bwd variant={f}: {np.median(res[f]):.4f} ms  (rounds {np.round(res[f], 4).tolist()})")
