@@ -13,6 +13,10 @@ for cfg in ${CONFIGS:-headline}; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_stats_$cfg -o run \
     -- python3 bench.py --config $cfg --steps 20 --warmup 5 --no-cpu-baseline --train-steps 5 \
     > gpurun_out/prof_bench_$cfg.log 2>&1 || exit $?
+  python3 tools/rocpd_stats.py gpurun_out/prof_stats_$cfg/run_results.db \
+    gpurun_out/kernel_stats_$cfg.csv || exit $?
+  # only the summaries travel back (gpurun returns at most 64 MiB)
+  rm -rf gpurun_out/pmc gpurun_out/prof_stats_$cfg
   timeout -k 10 600 python3 bench.py --config $cfg > gpurun_out/bench_$cfg.log 2>&1 || exit $?
   tail -n 1 gpurun_out/bench_$cfg.log
 done
