@@ -405,7 +405,10 @@ def main():
     dom = max(per_call, key=lambda k: per_call[k][2])
     dom_ms = per_call[dom][1]
     dom_bytes = ab.get(dom)
-    step_bytes = sum(b for k, b in ab.items() if k in per_call)  # entries this step ran
+    # the step's algorithmic bytes per view: SURVEY.md §8d's model (the per-entry models above
+    # count every radix pass; this one counts the binning as gsplat's map + one sort + bins)
+    step_bytes = (124 * N + 84 * I + 20 * P + 8 * T) if fwd_only else \
+        ((388 + 24 * K) * N + 124 * I + 44 * P + 8 * T)
     roofline = {
         "kernel": dom,
         "bound": "hbm",
