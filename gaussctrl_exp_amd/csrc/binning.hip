@@ -276,7 +276,7 @@ __global__ __launch_bounds__(TPB) void os_pass_kernel(
     const uint32_t *__restrict__ hist, uint32_t *__restrict__ ticket_ctr,
     uint32_t *__restrict__ status, uint32_t *__restrict__ err,
     unsigned long long *__restrict__ tbuf, bool use_ticket, const uint32_t *__restrict__ offs,
-    long long nblocks) {
+    long long nblocks, int32_t *__restrict__ bins = nullptr) {
   __shared__ OsSmem<K, ITEMS> sm;
   // optional phase timestamps (debug hook gsplat_debug_sort_timing): [ticket][6]
   unsigned long long ts0 = tbuf ? __builtin_amdgcn_s_memrealtime() : 0ull;
@@ -438,15 +438,35 @@ __global__ __launch_bounds__(TPB) void os_pass_kernel(
   __syncthreads();
   unsigned long long ts4 = tbuf ? __builtin_amdgcn_s_memrealtime() : 0ull;
   const long long cnt = min((long long)TPB * ITEMS, n - base);
+  if (bins) {
+    // last pass of the tile sort: the keys (tile ids) are not written; the tile table comes from
+    // the runs of equal keys instead.  This tile's LDS array is sorted by the whole key (this
+    // digit, then the previous passes' order of its contiguous input), and each run is one
+    // contiguous range of the output, so its ends are range ends unless a neighbouring tile
+    // continues the run: the start as I - pos (atomicMax, 0 = empty) and the end, both decoded
+    // by bins_decode_kernel.
 #pragma unroll
-  for (int r = 0; r < ITEMS; ++r) {
-    const int i = r * TPB + tid;
-    if (i < cnt) {
-      const K k = sm.keys[i];
-      const uint32_t d = (uint32_t)(k >> shift) & dmask;
-      const uint32_t pos = sm.gofs[d] + (uint32_t)i;
-      kout[pos] = k;
-      vout[pos] = sm.vals[i];
+    for (int r = 0; r < ITEMS; ++r) {
+      const int i = r * TPB + tid;
+      if (i < cnt) {
+        const K k = sm.keys[i];
+        const uint32_t pos = sm.gofs[(uint32_t)(k >> shift) & dmask] + (uint32_t)i;
+        vout[pos] = sm.vals[i];
+        if (i == 0 || sm.keys[i - 1] != k) atomicMax(&bins[2 * (size_t)k], (int32_t)(n - pos));
+        if (i == cnt - 1 || sm.keys[i + 1] != k) atomicMax(&bins[2 * (size_t)k + 1], (int32_t)pos + 1);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) {
+      const int i = r * TPB + tid;
+      if (i < cnt) {
+        const K k = sm.keys[i];
+        const uint32_t d = (uint32_t)(k >> shift) & dmask;
+        const uint32_t pos = sm.gofs[d] + (uint32_t)i;
+        kout[pos] = k;
+        vout[pos] = sm.vals[i];
+      }
     }
   }
   if (tbuf && tid == 0) {
@@ -472,6 +492,7 @@ constexpr int WD_DPT = WD_R / TPB;  // digits per thread
 constexpr int WD_ITEMS = 8;         // keys per thread (2,048-key tiles)
 constexpr int WD_TILE = TPB * WD_ITEMS;
 bool g_depth_sort_wide = false;  // ablation switch (gsplat_debug_depth_sort_wide)
+bool g_bins_from_sort = true;    // tile table from the last tile-sort pass (gsplat_debug_bins_from_sort)
 
 long long wd_nblocks(long long n) { return n > 0 ? cdiv(n, (long long)WD_TILE) : 0; }
 size_t radix_wide_ws_bytes(long long n) {
@@ -649,10 +670,21 @@ bool g_sort_rts = true;
 // there are more than two passes.  ws must hold radix_ws_bytes(n, begin_bit, end_bit).
 // first_counts_ready (reduce-then-scan only): the caller's key kernel already wrote pass 0's
 // tile digit counts to rts_tile_counts(ws) and cleared the error word.
+// tile_bins (uint32 tile-id keys only): the last pass writes no keys but the tile table --
+// zeroed by the caller, [first, last+1) per tile afterwards (bins_decode_kernel).
+__global__ __launch_bounds__(TPB) void bins_decode_kernel(long long T, long long n,
+                                                          int32_t *__restrict__ bins) {
+  const long long t = (long long)blockIdx.x * TPB + threadIdx.x;
+  if (t >= T) return;
+  const int32_t x = bins[2 * t];
+  if (x > 0) bins[2 * t] = (int32_t)(n - x);
+}
+
 template <typename K>
 int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t *vout,
                      long long n, int begin_bit, int end_bit, void *ws, hipStream_t st,
-                     bool first_counts_ready = false) {
+                     bool first_counts_ready = false, int32_t *tile_bins = nullptr,
+                     long long num_tiles = 0) {
   if (n <= 0) return 0;
   const SortPlan p = sort_plan(n, begin_bit, end_bit);
   if (p.passes == 0) {
@@ -711,7 +743,7 @@ int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t
                      kin, vin, ko, vo, n, begin_bit + q * p.width, p.width,                    \
                      rts ? rts_partial : hist + q * 256,                                       \
                      tickets + q, status + (size_t)q * p.nblocks * p.radix, err, tb,       \
-                     g_sort_ticket, offs, p.nblocks)
+                     g_sort_ticket, offs, p.nblocks, last ? tile_bins : nullptr)
 #define OS_PASS_W(Wd)                                                                       \
   do {                                                                                      \
     if (p.items == 16) OS_PASS(Wd, 16); else if (p.items == 8) OS_PASS(Wd, 8);             \
@@ -736,6 +768,9 @@ int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t
     kalt = kfree;
     valt = vfree;
   }
+  if (tile_bins)
+    hipLaunchKernelGGL(bins_decode_kernel, dim3(cdiv(num_tiles, TPB)), dim3(TPB), 0, st,
+                       num_tiles, n, tile_bins);
   return 0;
 }
 
@@ -1776,6 +1811,11 @@ extern "C" int gsplat_debug_sort_items(int items) {
   return 0;
 }
 
+extern "C" int gsplat_debug_bins_from_sort(int on) {
+  g_bins_from_sort = on != 0;
+  return 0;
+}
+
 extern "C" int gsplat_debug_depth_sort_wide(int on) {
   g_depth_sort_wide = on != 0;
   return 0;
@@ -1964,10 +2004,18 @@ extern "C" int gsplat_bin_emit(int num_points, int64_t num_intersects, int tile_
   const long long I = num_intersects;
   hipLaunchKernelGGL(emit_kernel, dim3(cdiv(n, TPB)), dim3(TPB), 0, st, n, p1.order, p1.cnt,
                      p1.off, p1.box, tile_bounds_x, tile_bounds_y, p2.tk_a, p2.tv_a, tile_bins);
-  radix_sort_pairs<uint32_t>(p2.tk_a, p2.tv_a, p2.tk_b, p2.tv_b, p2.tk_s,
-                             (uint32_t *)gaussian_ids_sorted, I, 0, bits_for(T), p2.rs_ws, st);
-  hipLaunchKernelGGL(bin_edges4_kernel, dim3(cdiv(cdiv(I, 4), TPB)), dim3(TPB), 0, st, I,
-                     p2.tk_s, tile_bins, T);
+  // the tile sort's last pass writes the tile table itself (runs of equal tile ids) instead of
+  // the sorted keys a bin-edges kernel would re-read (emit_kernel cleared the table)
+  if (g_bins_from_sort) {
+    radix_sort_pairs<uint32_t>(p2.tk_a, p2.tv_a, p2.tk_b, p2.tv_b, p2.tk_s,
+                               (uint32_t *)gaussian_ids_sorted, I, 0, bits_for(T), p2.rs_ws, st,
+                               false, tile_bins, T);
+  } else {
+    radix_sort_pairs<uint32_t>(p2.tk_a, p2.tv_a, p2.tk_b, p2.tv_b, p2.tk_s,
+                               (uint32_t *)gaussian_ids_sorted, I, 0, bits_for(T), p2.rs_ws, st);
+    hipLaunchKernelGGL(bin_edges4_kernel, dim3(cdiv(cdiv(I, 4), TPB)), dim3(TPB), 0, st, I,
+                       p2.tk_s, tile_bins, T);
+  }
   return check_launch("bin_emit");
 }
 

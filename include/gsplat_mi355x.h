@@ -401,6 +401,9 @@ int gsplat_debug_sort_scheme(int reduce_then_scan);
 /* Depth sort of gsplat_bin_count: four 8-bit passes (0, default) or three 11-bit passes (1,
  * slower: ablation); both give the identical stable order. */
 int gsplat_debug_depth_sort_wide(int on);
+/* Tile table of gsplat_bin_emit from the last tile-sort pass (1, default: no sorted keys are
+ * written or re-read) or from a bin-edges kernel over the sorted keys (0); identical tables. */
+int gsplat_debug_bins_from_sort(int on);
 /* Debug: force 4, 8 or 16 keys per thread in every radix-sort pass (0 = automatic). */
 int gsplat_debug_sort_items(int items);
 /* Binning scheme: 1 = tile bucketing + per-tile LDS sort (frames up to 16,447
