@@ -119,8 +119,31 @@ with torch.no_grad():
                     for b0 in range(0, ncand, 64):
                         it += int(v[b0:b0 + 64].sum(0).max()) if v.shape[0] else 0
                     add(name + "_lane_walk_iters", it)
+        # two-queue strip backward: a 16x8 strip whose lanes hold a pixel of the top 16x4 half
+        # (.x) and one of the bottom half (.y); each half walks its own candidate queue, so a
+        # 64-position batch takes max(top, bottom) iterations instead of |top u bottom|
+        for c0 in range(tx * 16, min(tx * 16 + 16, W), 16):
+            c1 = min(c0 + 15, W - 1)
+            for r0 in range(ty * 16, min(ty * 16 + 16, H), 8):
+                halves = []
+                for h0 in (r0, r0 + 4):
+                    h1 = min(h0 + 3, H - 1)
+                    if h0 > H - 1:
+                        halves.append(torch.zeros(e - s, dtype=torch.bool, device=dev))
+                        continue
+                    fs = fin[h0 - ty * 16: h1 - ty * 16 + 1, c0 - tx * 16: c1 - tx * 16 + 1]
+                    halves.append(touches_exact(gx, gy, a, bb, c, o, float(c0), float(c1),
+                                                float(h0), float(h1)) & (idx <= fs.max()))
+                top, bot = halves
+                it2 = 0
+                for b0 in range(0, e - s, 64):
+                    it2 += max(int(top[b0:b0 + 64].sum()), int(bot[b0:b0 + 64].sum()))
+                add("dual_iters", it2)
+                add("dual_union", int((top | bot).sum()))
     n = len(sample)
     print(f"config {cfg}: {n} sampled tiles; per tile:")
+    print(f"  two-queue strips: iterations/tile {acc['dual_iters'] / n:7.1f} "
+          f"(union of the halves' candidates {acc['dual_union'] / n:7.1f})")
     for k in ("list", "tile_last", "valid_bwd", "valid_fwd"):
         print(f"  {k:12s} {acc[k] / n:9.1f}")
     for name in ("fwd8x8", "bwd16x16", "bwd16x8", "bwd8x8", "bwd8x4"):
