@@ -91,11 +91,25 @@ __device__ __forceinline__ void activate(const float *__restrict__ ls, const flo
   for (int k = 0; k < 4; ++k) qn[k] = qr[k] / norm;
 }
 
+// activate() on values already in registers
+__device__ __forceinline__ void activate_vals(const float ls[3], const float q[4], float s[3],
+                                              float qr[4], float qn[4], float &norm) {
+#pragma unroll
+  for (int k = 0; k < 3; ++k) s[k] = expf(ls[k]);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) qr[k] = q[k];
+  norm = sqrtf((qr[0] * qr[0] + qr[1] * qr[1]) + (qr[2] * qr[2] + qr[3] * qr[3]));
+#pragma unroll
+  for (int k = 0; k < 4; ++k) qn[k] = qr[k] / norm;
+}
+
 // SH basis along the caller's view direction: viewdirs = (means - campos) / |means - campos|
 // (gc_model.py:197-198), which gsplat renormalises in-kernel (sh.cuh).
 __device__ __forceinline__ int view_basis(int degrees_to_use, float p0, float p1, float p2,
                                           const float *__restrict__ campos, float *b) {
-  float dx = p0 - campos[0], dy = p1 - campos[1], dz = p2 - campos[2];
+  typedef __attribute__((address_space(4))) const float cfloat;  // uniform: scalar loads
+  cfloat *cp = (cfloat *)campos;
+  float dx = p0 - cp[0], dy = p1 - cp[1], dz = p2 - cp[2];
   // torch's reduction order for the norm of a 3-vector (measured bit-identical on MI355X)
   const float dn = sqrtf((dx * dx + dz * dz) + dy * dy);
   dx = dx / dn;
@@ -104,31 +118,58 @@ __device__ __forceinline__ int view_basis(int degrees_to_use, float p0, float p1
   return sh_basis(degrees_to_use, dx, dy, dz, b);
 }
 
-template <int K>
-__global__ __launch_bounds__(sh_threads(K)) void fused_fwd_kernel(FusedFwdArgs a, ProjParams pp) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
+// Camera matrices through the constant address space: uniform scalar loads (lgkmcnt), which
+// leave the vector-memory counter to the per-Gaussian loads and the features_rest slab.
+__device__ __forceinline__ void load_cam_scalar(Cam &c, const float *viewmat,
+                                                const float *projmat) {
+  typedef __attribute__((address_space(4))) const float cfloat;
+  cfloat *vm = (cfloat *)viewmat;
+  cfloat *pm = (cfloat *)projmat;
+#pragma unroll
+  for (int k = 0; k < 12; ++k) c.vm[k] = vm[k];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) c.pm[k] = pm[k];
+}
+
+// One block's forward.  FULL (every block but a partial last one, slab 16-B aligned): no branch
+// between this Gaussian's own loads, the slab's loads and the projection, so the projection
+// waits only for its own inputs (vmcnt counts in issue order and a branch in between makes the
+// compiler drain the counter) while the features_rest slab stays in flight; the slab lands in
+// LDS after the projection.  Otherwise: guarded loads and stage_rows.
+template <int K, bool FULL>
+__device__ __forceinline__ void fused_fwd_body(const FusedFwdArgs &a, const ProjParams &pp,
+                                               float *smem, long long g0, int cnt) {
   constexpr int RROW = (K - 1) * 3;  // features_rest floats per Gaussian
   constexpr int RP = RROW | 1;       // odd LDS pitch: conflict-free per-thread rows
   constexpr int THR = sh_threads(K);
-  const long long g0 = (long long)blockIdx.x * THR;
-  const int cnt = (int)min((long long)THR, (long long)a.n - g0);
-  // the features_rest slab's loads go out first and land in LDS after the projection: the
-  // per-Gaussian math hides their latency (LDS caps the block count per CU)
-  const float *rest_src = K > 1 ? a.features_rest + g0 * RROW : nullptr;
-  RowStager<RROW, RP, THR> rs;
-  if constexpr (K > 1) rs.issue(rest_src, cnt);
+  constexpr int NV = THR * RROW / 4;  // the full slab's float4s
+  constexpr int PER = (NV + THR - 1) / THR;
   const int t = threadIdx.x;
-  const bool live = t < cnt;
+  const bool live = FULL || t < cnt;
   const long long g = g0 + (live ? t : 0);
-  float p0 = 0.f, p1 = 0.f, p2 = 0.f, dc[3] = {0.f, 0.f, 0.f};
+  Cam cam;
+  load_cam_scalar(cam, a.viewmat, a.projmat);
+  float p0, p1, p2, dc[3], lsv[3], qv[4], ologit;
+  p0 = a.means[3 * g];
+  p1 = a.means[3 * g + 1];
+  p2 = a.means[3 * g + 2];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) lsv[k] = a.log_scales[3 * g + k];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) qv[k] = a.quats[4 * g + k];
+  ologit = a.opacity_logits[g];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) dc[c] = a.features_dc[3 * g + c];
+  const float *rest_src = K > 1 ? a.features_rest + g0 * RROW : nullptr;
+  float4 slab[FULL && K > 1 ? PER : 1];
+  if constexpr (FULL && K > 1) {
+    const float4 *s4 = reinterpret_cast<const float4 *>(rest_src);
+#pragma unroll
+    for (int u = 0; u < PER; ++u) slab[u] = s4[min(u * THR + t, NV - 1)];  // clamped: no branch
+  }
   if (live) {
-    p0 = a.means[3 * g];
-    p1 = a.means[3 * g + 1];
-    p2 = a.means[3 * g + 2];
     float s[3], qr[4], qn[4], norm;
-    activate(a.log_scales, a.quats, g, s, qr, qn, norm);
-    Cam cam;
-    load_cam(cam, a.viewmat, a.projmat);
+    activate_vals(lsv, qv, s, qr, qn, norm);
     ProjOut o;
     project_one(cam, pp, p0, p1, p2, s[0], s[1], s[2], qn[0], qn[1], qn[2], qn[3], o);
     a.xys[2 * g] = o.xy[0];
@@ -162,9 +203,7 @@ __global__ __launch_bounds__(sh_threads(K)) void fused_fwd_kernel(FusedFwdArgs a
       r[2] = z;
       r[3] = z;
     }
-    a.opacity[g] = sigmoidf(a.opacity_logits[g]);  // gc_model.py:215
-#pragma unroll
-    for (int c = 0; c < 3; ++c) dc[c] = a.features_dc[3 * g + c];
+    a.opacity[g] = sigmoidf(ologit);  // gc_model.py:215
     if (a.scales_out) {
 #pragma unroll
       for (int k = 0; k < 3; ++k) a.scales_out[3 * g + k] = s[k];
@@ -180,7 +219,20 @@ __global__ __launch_bounds__(sh_threads(K)) void fused_fwd_kernel(FusedFwdArgs a
       for (int c = 0; c < 3; ++c) a.colors[3 * g + c] = sigmoidf(dc[c]);
     }
   } else {
-    rs.land(rest_src, cnt, smem);
+    if constexpr (FULL) {
+#pragma unroll
+      for (int u = 0; u < PER; ++u) {
+        const int k = u * THR + t;
+        if (NV % THR == 0 || k < NV) {
+          smem[sh_lds_index<RROW, RP>(4 * k)] = slab[u].x;
+          smem[sh_lds_index<RROW, RP>(4 * k + 1)] = slab[u].y;
+          smem[sh_lds_index<RROW, RP>(4 * k + 2)] = slab[u].z;
+          smem[sh_lds_index<RROW, RP>(4 * k + 3)] = slab[u].w;
+        }
+      }
+    } else {
+      stage_rows<RROW, RP, THR>(rest_src, cnt, smem);
+    }
     __syncthreads();
     if (live) {
       float b[25];
@@ -194,6 +246,21 @@ __global__ __launch_bounds__(sh_threads(K)) void fused_fwd_kernel(FusedFwdArgs a
       }
     }
   }
+}
+
+template <int K>
+__global__ __launch_bounds__(sh_threads(K)) void fused_fwd_kernel(FusedFwdArgs a, ProjParams pp) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int THR = sh_threads(K);
+  const long long g0 = (long long)blockIdx.x * THR;
+  const int cnt = (int)min((long long)THR, (long long)a.n - g0);
+  const bool aligned =
+      K == 1 || ((((uintptr_t)(a.features_rest + g0 * (K - 1) * 3)) & 15) == 0 &&
+                 (THR * (K - 1) * 3) % 4 == 0);
+  if (cnt == THR && aligned)
+    fused_fwd_body<K, true>(a, pp, smem, g0, cnt);
+  else
+    fused_fwd_body<K, false>(a, pp, smem, g0, cnt);
 }
 
 template <int K, bool ADAM = false>
