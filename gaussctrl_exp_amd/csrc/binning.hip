@@ -210,15 +210,20 @@ __global__ __launch_bounds__(TPB) void os_hist_kernel(const K *__restrict__ keys
 
 // Reduce-then-scan pass, part 1: the digit histogram of every tile of TPB*ITEMS keys, stored
 // digit-major (counts[d * nblocks + tile]) so one exclusive scan yields every tile's global
-// offset for every digit.
+// offset for every digit.  drop: all-ones keys (culled Gaussians' depth keys) are not counted
+// -- the pass drops them (compacting sort); n_dev: the key count is min(n, *n_dev) (the
+// compacted length, known on the device only).
 template <typename K, int ITEMS>
 __global__ __launch_bounds__(TPB) void rts_count_kernel(const K *__restrict__ keys, long long n,
                                                         int shift, int width, long long nblocks,
                                                         uint32_t *__restrict__ counts,
-                                                        uint32_t *__restrict__ err) {
+                                                        uint32_t *__restrict__ err,
+                                                        bool drop = false,
+                                                        const uint32_t *__restrict__ n_dev = nullptr) {
   __shared__ uint32_t h[256];
   const int tid = threadIdx.x;
   if (err && blockIdx.x == 0 && tid == 0) *err = 0;  // the look-back error word stays clear
+  if (n_dev) n = min(n, (long long)*n_dev);
   const int R = 1 << width;
   const uint32_t dmask = (uint32_t)(R - 1);
   h[tid] = 0;
@@ -232,7 +237,8 @@ __global__ __launch_bounds__(TPB) void rts_count_kernel(const K *__restrict__ ke
   }
 #pragma unroll
   for (int r = 0; r < ITEMS; ++r)
-    if (base + r * TPB + tid < n) atomicAdd(&h[(uint32_t)(k[r] >> shift) & dmask], 1u);
+    if (base + r * TPB + tid < n && !(drop && k[r] == (K)~(K)0))
+      atomicAdd(&h[(uint32_t)(k[r] >> shift) & dmask], 1u);
   __syncthreads();
   if (tid < R) counts[(size_t)tid * nblocks + blockIdx.x] = h[tid];
 }
@@ -267,6 +273,7 @@ struct OsSmem {
   uint32_t hscan[256];     // exclusive scan of this pass's global histogram
   uint32_t scan_tmp[4];
   uint32_t ticket;
+  uint32_t tile_n;         // keys this tile writes (all valid ones; fewer when dropping)
 };
 
 template <typename K, int WIDTH, int ITEMS>
@@ -276,7 +283,15 @@ __global__ __launch_bounds__(TPB) void os_pass_kernel(
     const uint32_t *__restrict__ hist, uint32_t *__restrict__ ticket_ctr,
     uint32_t *__restrict__ status, uint32_t *__restrict__ err,
     unsigned long long *__restrict__ tbuf, bool use_ticket, const uint32_t *__restrict__ offs,
-    long long nblocks, int32_t *__restrict__ bins = nullptr) {
+    long long nblocks, int32_t *__restrict__ bins = nullptr, bool drop = false,
+    const uint32_t *__restrict__ n_dev = nullptr, uint32_t *__restrict__ n_out = nullptr) {
+  // compacting sort (reduce-then-scan only): with drop, all-ones keys are left out (pass 0 of
+  // the depth sort: culled Gaussians), and block 0 stores the kept count to n_out; later passes
+  // sort min(n, *n_dev) keys and the workgroups past them exit at once.
+  if (n_dev) {
+    n = min(n, (long long)*n_dev);
+    if (!use_ticket && (long long)blockIdx.x * TPB * ITEMS >= n) return;  // whole workgroup
+  }
   __shared__ OsSmem<K, ITEMS> sm;
   // optional phase timestamps (debug hook gsplat_debug_sort_timing): [ticket][6]
   unsigned long long ts0 = tbuf ? __builtin_amdgcn_s_memrealtime() : 0ull;
@@ -293,6 +308,7 @@ __global__ __launch_bounds__(TPB) void os_pass_kernel(
      // totals (reduce-then-scan)
     uint32_t h = tid < R ? hist[tid] : 0u, tot;
     sm.hscan[tid] = block_exclusive_scan<TPB>(h, tot, sm.scan_tmp);  // contains barriers
+    if (n_out && blockIdx.x == 0 && tid == 0) *n_out = tot;
   }
   const uint32_t t = sm.ticket;
   unsigned long long ts1 = tbuf ? __builtin_amdgcn_s_memrealtime() : 0ull;
@@ -302,12 +318,14 @@ __global__ __launch_bounds__(TPB) void os_pass_kernel(
 
   K key[ITEMS];
   uint32_t val[ITEMS], rank[ITEMS];
+  bool ok[ITEMS];
 #pragma unroll
   for (int r = 0; r < ITEMS; ++r) {
     const long long i = seg + r * 64 + lane;
     const bool valid = i < n;
     key[r] = valid ? kin[i] : (K)0;
     val[r] = valid ? vin[i] : 0u;
+    ok[r] = valid && !(drop && key[r] == (K)~(K)0);
   }
   unsigned long long ts2 = 0ull;
   if (tbuf) {
@@ -324,7 +342,7 @@ __global__ __launch_bounds__(TPB) void os_pass_kernel(
   // (a wave's LDS atomics execute in issue order, so the rounds stay ordered).
 #pragma unroll
   for (int r = 0; r < ITEMS; ++r) {
-    const bool valid = seg + r * 64 + lane < n;
+    const bool valid = ok[r];
     const uint32_t d = (uint32_t)(key[r] >> shift) & dmask;
     unsigned long long peers = __ballot(valid);
 #pragma unroll
@@ -368,14 +386,14 @@ __global__ __launch_bounds__(TPB) void os_pass_kernel(
   {
     uint32_t tot;
     sm.loc_off[tid] = block_exclusive_scan<TPB>(local_count, tot, sm.scan_tmp);
+    if (tid == 0) sm.tile_n = tot;
   }
   __syncthreads();  // loc_off[d] is read by every thread below
   unsigned long long ts2b = tbuf ? __builtin_amdgcn_s_memrealtime() : 0ull;
   // stable local sort into LDS
 #pragma unroll
   for (int r = 0; r < ITEMS; ++r) {
-    const bool valid = seg + r * 64 + lane < n;
-    if (valid) {
+    if (ok[r]) {
       const uint32_t d = (uint32_t)(key[r] >> shift) & dmask;
       const uint32_t lp = sm.loc_off[d] + sm.wcnt[wave][d] + rank[r];
       sm.keys[lp] = key[r];
@@ -437,7 +455,7 @@ __global__ __launch_bounds__(TPB) void os_pass_kernel(
   }
   __syncthreads();
   unsigned long long ts4 = tbuf ? __builtin_amdgcn_s_memrealtime() : 0ull;
-  const long long cnt = min((long long)TPB * ITEMS, n - base);
+  const long long cnt = sm.tile_n;
   if (bins) {
     // last pass of the tile sort: the keys (tile ids) are not written; the tile table comes from
     // the runs of equal keys instead.  This tile's LDS array is sorted by the whole key (this
@@ -464,7 +482,7 @@ __global__ __launch_bounds__(TPB) void os_pass_kernel(
         const K k = sm.keys[i];
         const uint32_t d = (uint32_t)(k >> shift) & dmask;
         const uint32_t pos = sm.gofs[d] + (uint32_t)i;
-        kout[pos] = k;
+        if (kout) kout[pos] = k;  // null: only the values are wanted (compacted depth sort)
         vout[pos] = sm.vals[i];
       }
     }
@@ -493,6 +511,7 @@ constexpr int WD_ITEMS = 8;         // keys per thread (2,048-key tiles)
 constexpr int WD_TILE = TPB * WD_ITEMS;
 bool g_depth_sort_wide = false;  // ablation switch (gsplat_debug_depth_sort_wide)
 bool g_bins_from_sort = true;    // tile table from the last tile-sort pass (gsplat_debug_bins_from_sort)
+bool g_compact_depth_sort = true;  // depth sort drops culled keys (gsplat_debug_compact_depth_sort)
 
 long long wd_nblocks(long long n) { return n > 0 ? cdiv(n, (long long)WD_TILE) : 0; }
 size_t radix_wide_ws_bytes(long long n) {
@@ -654,6 +673,8 @@ void radix_sort_pairs_wide(uint32_t *ka, uint32_t *va, uint32_t *kb, uint32_t *v
 
 uint32_t *rts_tile_counts(void *ws) { return (uint32_t *)ws + OS_HEAD_WORDS; }
 uint32_t *sort_err_word(void *ws) { return (uint32_t *)ws + OS_MAX_PASSES * 256 + OS_MAX_PASSES; }
+// the compacting sort's kept-key count (a head pad word)
+uint32_t *sort_kept_word(void *ws) { return sort_err_word(ws) + 1; }
 
 // Debug hook (gsplat_debug_sort_timing): the next `calls` sort passes record per-workgroup
 // phase timestamps into consecutive [nblocks][6] slabs of this buffer.
@@ -672,6 +693,9 @@ bool g_sort_rts = true;
 // tile digit counts to rts_tile_counts(ws) and cleared the error word.
 // tile_bins (uint32 tile-id keys only): the last pass writes no keys but the tile table --
 // zeroed by the caller, [first, last+1) per tile afterwards (bins_decode_kernel).
+// drop (reduce-then-scan only; first_counts_ready then means counts without the all-ones
+// keys): the first pass leaves out all-ones keys, so the sort orders only the kept keys, whose
+// count it stores to sort_kept_word(ws) (the sorted output holds that many; kout may be null).
 __global__ __launch_bounds__(TPB) void bins_decode_kernel(long long T, long long n,
                                                           int32_t *__restrict__ bins) {
   const long long t = (long long)blockIdx.x * TPB + threadIdx.x;
@@ -684,7 +708,7 @@ template <typename K>
 int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t *vout,
                      long long n, int begin_bit, int end_bit, void *ws, hipStream_t st,
                      bool first_counts_ready = false, int32_t *tile_bins = nullptr,
-                     long long num_tiles = 0) {
+                     long long num_tiles = 0, bool drop = false) {
   if (n <= 0) return 0;
   const SortPlan p = sort_plan(n, begin_bit, end_bit);
   if (p.passes == 0) {
@@ -700,6 +724,8 @@ int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t
   const bool rts = g_sort_rts;
   uint32_t *rts_counts = status;
   uint32_t *rts_partial = status + (size_t)p.nblocks * p.radix;
+  uint32_t *kept = sort_kept_word(ws);
+  drop = drop && rts;
   if (!rts) {
     note(hipMemsetAsync(ws, 0, radix_ws_bytes(n, begin_bit, end_bit), st), "hipMemsetAsync");
     // Few, fat histogram blocks: every block flushes passes x 256 counters with global
@@ -724,17 +750,21 @@ int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t
     if (rts) {  // reduce-then-scan: tile digit counts -> one exclusive scan -> offsets
       offs = rts_counts;
       const int sh = begin_bit + q * p.width;
+      const uint32_t *ndev = drop && q > 0 ? kept : nullptr;
       if (q == 0 && first_counts_ready) {
         // the key producer already wrote pass 0's tile digit counts (and cleared err)
       } else if (p.items == 16)
         hipLaunchKernelGGL((rts_count_kernel<K, 16>), dim3((unsigned)p.nblocks), dim3(TPB), 0, st,
-                           kin, n, sh, p.width, p.nblocks, offs, q == 0 ? err : nullptr);
+                           kin, n, sh, p.width, p.nblocks, offs, q == 0 ? err : nullptr,
+                           drop && q == 0, ndev);
       else if (p.items == 8)
         hipLaunchKernelGGL((rts_count_kernel<K, 8>), dim3((unsigned)p.nblocks), dim3(TPB), 0, st,
-                           kin, n, sh, p.width, p.nblocks, offs, q == 0 ? err : nullptr);
+                           kin, n, sh, p.width, p.nblocks, offs, q == 0 ? err : nullptr,
+                           drop && q == 0, ndev);
       else
         hipLaunchKernelGGL((rts_count_kernel<K, 4>), dim3((unsigned)p.nblocks), dim3(TPB), 0, st,
-                           kin, n, sh, p.width, p.nblocks, offs, q == 0 ? err : nullptr);
+                           kin, n, sh, p.width, p.nblocks, offs, q == 0 ? err : nullptr,
+                           drop && q == 0, ndev);
       hipLaunchKernelGGL(rts_rowscan_kernel, dim3((unsigned)p.radix), dim3(1024), 0, st, offs,
                          p.nblocks, rts_partial);
     }
@@ -743,7 +773,8 @@ int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t
                      kin, vin, ko, vo, n, begin_bit + q * p.width, p.width,                    \
                      rts ? rts_partial : hist + q * 256,                                       \
                      tickets + q, status + (size_t)q * p.nblocks * p.radix, err, tb,       \
-                     g_sort_ticket, offs, p.nblocks, last ? tile_bins : nullptr)
+                     g_sort_ticket, offs, p.nblocks, last ? tile_bins : nullptr, drop && q == 0,  \
+                     drop && q > 0 ? kept : nullptr, drop && q == 0 ? kept : nullptr)
 #define OS_PASS_W(Wd)                                                                       \
   do {                                                                                      \
     if (p.items == 16) OS_PASS(Wd, 16); else if (p.items == 8) OS_PASS(Wd, 8);             \
@@ -792,8 +823,9 @@ __device__ __forceinline__ void tile_bbox(float x, float y, float radius, int tb
 // loads here so that the depth-ordered passes need ONE gather per Gaussian:
 // rec[g] = {tile allotment, x0 | y0 << 16, x1 | y1 << 16, 0} (tile bbox; < 65536 tiles per axis).
 // One workgroup per depth-sort tile (TPB * ITEMS keys): with counts != null it also writes the
-// tile's histogram of the first sort digit (reduce-then-scan pass 0) and clears the sort's
-// error word, saving the sort its first count launch.
+// tile's histogram of the first sort digit over the visible keys (reduce-then-scan pass 0 of
+// the compacting depth sort) and clears the sort's error word, saving the sort its first count
+// launch.
 template <int ITEMS>
 __global__ __launch_bounds__(TPB) void depth_keys_kernel(int n, const float *__restrict__ xys,
                                                          const float *__restrict__ depths,
@@ -823,7 +855,7 @@ __global__ __launch_bounds__(TPB) void depth_keys_kernel(int n, const float *__r
     const uint32_t key = vis ? __float_as_uint(depths[i]) : 0xFFFFFFFFu;
     keys[i] = key;
     vals[i] = (uint32_t)i;
-    if (counts) atomicAdd(&h[key & 0xFFu], 1u);
+    if (counts && vis) atomicAdd(&h[key & 0xFFu], 1u);  // the compacting sort drops culled keys
     const int c = vis ? num_tiles_hit[i] : 0;
     uint4 q = {c > 0 ? (uint32_t)c : 0u, 0u, 0u, 0u};
     if (c > 0) {
@@ -841,11 +873,14 @@ __global__ __launch_bounds__(TPB) void depth_keys_kernel(int n, const float *__r
 }
 
 // Depth-ordered allotments and boxes: cnt[p], box[p] from the p-th Gaussian's record (the
-// one random gather of the binning); the visible count is the index where the depth-sorted
-// keys reach the culled sentinel.  One workgroup per scan tile (SC_TILE entries): it also
-// writes the tile's allotment sum, the first step of the device scan of cnt.
+// one random gather of the binning).  The visible count: with kept (compacting depth sort) the
+// sort's kept-key count -- order holds only the visible Gaussians and the positions past them
+// get zero allotments; otherwise the index where the depth-sorted keys reach the culled
+// sentinel.  One workgroup per scan tile (SC_TILE entries): it also writes the tile's
+// allotment sum, the first step of the device scan of cnt.
 __global__ __launch_bounds__(TPB) void gather_counts_kernel(int n, const uint32_t *__restrict__ order,
                                                             const uint32_t *__restrict__ skeys,
+                                                            const uint32_t *__restrict__ kept,
                                                             const uint4 *__restrict__ rec,
                                                             uint32_t *__restrict__ cnt,
                                                             uint2 *__restrict__ box,
@@ -854,6 +889,26 @@ __global__ __launch_bounds__(TPB) void gather_counts_kernel(int n, const uint32_
   __shared__ uint32_t lds[TPB / 64];
   const long long base = (long long)blockIdx.x * SC_TILE;
   uint32_t sum = 0;
+  if (kept) {
+    const long long nv = min((long long)n, (long long)*kept);
+    if (blockIdx.x == 0 && threadIdx.x == 0) *num_visible = (int)nv;
+#pragma unroll
+    for (int k = 0; k < SC_ITEMS; ++k) {
+      const long long p = base + k * TPB + threadIdx.x;
+      if (p < nv) {
+        const uint4 q = rec[order[p]];
+        cnt[p] = q.x;
+        box[p] = make_uint2(q.y, q.z);
+        sum += q.x;
+      } else if (p < n) {
+        cnt[p] = 0u;
+      }
+    }
+    uint32_t total;
+    block_exclusive_scan<TPB>(sum, total, lds);
+    if (threadIdx.x == 0) partial[blockIdx.x] = total;
+    return;
+  }
 #pragma unroll
   for (int k = 0; k < SC_ITEMS; ++k) {
     const long long p = base + k * TPB + threadIdx.x;
@@ -1816,6 +1871,12 @@ extern "C" int gsplat_debug_bins_from_sort(int on) {
   return 0;
 }
 
+extern "C" int gsplat_debug_compact_depth_sort(int on) {
+  const int prev = g_compact_depth_sort;
+  if (on >= 0) g_compact_depth_sort = on != 0;
+  return prev;
+}
+
 extern "C" int gsplat_debug_depth_sort_wide(int on) {
   g_depth_sort_wide = on != 0;
   return 0;
@@ -1897,7 +1958,12 @@ static int bin_count_impl(int num_points, const float *xys, const float *depths,
   // depth keys + records; in reduce-then-scan mode also the sort's pass-0 tile counts
   const SortPlan sp = sort_plan(n, 0, 32);
   const bool wide = g_depth_sort_wide && g_sort_rts;  // three 11-bit passes (radix_sort_pairs_wide)
-  const bool pre = g_sort_rts && !keyed && !wide;  // keyed / wide: the sort counts pass 0 itself
+  // the reduce-then-scan depth sort compacts: its first pass drops the culled Gaussians'
+  // all-ones keys, so the later passes, the gather and the emission see only the visible ones
+  const bool compact = g_sort_rts && !wide && g_compact_depth_sort;
+  // depth_keys_kernel counts pass 0 (visible keys) for the compacting sort; keyed: the sort
+  // counts pass 0 itself
+  const bool pre = compact && !keyed;
   uint32_t *c0 = pre ? rts_tile_counts(p.rs_ws) : nullptr;
 #define DEPTH_KEYS(It)                                                                      \
   hipLaunchKernelGGL(depth_keys_kernel<It>, dim3((unsigned)sp.nblocks), dim3(TPB), 0, st, n, xys, \
@@ -1913,13 +1979,16 @@ static int bin_count_impl(int num_points, const float *xys, const float *depths,
     radix_sort_pairs_wide(p.dkeys_a, p.dvals_a, p.dkeys_b, p.dvals_b, p.dkeys_s, p.order, n,
                           p.rs_ws, st);
   else
-    radix_sort_pairs<uint32_t>(p.dkeys_a, p.dvals_a, p.dkeys_b, p.dvals_b, p.dkeys_s, p.order, n,
-                               0, 32, p.rs_ws, st, pre);
+    radix_sort_pairs<uint32_t>(p.dkeys_a, p.dvals_a, p.dkeys_b, p.dvals_b,
+                               compact ? nullptr : p.dkeys_s, p.order, n, 0, 32, p.rs_ws, st,
+                               pre, nullptr, 0, compact);
   // depth-ordered allotments (+ per-tile sums) -> scan -> offsets and I = d_counts[1]
   const int nb = (int)cdiv(n, SC_TILE);
-  uint32_t *partial = (uint32_t *)p.rs_ws;  // the sort is done with its workspace
+  // the kept count sits in the sort workspace's head, before the tile counts reused below
+  const uint32_t *kept = compact ? sort_kept_word(p.rs_ws) : nullptr;
+  uint32_t *partial = rts_tile_counts(p.rs_ws);  // the sort is done with its tile counts
   hipLaunchKernelGGL(gather_counts_kernel, dim3(nb), dim3(TPB), 0, st, n, p.order, p.dkeys_s,
-                     p.rec, p.cnt, p.box, d_counts, partial);
+                     kept, p.rec, p.cnt, p.box, d_counts, partial);
   hipLaunchKernelGGL(scan_partials_kernel, dim3(1), dim3(1024), 0, st, partial, nb,
                      (uint32_t *)(d_counts + 1));
   hipLaunchKernelGGL(scan_downsweep_kernel, dim3(nb), dim3(TPB), 0, st, p.cnt, (long long)n,

@@ -401,6 +401,11 @@ int gsplat_debug_sort_scheme(int reduce_then_scan);
 /* Depth sort of gsplat_bin_count: four 8-bit passes (0, default) or three 11-bit passes (1,
  * slower: ablation); both give the identical stable order. */
 int gsplat_debug_depth_sort_wide(int on);
+/* Depth sort of gsplat_bin_count (reduce-then-scan, 8-bit passes): its first pass drops the
+ * culled Gaussians' keys so that the later passes, the allotment gather and the emission run
+ * over the visible Gaussians only (1, default), or sorts all N keys (0).  Identical outputs.
+ * Returns the previous setting; -1 only queries. */
+int gsplat_debug_compact_depth_sort(int on);
 /* Tile table of gsplat_bin_emit from the last tile-sort pass (1, default: no sorted keys are
  * written or re-read) or from a bin-edges kernel over the sorted keys (0); identical tables. */
 int gsplat_debug_bins_from_sort(int on);

@@ -51,11 +51,11 @@ def headline(request, gpu, oracle_lib):
                 colors=colors, opac=opac, config=request.param)
 
 
-@pytest.mark.parametrize("scheme", ["rts", "rts11", "edges", "onesweep", "bucket"])
+@pytest.mark.parametrize("scheme", ["rts", "full", "rts11", "edges", "onesweep", "bucket"])
 def test_headline_binning_bitexact(gpu, headline, scheme):
     """Sorted binning under the radix-sort pass schemes (reduce-then-scan with four 8-bit
-    depth passes (shipped) or three 11-bit ones, one-sweep) and the tile-bucketing scheme
-    (per-tile LDS sort): all bit-exact."""
+    depth passes compacting the culled Gaussians away (shipped) or sorting all N keys, or three
+    11-bit ones, one-sweep) and the tile-bucketing scheme (per-tile LDS sort): all bit-exact."""
     h, cam = headline, headline["cam"]
     assert h["ref"]["num_intersects"] > 1 << 20
     if scheme != "rts" and h["config"] in ("c4", "c5"):
@@ -64,6 +64,7 @@ def test_headline_binning_bitexact(gpu, headline, scheme):
     _lib.call("gsplat_debug_binning_scheme", 1 if scheme == "bucket" else 0)
     _lib.call("gsplat_debug_depth_sort_wide", 1 if scheme == "rts11" else 0)
     _lib.call("gsplat_debug_bins_from_sort", 0 if scheme == "edges" else 1)
+    _lib.lib().gsplat_debug_compact_depth_sort(0 if scheme == "full" else 1)
     try:
         I, gids, bins = bin_gaussians(h["xys"], h["depths"], h["radii"], h["nth"], cam.height,
                                       cam.width)
@@ -72,6 +73,7 @@ def test_headline_binning_bitexact(gpu, headline, scheme):
         _lib.call("gsplat_debug_binning_scheme", 0)
         _lib.call("gsplat_debug_depth_sort_wide", 0)
         _lib.call("gsplat_debug_bins_from_sort", 1)
+        _lib.lib().gsplat_debug_compact_depth_sort(1)
     assert I == h["ref"]["num_intersects"]
     np.testing.assert_array_equal(_np(gids), h["ref"]["gaussian_ids_sorted"])
     np.testing.assert_array_equal(_np(bins), h["ref"]["tile_bins"])

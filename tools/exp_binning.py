@@ -1,0 +1,42 @@
+"""Binning switch A/B (same scene, same process): bin_gaussians time per call with the depth
+sort compacting the culled Gaussians away or not (gsplat_debug_compact_depth_sort) and the tile
+table from the last tile-sort pass or from a bin-edges kernel (gsplat_debug_bins_from_sort).
+CFGS (default "headline c4 c5").  Run under rocprofv3 --kernel-trace --stats for the split."""
+import os, sys
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+import torch
+import bench
+from gaussctrl_exp_amd import _lib
+from gaussctrl_exp_amd.project_gaussians import project_gaussians
+from gaussctrl_exp_amd.rasterize import bin_gaussians
+
+dev = torch.device("cuda:0")
+L = _lib.lib()
+for cfg in os.environ.get("CFGS", "headline c4 c5").split():
+    sc, cam = bench.make_workload(cfg, 0, dev)
+    cam = cam.to(dev)
+    with torch.no_grad():
+        xys, depths, radii, conics, nth, _ = project_gaussians(
+            sc.means, torch.exp(sc.scales), 1, sc.quats / sc.quats.norm(dim=-1, keepdim=True),
+            *cam.project_args())
+    del sc
+    for rep in range(2):
+        for compact in (1, 0):
+            for from_sort in (1, 0):
+                L.gsplat_debug_compact_depth_sort(compact)
+                _lib.call("gsplat_debug_bins_from_sort", from_sort)
+                for _ in range(3):
+                    bin_gaussians(xys, depths, radii, nth, cam.height, cam.width)
+                torch.cuda.synchronize()
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                for _ in range(20):
+                    bin_gaussians(xys, depths, radii, nth, cam.height, cam.width)
+                e.record()
+                torch.cuda.synchronize()
+                print(f"{cfg} compact={compact} bins_from_sort={from_sort}: bin_gaussians "
+                      f"{s.elapsed_time(e) / 20:.4f} ms", flush=True)
+    L.gsplat_debug_compact_depth_sort(1)
+    _lib.call("gsplat_debug_bins_from_sort", 1)
+    del xys, depths, radii, conics, nth
+    torch.cuda.empty_cache()
