@@ -1314,6 +1314,261 @@ __global__ __launch_bounds__(BK_NT) void bk_place_kernel(int n, const uint4 *__r
   }
 }
 
+// ---- tile counting sort of the depth-ordered intersections (ABLATION, bit-exact) ----
+// Measured (tools/exp_binning.py, bin_gaussians per call, same process): headline 0.267 ms
+// against 0.255 ms for emission + two LSD passes, c4 0.323 vs 0.333, c5 2.35 vs 1.93 ms.  The
+// placement writes are the cost: a (chunk, tile) cell holds I / (chunks x T) ~ 3.5 ids at the
+// headline, so every chunk writes thousands of 4-14 byte runs (partial lines), while an LSD
+// pass with 128 digits writes runs of ~32 per workgroup tile.  Fewer, larger chunks would
+// starve the GPU.  Kept behind gsplat_debug_tile_sort_counting(1).
+// The intersections in depth order (slot j of the exclusive scan `off` of the depth-ordered
+// allotments) are placed straight into their tile buckets, stably, without ever writing the
+// (tile, id) pairs: gsplat's stable sort by tile of its depth-sorted keys is exactly a
+// counting sort whose ties keep slot order.  Slots are cut into chunks of rpc rounds x 4,096
+// (16 waves x 256: one wave segment each); (1) tc_first_kernel records the owner of every
+// segment's first slot; (2) tc_count_kernel counts each chunk's tiles into LDS and writes one
+// column of the chunk x bucket matrix M; (3) bk_scan_kernel scans M per bucket (exclusive over
+// chunks) and writes tile_bins; (4) tc_place_kernel regenerates each round's 4,096 slots, ranks
+// them stably by tile with two 8-bit LDS radix passes (the ballot-match ranking of
+// os_pass_kernel), and writes every id at its bucket cursor + rank.  Four launches, no key
+// arrays: I x 4 bytes written, against the emission's 8 I plus two 16-byte-per-key sort passes
+// -- but in tiny runs (above).
+constexpr int TC_NT = 1024;
+constexpr int TC_NW = TC_NT / 64;
+constexpr int TC_SEG = 256;                 // slots per wave segment (4 per lane)
+constexpr int TC_ROUND = TC_SEG * TC_NW;    // slots per workgroup round
+constexpr int TC_MAX_CHUNKS = 512;
+
+struct TcSrc {
+  const uint32_t *first, *off, *cnt, *order;
+  const uint2 *box;
+  int n;
+  uint32_t I;
+  int tbx, tby;
+};
+
+__global__ __launch_bounds__(TPB) void tc_first_kernel(int n, const uint32_t *__restrict__ cnt,
+                                                       const uint32_t *__restrict__ off,
+                                                       uint32_t *__restrict__ first) {
+  const long long p = (long long)blockIdx.x * TPB + threadIdx.x;
+  if (p >= n) return;
+  const uint32_t c = cnt[p];
+  if (!c) return;
+  const uint32_t o = off[p];
+  for (uint32_t s = (o + TC_SEG - 1) / TC_SEG; s <= (o + c - 1) / TC_SEG; ++s) first[s] = (uint32_t)p;
+}
+
+// Slots seg * 256 + k * 64 + lane (k < 4) of the depth-ordered intersection list: tile (T for
+// an allotment's padding past its box, as emit_kernel; ~0 past I) and Gaussian id.  The wave
+// holds a window of 64 consecutive depth-ordered Gaussians starting at the segment's first
+// owner; a slot's owner is the largest window lane whose slot range starts at or before it (a
+// six-step shuffle search); the window moves on by 64 while slots lie past its end.
+__device__ __forceinline__ void tc_gen(const TcSrc &S, long long seg, uint32_t (&tile)[4],
+                                       uint32_t (&gid)[4]) {
+  const int lane = threadIdx.x & 63;
+  long long p0 = S.first[seg];
+  uint32_t o, c, b0, b1, g;
+  auto load = [&]() {
+    const long long p = p0 + lane;
+    o = S.I;
+    c = b0 = b1 = g = 0u;
+    if (p < S.n) {
+      o = S.off[p];
+      c = S.cnt[p];
+      if (c) {
+        const uint2 bb = S.box[p];
+        b0 = bb.x;
+        b1 = bb.y;
+        g = S.order[p];
+      }
+    }
+  };
+  load();
+  uint32_t wend = __shfl(o + c, 63, 64);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t j = (uint32_t)(seg * TC_SEG) + (uint32_t)(k * 64 + lane);
+    bool todo = j < S.I;
+    tile[k] = ~0u;
+    gid[k] = 0u;
+    while (true) {
+      const bool here = todo && j < wend;
+      int q = 0;
+#pragma unroll
+      for (int step = 32; step >= 1; step >>= 1) {
+        const uint32_t oq = __shfl(o, (q + step) & 63, 64);
+        if (q + step <= 63 && oq <= j) q += step;
+      }
+      const uint32_t li = j - __shfl(o, q, 64);
+      const uint32_t q0 = __shfl(b0, q, 64), q1 = __shfl(b1, q, 64), qg = __shfl(g, q, 64);
+      if (here) {
+        const int qx0 = (int)(q0 & 0xFFFFu), qy0 = (int)(q0 >> 16);
+        const int qx1 = (int)(q1 & 0xFFFFu), qy1 = (int)(q1 >> 16);
+        const int qbw = max(qx1 - qx0, 1);
+        const int qarea = max(qx1 - qx0, 0) * max(qy1 - qy0, 0);
+        uint32_t t;
+        if ((int)li < qarea) {
+          const int ly = li < (1u << 20)
+                             ? (int)(((float)li + 0.5f) * __builtin_amdgcn_rcpf((float)qbw))
+                             : (int)li / qbw;
+          t = (uint32_t)((qy0 + ly) * S.tbx + qx0 + ((int)li - ly * qbw));
+        } else {
+          t = (uint32_t)(S.tbx * S.tby);
+        }
+        tile[k] = t;
+        gid[k] = qg;
+        todo = false;
+      }
+      if (!__any(todo)) break;
+      p0 += 64;  // wave-uniform
+      load();
+      wend = __shfl(o + c, 63, 64);
+    }
+  }
+}
+
+__global__ __launch_bounds__(TC_NT) void tc_count_kernel(TcSrc S, int rpc, int nbk,
+                                                         uint32_t *__restrict__ M,
+                                                         uint32_t *__restrict__ ctr) {
+  extern __shared__ uint32_t hist[];
+  for (int i = threadIdx.x; i < nbk; i += TC_NT) hist[i] = 0u;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *ctr = 0u;  // bk_scan's last-block counter
+  __syncthreads();
+  const int wave = threadIdx.x >> 6;
+  for (int r = 0; r < rpc; ++r) {
+    const long long seg = ((long long)blockIdx.x * rpc + r) * TC_NW + wave;
+    if (seg * TC_SEG >= (long long)S.I) break;  // wave-uniform
+    uint32_t tile[4], gid[4];
+    tc_gen(S, seg, tile, gid);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (tile[k] != ~0u) atomicAdd(&hist[tile[k]], 1u);
+  }
+  __syncthreads();
+  uint32_t *col = M + (size_t)blockIdx.x * nbk;
+  for (int i = threadIdx.x; i < nbk; i += TC_NT) col[i] = hist[i];
+}
+
+// One stable LDS radix pass over the workgroup's 4,096 16-bit keys (item order: wave, k,
+// lane): digit (key >> shift) & 255 ranked by ballot match with per-wave counters, then
+// offset by the digit's exclusive count over earlier waves and earlier digits.
+__device__ __forceinline__ void tc_rank_pass(const uint32_t (&key)[4], int shift,
+                                             uint32_t (&pos)[4], uint32_t *wcnt /*[16][256]*/,
+                                             uint32_t *dofs /*[256]*/, uint32_t *tmp) {
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const unsigned long long lt = (1ull << lane) - 1ull;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) wcnt[wave * 256 + u * 64 + lane] = 0u;
+  wave_lds_sync();
+  uint32_t rank[4], dig[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t d = (key[k] >> shift) & 0xFFu;
+    dig[k] = d;
+    unsigned long long peers = ~0ull;
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const bool bit = (d >> b) & 1u;
+      const unsigned long long m = __ballot(bit);
+      peers &= bit ? m : ~m;
+    }
+    const int leader = (int)__builtin_ctzll(peers);
+    uint32_t old = 0;
+    if (leader == lane) old = atomicAdd(&wcnt[wave * 256 + d], (uint32_t)__popcll(peers));
+    old = __shfl(old, leader, 64);
+    rank[k] = old + (uint32_t)__popcll(peers & lt);
+  }
+  __syncthreads();
+  uint32_t s = 0;
+  if (tid < 256) {
+#pragma unroll
+    for (int w = 0; w < TC_NW; ++w) {
+      const uint32_t c = wcnt[w * 256 + tid];
+      wcnt[w * 256 + tid] = s;
+      s += c;
+    }
+  }
+  uint32_t tot;
+  const uint32_t ex = block_exclusive_scan<TC_NT>(tid < 256 ? s : 0u, tot, tmp);
+  if (tid < 256) dofs[tid] = ex;
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 4; ++k) pos[k] = dofs[dig[k]] + wcnt[wave * 256 + dig[k]] + rank[k];
+  __syncthreads();  // wcnt / dofs are reused by the next pass
+}
+
+__global__ __launch_bounds__(TC_NT) void tc_place_kernel(TcSrc S, int rpc, int nbk,
+                                                         const uint32_t *__restrict__ M,
+                                                         const uint32_t *__restrict__ start,
+                                                         uint32_t *__restrict__ ids) {
+  extern __shared__ uint32_t smem[];
+  uint32_t *cur = smem;                                          // [nbk]: bucket cursors
+  uint32_t *valA = cur + ((nbk + 3) & ~3);                       // [4096]
+  uint32_t *wcnt = valA + TC_ROUND;                              // [16][256]
+  uint32_t *dofs = wcnt + TC_NW * 256;                           // [256]
+  uint32_t *tmp = dofs + 256;                                    // [16]
+  uint16_t *keyA = reinterpret_cast<uint16_t *>(tmp + 16);       // [4096]
+  uint16_t *keyB = keyA + TC_ROUND;                              // [4096]
+  const uint32_t *col = M + (size_t)blockIdx.x * nbk;
+  for (int i = threadIdx.x; i < nbk; i += TC_NT) cur[i] = start[i] + col[i];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  for (int r = 0; r < rpc; ++r) {
+    const long long rbase = ((long long)blockIdx.x * rpc + r) * TC_ROUND;
+    if (rbase >= (long long)S.I) break;  // workgroup-uniform
+    const uint32_t nvalid = (uint32_t)min((long long)TC_ROUND, (long long)S.I - rbase);
+    const long long seg = rbase / TC_SEG + wave;
+    uint32_t key[4], gid[4], pos[4];
+    if (seg * TC_SEG < (long long)S.I) {
+      tc_gen(S, seg, key, gid);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) key[k] = ~0u, gid[k] = 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) key[k] = key[k] == ~0u ? 0xFFFFu : key[k];  // past I: last
+    __syncthreads();  // the previous round's readers of keyB / cur are done
+    tc_rank_pass(key, 0, pos, wcnt, dofs, tmp);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      keyA[pos[k]] = (uint16_t)key[k];
+      valA[pos[k]] = gid[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int i = wave * TC_SEG + k * 64 + lane;
+      key[k] = keyA[i];
+      gid[k] = valA[i];
+    }
+    tc_rank_pass(key, 8, pos, wcnt, dofs, tmp);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) keyB[pos[k]] = (uint16_t)key[k];
+    __syncthreads();
+    // bucket cursor minus the run's first sorted position at each run start, so that the id
+    // at sorted position i goes to cur[t] + i; then the run length is added at its end
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t i = pos[k];
+      if (i < nvalid && (i == 0 || keyB[i - 1] != (uint16_t)key[k])) cur[key[k]] -= i;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (pos[k] < nvalid) ids[cur[key[k]] + pos[k]] = gid[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t i = pos[k];
+      if (i < nvalid && (i == nvalid - 1 || keyB[i + 1] != (uint16_t)key[k])) cur[key[k]] += i + 1;
+    }
+  }
+}
+
+size_t tc_place_lds(int nbk) {
+  return (size_t)(((nbk + 3) & ~3) + TC_ROUND + TC_NW * 256 + 256 + 16) * 4 +
+         (size_t)2 * TC_ROUND * 2;
+}
+
 // ---- per-tile LSD radix sort (bk_sort_kernel) ----
 // ITEMS = 0: the MSD kernel's layout (key/val arrays of CAPX entries)
 template <int NT, int ITEMS>
@@ -1846,6 +2101,33 @@ BkWs carve_bk(void *base, int n, long long I, long long T) {
   return w;
 }
 
+// tile counting sort, phase 2: segment owners, the chunk x bucket matrix, bucket totals /
+// starts, the scan's last-block counter
+struct TcWs {
+  uint32_t *first, *M, *tot, *start, *ctr;
+  int nchunks, rpc, nbk;
+  size_t bytes;
+};
+
+TcWs carve_tc(void *base, long long I, long long T) {
+  TcWs w;
+  Carver c(base);
+  const long long rounds = I > 0 ? cdiv(I, (long long)TC_ROUND) : 1;
+  w.rpc = (int)max(1LL, cdiv(rounds, (long long)TC_MAX_CHUNKS));
+  w.nchunks = (int)cdiv(rounds, (long long)w.rpc);
+  w.nbk = (int)(T + 1);
+  w.first = c.take<uint32_t>((size_t)(I > 0 ? cdiv(I, (long long)TC_SEG) : 1) * 4);
+  w.M = c.take<uint32_t>((size_t)w.nchunks * w.nbk * 4);
+  w.tot = c.take<uint32_t>((size_t)w.nbk * 4);
+  w.start = c.take<uint32_t>((size_t)w.nbk * 4);
+  w.ctr = c.take<uint32_t>(4);
+  w.bytes = c.off;
+  return w;
+}
+
+bool g_tile_counting = false;  // gsplat_debug_tile_sort_counting (ablation; 0: two LSD passes)
+bool use_tc(long long T) { return g_tile_counting && T + 1 <= BK_MAX_BUCKETS; }
+
 bool g_bucket = false;  // gsplat_debug_binning_scheme
 int g_bk_dbg = 0;      // gsplat_debug_binning_scheme(bucket | ablation bits << 1)
 bool use_bucket(long long T) { return g_bucket && T + 1 <= BK_MAX_BUCKETS; }
@@ -1869,6 +2151,12 @@ extern "C" int gsplat_debug_sort_items(int items) {
 extern "C" int gsplat_debug_bins_from_sort(int on) {
   g_bins_from_sort = on != 0;
   return 0;
+}
+
+extern "C" int gsplat_debug_tile_sort_counting(int on) {
+  const int prev = g_tile_counting;
+  if (on >= 0) g_tile_counting = on != 0;
+  return prev;
 }
 
 extern "C" int gsplat_debug_compact_depth_sort(int on) {
@@ -1901,9 +2189,14 @@ extern "C" int gsplat_debug_binning_scheme(int bucket) {
 
 extern "C" size_t gsplat_bin_emit_workspace_size_for(int num_points, int64_t num_intersects,
                                                      int tile_bounds_x, int tile_bounds_y) {
-  const size_t sorted = carve_phase2(nullptr, num_intersects).bytes;
+  size_t sorted = carve_phase2(nullptr, num_intersects).bytes;
   const long long T = (long long)tile_bounds_x * tile_bounds_y;
-  if (num_points < 0 || num_intersects < 0 || T <= 0 || !use_bucket(T)) return sorted;
+  if (num_points < 0 || num_intersects < 0 || T <= 0) return sorted;
+  if (use_tc(T)) {
+    const size_t tc = carve_tc(nullptr, num_intersects, T).bytes;
+    if (tc > sorted) sorted = tc;
+  }
+  if (!use_bucket(T)) return sorted;
   const size_t bk = carve_bk(nullptr, num_points, num_intersects, T).bytes;
   return bk > sorted ? bk : sorted;
 }
@@ -2057,6 +2350,27 @@ extern "C" int gsplat_bin_emit(int num_points, int64_t num_intersects, int tile_
     hipLaunchKernelGGL((bk_sort_kernel<1024, 14>), dim3(w.nbk), dim3(1024), 0, st, w.nbk,
                        (uint32_t)(TPB * 16 + 1), 0xFFFFFFFFu, w.start, w.tot, w.ids, p1.dkeys_a,
                        (uint32_t *)gaussian_ids_sorted, w.ka, w.va, w.kb, w.vb, 0, w.fail);
+    return check_launch("bin_emit");
+  }
+  if (use_tc(T) && workspace1_bytes >= p1.bytes &&
+      workspace2_bytes >= carve_tc(nullptr, num_intersects, T).bytes) {
+    // tile counting sort straight from the depth-ordered allotments (see tc_place_kernel)
+    const TcWs w = carve_tc(workspace2, num_intersects, T);
+    if (num_intersects == 0 || num_points == 0) {
+      note(hipMemsetAsync(tile_bins, 0, (size_t)T * 2 * sizeof(int32_t), st), "hipMemsetAsync");
+      return check_launch("bin_emit");
+    }
+    const int n = num_points;
+    const TcSrc S{w.first, p1.off, p1.cnt, p1.order, p1.box, n, (uint32_t)num_intersects,
+                  tile_bounds_x, tile_bounds_y};
+    hipLaunchKernelGGL(tc_first_kernel, dim3(cdiv(n, TPB)), dim3(TPB), 0, st, n, p1.cnt, p1.off,
+                       w.first);
+    hipLaunchKernelGGL(tc_count_kernel, dim3(w.nchunks), dim3(TC_NT), (size_t)w.nbk * 4, st, S,
+                       w.rpc, w.nbk, w.M, w.ctr);
+    hipLaunchKernelGGL(bk_scan_kernel, dim3(cdiv(w.nbk, 64)), dim3(BK_NT), 0, st, w.nbk, w.nchunks,
+                       w.M, w.tot, w.start, w.ctr, (int)T, tile_bins);
+    hipLaunchKernelGGL(tc_place_kernel, dim3(w.nchunks), dim3(TC_NT), tc_place_lds(w.nbk), st, S,
+                       w.rpc, w.nbk, w.M, w.start, (uint32_t *)gaussian_ids_sorted);
     return check_launch("bin_emit");
   }
   Phase2 p2 = carve_phase2(workspace2, num_intersects);

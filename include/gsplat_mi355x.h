@@ -406,6 +406,11 @@ int gsplat_debug_depth_sort_wide(int on);
  * over the visible Gaussians only (1, default), or sorts all N keys (0).  Identical outputs.
  * Returns the previous setting; -1 only queries. */
 int gsplat_debug_compact_depth_sort(int on);
+/* Tile sort of gsplat_bin_emit: the emission of (tile, id) pairs plus two LSD radix passes
+ * (0, default), or a counting sort placing the depth-ordered intersections straight into their
+ * tile buckets, stably (1: ablation, frames up to 16,447 tiles; slower -- its placement writes
+ * are runs of a few ids).  Identical outputs.  Returns the previous setting; -1 only queries. */
+int gsplat_debug_tile_sort_counting(int on);
 /* Tile table of gsplat_bin_emit from the last tile-sort pass (1, default: no sorted keys are
  * written or re-read) or from a bin-edges kernel over the sorted keys (0); identical tables. */
 int gsplat_debug_bins_from_sort(int on);

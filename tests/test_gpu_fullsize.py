@@ -51,11 +51,14 @@ def headline(request, gpu, oracle_lib):
                 colors=colors, opac=opac, config=request.param)
 
 
-@pytest.mark.parametrize("scheme", ["rts", "full", "rts11", "edges", "onesweep", "bucket"])
+@pytest.mark.parametrize("scheme", ["rts", "counting", "full", "rts11", "edges", "onesweep",
+                                    "bucket"])
 def test_headline_binning_bitexact(gpu, headline, scheme):
-    """Sorted binning under the radix-sort pass schemes (reduce-then-scan with four 8-bit
-    depth passes compacting the culled Gaussians away (shipped) or sorting all N keys, or three
-    11-bit ones, one-sweep) and the tile-bucketing scheme (per-tile LDS sort): all bit-exact."""
+    """Sorted binning: the shipped scheme (depth sort of reduce-then-scan 8-bit passes compacting
+    the culled Gaussians away, then emission + two LSD tile passes writing the tile table), the
+    tile counting sort, the tile table from a bin-edges kernel, the depth sort over all N keys or
+    in three 11-bit passes or one-sweep, and the tile-bucketing scheme (per-tile LDS sort): all
+    bit-exact."""
     h, cam = headline, headline["cam"]
     assert h["ref"]["num_intersects"] > 1 << 20
     if scheme != "rts" and h["config"] in ("c4", "c5"):
@@ -65,6 +68,7 @@ def test_headline_binning_bitexact(gpu, headline, scheme):
     _lib.call("gsplat_debug_depth_sort_wide", 1 if scheme == "rts11" else 0)
     _lib.call("gsplat_debug_bins_from_sort", 0 if scheme == "edges" else 1)
     _lib.lib().gsplat_debug_compact_depth_sort(0 if scheme == "full" else 1)
+    _lib.lib().gsplat_debug_tile_sort_counting(1 if scheme == "counting" else 0)
     try:
         I, gids, bins = bin_gaussians(h["xys"], h["depths"], h["radii"], h["nth"], cam.height,
                                       cam.width)
@@ -74,6 +78,7 @@ def test_headline_binning_bitexact(gpu, headline, scheme):
         _lib.call("gsplat_debug_depth_sort_wide", 0)
         _lib.call("gsplat_debug_bins_from_sort", 1)
         _lib.lib().gsplat_debug_compact_depth_sort(1)
+        _lib.lib().gsplat_debug_tile_sort_counting(0)
     assert I == h["ref"]["num_intersects"]
     np.testing.assert_array_equal(_np(gids), h["ref"]["gaussian_ids_sorted"])
     np.testing.assert_array_equal(_np(bins), h["ref"]["tile_bins"])
