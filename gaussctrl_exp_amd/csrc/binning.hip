@@ -708,7 +708,7 @@ template <typename K>
 int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t *vout,
                      long long n, int begin_bit, int end_bit, void *ws, hipStream_t st,
                      bool first_counts_ready = false, int32_t *tile_bins = nullptr,
-                     long long num_tiles = 0, bool drop = false) {
+                     long long num_tiles = 0, bool drop = false, int first_pass = 0) {
   if (n <= 0) return 0;
   const SortPlan p = sort_plan(n, begin_bit, end_bit);
   if (p.passes == 0) {
@@ -734,9 +734,10 @@ int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t
     hipLaunchKernelGGL(os_hist_kernel<K>, dim3(hist_blocks), dim3(TPB), 0, st, ka, n, begin_bit,
                        p.width, p.passes, hist);
   }
-  K *kin = ka, *kalt = kb;
-  uint32_t *vin = va, *valt = vb;
-  for (int q = 0; q < p.passes; ++q) {
+  // first_pass = 1: the caller ran pass 0 itself, into (kb, vb)
+  K *kin = first_pass ? kb : ka, *kalt = first_pass ? ka : kb;
+  uint32_t *vin = first_pass ? vb : va, *valt = first_pass ? va : vb;
+  for (int q = first_pass; q < p.passes; ++q) {
     const bool last = q == p.passes - 1;
     K *ko = last ? kout : kalt;
     uint32_t *vo = last ? vout : valt;
@@ -1454,7 +1455,8 @@ __global__ __launch_bounds__(TC_NT) void tc_count_kernel(TcSrc S, int rpc, int n
 // offset by the digit's exclusive count over earlier waves and earlier digits.
 __device__ __forceinline__ void tc_rank_pass(const uint32_t (&key)[4], int shift,
                                              uint32_t (&pos)[4], uint32_t *wcnt /*[16][256]*/,
-                                             uint32_t *dofs /*[256]*/, uint32_t *tmp) {
+                                             uint32_t *dofs /*[256]*/, uint32_t *tmp,
+                                             int width = 8) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const unsigned long long lt = (1ull << lane) - 1ull;
 #pragma unroll
@@ -1463,11 +1465,12 @@ __device__ __forceinline__ void tc_rank_pass(const uint32_t (&key)[4], int shift
   uint32_t rank[4], dig[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    const uint32_t d = (key[k] >> shift) & 0xFFu;
+    const uint32_t d = (key[k] >> shift) & ((1u << width) - 1u);
     dig[k] = d;
     unsigned long long peers = ~0ull;
 #pragma unroll
     for (int b = 0; b < 8; ++b) {
+      if (b >= width) break;  // uniform
       const bool bit = (d >> b) & 1u;
       const unsigned long long m = __ballot(bit);
       peers &= bit ? m : ~m;
@@ -1560,6 +1563,87 @@ __global__ __launch_bounds__(TC_NT) void tc_place_kernel(TcSrc S, int rpc, int n
     for (int k = 0; k < 4; ++k) {
       const uint32_t i = pos[k];
       if (i < nvalid && (i == nvalid - 1 || keyB[i + 1] != (uint16_t)key[k])) cur[key[k]] += i + 1;
+    }
+  }
+}
+
+// ---- the tile sort's first LSD pass, generated (shipped) ----
+// Pass 0 of the tile-id radix sort takes its (tile, id) pairs straight from the depth-ordered
+// allotments (tc_gen) instead of from an emitted key array: ep0_count_kernel histograms each
+// 4,096-slot round's low tile digit (digit-major counts, the reduce-then-scan layout), the row
+// scan makes them offsets, and ep0_place_kernel regenerates the round, ranks it stably by the
+// digit in LDS and writes it out in digit order (runs of ~32 per digit, as an os_pass tile).
+// Saves the emission's 8 I-byte write and pass 0's re-read of it (used for I >= 2^24: see
+// use_emit_pass0).
+__global__ __launch_bounds__(TC_NT) void ep0_count_kernel(TcSrc S, int width, long long nrounds,
+                                                          uint32_t *__restrict__ counts,
+                                                          int *__restrict__ tile_bins) {
+  __shared__ uint32_t h[256];
+  const int tid = threadIdx.x, wave = tid >> 6;
+  // the tile table starts zeroed for the last pass's run ends (emit_kernel's job before)
+  for (long long i = (long long)blockIdx.x * TC_NT + tid; i < 2LL * S.tbx * S.tby;
+       i += (long long)gridDim.x * TC_NT)
+    tile_bins[i] = 0;
+  if (tid < 256) h[tid] = 0u;
+  __syncthreads();
+  const uint32_t mask = (1u << width) - 1u;
+  const long long seg = (long long)blockIdx.x * TC_NW + wave;
+  if (seg * TC_SEG < (long long)S.I) {
+    uint32_t tile[4], gid[4];
+    tc_gen(S, seg, tile, gid);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (tile[k] != ~0u) atomicAdd(&h[tile[k] & mask], 1u);
+  }
+  __syncthreads();
+  if (tid < (1 << width)) counts[(size_t)tid * nrounds + blockIdx.x] = h[tid];
+}
+
+__global__ __launch_bounds__(TC_NT) void ep0_place_kernel(TcSrc S, int width, long long nrounds,
+                                                          const uint32_t *__restrict__ rowtot,
+                                                          const uint32_t *__restrict__ offs,
+                                                          uint32_t *__restrict__ kout,
+                                                          uint32_t *__restrict__ vout) {
+  __shared__ uint32_t keys[TC_ROUND], vals[TC_ROUND];
+  __shared__ uint32_t wcnt[TC_NW * 256], dofs[256], gofs[256], tmp[16];
+  const int tid = threadIdx.x, wave = tid >> 6;
+  const int R = 1 << width;
+  const uint32_t mask = (uint32_t)(R - 1);
+  const long long rbase = (long long)blockIdx.x * TC_ROUND;
+  const uint32_t nvalid = (uint32_t)min((long long)TC_ROUND, (long long)S.I - rbase);
+  {  // digit bases: exclusive scan of the row totals
+    uint32_t tot;
+    const uint32_t hs = block_exclusive_scan<TC_NT>(tid < R ? rowtot[tid] : 0u, tot, tmp);
+    if (tid < R) gofs[tid] = hs + offs[(size_t)tid * nrounds + blockIdx.x];
+  }
+  const long long seg = rbase / TC_SEG + wave;
+  uint32_t key[4], gid[4], pos[4];
+  if (seg * TC_SEG < (long long)S.I) {
+    tc_gen(S, seg, key, gid);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) key[k] = ~0u, gid[k] = 0u;
+  }
+  // slots past I (last round only): the largest digit, so they rank after every valid key
+  uint32_t rk[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) rk[k] = key[k] == ~0u ? mask : key[k];
+  tc_rank_pass(rk, 0, pos, wcnt, dofs, tmp, width);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    keys[pos[k]] = key[k];
+    vals[pos[k]] = gid[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const uint32_t i = (uint32_t)(u * TC_NT + tid);
+    if (i < nvalid) {
+      const uint32_t k = keys[i];
+      const uint32_t d = k & mask;
+      const uint32_t g = gofs[d] + (i - dofs[d]);
+      kout[g] = k;
+      vout[g] = vals[i];
     }
   }
 }
@@ -2055,6 +2139,7 @@ int bits_for(long long v) {  // smallest b with (1 << b) > v
 
 struct Phase2 {
   uint32_t *tk_a, *tv_a, *tk_b, *tv_b, *tk_s;
+  uint32_t *first;  // segment owners of the generated first tile pass (tc_first_kernel)
   void *rs_ws;
   size_t bytes;
 };
@@ -2068,6 +2153,7 @@ Phase2 carve_phase2(void *base, long long I) {
   p.tk_b = c.take<uint32_t>(ii);
   p.tv_b = c.take<uint32_t>(ii);
   p.tk_s = c.take<uint32_t>(ii);
+  p.first = c.take<uint32_t>((size_t)(I > 0 ? cdiv(I, (long long)TC_SEG) : 1) * 4);
   p.rs_ws = c.take<char>(radix_ws_bytes(I, 0, 32));  // >= any tile-key width
   p.bytes = c.off;
   return p;
@@ -2126,6 +2212,15 @@ TcWs carve_tc(void *base, long long I, long long T) {
 }
 
 bool g_tile_counting = false;  // gsplat_debug_tile_sort_counting (ablation; 0: two LSD passes)
+// gsplat_debug_emit_pass0: 0 = emit_kernel + a plain first pass, 1 = generated first pass when
+// the emitted pairs (8 I bytes) would not stay in the 256 MB MALL (I >= 2^24), 2 = always.
+// Measured (tools/exp_binning.py): c5 (83M) 1.93 -> 1.78 ms; headline (7.7M) 0.256 -> 0.268 ms
+// and c4 (8.7M) 0.333 -> 0.338 ms, where the emitted pairs are re-read from the MALL cheaply and
+// the generation's dependent loads (segment owner, then its window) cost more.
+int g_emit_pass0 = 1;
+bool use_emit_pass0(long long I) {
+  return g_emit_pass0 == 2 || (g_emit_pass0 == 1 && I >= (1LL << 24));
+}
 bool use_tc(long long T) { return g_tile_counting && T + 1 <= BK_MAX_BUCKETS; }
 
 bool g_bucket = false;  // gsplat_debug_binning_scheme
@@ -2151,6 +2246,12 @@ extern "C" int gsplat_debug_sort_items(int items) {
 extern "C" int gsplat_debug_bins_from_sort(int on) {
   g_bins_from_sort = on != 0;
   return 0;
+}
+
+extern "C" int gsplat_debug_emit_pass0(int on) {
+  const int prev = g_emit_pass0;
+  if (on >= 0) g_emit_pass0 = on > 2 ? 2 : on;
+  return prev;
 }
 
 extern "C" int gsplat_debug_tile_sort_counting(int on) {
@@ -2385,6 +2486,28 @@ extern "C" int gsplat_bin_emit(int num_points, int64_t num_intersects, int tile_
   }
   const int n = num_points;
   const long long I = num_intersects;
+  const SortPlan tp = sort_plan(I, 0, bits_for(T));
+  if (use_emit_pass0(I) && g_sort_rts && g_bins_from_sort && tp.passes >= 2) {
+    // pass 0 of the tile sort generated from the allotments (ep0_place_kernel), the rest as below
+    const long long nrounds = cdiv(I, (long long)TC_ROUND);
+    uint32_t *ws = (uint32_t *)p2.rs_ws;
+    uint32_t *counts = ws + OS_HEAD_WORDS;                      // rts_tile_counts
+    uint32_t *rowtot = counts + (size_t)tp.nblocks * tp.radix;  // radix_sort_pairs' row totals
+    const TcSrc S{p2.first, p1.off, p1.cnt, p1.order, p1.box, n, (uint32_t)I, tile_bounds_x,
+                  tile_bounds_y};
+    hipLaunchKernelGGL(tc_first_kernel, dim3(cdiv(n, TPB)), dim3(TPB), 0, st, n, p1.cnt, p1.off,
+                       p2.first);
+    hipLaunchKernelGGL(ep0_count_kernel, dim3((unsigned)nrounds), dim3(TC_NT), 0, st, S, tp.width,
+                       nrounds, counts, tile_bins);
+    hipLaunchKernelGGL(rts_rowscan_kernel, dim3((unsigned)tp.radix), dim3(1024), 0, st, counts,
+                       nrounds, rowtot);
+    hipLaunchKernelGGL(ep0_place_kernel, dim3((unsigned)nrounds), dim3(TC_NT), 0, st, S, tp.width,
+                       nrounds, rowtot, counts, p2.tk_b, p2.tv_b);
+    radix_sort_pairs<uint32_t>(p2.tk_a, p2.tv_a, p2.tk_b, p2.tv_b, p2.tk_s,
+                               (uint32_t *)gaussian_ids_sorted, I, 0, bits_for(T), p2.rs_ws, st,
+                               false, tile_bins, T, false, 1);
+    return check_launch("bin_emit");
+  }
   hipLaunchKernelGGL(emit_kernel, dim3(cdiv(n, TPB)), dim3(TPB), 0, st, n, p1.order, p1.cnt,
                      p1.off, p1.box, tile_bounds_x, tile_bounds_y, p2.tk_a, p2.tv_a, tile_bins);
   // the tile sort's last pass writes the tile table itself (runs of equal tile ids) instead of

@@ -411,6 +411,11 @@ int gsplat_debug_compact_depth_sort(int on);
  * tile buckets, stably (1: ablation, frames up to 16,447 tiles; slower -- its placement writes
  * are runs of a few ids).  Identical outputs.  Returns the previous setting; -1 only queries. */
 int gsplat_debug_tile_sort_counting(int on);
+/* First pass of gsplat_bin_emit's tile sort: run over emitted (tile, id) pairs (0), generated
+ * from the depth-ordered allotments without an emitted key array when I >= 2^24 (1, default:
+ * the pairs would not stay in the MALL), or always generated (2).  Identical outputs.  Returns
+ * the previous setting; -1 only queries. */
+int gsplat_debug_emit_pass0(int on);
 /* Tile table of gsplat_bin_emit from the last tile-sort pass (1, default: no sorted keys are
  * written or re-read) or from a bin-edges kernel over the sorted keys (0); identical tables. */
 int gsplat_debug_bins_from_sort(int on);

@@ -150,21 +150,25 @@ def test_sh_unaligned_slab(gpu):
                                rtol=RTOL, atol=ATOL)
 
 
-@pytest.mark.parametrize("scheme", ["counting", "lsd", "bucket"])
+@pytest.mark.parametrize("scheme", ["lsd", "emit", "counting", "bucket"])
 @pytest.mark.parametrize("case", CASES)
 def test_binning_fused_bitexact(gpu, case, scheme):
-    """The tile sort as the shipped counting sort, as emission + two LSD passes, and the
-    tile-bucketing scheme: bit-exact against the oracle's stable sort of gsplat's keys."""
+    """The tile sort as shipped (first LSD pass generated from the depth-ordered allotments),
+    over emitted (tile, id) pairs, as the counting sort, and the tile-bucketing scheme:
+    bit-exact against the oracle's stable sort of gsplat's keys."""
     sc, cam, scales, quats = _inputs(*case)
     g, o = _project_both(gpu, sc, cam, scales, quats)
     xys, depths, radii, conics, nth, cov3d = g
+    L = _lib.lib()
     _lib.call("gsplat_debug_binning_scheme", 1 if scheme == "bucket" else 0)
-    prev = _lib.lib().gsplat_debug_tile_sort_counting(1 if scheme == "counting" else 0)
+    prev = L.gsplat_debug_tile_sort_counting(1 if scheme == "counting" else 0)
+    prev_e = L.gsplat_debug_emit_pass0(0 if scheme == "emit" else 2)
     try:
         I, gids, bins = bin_gaussians(xys, depths, radii, nth, cam.height, cam.width)
     finally:
         _lib.call("gsplat_debug_binning_scheme", 0)
-        _lib.lib().gsplat_debug_tile_sort_counting(prev)
+        L.gsplat_debug_tile_sort_counting(prev)
+        L.gsplat_debug_emit_pass0(prev_e)
     ref = O.bin_and_sort(o[0], o[1], o[2], o[4], cam.tile_bounds)
     assert I == ref["num_intersects"]
     np.testing.assert_array_equal(_np(gids), ref["gaussian_ids_sorted"])
@@ -173,9 +177,9 @@ def test_binning_fused_bitexact(gpu, case, scheme):
 
 def test_binning_counting_inconsistent_allotments(gpu):
     """Caller-supplied num_tiles_hit that disagree with the tile boxes (allotments larger than
-    the box are padded with the sentinel tile, smaller ones truncate the box): the counting
-    tile sort places exactly what the emission + LSD sort does, and the chunks cut Gaussians
-    whose allotment spans several rounds (one Gaussian over 600 tiles)."""
+    the box are padded with the sentinel tile, smaller ones truncate the box): the counting tile
+    sort and the generated first LSD pass place exactly what emission + LSD does, including
+    Gaussians whose allotment spans several rounds (one Gaussian over 600 tiles)."""
     sc, cam, scales, quats = _inputs(20000, 512, 512, 2, 0.003, 0.03, 1.5)
     g, _ = _project_both(gpu, sc, cam, scales, quats)
     xys, depths, radii, conics, nth, cov3d = [t.detach() for t in g]
@@ -185,16 +189,19 @@ def test_binning_counting_inconsistent_allotments(gpu):
     nth[vis[1::7]] = torch.clamp(nth[vis[1::7]] - 1, min=1)
     nth[vis[5]] = 600
     out = []
-    for counting in (1, 0):
-        prev = _lib.lib().gsplat_debug_tile_sort_counting(counting)
+    L = _lib.lib()
+    for counting, gen in ((1, 1), (0, 2), (0, 0)):
+        prev, prev_e = L.gsplat_debug_tile_sort_counting(counting), L.gsplat_debug_emit_pass0(gen)
         try:
             I, gids, bins = bin_gaussians(xys, depths, radii, nth, cam.height, cam.width)
         finally:
-            _lib.lib().gsplat_debug_tile_sort_counting(prev)
+            L.gsplat_debug_tile_sort_counting(prev)
+            L.gsplat_debug_emit_pass0(prev_e)
         out.append((I, _np(gids), _np(bins)))
-    assert out[0][0] == out[1][0] == int(nth[radii > 0].sum())
-    np.testing.assert_array_equal(out[0][1], out[1][1])
-    np.testing.assert_array_equal(out[0][2], out[1][2])
+    for o in out[1:]:
+        assert o[0] == out[0][0] == int(nth[radii > 0].sum())
+        np.testing.assert_array_equal(o[1], out[0][1])
+        np.testing.assert_array_equal(o[2], out[0][2])
 
 
 @pytest.mark.parametrize("W,H,tiles", [(4096, 2400, 38400), (4112, 4096, 65792)])

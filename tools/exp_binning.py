@@ -1,6 +1,7 @@
 """Binning switch A/B (same scene, same process): bin_gaussians time per call with the depth
 sort compacting the culled Gaussians away or not (gsplat_debug_compact_depth_sort) and the tile
-sort as the counting sort or as emission + two LSD passes (gsplat_debug_tile_sort_counting).
+sort's first LSD pass generated from the allotments or run over emitted pairs
+(gsplat_debug_emit_pass0).
 CFGS (default "headline c4 c5").  Run under rocprofv3 --kernel-trace --stats for the split."""
 import os, sys
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
@@ -22,9 +23,9 @@ for cfg in os.environ.get("CFGS", "headline c4 c5").split():
     del sc
     for rep in range(2):
         for compact in (1, 0):
-            for counting in (1, 0):
+            for gen in (2, 0):
                 L.gsplat_debug_compact_depth_sort(compact)
-                L.gsplat_debug_tile_sort_counting(counting)
+                L.gsplat_debug_emit_pass0(gen)
                 for _ in range(3):
                     bin_gaussians(xys, depths, radii, nth, cam.height, cam.width)
                 torch.cuda.synchronize()
@@ -34,9 +35,9 @@ for cfg in os.environ.get("CFGS", "headline c4 c5").split():
                     bin_gaussians(xys, depths, radii, nth, cam.height, cam.width)
                 e.record()
                 torch.cuda.synchronize()
-                print(f"{cfg} compact={compact} counting={counting}: bin_gaussians "
+                print(f"{cfg} compact={compact} gen_pass0={gen}: bin_gaussians "
                       f"{s.elapsed_time(e) / 20:.4f} ms", flush=True)
     L.gsplat_debug_compact_depth_sort(1)
-    L.gsplat_debug_tile_sort_counting(0)
+    L.gsplat_debug_emit_pass0(1)
     del xys, depths, radii, conics, nth
     torch.cuda.empty_cache()
