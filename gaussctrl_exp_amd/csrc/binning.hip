@@ -72,6 +72,24 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t &t
   return wbase + inc - v;
 }
 
+// The lanes of the wave whose digit d equals this lane's (a ballot match over the digit's
+// `width` bits; `valid` lanes only).  Per bit: one sign-extending bit extract (-1 if set), one
+// ballot and one three-input bit operation per 32-lane half: peers &= ~(ballot ^ mask).
+template <int MAXW>
+__device__ __forceinline__ unsigned long long digit_peers(uint32_t d, int width, bool valid) {
+  const unsigned long long v = __ballot(valid);
+  uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+#pragma unroll
+  for (int b = 0; b < MAXW; ++b) {
+    if (b >= width) break;  // uniform
+    const uint32_t mask = (uint32_t)((int32_t)(d << (31 - b)) >> 31);
+    const unsigned long long m = __ballot(mask != 0u);
+    lo &= ~((uint32_t)m ^ mask);
+    hi &= ~((uint32_t)(m >> 32) ^ mask);
+  }
+  return ((unsigned long long)hi << 32) | lo;
+}
+
 __global__ __launch_bounds__(TPB) void scan_reduce_kernel(const uint32_t *__restrict__ in,
                                                           long long m,
                                                           uint32_t *__restrict__ partial) {
@@ -277,7 +295,7 @@ struct OsSmem {
 };
 
 template <typename K, int WIDTH, int ITEMS>
-__global__ __launch_bounds__(TPB) void os_pass_kernel(
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) void os_pass_kernel(
     const K *__restrict__ kin, const uint32_t *__restrict__ vin, K *__restrict__ kout,
     uint32_t *__restrict__ vout, long long n, int shift, int width,
     const uint32_t *__restrict__ hist, uint32_t *__restrict__ ticket_ctr,
@@ -340,22 +358,28 @@ __global__ __launch_bounds__(TPB) void os_pass_kernel(
   // (peers); the group's lowest lane reserves popc(peers) slots of the wave's LDS counter for
   // that digit with ONE returning LDS atomic and the others read the old value from it
   // (a wave's LDS atomics execute in issue order, so the rounds stay ordered).
+  // In groups of four rounds, three sweeps each so the LDS round trips overlap: the matches,
+  // then the counter atomics (in round order), then the reads of the leaders' old values.
+  constexpr int GRP = ITEMS < 4 ? ITEMS : 4;
 #pragma unroll
-  for (int r = 0; r < ITEMS; ++r) {
-    const bool valid = ok[r];
-    const uint32_t d = (uint32_t)(key[r] >> shift) & dmask;
-    unsigned long long peers = __ballot(valid);
+  for (int r0 = 0; r0 < ITEMS; r0 += GRP) {
+    unsigned long long pr[GRP];
+    uint32_t old[GRP];
 #pragma unroll
-    for (int b = 0; b < WIDTH; ++b) {
-      const bool bit = (d >> b) & 1u;
-      const unsigned long long m = __ballot(bit);
-      peers &= bit ? m : ~m;
+    for (int u = 0; u < GRP; ++u)
+      pr[u] = digit_peers<WIDTH>((uint32_t)(key[r0 + u] >> shift) & dmask, WIDTH, ok[r0 + u]);
+#pragma unroll
+    for (int u = 0; u < GRP; ++u) {
+      old[u] = 0u;
+      if (ok[r0 + u] && (int)__builtin_ctzll(pr[u]) == lane)
+        old[u] = atomicAdd(&sm.wcnt[wave][(uint32_t)(key[r0 + u] >> shift) & dmask],
+                           (uint32_t)__popcll(pr[u]));
     }
-    const int leader = valid ? (int)__builtin_ctzll(peers) : lane;
-    uint32_t old = 0;
-    if (valid && leader == lane) old = atomicAdd(&sm.wcnt[wave][d], (uint32_t)__popcll(peers));
-    old = __shfl(old, leader, 64);
-    rank[r] = old + (uint32_t)__popcll(peers & lt);
+#pragma unroll
+    for (int u = 0; u < GRP; ++u) {
+      const int leader = ok[r0 + u] ? (int)__builtin_ctzll(pr[u]) : lane;
+      rank[r0 + u] = __shfl(old[u], leader, 64) + (uint32_t)__popcll(pr[u] & lt);
+    }
   }
   unsigned long long ts2a = 0ull;
   if (tbuf) {
@@ -1462,25 +1486,22 @@ __device__ __forceinline__ void tc_rank_pass(const uint32_t (&key)[4], int shift
 #pragma unroll
   for (int u = 0; u < 4; ++u) wcnt[wave * 256 + u * 64 + lane] = 0u;
   wave_lds_sync();
-  uint32_t rank[4], dig[4];
+  uint32_t rank[4], dig[4], old[4];
+  unsigned long long pr[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    const uint32_t d = (key[k] >> shift) & ((1u << width) - 1u);
-    dig[k] = d;
-    unsigned long long peers = ~0ull;
-#pragma unroll
-    for (int b = 0; b < 8; ++b) {
-      if (b >= width) break;  // uniform
-      const bool bit = (d >> b) & 1u;
-      const unsigned long long m = __ballot(bit);
-      peers &= bit ? m : ~m;
-    }
-    const int leader = (int)__builtin_ctzll(peers);
-    uint32_t old = 0;
-    if (leader == lane) old = atomicAdd(&wcnt[wave * 256 + d], (uint32_t)__popcll(peers));
-    old = __shfl(old, leader, 64);
-    rank[k] = old + (uint32_t)__popcll(peers & lt);
+    dig[k] = (key[k] >> shift) & ((1u << width) - 1u);
+    pr[k] = digit_peers<8>(dig[k], width, true);
   }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    old[k] = 0u;
+    if ((int)__builtin_ctzll(pr[k]) == lane)
+      old[k] = atomicAdd(&wcnt[wave * 256 + dig[k]], (uint32_t)__popcll(pr[k]));
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    rank[k] = __shfl(old[k], (int)__builtin_ctzll(pr[k]), 64) + (uint32_t)__popcll(pr[k] & lt);
   __syncthreads();
   uint32_t s = 0;
   if (tid < 256) {

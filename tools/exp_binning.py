@@ -21,7 +21,22 @@ for cfg in os.environ.get("CFGS", "headline c4 c5").split():
             sc.means, torch.exp(sc.scales), 1, sc.quats / sc.quats.norm(dim=-1, keepdim=True),
             *cam.project_args())
     del sc
-    for rep in range(2):
+    for items in [int(x) for x in os.environ.get("ITEMS_LIST", "").split()]:
+        # keys per thread of every radix pass (0 = automatic: 4 below 4M keys, 16 above)
+        _lib.call("gsplat_debug_sort_items", items)
+        for _ in range(3):
+            bin_gaussians(xys, depths, radii, nth, cam.height, cam.width)
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(20):
+            bin_gaussians(xys, depths, radii, nth, cam.height, cam.width)
+        e.record()
+        torch.cuda.synchronize()
+        print(f"{cfg} sort_items={items}: bin_gaussians {s.elapsed_time(e) / 20:.4f} ms",
+              flush=True)
+    _lib.call("gsplat_debug_sort_items", 0)
+    for rep in range(int(os.environ.get("REPS", "2"))):
         for compact in (1, 0):
             for gen in (2, 0):
                 L.gsplat_debug_compact_depth_sort(compact)
