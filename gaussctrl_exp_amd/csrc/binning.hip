@@ -319,30 +319,42 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
   // Tile index = dispatch order: workgroups are dispatched in increasing ID order, so every
   // tile a workgroup looks back at has already been dispatched and makes progress without it.
   // (An atomic ticket serialised ~1k workgroups on one counter: 9 us per pass.)
+  // the tile's keys are loaded before the digit-base scan (its barriers would otherwise keep
+  // the loads from going out): tile = blockIdx.x; the debug ticket mode reloads below
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  K key[ITEMS];
+  uint32_t val[ITEMS], rank[ITEMS];
+  bool ok[ITEMS];
+  // (indices clamped into [0, n): no per-element branch, so all 2 x ITEMS loads are in flight
+  // together; the validity mask is applied once they are consumed)
+  auto load_tile = [&](uint32_t tt) {
+    const long long sg = (long long)tt * TPB * ITEMS + (long long)wave * (ITEMS * 64);
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) {
+      const long long i = min(sg + r * 64 + lane, n - 1);
+      key[r] = kin[i];
+      val[r] = vin[i];
+    }
+  };
+  // the digit total first: vmcnt retires in issue order, so the scan below waits for it alone
+  const uint32_t hval = hist[min(tid, R - 1)];
+  load_tile(blockIdx.x);
   if (tid == 0) sm.ticket = use_ticket ? atomicAdd(ticket_ctr, 1u) : blockIdx.x;
 #pragma unroll
   for (int w = 0; w < 4; ++w) sm.wcnt[w][tid] = 0;
   {  // digit bases: exclusive scan of the pass histogram (one-sweep) or of the digit row
      // totals (reduce-then-scan)
-    uint32_t h = tid < R ? hist[tid] : 0u, tot;
+    uint32_t h = tid < R ? hval : 0u, tot;
     sm.hscan[tid] = block_exclusive_scan<TPB>(h, tot, sm.scan_tmp);  // contains barriers
     if (n_out && blockIdx.x == 0 && tid == 0) *n_out = tot;
   }
   const uint32_t t = sm.ticket;
   unsigned long long ts1 = tbuf ? __builtin_amdgcn_s_memrealtime() : 0ull;
+  if (use_ticket) load_tile(t);
   const long long base = (long long)t * TPB * ITEMS;
-  const long long seg = base + (long long)wave * (ITEMS * 64);
-  const unsigned long long lt = (1ull << lane) - 1ull;
-
-  K key[ITEMS];
-  uint32_t val[ITEMS], rank[ITEMS];
-  bool ok[ITEMS];
 #pragma unroll
   for (int r = 0; r < ITEMS; ++r) {
-    const long long i = seg + r * 64 + lane;
-    const bool valid = i < n;
-    key[r] = valid ? kin[i] : (K)0;
-    val[r] = valid ? vin[i] : 0u;
+    const bool valid = base + (long long)wave * (ITEMS * 64) + r * 64 + lane < n;
     ok[r] = valid && !(drop && key[r] == (K)~(K)0);
   }
   unsigned long long ts2 = 0ull;
