@@ -883,21 +883,34 @@ __global__ __launch_bounds__(TPB) void depth_keys_kernel(int n, const float *__r
     __syncthreads();
   }
   const long long base = (long long)blockIdx.x * TPB * ITEMS;
+  // every input of the tile loaded up front (clamped indices, no per-item branch): the loads
+  // are in flight together instead of one wait per Gaussian
+  int rr[ITEMS], cc[ITEMS];
+  float dd[ITEMS];
+  float2 xy[ITEMS];
+#pragma unroll
+  for (int k = 0; k < ITEMS; ++k) {
+    const long long i = min(base + k * TPB + tid, (long long)n - 1);
+    rr[k] = radii[i];
+    dd[k] = depths[i];
+    cc[k] = num_tiles_hit[i];
+    xy[k] = reinterpret_cast<const float2 *>(xys)[i];
+  }
 #pragma unroll
   for (int k = 0; k < ITEMS; ++k) {
     const long long i = base + k * TPB + tid;
     if (i >= n) break;
-    const int r = radii[i];
+    const int r = rr[k];
     const bool vis = r > 0;
-    const uint32_t key = vis ? __float_as_uint(depths[i]) : 0xFFFFFFFFu;
+    const uint32_t key = vis ? __float_as_uint(dd[k]) : 0xFFFFFFFFu;
     keys[i] = key;
     vals[i] = (uint32_t)i;
     if (counts && vis) atomicAdd(&h[key & 0xFFu], 1u);  // the compacting sort drops culled keys
-    const int c = vis ? num_tiles_hit[i] : 0;
+    const int c = vis ? cc[k] : 0;
     uint4 q = {c > 0 ? (uint32_t)c : 0u, 0u, 0u, 0u};
     if (c > 0) {
       int x0, x1, y0, y1;
-      tile_bbox(xys[2 * i], xys[2 * i + 1], (float)r, tbx, tby, x0, x1, y0, y1);
+      tile_bbox(xy[k].x, xy[k].y, (float)r, tbx, tby, x0, x1, y0, y1);
       q.y = (uint32_t)x0 | ((uint32_t)y0 << 16);
       q.z = (uint32_t)x1 | ((uint32_t)y1 << 16);
     }
@@ -929,16 +942,32 @@ __global__ __launch_bounds__(TPB) void gather_counts_kernel(int n, const uint32_
   if (kept) {
     const long long nv = min((long long)n, (long long)*kept);
     if (blockIdx.x == 0 && threadIdx.x == 0) *num_visible = (int)nv;
+    if (base < nv) {  // workgroup-uniform
+      // all ids, then all records, with clamped indices and no per-item branch, so each level
+      // of the gather has its 16 loads in flight together
+      uint32_t ord[SC_ITEMS];
+      uint4 q[SC_ITEMS];
 #pragma unroll
-    for (int k = 0; k < SC_ITEMS; ++k) {
-      const long long p = base + k * TPB + threadIdx.x;
-      if (p < nv) {
-        const uint4 q = rec[order[p]];
-        cnt[p] = q.x;
-        box[p] = make_uint2(q.y, q.z);
-        sum += q.x;
-      } else if (p < n) {
-        cnt[p] = 0u;
+      for (int k = 0; k < SC_ITEMS; ++k)
+        ord[k] = order[min(base + k * TPB + threadIdx.x, nv - 1)];
+#pragma unroll
+      for (int k = 0; k < SC_ITEMS; ++k) q[k] = rec[ord[k]];
+#pragma unroll
+      for (int k = 0; k < SC_ITEMS; ++k) {
+        const long long p = base + k * TPB + threadIdx.x;
+        if (p < nv) {
+          cnt[p] = q[k].x;
+          box[p] = make_uint2(q[k].y, q[k].z);
+          sum += q[k].x;
+        } else if (p < n) {
+          cnt[p] = 0u;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < SC_ITEMS; ++k) {
+        const long long p = base + k * TPB + threadIdx.x;
+        if (p < n) cnt[p] = 0u;
       }
     }
     uint32_t total;
