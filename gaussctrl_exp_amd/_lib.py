@@ -75,6 +75,7 @@ SIGNATURES = {
     "gsplat_debug_sort_scheme": (_I, [_I]),
     "gsplat_debug_depth_sort_wide": (_I, [_I]),
     "gsplat_debug_compact_depth_sort": (_I, [_I]),
+    "gsplat_debug_depth_key_range": (_I, [_I]),
     "gsplat_debug_tile_sort_counting": (_I, [_I]),
     "gsplat_debug_emit_pass0": (_I, [_I]),
     "gsplat_debug_bins_from_sort": (_I, [_I]),

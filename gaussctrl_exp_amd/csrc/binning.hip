@@ -184,12 +184,31 @@ constexpr size_t OS_HEAD_WORDS = OS_MAX_PASSES * 256 + OS_MAX_PASSES + 8;
 
 // [head words][one-sweep status: passes x nblocks x radix | reduce-then-scan tile counts
 // nblocks x radix + scan scratch]
-size_t radix_ws_bytes(long long n, int begin_bit, int end_bit) {
-  SortPlan p = sort_plan(n, begin_bit, end_bit);
+size_t radix_main_bytes(const SortPlan &p) {
   const size_t onesweep = (size_t)p.passes * p.nblocks * p.radix * sizeof(uint32_t);
   const size_t rts = (size_t)p.nblocks * p.radix * sizeof(uint32_t) +
                      scan_ws_bytes((long long)p.nblocks * p.radix);
   return OS_HEAD_WORDS * sizeof(uint32_t) + (onesweep > rts ? onesweep : rts);
+}
+
+// [head][per-pass state][per-tile key range: nblocks x (and, or)]
+size_t radix_ws_bytes(long long n, int begin_bit, int end_bit) {
+  const SortPlan p = sort_plan(n, begin_bit, end_bit);
+  return radix_main_bytes(p) + (size_t)p.nblocks * 2 * sizeof(uint32_t);
+}
+
+// Key range of the compacting depth sort: the AND and OR of all kept keys.  A digit on which
+// they agree is the same for every key, so its LSD pass is the identity permutation: its count
+// and row-scan kernels return at once and its pass kernel only copies (the launches are issued
+// before the range is known).  blk: per-tile (and, or) from pass 0's count (or the key kernel);
+// fin: their reduction, by pass 0's row scan.
+struct KeyRange {
+  uint32_t *blk = nullptr;
+  uint32_t *fin = nullptr;
+  long long nblk = 0;
+};
+__device__ __forceinline__ bool digit_constant(const uint32_t *fin, int shift, int width) {
+  return fin && ((((fin[0] ^ fin[1]) >> shift) & ((1u << width) - 1u)) == 0u);
 }
 
 template <typename K>
@@ -237,14 +256,18 @@ __global__ __launch_bounds__(TPB) void rts_count_kernel(const K *__restrict__ ke
                                                         uint32_t *__restrict__ counts,
                                                         uint32_t *__restrict__ err,
                                                         bool drop = false,
-                                                        const uint32_t *__restrict__ n_dev = nullptr) {
+                                                        const uint32_t *__restrict__ n_dev = nullptr,
+                                                        KeyRange kr = {}, int pass = 0) {
   __shared__ uint32_t h[256];
+  __shared__ uint32_t kand, kor;
   const int tid = threadIdx.x;
   if (err && blockIdx.x == 0 && tid == 0) *err = 0;  // the look-back error word stays clear
+  if (pass > 0 && digit_constant(kr.fin, shift, width)) return;  // identity pass
   if (n_dev) n = min(n, (long long)*n_dev);
   const int R = 1 << width;
   const uint32_t dmask = (uint32_t)(R - 1);
   h[tid] = 0;
+  if (tid == 0) kand = ~0u, kor = 0u;
   __syncthreads();
   const long long base = (long long)blockIdx.x * TPB * ITEMS;
   K k[ITEMS];
@@ -253,12 +276,24 @@ __global__ __launch_bounds__(TPB) void rts_count_kernel(const K *__restrict__ ke
     const long long i = base + r * TPB + tid;
     k[r] = i < n ? keys[i] : (K)0;
   }
+  uint32_t a = ~0u, o = 0u;
 #pragma unroll
   for (int r = 0; r < ITEMS; ++r)
-    if (base + r * TPB + tid < n && !(drop && k[r] == (K)~(K)0))
+    if (base + r * TPB + tid < n && !(drop && k[r] == (K)~(K)0)) {
       atomicAdd(&h[(uint32_t)(k[r] >> shift) & dmask], 1u);
+      a &= (uint32_t)k[r];
+      o |= (uint32_t)k[r];
+    }
+  if (pass == 0 && kr.blk) {
+    atomicAnd(&kand, a);
+    atomicOr(&kor, o);
+  }
   __syncthreads();
   if (tid < R) counts[(size_t)tid * nblocks + blockIdx.x] = h[tid];
+  if (pass == 0 && kr.blk && tid == 0) {
+    kr.blk[2 * blockIdx.x] = kand;
+    kr.blk[2 * blockIdx.x + 1] = kor;
+  }
 }
 
 // Reduce-then-scan pass, part 2: one workgroup per digit scans that digit's row of tile
@@ -266,8 +301,30 @@ __global__ __launch_bounds__(TPB) void rts_count_kernel(const K *__restrict__ ke
 // totals into digit bases itself.  (One launch instead of a three-kernel device scan.)
 __global__ __launch_bounds__(1024) void rts_rowscan_kernel(uint32_t *__restrict__ counts,
                                                            long long nblocks,
-                                                           uint32_t *__restrict__ rowtot) {
+                                                           uint32_t *__restrict__ rowtot,
+                                                           KeyRange kr = {}, int pass = 0,
+                                                           int shift = 0, int width = 8) {
   __shared__ uint32_t lds[16];
+  __shared__ uint32_t kand, kor;
+  if (pass > 0 && digit_constant(kr.fin, shift, width)) return;  // identity pass
+  if (blockIdx.x == gridDim.x - 1 && pass == 0 && kr.blk) {
+    // the extra last workgroup: the key range of the whole sort (off the rows' critical path)
+    if (threadIdx.x == 0) kand = ~0u, kor = 0u;
+    __syncthreads();
+    uint32_t a = ~0u, o = 0u;
+    for (long long i = threadIdx.x; i < kr.nblk; i += 1024) {
+      a &= kr.blk[2 * i];
+      o |= kr.blk[2 * i + 1];
+    }
+    atomicAnd(&kand, a);
+    atomicOr(&kor, o);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      kr.fin[0] = kand;
+      kr.fin[1] = kor;
+    }
+    return;
+  }
   uint32_t *row = counts + (size_t)blockIdx.x * nblocks;
   uint32_t running = 0;
   for (long long c0 = 0; c0 < nblocks; c0 += 1024) {
@@ -302,13 +359,34 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     uint32_t *__restrict__ status, uint32_t *__restrict__ err,
     unsigned long long *__restrict__ tbuf, bool use_ticket, const uint32_t *__restrict__ offs,
     long long nblocks, int32_t *__restrict__ bins = nullptr, bool drop = false,
-    const uint32_t *__restrict__ n_dev = nullptr, uint32_t *__restrict__ n_out = nullptr) {
+    const uint32_t *__restrict__ n_dev = nullptr, uint32_t *__restrict__ n_out = nullptr,
+    const uint32_t *__restrict__ kfin = nullptr) {
   // compacting sort (reduce-then-scan only): with drop, all-ones keys are left out (pass 0 of
   // the depth sort: culled Gaussians), and block 0 stores the kept count to n_out; later passes
   // sort min(n, *n_dev) keys and the workgroups past them exit at once.
   if (n_dev) {
     n = min(n, (long long)*n_dev);
     if (!use_ticket && (long long)blockIdx.x * TPB * ITEMS >= n) return;  // whole workgroup
+  }
+  if (digit_constant(kfin, shift, width)) {  // every key has the same digit: a stable copy
+    const long long b0 = (long long)blockIdx.x * TPB * ITEMS;
+    K ck[ITEMS];
+    uint32_t cv[ITEMS];
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) {  // all loads in flight before the first store
+      const long long i = min(b0 + r * TPB + threadIdx.x, n - 1);
+      if (kout) ck[r] = kin[i];
+      cv[r] = vin[i];
+    }
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) {
+      const long long i = b0 + r * TPB + threadIdx.x;
+      if (i < n) {
+        if (kout) kout[i] = ck[r];
+        vout[i] = cv[r];
+      }
+    }
+    return;
   }
   __shared__ OsSmem<K, ITEMS> sm;
   // optional phase timestamps (debug hook gsplat_debug_sort_timing): [ticket][6]
@@ -548,6 +626,12 @@ constexpr int WD_TILE = TPB * WD_ITEMS;
 bool g_depth_sort_wide = false;  // ablation switch (gsplat_debug_depth_sort_wide)
 bool g_bins_from_sort = true;    // tile table from the last tile-sort pass (gsplat_debug_bins_from_sort)
 bool g_compact_depth_sort = true;  // depth sort drops culled keys (gsplat_debug_compact_depth_sort)
+// constant-digit depth passes only copy (gsplat_debug_depth_key_range: 0 off, 1 from 2^22 keys,
+// 2 always).  The range costs ~8 us (the AND / OR in the first count and a reduction block in
+// its row scan) and a skipped pass saves its ranking, worth it for large sorts only: c5 (4.8M
+// keys) -25 us, c4 (1.1M, no constant digit) +10 us (tools/exp_binning.py, RANGE_LIST).
+int g_key_range = 1;
+bool use_key_range(long long n) { return g_key_range == 2 || (g_key_range == 1 && n >= (1LL << 22)); }
 
 long long wd_nblocks(long long n) { return n > 0 ? cdiv(n, (long long)WD_TILE) : 0; }
 size_t radix_wide_ws_bytes(long long n) {
@@ -762,6 +846,12 @@ int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t
   uint32_t *rts_partial = status + (size_t)p.nblocks * p.radix;
   uint32_t *kept = sort_kept_word(ws);
   drop = drop && rts;
+  KeyRange kr;
+  if (drop && use_key_range(n)) {
+    kr.blk = (uint32_t *)((char *)ws + radix_main_bytes(p));
+    kr.fin = sort_kept_word(ws) + 1;
+    kr.nblk = p.nblocks;
+  }
   if (!rts) {
     note(hipMemsetAsync(ws, 0, radix_ws_bytes(n, begin_bit, end_bit), st), "hipMemsetAsync");
     // Few, fat histogram blocks: every block flushes passes x 256 counters with global
@@ -788,22 +878,24 @@ int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t
       offs = rts_counts;
       const int sh = begin_bit + q * p.width;
       const uint32_t *ndev = drop && q > 0 ? kept : nullptr;
+      // first_counts_ready: the key kernel wrote pass 0's counts and key ranges (kr.blk)
       if (q == 0 && first_counts_ready) {
         // the key producer already wrote pass 0's tile digit counts (and cleared err)
       } else if (p.items == 16)
         hipLaunchKernelGGL((rts_count_kernel<K, 16>), dim3((unsigned)p.nblocks), dim3(TPB), 0, st,
                            kin, n, sh, p.width, p.nblocks, offs, q == 0 ? err : nullptr,
-                           drop && q == 0, ndev);
+                           drop && q == 0, ndev, kr, q);
       else if (p.items == 8)
         hipLaunchKernelGGL((rts_count_kernel<K, 8>), dim3((unsigned)p.nblocks), dim3(TPB), 0, st,
                            kin, n, sh, p.width, p.nblocks, offs, q == 0 ? err : nullptr,
-                           drop && q == 0, ndev);
+                           drop && q == 0, ndev, kr, q);
       else
         hipLaunchKernelGGL((rts_count_kernel<K, 4>), dim3((unsigned)p.nblocks), dim3(TPB), 0, st,
                            kin, n, sh, p.width, p.nblocks, offs, q == 0 ? err : nullptr,
-                           drop && q == 0, ndev);
-      hipLaunchKernelGGL(rts_rowscan_kernel, dim3((unsigned)p.radix), dim3(1024), 0, st, offs,
-                         p.nblocks, rts_partial);
+                           drop && q == 0, ndev, kr, q);
+      hipLaunchKernelGGL(rts_rowscan_kernel,
+                         dim3((unsigned)p.radix + (q == 0 && kr.blk ? 1u : 0u)), dim3(1024), 0,
+                         st, offs, p.nblocks, rts_partial, kr, q, sh, p.width);
     }
 #define OS_PASS(Wd, It)                                                                     \
   hipLaunchKernelGGL((os_pass_kernel<K, Wd, It>), dim3((unsigned)p.nblocks), dim3(TPB), 0, st,   \
@@ -811,7 +903,8 @@ int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t
                      rts ? rts_partial : hist + q * 256,                                       \
                      tickets + q, status + (size_t)q * p.nblocks * p.radix, err, tb,       \
                      g_sort_ticket, offs, p.nblocks, last ? tile_bins : nullptr, drop && q == 0,  \
-                     drop && q > 0 ? kept : nullptr, drop && q == 0 ? kept : nullptr)
+                     drop && q > 0 ? kept : nullptr, drop && q == 0 ? kept : nullptr,          \
+                     q > 0 ? kr.fin : nullptr)
 #define OS_PASS_W(Wd)                                                                       \
   do {                                                                                      \
     if (p.items == 16) OS_PASS(Wd, 16); else if (p.items == 8) OS_PASS(Wd, 8);             \
@@ -874,14 +967,18 @@ __global__ __launch_bounds__(TPB) void depth_keys_kernel(int n, const float *__r
                                                          uint4 *__restrict__ rec,
                                                          uint32_t *__restrict__ counts,
                                                          long long nblocks,
-                                                         uint32_t *__restrict__ err) {
+                                                         uint32_t *__restrict__ err,
+                                                         uint32_t *__restrict__ kblk = nullptr) {
   __shared__ uint32_t h[256];
+  __shared__ uint32_t kand, kor;
   const int tid = threadIdx.x;
   if (counts) {
     h[tid] = 0;
+    if (tid == 0) kand = ~0u, kor = 0u;
     if (blockIdx.x == 0 && tid == 0) *err = 0;
     __syncthreads();
   }
+  uint32_t ka = ~0u, ko = 0u;  // the visible keys' AND / OR (KeyRange)
   const long long base = (long long)blockIdx.x * TPB * ITEMS;
   // every input of the tile loaded up front (clamped indices, no per-item branch): the loads
   // are in flight together instead of one wait per Gaussian
@@ -905,7 +1002,11 @@ __global__ __launch_bounds__(TPB) void depth_keys_kernel(int n, const float *__r
     const uint32_t key = vis ? __float_as_uint(dd[k]) : 0xFFFFFFFFu;
     keys[i] = key;
     vals[i] = (uint32_t)i;
-    if (counts && vis) atomicAdd(&h[key & 0xFFu], 1u);  // the compacting sort drops culled keys
+    if (counts && vis) {  // the compacting sort drops culled keys
+      atomicAdd(&h[key & 0xFFu], 1u);
+      ka &= key;
+      ko |= key;
+    }
     const int c = vis ? cc[k] : 0;
     uint4 q = {c > 0 ? (uint32_t)c : 0u, 0u, 0u, 0u};
     if (c > 0) {
@@ -917,8 +1018,16 @@ __global__ __launch_bounds__(TPB) void depth_keys_kernel(int n, const float *__r
     rec[i] = q;
   }
   if (counts) {
+    if (kblk) {
+      atomicAnd(&kand, ka);
+      atomicOr(&kor, ko);
+    }
     __syncthreads();
     counts[(size_t)tid * nblocks + blockIdx.x] = h[tid];
+    if (kblk && tid == 0) {
+      kblk[2 * blockIdx.x] = kand;
+      kblk[2 * blockIdx.x + 1] = kor;
+    }
   }
 }
 
@@ -2322,6 +2431,12 @@ extern "C" int gsplat_debug_tile_sort_counting(int on) {
   return prev;
 }
 
+extern "C" int gsplat_debug_depth_key_range(int on) {
+  const int prev = g_key_range;
+  if (on >= 0) g_key_range = on > 2 ? 2 : on;
+  return prev;
+}
+
 extern "C" int gsplat_debug_compact_depth_sort(int on) {
   const int prev = g_compact_depth_sort;
   if (on >= 0) g_compact_depth_sort = on != 0;
@@ -2424,7 +2539,9 @@ static int bin_count_impl(int num_points, const float *xys, const float *depths,
 #define DEPTH_KEYS(It)                                                                      \
   hipLaunchKernelGGL(depth_keys_kernel<It>, dim3((unsigned)sp.nblocks), dim3(TPB), 0, st, n, xys, \
                      depths, radii, num_tiles_hit, tile_bounds_x, tile_bounds_y, p.dkeys_a,    \
-                     p.dvals_a, p.rec, c0, sp.nblocks, sort_err_word(p.rs_ws))
+                     p.dvals_a, p.rec, c0, sp.nblocks, sort_err_word(p.rs_ws),                 \
+                     pre && use_key_range(n)                                                  \
+                         ? (uint32_t *)((char *)p.rs_ws + radix_main_bytes(sp)) : nullptr)
   if (keyed) {
     // keys, ids and records already written (gsplat_fused_preprocess_forward_binned)
   } else if (sp.items == 16) DEPTH_KEYS(16);

@@ -406,6 +406,11 @@ int gsplat_debug_depth_sort_wide(int on);
  * over the visible Gaussians only (1, default), or sorts all N keys (0).  Identical outputs.
  * Returns the previous setting; -1 only queries. */
 int gsplat_debug_compact_depth_sort(int on);
+/* Depth sort of gsplat_bin_count: LSD passes whose digit is the same for every kept key (from
+ * the keys' AND / OR, found during the first pass) only copy -- from 2^22 keys (1, default),
+ * always (2) -- or rank as any pass (0).  Identical outputs.  Returns the previous setting; -1
+ * only queries. */
+int gsplat_debug_depth_key_range(int on);
 /* Tile sort of gsplat_bin_emit: the emission of (tile, id) pairs plus two LSD radix passes
  * (0, default), or a counting sort placing the depth-ordered intersections straight into their
  * tile buckets, stably (1: ablation, frames up to 16,447 tiles; slower -- its placement writes

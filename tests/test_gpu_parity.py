@@ -204,6 +204,32 @@ def test_binning_counting_inconsistent_allotments(gpu):
         np.testing.assert_array_equal(o[2], out[0][2])
 
 
+@pytest.mark.parametrize("fixed", [(0x5A00, 0xFF00), (0x5A5A00, 0xFFFF00), (0x0, 0x0)])
+def test_binning_depth_key_range(gpu, fixed):
+    """Depth keys whose bytes 1 (and 2) are the same for every visible Gaussian: those LSD
+    passes are identities and only copy (gsplat_debug_depth_key_range), also in the middle of
+    the pass sequence -- bit-exact vs the oracle with and without the shortcut."""
+    sc, cam, scales, quats = _inputs(20000, 512, 512, 2, 0.003, 0.03, 1.5)
+    g, o = _project_both(gpu, sc, cam, scales, quats)
+    xys, depths, radii, conics, nth, cov3d = [t.detach() for t in g]
+    val, mask = fixed
+    bits = np.random.default_rng(7).integers(0, 1 << 23, size=depths.shape[0], dtype=np.uint32)
+    bits = (bits & ~np.uint32(mask)) | np.uint32(val) | np.uint32(0x40000000)  # in [2, 4)
+    d = bits.view(np.float32)
+    ref = O.bin_and_sort(o[0], d, o[2], o[4], cam.tile_bounds)
+    L = _lib.lib()
+    for on in (2, 0):
+        prev = L.gsplat_debug_depth_key_range(on)
+        try:
+            I, gids, bins = bin_gaussians(xys, torch.from_numpy(d).to(gpu), radii, nth,
+                                          cam.height, cam.width)
+        finally:
+            L.gsplat_debug_depth_key_range(prev)
+        assert I == ref["num_intersects"]
+        np.testing.assert_array_equal(_np(gids), ref["gaussian_ids_sorted"])
+        np.testing.assert_array_equal(_np(bins), ref["tile_bins"])
+
+
 @pytest.mark.parametrize("W,H,tiles", [(4096, 2400, 38400), (4112, 4096, 65792)])
 def test_binning_large_tile_grid_bitexact(gpu, W, H, tiles):
     """Large tile grids: 38,400 tiles (16-bit tile keys, two 8-bit sort passes) and 65,792

@@ -36,6 +36,20 @@ for cfg in os.environ.get("CFGS", "headline c4 c5").split():
         print(f"{cfg} sort_items={items}: bin_gaussians {s.elapsed_time(e) / 20:.4f} ms",
               flush=True)
     _lib.call("gsplat_debug_sort_items", 0)
+    for rng in [int(x) for x in os.environ.get("RANGE_LIST", "").split()]:
+        # depth passes whose digit is constant only copy (2: always, 1: auto) or rank (0)
+        L.gsplat_debug_depth_key_range(rng)
+        for _ in range(3):
+            bin_gaussians(xys, depths, radii, nth, cam.height, cam.width)
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(20):
+            bin_gaussians(xys, depths, radii, nth, cam.height, cam.width)
+        e.record()
+        torch.cuda.synchronize()
+        print(f"{cfg} key_range={rng}: bin_gaussians {s.elapsed_time(e) / 20:.4f} ms", flush=True)
+    L.gsplat_debug_depth_key_range(1)
     for rep in range(int(os.environ.get("REPS", "2"))):
         for compact in (1, 0):
             for gen in (2, 0):
