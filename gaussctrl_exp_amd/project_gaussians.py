@@ -15,6 +15,7 @@ from torch import Tensor
 from torch.autograd import Function
 
 from . import _lib
+from .ops import ops
 
 
 def project_gaussians(
@@ -119,16 +120,10 @@ class _ProjectGaussians(Function):
             torch.zeros((n, 3), device=dev, dtype=torch.float32)
         if v_depths is not None:  # NULL = zero depth gradient
             v_depths = _as_f32(v_depths).contiguous()
-        v_mean3d = torch.empty((n, 3), device=dev, dtype=torch.float32)
-        v_scale = torch.empty((n, 3), device=dev, dtype=torch.float32)
-        v_quat = torch.empty((n, 4), device=dev, dtype=torch.float32)
-        P = _lib.ptr
-        _lib.call("gsplat_project_gaussians_backward", n, P(means3d), P(scales),
-                  float(ctx.glob_scale), P(quats), P(viewmat), P(projmat), float(ctx.fx),
-                  float(ctx.fy), float(ctx.cx), float(ctx.cy), int(ctx.img_height),
-                  int(ctx.img_width), P(cov3d), P(radii), P(conics), P(v_xys), P(v_depths),
-                  P(v_conics), None, None, P(v_mean3d), P(v_scale), P(v_quat),
-                  _lib.stream(dev))
+        v_mean3d, v_scale, v_quat = ops().project_bwd(
+            means3d, scales, float(ctx.glob_scale), quats, viewmat, projmat, float(ctx.fx),
+            float(ctx.fy), float(ctx.cx), float(ctx.cy), int(ctx.img_height),
+            int(ctx.img_width), cov3d, radii, conics, v_xys, v_depths, v_conics)
         # one gradient per input of forward (gsplat 0.1.2.1 returns None for the rest)
         return (v_mean3d, v_scale, None, v_quat, None, None, None, None, None, None, None,
                 None, None, None)

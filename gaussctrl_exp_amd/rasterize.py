@@ -23,6 +23,7 @@ from torch import Tensor
 from torch.autograd import Function
 
 from . import _lib, quirks
+from .ops import ops
 
 BLOCK_X, BLOCK_Y = 16, 16
 
@@ -330,14 +331,15 @@ class _RasterizeGaussians(Function):
             final_Ts = torch.zeros(H, W, device=dev)
             final_idx = torch.zeros(H, W, device=dev, dtype=torch.int32)
         else:
-            out_img = torch.empty((H, W, C), device=dev, dtype=torch.float32)
-            final_Ts = torch.empty((H, W), device=dev, dtype=torch.float32)
-            final_idx = torch.empty((H, W), device=dev, dtype=torch.int32)
             P = _lib.ptr
             grads = C == 3 and any(ctx.needs_input_grad)
             # list-split backward (C = 3, gradients wanted): the forward records checkpoints
             chunk = _lib.query("gsplat_rasterize_chunk_size", tbx, tby, num_intersects) \
                 if grads else 0
+            if chunk > 0 or (grads and _lib.lib().gsplat_debug_raster_variant_is_default()):
+                out_img = torch.empty((H, W, C), device=dev, dtype=torch.float32)
+                final_Ts = torch.empty((H, W), device=dev, dtype=torch.float32)
+                final_idx = torch.empty((H, W), device=dev, dtype=torch.int32)
             if grads and _lib.lib().gsplat_debug_raster_variant_is_default():
                 # the backward accumulates into per-Gaussian gradient records that this blend
                 # zeroes as its waves finish (no memset in the backward; every record, since
@@ -363,9 +365,9 @@ class _RasterizeGaussians(Function):
                           num_intersects, chunk, P(ckpt), ckpt.numel(), _lib.stream(dev))
                 ctx.chunk, ctx.ckpt = chunk, ckpt
             else:
-                _lib.call("gsplat_rasterize_forward", tbx, tby, H, W, C, P(gaussian_ids_sorted),
-                          P(tile_bins), P(xys), P(conics), P(colors), P(opacity), P(background),
-                          P(out_img), P(final_Ts), P(final_idx), _lib.stream(dev))
+                out_img, final_Ts, final_idx = ops().raster_fwd(
+                    tbx, tby, H, W, gaussian_ids_sorted, tile_bins, xys, conics, colors,
+                    opacity, background)
         if not hasattr(ctx, "chunk"):
             ctx.chunk, ctx.ckpt = 0, None
         if not hasattr(ctx, "rec"):
@@ -403,13 +405,20 @@ class _RasterizeGaussians(Function):
             v_out_img = v_out_img.float().contiguous()
             if v_out_alpha is not None:  # NULL = zero alpha gradient
                 v_out_alpha = v_out_alpha.float().contiguous()
+            tbx = (W + BLOCK_X - 1) // BLOCK_X
+            tby = (H + BLOCK_Y - 1) // BLOCK_Y
+            if ctx.rec is None and ctx.chunk == 0:  # plain list walk: the torch op layer
+                v_xy, v_conic, v_colors, v_opacity = ops().raster_bwd(
+                    tbx, tby, H, W, gaussian_ids_sorted, tile_bins, xys, conics, colors, opacity,
+                    background, final_Ts, final_idx, v_out_img, v_out_alpha,
+                    quirks.backward_alpha_clamp())
+                return (v_xy, None, None, v_conic, None, v_colors,
+                        v_opacity.view(ctx.opacity_shape), None, None, None, None)
             v_xy = torch.empty((num_points, 2), device=dev, dtype=torch.float32)
             v_conic = torch.empty((num_points, 3), device=dev, dtype=torch.float32)
             v_colors = torch.empty((num_points, C), device=dev, dtype=torch.float32)
             v_opacity = torch.empty(ctx.opacity_shape, device=dev, dtype=torch.float32)
             P = _lib.ptr
-            tbx = (W + BLOCK_X - 1) // BLOCK_X
-            tby = (H + BLOCK_Y - 1) // BLOCK_Y
             if ctx.rec is not None:  # records cleared by the forward blend
                 rec, st = ctx.rec, _lib.stream(dev)
                 _lib.call("gsplat_rasterize_backward_records", tbx, tby, H, W, num_points,
@@ -425,19 +434,12 @@ class _RasterizeGaussians(Function):
                         None)
             wsz = _lib.query("gsplat_rasterize_backward_workspace_size", num_points, C)
             ws = torch.empty((max(wsz, 1),), device=dev, dtype=torch.uint8)
-            if ctx.chunk > 0:
-                _lib.call("gsplat_rasterize_backward_chunked", tbx, tby, H, W, num_points,
-                          P(gaussian_ids_sorted), P(tile_bins), P(xys), P(conics), P(colors),
-                          P(opacity), P(background), P(final_Ts), P(final_idx), P(v_out_img),
-                          P(v_out_alpha), quirks.backward_alpha_clamp(), P(v_xy), P(v_conic),
-                          P(v_colors), P(v_opacity), ctx.num_intersects, ctx.chunk,
-                          P(ctx.ckpt), ctx.ckpt.numel(), P(ws), wsz, _lib.stream(dev))
-            else:
-                _lib.call("gsplat_rasterize_backward", tbx, tby, H, W, C, num_points,
-                          P(gaussian_ids_sorted), P(tile_bins), P(xys), P(conics), P(colors),
-                          P(opacity), P(background), P(final_Ts), P(final_idx), P(v_out_img),
-                          P(v_out_alpha), quirks.backward_alpha_clamp(), P(v_xy), P(v_conic),
-                          P(v_colors), P(v_opacity), P(ws), wsz, _lib.stream(dev))
+            _lib.call("gsplat_rasterize_backward_chunked", tbx, tby, H, W, num_points,
+                      P(gaussian_ids_sorted), P(tile_bins), P(xys), P(conics), P(colors),
+                      P(opacity), P(background), P(final_Ts), P(final_idx), P(v_out_img),
+                      P(v_out_alpha), quirks.backward_alpha_clamp(), P(v_xy), P(v_conic),
+                      P(v_colors), P(v_opacity), ctx.num_intersects, ctx.chunk,
+                      P(ctx.ckpt), ctx.ckpt.numel(), P(ws), wsz, _lib.stream(dev))
 
         return (
             v_xy,  # xys

@@ -12,6 +12,7 @@ from torch import Tensor
 from torch.autograd import Function
 
 from . import _lib, exchange
+from .ops import ops
 
 
 def num_sh_bases(degree: int) -> int:
@@ -99,31 +100,22 @@ class _SphericalHarmonics(Function):
                              f"viewdirs {tuple(viewdirs.shape)}")
         viewdirs = viewdirs.float().contiguous()
         coeffs = coeffs.float().contiguous()
-        dev = _lib.check_device("spherical_harmonics", viewdirs, coeffs)
+        _lib.check_device("spherical_harmonics", viewdirs, coeffs)
         ctx.degree = degree
         ctx.degrees_to_use = degrees_to_use
         ctx.save_for_backward(viewdirs)
         ctx.exchange = exchange.active()  # data-parallel SH-gradient exchange, if any
-        colors = torch.empty((num_points, 3), device=dev, dtype=torch.float32)
-        _lib.call("gsplat_compute_sh_forward", num_points, degree, int(degrees_to_use),
-                  _lib.ptr(viewdirs), _lib.ptr(coeffs), _lib.ptr(colors), _lib.stream(dev))
-        return colors
+        return ops().sh_fwd(degree, int(degrees_to_use), viewdirs, coeffs)
 
     @staticmethod
     def backward(ctx, v_colors: Tensor):
         (viewdirs,) = ctx.saved_tensors
-        num_points = v_colors.shape[0]
-        K = num_sh_bases(ctx.degree)
-        dev = viewdirs.device
         v_colors = v_colors.float().contiguous()
         if ctx.exchange is not None:
             degree, dtu = ctx.degree, int(ctx.degrees_to_use)
             return None, None, ctx.exchange.reduce(
                 v_colors, lambda means, views: sh_backward_views(degree, dtu, means, views))
-        v_coeffs = torch.empty((num_points, K, 3), device=dev, dtype=torch.float32)
-        _lib.call("gsplat_compute_sh_backward", num_points, ctx.degree, int(ctx.degrees_to_use),
-                  _lib.ptr(viewdirs), _lib.ptr(v_colors), _lib.ptr(v_coeffs), _lib.stream(dev))
-        return None, None, v_coeffs
+        return None, None, ops().sh_bwd(ctx.degree, int(ctx.degrees_to_use), viewdirs, v_colors)
 
 
 class _SphericalHarmonicsSplit(Function):

@@ -11,6 +11,7 @@ import torch
 from torch import Tensor
 
 from . import _lib
+from .ops import ops
 
 
 def _bits_for(v: int) -> int:
@@ -27,14 +28,13 @@ def map_gaussian_to_intersects(num_points: int, num_intersects: int, xys: Tensor
     xys, depths = xys.float().contiguous(), depths.float().contiguous()
     radii = radii.to(torch.int32).contiguous()
     cum_tiles_hit = cum_tiles_hit.to(torch.int32).contiguous()
-    dev = _lib.check_device("map_gaussian_to_intersects", xys, depths, radii, cum_tiles_hit)
-    isect_ids = torch.zeros((num_intersects,), device=dev, dtype=torch.int64)
-    gaussian_ids = torch.zeros((num_intersects,), device=dev, dtype=torch.int32)
-    P = _lib.ptr
-    _lib.call("gsplat_map_gaussian_to_intersects", int(num_points), P(xys), P(depths), P(radii),
-              P(cum_tiles_hit), int(tile_bounds[0]), int(tile_bounds[1]), P(isect_ids),
-              P(gaussian_ids), _lib.stream(dev))
-    return isect_ids, gaussian_ids
+    _lib.check_device("map_gaussian_to_intersects", xys, depths, radii, cum_tiles_hit)
+    n = int(num_points)  # gsplat reads the first num_points entries
+    if xys.shape[0] < n:
+        raise ValueError("map_gaussian_to_intersects: num_points > xys.shape[0]")
+    xys, depths, radii, cum_tiles_hit = xys[:n], depths[:n], radii[:n], cum_tiles_hit[:n]
+    return ops().map_intersects(xys, depths, radii, cum_tiles_hit, int(tile_bounds[0]),
+                                int(tile_bounds[1]), int(num_intersects))
 
 
 def get_tile_bin_edges(num_intersects: int, isect_ids_sorted: Tensor,
@@ -49,11 +49,10 @@ def get_tile_bin_edges(num_intersects: int, isect_ids_sorted: Tensor,
     if tile_bounds is not None:
         rows = max(rows, int(tile_bounds[0]) * int(tile_bounds[1]))
     isect_ids_sorted = isect_ids_sorted.contiguous()
-    dev = _lib.check_device("get_tile_bin_edges", isect_ids_sorted)
-    tile_bins = torch.empty((rows, 2), device=dev, dtype=torch.int32)
-    _lib.call("gsplat_get_tile_bin_edges", int(num_intersects), _lib.ptr(isect_ids_sorted),
-              _lib.ptr(tile_bins), rows, _lib.stream(dev))
-    return tile_bins
+    _lib.check_device("get_tile_bin_edges", isect_ids_sorted)
+    if isect_ids_sorted.numel() < int(num_intersects):
+        raise ValueError("get_tile_bin_edges: num_intersects > isect_ids_sorted.numel()")
+    return ops().tile_bins(isect_ids_sorted[:int(num_intersects)], rows)
 
 
 def compute_cov2d_bounds(cov2d: Tensor) -> Tuple[Tensor, Tensor]:
@@ -82,18 +81,10 @@ def sort_isect_pairs(isect_ids: Tensor, gaussian_ids: Tensor,
 
     Replaces `torch.sort(isect_ids)` + `torch.gather` of utils.bin_and_sort_gaussians; the
     order of equal keys is the input order (torch.sort gives no such guarantee)."""
-    n = isect_ids.shape[0]
     isect_ids = isect_ids.contiguous()
     gaussian_ids = gaussian_ids.to(torch.int32).contiguous()
-    dev = _lib.check_device("sort_isect_pairs", isect_ids, gaussian_ids)
-    keys_out = torch.empty_like(isect_ids)
-    vals_out = torch.empty_like(gaussian_ids)
-    ws = torch.empty((_lib.query("gsplat_sort_isect_pairs_workspace_size", n),),
-                     device=dev, dtype=torch.uint8)
-    _lib.call("gsplat_sort_isect_pairs", n, int(key_bits), _lib.ptr(isect_ids),
-              _lib.ptr(gaussian_ids), _lib.ptr(keys_out), _lib.ptr(vals_out), _lib.ptr(ws),
-              ws.numel(), _lib.stream(dev))
-    return keys_out, vals_out
+    _lib.check_device("sort_isect_pairs", isect_ids, gaussian_ids)
+    return ops().sort_pairs(isect_ids, gaussian_ids, int(key_bits))
 
 
 def bin_and_sort_gaussians(num_points: int, num_intersects: int, xys: Tensor, depths: Tensor,
