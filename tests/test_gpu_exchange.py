@@ -86,8 +86,12 @@ def test_exchange_over_rccl_world1_matches_plain(gpu):
     from gaussctrl_exp_amd.exchange import ShViewExchange
     from gaussctrl_exp_amd.scene import render, synthetic_scene
 
+    from gaussctrl_exp_amd import _lib
     store = dist.TCPStore("127.0.0.1", _free_port(), 1, True)
     dist.init_process_group("nccl", store=store, rank=0, world_size=1, device_id=gpu)
+    # deterministic rasterizer backward: the two renders' float-atomic summation orders would
+    # otherwise differ run to run (means.grad comes only through the rasterizer's atomics)
+    prev = _lib.set_deterministic(True)
     try:
         cam = synthetic_camera(256, 192).to(gpu)
         bg = torch.tensor([0.1, 0.2, 0.3], device=gpu)
@@ -108,6 +112,7 @@ def test_exchange_over_rccl_world1_matches_plain(gpu):
             assert np.abs(b).max() > 0
             np.testing.assert_allclose(a, b, rtol=1e-5, atol=1e-6)
     finally:
+        _lib.set_deterministic(prev)
         dist.destroy_process_group()
 
 
@@ -121,8 +126,11 @@ def test_trainstep_multirank_path_over_rccl_world1(gpu):
     from gaussctrl_exp_amd.scene import synthetic_scene
     from gaussctrl_exp_amd.train import TrainStep
 
+    from gaussctrl_exp_amd import _lib
     store = dist.TCPStore("127.0.0.1", _free_port(), 1, True)
     dist.init_process_group("nccl", store=store, rank=0, world_size=1, device_id=gpu)
+    # deterministic rasterizer backward: bit-comparable gradients between the two steps
+    prev = _lib.set_deterministic(True)
     try:
         cam = synthetic_camera(256, 192).to(gpu)
         gt = torch.rand(192, 256, 3, generator=torch.Generator().manual_seed(2)).to(gpu)
@@ -155,4 +163,5 @@ def test_trainstep_multirank_path_over_rccl_world1(gpu):
         t.step(away, gt, background=bg, optimizer=True)
         assert all(p.grad is not None and not p.grad.any() for p in t.params)
     finally:
+        _lib.set_deterministic(prev)
         dist.destroy_process_group()
