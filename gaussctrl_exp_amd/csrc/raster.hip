@@ -184,13 +184,59 @@ __device__ __forceinline__ bool touches_rect(float gx, float gy, float a, float 
   return !(sigma_lb > __logf(255.f * o));
 }
 
+// The same cull as touches_rect, branch-free for the staging loops: every lane evaluates all
+// of it (the wave executes the union of the branches anyway), the clamped minimiser of each
+// edge uses the hardware reciprocal instead of an IEEE division (~10 instructions each), and
+// log(255 o) the hardware log2 (255 o >= 1 for every Gaussian that is not dropped, so no
+// denormal scaling).  Still exactness-preserving: a perturbed minimiser f' gives
+// q(f') >= q(f*) only by diag_f (f' - f*)^2, a relative 2^-44 for an ulp-level error of f,
+// and the log error is ~1e-7 -- both far inside the rounding margin (1e-5 |terms| + 1e-3)
+// the bound already subtracts.  Non-positive-definite conics and NaNs are kept.
+__device__ __forceinline__ float q_edge_r(float e, float lo, float hi, float diag_e, float rdiag_f,
+                                          float diag_f, float b, float &mag) {
+  const float f = fminf(fmaxf(-b * e * rdiag_f, lo), hi);
+  const float t0 = diag_e * e * e, t1 = 2.f * b * e * f, t2 = diag_f * f * f;
+  mag = t0 + fabsf(t1) + t2;
+  return t0 + t1 + t2;
+}
+__device__ __forceinline__ bool touches_rect_bf(float gx, float gy, float a, float b, float c,
+                                                float o, float rx0, float rx1, float ry0,
+                                                float ry1) {
+  const float dx0 = gx - rx1, dx1 = gx - rx0, dy0 = gy - ry1, dy1 = gy - ry0;
+  const float ra = __builtin_amdgcn_rcpf(a), rc = __builtin_amdgcn_rcpf(c);
+  float m0, m1, m2, m3;
+  const float q0 = q_edge_r(dx0, dy0, dy1, a, rc, c, b, m0);
+  const float q1 = q_edge_r(dx1, dy0, dy1, a, rc, c, b, m1);
+  const float q2 = q_edge_r(dy0, dx0, dx1, c, ra, a, b, m2);
+  const float q3 = q_edge_r(dy1, dx0, dx1, c, ra, a, b, m3);
+  float q = q0, m = m0;
+  if (q1 < q) { q = q1; m = m1; }
+  if (q2 < q) { q = q2; m = m2; }
+  if (q3 < q) { q = q3; m = m3; }
+  const float sigma_lb = 0.5f * (q - 1e-5f * m) - 1e-3f;
+  const bool far = sigma_lb > __builtin_amdgcn_logf(255.f * o) * 0x1.62e430p-1f;  // ln 2
+  const bool pd = a > 0.f && a * c - b * b > 0.f;  // false for NaN
+  const bool inside = dx0 <= 0.f && dx1 >= 0.f && dy0 <= 0.f && dy1 >= 0.f;
+  return o >= ALPHA_MIN && (!pd || inside || !far);
+}
+
 __device__ __forceinline__ uint32_t lanes_below(unsigned long long mask) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
                                    __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
 // Stage this lane's Gaussian (list position idx) if it can touch the wave's rectangle.
-// Returns keep; fills s (colour and ids only when kept).
+// Returns keep; fills s.  EAGER: after the id, every load of the Gaussian -- mean, conic, opacity
+// AND colour -- is issued at once, so staging costs two dependent memory round trips (id,
+// then the rest) instead of four (id, opacity, conic + mean, then the colour of the kept
+// ones); the empty asm makes the colour a use before the keep branch, so the compiler cannot
+// sink its load into that branch.
+//
+// EAGER = false (the forward kernels): the branchy cull and the colour loaded only for kept
+// Gaussians -- the forward's 8x8 blocks keep few of the staged ones, and the eager form's
+// extra live registers cost it an occupancy level (62 -> 66 VGPRs: 0.132 -> 0.137 ms at the
+// headline), while the backward gains (0.316 -> 0.313 ms).
+template <bool EAGER = false>
 __device__ __forceinline__ bool stage_gaussian(int idx, const int *__restrict__ gids,
                                                const float2 *__restrict__ xys,
                                                const float *__restrict__ conics,
@@ -201,7 +247,26 @@ __device__ __forceinline__ bool stage_gaussian(int idx, const int *__restrict__ 
   const float2 xy = xys[g];
   const float a = conics[3 * g], b = conics[3 * g + 1], c = conics[3 * g + 2];
   const float o = opacity[g];
-  const bool keep = touches_rect(xy.x, xy.y, a, b, c, o, rx0, rx1, ry0, ry1);
+  if constexpr (!EAGER) {
+    const bool keep = touches_rect(xy.x, xy.y, a, b, c, o, rx0, rx1, ry0, ry1);
+    if (keep) {
+      s.x = xy.x;
+      s.y = xy.y;
+      s.ha = 0.5f * a;
+      s.b = b;
+      s.hc = 0.5f * c;
+      s.o = o;
+      s.r = colors[3 * g];
+      s.g = colors[3 * g + 1];
+      s.bl = colors[3 * g + 2];
+      s.idx = idx;
+      s.id = g;
+    }
+    return keep;
+  }
+  float cr = colors[3 * g], cg = colors[3 * g + 1], cb = colors[3 * g + 2];
+  const bool keep = touches_rect_bf(xy.x, xy.y, a, b, c, o, rx0, rx1, ry0, ry1);
+  asm volatile("" : "+v"(cr), "+v"(cg), "+v"(cb));
   if (keep) {
     s.x = xy.x;
     s.y = xy.y;
@@ -209,9 +274,9 @@ __device__ __forceinline__ bool stage_gaussian(int idx, const int *__restrict__ 
     s.b = b;
     s.hc = 0.5f * c;
     s.o = o;
-    s.r = colors[3 * g];
-    s.g = colors[3 * g + 1];
-    s.bl = colors[3 * g + 2];
+    s.r = cr;
+    s.g = cg;
+    s.bl = cb;
     s.idx = idx;
     s.id = g;
   }
@@ -870,13 +935,15 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
   }
   maxbin = wave_max_int(maxbin);
   const int slot = reduce9_slot();
+  // canonical once, so fminf needs no per-iteration canonicalisation of the bound
+  const float amax = __builtin_canonicalizef(alpha_max);
   const int last = min(maxbin, hi - 1);
   GStage *stage = lds[wave];
   for (int b = last; b >= lo; b -= 64) {
     const int idx = b - lane;
     GStage s;
     const bool keep = idx >= lo &&
-                      stage_gaussian(idx, gids, xys, conics, colors, opacity, rx0, rx1, ry0,
+                      stage_gaussian<true>(idx, gids, xys, conics, colors, opacity, rx0, rx1, ry0,
                                      ry1, s);
     const unsigned long long kmask = __ballot(keep);
     if (keep) stage[lanes_below(kmask)] = s;
@@ -895,7 +962,10 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
         gid[u] = G.id;
         const float dx = G.x - px;
         const float hA = G.ha * dx * dx, bdx = G.b * dx;
-        PV sr = 0.f, sg = 0.f, sb = 0.f, so = 0.f, V = 0.f, Vy = 0.f, Vyy = 0.f;
+        // per-lane sums as scalar dot products over the pixel pair (two scalar fmas cost what
+        // one packed fma does on gfx950, and need no packed horizontal add afterwards); the
+        // -o factor of the sigma gradient is applied once to the sums, not per pixel
+        float sr = 0.f, sg = 0.f, sb = 0.f, sa = 0.f, my = 0.f, myy = 0.f;
         bool any = false;
 #pragma unroll
         for (int p = 0; p < NP; ++p) {
@@ -903,7 +973,7 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
           const PV sig = gs_sigma2v<PV>(G.hc, bdx, hA, dy);
           const PV vis = gs_vis2v<PV>(sig);
           const PV ov = G.o * vis;
-          const PV al = {fminf(alpha_max, ov.x), fminf(alpha_max, ov.y)};
+          const PV al = {fminf(amax, ov.x), fminf(amax, ov.y)};
           const bool v0 = live && G.idx <= binf[2 * p] && sig.x >= 0.f && al.x >= ALPHA_MIN;
           const bool v1 =
               live && G.idx <= binf[2 * p + 1] && sig.y >= 0.f && al.y >= ALPHA_MIN;
@@ -914,38 +984,37 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
           const PV ra = {__builtin_amdgcn_rcpf(om.x), __builtin_amdgcn_rcpf(om.y)};
           T[p] = T[p] * ra;
           const PV fac = am * T[p];
-          sr = vfma(fac, vr[p], sr);
-          sg = vfma(fac, vg[p], sg);
-          sb = vfma(fac, vb[p], sb);
+          // (the first pair's terms start the sums: no 0 + x kept for signed zeros)
+          sr = fmaf(fac.y, vr[p].y, p ? fmaf(fac.x, vr[p].x, sr) : fac.x * vr[p].x);
+          sg = fmaf(fac.y, vg[p].y, p ? fmaf(fac.x, vg[p].x, sg) : fac.x * vg[p].x);
+          sb = fmaf(fac.y, vb[p].y, p ? fmaf(fac.x, vb[p].x, sb) : fac.x * vb[p].x);
           const PV gv = vfma(
               PV(G.r), vr[p], vfma(PV(G.g), vg[p], G.bl * vb[p]));
           const PV v_alpha = vfma(gv, T[p], ra * (q[p] - Sb[p]));
           Sb[p] = vfma(fac, gv, Sb[p]);
           const PV vva = vm * v_alpha;
-          so += vva;
-          const PV vs = vva * (-G.o);
-          const PV vsdy = vs * dy;
-          V += vs;
-          Vy += vsdy;
-          Vyy = vfma(vsdy, dy, Vyy);
+          const PV vdy = vva * dy;
+          sa = p ? sa + (vva.x + vva.y) : vva.x + vva.y;
+          my = fmaf(vva.y, dy.y, p ? fmaf(vva.x, dy.x, my) : vva.x * dy.x);
+          myy = fmaf(vdy.y, dy.y, p ? fmaf(vdy.x, dy.x, myy) : vdy.x * dy.x);
         }
         anyv[u] = any;
-        const float Vs = V.x + V.y, Vys = Vy.x + Vy.y;
+        const float Vs = -G.o * sa, Vys = -G.o * my;
         const float dxV = dx * Vs;
         parts[u][0] = fmaf(2.f * G.ha, dxV, G.b * Vys);  // v_x
         parts[u][1] = fmaf(G.b, dxV, 2.f * G.hc * Vys);  // v_y
         parts[u][2] = dx * dxV;                          // 2 v_conic.a
         parts[u][3] = dx * Vys;                          // 2 v_conic.b
-        parts[u][4] = Vyy.x + Vyy.y;                     // 2 v_conic.c
-        parts[u][5] = sr.x + sr.y;
-        parts[u][6] = sg.x + sg.y;
-        parts[u][7] = sb.x + sb.y;
-        parts[u][8] = so.x + so.y;
+        parts[u][4] = -G.o * myy;                        // 2 v_conic.c
+        parts[u][5] = sr;
+        parts[u][6] = sg;
+        parts[u][7] = sb;
+        parts[u][8] = sa;
       }
       bool any_all = false;
 #pragma unroll
       for (int u = 0; u < U; ++u) any_all = any_all || anyv[u];
-      if (__any(any_all)) {
+      if (__builtin_amdgcn_ballot_w64(any_all)) {  // (an SGPR test, no VGPR round trip)
         float v[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) v[u] = reduce9(parts[u]);
