@@ -316,11 +316,29 @@ struct WaveLog {
 // workgroups to the 8 XCDs round-robin, so consecutive blocks -- neighbouring tiles, which
 // stage largely the same Gaussians -- land on different L2s.  With the remap each XCD takes a
 // contiguous run of blocks (bijective for any grid size).
-__device__ int g_xcd_remap = 0;
+// g_xcd_remap: 0 off, -1 contiguous runs (flag 1024), K > 0 chunked: the grid is cut into
+// chunks of K consecutive block slots and chunk c goes to XCD c % 8, so a chunk's neighbouring
+// tiles share one L2 while a heavy image region is still dealt over all eight XCDs (bijective:
+// the tail past the last whole round of 8K blocks keeps its slots).  Shipped: K = 8 (8 tiles
+// of the forward, 16 of the backward per chunk; tools/exp_xcd.py, same-process medians vs
+// dispatch order: headline fwd 0.123 -> 0.118 / bwd 0.331 -> 0.319 ms, garden c4 fwd 0.195 ->
+// 0.151 / bwd 0.393 -> 0.400, c5 0.254 -> 0.248 / 0.746 -> 0.740, bear c3 unchanged).
+// Flags bits 20-27 (gsplat_debug_set_raster_variant): 0 the default, 255 dispatch order,
+// else K; flag 1024 contiguous runs.
+constexpr int XCD_CHUNK = 8;
+__device__ int g_xcd_remap = XCD_CHUNK;
 __device__ __forceinline__ int block_slot() {
   const int b = blockIdx.x;
-  if (!g_xcd_remap) return b;
-  const int n = gridDim.x, q = n >> 3, r = n & 7, x = b & 7, k = b >> 3;
+  const int K = g_xcd_remap;
+  if (!K) return b;
+  const int n = gridDim.x;
+  if (K > 0) {
+    const int full = n - n % (8 * K);
+    if (b >= full) return b;
+    const int x = b & 7, k = b >> 3;
+    return ((k / K) * 8 + x) * K + k % K;
+  }
+  const int q = n >> 3, r = n & 7, x = b & 7, k = b >> 3;
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
 }
 
@@ -1988,8 +2006,9 @@ extern "C" int gsplat_debug_set_raster_variant(int fwd_pxl, int bwd_pxl, int bwd
   }
   g_fwd_pxl = fwd_pxl;
   g_bwd_pxl = bwd_pxl;
-  g_bwd_flags = bwd_flags & ~1024;
-  const int remap = (bwd_flags & 1024) ? 1 : 0;
+  g_bwd_flags = bwd_flags & ~(1024 | (0xff << 20));
+  const int chunk = (bwd_flags >> 20) & 0xff;
+  const int remap = (bwd_flags & 1024) ? -1 : chunk == 0xff ? 0 : chunk ? chunk : XCD_CHUNK;
   if (hipMemcpyToSymbol(HIP_SYMBOL(g_xcd_remap), &remap, sizeof(int)) != hipSuccess) {
     set_error("debug_set_raster_variant: hipMemcpyToSymbol failed");
     return 1;

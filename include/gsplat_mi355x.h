@@ -385,7 +385,9 @@ int gsplat_grad_records_split(int num_points, const void *records, size_t record
  * one backward wave per 16x16 tile (four pixels per lane as two float2 pairs, per-half cull
  * bits; also used by the list-split backward), with bit 13 one-wave workgroups, bit 14 tiles
  * dealt longest-list-first, bits 15-17 = p > 0: p persistent waves per SIMD taking tiles from a
- * queue.  Every variant produces results within the same parity bar.  Process-wide;
+ * queue; bits 20-27 = K: the block -> tile order of the blend kernels, chunks of K block slots
+ * dealt round-robin over the 8 XCDs (0: the shipped K = 8, 255: plain dispatch order).  Every
+ * variant produces results within the same parity bar.  Process-wide;
  * defaults (1, 2, 0) are the shipped configuration. */
 int gsplat_debug_set_raster_variant(int fwd_pxl, int bwd_pxl, int bwd_flags);
 /* 1 while the shipped raster variants are selected (the record-based entries need them). */

@@ -320,13 +320,15 @@ def test_raster_backward(gpu, case, quirk_mask):
 
 # (fwd pixels/lane, bwd pixels/lane, flags): see gsplat_debug_set_raster_variant in
 # include/gsplat_mi355x.h (1 no atomics, 2 scalar bwd, 4 scalar fwd, 8 packed fwd, 16 wide
-# fwd, 32 narrow bwd, 1024 XCD-contiguous block order, 2048
+# fwd, 32 narrow bwd, 1024 XCD-contiguous block order, K << 20 chunks of K block slots per XCD
+# (shipped K = 8; 255 << 20 plain dispatch order), 2048
 # sub-wave-list backward, 4096 one wave per tile (+8192 one-wave workgroups, +16384 tiles
 # longest-first, + 4 << 15 four persistent waves per SIMD pulling tiles from a queue)).
 RASTER_VARIANTS = [(1, 2, 0), (1, 2, 4), (1, 2, 16), (2, 2, 0), (2, 2, 8), (2, 2, 6), (4, 4, 0),
                    (4, 4, 8), (4, 4, 6), (1, 1, 0), (1, 2, 32), (1, 2, 1024),
                    (1, 2, 2048), (1, 2, 4096), (1, 2, 4096 | 8192), (1, 2, 4096 | 16384),
-                   (1, 2, 4096 | (4 << 15))]
+                   (1, 2, 4096 | (4 << 15)), (1, 2, 255 << 20), (1, 2, 1 << 20),
+                   (1, 2, 3 << 20)]
 
 
 @pytest.mark.parametrize("variant", RASTER_VARIANTS)
