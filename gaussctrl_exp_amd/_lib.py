@@ -29,6 +29,7 @@ SIGNATURES = {
     "gsplat_set_quirks": (_I, [_I]),
     "gsplat_get_quirks": (_I, []),
     "gsplat_set_deterministic": (_I, [_I]),
+    "gsplat_debug_set_tile_swizzle": (_I, [_I, _I]),
     "gsplat_get_deterministic": (_I, []),
     "gsplat_last_error": (_c.c_char_p, []),
     "gsplat_project_gaussians_forward": (_I, [

@@ -348,6 +348,32 @@ __device__ __forceinline__ int wave_slot() {
   constexpr int WPT = (GS_BLOCK / COLS) * (GS_BLOCK / ((64 / COLS) * PXL));
   return block_slot() * (4 / WPT) + (threadIdx.x >> 6) / WPT;
 }
+// Tile swizzle of the work slots (gsplat_debug_set_tile_swizzle): slots run through bands of
+// GH tile rows in groups of GW x GH tiles (row-major inside a group), so the XCD chunks above
+// hold 2-D neighbourhoods instead of runs along one tile row.  Bijective over [0, T): a band's
+// last group is narrower when GW does not divide tbx, rows below the last full band keep
+// their slot order.  GW = GH = 1: the plain row-major order.
+__device__ int g_tile_gw = 1, g_tile_gh = 1;
+__device__ __forceinline__ int swizzle_tile(int s, int tbx, int tby) {
+  const int gw = g_tile_gw, gh = g_tile_gh;
+  if (gw * gh == 1) return s;
+  const int band_slots = gh * tbx, nbands = tby / gh;
+  const int band = s / band_slots;
+  if (band >= nbands) return s;
+  const int w = s - band * band_slots, gsz = gw * gh, nfull = tbx / gw;
+  int tx, ty;
+  if (w < nfull * gsz) {
+    const int cg = w / gsz, r = w - cg * gsz;
+    tx = cg * gw + r % gw;
+    ty = r / gw;
+  } else {
+    const int rw = tbx - nfull * gw, r = w - nfull * gsz;
+    tx = nfull * gw + r % rw;
+    ty = r / rw;
+  }
+  return (band * gh + ty) * tbx + tx;
+}
+
 template <int PXL, int COLS>
 __device__ __forceinline__ WaveRect wave_rect(int tbx, int tby, int H, int W, int tile = -1) {
   constexpr int LROWS = 64 / COLS;      // rows per lane pass
@@ -357,7 +383,12 @@ __device__ __forceinline__ WaveRect wave_rect(int tbx, int tby, int H, int W, in
   static_assert(WPT >= 1 && WPT <= 4 && 4 % WPT == 0, "wave footprint must tile 16x16");
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   WaveRect r;
-  r.tile = tile >= 0 ? tile : wave_slot<PXL, COLS>();
+  if (tile >= 0) {
+    r.tile = tile;
+  } else {
+    const int slot = wave_slot<PXL, COLS>();
+    r.tile = slot < tbx * tby ? swizzle_tile(slot, tbx, tby) : slot;
+  }
   const int wt = wave % WPT;
   const int tx = r.tile % tbx, ty = r.tile / tbx;
   const int c0 = tx * GS_BLOCK + (wt % WX) * COLS, r0 = ty * GS_BLOCK + (wt / WX) * WROWS;
@@ -2011,6 +2042,19 @@ extern "C" int gsplat_debug_set_raster_variant(int fwd_pxl, int bwd_pxl, int bwd
   const int remap = (bwd_flags & 1024) ? -1 : chunk == 0xff ? 0 : chunk ? chunk : XCD_CHUNK;
   if (hipMemcpyToSymbol(HIP_SYMBOL(g_xcd_remap), &remap, sizeof(int)) != hipSuccess) {
     set_error("debug_set_raster_variant: hipMemcpyToSymbol failed");
+    return 1;
+  }
+  return 0;
+}
+
+extern "C" int gsplat_debug_set_tile_swizzle(int gw, int gh) {
+  if (gw < 1 || gh < 1 || gw > 64 || gh > 64) {
+    set_error("debug_set_tile_swizzle: group sides must be in 1..64");
+    return 1;
+  }
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_tile_gw), &gw, sizeof(int)) != hipSuccess ||
+      hipMemcpyToSymbol(HIP_SYMBOL(g_tile_gh), &gh, sizeof(int)) != hipSuccess) {
+    set_error("debug_set_tile_swizzle: hipMemcpyToSymbol failed");
     return 1;
   }
   return 0;

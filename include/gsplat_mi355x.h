@@ -390,6 +390,9 @@ int gsplat_grad_records_split(int num_points, const void *records, size_t record
  * variant produces results within the same parity bar.  Process-wide;
  * defaults (1, 2, 0) are the shipped configuration. */
 int gsplat_debug_set_raster_variant(int fwd_pxl, int bwd_pxl, int bwd_flags);
+/* Tuning hook: the blend kernels visit tiles in groups of gw x gh tiles (bands of gh tile rows,
+ * row-major inside a group) instead of row-major order; (1, 1) is row-major.  Process-wide. */
+int gsplat_debug_set_tile_swizzle(int gw, int gh);
 /* 1 while the shipped raster variants are selected (the record-based entries need them). */
 int gsplat_debug_raster_variant_is_default(void);
 

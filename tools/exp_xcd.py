@@ -13,8 +13,17 @@ from gaussctrl_exp_amd.rasterize import bin_gaussians
 
 dev = torch.device("cuda:0")
 P = _lib.ptr
-chunks = [int(x) for x in os.environ.get("CHUNKS", "255,-1,2,4,8,16,32").split(",")]
+# variants "K:GWxGH" (K as in the flags; GW x GH: gsplat_debug_set_tile_swizzle)
+chunks = [x if ":" in x else x + ":1x1"
+          for x in os.environ.get("CHUNKS", "255,-1,2,4,8,16,32").split(",")]
 flag = lambda k: 1024 if k < 0 else k << 20
+
+
+def apply(v):
+    k, sw = v.split(":")
+    gw, gh = (int(t) for t in sw.split("x"))
+    _lib.call("gsplat_debug_set_raster_variant", 1, 2, flag(int(k)))
+    _lib.call("gsplat_debug_set_tile_swizzle", gw, gh)
 
 
 def timeit(fn, reps=10):
@@ -61,7 +70,7 @@ for cfg in os.environ.get("CFGS", "headline,c4").split(","):
     ref_img = None
     ref_g = None
     for k in chunks:
-        _lib.call("gsplat_debug_set_raster_variant", 1, 2, flag(k))
+        apply(k)
         fwd(); bwd(); torch.cuda.synchronize()
         if ref_img is None:
             ref_img, ref_g = out.clone(), [x.clone() for x in g]
@@ -73,11 +82,11 @@ for cfg in os.environ.get("CFGS", "headline,c4").split(","):
     res = {k: ([], []) for k in chunks}
     for rnd in range(5):
         for k in chunks:
-            _lib.call("gsplat_debug_set_raster_variant", 1, 2, flag(k))
+            apply(k)
             res[k][0].append(timeit(fwd))
             res[k][1].append(timeit(bwd))
-    _lib.call("gsplat_debug_set_raster_variant", 1, 2, 0)
+    apply("0:1x1")
     print(f"{cfg}: N={N} I={I} tiles={tb[0] * tb[1]}", flush=True)
     for k in chunks:
-        print(f"  order {k:>3}: fwd {np.median(res[k][0]):.4f} ms  bwd {np.median(res[k][1]):.4f} ms",
+        print(f"  order {k:>9}: fwd {np.median(res[k][0]):.4f} ms  bwd {np.median(res[k][1]):.4f} ms",
               flush=True)
