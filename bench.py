@@ -168,10 +168,11 @@ def pmc_traffic(entry, config):
 
 
 def pmc_valu_busy(entry, config, ms_per_call, n_simd=256 * 4, clock_hz=2.4e9):
-    """Fraction of the chip's VALU issue slots the entry's kernels used on `config`: rocprofv3
-    SQ_ACTIVE_INST_VALU (quad-cycles) per call / (SIMDs x call duration in quad-cycles at the
-    peak engine clock).  The blend kernels are VALU-issue bound, so this -- not the HBM
-    fraction -- is the roofline that binds them.  None without that config's counters."""
+    """rocprofv3 SQ_ACTIVE_INST_VALU (counted in quad-cycles) per call / (SIMDs x call duration
+    in quad-cycles at the peak engine clock): the VALU pipe's active share if every wave64 VALU
+    op held it for 4 cycles.  gfx950's 32-lane SIMD issues one in 2 (MI355X_MICROARCH.md), so
+    this overstates the issue share ~2x; valu_issue_frac (pmc_issue_and_wait) is the issue
+    bound, wait_frac the stall share.  None without that config's counters."""
     kern = _pmc_kernels(config)
     pats, _ = ENTRY_KERNELS.get(entry, ((), False))
     if not kern or not pats or not ms_per_call:
@@ -182,6 +183,32 @@ def pmc_valu_busy(entry, config, ms_per_call, n_simd=256 * 4, clock_hz=2.4e9):
             tot += v["valu_quad_cycles"]
             hit = True
     return round(tot / (n_simd * ms_per_call * 1e-3 * clock_hz / 4.0), 3) if hit else None
+
+
+def pmc_issue_and_wait(entry, config, ms_per_call, n_simd=256 * 4, clock_hz=2.4e9):
+    """(valu_issue_frac, wait_frac) of the entry's kernels on `config`: the lower bound on the
+    SIMD issue cycles its VALU instructions take -- SQ_INSTS_VALU x 2 cycles (a wave64 VALU op
+    issues over 2 cycles on gfx950's 32-lane SIMD) + SQ_INSTS_VALU_TRANS_F32 x 2 more (a
+    transcendental takes 4), packed ops counted at the scalar cost -- per SIMD-cycle of the
+    call, and SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES, the share of its waves' lifetime spent stalled
+    on s_waitcnt.  (None, None) without that config's counters."""
+    kern = _pmc_kernels(config)
+    pats, _ = ENTRY_KERNELS.get(entry, ((), False))
+    if not kern or not pats or not ms_per_call:
+        return None, None
+    iv = it = wi = wc = 0.0
+    hit = False
+    for name, v in kern.items():
+        if any(p in name for p in pats) and v.get("insts_valu") is not None:
+            iv += v["insts_valu"]
+            it += v.get("insts_trans") or 0.0
+            wi += v.get("wait_inst_any") or 0.0
+            wc += v.get("wave_cycles") or 0.0
+            hit = True
+    if not hit:
+        return None, None
+    issue = (2.0 * iv + 2.0 * it) / (n_simd * ms_per_call * 1e-3 * clock_hz)
+    return round(issue, 3), (round(wi / wc, 3) if wc else None)
 
 
 def cpu_threads():
@@ -419,6 +446,8 @@ def main():
         "traffic": pmc_traffic(dom, args.config),
         "traffic_fetch_scale": 2 if ENTRY_KERNELS.get(dom, ((), False))[1] else 1,
         "valu_busy": pmc_valu_busy(dom, args.config, dom_ms),
+        "valu_issue_frac": pmc_issue_and_wait(dom, args.config, dom_ms)[0],
+        "wait_frac": pmc_issue_and_wait(dom, args.config, dom_ms)[1],
         "step_algorithmic_bytes": step_bytes,
         "step_frac": round(step_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
         "roofline_mpix_s": round(P / (step_bytes / (HBM_PEAK_GBS * 1e9)) / 1e6, 1),

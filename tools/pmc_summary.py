@@ -34,7 +34,11 @@ for k, d in sorted(acc.items()):
 cols = sorted({c for r in rows for c in r if c != "kernel"})
 if len(sys.argv) > 3:
     tj = {r["kernel"]: {"fetch_kb": r.get("FETCH_SIZE"), "write_kb": r.get("WRITE_SIZE"),
-                        "valu_quad_cycles": r.get("SQ_ACTIVE_INST_VALU")}
+                        "valu_quad_cycles": r.get("SQ_ACTIVE_INST_VALU"),
+                        "insts_valu": r.get("SQ_INSTS_VALU"),
+                        "insts_trans": r.get("SQ_INSTS_VALU_TRANS_F32"),
+                        "wait_inst_any": r.get("SQ_WAIT_INST_ANY"),
+                        "wave_cycles": r.get("SQ_WAVE_CYCLES")}
           for r in rows if "FETCH_SIZE" in r and "WRITE_SIZE" in r}
     cfg = cfg_arg
     try:
