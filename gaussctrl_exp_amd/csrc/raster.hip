@@ -39,6 +39,8 @@ namespace gs {
 namespace {
 
 constexpr float ALPHA_MIN = 1.f / 255.f;
+// The backward's record atomics use 32-bit element offsets (id * REC + slot < 2^31).
+constexpr int MAX_BWD_POINTS = 1 << 27;
 constexpr int REC = 16;  // floats per gradient record: x y a b c r g b o + pad = 64 B
 
 // Deterministic backward (gsplat_set_deterministic): every wave's nine per-Gaussian totals
@@ -1009,6 +1011,9 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
         const bool live = t + u < n;
         if (!live) G.r = G.g = G.bl = G.o = 0.f;  // stale slot: keep T / Sb finite
         gid[u] = G.id;
+        // read with the rest of the staged record at the top of the iteration: left to the
+        // compiler, the id's LDS read sank to the atomic at the end -- a second LDS round trip
+        asm volatile("" : "+v"(gid[u]));
         const float dx = G.x - px;
         const float hA = G.ha * dx * dx, bdx = G.b * dx;
         // per-lane sums as scalar dot products over the pixel pair (two scalar fmas cost what
@@ -1073,7 +1078,10 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
             if (__any(anyv[u]) && slot >= 0)
               atomicAdd(det + (size_t)gid[u] * DET_REC + slot, det_quantize(v[u]));
           } else if constexpr (ATOMICS) {
-            if (__any(anyv[u]) && slot >= 0) atomicAdd(rec + (size_t)gid[u] * REC + slot, v[u]);
+            // 32-bit element offset (the entry points reject N >= 2^27): the atomic takes the
+            // SGPR base + a VGPR offset, no 64-bit address arithmetic per iteration
+            if (__any(anyv[u]) && slot >= 0)
+              atomicAdd(rec + (uint32_t)(gid[u] * REC + slot), v[u]);
           } else {
             asm volatile("" ::"v"(v[u]));
           }
@@ -2108,7 +2116,7 @@ extern "C" int gsplat_rasterize_backward(int tile_bounds_x, int tile_bounds_y, i
                                          size_t workspace_bytes, void *stream) {
   hipStream_t st = (hipStream_t)stream;
   if (tile_bounds_x <= 0 || tile_bounds_y <= 0 || img_height <= 0 || img_width <= 0 ||
-      channels < 1 || channels > 64 || num_points < 0 ||
+      channels < 1 || channels > 64 || num_points < 0 || num_points >= MAX_BWD_POINTS ||
       (long long)tile_bounds_x * GS_BLOCK < img_width ||
       (long long)tile_bounds_y * GS_BLOCK < img_height) {
     set_error("rasterize_backward: bad sizes (tiles=%dx%d H=%d W=%d C=%d N=%d)", tile_bounds_x,
@@ -2374,7 +2382,8 @@ extern "C" int gsplat_rasterize_backward_chunked(
                                      v_opacity, workspace, workspace_bytes, stream);
   hipStream_t st = (hipStream_t)stream;
   if (tile_bounds_x <= 0 || tile_bounds_y <= 0 || img_height <= 0 || img_width <= 0 ||
-      num_points < 0 || (long long)tile_bounds_x * GS_BLOCK < img_width ||
+      num_points < 0 || num_points >= MAX_BWD_POINTS ||
+      (long long)tile_bounds_x * GS_BLOCK < img_width ||
       (long long)tile_bounds_y * GS_BLOCK < img_height || chunk % 64 || num_intersects < 0) {
     set_error("rasterize_backward_chunked: bad sizes (tiles=%dx%d H=%d W=%d N=%d chunk=%d)",
               tile_bounds_x, tile_bounds_y, img_height, img_width, num_points, chunk);
@@ -2439,7 +2448,8 @@ extern "C" int gsplat_rasterize_backward_records(
   hipStream_t st = (hipStream_t)stream;
   const size_t need = gsplat_grad_records_bytes(num_points);
   if (tile_bounds_x <= 0 || tile_bounds_y <= 0 || img_height <= 0 || img_width <= 0 ||
-      num_points < 0 || (long long)tile_bounds_x * GS_BLOCK < img_width ||
+      num_points < 0 || num_points >= MAX_BWD_POINTS ||
+      (long long)tile_bounds_x * GS_BLOCK < img_width ||
       (long long)tile_bounds_y * GS_BLOCK < img_height || num_intersects < 0 ||
       (chunk > 0 && chunk % 64) || records_bytes < need || (need && !records)) {
     set_error("rasterize_backward_records: bad sizes (tiles=%dx%d H=%d W=%d N=%d chunk=%d "
