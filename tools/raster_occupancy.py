@@ -119,6 +119,31 @@ with torch.no_grad():
                     for b0 in range(0, ncand, 64):
                         it += int(v[b0:b0 + 64].sum(0).max()) if v.shape[0] else 0
                     add(name + "_lane_walk_iters", it)
+        # active-rectangle cull for the 16x8 backward strips: the strip walks its list from its
+        # last contributing position down in 64-position batches; in a batch whose lowest
+        # position is p0 only pixels with final index >= p0 can use any of its Gaussians, so the
+        # batch's candidates could be culled against the bounding box of those pixels
+        for c0 in range(tx * 16, min(tx * 16 + 16, W), 16):
+            c1 = min(c0 + 15, W - 1)
+            for r0 in range(ty * 16, min(ty * 16 + 16, H), 8):
+                r1 = min(r0 + 7, H - 1)
+                fs = fin[r0 - ty * 16: r1 - ty * 16 + 1, c0 - tx * 16: c1 - tx * 16 + 1]
+                last = int(fs.max().item())
+                kept = 0
+                bhi = last
+                while bhi >= s:
+                    p0 = max(bhi - 63, s)
+                    act = (fs >= p0).nonzero()
+                    if len(act):
+                        ar0 = float(r0 + act[:, 0].min().item())
+                        ar1 = float(r0 + act[:, 0].max().item())
+                        ac0 = float(c0 + act[:, 1].min().item())
+                        ac1 = float(c0 + act[:, 1].max().item())
+                        sl = slice(p0 - s, bhi - s + 1)
+                        kept += int(touches_exact(gx[sl], gy[sl], a[sl], bb[sl], c[sl], o[sl],
+                                                  ac0, ac1, ar0, ar1).sum())
+                    bhi -= 64
+                add("active_cand", kept)
         # two-queue strip backward: a 16x8 strip whose lanes hold a pixel of the top 16x4 half
         # (.x) and one of the bottom half (.y); each half walks its own candidate queue, so a
         # 64-position batch takes max(top, bottom) iterations instead of |top u bottom|
@@ -142,6 +167,7 @@ with torch.no_grad():
                 add("dual_union", int((top | bot).sum()))
     n = len(sample)
     print(f"config {cfg}: {n} sampled tiles; per tile:")
+    print(f"  active-rectangle strips: candidates/tile {acc['active_cand'] / n:7.1f}")
     print(f"  two-queue strips: iterations/tile {acc['dual_iters'] / n:7.1f} "
           f"(union of the halves' candidates {acc['dual_union'] / n:7.1f})")
     for k in ("list", "tile_last", "valid_bwd", "valid_fwd"):
