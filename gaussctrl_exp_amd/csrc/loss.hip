@@ -186,7 +186,20 @@ __global__ __launch_bounds__(256) void l1_only_fwd_kernel(long long n, const flo
                                                           float *__restrict__ partials) {
   __shared__ float red[4];
   float acc = 0.f;
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n;
+  long long i0 = 0;
+  if ((((uintptr_t)pred | (uintptr_t)gt) & 15) == 0) {  // 16-B vectors, then the tail
+    const long long n4 = n >> 2;
+    const float4 *p4 = reinterpret_cast<const float4 *>(pred);
+    const float4 *g4 = reinterpret_cast<const float4 *>(gt);
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n4;
+         i += (long long)gridDim.x * 256) {
+      const float4 p = p4[i], g = g4[i];
+      acc += fabsf(g.x - clamp_pred<CLAMP>(p.x)) + fabsf(g.y - clamp_pred<CLAMP>(p.y)) +
+             fabsf(g.z - clamp_pred<CLAMP>(p.z)) + fabsf(g.w - clamp_pred<CLAMP>(p.w));
+    }
+    i0 = n4 << 2;
+  }
+  for (long long i = i0 + (long long)blockIdx.x * 256 + threadIdx.x; i < n;
        i += (long long)gridDim.x * 256)
     acc += fabsf(gt[i] - clamp_pred<CLAMP>(pred[i]));
   acc = block_sum(acc, red);
@@ -203,12 +216,26 @@ __global__ __launch_bounds__(256) void l1_only_bwd_kernel(long long n, const flo
                                                           float l1_scale,
                                                           float *__restrict__ v_pred) {
   const float gl = grad_out[0] * l1_scale;
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n;
-       i += (long long)gridDim.x * 256) {
-    const float p = pred[i];
-    const float d = clamp_pred<CLAMP>(p) - gt[i];
-    v_pred[i] = gl * (d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f)) * clamp_mask<CLAMP>(p);
+  auto g1 = [&](float p, float g) {
+    const float d = clamp_pred<CLAMP>(p) - g;
+    return gl * (d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f)) * clamp_mask<CLAMP>(p);
+  };
+  long long i0 = 0;
+  if ((((uintptr_t)pred | (uintptr_t)gt | (uintptr_t)v_pred) & 15) == 0) {  // 16-B vectors
+    const long long n4 = n >> 2;
+    const float4 *p4 = reinterpret_cast<const float4 *>(pred);
+    const float4 *g4 = reinterpret_cast<const float4 *>(gt);
+    float4 *v4 = reinterpret_cast<float4 *>(v_pred);
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n4;
+         i += (long long)gridDim.x * 256) {
+      const float4 p = p4[i], g = g4[i];
+      v4[i] = make_float4(g1(p.x, g.x), g1(p.y, g.y), g1(p.z, g.z), g1(p.w, g.w));
+    }
+    i0 = n4 << 2;
   }
+  for (long long i = i0 + (long long)blockIdx.x * 256 + threadIdx.x; i < n;
+       i += (long long)gridDim.x * 256)
+    v_pred[i] = g1(pred[i], gt[i]);
 }
 
 // loss = (1 - lambda) * L1 / (C H W) + lambda * (1 - SSIM_sum / (C Ho Wo)); one workgroup,

@@ -49,6 +49,27 @@ def test_fused_loss_has_no_cpu_path():
 
 
 @pytest.mark.gpu
+def test_l1_only_unaligned_inputs(gpu):
+    """The L1-only kernels' scalar path (inputs not 16-byte aligned: views at an odd offset)
+    gives the same loss and gradient as the aligned 16-byte-vector path."""
+    g = torch.Generator().manual_seed(7)
+    full_p = torch.rand(33 * 17 * 3 + 1, generator=g).to(gpu)
+    full_g = torch.rand(33 * 17 * 3 + 1, generator=g).to(gpu)
+    outs = []
+    for off in (1, None):
+        if off:
+            p0, g0 = full_p[off:].view(33, 17, 3), full_g[off:].view(33, 17, 3)
+        else:
+            p0, g0 = full_p[1:].clone().view(33, 17, 3), full_g[1:].clone().view(33, 17, 3)
+        p = p0.detach().requires_grad_()
+        loss = fused_splatfacto_loss(p, g0, 0.0)
+        loss.backward()
+        outs.append((loss.item(), p.grad.clone()))
+    assert abs(outs[0][0] - outs[1][0]) <= 1e-6 * max(1.0, outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.gpu
 def test_fused_loss_rejects_small_images(gpu):
     with pytest.raises(RuntimeError, match="H, W >= 11"):
         fused_splatfacto_loss(torch.rand(10, 20, 3, device=gpu), torch.rand(10, 20, 3, device=gpu))
