@@ -336,10 +336,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # one GPU per rank (RCCL); BENCH_DIST_BACKEND=gloo lets a one-GPU box rehearse the N > 1
+    # path with every rank on its one device (ranks share it; not a scaling measurement)
+    backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local_rank %= max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     N, W, H, deg, lo, hi, seed, real, desc = CONFIGS[args.config]
     K = num_sh_bases(deg)
