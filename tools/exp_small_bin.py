@@ -12,7 +12,9 @@ from gaussctrl_exp_amd.rasterize import bin_gaussians
 
 dev = torch.device("cuda:0")
 L = _lib.lib()
-SETTINGS = [(w, it) for w in (0, 1) for it in (0, 8, 16)]
+# (depth_sort_wide, sort_items, depth_key_range): SETTINGS env "w:i:r,..." overrides
+SETTINGS = [tuple(int(v) for v in x.split(":")) for x in os.environ["SETTINGS"].split(",")] \
+    if os.environ.get("SETTINGS") else [(w, it, 1) for w in (0, 1) for it in (0, 8, 16)]
 for cfg in os.environ.get("CFGS", "c2 c3 headline").split():
     sc, cam = bench.make_workload(cfg, 0, dev)
     cam = cam.to(dev)
@@ -27,6 +29,7 @@ for cfg in os.environ.get("CFGS", "c2 c3 headline").split():
         for s in SETTINGS:
             L.gsplat_debug_depth_sort_wide(s[0])
             _lib.call("gsplat_debug_sort_items", s[1])
+            L.gsplat_debug_depth_key_range(s[2])
             out = bin_gaussians(xys, depths, radii, nth, cam.height, cam.width)
             if ref is None:
                 ref = out
@@ -41,6 +44,8 @@ for cfg in os.environ.get("CFGS", "c2 c3 headline").split():
             res[s].append(e0.elapsed_time(e1) / 20)
     L.gsplat_debug_depth_sort_wide(0)
     _lib.call("gsplat_debug_sort_items", 0)
+    L.gsplat_debug_depth_key_range(1)
     print(f"{cfg}: I={ref[0]}", flush=True)
     for s in SETTINGS:
-        print(f"  wide={s[0]} items={s[1]}: {np.median(res[s]):.4f} ms", flush=True)
+        print(f"  wide={s[0]} items={s[1]} key_range={s[2]}: {np.median(res[s]):.4f} ms",
+              flush=True)
