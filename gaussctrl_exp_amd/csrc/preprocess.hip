@@ -339,15 +339,41 @@ __global__ __launch_bounds__(sh_threads(K)) void fused_bwd_kernel(FusedBwdArgs a
         o.m[grp][idx] = mv;
         o.v[grp][idx] = vv;
       };
+      // a group's W floats of this Gaussian as one vector access per array (p, m, v): 12-B
+      // rows as dwordx3, the quaternion's 16-B row as dwordx4 when the three arrays are
+      // 16-B aligned -- a third of the per-element dword accesses
+      struct __attribute__((aligned(4))) F3 { float x[3]; };
+      struct __attribute__((aligned(16))) F4 { float x[4]; };
+      auto upd3 = [&](int grp, const float gv[3]) {
+        F3 pv = reinterpret_cast<const F3 *>(o.p[grp])[g];
+        F3 mv = reinterpret_cast<const F3 *>(o.m[grp])[g];
+        F3 vv = reinterpret_cast<const F3 *>(o.v[grp])[g];
 #pragma unroll
-      for (int k = 0; k < 3; ++k) upd(0, 3 * g + k, vmean[k]);
+        for (int k = 0; k < 3; ++k)
+          adam_elem(pv.x[k], gv[k], mv.x[k], vv.x[k], w1, o.beta2, w2, o.ss[grp], o.bc2s[grp],
+                    o.eps);
+        reinterpret_cast<F3 *>(o.p[grp])[g] = pv;
+        reinterpret_cast<F3 *>(o.m[grp])[g] = mv;
+        reinterpret_cast<F3 *>(o.v[grp])[g] = vv;
+      };
+      upd3(0, vmean);
+      upd3(1, vls);
+      if (((((uintptr_t)o.p[2]) | ((uintptr_t)o.m[2]) | ((uintptr_t)o.v[2])) & 15) == 0) {
+        F4 pv = reinterpret_cast<const F4 *>(o.p[2])[g];
+        F4 mv = reinterpret_cast<const F4 *>(o.m[2])[g];
+        F4 vv = reinterpret_cast<const F4 *>(o.v[2])[g];
 #pragma unroll
-      for (int k = 0; k < 3; ++k) upd(1, 3 * g + k, vls[k]);
+        for (int k = 0; k < 4; ++k)
+          adam_elem(pv.x[k], vq[k], mv.x[k], vv.x[k], w1, o.beta2, w2, o.ss[2], o.bc2s[2], o.eps);
+        reinterpret_cast<F4 *>(o.p[2])[g] = pv;
+        reinterpret_cast<F4 *>(o.m[2])[g] = mv;
+        reinterpret_cast<F4 *>(o.v[2])[g] = vv;
+      } else {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) upd(2, 4 * g + k, vq[k]);
+        for (int k = 0; k < 4; ++k) upd(2, 4 * g + k, vq[k]);
+      }
       upd(3, g, vlogit);
-#pragma unroll
-      for (int c = 0; c < 3; ++c) upd(4, 3 * g + c, vdc[c]);
+      upd3(4, vdc);
     } else {
 #pragma unroll
       for (int k = 0; k < 3; ++k) a.v_means[3 * g + k] = vmean[k];
