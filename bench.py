@@ -29,7 +29,7 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from gaussctrl_exp_amd import timing  # noqa: E402
+from gaussctrl_exp_amd import _lib, timing  # noqa: E402
 from gaussctrl_exp_amd.camera import gc_camera, look_at_c2w  # noqa: E402
 from gaussctrl_exp_amd.fused import render_fused  # noqa: E402
 from gaussctrl_exp_amd.rasterize import bin_gaussians  # noqa: E402
@@ -209,6 +209,49 @@ def pmc_issue_and_wait(entry, config, ms_per_call, n_simd=256 * 4, clock_hz=2.4e
         return None, None
     issue = (2.0 * iv + 2.0 * it) / (n_simd * ms_per_call * 1e-3 * clock_hz)
     return round(issue, 3), (round(wi / wc, 3) if wc else None)
+
+
+def pmc_insts_valu(entry, config):
+    """SQ_INSTS_VALU (wave64 VALU instructions) per call of the entry's kernels on `config`, or
+    None without that config's counters."""
+    kern = _pmc_kernels(config)
+    pats, _ = ENTRY_KERNELS.get(entry, ((), False))
+    if not kern or not pats:
+        return None
+    vals = [v["insts_valu"] for name, v in kern.items()
+            if any(p in name for p in pats) and v.get("insts_valu") is not None]
+    return sum(vals) if vals else None
+
+
+def lane_occupancy(step, dev, config):
+    """Lane-slot accounting of the blend kernels over one extra step (outside every timed
+    region), from the counting instantiations behind gsplat_debug_pair_count: per kernel the
+    share of the pixel slots its wave iterations issue whose pixel is still live for the staged
+    Gaussian (inside the image, not terminated / idx <= final_idx) and the share holding a
+    valid pixel-Gaussian pair (sigma >= 0, alpha >= 1/255 as well) -- the work the VALU-bound
+    blend loops actually do -- plus, where that config's PMC is committed, wave64 VALU
+    instructions x 64 per valid pair."""
+    buf = torch.zeros(6, dtype=torch.int64, device=dev)
+    _lib.call("gsplat_debug_pair_count", _lib.ptr(buf))
+    try:
+        step()
+        torch.cuda.synchronize()
+    finally:
+        _lib.call("gsplat_debug_pair_count", None)
+    c = buf.tolist()
+    out = {}
+    for entry, (s, live, valid) in (("gsplat_rasterize_backward_records", c[0:3]),
+                                    ("gsplat_rasterize_forward_clearing", c[3:6])):
+        if not s:
+            continue
+        iv = pmc_insts_valu(entry, config)
+        out[entry] = {
+            "lane_slots": s,
+            "live_frac": round(live / s, 4),
+            "valid_pair_frac": round(valid / s, 4),
+            "valu_lane_ops_per_valid_pair": round(iv * 64 / valid, 1) if iv and valid else None,
+        }
+    return out
 
 
 def cpu_threads():
@@ -461,6 +504,8 @@ def main():
         "roofline_mpix_s": round(P / (step_bytes / (HBM_PEAK_GBS * 1e9)) / 1e6, 1),
     }
 
+    lanes = lane_occupancy(step, dev, args.config)
+
     # full train step: splatfacto loss + backward + all-reduce + Adam
     tsteps = args.train_steps if args.train_steps is not None else args.steps
     trainer.loss_kind = "splatfacto"
@@ -517,6 +562,7 @@ def main():
             "train_iters_per_s": round(tsteps / tdt, 2),
             "train_views_per_s": round(world * tsteps / tdt, 2),
             "roofline": roofline,
+            "lane_occupancy": lanes,
             "kernels": kernels,
             "cpu_baseline": cpu,
         }

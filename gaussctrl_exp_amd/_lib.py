@@ -82,6 +82,7 @@ SIGNATURES = {
     "gsplat_debug_bins_from_sort": (_I, [_I]),
     "gsplat_debug_sort_items": (_I, [_I]),
     "gsplat_debug_wave_log": (_I, [_P]),
+    "gsplat_debug_pair_count": (_I, [_P]),
     "gsplat_l1_ssim_num_blocks": (_I, [_I, _I]),
     "gsplat_l1_ssim_forward": (_I, [_I, _I, _I, _P, _P, _P, _F, _I, _P, _P, _P, _P]),
     "gsplat_l1_ssim_backward": (_I, [_I, _I, _I, _P, _P, _P, _F, _I, _P, _P, _P, _P]),

@@ -314,6 +314,31 @@ struct WaveLog {
   }
 };
 
+// Debug hook (gsplat_debug_pair_count): lane-slot accounting of the shipped blend kernels,
+// counted by separate <..., CNT = true> instantiations (the shipped code is unchanged).  Per
+// kernel three u64 sums: lane slots issued (wave iterations x pixel slots a wave iteration
+// spans), pairs whose pixel is still live for the Gaussian (inside the image and, in the
+// backward, idx <= final_idx; in the forward, not yet terminated), and pairs that are
+// composited (valid: sigma >= 0 and alpha >= 1/255 as well).  [0..2] backward, [3..5] forward.
+__device__ unsigned long long *g_pair_count = nullptr;
+static bool g_pair_count_on = false;
+__device__ __forceinline__ void pair_count_flush(int base, unsigned slots, unsigned live,
+                                                 unsigned valid) {
+  // slots is wave-uniform (counted once per wave); live/valid are per-lane
+  unsigned long long l = live, v = valid;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    l += __shfl_xor(l, o);
+    v += __shfl_xor(v, o);
+  }
+  unsigned long long *c = g_pair_count;
+  if (c && (threadIdx.x & 63) == 0) {
+    atomicAdd(c + base, (unsigned long long)slots);
+    atomicAdd(c + base + 1, l);
+    atomicAdd(c + base + 2, v);
+  }
+}
+
 // XCD-aware block order (gsplat_debug_set_raster_variant flag 1024): the dispatcher deals
 // workgroups to the 8 XCDs round-robin, so consecutive blocks -- neighbouring tiles, which
 // stage largely the same Gaussians -- land on different L2s.  With the remap each XCD takes a
@@ -519,7 +544,7 @@ __global__ __launch_bounds__(256) void raster_fwd3_kernel(
 // CKPT (list-split backward, see chunk_plan_kernel): for a tile whose list is longer than
 // `chunk`, each pixel's state (T, accumulated colour) is recorded after every `chunk` list
 // positions and at the end, so the backward can start each chunk from it.
-template <int PXL, int COLS, bool DEPTH = false, bool CKPT = false>
+template <int PXL, int COLS, bool DEPTH = false, bool CKPT = false, bool CNT = false>
 __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
     int tbx, int tby, int H, int W, const int *__restrict__ gids, const int2 *__restrict__ bins,
     const float2 *__restrict__ xys, const float *__restrict__ conics,
@@ -566,6 +591,7 @@ __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
   }
   const int2 range = bins[tile];
   GStage *stage = lds[wave];
+  unsigned c_slots = 0, c_live = 0, c_valid = 0;  // (CNT only)
   // checkpoints (CKPT): m states per chunked tile, state k after list position
   // range.x + (k + 1) * chunk (k = m - 1: the final state)
   int m = 0, nextk = 0;
@@ -605,6 +631,7 @@ __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
       G[1] = stage[min(t + 1, 63)];
       const bool live1 = t + 1 < n;
       if (!live1) G[1].r = G[1].g = G[1].bl = G[1].d = 0.f;  // stale slot: keep 0 * x finite
+      if constexpr (CNT) c_slots += 2 * PXL * 64;
       float sg[2][PXL], al[2][PXL];
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
@@ -623,6 +650,10 @@ __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
         for (int u = 0; u < 2; ++u) {
           const bool v = !done[k] && (u == 0 || live1) && sg[u][k] >= 0.f &&
                          al[u][k] >= ALPHA_MIN;
+          if constexpr (CNT) {
+            c_live += (!done[k] && (u == 0 || live1)) ? 1u : 0u;
+            c_valid += v ? 1u : 0u;
+          }
           const float nT = T[k] * (1.f - al[u][k]);
           const bool term = v && nT <= 1e-4f, comp = v && !term;
           done[k] = done[k] || term;
@@ -657,6 +688,7 @@ __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
       if (DEPTH) out_depth[pix] = cd[k] + T[k] * 0.f;  // the depth render's zero background
     }
   }
+  if constexpr (CNT) pair_count_flush(3, c_slots, c_live, c_valid);
   wlog.done(tile);
   clear_side_job();
 }
@@ -900,7 +932,7 @@ __global__ __launch_bounds__(256) void raster_bwd3_kernel(
 // after its last position: T = checkpoint T, and the colour behind it, Sb = (C_final - C_j) . v,
 // instead of T_final and 0 -- so long lists and small images (few tiles) still fill the GPU.
 template <int NP, bool ATOMICS, int COLS, bool CHUNKED = false, typename PV = f2,
-          bool DET = false>
+          bool DET = false, bool CNT = false>
 __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
     int tbx, int tby, int H, int W, const int *__restrict__ gids, const int2 *__restrict__ bins,
     const float2 *__restrict__ xys, const float *__restrict__ conics,
@@ -990,6 +1022,7 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
   const float amax = __builtin_canonicalizef(alpha_max);
   const int last = min(maxbin, hi - 1);
   GStage *stage = lds[wave];
+  unsigned c_slots = 0, c_live = 0, c_valid = 0;  // (CNT only)
   for (int b = last; b >= lo; b -= 64) {
     const int idx = b - lane;
     GStage s;
@@ -1005,6 +1038,7 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
       float parts[U][9];
       bool anyv[U];
       int gid[U];
+      if constexpr (CNT) c_slots += U * PXL * 64;
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         GStage G = stage[min(t + u, 63)];
@@ -1032,6 +1066,11 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
           const bool v1 =
               live && G.idx <= binf[2 * p + 1] && sig.y >= 0.f && al.y >= ALPHA_MIN;
           any = any || v0 || v1;
+          if constexpr (CNT) {
+            c_live += (live && G.idx <= binf[2 * p] ? 1u : 0u) +
+                      (live && G.idx <= binf[2 * p + 1] ? 1u : 0u);
+            c_valid += (v0 ? 1u : 0u) + (v1 ? 1u : 0u);
+          }
           const PV am = {v0 ? al.x : 0.f, v1 ? al.y : 0.f};
           const PV vm = {v0 ? vis.x : 0.f, v1 ? vis.y : 0.f};
           const PV om = 1.f - am;
@@ -1090,6 +1129,7 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
     }
     wave_lds_sync();
   }
+  if constexpr (CNT) pair_count_flush(0, c_slots, c_live, c_valid);
   wlog.done(tile);
 }
 
@@ -2085,6 +2125,16 @@ extern "C" int gsplat_debug_wave_log(void *buffer) {
   return 0;
 }
 
+extern "C" int gsplat_debug_pair_count(void *buffer) {
+  unsigned long long *p = (unsigned long long *)buffer;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_pair_count), &p, sizeof(p)) != hipSuccess) {
+    set_error("debug_pair_count: hipMemcpyToSymbol failed");
+    return 1;
+  }
+  g_pair_count_on = p != nullptr;
+  return 0;
+}
+
 // The shipped 16x8-strip backward in deterministic mode (integer accumulators in det).
 static void launch_bwd_det(hipStream_t st, int tbx, int tby, int H, int W, const int32_t *gids,
                            const int32_t *bins, const float *xys, const float *conics,
@@ -2277,11 +2327,15 @@ static int rasterize_forward_impl(int tile_bounds_x, int tile_bounds_y, int img_
                                       gaussian_ids_sorted, tile_bins, xys, conics, colors,
                                       opacity, background, out_img, final_Ts, final_idx, stream);
     }
-    hipLaunchKernelGGL((raster_fwd3u_kernel<1, 8>), dim3(cdiv(T, (tiles_per_block<1, 8>()))),
-                       dim3(256), 0, st, tile_bounds_x, tile_bounds_y, img_height, img_width,
-                       gaussian_ids_sorted, (const int2 *)tile_bins, (const float2 *)xys,
-                       conics, colors, opacity, background, out_img, final_Ts, final_idx,
-                       nullptr, nullptr, 0, nullptr, nullptr, (float4 *)zero, zn, zero_radii);
+#define FWDU(CNT)                                                                          \
+  hipLaunchKernelGGL((raster_fwd3u_kernel<1, 8, false, false, CNT>),                          \
+                     dim3(cdiv(T, (tiles_per_block<1, 8>()))), dim3(256), 0, st, tile_bounds_x, \
+                     tile_bounds_y, img_height, img_width, gaussian_ids_sorted,                 \
+                     (const int2 *)tile_bins, (const float2 *)xys, conics, colors, opacity,     \
+                     background, out_img, final_Ts, final_idx, nullptr, nullptr, 0, nullptr,    \
+                     nullptr, (float4 *)zero, zn, zero_radii)
+    if (g_pair_count_on) FWDU(true); else FWDU(false);
+#undef FWDU
     return check_launch(who);
   }
   const ChunkWs w = carve_chunk_ws(checkpoints, T, num_intersects, chunk);
@@ -2292,12 +2346,15 @@ static int rasterize_forward_impl(int tile_bounds_x, int tile_bounds_y, int img_
   }
   hipLaunchKernelGGL(chunk_plan_kernel, dim3(1), dim3(1024), 0, st, T, (const int2 *)tile_bins,
                      chunk, w.item_off, w.ckpt_off, w.item_tile);
-  hipLaunchKernelGGL((raster_fwd3u_kernel<1, 8, false, true>),
-                     dim3(cdiv(T, (tiles_per_block<1, 8>()))), dim3(256), 0, st, tile_bounds_x,
-                     tile_bounds_y, img_height, img_width, gaussian_ids_sorted,
-                     (const int2 *)tile_bins, (const float2 *)xys, conics, colors, opacity,
-                     background, out_img, final_Ts, final_idx, nullptr, nullptr, chunk,
-                     w.ckpt_off, w.ckpt, (float4 *)zero, zn, zero_radii);
+#define FWDC(CNT)                                                                          \
+  hipLaunchKernelGGL((raster_fwd3u_kernel<1, 8, false, true, CNT>),                           \
+                     dim3(cdiv(T, (tiles_per_block<1, 8>()))), dim3(256), 0, st, tile_bounds_x, \
+                     tile_bounds_y, img_height, img_width, gaussian_ids_sorted,                 \
+                     (const int2 *)tile_bins, (const float2 *)xys, conics, colors, opacity,     \
+                     background, out_img, final_Ts, final_idx, nullptr, nullptr, chunk,         \
+                     w.ckpt_off, w.ckpt, (float4 *)zero, zn, zero_radii)
+  if (g_pair_count_on) FWDC(true); else FWDC(false);
+#undef FWDC
   return check_launch(who);
 }
 
@@ -2351,12 +2408,15 @@ static void launch_bwd_chunked(hipStream_t st, int tbx, int tby, int H, int W, c
     return;
   }
   if (!(g_bwd_flags & 4096)) {
-    hipLaunchKernelGGL((raster_bwd3p_kernel<1, true, 16, true>),
-                       dim3((unsigned)cdiv(w.items_bound, (long long)(tiles_per_block<2, 16>()))),
-                       dim3(256), 0, st, tbx, tby, H, W, gids, (const int2 *)bins,
-                       (const float2 *)xys, conics, colors, opacity, background, final_Ts,
-                       final_idx, v_output, v_output_alpha, alpha_max, rec, false, chunk,
-                       w.item_off, w.item_tile, w.ckpt_off, w.ckpt);
+#define BWDC(CNT)                                                                          \
+  hipLaunchKernelGGL((raster_bwd3p_kernel<1, true, 16, true, f2, false, CNT>),                \
+                     dim3((unsigned)cdiv(w.items_bound, (long long)(tiles_per_block<2, 16>()))),\
+                     dim3(256), 0, st, tbx, tby, H, W, gids, (const int2 *)bins,                \
+                     (const float2 *)xys, conics, colors, opacity, background, final_Ts,        \
+                     final_idx, v_output, v_output_alpha, alpha_max, rec, false, chunk,         \
+                     w.item_off, w.item_tile, w.ckpt_off, w.ckpt)
+    if (g_pair_count_on) BWDC(true); else BWDC(false);
+#undef BWDC
     return;
   }
   hipLaunchKernelGGL((raster_bwd4_kernel<true>), dim3((unsigned)cdiv(w.items_bound, 4LL)),
@@ -2492,12 +2552,15 @@ extern "C" int gsplat_rasterize_backward_records(
                        (const int2 *)tile_bins, (const float2 *)xys, conics, colors, opacity,
                        background, final_Ts, final_idx, v_output, v_output_alpha, alpha_max, rec);
   } else {
-    hipLaunchKernelGGL((raster_bwd3p_kernel<1, true, 16>),
-                       dim3(cdiv(T, (tiles_per_block<2, 16>()))), dim3(256), 0, st,
-                       tile_bounds_x, tile_bounds_y, img_height, img_width, gaussian_ids_sorted,
-                       (const int2 *)tile_bins, (const float2 *)xys, conics, colors, opacity,
-                       background, final_Ts, final_idx, v_output, v_output_alpha, alpha_max, rec,
-                       false);
+#define BWDR(CNT)                                                                          \
+  hipLaunchKernelGGL((raster_bwd3p_kernel<1, true, 16, false, f2, false, CNT>),               \
+                     dim3(cdiv(T, (tiles_per_block<2, 16>()))), dim3(256), 0, st,              \
+                     tile_bounds_x, tile_bounds_y, img_height, img_width, gaussian_ids_sorted,  \
+                     (const int2 *)tile_bins, (const float2 *)xys, conics, colors, opacity,     \
+                     background, final_Ts, final_idx, v_output, v_output_alpha, alpha_max, rec, \
+                     false)
+    if (g_pair_count_on) BWDR(true); else BWDR(false);
+#undef BWDR
   }
   if (det)
     hipLaunchKernelGGL(det_finish_kernel, dim3(cdiv(num_points, 256)), dim3(256), 0, st,

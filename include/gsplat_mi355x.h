@@ -439,6 +439,14 @@ int gsplat_debug_binning_scheme(int bucket);
  * 100 MHz), HW_ID, XCC_ID, work slot} as [waves][5] uint64 into the device buffer (NULL
  * disables); the buffer needs 5 entries per launched wave. */
 int gsplat_debug_wave_log(void *buffer);
+/* Debug: lane-slot accounting of the shipped blend kernels (separate counting instantiations,
+ * the shipped code is unchanged).  buffer = device u64[6], accumulated by every later forward
+ * (clearing / chunked) and record backward launch until called again with NULL:
+ * [0] backward lane slots (wave iterations x 128 pixel slots), [1] slots whose pixel is live for
+ * the Gaussian (in the image, idx <= final_idx), [2] valid pairs (sigma >= 0, alpha >= 1/255);
+ * [3..5] the same for the forward (wave iterations x 2 Gaussians x 64 pixels; live = not yet
+ * terminated). */
+int gsplat_debug_pair_count(void *buffer);
 
 /* ---- training-step photometric loss -------------------------------------
  * nerfstudio 1.0 splatfacto get_loss_dict's main loss, which the reference's training step
