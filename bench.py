@@ -369,6 +369,9 @@ def main():
     ap.add_argument("--config", default="headline", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--train-steps", type=int, default=None)
+    ap.add_argument("--no-lane-occupancy", action="store_true",
+                    help="skip the counted extra step (profiler runs: keeps the counting "
+                         "kernels out of the PMC and kernel-trace summaries)")
     ap.add_argument("--forward-only", action="store_true",
                     help="time the render without backward (default for config c2)")
     ap.add_argument("--render", default="fused", choices=("fused", "caller"),
@@ -504,7 +507,7 @@ def main():
         "roofline_mpix_s": round(P / (step_bytes / (HBM_PEAK_GBS * 1e9)) / 1e6, 1),
     }
 
-    lanes = lane_occupancy(step, dev, args.config)
+    lanes = None if args.no_lane_occupancy else lane_occupancy(step, dev, args.config)
 
     # full train step: splatfacto loss + backward + all-reduce + Adam
     tsteps = args.train_steps if args.train_steps is not None else args.steps

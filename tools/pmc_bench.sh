@@ -5,7 +5,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 CONFIG=${CONFIG:-headline}
-ARGS=${BENCH_ARGS:---steps 3 --warmup 1 --no-cpu-baseline --train-steps 1}
+ARGS=${BENCH_ARGS:---steps 3 --warmup 1 --no-cpu-baseline --no-lane-occupancy --train-steps 1}
 mkdir -p gpurun_out/pmc
 run() {  # run <name> <counters...>
   local name=$1; shift

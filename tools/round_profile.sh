@@ -11,7 +11,7 @@ for cfg in ${CONFIGS:-headline}; do
   python3 tools/pmc_summary.py gpurun_out gpurun_out/pmc_summary_$cfg.csv \
     profiles/pmc_traffic.json $cfg || exit $?
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_stats_$cfg -o run \
-    -- python3 bench.py --config $cfg --steps 20 --warmup 5 --no-cpu-baseline --train-steps 5 \
+    -- python3 bench.py --config $cfg --steps 20 --warmup 5 --no-cpu-baseline --no-lane-occupancy --train-steps 5 \
     > gpurun_out/prof_bench_$cfg.log 2>&1 || exit $?
   python3 tools/rocpd_stats.py gpurun_out/prof_stats_$cfg/run_results.db \
     gpurun_out/kernel_stats_$cfg.csv || exit $?
