@@ -1266,7 +1266,6 @@ constexpr int BK_NT = 1024;               // threads of the bucket count / place
 constexpr int BK_CHUNK = 4096;            // Gaussians per bucket workgroup
 constexpr int BK_MAX_BUCKETS = 16448;     // tiles + 1 (sentinel bucket) held in LDS (~64 KB)
 constexpr int BS_ITEMS = 16;
-constexpr int BS_CAP = TPB * BS_ITEMS;    // list length sorted entirely in LDS
 
 // phase 1: per block, the sum of tile allotments and the number of visible Gaussians
 __global__ __launch_bounds__(TPB) void bk_totals_kernel(int n, const uint4 *__restrict__ rec,

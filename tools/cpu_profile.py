@@ -7,13 +7,16 @@ import bench
 from gaussctrl_exp_amd.scene import synthetic_scene
 from gaussctrl_exp_amd.train import TrainStep
 
-N, W, H, deg, lo, hi, seed, _real, desc = bench.CONFIGS["headline"]
+cfg = os.environ.get("CFG", "headline")
+N, W, H, deg, lo, hi, seed, _real, desc = bench.CONFIGS[cfg]
 dev = torch.device("cuda:0")
-scene = synthetic_scene(N, deg, seed=seed, scale_lo=lo, scale_hi=hi, device=dev)
-cam = bench.view_camera(W, H, 0).to(dev)
+scene, cam = bench.make_workload(cfg, 0, dev)
+cam = cam.to(dev)
+H, W = cam.height, cam.width
 gt = torch.rand(H, W, 3, device=dev)
 bg = torch.zeros(3, device=dev)
-tr = TrainStep(scene, sh_degree=deg, world_size=1, loss="l1")
+tr = TrainStep(scene, sh_degree=deg, world_size=1, loss="l1",
+               render_mode=os.environ.get("RENDER", "fused"))
 
 
 def step():
@@ -39,3 +42,12 @@ with profile(activities=[ProfilerActivity.CPU]) as prof:
         step()
     torch.cuda.synchronize()
 print(prof.key_averages().table(sort_by="self_cpu_time_total", row_limit=40))
+import cProfile
+import pstats
+pr = cProfile.Profile()
+pr.enable()
+for _ in range(50):
+    step()
+torch.cuda.synchronize()
+pr.disable()
+pstats.Stats(pr).sort_stats("tottime").print_stats(35)
