@@ -10,6 +10,9 @@ Gaussian gradients -- the multi-view exchange of the data-parallel train step
 full train step (splatfacto 0.8 L1 + 0.2 SSIM loss + Adam) is timed separately and
 reported as `train_iters_per_s`.  Inputs are synthetic (SURVEY.md §8d scene: random
 Gaussians in [-1.5,1.5]^3 seen from (0,0,4), fov 50 deg) and resident in HBM before timing.
+`roofline` describes the dominant entry (HBM fraction plus its PMC issue / wait shares);
+`lane_occupancy` gives the blend kernels' live and valid-pair shares of their lane slots,
+counted on one extra, untimed step.
 
 Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--config headline|c2|c3|c4|c5]
 (N > 1 under torch.distributed.run, one process per GPU, backend nccl = RCCL.)
