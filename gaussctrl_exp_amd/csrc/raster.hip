@@ -1038,6 +1038,7 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
       float parts[U][9];
       bool anyv[U];
       int gid[U];
+      unsigned long long anyw[U];
       if constexpr (CNT) c_slots += U * PXL * 64;
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -1055,6 +1056,7 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
         // -o factor of the sigma gradient is applied once to the sums, not per pixel
         float sr = 0.f, sg = 0.f, sb = 0.f, sa = 0.f, my = 0.f, myy = 0.f;
         bool any = false;
+        unsigned long long anym = 0;  // wave mask of lanes with a valid pair (SGPR)
 #pragma unroll
         for (int p = 0; p < NP; ++p) {
           const PV dy = G.y - py[p];
@@ -1066,6 +1068,7 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
           const bool v1 =
               live && G.idx <= binf[2 * p + 1] && sig.y >= 0.f && al.y >= ALPHA_MIN;
           any = any || v0 || v1;
+          anym |= __builtin_amdgcn_ballot_w64(v0 || v1);
           if constexpr (CNT) {
             c_live += (live && G.idx <= binf[2 * p] ? 1u : 0u) +
                       (live && G.idx <= binf[2 * p + 1] ? 1u : 0u);
@@ -1092,6 +1095,7 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
           myy = fmaf(vdy.y, dy.y, p ? fmaf(vdy.x, dy.x, myy) : vdy.x * dy.x);
         }
         anyv[u] = any;
+        anyw[u] = anym;
         const float Vs = -G.o * sa, Vys = -G.o * my;
         const float dxV = dx * Vs;
         parts[u][0] = fmaf(2.f * G.ha, dxV, G.b * Vys);  // v_x
@@ -1104,10 +1108,10 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
         parts[u][7] = sb;
         parts[u][8] = sa;
       }
-      bool any_all = false;
+      unsigned long long any_all = 0;
 #pragma unroll
-      for (int u = 0; u < U; ++u) any_all = any_all || anyv[u];
-      if (__builtin_amdgcn_ballot_w64(any_all)) {  // (an SGPR test, no VGPR round trip)
+      for (int u = 0; u < U; ++u) any_all |= anyw[u];
+      if (any_all) {  // (an SGPR test, no VGPR round trip)
         float v[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) v[u] = reduce9(parts[u]);
@@ -1119,7 +1123,7 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
           } else if constexpr (ATOMICS) {
             // 32-bit element offset (the entry points reject N >= 2^27): the atomic takes the
             // SGPR base + a VGPR offset, no 64-bit address arithmetic per iteration
-            if (__any(anyv[u]) && slot >= 0)
+            if (anyw[u] && slot >= 0)
               atomicAdd(rec + (uint32_t)(gid[u] * REC + slot), v[u]);
           } else {
             asm volatile("" ::"v"(v[u]));
