@@ -29,7 +29,6 @@ SIGNATURES = {
     "gsplat_set_quirks": (_I, [_I]),
     "gsplat_get_quirks": (_I, []),
     "gsplat_set_deterministic": (_I, [_I]),
-    "gsplat_debug_set_tile_swizzle": (_I, [_I, _I]),
     "gsplat_get_deterministic": (_I, []),
     "gsplat_last_error": (_c.c_char_p, []),
     "gsplat_project_gaussians_forward": (_I, [
@@ -99,12 +98,12 @@ SIGNATURES = {
     "gsplat_fused_preprocess_backward_adam": (_I, [_I, _I, _I] + [_P] * 9 + [_F] * 4 +
                                               [_I, _I] + [_P] * 8 + [_I, _F, _F, _F, _P]),
     "gsplat_grad_records_bytes": (_SZ, [_I]),
-    "gsplat_grad_records_split": (_I, [_I, _P, _SZ, _P, _P, _P, _P, _P]),
+    "gsplat_grad_records_split": (_I, [_I, _P, _SZ, _P, _P, _P, _P, _P, _P, _P]),
     "gsplat_rasterize_backward_records": (_I, [_I] * 5 + [_P] * 11 + [_F, _I64, _I, _P, _SZ,
                                                                        _P, _SZ, _P]),
 }
 
-ABI_VERSION = 7  # include/gsplat_mi355x.h GSPLAT_MI355X_ABI_VERSION
+ABI_VERSION = 8  # include/gsplat_mi355x.h GSPLAT_MI355X_ABI_VERSION
 
 _lib = None
 _DETERMINISTIC = os.environ.get("GSPLAT_MI355X_DETERMINISTIC", "0") not in ("", "0")

@@ -139,6 +139,73 @@ __device__ __forceinline__ int reduce9_slot() {
   return (lane & 3) == 0 ? s : -1;
 }
 
+// ---- wave64 reduce-scatter of eighteen values (two Gaussians' nine record moments) -------
+// The same halving ladder as reduce9 with one more rung: l^32 (18 -> 9: lanes 0-31 keep the
+// first nine, 32-63 the second nine), l^16 (9 -> 5), l^8 (5 -> 3), 7-l within eight (3 -> 2),
+// l^1 (2 -> 1), and a final sum with l^2.  Each value's total ends in two lanes (l, l^2) of
+// one quad: 47 VALU ops for 18 values (two reduce9s: 54).
+__device__ __forceinline__ float reduce18(const float (&v)[18]) {
+  const int lane = __lane_id();
+  float a[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) a[k] = swap32_sum(v[k], v[k + 9]);
+  float b[5];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) b[k] = swap16_sum(a[2 * k], a[2 * k + 1]);
+  b[4] = swap16_sum(a[8], 0.f);
+  const bool h8 = lane & 8, h4 = lane & 4, h1 = lane & 1;
+  const float c0 = dpp_pair_sum<0x128>(b[0], b[1], h8), c1 = dpp_pair_sum<0x128>(b[2], b[3], h8),
+              c2 = dpp_pair_sum<0x128>(b[4], 0.f, h8);
+  const float d0 = dpp_pair_sum<0x141>(c0, c1, h4), d1 = dpp_pair_sum<0x141>(c2, 0.f, h4);
+  float e = dpp_pair_sum<0xB1>(d0, d1, h1);  // quad_perm [1,0,3,2]
+  e += dpp_f<0x4E>(e);                        // quad_perm [2,3,0,1]
+  return e;
+}
+
+// Which of the eighteen values reduce18() leaves in this lane: 0..17 for one lane of each
+// holding pair (lane bit 1 clear), -1 elsewhere (found by a probe, like reduce9_slot).
+__device__ __forceinline__ int reduce18_slot() {
+  const int lane = __lane_id();
+  float p[18];
+#pragma unroll
+  for (int k = 0; k < 18; ++k) p[k] = lane == 0 ? (float)(k + 1) : 0.f;
+  const int s = (int)reduce18(p) - 1;
+  return (lane & 2) == 0 ? s : -1;
+}
+
+// ---- per-Gaussian gradient records (the C=3 backward's accumulators) -----------------------
+// One 64-B record per Gaussian holds the raster gradient as pixel moments, summed over every
+// pixel p the Gaussian is composited at (over all tiles), with d = xy - p and
+// w_p = vis_p * v_alpha_p (the per-pixel opacity gradient, gsplat backward.cu's vis * v_alpha):
+//   0 Sx = sum dx w, 1 Sy = sum dy w, 2 Sxx = sum dx^2 w, 3 Sxy = sum dx dy w,
+//   4 Syy = sum dy^2 w, 5..7 v_rgb = sum alpha T v_out, 8 S0 = sum w (= v_opacity).
+// Every pixel of a Gaussian shares its conic and opacity o, so gsplat's per-pixel
+//   v_sigma = -o w,  v_conic = 1/2 v_sigma (dx^2, dx dy, dy^2),
+//   v_xy = v_sigma (a dx + b dy, b dx + c dy)
+// sum to the closed forms of record_grads() -- applied once per Gaussian when the record is
+// read, instead of per pixel or per wave iteration.
+enum { REC_SX = 0, REC_SY, REC_SXX, REC_SXY, REC_SYY, REC_R, REC_G, REC_B, REC_S0, REC_FIELDS };
+struct RasterGrads {
+  float vxy[2], vconic[3], vrgb[3], vopacity;
+};
+// conic_y_full: GSPLAT_QUIRK_CONIC_HALF off (v_conic.y = d loss / d conic.y = -o Sxy).
+__host__ __device__ __forceinline__ RasterGrads record_grads(const float *r, float ca, float cb,
+                                                              float cc, float o,
+                                                              bool conic_y_full) {
+  RasterGrads g;
+  const float no = -o;
+  g.vxy[0] = no * (ca * r[REC_SX] + cb * r[REC_SY]);
+  g.vxy[1] = no * (cb * r[REC_SX] + cc * r[REC_SY]);
+  g.vconic[0] = 0.5f * no * r[REC_SXX];
+  g.vconic[1] = (conic_y_full ? 1.f : 0.5f) * no * r[REC_SXY];
+  g.vconic[2] = 0.5f * no * r[REC_SYY];
+  g.vrgb[0] = r[REC_R];
+  g.vrgb[1] = r[REC_G];
+  g.vrgb[2] = r[REC_B];
+  g.vopacity = r[REC_S0];
+  return g;
+}
+
 __device__ __forceinline__ int wave_max_int(int v) {
   for (int off = 32; off >= 1; off >>= 1) {
     int o = __shfl_xor(v, off, 64);

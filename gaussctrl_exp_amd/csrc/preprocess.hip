@@ -62,7 +62,6 @@ struct FusedBwdArgs {
   const float *means, *log_scales, *quats, *viewmat, *projmat, *campos;
   const int *radii;
   const float *conics, *colors, *opacity, *records;
-  float conic_scale;
   float *v_means, *v_log_scales, *v_quats, *v_opacity_logits, *v_dc, *v_rest;
   float *v_colors;  // non-NULL: write the SH-output gradient here instead of v_dc / v_rest
 };
@@ -283,6 +282,12 @@ __global__ __launch_bounds__(sh_threads(K)) void fused_bwd_kernel(FusedBwdArgs a
     if (vis) {
       const float4 *rec = reinterpret_cast<const float4 *>(a.records + g * RECF);
       const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2];
+      const float rv[9] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x};
+      const float ca = a.conics[3 * g], cb = a.conics[3 * g + 1], cc = a.conics[3 * g + 2];
+      const float y = a.opacity[g];
+      // raster gradients from the record's moments (common.h record_grads)
+      const RasterGrads rg =
+          record_grads(rv, ca, cb, cc, y, !(pp.quirks & GSPLAT_QUIRK_CONIC_HALF));
       float s[3], qr[4], qn[4], norm;
       activate(a.log_scales, a.quats, g, s, qr, qn, norm);
       Cam cam;
@@ -290,12 +295,9 @@ __global__ __launch_bounds__(sh_threads(K)) void fused_bwd_kernel(FusedBwdArgs a
       float cv[6];
       cov3d_one(pp.glob_scale, s[0], s[1], s[2], qn[0], qn[1], qn[2], qn[3], cv);
       ProjGrad pg;
-      const float cs = a.conic_scale;
       project_backward_one(cam, pp, p0, p1, p2, s[0], s[1], s[2], qn[0], qn[1], qn[2], qn[3],
-                           cv, a.conics[3 * g], a.conics[3 * g + 1], a.conics[3 * g + 2], r0.x,
-                           r0.y, 0.f, cs * r0.z,
-                           (pp.quirks & GSPLAT_QUIRK_CONIC_HALF ? cs : 2.f * cs) * r0.w, cs * r1.x,
-                           pg);
+                           cv, ca, cb, cc, rg.vxy[0], rg.vxy[1], 0.f, rg.vconic[0], rg.vconic[1],
+                           rg.vconic[2], pg);
 #pragma unroll
       for (int k = 0; k < 3; ++k) vmean[k] = pg.vmean[k];
       // exp backward: grad * result
@@ -309,9 +311,8 @@ __global__ __launch_bounds__(sh_threads(K)) void fused_bwd_kernel(FusedBwdArgs a
 #pragma unroll
       for (int k = 0; k < 4; ++k) vq[k] = pg.vquat[k] / norm + qr[k] * (gn / norm);
       // sigmoid backward: grad * (1 - y) * y
-      const float y = a.opacity[g];
-      vlogit = r2.x * (1.f - y) * y;
-      const float vrgb[3] = {r1.y, r1.z, r1.w};
+      vlogit = rg.vopacity * (1.f - y) * y;
+      const float *vrgb = rg.vrgb;
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
         const float col = a.colors[3 * g + c];
@@ -567,7 +568,7 @@ extern "C" int gsplat_fused_preprocess_backward(
   if (num_points == 0) return 0;
   // 0.5: the shipped packed backward accumulates 2 v_conic (raster.hip split_grads_kernel)
   FusedBwdArgs args{num_points, degrees_to_use, means3d, log_scales, quats, viewmat, projmat,
-                    campos, radii, conics, colors, opacity, (const float *)grad_records, 0.5f,
+                    campos, radii, conics, colors, opacity, (const float *)grad_records,
                     v_means3d, v_log_scales, v_quats, v_opacity_logits, v_features_dc,
                     v_features_rest, K > 1 ? v_colors : nullptr};
   const ProjParams pp = make_proj_params(fx, fy, cx, cy, 1.f, 0.f, img_height, img_width, 1, 1);
@@ -599,7 +600,7 @@ extern "C" int gsplat_fused_preprocess_backward_adam(
   }
   if (num_points == 0) return 0;
   FusedBwdArgs args{num_points, degrees_to_use, means3d, log_scales, quats, viewmat, projmat,
-                    campos, radii, conics, colors, opacity, (const float *)grad_records, 0.5f,
+                    campos, radii, conics, colors, opacity, (const float *)grad_records,
                     nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   FusedAdamArgs o{};
   float *params[6] = {means3d, log_scales, quats, opacity_logits, features_dc, features_rest};

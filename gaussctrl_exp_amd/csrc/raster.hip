@@ -33,6 +33,7 @@
 #include "common.h"
 
 #include <algorithm>
+#include <mutex>
 #include <type_traits>
 
 namespace gs {
@@ -43,17 +44,39 @@ constexpr float ALPHA_MIN = 1.f / 255.f;
 constexpr int MAX_BWD_POINTS = 1 << 27;
 constexpr int REC = 16;  // floats per gradient record: x y a b c r g b o + pad = 64 B
 
-// Deterministic backward (gsplat_set_deterministic): every wave's nine per-Gaussian totals
-// (reduce9: a fixed reduction order, so run-independent) are added as 64-bit fixed-point
-// integers (2^-32 units) instead of fp32 atomics.  Integer addition is associative, so the
-// sums -- and every gradient downstream -- are bit-identical from run to run whatever order
-// the waves finish in; det_finish_kernel converts them into the usual float records.  The
-// quantisation error (<= 2^-33 per wave total) is far below the fp32 atomics' own.
-constexpr int DET_REC = 9;
-constexpr float DET_SCALE = 4294967296.f;  // 2^32
-__device__ __forceinline__ unsigned long long det_quantize(float v) {
-  const float s = fminf(fmaxf(v * DET_SCALE, -9.2e18f), 9.2e18f);  // |v| < 2^31
-  return (unsigned long long)__float2ll_rn(s);
+// Deterministic backward (gsplat_set_deterministic): every wave's per-Gaussian totals
+// (reduce18 / reduce9: a fixed reduction order, so run-independent) are added as exact
+// integers instead of fp32 atomics.  A total v is quantised to X = trunc(v * 2^80), split into
+// three signed 40-bit limbs (v ~ l0 2^-80 + l1 2^-40 + l2), and each limb is added to a 64-bit
+// integer accumulator; integer addition is associative, so the sums -- and every gradient
+// downstream -- are bit-identical from run to run whatever order the waves finish in, and
+// det_finish_kernel converts them into the usual float records.  The resolution (2^-80 ~ 8e-25)
+// is relative to nothing: a mean-reduced loss's 1e-9 wave totals keep ~50 significant bits
+// (a fixed 2^-32 step lost them).  |v| is clamped below 2^40; a limb sum stays below
+// 2^63 for up to 2^22 totals per Gaussian and field (an 8x8 block per total: 2^28 pixels).
+constexpr int DET_LIMBS = 3;
+__device__ __forceinline__ void det_add(unsigned long long *acc, float v) {
+  const uint32_t u = __float_as_uint(v);
+  int e = (int)((u >> 23) & 0xff);
+  if (e == 0) return;                 // zero or denormal (< 2^-126: below the resolution)
+  if (e > 126 + 40) e = 126 + 40;     // |v| < 2^40 (inf / NaN saturate)
+  const unsigned long long m = (u & 0x7fffffu) | 0x800000u;  // v = m 2^(e - 150)
+  const int sh = e - 70;                                      // X = v 2^80 = m 2^(e - 70)
+  unsigned __int128 X;
+  if (sh >= 0) X = (unsigned __int128)m << sh;
+  else X = sh > -64 ? (unsigned __int128)(m >> -sh) : 0;
+  constexpr unsigned long long M40 = (1ull << 40) - 1;
+  long long l0 = (long long)((unsigned long long)X & M40);
+  long long l1 = (long long)((unsigned long long)(X >> 40) & M40);
+  long long l2 = (long long)(unsigned long long)(X >> 80);
+  if (u >> 31) {
+    l0 = -l0;
+    l1 = -l1;
+    l2 = -l2;
+  }
+  atomicAdd(acc, (unsigned long long)l0);
+  atomicAdd(acc + 1, (unsigned long long)l1);
+  atomicAdd(acc + 2, (unsigned long long)l2);
 }
 __global__ __launch_bounds__(256) void det_finish_kernel(int n,
                                                          const unsigned long long *__restrict__ det,
@@ -61,28 +84,66 @@ __global__ __launch_bounds__(256) void det_finish_kernel(int n,
   const int g = blockIdx.x * 256 + threadIdx.x;
   if (g >= n) return;
 #pragma unroll
-  for (int k = 0; k < DET_REC; ++k)
-    rec[(size_t)g * REC + k] =
-        (float)((double)(long long)det[(size_t)g * DET_REC + k] * (1.0 / 4294967296.0));
+  for (int k = 0; k < REC_FIELDS; ++k) {
+    const unsigned long long *a = det + ((size_t)g * REC_FIELDS + k) * DET_LIMBS;
+    const double v = ((double)(long long)a[2] + (double)(long long)a[1] * 0x1p-40) +
+                     (double)(long long)a[0] * 0x1p-80;
+    rec[(size_t)g * REC + k] = (float)v;
+  }
 }
 bool g_det = false;
-unsigned long long *g_det_buf = nullptr;
-size_t g_det_cap = 0;
-// The deterministic accumulators (debug mode only: allocated on first use, grown as needed,
-// then cleared on the call's stream).
-unsigned long long *det_buffer(int n, hipStream_t st) {
-  const size_t need = (size_t)n * DET_REC * sizeof(unsigned long long);
-  if (need > g_det_cap) {
-    if (g_det_buf) note(hipFree(g_det_buf), "hipFree");
-    g_det_buf = nullptr;
-    note(hipMalloc(&g_det_buf, need), "hipMalloc");
-    g_det_cap = g_det_buf ? need : 0;
+// The deterministic accumulators (debug mode only): one buffer per device, allocated on first
+// use and grown as needed.  A use (DetLease) holds a process-wide lock from the clear to the
+// enqueue of det_finish_kernel, and the next use -- on any stream or thread -- waits for the
+// event recorded after the previous one's finish before clearing, so two backwards in flight
+// never share the accumulators.  Growing synchronises the device first (no queued kernel still
+// reads the old buffer).
+constexpr int DET_MAX_DEVICES = 64;
+struct DetState {
+  unsigned long long *buf = nullptr;
+  size_t cap = 0;
+  hipEvent_t done = nullptr;
+};
+std::mutex g_det_mu;
+DetState g_det_dev[DET_MAX_DEVICES];
+struct DetLease {
+  std::unique_lock<std::mutex> lock;
+  DetState *s = nullptr;
+  unsigned long long *buf = nullptr;
+  hipStream_t st = nullptr;
+  DetLease(int n, hipStream_t stream) : lock(g_det_mu), st(stream) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= DET_MAX_DEVICES) {
+      set_error("deterministic backward: no usable device");
+      return;
+    }
+    s = &g_det_dev[dev];
+    const size_t need = (size_t)n * REC_FIELDS * DET_LIMBS * sizeof(unsigned long long);
+    if (!s->done) note(hipEventCreateWithFlags(&s->done, hipEventDisableTiming), "hipEventCreate");
+    else note(hipStreamWaitEvent(st, s->done, 0), "hipStreamWaitEvent");
+    if (need > s->cap) {
+      if (s->buf) {
+        note(hipDeviceSynchronize(), "hipDeviceSynchronize");
+        note(hipFree(s->buf), "hipFree");
+      }
+      s->buf = nullptr;
+      s->cap = 0;
+      if (hipMalloc(&s->buf, need) == hipSuccess) s->cap = need;
+      else s->buf = nullptr;
+    }
+    if (s->buf) note(hipMemsetAsync(s->buf, 0, need, st), "hipMemsetAsync");
+    buf = s->buf;
   }
-  if (g_det_buf) note(hipMemsetAsync(g_det_buf, 0, need, st), "hipMemsetAsync");
-  return g_det_buf;
-}
+  // call after det_finish_kernel has been enqueued on st
+  void finish() {
+    if (s && s->done) note(hipEventRecord(s->done, st), "hipEventRecord");
+  }
+};
 constexpr int FWD_PXL = 1;  // forward: 8x8 blocks, two Gaussians per iteration (4 waves/tile)
-constexpr int BWD_PXL = 2;  // packed backward, 16x8 strips (2 waves per tile)
+// backward geometry (gsplat_debug_set_raster_variant's bwd_pxl): 1 = 8x8 blocks, one pixel per
+// lane, two Gaussians per iteration (raster_bwd8_kernel, shipped); 2 = 16x8 strips, two pixels
+// per lane (raster_bwd3p_kernel, the round-2 kernel kept for A/B measurements)
+constexpr int BWD_PXL = 1;
 // Tuning / ablation knobs (gsplat_debug_set_raster_variant); defaults are the shipped ones.
 int g_fwd_pxl = FWD_PXL, g_bwd_pxl = BWD_PXL, g_bwd_flags = 0;
 
@@ -105,39 +166,12 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ float gs_sigma(float hc, float bdx, float hA, float dy) {
   return fmaf(fmaf(hc, dy, bdx), dy, hA);
 }
-__device__ __forceinline__ f2 gs_sigma2(float hc, float bdx, float hA, f2 dy) {
-  return __builtin_elementwise_fma(__builtin_elementwise_fma((f2)hc, dy, (f2)bdx), dy, (f2)hA);
-}
 // exp(-sigma) with the hardware exp2 (gsplat: __expf).
 constexpr float NEG_LOG2E = -0x1.715476p+0f;
 __device__ __forceinline__ float gs_vis(float sigma) {
   return __builtin_amdgcn_exp2f(sigma * NEG_LOG2E);
 }
-__device__ __forceinline__ f2 gs_vis2(f2 sigma) {
-  const f2 e = sigma * NEG_LOG2E;
-  return (f2){__builtin_amdgcn_exp2f(e.x), __builtin_amdgcn_exp2f(e.y)};
-}
 
-// A pixel pair as two scalars (s2) or one packed register pair (f2): the same arithmetic,
-// rounding and decisions either way; s2 compiles to scalar v_fma/v_mul (gfx950 issues packed
-// fp32 ops no faster than two scalar ones), f2 to v_pk_*.
-struct s2 {
-  float x, y;
-  __device__ __forceinline__ s2() {}
-  __device__ __forceinline__ s2(float v) : x(v), y(v) {}
-  __device__ __forceinline__ s2(float a, float b) : x(a), y(b) {}
-};
-__device__ __forceinline__ s2 operator+(s2 a, s2 b) { return s2(a.x + b.x, a.y + b.y); }
-__device__ __forceinline__ s2 operator-(s2 a, s2 b) { return s2(a.x - b.x, a.y - b.y); }
-__device__ __forceinline__ s2 operator*(s2 a, s2 b) { return s2(a.x * b.x, a.y * b.y); }
-__device__ __forceinline__ s2 operator+(float a, s2 b) { return s2(a) + b; }
-__device__ __forceinline__ s2 operator-(float a, s2 b) { return s2(a) - b; }
-__device__ __forceinline__ s2 operator*(float a, s2 b) { return s2(a) * b; }
-__device__ __forceinline__ s2 operator*(s2 a, float b) { return a * s2(b); }
-__device__ __forceinline__ s2 &operator+=(s2 &a, s2 b) { a = a + b; return a; }
-__device__ __forceinline__ s2 vfma(s2 a, s2 b, s2 c) {
-  return s2(fmaf(a.x, b.x, c.x), fmaf(a.y, b.y, c.y));
-}
 __device__ __forceinline__ f2 vfma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
 template <typename V>
 __device__ __forceinline__ V gs_sigma2v(float hc, float bdx, float hA, V dy) {
@@ -375,32 +409,6 @@ __device__ __forceinline__ int wave_slot() {
   constexpr int WPT = (GS_BLOCK / COLS) * (GS_BLOCK / ((64 / COLS) * PXL));
   return block_slot() * (4 / WPT) + (threadIdx.x >> 6) / WPT;
 }
-// Tile swizzle of the work slots (gsplat_debug_set_tile_swizzle): slots run through bands of
-// GH tile rows in groups of GW x GH tiles (row-major inside a group), so the XCD chunks above
-// hold 2-D neighbourhoods instead of runs along one tile row.  Bijective over [0, T): a band's
-// last group is narrower when GW does not divide tbx, rows below the last full band keep
-// their slot order.  GW = GH = 1: the plain row-major order.
-__device__ int g_tile_gw = 1, g_tile_gh = 1;
-__device__ __forceinline__ int swizzle_tile(int s, int tbx, int tby) {
-  const int gw = g_tile_gw, gh = g_tile_gh;
-  if (gw * gh == 1) return s;
-  const int band_slots = gh * tbx, nbands = tby / gh;
-  const int band = s / band_slots;
-  if (band >= nbands) return s;
-  const int w = s - band * band_slots, gsz = gw * gh, nfull = tbx / gw;
-  int tx, ty;
-  if (w < nfull * gsz) {
-    const int cg = w / gsz, r = w - cg * gsz;
-    tx = cg * gw + r % gw;
-    ty = r / gw;
-  } else {
-    const int rw = tbx - nfull * gw, r = w - nfull * gsz;
-    tx = nfull * gw + r % rw;
-    ty = r / rw;
-  }
-  return (band * gh + ty) * tbx + tx;
-}
-
 template <int PXL, int COLS>
 __device__ __forceinline__ WaveRect wave_rect(int tbx, int tby, int H, int W, int tile = -1) {
   constexpr int LROWS = 64 / COLS;      // rows per lane pass
@@ -414,7 +422,7 @@ __device__ __forceinline__ WaveRect wave_rect(int tbx, int tby, int H, int W, in
     r.tile = tile;
   } else {
     const int slot = wave_slot<PXL, COLS>();
-    r.tile = slot < tbx * tby ? swizzle_tile(slot, tbx, tby) : slot;
+    r.tile = slot;
   }
   const int wt = wave % WPT;
   const int tx = r.tile % tbx, ty = r.tile / tbx;
@@ -434,103 +442,6 @@ constexpr int tiles_per_block() {
 }
 
 // ---------------------------------------------------------------- forward, C = 3
-// Scalar variant: PXL pixels per lane (rows i0 + 4k of one column).
-template <int PXL>
-__global__ __launch_bounds__(256) void raster_fwd3_kernel(
-    int tbx, int tby, int H, int W, const int *__restrict__ gids, const int2 *__restrict__ bins,
-    const float2 *__restrict__ xys, const float *__restrict__ conics,
-    const float *__restrict__ colors, const float *__restrict__ opacity,
-    const float *__restrict__ background, float *__restrict__ out_img,
-    float *__restrict__ final_Ts, int *__restrict__ final_idx) {
-  constexpr int WPT = 4 / PXL;    // waves per tile
-  constexpr int TPBLK = 4 / WPT;  // tiles per workgroup
-  constexpr int ROWS = 4 * PXL;   // rows per strip
-  __shared__ GStage lds[4][64];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int tile = blockIdx.x * TPBLK + wave / WPT;
-  const int strip = wave % WPT;
-  if (tile >= tbx * tby) return;  // wave-uniform
-  const int tx = tile % tbx, ty = tile / tbx;
-  const int r0 = ty * GS_BLOCK + strip * ROWS;
-  if (r0 >= H) return;  // strip entirely below the image
-  const int j = tx * GS_BLOCK + (lane & 15);
-  const int i0 = r0 + (lane >> 4);
-  const float px = (float)j;
-  const float rx0 = (float)(tx * GS_BLOCK), rx1 = (float)min(tx * GS_BLOCK + 15, W - 1);
-  const float ry0 = (float)r0, ry1 = (float)min(r0 + ROWS - 1, H - 1);
-  float py[PXL], T[PXL], cr[PXL], cg[PXL], cb[PXL];
-  int cur[PXL];
-  bool done[PXL];
-#pragma unroll
-  for (int k = 0; k < PXL; ++k) {
-    const int i = i0 + 4 * k;
-    py[k] = (float)i;
-    T[k] = 1.f;
-    cr[k] = cg[k] = cb[k] = 0.f;
-    cur[k] = 0;
-    done[k] = !(i < H && j < W);
-  }
-  const int2 range = bins[tile];
-  GStage *stage = lds[wave];
-  for (int b = range.x; b < range.y; b += 64) {
-    bool all_done = true;
-#pragma unroll
-    for (int k = 0; k < PXL; ++k) all_done = all_done && done[k];
-    if (__all(all_done)) break;
-    const int idx = b + lane;
-    GStage s;
-    const bool keep = idx < range.y &&
-                      stage_gaussian(idx, gids, xys, conics, colors, opacity, rx0, rx1, ry0,
-                                     ry1, s);
-    const unsigned long long kmask = __ballot(keep);
-    if (keep) stage[lanes_below(kmask)] = s;
-    const int n = __popcll(kmask);
-    wave_lds_sync();
-    for (int t = 0; t < n; ++t) {
-      const GStage G = stage[t];
-      const float dx = G.x - px;
-      const float hA = G.ha * dx * dx, bdx = G.b * dx;
-      bool fin = true;
-#pragma unroll
-      for (int k = 0; k < PXL; ++k) {
-        if (!done[k]) {
-          const float sigma = gs_sigma(G.hc, bdx, hA, G.y - py[k]);
-          const float alpha = fminf(0.999f, G.o * gs_vis(sigma));
-          if (sigma >= 0.f && alpha >= ALPHA_MIN) {
-            const float nT = T[k] * (1.f - alpha);
-            if (nT <= 1e-4f) {
-              done[k] = true;
-            } else {
-              const float vis = alpha * T[k];
-              cr[k] += G.r * vis;
-              cg[k] += G.g * vis;
-              cb[k] += G.bl * vis;
-              T[k] = nT;
-              cur[k] = G.idx;
-            }
-          }
-        }
-        fin = fin && done[k];
-      }
-      if (__all(fin)) break;
-    }
-    wave_lds_sync();
-  }
-  const float bg0 = background[0], bg1 = background[1], bg2 = background[2];
-#pragma unroll
-  for (int k = 0; k < PXL; ++k) {
-    const int i = i0 + 4 * k;
-    if (i < H && j < W) {
-      const int pix = i * W + j;
-      final_Ts[pix] = T[k];
-      final_idx[pix] = cur[k];
-      out_img[3 * pix] = cr[k] + T[k] * bg0;
-      out_img[3 * pix + 1] = cg[k] + T[k] * bg1;
-      out_img[3 * pix + 2] = cb[k] + T[k] * bg2;
-    }
-  }
-}
-
 // Two staged Gaussians per iteration (PXL pixels per lane, branch-free): both Gaussians'
 // sigma / exp / alpha are independent and evaluated together; only the transmittance
 // update is applied in list order, so every pixel sees exactly the scalar kernel's
@@ -693,232 +604,7 @@ __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
   clear_side_job();
 }
 
-// Packed variant: 2*NP pixels per lane held as NP float2 pairs and blended branch-free
-// with v_pk_{fma,mul,add}_f32 (two fp32 lanes per VALU op).  A pixel that is not composited
-// this step gets alpha 0, which leaves T and the colour sums exactly unchanged.
-template <int NP>
-__global__ __launch_bounds__(256) void raster_fwd3p_kernel(
-    int tbx, int tby, int H, int W, const int *__restrict__ gids, const int2 *__restrict__ bins,
-    const float2 *__restrict__ xys, const float *__restrict__ conics,
-    const float *__restrict__ colors, const float *__restrict__ opacity,
-    const float *__restrict__ background, float *__restrict__ out_img,
-    float *__restrict__ final_Ts, int *__restrict__ final_idx) {
-  constexpr int PXL = 2 * NP;
-  constexpr int WPT = 4 / PXL;
-  constexpr int TPBLK = 4 / WPT;
-  constexpr int ROWS = 4 * PXL;
-  __shared__ GStage lds[4][64];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int tile = blockIdx.x * TPBLK + wave / WPT;
-  const int strip = wave % WPT;
-  if (tile >= tbx * tby) return;
-  const int tx = tile % tbx, ty = tile / tbx;
-  const int r0 = ty * GS_BLOCK + strip * ROWS;
-  if (r0 >= H) return;
-  const int j = tx * GS_BLOCK + (lane & 15);
-  const int i0 = r0 + (lane >> 4);
-  const float px = (float)j;
-  const float rx0 = (float)(tx * GS_BLOCK), rx1 = (float)min(tx * GS_BLOCK + 15, W - 1);
-  const float ry0 = (float)r0, ry1 = (float)min(r0 + ROWS - 1, H - 1);
-  f2 py[NP], T[NP], cr[NP], cg[NP], cb[NP];
-  int cur[PXL];
-  bool done[PXL];
-#pragma unroll
-  for (int p = 0; p < NP; ++p) {
-    const int ia = i0 + 8 * p, ib = ia + 4;
-    py[p] = (f2){(float)ia, (float)ib};
-    T[p] = (f2)1.f;
-    cr[p] = cg[p] = cb[p] = (f2)0.f;
-    cur[2 * p] = cur[2 * p + 1] = 0;
-    done[2 * p] = !(ia < H && j < W);
-    done[2 * p + 1] = !(ib < H && j < W);
-  }
-  const int2 range = bins[tile];
-  GStage *stage = lds[wave];
-  for (int b = range.x; b < range.y; b += 64) {
-    bool all_done = true;
-#pragma unroll
-    for (int k = 0; k < PXL; ++k) all_done = all_done && done[k];
-    if (__all(all_done)) break;
-    const int idx = b + lane;
-    GStage s;
-    const bool keep = idx < range.y &&
-                      stage_gaussian(idx, gids, xys, conics, colors, opacity, rx0, rx1, ry0,
-                                     ry1, s);
-    const unsigned long long kmask = __ballot(keep);
-    if (keep) stage[lanes_below(kmask)] = s;
-    const int n = __popcll(kmask);
-    wave_lds_sync();
-    for (int t = 0; t < n; ++t) {
-      const GStage G = stage[t];
-      const float dx = G.x - px;
-      const float hA = G.ha * dx * dx, bdx = G.b * dx;
-      bool fin = true;
-#pragma unroll
-      for (int p = 0; p < NP; ++p) {
-        const f2 sg = gs_sigma2(G.hc, bdx, hA, G.y - py[p]);
-        const f2 ov = G.o * gs_vis2(sg);
-        const f2 al = {fminf(0.999f, ov.x), fminf(0.999f, ov.y)};
-        const f2 nT = T[p] * (1.f - al);
-        const bool v0 = !done[2 * p] && sg.x >= 0.f && al.x >= ALPHA_MIN;
-        const bool v1 = !done[2 * p + 1] && sg.y >= 0.f && al.y >= ALPHA_MIN;
-        const bool t0 = v0 && nT.x <= 1e-4f, t1 = v1 && nT.y <= 1e-4f;
-        const bool c0 = v0 && !t0, c1 = v1 && !t1;
-        done[2 * p] = done[2 * p] || t0;
-        done[2 * p + 1] = done[2 * p + 1] || t1;
-        const f2 w = (f2){c0 ? al.x : 0.f, c1 ? al.y : 0.f} * T[p];
-        cr[p] = __builtin_elementwise_fma((f2)G.r, w, cr[p]);
-        cg[p] = __builtin_elementwise_fma((f2)G.g, w, cg[p]);
-        cb[p] = __builtin_elementwise_fma((f2)G.bl, w, cb[p]);
-        T[p] = (f2){c0 ? nT.x : T[p].x, c1 ? nT.y : T[p].y};
-        cur[2 * p] = c0 ? G.idx : cur[2 * p];
-        cur[2 * p + 1] = c1 ? G.idx : cur[2 * p + 1];
-        fin = fin && done[2 * p] && done[2 * p + 1];
-      }
-      if (__all(fin)) break;
-    }
-    wave_lds_sync();
-  }
-  const float bg0 = background[0], bg1 = background[1], bg2 = background[2];
-#pragma unroll
-  for (int k = 0; k < PXL; ++k) {
-    const int i = i0 + 4 * k;
-    const int p = k >> 1;
-    const float Tk = (k & 1) ? T[p].y : T[p].x;
-    if (i < H && j < W) {
-      const int pix = i * W + j;
-      final_Ts[pix] = Tk;
-      final_idx[pix] = cur[k];
-      out_img[3 * pix] = ((k & 1) ? cr[p].y : cr[p].x) + Tk * bg0;
-      out_img[3 * pix + 1] = ((k & 1) ? cg[p].y : cg[p].x) + Tk * bg1;
-      out_img[3 * pix + 2] = ((k & 1) ? cb[p].y : cb[p].x) + Tk * bg2;
-    }
-  }
-}
-
 // ---------------------------------------------------------------- backward, C = 3
-// Record fields: 0 v_x, 1 v_y, 2..4 v_conic (a, b, c) * CONIC_SCALE^-1, 5..7 v_rgb,
-// 8 v_opacity.  The scalar kernel stores v_conic itself (scale 1); the packed kernel stores
-// 2*v_conic (the 0.5 is applied once in split_grads_kernel, exact).
-template <int PXL, bool ATOMICS>
-__global__ __launch_bounds__(256) void raster_bwd3_kernel(
-    int tbx, int tby, int H, int W, const int *__restrict__ gids, const int2 *__restrict__ bins,
-    const float2 *__restrict__ xys, const float *__restrict__ conics,
-    const float *__restrict__ colors, const float *__restrict__ opacity,
-    const float *__restrict__ background, const float *__restrict__ final_Ts,
-    const int *__restrict__ final_idx, const float *__restrict__ v_out,
-    const float *__restrict__ v_out_alpha, float alpha_max, float *__restrict__ rec) {
-  constexpr int WPT = 4 / PXL;
-  constexpr int TPBLK = 4 / WPT;
-  constexpr int ROWS = 4 * PXL;
-  __shared__ GStage lds[4][64];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int tile = blockIdx.x * TPBLK + wave / WPT;
-  const int strip = wave % WPT;
-  if (tile >= tbx * tby) return;
-  const int tx = tile % tbx, ty = tile / tbx;
-  const int r0 = ty * GS_BLOCK + strip * ROWS;
-  if (r0 >= H) return;
-  const int j = tx * GS_BLOCK + (lane & 15);
-  const int i0 = r0 + (lane >> 4);
-  const float px = (float)j;
-  const float rx0 = (float)(tx * GS_BLOCK), rx1 = (float)min(tx * GS_BLOCK + 15, W - 1);
-  const float ry0 = (float)r0, ry1 = (float)min(r0 + ROWS - 1, H - 1);
-  const float bg0 = background[0], bg1 = background[1], bg2 = background[2];
-  float py[PXL], T[PXL], Tf[PXL], vr[PXL], vg[PXL], vb[PXL], va[PXL], bgdot[PXL];
-  float br[PXL], bgr[PXL], bb[PXL];
-  int binf[PXL];
-  int maxbin = -1;
-#pragma unroll
-  for (int k = 0; k < PXL; ++k) {
-    const int i = i0 + 4 * k;
-    py[k] = (float)i;
-    br[k] = bgr[k] = bb[k] = 0.f;
-    if (i < H && j < W) {
-      const int pix = i * W + j;
-      Tf[k] = final_Ts[pix];
-      binf[k] = final_idx[pix];
-      vr[k] = v_out[3 * pix];
-      vg[k] = v_out[3 * pix + 1];
-      vb[k] = v_out[3 * pix + 2];
-      va[k] = v_out_alpha ? v_out_alpha[pix] : 0.f;
-    } else {
-      Tf[k] = 0.f;
-      binf[k] = -1;
-      vr[k] = vg[k] = vb[k] = va[k] = 0.f;
-    }
-    T[k] = Tf[k];
-    bgdot[k] = bg0 * vr[k] + bg1 * vg[k] + bg2 * vb[k];
-    maxbin = max(maxbin, binf[k]);
-  }
-  maxbin = wave_max_int(maxbin);
-  const int slot = reduce9_slot();  // record field this lane adds (reduce9), or -1
-  const int2 range = bins[tile];
-  const int last = min(maxbin, range.y - 1);
-  GStage *stage = lds[wave];
-  for (int b = last; b >= range.x; b -= 64) {
-    const int idx = b - lane;
-    GStage s;
-    const bool keep = idx >= range.x &&
-                      stage_gaussian(idx, gids, xys, conics, colors, opacity, rx0, rx1, ry0,
-                                     ry1, s);
-    const unsigned long long kmask = __ballot(keep);
-    if (keep) stage[lanes_below(kmask)] = s;
-    const int n = __popcll(kmask);
-    wave_lds_sync();
-    for (int t = 0; t < n; ++t) {
-      const GStage G = stage[t];
-      const float dx = G.x - px;
-      const float hA = G.ha * dx * dx, bdx = G.b * dx;
-      const float a2 = 2.f * G.ha, c2 = 2.f * G.hc;
-      float s_x = 0.f, s_y = 0.f, s_a = 0.f, s_b = 0.f, s_c = 0.f, s_r = 0.f, s_g = 0.f,
-            s_bl = 0.f, s_o = 0.f;
-      bool anyv = false;
-#pragma unroll
-      for (int k = 0; k < PXL; ++k) {
-        const float dy = G.y - py[k];
-        const float sigma = gs_sigma(G.hc, bdx, hA, dy);
-        const float vis = gs_vis(sigma);
-        const float alpha = fminf(alpha_max, G.o * vis);
-        const bool valid = G.idx <= binf[k] && sigma >= 0.f && alpha >= ALPHA_MIN;
-        if (valid) {
-          anyv = true;
-          const float ra = __builtin_amdgcn_rcpf(1.f - alpha);
-          T[k] *= ra;
-          const float fac = alpha * T[k];
-          s_r += fac * vr[k];
-          s_g += fac * vg[k];
-          s_bl += fac * vb[k];
-          float v_alpha = (G.r * T[k] - br[k] * ra) * vr[k] + (G.g * T[k] - bgr[k] * ra) * vg[k] +
-                          (G.bl * T[k] - bb[k] * ra) * vb[k];
-          v_alpha += Tf[k] * ra * va[k];
-          v_alpha += -Tf[k] * ra * bgdot[k];
-          br[k] += G.r * fac;
-          bgr[k] += G.g * fac;
-          bb[k] += G.bl * fac;
-          const float v_sigma = -G.o * vis * v_alpha;
-          s_a += 0.5f * v_sigma * dx * dx;
-          s_b += 0.5f * v_sigma * dx * dy;
-          s_c += 0.5f * v_sigma * dy * dy;
-          s_x += v_sigma * (a2 * dx + G.b * dy);
-          s_y += v_sigma * (G.b * dx + c2 * dy);
-          s_o += vis * v_alpha;
-        }
-      }
-      if (__any(anyv)) {
-        const float parts[9] = {s_x, s_y, s_a, s_b, s_c, s_r, s_g, s_bl, s_o};
-        const float v = reduce9(parts);
-        if constexpr (ATOMICS) {
-          if (slot >= 0) atomicAdd(rec + (size_t)G.id * REC + slot, v);
-        } else {
-          asm volatile("" ::"v"(v));  // ablation build: keep the reduction, drop the atomic
-        }
-      }
-    }
-    wave_lds_sync();
-  }
-}
-
 // Packed backward: 2*NP pixels per lane as float2 pairs, branch-free (an invalid pixel gets
 // alpha = vis = 0: T, the colour buffer and every partial sum are unchanged exactly).
 // Per pixel the colour buffer is carried as one dot product Sb = sum_c buf_c * v_c, and the
@@ -1096,30 +782,40 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
         }
         anyv[u] = any;
         anyw[u] = anym;
-        const float Vs = -G.o * sa, Vys = -G.o * my;
-        const float dxV = dx * Vs;
-        parts[u][0] = fmaf(2.f * G.ha, dxV, G.b * Vys);  // v_x
-        parts[u][1] = fmaf(G.b, dxV, 2.f * G.hc * Vys);  // v_y
-        parts[u][2] = dx * dxV;                          // 2 v_conic.a
-        parts[u][3] = dx * Vys;                          // 2 v_conic.b
-        parts[u][4] = -G.o * myy;                        // 2 v_conic.c
-        parts[u][5] = sr;
-        parts[u][6] = sg;
-        parts[u][7] = sb;
-        parts[u][8] = sa;
+        // the record moments (common.h record_grads), dx constant along the lane's column
+        const float sx = dx * sa;
+        parts[u][REC_SX] = sx;
+        parts[u][REC_SY] = my;
+        parts[u][REC_SXX] = dx * sx;
+        parts[u][REC_SXY] = dx * my;
+        parts[u][REC_SYY] = myy;
+        parts[u][REC_R] = sr;
+        parts[u][REC_G] = sg;
+        parts[u][REC_B] = sb;
+        parts[u][REC_S0] = sa;
       }
       unsigned long long any_all = 0;
 #pragma unroll
       for (int u = 0; u < U; ++u) any_all |= anyw[u];
       if (any_all) {  // (an SGPR test, no VGPR round trip)
         float v[U];
+#ifdef GS_ABLATE_NO_REDUCE  // attribution build (tools/attr_bwd.sh): a lane-local sum instead
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          float s = parts[u][0];
+#pragma unroll
+          for (int k = 1; k < 9; ++k) s += parts[u][k];
+          v[u] = s;
+        }
+#else
 #pragma unroll
         for (int u = 0; u < U; ++u) v[u] = reduce9(parts[u]);
+#endif
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           if constexpr (DET) {  // deterministic mode: exact integer sums of the wave totals
             if (__any(anyv[u]) && slot >= 0)
-              atomicAdd(det + (size_t)gid[u] * DET_REC + slot, det_quantize(v[u]));
+              det_add(det + ((size_t)gid[u] * REC_FIELDS + slot) * DET_LIMBS, v[u]);
           } else if constexpr (ATOMICS) {
             // 32-bit element offset (the entry points reject N >= 2^27): the atomic takes the
             // SGPR base + a VGPR offset, no 64-bit address arithmetic per iteration
@@ -1137,33 +833,29 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
   wlog.done(tile);
 }
 
-// ---------------------------------------------------------------- tile-wave backward
-// One wave per 16x16 tile.  Lane l holds column l & 15 and rows rg, rg+4 | rg+8, rg+12
-// (rg = l >> 4) as two float2 pixel pairs: pair 0 lies in the tile's top 16x8 half, pair 1 in
-// the bottom half.  Each staged Gaussian carries two cull bits (top / bottom half, each also
-// limited to that half's last contributing list position), and the blend of a pair runs only
-// when its half is touched (a wave-uniform branch).  The per-Gaussian fixed cost -- LDS read,
-// the nine partial sums, the reduce-scatter and the atomic -- is paid once per tile instead of
-// once per 16x8 strip, while the per-pixel work keeps the 16x8 cull (measured on the headline
-// scene: 191.5 staged Gaussians per tile against 293.2 strip iterations).
+// ---------------------------------------------------------------- block backward (shipped)
+// The forward's geometry: a wave owns an 8x8 block of its tile (4 waves per tile, one pixel
+// per lane) and walks the block's culled list back to front two staged Gaussians per
+// iteration.  Against the 16x8 strips with two pixels per lane:
+//  * the exact rectangle cull against an 8x8 block keeps fewer Gaussians, so more of the
+//    lane slots an iteration spends are valid pixel-Gaussian pairs (forward: 52 % vs 40 %);
+//  * twice as many waves of half the length: the part of the kernel in which fewer waves than
+//    wave slots remain (the tail) shrinks;
+//  * the two Gaussians' sigma / exp / alpha / cull tests are independent instruction chains;
+//    only the transmittance and colour-behind updates run in list order;
+//  * per pixel the lane forms the record moments (w, dx w, dy w, dx^2 w, dx dy w, dy^2 w and
+//    alpha T v_out: record_grads() in common.h) with five products, and ONE 18-value
+//    reduce-scatter (reduce18) sums both Gaussians' nine moments, whose totals one atomic
+//    instruction (18 lanes, two records) adds to the records.
+// Per pixel the arithmetic is gsplat's backward (T recovered by dividing by 1 - alpha with the
+// hardware reciprocal, v_alpha from the colour behind); the per-pixel decisions (sigma >= 0,
+// alpha >= 1/255, idx <= final_idx) are the forward's bit for bit (gs_sigma / gs_vis).
 //
-// Per pixel the blend drops two products and two selects of raster_bwd3p_kernel: for a
-// Gaussian with o <= alpha_max the alpha clamp cannot bind (vis <= 1 wherever sigma >= 0), so
-// alpha = o * vis and vis * v_alpha = (alpha * v_alpha) / o.  The lanes accumulate
-// alpha * v_alpha and its dy moments; the factors -o and 1/o are applied once per Gaussian
-// before the reduction.  A Gaussian with o > alpha_max takes the clamped form.
-struct __attribute__((aligned(16))) GStageB {
-  float x, y, ha, b;   // mean, 0.5*conic.a, conic.b
-  float hc, o, r, g;   // 0.5*conic.c, opacity, colour
-  float bl;
-  int idx;             // position in the tile's sorted list
-  int id;              // Gaussian id
-  int halves;          // bit 0: touches the top 16x8 half, bit 1: the bottom half
-};
-
-template <bool CHUNKED = false, int WPB = 4>
-__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(5, 8))) void
-raster_bwd4_kernel(
+// CHUNKED: list-split items as raster_bwd3p_kernel (the four waves of a workgroup take the four
+// 8x8 blocks of one (tile, chunk) item).  DET: integer accumulation (det_add).  CNT: lane-slot
+// accounting (gsplat_debug_pair_count).
+template <bool CHUNKED = false, bool DET = false, bool CNT = false>
+__global__ __launch_bounds__(256) void raster_bwd8_kernel(
     int tbx, int tby, int H, int W, const int *__restrict__ gids, const int2 *__restrict__ bins,
     const float2 *__restrict__ xys, const float *__restrict__ conics,
     const float *__restrict__ colors, const float *__restrict__ opacity,
@@ -1172,60 +864,34 @@ raster_bwd4_kernel(
     const float *__restrict__ v_out_alpha, float alpha_max, float *__restrict__ rec,
     int chunk = 0, const int *__restrict__ item_off = nullptr,
     const int *__restrict__ item_tile = nullptr, const int *__restrict__ ckpt_off = nullptr,
-    const float4 *__restrict__ ckpt = nullptr, const int *__restrict__ order = nullptr,
-    int *__restrict__ queue = nullptr) {
-  constexpr int PXL = 4, LROWS = 4;
-  const WaveLog wlog;
-  __shared__ GStageB lds[WPB][64];
-  const int nslots = CHUNKED ? item_off[tbx * tby] : tbx * tby;
-  // one work slot (tile, or list-split item) per wave; with a queue, waves are persistent and
-  // take further slots from it (first slots dealt in launch order, then queue + #waves)
-  int tile = -1;
-  auto run = [&](const int wslot) {
-  int ctile = wslot, cj = 0;
-  if (!CHUNKED && order && wslot < tbx * tby) ctile = order[wslot];
+    const float4 *__restrict__ ckpt = nullptr, unsigned long long *__restrict__ det = nullptr) {
+  int ctile = -1, cj = 0;
   if (CHUNKED) {
-    ctile = item_tile[wslot];
-    cj = wslot - item_off[ctile];
+    const int slot = wave_slot<1, 8>();
+    if (slot >= item_off[tbx * tby]) return;  // wave-uniform: past the last item
+    ctile = item_tile[slot];
+    cj = slot - item_off[ctile];
   }
-  const WaveRect R = wave_rect<PXL, 16>(tbx, tby, H, W, ctile);
+  const WaveLog wlog;
+  const WaveRect R = wave_rect<1, 8>(tbx, tby, H, W, ctile);
   if (!R.live) return;  // wave-uniform
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  tile = R.tile;
-  const int j = R.j, i0 = R.i0;
-  const float px = (float)j;
-  // the two halves' pixel-centre rectangles (the bottom one may lie below the image)
-  const float rx0 = R.rx0, rx1 = R.rx1;
-  const float ty0 = R.ry0, ty1 = fminf(R.ry0 + 7.f, R.ry1);
-  const float by0 = R.ry0 + 8.f, by1 = R.ry1;
-  const bool bottom_live = by0 <= by1;
-  const float bg0 = background[0], bg1 = background[1], bg2 = background[2];
-  f2 py[2], T[2], vr[2], vg[2], vb[2], q[2], Sb[2];
-  int binf[PXL];
-  int mb0 = -1, mb1 = -1;
-#pragma unroll
-  for (int k = 0; k < PXL; ++k) {
-    const int i = i0 + LROWS * k, p = k >> 1;
-    float Tf = 0.f, r = 0.f, g = 0.f, bl = 0.f, a = 0.f;
-    int bf = -1;
-    if (i < H && j < W) {
-      const int pix = i * W + j;
-      Tf = final_Ts[pix];
-      bf = final_idx[pix];
-      r = v_out[3 * pix];
-      g = v_out[3 * pix + 1];
-      bl = v_out[3 * pix + 2];
-      a = v_out_alpha ? v_out_alpha[pix] : 0.f;
-    }
-    const float qk = Tf * (a - (bg0 * r + bg1 * g + bg2 * bl));
-    if (k & 1) {
-      py[p].y = (float)i; T[p].y = Tf; vr[p].y = r; vg[p].y = g; vb[p].y = bl; q[p].y = qk;
-    } else {
-      py[p].x = (float)i; T[p].x = Tf; vr[p].x = r; vg[p].x = g; vb[p].x = bl; q[p].x = qk;
-    }
-    Sb[p] = (f2)0.f;
-    binf[k] = bf;
-    if (p == 0) mb0 = max(mb0, bf); else mb1 = max(mb1, bf);
+  __shared__ GStage lds[4][64];
+  const int wave = threadIdx.x >> 6;
+  const int tile = R.tile, j = R.j, i = R.i0;
+  const float px = (float)j, py = (float)i;
+  float T = 0.f, vr = 0.f, vg = 0.f, vb = 0.f, q = 0.f, Sb = 0.f;
+  int bf = -1;
+  const bool inside = i < H && j < W;
+  if (inside) {
+    const int pix = i * W + j;
+    T = final_Ts[pix];
+    bf = final_idx[pix];
+    vr = v_out[3 * pix];
+    vg = v_out[3 * pix + 1];
+    vb = v_out[3 * pix + 2];
+    const float a = v_out_alpha ? v_out_alpha[pix] : 0.f;
+    // v_alpha's background / alpha-output terms: T_final / (1 - alpha) * (v_alpha_out - bg . v)
+    q = T * (a - (background[0] * vr + background[1] * vg + background[2] * vb));
   }
   const int2 range = bins[tile];
   int lo = range.x, hi = range.y;
@@ -1235,180 +901,118 @@ raster_bwd4_kernel(
     if (m > 1) {
       lo = range.x + cj * chunk;
       hi = min(lo + chunk, range.y);
-      if (cj < m - 1) {  // start from the checkpoint after this chunk
+      if (cj < m - 1 && inside) {  // start from the forward's checkpoint after this chunk
         const size_t cb = (size_t)ckpt_off[tile] * (GS_BLOCK * GS_BLOCK);
-        const int oy = (tile / tbx) * GS_BLOCK, ox = (tile % tbx) * GS_BLOCK;
-#pragma unroll
-        for (int k = 0; k < PXL; ++k) {
-          const int i = i0 + LROWS * k, p = k >> 1;
-          if (i < H && j < W) {
-            const int lpix = (i - oy) * GS_BLOCK + (j - ox);
-            const float4 cj4 = ckpt[cb + (size_t)cj * (GS_BLOCK * GS_BLOCK) + lpix];
-            const float4 cf4 = ckpt[cb + (size_t)(m - 1) * (GS_BLOCK * GS_BLOCK) + lpix];
-            const float vr_ = (k & 1) ? vr[p].y : vr[p].x, vg_ = (k & 1) ? vg[p].y : vg[p].x,
-                        vb_ = (k & 1) ? vb[p].y : vb[p].x;
-            const float sb = (cf4.y - cj4.y) * vr_ + (cf4.z - cj4.z) * vg_ + (cf4.w - cj4.w) * vb_;
-            if (k & 1) { T[p].y = cj4.x; Sb[p].y = sb; } else { T[p].x = cj4.x; Sb[p].x = sb; }
-          }
+        const int lpix = (i - (tile / tbx) * GS_BLOCK) * GS_BLOCK + (j - (tile % tbx) * GS_BLOCK);
+        const float4 c4 = ckpt[cb + (size_t)cj * (GS_BLOCK * GS_BLOCK) + lpix];
+        const float4 f4 = ckpt[cb + (size_t)(m - 1) * (GS_BLOCK * GS_BLOCK) + lpix];
+        T = c4.x;
+        Sb = (f4.y - c4.y) * vr + (f4.z - c4.z) * vg + (f4.w - c4.w) * vb;
+      }
+    }
+  }
+  const int maxbin = wave_max_int(bf);
+  // reduce18 lane roles, learned once: value k = slot (Gaussian slot / 9, field slot % 9)
+  const int slot = reduce18_slot();
+  const bool for0 = slot >= 0 && slot < 9, for1 = slot >= 9;
+  const int field = slot >= 9 ? slot - 9 : slot;
+  const float amax = __builtin_canonicalizef(alpha_max);
+  const int last = min(maxbin, hi - 1);
+  GStage *stage = lds[wave];
+  unsigned c_slots = 0, c_live = 0, c_valid = 0;  // (CNT only)
+  for (int b = last; b >= lo; b -= 64) {
+    const int idx = b - (threadIdx.x & 63);
+    GStage s;
+    const bool keep = idx >= lo && stage_gaussian<true>(idx, gids, xys, conics, colors, opacity,
+                                                        R.rx0, R.rx1, R.ry0, R.ry1, s);
+    const unsigned long long kmask = __ballot(keep);
+    if (keep) stage[lanes_below(kmask)] = s;
+    const int n = __popcll(kmask);
+    wave_lds_sync();
+    for (int t = 0; t < n; t += 2) {
+      GStage G0 = stage[t], G1 = stage[min(t + 1, 63)];
+      const bool live1 = t + 1 < n;
+      if (!live1) G1.r = G1.g = G1.bl = G1.o = 0.f;  // stale slot: alpha 0, finite terms
+      int gid0 = G0.id, gid1 = G1.id;
+      asm volatile("" : "+v"(gid0), "+v"(gid1));  // read with the records, not at the atomic
+      // the two Gaussians' per-pixel terms (independent)
+      const float dx0 = G0.x - px, dy0 = G0.y - py, dx1 = G1.x - px, dy1 = G1.y - py;
+      const float sg0 = gs_sigma(G0.hc, G0.b * dx0, G0.ha * dx0 * dx0, dy0);
+      const float sg1 = gs_sigma(G1.hc, G1.b * dx1, G1.ha * dx1 * dx1, dy1);
+      const float vis0 = gs_vis(sg0), vis1 = gs_vis(sg1);
+      const float al0 = fminf(amax, G0.o * vis0), al1 = fminf(amax, G1.o * vis1);
+      const bool v0 = G0.idx <= bf && sg0 >= 0.f && al0 >= ALPHA_MIN;
+      const bool v1 = live1 && G1.idx <= bf && sg1 >= 0.f && al1 >= ALPHA_MIN;
+      const unsigned long long any0 = __builtin_amdgcn_ballot_w64(v0),
+                               any1 = __builtin_amdgcn_ballot_w64(v1);
+      if constexpr (CNT) {
+        c_slots += 2 * 64;
+        c_live += (G0.idx <= bf ? 1u : 0u) + (live1 && G1.idx <= bf ? 1u : 0u);
+        c_valid += (v0 ? 1u : 0u) + (v1 ? 1u : 0u);
+      }
+      // list order (back to front): G0 then G1 -- T and the colour behind are sequential
+      const float am0 = v0 ? al0 : 0.f, am1 = v1 ? al1 : 0.f;
+      const float ra0 = __builtin_amdgcn_rcpf(1.f - am0);
+      T = T * ra0;
+      const float fac0 = am0 * T;
+      const float gv0 = fmaf(G0.r, vr, fmaf(G0.g, vg, G0.bl * vb));
+      const float va0 = fmaf(gv0, T, ra0 * (q - Sb));
+      Sb = fmaf(fac0, gv0, Sb);
+      const float ra1 = __builtin_amdgcn_rcpf(1.f - am1);
+      T = T * ra1;
+      const float fac1 = am1 * T;
+      const float gv1 = fmaf(G1.r, vr, fmaf(G1.g, vg, G1.bl * vb));
+      const float va1 = fmaf(gv1, T, ra1 * (q - Sb));
+      Sb = fmaf(fac1, gv1, Sb);
+      if (any0 | any1) {  // (an SGPR test)
+        const float w0 = (v0 ? vis0 : 0.f) * va0, w1 = (v1 ? vis1 : 0.f) * va1;
+        const float sx0 = dx0 * w0, sy0 = dy0 * w0, sx1 = dx1 * w1, sy1 = dy1 * w1;
+        const float m[18] = {sx0, sy0, dx0 * sx0, dy0 * sx0, dy0 * sy0,
+                             fac0 * vr, fac0 * vg, fac0 * vb, w0,
+                             sx1, sy1, dx1 * sx1, dy1 * sx1, dy1 * sy1,
+                             fac1 * vr, fac1 * vg, fac1 * vb, w1};
+        const float v = reduce18(m);
+        const bool act = (for0 && any0) || (for1 && any1);
+        const int g = for1 ? gid1 : gid0;
+        if constexpr (DET) {
+          if (act) det_add(det + ((size_t)g * REC_FIELDS + field) * DET_LIMBS, v);
+        } else {
+          // 32-bit element offset (the entry points reject N >= 2^27)
+          if (act) atomicAdd(rec + (uint32_t)(g * REC + field), v);
         }
       }
     }
-  }
-  mb0 = min(wave_max_int(mb0), hi - 1);
-  mb1 = min(wave_max_int(mb1), hi - 1);
-  const int slot = reduce9_slot();
-  const int last = max(mb0, mb1);
-  GStageB *stage = lds[wave];
-  for (int b = last; b >= lo; b -= 64) {
-    const int idx = b - lane;
-    int halves = 0;
-    GStageB s;
-    if (idx >= lo) {
-      const int g = gids[idx];
-      const float2 xy = xys[g];
-      const float a = conics[3 * g], bb = conics[3 * g + 1], c = conics[3 * g + 2];
-      const float o = opacity[g];
-      if (idx <= mb0 && touches_rect(xy.x, xy.y, a, bb, c, o, rx0, rx1, ty0, ty1)) halves = 1;
-      if (bottom_live && idx <= mb1 &&
-          touches_rect(xy.x, xy.y, a, bb, c, o, rx0, rx1, by0, by1))
-        halves |= 2;
-      if (halves) {
-        s.x = xy.x;
-        s.y = xy.y;
-        s.ha = 0.5f * a;
-        s.b = bb;
-        s.hc = 0.5f * c;
-        s.o = o;
-        s.r = colors[3 * g];
-        s.g = colors[3 * g + 1];
-        s.bl = colors[3 * g + 2];
-        s.idx = idx;
-        s.id = g;
-        s.halves = halves | (o <= alpha_max ? 0 : 4);
-      }
-    }
-    const unsigned long long kmask = __ballot(halves != 0);
-    if (halves) stage[lanes_below(kmask)] = s;
-    const int n = __popcll(kmask);
-    wave_lds_sync();
-    for (int t = 0; t < n; ++t) {
-      const GStageB G = stage[t];
-      // bits 0/1: halves touched; bit 2: o > alpha_max (the clamped form)
-      const int hv = __builtin_amdgcn_readfirstlane(G.halves);
-      const float dx = G.x - px;
-      const float hA = G.ha * dx * dx, bdx = G.b * dx;
-      f2 sr = 0.f, sg = 0.f, sb = 0.f, sa = 0.f, Vy = 0.f, Vyy = 0.f;
-      bool any = false;
-      // one pixel pair: sa accumulates o * vis * v_alpha (the unclamped alpha times v_alpha)
-      auto pair = [&](auto clamped, int p, int k0) {
-        constexpr bool CL = decltype(clamped)::value;
-        const f2 dy = G.y - py[p];
-        const f2 sig = gs_sigma2v<f2>(G.hc, bdx, hA, dy);
-        const f2 vis = gs_vis2v<f2>(sig);
-        const f2 ov = G.o * vis;
-        f2 al = ov;
-        if constexpr (CL) al = (f2){fminf(alpha_max, ov.x), fminf(alpha_max, ov.y)};
-        const bool v0 = G.idx <= binf[k0] && sig.x >= 0.f && al.x >= ALPHA_MIN;
-        const bool v1 = G.idx <= binf[k0 + 1] && sig.y >= 0.f && al.y >= ALPHA_MIN;
-        any = any || v0 || v1;
-        const f2 am = {v0 ? al.x : 0.f, v1 ? al.y : 0.f};
-        f2 ovm = am;
-        if constexpr (CL) ovm = (f2){v0 ? ov.x : 0.f, v1 ? ov.y : 0.f};
-        const f2 om = 1.f - am;
-        const f2 ra = {__builtin_amdgcn_rcpf(om.x), __builtin_amdgcn_rcpf(om.y)};
-        T[p] = T[p] * ra;
-        const f2 fac = am * T[p];
-        sr = vfma(fac, vr[p], sr);
-        sg = vfma(fac, vg[p], sg);
-        sb = vfma(fac, vb[p], sb);
-        const f2 gv = vfma((f2)G.r, vr[p], vfma((f2)G.g, vg[p], G.bl * vb[p]));
-        const f2 v_alpha = vfma(gv, T[p], ra * (q[p] - Sb[p]));
-        Sb[p] = vfma(fac, gv, Sb[p]);
-        const f2 va = ovm * v_alpha;
-        sa += va;
-        const f2 vady = va * dy;
-        Vy += vady;
-        Vyy = vfma(vady, dy, Vyy);
-      };
-      using F = std::integral_constant<bool, false>;
-      using Tr = std::integral_constant<bool, true>;
-      if (hv & 4) {
-        if (hv & 1) pair(Tr{}, 0, 0);
-        if (hv & 2) pair(Tr{}, 1, 2);
-      } else {
-        if (hv & 1) pair(F{}, 0, 0);
-        if (hv & 2) pair(F{}, 1, 2);
-      }
-      if (__any(any)) {
-        const float Sa = sa.x + sa.y;
-        const float Vs = -Sa, Vys = -(Vy.x + Vy.y);
-        const float dxV = dx * Vs;
-        float parts[9];
-        parts[0] = fmaf(2.f * G.ha, dxV, G.b * Vys);  // v_x
-        parts[1] = fmaf(G.b, dxV, 2.f * G.hc * Vys);  // v_y
-        parts[2] = dx * dxV;                          // 2 v_conic.a
-        parts[3] = dx * Vys;                          // 2 v_conic.b
-        parts[4] = -(Vyy.x + Vyy.y);                  // 2 v_conic.c
-        parts[5] = sr.x + sr.y;
-        parts[6] = sg.x + sg.y;
-        parts[7] = sb.x + sb.y;
-        parts[8] = Sa * __builtin_amdgcn_rcpf(G.o);  // v_opacity = sum vis * v_alpha
-        const float v = reduce9(parts);
-        if (slot >= 0) atomicAdd(rec + (size_t)G.id * REC + slot, v);
-      }
-    }
     wave_lds_sync();
   }
-  };
-  const int nw = gridDim.x * WPB;
-  for (int wslot = block_slot() * WPB + (threadIdx.x >> 6); wslot < nslots;) {
-    run(wslot);
-    if (!queue) break;
-    int v = 0;
-    if ((threadIdx.x & 63) == 0) v = atomicAdd(queue, 1);
-    wslot = nw + __builtin_amdgcn_readfirstlane(v);
-  }
+  if constexpr (CNT) pair_count_flush(0, c_slots, c_live, c_valid);
   wlog.done(tile);
 }
 
-// ---------------------------------------------------------------- grouped backward
-// Row-local reduce-scatter of nine values over each 16-lane DPP row (row_ror:8,
-// row_half_mirror, quad perms): afterwards nine lanes of every row each hold the row sum of
-// one value (reduce9_row_slot() says which) -- four independent reductions per instruction.
-__device__ __forceinline__ float reduce9_row(const float (&v)[9]) {
-  const int lane = __lane_id();
-  const bool h8 = lane & 8, h4 = lane & 4, h2 = lane & 2, h1 = lane & 1;
-  const float a0 = dpp_pair_sum<0x128>(v[0], v[5], h8), a1 = dpp_pair_sum<0x128>(v[1], v[6], h8),
-              a2 = dpp_pair_sum<0x128>(v[2], v[7], h8), a3 = dpp_pair_sum<0x128>(v[3], v[8], h8),
-              a4 = dpp_pair_sum<0x128>(v[4], 0.f, h8);
-  const float b0 = dpp_pair_sum<0x141>(a0, a2, h4), b1 = dpp_pair_sum<0x141>(a1, a3, h4),
-              b2 = dpp_pair_sum<0x141>(a4, 0.f, h4);
-  const float c0 = dpp_pair_sum<0x4E>(b0, b1, h2), c1 = dpp_pair_sum<0x4E>(b2, 0.f, h2);
-  return dpp_pair_sum<0xB1>(c0, c1, h1);
-}
-__device__ __forceinline__ int reduce9_row_slot() {
-  float p[9];
-#pragma unroll
-  for (int k = 0; k < 9; ++k) p[k] = (__lane_id() & 15) == 0 ? (float)(k + 1) : 0.f;
-  return (int)reduce9_row(p) - 1;
-}
-__device__ __forceinline__ int row_max_int(int v) {  // max over the lane's 16-lane row
-  for (int off = 8; off >= 1; off >>= 1) {
-    const int o = __shfl_xor(v, off, 64);
-    v = v > o ? v : o;
-  }
-  return v;
-}
-
-// Backward with sub-wave lists (gsplat_debug_set_raster_variant flag 2048): the wave's 16x8
-// strip is split into four 8x4 rectangles, one per 16-lane row (two vertically adjacent
-// pixels per lane), and each row walks its own culled list of the staged Gaussians -- a
-// Gaussian is visited only by the rows whose rectangle it can touch (exact min-sigma cull per
-// rectangle, and idx <= the rectangle's largest final_idx), so a wave iteration carries up to
-// four different Gaussians.  Per iteration each row reduce-scatters its nine partial sums
-// with row-local DPP and one atomic instruction adds all four rows' records.
-template <bool CHUNKED = false>
-__global__ __launch_bounds__(256) void raster_bwd3g_kernel(
+// ---------------------------------------------------------------- MFMA-reduced block backward
+// raster_bwd8_kernel's geometry and per-pixel arithmetic, with the per-Gaussian sums over the
+// block's 64 pixels done by the matrix cores instead of a cross-lane reduce-scatter.  Every
+// record moment is a pixel-feature-weighted sum of one of two per-pixel scalars,
+// w = vis * v_alpha and fac = alpha * T:
+//   sum w F(p) for F in {1, u, v, u^2, u v, v^2}    (u, v: the pixel's position in the block)
+//   sum fac v_c(p) for c in {r, g, b}
+// so for a group of 8 staged Gaussians they are ONE matrix product
+//   D[16 features x 16 columns] = A[16 x 64 pixels] . B[64 pixels x 16 columns],
+// A = the wave's pixel features (rows 0-5 geometric, 6-8 the upstream colour, constant per
+// wave: 16 registers), B = (w of the 8 Gaussians | fac of the 8 Gaussians): 16
+// v_mfma_f32_16x16x4_f32 (K = 4 pixels each; exact f32, a k-ordered fma chain).  Each lane
+// writes its pixel's w / fac into a per-wave LDS image laid out so that every MFMA's B operand
+// is 4 contiguous ds_read_b128 per lane (conflict-free); the 8 Gaussians' local moments are
+// re-centred on the Gaussian (d = xy - pixel: Sx = gx' S0 - Su, ...) in 16 lanes and added to
+// the records with 3 atomic instructions per group.  The VALU keeps only the per-pixel blend
+// arithmetic (~28 instructions per pixel-Gaussian pair), and the matrix pipe -- idle in every
+// other rasterizer kernel -- does the reduction (16 MFMAs = 512 cycles per group of 8, run by
+// the SIMD alongside other waves' VALU work).
+typedef float f4v __attribute__((ext_vector_type(4)));
+constexpr int BM_K = 264;   // LDS image: (pixel p, column j) at BM_K (p & 3) + BM_J j + (p >> 2)
+constexpr int BM_J = 20;    // (16-B aligned rows; ds_read_b128 over 16 lanes hits 64 banks)
+constexpr int BM_FLOATS = BM_K * 3 + BM_J * 15 + 16;  // 1108
+template <bool CHUNKED = false, bool DET = false, bool CNT = false>
+__global__ __launch_bounds__(256) void raster_bwdm_kernel(
     int tbx, int tby, int H, int W, const int *__restrict__ gids, const int2 *__restrict__ bins,
     const float2 *__restrict__ xys, const float *__restrict__ conics,
     const float *__restrict__ colors, const float *__restrict__ opacity,
@@ -1417,231 +1021,203 @@ __global__ __launch_bounds__(256) void raster_bwd3g_kernel(
     const float *__restrict__ v_out_alpha, float alpha_max, float *__restrict__ rec,
     int chunk = 0, const int *__restrict__ item_off = nullptr,
     const int *__restrict__ item_tile = nullptr, const int *__restrict__ ckpt_off = nullptr,
-    const float4 *__restrict__ ckpt = nullptr) {
-  constexpr int PXL = 2, COLS = 16;
-  typedef f2 PV;
+    const float4 *__restrict__ ckpt = nullptr, unsigned long long *__restrict__ det = nullptr) {
   int ctile = -1, cj = 0;
   if (CHUNKED) {
-    const int slot = wave_slot<PXL, COLS>();
+    const int slot = wave_slot<1, 8>();
     if (slot >= item_off[tbx * tby]) return;  // wave-uniform: past the last item
     ctile = item_tile[slot];
     cj = slot - item_off[ctile];
   }
-  const WaveRect R = wave_rect<PXL, COLS>(tbx, tby, H, W, ctile);
+  const WaveLog wlog;
+  const WaveRect R = wave_rect<1, 8>(tbx, tby, H, W, ctile);
   if (!R.live) return;  // wave-uniform
   __shared__ GStage lds[4][64];
-  __shared__ unsigned char lists[4][4][64];
+  __shared__ __attribute__((aligned(16))) float bmat[4][BM_FLOATS];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int grp = lane >> 4, m = lane & 15;
-  const int tile = R.tile;
-  const int c0 = (int)R.rx0, r0 = (int)R.ry0;
-  const int j = c0 + (grp & 1) * 8 + (m & 7);
-  const int i0 = r0 + (grp >> 1) * 4 + (m >> 3) * 2;
-  const float px = (float)j;
-  const float bg0 = background[0], bg1 = background[1], bg2 = background[2];
-  PV py, T, vr, vg, vb, q, Sb;
-  int binf[2];
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int i = i0 + k;
-    float Tf = 0.f, r = 0.f, g = 0.f, bl = 0.f, a = 0.f;
-    int bf = -1;
-    if (i < H && j < W) {
-      const int pix = i * W + j;
-      Tf = final_Ts[pix];
-      bf = final_idx[pix];
-      r = v_out[3 * pix];
-      g = v_out[3 * pix + 1];
-      bl = v_out[3 * pix + 2];
-      a = v_out_alpha ? v_out_alpha[pix] : 0.f;
-    }
-    const float qk = Tf * (a - (bg0 * r + bg1 * g + bg2 * bl));
-    if (k) {
-      py.y = (float)i; T.y = Tf; vr.y = r; vg.y = g; vb.y = bl; q.y = qk;
-    } else {
-      py.x = (float)i; T.x = Tf; vr.x = r; vg.x = g; vb.x = bl; q.x = qk;
-    }
-    binf[k] = bf;
+  const int tile = R.tile, j = R.j, i = R.i0;
+  const float px = (float)j, py = (float)i;
+  const float c0 = R.rx0, r0 = R.ry0;  // the block's origin: u = j - c0 = lane & 7, v = lane >> 3
+  float T = 0.f, vr = 0.f, vg = 0.f, vb = 0.f, q = 0.f, Sb = 0.f;
+  int bf = -1;
+  const bool inside = i < H && j < W;
+  if (inside) {
+    const int pix = i * W + j;
+    T = final_Ts[pix];
+    bf = final_idx[pix];
+    vr = v_out[3 * pix];
+    vg = v_out[3 * pix + 1];
+    vb = v_out[3 * pix + 2];
+    const float a = v_out_alpha ? v_out_alpha[pix] : 0.f;
+    q = T * (a - (background[0] * vr + background[1] * vg + background[2] * vb));
   }
-  Sb = PV(0.f);
   const int2 range = bins[tile];
   int lo = range.x, hi = range.y;
   if (CHUNKED) {
     const int len = range.y - range.x;
-    const int nch = len > chunk ? (len + chunk - 1) / chunk : 1;
-    if (nch > 1) {
+    const int m = len > chunk ? (len + chunk - 1) / chunk : 1;
+    if (m > 1) {
       lo = range.x + cj * chunk;
       hi = min(lo + chunk, range.y);
-      if (cj < nch - 1) {  // start from the checkpoint after this chunk
+      if (cj < m - 1 && inside) {
         const size_t cb = (size_t)ckpt_off[tile] * (GS_BLOCK * GS_BLOCK);
-        const int oy = (tile / tbx) * GS_BLOCK, ox = (tile % tbx) * GS_BLOCK;
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-          const int i = i0 + k;
-          if (i < H && j < W) {
-            const int lpix = (i - oy) * GS_BLOCK + (j - ox);
-            const float4 cj4 = ckpt[cb + (size_t)cj * (GS_BLOCK * GS_BLOCK) + lpix];
-            const float4 cf4 = ckpt[cb + (size_t)(nch - 1) * (GS_BLOCK * GS_BLOCK) + lpix];
-            const float vr_ = k ? vr.y : vr.x, vg_ = k ? vg.y : vg.x, vb_ = k ? vb.y : vb.x;
-            const float sb = (cf4.y - cj4.y) * vr_ + (cf4.z - cj4.z) * vg_ + (cf4.w - cj4.w) * vb_;
-            if (k) { T.y = cj4.x; Sb.y = sb; } else { T.x = cj4.x; Sb.x = sb; }
-          }
-        }
+        const int lpix = (i - (tile / tbx) * GS_BLOCK) * GS_BLOCK + (j - (tile % tbx) * GS_BLOCK);
+        const float4 c4 = ckpt[cb + (size_t)cj * (GS_BLOCK * GS_BLOCK) + lpix];
+        const float4 f4 = ckpt[cb + (size_t)(m - 1) * (GS_BLOCK * GS_BLOCK) + lpix];
+        T = c4.x;
+        Sb = (f4.y - c4.y) * vr + (f4.z - c4.z) * vg + (f4.w - c4.w) * vb;
       }
     }
   }
-  // per-row (8x4 rectangle) largest final_idx, and the rectangles (wave-uniform)
-  const int rmax = row_max_int(max(binf[0], binf[1]));
-  int gmax[4];
-  float gx0[4], gx1[4], gy0[4], gy1[4];
-  bool gok[4];
+  const int maxbin = wave_max_int(bf);
+  float *bm = bmat[wave];
+  // A operand of MFMA s (pixels 4s .. 4s + 3): lane l holds feature l & 15 of pixel 4s + (l >> 4)
+  // (the colour rows read the other lanes' upstream gradient through the LDS image)
+  bm[3 * lane] = vr;
+  bm[3 * lane + 1] = vg;
+  bm[3 * lane + 2] = vb;
+  wave_lds_sync();
+  const int feat = lane & 15, kq = lane >> 4;
+  float amat[16];
 #pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    gmax[g] = __builtin_amdgcn_readlane(rmax, 16 * g);
-    const int sx0 = c0 + (g & 1) * 8, sy0 = r0 + (g >> 1) * 4;
-    gok[g] = sx0 < W && sy0 < H && gmax[g] >= 0;
-    gx0[g] = (float)sx0;
-    gx1[g] = (float)min(sx0 + 7, W - 1);
-    gy0[g] = (float)sy0;
-    gy1[g] = (float)min(sy0 + 3, H - 1);
+  for (int s = 0; s < 16; ++s) {
+    const int p = 4 * s + kq;
+    const float u = (float)(p & 7), v = (float)(p >> 3);
+    float a = 0.f;
+    if (feat == 0) a = 1.f;
+    else if (feat == 1) a = u;
+    else if (feat == 2) a = v;
+    else if (feat == 3) a = u * u;
+    else if (feat == 4) a = u * v;
+    else if (feat == 5) a = v * v;
+    else if (feat < 9) a = bm[3 * p + feat - 6];
+    amat[s] = a;
   }
-  const int maxbin = max(max(gmax[0], gmax[1]), max(gmax[2], gmax[3]));
-  const int slot = reduce9_row_slot();
+  wave_lds_sync();
+  const int wbase = BM_K * (lane & 3) + (lane >> 2);     // this pixel's row in the image
+  const int rbase = BM_K * kq + BM_J * feat;             // this lane's B operand column
+  // epilogue roles: lanes 0-7 / 16-23 own Gaussian (lane & 7)'s geometric fields, lanes 24-31
+  // and 40-47 its colour fields
+  const int gc = lane & 7;
+  const bool geo0 = lane < 8, geo1 = lane >= 16 && lane < 24, colrg = lane >= 24 && lane < 32,
+             colb = lane >= 40 && lane < 48;
+  const float amax = __builtin_canonicalizef(alpha_max);
   const int last = min(maxbin, hi - 1);
   GStage *stage = lds[wave];
+  unsigned c_slots = 0, c_live = 0, c_valid = 0;  // (CNT only)
   for (int b = last; b >= lo; b -= 64) {
     const int idx = b - lane;
     GStage s;
-    bool kg[4] = {false, false, false, false};
-    if (idx >= lo) {
-      const int gid = gids[idx];
-      const float2 xy = xys[gid];
-      const float a = conics[3 * gid], bb = conics[3 * gid + 1], c = conics[3 * gid + 2];
-      const float o = opacity[gid];
-#pragma unroll
-      for (int g = 0; g < 4; ++g)
-        kg[g] = gok[g] && idx <= gmax[g] &&
-                touches_rect(xy.x, xy.y, a, bb, c, o, gx0[g], gx1[g], gy0[g], gy1[g]);
-      if (kg[0] || kg[1] || kg[2] || kg[3]) {
-        s.x = xy.x;
-        s.y = xy.y;
-        s.ha = 0.5f * a;
-        s.b = bb;
-        s.hc = 0.5f * c;
-        s.o = o;
-        s.r = colors[3 * gid];
-        s.g = colors[3 * gid + 1];
-        s.bl = colors[3 * gid + 2];
-        s.idx = idx;
-        s.id = gid;
-      }
-    }
-    const bool keep = kg[0] || kg[1] || kg[2] || kg[3];
+    const bool keep = idx >= lo && stage_gaussian<true>(idx, gids, xys, conics, colors, opacity,
+                                                        R.rx0, R.rx1, R.ry0, R.ry1, s);
     const unsigned long long kmask = __ballot(keep);
-    const int my_slot = (int)lanes_below(kmask);
-    if (keep) stage[my_slot] = s;
-    int ng[4];
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const unsigned long long gm = __ballot(kg[g]);
-      ng[g] = __popcll(gm);
-      if (kg[g]) lists[wave][g][lanes_below(gm)] = (unsigned char)my_slot;
-    }
+    if (keep) stage[lanes_below(kmask)] = s;
+    const int n = __popcll(kmask);
     wave_lds_sync();
-    const int nmax = max(max(ng[0], ng[1]), max(ng[2], ng[3]));
-    const int myn = grp == 0 ? ng[0] : grp == 1 ? ng[1] : grp == 2 ? ng[2] : ng[3];
-    for (int t = 0; t < nmax; ++t) {
-      const bool live = t < myn;
-      GStage G = stage[lists[wave][grp][live ? t : 0] & 63];
-      if (!live) G.r = G.g = G.bl = G.o = 0.f;  // keep T / Sb finite; no contribution
-      const float dx = G.x - px;
-      const float hA = G.ha * dx * dx, bdx = G.b * dx;
-      const PV dy = G.y - py;
-      const PV sig = gs_sigma2v<PV>(G.hc, bdx, hA, dy);
-      const PV vis = gs_vis2v<PV>(sig);
-      const PV ov = G.o * vis;
-      const PV al = {fminf(alpha_max, ov.x), fminf(alpha_max, ov.y)};
-      const bool v0 = live && G.idx <= binf[0] && sig.x >= 0.f && al.x >= ALPHA_MIN;
-      const bool v1 = live && G.idx <= binf[1] && sig.y >= 0.f && al.y >= ALPHA_MIN;
-      const PV am = {v0 ? al.x : 0.f, v1 ? al.y : 0.f};
-      const PV vm = {v0 ? vis.x : 0.f, v1 ? vis.y : 0.f};
-      const PV om = 1.f - am;
-      const PV ra = {__builtin_amdgcn_rcpf(om.x), __builtin_amdgcn_rcpf(om.y)};
-      T = T * ra;
-      const PV fac = am * T;
-      const PV gv = vfma(PV(G.r), vr, vfma(PV(G.g), vg, G.bl * vb));
-      const PV v_alpha = vfma(gv, T, ra * (q - Sb));
-      Sb = vfma(fac, gv, Sb);
-      const unsigned long long amask = __ballot(v0 || v1);
-      if (amask) {
-        const PV vva = vm * v_alpha;
-        const PV vs = vva * (-G.o);
-        const PV vsdy = vs * dy;
-        const float Vs = vs.x + vs.y, Vys = vsdy.x + vsdy.y;
-        const float dxV = dx * Vs;
-        float parts[9];
-        parts[0] = fmaf(2.f * G.ha, dxV, G.b * Vys);  // v_x
-        parts[1] = fmaf(G.b, dxV, 2.f * G.hc * Vys);  // v_y
-        parts[2] = dx * dxV;                          // 2 v_conic.a
-        parts[3] = dx * Vys;                          // 2 v_conic.b
-        const PV vsdy2 = vsdy * dy;
-        parts[4] = vsdy2.x + vsdy2.y;                 // 2 v_conic.c
-        const PV fr = fac * vr, fg = fac * vg, fb = fac * vb;
-        parts[5] = fr.x + fr.y;
-        parts[6] = fg.x + fg.y;
-        parts[7] = fb.x + fb.y;
-        parts[8] = vva.x + vva.y;
-        const float v = reduce9_row(parts);
-        const bool row_any = ((amask >> (16 * grp)) & 0xFFFFull) != 0;
-        if (row_any && slot >= 0) atomicAdd(rec + (size_t)G.id * REC + slot, v);
+    for (int t = 0; t < n; t += 8) {  // groups of up to 8 staged Gaussians
+      const int cnt = min(8, n - t);
+      unsigned long long anyv = 0;
+      for (int u = 0; u < cnt; u += 2) {  // two per step, as raster_bwd8_kernel
+        GStage G0 = stage[t + u], G1 = stage[min(t + u + 1, 63)];
+        const bool live1 = u + 1 < cnt;
+        if (!live1) G1.r = G1.g = G1.bl = G1.o = 0.f;
+        const float dx0 = G0.x - px, dy0 = G0.y - py, dx1 = G1.x - px, dy1 = G1.y - py;
+        const float sg0 = gs_sigma(G0.hc, G0.b * dx0, G0.ha * dx0 * dx0, dy0);
+        const float sg1 = gs_sigma(G1.hc, G1.b * dx1, G1.ha * dx1 * dx1, dy1);
+        const float vis0 = gs_vis(sg0), vis1 = gs_vis(sg1);
+        const float al0 = fminf(amax, G0.o * vis0), al1 = fminf(amax, G1.o * vis1);
+        const bool v0 = G0.idx <= bf && sg0 >= 0.f && al0 >= ALPHA_MIN;
+        const bool v1 = live1 && G1.idx <= bf && sg1 >= 0.f && al1 >= ALPHA_MIN;
+        anyv |= __builtin_amdgcn_ballot_w64(v0 || v1);
+        if constexpr (CNT) {
+          c_slots += (live1 ? 2 : 1) * 64;
+          c_live += (G0.idx <= bf ? 1u : 0u) + (live1 && G1.idx <= bf ? 1u : 0u);
+          c_valid += (v0 ? 1u : 0u) + (v1 ? 1u : 0u);
+        }
+        const float am0 = v0 ? al0 : 0.f, am1 = v1 ? al1 : 0.f;
+        const float ra0 = __builtin_amdgcn_rcpf(1.f - am0);
+        T = T * ra0;
+        const float fac0 = am0 * T;
+        const float gv0 = fmaf(G0.r, vr, fmaf(G0.g, vg, G0.bl * vb));
+        const float va0 = fmaf(gv0, T, ra0 * (q - Sb));
+        Sb = fmaf(fac0, gv0, Sb);
+        const float ra1 = __builtin_amdgcn_rcpf(1.f - am1);
+        T = T * ra1;
+        const float fac1 = am1 * T;
+        const float gv1 = fmaf(G1.r, vr, fmaf(G1.g, vg, G1.bl * vb));
+        const float va1 = fmaf(gv1, T, ra1 * (q - Sb));
+        Sb = fmaf(fac1, gv1, Sb);
+        bm[wbase + BM_J * u] = (v0 ? vis0 : 0.f) * va0;
+        bm[wbase + BM_J * (8 + u)] = fac0;
+        bm[wbase + BM_J * (u + 1)] = (v1 ? vis1 : 0.f) * va1;  // (u + 1 <= 7: cnt <= 8)
+        bm[wbase + BM_J * (9 + u)] = fac1;
       }
-    }
-    wave_lds_sync();
-  }
-}
-
-// Tile processing order (one workgroup): tiles by decreasing list length, ties by tile id.
-// The backward deals consecutive work slots to CUs round-robin, so each SIMD receives one tile
-// from every cost tier and the per-SIMD sums even out (longest-processing-time-first dealing).
-// Keys (log2-spaced length bucket, tile) are sorted by an LDS bitonic sort; frames with more
-// than 16,384 tiles keep the identity order.
-constexpr int ORDER_MAX = 16384;
-__global__ __launch_bounds__(1024) void tile_order_kernel(int T, const int2 *__restrict__ bins,
-                                                          int *__restrict__ order) {
-  __shared__ uint32_t key[ORDER_MAX];
-  const int tid = threadIdx.x;
-  if (T > ORDER_MAX) {
-    for (int t = tid; t < T; t += 1024) order[t] = t;
-    return;
-  }
-  int n = 1;
-  while (n < T) n <<= 1;
-  for (int t = tid; t < n; t += 1024) {
-    uint32_t k = 0xFFFFFFFFu;  // padding sorts last
-    if (t < T) {
-      const int2 r = bins[t];
-      const int len = max(r.y - r.x, 0);
-      const uint32_t b = min(1023u, (uint32_t)(log2f((float)len + 1.f) * 64.f));
-      k = ((1023u - b) << 18) | (uint32_t)t;  // descending length, ascending tile
-    }
-    key[t] = k;
-  }
-  __syncthreads();
-  for (int size = 2; size <= n; size <<= 1) {
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int i = tid; i < (n >> 1); i += 1024) {
-        const int lo = 2 * i - (i & (stride - 1)), hi = lo + stride;
-        const bool up = (lo & size) == 0;
-        const uint32_t a = key[lo], b = key[hi];
-        if ((a > b) == up) {
-          key[lo] = b;
-          key[hi] = a;
+      if (!anyv) continue;  // (SGPR test) no pixel of the block composites this group
+      wave_lds_sync();
+      // D = A . B over the 64 pixels: 16 MFMAs, two accumulators (40-cycle dependency)
+      float bv[16];
+#pragma unroll
+      for (int k4 = 0; k4 < 4; ++k4) {
+        const float4 x = *reinterpret_cast<const float4 *>(bm + rbase + 4 * k4);
+        bv[4 * k4] = x.x;
+        bv[4 * k4 + 1] = x.y;
+        bv[4 * k4 + 2] = x.z;
+        bv[4 * k4 + 3] = x.w;
+      }
+      f4v acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s2 = 0; s2 < 16; s2 += 2) {
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(amat[s2], bv[s2], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(amat[s2 + 1], bv[s2 + 1], acc1, 0, 0, 0);
+      }
+      const f4v acc = acc0 + acc1;  // lane l: D[4 (l >> 4) + r][l & 15]
+      // local moments of Gaussian gc: S0 Su Sv Suu in lane gc (column gc, rows 0-3), Suv Svv
+      // in lane gc + 16 (rows 4, 5); exchange so that both lanes hold all six
+      const float x0 = __shfl_xor(acc[0], 16), x1 = __shfl_xor(acc[1], 16),
+                  x2 = __shfl_xor(acc[2], 16), x3 = __shfl_xor(acc[3], 16);
+      const bool lo16 = lane < 16;
+      const float S0 = lo16 ? acc[0] : x0, Su = lo16 ? acc[1] : x1, Sv = lo16 ? acc[2] : x2,
+                  Suu = lo16 ? acc[3] : x3, Suv = lo16 ? x0 : acc[0], Svv = lo16 ? x1 : acc[1];
+      const GStage &Gc = stage[t + gc];
+      const float gx = Gc.x - c0, gy = Gc.y - r0;  // the Gaussian's mean in block coordinates
+      const int gid = Gc.id;
+      const float Sx = fmaf(gx, S0, -Su), Sy = fmaf(gy, S0, -Sv);
+      float v1 = 0.f, v2 = 0.f, v3 = 0.f;
+      int f1 = 0, f2 = 0, f3 = 0;
+      if (geo0) {
+        v1 = Sx; f1 = REC_SX;
+        v2 = Sy; f2 = REC_SY;
+        v3 = fmaf(gx, Sx - Su, Suu); f3 = REC_SXX;           // gx^2 S0 - 2 gx Su + Suu
+      } else if (geo1) {
+        v1 = fmaf(gx, Sy, fmaf(-gy, Su, Suv)); f1 = REC_SXY;  // gx gy S0 - gx Sv - gy Su + Suv
+        v2 = fmaf(gy, Sy - Sv, Svv); f2 = REC_SYY;           // gy^2 S0 - 2 gy Sv + Svv
+        v3 = S0; f3 = REC_S0;
+      } else if (colrg) {
+        v1 = acc[2]; f1 = REC_R;  // row 6 (column 8 + gc: fac)
+        v2 = acc[3]; f2 = REC_G;  // row 7
+      } else if (colb) {
+        v1 = acc[0]; f1 = REC_B;  // row 8
+      }
+      const bool mine = gc < cnt && (geo0 || geo1 || colrg || colb);
+      if (mine) {
+        if constexpr (DET) {
+          unsigned long long *d = det + (size_t)gid * REC_FIELDS * DET_LIMBS;
+          det_add(d + f1 * DET_LIMBS, v1);
+          if (!colb) det_add(d + f2 * DET_LIMBS, v2);
+          if (geo0 || geo1) det_add(d + f3 * DET_LIMBS, v3);
+        } else {
+          float *r = rec + (uint32_t)(gid * REC);
+          atomicAdd(r + f1, v1);
+          if (!colb) atomicAdd(r + f2, v2);
+          if (geo0 || geo1) atomicAdd(r + f3, v3);
         }
       }
-      __syncthreads();
+      wave_lds_sync();  // the next group's writes reuse the image
     }
+    wave_lds_sync();
   }
-  for (int t = tid; t < T; t += 1024) order[t] = (int)(key[t] & 0x3FFFFu);
+  if constexpr (CNT) pair_count_flush(0, c_slots, c_live, c_valid);
+  wlog.done(tile);
 }
 
 // List-split plan (one workgroup): per tile, the number of backward items (chunks of the
@@ -1695,17 +1271,16 @@ __global__ __launch_bounds__(1024) void chunk_plan_kernel(int T, const int2 *__r
   }
 }
 
-// Gradient records -> gsplat's v_xy [N,2], v_conic [N,3], v_colors [N,3], v_opacity [N].
-// Scale of a record's conic.y sum into gsplat's v_conic.y: the records hold the gradient of
-// each conic entry in gsplat's halved convention times 1/s; without the CONIC_HALF quirk
-// v_conic.y is d loss / d conic.y, twice that.
-static inline float conic_y_scale(float s) {
-  return (g_quirks & GSPLAT_QUIRK_CONIC_HALF) ? s : 2.f * s;
-}
+// Gradient records (moments, common.h record_grads) -> gsplat's v_xy [N,2], v_conic [N,3],
+// v_colors [N,3], v_opacity [N].  A Gaussian no pixel was composited at has an all-zero
+// record and gets exact +0 gradients (gsplat's untouched zero-initialised sums), whatever
+// its conic holds.
+static inline bool conic_y_full() { return !(g_quirks & GSPLAT_QUIRK_CONIC_HALF); }
 
 __global__ __launch_bounds__(256) void split_grads_kernel(int n, const float4 *__restrict__ rec,
-                                                          float conic_scale, float conic_scale_b,
-                                                          float *__restrict__ v_xy,
+                                                          const float *__restrict__ conics,
+                                                          const float *__restrict__ opacity,
+                                                          bool cy_full, float *__restrict__ v_xy,
                                                           float *__restrict__ v_conic,
                                                           float *__restrict__ v_rgb,
                                                           float *__restrict__ v_opacity) {
@@ -1713,15 +1288,21 @@ __global__ __launch_bounds__(256) void split_grads_kernel(int n, const float4 *_
   if (g >= n) return;
   const float4 r0 = rec[(size_t)g * (REC / 4)], r1 = rec[(size_t)g * (REC / 4) + 1],
                r2 = rec[(size_t)g * (REC / 4) + 2];
-  v_xy[2 * g] = r0.x;
-  v_xy[2 * g + 1] = r0.y;
-  v_conic[3 * g] = conic_scale * r0.z;
-  v_conic[3 * g + 1] = conic_scale_b * r0.w;
-  v_conic[3 * g + 2] = conic_scale * r1.x;
-  v_rgb[3 * g] = r1.y;
-  v_rgb[3 * g + 1] = r1.z;
-  v_rgb[3 * g + 2] = r1.w;
-  v_opacity[g] = r2.x;
+  const float r[9] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x};
+  bool touched = false;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) touched = touched || r[k] != 0.f;
+  RasterGrads d{};
+  if (touched)
+    d = record_grads(r, conics[3 * g], conics[3 * g + 1], conics[3 * g + 2], opacity[g], cy_full);
+  v_xy[2 * g] = d.vxy[0];
+  v_xy[2 * g + 1] = d.vxy[1];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    v_conic[3 * g + k] = d.vconic[k];
+    v_rgb[3 * g + k] = d.vrgb[k];
+  }
+  v_opacity[g] = d.vopacity;
 }
 
 // ---------------------------------------------------------------- N-channel variants
@@ -1812,8 +1393,10 @@ __global__ __launch_bounds__(256) void raster_bwdn_kernel(
     const float *__restrict__ opacity, const float *__restrict__ background,
     const float *__restrict__ final_Ts, const int *__restrict__ final_idx,
     const float *__restrict__ v_out, const float *__restrict__ v_out_alpha, float alpha_max,
-    float *__restrict__ v_xy, float *__restrict__ v_conic, float *__restrict__ v_colors,
-    float *__restrict__ v_opacity) {
+    float conic_b_scale, float *__restrict__ v_xy, float *__restrict__ v_conic,
+    float *__restrict__ v_colors, float *__restrict__ v_opacity) {
+  // conic_b_scale: gsplat's v_conic.y = 1/2 v_sigma dx dy under GSPLAT_QUIRK_CONIC_HALF,
+  // d loss / d conic.y = v_sigma dx dy without it (what record_grads() gives the C = 3 path)
   __shared__ GN lds[256];
   const int tile = blockIdx.x;
   const int lane = threadIdx.x & 63;
@@ -1890,7 +1473,7 @@ __global__ __launch_bounds__(256) void raster_bwdn_kernel(
         v_alpha += -Tf * ra * bgdot;
         const float v_sigma = -G.o * vis * v_alpha;
         s_a = 0.5f * v_sigma * dx * dx;
-        s_b = 0.5f * v_sigma * dx * dy;
+        s_b = conic_b_scale * v_sigma * dx * dy;
         s_c = 0.5f * v_sigma * dy * dy;
         s_x = v_sigma * (G.a * dx + G.b * dy);
         s_y = v_sigma * (G.b * dx + G.c * dy);
@@ -1968,8 +1551,8 @@ static ChunkWs carve_chunk_ws(void *base, long long T, long long I, int chunk) {
   w.bytes = off;
   return w;
 }
-static bool default_variants() {  // (flag 4096, the tile-wave backward, keeps the layout)
-  return g_fwd_pxl == FWD_PXL && g_bwd_pxl == BWD_PXL && (g_bwd_flags & ~4096) == 0;
+static bool default_variants() {
+  return g_fwd_pxl == FWD_PXL && g_bwd_pxl == BWD_PXL && g_bwd_flags == 0;
 }
 
 extern "C" int gsplat_rasterize_chunk_size(int tile_bounds_x, int tile_bounds_y,
@@ -1999,6 +1582,30 @@ extern "C" int gsplat_debug_set_chunk(int chunk) {
   return 0;
 }
 
+static bool bad_frame(int tbx, int tby, int H, int W) {
+  return tbx <= 0 || tby <= 0 || H <= 0 || W <= 0 || (long long)tbx * GS_BLOCK < W ||
+         (long long)tby * GS_BLOCK < H;
+}
+
+// The shipped C = 3 forward: 8x8 blocks, two Gaussians per iteration (CNT: the lane-slot
+// counting instantiation, same arithmetic), optional checkpoints (chunk > 0) and record clear.
+template <bool DEPTH, bool CKPT>
+static void launch_fwd(hipStream_t st, int tbx, int tby, int H, int W, const int32_t *gids,
+                       const int32_t *bins, const float *xys, const float *conics,
+                       const float *colors, const float *opacity, const float *background,
+                       float *out_img, float *final_Ts, int32_t *final_idx, const float *depths,
+                       float *out_depth, int chunk, const int *ckpt_off, float4 *ckpt,
+                       float4 *zero, long long zn, const int32_t *zero_radii) {
+  const unsigned grid = cdiv((long long)tbx * tby, (tiles_per_block<1, 8>()));
+#define FWDK(CNT)                                                                          \
+  hipLaunchKernelGGL((raster_fwd3u_kernel<1, 8, DEPTH, CKPT, CNT>), dim3(grid), dim3(256), 0, st, \
+                     tbx, tby, H, W, gids, (const int2 *)bins, (const float2 *)xys, conics,      \
+                     colors, opacity, background, out_img, final_Ts, final_idx, depths,          \
+                     out_depth, chunk, ckpt_off, ckpt, zero, zn, zero_radii)
+  if (!DEPTH && g_pair_count_on) FWDK(true); else FWDK(false);
+#undef FWDK
+}
+
 extern "C" int gsplat_rasterize_forward(int tile_bounds_x, int tile_bounds_y, int img_height,
                                         int img_width, int channels,
                                         const int32_t *gaussian_ids_sorted,
@@ -2008,45 +1615,18 @@ extern "C" int gsplat_rasterize_forward(int tile_bounds_x, int tile_bounds_y, in
                                         float *out_img, float *final_Ts, int32_t *final_idx,
                                         void *stream) {
   hipStream_t st = (hipStream_t)stream;
-  if (tile_bounds_x <= 0 || tile_bounds_y <= 0 || img_height <= 0 || img_width <= 0 ||
-      channels < 1 || channels > 64 ||
-      (long long)tile_bounds_x * GS_BLOCK < img_width ||
-      (long long)tile_bounds_y * GS_BLOCK < img_height) {
+  if (bad_frame(tile_bounds_x, tile_bounds_y, img_height, img_width) || channels < 1 ||
+      channels > 64) {
     set_error("rasterize_forward: bad sizes (tiles=%dx%d H=%d W=%d C=%d)", tile_bounds_x,
               tile_bounds_y, img_height, img_width, channels);
     return 1;
   }
   const int T = tile_bounds_x * tile_bounds_y;
   if (channels == 3) {
-#define FWD3(P)                                                                            \
-  hipLaunchKernelGGL(raster_fwd3_kernel<P>, dim3(cdiv(T, P)), dim3(256), 0, st, tile_bounds_x, \
-                     tile_bounds_y, img_height, img_width, gaussian_ids_sorted,                \
-                     (const int2 *)tile_bins, (const float2 *)xys, conics, colors, opacity,    \
-                     background, out_img, final_Ts, final_idx)
-#define FWD3P(NP)                                                                          \
-  hipLaunchKernelGGL(raster_fwd3p_kernel<NP>, dim3(cdiv(T, 2 * NP)), dim3(256), 0, st,          \
-                     tile_bounds_x, tile_bounds_y, img_height, img_width, gaussian_ids_sorted,  \
-                     (const int2 *)tile_bins, (const float2 *)xys, conics, colors, opacity,     \
-                     background, out_img, final_Ts, final_idx)
-#define FWD3U(P, C)                                                                        \
-  hipLaunchKernelGGL((raster_fwd3u_kernel<P, C>), dim3(cdiv(T, (tiles_per_block<P, C>()))),    \
-                     dim3(256), 0, st, tile_bounds_x, tile_bounds_y, img_height, img_width,     \
-                     gaussian_ids_sorted, (const int2 *)tile_bins, (const float2 *)xys, conics, \
-                     colors, opacity, background, out_img, final_Ts, final_idx)
-    // flags: 4 scalar one-Gaussian-per-iteration kernel, 8 packed float2 kernel, 16 full-width
-    // (16-column) rectangles; default: two Gaussians per iteration on 8-column rectangles.
-    const bool scalar = g_bwd_flags & 4, packed = g_bwd_flags & 8, wide = g_bwd_flags & 16;
-    if (g_fwd_pxl == 4) {
-      if (scalar) FWD3(4); else if (packed) FWD3P(2); else FWD3U(4, 16);
-    } else if (g_fwd_pxl == 2) {
-      if (scalar) FWD3(2); else if (packed) FWD3P(1); else if (wide) FWD3U(2, 16); else FWD3U(2, 8);
-    } else {
-      if (scalar) FWD3(1); else if (wide) FWD3U(1, 16);
-      else FWD3U(1, 8);
-    }
-#undef FWD3U
-#undef FWD3
-#undef FWD3P
+    launch_fwd<false, false>(st, tile_bounds_x, tile_bounds_y, img_height, img_width,
+                             gaussian_ids_sorted, tile_bins, xys, conics, colors, opacity,
+                             background, out_img, final_Ts, final_idx, nullptr, nullptr, 0,
+                             nullptr, nullptr, nullptr, 0, nullptr);
   } else {
     ND_DISPATCH(raster_fwdn_kernel, tile_bounds_x, tile_bounds_y, img_height, img_width,
                 channels, gaussian_ids_sorted, (const int2 *)tile_bins, (const float2 *)xys,
@@ -2065,48 +1645,33 @@ extern "C" int gsplat_rasterize_forward_rgbd(int tile_bounds_x, int tile_bounds_
                                              float *out_depth, float *final_Ts,
                                              int32_t *final_idx, void *stream) {
   hipStream_t st = (hipStream_t)stream;
-  if (tile_bounds_x <= 0 || tile_bounds_y <= 0 || img_height <= 0 || img_width <= 0 ||
-      (long long)tile_bounds_x * GS_BLOCK < img_width ||
-      (long long)tile_bounds_y * GS_BLOCK < img_height || !depths || !out_depth) {
+  if (bad_frame(tile_bounds_x, tile_bounds_y, img_height, img_width) || !depths || !out_depth) {
     set_error("rasterize_forward_rgbd: bad sizes or NULL depth buffers (tiles=%dx%d H=%d W=%d)",
               tile_bounds_x, tile_bounds_y, img_height, img_width);
     return 1;
   }
-  const int T = tile_bounds_x * tile_bounds_y;
-  hipLaunchKernelGGL((raster_fwd3u_kernel<1, 8, true>), dim3(cdiv(T, (tiles_per_block<1, 8>()))),
-                     dim3(256), 0, st, tile_bounds_x, tile_bounds_y, img_height, img_width,
-                     gaussian_ids_sorted, (const int2 *)tile_bins, (const float2 *)xys, conics,
-                     colors, opacity, background, out_img, final_Ts, final_idx, depths,
-                     out_depth);
+  launch_fwd<true, false>(st, tile_bounds_x, tile_bounds_y, img_height, img_width,
+                          gaussian_ids_sorted, tile_bins, xys, conics, colors, opacity,
+                          background, out_img, final_Ts, final_idx, depths, out_depth, 0, nullptr,
+                          nullptr, nullptr, 0, nullptr);
   return check_launch("rasterize_forward_rgbd");
 }
 
+// Measurement knob: bwd_pxl picks the backward geometry (BWD_PXL above); bits 20-27 of flags
+// the XCD chunk of the blend kernels' block order (0 the default K = 8, 255 dispatch order).
 extern "C" int gsplat_debug_set_raster_variant(int fwd_pxl, int bwd_pxl, int bwd_flags) {
-  auto ok = [](int p) { return p == 1 || p == 2 || p == 4; };
-  if (!ok(fwd_pxl) || !ok(bwd_pxl)) {
-    set_error("debug_set_raster_variant: pixels per lane must be 1, 2 or 4");
+  if (fwd_pxl != 1 || bwd_pxl < 1 || bwd_pxl > 3 || (bwd_flags & ~(0xff << 20))) {
+    set_error("debug_set_raster_variant: fwd_pxl must be 1, bwd_pxl 1 (8x8 blocks) or 2 "
+              "(16x8 strips), flags only the XCD chunk (bits 20-27)");
     return 1;
   }
   g_fwd_pxl = fwd_pxl;
   g_bwd_pxl = bwd_pxl;
-  g_bwd_flags = bwd_flags & ~(1024 | (0xff << 20));
+  g_bwd_flags = bwd_flags;
   const int chunk = (bwd_flags >> 20) & 0xff;
-  const int remap = (bwd_flags & 1024) ? -1 : chunk == 0xff ? 0 : chunk ? chunk : XCD_CHUNK;
+  const int remap = chunk == 0xff ? 0 : chunk ? chunk : XCD_CHUNK;
   if (hipMemcpyToSymbol(HIP_SYMBOL(g_xcd_remap), &remap, sizeof(int)) != hipSuccess) {
     set_error("debug_set_raster_variant: hipMemcpyToSymbol failed");
-    return 1;
-  }
-  return 0;
-}
-
-extern "C" int gsplat_debug_set_tile_swizzle(int gw, int gh) {
-  if (gw < 1 || gh < 1 || gw > 64 || gh > 64) {
-    set_error("debug_set_tile_swizzle: group sides must be in 1..64");
-    return 1;
-  }
-  if (hipMemcpyToSymbol(HIP_SYMBOL(g_tile_gw), &gw, sizeof(int)) != hipSuccess ||
-      hipMemcpyToSymbol(HIP_SYMBOL(g_tile_gh), &gh, sizeof(int)) != hipSuccess) {
-    set_error("debug_set_tile_swizzle: hipMemcpyToSymbol failed");
     return 1;
   }
   return 0;
@@ -2139,18 +1704,109 @@ extern "C" int gsplat_debug_pair_count(void *buffer) {
   return 0;
 }
 
-// The shipped 16x8-strip backward in deterministic mode (integer accumulators in det).
-static void launch_bwd_det(hipStream_t st, int tbx, int tby, int H, int W, const int32_t *gids,
-                           const int32_t *bins, const float *xys, const float *conics,
-                           const float *colors, const float *opacity, const float *background,
-                           const float *final_Ts, const int32_t *final_idx,
-                           const float *v_output, const float *v_output_alpha, float alpha_max,
-                           float *rec, unsigned long long *det) {
-  hipLaunchKernelGGL((raster_bwd3p_kernel<1, true, 16, false, f2, true>),
-                     dim3(cdiv((long long)tbx * tby, (tiles_per_block<2, 16>()))), dim3(256), 0,
-                     st, tbx, tby, H, W, gids, (const int2 *)bins, (const float2 *)xys, conics,
-                     colors, opacity, background, final_Ts, final_idx, v_output, v_output_alpha,
-                     alpha_max, rec, false, 0, nullptr, nullptr, nullptr, nullptr, det);
+// The C = 3 backward into the records `rec` (which the caller cleared), with the list split
+// when w != NULL, the integer accumulators when det != NULL (then det_finish_kernel writes the
+// records), the lane-slot counting instantiation when the pair-count hook is on.
+static void launch_bwd(hipStream_t st, int tbx, int tby, int H, int W, int n,
+                       const int32_t *gids, const int32_t *bins, const float *xys,
+                       const float *conics, const float *colors, const float *opacity,
+                       const float *background, const float *final_Ts, const int32_t *final_idx,
+                       const float *v_output, const float *v_output_alpha, float alpha_max,
+                       float *rec, int chunk, const ChunkWs *w, unsigned long long *det) {
+  const long long slots = w ? w->items_bound : (long long)tbx * tby;
+  const int *io = w ? w->item_off : nullptr, *it = w ? w->item_tile : nullptr,
+            *co = w ? w->ckpt_off : nullptr;
+  const float4 *ck = w ? w->ckpt : nullptr;
+  const bool cnt = g_pair_count_on && !det;
+  if (g_bwd_pxl == 3) {
+    const unsigned grid = cdiv(slots, (tiles_per_block<1, 8>()));
+#define BWDM(CH, DET, CNT)                                                                 \
+  hipLaunchKernelGGL((raster_bwdm_kernel<CH, DET, CNT>), dim3(grid), dim3(256), 0, st, tbx, tby, \
+                     H, W, gids, (const int2 *)bins, (const float2 *)xys, conics, colors,       \
+                     opacity, background, final_Ts, final_idx, v_output, v_output_alpha,        \
+                     alpha_max, rec, chunk, io, it, co, ck, det)
+    if (w) {
+      if (det) BWDM(true, true, false); else if (cnt) BWDM(true, false, true);
+      else BWDM(true, false, false);
+    } else {
+      if (det) BWDM(false, true, false); else if (cnt) BWDM(false, false, true);
+      else BWDM(false, false, false);
+    }
+#undef BWDM
+  } else if (g_bwd_pxl == 1) {
+    const unsigned grid = cdiv(slots, (tiles_per_block<1, 8>()));
+#define BWD8(CH, DET, CNT)                                                                 \
+  hipLaunchKernelGGL((raster_bwd8_kernel<CH, DET, CNT>), dim3(grid), dim3(256), 0, st, tbx, tby, \
+                     H, W, gids, (const int2 *)bins, (const float2 *)xys, conics, colors,       \
+                     opacity, background, final_Ts, final_idx, v_output, v_output_alpha,        \
+                     alpha_max, rec, chunk, io, it, co, ck, det)
+    if (w) {
+      if (det) BWD8(true, true, false); else if (cnt) BWD8(true, false, true);
+      else BWD8(true, false, false);
+    } else {
+      if (det) BWD8(false, true, false); else if (cnt) BWD8(false, false, true);
+      else BWD8(false, false, false);
+    }
+#undef BWD8
+  } else {
+    const unsigned grid = cdiv(slots, (tiles_per_block<2, 16>()));
+#define BWDS(CH, DET, CNT)                                                                 \
+  hipLaunchKernelGGL((raster_bwd3p_kernel<1, true, 16, CH, f2, DET, CNT>), dim3(grid), dim3(256), \
+                     0, st, tbx, tby, H, W, gids, (const int2 *)bins, (const float2 *)xys,      \
+                     conics, colors, opacity, background, final_Ts, final_idx, v_output,        \
+                     v_output_alpha, alpha_max, rec, false, chunk, io, it, co, ck, det)
+    if (w) {
+      if (det) BWDS(true, true, false); else if (cnt) BWDS(true, false, true);
+      else BWDS(true, false, false);
+    } else {
+      if (det) BWDS(false, true, false); else if (cnt) BWDS(false, false, true);
+      else BWDS(false, false, false);
+    }
+#undef BWDS
+  }
+  if (det)
+    hipLaunchKernelGGL(det_finish_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, n, det, rec);
+}
+
+// Validates, leases the deterministic accumulators if on, and runs launch_bwd.
+static int backward_into_records(const char *who, hipStream_t st, int tbx, int tby, int H,
+                                 int W, int n, const int32_t *gids, const int32_t *bins,
+                                 const float *xys, const float *conics, const float *colors,
+                                 const float *opacity, const float *background,
+                                 const float *final_Ts, const int32_t *final_idx,
+                                 const float *v_output, const float *v_output_alpha,
+                                 float alpha_max, float *rec, int64_t num_intersects, int chunk,
+                                 const void *checkpoints, size_t checkpoint_bytes) {
+  ChunkWs w{};
+  if (chunk > 0) {
+    w = carve_chunk_ws(const_cast<void *>(checkpoints), (long long)tbx * tby, num_intersects,
+                       chunk);
+    if (!checkpoints || checkpoint_bytes < w.bytes) {
+      set_error("%s: checkpoint buffer %zu < %zu bytes", who, checkpoint_bytes, w.bytes);
+      return 1;
+    }
+  }
+  if (g_det) {
+    DetLease lease(n, st);
+    if (!lease.buf) return check_launch(who);
+    launch_bwd(st, tbx, tby, H, W, n, gids, bins, xys, conics, colors, opacity, background,
+               final_Ts, final_idx, v_output, v_output_alpha, alpha_max, rec, chunk,
+               chunk > 0 ? &w : nullptr, lease.buf);
+    lease.finish();
+  } else {
+    launch_bwd(st, tbx, tby, H, W, n, gids, bins, xys, conics, colors, opacity, background,
+               final_Ts, final_idx, v_output, v_output_alpha, alpha_max, rec, chunk,
+               chunk > 0 ? &w : nullptr, nullptr);
+  }
+  return 0;
+}
+
+static void launch_split(hipStream_t st, int n, const float *rec, const float *conics,
+                         const float *opacity, float *v_xy, float *v_conic, float *v_colors,
+                         float *v_opacity) {
+  hipLaunchKernelGGL(split_grads_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, n,
+                     (const float4 *)rec, conics, opacity, conic_y_full(), v_xy, v_conic,
+                     v_colors, v_opacity);
 }
 
 extern "C" size_t gsplat_rasterize_backward_workspace_size(int num_points, int channels) {
@@ -2169,10 +1825,8 @@ extern "C" int gsplat_rasterize_backward(int tile_bounds_x, int tile_bounds_y, i
                                          float *v_colors, float *v_opacity, void *workspace,
                                          size_t workspace_bytes, void *stream) {
   hipStream_t st = (hipStream_t)stream;
-  if (tile_bounds_x <= 0 || tile_bounds_y <= 0 || img_height <= 0 || img_width <= 0 ||
-      channels < 1 || channels > 64 || num_points < 0 || num_points >= MAX_BWD_POINTS ||
-      (long long)tile_bounds_x * GS_BLOCK < img_width ||
-      (long long)tile_bounds_y * GS_BLOCK < img_height) {
+  if (bad_frame(tile_bounds_x, tile_bounds_y, img_height, img_width) || channels < 1 ||
+      channels > 64 || num_points < 0 || num_points >= MAX_BWD_POINTS) {
     set_error("rasterize_backward: bad sizes (tiles=%dx%d H=%d W=%d C=%d N=%d)", tile_bounds_x,
               tile_bounds_y, img_height, img_width, channels, num_points);
     return 1;
@@ -2187,101 +1841,12 @@ extern "C" int gsplat_rasterize_backward(int tile_bounds_x, int tile_bounds_y, i
     if (num_points == 0) return check_launch("rasterize_backward");
     float *rec = (float *)workspace;
     note(hipMemsetAsync(rec, 0, need, st), "hipMemsetAsync");
-#define BWD3(P, A)                                                                         \
-  hipLaunchKernelGGL((raster_bwd3_kernel<P, A>), dim3(cdiv(T, P)), dim3(256), 0, st,          \
-                     tile_bounds_x, tile_bounds_y, img_height, img_width, gaussian_ids_sorted,  \
-                     (const int2 *)tile_bins, (const float2 *)xys, conics, colors, opacity,     \
-                     background, final_Ts, final_idx, v_output, v_output_alpha, alpha_max, rec)
-#define BWD3P(NP, A, C)                                                                    \
-  hipLaunchKernelGGL((raster_bwd3p_kernel<NP, A, C>),                                       \
-                     dim3(cdiv(T, (tiles_per_block<2 * NP, C>()))), dim3(256), 0, st,         \
-                     tile_bounds_x, tile_bounds_y, img_height, img_width, gaussian_ids_sorted,  \
-                     (const int2 *)tile_bins, (const float2 *)xys, conics, colors, opacity,     \
-                     background, final_Ts, final_idx, v_output, v_output_alpha, alpha_max, rec, \
-                     (g_bwd_flags & 64) != 0)
-    const bool atomics = !(g_bwd_flags & 1);
-    const bool packed = g_bwd_pxl >= 2 && !(g_bwd_flags & 2);
-    const bool narrow = g_bwd_flags & 32;  // 8-column wave rectangles
-    if (g_det) {
-      if (!default_variants() || (g_bwd_flags & 4096)) {
-        set_error("rasterize_backward: deterministic mode needs the default raster variant");
-        return 1;
-      }
-      unsigned long long *det = det_buffer(num_points, st);
-      if (!det) return check_launch("rasterize_backward");
-      launch_bwd_det(st, tile_bounds_x, tile_bounds_y, img_height, img_width, gaussian_ids_sorted,
-                     tile_bins, xys, conics, colors, opacity, background, final_Ts, final_idx,
-                     v_output, v_output_alpha, alpha_max, rec, det);
-      hipLaunchKernelGGL(det_finish_kernel, dim3(cdiv(num_points, 256)), dim3(256), 0, st,
-                         num_points, det, rec);
-    } else if (packed) {
-      if (g_bwd_pxl == 4) {
-        if (atomics) BWD3P(2, true, 16); else BWD3P(2, false, 16);  // 16x16: one wave
-      } else {
-        if (narrow) { if (atomics) BWD3P(1, true, 8); else BWD3P(1, false, 8); }
-        else if (atomics && (g_bwd_flags & 2048)) {  // sub-wave lists (8x4 rectangles per row)
-          hipLaunchKernelGGL((raster_bwd3g_kernel<false>),
-                             dim3(cdiv(T, (tiles_per_block<2, 16>()))), dim3(256), 0, st,
-                             tile_bounds_x, tile_bounds_y, img_height, img_width,
-                             gaussian_ids_sorted, (const int2 *)tile_bins, (const float2 *)xys,
-                             conics, colors, opacity, background, final_Ts, final_idx, v_output,
-                             v_output_alpha, alpha_max, rec);
-        }
-        else if (atomics && (g_bwd_flags & 512)) {  // ablation: scalar pixel pairs
-          hipLaunchKernelGGL((raster_bwd3p_kernel<1, true, 16, false, s2>),
-                             dim3(cdiv(T, (tiles_per_block<2, 16>()))), dim3(256), 0, st,
-                             tile_bounds_x, tile_bounds_y, img_height, img_width,
-                             gaussian_ids_sorted, (const int2 *)tile_bins, (const float2 *)xys,
-                             conics, colors, opacity, background, final_Ts, final_idx, v_output,
-                             v_output_alpha, alpha_max, rec, (g_bwd_flags & 64) != 0);
-        } else if (atomics && (g_bwd_flags & 4096)) {  // ablation: one wave per tile
-          if (g_bwd_flags & 8192)
-            hipLaunchKernelGGL((raster_bwd4_kernel<false, 1>), dim3(T), dim3(64), 0, st,
-                               tile_bounds_x, tile_bounds_y, img_height, img_width,
-                               gaussian_ids_sorted, (const int2 *)tile_bins, (const float2 *)xys,
-                               conics, colors, opacity, background, final_Ts, final_idx, v_output,
-                               v_output_alpha, alpha_max, rec);
-          else {
-            const int *ord = nullptr;
-            if (g_bwd_flags & 16384) {
-              static int *buf = nullptr;
-              static int cap = 0;
-              if (cap < T) {
-                if (buf) (void)hipFree(buf);
-                note(hipMalloc(&buf, (size_t)T * sizeof(int)), "hipMalloc");
-                cap = T;
-              }
-              hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, st, T,
-                                 (const int2 *)tile_bins, buf);
-              ord = buf;
-            }
-            int *queue = nullptr;
-            unsigned grid = cdiv(T, 4);
-            const int pw = (g_bwd_flags >> 15) & 7;  // persistent waves per SIMD (0: off)
-            if (pw && (unsigned)(256 * pw) < grid) {
-              static int *qbuf = nullptr;
-              if (!qbuf) note(hipMalloc(&qbuf, sizeof(int)), "hipMalloc");
-              note(hipMemsetAsync(qbuf, 0, sizeof(int), st), "hipMemsetAsync");
-              queue = qbuf;
-              grid = 256 * pw;
-            }
-            hipLaunchKernelGGL((raster_bwd4_kernel<false>), dim3(grid), dim3(256), 0, st,
-                               tile_bounds_x, tile_bounds_y, img_height, img_width,
-                               gaussian_ids_sorted, (const int2 *)tile_bins, (const float2 *)xys,
-                               conics, colors, opacity, background, final_Ts, final_idx, v_output,
-                               v_output_alpha, alpha_max, rec, 0, nullptr, nullptr, nullptr,
-                               nullptr, ord, queue);
-          }
-        } else { if (atomics) BWD3P(1, true, 16); else BWD3P(1, false, 16); }  // 16x8 strips
-      }
-    } else if (g_bwd_pxl == 4) { if (atomics) BWD3(4, true); else BWD3(4, false); }
-    else if (g_bwd_pxl == 1) { if (atomics) BWD3(1, true); else BWD3(1, false); }
-    else { if (atomics) BWD3(2, true); else BWD3(2, false); }
-#undef BWD3
-#undef BWD3P
-    hipLaunchKernelGGL(split_grads_kernel, dim3(cdiv(num_points, 256)), dim3(256), 0, st,
-                       num_points, (const float4 *)rec, packed ? 0.5f : 1.f,
-                       conic_y_scale(packed ? 0.5f : 1.f), v_xy, v_conic, v_colors, v_opacity);
+    if (backward_into_records("rasterize_backward", st, tile_bounds_x, tile_bounds_y,
+                              img_height, img_width, num_points, gaussian_ids_sorted, tile_bins,
+                              xys, conics, colors, opacity, background, final_Ts, final_idx,
+                              v_output, v_output_alpha, alpha_max, rec, 0, 0, nullptr, 0))
+      return 1;
+    launch_split(st, num_points, rec, conics, opacity, v_xy, v_conic, v_colors, v_opacity);
   } else {
     if (num_points > 0) {
       note(hipMemsetAsync(v_xy, 0, (size_t)num_points * 2 * sizeof(float), st), "hipMemsetAsync");
@@ -2295,7 +1860,8 @@ extern "C" int gsplat_rasterize_backward(int tile_bounds_x, int tile_bounds_y, i
     ND_DISPATCH(raster_bwdn_kernel, tile_bounds_x, tile_bounds_y, img_height, img_width,
                 channels, gaussian_ids_sorted, (const int2 *)tile_bins, (const float2 *)xys,
                 conics, colors, opacity, background, final_Ts, final_idx, v_output,
-                v_output_alpha, alpha_max, v_xy, v_conic, v_colors, v_opacity);
+                v_output_alpha, alpha_max, conic_y_full() ? 1.f : 0.5f, v_xy, v_conic, v_colors,
+                v_opacity);
   }
   return check_launch("rasterize_backward");
 }
@@ -2310,11 +1876,9 @@ static int rasterize_forward_impl(int tile_bounds_x, int tile_bounds_y, int img_
                                   size_t zero_bytes, const int32_t *zero_radii, void *stream,
                                   const char *who) {
   hipStream_t st = (hipStream_t)stream;
-  if (tile_bounds_x <= 0 || tile_bounds_y <= 0 || img_height <= 0 || img_width <= 0 ||
-      (long long)tile_bounds_x * GS_BLOCK < img_width ||
-      (long long)tile_bounds_y * GS_BLOCK < img_height || (chunk > 0 && chunk % 64) ||
-      num_intersects < 0 || zero_bytes % 16 || (zero_bytes && !zero) ||
-      (zero_radii && zero_bytes % 64)) {
+  if (bad_frame(tile_bounds_x, tile_bounds_y, img_height, img_width) ||
+      (chunk > 0 && chunk % 64) || num_intersects < 0 || zero_bytes % 16 ||
+      (zero_bytes && !zero) || (zero_radii && zero_bytes % 64)) {
     set_error("%s: bad sizes (tiles=%dx%d H=%d W=%d chunk=%d zero=%zu)", who, tile_bounds_x,
               tile_bounds_y, img_height, img_width, chunk, zero_bytes);
     return 1;
@@ -2322,43 +1886,23 @@ static int rasterize_forward_impl(int tile_bounds_x, int tile_bounds_y, int img_
   const int T = tile_bounds_x * tile_bounds_y;
   const long long zn = (long long)(zero_bytes / 16);
   if (chunk <= 0) {
-    if (!default_variants()) {  // debug variants: clear up front, then the variant's launch
-      if (zn && hipMemsetAsync(zero, 0, zero_bytes, st) != hipSuccess) {
-        set_error("%s: memset failed", who);
-        return 1;
-      }
-      return gsplat_rasterize_forward(tile_bounds_x, tile_bounds_y, img_height, img_width, 3,
-                                      gaussian_ids_sorted, tile_bins, xys, conics, colors,
-                                      opacity, background, out_img, final_Ts, final_idx, stream);
-    }
-#define FWDU(CNT)                                                                          \
-  hipLaunchKernelGGL((raster_fwd3u_kernel<1, 8, false, false, CNT>),                          \
-                     dim3(cdiv(T, (tiles_per_block<1, 8>()))), dim3(256), 0, st, tile_bounds_x, \
-                     tile_bounds_y, img_height, img_width, gaussian_ids_sorted,                 \
-                     (const int2 *)tile_bins, (const float2 *)xys, conics, colors, opacity,     \
-                     background, out_img, final_Ts, final_idx, nullptr, nullptr, 0, nullptr,    \
-                     nullptr, (float4 *)zero, zn, zero_radii)
-    if (g_pair_count_on) FWDU(true); else FWDU(false);
-#undef FWDU
+    launch_fwd<false, false>(st, tile_bounds_x, tile_bounds_y, img_height, img_width,
+                             gaussian_ids_sorted, tile_bins, xys, conics, colors, opacity,
+                             background, out_img, final_Ts, final_idx, nullptr, nullptr, 0,
+                             nullptr, nullptr, (float4 *)zero, zn, zero_radii);
     return check_launch(who);
   }
   const ChunkWs w = carve_chunk_ws(checkpoints, T, num_intersects, chunk);
-  if (!checkpoints || checkpoint_bytes < w.bytes || !default_variants()) {
-    set_error("%s: checkpoint buffer %zu < %zu bytes (or non-default raster variant)", who,
-              checkpoint_bytes, w.bytes);
+  if (!checkpoints || checkpoint_bytes < w.bytes) {
+    set_error("%s: checkpoint buffer %zu < %zu bytes", who, checkpoint_bytes, w.bytes);
     return 1;
   }
   hipLaunchKernelGGL(chunk_plan_kernel, dim3(1), dim3(1024), 0, st, T, (const int2 *)tile_bins,
                      chunk, w.item_off, w.ckpt_off, w.item_tile);
-#define FWDC(CNT)                                                                          \
-  hipLaunchKernelGGL((raster_fwd3u_kernel<1, 8, false, true, CNT>),                           \
-                     dim3(cdiv(T, (tiles_per_block<1, 8>()))), dim3(256), 0, st, tile_bounds_x, \
-                     tile_bounds_y, img_height, img_width, gaussian_ids_sorted,                 \
-                     (const int2 *)tile_bins, (const float2 *)xys, conics, colors, opacity,     \
-                     background, out_img, final_Ts, final_idx, nullptr, nullptr, chunk,         \
-                     w.ckpt_off, w.ckpt, (float4 *)zero, zn, zero_radii)
-  if (g_pair_count_on) FWDC(true); else FWDC(false);
-#undef FWDC
+  launch_fwd<false, true>(st, tile_bounds_x, tile_bounds_y, img_height, img_width,
+                          gaussian_ids_sorted, tile_bins, xys, conics, colors, opacity,
+                          background, out_img, final_Ts, final_idx, nullptr, nullptr, chunk,
+                          w.ckpt_off, w.ckpt, (float4 *)zero, zn, zero_radii);
   return check_launch(who);
 }
 
@@ -2368,10 +1912,6 @@ extern "C" int gsplat_rasterize_forward_chunked(
     const float *conics, const float *colors, const float *opacity, const float *background,
     float *out_img, float *final_Ts, int32_t *final_idx, int64_t num_intersects, int chunk,
     void *checkpoints, size_t checkpoint_bytes, void *stream) {
-  if (chunk <= 0)
-    return gsplat_rasterize_forward(tile_bounds_x, tile_bounds_y, img_height, img_width, 3,
-                                    gaussian_ids_sorted, tile_bins, xys, conics, colors, opacity,
-                                    background, out_img, final_Ts, final_idx, stream);
   return rasterize_forward_impl(tile_bounds_x, tile_bounds_y, img_height, img_width,
                                 gaussian_ids_sorted, tile_bins, xys, conics, colors, opacity,
                                 background, out_img, final_Ts, final_idx, num_intersects, chunk,
@@ -2393,43 +1933,6 @@ extern "C" int gsplat_rasterize_forward_clearing(
                                 stream, "rasterize_forward_clearing");
 }
 
-// List-split backward launch: two waves (16x8 strips) per (tile, chunk) item, or one wave per
-// item with the tile-wave kernel (ablation flag 4096).
-static void launch_bwd_chunked(hipStream_t st, int tbx, int tby, int H, int W, const int32_t *gids,
-                               const int32_t *bins, const float *xys, const float *conics,
-                               const float *colors, const float *opacity, const float *background,
-                               const float *final_Ts, const int32_t *final_idx,
-                               const float *v_output, const float *v_output_alpha,
-                               float alpha_max, float *rec, int chunk, const ChunkWs &w,
-                               unsigned long long *det = nullptr) {
-  if (g_det) {
-    hipLaunchKernelGGL((raster_bwd3p_kernel<1, true, 16, true, f2, true>),
-                       dim3((unsigned)cdiv(w.items_bound, (long long)(tiles_per_block<2, 16>()))),
-                       dim3(256), 0, st, tbx, tby, H, W, gids, (const int2 *)bins,
-                       (const float2 *)xys, conics, colors, opacity, background, final_Ts,
-                       final_idx, v_output, v_output_alpha, alpha_max, rec, false, chunk,
-                       w.item_off, w.item_tile, w.ckpt_off, w.ckpt, det);
-    return;
-  }
-  if (!(g_bwd_flags & 4096)) {
-#define BWDC(CNT)                                                                          \
-  hipLaunchKernelGGL((raster_bwd3p_kernel<1, true, 16, true, f2, false, CNT>),                \
-                     dim3((unsigned)cdiv(w.items_bound, (long long)(tiles_per_block<2, 16>()))),\
-                     dim3(256), 0, st, tbx, tby, H, W, gids, (const int2 *)bins,                \
-                     (const float2 *)xys, conics, colors, opacity, background, final_Ts,        \
-                     final_idx, v_output, v_output_alpha, alpha_max, rec, false, chunk,         \
-                     w.item_off, w.item_tile, w.ckpt_off, w.ckpt)
-    if (g_pair_count_on) BWDC(true); else BWDC(false);
-#undef BWDC
-    return;
-  }
-  hipLaunchKernelGGL((raster_bwd4_kernel<true>), dim3((unsigned)cdiv(w.items_bound, 4LL)),
-                     dim3(256), 0, st, tbx, tby, H, W, gids, (const int2 *)bins,
-                     (const float2 *)xys, conics, colors, opacity, background, final_Ts,
-                     final_idx, v_output, v_output_alpha, alpha_max, rec, chunk, w.item_off,
-                     w.item_tile, w.ckpt_off, w.ckpt);
-}
-
 extern "C" int gsplat_rasterize_backward_chunked(
     int tile_bounds_x, int tile_bounds_y, int img_height, int img_width, int num_points,
     const int32_t *gaussian_ids_sorted, const int32_t *tile_bins, const float *xys,
@@ -2445,55 +1948,42 @@ extern "C" int gsplat_rasterize_backward_chunked(
                                      v_output_alpha, alpha_max, v_xy, v_conic, v_colors,
                                      v_opacity, workspace, workspace_bytes, stream);
   hipStream_t st = (hipStream_t)stream;
-  if (tile_bounds_x <= 0 || tile_bounds_y <= 0 || img_height <= 0 || img_width <= 0 ||
-      num_points < 0 || num_points >= MAX_BWD_POINTS ||
-      (long long)tile_bounds_x * GS_BLOCK < img_width ||
-      (long long)tile_bounds_y * GS_BLOCK < img_height || chunk % 64 || num_intersects < 0) {
-    set_error("rasterize_backward_chunked: bad sizes (tiles=%dx%d H=%d W=%d N=%d chunk=%d)",
-              tile_bounds_x, tile_bounds_y, img_height, img_width, num_points, chunk);
-    return 1;
-  }
-  const int T = tile_bounds_x * tile_bounds_y;
-  const ChunkWs w =
-      carve_chunk_ws(const_cast<void *>(checkpoints), T, num_intersects, chunk);
   const size_t need = gsplat_rasterize_backward_workspace_size(num_points, 3);
-  if (!checkpoints || checkpoint_bytes < w.bytes || workspace_bytes < need ||
-      (need && !workspace) || !default_variants()) {
-    set_error("rasterize_backward_chunked: buffers too small (checkpoints %zu < %zu or "
-              "workspace %zu < %zu) or non-default raster variant",
-              checkpoint_bytes, w.bytes, workspace_bytes, need);
+  if (bad_frame(tile_bounds_x, tile_bounds_y, img_height, img_width) || num_points < 0 ||
+      num_points >= MAX_BWD_POINTS || chunk % 64 || num_intersects < 0 ||
+      workspace_bytes < need || (need && !workspace)) {
+    set_error("rasterize_backward_chunked: bad sizes (tiles=%dx%d H=%d W=%d N=%d chunk=%d) or "
+              "workspace %zu < %zu bytes", tile_bounds_x, tile_bounds_y, img_height, img_width,
+              num_points, chunk, workspace_bytes, need);
     return 1;
   }
   if (num_points == 0) return check_launch("rasterize_backward_chunked");
   float *rec = (float *)workspace;
   note(hipMemsetAsync(rec, 0, need, st), "hipMemsetAsync");
-  unsigned long long *det = g_det ? det_buffer(num_points, st) : nullptr;
-  if (g_det && !det) return check_launch("rasterize_backward_chunked");
-  launch_bwd_chunked(st, tile_bounds_x, tile_bounds_y, img_height, img_width,
-                     gaussian_ids_sorted, tile_bins, xys, conics, colors, opacity, background,
-                     final_Ts, final_idx, v_output, v_output_alpha, alpha_max, rec, chunk, w, det);
-  if (det)
-    hipLaunchKernelGGL(det_finish_kernel, dim3(cdiv(num_points, 256)), dim3(256), 0, st,
-                       num_points, det, rec);
-  hipLaunchKernelGGL(split_grads_kernel, dim3(cdiv(num_points, 256)), dim3(256), 0, st,
-                     num_points, (const float4 *)rec, 0.5f, conic_y_scale(0.5f), v_xy, v_conic,
-                     v_colors, v_opacity);
+  if (backward_into_records("rasterize_backward_chunked", st, tile_bounds_x, tile_bounds_y,
+                            img_height, img_width, num_points, gaussian_ids_sorted, tile_bins, xys,
+                            conics, colors, opacity, background, final_Ts, final_idx, v_output,
+                            v_output_alpha, alpha_max, rec, num_intersects, chunk, checkpoints,
+                            checkpoint_bytes))
+    return 1;
+  launch_split(st, num_points, rec, conics, opacity, v_xy, v_conic, v_colors, v_opacity);
   return check_launch("rasterize_backward_chunked");
 }
 
 extern "C" int gsplat_grad_records_split(int num_points, const void *records,
-                                         size_t records_bytes, float *v_xy, float *v_conic,
+                                         size_t records_bytes, const float *conics,
+                                         const float *opacity, float *v_xy, float *v_conic,
                                          float *v_colors, float *v_opacity, void *stream) {
   const size_t need = num_points > 0 ? (size_t)num_points * REC * sizeof(float) : 0;
-  if (num_points < 0 || records_bytes < need || (need && !records)) {
-    set_error("grad_records_split: records %zu < %zu bytes (N=%d)", records_bytes, need,
-              num_points);
+  if (num_points < 0 || records_bytes < need ||
+      (need && (!records || !conics || !opacity))) {
+    set_error("grad_records_split: records %zu < %zu bytes or NULL conics/opacity (N=%d)",
+              records_bytes, need, num_points);
     return 1;
   }
   if (num_points == 0) return 0;
-  hipLaunchKernelGGL(split_grads_kernel, dim3(cdiv(num_points, 256)), dim3(256), 0,
-                     (hipStream_t)stream, num_points, (const float4 *)records, 0.5f,
-                     conic_y_scale(0.5f), v_xy, v_conic, v_colors, v_opacity);
+  launch_split((hipStream_t)stream, num_points, (const float *)records, conics, opacity, v_xy,
+               v_conic, v_colors, v_opacity);
   return check_launch("grad_records_split");
 }
 
@@ -2511,63 +2001,21 @@ extern "C" int gsplat_rasterize_backward_records(
     void *stream) {
   hipStream_t st = (hipStream_t)stream;
   const size_t need = gsplat_grad_records_bytes(num_points);
-  if (tile_bounds_x <= 0 || tile_bounds_y <= 0 || img_height <= 0 || img_width <= 0 ||
-      num_points < 0 || num_points >= MAX_BWD_POINTS ||
-      (long long)tile_bounds_x * GS_BLOCK < img_width ||
-      (long long)tile_bounds_y * GS_BLOCK < img_height || num_intersects < 0 ||
-      (chunk > 0 && chunk % 64) || records_bytes < need || (need && !records)) {
+  if (bad_frame(tile_bounds_x, tile_bounds_y, img_height, img_width) || num_points < 0 ||
+      num_points >= MAX_BWD_POINTS || num_intersects < 0 || (chunk > 0 && chunk % 64) ||
+      records_bytes < need || (need && !records)) {
     set_error("rasterize_backward_records: bad sizes (tiles=%dx%d H=%d W=%d N=%d chunk=%d "
               "records %zu < %zu bytes)", tile_bounds_x, tile_bounds_y, img_height, img_width,
               num_points, chunk, records_bytes, need);
     return 1;
   }
-  if (!default_variants()) {
-    set_error("rasterize_backward_records: needs the default raster variant");
-    return 1;
-  }
   if (num_points == 0 || num_intersects == 0) return check_launch("rasterize_backward_records");
-  const int T = tile_bounds_x * tile_bounds_y;
-  float *rec = (float *)records;
-  if (g_det && (g_bwd_flags & 4096)) {
-    set_error("rasterize_backward_records: deterministic mode needs the strip backward");
+  // deterministic mode: the records' clear by the forward is superseded by det_finish_kernel
+  if (backward_into_records("rasterize_backward_records", st, tile_bounds_x, tile_bounds_y,
+                            img_height, img_width, num_points, gaussian_ids_sorted, tile_bins, xys,
+                            conics, colors, opacity, background, final_Ts, final_idx, v_output,
+                            v_output_alpha, alpha_max, (float *)records, num_intersects, chunk,
+                            checkpoints, checkpoint_bytes))
     return 1;
-  }
-  // deterministic mode: the records' clear by the forward is superseded by the integer sums
-  unsigned long long *det = g_det ? det_buffer(num_points, st) : nullptr;
-  if (g_det && !det) return check_launch("rasterize_backward_records");
-  if (chunk > 0) {
-    const ChunkWs w = carve_chunk_ws(const_cast<void *>(checkpoints), T, num_intersects, chunk);
-    if (!checkpoints || checkpoint_bytes < w.bytes) {
-      set_error("rasterize_backward_records: checkpoint buffer %zu < %zu bytes", checkpoint_bytes,
-                w.bytes);
-      return 1;
-    }
-    launch_bwd_chunked(st, tile_bounds_x, tile_bounds_y, img_height, img_width,
-                       gaussian_ids_sorted, tile_bins, xys, conics, colors, opacity, background,
-                       final_Ts, final_idx, v_output, v_output_alpha, alpha_max, rec, chunk, w,
-                       det);
-  } else if (det) {
-    launch_bwd_det(st, tile_bounds_x, tile_bounds_y, img_height, img_width, gaussian_ids_sorted,
-                   tile_bins, xys, conics, colors, opacity, background, final_Ts, final_idx,
-                   v_output, v_output_alpha, alpha_max, rec, det);
-  } else if (g_bwd_flags & 4096) {
-    hipLaunchKernelGGL((raster_bwd4_kernel<false>), dim3(cdiv(T, 4)), dim3(256), 0, st,
-                       tile_bounds_x, tile_bounds_y, img_height, img_width, gaussian_ids_sorted,
-                       (const int2 *)tile_bins, (const float2 *)xys, conics, colors, opacity,
-                       background, final_Ts, final_idx, v_output, v_output_alpha, alpha_max, rec);
-  } else {
-#define BWDR(CNT)                                                                          \
-  hipLaunchKernelGGL((raster_bwd3p_kernel<1, true, 16, false, f2, false, CNT>),               \
-                     dim3(cdiv(T, (tiles_per_block<2, 16>()))), dim3(256), 0, st,              \
-                     tile_bounds_x, tile_bounds_y, img_height, img_width, gaussian_ids_sorted,  \
-                     (const int2 *)tile_bins, (const float2 *)xys, conics, colors, opacity,     \
-                     background, final_Ts, final_idx, v_output, v_output_alpha, alpha_max, rec, \
-                     false)
-    if (g_pair_count_on) BWDR(true); else BWDR(false);
-#undef BWDR
-  }
-  if (det)
-    hipLaunchKernelGGL(det_finish_kernel, dim3(cdiv(num_points, 256)), dim3(256), 0, st,
-                       num_points, det, rec);
   return check_launch("rasterize_backward_records");
 }

@@ -240,26 +240,31 @@ def render_fused(scene, cam: GCCamera, sh_degree_to_use: int, background: Tensor
     img, alpha = (out if return_alpha else (out, None))
     rgb = torch.clamp(img, max=1.0) if clamp else img
 
-    def xys_grad() -> Optional[Tensor]:
+    def split_records():
+        """The records (pixel moments, include/gsplat_mi355x.h) -> gsplat's four rasterize
+        gradients by gsplat_grad_records_split; zero for culled Gaussians."""
         rec = aux.get("records")
         if rec is None:
             return None
-        v = rec[:aux["num_points"] * 64].view(torch.float32).view(-1, 16)[:, :2]
-        return torch.where(aux["radii"][:, None] > 0, v, torch.zeros_like(v))  # culled: 0
+        n, dev = aux["num_points"], rec.device
+        out = [torch.empty(n, k, device=dev) for k in (2, 3, 3, 1)]
+        P = _lib.ptr
+        _lib.call("gsplat_grad_records_split", n, P(rec), rec.numel(), P(aux["conics"]),
+                  P(aux["opacity"]), *[P(t) for t in out], _lib.stream(dev))
+        vis = aux["radii"][:, None] > 0
+        return [torch.where(vis, t, torch.zeros_like(t)) for t in out]
+
+    def xys_grad() -> Optional[Tensor]:
+        g = split_records()
+        return None if g is None else g[0]
 
     def raster_grads():
         """After backward: the rasterizer-level gradients in gsplat's convention -- v_xy [N,2],
         v_conic [N,3] (v_conic.y per the CONIC_HALF quirk), v_colors [N,3], v_opacity [N,1] --
         i.e. what gsplat's rasterize_gaussians backward returns for this render; zero for
         culled Gaussians.  None without records (no gradient requested)."""
-        rec = aux.get("records")
-        if rec is None:
-            return None
-        r = rec[:aux["num_points"] * 64].view(torch.float32).view(-1, 16)
-        cy = 0.5 if quirks.get() & quirks.CONIC_HALF else 1.0
-        scale = torch.tensor([1.0, 1.0, 0.5, cy, 0.5, 1.0, 1.0, 1.0, 1.0], device=r.device)
-        g = torch.where(aux["radii"][:, None] > 0, r[:, :9] * scale, torch.zeros_like(r[:, :9]))
-        return g[:, 0:2], g[:, 2:5], g[:, 5:8], g[:, 8:9]
+        g = split_records()
+        return None if g is None else tuple(g)
 
     return {"rgb": rgb, "clamped": bool(clamp),
             "accumulation": alpha[..., None] if alpha is not None else None,

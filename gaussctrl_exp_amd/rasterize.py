@@ -427,8 +427,9 @@ class _RasterizeGaussians(Function):
                           P(v_out_alpha), quirks.backward_alpha_clamp(), ctx.num_intersects,
                           ctx.chunk, P(ctx.ckpt), ctx.ckpt.numel() if ctx.ckpt is not None
                           else 0, P(rec), rec.numel(), st)
-                _lib.call("gsplat_grad_records_split", num_points, P(rec), rec.numel(), P(v_xy),
-                          P(v_conic), P(v_colors), P(v_opacity), st)
+                _lib.call("gsplat_grad_records_split", num_points, P(rec), rec.numel(),
+                          P(conics), P(opacity), P(v_xy), P(v_conic), P(v_colors), P(v_opacity),
+                          st)
                 ctx.rec = None
                 return (v_xy, None, None, v_conic, None, v_colors, v_opacity, None, None, None,
                         None)

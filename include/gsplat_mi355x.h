@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define GSPLAT_MI355X_ABI_VERSION 7
+#define GSPLAT_MI355X_ABI_VERSION 8
 
 int gsplat_abi_version(void);
 const char *gsplat_last_error(void);
@@ -67,11 +67,13 @@ int gsplat_get_quirks(void);
 
 /* ---- deterministic backward (debugging) -------------------------------
  * on != 0: the C = 3 rasterize backward entries (gsplat_rasterize_backward,
- * _backward_chunked, _backward_records) add every wave's per-Gaussian totals as 64-bit
- * fixed-point integers (2^-32 units) instead of fp32 atomics, then convert: gradients are
- * bit-identical from run to run.  Slower (integer atomics, an extra pass over N); the
- * accumulator buffer is allocated by the library on first use (debug mode only).  Replaces no
- * gsplat entry point (gsplat's backward.cu atomics are order-nondeterministic). */
+ * _backward_chunked, _backward_records) add every wave's per-Gaussian totals as exact
+ * integers (each total truncated to a multiple of 2^-80 and added as three 40-bit limbs into
+ * 64-bit accumulators) instead of fp32 atomics, then convert: gradients are bit-identical from
+ * run to run at any gradient magnitude.  Slower (integer atomics, an extra pass over N); the
+ * accumulators are one library-owned buffer per device, allocated on first use, and calls on
+ * different streams or threads are serialised on it (debug mode only).  Replaces no gsplat
+ * entry point (gsplat's backward.cu atomics are order-nondeterministic). */
 int gsplat_set_deterministic(int on);
 int gsplat_get_deterministic(void);
 
@@ -350,7 +352,11 @@ int gsplat_fused_preprocess_backward_adam(
     void *stream);
 
 /* Per-Gaussian gradient records (64 B each) the fused path's rasterize backward accumulates
- * into: gsplat_rasterize_backward_records is gsplat_rasterize_backward (C = 3, default
+ * into, as pixel moments over every pixel the Gaussian is composited at (d = xy - pixel,
+ * w = vis * v_alpha): floats 0 sum dx w, 1 sum dy w, 2 sum dx^2 w, 3 sum dx dy w, 4 sum dy^2 w,
+ * 5-7 v_colors, 8 sum w (= v_opacity), 9-15 unused; gsplat's gradients follow per Gaussian as
+ * v_xy = -o (a Sx + b Sy, b Sx + c Sy), v_conic = -o/2 (Sxx, Sxy, Syy) (conic = (a, b, c),
+ * o = opacity; v_conic.y doubled without GSPLAT_QUIRK_CONIC_HALF).  gsplat_rasterize_backward_records is gsplat_rasterize_backward (C = 3, default
  * variant, list-split when chunk > 0 as in the _chunked entry) without the zero fill and
  * without the split into v_xy / v_conic / v_colors / v_opacity -- the records must be zeroed
  * by the caller (gsplat_fused_preprocess_forward does it for the visible Gaussians, the
@@ -371,28 +377,17 @@ int gsplat_rasterize_backward_records(
  * (gsplat_rasterize_forward_clearing) and accumulated them with
  * gsplat_rasterize_backward_records (the drop-in rasterize_gaussians does). */
 int gsplat_grad_records_split(int num_points, const void *records, size_t records_bytes,
-                              float *v_xy, float *v_conic, float *v_colors, float *v_opacity,
-                              void *stream);
+                              const float *conics, const float *opacity, float *v_xy,
+                              float *v_conic, float *v_colors, float *v_opacity, void *stream);
 
-/* Tuning / ablation hook (not part of the gsplat surface): pixels per lane of the 3-channel
- * forward and backward kernels (1, 2 or 4; a 16x16 tile is covered by 4/pxl waves), and
- * flags: bit 0 drops the gradient atomics (timing ablation only, results wrong); bit 1
- * scalar backward; bit 2 scalar forward (one Gaussian per iteration, 16-column strips);
- * bit 3 packed float2 forward; bit 4 16-column forward rectangles; bit 5 8-column backward
- * rectangles; bit 6 backward stages and culls but skips the blend (timing ablation only); bit 10
- * XCD-contiguous block order in the shipped forward and backward kernels; bit 11 backward with
- * sub-wave lists (each 16-lane row of a wave walks its own 8x4 rectangle's culled list); bit 12
- * one backward wave per 16x16 tile (four pixels per lane as two float2 pairs, per-half cull
- * bits; also used by the list-split backward), with bit 13 one-wave workgroups, bit 14 tiles
- * dealt longest-list-first, bits 15-17 = p > 0: p persistent waves per SIMD taking tiles from a
- * queue; bits 20-27 = K: the block -> tile order of the blend kernels, chunks of K block slots
- * dealt round-robin over the 8 XCDs (0: the shipped K = 8, 255: plain dispatch order).  Every
- * variant produces results within the same parity bar.  Process-wide;
- * defaults (1, 2, 0) are the shipped configuration. */
+/* Measurement hook (not part of the gsplat surface): fwd_pxl must be 1 (the forward's 8x8
+ * blocks); bwd_pxl selects the C = 3 backward's geometry: 1 = 8x8 blocks, one pixel per lane,
+ * two Gaussians per iteration (shipped), 2 = 16x8 strips, two pixels per lane (the round-2
+ * kernel, kept for A/B timing); bwd_flags bits 20-27 = K: the block -> tile order of the blend
+ * kernels, chunks of K block slots dealt round-robin over the 8 XCDs (0: the shipped K = 8, 255:
+ * plain dispatch order).  Both geometries meet the same parity bar.  Process-wide; (1, 1, 0) is
+ * the shipped configuration. */
 int gsplat_debug_set_raster_variant(int fwd_pxl, int bwd_pxl, int bwd_flags);
-/* Tuning hook: the blend kernels visit tiles in groups of gw x gh tiles (bands of gh tile rows,
- * row-major inside a group) instead of row-major order; (1, 1) is row-major.  Process-wide. */
-int gsplat_debug_set_tile_swizzle(int gw, int gh);
 /* 1 while the shipped raster variants are selected (the record-based entries need them). */
 int gsplat_debug_raster_variant_is_default(void);
 

@@ -12,6 +12,18 @@ for p in (ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a ROCm GPU (MI355X); run with -m gpu")
     config.addinivalue_line("markers", "slow: long-running")
+    config.addinivalue_line(
+        "markers", "ablation: checks a measured-slower, non-shipped code path kept for A/B "
+        "timing; skipped unless GSPLAT_TEST_ABLATION=1")
+
+
+def pytest_collection_modifyitems(config, items):
+    if os.environ.get("GSPLAT_TEST_ABLATION") == "1":
+        return
+    skip = pytest.mark.skip(reason="ablation path (set GSPLAT_TEST_ABLATION=1 to run)")
+    for item in items:
+        if "ablation" in item.keywords:
+            item.add_marker(skip)
 
 
 @pytest.fixture(scope="session")

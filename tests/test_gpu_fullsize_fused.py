@@ -97,12 +97,13 @@ class FusedRun:
                   self.chunk, P(self.ckpt), self.ckpt.numel(), P(self.rec), self.rec.numel(), st)
 
     def raster_grads(self):
-        r = self.rec.view(torch.float32).view(-1, 16)[:, :9]
-        cy = 0.5 if quirks.get() & quirks.CONIC_HALF else 1.0
-        g = r * torch.tensor([1, 1, 0.5, cy, 0.5, 1, 1, 1, 1], device=r.device)
-        g = torch.where(self.radii[:, None] > 0, g, torch.zeros_like(g))
-        g = _np(g)
-        return g[:, 0:2], g[:, 2:5], g[:, 5:8], g[:, 8:9]
+        """The records (pixel moments) -> gsplat's four raster gradients (the split kernel)."""
+        P, n = _lib.ptr, self.n
+        out = [torch.empty(n, k, device=self.gpu) for k in (2, 3, 3, 1)]
+        _lib.call("gsplat_grad_records_split", n, P(self.rec), self.rec.numel(), P(self.conics),
+                  P(self.opac), *[P(t) for t in out], _lib.stream(self.gpu))
+        vis = self.radii[:, None] > 0
+        return tuple(_np(torch.where(vis, t, torch.zeros_like(t))) for t in out)
 
     def param_grads(self):
         P, st, gpu, n, K, sc, c = _lib.ptr, _lib.stream(self.gpu), self.gpu, self.n, self.K, \

@@ -319,18 +319,13 @@ def test_raster_backward(gpu, case, quirk_mask):
 
 
 # (fwd pixels/lane, bwd pixels/lane, flags): see gsplat_debug_set_raster_variant in
-# include/gsplat_mi355x.h (1 no atomics, 2 scalar bwd, 4 scalar fwd, 8 packed fwd, 16 wide
-# fwd, 32 narrow bwd, 1024 XCD-contiguous block order, K << 20 chunks of K block slots per XCD
-# (shipped K = 8; 255 << 20 plain dispatch order), 2048
-# sub-wave-list backward, 4096 one wave per tile (+8192 one-wave workgroups, +16384 tiles
-# longest-first, + 4 << 15 four persistent waves per SIMD pulling tiles from a queue)).
-RASTER_VARIANTS = [(1, 2, 0), (1, 2, 4), (1, 2, 16), (2, 2, 0), (2, 2, 8), (2, 2, 6), (4, 4, 0),
-                   (4, 4, 8), (4, 4, 6), (1, 1, 0), (1, 2, 32), (1, 2, 1024),
-                   (1, 2, 2048), (1, 2, 4096), (1, 2, 4096 | 8192), (1, 2, 4096 | 16384),
-                   (1, 2, 4096 | (4 << 15)), (1, 2, 255 << 20), (1, 2, 1 << 20),
-                   (1, 2, 3 << 20)]
+# include/gsplat_mi355x.h -- bwd 2 = the 16x8-strip backward kept for A/B timing; K << 20 the
+# blend kernels' block order in chunks of K block slots per XCD (shipped K = 8; 255 << 20 plain
+# dispatch order).
+RASTER_VARIANTS = [(1, 2, 0), (1, 3, 0), (1, 1, 255 << 20), (1, 1, 1 << 20), (1, 1, 3 << 20)]
 
 
+@pytest.mark.ablation
 @pytest.mark.parametrize("variant", RASTER_VARIANTS)
 @pytest.mark.parametrize("case", [CASES[0], CASES[1], CASES[3]])
 def test_raster_variants(gpu, case, variant):
@@ -341,7 +336,7 @@ def test_raster_variants(gpu, case, variant):
         _check_raster_forward(gpu, case)
         _check_raster_backward(gpu, case)
     finally:
-        _lib.call("gsplat_debug_set_raster_variant", 1, 2, 0)
+        _lib.call("gsplat_debug_set_raster_variant", 1, 1, 0)
 
 
 def _check_raster_backward(gpu, case):
@@ -381,32 +376,37 @@ def _check_raster_backward(gpu, case):
         assert frac == 0.0, f"{name}: {frac:.2e} out of tolerance (max {mx:.3e})"
 
 
-@pytest.mark.parametrize("flags", [0, 4096])
+@pytest.mark.parametrize("bwd", [1, pytest.param(2, marks=pytest.mark.ablation), pytest.param(3, marks=pytest.mark.ablation)])
 @pytest.mark.parametrize("chunk", [64, 128, 256])
 @pytest.mark.parametrize("case", CASES[1:3])
-def test_raster_backward_list_split(gpu, case, chunk, flags):
+def test_raster_backward_list_split(gpu, case, chunk, bwd):
     """The list-split backward (checkpointed forward + per-chunk backward, forced chunk
-    size; strip waves or, flag 4096, one wave per item): identical forward, gradients within
-    the same bar vs the oracle."""
+    size; 8x8 block waves or, bwd 2, 16x8 strips): identical forward, gradients within the
+    same bar vs the oracle."""
     _lib.call("gsplat_debug_set_chunk", chunk)
-    _lib.call("gsplat_debug_set_raster_variant", 1, 2, flags)
+    _lib.call("gsplat_debug_set_raster_variant", 1, bwd, 0)
     try:
         _check_raster_forward(gpu, case)
         _check_raster_backward(gpu, case)
     finally:
         _lib.call("gsplat_debug_set_chunk", 0)
-        _lib.call("gsplat_debug_set_raster_variant", 1, 2, 0)
+        _lib.call("gsplat_debug_set_raster_variant", 1, 1, 0)
 
 
+@pytest.mark.parametrize("quirk_mask", [7, 0], indirect=True)
 @pytest.mark.parametrize("C", [1, 4, 7])
-def test_nd_rasterize(gpu, C):
+def test_nd_rasterize(gpu, C, quirk_mask):
+    """N-channel rasterize (gsplat nd_rasterize) forward and all four backward gradients vs the
+    oracle, under gsplat's quirks and without them (v_conic.y = d loss / d conic.y: ADVICE r2)."""
     case = CASES[1]
     sc, cam, g, o, colors, opac, bg = _raster_case(gpu, case, C=C)
     xys, depths, radii, conics, nth, cov3d = [t.detach() for t in g]
     H, W = cam.height, cam.width
+    xy = xys.clone().requires_grad_()
+    cn = conics.clone().requires_grad_()
     col = colors.to(gpu).requires_grad_()
     op = opac.to(gpu).requires_grad_()
-    img, alpha = rasterize_gaussians(xys, depths, radii, conics, nth, col, op, H, W,
+    img, alpha = rasterize_gaussians(xy, depths, radii, cn, nth, col, op, H, W,
                                      bg.to(gpu), return_alpha=True)
     f = O.render_forward(o[0], o[1], o[2], o[3], o[4], colors.numpy(), opac.numpy(), H, W,
                          bg.numpy())
@@ -415,11 +415,16 @@ def test_nd_rasterize(gpu, C):
     gen = torch.Generator().manual_seed(8)
     v_img = torch.randn(H, W, C, generator=gen)
     (img * v_img.to(gpu)).sum().backward()
-    ref = O.render_backward(f, o[0], o[3], colors.numpy(), opac.numpy(), bg.numpy(),
-                            v_img.numpy(), np.zeros((H, W), np.float32),
-                            alpha_max=quirks.backward_alpha_clamp())
-    frac, mx = _close_frac(_np(col.grad), ref[2])
-    assert frac == 0, (frac, mx)
+    # the oracle's backward on the oracle's own forward state
+    ref, absum = O.rasterize_backward(f["tile_bounds"], H, W, f["gaussian_ids_sorted"],
+                                      f["tile_bins"], o[0], o[3], colors.numpy(), opac.numpy(),
+                                      bg.numpy(), f["final_Ts"], f["final_idx"], v_img.numpy(),
+                                      np.zeros((H, W), np.float32),
+                                      alpha_max=quirks.backward_alpha_clamp(), return_abs=True)
+    for k, (name, gt) in enumerate((("xys", xy.grad), ("conics", cn.grad), ("colors", col.grad),
+                                    ("opacity", op.grad))):
+        frac, mx = _close_frac(_np(gt), ref[k].reshape(gt.shape), abs_sum=absum[k])
+        assert frac == 0, f"{name}: {frac:.2e} out of tolerance (max {mx:.3e})"
 
 
 def test_uint8_colors(gpu):

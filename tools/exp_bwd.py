@@ -1,5 +1,6 @@
-"""A/B of the shipped raster backward against the 16x8-strip kernel (flag 4096): gradient
-agreement (max |diff| relative to max |grad|) and interleaved timing, on a bench config."""
+"""A/B of raster backward variants (gsplat_debug_set_raster_variant; default: the shipped 8x8
+block backward vs the 16x8-strip kernel): gradient agreement and interleaved timing, on a
+bench config (CFG)."""
 import os, sys
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 import numpy as np
@@ -53,7 +54,7 @@ def timeit(fn, reps=10):
 if os.environ.get("VARIANTS"):
     variants = [tuple(int(v) for v in x.split(":")) for x in os.environ["VARIANTS"].split(",")]
 else:
-    variants = [(1, 2, int(x)) for x in os.environ.get("FLAGS", "0,4096").split(",")]
+    variants = [(1, int(x), 0) for x in os.environ.get("BWD", "1,2").split(",")]
 fwd(); torch.cuda.synchronize()
 grads = {}
 for f in variants:
@@ -75,7 +76,7 @@ for rnd in range(5):
         _lib.call("gsplat_debug_set_raster_variant", *f)
         g = grads[f]
         res[f].append(timeit(lambda: bwd(g)))
-_lib.call("gsplat_debug_set_raster_variant", 1, 2, 0)
+_lib.call("gsplat_debug_set_raster_variant", 1, 1, 0)
 print(f"{cfg}: N={N} I={I} tiles={tb[0]*tb[1]}")
 for f in variants:
     print(f"bwd variant={f}: {np.median(res[f]):.4f} ms  (rounds {np.round(res[f], 4).tolist()})")
