@@ -144,6 +144,14 @@ def lib():
         if L.gsplat_set_quirks(quirks.get()) != 0:
             raise RuntimeError(L.gsplat_last_error().decode(errors="replace"))
         L.gsplat_set_deterministic(int(_DETERMINISTIC))
+        # measurement hooks (A/B runs of bench.py / tools): GSPLAT_MI355X_RASTER_VARIANT =
+        # "fwd_pxl,bwd_pxl,flags" (gsplat_debug_set_raster_variant), GSPLAT_MI355X_CHUNK = the
+        # list-split chunk override (gsplat_debug_set_chunk)
+        var = os.environ.get("GSPLAT_MI355X_RASTER_VARIANT")
+        if var and L.gsplat_debug_set_raster_variant(*[int(x) for x in var.split(",")]) != 0:
+            raise RuntimeError(L.gsplat_last_error().decode(errors="replace"))
+        if os.environ.get("GSPLAT_MI355X_CHUNK"):
+            L.gsplat_debug_set_chunk(int(os.environ["GSPLAT_MI355X_CHUNK"]))
         _lib = L
     return _lib
 

@@ -141,9 +141,9 @@ struct DetLease {
 };
 constexpr int FWD_PXL = 1;  // forward: 8x8 blocks, two Gaussians per iteration (4 waves/tile)
 // backward geometry (gsplat_debug_set_raster_variant's bwd_pxl): 1 = 8x8 blocks, one pixel per
-// lane, two Gaussians per iteration (raster_bwd8_kernel, shipped); 2 = 16x8 strips, two pixels
-// per lane (raster_bwd3p_kernel, the round-2 kernel kept for A/B measurements)
-constexpr int BWD_PXL = 1;
+// lane, two Gaussians per iteration (raster_bwd8_kernel); 2 = 16x8 strips, two pixels per lane
+// (raster_bwd3p_kernel); 0 = by frame size, see bwd_geometry()
+constexpr int BWD_PXL = 0;  // 0: by frame size (bwd_geometry)
 // Tuning / ablation knobs (gsplat_debug_set_raster_variant); defaults are the shipped ones.
 int g_fwd_pxl = FWD_PXL, g_bwd_pxl = BWD_PXL, g_bwd_flags = 0;
 
@@ -988,238 +988,6 @@ __global__ __launch_bounds__(256) void raster_bwd8_kernel(
   wlog.done(tile);
 }
 
-// ---------------------------------------------------------------- MFMA-reduced block backward
-// raster_bwd8_kernel's geometry and per-pixel arithmetic, with the per-Gaussian sums over the
-// block's 64 pixels done by the matrix cores instead of a cross-lane reduce-scatter.  Every
-// record moment is a pixel-feature-weighted sum of one of two per-pixel scalars,
-// w = vis * v_alpha and fac = alpha * T:
-//   sum w F(p) for F in {1, u, v, u^2, u v, v^2}    (u, v: the pixel's position in the block)
-//   sum fac v_c(p) for c in {r, g, b}
-// so for a group of 8 staged Gaussians they are ONE matrix product
-//   D[16 features x 16 columns] = A[16 x 64 pixels] . B[64 pixels x 16 columns],
-// A = the wave's pixel features (rows 0-5 geometric, 6-8 the upstream colour, constant per
-// wave: 16 registers), B = (w of the 8 Gaussians | fac of the 8 Gaussians): 16
-// v_mfma_f32_16x16x4_f32 (K = 4 pixels each; exact f32, a k-ordered fma chain).  Each lane
-// writes its pixel's w / fac into a per-wave LDS image laid out so that every MFMA's B operand
-// is 4 contiguous ds_read_b128 per lane (conflict-free); the 8 Gaussians' local moments are
-// re-centred on the Gaussian (d = xy - pixel: Sx = gx' S0 - Su, ...) in 16 lanes and added to
-// the records with 3 atomic instructions per group.  The VALU keeps only the per-pixel blend
-// arithmetic (~28 instructions per pixel-Gaussian pair), and the matrix pipe -- idle in every
-// other rasterizer kernel -- does the reduction (16 MFMAs = 512 cycles per group of 8, run by
-// the SIMD alongside other waves' VALU work).
-typedef float f4v __attribute__((ext_vector_type(4)));
-constexpr int BM_K = 264;   // LDS image: (pixel p, column j) at BM_K (p & 3) + BM_J j + (p >> 2)
-constexpr int BM_J = 20;    // (16-B aligned rows; ds_read_b128 over 16 lanes hits 64 banks)
-constexpr int BM_FLOATS = BM_K * 3 + BM_J * 15 + 16;  // 1108
-template <bool CHUNKED = false, bool DET = false, bool CNT = false>
-__global__ __launch_bounds__(256) void raster_bwdm_kernel(
-    int tbx, int tby, int H, int W, const int *__restrict__ gids, const int2 *__restrict__ bins,
-    const float2 *__restrict__ xys, const float *__restrict__ conics,
-    const float *__restrict__ colors, const float *__restrict__ opacity,
-    const float *__restrict__ background, const float *__restrict__ final_Ts,
-    const int *__restrict__ final_idx, const float *__restrict__ v_out,
-    const float *__restrict__ v_out_alpha, float alpha_max, float *__restrict__ rec,
-    int chunk = 0, const int *__restrict__ item_off = nullptr,
-    const int *__restrict__ item_tile = nullptr, const int *__restrict__ ckpt_off = nullptr,
-    const float4 *__restrict__ ckpt = nullptr, unsigned long long *__restrict__ det = nullptr) {
-  int ctile = -1, cj = 0;
-  if (CHUNKED) {
-    const int slot = wave_slot<1, 8>();
-    if (slot >= item_off[tbx * tby]) return;  // wave-uniform: past the last item
-    ctile = item_tile[slot];
-    cj = slot - item_off[ctile];
-  }
-  const WaveLog wlog;
-  const WaveRect R = wave_rect<1, 8>(tbx, tby, H, W, ctile);
-  if (!R.live) return;  // wave-uniform
-  __shared__ GStage lds[4][64];
-  __shared__ __attribute__((aligned(16))) float bmat[4][BM_FLOATS];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int tile = R.tile, j = R.j, i = R.i0;
-  const float px = (float)j, py = (float)i;
-  const float c0 = R.rx0, r0 = R.ry0;  // the block's origin: u = j - c0 = lane & 7, v = lane >> 3
-  float T = 0.f, vr = 0.f, vg = 0.f, vb = 0.f, q = 0.f, Sb = 0.f;
-  int bf = -1;
-  const bool inside = i < H && j < W;
-  if (inside) {
-    const int pix = i * W + j;
-    T = final_Ts[pix];
-    bf = final_idx[pix];
-    vr = v_out[3 * pix];
-    vg = v_out[3 * pix + 1];
-    vb = v_out[3 * pix + 2];
-    const float a = v_out_alpha ? v_out_alpha[pix] : 0.f;
-    q = T * (a - (background[0] * vr + background[1] * vg + background[2] * vb));
-  }
-  const int2 range = bins[tile];
-  int lo = range.x, hi = range.y;
-  if (CHUNKED) {
-    const int len = range.y - range.x;
-    const int m = len > chunk ? (len + chunk - 1) / chunk : 1;
-    if (m > 1) {
-      lo = range.x + cj * chunk;
-      hi = min(lo + chunk, range.y);
-      if (cj < m - 1 && inside) {
-        const size_t cb = (size_t)ckpt_off[tile] * (GS_BLOCK * GS_BLOCK);
-        const int lpix = (i - (tile / tbx) * GS_BLOCK) * GS_BLOCK + (j - (tile % tbx) * GS_BLOCK);
-        const float4 c4 = ckpt[cb + (size_t)cj * (GS_BLOCK * GS_BLOCK) + lpix];
-        const float4 f4 = ckpt[cb + (size_t)(m - 1) * (GS_BLOCK * GS_BLOCK) + lpix];
-        T = c4.x;
-        Sb = (f4.y - c4.y) * vr + (f4.z - c4.z) * vg + (f4.w - c4.w) * vb;
-      }
-    }
-  }
-  const int maxbin = wave_max_int(bf);
-  float *bm = bmat[wave];
-  // A operand of MFMA s (pixels 4s .. 4s + 3): lane l holds feature l & 15 of pixel 4s + (l >> 4)
-  // (the colour rows read the other lanes' upstream gradient through the LDS image)
-  bm[3 * lane] = vr;
-  bm[3 * lane + 1] = vg;
-  bm[3 * lane + 2] = vb;
-  wave_lds_sync();
-  const int feat = lane & 15, kq = lane >> 4;
-  float amat[16];
-#pragma unroll
-  for (int s = 0; s < 16; ++s) {
-    const int p = 4 * s + kq;
-    const float u = (float)(p & 7), v = (float)(p >> 3);
-    float a = 0.f;
-    if (feat == 0) a = 1.f;
-    else if (feat == 1) a = u;
-    else if (feat == 2) a = v;
-    else if (feat == 3) a = u * u;
-    else if (feat == 4) a = u * v;
-    else if (feat == 5) a = v * v;
-    else if (feat < 9) a = bm[3 * p + feat - 6];
-    amat[s] = a;
-  }
-  wave_lds_sync();
-  const int wbase = BM_K * (lane & 3) + (lane >> 2);     // this pixel's row in the image
-  const int rbase = BM_K * kq + BM_J * feat;             // this lane's B operand column
-  // epilogue roles: lanes 0-7 / 16-23 own Gaussian (lane & 7)'s geometric fields, lanes 24-31
-  // and 40-47 its colour fields
-  const int gc = lane & 7;
-  const bool geo0 = lane < 8, geo1 = lane >= 16 && lane < 24, colrg = lane >= 24 && lane < 32,
-             colb = lane >= 40 && lane < 48;
-  const float amax = __builtin_canonicalizef(alpha_max);
-  const int last = min(maxbin, hi - 1);
-  GStage *stage = lds[wave];
-  unsigned c_slots = 0, c_live = 0, c_valid = 0;  // (CNT only)
-  for (int b = last; b >= lo; b -= 64) {
-    const int idx = b - lane;
-    GStage s;
-    const bool keep = idx >= lo && stage_gaussian<true>(idx, gids, xys, conics, colors, opacity,
-                                                        R.rx0, R.rx1, R.ry0, R.ry1, s);
-    const unsigned long long kmask = __ballot(keep);
-    if (keep) stage[lanes_below(kmask)] = s;
-    const int n = __popcll(kmask);
-    wave_lds_sync();
-    for (int t = 0; t < n; t += 8) {  // groups of up to 8 staged Gaussians
-      const int cnt = min(8, n - t);
-      unsigned long long anyv = 0;
-      for (int u = 0; u < cnt; u += 2) {  // two per step, as raster_bwd8_kernel
-        GStage G0 = stage[t + u], G1 = stage[min(t + u + 1, 63)];
-        const bool live1 = u + 1 < cnt;
-        if (!live1) G1.r = G1.g = G1.bl = G1.o = 0.f;
-        const float dx0 = G0.x - px, dy0 = G0.y - py, dx1 = G1.x - px, dy1 = G1.y - py;
-        const float sg0 = gs_sigma(G0.hc, G0.b * dx0, G0.ha * dx0 * dx0, dy0);
-        const float sg1 = gs_sigma(G1.hc, G1.b * dx1, G1.ha * dx1 * dx1, dy1);
-        const float vis0 = gs_vis(sg0), vis1 = gs_vis(sg1);
-        const float al0 = fminf(amax, G0.o * vis0), al1 = fminf(amax, G1.o * vis1);
-        const bool v0 = G0.idx <= bf && sg0 >= 0.f && al0 >= ALPHA_MIN;
-        const bool v1 = live1 && G1.idx <= bf && sg1 >= 0.f && al1 >= ALPHA_MIN;
-        anyv |= __builtin_amdgcn_ballot_w64(v0 || v1);
-        if constexpr (CNT) {
-          c_slots += (live1 ? 2 : 1) * 64;
-          c_live += (G0.idx <= bf ? 1u : 0u) + (live1 && G1.idx <= bf ? 1u : 0u);
-          c_valid += (v0 ? 1u : 0u) + (v1 ? 1u : 0u);
-        }
-        const float am0 = v0 ? al0 : 0.f, am1 = v1 ? al1 : 0.f;
-        const float ra0 = __builtin_amdgcn_rcpf(1.f - am0);
-        T = T * ra0;
-        const float fac0 = am0 * T;
-        const float gv0 = fmaf(G0.r, vr, fmaf(G0.g, vg, G0.bl * vb));
-        const float va0 = fmaf(gv0, T, ra0 * (q - Sb));
-        Sb = fmaf(fac0, gv0, Sb);
-        const float ra1 = __builtin_amdgcn_rcpf(1.f - am1);
-        T = T * ra1;
-        const float fac1 = am1 * T;
-        const float gv1 = fmaf(G1.r, vr, fmaf(G1.g, vg, G1.bl * vb));
-        const float va1 = fmaf(gv1, T, ra1 * (q - Sb));
-        Sb = fmaf(fac1, gv1, Sb);
-        bm[wbase + BM_J * u] = (v0 ? vis0 : 0.f) * va0;
-        bm[wbase + BM_J * (8 + u)] = fac0;
-        bm[wbase + BM_J * (u + 1)] = (v1 ? vis1 : 0.f) * va1;  // (u + 1 <= 7: cnt <= 8)
-        bm[wbase + BM_J * (9 + u)] = fac1;
-      }
-      if (!anyv) continue;  // (SGPR test) no pixel of the block composites this group
-      wave_lds_sync();
-      // D = A . B over the 64 pixels: 16 MFMAs, two accumulators (40-cycle dependency)
-      float bv[16];
-#pragma unroll
-      for (int k4 = 0; k4 < 4; ++k4) {
-        const float4 x = *reinterpret_cast<const float4 *>(bm + rbase + 4 * k4);
-        bv[4 * k4] = x.x;
-        bv[4 * k4 + 1] = x.y;
-        bv[4 * k4 + 2] = x.z;
-        bv[4 * k4 + 3] = x.w;
-      }
-      f4v acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s2 = 0; s2 < 16; s2 += 2) {
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(amat[s2], bv[s2], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(amat[s2 + 1], bv[s2 + 1], acc1, 0, 0, 0);
-      }
-      const f4v acc = acc0 + acc1;  // lane l: D[4 (l >> 4) + r][l & 15]
-      // local moments of Gaussian gc: S0 Su Sv Suu in lane gc (column gc, rows 0-3), Suv Svv
-      // in lane gc + 16 (rows 4, 5); exchange so that both lanes hold all six
-      const float x0 = __shfl_xor(acc[0], 16), x1 = __shfl_xor(acc[1], 16),
-                  x2 = __shfl_xor(acc[2], 16), x3 = __shfl_xor(acc[3], 16);
-      const bool lo16 = lane < 16;
-      const float S0 = lo16 ? acc[0] : x0, Su = lo16 ? acc[1] : x1, Sv = lo16 ? acc[2] : x2,
-                  Suu = lo16 ? acc[3] : x3, Suv = lo16 ? x0 : acc[0], Svv = lo16 ? x1 : acc[1];
-      const GStage &Gc = stage[t + gc];
-      const float gx = Gc.x - c0, gy = Gc.y - r0;  // the Gaussian's mean in block coordinates
-      const int gid = Gc.id;
-      const float Sx = fmaf(gx, S0, -Su), Sy = fmaf(gy, S0, -Sv);
-      float v1 = 0.f, v2 = 0.f, v3 = 0.f;
-      int f1 = 0, f2 = 0, f3 = 0;
-      if (geo0) {
-        v1 = Sx; f1 = REC_SX;
-        v2 = Sy; f2 = REC_SY;
-        v3 = fmaf(gx, Sx - Su, Suu); f3 = REC_SXX;           // gx^2 S0 - 2 gx Su + Suu
-      } else if (geo1) {
-        v1 = fmaf(gx, Sy, fmaf(-gy, Su, Suv)); f1 = REC_SXY;  // gx gy S0 - gx Sv - gy Su + Suv
-        v2 = fmaf(gy, Sy - Sv, Svv); f2 = REC_SYY;           // gy^2 S0 - 2 gy Sv + Svv
-        v3 = S0; f3 = REC_S0;
-      } else if (colrg) {
-        v1 = acc[2]; f1 = REC_R;  // row 6 (column 8 + gc: fac)
-        v2 = acc[3]; f2 = REC_G;  // row 7
-      } else if (colb) {
-        v1 = acc[0]; f1 = REC_B;  // row 8
-      }
-      const bool mine = gc < cnt && (geo0 || geo1 || colrg || colb);
-      if (mine) {
-        if constexpr (DET) {
-          unsigned long long *d = det + (size_t)gid * REC_FIELDS * DET_LIMBS;
-          det_add(d + f1 * DET_LIMBS, v1);
-          if (!colb) det_add(d + f2 * DET_LIMBS, v2);
-          if (geo0 || geo1) det_add(d + f3 * DET_LIMBS, v3);
-        } else {
-          float *r = rec + (uint32_t)(gid * REC);
-          atomicAdd(r + f1, v1);
-          if (!colb) atomicAdd(r + f2, v2);
-          if (geo0 || geo1) atomicAdd(r + f3, v3);
-        }
-      }
-      wave_lds_sync();  // the next group's writes reuse the image
-    }
-    wave_lds_sync();
-  }
-  if constexpr (CNT) pair_count_flush(0, c_slots, c_live, c_valid);
-  wlog.done(tile);
-}
-
 // List-split plan (one workgroup): per tile, the number of backward items (chunks of the
 // depth-sorted list, 1 for a tile no longer than `chunk`, 0 for an empty one) and of forward
 // checkpoints (as many as chunks for a split tile, else 0); exclusive scans of both give
@@ -1557,7 +1325,7 @@ static bool default_variants() {
 
 extern "C" int gsplat_rasterize_chunk_size(int tile_bounds_x, int tile_bounds_y,
                                            int64_t num_intersects) {
-  if (g_chunk_override < 0 || !default_variants() || num_intersects <= 0) return 0;
+  if (g_chunk_override < 0 || num_intersects <= 0) return 0;
   if (g_chunk_override > 0) return (g_chunk_override + 63) / 64 * 64;
   // Split only frames with too few tiles to occupy the chip: the backward runs 2 waves per
   // tile and ~7 fit per SIMD (7,168 on 256 CUs), so below ~3,584 tiles (e.g. 512x512 =
@@ -1660,9 +1428,9 @@ extern "C" int gsplat_rasterize_forward_rgbd(int tile_bounds_x, int tile_bounds_
 // Measurement knob: bwd_pxl picks the backward geometry (BWD_PXL above); bits 20-27 of flags
 // the XCD chunk of the blend kernels' block order (0 the default K = 8, 255 dispatch order).
 extern "C" int gsplat_debug_set_raster_variant(int fwd_pxl, int bwd_pxl, int bwd_flags) {
-  if (fwd_pxl != 1 || bwd_pxl < 1 || bwd_pxl > 3 || (bwd_flags & ~(0xff << 20))) {
-    set_error("debug_set_raster_variant: fwd_pxl must be 1, bwd_pxl 1 (8x8 blocks) or 2 "
-              "(16x8 strips), flags only the XCD chunk (bits 20-27)");
+  if (fwd_pxl != 1 || bwd_pxl < 0 || bwd_pxl > 2 || (bwd_flags & ~(0xff << 20))) {
+    set_error("debug_set_raster_variant: fwd_pxl must be 1, bwd_pxl 0 (by frame size), 1 (8x8 "
+              "blocks) or 2 (16x8 strips), flags only the XCD chunk (bits 20-27)");
     return 1;
   }
   g_fwd_pxl = fwd_pxl;
@@ -1704,6 +1472,16 @@ extern "C" int gsplat_debug_pair_count(void *buffer) {
   return 0;
 }
 
+// Backward geometry of a frame: the 8x8 blocks (4 waves per tile) for frames with few tiles,
+// where the strips' 2 waves per tile leave SIMDs idle (512^2, c3 bear: 0.231 -> 0.160 ms
+// without the list split); the 16x8 strips from 3,584 tiles up, where the chip is full and
+// their reduce-scatter per 128 pixels (against one per 64) is cheaper per pixel-Gaussian pair
+// (headline 0.296 vs 0.308 ms, c4 0.364 vs 0.367, c5 0.692 vs 0.806; profiles/r03_bwd_geometry.txt).
+static int bwd_geometry(int tbx, int tby) {
+  if (g_bwd_pxl) return g_bwd_pxl;
+  return (long long)tbx * tby < 3584 ? 1 : 2;
+}
+
 // The C = 3 backward into the records `rec` (which the caller cleared), with the list split
 // when w != NULL, the integer accumulators when det != NULL (then det_finish_kernel writes the
 // records), the lane-slot counting instantiation when the pair-count hook is on.
@@ -1718,22 +1496,7 @@ static void launch_bwd(hipStream_t st, int tbx, int tby, int H, int W, int n,
             *co = w ? w->ckpt_off : nullptr;
   const float4 *ck = w ? w->ckpt : nullptr;
   const bool cnt = g_pair_count_on && !det;
-  if (g_bwd_pxl == 3) {
-    const unsigned grid = cdiv(slots, (tiles_per_block<1, 8>()));
-#define BWDM(CH, DET, CNT)                                                                 \
-  hipLaunchKernelGGL((raster_bwdm_kernel<CH, DET, CNT>), dim3(grid), dim3(256), 0, st, tbx, tby, \
-                     H, W, gids, (const int2 *)bins, (const float2 *)xys, conics, colors,       \
-                     opacity, background, final_Ts, final_idx, v_output, v_output_alpha,        \
-                     alpha_max, rec, chunk, io, it, co, ck, det)
-    if (w) {
-      if (det) BWDM(true, true, false); else if (cnt) BWDM(true, false, true);
-      else BWDM(true, false, false);
-    } else {
-      if (det) BWDM(false, true, false); else if (cnt) BWDM(false, false, true);
-      else BWDM(false, false, false);
-    }
-#undef BWDM
-  } else if (g_bwd_pxl == 1) {
+  if (bwd_geometry(tbx, tby) == 1) {
     const unsigned grid = cdiv(slots, (tiles_per_block<1, 8>()));
 #define BWD8(CH, DET, CNT)                                                                 \
   hipLaunchKernelGGL((raster_bwd8_kernel<CH, DET, CNT>), dim3(grid), dim3(256), 0, st, tbx, tby, \

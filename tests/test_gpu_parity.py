@@ -318,25 +318,37 @@ def test_raster_backward(gpu, case, quirk_mask):
     _check_raster_backward(gpu, case)
 
 
-# (fwd pixels/lane, bwd pixels/lane, flags): see gsplat_debug_set_raster_variant in
-# include/gsplat_mi355x.h -- bwd 2 = the 16x8-strip backward kept for A/B timing; K << 20 the
-# blend kernels' block order in chunks of K block slots per XCD (shipped K = 8; 255 << 20 plain
-# dispatch order).
-RASTER_VARIANTS = [(1, 2, 0), (1, 3, 0), (1, 1, 255 << 20), (1, 1, 1 << 20), (1, 1, 3 << 20)]
+@pytest.mark.parametrize("quirk_mask", [7, 0], indirect=True)
+@pytest.mark.parametrize("bwd", [1, 2])
+@pytest.mark.parametrize("case", CASES)
+def test_raster_backward_geometries(gpu, case, bwd, quirk_mask):
+    """Both shipped backward geometries on every case, whatever the frame size picks: 8x8 blocks
+    (bwd 1, small frames) and 16x8 strips (bwd 2, from 3,584 tiles)."""
+    _lib.call("gsplat_debug_set_raster_variant", 1, bwd, 0)
+    try:
+        _check_raster_backward(gpu, case)
+    finally:
+        _lib.call("gsplat_debug_set_raster_variant", 1, 0, 0)
+
+
+# (fwd pixels/lane, bwd geometry, flags): see gsplat_debug_set_raster_variant in
+# include/gsplat_mi355x.h -- K << 20 the blend kernels' block order in chunks of K block slots
+# per XCD (shipped K = 8; 255 << 20 plain dispatch order).
+RASTER_VARIANTS = [(1, 0, 255 << 20), (1, 0, 1 << 20), (1, 0, 3 << 20)]
 
 
 @pytest.mark.ablation
 @pytest.mark.parametrize("variant", RASTER_VARIANTS)
 @pytest.mark.parametrize("case", [CASES[0], CASES[1], CASES[3]])
 def test_raster_variants(gpu, case, variant):
-    """Every blend-kernel variant reachable through gsplat_debug_set_raster_variant meets the
+    """Every blend-kernel block order reachable through gsplat_debug_set_raster_variant meets the
     same bar as the shipped one."""
     _lib.call("gsplat_debug_set_raster_variant", *variant)
     try:
         _check_raster_forward(gpu, case)
         _check_raster_backward(gpu, case)
     finally:
-        _lib.call("gsplat_debug_set_raster_variant", 1, 1, 0)
+        _lib.call("gsplat_debug_set_raster_variant", 1, 0, 0)
 
 
 def _check_raster_backward(gpu, case):
@@ -376,7 +388,7 @@ def _check_raster_backward(gpu, case):
         assert frac == 0.0, f"{name}: {frac:.2e} out of tolerance (max {mx:.3e})"
 
 
-@pytest.mark.parametrize("bwd", [1, pytest.param(2, marks=pytest.mark.ablation), pytest.param(3, marks=pytest.mark.ablation)])
+@pytest.mark.parametrize("bwd", [1, 2])
 @pytest.mark.parametrize("chunk", [64, 128, 256])
 @pytest.mark.parametrize("case", CASES[1:3])
 def test_raster_backward_list_split(gpu, case, chunk, bwd):
@@ -390,7 +402,7 @@ def test_raster_backward_list_split(gpu, case, chunk, bwd):
         _check_raster_backward(gpu, case)
     finally:
         _lib.call("gsplat_debug_set_chunk", 0)
-        _lib.call("gsplat_debug_set_raster_variant", 1, 1, 0)
+        _lib.call("gsplat_debug_set_raster_variant", 1, 0, 0)
 
 
 @pytest.mark.parametrize("quirk_mask", [7, 0], indirect=True)

@@ -76,7 +76,7 @@ for rnd in range(5):
         _lib.call("gsplat_debug_set_raster_variant", *f)
         g = grads[f]
         res[f].append(timeit(lambda: bwd(g)))
-_lib.call("gsplat_debug_set_raster_variant", 1, 1, 0)
+_lib.call("gsplat_debug_set_raster_variant", 1, 0, 0)
 print(f"{cfg}: N={N} I={I} tiles={tb[0]*tb[1]}")
 for f in variants:
     print(f"bwd variant={f}: {np.median(res[f]):.4f} ms  (rounds {np.round(res[f], 4).tolist()})")
