@@ -143,6 +143,16 @@ PMC_TRAFFIC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles
                            "pmc_traffic.json")
 
 
+def _pmc_entry(entry, config):
+    """Per-call counter sums of a C-ABI entry whose kernels the PMC summary attributed by
+    dispatch order (the binning: tools/pmc_summary.py), or None."""
+    try:
+        with open(PMC_TRAFFIC) as f:
+            return json.load(f)["configs"][config]["entries"][entry]
+    except (OSError, ValueError, KeyError):
+        return None
+
+
 def _pmc_kernels(config):
     """The committed rocprofv3 PMC summary of `config` (profiles/pmc_traffic.json, written by
     tools/pmc_bench.sh + tools/pmc_summary.py on that config), or None: counters collected on
@@ -157,6 +167,9 @@ def _pmc_kernels(config):
 def pmc_traffic(entry, config):
     """HBM bytes per call of a C-ABI entry on `config`: FETCH_SIZE (x2 only for streaming
     16-B-per-lane kernels, see ENTRY_KERNELS) + WRITE_SIZE; None without counters."""
+    e = _pmc_entry(entry, config)
+    if e and e.get("fetch_kb") is not None:  # binning entries: raw FETCH_SIZE (gathers)
+        return int((e["fetch_kb"] + (e.get("write_kb") or 0.0)) * 1024.0)
     kern = _pmc_kernels(config)
     pats, streaming = ENTRY_KERNELS.get(entry, ((), False))
     if not kern or not pats:
@@ -176,6 +189,9 @@ def pmc_valu_busy(entry, config, ms_per_call, n_simd=256 * 4, clock_hz=2.4e9):
     op held it for 4 cycles.  gfx950's 32-lane SIMD issues one in 2 (MI355X_MICROARCH.md), so
     this overstates the issue share ~2x; valu_issue_frac (pmc_issue_and_wait) is the issue
     bound, wait_frac the stall share.  None without that config's counters."""
+    e = _pmc_entry(entry, config)
+    if e and e.get("valu_quad_cycles") is not None and ms_per_call:
+        return round(e["valu_quad_cycles"] / (n_simd * ms_per_call * 1e-3 * clock_hz / 4.0), 3)
     kern = _pmc_kernels(config)
     pats, _ = ENTRY_KERNELS.get(entry, ((), False))
     if not kern or not pats or not ms_per_call:
@@ -189,29 +205,35 @@ def pmc_valu_busy(entry, config, ms_per_call, n_simd=256 * 4, clock_hz=2.4e9):
 
 
 def pmc_issue_and_wait(entry, config, ms_per_call, n_simd=256 * 4, clock_hz=2.4e9):
-    """(valu_issue_frac, wait_frac) of the entry's kernels on `config`: the lower bound on the
-    SIMD issue cycles its VALU instructions take -- SQ_INSTS_VALU x 2 cycles (a wave64 VALU op
-    issues over 2 cycles on gfx950's 32-lane SIMD) + SQ_INSTS_VALU_TRANS_F32 x 2 more (a
-    transcendental takes 4), packed ops counted at the scalar cost -- per SIMD-cycle of the
-    call, and SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES, the share of its waves' lifetime spent stalled
-    on s_waitcnt.  (None, None) without that config's counters."""
-    kern = _pmc_kernels(config)
-    pats, _ = ENTRY_KERNELS.get(entry, ((), False))
-    if not kern or not pats or not ms_per_call:
-        return None, None
-    iv = it = wi = wc = 0.0
-    hit = False
-    for name, v in kern.items():
-        if any(p in name for p in pats) and v.get("insts_valu") is not None:
-            iv += v["insts_valu"]
-            it += v.get("insts_trans") or 0.0
-            wi += v.get("wait_inst_any") or 0.0
-            wc += v.get("wave_cycles") or 0.0
-            hit = True
-    if not hit:
-        return None, None
+    """(valu_issue_frac, wait_frac, issue_stall_frac) of the entry's kernels on `config`: the
+    lower bound on the SIMD issue cycles its VALU instructions take -- SQ_INSTS_VALU x 2 cycles
+    (a wave64 VALU op issues over 2 cycles on gfx950's 32-lane SIMD) + SQ_INSTS_VALU_TRANS_F32
+    x 2 more (a transcendental takes 4), packed ops counted at the scalar cost -- per
+    SIMD-cycle of the call; SQ_WAIT_ANY / SQ_WAVE_CYCLES, the share of its waves' lifetime
+    parked on s_waitcnt / barriers; SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES, the share spent ready but
+    not issuing (dependency / pipe / arbitration stalls; MI355X_MICROARCH.md counter table).
+    Nones without that config's counters."""
+    e = _pmc_entry(entry, config)
+    if e and e.get("insts_valu") is not None:
+        rows = [e]
+    else:
+        kern = _pmc_kernels(config)
+        pats, _ = ENTRY_KERNELS.get(entry, ((), False))
+        if not kern or not pats:
+            return None, None, None
+        rows = [v for name, v in kern.items()
+                if any(p in name for p in pats) and v.get("insts_valu") is not None]
+    if not rows or not ms_per_call:
+        return None, None, None
+    iv = sum(v["insts_valu"] for v in rows)
+    it = sum(v.get("insts_trans") or 0.0 for v in rows)
+    wa = sum(v.get("wait_any") or 0.0 for v in rows)
+    wi = sum(v.get("wait_inst_any") or 0.0 for v in rows)
+    wc = sum(v.get("wave_cycles") or 0.0 for v in rows)
     issue = (2.0 * iv + 2.0 * it) / (n_simd * ms_per_call * 1e-3 * clock_hz)
-    return round(issue, 3), (round(wi / wc, 3) if wc else None)
+    has_wa = any(v.get("wait_any") is not None for v in rows)
+    return (round(issue, 3), (round(wa / wc, 3) if wc and has_wa else None),
+            (round(wi / wc, 3) if wc else None))
 
 
 def pmc_insts_valu(entry, config):
@@ -364,6 +386,42 @@ def c_oracle_baseline(scene, cam, sh_degree, budget_tiles=64, seed=0):
     }
 
 
+def exchange_profile(scene, cam, gt, bg, deg, world, dev, steps, timed):
+    """N > 1 only: what the data-parallel exchange costs this rank and how much of it the step
+    hides.  Times (max over ranks, same `steps`): the step's compute alone (the
+    same render + loss + backward on a world-size-1 TrainStep: no collectives), the SH record
+    all-gather alone and the flat all-reduce of the other four gradients alone, and reports
+    the bytes each rank moves.  hidden_frac = 1 - (t_step - t_compute) / (t_allgather +
+    t_allreduce): the share of the collectives' time that overlapped compute."""
+    n = scene.num_points
+    solo = TrainStep(scene, sh_degree=deg, world_size=1, loss="l1", render_mode="fused")
+
+    def compute_only():
+        solo.zero_grad()
+        solo.forward_backward(cam, gt, bg)
+    for _ in range(3):
+        compute_only()
+    t_comp = timed(compute_only, steps) / steps * 1e3
+    rec = torch.zeros(3 * n + 4, device=dev)
+    gathered = torch.empty(world * (3 * n + 4), device=dev)
+    flat = torch.zeros(11 * n, device=dev)  # means 3 + scales 3 + quats 4 + opacity 1 floats
+    for _ in range(3):
+        dist.all_gather_into_tensor(gathered, rec)
+        dist.all_reduce(flat)
+    t_ag = timed(lambda: dist.all_gather_into_tensor(gathered, rec), steps) / steps * 1e3
+    t_ar = timed(lambda: dist.all_reduce(flat), steps) / steps * 1e3
+    for p in scene.params():
+        p.grad = None
+    return {
+        "t_compute_only_ms": round(t_comp, 4),
+        "t_allgather_ms": round(t_ag, 4),
+        "t_allreduce_ms": round(t_ar, 4),
+        "bytes_allgather_recv_per_rank": (world - 1) * (3 * n + 4) * 4,
+        "bytes_allreduce_per_rank": int(2 * (world - 1) / world * 11 * n * 4),  # ring send+recv
+        "collectives_per_step": 2,
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -456,6 +514,14 @@ def main():
         dt = float(t.item())
     ms_per_step = dt / args.steps * 1e3
     value = world * H * W * args.steps / dt / 1e6
+    exch = None
+    if world > 1 and not fwd_only:
+        exch = exchange_profile(scene, cam, gt, bg, deg, world, dev, args.steps, timed)
+        comm = exch["t_allgather_ms"] + exch["t_allreduce_ms"]
+        exch["t_step_ms"] = round(ms_per_step, 4)
+        exch["exposed_ms"] = round(ms_per_step - exch["t_compute_only_ms"], 4)
+        exch["hidden_frac"] = round(1 - exch["exposed_ms"] / comm, 3) if comm > 0 else None
+        exch["backend"] = backend
     # the same step through the unchanged caller's torch glue (gc_model.py as it runs on the
     # gsplat drop-in), for comparison
     for _ in range(max(args.warmup // 2, 1)):
@@ -505,6 +571,7 @@ def main():
         "valu_busy": pmc_valu_busy(dom, args.config, dom_ms),
         "valu_issue_frac": pmc_issue_and_wait(dom, args.config, dom_ms)[0],
         "wait_frac": pmc_issue_and_wait(dom, args.config, dom_ms)[1],
+        "issue_stall_frac": pmc_issue_and_wait(dom, args.config, dom_ms)[2],
         "step_algorithmic_bytes": step_bytes,
         "step_frac": round(step_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
         "roofline_mpix_s": round(P / (step_bytes / (HBM_PEAK_GBS * 1e9)) / 1e6, 1),
@@ -564,6 +631,7 @@ def main():
                                else "dp1",
             },
             "render": args.render,
+            "exchange": exch,
             "value_unchanged_caller": round(caller_value, 2),
             "train_iters_per_s": round(tsteps / tdt, 2),
             "train_views_per_s": round(world * tsteps / tdt, 2),

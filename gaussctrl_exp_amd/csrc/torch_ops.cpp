@@ -15,6 +15,7 @@
 //   raster_fwd       gsplat_rasterize_forward                  _C.rasterize_forward / nd_...
 //   raster_bwd       gsplat_rasterize_backward                 _C.rasterize_backward / nd_...
 // (the reference's call sites: gc_model.py:174-236 through gsplat's autograd wrappers)
+#include <c10/core/DeviceGuard.h>
 #include <c10/hip/HIPStream.h>
 #include <torch/library.h>
 
@@ -34,8 +35,13 @@ void check(int rc, const char *what) {
   TORCH_CHECK(rc == 0, "gsplat_mi355x::", what, ": ", gsplat_last_error());
 }
 
+// Every op runs its launcher on the device of its first tensor argument (a device guard makes it
+// current) and requires all its tensors there.
+thread_local c10::Device g_op_device = c10::Device(c10::kCPU);
 void need(const Tensor &t, const char *name, at::ScalarType dt) {
   TORCH_CHECK(t.is_cuda(), "gsplat_mi355x: ", name, " must be a ROCm device tensor");
+  TORCH_CHECK(g_op_device.is_cpu() || t.device() == g_op_device, "gsplat_mi355x: ", name,
+              " is on ", t.device(), ", the op's other tensors on ", g_op_device);
   TORCH_CHECK(t.scalar_type() == dt, "gsplat_mi355x: ", name, " must be ", dt, ", got ",
               t.scalar_type());
   TORCH_CHECK(t.is_contiguous(), "gsplat_mi355x: ", name, " must be contiguous");
@@ -45,6 +51,16 @@ void need_rows(const Tensor &t, const char *name, int64_t n, int64_t cols) {
   TORCH_CHECK(t.numel() == n * cols, "gsplat_mi355x: ", name, " must hold ", n, " x ", cols,
               " values, got shape ", t.sizes());
 }
+
+struct OpDevice {  // the op's device: guard + same-device checks in need()
+  c10::OptionalDeviceGuard guard;
+  explicit OpDevice(const Tensor &first) {
+    TORCH_CHECK(first.is_cuda(), "gsplat_mi355x: expected ROCm device tensors (no CPU path)");
+    guard.reset_device(first.device());
+    g_op_device = first.device();
+  }
+  ~OpDevice() { g_op_device = c10::Device(c10::kCPU); }
+};
 
 int sh_bases(int64_t degree) {
   TORCH_CHECK(degree >= 0 && degree <= 4, "gsplat_mi355x: SH degree must be in [0, 4]");
@@ -61,6 +77,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> project_fwd(
     int64_t img_height, int64_t img_width, int64_t tile_bounds_x, int64_t tile_bounds_y,
     double clip_thresh) {
   const int64_t n = means3d.size(0);
+  OpDevice od(means3d);
   need(means3d, "means3d", at::kFloat);
   need(scales, "scales", at::kFloat);
   need(quats, "quats", at::kFloat);
@@ -92,6 +109,7 @@ std::tuple<Tensor, Tensor, Tensor> project_bwd(
     const Tensor &conics, const Tensor &v_xy, const c10::optional<Tensor> &v_depth,
     const Tensor &v_conic) {
   const int64_t n = means3d.size(0);
+  OpDevice od(means3d);
   need(means3d, "means3d", at::kFloat);
   need(scales, "scales", at::kFloat);
   need(quats, "quats", at::kFloat);
@@ -102,6 +120,14 @@ std::tuple<Tensor, Tensor, Tensor> project_bwd(
   need(conics, "conics", at::kFloat);
   need(v_xy, "v_xy", at::kFloat);
   need(v_conic, "v_conic", at::kFloat);
+  need_rows(means3d, "means3d", n, 3);
+  need_rows(scales, "scales", n, 3);
+  need_rows(quats, "quats", n, 4);
+  need_rows(cov3d, "cov3d", n, 6);
+  need_rows(radii, "radii", n, 1);
+  need_rows(conics, "conics", n, 3);
+  TORCH_CHECK(viewmat.numel() >= 12 && projmat.numel() == 16,
+              "gsplat_mi355x: viewmat needs >= 12 values, projmat 16");
   need_rows(v_xy, "v_xy", n, 2);
   need_rows(v_conic, "v_conic", n, 3);
   const float *vd = nullptr;
@@ -127,6 +153,7 @@ std::tuple<Tensor, Tensor, Tensor> project_bwd(
 Tensor sh_fwd(int64_t degree, int64_t degrees_to_use, const Tensor &viewdirs,
               const Tensor &coeffs) {
   const int64_t n = viewdirs.size(0);
+  OpDevice od(viewdirs);
   const int K = sh_bases(degree);
   need(viewdirs, "viewdirs", at::kFloat);
   need(coeffs, "coeffs", at::kFloat);
@@ -143,6 +170,7 @@ Tensor sh_fwd(int64_t degree, int64_t degrees_to_use, const Tensor &viewdirs,
 Tensor sh_bwd(int64_t degree, int64_t degrees_to_use, const Tensor &viewdirs,
               const Tensor &v_colors) {
   const int64_t n = viewdirs.size(0);
+  OpDevice od(viewdirs);
   const int K = sh_bases(degree);
   need(viewdirs, "viewdirs", at::kFloat);
   need(v_colors, "v_colors", at::kFloat);
@@ -162,11 +190,15 @@ std::tuple<Tensor, Tensor> map_intersects(const Tensor &xys, const Tensor &depth
                                           int64_t tile_bounds_x, int64_t tile_bounds_y,
                                           int64_t num_intersects) {
   const int64_t n = xys.size(0);
+  OpDevice od(xys);
   need(xys, "xys", at::kFloat);
   need(depths, "depths", at::kFloat);
   need(radii, "radii", at::kInt);
   need(cum_tiles_hit, "cum_tiles_hit", at::kInt);
   need_rows(xys, "xys", n, 2);
+  need_rows(depths, "depths", n, 1);
+  need_rows(radii, "radii", n, 1);
+  need_rows(cum_tiles_hit, "cum_tiles_hit", n, 1);
   TORCH_CHECK(num_intersects >= 0, "gsplat_mi355x: num_intersects must be >= 0");
   // zero-filled like gsplat's torch.zeros outputs: slots past cum_tiles_hit[-1] stay 0
   Tensor isect = at::zeros({num_intersects}, xys.options().dtype(at::kLong));
@@ -181,6 +213,7 @@ std::tuple<Tensor, Tensor> map_intersects(const Tensor &xys, const Tensor &depth
 }
 
 std::tuple<Tensor, Tensor> sort_pairs(const Tensor &keys, const Tensor &vals, int64_t key_bits) {
+  OpDevice od(keys);
   need(keys, "keys", at::kLong);
   need(vals, "vals", at::kInt);
   const int64_t m = keys.numel();
@@ -199,6 +232,7 @@ std::tuple<Tensor, Tensor> sort_pairs(const Tensor &keys, const Tensor &vals, in
 }
 
 Tensor tile_bins(const Tensor &isect_ids_sorted, int64_t num_rows) {
+  OpDevice od(isect_ids_sorted);
   need(isect_ids_sorted, "isect_ids_sorted", at::kLong);
   Tensor bins = at::empty({num_rows, 2}, i32(isect_ids_sorted));
   check(gsplat_get_tile_bin_edges(isect_ids_sorted.numel(), isect_ids_sorted.data_ptr<int64_t>(),
@@ -231,6 +265,7 @@ std::tuple<Tensor, Tensor, Tensor> raster_fwd(int64_t tbx, int64_t tby, int64_t 
                                               const Tensor &xys, const Tensor &conics,
                                               const Tensor &colors, const Tensor &opacity,
                                               const Tensor &background) {
+  OpDevice od(xys);
   check_raster_inputs(gids, bins, xys, conics, colors, opacity, background, tbx, tby);
   const int64_t C = colors.size(1);
   Tensor out = at::empty({H, W, C}, f32(xys)), fT = at::empty({H, W}, f32(xys));
@@ -250,11 +285,14 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> raster_bwd(
     const Tensor &xys, const Tensor &conics, const Tensor &colors, const Tensor &opacity,
     const Tensor &background, const Tensor &final_Ts, const Tensor &final_idx,
     const Tensor &v_output, const c10::optional<Tensor> &v_output_alpha, double alpha_max) {
+  OpDevice od(xys);
   check_raster_inputs(gids, bins, xys, conics, colors, opacity, background, tbx, tby);
   need(final_Ts, "final_Ts", at::kFloat);
   need(final_idx, "final_idx", at::kInt);
   need(v_output, "v_output", at::kFloat);
   const int64_t n = xys.size(0), C = colors.size(1);
+  need_rows(final_Ts, "final_Ts", H * W, 1);
+  need_rows(final_idx, "final_idx", H * W, 1);
   need_rows(v_output, "v_output", H * W, C);
   const float *va = nullptr;
   if (v_output_alpha.has_value()) {

@@ -225,13 +225,25 @@ class _KeyedWorkspaces:
     """The depth-sort inputs project_gaussians wrote for its latest outputs
     (gsplat_project_gaussians_forward_binned), handed to the rasterize call that bins exactly
     those outputs -- the same tensor objects (weak references), unmodified (version counters),
-    for the same tile grid, on the same stream.  Single use: the sort consumes the workspace."""
+    for the same tile grid, on the same stream.  Single use: the sort consumes the workspace.
+
+    The entry never outlives its key: it is dropped when taken, when the binning cache
+    answers the rasterize call instead (_binning), and when the projection outputs it was
+    written for are freed (a finalizer on xys) -- so an unrasterized projection does not pin
+    the ~60 B/Gaussian workspace."""
 
     def __init__(self):
         self.cache = _BinCache()
+        self.serial = 0
 
     def put(self, tensors, tbx, tby, ws1):
         self.cache.put(tensors, tbx, tby, _lib.stream(tensors[0].device), ws1)
+        self.serial += 1
+        weakref.finalize(tensors[0], self._expire, self.serial)
+
+    def _expire(self, serial):
+        if serial == self.serial:
+            self.cache.clear()
 
     def take(self, tensors, tbx, tby, stream):
         ws1 = self.cache.get(tensors, tbx, tby, stream)
@@ -249,9 +261,10 @@ def _binning(xys, depths, radii, num_tiles_hit, H, W):
     key_tensors = (xys, depths, radii, num_tiles_hit)
     st = _lib.stream(xys.device)
     hit = _BIN_CACHE.get(key_tensors, H, W, st)
-    if hit is not None:
-        return hit
     tbx, tby = (W + BLOCK_X - 1) // BLOCK_X, (H + BLOCK_Y - 1) // BLOCK_Y
+    if hit is not None:
+        keyed_workspaces.take(key_tensors, tbx, tby, st)  # (unused: release it)
+        return hit
     ws1 = keyed_workspaces.take(key_tensors, tbx, tby, st)
     res = bin_gaussians(xys, depths, radii, num_tiles_hit, H, W, keyed_workspace=ws1)
     _BIN_CACHE.put(key_tensors, H, W, st, res)

@@ -642,16 +642,34 @@ void oracle_rasterize_backward(int tbx, int tby, int H, int W, int C, int num_po
                                const float *v_out, const float *v_out_alpha, float alpha_max,
                                const int *tile_list, int num_tile_list, float *v_xy,
                                float *v_conic, float *v_colors, float *v_opacity,
-                               float *abs_sum) {
+                               float *abs_sum, float *drift_sum, float *flip_sum) {
     /* abs_sum (optional, [num_points, 6+C] in the order xy0 xy1 con0 con1 con2 opac colors):
      * the sum of |term| over the per-pixel contributions of each gradient element -- the
-     * scale of the fp32 summation error any implementation accumulating in fp32 incurs. */
+     * scale of the fp32 summation error any implementation accumulating in fp32 incurs.
+     * drift_sum (optional, same layout): the sum over the contributions of n * |term|', where
+     * n is the number of divisions T /= (1 - alpha) the pixel's walk has done at that term (the
+     * transmittance-recovery drift is ~ n ulps relative) and |term|' the term with v_alpha
+     * replaced by the sum of the absolute values of its components (their relative errors do
+     * not cancel when v_alpha does).
+     * flip_sum (optional, same layout): what threshold flips can change -- a Gaussian whose
+     * decision sits within 1e-5 of its threshold (alpha vs 1/255, sigma vs 0) may be decided
+     * the other way by another fp32 implementation (different sigma / exp rounding): its own
+     * term (computed as if composited when this walk skips it) may appear or vanish, and the
+     * T of every term the walk reaches after it (earlier in the list) scales by 1/(1 - alpha).
+     * Accumulates 1.1 * (|own term|' + rel * |term|'), rel = the sum over the flippable
+     * Gaussians already passed of 1/(1 - alpha) - 1. */
     /* gsplat's v_conic.y carries 1/2 (CONIC_HALF); else d sigma / d conic.y = dx dy */
     const float hb = (g_quirks & Q_CONIC_HALF) ? 0.5f : 1.0f;
     double *acc = (double *)calloc((size_t)num_points * (9 + (size_t)C), sizeof(double));
     double *aacc = abs_sum ? (double *)calloc((size_t)num_points * (9 + (size_t)C),
                                               sizeof(double))
                            : NULL;
+    double *dacc = drift_sum ? (double *)calloc((size_t)num_points * (9 + (size_t)C),
+                                                sizeof(double))
+                             : NULL;
+    double *facc = flip_sum ? (double *)calloc((size_t)num_points * (9 + (size_t)C),
+                                               sizeof(double))
+                            : NULL;
     /* per Gaussian: [xy0 xy1 con0 con1 con2 opac | C colors] */
     const int S = 6 + C;
     int ntiles = tile_list ? num_tile_list : tbx * tby;
@@ -672,6 +690,8 @@ void oracle_rasterize_backward(int tbx, int tby, int H, int W, int C, int num_po
                 const float *vo = v_out + (size_t)C * pix;
                 float va_out = v_out_alpha[pix];
                 for (int c = 0; c < C; ++c) buf[c] = 0.f;
+                int ndiv = 0; /* divisions T /= (1 - alpha) so far on this pixel */
+                double flip_rel = 0.0; /* relative T change from flippable decisions passed */
                 int kstart = bin_final < end - 1 ? bin_final : end - 1;
                 for (int k = kstart; k >= start; --k) {
                     int g = gids_sorted[k];
@@ -681,19 +701,50 @@ void oracle_rasterize_backward(int tbx, int tby, int H, int W, int C, int num_po
                     float opac = opacity[g];
                     float vis = expf(-sigma);
                     float alpha = fminf(alpha_max, opac * vis);
-                    if (sigma < 0.f || alpha < 1.f / 255.f) continue;
+                    const int near = facc && ((fabs((double)alpha * 255.0 - 1.0) <= 1e-5) ||
+                                              (fabs((double)sigma) <= 1e-6 &&
+                                               alpha >= 1.f / 255.f));
+                    const int skip = sigma < 0.f || alpha < 1.f / 255.f;
+                    if (facc && (near || (!skip && flip_rel > 0.0))) {
+                        /* |term|' of this Gaussian at this pixel (as if composited) */
+                        const float ra_ = 1.f / (1.f - alpha), T_ = T * ra_, fac_ = alpha * T_;
+                        double vabs = fabs((double)T_final * ra_ * va_out);
+                        for (int c = 0; c < C; ++c)
+                            vabs += fabs((double)colors[(size_t)C * g + c] * T_ * vo[c]) +
+                                    fabs((double)buf[c] * ra_ * vo[c]) +
+                                    fabs((double)T_final * ra_ * bg[c] * vo[c]);
+                        const double w = (near ? 1.0 : 0.0) + flip_rel;
+                        double *fa = facc + (size_t)g * S;
+                        const double ws = 1.1 * w * opac * vis * vabs;
+                        fa[0] += ws * fabs((double)cn[0] * dx + (double)cn[1] * dy);
+                        fa[1] += ws * fabs((double)cn[1] * dx + (double)cn[2] * dy);
+                        fa[2] += ws * 0.5 * (double)dx * dx;
+                        fa[3] += ws * hb * fabs((double)dx * dy);
+                        fa[4] += ws * 0.5 * (double)dy * dy;
+                        fa[5] += 1.1 * w * vis * vabs;
+                        for (int c = 0; c < C; ++c) fa[6 + c] += 1.1 * w * fabs((double)fac_ * vo[c]);
+                    }
+                    if (near) flip_rel += 1.0 / (1.0 - (double)alpha) - 1.0;
+                    if (skip) continue;
                     float ra = 1.f / (1.f - alpha);
                     T *= ra;
+                    ++ndiv;
                     float fac = alpha * T;
                     float v_alpha = 0.f;
+                    double va_abs = 0.0; /* sum of |components| of v_alpha */
                     const float *rgb = colors + (size_t)C * g;
                     double *a = acc + (size_t)g * S;
                     double *aa = aacc ? aacc + (size_t)g * S : NULL;
+                    double *da = dacc ? dacc + (size_t)g * S : NULL;
                     for (int c = 0; c < C; ++c) {
                         a[6 + c] += (double)(fac * vo[c]);
                         if (aa) aa[6 + c] += fabs((double)(fac * vo[c]));
+                        if (da) da[6 + c] += ndiv * fabs((double)(fac * vo[c]));
                         v_alpha += (rgb[c] * T - buf[c] * ra) * vo[c];
+                        va_abs += fabs((double)rgb[c] * T * vo[c]) + fabs((double)buf[c] * ra * vo[c]) +
+                                  fabs((double)T_final * ra * bg[c] * vo[c]);
                     }
+                    va_abs += fabs((double)T_final * ra * va_out);
                     v_alpha += T_final * ra * va_out;
                     for (int c = 0; c < C; ++c) v_alpha += -T_final * ra * bg[c] * vo[c];
                     for (int c = 0; c < C; ++c) buf[c] += rgb[c] * fac;
@@ -712,6 +763,15 @@ void oracle_rasterize_backward(int tbx, int tby, int H, int W, int C, int num_po
                         aa[4] += fabs((double)(0.5f * v_sigma * dy * dy));
                         aa[5] += fabs((double)(vis * v_alpha));
                     }
+                    if (da) {
+                        const double ws = (double)opac * vis * va_abs * ndiv;
+                        da[0] += ws * fabs((double)cn[0] * dx + (double)cn[1] * dy);
+                        da[1] += ws * fabs((double)cn[1] * dx + (double)cn[2] * dy);
+                        da[2] += ws * 0.5 * (double)dx * dx;
+                        da[3] += ws * hb * fabs((double)dx * dy);
+                        da[4] += ws * 0.5 * (double)dy * dy;
+                        da[5] += (double)vis * va_abs * ndiv;
+                    }
                 }
             }
     }
@@ -726,7 +786,15 @@ void oracle_rasterize_backward(int tbx, int tby, int H, int W, int C, int num_po
         for (int c = 0; c < C; ++c) v_colors[(size_t)C * g + c] = (float)a[6 + c];
         if (aacc)
             for (int k = 0; k < S; ++k) abs_sum[(size_t)g * S + k] = (float)aacc[(size_t)g * S + k];
+        if (dacc)
+            for (int k = 0; k < S; ++k)
+                drift_sum[(size_t)g * S + k] = (float)dacc[(size_t)g * S + k];
+        if (facc)
+            for (int k = 0; k < S; ++k)
+                flip_sum[(size_t)g * S + k] = (float)facc[(size_t)g * S + k];
     }
     free(acc);
     free(aacc);
+    free(dacc);
+    free(facc);
 }

@@ -218,9 +218,13 @@ def rasterize_forward(tile_bounds, H, W, gids_sorted, tile_bins, xys, conics, co
 
 def rasterize_backward(tile_bounds, H, W, gids_sorted, tile_bins, xys, conics, colors,
                        opacity, background, final_Ts, final_idx, v_out, v_out_alpha,
-                       alpha_max=0.99, tile_list=None, return_abs=False):
+                       alpha_max=0.99, tile_list=None, return_abs=False, return_drift=False,
+                       return_flip=False):
     """Returns (v_xy, v_conic, v_colors, v_opacity) [+ abs-sum tuple of the same shapes:
-    sum over pixels of |contribution|, the fp32 accumulation-error scale]."""
+    sum over pixels of |contribution|, the fp32 accumulation-error scale] [+ drift-sum tuple:
+    sum over pixels of n_div * |contribution with |v_alpha| componentwise|, the
+    transmittance-recovery drift scale (gsplat_oracle.c)] [+ flip-sum tuple: what decisions
+    within 1e-5 of their thresholds can change, gsplat_oracle.c]."""
     colors = _f(colors)
     n, C = colors.shape
     v_xy = np.zeros((n, 2), np.float32)
@@ -229,6 +233,8 @@ def rasterize_backward(tile_bounds, H, W, gids_sorted, tile_bins, xys, conics, c
     v_opac = np.zeros((n, 1), np.float32)
     tl = None if tile_list is None else np.ascontiguousarray(tile_list, np.int32)
     absum = np.zeros((n, 6 + C), np.float32) if return_abs else None
+    drift = np.zeros((n, 6 + C), np.float32) if return_drift else None
+    flip = np.zeros((n, 6 + C), np.float32) if return_flip else None
     lib().oracle_rasterize_backward(
         int(tile_bounds[0]), int(tile_bounds[1]), int(H), int(W), C, n,
         _p(np.ascontiguousarray(gids_sorted, np.int32)),
@@ -236,11 +242,16 @@ def rasterize_backward(tile_bounds, H, W, gids_sorted, tile_bins, xys, conics, c
         _p(colors), _p(_f(opacity).reshape(-1)), _p(_f(background)), _p(_f(final_Ts)),
         _p(np.ascontiguousarray(final_idx, np.int32)), _p(_f(v_out)), _p(_f(v_out_alpha)),
         ctypes.c_float(alpha_max), _p(tl), 0 if tl is None else tl.shape[0], _p(v_xy),
-        _p(v_conic), _p(v_colors), _p(v_opac), _p(absum))
+        _p(v_conic), _p(v_colors), _p(v_opac), _p(absum), _p(drift), _p(flip))
+    split = lambda a: (a[:, 0:2], a[:, 2:5], a[:, 6:], a[:, 5:6])
+    out = [(v_xy, v_conic, v_colors, v_opac)]
     if return_abs:
-        return (v_xy, v_conic, v_colors, v_opac), (absum[:, 0:2], absum[:, 2:5], absum[:, 6:],
-                                                    absum[:, 5:6])
-    return v_xy, v_conic, v_colors, v_opac
+        out.append(split(absum))
+    if return_drift:
+        out.append(split(drift))
+    if return_flip:
+        out.append(split(flip))
+    return out[0] if len(out) == 1 else tuple(out)
 
 
 def render_forward(xys, depths, radii, conics, num_tiles_hit, colors, opacity, H, W,

@@ -9,11 +9,13 @@ explicitly instead of by an outlier allowance:
   double.  The difference is bounded by ~ count * 2^-24 * sum|terms|; the oracle returns
   sum|terms| per element and the bar adds 2^-20 * sum|terms| (raster level only).
 * Transmittance recovery.  The backward recovers each Gaussian's T by dividing T_final back
-  through every later Gaussian of the tile's list -- gsplat with fp32 division, this rasterizer
-  with the hardware reciprocal (1 ulp) -- so recovered T's drift apart by up to ~L ulps for a
-  list of length L (the list-split backward restarts T from the forward's checkpoints instead,
-  which is within the same bound).  The bar adds L_max * 2^-23 * sum|terms|, L_max the longest
-  list among the tiles that contribute (recovery_drift).
+  through every later composited Gaussian of the pixel -- gsplat with fp32 division, this
+  rasterizer with the hardware reciprocal (1 ulp) -- so at the n-th division the recovered T's
+  drift apart by up to ~n ulps (the list-split backward restarts T from the forward's
+  checkpoints instead, within the same bound).  Per term, not per tile: the oracle returns
+  sum over the pixel-Gaussian terms of n * |term| (with v_alpha's components in absolute value,
+  since their errors need not cancel when v_alpha does), and the bar adds 2^-23 times that
+  (drift_slack).  Each check reports its worst |diff| / allowed ratio (worst_ratio).
 * Propagation of that slack.  End to end, the parameter gradients are the projection / SH /
   activation VJPs of the raster-level gradients.  The end-to-end check therefore splits in two:
   (1) the GPU's raster-level gradients (captured at the rasterizer's inputs) vs the oracle's
@@ -53,9 +55,56 @@ def close_frac(a, b, atol=ATOL, rtol=RTOL, abs_sum=None, extra=None):
     return (bad.mean() if bad.size else 0.0), (np.abs(a - b).max() if a.size else 0.0)
 
 
+def worst_ratio(a, b, atol=ATOL, rtol=RTOL, abs_sum=None, extra=None):
+    """max over elements of |a - b| / allowed (the bar of close_frac): how much of the slack
+    the worst element uses (< 1 passes)."""
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    tol = atol + rtol * np.abs(b)
+    if abs_sum is not None:
+        tol = tol + np.asarray(abs_sum, np.float64).reshape(b.shape) * 2.0 ** -20
+    if extra is not None:
+        tol = tol + np.asarray(extra, np.float64).reshape(b.shape)
+    return float((np.abs(a - b) / tol).max()) if a.size else 0.0
+
+
+def _worst_detail(a, b, atol=ATOL, rtol=RTOL, abs_sum=None, extra=None):
+    a, b = np.asarray(a, np.float64).reshape(-1), np.asarray(b, np.float64).reshape(-1)
+    s = (np.asarray(abs_sum, np.float64).reshape(-1) * 2.0 ** -20 if abs_sum is not None
+         else np.zeros_like(b))
+    e = np.asarray(extra, np.float64).reshape(-1) if extra is not None else np.zeros_like(b)
+    tol = atol + rtol * np.abs(b) + s + e
+    i = int(np.nanargmax(np.abs(a - b) / tol))
+    return (f"worst element {i}: got {a[i]:.9g} ref {b[i]:.9g} |diff| {abs(a[i] - b[i]):.3e} "
+            f"allowed {tol[i]:.3e} (abs_sum term {s[i]:.3e}, extra {e[i]:.3e})")
+
+
 def assert_close(name, a, b, **kw):
     frac, mx = close_frac(a, b, **kw)
-    assert frac == 0.0, f"{name}: {frac:.2e} of elements out of tolerance (max |diff| {mx:.3e})"
+    assert frac == 0.0, (f"{name}: {frac:.2e} of elements out of tolerance (max |diff| "
+                         f"{mx:.3e}); {_worst_detail(a, b, **kw)}")
+    print(f"[parity] {name}: max |diff| {mx:.3e}, worst diff/allowed {worst_ratio(a, b, **kw):.3f}")
+    return mx
+
+
+def drift_slack(drift_sum):
+    """The transmittance-recovery slack of each element: 2^-23 * the oracle's drift sum."""
+    return np.asarray(drift_sum, np.float64) * 2.0 ** -23
+
+
+def assert_raster_close(name, a, b, abs_sum, drift_sum, flip_sum):
+    """A raster-level gradient vs the oracle's: the bar + fp32 summation slack + per-term
+    recovery drift, plus -- for the elements that need it -- what the oracle's threshold-flip
+    sum allows (decisions within 1e-5 of alpha = 1/255 or sigma = 0 that another fp32
+    implementation may take the other way, gsplat_oracle.c).  Reports how many elements used
+    the flip allowance; zero elements outside both."""
+    b = np.asarray(b, np.float64).reshape(np.shape(a))
+    drift = drift_slack(drift_sum).reshape(b.shape)
+    flip = np.asarray(flip_sum, np.float64).reshape(b.shape)
+    frac, _ = close_frac(a, b, abs_sum=abs_sum, extra=drift)
+    mx = assert_close(name, a, b, abs_sum=abs_sum, extra=drift + flip)
+    if frac:
+        print(f"[parity] {name}: {int(round(frac * b.size))} elements within a threshold-flip "
+              f"allowance only")
     return mx
 
 
@@ -151,15 +200,6 @@ def gpu_forward_state(gpu, xys, depths, radii, conics, nth, colors, opacity, bac
                 final_idx=np_(fi), tile_bounds=tb)
 
 
-def recovery_drift(bins, tile_list=None) -> float:
-    """L_max * 2^-23: the relative transmittance-recovery drift bound (module docstring) for the
-    longest list among `tile_list` (default: all tiles) of tile_bins `bins`."""
-    b = np.asarray(bins)
-    if tile_list is not None:
-        b = b[np.asarray(tile_list)]
-    return float((b[:, 1] - b[:, 0]).max()) * 2.0 ** -23 if b.size else 0.0
-
-
 def check_raster_level(gpu, xys, depths, radii, conics, nth, colors, opacity, background, H, W,
                        v_img, v_alpha, got, tile_list=None, label=""):
     """The GPU's raster-level gradients `got` (v_xy, v_conic, v_colors, v_opacity) vs the
@@ -170,15 +210,67 @@ def check_raster_level(gpu, xys, depths, radii, conics, nth, colors, opacity, ba
                            W)
     if v_alpha is None or np.asarray(v_alpha).dtype == object:
         v_alpha = np.zeros((H, W), np.float32)
-    ref, absum = O.rasterize_backward(st["tile_bounds"], H, W, st["gids"], st["bins"], xys,
-                                      conics, colors, np.asarray(opacity).reshape(-1),
-                                      background, st["final_Ts"], st["final_idx"], v_img,
-                                      v_alpha, alpha_max=quirks.backward_alpha_clamp(),
-                                      tile_list=tile_list, return_abs=True)
-    drift = recovery_drift(st["bins"], tile_list)
+    ref, absum, drift, flip = O.rasterize_backward(
+        st["tile_bounds"], H, W, st["gids"], st["bins"], xys, conics, colors,
+        np.asarray(opacity).reshape(-1), background, st["final_Ts"], st["final_idx"], v_img,
+        v_alpha, alpha_max=quirks.backward_alpha_clamp(), tile_list=tile_list, return_abs=True,
+        return_drift=True, return_flip=True)
     mx = {}
     for k, name in enumerate(("v_xy", "v_conic", "v_colors", "v_opacity")):
         a = np.asarray(got[k], np.float64).reshape(ref[k].shape)
-        mx[name] = assert_close(f"{label}{name}", a, ref[k], abs_sum=absum[k],
-                                extra=drift * np.asarray(absum[k], np.float64))
+        mx[name] = assert_raster_close(f"{label}{name}", a, ref[k], absum[k], drift[k], flip[k])
     return mx
+
+
+def near_threshold_pixel(i, j, xys, conics, opacity, gids, bins, tbx, alpha_max=0.999,
+                         rel=1e-5):
+    """True if the oracle's front-to-back walk of pixel (i, j) (gsplat's forward, SURVEY A9, in
+    float32 as oracle/gsplat_oracle.c evaluates it) meets a decision within `rel` of its
+    threshold: sigma >= 0 with |sigma| tiny, alpha within rel of 1/255, or T (1 - alpha) within
+    rel of 1e-4.  Two fp32 implementations whose sigma / exp round differently (the GPU:
+    fma-ordered sigma and the hardware exp2, as gsplat's __expf; the oracle: expf) may decide
+    such a Gaussian differently -- a 'threshold flip', which changes the pixel by about that
+    Gaussian's alpha T colour and is the only mismatch the bar allows to be explained rather
+    than bounded."""
+    f = np.float32
+    t = (i // 16) * tbx + j // 16
+    T = f(1.0)
+    for k in range(int(bins[t][0]), int(bins[t][1])):
+        g = int(gids[k])
+        a, b, c = (f(v) for v in conics[g])
+        dx, dy = f(xys[g][0]) - f(j), f(xys[g][1]) - f(i)
+        sigma = f(0.5) * (a * dx * dx + c * dy * dy) + b * dx * dy
+        alpha = min(f(alpha_max), f(opacity[g]) * np.exp(-sigma, dtype=np.float32))
+        if abs(float(sigma)) <= 1e-6 and float(alpha) >= 1 / 255:
+            return True
+        if abs(float(alpha) * 255.0 - 1.0) <= rel:
+            return True
+        if sigma < 0 or alpha < f(1.0 / 255.0):
+            continue
+        nT = T * (f(1.0) - alpha)
+        if abs(float(nT) / 1e-4 - 1.0) <= rel:
+            return True
+        if nT <= f(1e-4):
+            break
+        T = nT
+    return False
+
+
+def assert_close_or_flip(name, img, ref, xys, conics, opacity, gids, bins, tbx, **kw):
+    """assert_close on an [H, W, C] image, except that a pixel whose every out-of-bar channel
+    lies on a threshold flip of the oracle's walk (near_threshold_pixel) is counted and reported
+    instead of failing; returns the number of such pixels."""
+    img, ref = np.asarray(img, np.float64), np.asarray(ref, np.float64)
+    tol = ATOL + RTOL * np.abs(ref)
+    if kw.get("extra") is not None:
+        tol = tol + np.asarray(kw["extra"], np.float64).reshape(ref.shape)
+    bad = ~(np.abs(img - ref) <= tol)
+    pix = np.argwhere(bad.reshape(ref.shape[0], ref.shape[1], -1).any(-1))
+    unexplained = [(int(i), int(j)) for i, j in pix
+                   if not near_threshold_pixel(i, j, xys, conics, np.asarray(opacity).reshape(-1),
+                                               gids, bins, tbx)]
+    assert not unexplained, (f"{name}: {len(unexplained)} pixels out of tolerance without a "
+                             f"threshold flip, e.g. {unexplained[:5]}; "
+                             f"{_worst_detail(img, ref, **kw)}")
+    print(f"[parity] {name}: {len(pix)} pixels differ by a threshold flip, 0 unexplained")
+    return len(pix)

@@ -60,6 +60,25 @@ def test_sh_backward_views_vs_oracle(gpu, oracle_lib, degree, dtu, n, R, pad):
         assert not got[:, num_sh_bases(dtu):].any()
 
 
+def test_sh_backward_views_garden_r8(gpu, oracle_lib):
+    """BASELINE config c4's exchange at its real size: the 2M garden Gaussians, the first 8
+    garden cameras as the 8 ranks' views (R = 8), SH degree 3, vs the oracle."""
+    import bench
+    scene, _ = bench.make_workload("c4", 0, torch.device("cpu"))
+    cams = [bench.make_workload("c4", r, torch.device("cpu"))[1] for r in range(8)]
+    means = scene.means.contiguous()
+    n, R, K = means.shape[0], 8, 16
+    g = torch.Generator().manual_seed(44)
+    views = torch.zeros(R, 3 * n + 4)
+    views[:, :3 * n] = torch.randn(R, 3 * n, generator=g) * 1e-3
+    for r, c in enumerate(cams):
+        views[r, 3 * n:3 * n + 3] = c.c2w[:3, 3]
+    got = sh_backward_views(3, 3, means.to(gpu), views.to(gpu)).cpu().numpy()
+    ref = O.sh_backward_views(3, means.numpy(), views.numpy(), K)
+    assert got.shape == (n, K, 3) and np.abs(ref).max() > 0
+    np.testing.assert_allclose(got, ref, rtol=1e-4, atol=1e-5 * 1e-3)
+
+
 def test_sh_backward_views_rejects_short_stride(gpu):
     from gaussctrl_exp_amd import _lib
     means = torch.zeros(10, 3, device=gpu)

@@ -25,7 +25,7 @@ import bench
 import oracle as O
 from gaussctrl_exp_amd import _lib, quirks
 from gaussctrl_exp_amd.rasterize import bin_gaussians
-from parity import assert_close, close_frac, recovery_drift
+from parity import assert_close, assert_raster_close, close_frac
 
 pytestmark = pytest.mark.gpu
 
@@ -39,7 +39,7 @@ class FusedRun:
 
     def __init__(self, config, gpu):
         sc, cam = bench.make_workload(config, 0, gpu)
-        self.sc, self.cam, self.gpu = sc, cam.to(gpu), gpu
+        self.sc, self.cam, self.gpu, self.config = sc, cam.to(gpu), gpu, config
         c = self.cam
         n = sc.means.shape[0]
         K = 1 + sc.features_rest.shape[1]
@@ -87,12 +87,15 @@ class FusedRun:
         self.fT, self.fi = fT, fi
         return img, fT, fi
 
-    def backward(self, v_img, v_alpha):
+    def backward(self, v_img, v_alpha, final_Ts=None, final_idx=None):
+        """The record backward from the forward's state (or the given final_Ts / final_idx)."""
         P, st = _lib.ptr, _lib.stream(self.gpu)
         self.v_img, self.v_alpha = v_img.to(self.gpu).contiguous(), v_alpha.to(self.gpu).contiguous()
+        fT = self.fT if final_Ts is None else final_Ts
+        fi = self.fi if final_idx is None else final_idx
         _lib.call("gsplat_rasterize_backward_records", self.tb[0], self.tb[1], self.H, self.W,
                   self.n, P(self.gids), P(self.bins), P(self.xys), P(self.conics),
-                  P(self.colors), P(self.opac), P(self.bg), P(self.fT), P(self.fi),
+                  P(self.colors), P(self.opac), P(self.bg), P(fT), P(fi),
                   P(self.v_img), P(self.v_alpha), quirks.backward_alpha_clamp(), self.I,
                   self.chunk, P(self.ckpt), self.ckpt.numel(), P(self.rec), self.rec.numel(), st)
 
@@ -166,22 +169,35 @@ def test_blend_and_records_on_sampled_tiles(gpu, run):
                                          conics, colors, opac, bg, tile_list=tiles)
     assert_close("image (sampled tiles)", _np(img)[mask], rimg[mask])
     assert_close("alpha (sampled tiles)", 1 - _np(fT)[mask], 1 - rT[mask])
+    # final_idx: the integer forward state the backward walks from, bit-exact
+    np.testing.assert_array_equal(_np(fi)[mask], ridx[mask], err_msg="final_idx")
     gen = torch.Generator().manual_seed(9)
     m = torch.from_numpy(mask)
     v_img = torch.randn(run.H, run.W, 3, generator=gen) * m[..., None]
     v_alpha = torch.randn(run.H, run.W, generator=gen) * m
     run.backward(v_img, v_alpha)
     got = run.raster_grads()
-    ref, absum = O.rasterize_backward(run.tb, run.H, run.W, _np(run.gids), _np(run.bins), xys,
-                                      conics, colors, opac, bg, _np(fT), _np(fi), v_img.numpy(),
-                                      v_alpha.numpy(), alpha_max=quirks.backward_alpha_clamp(),
-                                      tile_list=tiles, return_abs=True)
-    drift = recovery_drift(_np(run.bins), tiles)  # tests/parity.py
+    ref, absum, drift, flip = O.rasterize_backward(
+        run.tb, run.H, run.W, _np(run.gids), _np(run.bins), xys, conics, colors, opac, bg,
+        _np(fT), _np(fi), v_img.numpy(), v_alpha.numpy(), alpha_max=quirks.backward_alpha_clamp(),
+        tile_list=tiles, return_abs=True, return_drift=True, return_flip=True)
     for k, name in enumerate(("v_xy", "v_conic", "v_colors", "v_opacity")):
         assert np.abs(ref[k]).max() > 0
-        mx = assert_close(name, got[k], ref[k].reshape(got[k].shape), abs_sum=absum[k],
-                          extra=drift * absum[k])
-        print(f"{run.n}: {name} max |diff| {mx:.3e}")
+        assert_raster_close(f"{run.config} {name}", got[k], ref[k], absum[k], drift[k], flip[k])
+    # the same backward fed the ORACLE's forward state (its final_Ts / final_idx; zero outside the
+    # sampled tiles, where the upstream gradient is zero too) instead of the GPU's
+    run.rec.fill_(0)
+    fT_o = torch.from_numpy(np.ascontiguousarray(rT)).to(gpu)
+    fi_o = torch.from_numpy(np.ascontiguousarray(ridx)).to(gpu)
+    run.backward(v_img, v_alpha, final_Ts=fT_o, final_idx=fi_o)
+    got_o = run.raster_grads()
+    ref_o, absum_o, drift_o, flip_o = O.rasterize_backward(
+        run.tb, run.H, run.W, _np(run.gids), _np(run.bins), xys, conics, colors, opac, bg, rT,
+        ridx, v_img.numpy(), v_alpha.numpy(), alpha_max=quirks.backward_alpha_clamp(),
+        tile_list=tiles, return_abs=True, return_drift=True, return_flip=True)
+    for k, name in enumerate(("v_xy", "v_conic", "v_colors", "v_opacity")):
+        assert_raster_close(f"{run.config} {name} (oracle forward state)", got_o[k], ref_o[k],
+                            absum_o[k], drift_o[k], flip_o[k])
 
 
 def test_fused_backward_chain_all_gaussians(gpu, run):
@@ -237,7 +253,7 @@ def test_c2_forward_full_image(gpu, oracle_lib):
     """c2 (100k @ 512², SH degree 0: sigmoid colours, forward only): the full image and alpha
     of the fused forward vs the oracle, zero outliers."""
     run = FusedRun("c2", gpu)
-    img, fT, _ = run.forward()
+    img, fT, fi = run.forward()
     r = O.render_forward(_np(run.xys), _np(run.depths), _np(run.radii), _np(run.conics),
                          _np(run.nth), _np(run.colors), _np(run.opac), run.H, run.W,
                          _np(run.bg))
@@ -247,5 +263,6 @@ def test_c2_forward_full_image(gpu, oracle_lib):
     frac, mx = close_frac(_np(img), r["img"])
     assert frac == 0, (frac, mx)
     assert_close("alpha", 1 - _np(fT), r["alpha"])
+    np.testing.assert_array_equal(_np(fi), r["final_idx"], err_msg="final_idx")
     # colours are sigmoid(features_dc) (gc_model.py:203)
     np.testing.assert_array_equal(_np(run.colors), _np(torch.sigmoid(run.sc.features_dc)))

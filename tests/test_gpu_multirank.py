@@ -99,3 +99,64 @@ def test_fused_ranks_sum_the_view_gradients(tmp_path, mode, world):
         _lib.set_deterministic(prev)
     assert np.abs(ref).max() > 0
     assert_close("summed view gradients", g0, ref, atol=1e-6, rtol=1e-4)
+
+
+def _garden_worker(rank, world, port, out_dir):
+    """BASELINE config c4 as stated: the 2M-Gaussian garden scene at 1080^2, rank r rendering
+    garden camera r (bench.make_workload), gradients summed across the ranks."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    from gaussctrl_exp_amd.train import TrainStep
+    scene, cam = bench.make_workload("c4", rank, dev)
+    cam = cam.to(dev)
+    gt = torch.rand(cam.height, cam.width, 3, generator=torch.Generator().manual_seed(rank)).to(dev)
+    t = TrainStep(scene, sh_degree=3, world_size=world, loss="l1", render_mode="fused")
+    t.step(cam, gt, background=torch.tensor(BG, device=dev), optimizer=False)
+    np.save(os.path.join(out_dir, f"grad{rank}.npy"), t.flat_grad().cpu().numpy())
+    assert t.sh_exchange.early_steps == 1
+    t.step(cam, gt, background=torch.tensor(BG, device=dev))
+    np.save(os.path.join(out_dir, f"params{rank}.npy"),
+            torch.cat([p.detach().reshape(-1) for p in t.params]).cpu().numpy())
+    torch.cuda.synchronize()
+    dist.destroy_process_group()
+
+
+def test_garden_two_views_sum(tmp_path):
+    """c4 (garden, 2M Gaussians @ 1080^2, 1 view per rank, summed gradients): at world size 2
+    each rank's flat gradient equals the sum of the two single-view fused gradients, and both
+    ranks hold identical parameters after the Adam step (deterministic rasterizer backward)."""
+    from gaussctrl_exp_amd import _lib
+    from parity import assert_close
+    import bench
+    port = _free_port()
+    os.environ["GSPLAT_MI355X_DETERMINISTIC"] = "1"
+    try:
+        mp.spawn(_garden_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    finally:
+        os.environ.pop("GSPLAT_MI355X_DETERMINISTIC", None)
+    g0 = np.load(tmp_path / "grad0.npy")
+    np.testing.assert_array_equal(np.load(tmp_path / "grad1.npy"), g0)
+    np.testing.assert_array_equal(np.load(tmp_path / "params1.npy"),
+                                  np.load(tmp_path / "params0.npy"))
+    from gaussctrl_exp_amd.train import TrainStep
+    dev = torch.device("cuda:0")
+    ref = None
+    prev = _lib.set_deterministic(True)
+    try:
+        for r in range(2):
+            scene, cam = bench.make_workload("c4", r, dev)
+            cam = cam.to(dev)
+            gt = torch.rand(cam.height, cam.width, 3,
+                            generator=torch.Generator().manual_seed(r)).to(dev)
+            t = TrainStep(scene, sh_degree=3, world_size=1, loss="l1", render_mode="fused")
+            t.step(cam, gt, background=torch.tensor(BG, device=dev), optimizer=False)
+            g = t.flat_grad().cpu().numpy()
+            ref = g if ref is None else ref + g
+            del t, scene
+    finally:
+        _lib.set_deterministic(prev)
+    assert np.abs(ref).max() > 0 and g0.size == ref.size == 2_000_000 * 59
+    assert_close("garden summed view gradients", g0, ref, atol=1e-6, rtol=1e-4)

@@ -377,15 +377,15 @@ def _check_raster_backward(gpu, case):
     _lib.call("gsplat_rasterize_forward", tb[0], tb[1], H, W, 3, P(gids), P(bins), P(xys),
               P(conics), P(col.detach()), P(op.detach()), P(bg_d), P(out), P(fT), P(fi),
               _lib.stream(gpu))
-    ref = O.rasterize_backward(tb, H, W, _np(gids), _np(bins), _np(xys), _np(conics),
-                               colors.numpy(), opac.numpy(), bg.numpy(), _np(fT), _np(fi),
-                               v_img.numpy(), v_alpha.numpy(), alpha_max=quirks.backward_alpha_clamp(),
-                               return_abs=True)
-    ref, absum = ref
+    ref, absum, drift, flip = O.rasterize_backward(
+        tb, H, W, _np(gids), _np(bins), _np(xys), _np(conics), colors.numpy(), opac.numpy(),
+        bg.numpy(), _np(fT), _np(fi), v_img.numpy(), v_alpha.numpy(),
+        alpha_max=quirks.backward_alpha_clamp(), return_abs=True, return_drift=True,
+        return_flip=True)
+    from parity import assert_raster_close
     for k, (name, gt) in enumerate((("xys", xy.grad), ("conics", cn.grad), ("colors", col.grad),
                                     ("opacity", op.grad))):
-        frac, mx = _close_frac(_np(gt), ref[k].reshape(gt.shape), abs_sum=absum[k])
-        assert frac == 0.0, f"{name}: {frac:.2e} out of tolerance (max {mx:.3e})"
+        assert_raster_close(name, _np(gt), ref[k], absum[k], drift[k], flip[k])
 
 
 @pytest.mark.parametrize("bwd", [1, 2])
@@ -428,15 +428,15 @@ def test_nd_rasterize(gpu, C, quirk_mask):
     v_img = torch.randn(H, W, C, generator=gen)
     (img * v_img.to(gpu)).sum().backward()
     # the oracle's backward on the oracle's own forward state
-    ref, absum = O.rasterize_backward(f["tile_bounds"], H, W, f["gaussian_ids_sorted"],
-                                      f["tile_bins"], o[0], o[3], colors.numpy(), opac.numpy(),
-                                      bg.numpy(), f["final_Ts"], f["final_idx"], v_img.numpy(),
-                                      np.zeros((H, W), np.float32),
-                                      alpha_max=quirks.backward_alpha_clamp(), return_abs=True)
+    ref, absum, drift, flip = O.rasterize_backward(
+        f["tile_bounds"], H, W, f["gaussian_ids_sorted"], f["tile_bins"], o[0], o[3],
+        colors.numpy(), opac.numpy(), bg.numpy(), f["final_Ts"], f["final_idx"], v_img.numpy(),
+        np.zeros((H, W), np.float32), alpha_max=quirks.backward_alpha_clamp(), return_abs=True,
+        return_drift=True, return_flip=True)
+    from parity import assert_raster_close
     for k, (name, gt) in enumerate((("xys", xy.grad), ("conics", cn.grad), ("colors", col.grad),
                                     ("opacity", op.grad))):
-        frac, mx = _close_frac(_np(gt), ref[k].reshape(gt.shape), abs_sum=absum[k])
-        assert frac == 0, f"{name}: {frac:.2e} out of tolerance (max {mx:.3e})"
+        assert_raster_close(f"C={C} {name}", _np(gt), ref[k], absum[k], drift[k], flip[k])
 
 
 def test_uint8_colors(gpu):

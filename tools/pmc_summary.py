@@ -25,6 +25,47 @@ for f in files:
         else:
             continue
         acc[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
+# Per C-ABI entry of the binning, whose kernels (radix passes, scans) are shared between the
+# depth sort (gsplat_bin_count_keyed) and the tile sort (gsplat_bin_emit): segment each pass's
+# dispatch sequence -- a fused forward kernel starts a step's binning, the emission's first
+# kernel (emit / tc_first / ep0_count) starts bin_emit, bins_decode ends it -- and average the
+# per-call sums of every counter over the calls seen.
+EMIT_START = ("emit_kernel", "tc_first_kernel", "ep0_count_kernel")
+entries = collections.defaultdict(lambda: collections.defaultdict(float))
+calls = collections.defaultdict(set)
+for f in files:
+    disp = collections.defaultdict(dict)
+    names = {}
+    for r in csv.DictReader(open(f)):
+        if "Dispatch_Id" not in r:
+            break
+        d = int(r["Dispatch_Id"])
+        names[d] = r["Kernel_Name"]
+        disp[d][r["Counter_Name"]] = disp[d].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    state, seg = None, 0
+    for d in sorted(disp):
+        k = names[d]
+        if "fused_fwd_kernel" in k or "project_fwd_kernel" in k:
+            state, seg = "gsplat_bin_count_keyed", seg + 1
+            continue
+        if state == "gsplat_bin_count_keyed" and any(s in k for s in EMIT_START):
+            state = "gsplat_bin_emit"
+        if state is None:
+            continue
+        if not k.startswith("gs::") and not k.startswith("void gs::"):
+            continue
+        for c, v in disp[d].items():
+            entries[state][(os.path.dirname(f), c)] += v
+        calls[state].add((os.path.dirname(f), seg))
+        if state == "gsplat_bin_emit" and "bins_decode_kernel" in k:
+            state = None
+entry_rows = {}
+for e, d in entries.items():
+    per = collections.defaultdict(list)
+    ncall = collections.Counter(run for run, _ in calls[e])
+    for (run, c), v in d.items():
+        per[c].append(v / max(ncall[run], 1))
+    entry_rows[e] = {c: sum(v) / len(v) for c, v in per.items()}
 rows = []
 for k, d in sorted(acc.items()):
     row = {"kernel": k}
@@ -33,13 +74,16 @@ for k, d in sorted(acc.items()):
     rows.append(row)
 cols = sorted({c for r in rows for c in r if c != "kernel"})
 if len(sys.argv) > 3:
-    tj = {r["kernel"]: {"fetch_kb": r.get("FETCH_SIZE"), "write_kb": r.get("WRITE_SIZE"),
-                        "valu_quad_cycles": r.get("SQ_ACTIVE_INST_VALU"),
-                        "insts_valu": r.get("SQ_INSTS_VALU"),
-                        "insts_trans": r.get("SQ_INSTS_VALU_TRANS_F32"),
-                        "wait_inst_any": r.get("SQ_WAIT_INST_ANY"),
-                        "wave_cycles": r.get("SQ_WAVE_CYCLES")}
-          for r in rows if "FETCH_SIZE" in r and "WRITE_SIZE" in r}
+    def pick(r):
+        return {"fetch_kb": r.get("FETCH_SIZE"), "write_kb": r.get("WRITE_SIZE"),
+                "valu_quad_cycles": r.get("SQ_ACTIVE_INST_VALU"),
+                "insts_valu": r.get("SQ_INSTS_VALU"),
+                "insts_trans": r.get("SQ_INSTS_VALU_TRANS_F32"),
+                "wait_any": r.get("SQ_WAIT_ANY"),
+                "wait_inst_any": r.get("SQ_WAIT_INST_ANY"),
+                "wave_cycles": r.get("SQ_WAVE_CYCLES")}
+    tj = {r["kernel"]: pick(r) for r in rows if "FETCH_SIZE" in r and "WRITE_SIZE" in r}
+    ej = {e: pick(r) for e, r in entry_rows.items() if "FETCH_SIZE" in r and "WRITE_SIZE" in r}
     cfg = cfg_arg
     try:
         with open(sys.argv[3]) as f:
@@ -48,7 +92,7 @@ if len(sys.argv) > 3:
         doc = {}
     doc.setdefault("source", "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE / SQ_ACTIVE_INST_VALU "
                              "(quad-cycles), separate passes, tools/pmc_bench.sh")
-    doc.setdefault("configs", {})[cfg] = {"kernels": tj}
+    doc.setdefault("configs", {})[cfg] = {"kernels": tj, "entries": ej}
     with open(sys.argv[3], "w") as f:
         json.dump(doc, f, indent=1)
 out = sys.argv[2] if len(sys.argv) > 2 else None
