@@ -451,11 +451,7 @@ constexpr int tiles_per_block() {
 // depth, accumulated with the same weight as the colour channels into out_depth -- exactly
 // channel 0 of a second render with colours = depth and a zero background (gc_model.py:
 // 225-238), without the second binning and traversal.
-//
-// CKPT (list-split backward, see chunk_plan_kernel): for a tile whose list is longer than
-// `chunk`, each pixel's state (T, accumulated colour) is recorded after every `chunk` list
-// positions and at the end, so the backward can start each chunk from it.
-template <int PXL, int COLS, bool DEPTH = false, bool CKPT = false, bool CNT = false>
+template <int PXL, int COLS, bool DEPTH = false, bool CNT = false>
 __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
     int tbx, int tby, int H, int W, const int *__restrict__ gids, const int2 *__restrict__ bins,
     const float2 *__restrict__ xys, const float *__restrict__ conics,
@@ -463,8 +459,7 @@ __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
     const float *__restrict__ background, float *__restrict__ out_img,
     float *__restrict__ final_Ts, int *__restrict__ final_idx,
     const float *__restrict__ depths = nullptr, float *__restrict__ out_depth = nullptr,
-    int chunk = 0, const int *__restrict__ ckpt_off = nullptr,
-    float4 *__restrict__ ckpt = nullptr, float4 *__restrict__ zero = nullptr,
+    float4 *__restrict__ zero = nullptr,
     long long zero_n = 0, const int *__restrict__ zero_radii = nullptr) {
   // Side job: clear a buffer (the fused path's gradient records) with the memory bandwidth the
   // VALU-bound blend leaves idle -- a grid-stride sweep of coalesced 16-B stores, issued by each
@@ -503,25 +498,7 @@ __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
   const int2 range = bins[tile];
   GStage *stage = lds[wave];
   unsigned c_slots = 0, c_live = 0, c_valid = 0;  // (CNT only)
-  // checkpoints (CKPT): m states per chunked tile, state k after list position
-  // range.x + (k + 1) * chunk (k = m - 1: the final state)
-  int m = 0, nextk = 0;
-  if (CKPT) {
-    const int len = range.y - range.x;
-    if (len > chunk) m = (len + chunk - 1) / chunk;
-  }
-  auto write_ckpt = [&](int kk) {  // (addresses recomputed here: fewer live registers)
-    const size_t base = ((size_t)ckpt_off[tile] + kk) * (GS_BLOCK * GS_BLOCK);
-    const int ly0 = i0 - (tile / tbx) * GS_BLOCK, lx = j - (tile % tbx) * GS_BLOCK;
-#pragma unroll
-    for (int k = 0; k < PXL; ++k)
-      if (i0 + LROWS * k < H && j < W)
-        ckpt[base + (ly0 + LROWS * k) * GS_BLOCK + lx] = make_float4(T[k], cr[k], cg[k], cb[k]);
-  };
   for (int b = range.x; b < range.y; b += 64) {
-    if (CKPT && m) {
-      if (nextk < m - 1 && b - range.x == (nextk + 1) * chunk) write_ckpt(nextk++);
-    }
     bool all_done = true;
 #pragma unroll
     for (int k = 0; k < PXL; ++k) all_done = all_done && done[k];
@@ -582,9 +559,6 @@ __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
     }
     wave_lds_sync();
   }
-  if (CKPT) {  // boundaries after an early exit, and the final state
-    for (int kk = nextk; kk < m; ++kk) write_ckpt(kk);
-  }
   const float bg0 = background[0], bg1 = background[1], bg2 = background[2];
 #pragma unroll
   for (int k = 0; k < PXL; ++k) {
@@ -612,12 +586,14 @@ __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
 // (dx is constant along the lane's column), from which
 //   v_conic = 0.5 (dx^2 V, dx Vy, Vyy),  v_xy = (a dx V + b Vy, b dx V + c Vy).
 //
-// CHUNKED (list-split backward): the work slots are (tile, chunk) items of chunk_plan_kernel's
-// table instead of tiles.  Chunk j of a tile covers list positions
-// [range.x + j * chunk, range.x + (j + 1) * chunk) and starts from the forward's checkpoint
-// after its last position: T = checkpoint T, and the colour behind it, Sb = (C_final - C_j) . v,
-// instead of T_final and 0 -- so long lists and small images (few tiles) still fill the GPU.
-template <int NP, bool ATOMICS, int COLS, bool CHUNKED = false, typename PV = f2,
+// SPLIT (list-split backward, see split_plan_kernel): the work slots are (tile, part) items
+// instead of tiles.  Part j covers list positions [range.x + j chunk, range.x + (j + 1) chunk);
+// its waves first walk the positions behind the part (pre_walk: T recovered and the colour
+// behind accumulated with exactly the operations of the full walk, no gradient) and then
+// blend the part itself -- per pixel the same arithmetic in the same order as the unsplit
+// walk, so the per-wave totals (and the deterministic mode's sums) are unchanged, while a
+// long list's parts run as separate, earlier-dispatched waves.
+template <int NP, bool ATOMICS, int COLS, bool SPLIT = false, typename PV = f2,
           bool DET = false, bool CNT = false>
 __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
     int tbx, int tby, int H, int W, const int *__restrict__ gids, const int2 *__restrict__ bins,
@@ -626,17 +602,17 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
     const float *__restrict__ background, const float *__restrict__ final_Ts,
     const int *__restrict__ final_idx, const float *__restrict__ v_out,
     const float *__restrict__ v_out_alpha, float alpha_max, float *__restrict__ rec,
-    bool stage_only, int chunk = 0, const int *__restrict__ item_off = nullptr,
-    const int *__restrict__ item_tile = nullptr, const int *__restrict__ ckpt_off = nullptr,
-    const float4 *__restrict__ ckpt = nullptr, unsigned long long *__restrict__ det = nullptr) {
+    int chunk = 0, const int2 *__restrict__ items = nullptr,
+    const int *__restrict__ n_items = nullptr, unsigned long long *__restrict__ det = nullptr) {
   constexpr int PXL = 2 * NP;
   constexpr int LROWS = 64 / COLS;
-  int ctile = -1, cj = 0;
-  if (CHUNKED) {
+  int ctile = -1, part = 0;
+  if (SPLIT) {
     const int slot = wave_slot<PXL, COLS>();
-    if (slot >= item_off[tbx * tby]) return;  // wave-uniform: past the last item
-    ctile = item_tile[slot];
-    cj = slot - item_off[ctile];
+    if (slot >= *n_items) return;  // wave-uniform: past the last item
+    const int2 it = items[slot];
+    ctile = it.x;
+    part = it.y;
   }
   const WaveLog wlog;
   const WaveRect R = wave_rect<PXL, COLS>(tbx, tby, H, W, ctile);
@@ -677,37 +653,51 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
   }
   const int2 range = bins[tile];
   int lo = range.x, hi = range.y;
-  if (CHUNKED) {
-    const int len = range.y - range.x;
-    const int m = len > chunk ? (len + chunk - 1) / chunk : 1;
-    if (m > 1) {
-      lo = range.x + cj * chunk;
-      hi = min(lo + chunk, range.y);
-      if (cj < m - 1) {  // start from the checkpoint after this chunk
-        const size_t cb = (size_t)ckpt_off[tile] * (GS_BLOCK * GS_BLOCK);
-        const int oy = (tile / tbx) * GS_BLOCK, ox = (tile % tbx) * GS_BLOCK;
-#pragma unroll
-        for (int k = 0; k < PXL; ++k) {
-          const int i = i0 + LROWS * k, p = k >> 1;
-          if (i < H && j < W) {
-            const int lpix = (i - oy) * GS_BLOCK + (j - ox);
-            const float4 cj4 = ckpt[cb + (size_t)cj * (GS_BLOCK * GS_BLOCK) + lpix];
-            const float4 cf4 = ckpt[cb + (size_t)(m - 1) * (GS_BLOCK * GS_BLOCK) + lpix];
-            const float vr_ = (k & 1) ? vr[p].y : vr[p].x, vg_ = (k & 1) ? vg[p].y : vg[p].x,
-                        vb_ = (k & 1) ? vb[p].y : vb[p].x;
-            const float sb = (cf4.y - cj4.y) * vr_ + (cf4.z - cj4.z) * vg_ + (cf4.w - cj4.w) * vb_;
-            if (k & 1) { T[p].y = cj4.x; Sb[p].y = sb; } else { T[p].x = cj4.x; Sb[p].x = sb; }
-          }
-        }
-      }
-    }
+  if (SPLIT) {
+    lo = range.x + part * chunk;
+    hi = min(lo + chunk, range.y);
   }
   maxbin = wave_max_int(maxbin);
   const int slot = reduce9_slot();
   // canonical once, so fminf needs no per-iteration canonicalisation of the bound
   const float amax = __builtin_canonicalizef(alpha_max);
-  const int last = min(maxbin, hi - 1);
   GStage *stage = lds[wave];
+  if (SPLIT) {  // the positions behind this part: T and the colour behind only
+    for (int b = min(maxbin, range.y - 1); b >= hi; b -= 64) {
+      const int idx = b - lane;
+      GStage s;
+      const bool keep = idx >= hi && stage_gaussian<true>(idx, gids, xys, conics, colors,
+                                                          opacity, rx0, rx1, ry0, ry1, s);
+      const unsigned long long kmask = __ballot(keep);
+      if (keep) stage[lanes_below(kmask)] = s;
+      const int n = __popcll(kmask);
+      wave_lds_sync();
+      for (int t = 0; t < n; ++t) {
+        const GStage G = stage[t];
+        const float dx = G.x - px;
+        const float hA = G.ha * dx * dx, bdx = G.b * dx;
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {  // (the main loop's T / Sb operations, nothing else)
+          const PV dy = G.y - py[p];
+          const PV sig = gs_sigma2v<PV>(G.hc, bdx, hA, dy);
+          const PV vis = gs_vis2v<PV>(sig);
+          const PV ov = G.o * vis;
+          const PV al = {fminf(amax, ov.x), fminf(amax, ov.y)};
+          const bool v0 = G.idx <= binf[2 * p] && sig.x >= 0.f && al.x >= ALPHA_MIN;
+          const bool v1 = G.idx <= binf[2 * p + 1] && sig.y >= 0.f && al.y >= ALPHA_MIN;
+          const PV am = {v0 ? al.x : 0.f, v1 ? al.y : 0.f};
+          const PV om = 1.f - am;
+          const PV ra = {__builtin_amdgcn_rcpf(om.x), __builtin_amdgcn_rcpf(om.y)};
+          T[p] = T[p] * ra;
+          const PV fac = am * T[p];
+          const PV gv = vfma(PV(G.r), vr[p], vfma(PV(G.g), vg[p], G.bl * vb[p]));
+          Sb[p] = vfma(fac, gv, Sb[p]);
+        }
+      }
+      wave_lds_sync();
+    }
+  }
+  const int last = min(maxbin, hi - 1);
   unsigned c_slots = 0, c_live = 0, c_valid = 0;  // (CNT only)
   for (int b = last; b >= lo; b -= 64) {
     const int idx = b - lane;
@@ -720,7 +710,7 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
     const int n = __popcll(kmask);
     wave_lds_sync();
     constexpr int U = 1;  // (two per iteration measured slower: register pressure)
-    for (int t = 0; t < (stage_only ? 0 : n); t += U) {
+    for (int t = 0; t < n; t += U) {
       float parts[U][9];
       bool anyv[U];
       int gid[U];
@@ -851,10 +841,10 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
 // hardware reciprocal, v_alpha from the colour behind); the per-pixel decisions (sigma >= 0,
 // alpha >= 1/255, idx <= final_idx) are the forward's bit for bit (gs_sigma / gs_vis).
 //
-// CHUNKED: list-split items as raster_bwd3p_kernel (the four waves of a workgroup take the four
-// 8x8 blocks of one (tile, chunk) item).  DET: integer accumulation (det_add).  CNT: lane-slot
-// accounting (gsplat_debug_pair_count).
-template <bool CHUNKED = false, bool DET = false, bool CNT = false>
+// SPLIT: list-split items as raster_bwd3p_kernel (the four waves of a workgroup take the four
+// 8x8 blocks of one (tile, part) item, with the same pre-walk).  DET: integer accumulation
+// (det_add).  CNT: lane-slot accounting (gsplat_debug_pair_count).
+template <bool SPLIT = false, bool DET = false, bool CNT = false>
 __global__ __launch_bounds__(256) void raster_bwd8_kernel(
     int tbx, int tby, int H, int W, const int *__restrict__ gids, const int2 *__restrict__ bins,
     const float2 *__restrict__ xys, const float *__restrict__ conics,
@@ -862,15 +852,15 @@ __global__ __launch_bounds__(256) void raster_bwd8_kernel(
     const float *__restrict__ background, const float *__restrict__ final_Ts,
     const int *__restrict__ final_idx, const float *__restrict__ v_out,
     const float *__restrict__ v_out_alpha, float alpha_max, float *__restrict__ rec,
-    int chunk = 0, const int *__restrict__ item_off = nullptr,
-    const int *__restrict__ item_tile = nullptr, const int *__restrict__ ckpt_off = nullptr,
-    const float4 *__restrict__ ckpt = nullptr, unsigned long long *__restrict__ det = nullptr) {
-  int ctile = -1, cj = 0;
-  if (CHUNKED) {
+    int chunk = 0, const int2 *__restrict__ items = nullptr,
+    const int *__restrict__ n_items = nullptr, unsigned long long *__restrict__ det = nullptr) {
+  int ctile = -1, part = 0;
+  if (SPLIT) {
     const int slot = wave_slot<1, 8>();
-    if (slot >= item_off[tbx * tby]) return;  // wave-uniform: past the last item
-    ctile = item_tile[slot];
-    cj = slot - item_off[ctile];
+    if (slot >= *n_items) return;  // wave-uniform: past the last item
+    const int2 it = items[slot];
+    ctile = it.x;
+    part = it.y;
   }
   const WaveLog wlog;
   const WaveRect R = wave_rect<1, 8>(tbx, tby, H, W, ctile);
@@ -895,21 +885,9 @@ __global__ __launch_bounds__(256) void raster_bwd8_kernel(
   }
   const int2 range = bins[tile];
   int lo = range.x, hi = range.y;
-  if (CHUNKED) {
-    const int len = range.y - range.x;
-    const int m = len > chunk ? (len + chunk - 1) / chunk : 1;
-    if (m > 1) {
-      lo = range.x + cj * chunk;
-      hi = min(lo + chunk, range.y);
-      if (cj < m - 1 && inside) {  // start from the forward's checkpoint after this chunk
-        const size_t cb = (size_t)ckpt_off[tile] * (GS_BLOCK * GS_BLOCK);
-        const int lpix = (i - (tile / tbx) * GS_BLOCK) * GS_BLOCK + (j - (tile % tbx) * GS_BLOCK);
-        const float4 c4 = ckpt[cb + (size_t)cj * (GS_BLOCK * GS_BLOCK) + lpix];
-        const float4 f4 = ckpt[cb + (size_t)(m - 1) * (GS_BLOCK * GS_BLOCK) + lpix];
-        T = c4.x;
-        Sb = (f4.y - c4.y) * vr + (f4.z - c4.z) * vg + (f4.w - c4.w) * vb;
-      }
-    }
+  if (SPLIT) {
+    lo = range.x + part * chunk;
+    hi = min(lo + chunk, range.y);
   }
   const int maxbin = wave_max_int(bf);
   // reduce18 lane roles, learned once: value k = slot (Gaussian slot / 9, field slot % 9)
@@ -917,8 +895,32 @@ __global__ __launch_bounds__(256) void raster_bwd8_kernel(
   const bool for0 = slot >= 0 && slot < 9, for1 = slot >= 9;
   const int field = slot >= 9 ? slot - 9 : slot;
   const float amax = __builtin_canonicalizef(alpha_max);
-  const int last = min(maxbin, hi - 1);
   GStage *stage = lds[wave];
+  if (SPLIT) {  // the positions behind this part: T and the colour behind only
+    for (int b = min(maxbin, range.y - 1); b >= hi; b -= 64) {
+      const int idx = b - (threadIdx.x & 63);
+      GStage s;
+      const bool keep = idx >= hi && stage_gaussian<true>(idx, gids, xys, conics, colors,
+                                                          opacity, R.rx0, R.rx1, R.ry0, R.ry1, s);
+      const unsigned long long kmask = __ballot(keep);
+      if (keep) stage[lanes_below(kmask)] = s;
+      const int n = __popcll(kmask);
+      wave_lds_sync();
+      for (int t = 0; t < n; ++t) {  // (the main loop's T / Sb operations, nothing else)
+        const GStage G = stage[t];
+        const float dx = G.x - px, dy = G.y - py;
+        const float sg = gs_sigma(G.hc, G.b * dx, G.ha * dx * dx, dy);
+        const float al = fminf(amax, G.o * gs_vis(sg));
+        const bool v = G.idx <= bf && sg >= 0.f && al >= ALPHA_MIN;
+        const float am = v ? al : 0.f;
+        T = T * __builtin_amdgcn_rcpf(1.f - am);
+        const float fac = am * T;
+        Sb = fmaf(fac, fmaf(G.r, vr, fmaf(G.g, vg, G.bl * vb)), Sb);
+      }
+      wave_lds_sync();
+    }
+  }
+  const int last = min(maxbin, hi - 1);
   unsigned c_slots = 0, c_live = 0, c_valid = 0;  // (CNT only)
   for (int b = last; b >= lo; b -= 64) {
     const int idx = b - (threadIdx.x & 63);
@@ -988,54 +990,84 @@ __global__ __launch_bounds__(256) void raster_bwd8_kernel(
   wlog.done(tile);
 }
 
-// List-split plan (one workgroup): per tile, the number of backward items (chunks of the
-// depth-sorted list, 1 for a tile no longer than `chunk`, 0 for an empty one) and of forward
-// checkpoints (as many as chunks for a split tile, else 0); exclusive scans of both give
-// item_off[T + 1] / ckpt_off[T + 1], and item_tile[] maps each item back to its tile.
-__global__ __launch_bounds__(1024) void chunk_plan_kernel(int T, const int2 *__restrict__ bins,
-                                                          int chunk, int *__restrict__ item_off,
-                                                          int *__restrict__ ckpt_off,
-                                                          int *__restrict__ item_tile) {
-  __shared__ int sa[1024], sc[1024];
-  const int tid = threadIdx.x;
-  const int per = (T + 1023) / 1024;
-  const int t0 = min(T, tid * per), t1 = min(T, t0 + per);
-  auto items = [&](int t, int &mi, int &mc) {
-    const int2 r = bins[t];
-    const int len = r.y - r.x;
-    mi = len <= 0 ? 0 : (len > chunk ? (len + chunk - 1) / chunk : 1);
-    mc = len > chunk ? mi : 0;
-  };
-  int a = 0, c = 0;
-  for (int t = t0; t < t1; ++t) {
-    int mi, mc;
-    items(t, mi, mc);
-    a += mi;
-    c += mc;
-  }
-  sa[tid] = a;
-  sc[tid] = c;
+// ---- list-split plan of the backward (SPLIT kernels) -------------------------------------
+// split_work_kernel (one workgroup per tile): the tile's backward walk length -- list positions
+// from range.x up to the last one any of its pixels composites (max final_idx; 0 when no pixel
+// composites anything: the tile has no backward work at all).
+__global__ __launch_bounds__(256) void split_work_kernel(int tbx, int tby, int H, int W,
+                                                         const int2 *__restrict__ bins,
+                                                         const int *__restrict__ final_idx,
+                                                         int *__restrict__ work) {
+  const int t = blockIdx.x;
+  const int i = (t / tbx) * GS_BLOCK + (threadIdx.x >> 4), j = (t % tbx) * GS_BLOCK + (threadIdx.x & 15);
+  const int2 r = bins[t];
+  int m = -1;
+  if (i < H && j < W) m = final_idx[i * W + j];
+  // a pixel that composited nothing has final_idx 0: count it only when 0 lies in the list
+  if (m < r.x) m = -1;
+  m = wave_max_int(m);
+  __shared__ int wm[4];
+  if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
   __syncthreads();
-  for (int d = 1; d < 1024; d <<= 1) {  // inclusive Hillis-Steele scan
-    const int va = tid >= d ? sa[tid - d] : 0, vc = tid >= d ? sc[tid - d] : 0;
-    __syncthreads();
-    sa[tid] += va;
-    sc[tid] += vc;
-    __syncthreads();
+  if (threadIdx.x == 0) {
+    const int mm = max(max(wm[0], wm[1]), max(wm[2], wm[3]));
+    work[t] = mm < r.x ? 0 : min(mm, r.y - 1) - r.x + 1;
   }
-  int ra = sa[tid] - a, rc = sc[tid] - c;
-  for (int t = t0; t < t1; ++t) {
-    int mi, mc;
-    items(t, mi, mc);
-    item_off[t] = ra;
-    ckpt_off[t] = rc;
-    for (int k = 0; k < mi; ++k) item_tile[ra + k] = t;
-    ra += mi;
-    rc += mc;
+}
+
+// split_plan_kernel (one workgroup): the backward's work items, longest first.  A tile with
+// walk length L (split_work_kernel) becomes one item when L <= chunk, else ceil(L / chunk) parts
+// (part k: positions [k chunk, (k + 1) chunk) of the walk).  An item's cost is its own positions
+// plus SPLIT_PREWALK_COST times the positions behind it it re-walks; items are dispatched in
+// decreasing cost (quarter-octave buckets), which is the longest-processing-time-first schedule
+// that bounds a launch's tail by its longest item rather than by where the longest tiles sit.
+// items[s] = (tile, part) of work slot s, *n_items the count.  (Order within a bucket follows
+// LDS atomics; every item is independent, so the order changes timing only.)
+constexpr float SPLIT_PREWALK_COST = 0.35f;
+__device__ __forceinline__ int split_cost_bucket(int L, int k, int chunk, bool split) {
+  const int own = split ? min(chunk, L - k * chunk) : L;
+  const int behind = split ? max(0, L - (k + 1) * chunk) : 0;
+  const unsigned c = 1u + (unsigned)(own + SPLIT_PREWALK_COST * (float)behind);
+  const int oct = 31 - __clz(c);
+  const int q = oct >= 2 ? (int)((c >> (oct - 2)) & 3u) : 0;
+  return 63 - min(63, 4 * oct + q);  // bucket 0: the costliest
+}
+
+__global__ __launch_bounds__(1024) void split_plan_kernel(int T, int chunk,
+                                                          const int *__restrict__ work,
+                                                          int2 *__restrict__ items,
+                                                          int *__restrict__ n_items) {
+  __shared__ int hist[64], cur[64];
+  const int tid = threadIdx.x;
+  if (tid < 64) hist[tid] = 0;
+  __syncthreads();
+  for (int t = tid; t < T; t += 1024) {
+    const int L = work[t];
+    if (L <= 0) continue;
+    const bool split = L > chunk;
+    const int m = split ? (L + chunk - 1) / chunk : 1;
+    for (int k = 0; k < m; ++k) atomicAdd(&hist[split_cost_bucket(L, k, chunk, split)], 1);
   }
-  if (tid == 1023) {
-    item_off[T] = sa[1023];
-    ckpt_off[T] = sc[1023];
+  __syncthreads();
+  if (tid < 64) {  // exclusive scan of the 64 bucket counts (one wave)
+    const int h = hist[tid];
+    int x = h;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int y = __shfl_up(x, d, 64);
+      if (tid >= d) x += y;
+    }
+    cur[tid] = x - h;
+    if (tid == 63) *n_items = x;
+  }
+  __syncthreads();
+  for (int t = tid; t < T; t += 1024) {
+    const int L = work[t];
+    if (L <= 0) continue;
+    const bool split = L > chunk;
+    const int m = split ? (L + chunk - 1) / chunk : 1;
+    for (int k = 0; k < m; ++k)
+      items[atomicAdd(&cur[split_cost_bucket(L, k, chunk, split)], 1)] = make_int2(t, k);
   }
 }
 
@@ -1291,31 +1323,31 @@ using namespace gs;
       hipLaunchKernelGGL(KERNEL<64>, dim3(T), dim3(256), 0, st, __VA_ARGS__);             \
   } while (0)
 
-// ---- list-split backward (checkpointed forward) ----------------------------------------
-// Workspace layout (gsplat_rasterize_checkpoint_bytes): item_off[T+1], ckpt_off[T+1],
-// item_tile[T + ceil(I/chunk)], 16-B aligned float4 ckpt[(2 ceil(I/chunk) + 1) * 256].
+// ---- list-split backward ------------------------------------------------------------------
+// Plan workspace (gsplat_rasterize_split_bytes): work[T] int, items[T + ceil(I/chunk)] int2,
+// n_items int, filled by split_work_kernel / split_plan_kernel at the start of the backward.
 int g_chunk_override = 0;  // gsplat_debug_set_chunk: 0 auto, > 0 forced, < 0 off
-struct ChunkWs {
-  int *item_off, *ckpt_off, *item_tile;
-  float4 *ckpt;
-  long long items_bound, ckpt_bound;
+constexpr double SPLIT_MEANS = 0.6;
+constexpr long long SPLIT_MAX_TILES = 12288;
+struct SplitWs {
+  int *work;
+  int2 *items;
+  int *n_items;
+  long long items_bound;
   size_t bytes;
 };
-static ChunkWs carve_chunk_ws(void *base, long long T, long long I, int chunk) {
-  ChunkWs w{};
-  const long long per = (I + chunk - 1) / chunk;
-  w.items_bound = T + per;
-  w.ckpt_bound = 2 * per + 1;
+static SplitWs carve_split_ws(void *base, long long T, long long I, int chunk) {
+  SplitWs w{};
+  w.items_bound = T + (I + chunk - 1) / chunk;
   size_t off = 0;
   auto take = [&](size_t bytes) {
     const size_t o = off;
     off += (bytes + 255) & ~(size_t)255;
     return (char *)base + o;
   };
-  w.item_off = (int *)take((size_t)(T + 1) * sizeof(int));
-  w.ckpt_off = (int *)take((size_t)(T + 1) * sizeof(int));
-  w.item_tile = (int *)take((size_t)w.items_bound * sizeof(int));
-  w.ckpt = (float4 *)take((size_t)w.ckpt_bound * GS_BLOCK * GS_BLOCK * sizeof(float4));
+  w.work = (int *)take((size_t)T * sizeof(int));
+  w.items = (int2 *)take((size_t)w.items_bound * sizeof(int2));
+  w.n_items = (int *)take(sizeof(int));
   w.bytes = off;
   return w;
 }
@@ -1325,23 +1357,25 @@ static bool default_variants() {
 
 extern "C" int gsplat_rasterize_chunk_size(int tile_bounds_x, int tile_bounds_y,
                                            int64_t num_intersects) {
-  if (g_chunk_override < 0 || num_intersects <= 0) return 0;
+  if (g_chunk_override < 0 || num_intersects <= 0 || tile_bounds_x <= 0 || tile_bounds_y <= 0)
+    return 0;
   if (g_chunk_override > 0) return (g_chunk_override + 63) / 64 * 64;
-  // Split only frames with too few tiles to occupy the chip: the backward runs 2 waves per
-  // tile and ~7 fit per SIMD (7,168 on 256 CUs), so below ~3,584 tiles (e.g. 512x512 =
-  // 1,024) CUs sit idle and splitting lists into 256-position chunks pays (bear c3: backward
-  // 0.269 -> 0.195 ms).  At 1080x1080 (4,624 tiles) the tile count already fills the chip
-  // and splitting measured 12-30 % slower (pixels saturate early, so the front chunk keeps
-  // the critical path while checkpoints cost traffic) -- see DESIGN.md.
+  // Parts of about SPLIT_MEANS mean list lengths, longest items first (split_plan_kernel).
+  // From SPLIT_MAX_TILES tiles up the frame alone fills the chip many times over and the
+  // cost-ordered dispatch loses more L2 locality than it saves in tail (c5 2048^2, 16,384
+  // tiles: 0.646 ms unsplit vs 0.657; headline 0.302 -> 0.276, c3 bear 0.162 -> 0.132, c4
+  // garden 0.351 -> 0.334 at 0.6 means; profiles/r03_split_sweep.txt).
   const long long T = (long long)tile_bounds_x * tile_bounds_y;
-  return T < 3584 ? 256 : 0;
+  if (T >= SPLIT_MAX_TILES) return 0;
+  const long long c = (long long)(SPLIT_MEANS * (double)num_intersects / (double)T);
+  return (int)std::min<long long>(1 << 20, std::max<long long>(256, (c + 63) / 64 * 64));
 }
 
-extern "C" size_t gsplat_rasterize_checkpoint_bytes(int tile_bounds_x, int tile_bounds_y,
-                                                    int64_t num_intersects, int chunk) {
+extern "C" size_t gsplat_rasterize_split_bytes(int tile_bounds_x, int tile_bounds_y,
+                                               int64_t num_intersects, int chunk) {
   if (chunk <= 0 || chunk % 64 || tile_bounds_x <= 0 || tile_bounds_y <= 0 || num_intersects < 0)
     return 0;
-  return carve_chunk_ws(nullptr, (long long)tile_bounds_x * tile_bounds_y, num_intersects, chunk)
+  return carve_split_ws(nullptr, (long long)tile_bounds_x * tile_bounds_y, num_intersects, chunk)
       .bytes;
 }
 
@@ -1356,20 +1390,19 @@ static bool bad_frame(int tbx, int tby, int H, int W) {
 }
 
 // The shipped C = 3 forward: 8x8 blocks, two Gaussians per iteration (CNT: the lane-slot
-// counting instantiation, same arithmetic), optional checkpoints (chunk > 0) and record clear.
-template <bool DEPTH, bool CKPT>
+// counting instantiation, same arithmetic), optional record clear.
+template <bool DEPTH>
 static void launch_fwd(hipStream_t st, int tbx, int tby, int H, int W, const int32_t *gids,
                        const int32_t *bins, const float *xys, const float *conics,
                        const float *colors, const float *opacity, const float *background,
                        float *out_img, float *final_Ts, int32_t *final_idx, const float *depths,
-                       float *out_depth, int chunk, const int *ckpt_off, float4 *ckpt,
-                       float4 *zero, long long zn, const int32_t *zero_radii) {
+                       float *out_depth, float4 *zero, long long zn, const int32_t *zero_radii) {
   const unsigned grid = cdiv((long long)tbx * tby, (tiles_per_block<1, 8>()));
 #define FWDK(CNT)                                                                          \
-  hipLaunchKernelGGL((raster_fwd3u_kernel<1, 8, DEPTH, CKPT, CNT>), dim3(grid), dim3(256), 0, st, \
-                     tbx, tby, H, W, gids, (const int2 *)bins, (const float2 *)xys, conics,      \
-                     colors, opacity, background, out_img, final_Ts, final_idx, depths,          \
-                     out_depth, chunk, ckpt_off, ckpt, zero, zn, zero_radii)
+  hipLaunchKernelGGL((raster_fwd3u_kernel<1, 8, DEPTH, CNT>), dim3(grid), dim3(256), 0, st, tbx, \
+                     tby, H, W, gids, (const int2 *)bins, (const float2 *)xys, conics, colors,  \
+                     opacity, background, out_img, final_Ts, final_idx, depths, out_depth, zero, \
+                     zn, zero_radii)
   if (!DEPTH && g_pair_count_on) FWDK(true); else FWDK(false);
 #undef FWDK
 }
@@ -1391,10 +1424,9 @@ extern "C" int gsplat_rasterize_forward(int tile_bounds_x, int tile_bounds_y, in
   }
   const int T = tile_bounds_x * tile_bounds_y;
   if (channels == 3) {
-    launch_fwd<false, false>(st, tile_bounds_x, tile_bounds_y, img_height, img_width,
-                             gaussian_ids_sorted, tile_bins, xys, conics, colors, opacity,
-                             background, out_img, final_Ts, final_idx, nullptr, nullptr, 0,
-                             nullptr, nullptr, nullptr, 0, nullptr);
+    launch_fwd<false>(st, tile_bounds_x, tile_bounds_y, img_height, img_width,
+                      gaussian_ids_sorted, tile_bins, xys, conics, colors, opacity, background,
+                      out_img, final_Ts, final_idx, nullptr, nullptr, nullptr, 0, nullptr);
   } else {
     ND_DISPATCH(raster_fwdn_kernel, tile_bounds_x, tile_bounds_y, img_height, img_width,
                 channels, gaussian_ids_sorted, (const int2 *)tile_bins, (const float2 *)xys,
@@ -1418,10 +1450,9 @@ extern "C" int gsplat_rasterize_forward_rgbd(int tile_bounds_x, int tile_bounds_
               tile_bounds_x, tile_bounds_y, img_height, img_width);
     return 1;
   }
-  launch_fwd<true, false>(st, tile_bounds_x, tile_bounds_y, img_height, img_width,
-                          gaussian_ids_sorted, tile_bins, xys, conics, colors, opacity,
-                          background, out_img, final_Ts, final_idx, depths, out_depth, 0, nullptr,
-                          nullptr, nullptr, 0, nullptr);
+  launch_fwd<true>(st, tile_bounds_x, tile_bounds_y, img_height, img_width,
+                   gaussian_ids_sorted, tile_bins, xys, conics, colors, opacity, background,
+                   out_img, final_Ts, final_idx, depths, out_depth, nullptr, 0, nullptr);
   return check_launch("rasterize_forward_rgbd");
 }
 
@@ -1490,11 +1521,17 @@ static void launch_bwd(hipStream_t st, int tbx, int tby, int H, int W, int n,
                        const float *conics, const float *colors, const float *opacity,
                        const float *background, const float *final_Ts, const int32_t *final_idx,
                        const float *v_output, const float *v_output_alpha, float alpha_max,
-                       float *rec, int chunk, const ChunkWs *w, unsigned long long *det) {
+                       float *rec, int chunk, const SplitWs *w, unsigned long long *det) {
   const long long slots = w ? w->items_bound : (long long)tbx * tby;
-  const int *io = w ? w->item_off : nullptr, *it = w ? w->item_tile : nullptr,
-            *co = w ? w->ckpt_off : nullptr;
-  const float4 *ck = w ? w->ckpt : nullptr;
+  const int2 *its = w ? w->items : nullptr;
+  const int *ni = w ? w->n_items : nullptr;
+  if (w) {
+    const int T = tbx * tby;
+    hipLaunchKernelGGL(split_work_kernel, dim3(T), dim3(256), 0, st, tbx, tby, H, W,
+                       (const int2 *)bins, final_idx, w->work);
+    hipLaunchKernelGGL(split_plan_kernel, dim3(1), dim3(1024), 0, st, T, chunk,
+                       (const int *)w->work, w->items, w->n_items);
+  }
   const bool cnt = g_pair_count_on && !det;
   if (bwd_geometry(tbx, tby) == 1) {
     const unsigned grid = cdiv(slots, (tiles_per_block<1, 8>()));
@@ -1502,7 +1539,7 @@ static void launch_bwd(hipStream_t st, int tbx, int tby, int H, int W, int n,
   hipLaunchKernelGGL((raster_bwd8_kernel<CH, DET, CNT>), dim3(grid), dim3(256), 0, st, tbx, tby, \
                      H, W, gids, (const int2 *)bins, (const float2 *)xys, conics, colors,       \
                      opacity, background, final_Ts, final_idx, v_output, v_output_alpha,        \
-                     alpha_max, rec, chunk, io, it, co, ck, det)
+                     alpha_max, rec, chunk, its, ni, det)
     if (w) {
       if (det) BWD8(true, true, false); else if (cnt) BWD8(true, false, true);
       else BWD8(true, false, false);
@@ -1517,7 +1554,7 @@ static void launch_bwd(hipStream_t st, int tbx, int tby, int H, int W, int n,
   hipLaunchKernelGGL((raster_bwd3p_kernel<1, true, 16, CH, f2, DET, CNT>), dim3(grid), dim3(256), \
                      0, st, tbx, tby, H, W, gids, (const int2 *)bins, (const float2 *)xys,      \
                      conics, colors, opacity, background, final_Ts, final_idx, v_output,        \
-                     v_output_alpha, alpha_max, rec, false, chunk, io, it, co, ck, det)
+                     v_output_alpha, alpha_max, rec, chunk, its, ni, det)
     if (w) {
       if (det) BWDS(true, true, false); else if (cnt) BWDS(true, false, true);
       else BWDS(true, false, false);
@@ -1539,13 +1576,12 @@ static int backward_into_records(const char *who, hipStream_t st, int tbx, int t
                                  const float *final_Ts, const int32_t *final_idx,
                                  const float *v_output, const float *v_output_alpha,
                                  float alpha_max, float *rec, int64_t num_intersects, int chunk,
-                                 const void *checkpoints, size_t checkpoint_bytes) {
-  ChunkWs w{};
+                                 void *plan, size_t plan_bytes) {
+  SplitWs w{};
   if (chunk > 0) {
-    w = carve_chunk_ws(const_cast<void *>(checkpoints), (long long)tbx * tby, num_intersects,
-                       chunk);
-    if (!checkpoints || checkpoint_bytes < w.bytes) {
-      set_error("%s: checkpoint buffer %zu < %zu bytes", who, checkpoint_bytes, w.bytes);
+    w = carve_split_ws(plan, (long long)tbx * tby, num_intersects, chunk);
+    if (!plan || plan_bytes < w.bytes) {
+      set_error("%s: split plan buffer %zu < %zu bytes", who, plan_bytes, w.bytes);
       return 1;
     }
   }
@@ -1629,71 +1665,26 @@ extern "C" int gsplat_rasterize_backward(int tile_bounds_x, int tile_bounds_y, i
   return check_launch("rasterize_backward");
 }
 
-static int rasterize_forward_impl(int tile_bounds_x, int tile_bounds_y, int img_height,
-                                  int img_width, const int32_t *gaussian_ids_sorted,
-                                  const int32_t *tile_bins, const float *xys, const float *conics,
-                                  const float *colors, const float *opacity,
-                                  const float *background, float *out_img, float *final_Ts,
-                                  int32_t *final_idx, int64_t num_intersects, int chunk,
-                                  void *checkpoints, size_t checkpoint_bytes, void *zero,
-                                  size_t zero_bytes, const int32_t *zero_radii, void *stream,
-                                  const char *who) {
-  hipStream_t st = (hipStream_t)stream;
-  if (bad_frame(tile_bounds_x, tile_bounds_y, img_height, img_width) ||
-      (chunk > 0 && chunk % 64) || num_intersects < 0 || zero_bytes % 16 ||
-      (zero_bytes && !zero) || (zero_radii && zero_bytes % 64)) {
-    set_error("%s: bad sizes (tiles=%dx%d H=%d W=%d chunk=%d zero=%zu)", who, tile_bounds_x,
-              tile_bounds_y, img_height, img_width, chunk, zero_bytes);
-    return 1;
-  }
-  const int T = tile_bounds_x * tile_bounds_y;
-  const long long zn = (long long)(zero_bytes / 16);
-  if (chunk <= 0) {
-    launch_fwd<false, false>(st, tile_bounds_x, tile_bounds_y, img_height, img_width,
-                             gaussian_ids_sorted, tile_bins, xys, conics, colors, opacity,
-                             background, out_img, final_Ts, final_idx, nullptr, nullptr, 0,
-                             nullptr, nullptr, (float4 *)zero, zn, zero_radii);
-    return check_launch(who);
-  }
-  const ChunkWs w = carve_chunk_ws(checkpoints, T, num_intersects, chunk);
-  if (!checkpoints || checkpoint_bytes < w.bytes) {
-    set_error("%s: checkpoint buffer %zu < %zu bytes", who, checkpoint_bytes, w.bytes);
-    return 1;
-  }
-  hipLaunchKernelGGL(chunk_plan_kernel, dim3(1), dim3(1024), 0, st, T, (const int2 *)tile_bins,
-                     chunk, w.item_off, w.ckpt_off, w.item_tile);
-  launch_fwd<false, true>(st, tile_bounds_x, tile_bounds_y, img_height, img_width,
-                          gaussian_ids_sorted, tile_bins, xys, conics, colors, opacity,
-                          background, out_img, final_Ts, final_idx, nullptr, nullptr, chunk,
-                          w.ckpt_off, w.ckpt, (float4 *)zero, zn, zero_radii);
-  return check_launch(who);
-}
-
-extern "C" int gsplat_rasterize_forward_chunked(
-    int tile_bounds_x, int tile_bounds_y, int img_height, int img_width,
-    const int32_t *gaussian_ids_sorted, const int32_t *tile_bins, const float *xys,
-    const float *conics, const float *colors, const float *opacity, const float *background,
-    float *out_img, float *final_Ts, int32_t *final_idx, int64_t num_intersects, int chunk,
-    void *checkpoints, size_t checkpoint_bytes, void *stream) {
-  return rasterize_forward_impl(tile_bounds_x, tile_bounds_y, img_height, img_width,
-                                gaussian_ids_sorted, tile_bins, xys, conics, colors, opacity,
-                                background, out_img, final_Ts, final_idx, num_intersects, chunk,
-                                checkpoints, checkpoint_bytes, nullptr, 0, nullptr, stream,
-                                "rasterize_forward_chunked");
-}
-
+// The RGB forward that also clears the gradient records of the Gaussians the backward will
+// accumulate into (all records, or those with radii > 0 when clear_radii is given).
 extern "C" int gsplat_rasterize_forward_clearing(
     int tile_bounds_x, int tile_bounds_y, int img_height, int img_width,
     const int32_t *gaussian_ids_sorted, const int32_t *tile_bins, const float *xys,
     const float *conics, const float *colors, const float *opacity, const float *background,
-    float *out_img, float *final_Ts, int32_t *final_idx, int64_t num_intersects, int chunk,
-    void *checkpoints, size_t checkpoint_bytes, void *clear, size_t clear_bytes,
+    float *out_img, float *final_Ts, int32_t *final_idx, void *clear, size_t clear_bytes,
     const int32_t *clear_radii, void *stream) {
-  return rasterize_forward_impl(tile_bounds_x, tile_bounds_y, img_height, img_width,
-                                gaussian_ids_sorted, tile_bins, xys, conics, colors, opacity,
-                                background, out_img, final_Ts, final_idx, num_intersects, chunk,
-                                checkpoints, checkpoint_bytes, clear, clear_bytes, clear_radii,
-                                stream, "rasterize_forward_clearing");
+  const char *who = "rasterize_forward_clearing";
+  if (bad_frame(tile_bounds_x, tile_bounds_y, img_height, img_width) || clear_bytes % 16 ||
+      (clear_bytes && !clear) || (clear_radii && clear_bytes % 64)) {
+    set_error("%s: bad sizes (tiles=%dx%d H=%d W=%d clear=%zu)", who, tile_bounds_x,
+              tile_bounds_y, img_height, img_width, clear_bytes);
+    return 1;
+  }
+  launch_fwd<false>((hipStream_t)stream, tile_bounds_x, tile_bounds_y, img_height, img_width,
+                    gaussian_ids_sorted, tile_bins, xys, conics, colors, opacity, background,
+                    out_img, final_Ts, final_idx, nullptr, nullptr, (float4 *)clear,
+                    (long long)(clear_bytes / 16), clear_radii);
+  return check_launch(who);
 }
 
 extern "C" int gsplat_rasterize_backward_chunked(
@@ -1702,8 +1693,8 @@ extern "C" int gsplat_rasterize_backward_chunked(
     const float *conics, const float *colors, const float *opacity, const float *background,
     const float *final_Ts, const int32_t *final_idx, const float *v_output,
     const float *v_output_alpha, float alpha_max, float *v_xy, float *v_conic, float *v_colors,
-    float *v_opacity, int64_t num_intersects, int chunk, const void *checkpoints,
-    size_t checkpoint_bytes, void *workspace, size_t workspace_bytes, void *stream) {
+    float *v_opacity, int64_t num_intersects, int chunk, void *plan, size_t plan_bytes,
+    void *workspace, size_t workspace_bytes, void *stream) {
   if (chunk <= 0)
     return gsplat_rasterize_backward(tile_bounds_x, tile_bounds_y, img_height, img_width, 3,
                                      num_points, gaussian_ids_sorted, tile_bins, xys, conics,
@@ -1726,8 +1717,8 @@ extern "C" int gsplat_rasterize_backward_chunked(
   if (backward_into_records("rasterize_backward_chunked", st, tile_bounds_x, tile_bounds_y,
                             img_height, img_width, num_points, gaussian_ids_sorted, tile_bins, xys,
                             conics, colors, opacity, background, final_Ts, final_idx, v_output,
-                            v_output_alpha, alpha_max, rec, num_intersects, chunk, checkpoints,
-                            checkpoint_bytes))
+                            v_output_alpha, alpha_max, rec, num_intersects, chunk, plan,
+                            plan_bytes))
     return 1;
   launch_split(st, num_points, rec, conics, opacity, v_xy, v_conic, v_colors, v_opacity);
   return check_launch("rasterize_backward_chunked");
@@ -1760,8 +1751,7 @@ extern "C" int gsplat_rasterize_backward_records(
     const float *conics, const float *colors, const float *opacity, const float *background,
     const float *final_Ts, const int32_t *final_idx, const float *v_output,
     const float *v_output_alpha, float alpha_max, int64_t num_intersects, int chunk,
-    const void *checkpoints, size_t checkpoint_bytes, void *records, size_t records_bytes,
-    void *stream) {
+    void *plan, size_t plan_bytes, void *records, size_t records_bytes, void *stream) {
   hipStream_t st = (hipStream_t)stream;
   const size_t need = gsplat_grad_records_bytes(num_points);
   if (bad_frame(tile_bounds_x, tile_bounds_y, img_height, img_width) || num_points < 0 ||
@@ -1778,7 +1768,7 @@ extern "C" int gsplat_rasterize_backward_records(
                             img_height, img_width, num_points, gaussian_ids_sorted, tile_bins, xys,
                             conics, colors, opacity, background, final_Ts, final_idx, v_output,
                             v_output_alpha, alpha_max, (float *)records, num_intersects, chunk,
-                            checkpoints, checkpoint_bytes))
+                            plan, plan_bytes))
     return 1;
   return check_launch("rasterize_backward_records");
 }

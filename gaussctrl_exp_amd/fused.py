@@ -76,7 +76,7 @@ class _FusedRender(Function):
                   ws1.numel(), st)
         num_intersects, gids, bins = bin_gaussians(xys, depths, radii, nth, H, W,
                                                    keyed_workspace=ws1)
-        chunk, ckpt = 0, None
+        chunk, plan = 0, None
         if num_intersects < 1:
             # nothing visible: the background (the caller returns it at gc_model.py:189-190),
             # and every gradient is zero
@@ -91,23 +91,21 @@ class _FusedRender(Function):
             final_idx = torch.empty((H, W), device=dev, dtype=torch.int32)
             chunk = _lib.query("gsplat_rasterize_chunk_size", tbx, tby, num_intersects) \
                 if need_grad else 0
-            if chunk > 0:
-                ckpt = torch.empty((_lib.query("gsplat_rasterize_checkpoint_bytes", tbx, tby,
+            if chunk > 0:  # the list-split backward's plan (filled at the backward's start)
+                plan = torch.empty((_lib.query("gsplat_rasterize_split_bytes", tbx, tby,
                                                num_intersects, chunk),),
                                    device=dev, dtype=torch.uint8)
             # the blend kernel also clears the gradient records the backward accumulates into
             _lib.call("gsplat_rasterize_forward_clearing", tbx, tby, H, W, P(gids), P(bins),
                       P(xys), P(conics), P(colors), P(opac), P(background), P(out_img),
-                      P(final_Ts), P(final_idx), num_intersects, chunk, P(ckpt),
-                      ckpt.numel() if ckpt is not None else 0, P(rec),
-                      rec.numel() if rec is not None else 0,
+                      P(final_Ts), P(final_idx), P(rec), rec.numel() if rec is not None else 0,
                       # skip culled Gaussians' records when many are culled (real scenes);
                       # at ~all visible the radii loads cost more than the stores they save
                       P(radii) if rec is not None and last_num_visible(dev) < 0.9 * n else None,
                       st)
         ctx.meta = (n, K, int(degrees_to_use), float(fx), float(fy), float(cx), float(cy), H, W,
                     tbx, tby, num_intersects, chunk)
-        ctx.ckpt, ctx.rec = ckpt, rec
+        ctx.plan, ctx.rec = plan, rec
         ctx.opac_shape = opacities.shape
         ctx.exchange = exchange.active() if K > 1 else None
         # data-parallel: all-reduce the four non-SH gradients from inside the backward (one flat
@@ -153,7 +151,7 @@ class _FusedRender(Function):
             _lib.call("gsplat_rasterize_backward_records", tbx, tby, H, W, n, P(gids), P(bins),
                       P(xys), P(conics), P(colors), P(opac), P(background), P(final_Ts),
                       P(final_idx), P(v_img), P(v_alpha), quirks.backward_alpha_clamp(), I, chunk,
-                      P(ctx.ckpt), ctx.ckpt.numel() if ctx.ckpt is not None else 0, P(rec),
+                      P(ctx.plan), ctx.plan.numel() if ctx.plan is not None else 0, P(rec),
                       rec.numel(), st)
         if ctx.adam is not None:
             # Adam inside the backward: parameters (and moments) updated in place, no gradients

@@ -345,44 +345,25 @@ class _RasterizeGaussians(Function):
             final_idx = torch.zeros(H, W, device=dev, dtype=torch.int32)
         else:
             P = _lib.ptr
-            grads = C == 3 and any(ctx.needs_input_grad)
-            # list-split backward (C = 3, gradients wanted): the forward records checkpoints
-            chunk = _lib.query("gsplat_rasterize_chunk_size", tbx, tby, num_intersects) \
-                if grads else 0
-            if chunk > 0 or (grads and _lib.lib().gsplat_debug_raster_variant_is_default()):
-                out_img = torch.empty((H, W, C), device=dev, dtype=torch.float32)
-                final_Ts = torch.empty((H, W), device=dev, dtype=torch.float32)
-                final_idx = torch.empty((H, W), device=dev, dtype=torch.int32)
-            if grads and _lib.lib().gsplat_debug_raster_variant_is_default():
+            if C == 3 and any(ctx.needs_input_grad) and \
+                    _lib.lib().gsplat_debug_raster_variant_is_default():
                 # the backward accumulates into per-Gaussian gradient records that this blend
                 # zeroes as its waves finish (no memset in the backward; every record, since
                 # gsplat_grad_records_split reads the culled Gaussians' zeros too)
-                ckpt = torch.empty((max(_lib.query("gsplat_rasterize_checkpoint_bytes", tbx,
-                                                   tby, num_intersects, chunk), 1),),
-                                   device=dev, dtype=torch.uint8) if chunk > 0 else None
+                out_img = torch.empty((H, W, C), device=dev, dtype=torch.float32)
+                final_Ts = torch.empty((H, W), device=dev, dtype=torch.float32)
+                final_idx = torch.empty((H, W), device=dev, dtype=torch.int32)
                 rec = torch.empty((_lib.query("gsplat_grad_records_bytes", num_points),),
                                   device=dev, dtype=torch.uint8)
                 _lib.call("gsplat_rasterize_forward_clearing", tbx, tby, H, W,
                           P(gaussian_ids_sorted), P(tile_bins), P(xys), P(conics), P(colors),
                           P(opacity), P(background), P(out_img), P(final_Ts), P(final_idx),
-                          num_intersects, chunk, P(ckpt), ckpt.numel() if chunk > 0 else 0,
                           P(rec), rec.numel(), None, _lib.stream(dev))
-                ctx.chunk, ctx.ckpt, ctx.rec = chunk, ckpt, rec
-            elif chunk > 0:
-                ckpt = torch.empty((_lib.query("gsplat_rasterize_checkpoint_bytes", tbx, tby,
-                                               num_intersects, chunk),),
-                                   device=dev, dtype=torch.uint8)
-                _lib.call("gsplat_rasterize_forward_chunked", tbx, tby, H, W,
-                          P(gaussian_ids_sorted), P(tile_bins), P(xys), P(conics), P(colors),
-                          P(opacity), P(background), P(out_img), P(final_Ts), P(final_idx),
-                          num_intersects, chunk, P(ckpt), ckpt.numel(), _lib.stream(dev))
-                ctx.chunk, ctx.ckpt = chunk, ckpt
+                ctx.rec = rec
             else:
                 out_img, final_Ts, final_idx = ops().raster_fwd(
                     tbx, tby, H, W, gaussian_ids_sorted, tile_bins, xys, conics, colors,
                     opacity, background)
-        if not hasattr(ctx, "chunk"):
-            ctx.chunk, ctx.ckpt = 0, None
         if not hasattr(ctx, "rec"):
             ctx.rec = None
 
@@ -420,7 +401,10 @@ class _RasterizeGaussians(Function):
                 v_out_alpha = v_out_alpha.float().contiguous()
             tbx = (W + BLOCK_X - 1) // BLOCK_X
             tby = (H + BLOCK_Y - 1) // BLOCK_Y
-            if ctx.rec is None and ctx.chunk == 0:  # plain list walk: the torch op layer
+            # list-split backward (C = 3): the plan buffer its first two kernels fill
+            chunk = _lib.query("gsplat_rasterize_chunk_size", tbx, tby, ctx.num_intersects) \
+                if C == 3 else 0
+            if ctx.rec is None and chunk == 0:  # plain list walk: the torch op layer
                 v_xy, v_conic, v_colors, v_opacity = ops().raster_bwd(
                     tbx, tby, H, W, gaussian_ids_sorted, tile_bins, xys, conics, colors, opacity,
                     background, final_Ts, final_idx, v_out_img, v_out_alpha,
@@ -432,14 +416,18 @@ class _RasterizeGaussians(Function):
             v_colors = torch.empty((num_points, C), device=dev, dtype=torch.float32)
             v_opacity = torch.empty(ctx.opacity_shape, device=dev, dtype=torch.float32)
             P = _lib.ptr
+            plan = torch.empty((max(_lib.query("gsplat_rasterize_split_bytes", tbx, tby,
+                                               ctx.num_intersects, chunk), 1),),
+                               device=dev, dtype=torch.uint8)
+            plan_bytes = plan.numel() if chunk > 0 else 0
+            st = _lib.stream(dev)
             if ctx.rec is not None:  # records cleared by the forward blend
-                rec, st = ctx.rec, _lib.stream(dev)
+                rec = ctx.rec
                 _lib.call("gsplat_rasterize_backward_records", tbx, tby, H, W, num_points,
                           P(gaussian_ids_sorted), P(tile_bins), P(xys), P(conics), P(colors),
                           P(opacity), P(background), P(final_Ts), P(final_idx), P(v_out_img),
                           P(v_out_alpha), quirks.backward_alpha_clamp(), ctx.num_intersects,
-                          ctx.chunk, P(ctx.ckpt), ctx.ckpt.numel() if ctx.ckpt is not None
-                          else 0, P(rec), rec.numel(), st)
+                          chunk, P(plan), plan_bytes, P(rec), rec.numel(), st)
                 _lib.call("gsplat_grad_records_split", num_points, P(rec), rec.numel(),
                           P(conics), P(opacity), P(v_xy), P(v_conic), P(v_colors), P(v_opacity),
                           st)
@@ -452,8 +440,8 @@ class _RasterizeGaussians(Function):
                       P(gaussian_ids_sorted), P(tile_bins), P(xys), P(conics), P(colors),
                       P(opacity), P(background), P(final_Ts), P(final_idx), P(v_out_img),
                       P(v_out_alpha), quirks.backward_alpha_clamp(), P(v_xy), P(v_conic),
-                      P(v_colors), P(v_opacity), ctx.num_intersects, ctx.chunk,
-                      P(ctx.ckpt), ctx.ckpt.numel(), P(ws), wsz, _lib.stream(dev))
+                      P(v_colors), P(v_opacity), ctx.num_intersects, chunk, P(plan),
+                      plan_bytes, P(ws), wsz, st)
 
         return (
             v_xy,  # xys

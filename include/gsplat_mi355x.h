@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define GSPLAT_MI355X_ABI_VERSION 8
+#define GSPLAT_MI355X_ABI_VERSION 9
 
 int gsplat_abi_version(void);
 const char *gsplat_last_error(void);
@@ -229,45 +229,40 @@ int gsplat_rasterize_forward_rgbd(int tile_bounds_x, int tile_bounds_y, int img_
  * records the kernel accumulates into (gsplat_rasterize_backward_workspace_size bytes;
  * may be 0 / NULL when that size is 0). */
 /* List-split backward (C = 3; no gsplat counterpart).  gsplat's backward walks each tile's
- * whole depth-sorted list from the back; with few tiles (small images) or a few very long
- * lists (real scenes) that leaves the GPU idle.  The chunked forward records, for every tile
- * whose list is longer than `chunk` (a multiple of 64), each pixel's (T, accumulated RGB)
- * after every `chunk` list positions and at the end; the chunked backward then processes
- * every (tile, chunk) pair independently, starting from those states.  Outputs equal the
- * unchunked entry points' (forward: identical; gradients: within fp32 rounding).
- * gsplat_rasterize_chunk_size picks `chunk` (0 = do not split) for a frame's intersection
- * count; gsplat_rasterize_checkpoint_bytes sizes the buffer the forward fills and the
- * backward reads.  chunk <= 0 makes both entries the plain ones. */
+ * whole depth-sorted list from the back, one block per tile; with few tiles (small images) or
+ * a few very long lists (real scenes) the longest tiles' waves bound the launch while the rest
+ * of the GPU idles.  The chunked backward cuts every tile's walk (list positions up to the
+ * last one any of its pixels composites, from final_idx) into parts of `chunk` (a multiple of
+ * 64) positions and runs each part as its own waves, the long tiles' parts dispatched first.
+ * A part's waves first re-walk the positions behind it computing only transmittance and the
+ * colour behind, with the very operations of the full walk, so every wave's per-Gaussian totals
+ * are bit-identical to the unsplit walk's (gradients: within fp32 atomic-order rounding, and
+ * bit-identical in the deterministic mode).  gsplat_rasterize_chunk_size picks `chunk` (0 = do
+ * not split) for a frame; gsplat_rasterize_split_bytes sizes the plan buffer the backward
+ * fills at its start (per-tile walk lengths and the (tile, part) dispatch list).
+ * chunk <= 0 makes the entry the plain gsplat_rasterize_backward (C = 3). */
 int gsplat_rasterize_chunk_size(int tile_bounds_x, int tile_bounds_y, int64_t num_intersects);
-size_t gsplat_rasterize_checkpoint_bytes(int tile_bounds_x, int tile_bounds_y,
-                                         int64_t num_intersects, int chunk);
-int gsplat_rasterize_forward_chunked(
-    int tile_bounds_x, int tile_bounds_y, int img_height, int img_width,
-    const int32_t *gaussian_ids_sorted, const int32_t *tile_bins, const float *xys,
-    const float *conics, const float *colors, const float *opacity, const float *background,
-    float *out_img, float *final_Ts, int32_t *final_idx, int64_t num_intersects, int chunk,
-    void *checkpoints, size_t checkpoint_bytes, void *stream);
+size_t gsplat_rasterize_split_bytes(int tile_bounds_x, int tile_bounds_y, int64_t num_intersects,
+                                    int chunk);
 int gsplat_rasterize_backward_chunked(
     int tile_bounds_x, int tile_bounds_y, int img_height, int img_width, int num_points,
     const int32_t *gaussian_ids_sorted, const int32_t *tile_bins, const float *xys,
     const float *conics, const float *colors, const float *opacity, const float *background,
     const float *final_Ts, const int32_t *final_idx, const float *v_output,
     const float *v_output_alpha, float alpha_max, float *v_xy, float *v_conic, float *v_colors,
-    float *v_opacity, int64_t num_intersects, int chunk, const void *checkpoints,
-    size_t checkpoint_bytes, void *workspace, size_t workspace_bytes, void *stream);
-/* The RGB forward (plain when chunk <= 0, chunked otherwise) that also clears
- * `clear_bytes` (a multiple of 16) at `clear`: the fused training render hands it the
- * per-Gaussian gradient records, which the blend kernel zeroes with the memory bandwidth its
- * VALU-bound loop leaves idle (instead of the preprocess kernel spending ~18 us on it).
- * With clear_radii != NULL the buffer is 64-B records and record g is cleared only when
- * clear_radii[g] > 0 (the backward touches no other).  Outputs equal
- * gsplat_rasterize_forward(_chunked)'s. */
+    float *v_opacity, int64_t num_intersects, int chunk, void *plan, size_t plan_bytes,
+    void *workspace, size_t workspace_bytes, void *stream);
+/* The RGB forward (C = 3) that also clears `clear_bytes` (a multiple of 16) at `clear`: the
+ * fused training render hands it the per-Gaussian gradient records, which the blend kernel
+ * zeroes with the memory bandwidth its VALU-bound loop leaves idle (instead of the preprocess
+ * kernel spending ~18 us on it).  With clear_radii != NULL the buffer is 64-B records and
+ * record g is cleared only when clear_radii[g] > 0 (the backward touches no other).  Outputs
+ * equal gsplat_rasterize_forward's. */
 int gsplat_rasterize_forward_clearing(
     int tile_bounds_x, int tile_bounds_y, int img_height, int img_width,
     const int32_t *gaussian_ids_sorted, const int32_t *tile_bins, const float *xys,
     const float *conics, const float *colors, const float *opacity, const float *background,
-    float *out_img, float *final_Ts, int32_t *final_idx, int64_t num_intersects, int chunk,
-    void *checkpoints, size_t checkpoint_bytes, void *clear, size_t clear_bytes,
+    float *out_img, float *final_Ts, int32_t *final_idx, void *clear, size_t clear_bytes,
     const int32_t *clear_radii, void *stream);
 /* Debug: force the list-split chunk (> 0, rounded up to 64), disable it (< 0) or restore
  * the automatic choice (0). */
@@ -369,8 +364,7 @@ int gsplat_rasterize_backward_records(
     const float *conics, const float *colors, const float *opacity, const float *background,
     const float *final_Ts, const int32_t *final_idx, const float *v_output,
     const float *v_output_alpha, float alpha_max, int64_t num_intersects, int chunk,
-    const void *checkpoints, size_t checkpoint_bytes, void *records, size_t records_bytes,
-    void *stream);
+    void *plan, size_t plan_bytes, void *records, size_t records_bytes, void *stream);
 /* The records -> gsplat's four rasterize gradients (v_xy [N,2], v_conic [N,3] in gsplat's
  * convention (GSPLAT_QUIRK_CONIC_HALF), v_colors [N,3], v_opacity [N]) -- the tail of
  * gsplat_rasterize_backward, for a caller that cleared the records in the forward blend
@@ -381,11 +375,11 @@ int gsplat_grad_records_split(int num_points, const void *records, size_t record
                               float *v_conic, float *v_colors, float *v_opacity, void *stream);
 
 /* Measurement hook (not part of the gsplat surface): fwd_pxl must be 1 (the forward's 8x8
- * blocks); bwd_pxl selects the C = 3 backward's geometry: 1 = 8x8 blocks, one pixel per lane,
- * two Gaussians per iteration (shipped), 2 = 16x8 strips, two pixels per lane (the round-2
- * kernel, kept for A/B timing); bwd_flags bits 20-27 = K: the block -> tile order of the blend
+ * blocks); bwd_pxl selects the C = 3 backward's geometry: 0 = by frame size (shipped: blocks
+ * below 3,584 tiles, strips above), 1 = 8x8 blocks, one pixel per lane, two Gaussians per
+ * iteration, 2 = 16x8 strips, two pixels per lane; bwd_flags bits 20-27 = K: the block -> tile order of the blend
  * kernels, chunks of K block slots dealt round-robin over the 8 XCDs (0: the shipped K = 8, 255:
- * plain dispatch order).  Both geometries meet the same parity bar.  Process-wide; (1, 1, 0) is
+ * plain dispatch order).  Both geometries meet the same parity bar.  Process-wide; (1, 0, 0) is
  * the shipped configuration. */
 int gsplat_debug_set_raster_variant(int fwd_pxl, int bwd_pxl, int bwd_flags);
 /* 1 while the shipped raster variants are selected (the record-based entries need them). */
@@ -436,7 +430,7 @@ int gsplat_debug_binning_scheme(int bucket);
 int gsplat_debug_wave_log(void *buffer);
 /* Debug: lane-slot accounting of the shipped blend kernels (separate counting instantiations,
  * the shipped code is unchanged).  buffer = device u64[6], accumulated by every later forward
- * (clearing / chunked) and record backward launch until called again with NULL:
+ * (clearing) and record backward launch until called again with NULL:
  * [0] backward lane slots (wave iterations x 128 pixel slots), [1] slots whose pixel is live for
  * the Gaussian (in the image, idx <= final_idx), [2] valid pairs (sigma >= 0, alpha >= 1/255);
  * [3..5] the same for the forward (wave iterations x 2 Gaussians x 64 pixels; live = not yet

@@ -67,7 +67,7 @@ class FusedRun:
         self.rec = torch.full((_lib.query("gsplat_grad_records_bytes", n),), 0x7F, device=gpu,
                               dtype=torch.uint8)
         self.chunk = _lib.query("gsplat_rasterize_chunk_size", self.tb[0], self.tb[1], self.I)
-        self.ckpt = torch.empty((max(_lib.query("gsplat_rasterize_checkpoint_bytes", self.tb[0],
+        self.plan = torch.empty((max(_lib.query("gsplat_rasterize_split_bytes", self.tb[0],
                                                 self.tb[1], self.I, self.chunk), 1),),
                                 device=gpu, dtype=torch.uint8)
         self.bg = torch.tensor([0.3, 0.2, 0.1], device=gpu)
@@ -82,8 +82,8 @@ class FusedRun:
         vis_only = self.radii if int((self.radii > 0).sum()) < 0.9 * self.n else None
         _lib.call("gsplat_rasterize_forward_clearing", self.tb[0], self.tb[1], H, W, P(self.gids),
                   P(self.bins), P(self.xys), P(self.conics), P(self.colors), P(self.opac),
-                  P(self.bg), P(img), P(fT), P(fi), self.I, self.chunk, P(self.ckpt),
-                  self.ckpt.numel(), P(self.rec), self.rec.numel(), P(vis_only), st)
+                  P(self.bg), P(img), P(fT), P(fi), P(self.rec), self.rec.numel(), P(vis_only),
+                  st)
         self.fT, self.fi = fT, fi
         return img, fT, fi
 
@@ -97,7 +97,8 @@ class FusedRun:
                   self.n, P(self.gids), P(self.bins), P(self.xys), P(self.conics),
                   P(self.colors), P(self.opac), P(self.bg), P(fT), P(fi),
                   P(self.v_img), P(self.v_alpha), quirks.backward_alpha_clamp(), self.I,
-                  self.chunk, P(self.ckpt), self.ckpt.numel(), P(self.rec), self.rec.numel(), st)
+                  self.chunk, P(self.plan), self.plan.numel() if self.chunk > 0 else 0, P(self.rec),
+                  self.rec.numel(), st)
 
     def raster_grads(self):
         """The records (pixel moments) -> gsplat's four raster gradients (the split kernel)."""

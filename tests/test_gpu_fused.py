@@ -130,9 +130,8 @@ def test_fused_forward_bitexact_given_activations(gpu, case):
 
 
 @pytest.mark.parametrize("case", [CASES[0], CASES[1], CASES[6]])
-@pytest.mark.parametrize("chunked", [False, True])
-def test_forward_clearing_equals_forward_and_clears_records(gpu, case, chunked):
-    """gsplat_rasterize_forward_clearing: the blend's outputs are those of the plain (chunked)
+def test_forward_clearing_equals_forward_and_clears_records(gpu, case):
+    """gsplat_rasterize_forward_clearing: the blend's outputs are those of the plain
     forward, and the record buffer is all zero afterwards whatever it held."""
     from gaussctrl_exp_amd.project_gaussians import project_gaussians
     from gaussctrl_exp_amd.rasterize import bin_gaussians
@@ -150,9 +149,6 @@ def test_forward_clearing_equals_forward_and_clears_records(gpu, case, chunked):
     opac = torch.rand(n, device=gpu)
     bg = torch.tensor([0.2, 0.4, 0.6], device=gpu)
     P, st = _lib.ptr, _lib.stream(gpu)
-    chunk = 64 if chunked else 0
-    ckpt = torch.empty(max(_lib.query("gsplat_rasterize_checkpoint_bytes", tb[0], tb[1], I,
-                                      chunk), 1), device=gpu, dtype=torch.uint8)
     outs = []
     for clear in (False, True):
         img = torch.full((H, W, 3), float("nan"), device=gpu)
@@ -162,32 +158,31 @@ def test_forward_clearing_equals_forward_and_clears_records(gpu, case, chunked):
             rec = torch.full((_lib.query("gsplat_grad_records_bytes", n),), 255, device=gpu,
                              dtype=torch.uint8)
             _lib.call("gsplat_rasterize_forward_clearing", tb[0], tb[1], H, W, P(gids), P(bins),
-                      P(xys), P(conics), P(colors), P(opac), P(bg), P(img), P(fT), P(fi), I,
-                      chunk, P(ckpt), ckpt.numel(), P(rec), rec.numel(), None, st)
+                      P(xys), P(conics), P(colors), P(opac), P(bg), P(img), P(fT), P(fi),
+                      P(rec), rec.numel(), None, st)
             torch.cuda.synchronize()
             assert int(rec.count_nonzero()) == 0
             # visible-only clearing: culled Gaussians' records keep their bytes
             rec.fill_(255)
             img2 = torch.empty_like(img)
             _lib.call("gsplat_rasterize_forward_clearing", tb[0], tb[1], H, W, P(gids), P(bins),
-                      P(xys), P(conics), P(colors), P(opac), P(bg), P(img2), P(fT), P(fi), I,
-                      chunk, P(ckpt), ckpt.numel(), P(rec), rec.numel(), P(radii), st)
+                      P(xys), P(conics), P(colors), P(opac), P(bg), P(img2), P(fT), P(fi),
+                      P(rec), rec.numel(), P(radii), st)
             r = rec.view(n, 64)
             vis = radii > 0
             assert (~vis).any() or n == int(vis.sum())
             assert int(r[vis].count_nonzero()) == 0 and bool((r[~vis] == 255).all())
             assert torch.equal(img2, img)
         else:
-            _lib.call("gsplat_rasterize_forward_chunked", tb[0], tb[1], H, W, P(gids), P(bins),
-                      P(xys), P(conics), P(colors), P(opac), P(bg), P(img), P(fT), P(fi), I,
-                      chunk, P(ckpt), ckpt.numel(), st)
+            _lib.call("gsplat_rasterize_forward", tb[0], tb[1], H, W, 3, P(gids), P(bins),
+                      P(xys), P(conics), P(colors), P(opac), P(bg), P(img), P(fT), P(fi), st)
         outs.append((img, fT, fi))
     for name, a, b in zip(("img", "final_Ts", "final_idx"), *outs):
         assert torch.equal(a, b), name
     with pytest.raises(RuntimeError):  # clear size must be a multiple of 16 bytes
         _lib.call("gsplat_rasterize_forward_clearing", tb[0], tb[1], H, W, P(gids), P(bins),
-                  P(xys), P(conics), P(colors), P(opac), P(bg), P(img), P(fT), P(fi), I,
-                  chunk, P(ckpt), ckpt.numel(), P(rec), 24, None, st)
+                  P(xys), P(conics), P(colors), P(opac), P(bg), P(img), P(fT), P(fi),
+                  P(rec), 24, None, st)
 
 
 @pytest.mark.parametrize("case", [CASES[0], CASES[2], CASES[3], CASES[6]])

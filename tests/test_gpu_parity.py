@@ -392,8 +392,8 @@ def _check_raster_backward(gpu, case):
 @pytest.mark.parametrize("chunk", [64, 128, 256])
 @pytest.mark.parametrize("case", CASES[1:3])
 def test_raster_backward_list_split(gpu, case, chunk, bwd):
-    """The list-split backward (checkpointed forward + per-chunk backward, forced chunk
-    size; 8x8 block waves or, bwd 2, 16x8 strips): identical forward, gradients within the
+    """The list-split backward (parts of a forced chunk size, each re-walking the positions
+    behind it; 8x8 block waves or, bwd 2, 16x8 strips): identical forward, gradients within the
     same bar vs the oracle."""
     _lib.call("gsplat_debug_set_chunk", chunk)
     _lib.call("gsplat_debug_set_raster_variant", 1, bwd, 0)

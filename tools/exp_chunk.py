@@ -1,5 +1,6 @@
 """List-split backward: raster forward/backward time vs the chunk size, through the autograd
-wrappers (forward with checkpoints + chunked backward), on one config (CFG env)."""
+wrapper (clearing forward + record backward with its split plan), on one config (CFG env;
+CHUNKS env: comma-separated chunk sizes, -1 = off, 0 = auto)."""
 import os
 import sys
 
@@ -36,11 +37,12 @@ def step():
 
 auto = None
 res = {}
-for ch in [-1, 0, 256, 512, 1024, 2048]:
+chunks = [int(c) for c in os.environ.get("CHUNKS", "-1,0,64,128,256,512,1024").split(",")]
+for ch in chunks:
     _lib.call("gsplat_debug_set_chunk", ch)
     for _ in range(3):
         g = step()
-    if ch == -1:
+    if ch == chunks[0]:
         ref = g.clone()
     else:
         err = (g - ref).abs().max().item() / ref.abs().max().item()
@@ -51,8 +53,9 @@ for ch in [-1, 0, 256, 512, 1024, 2048]:
             for _ in range(5):
                 step()
             s = tm.summary()
-        fw.append(s["gsplat_rasterize_forward"][1])
-        bw.append(s["gsplat_rasterize_backward"][1])
+        fw.append(sum(v[1] for k, v in s.items() if "rasterize_forward" in k))
+        bw.append(sum(v[1] for k, v in s.items() if "rasterize_backward" in k or
+                      "grad_records_split" in k))
     res[ch] = (np.median(fw), np.median(bw))
 _lib.call("gsplat_debug_set_chunk", 0)
 print(f"{cfg}: N={N} image {W}x{H} auto chunk ="

@@ -1,6 +1,7 @@
 """Per-wave timeline of the raster backward (gsplat_debug_wave_log): how long waves live, when
-they start, how busy each SIMD is and how long the tail is.  FLAGS selects the variants
-(gsplat_debug_set_raster_variant bwd_flags), CFG the bench config."""
+they start, how busy each SIMD is and how long the tail is.  BWD selects the backward
+geometries (gsplat_debug_set_raster_variant bwd_pxl: 1 blocks, 2 strips), CFG the bench
+config."""
 import os, sys
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 import numpy as np
@@ -46,11 +47,11 @@ def bwd():
               *[P(x) for x in g], P(ws), wsz, st)
 
 log = torch.zeros(4 * T * 5, dtype=torch.int64, device=dev)
-runs = [("bwd", int(x)) for x in os.environ.get("FLAGS", "0,4096").split(",")]
+runs = [("bwd", int(x)) for x in os.environ.get("BWD", "2,1").split(",")]
 if os.environ.get("FWD", "1") == "1":
     runs.append(("fwd", 0))
 for kind, f in runs:
-    _lib.call("gsplat_debug_set_raster_variant", 1, 2, f)
+    _lib.call("gsplat_debug_set_raster_variant", 1, f if kind == "bwd" else 0, 0)
     fn = bwd if kind == "bwd" else fwd
     for _ in range(3):
         fn()
@@ -72,7 +73,7 @@ for kind, f in runs:
     busy = np.bincount(inv, weights=d)
     last = np.zeros(len(us)); np.maximum.at(last, inv, e)
     nw = np.bincount(inv)
-    print(f"== {cfg} {kind} flags={f}: {len(L)} waves on {len(us)} SIMDs; span {span:.1f} us")
+    print(f"== {cfg} {kind} geometry={f}: {len(L)} waves on {len(us)} SIMDs; span {span:.1f} us")
     print(f"  wave duration us: mean {d.mean():.1f} p50 {np.median(d):.1f} p90 "
           f"{np.percentile(d, 90):.1f} max {d.max():.1f}")
     print(f"  wave start us: p50 {np.median(s):.1f} p90 {np.percentile(s, 90):.1f} "
@@ -84,4 +85,53 @@ for kind, f in runs:
     bins_t = np.linspace(0, span, 11)
     act = [int(((s <= t) & (e > t)).sum()) for t in bins_t[:-1] + span / 20]
     print(f"  resident waves at 5%,15%..95% of span: {act}")
-_lib.call("gsplat_debug_set_raster_variant", 1, 2, 0)
+_lib.call("gsplat_debug_set_raster_variant", 1, 0, 0)
+
+
+def simulate(dur, order, slots):
+    """Greedy list schedule: waves in `order` each take the earliest free slot of `slots`
+    (first-order model of the dispatcher; durations held at their measured values)."""
+    import heapq
+    free = [0.0] * slots
+    heapq.heapify(free)
+    end = 0.0
+    for w in order:
+        t = heapq.heappop(free)
+        e = t + dur[w]
+        end = max(end, e)
+        heapq.heappush(free, e)
+    return end
+
+
+# Schedule estimates from the last measured kernel of each kind (SIM=1): dispatch order as
+# measured (model check), waves longest-first, and 8-tile chunks (the XCD chunk of the block
+# order) longest-chunk-first with the chunk's tiles kept together.
+if os.environ.get("SIM", "1") == "1":
+    for kind, f in runs:
+        _lib.call("gsplat_debug_set_raster_variant", 1, f if kind == "bwd" else 0, 0)
+        fn = bwd if kind == "bwd" else fwd
+        fn()
+        log.zero_()
+        _lib.call("gsplat_debug_wave_log", P(log))
+        fn()
+        torch.cuda.synchronize()
+        _lib.call("gsplat_debug_wave_log", None)
+        L = log.view(-1, 5).cpu().numpy()
+        L = L[L[:, 1] > 0]
+        t0 = L[:, 0].min()
+        s, e = (L[:, 0] - t0) / 100.0, (L[:, 1] - t0) / 100.0
+        dur = e - s
+        slot = L[:, 4]
+        resident = int(max(((s <= t) & (e > t)).sum() for t in np.linspace(0, e.max(), 50)))
+        disp = np.argsort(s, kind="stable")
+        lpt = np.argsort(-dur, kind="stable")
+        chunk = slot // 8
+        csum = np.bincount(chunk, weights=dur)
+        corder = np.argsort(-csum[chunk], kind="stable")
+        corder = corder[np.lexsort((slot[corder], -csum[chunk[corder]]))]
+        print(f"== {cfg} {kind} geometry={f}: measured span {e.max():.1f} us, {resident} slots; "
+              f"simulated dispatch order {simulate(dur, disp, resident):.1f}, waves longest-first "
+              f"{simulate(dur, lpt, resident):.1f}, 8-tile chunks longest-first "
+              f"{simulate(dur, corder, resident):.1f}; ideal sum/slots "
+              f"{dur.sum() / resident:.1f}, longest wave {dur.max():.1f}")
+    _lib.call("gsplat_debug_set_raster_variant", 1, 0, 0)
