@@ -1,6 +1,7 @@
 """List-split backward: raster forward/backward time vs the chunk size, through the autograd
 wrapper (clearing forward + record backward with its split plan), on one config (CFG env;
-CHUNKS env: comma-separated chunk sizes, -1 = off, 0 = auto)."""
+CHUNKS env: comma-separated chunk sizes, -1 = off, 0 = auto; FLAGS env: comma-separated
+gsplat_debug_set_raster_variant flag words, each swept over CHUNKS)."""
 import os
 import sys
 
@@ -38,11 +39,13 @@ def step():
 auto = None
 res = {}
 chunks = [int(c) for c in os.environ.get("CHUNKS", "-1,0,64,128,256,512,1024").split(",")]
-for ch in chunks:
+flags = [int(f, 0) for f in os.environ.get("FLAGS", "0").split(",")]
+for fl, ch in [(f, c) for f in flags for c in chunks]:
+    _lib.call("gsplat_debug_set_raster_variant", 1, 0, fl)
     _lib.call("gsplat_debug_set_chunk", ch)
     for _ in range(3):
         g = step()
-    if ch == chunks[0]:
+    if (fl, ch) == (flags[0], chunks[0]):
         ref = g.clone()
     else:
         err = (g - ref).abs().max().item() / ref.abs().max().item()
@@ -56,11 +59,12 @@ for ch in chunks:
         fw.append(sum(v[1] for k, v in s.items() if "rasterize_forward" in k))
         bw.append(sum(v[1] for k, v in s.items() if "rasterize_backward" in k or
                       "grad_records_split" in k))
-    res[ch] = (np.median(fw), np.median(bw))
+    res[fl, ch] = (np.median(fw), np.median(bw))
 _lib.call("gsplat_debug_set_chunk", 0)
+_lib.call("gsplat_debug_set_raster_variant", 1, 0, 0)
 print(f"{cfg}: N={N} image {W}x{H} auto chunk ="
       f" {_lib.query('gsplat_rasterize_chunk_size', cam.tile_bounds[0], cam.tile_bounds[1], 10**6)}"
       " (per 1M intersections)")
-for ch, (f, b) in res.items():
+for (fl, ch), (f, b) in res.items():
     lbl = {-1: "off", 0: "auto"}.get(ch, str(ch))
-    print(f"  chunk {lbl:>5s}: fwd {f:.3f} ms  bwd {b:.3f} ms  sum {f + b:.3f}")
+    print(f"  flags {fl:#x} chunk {lbl:>5s}: fwd {f:.3f} ms  bwd {b:.3f} ms  sum {f + b:.3f}")
