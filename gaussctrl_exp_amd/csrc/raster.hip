@@ -146,6 +146,15 @@ constexpr int FWD_PXL = 1;  // forward: 8x8 blocks, two Gaussians per iteration 
 constexpr int BWD_PXL = 0;  // 0: by frame size (bwd_geometry)
 // Tuning / ablation knobs (gsplat_debug_set_raster_variant); defaults are the shipped ones.
 int g_fwd_pxl = FWD_PXL, g_bwd_pxl = BWD_PXL, g_bwd_flags = 0;
+// forward staging pipelined one batch ahead (the PF instantiation, see RawG): -1 by frame
+// size (below 3,584 tiles, where the longest waves bound the launch), 0 off, 1 on
+// (gsplat_debug_set_raster_variant flags bits 28-29: 0 auto, 1 off, 2 on).  (The same pipeline
+// in the 8x8 backward measured no gain: c3 0.132 -> 0.134 ms, c2 0.123 -> 0.125 ms; its
+// EAGER staging already overlaps the data loads, and its blend per batch is longer.)
+int g_pf_mode = -1;
+static bool pipelined_staging(int tbx, int tby) {
+  return g_pf_mode < 0 ? (long long)tbx * tby < 3584 : g_pf_mode > 0;
+}
 
 struct __attribute__((aligned(16))) GStage {
   float x, y, ha, b;  // mean, 0.5*conic.a, conic.b
@@ -319,6 +328,61 @@ __device__ __forceinline__ bool stage_gaussian(int idx, const int *__restrict__ 
   return keep;
 }
 
+// Software-pipelined staging (the PF forward, frames below 3,584 tiles): a batch's data is
+// loaded (RawG, all of it, whatever the cull decides) one batch ahead and its ids two batches
+// ahead, so a wave walking a long list overlaps both dependent memory round trips of the next
+// batch with the blending of this one instead of waiting for them every 64 positions.  Worth it
+// where the longest waves bound the launch (small frames: c3 bear forward 0.124 -> 0.094 ms);
+// on full frames the 12 extra VGPRs (one occupancy level) and the loads of culled Gaussians'
+// colours cost more (headline forward 0.125 -> 0.144 ms).
+struct RawG {
+  float2 xy;
+  float a, b, c, o, r, g, bl;
+};
+__device__ __forceinline__ RawG raw_load(int g, const float2 *__restrict__ xys,
+                                         const float *__restrict__ conics,
+                                         const float *__restrict__ colors,
+                                         const float *__restrict__ opacity) {
+  RawG q;
+  q.xy = xys[g];
+  q.a = conics[3 * g];
+  q.b = conics[3 * g + 1];
+  q.c = conics[3 * g + 2];
+  q.o = opacity[g];
+  q.r = colors[3 * g];
+  q.g = colors[3 * g + 1];
+  q.bl = colors[3 * g + 2];
+  return q;
+}
+// stage_gaussian's cull and fill on prefetched data (BF: the branch-free cull of the backward)
+template <bool BF>
+__device__ __forceinline__ bool stage_raw(const RawG &q, bool live, int idx, int g, float rx0,
+                                          float rx1, float ry0, float ry1, GStage &s) {
+  const bool keep =
+      live && (BF ? touches_rect_bf(q.xy.x, q.xy.y, q.a, q.b, q.c, q.o, rx0, rx1, ry0, ry1)
+                  : touches_rect(q.xy.x, q.xy.y, q.a, q.b, q.c, q.o, rx0, rx1, ry0, ry1));
+  if (keep) {
+    s.x = q.xy.x;
+    s.y = q.xy.y;
+    s.ha = 0.5f * q.a;
+    s.b = q.b;
+    s.hc = 0.5f * q.c;
+    s.o = q.o;
+    s.r = q.r;
+    s.g = q.g;
+    s.bl = q.bl;
+    s.idx = idx;
+    s.id = g;
+  }
+  return keep;
+}
+// The pipeline state: ids of batch k+1 (loaded) and k+2 (in flight), data of batch k+1 (in
+// flight).
+struct StagePipe {
+  int g_next, g_after;
+  RawG r_next;
+};
+
 // A workgroup of 4 waves covers 4 / (waves per tile) tiles.  A wave owns a COLS-wide
 // rectangle of its tile: lanes map to (column lane % COLS, row lane / COLS), and each lane
 // holds PXL pixels spaced 64 / COLS rows apart.  COLS = 16 gives full-width strips, COLS = 8
@@ -451,7 +515,7 @@ constexpr int tiles_per_block() {
 // depth, accumulated with the same weight as the colour channels into out_depth -- exactly
 // channel 0 of a second render with colours = depth and a zero background (gc_model.py:
 // 225-238), without the second binning and traversal.
-template <int PXL, int COLS, bool DEPTH = false, bool CNT = false>
+template <int PXL, int COLS, bool DEPTH = false, bool CNT = false, bool PF = false>
 __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
     int tbx, int tby, int H, int W, const int *__restrict__ gids, const int2 *__restrict__ bins,
     const float2 *__restrict__ xys, const float *__restrict__ conics,
@@ -498,6 +562,12 @@ __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
   const int2 range = bins[tile];
   GStage *stage = lds[wave];
   unsigned c_slots = 0, c_live = 0, c_valid = 0;  // (CNT only)
+  StagePipe pipe{};  // (PF: see RawG)
+  if (PF && range.x < range.y) {
+    pipe.g_next = gids[min(range.x + lane, range.y - 1)];
+    pipe.r_next = raw_load(pipe.g_next, xys, conics, colors, opacity);
+    pipe.g_after = gids[min(range.x + 64 + lane, range.y - 1)];
+  }
   for (int b = range.x; b < range.y; b += 64) {
     bool all_done = true;
 #pragma unroll
@@ -505,9 +575,19 @@ __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
     if (__all(all_done)) break;
     const int idx = b + lane;
     GStage s;
-    const bool keep = idx < range.y &&
-                      stage_gaussian(idx, gids, xys, conics, colors, opacity, rx0, rx1, ry0,
-                                     ry1, s);
+    bool keep;
+    if constexpr (PF) {
+      const int g = pipe.g_next;
+      const RawG q = pipe.r_next;
+      // the next batch's data and the one after's ids (clamped into the list: unused past it)
+      pipe.g_next = pipe.g_after;
+      pipe.r_next = raw_load(pipe.g_next, xys, conics, colors, opacity);
+      pipe.g_after = gids[min(b + 128 + lane, range.y - 1)];
+      keep = stage_raw<false>(q, idx < range.y, idx, g, rx0, rx1, ry0, ry1, s);
+    } else {
+      keep = idx < range.y &&
+             stage_gaussian(idx, gids, xys, conics, colors, opacity, rx0, rx1, ry0, ry1, s);
+    }
     if (DEPTH && keep) s.d = depths[s.id];
     const unsigned long long kmask = __ballot(keep);
     if (keep) stage[lanes_below(kmask)] = s;
@@ -896,12 +976,16 @@ __global__ __launch_bounds__(256) void raster_bwd8_kernel(
   const int field = slot >= 9 ? slot - 9 : slot;
   const float amax = __builtin_canonicalizef(alpha_max);
   GStage *stage = lds[wave];
+  // this batch's staged Gaussian (b: the batch top, bottom: the lowest position staged)
+  auto stage_next = [&](int b, int bottom, GStage &s) {
+    const int idx = b - (int)(threadIdx.x & 63);
+    return idx >= bottom && stage_gaussian<true>(idx, gids, xys, conics, colors, opacity, R.rx0,
+                                                 R.rx1, R.ry0, R.ry1, s);
+  };
   if (SPLIT) {  // the positions behind this part: T and the colour behind only
     for (int b = min(maxbin, range.y - 1); b >= hi; b -= 64) {
-      const int idx = b - (threadIdx.x & 63);
       GStage s;
-      const bool keep = idx >= hi && stage_gaussian<true>(idx, gids, xys, conics, colors,
-                                                          opacity, R.rx0, R.rx1, R.ry0, R.ry1, s);
+      const bool keep = stage_next(b, hi, s);
       const unsigned long long kmask = __ballot(keep);
       if (keep) stage[lanes_below(kmask)] = s;
       const int n = __popcll(kmask);
@@ -923,10 +1007,8 @@ __global__ __launch_bounds__(256) void raster_bwd8_kernel(
   const int last = min(maxbin, hi - 1);
   unsigned c_slots = 0, c_live = 0, c_valid = 0;  // (CNT only)
   for (int b = last; b >= lo; b -= 64) {
-    const int idx = b - (threadIdx.x & 63);
     GStage s;
-    const bool keep = idx >= lo && stage_gaussian<true>(idx, gids, xys, conics, colors, opacity,
-                                                        R.rx0, R.rx1, R.ry0, R.ry1, s);
+    const bool keep = stage_next(b, lo, s);
     const unsigned long long kmask = __ballot(keep);
     if (keep) stage[lanes_below(kmask)] = s;
     const int n = __popcll(kmask);
@@ -1352,7 +1434,8 @@ static SplitWs carve_split_ws(void *base, long long T, long long I, int chunk) {
   return w;
 }
 static bool default_variants() {
-  return g_fwd_pxl == FWD_PXL && g_bwd_pxl == BWD_PXL && g_bwd_flags == 0;
+  // (the staging pipeline bits change the schedule only)
+  return g_fwd_pxl == FWD_PXL && g_bwd_pxl == BWD_PXL && (g_bwd_flags & ~(3 << 28)) == 0;
 }
 
 extern "C" int gsplat_rasterize_chunk_size(int tile_bounds_x, int tile_bounds_y,
@@ -1398,12 +1481,17 @@ static void launch_fwd(hipStream_t st, int tbx, int tby, int H, int W, const int
                        float *out_img, float *final_Ts, int32_t *final_idx, const float *depths,
                        float *out_depth, float4 *zero, long long zn, const int32_t *zero_radii) {
   const unsigned grid = cdiv((long long)tbx * tby, (tiles_per_block<1, 8>()));
-#define FWDK(CNT)                                                                          \
-  hipLaunchKernelGGL((raster_fwd3u_kernel<1, 8, DEPTH, CNT>), dim3(grid), dim3(256), 0, st, tbx, \
-                     tby, H, W, gids, (const int2 *)bins, (const float2 *)xys, conics, colors,  \
-                     opacity, background, out_img, final_Ts, final_idx, depths, out_depth, zero, \
-                     zn, zero_radii)
-  if (!DEPTH && g_pair_count_on) FWDK(true); else FWDK(false);
+#define FWDK(CNT, PF)                                                                      \
+  hipLaunchKernelGGL((raster_fwd3u_kernel<1, 8, DEPTH, CNT, PF>), dim3(grid), dim3(256), 0, st, \
+                     tbx, tby, H, W, gids, (const int2 *)bins, (const float2 *)xys, conics,     \
+                     colors, opacity, background, out_img, final_Ts, final_idx, depths,         \
+                     out_depth, zero, zn, zero_radii)
+  const bool pf = pipelined_staging(tbx, tby);
+  if (!DEPTH && g_pair_count_on) {
+    if (pf) FWDK(true, true); else FWDK(true, false);
+  } else {
+    if (pf) FWDK(false, true); else FWDK(false, false);
+  }
 #undef FWDK
 }
 
@@ -1459,14 +1547,18 @@ extern "C" int gsplat_rasterize_forward_rgbd(int tile_bounds_x, int tile_bounds_
 // Measurement knob: bwd_pxl picks the backward geometry (BWD_PXL above); bits 20-27 of flags
 // the XCD chunk of the blend kernels' block order (0 the default K = 8, 255 dispatch order).
 extern "C" int gsplat_debug_set_raster_variant(int fwd_pxl, int bwd_pxl, int bwd_flags) {
-  if (fwd_pxl != 1 || bwd_pxl < 0 || bwd_pxl > 2 || (bwd_flags & ~(0xff << 20))) {
+  if (fwd_pxl != 1 || bwd_pxl < 0 || bwd_pxl > 2 || (bwd_flags & ~(0x3ff << 20)) ||
+      ((bwd_flags >> 28) & 3) == 3) {
     set_error("debug_set_raster_variant: fwd_pxl must be 1, bwd_pxl 0 (by frame size), 1 (8x8 "
-              "blocks) or 2 (16x8 strips), flags only the XCD chunk (bits 20-27)");
+              "blocks) or 2 (16x8 strips), flags only the XCD chunk (bits 20-27) and the "
+              "staging pipeline (bits 28-29: 0 auto, 1 off, 2 on)");
     return 1;
   }
   g_fwd_pxl = fwd_pxl;
   g_bwd_pxl = bwd_pxl;
   g_bwd_flags = bwd_flags;
+  const int pfm = (bwd_flags >> 28) & 3;
+  g_pf_mode = pfm == 0 ? -1 : pfm == 1 ? 0 : 1;
   const int chunk = (bwd_flags >> 20) & 0xff;
   const int remap = chunk == 0xff ? 0 : chunk ? chunk : XCD_CHUNK;
   if (hipMemcpyToSymbol(HIP_SYMBOL(g_xcd_remap), &remap, sizeof(int)) != hipSuccess) {
@@ -1547,6 +1639,7 @@ static void launch_bwd(hipStream_t st, int tbx, int tby, int H, int W, int n,
       if (det) BWD8(false, true, false); else if (cnt) BWD8(false, false, true);
       else BWD8(false, false, false);
     }
+
 #undef BWD8
   } else {
     const unsigned grid = cdiv(slots, (tiles_per_block<2, 16>()));

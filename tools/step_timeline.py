@@ -40,3 +40,15 @@ for s in range(min(nsteps, len(cuts) - 1)):
         print(f"    gap {g / 1e3:7.1f} us  after {p}  before {n}")
     for g, p, n in gaps:
         gap_tot[(p, n)] = gap_tot.get((p, n), 0) + g
+if gap_tot:
+    print("largest gaps summed over the steps:")
+    for (p, n), g in sorted(gap_tot.items(), key=lambda x: -x[1])[:8]:
+        print(f"    {g / 1e3:8.1f} us  {p} -> {n}")
+# one step's dispatch sequence (offset from the step start, duration), the last printed step
+if len(cuts) > 1:
+    s = min(nsteps, len(cuts) - 1) - 1
+    a, b = cuts[s], cuts[s + 1]
+    t0 = rows[a][1]
+    print(f"step {s} sequence:")
+    for n, st, e in rows[a:b]:
+        print(f"    +{(st - t0) / 1e3:7.1f} us  {(e - st) / 1e3:7.1f} us  {short(n)}")
