@@ -377,10 +377,12 @@ int gsplat_grad_records_split(int num_points, const void *records, size_t record
 /* Measurement hook (not part of the gsplat surface): fwd_pxl must be 1 (the forward's 8x8
  * blocks); bwd_pxl selects the C = 3 backward's geometry: 0 = by frame size (shipped: blocks
  * below 3,584 tiles, strips above), 1 = 8x8 blocks, one pixel per lane, two Gaussians per
- * iteration, 2 = 16x8 strips, two pixels per lane; bwd_flags bits 20-27 = K: the block -> tile order of the blend
- * kernels, chunks of K block slots dealt round-robin over the 8 XCDs (0: the shipped K = 8, 255:
- * plain dispatch order).  Both geometries meet the same parity bar.  Process-wide; (1, 0, 0) is
- * the shipped configuration. */
+ * iteration, 2 = 16x8 strips, two pixels per lane; bwd_flags bits 20-27 = K: the block -> tile
+ * order of the blend kernels, chunks of K block slots dealt round-robin over the 8 XCDs (0: the
+ * shipped K = 8, 255: plain dispatch order); bits 28-29: the forward's staging pipeline (0: by
+ * frame size, shipped -- on below 3,584 tiles; 1 off; 2 on).  Every variant meets the same
+ * parity bar (none changes the arithmetic).  Process-wide; (1, 0, 0) is the shipped
+ * configuration. */
 int gsplat_debug_set_raster_variant(int fwd_pxl, int bwd_pxl, int bwd_flags);
 /* 1 while the shipped raster variants are selected (the record-based entries need them). */
 int gsplat_debug_raster_variant_is_default(void);
