@@ -68,15 +68,8 @@ SIGNATURES = {
     "gsplat_debug_set_chunk": (_I, [_I]),
     "gsplat_debug_set_raster_variant": (_I, [_I, _I, _I]),
     "gsplat_debug_raster_variant_is_default": (_I, []),
-    "gsplat_debug_sort_timing": (_I, [_P, _I]),
-    "gsplat_debug_sort_scheme": (_I, [_I]),
-    "gsplat_debug_depth_sort_wide": (_I, [_I]),
-    "gsplat_debug_compact_depth_sort": (_I, [_I]),
     "gsplat_debug_depth_key_range": (_I, [_I]),
-    "gsplat_debug_tile_sort_counting": (_I, [_I]),
     "gsplat_debug_emit_pass0": (_I, [_I]),
-    "gsplat_debug_bins_from_sort": (_I, [_I]),
-    "gsplat_debug_sort_items": (_I, [_I]),
     "gsplat_debug_wave_log": (_I, [_P]),
     "gsplat_debug_pair_count": (_I, [_P]),
     "gsplat_l1_ssim_num_blocks": (_I, [_I, _I]),
@@ -100,7 +93,7 @@ SIGNATURES = {
                                                                        _P, _SZ, _P]),
 }
 
-ABI_VERSION = 9  # include/gsplat_mi355x.h GSPLAT_MI355X_ABI_VERSION
+ABI_VERSION = 10  # include/gsplat_mi355x.h GSPLAT_MI355X_ABI_VERSION
 
 _lib = None
 _DETERMINISTIC = os.environ.get("GSPLAT_MI355X_DETERMINISTIC", "0") not in ("", "0")

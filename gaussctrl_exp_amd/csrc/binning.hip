@@ -34,16 +34,7 @@ constexpr int SC_ITEMS = 16;
 constexpr int SC_TILE = TPB * SC_ITEMS;  // elements per scan workgroup
 // keys per thread of a sort pass (workgroup tile = TPB * items): small sorts use short tiles
 // so that more, shorter workgroups run at once (a pass is a chain of latencies per workgroup)
-int g_items_override = 0;  // experiment hook (gsplat_debug_sort_items)
-int os_items_for(long long n) {
-  if (g_items_override) return g_items_override;
-  return n >= (4LL << 20) ? 16 : 4;
-}
-constexpr int OS_MAX_PASSES = 8;
-constexpr uint32_t ST_AGG = 1u << 30;    // status word: aggregate of this tile only
-constexpr uint32_t ST_PRE = 2u << 30;    // status word: inclusive prefix up to this tile
-constexpr uint32_t ST_VAL = (1u << 30) - 1u;
-constexpr uint32_t SPIN_LIMIT = 1u << 24;
+int os_items_for(long long n) { return n >= (4LL << 20) ? 16 : 4; }
 
 // ------------------------------------------------------------------ block scan helpers
 
@@ -179,16 +170,14 @@ SortPlan sort_plan(long long n, int begin_bit, int end_bit) {
   return p;
 }
 
-// Workspace: [hist: MAX_PASSES x 256][tickets: MAX_PASSES][error][pad] | status[passes][nblocks][radix]
-constexpr size_t OS_HEAD_WORDS = OS_MAX_PASSES * 256 + OS_MAX_PASSES + 8;
+// Workspace: [head: 16 words (1: kept-key count, 2-3: key range)] | tile digit counts
+// [radix][nblocks] | row totals | per-tile key ranges
+constexpr size_t OS_HEAD_WORDS = 16;
 
 // [head words][one-sweep status: passes x nblocks x radix | reduce-then-scan tile counts
 // nblocks x radix + scan scratch]
 size_t radix_main_bytes(const SortPlan &p) {
-  const size_t onesweep = (size_t)p.passes * p.nblocks * p.radix * sizeof(uint32_t);
-  const size_t rts = (size_t)p.nblocks * p.radix * sizeof(uint32_t) +
-                     scan_ws_bytes((long long)p.nblocks * p.radix);
-  return OS_HEAD_WORDS * sizeof(uint32_t) + (onesweep > rts ? onesweep : rts);
+  return (OS_HEAD_WORDS + (size_t)p.nblocks * p.radix + 256) * sizeof(uint32_t);
 }
 
 // [head][per-pass state][per-tile key range: nblocks x (and, or)]
@@ -211,40 +200,6 @@ __device__ __forceinline__ bool digit_constant(const uint32_t *fin, int shift, i
   return fin && ((((fin[0] ^ fin[1]) >> shift) & ((1u << width) - 1u)) == 0u);
 }
 
-template <typename K>
-__global__ __launch_bounds__(TPB) void os_hist_kernel(const K *__restrict__ keys, long long n,
-                                                      int begin_bit, int width, int passes,
-                                                      uint32_t *__restrict__ hist) {
-  __shared__ uint32_t lh[OS_MAX_PASSES * 256];
-  const int R = 1 << width;
-  for (int i = threadIdx.x; i < passes * 256; i += TPB) lh[i] = 0;
-  __syncthreads();
-  const long long stride = (long long)gridDim.x * TPB;
-  long long i = (long long)blockIdx.x * TPB + threadIdx.x;
-  for (; i + 3 * stride < n; i += 4 * stride) {  // four independent loads in flight
-    K k[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) k[u] = keys[i + u * stride];
-    for (int p = 0; p < passes; ++p) {
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const uint32_t d = (uint32_t)(k[u] >> (begin_bit + p * width)) & (uint32_t)(R - 1);
-        atomicAdd(&lh[p * 256 + d], 1u);
-      }
-    }
-  }
-  for (; i < n; i += stride) {
-    const K k = keys[i];
-    for (int p = 0; p < passes; ++p) {
-      const uint32_t d = (uint32_t)(k >> (begin_bit + p * width)) & (uint32_t)(R - 1);
-      atomicAdd(&lh[p * 256 + d], 1u);
-    }
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < passes * 256; i += TPB)
-    if (lh[i]) atomicAdd(&hist[i], lh[i]);
-}
-
 // Reduce-then-scan pass, part 1: the digit histogram of every tile of TPB*ITEMS keys, stored
 // digit-major (counts[d * nblocks + tile]) so one exclusive scan yields every tile's global
 // offset for every digit.  drop: all-ones keys (culled Gaussians' depth keys) are not counted
@@ -254,14 +209,12 @@ template <typename K, int ITEMS>
 __global__ __launch_bounds__(TPB) void rts_count_kernel(const K *__restrict__ keys, long long n,
                                                         int shift, int width, long long nblocks,
                                                         uint32_t *__restrict__ counts,
-                                                        uint32_t *__restrict__ err,
                                                         bool drop = false,
                                                         const uint32_t *__restrict__ n_dev = nullptr,
                                                         KeyRange kr = {}, int pass = 0) {
   __shared__ uint32_t h[256];
   __shared__ uint32_t kand, kor;
   const int tid = threadIdx.x;
-  if (err && blockIdx.x == 0 && tid == 0) *err = 0;  // the look-back error word stays clear
   if (pass > 0 && digit_constant(kr.fin, shift, width)) return;  // identity pass
   if (n_dev) n = min(n, (long long)*n_dev);
   const int R = 1 << width;
@@ -347,26 +300,27 @@ struct OsSmem {
   uint32_t gofs[256];      // global output offset of each digit, minus loc_off
   uint32_t hscan[256];     // exclusive scan of this pass's global histogram
   uint32_t scan_tmp[4];
-  uint32_t ticket;
   uint32_t tile_n;         // keys this tile writes (all valid ones; fewer when dropping)
 };
 
+// Reduce-then-scan pass, part 3: each workgroup ranks its tile of TPB * ITEMS keys stably in
+// LDS, takes its digits' global offsets from the row-scanned tile counts plus the digit bases
+// (the exclusive scan of the row totals), and writes the tile out in digit order, so each
+// digit's run is written by consecutive lanes.
 template <typename K, int WIDTH, int ITEMS>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) void os_pass_kernel(
     const K *__restrict__ kin, const uint32_t *__restrict__ vin, K *__restrict__ kout,
     uint32_t *__restrict__ vout, long long n, int shift, int width,
-    const uint32_t *__restrict__ hist, uint32_t *__restrict__ ticket_ctr,
-    uint32_t *__restrict__ status, uint32_t *__restrict__ err,
-    unsigned long long *__restrict__ tbuf, bool use_ticket, const uint32_t *__restrict__ offs,
-    long long nblocks, int32_t *__restrict__ bins = nullptr, bool drop = false,
+    const uint32_t *__restrict__ rowtot, const uint32_t *__restrict__ offs, long long nblocks,
+    int32_t *__restrict__ bins = nullptr, bool drop = false,
     const uint32_t *__restrict__ n_dev = nullptr, uint32_t *__restrict__ n_out = nullptr,
     const uint32_t *__restrict__ kfin = nullptr) {
-  // compacting sort (reduce-then-scan only): with drop, all-ones keys are left out (pass 0 of
-  // the depth sort: culled Gaussians), and block 0 stores the kept count to n_out; later passes
-  // sort min(n, *n_dev) keys and the workgroups past them exit at once.
+  // compacting sort: with drop, all-ones keys are left out (pass 0 of the depth sort: culled
+  // Gaussians), and block 0 stores the kept count to n_out; later passes sort min(n, *n_dev)
+  // keys and the workgroups past them exit at once.
   if (n_dev) {
     n = min(n, (long long)*n_dev);
-    if (!use_ticket && (long long)blockIdx.x * TPB * ITEMS >= n) return;  // whole workgroup
+    if ((long long)blockIdx.x * TPB * ITEMS >= n) return;  // whole workgroup
   }
   if (digit_constant(kfin, shift, width)) {  // every key has the same digit: a stable copy
     const long long b0 = (long long)blockIdx.x * TPB * ITEMS;
@@ -389,60 +343,38 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     return;
   }
   __shared__ OsSmem<K, ITEMS> sm;
-  // optional phase timestamps (debug hook gsplat_debug_sort_timing): [ticket][6]
-  unsigned long long ts0 = tbuf ? __builtin_amdgcn_s_memrealtime() : 0ull;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int R = 1 << width;
   const uint32_t dmask = (uint32_t)(R - 1);
-  // Tile index = dispatch order: workgroups are dispatched in increasing ID order, so every
-  // tile a workgroup looks back at has already been dispatched and makes progress without it.
-  // (An atomic ticket serialised ~1k workgroups on one counter: 9 us per pass.)
-  // the tile's keys are loaded before the digit-base scan (its barriers would otherwise keep
-  // the loads from going out): tile = blockIdx.x; the debug ticket mode reloads below
+  const uint32_t t = blockIdx.x;
   const unsigned long long lt = (1ull << lane) - 1ull;
   K key[ITEMS];
   uint32_t val[ITEMS], rank[ITEMS];
   bool ok[ITEMS];
-  // (indices clamped into [0, n): no per-element branch, so all 2 x ITEMS loads are in flight
-  // together; the validity mask is applied once they are consumed)
-  auto load_tile = [&](uint32_t tt) {
-    const long long sg = (long long)tt * TPB * ITEMS + (long long)wave * (ITEMS * 64);
+  // the digit total first: vmcnt retires in issue order, so the scan below waits for it alone
+  const uint32_t hval = rowtot[min(tid, R - 1)];
+  {  // (indices clamped into [0, n): no per-element branch, so all 2 x ITEMS loads are in
+     // flight together; the validity mask is applied once they are consumed)
+    const long long sg = (long long)t * TPB * ITEMS + (long long)wave * (ITEMS * 64);
 #pragma unroll
     for (int r = 0; r < ITEMS; ++r) {
       const long long i = min(sg + r * 64 + lane, n - 1);
       key[r] = kin[i];
       val[r] = vin[i];
     }
-  };
-  // the digit total first: vmcnt retires in issue order, so the scan below waits for it alone
-  const uint32_t hval = hist[min(tid, R - 1)];
-  load_tile(blockIdx.x);
-  if (tid == 0) sm.ticket = use_ticket ? atomicAdd(ticket_ctr, 1u) : blockIdx.x;
+  }
 #pragma unroll
   for (int w = 0; w < 4; ++w) sm.wcnt[w][tid] = 0;
-  {  // digit bases: exclusive scan of the pass histogram (one-sweep) or of the digit row
-     // totals (reduce-then-scan)
+  {  // digit bases: exclusive scan of the digit row totals
     uint32_t h = tid < R ? hval : 0u, tot;
     sm.hscan[tid] = block_exclusive_scan<TPB>(h, tot, sm.scan_tmp);  // contains barriers
     if (n_out && blockIdx.x == 0 && tid == 0) *n_out = tot;
   }
-  const uint32_t t = sm.ticket;
-  unsigned long long ts1 = tbuf ? __builtin_amdgcn_s_memrealtime() : 0ull;
-  if (use_ticket) load_tile(t);
   const long long base = (long long)t * TPB * ITEMS;
 #pragma unroll
   for (int r = 0; r < ITEMS; ++r) {
     const bool valid = base + (long long)wave * (ITEMS * 64) + r * 64 + lane < n;
     ok[r] = valid && !(drop && key[r] == (K)~(K)0);
-  }
-  unsigned long long ts2 = 0ull;
-  if (tbuf) {
-    // the loads are consumed by the ranking below; force them complete for the timestamp
-    uint32_t acc = 0;
-#pragma unroll
-    for (int r = 0; r < ITEMS; ++r) acc ^= (uint32_t)key[r] ^ val[r];
-    asm volatile("" ::"v"(acc));
-    ts2 = __builtin_amdgcn_s_memrealtime();
   }
   // Stable rank within the wave: a ballot match finds the lanes sharing this key's digit
   // (peers); the group's lowest lane reserves popc(peers) slots of the wave's LDS counter for
@@ -471,14 +403,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
       rank[r0 + u] = __shfl(old[u], leader, 64) + (uint32_t)__popcll(pr[u] & lt);
     }
   }
-  unsigned long long ts2a = 0ull;
-  if (tbuf) {
-    uint32_t acc = 0;
-#pragma unroll
-    for (int r = 0; r < ITEMS; ++r) acc ^= rank[r];
-    asm volatile("" ::"v"(acc));
-    ts2a = __builtin_amdgcn_s_memrealtime();
-  }
   __syncthreads();
   uint32_t local_count = 0;
   {
@@ -491,19 +415,12 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     }
     local_count = s;  // digit tid's count in this tile (0 for tid >= R)
   }
-  // publish this tile's aggregate as early as possible (tile 0 publishes its prefix)
-  if (!offs && tid < R) {
-    uint32_t word = (t == 0 ? ST_PRE : ST_AGG) | local_count;
-    __hip_atomic_store(&status[(size_t)t * R + tid], word, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-  }
   {
     uint32_t tot;
     sm.loc_off[tid] = block_exclusive_scan<TPB>(local_count, tot, sm.scan_tmp);
     if (tid == 0) sm.tile_n = tot;
   }
   __syncthreads();  // loc_off[d] is read by every thread below
-  unsigned long long ts2b = tbuf ? __builtin_amdgcn_s_memrealtime() : 0ull;
   // stable local sort into LDS
 #pragma unroll
   for (int r = 0; r < ITEMS; ++r) {
@@ -514,61 +431,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
       sm.vals[lp] = val[r];
     }
   }
-  unsigned long long ts3 = tbuf ? __builtin_amdgcn_s_memrealtime() : 0ull;
-  // decoupled look-back for this digit's exclusive prefix over the preceding tiles.  The
-  // status words are agent-scope (they cross XCDs, so every read misses the per-XCD L2): the
-  // walk reads LB_WIN predecessors per round trip and consumes them nearest first until it
-  // meets an inclusive prefix; a not-yet-published word ends the round.
-  if (offs && tid < R) {  // reduce-then-scan: offsets come from the scanned tile counts
-    sm.gofs[tid] = sm.hscan[tid] + offs[(size_t)tid * nblocks + t] - sm.loc_off[tid];
-  } else if (tid < R) {
-    uint32_t excl = 0;
-    if (t > 0) {
-      constexpr int LB_WIN = 16;
-      long long j = (long long)t - 1;
-      uint32_t spins = 0;
-      bool done = false;
-      while (!done) {
-        uint32_t st[LB_WIN];
-#pragma unroll
-        for (int k = 0; k < LB_WIN; ++k)
-          st[k] = j - k >= 0 ? __hip_atomic_load(&status[(size_t)(j - k) * R + tid],
-                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                             : 0u;
-        int used = 0;
-        bool stop = false;
-#pragma unroll
-        for (int k = 0; k < LB_WIN; ++k) {
-          if (stop) continue;
-          const uint32_t sv = st[k];
-          if (j - k < 0 || (sv & ~ST_VAL) == 0) {  // not published yet: next round
-            stop = true;
-            continue;
-          }
-          excl += sv & ST_VAL;
-          used = k + 1;
-          if ((sv & ST_PRE) || j - k == 0) {
-            done = true;
-            stop = true;
-          }
-        }
-        if (done) break;
-        if (used == 0) {
-          if (++spins > SPIN_LIMIT) {  // bounded: report instead of hanging
-            atomicOr(err, 1u);
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-        }
-        j -= used;
-      }
-      __hip_atomic_store(&status[(size_t)t * R + tid], ST_PRE | (excl + local_count),
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    sm.gofs[tid] = sm.hscan[tid] + excl - sm.loc_off[tid];
-  }
+  if (tid < R) sm.gofs[tid] = sm.hscan[tid] + offs[(size_t)tid * nblocks + t] - sm.loc_off[tid];
   __syncthreads();
-  unsigned long long ts4 = tbuf ? __builtin_amdgcn_s_memrealtime() : 0ull;
   const long long cnt = sm.tile_n;
   if (bins) {
     // last pass of the tile sort: the keys (tile ids) are not written; the tile table comes from
@@ -601,31 +465,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
       }
     }
   }
-  if (tbuf && tid == 0) {
-    __builtin_amdgcn_s_waitcnt(0);
-    const unsigned long long ts5 = __builtin_amdgcn_s_memrealtime();
-    unsigned long long *o = tbuf + (size_t)t * 8;
-    o[0] = ts0; o[1] = ts1; o[2] = ts2; o[3] = ts2a; o[4] = ts2b; o[5] = ts3; o[6] = ts4;
-    o[7] = ts5;
-  }
 }
 
-// ---------------------------------------------------------- wide-digit LSD sort (depth keys)
-// ABLATION (gsplat_debug_depth_sort_wide(1); bit-exact, not shipped).  The depth sort of
-// bin_count orders N <= a few million 32-bit keys, four 8-bit passes of three short,
-// latency-bound launches each (~23 us per pass at 1M keys).  Here the 32 key bits take three
-// passes of WD_WIDTH = 11 bits (2,048 digits) with the same reduce-then-scan structure.
-// Measured at the headline (1M keys): count 11.8 us (2,048 strided count stores per tile),
-// row scan ~8 us (2,048 rows), scatter 22.8 us (64 KB of LDS: 2 workgroups per CU) -- ~42 us a
-// pass, 126 us against 91 us for the four 8-bit passes.
-constexpr int WD_WIDTH = 11;
-constexpr int WD_R = 1 << WD_WIDTH;
-constexpr int WD_DPT = WD_R / TPB;  // digits per thread
-constexpr int WD_ITEMS = 8;         // keys per thread (2,048-key tiles)
-constexpr int WD_TILE = TPB * WD_ITEMS;
-bool g_depth_sort_wide = false;  // ablation switch (gsplat_debug_depth_sort_wide)
-bool g_bins_from_sort = true;    // tile table from the last tile-sort pass (gsplat_debug_bins_from_sort)
-bool g_compact_depth_sort = true;  // depth sort drops culled keys (gsplat_debug_compact_depth_sort)
 // constant-digit depth passes only copy (gsplat_debug_depth_key_range: 0 off, 1 from 2^22 keys,
 // 2 always).  The range costs ~8 us (the AND / OR in the first count and a reduction block in
 // its row scan) and a skipped pass saves its ranking, worth it for large sorts only: c5 (4.8M
@@ -633,188 +474,18 @@ bool g_compact_depth_sort = true;  // depth sort drops culled keys (gsplat_debug
 int g_key_range = 1;
 bool use_key_range(long long n) { return g_key_range == 2 || (g_key_range == 1 && n >= (1LL << 22)); }
 
-long long wd_nblocks(long long n) { return n > 0 ? cdiv(n, (long long)WD_TILE) : 0; }
-size_t radix_wide_ws_bytes(long long n) {
-  return ((size_t)wd_nblocks(n) * WD_R + WD_R + 64) * sizeof(uint32_t);
-}
-
-__global__ __launch_bounds__(TPB) void wd_count_kernel(const uint32_t *__restrict__ keys,
-                                                       long long n, int shift, long long nblocks,
-                                                       uint32_t *__restrict__ counts) {
-  __shared__ uint32_t h[WD_R];
-  const int tid = threadIdx.x;
-#pragma unroll
-  for (int j = 0; j < WD_DPT; ++j) h[tid + j * TPB] = 0;
-  __syncthreads();
-  const long long base = (long long)blockIdx.x * WD_TILE;
-  uint32_t k[WD_ITEMS];
-#pragma unroll
-  for (int r = 0; r < WD_ITEMS; ++r) {
-    const long long i = base + r * TPB + tid;
-    k[r] = i < n ? keys[i] : 0u;
-  }
-#pragma unroll
-  for (int r = 0; r < WD_ITEMS; ++r)
-    if (base + r * TPB + tid < n) atomicAdd(&h[(k[r] >> shift) & (WD_R - 1)], 1u);
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < WD_DPT; ++j) {
-    const int d = tid + j * TPB;
-    counts[(size_t)d * nblocks + blockIdx.x] = h[d];
-  }
-}
-
-struct WdSmem {
-  uint32_t keys[WD_TILE];
-  uint32_t vals[WD_TILE];
-  uint32_t wcnt[4][WD_R];  // per-wave digit counters, then per-wave exclusive offsets
-  uint32_t loc_off[WD_R];  // tile-local exclusive offset of each digit
-  uint32_t gofs[WD_R];     // global output offset of each digit, minus loc_off
-  uint32_t scan_tmp[8];
-};
-
-// One stable scatter pass: tile digit ranks by wave64 ballot match (as os_pass_kernel) over
-// WD_WIDTH bits; `offs` [WD_R][nblocks] holds the row-scanned tile counts, `rowtot` [WD_R]
-// the per-digit totals.
-__global__ __launch_bounds__(TPB) void wd_pass_kernel(
-    const uint32_t *__restrict__ kin, const uint32_t *__restrict__ vin, uint32_t *__restrict__ kout,
-    uint32_t *__restrict__ vout, long long n, int shift, const uint32_t *__restrict__ rowtot,
-    const uint32_t *__restrict__ offs, long long nblocks) {
-  __shared__ WdSmem sm;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const uint32_t dmask = WD_R - 1;
-#pragma unroll
-  for (int w = 0; w < 4; ++w)
-#pragma unroll
-    for (int j = 0; j < WD_DPT; ++j) sm.wcnt[w][tid + j * TPB] = 0;
-  const long long base = (long long)blockIdx.x * WD_TILE;
-  const long long seg = base + (long long)wave * (WD_ITEMS * 64);
-  const unsigned long long lt = (1ull << lane) - 1ull;
-  uint32_t key[WD_ITEMS], val[WD_ITEMS], rank[WD_ITEMS];
-#pragma unroll
-  for (int r = 0; r < WD_ITEMS; ++r) {
-    const long long i = seg + r * 64 + lane;
-    const bool valid = i < n;
-    key[r] = valid ? kin[i] : 0u;
-    val[r] = valid ? vin[i] : 0u;
-  }
-  __syncthreads();  // counters cleared
-#pragma unroll
-  for (int r = 0; r < WD_ITEMS; ++r) {
-    const bool valid = seg + r * 64 + lane < n;
-    const uint32_t d = (key[r] >> shift) & dmask;
-    unsigned long long peers = __ballot(valid);
-#pragma unroll
-    for (int b = 0; b < WD_WIDTH; ++b) {
-      const bool bit = (d >> b) & 1u;
-      const unsigned long long m = __ballot(bit);
-      peers &= bit ? m : ~m;
-    }
-    const int leader = valid ? (int)__builtin_ctzll(peers) : lane;
-    uint32_t old = 0;
-    if (valid && leader == lane) old = atomicAdd(&sm.wcnt[wave][d], (uint32_t)__popcll(peers));
-    old = __shfl(old, leader, 64);
-    rank[r] = old + (uint32_t)__popcll(peers & lt);
-  }
-  __syncthreads();
-  // per digit (WD_DPT contiguous digits per thread): wave prefixes, tile-local and global bases
-  uint32_t lc[WD_DPT], tsum = 0, rsum = 0;
-#pragma unroll
-  for (int j = 0; j < WD_DPT; ++j) {
-    const int d = tid * WD_DPT + j;
-    uint32_t s = 0;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      const uint32_t c = sm.wcnt[w][d];
-      sm.wcnt[w][d] = s;
-      s += c;
-    }
-    lc[j] = s;
-    tsum += s;
-    rsum += rowtot[d];
-  }
-  uint32_t tot;
-  uint32_t lrun = block_exclusive_scan<TPB>(tsum, tot, sm.scan_tmp);
-  uint32_t grun = block_exclusive_scan<TPB>(rsum, tot, sm.scan_tmp + 4);
-#pragma unroll
-  for (int j = 0; j < WD_DPT; ++j) {
-    const int d = tid * WD_DPT + j;
-    sm.loc_off[d] = lrun;
-    sm.gofs[d] = grun + offs[(size_t)d * nblocks + blockIdx.x] - lrun;
-    lrun += lc[j];
-    grun += rowtot[d];
-  }
-  __syncthreads();
-#pragma unroll
-  for (int r = 0; r < WD_ITEMS; ++r) {
-    if (seg + r * 64 + lane < n) {
-      const uint32_t d = (key[r] >> shift) & dmask;
-      const uint32_t lp = sm.loc_off[d] + sm.wcnt[wave][d] + rank[r];
-      sm.keys[lp] = key[r];
-      sm.vals[lp] = val[r];
-    }
-  }
-  __syncthreads();
-  const long long cnt = min((long long)WD_TILE, n - base);
-#pragma unroll
-  for (int r = 0; r < WD_ITEMS; ++r) {
-    const int i = r * TPB + tid;
-    if (i < cnt) {
-      const uint32_t k = sm.keys[i];
-      const uint32_t pos = sm.gofs[(k >> shift) & dmask] + (uint32_t)i;
-      kout[pos] = k;
-      vout[pos] = sm.vals[i];
-    }
-  }
-}
-
-// Stable LSD sort of 32-bit (keys, vals) in three 11-bit passes, (ka, va) -> (kb, vb) ->
-// (ka, va) -> (kout, vout).  ws: radix_wide_ws_bytes(n).
-void radix_sort_pairs_wide(uint32_t *ka, uint32_t *va, uint32_t *kb, uint32_t *vb,
-                           uint32_t *kout, uint32_t *vout, long long n, void *ws,
-                           hipStream_t st) {
-  if (n <= 0) return;
-  const long long nb = wd_nblocks(n);
-  uint32_t *counts = (uint32_t *)ws;
-  uint32_t *rowtot = counts + (size_t)nb * WD_R;
-  uint32_t *kin = ka, *vin = va;
-  uint32_t *outs_k[3] = {kb, ka, kout}, *outs_v[3] = {vb, va, vout};
-  for (int q = 0; q < 3; ++q) {
-    const int sh = q * WD_WIDTH;
-    hipLaunchKernelGGL(wd_count_kernel, dim3((unsigned)nb), dim3(TPB), 0, st, kin, n, sh, nb,
-                       counts);
-    hipLaunchKernelGGL(rts_rowscan_kernel, dim3(WD_R), dim3(1024), 0, st, counts, nb, rowtot);
-    hipLaunchKernelGGL(wd_pass_kernel, dim3((unsigned)nb), dim3(TPB), 0, st, kin, vin,
-                       outs_k[q], outs_v[q], n, sh, rowtot, counts, nb);
-    kin = outs_k[q];
-    vin = outs_v[q];
-  }
-}
-
 uint32_t *rts_tile_counts(void *ws) { return (uint32_t *)ws + OS_HEAD_WORDS; }
-uint32_t *sort_err_word(void *ws) { return (uint32_t *)ws + OS_MAX_PASSES * 256 + OS_MAX_PASSES; }
-// the compacting sort's kept-key count (a head pad word)
-uint32_t *sort_kept_word(void *ws) { return sort_err_word(ws) + 1; }
-
-// Debug hook (gsplat_debug_sort_timing): the next `calls` sort passes record per-workgroup
-// phase timestamps into consecutive [nblocks][6] slabs of this buffer.
-unsigned long long *g_sort_timing = nullptr;
-int g_sort_timing_calls = 0;
-bool g_sort_ticket = false;  // debug: atomic tickets instead of dispatch order
-// Pass scheme: reduce-then-scan (tile digit counts -> device scan -> scatter; no cross-
-// workgroup waiting) or one-sweep decoupled look-back.  Per-workgroup phase timing showed the
-// look-back chain dominating one-sweep passes on MI355X (status words cross XCDs).
-bool g_sort_rts = true;
+// the compacting sort's kept-key count (a head word)
+uint32_t *sort_kept_word(void *ws) { return (uint32_t *)ws + 1; }
 
 // Stable LSD sort of (keys, vals) by bits [begin_bit, end_bit).  Ping-pongs between
 // (ka, va) and (kb, vb); the last pass writes (kout, vout).  (ka, va) are clobbered when
 // there are more than two passes.  ws must hold radix_ws_bytes(n, begin_bit, end_bit).
-// first_counts_ready (reduce-then-scan only): the caller's key kernel already wrote pass 0's
-// tile digit counts to rts_tile_counts(ws) and cleared the error word.
+// first_counts_ready: the caller's key kernel already wrote pass 0's tile digit counts to
+// rts_tile_counts(ws).
 // tile_bins (uint32 tile-id keys only): the last pass writes no keys but the tile table --
 // zeroed by the caller, [first, last+1) per tile afterwards (bins_decode_kernel).
-// drop (reduce-then-scan only; first_counts_ready then means counts without the all-ones
-// keys): the first pass leaves out all-ones keys, so the sort orders only the kept keys, whose
+// drop (first_counts_ready then means counts without the all-ones keys): the first pass leaves out all-ones keys, so the sort orders only the kept keys, whose
 // count it stores to sort_kept_word(ws) (the sorted output holds that many; kout may be null).
 __global__ __launch_bounds__(TPB) void bins_decode_kernel(long long T, long long n,
                                                           int32_t *__restrict__ bins) {
@@ -837,28 +508,14 @@ int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t
          "hipMemcpyAsync");
     return 0;
   }
-  uint32_t *hist = (uint32_t *)ws;
-  uint32_t *tickets = hist + OS_MAX_PASSES * 256;
-  uint32_t *err = tickets + OS_MAX_PASSES;
-  uint32_t *status = (uint32_t *)ws + OS_HEAD_WORDS;
-  const bool rts = g_sort_rts;
-  uint32_t *rts_counts = status;
-  uint32_t *rts_partial = status + (size_t)p.nblocks * p.radix;
+  uint32_t *counts = rts_tile_counts(ws);                      // tile digit counts
+  uint32_t *rowtot = counts + (size_t)p.nblocks * p.radix;     // their row totals
   uint32_t *kept = sort_kept_word(ws);
-  drop = drop && rts;
   KeyRange kr;
   if (drop && use_key_range(n)) {
     kr.blk = (uint32_t *)((char *)ws + radix_main_bytes(p));
     kr.fin = sort_kept_word(ws) + 1;
     kr.nblk = p.nblocks;
-  }
-  if (!rts) {
-    note(hipMemsetAsync(ws, 0, radix_ws_bytes(n, begin_bit, end_bit), st), "hipMemsetAsync");
-    // Few, fat histogram blocks: every block flushes passes x 256 counters with global
-    // atomics onto the SAME addresses, which the L2 serialises -- 2048 blocks cost ~35 us.
-    const int hist_blocks = (int)min((long long)cdiv(n, TPB * 64), 256LL);
-    hipLaunchKernelGGL(os_hist_kernel<K>, dim3(hist_blocks), dim3(TPB), 0, st, ka, n, begin_bit,
-                       p.width, p.passes, hist);
   }
   // first_pass = 1: the caller ran pass 0 itself, into (kb, vb)
   K *kin = first_pass ? kb : ka, *kalt = first_pass ? ka : kb;
@@ -867,42 +524,27 @@ int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t
     const bool last = q == p.passes - 1;
     K *ko = last ? kout : kalt;
     uint32_t *vo = last ? vout : valt;
-    unsigned long long *tb = nullptr;
-    if (g_sort_timing && g_sort_timing_calls > 0) {  // debug hook: time this pass
-      tb = g_sort_timing;
-      --g_sort_timing_calls;
-      g_sort_timing += (size_t)p.nblocks * 8;
-    }
-    uint32_t *offs = nullptr;
-    if (rts) {  // reduce-then-scan: tile digit counts -> one exclusive scan -> offsets
-      offs = rts_counts;
-      const int sh = begin_bit + q * p.width;
-      const uint32_t *ndev = drop && q > 0 ? kept : nullptr;
-      // first_counts_ready: the key kernel wrote pass 0's counts and key ranges (kr.blk)
-      if (q == 0 && first_counts_ready) {
-        // the key producer already wrote pass 0's tile digit counts (and cleared err)
-      } else if (p.items == 16)
-        hipLaunchKernelGGL((rts_count_kernel<K, 16>), dim3((unsigned)p.nblocks), dim3(TPB), 0, st,
-                           kin, n, sh, p.width, p.nblocks, offs, q == 0 ? err : nullptr,
-                           drop && q == 0, ndev, kr, q);
-      else if (p.items == 8)
-        hipLaunchKernelGGL((rts_count_kernel<K, 8>), dim3((unsigned)p.nblocks), dim3(TPB), 0, st,
-                           kin, n, sh, p.width, p.nblocks, offs, q == 0 ? err : nullptr,
-                           drop && q == 0, ndev, kr, q);
-      else
-        hipLaunchKernelGGL((rts_count_kernel<K, 4>), dim3((unsigned)p.nblocks), dim3(TPB), 0, st,
-                           kin, n, sh, p.width, p.nblocks, offs, q == 0 ? err : nullptr,
-                           drop && q == 0, ndev, kr, q);
-      hipLaunchKernelGGL(rts_rowscan_kernel,
-                         dim3((unsigned)p.radix + (q == 0 && kr.blk ? 1u : 0u)), dim3(1024), 0,
-                         st, offs, p.nblocks, rts_partial, kr, q, sh, p.width);
-    }
+    // tile digit counts -> row scans -> offsets
+    const int sh = begin_bit + q * p.width;
+    const uint32_t *ndev = drop && q > 0 ? kept : nullptr;
+    // first_counts_ready: the key kernel wrote pass 0's counts and key ranges (kr.blk)
+    if (q == 0 && first_counts_ready) {
+    } else if (p.items == 16)
+      hipLaunchKernelGGL((rts_count_kernel<K, 16>), dim3((unsigned)p.nblocks), dim3(TPB), 0, st,
+                         kin, n, sh, p.width, p.nblocks, counts, drop && q == 0, ndev, kr, q);
+    else if (p.items == 8)
+      hipLaunchKernelGGL((rts_count_kernel<K, 8>), dim3((unsigned)p.nblocks), dim3(TPB), 0, st,
+                         kin, n, sh, p.width, p.nblocks, counts, drop && q == 0, ndev, kr, q);
+    else
+      hipLaunchKernelGGL((rts_count_kernel<K, 4>), dim3((unsigned)p.nblocks), dim3(TPB), 0, st,
+                         kin, n, sh, p.width, p.nblocks, counts, drop && q == 0, ndev, kr, q);
+    hipLaunchKernelGGL(rts_rowscan_kernel,
+                       dim3((unsigned)p.radix + (q == 0 && kr.blk ? 1u : 0u)), dim3(1024), 0,
+                       st, counts, p.nblocks, rowtot, kr, q, sh, p.width);
 #define OS_PASS(Wd, It)                                                                     \
   hipLaunchKernelGGL((os_pass_kernel<K, Wd, It>), dim3((unsigned)p.nblocks), dim3(TPB), 0, st,   \
-                     kin, vin, ko, vo, n, begin_bit + q * p.width, p.width,                    \
-                     rts ? rts_partial : hist + q * 256,                                       \
-                     tickets + q, status + (size_t)q * p.nblocks * p.radix, err, tb,       \
-                     g_sort_ticket, offs, p.nblocks, last ? tile_bins : nullptr, drop && q == 0,  \
+                     kin, vin, ko, vo, n, sh, p.width, rowtot, counts, p.nblocks,              \
+                     last ? tile_bins : nullptr, drop && q == 0,                               \
                      drop && q > 0 ? kept : nullptr, drop && q == 0 ? kept : nullptr,          \
                      q > 0 ? kr.fin : nullptr)
 #define OS_PASS_W(Wd)                                                                       \
@@ -954,8 +596,7 @@ __device__ __forceinline__ void tile_bbox(float x, float y, float radius, int tb
 // rec[g] = {tile allotment, x0 | y0 << 16, x1 | y1 << 16, 0} (tile bbox; < 65536 tiles per axis).
 // One workgroup per depth-sort tile (TPB * ITEMS keys): with counts != null it also writes the
 // tile's histogram of the first sort digit over the visible keys (reduce-then-scan pass 0 of
-// the compacting depth sort) and clears the sort's error word, saving the sort its first count
-// launch.
+// the compacting depth sort), saving the sort its first count launch.
 template <int ITEMS>
 __global__ __launch_bounds__(TPB) void depth_keys_kernel(int n, const float *__restrict__ xys,
                                                          const float *__restrict__ depths,
@@ -967,7 +608,6 @@ __global__ __launch_bounds__(TPB) void depth_keys_kernel(int n, const float *__r
                                                          uint4 *__restrict__ rec,
                                                          uint32_t *__restrict__ counts,
                                                          long long nblocks,
-                                                         uint32_t *__restrict__ err,
                                                          uint32_t *__restrict__ kblk = nullptr) {
   __shared__ uint32_t h[256];
   __shared__ uint32_t kand, kor;
@@ -975,7 +615,6 @@ __global__ __launch_bounds__(TPB) void depth_keys_kernel(int n, const float *__r
   if (counts) {
     h[tid] = 0;
     if (tid == 0) kand = ~0u, kor = 0u;
-    if (blockIdx.x == 0 && tid == 0) *err = 0;
     __syncthreads();
   }
   uint32_t ka = ~0u, ko = 0u;  // the visible keys' AND / OR (KeyRange)
@@ -1032,13 +671,11 @@ __global__ __launch_bounds__(TPB) void depth_keys_kernel(int n, const float *__r
 }
 
 // Depth-ordered allotments and boxes: cnt[p], box[p] from the p-th Gaussian's record (the
-// one random gather of the binning).  The visible count: with kept (compacting depth sort) the
-// sort's kept-key count -- order holds only the visible Gaussians and the positions past them
-// get zero allotments; otherwise the index where the depth-sorted keys reach the culled
-// sentinel.  One workgroup per scan tile (SC_TILE entries): it also writes the tile's
+// one random gather of the binning).  kept = the compacting depth sort's kept-key count (the
+// visible count): order holds only the visible Gaussians and the positions past them get zero
+// allotments.  One workgroup per scan tile (SC_TILE entries): it also writes the tile's
 // allotment sum, the first step of the device scan of cnt.
 __global__ __launch_bounds__(TPB) void gather_counts_kernel(int n, const uint32_t *__restrict__ order,
-                                                            const uint32_t *__restrict__ skeys,
                                                             const uint32_t *__restrict__ kept,
                                                             const uint4 *__restrict__ rec,
                                                             uint32_t *__restrict__ cnt,
@@ -1048,53 +685,34 @@ __global__ __launch_bounds__(TPB) void gather_counts_kernel(int n, const uint32_
   __shared__ uint32_t lds[TPB / 64];
   const long long base = (long long)blockIdx.x * SC_TILE;
   uint32_t sum = 0;
-  if (kept) {
-    const long long nv = min((long long)n, (long long)*kept);
-    if (blockIdx.x == 0 && threadIdx.x == 0) *num_visible = (int)nv;
-    if (base < nv) {  // workgroup-uniform
-      // all ids, then all records, with clamped indices and no per-item branch, so each level
-      // of the gather has its 16 loads in flight together
-      uint32_t ord[SC_ITEMS];
-      uint4 q[SC_ITEMS];
+  const long long nv = min((long long)n, (long long)*kept);
+  if (blockIdx.x == 0 && threadIdx.x == 0) *num_visible = (int)nv;
+  if (base < nv) {  // workgroup-uniform
+    // all ids, then all records, with clamped indices and no per-item branch, so each level
+    // of the gather has its 16 loads in flight together
+    uint32_t ord[SC_ITEMS];
+    uint4 q[SC_ITEMS];
 #pragma unroll
-      for (int k = 0; k < SC_ITEMS; ++k)
-        ord[k] = order[min(base + k * TPB + threadIdx.x, nv - 1)];
+    for (int k = 0; k < SC_ITEMS; ++k)
+      ord[k] = order[min(base + k * TPB + threadIdx.x, nv - 1)];
 #pragma unroll
-      for (int k = 0; k < SC_ITEMS; ++k) q[k] = rec[ord[k]];
+    for (int k = 0; k < SC_ITEMS; ++k) q[k] = rec[ord[k]];
 #pragma unroll
-      for (int k = 0; k < SC_ITEMS; ++k) {
-        const long long p = base + k * TPB + threadIdx.x;
-        if (p < nv) {
-          cnt[p] = q[k].x;
-          box[p] = make_uint2(q[k].y, q[k].z);
-          sum += q[k].x;
-        } else if (p < n) {
-          cnt[p] = 0u;
-        }
-      }
-    } else {
-#pragma unroll
-      for (int k = 0; k < SC_ITEMS; ++k) {
-        const long long p = base + k * TPB + threadIdx.x;
-        if (p < n) cnt[p] = 0u;
+    for (int k = 0; k < SC_ITEMS; ++k) {
+      const long long p = base + k * TPB + threadIdx.x;
+      if (p < nv) {
+        cnt[p] = q[k].x;
+        box[p] = make_uint2(q[k].y, q[k].z);
+        sum += q[k].x;
+      } else if (p < n) {
+        cnt[p] = 0u;
       }
     }
-    uint32_t total;
-    block_exclusive_scan<TPB>(sum, total, lds);
-    if (threadIdx.x == 0) partial[blockIdx.x] = total;
-    return;
-  }
+  } else {
 #pragma unroll
-  for (int k = 0; k < SC_ITEMS; ++k) {
-    const long long p = base + k * TPB + threadIdx.x;
-    if (p < n) {
-      const uint4 q = rec[order[p]];
-      cnt[p] = q.x;
-      box[p] = make_uint2(q.y, q.z);
-      sum += q.x;
-      const bool vis = skeys[p] != 0xFFFFFFFFu;
-      if (vis && (p == n - 1 || skeys[p + 1] == 0xFFFFFFFFu)) *num_visible = (int)(p + 1);
-      if (p == 0 && !vis) *num_visible = 0;  // nothing visible
+    for (int k = 0; k < SC_ITEMS; ++k) {
+      const long long p = base + k * TPB + threadIdx.x;
+      if (p < n) cnt[p] = 0u;
     }
   }
   uint32_t total;
@@ -1191,40 +809,6 @@ __global__ __launch_bounds__(TPB) void bin_edges_kernel(long long n, const K *__
   }
 }
 
-// The same for the fused binning's 32-bit tile keys, four keys per thread: one 16-B load,
-// the predecessor of the first from the neighbouring lane (lane 0 loads it).
-__global__ __launch_bounds__(TPB) void bin_edges4_kernel(long long n, const uint32_t *__restrict__ keys,
-                                                         int *__restrict__ bins, long long rows) {
-  const long long q = (long long)blockIdx.x * TPB + threadIdx.x;  // keys [4q, 4q + 4)
-  const long long k0 = 4 * q;
-  uint32_t v[4];
-  if (k0 + 3 < n) {
-    const uint4 w = *reinterpret_cast<const uint4 *>(keys + k0);
-    v[0] = w.x; v[1] = w.y; v[2] = w.z; v[3] = w.w;
-  } else {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] = k0 + r < n ? keys[k0 + r] : 0u;
-  }
-  uint32_t prev = __shfl_up(v[3], 1, 64);
-  if ((threadIdx.x & 63) == 0 && k0 > 0 && k0 - 1 < n) prev = keys[k0 - 1];
-  if (k0 >= n) return;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const long long k = k0 + r;
-    if (k >= n) break;
-    const long long cur = (long long)(int32_t)v[r];
-    if (k == 0 && cur >= 0 && cur < rows) bins[2 * cur] = 0;
-    if (k == n - 1 && cur >= 0 && cur < rows) bins[2 * cur + 1] = (int)n;
-    if (k > 0) {
-      const long long pv = (long long)(int32_t)(r == 0 ? prev : v[r - 1]);
-      if (pv != cur) {
-        if (pv >= 0 && pv < rows) bins[2 * pv + 1] = (int)k;
-        if (cur >= 0 && cur < rows) bins[2 * cur] = (int)k;
-      }
-    }
-  }
-}
-
 // map_gaussian_to_intersects (gsplat layout: Gaussian-major, bbox row-major).
 __global__ __launch_bounds__(TPB) void map_intersects_kernel(
     int n, const float *__restrict__ xys, const float *__restrict__ depths,
@@ -1265,7 +849,6 @@ __global__ __launch_bounds__(TPB) void map_intersects_kernel(
 constexpr int BK_NT = 1024;               // threads of the bucket count / place / scan kernels
 constexpr int BK_CHUNK = 4096;            // Gaussians per bucket workgroup
 constexpr int BK_MAX_BUCKETS = 16448;     // tiles + 1 (sentinel bucket) held in LDS (~64 KB)
-constexpr int BS_ITEMS = 16;
 
 // phase 1: per block, the sum of tile allotments and the number of visible Gaussians
 __global__ __launch_bounds__(TPB) void bk_totals_kernel(int n, const uint4 *__restrict__ rec,
@@ -1488,30 +1071,18 @@ __global__ __launch_bounds__(BK_NT) void bk_place_kernel(int n, const uint4 *__r
   }
 }
 
-// ---- tile counting sort of the depth-ordered intersections (ABLATION, bit-exact) ----
-// Measured (tools/exp_binning.py, bin_gaussians per call, same process): headline 0.267 ms
-// against 0.255 ms for emission + two LSD passes, c4 0.323 vs 0.333, c5 2.35 vs 1.93 ms.  The
-// placement writes are the cost: a (chunk, tile) cell holds I / (chunks x T) ~ 3.5 ids at the
-// headline, so every chunk writes thousands of 4-14 byte runs (partial lines), while an LSD
-// pass with 128 digits writes runs of ~32 per workgroup tile.  Fewer, larger chunks would
-// starve the GPU.  Kept behind gsplat_debug_tile_sort_counting(1).
+// ---- intersection generation from the depth-ordered allotments (large frames) ----
 // The intersections in depth order (slot j of the exclusive scan `off` of the depth-ordered
-// allotments) are placed straight into their tile buckets, stably, without ever writing the
-// (tile, id) pairs: gsplat's stable sort by tile of its depth-sorted keys is exactly a
-// counting sort whose ties keep slot order.  Slots are cut into chunks of rpc rounds x 4,096
-// (16 waves x 256: one wave segment each); (1) tc_first_kernel records the owner of every
-// segment's first slot; (2) tc_count_kernel counts each chunk's tiles into LDS and writes one
-// column of the chunk x bucket matrix M; (3) bk_scan_kernel scans M per bucket (exclusive over
-// chunks) and writes tile_bins; (4) tc_place_kernel regenerates each round's 4,096 slots, ranks
-// them stably by tile with two 8-bit LDS radix passes (the ballot-match ranking of
-// os_pass_kernel), and writes every id at its bucket cursor + rank.  Four launches, no key
-// arrays: I x 4 bytes written, against the emission's 8 I plus two 16-byte-per-key sort passes
-// -- but in tiny runs (above).
+// allotments), generated on the fly without an emitted (tile, id) array: slots are cut into
+// wave segments of 256 (4 per lane); tc_first_kernel records the owner of every segment's
+// first slot, and tc_gen regenerates a segment's (tile, id) pairs from it (ep0_* below).  (A
+// counting sort placing them straight into their tile buckets was measured slower at every
+// size: a (chunk, tile) cell holds ~3.5 ids at the headline, so its placement writes are runs
+// of 4-14 bytes; headline 0.267 vs 0.255 ms, c5 2.35 vs 1.93 ms.)
 constexpr int TC_NT = 1024;
 constexpr int TC_NW = TC_NT / 64;
 constexpr int TC_SEG = 256;                 // slots per wave segment (4 per lane)
 constexpr int TC_ROUND = TC_SEG * TC_NW;    // slots per workgroup round
-constexpr int TC_MAX_CHUNKS = 512;
 
 struct TcSrc {
   const uint32_t *first, *off, *cnt, *order;
@@ -1601,28 +1172,6 @@ __device__ __forceinline__ void tc_gen(const TcSrc &S, long long seg, uint32_t (
   }
 }
 
-__global__ __launch_bounds__(TC_NT) void tc_count_kernel(TcSrc S, int rpc, int nbk,
-                                                         uint32_t *__restrict__ M,
-                                                         uint32_t *__restrict__ ctr) {
-  extern __shared__ uint32_t hist[];
-  for (int i = threadIdx.x; i < nbk; i += TC_NT) hist[i] = 0u;
-  if (blockIdx.x == 0 && threadIdx.x == 0) *ctr = 0u;  // bk_scan's last-block counter
-  __syncthreads();
-  const int wave = threadIdx.x >> 6;
-  for (int r = 0; r < rpc; ++r) {
-    const long long seg = ((long long)blockIdx.x * rpc + r) * TC_NW + wave;
-    if (seg * TC_SEG >= (long long)S.I) break;  // wave-uniform
-    uint32_t tile[4], gid[4];
-    tc_gen(S, seg, tile, gid);
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (tile[k] != ~0u) atomicAdd(&hist[tile[k]], 1u);
-  }
-  __syncthreads();
-  uint32_t *col = M + (size_t)blockIdx.x * nbk;
-  for (int i = threadIdx.x; i < nbk; i += TC_NT) col[i] = hist[i];
-}
-
 // One stable LDS radix pass over the workgroup's 4,096 16-bit keys (item order: wave, k,
 // lane): digit (key >> shift) & 255 ranked by ballot match with per-wave counters, then
 // offset by the digit's exclusive count over earlier waves and earlier digits.
@@ -1668,73 +1217,6 @@ __device__ __forceinline__ void tc_rank_pass(const uint32_t (&key)[4], int shift
 #pragma unroll
   for (int k = 0; k < 4; ++k) pos[k] = dofs[dig[k]] + wcnt[wave * 256 + dig[k]] + rank[k];
   __syncthreads();  // wcnt / dofs are reused by the next pass
-}
-
-__global__ __launch_bounds__(TC_NT) void tc_place_kernel(TcSrc S, int rpc, int nbk,
-                                                         const uint32_t *__restrict__ M,
-                                                         const uint32_t *__restrict__ start,
-                                                         uint32_t *__restrict__ ids) {
-  extern __shared__ uint32_t smem[];
-  uint32_t *cur = smem;                                          // [nbk]: bucket cursors
-  uint32_t *valA = cur + ((nbk + 3) & ~3);                       // [4096]
-  uint32_t *wcnt = valA + TC_ROUND;                              // [16][256]
-  uint32_t *dofs = wcnt + TC_NW * 256;                           // [256]
-  uint32_t *tmp = dofs + 256;                                    // [16]
-  uint16_t *keyA = reinterpret_cast<uint16_t *>(tmp + 16);       // [4096]
-  uint16_t *keyB = keyA + TC_ROUND;                              // [4096]
-  const uint32_t *col = M + (size_t)blockIdx.x * nbk;
-  for (int i = threadIdx.x; i < nbk; i += TC_NT) cur[i] = start[i] + col[i];
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  for (int r = 0; r < rpc; ++r) {
-    const long long rbase = ((long long)blockIdx.x * rpc + r) * TC_ROUND;
-    if (rbase >= (long long)S.I) break;  // workgroup-uniform
-    const uint32_t nvalid = (uint32_t)min((long long)TC_ROUND, (long long)S.I - rbase);
-    const long long seg = rbase / TC_SEG + wave;
-    uint32_t key[4], gid[4], pos[4];
-    if (seg * TC_SEG < (long long)S.I) {
-      tc_gen(S, seg, key, gid);
-    } else {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) key[k] = ~0u, gid[k] = 0u;
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) key[k] = key[k] == ~0u ? 0xFFFFu : key[k];  // past I: last
-    __syncthreads();  // the previous round's readers of keyB / cur are done
-    tc_rank_pass(key, 0, pos, wcnt, dofs, tmp);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      keyA[pos[k]] = (uint16_t)key[k];
-      valA[pos[k]] = gid[k];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int i = wave * TC_SEG + k * 64 + lane;
-      key[k] = keyA[i];
-      gid[k] = valA[i];
-    }
-    tc_rank_pass(key, 8, pos, wcnt, dofs, tmp);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) keyB[pos[k]] = (uint16_t)key[k];
-    __syncthreads();
-    // bucket cursor minus the run's first sorted position at each run start, so that the id
-    // at sorted position i goes to cur[t] + i; then the run length is added at its end
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint32_t i = pos[k];
-      if (i < nvalid && (i == 0 || keyB[i - 1] != (uint16_t)key[k])) cur[key[k]] -= i;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (pos[k] < nvalid) ids[cur[key[k]] + pos[k]] = gid[k];
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint32_t i = pos[k];
-      if (i < nvalid && (i == nvalid - 1 || keyB[i + 1] != (uint16_t)key[k])) cur[key[k]] += i + 1;
-    }
-  }
 }
 
 // ---- the tile sort's first LSD pass, generated (shipped) ----
@@ -1818,10 +1300,6 @@ __global__ __launch_bounds__(TC_NT) void ep0_place_kernel(TcSrc S, int width, lo
   }
 }
 
-size_t tc_place_lds(int nbk) {
-  return (size_t)(((nbk + 3) & ~3) + TC_ROUND + TC_NW * 256 + 256 + 16) * 4 +
-         (size_t)2 * TC_ROUND * 2;
-}
 
 // ---- per-tile LSD radix sort (bk_sort_kernel) ----
 // ITEMS = 0: the MSD kernel's layout (key/val arrays of CAPX entries)
@@ -1924,12 +1402,8 @@ constexpr int BS_MSD_MAXB = 64;
 template <int NT, int ITEMS, int SI>
 __device__ bool bs_msd_sort(uint32_t s0, uint32_t L, const uint32_t *__restrict__ ids,
                             const uint32_t *__restrict__ dkeys, uint32_t *__restrict__ out,
-                            BsSmem<NT, SI> &sm, unsigned long long *tl = nullptr) {
+                            BsSmem<NT, SI> &sm) {
   constexpr int MB = BsSmem<NT, SI>::MB;
-  auto stamp = [&](int k) {
-    if (tl && threadIdx.x == 0) tl[k] = __builtin_amdgcn_s_memrealtime();
-  };
-  stamp(0);
   constexpr int LOGMB = MB == 2048 ? 11 : MB == 1024 ? 10 : MB == 512 ? 9 : 8;
   static_assert((1 << LOGMB) == MB, "MSD bucket count must be 256..2048");
   const int tid = threadIdx.x;
@@ -1945,13 +1419,6 @@ __device__ bool bs_msd_sort(uint32_t s0, uint32_t L, const uint32_t *__restrict_
       kmx = max(kmx, k[r]);
     }
   }
-  if (tl) {  // force the loads for the timestamp
-    uint32_t acc = 0;
-#pragma unroll
-    for (int r = 0; r < ITEMS; ++r) if (tid + r * NT < L) acc ^= k[r];
-    asm volatile("" ::"v"(acc));
-  }
-  stamp(1);
   uint32_t *hist = sm.mtab, *bstart = sm.mtab + MB;
   for (int e = tid; e < MB; e += NT) hist[e] = 0;
   // min and max in one round: sm.red2 = {min k, min ~k}
@@ -1971,7 +1438,6 @@ __device__ bool bs_msd_sort(uint32_t s0, uint32_t L, const uint32_t *__restrict_
   }
   __syncthreads();
   const uint32_t kmin = sm.red2[0], kmax = sm.red2[1];
-  stamp(2);
   const int bits = 32 - __builtin_clz((kmax - kmin) | 1u);
   const int shift = bits > LOGMB ? bits - LOGMB : 0;
 #pragma unroll
@@ -1982,7 +1448,6 @@ __device__ bool bs_msd_sort(uint32_t s0, uint32_t L, const uint32_t *__restrict_
     }
   }
   __syncthreads();
-  stamp(3);
   constexpr int PER = MB / NT;
   uint32_t c[PER], sum = 0, mx = 0;
 #pragma unroll
@@ -2004,7 +1469,6 @@ __device__ bool bs_msd_sort(uint32_t s0, uint32_t L, const uint32_t *__restrict_
     run += c[j];
   }
   __syncthreads();
-  stamp(4);
   if (sm.red2[2] > (uint32_t)BS_MSD_MAXB) return false;
 #pragma unroll
   for (int r = 0; r < ITEMS; ++r) {
@@ -2015,7 +1479,6 @@ __device__ bool bs_msd_sort(uint32_t s0, uint32_t L, const uint32_t *__restrict_
     }
   }
   __syncthreads();
-  stamp(5);
 #pragma unroll
   for (int r = 0; r < ITEMS; ++r) {
     if (tid + r * NT < L) {
@@ -2029,11 +1492,6 @@ __device__ bool bs_msd_sort(uint32_t s0, uint32_t L, const uint32_t *__restrict_
       out[s0 + bs + rank] = v[r];
     }
   }
-  if (tl) {
-    __builtin_amdgcn_s_waitcnt(0);
-    __syncthreads();
-    stamp(6);
-  }
   return true;
 }
 
@@ -2045,8 +1503,7 @@ __global__ __launch_bounds__(NT) void bk_msd_kernel(int nbk, const uint32_t *__r
                                                     const uint32_t *__restrict__ ids,
                                                     const uint32_t *__restrict__ dkeys,
                                                     uint32_t *__restrict__ out,
-                                                    uint32_t *__restrict__ fail,
-                                                    unsigned long long *__restrict__ tlog) {
+                                                    uint32_t *__restrict__ fail) {
   __shared__ BsSmem<NT, 0> sm;
   const int b = blockIdx.x;
   const uint32_t s0 = start[b], L = tot[b];
@@ -2055,7 +1512,7 @@ __global__ __launch_bounds__(NT) void bk_msd_kernel(int nbk, const uint32_t *__r
     if (threadIdx.x == 0) out[s0] = ids[s0];
   } else if (L > 1) {
     ok = L <= (uint32_t)(NT * ITEMS) &&
-         bs_msd_sort<NT, ITEMS>(s0, L, ids, dkeys, out, sm, tlog ? tlog + 8 * b : nullptr);
+         bs_msd_sort<NT, ITEMS>(s0, L, ids, dkeys, out, sm);
   }
   if (threadIdx.x == 0) fail[b] = ok ? 0u : 1u;
 }
@@ -2073,7 +1530,7 @@ __global__ __launch_bounds__(NT) void bk_sort_kernel(int nbk, uint32_t lo, uint3
                                                      const uint32_t *__restrict__ dkeys,
                                                      uint32_t *__restrict__ out, uint32_t *ka,
                                                      uint32_t *va, uint32_t *kb, uint32_t *vb,
-                                                     int dbg, const uint32_t *__restrict__ fail) {
+                                                     const uint32_t *__restrict__ fail) {
   constexpr int CAP = NT * ITEMS;
   __shared__ BsSmem<NT, ITEMS> sm;
   const int b = blockIdx.x;
@@ -2087,10 +1544,6 @@ __global__ __launch_bounds__(NT) void bk_sort_kernel(int nbk, uint32_t lo, uint3
   }
   if (L <= (uint32_t)CAP) {
     const int R = (int)((L + NT - 1) / NT);  // rows per wave
-    if (dbg & 1) {  // timing ablation: copy only
-      for (uint32_t i = tid; i < L; i += NT) out[s0 + i] = ids[s0 + i];
-      return;
-    }
     uint32_t k[ITEMS], v[ITEMS], dg[ITEMS], dst[ITEMS];
     uint32_t kmn = 0xFFFFFFFFu;
 #pragma unroll
@@ -2113,7 +1566,6 @@ __global__ __launch_bounds__(NT) void bk_sort_kernel(int nbk, uint32_t lo, uint3
       const uint32_t x = bs_block_reduce(xv, false, sm);
       for (int d = 0; d < 4; ++d) keymask |= ((x >> (8 * d)) & 0xFFu) ? 1u << d : 0u;
     }
-    if (dbg & 2) keymask = 0;  // timing ablation: loads, reductions and the tie check only
     for (int phase = 0;; ++phase) {
       // passes: id digits (idmask) then key digits (keymask), least significant first
       for (int q = 0; q < 8; ++q) {
@@ -2271,7 +1723,7 @@ struct Carver {
 };
 
 struct Phase1 {
-  uint32_t *dkeys_a, *dvals_a, *dkeys_b, *dvals_b, *dkeys_s, *order, *cnt, *off;
+  uint32_t *dkeys_a, *dvals_a, *dkeys_b, *dvals_b, *order, *cnt, *off;
   uint4 *rec;  // per-Gaussian binning record (Gaussian order)
   uint2 *box;  // tile bbox in depth order
   void *rs_ws;
@@ -2286,15 +1738,12 @@ Phase1 carve_phase1(void *base, int n) {
   p.dvals_a = c.take<uint32_t>(nn);
   p.dkeys_b = c.take<uint32_t>(nn);
   p.dvals_b = c.take<uint32_t>(nn);
-  p.dkeys_s = c.take<uint32_t>(nn);
   p.order = c.take<uint32_t>(nn);
   p.cnt = c.take<uint32_t>(nn);
   p.off = c.take<uint32_t>(nn);
   p.rec = c.take<uint4>(nn * 4);
   p.box = c.take<uint2>(nn * 2);
   size_t rs = radix_ws_bytes(n, 0, 32);
-  const size_t rw = radix_wide_ws_bytes(n);
-  if (rw > rs) rs = rw;
   size_t sc = scan_ws_bytes(n);
   p.rs_ws = c.take<char>(rs > sc ? rs : sc);
   p.bytes = c.off;
@@ -2308,7 +1757,7 @@ int bits_for(long long v) {  // smallest b with (1 << b) > v
 }
 
 struct Phase2 {
-  uint32_t *tk_a, *tv_a, *tk_b, *tv_b, *tk_s;
+  uint32_t *tk_a, *tv_a, *tk_b, *tv_b;
   uint32_t *first;  // segment owners of the generated first tile pass (tc_first_kernel)
   void *rs_ws;
   size_t bytes;
@@ -2322,7 +1771,6 @@ Phase2 carve_phase2(void *base, long long I) {
   p.tv_a = c.take<uint32_t>(ii);
   p.tk_b = c.take<uint32_t>(ii);
   p.tv_b = c.take<uint32_t>(ii);
-  p.tk_s = c.take<uint32_t>(ii);
   p.first = c.take<uint32_t>((size_t)(I > 0 ? cdiv(I, (long long)TC_SEG) : 1) * 4);
   p.rs_ws = c.take<char>(radix_ws_bytes(I, 0, 32));  // >= any tile-key width
   p.bytes = c.off;
@@ -2359,29 +1807,6 @@ BkWs carve_bk(void *base, int n, long long I, long long T) {
 
 // tile counting sort, phase 2: segment owners, the chunk x bucket matrix, bucket totals /
 // starts, the scan's last-block counter
-struct TcWs {
-  uint32_t *first, *M, *tot, *start, *ctr;
-  int nchunks, rpc, nbk;
-  size_t bytes;
-};
-
-TcWs carve_tc(void *base, long long I, long long T) {
-  TcWs w;
-  Carver c(base);
-  const long long rounds = I > 0 ? cdiv(I, (long long)TC_ROUND) : 1;
-  w.rpc = (int)max(1LL, cdiv(rounds, (long long)TC_MAX_CHUNKS));
-  w.nchunks = (int)cdiv(rounds, (long long)w.rpc);
-  w.nbk = (int)(T + 1);
-  w.first = c.take<uint32_t>((size_t)(I > 0 ? cdiv(I, (long long)TC_SEG) : 1) * 4);
-  w.M = c.take<uint32_t>((size_t)w.nchunks * w.nbk * 4);
-  w.tot = c.take<uint32_t>((size_t)w.nbk * 4);
-  w.start = c.take<uint32_t>((size_t)w.nbk * 4);
-  w.ctr = c.take<uint32_t>(4);
-  w.bytes = c.off;
-  return w;
-}
-
-bool g_tile_counting = false;  // gsplat_debug_tile_sort_counting (ablation; 0: two LSD passes)
 // gsplat_debug_emit_pass0: 0 = emit_kernel + a plain first pass, 1 = generated first pass when
 // the emitted pairs (8 I bytes) would not stay in the 256 MB MALL (I >= 2^24), 2 = always.
 // Measured (tools/exp_binning.py): c5 (83M) 1.93 -> 1.78 ms; headline (7.7M) 0.256 -> 0.268 ms
@@ -2391,11 +1816,17 @@ int g_emit_pass0 = 1;
 bool use_emit_pass0(long long I) {
   return g_emit_pass0 == 2 || (g_emit_pass0 == 1 && I >= (1LL << 24));
 }
-bool use_tc(long long T) { return g_tile_counting && T + 1 <= BK_MAX_BUCKETS; }
-
-bool g_bucket = false;  // gsplat_debug_binning_scheme
-int g_bk_dbg = 0;      // gsplat_debug_binning_scheme(bucket | ablation bits << 1)
-bool use_bucket(long long T) { return g_bucket && T + 1 <= BK_MAX_BUCKETS; }
+// Binning scheme (gsplat_debug_binning_scheme): -1 by size (shipped), 0 depth sort + tile sort,
+// 1 tile buckets + per-tile sorts.  The buckets need far fewer launches (8 against ~23), which
+// wins where every launch is short: small scenes, whose tile lists are short too (c2, 100k
+// Gaussians @ 512^2, max list 837: 0.100 vs 0.112 ms).  A long list is sorted by one
+// workgroup, so real scenes lose (c3 bear, 300k, max list 7,984: 0.365 vs 0.144 ms; headline
+// 1M: 0.287 vs 0.243); the cut is on N, which the count phase must know before I exists.
+int g_bin_scheme = -1;
+bool use_bucket(long long n, long long T) {
+  if (T + 1 > BK_MAX_BUCKETS) return false;
+  return g_bin_scheme < 0 ? n <= (1LL << 17) : g_bin_scheme == 1;
+}
 
 }  // namespace
 
@@ -2408,25 +1839,9 @@ BinKeys bin_keys_view(void *workspace1, int n) {
 
 using namespace gs;
 
-extern "C" int gsplat_debug_sort_items(int items) {
-  g_items_override = (items == 4 || items == 8 || items == 16) ? items : 0;
-  return 0;
-}
-
-extern "C" int gsplat_debug_bins_from_sort(int on) {
-  g_bins_from_sort = on != 0;
-  return 0;
-}
-
 extern "C" int gsplat_debug_emit_pass0(int on) {
   const int prev = g_emit_pass0;
   if (on >= 0) g_emit_pass0 = on > 2 ? 2 : on;
-  return prev;
-}
-
-extern "C" int gsplat_debug_tile_sort_counting(int on) {
-  const int prev = g_tile_counting;
-  if (on >= 0) g_tile_counting = on != 0;
   return prev;
 }
 
@@ -2436,32 +1851,10 @@ extern "C" int gsplat_debug_depth_key_range(int on) {
   return prev;
 }
 
-extern "C" int gsplat_debug_compact_depth_sort(int on) {
-  const int prev = g_compact_depth_sort;
-  if (on >= 0) g_compact_depth_sort = on != 0;
+extern "C" int gsplat_debug_binning_scheme(int scheme) {
+  const int prev = g_bin_scheme;
+  if (scheme >= -1 && scheme <= 1) g_bin_scheme = scheme;
   return prev;
-}
-
-extern "C" int gsplat_debug_depth_sort_wide(int on) {
-  g_depth_sort_wide = on != 0;
-  return 0;
-}
-
-extern "C" int gsplat_debug_sort_scheme(int reduce_then_scan) {
-  g_sort_rts = reduce_then_scan != 0;
-  return 0;
-}
-
-extern "C" int gsplat_debug_sort_timing(void *buffer, int calls) {
-  g_sort_timing = (unsigned long long *)buffer;
-  g_sort_timing_calls = buffer ? calls : 0;
-  return 0;
-}
-
-extern "C" int gsplat_debug_binning_scheme(int bucket) {
-  g_bucket = (bucket & 1) != 0;
-  g_bk_dbg = bucket >> 1;
-  return 0;
 }
 
 extern "C" size_t gsplat_bin_emit_workspace_size_for(int num_points, int64_t num_intersects,
@@ -2469,11 +1862,7 @@ extern "C" size_t gsplat_bin_emit_workspace_size_for(int num_points, int64_t num
   size_t sorted = carve_phase2(nullptr, num_intersects).bytes;
   const long long T = (long long)tile_bounds_x * tile_bounds_y;
   if (num_points < 0 || num_intersects < 0 || T <= 0) return sorted;
-  if (use_tc(T)) {
-    const size_t tc = carve_tc(nullptr, num_intersects, T).bytes;
-    if (tc > sorted) sorted = tc;
-  }
-  if (!use_bucket(T)) return sorted;
+  if (!use_bucket(num_points, T)) return sorted;
   const size_t bk = carve_bk(nullptr, num_points, num_intersects, T).bytes;
   return bk > sorted ? bk : sorted;
 }
@@ -2508,7 +1897,7 @@ static int bin_count_impl(int num_points, const float *xys, const float *depths,
     return check_launch("bin_count");
   }
   const int n = num_points;
-  if (use_bucket(T)) {  // bucket scheme: depth keys + records, then I and the visible count
+  if (use_bucket(num_points, T)) {  // buckets: depth keys + records, then I and the visible count
     const SortPlan sp = sort_plan(n, 0, 32);
 #define DEPTH_KEYS0(It)                                                                     \
   hipLaunchKernelGGL(depth_keys_kernel<It>, dim3((unsigned)sp.nblocks), dim3(TPB), 0, st, n, xys, \
@@ -2525,20 +1914,17 @@ static int bin_count_impl(int num_points, const float *xys, const float *depths,
     hipLaunchKernelGGL(bk_finalize_kernel, dim3(1), dim3(1024), 0, st, nb, partial, d_counts);
     return check_launch("bin_count");
   }
-  // depth keys + records; in reduce-then-scan mode also the sort's pass-0 tile counts
+  // depth keys + records + the sort's pass-0 tile counts.  The depth sort compacts: its first
+  // pass drops the culled Gaussians' all-ones keys, so the later passes, the gather and the
+  // emission see only the visible ones.  depth_keys_kernel counts pass 0 (visible keys);
+  // keyed: the sort counts pass 0 itself
   const SortPlan sp = sort_plan(n, 0, 32);
-  const bool wide = g_depth_sort_wide && g_sort_rts;  // three 11-bit passes (radix_sort_pairs_wide)
-  // the reduce-then-scan depth sort compacts: its first pass drops the culled Gaussians'
-  // all-ones keys, so the later passes, the gather and the emission see only the visible ones
-  const bool compact = g_sort_rts && !wide && g_compact_depth_sort;
-  // depth_keys_kernel counts pass 0 (visible keys) for the compacting sort; keyed: the sort
-  // counts pass 0 itself
-  const bool pre = compact && !keyed;
+  const bool pre = !keyed;
   uint32_t *c0 = pre ? rts_tile_counts(p.rs_ws) : nullptr;
 #define DEPTH_KEYS(It)                                                                      \
   hipLaunchKernelGGL(depth_keys_kernel<It>, dim3((unsigned)sp.nblocks), dim3(TPB), 0, st, n, xys, \
                      depths, radii, num_tiles_hit, tile_bounds_x, tile_bounds_y, p.dkeys_a,    \
-                     p.dvals_a, p.rec, c0, sp.nblocks, sort_err_word(p.rs_ws),                 \
+                     p.dvals_a, p.rec, c0, sp.nblocks,                                         \
                      pre && use_key_range(n)                                                  \
                          ? (uint32_t *)((char *)p.rs_ws + radix_main_bytes(sp)) : nullptr)
   if (keyed) {
@@ -2547,20 +1933,15 @@ static int bin_count_impl(int num_points, const float *xys, const float *depths,
   else if (sp.items == 8) DEPTH_KEYS(8);
   else DEPTH_KEYS(4);
 #undef DEPTH_KEYS
-  if (wide)
-    radix_sort_pairs_wide(p.dkeys_a, p.dvals_a, p.dkeys_b, p.dvals_b, p.dkeys_s, p.order, n,
-                          p.rs_ws, st);
-  else
-    radix_sort_pairs<uint32_t>(p.dkeys_a, p.dvals_a, p.dkeys_b, p.dvals_b,
-                               compact ? nullptr : p.dkeys_s, p.order, n, 0, 32, p.rs_ws, st,
-                               pre, nullptr, 0, compact);
+  radix_sort_pairs<uint32_t>(p.dkeys_a, p.dvals_a, p.dkeys_b, p.dvals_b, nullptr, p.order, n, 0,
+                             32, p.rs_ws, st, pre, nullptr, 0, true);
   // depth-ordered allotments (+ per-tile sums) -> scan -> offsets and I = d_counts[1]
   const int nb = (int)cdiv(n, SC_TILE);
   // the kept count sits in the sort workspace's head, before the tile counts reused below
-  const uint32_t *kept = compact ? sort_kept_word(p.rs_ws) : nullptr;
+  const uint32_t *kept = sort_kept_word(p.rs_ws);
   uint32_t *partial = rts_tile_counts(p.rs_ws);  // the sort is done with its tile counts
-  hipLaunchKernelGGL(gather_counts_kernel, dim3(nb), dim3(TPB), 0, st, n, p.order, p.dkeys_s,
-                     kept, p.rec, p.cnt, p.box, d_counts, partial);
+  hipLaunchKernelGGL(gather_counts_kernel, dim3(nb), dim3(TPB), 0, st, n, p.order, kept, p.rec,
+                     p.cnt, p.box, d_counts, partial);
   hipLaunchKernelGGL(scan_partials_kernel, dim3(1), dim3(1024), 0, st, partial, nb,
                      (uint32_t *)(d_counts + 1));
   hipLaunchKernelGGL(scan_downsweep_kernel, dim3(nb), dim3(TPB), 0, st, p.cnt, (long long)n,
@@ -2598,7 +1979,7 @@ extern "C" int gsplat_bin_emit(int num_points, int64_t num_intersects, int tile_
     return 1;
   }
   Phase1 p1 = carve_phase1(const_cast<void *>(workspace1), num_points);
-  if (use_bucket(T)) {
+  if (use_bucket(num_points, T)) {
     const BkWs w = carve_bk(workspace2, num_points, num_intersects, T);
     if (workspace1_bytes < p1.bytes || workspace2_bytes < w.bytes) {
       set_error("bin_emit: workspaces %zu/%zu < %zu/%zu bytes (phase-2 size from "
@@ -2621,35 +2002,13 @@ extern "C" int gsplat_bin_emit(int num_points, int64_t num_intersects, int tile_
     // 4,096: 256 threads; longer: 1,024 threads, in LDS up to 14,336, then through the
     // ping-pong buffers)
     hipLaunchKernelGGL((bk_msd_kernel<TPB, 16>), dim3(w.nbk), dim3(TPB), 0, st, w.nbk, w.start,
-                       w.tot, w.ids, p1.dkeys_a, (uint32_t *)gaussian_ids_sorted, w.fail,
-                       g_sort_timing);
+                       w.tot, w.ids, p1.dkeys_a, (uint32_t *)gaussian_ids_sorted, w.fail);
     hipLaunchKernelGGL((bk_sort_kernel<TPB, 16>), dim3(w.nbk), dim3(TPB), 0, st, w.nbk, 0u,
                        (uint32_t)(TPB * 16), w.start, w.tot, w.ids, p1.dkeys_a,
-                       (uint32_t *)gaussian_ids_sorted, w.ka, w.va, w.kb, w.vb, g_bk_dbg, w.fail);
+                       (uint32_t *)gaussian_ids_sorted, w.ka, w.va, w.kb, w.vb, w.fail);
     hipLaunchKernelGGL((bk_sort_kernel<1024, 14>), dim3(w.nbk), dim3(1024), 0, st, w.nbk,
                        (uint32_t)(TPB * 16 + 1), 0xFFFFFFFFu, w.start, w.tot, w.ids, p1.dkeys_a,
-                       (uint32_t *)gaussian_ids_sorted, w.ka, w.va, w.kb, w.vb, 0, w.fail);
-    return check_launch("bin_emit");
-  }
-  if (use_tc(T) && workspace1_bytes >= p1.bytes &&
-      workspace2_bytes >= carve_tc(nullptr, num_intersects, T).bytes) {
-    // tile counting sort straight from the depth-ordered allotments (see tc_place_kernel)
-    const TcWs w = carve_tc(workspace2, num_intersects, T);
-    if (num_intersects == 0 || num_points == 0) {
-      note(hipMemsetAsync(tile_bins, 0, (size_t)T * 2 * sizeof(int32_t), st), "hipMemsetAsync");
-      return check_launch("bin_emit");
-    }
-    const int n = num_points;
-    const TcSrc S{w.first, p1.off, p1.cnt, p1.order, p1.box, n, (uint32_t)num_intersects,
-                  tile_bounds_x, tile_bounds_y};
-    hipLaunchKernelGGL(tc_first_kernel, dim3(cdiv(n, TPB)), dim3(TPB), 0, st, n, p1.cnt, p1.off,
-                       w.first);
-    hipLaunchKernelGGL(tc_count_kernel, dim3(w.nchunks), dim3(TC_NT), (size_t)w.nbk * 4, st, S,
-                       w.rpc, w.nbk, w.M, w.ctr);
-    hipLaunchKernelGGL(bk_scan_kernel, dim3(cdiv(w.nbk, 64)), dim3(BK_NT), 0, st, w.nbk, w.nchunks,
-                       w.M, w.tot, w.start, w.ctr, (int)T, tile_bins);
-    hipLaunchKernelGGL(tc_place_kernel, dim3(w.nchunks), dim3(TC_NT), tc_place_lds(w.nbk), st, S,
-                       w.rpc, w.nbk, w.M, w.start, (uint32_t *)gaussian_ids_sorted);
+                       (uint32_t *)gaussian_ids_sorted, w.ka, w.va, w.kb, w.vb, w.fail);
     return check_launch("bin_emit");
   }
   Phase2 p2 = carve_phase2(workspace2, num_intersects);
@@ -2665,7 +2024,7 @@ extern "C" int gsplat_bin_emit(int num_points, int64_t num_intersects, int tile_
   const int n = num_points;
   const long long I = num_intersects;
   const SortPlan tp = sort_plan(I, 0, bits_for(T));
-  if (use_emit_pass0(I) && g_sort_rts && g_bins_from_sort && tp.passes >= 2) {
+  if (use_emit_pass0(I) && tp.passes >= 2) {
     // pass 0 of the tile sort generated from the allotments (ep0_place_kernel), the rest as below
     const long long nrounds = cdiv(I, (long long)TC_ROUND);
     uint32_t *ws = (uint32_t *)p2.rs_ws;
@@ -2681,7 +2040,7 @@ extern "C" int gsplat_bin_emit(int num_points, int64_t num_intersects, int tile_
                        nrounds, rowtot);
     hipLaunchKernelGGL(ep0_place_kernel, dim3((unsigned)nrounds), dim3(TC_NT), 0, st, S, tp.width,
                        nrounds, rowtot, counts, p2.tk_b, p2.tv_b);
-    radix_sort_pairs<uint32_t>(p2.tk_a, p2.tv_a, p2.tk_b, p2.tv_b, p2.tk_s,
+    radix_sort_pairs<uint32_t>(p2.tk_a, p2.tv_a, p2.tk_b, p2.tv_b, nullptr,
                                (uint32_t *)gaussian_ids_sorted, I, 0, bits_for(T), p2.rs_ws, st,
                                false, tile_bins, T, false, 1);
     return check_launch("bin_emit");
@@ -2690,16 +2049,9 @@ extern "C" int gsplat_bin_emit(int num_points, int64_t num_intersects, int tile_
                      p1.off, p1.box, tile_bounds_x, tile_bounds_y, p2.tk_a, p2.tv_a, tile_bins);
   // the tile sort's last pass writes the tile table itself (runs of equal tile ids) instead of
   // the sorted keys a bin-edges kernel would re-read (emit_kernel cleared the table)
-  if (g_bins_from_sort) {
-    radix_sort_pairs<uint32_t>(p2.tk_a, p2.tv_a, p2.tk_b, p2.tv_b, p2.tk_s,
-                               (uint32_t *)gaussian_ids_sorted, I, 0, bits_for(T), p2.rs_ws, st,
-                               false, tile_bins, T);
-  } else {
-    radix_sort_pairs<uint32_t>(p2.tk_a, p2.tv_a, p2.tk_b, p2.tv_b, p2.tk_s,
-                               (uint32_t *)gaussian_ids_sorted, I, 0, bits_for(T), p2.rs_ws, st);
-    hipLaunchKernelGGL(bin_edges4_kernel, dim3(cdiv(cdiv(I, 4), TPB)), dim3(TPB), 0, st, I,
-                       p2.tk_s, tile_bins, T);
-  }
+  radix_sort_pairs<uint32_t>(p2.tk_a, p2.tv_a, p2.tk_b, p2.tv_b, nullptr,
+                             (uint32_t *)gaussian_ids_sorted, I, 0, bits_for(T), p2.rs_ws, st,
+                             false, tile_bins, T);
   return check_launch("bin_emit");
 }
 

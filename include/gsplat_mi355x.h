@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define GSPLAT_MI355X_ABI_VERSION 9
+#define GSPLAT_MI355X_ABI_VERSION 10
 
 int gsplat_abi_version(void);
 const char *gsplat_last_error(void);
@@ -387,45 +387,22 @@ int gsplat_debug_set_raster_variant(int fwd_pxl, int bwd_pxl, int bwd_flags);
 /* 1 while the shipped raster variants are selected (the record-based entries need them). */
 int gsplat_debug_raster_variant_is_default(void);
 
-/* Profiling hook (not part of the gsplat surface): the next `calls` radix-sort passes write
- * per-workgroup phase timestamps (s_memrealtime, 100 MHz: start, ticket, keys loaded, ranked,
- * tile counts scanned, scattered to LDS, offsets resolved, end) as consecutive
- * [workgroups][8] uint64 slabs into the device buffer (NULL disables). */
-int gsplat_debug_sort_timing(void *buffer, int calls);
-/* Radix-sort pass scheme: 1 = reduce-then-scan (default), 0 = one-sweep decoupled look-back. */
-int gsplat_debug_sort_scheme(int reduce_then_scan);
-/* Depth sort of gsplat_bin_count: four 8-bit passes (0, default) or three 11-bit passes (1,
- * slower: ablation); both give the identical stable order. */
-int gsplat_debug_depth_sort_wide(int on);
-/* Depth sort of gsplat_bin_count (reduce-then-scan, 8-bit passes): its first pass drops the
- * culled Gaussians' keys so that the later passes, the allotment gather and the emission run
- * over the visible Gaussians only (1, default), or sorts all N keys (0).  Identical outputs.
- * Returns the previous setting; -1 only queries. */
-int gsplat_debug_compact_depth_sort(int on);
-/* Depth sort of gsplat_bin_count: LSD passes whose digit is the same for every kept key (from
- * the keys' AND / OR, found during the first pass) only copy -- from 2^22 keys (1, default),
- * always (2) -- or rank as any pass (0).  Identical outputs.  Returns the previous setting; -1
- * only queries. */
-int gsplat_debug_depth_key_range(int on);
-/* Tile sort of gsplat_bin_emit: the emission of (tile, id) pairs plus two LSD radix passes
- * (0, default), or a counting sort placing the depth-ordered intersections straight into their
- * tile buckets, stably (1: ablation, frames up to 16,447 tiles; slower -- its placement writes
- * are runs of a few ids).  Identical outputs.  Returns the previous setting; -1 only queries. */
-int gsplat_debug_tile_sort_counting(int on);
-/* First pass of gsplat_bin_emit's tile sort: run over emitted (tile, id) pairs (0), generated
- * from the depth-ordered allotments without an emitted key array when I >= 2^24 (1, default:
- * the pairs would not stay in the MALL), or always generated (2).  Identical outputs.  Returns
- * the previous setting; -1 only queries. */
+/* Binning dispatch switches (not part of the gsplat surface; every setting gives the identical
+ * output, tests cover each).  Each returns the previous setting; -1 (or, for the scheme, -2)
+ * only queries.
+ * gsplat_debug_emit_pass0: the tile sort's first pass run over emitted (tile, id) pairs (0),
+ *   generated from the depth-ordered allotments without an emitted key array when I >= 2^24
+ *   (1, shipped: the pairs would not stay in the MALL), or always generated (2).
+ * gsplat_debug_depth_key_range: depth-sort passes whose digit is the same for every kept key
+ *   (from the keys' AND / OR, found during the first pass) only copy -- from 2^22 keys (1,
+ *   shipped), always (2) -- or rank as any pass (0).
+ * gsplat_debug_binning_scheme: -1 by size (shipped: tile buckets + per-tile LDS sorts for
+ *   scenes of <= 131,072 Gaussians on frames up to 16,447 tiles, else the depth sort + stable
+ *   tile sort), 0 depth sort + tile sort, 1 tile buckets.  Must not change between a
+ *   gsplat_bin_count and its gsplat_bin_emit. */
 int gsplat_debug_emit_pass0(int on);
-/* Tile table of gsplat_bin_emit from the last tile-sort pass (1, default: no sorted keys are
- * written or re-read) or from a bin-edges kernel over the sorted keys (0); identical tables. */
-int gsplat_debug_bins_from_sort(int on);
-/* Debug: force 4, 8 or 16 keys per thread in every radix-sort pass (0 = automatic). */
-int gsplat_debug_sort_items(int items);
-/* Binning scheme: 1 = tile bucketing + per-tile LDS sort (frames up to 16,447
- * tiles), 0 = depth sort + stable tile sort (default).  Same output either way.  Must not change between
- * a gsplat_bin_count and its gsplat_bin_emit. */
-int gsplat_debug_binning_scheme(int bucket);
+int gsplat_debug_depth_key_range(int on);
+int gsplat_debug_binning_scheme(int scheme);
 /* Profiling hook: the backward blend kernels record per wave {start, end (s_memrealtime,
  * 100 MHz), HW_ID, XCC_ID, work slot} as [waves][5] uint64 into the device buffer (NULL
  * disables); the buffer needs 5 entries per launched wave. */

@@ -51,40 +51,30 @@ def headline(request, gpu, oracle_lib):
                 colors=colors, opac=opac, config=request.param)
 
 
-@pytest.mark.parametrize("scheme", ["rts", "norange", "range", "gen", "emit", "counting", "full", "rts11",
-                                    "edges", "onesweep", "bucket"])
+@pytest.mark.parametrize("scheme", ["shipped", "norange", "range", "gen", "emit", "bucket"])
 def test_headline_binning_bitexact(gpu, headline, scheme):
-    """Sorted binning: the shipped scheme (depth sort of reduce-then-scan 8-bit passes compacting
-    the culled Gaussians away, constant-digit passes copying from 2^22 keys; then two LSD tile
-    passes, the first generated from the depth-ordered allotments at I >= 2^24 (c5) and over
-    emitted pairs below, the last writing the tile table); the key-range shortcut off or always
-    on; the first tile pass always generated or always over emitted pairs; the tile counting
-    sort; the tile table from a bin-edges kernel; the depth sort over all N keys, in three 11-bit
-    passes or one-sweep; and the tile-bucketing scheme (per-tile LDS sort): all bit-exact."""
+    """Binning bit-exact at full size: the shipped dispatch (for these scenes the depth sort of
+    8-bit reduce-then-scan passes compacting the culled Gaussians away, constant-digit passes
+    copying from 2^22 keys; then two LSD tile passes, the first generated from the depth-ordered
+    allotments at I >= 2^24 (c5) and over emitted pairs below, the last writing the tile table);
+    and every other setting a shipped dispatch takes elsewhere: the key-range shortcut off or
+    always on, the first tile pass always generated or always over emitted pairs, and the tile
+    buckets with per-tile LDS sorts (shipped for small scenes)."""
     h, cam = headline, headline["cam"]
     assert h["ref"]["num_intersects"] > 1 << 20
-    if scheme != "rts" and h["config"] in ("c4", "c5"):
-        pytest.skip("ablation schemes: headline and c3 only")
-    _lib.call("gsplat_debug_sort_scheme", 0 if scheme == "onesweep" else 1)
-    _lib.call("gsplat_debug_binning_scheme", 1 if scheme == "bucket" else 0)
-    _lib.call("gsplat_debug_depth_sort_wide", 1 if scheme == "rts11" else 0)
-    _lib.call("gsplat_debug_bins_from_sort", 0 if scheme == "edges" else 1)
-    _lib.lib().gsplat_debug_compact_depth_sort(0 if scheme == "full" else 1)
-    _lib.lib().gsplat_debug_tile_sort_counting(1 if scheme == "counting" else 0)
-    _lib.lib().gsplat_debug_emit_pass0({"emit": 0, "gen": 2}.get(scheme, 1))
-    _lib.lib().gsplat_debug_depth_key_range({"norange": 0, "range": 2}.get(scheme, 1))
+    if scheme != "shipped" and h["config"] in ("c4", "c5"):
+        pytest.skip("the other dispatches: headline and c3 only")
+    L = _lib.lib()
+    L.gsplat_debug_binning_scheme(1 if scheme == "bucket" else -1)
+    L.gsplat_debug_emit_pass0({"emit": 0, "gen": 2}.get(scheme, 1))
+    L.gsplat_debug_depth_key_range({"norange": 0, "range": 2}.get(scheme, 1))
     try:
         I, gids, bins = bin_gaussians(h["xys"], h["depths"], h["radii"], h["nth"], cam.height,
                                       cam.width)
     finally:
-        _lib.call("gsplat_debug_sort_scheme", 1)
-        _lib.call("gsplat_debug_binning_scheme", 0)
-        _lib.call("gsplat_debug_depth_sort_wide", 0)
-        _lib.call("gsplat_debug_bins_from_sort", 1)
-        _lib.lib().gsplat_debug_compact_depth_sort(1)
-        _lib.lib().gsplat_debug_tile_sort_counting(0)
-        _lib.lib().gsplat_debug_emit_pass0(1)
-        _lib.lib().gsplat_debug_depth_key_range(1)
+        L.gsplat_debug_binning_scheme(-1)
+        L.gsplat_debug_emit_pass0(1)
+        L.gsplat_debug_depth_key_range(1)
     assert I == h["ref"]["num_intersects"]
     np.testing.assert_array_equal(_np(gids), h["ref"]["gaussian_ids_sorted"])
     np.testing.assert_array_equal(_np(bins), h["ref"]["tile_bins"])

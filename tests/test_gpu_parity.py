@@ -150,24 +150,27 @@ def test_sh_unaligned_slab(gpu):
                                rtol=RTOL, atol=ATOL)
 
 
-@pytest.mark.parametrize("scheme", ["lsd", "emit", "counting", "bucket"])
+# binning dispatch settings: (gsplat_debug_binning_scheme, gsplat_debug_emit_pass0)
+BIN_SETTINGS = {"shipped": (-1, 1), "gen": (0, 2), "emit": (0, 0), "bucket": (1, 1)}
+
+
+@pytest.mark.parametrize("scheme", list(BIN_SETTINGS))
 @pytest.mark.parametrize("case", CASES)
 def test_binning_fused_bitexact(gpu, case, scheme):
-    """The tile sort as shipped (first LSD pass generated from the depth-ordered allotments),
-    over emitted (tile, id) pairs, as the counting sort, and the tile-bucketing scheme:
-    bit-exact against the oracle's stable sort of gsplat's keys."""
+    """The binning as dispatched for each case, the depth sort + tile sort with the first LSD
+    tile pass generated from the depth-ordered allotments or run over emitted (tile, id) pairs,
+    and the tile buckets with per-tile LDS sorts: bit-exact against the oracle's stable sort of
+    gsplat's keys."""
     sc, cam, scales, quats = _inputs(*case)
     g, o = _project_both(gpu, sc, cam, scales, quats)
     xys, depths, radii, conics, nth, cov3d = g
     L = _lib.lib()
-    _lib.call("gsplat_debug_binning_scheme", 1 if scheme == "bucket" else 0)
-    prev = L.gsplat_debug_tile_sort_counting(1 if scheme == "counting" else 0)
-    prev_e = L.gsplat_debug_emit_pass0(0 if scheme == "emit" else 2)
+    b, e = BIN_SETTINGS[scheme]
+    prev, prev_e = L.gsplat_debug_binning_scheme(b), L.gsplat_debug_emit_pass0(e)
     try:
         I, gids, bins = bin_gaussians(xys, depths, radii, nth, cam.height, cam.width)
     finally:
-        _lib.call("gsplat_debug_binning_scheme", 0)
-        L.gsplat_debug_tile_sort_counting(prev)
+        L.gsplat_debug_binning_scheme(prev)
         L.gsplat_debug_emit_pass0(prev_e)
     ref = O.bin_and_sort(o[0], o[1], o[2], o[4], cam.tile_bounds)
     assert I == ref["num_intersects"]
@@ -175,10 +178,10 @@ def test_binning_fused_bitexact(gpu, case, scheme):
     np.testing.assert_array_equal(_np(bins), ref["tile_bins"])
 
 
-def test_binning_counting_inconsistent_allotments(gpu):
+def test_binning_inconsistent_allotments(gpu):
     """Caller-supplied num_tiles_hit that disagree with the tile boxes (allotments larger than
-    the box are padded with the sentinel tile, smaller ones truncate the box): the counting tile
-    sort and the generated first LSD pass place exactly what emission + LSD does, including
+    the box are padded with the sentinel tile, smaller ones truncate the box): the generated
+    first LSD tile pass and the tile buckets place exactly what emission + LSD does, including
     Gaussians whose allotment spans several rounds (one Gaussian over 600 tiles)."""
     sc, cam, scales, quats = _inputs(20000, 512, 512, 2, 0.003, 0.03, 1.5)
     g, _ = _project_both(gpu, sc, cam, scales, quats)
@@ -190,12 +193,13 @@ def test_binning_counting_inconsistent_allotments(gpu):
     nth[vis[5]] = 600
     out = []
     L = _lib.lib()
-    for counting, gen in ((1, 1), (0, 2), (0, 0)):
-        prev, prev_e = L.gsplat_debug_tile_sort_counting(counting), L.gsplat_debug_emit_pass0(gen)
+    for scheme in ("emit", "gen", "bucket"):
+        b, e = BIN_SETTINGS[scheme]
+        prev, prev_e = L.gsplat_debug_binning_scheme(b), L.gsplat_debug_emit_pass0(e)
         try:
             I, gids, bins = bin_gaussians(xys, depths, radii, nth, cam.height, cam.width)
         finally:
-            L.gsplat_debug_tile_sort_counting(prev)
+            L.gsplat_debug_binning_scheme(prev)
             L.gsplat_debug_emit_pass0(prev_e)
         out.append((I, _np(gids), _np(bins)))
     for o in out[1:]:

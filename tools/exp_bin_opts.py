@@ -1,6 +1,6 @@
-"""Binning option A/B per config (same process): bin_gaussians per call (events around 20
-calls) with the shipped settings, the 11-bit depth sort (gsplat_debug_depth_sort_wide) and the
-one-sweep look-back passes (gsplat_debug_sort_scheme 0); outputs must stay identical.  CFGS env
+"""Binning scheme A/B per config (same process): bin_gaussians per call (events around 20
+calls) with the shipped dispatch, the depth sort + tile sort forced, and the tile buckets
+forced (gsplat_debug_binning_scheme -1 / 0 / 1); outputs must stay identical.  CFGS env
 (default "c2 c3 headline")."""
 import os, sys
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
@@ -11,9 +11,8 @@ from gaussctrl_exp_amd.project_gaussians import project_gaussians
 from gaussctrl_exp_amd.rasterize import bin_gaussians
 
 dev = torch.device("cuda:0")
-OPTS = {"shipped": [], "wide": [("gsplat_debug_depth_sort_wide", 1, 0)],
-        "onesweep": [("gsplat_debug_sort_scheme", 0, 1)],
-        "bucket": [("gsplat_debug_binning_scheme", 1, 0)]}
+OPTS = {"shipped": [], "sorted": [("gsplat_debug_binning_scheme", 0, -1)],
+        "bucket": [("gsplat_debug_binning_scheme", 1, -1)]}
 for cfg in os.environ.get("CFGS", "c2 c3 headline").split():
     sc, cam = bench.make_workload(cfg, 0, dev)
     cam = cam.to(dev)
@@ -25,7 +24,7 @@ for cfg in os.environ.get("CFGS", "c2 c3 headline").split():
     ref = None
     for name, sets in OPTS.items():
         for fn, on, _ in sets:
-            _lib.call(fn, on)
+            getattr(_lib.lib(), fn)(on)
         for _ in range(3):
             out = bin_gaussians(xys, depths, radii, nth, cam.height, cam.width)
         if ref is None:
@@ -39,6 +38,6 @@ for cfg in os.environ.get("CFGS", "c2 c3 headline").split():
         e.record()
         torch.cuda.synchronize()
         for fn, _, off in sets:
-            _lib.call(fn, off)
+            getattr(_lib.lib(), fn)(off)
         print(f"{cfg} {name:9s}: bin_gaussians {s.elapsed_time(e) / 20:.4f} ms, identical {same}",
               flush=True)
