@@ -171,16 +171,34 @@ def bin_gaussians(xys: Tensor, depths: Tensor, radii: Tensor, num_tiles_hit: Ten
                               dtype=torch.uint8)
             _lib.call("gsplat_bin_count", n, P(xys), P(depths), P(radii), P(num_tiles_hit), tbx,
                       tby, P(counts), P(ws1), ws1.numel(), st)
+        # the phase-2 outputs are allocated while the count phase runs, sized by the last
+        # intersection count of this frame shape (+1/8): the host's work between reading I and
+        # launching the emission -- the GPU's one idle gap of the binning -- is the launch alone
+        key = (dev, n, tbx, tby)
+        cap = _EMIT_CAP.get(key, 0)
+        pre = _emit_buffers(dev, n, cap, tbx, tby) if cap else None
         num_intersects = _wait_count(host, torch.cuda.current_stream(dev))
         visible = int(host[0])
     finally:
         _COUNTS.release(dev, slot, visible)
-    gaussian_ids_sorted = torch.empty((max(num_intersects, 0),), device=dev, dtype=torch.int32)
-    ws2 = torch.empty((_lib.query("gsplat_bin_emit_workspace_size_for", n, num_intersects, tbx,
-                                  tby),), device=dev, dtype=torch.uint8)
-    _lib.call("gsplat_bin_emit", n, num_intersects, tbx, tby, P(gaussian_ids_sorted),
-              P(tile_bins), P(ws1), ws1.numel(), P(ws2), ws2.numel(), st)
-    return num_intersects, gaussian_ids_sorted, tile_bins
+    if pre is None or num_intersects > cap:
+        pre = _emit_buffers(dev, n, num_intersects, tbx, tby)
+    _EMIT_CAP[key] = num_intersects + (num_intersects >> 3)
+    ids_buf, ws2 = pre
+    _lib.call("gsplat_bin_emit", n, num_intersects, tbx, tby, P(ids_buf), P(tile_bins), P(ws1),
+              ws1.numel(), P(ws2), ws2.numel(), st)
+    return num_intersects, ids_buf[:max(num_intersects, 0)], tile_bins
+
+
+# frame shape -> the intersection capacity to pre-allocate the emission's outputs for
+_EMIT_CAP = {}
+
+
+def _emit_buffers(dev, n, cap, tbx, tby):
+    ids = torch.empty((max(cap, 0),), device=dev, dtype=torch.int32)
+    ws2 = torch.empty((_lib.query("gsplat_bin_emit_workspace_size_for", n, cap, tbx, tby),),
+                      device=dev, dtype=torch.uint8)
+    return ids, ws2
 
 
 class _BinCache:
