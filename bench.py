@@ -99,15 +99,25 @@ def algorithmic_bytes(N, I, P, T, K, nvis):
     """Per-view algorithmic HBM bytes of each C-ABI entry point (SURVEY.md §8d model; the
     binning entries count every radix pass's key/value reads and writes)."""
     tile_passes = max(1, -(-max(1, (T - 1).bit_length()) // 8))  # 8-bit digits of the tile id
+    # the tile buckets (gsplat_debug_binning_scheme; shipped for N <= 2^17 on <= 16,447 tiles)
+    setting = int(_lib.lib().gsplat_debug_binning_scheme(-2))
+    bucket = setting == 1 or (setting == -1 and N <= (1 << 17) and T + 1 <= 16448)
+    if bucket:
+        # count: allotment + visibility sums over the records and keys (20 N); emit: the
+        # records twice (bucket counts, placement: 32 N), ids placed (4 I), then per tile the ids
+        # and their depth keys read and the sorted ids written (12 I), the tile table (8 T)
+        bin_count, bin_emit = 20 * N, 32 * N + 16 * I + 8 * T
+    else:
+        # depth keys (44 N) + 4 radix passes (count 4 N, scatter 16 N each) + the depth-ordered
+        # record gather (36 N) + the allotment scan (8 N); keyed: without the key pass
+        # emission (records in, (tile, id) pairs out) + per tile-digit pass 20 I + bin edges
+        bin_count, bin_emit = 168 * N, 20 * N + 8 * I + 20 * tile_passes * I + 4 * I + 8 * T
     return {
         "gsplat_project_gaussians_forward": 96 * N,
         "gsplat_compute_sh_forward": (24 + 12 * K) * N,
-        # depth keys (44 N) + 4 radix passes (count 4 N, scatter 16 N each) + the depth-ordered
-        # record gather (36 N) + the allotment scan (8 N)
-        "gsplat_bin_count": 168 * N,
-        "gsplat_bin_count_keyed": 124 * N,
-        # emission (records in, (tile, id) pairs out) + per tile-digit pass 20 I + bin edges
-        "gsplat_bin_emit": 20 * N + 8 * I + 20 * tile_passes * I + 4 * I + 8 * T,
+        "gsplat_bin_count": bin_count,
+        "gsplat_bin_count_keyed": bin_count if bucket else bin_count - 44 * N,
+        "gsplat_bin_emit": bin_emit,
         "gsplat_rasterize_forward": 40 * I + 20 * P,
         "gsplat_rasterize_backward": 40 * I + 24 * P + 36 * N,
         "gsplat_compute_sh_backward": (24 + 12 * K) * N,

@@ -28,9 +28,11 @@ for f in files:
 # Per C-ABI entry of the binning, whose kernels (radix passes, scans) are shared between the
 # depth sort (gsplat_bin_count_keyed) and the tile sort (gsplat_bin_emit): segment each pass's
 # dispatch sequence -- a fused forward kernel starts a step's binning, the emission's first
-# kernel (emit / tc_first / ep0_count) starts bin_emit, bins_decode ends it -- and average the
-# per-call sums of every counter over the calls seen.
-EMIT_START = ("emit_kernel", "tc_first_kernel", "ep0_count_kernel")
+# kernel (emit / tc_first / ep0_count, or the tile buckets' bk_count) starts bin_emit,
+# bins_decode (the buckets: the long-list bk_sort) ends it -- and average the per-call sums of
+# every counter over the calls seen.
+EMIT_START = ("emit_kernel", "tc_first_kernel", "ep0_count_kernel", "bk_count_kernel")
+EMIT_END = ("bins_decode_kernel", "bk_sort_kernel<1024")
 entries = collections.defaultdict(lambda: collections.defaultdict(float))
 calls = collections.defaultdict(set)
 for f in files:
@@ -57,7 +59,7 @@ for f in files:
         for c, v in disp[d].items():
             entries[state][(os.path.dirname(f), c)] += v
         calls[state].add((os.path.dirname(f), seg))
-        if state == "gsplat_bin_emit" and "bins_decode_kernel" in k:
+        if state == "gsplat_bin_emit" and any(s in k for s in EMIT_END):
             state = None
 entry_rows = {}
 for e, d in entries.items():
