@@ -58,6 +58,33 @@ def test_host_queries_without_gpu():
     assert _lib.query("gsplat_sort_isect_pairs_workspace_size", 0) > 0
 
 
+def test_list_split_policy_without_gpu():
+    """gsplat_rasterize_chunk_size: parts of ~0.6 mean list lengths (a multiple of 64, at least
+    256) below 12,288 tiles, no split above (c5's 16,384 tiles) or without intersections; the
+    debug override forces / disables it; the plan buffer grows with the part count."""
+    from gaussctrl_exp_amd import _lib
+    q = lambda *a: _lib.query("gsplat_rasterize_chunk_size", *a)
+    assert q(68, 68, 7_717_748) == 1024  # headline: mean 1,669 per tile
+    assert q(32, 32, 1_686_461) == 1024  # c3 bear: mean 1,647
+    assert q(32, 32, 10_000) == 256      # short lists: the floor
+    assert q(128, 128, 83_276_610) == 0  # c5: 16,384 tiles, unsplit
+    assert q(32, 32, 0) == 0
+    for t, i in ((68, 7_717_748), (32, 1_686_461), (50, 123_457)):
+        c = q(t, t, i)
+        assert c % 64 == 0 and c >= 256
+    L = _lib.lib()
+    try:
+        L.gsplat_debug_set_chunk(100)
+        assert q(68, 68, 7_717_748) == 128  # forced, rounded up to 64
+        L.gsplat_debug_set_chunk(-1)
+        assert q(68, 68, 7_717_748) == 0
+    finally:
+        L.gsplat_debug_set_chunk(0)
+    b = lambda c: _lib.query("gsplat_rasterize_split_bytes", 68, 68, 7_717_748, c)
+    assert b(0) == 0 and b(100) == 0  # no split / not a multiple of 64
+    assert b(256) > b(1024) > 4624 * (4 + 8)  # work[T] + items[>= T]
+
+
 def test_quirk_switch_reaches_the_library():
     """GSPLAT_MI355X_QUIRKS / quirks.set select the [VERIFY] behaviours in the library."""
     from gaussctrl_exp_amd import _lib, quirks
