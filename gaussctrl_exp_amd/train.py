@@ -223,7 +223,12 @@ class TrainStep:
             out = self._render(cam, background, adam=adam)
         loss = self.loss(out["rgb"], gt, clamp_pred=not out.get("clamped", True))
         if loss.requires_grad:
-            loss.backward()
+            # a kept ones() seed: autograd's own seed is a fill kernel per step
+            seed = getattr(self, "_seed", None)
+            if seed is None or seed.device != loss.device or seed.dtype != loss.dtype or \
+                    seed.shape != loss.shape:
+                seed = self._seed = torch.ones_like(loss)
+            loss.backward(seed)
         elif self.sh_exchange is not None and self.scene.features_rest.shape[1] > 0:
             # no Gaussian in view (the caller returned the background): no local gradient,
             # but the other ranks' SH exchange still needs this rank's (zero) record
