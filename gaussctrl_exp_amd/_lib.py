@@ -161,11 +161,14 @@ def query(name: str, *args) -> int:
 
 
 def ptr(t):
-    return None if t is None else _c.c_void_p(t.data_ptr())
+    """A tensor's device address for a `void *` argument (a plain int: ctypes converts it per
+    the entry's argtypes, without a c_void_p object per argument)."""
+    return None if t is None else t.data_ptr()
 
 
-def stream(device) -> _c.c_void_p:
-    return _c.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+def stream(device) -> int:
+    """The current HIP stream of `device`, as the `void *stream` argument."""
+    return torch.cuda.current_stream(device).cuda_stream
 
 
 def check_device(name: str, *tensors):

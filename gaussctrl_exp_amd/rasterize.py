@@ -215,7 +215,7 @@ class _BinCache:
     @staticmethod
     def _key(tensors, H, W, stream):
         return (tuple((t._version, tuple(t.shape), t.dtype) for t in tensors), H, W,
-                stream.value)
+                stream)
 
     def get(self, tensors, H, W, stream):
         if self.refs is None or len(self.refs) != len(tensors):
