@@ -1,6 +1,6 @@
-"""The one-sweep LSD radix sort (C ABI gsplat_sort_isect_pairs) vs numpy's stable sort,
-from one tile to BASELINE-scale intersection counts, with the look-back error word
-(bounded-spin give-up flag) checked to be clear."""
+"""The LSD radix sort (C ABI gsplat_sort_isect_pairs: reduce-then-scan passes -- digit counts,
+row scans, stable LDS-ranked scatter) vs numpy's stable sort, from one tile to BASELINE-scale
+intersection counts, on a poisoned workspace."""
 import numpy as np
 import pytest
 import torch
@@ -8,13 +8,6 @@ import torch
 from gaussctrl_exp_amd import _lib
 
 pytestmark = pytest.mark.gpu
-
-HEAD_ERR_OFF = (8 * 256 + 8) * 4  # binning.hip: hist[8][256], tickets[8], error word
-
-
-def _al(x):
-    return (x + 255) // 256 * 256
-
 
 @pytest.mark.parametrize("n,bits,hi", [
     (1, 13, 4624), (100, 13, 4624), (4096, 13, 4624), (4097, 13, 4624), (20000, 41, 1 << 41),
@@ -33,9 +26,6 @@ def test_radix_sort_matches_stable_sort(gpu, n, bits, hi):
     P = _lib.ptr
     _lib.call("gsplat_sort_isect_pairs", n, bits, P(k), P(v), P(ko), P(vo), P(ws), wsz,
               _lib.stream(gpu))
-    rs_off = 2 * _al(n * 8) + 2 * _al(n * 4)
-    err = int(ws[rs_off + HEAD_ERR_OFF: rs_off + HEAD_ERR_OFF + 4].cpu().view(torch.int32)[0])
-    assert err == 0, "look-back gave up waiting for a predecessor tile"
     order = np.argsort(keys, kind="stable")
     np.testing.assert_array_equal(ko.cpu().numpy(), keys[order])
     np.testing.assert_array_equal(vo.cpu().numpy(), vals[order])
