@@ -56,6 +56,8 @@ SIGNATURES = {
     "gsplat_debug_binning_scheme": (_I, [_I]),
     "gsplat_bin_count": (_I, [_I, _P, _P, _P, _P, _I, _I, _P, _P, _SZ, _P]),
     "gsplat_bin_emit": (_I, [_I, _I64, _I, _I, _P, _P, _P, _SZ, _P, _SZ, _P]),
+    "gsplat_bin_emit_prelaunch": (_I, [_I, _I64, _I, _I, _P, _P, _SZ, _P, _SZ, _P]),
+    "gsplat_bin_emit_finish": (_I, [_I, _I64, _I64, _I, _I, _P, _P, _P, _SZ, _P, _SZ, _P]),
     "gsplat_rasterize_forward": (_I, [_I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                                       _P, _P]),
     "gsplat_rasterize_forward_rgbd": (_I, [_I, _I, _I, _I] + [_P] * 13),
@@ -93,7 +95,7 @@ SIGNATURES = {
                                                                        _P, _SZ, _P]),
 }
 
-ABI_VERSION = 10  # include/gsplat_mi355x.h GSPLAT_MI355X_ABI_VERSION
+ABI_VERSION = 11  # include/gsplat_mi355x.h GSPLAT_MI355X_ABI_VERSION
 
 _lib = None
 _DETERMINISTIC = os.environ.get("GSPLAT_MI355X_DETERMINISTIC", "0") not in ("", "0")

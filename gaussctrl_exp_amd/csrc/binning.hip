@@ -99,7 +99,8 @@ __global__ __launch_bounds__(TPB) void scan_reduce_kernel(const uint32_t *__rest
 
 // Single workgroup: exclusive scan of partial[0..nb) in place; grand total -> *total.
 __global__ __launch_bounds__(1024) void scan_partials_kernel(uint32_t *__restrict__ partial,
-                                                             int nb, uint32_t *__restrict__ total_out) {
+                                                             int nb, uint32_t *__restrict__ total_out,
+                                                             uint32_t *__restrict__ total_dev = nullptr) {
   __shared__ uint32_t lds[16];
   uint32_t running = 0;
   for (int c = 0; c < nb; c += 1024) {
@@ -110,7 +111,10 @@ __global__ __launch_bounds__(1024) void scan_partials_kernel(uint32_t *__restric
     if (i < nb) partial[i] = running + ex;
     running += tot;
   }
-  if (total_out && threadIdx.x == 0) *total_out = running;
+  if (threadIdx.x == 0) {
+    if (total_dev) *total_dev = running;  // device copy (read by the pre-launched emission)
+    if (total_out) *total_out = running;
+  }
 }
 
 // out[i] = partial[block] + exclusive prefix inside the block's tile.  In place is allowed.
@@ -731,7 +735,12 @@ __global__ __launch_bounds__(TPB) void emit_kernel(int n, const uint32_t *__rest
                                                    const uint2 *__restrict__ box, int tbx,
                                                    int tby, uint32_t *__restrict__ tkeys,
                                                    uint32_t *__restrict__ tvals,
-                                                   int *__restrict__ tile_bins) {
+                                                   int *__restrict__ tile_bins,
+                                                   const uint32_t *__restrict__ i_dev = nullptr,
+                                                   uint32_t cap = 0) {
+  // pre-launched before the host knows I (gsplat_bin_emit_prelaunch): outputs hold cap slots;
+  // a larger I writes nothing (the host then re-runs the emission into larger buffers)
+  if (i_dev && *i_dev > cap) return;
   // tile_bins starts zeroed for bin_edges_kernel (empty tiles stay (0, 0)): cleared here
   // instead of by a separate fill launch
   for (long long i = (long long)blockIdx.x * TPB + threadIdx.x; i < 2LL * tbx * tby;
@@ -876,7 +885,8 @@ __global__ __launch_bounds__(TPB) void bk_totals_kernel(int n, const uint4 *__re
 
 // One workgroup: d_counts[0] = visible count, d_counts[1] = I (pinned host memory).
 __global__ __launch_bounds__(1024) void bk_finalize_kernel(int nb, const uint32_t *__restrict__ partial,
-                                                           int *__restrict__ d_counts) {
+                                                           int *__restrict__ d_counts,
+                                                           uint32_t *__restrict__ i_dev) {
   __shared__ uint32_t lds[16];
   uint32_t c = 0, v = 0;
   for (int i = threadIdx.x; i < nb; i += 1024) {
@@ -887,6 +897,7 @@ __global__ __launch_bounds__(1024) void bk_finalize_kernel(int nb, const uint32_
   block_exclusive_scan<1024>(c, tc, lds);
   block_exclusive_scan<1024>(v, tv, lds);
   if (threadIdx.x == 0) {
+    *i_dev = tc;  // device copy (read by the pre-launched placement)
     d_counts[0] = (int)tv;
     __threadfence_system();
     d_counts[1] = (int)tc;  // written last: the host polls this word
@@ -1054,9 +1065,12 @@ __global__ __launch_bounds__(BK_NT) void bk_place_kernel(int n, const uint4 *__r
                                                          int tby, int nbk,
                                                          const uint32_t *__restrict__ M,
                                                          const uint32_t *__restrict__ start,
-                                                         uint32_t *__restrict__ ids) {
+                                                         uint32_t *__restrict__ ids,
+                                                         const uint32_t *__restrict__ i_dev = nullptr,
+                                                         uint32_t cap = 0) {
   constexpr int NW = BK_NT / 64;
   __shared__ uint32_t cur[BK_MAX_BUCKETS];
+  if (i_dev && *i_dev > cap) return;  // pre-launched: as emit_kernel
   const uint32_t *col = M + (size_t)blockIdx.x * nbk;
   for (int i = threadIdx.x; i < nbk; i += BK_NT) cur[i] = start[i] + col[i];
   __syncthreads();
@@ -1726,6 +1740,7 @@ struct Phase1 {
   uint32_t *dkeys_a, *dvals_a, *dkeys_b, *dvals_b, *order, *cnt, *off;
   uint4 *rec;  // per-Gaussian binning record (Gaussian order)
   uint2 *box;  // tile bbox in depth order
+  uint32_t *dcount;  // I on the device (the pre-launched emission's bound check)
   void *rs_ws;
   size_t bytes;
 };
@@ -1743,6 +1758,7 @@ Phase1 carve_phase1(void *base, int n) {
   p.off = c.take<uint32_t>(nn);
   p.rec = c.take<uint4>(nn * 4);
   p.box = c.take<uint2>(nn * 2);
+  p.dcount = c.take<uint32_t>(4 * sizeof(uint32_t));
   size_t rs = radix_ws_bytes(n, 0, 32);
   size_t sc = scan_ws_bytes(n);
   p.rs_ws = c.take<char>(rs > sc ? rs : sc);
@@ -1911,7 +1927,8 @@ static int bin_count_impl(int num_points, const float *xys, const float *depths,
     const int nb = (int)cdiv(n, SC_TILE);
     uint32_t *partial = (uint32_t *)p.rs_ws;
     hipLaunchKernelGGL(bk_totals_kernel, dim3(nb), dim3(TPB), 0, st, n, p.rec, p.dkeys_a, partial);
-    hipLaunchKernelGGL(bk_finalize_kernel, dim3(1), dim3(1024), 0, st, nb, partial, d_counts);
+    hipLaunchKernelGGL(bk_finalize_kernel, dim3(1), dim3(1024), 0, st, nb, partial, d_counts,
+                       p.dcount);
     return check_launch("bin_count");
   }
   // depth keys + records + the sort's pass-0 tile counts.  The depth sort compacts: its first
@@ -1943,7 +1960,7 @@ static int bin_count_impl(int num_points, const float *xys, const float *depths,
   hipLaunchKernelGGL(gather_counts_kernel, dim3(nb), dim3(TPB), 0, st, n, p.order, kept, p.rec,
                      p.cnt, p.box, d_counts, partial);
   hipLaunchKernelGGL(scan_partials_kernel, dim3(1), dim3(1024), 0, st, partial, nb,
-                     (uint32_t *)(d_counts + 1));
+                     (uint32_t *)(d_counts + 1), p.dcount);
   hipLaunchKernelGGL(scan_downsweep_kernel, dim3(nb), dim3(TPB), 0, st, p.cnt, (long long)n,
                      partial, p.off);
   return check_launch("bin_count");
@@ -1964,40 +1981,62 @@ extern "C" int gsplat_bin_count_keyed(int num_points, int tile_bounds_x, int til
                         tile_bounds_y, d_counts, workspace1, workspace1_bytes, true, stream);
 }
 
-extern "C" int gsplat_bin_emit(int num_points, int64_t num_intersects, int tile_bounds_x,
-                               int tile_bounds_y, int32_t *gaussian_ids_sorted,
-                               int32_t *tile_bins, const void *workspace1,
-                               size_t workspace1_bytes, void *workspace2,
-                               size_t workspace2_bytes, void *stream) {
+// The emission in two halves around the host's read of I: HEAD = the launches that need only
+// the phase-1 workspace and output buffers of `cap` intersections (sorted scheme: emit_kernel
+// unless the generated first pass is chosen; bucket scheme: count, scan and placement), each
+// checking the device copy of I against cap; TAIL = the rest (the tile sort / the per-tile
+// sorts).  EMIT_ALL = both, with cap = I (gsplat_bin_emit).
+enum { EMIT_HEAD = 1, EMIT_TAIL = 2, EMIT_ALL = 3 };
+
+static bool emit_head_splits(int n, long long cap, long long T) {
+  if (use_bucket(n, T)) return true;
+  return !(use_emit_pass0(cap) && sort_plan(cap, 0, bits_for(T)).passes >= 2);
+}
+
+static int bin_emit_impl(int num_points, int64_t num_intersects, int64_t capacity,
+                         int tile_bounds_x, int tile_bounds_y, int32_t *gaussian_ids_sorted,
+                         int32_t *tile_bins, const void *workspace1, size_t workspace1_bytes,
+                         void *workspace2, size_t workspace2_bytes, void *stream, int phase) {
   hipStream_t st = (hipStream_t)stream;
   const long long T = (long long)tile_bounds_x * tile_bounds_y;
-  if (num_points < 0 || num_intersects < 0 || num_intersects > 0x3FFFFFFFLL ||
-      tile_bounds_x <= 0 || tile_bounds_y <= 0 || tile_bounds_x > 65535 ||
-      tile_bounds_y > 65535 || T >= (1LL << 31)) {
-    set_error("bin_emit: bad sizes (N=%d I=%lld tiles=%dx%d)", num_points,
-              (long long)num_intersects, tile_bounds_x, tile_bounds_y);
+  if (num_points < 0 || num_intersects < 0 || capacity < num_intersects ||
+      capacity > 0x3FFFFFFFLL || tile_bounds_x <= 0 || tile_bounds_y <= 0 ||
+      tile_bounds_x > 65535 || tile_bounds_y > 65535 || T >= (1LL << 31)) {
+    set_error("bin_emit: bad sizes (N=%d I=%lld capacity=%lld tiles=%dx%d)", num_points,
+              (long long)num_intersects, (long long)capacity, tile_bounds_x, tile_bounds_y);
     return 1;
   }
   Phase1 p1 = carve_phase1(const_cast<void *>(workspace1), num_points);
+  const long long cap = capacity;
+  // the head's launches run here unless they were pre-launched for this capacity
+  const bool split = phase != EMIT_ALL && emit_head_splits(num_points, cap, T);
+  const bool head = phase == EMIT_ALL || (phase == EMIT_HEAD && split) || (phase == EMIT_TAIL && !split);
+  const bool tail = phase != EMIT_HEAD;
+  const uint32_t *idev = phase == EMIT_HEAD ? p1.dcount : nullptr;  // bound check when pre-launched
   if (use_bucket(num_points, T)) {
-    const BkWs w = carve_bk(workspace2, num_points, num_intersects, T);
+    const BkWs w = carve_bk(workspace2, num_points, cap, T);
     if (workspace1_bytes < p1.bytes || workspace2_bytes < w.bytes) {
       set_error("bin_emit: workspaces %zu/%zu < %zu/%zu bytes (phase-2 size from "
                 "gsplat_bin_emit_workspace_size_for)", workspace1_bytes, workspace2_bytes,
                 p1.bytes, w.bytes);
       return 1;
     }
-    if (num_intersects == 0 || num_points == 0) {
-      note(hipMemsetAsync(tile_bins, 0, (size_t)T * 2 * sizeof(int32_t), st), "hipMemsetAsync");
+    if (num_points == 0 || (phase != EMIT_HEAD && num_intersects == 0)) {
+      if (tail)
+        note(hipMemsetAsync(tile_bins, 0, (size_t)T * 2 * sizeof(int32_t), st), "hipMemsetAsync");
       return check_launch("bin_emit");
     }
     const int n = num_points;
-    hipLaunchKernelGGL(bk_count_kernel, dim3(w.nwg), dim3(BK_NT), 0, st, n, p1.rec, tile_bounds_x,
-                       tile_bounds_y, w.nbk, w.M, w.ctr);
-    hipLaunchKernelGGL(bk_scan_kernel, dim3(cdiv(w.nbk, 64)), dim3(BK_NT), 0, st, w.nbk, w.nwg, w.M,
-                       w.tot, w.start, w.ctr, (int)T, tile_bins);
-    hipLaunchKernelGGL(bk_place_kernel, dim3(w.nwg), dim3(BK_NT), 0, st, n, p1.rec, tile_bounds_x,
-                       tile_bounds_y, w.nbk, w.M, w.start, w.ids);
+    if (head) {
+      hipLaunchKernelGGL(bk_count_kernel, dim3(w.nwg), dim3(BK_NT), 0, st, n, p1.rec, tile_bounds_x,
+                         tile_bounds_y, w.nbk, w.M, w.ctr);
+      hipLaunchKernelGGL(bk_scan_kernel, dim3(cdiv(w.nbk, 64)), dim3(BK_NT), 0, st, w.nbk, w.nwg,
+                         w.M, w.tot, w.start, w.ctr, (int)T, tile_bins);
+      hipLaunchKernelGGL(bk_place_kernel, dim3(w.nwg), dim3(BK_NT), 0, st, n, p1.rec,
+                         tile_bounds_x, tile_bounds_y, w.nbk, w.M, w.start, w.ids, idev,
+                         (uint32_t)cap);
+    }
+    if (!tail) return check_launch("bin_emit");
     // MSD + bucket ranking for lists up to 4,096 long; then the LSD sort for the others (up to
     // 4,096: 256 threads; longer: 1,024 threads, in LDS up to 14,336, then through the
     // ping-pong buffers)
@@ -2011,21 +2050,23 @@ extern "C" int gsplat_bin_emit(int num_points, int64_t num_intersects, int tile_
                        (uint32_t *)gaussian_ids_sorted, w.ka, w.va, w.kb, w.vb, w.fail);
     return check_launch("bin_emit");
   }
-  Phase2 p2 = carve_phase2(workspace2, num_intersects);
+  Phase2 p2 = carve_phase2(workspace2, cap);
   if (workspace1_bytes < p1.bytes || workspace2_bytes < p2.bytes) {
     set_error("bin_emit: workspaces %zu/%zu < %zu/%zu bytes", workspace1_bytes,
               workspace2_bytes, p1.bytes, p2.bytes);
     return 1;
   }
-  if (num_intersects == 0 || num_points == 0) {
-    note(hipMemsetAsync(tile_bins, 0, (size_t)T * 2 * sizeof(int32_t), st), "hipMemsetAsync");
+  if (num_points == 0 || (phase != EMIT_HEAD && num_intersects == 0)) {
+    if (tail)
+      note(hipMemsetAsync(tile_bins, 0, (size_t)T * 2 * sizeof(int32_t), st), "hipMemsetAsync");
     return check_launch("bin_emit");
   }
   const int n = num_points;
   const long long I = num_intersects;
-  const SortPlan tp = sort_plan(I, 0, bits_for(T));
-  if (use_emit_pass0(I) && tp.passes >= 2) {
+  if (phase != EMIT_HEAD && !split && use_emit_pass0(I) &&
+      sort_plan(I, 0, bits_for(T)).passes >= 2) {
     // pass 0 of the tile sort generated from the allotments (ep0_place_kernel), the rest as below
+    const SortPlan tp = sort_plan(I, 0, bits_for(T));
     const long long nrounds = cdiv(I, (long long)TC_ROUND);
     uint32_t *ws = (uint32_t *)p2.rs_ws;
     uint32_t *counts = ws + OS_HEAD_WORDS;                      // rts_tile_counts
@@ -2045,14 +2086,47 @@ extern "C" int gsplat_bin_emit(int num_points, int64_t num_intersects, int tile_
                                false, tile_bins, T, false, 1);
     return check_launch("bin_emit");
   }
-  hipLaunchKernelGGL(emit_kernel, dim3(cdiv(n, TPB)), dim3(TPB), 0, st, n, p1.order, p1.cnt,
-                     p1.off, p1.box, tile_bounds_x, tile_bounds_y, p2.tk_a, p2.tv_a, tile_bins);
+  if (head)
+    hipLaunchKernelGGL(emit_kernel, dim3(cdiv(n, TPB)), dim3(TPB), 0, st, n, p1.order, p1.cnt,
+                       p1.off, p1.box, tile_bounds_x, tile_bounds_y, p2.tk_a, p2.tv_a, tile_bins,
+                       idev, (uint32_t)cap);
+  if (!tail) return check_launch("bin_emit");
   // the tile sort's last pass writes the tile table itself (runs of equal tile ids) instead of
   // the sorted keys a bin-edges kernel would re-read (emit_kernel cleared the table)
   radix_sort_pairs<uint32_t>(p2.tk_a, p2.tv_a, p2.tk_b, p2.tv_b, nullptr,
                              (uint32_t *)gaussian_ids_sorted, I, 0, bits_for(T), p2.rs_ws, st,
                              false, tile_bins, T);
   return check_launch("bin_emit");
+}
+
+extern "C" int gsplat_bin_emit(int num_points, int64_t num_intersects, int tile_bounds_x,
+                               int tile_bounds_y, int32_t *gaussian_ids_sorted,
+                               int32_t *tile_bins, const void *workspace1,
+                               size_t workspace1_bytes, void *workspace2,
+                               size_t workspace2_bytes, void *stream) {
+  return bin_emit_impl(num_points, num_intersects, num_intersects, tile_bounds_x, tile_bounds_y,
+                       gaussian_ids_sorted, tile_bins, workspace1, workspace1_bytes, workspace2,
+                       workspace2_bytes, stream, EMIT_ALL);
+}
+
+extern "C" int gsplat_bin_emit_prelaunch(int num_points, int64_t capacity, int tile_bounds_x,
+                                         int tile_bounds_y, int32_t *tile_bins,
+                                         const void *workspace1, size_t workspace1_bytes,
+                                         void *workspace2, size_t workspace2_bytes,
+                                         void *stream) {
+  return bin_emit_impl(num_points, 0, capacity, tile_bounds_x, tile_bounds_y, nullptr, tile_bins,
+                       workspace1, workspace1_bytes, workspace2, workspace2_bytes, stream,
+                       EMIT_HEAD);
+}
+
+extern "C" int gsplat_bin_emit_finish(int num_points, int64_t num_intersects, int64_t capacity,
+                                      int tile_bounds_x, int tile_bounds_y,
+                                      int32_t *gaussian_ids_sorted, int32_t *tile_bins,
+                                      const void *workspace1, size_t workspace1_bytes,
+                                      void *workspace2, size_t workspace2_bytes, void *stream) {
+  return bin_emit_impl(num_points, num_intersects, capacity, tile_bounds_x, tile_bounds_y,
+                       gaussian_ids_sorted, tile_bins, workspace1, workspace1_bytes, workspace2,
+                       workspace2_bytes, stream, EMIT_TAIL);
 }
 
 extern "C" int gsplat_map_gaussian_to_intersects(int num_points, const float *xys,

@@ -172,26 +172,41 @@ def bin_gaussians(xys: Tensor, depths: Tensor, radii: Tensor, num_tiles_hit: Ten
             _lib.call("gsplat_bin_count", n, P(xys), P(depths), P(radii), P(num_tiles_hit), tbx,
                       tby, P(counts), P(ws1), ws1.numel(), st)
         # the phase-2 outputs are allocated while the count phase runs, sized by the last
-        # intersection count of this frame shape (+1/8): the host's work between reading I and
-        # launching the emission -- the GPU's one idle gap of the binning -- is the launch alone
+        # intersection count of this frame shape (+1/8), and the part of the emission that needs
+        # only phase 1 is launched into them before the host waits for I: the GPU works through
+        # the host's read of I and its launch of the rest instead of idling
         key = (dev, n, tbx, tby)
         cap = _EMIT_CAP.get(key, 0)
-        pre = _emit_buffers(dev, n, cap, tbx, tby) if cap else None
+        pre = None
+        if cap:
+            pre = _emit_buffers(dev, n, cap, tbx, tby)
+        if cap and PRELAUNCH_EMISSION:
+            _lib.call("gsplat_bin_emit_prelaunch", n, cap, tbx, tby, P(tile_bins), P(ws1),
+                      ws1.numel(), P(pre[1]), pre[1].numel(), st)
         num_intersects = _wait_count(host, torch.cuda.current_stream(dev))
         visible = int(host[0])
     finally:
         _COUNTS.release(dev, slot, visible)
-    if pre is None or num_intersects > cap:
-        pre = _emit_buffers(dev, n, num_intersects, tbx, tby)
     _EMIT_CAP[key] = num_intersects + (num_intersects >> 3)
-    ids_buf, ws2 = pre
-    _lib.call("gsplat_bin_emit", n, num_intersects, tbx, tby, P(ids_buf), P(tile_bins), P(ws1),
-              ws1.numel(), P(ws2), ws2.numel(), st)
+    if pre is not None and num_intersects <= cap and not PRELAUNCH_EMISSION:  # (A/B runs)
+        ids_buf, ws2 = pre
+        _lib.call("gsplat_bin_emit", n, num_intersects, tbx, tby, P(ids_buf), P(tile_bins),
+                  P(ws1), ws1.numel(), P(ws2), ws2.numel(), st)
+    elif pre is not None and num_intersects <= cap:
+        ids_buf, ws2 = pre
+        _lib.call("gsplat_bin_emit_finish", n, num_intersects, cap, tbx, tby, P(ids_buf),
+                  P(tile_bins), P(ws1), ws1.numel(), P(ws2), ws2.numel(), st)
+    else:  # first call of this frame shape, or more intersections than the capacity
+        ids_buf, ws2 = _emit_buffers(dev, n, num_intersects, tbx, tby)
+        _lib.call("gsplat_bin_emit", n, num_intersects, tbx, tby, P(ids_buf), P(tile_bins),
+                  P(ws1), ws1.numel(), P(ws2), ws2.numel(), st)
     return num_intersects, ids_buf[:max(num_intersects, 0)], tile_bins
 
 
 # frame shape -> the intersection capacity to pre-allocate the emission's outputs for
 _EMIT_CAP = {}
+# launch the emission's first part before the host reads I (False: after it; A/B runs only)
+PRELAUNCH_EMISSION = True
 
 
 def _emit_buffers(dev, n, cap, tbx, tby):

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define GSPLAT_MI355X_ABI_VERSION 10
+#define GSPLAT_MI355X_ABI_VERSION 11
 
 int gsplat_abi_version(void);
 const char *gsplat_last_error(void);
@@ -200,6 +200,24 @@ int gsplat_bin_emit(int num_points, int64_t num_intersects, int tile_bounds_x,
                     int tile_bounds_y, int32_t *gaussian_ids_sorted, int32_t *tile_bins,
                     const void *workspace1, size_t workspace1_bytes, void *workspace2,
                     size_t workspace2_bytes, void *stream);
+/* Phase 2 split around the host's read of I, so that the GPU is not idle while the host
+ * waits for it: gsplat_bin_emit_prelaunch, issued right after phase 1 with buffers sized for
+ * `capacity` intersections (e.g. the last call's I plus a margin), launches the part of the
+ * emission that needs only phase 1's results -- each of its kernels compares the device-side
+ * I with capacity and writes nothing when I > capacity.  Then, with the host's I:
+ *   I <= capacity: gsplat_bin_emit_finish(..., I, capacity, ...) with the SAME buffers, stream
+ *                  and capacity (the workspace layout follows capacity);
+ *   I >  capacity: gsplat_bin_emit (or a new prelaunch + finish) into buffers sized for I.
+ * gaussian_ids_sorted needs capacity slots; workspace2 gsplat_bin_emit_workspace_size_for(N,
+ * capacity, ...) bytes.  Results are identical to gsplat_bin_emit's. */
+int gsplat_bin_emit_prelaunch(int num_points, int64_t capacity, int tile_bounds_x,
+                              int tile_bounds_y, int32_t *tile_bins, const void *workspace1,
+                              size_t workspace1_bytes, void *workspace2, size_t workspace2_bytes,
+                              void *stream);
+int gsplat_bin_emit_finish(int num_points, int64_t num_intersects, int64_t capacity,
+                           int tile_bounds_x, int tile_bounds_y, int32_t *gaussian_ids_sorted,
+                           int32_t *tile_bins, const void *workspace1, size_t workspace1_bytes,
+                           void *workspace2, size_t workspace2_bytes, void *stream);
 
 /* ---- rasterization (forward.cu rasterize_forward, backward.cu rasterize_backward) -----
  * colors [N,C], opacity [N] (or [N,1]), background [C]; out_img [H,W,C], final_Ts [H,W],

@@ -208,6 +208,39 @@ def test_binning_inconsistent_allotments(gpu):
         np.testing.assert_array_equal(o[2], out[0][2])
 
 
+@pytest.mark.parametrize("scheme", list(BIN_SETTINGS))
+def test_binning_prelaunched_emission(gpu, scheme):
+    """The emission pre-launched before the host reads I (gsplat_bin_emit_prelaunch into
+    buffers of the last call's capacity, then gsplat_bin_emit_finish): bit-exact vs the oracle
+    with no capacity (first call: gsplat_bin_emit), a capacity of exactly I, a larger one, and
+    one intersection too few (the pre-launched kernels write nothing and the emission re-runs
+    into buffers sized for I) -- for every binning scheme."""
+    from gaussctrl_exp_amd import rasterize as R
+    sc, cam, scales, quats = _inputs(20000, 512, 512, 2, 0.003, 0.03, 1.5)
+    g, o = _project_both(gpu, sc, cam, scales, quats)
+    xys, depths, radii, conics, nth, cov3d = [t.detach() for t in g]
+    ref = O.bin_and_sort(o[0], o[1], o[2], o[4], cam.tile_bounds)
+    n_ref = ref["num_intersects"]
+    key = (xys.device, xys.shape[0], cam.tile_bounds[0], cam.tile_bounds[1])
+    L = _lib.lib()
+    b, e = BIN_SETTINGS[scheme]
+    prev, prev_e = L.gsplat_debug_binning_scheme(b), L.gsplat_debug_emit_pass0(e)
+    try:
+        for cap in (None, n_ref, n_ref + 1000, n_ref - 1, n_ref):
+            if cap is None:
+                R._EMIT_CAP.pop(key, None)
+            else:
+                R._EMIT_CAP[key] = cap
+            I, gids, bins = bin_gaussians(xys, depths, radii, nth, cam.height, cam.width)
+            assert I == n_ref, cap
+            np.testing.assert_array_equal(_np(gids), ref["gaussian_ids_sorted"])
+            np.testing.assert_array_equal(_np(bins), ref["tile_bins"])
+    finally:
+        L.gsplat_debug_binning_scheme(prev)
+        L.gsplat_debug_emit_pass0(prev_e)
+        R._EMIT_CAP.pop(key, None)
+
+
 @pytest.mark.parametrize("fixed", [(0x5A00, 0xFF00), (0x5A5A00, 0xFFFF00), (0x0, 0x0)])
 def test_binning_depth_key_range(gpu, fixed):
     """Depth keys whose bytes 1 (and 2) are the same for every visible Gaussian: those LSD
