@@ -64,7 +64,8 @@ SIGNATURES = {
     "gsplat_rasterize_backward_workspace_size": (_SZ, [_I, _I]),
     "gsplat_rasterize_chunk_size": (_I, [_I, _I, _I64]),
     "gsplat_rasterize_split_bytes": (_SZ, [_I, _I, _I64, _I]),
-    "gsplat_rasterize_forward_clearing": (_I, [_I, _I, _I, _I] + [_P] * 10 + [_P, _SZ, _P, _P]),
+    "gsplat_rasterize_forward_clearing": (_I, [_I, _I, _I, _I] + [_P] * 10 +
+                                          [_P, _SZ, _P, _I64, _I, _P, _SZ, _P]),
     "gsplat_rasterize_backward_chunked": (_I, [_I, _I, _I, _I, _I] + [_P] * 11 + [_F] +
                                           [_P] * 4 + [_I64, _I, _P, _SZ, _P, _SZ, _P]),
     "gsplat_debug_set_chunk": (_I, [_I]),
@@ -92,10 +93,10 @@ SIGNATURES = {
     "gsplat_grad_records_bytes": (_SZ, [_I]),
     "gsplat_grad_records_split": (_I, [_I, _P, _SZ, _P, _P, _P, _P, _P, _P, _P]),
     "gsplat_rasterize_backward_records": (_I, [_I] * 5 + [_P] * 11 + [_F, _I64, _I, _P, _SZ,
-                                                                       _P, _SZ, _P]),
+                                                                       _I, _P, _SZ, _P]),
 }
 
-ABI_VERSION = 11  # include/gsplat_mi355x.h GSPLAT_MI355X_ABI_VERSION
+ABI_VERSION = 12  # include/gsplat_mi355x.h GSPLAT_MI355X_ABI_VERSION
 
 _lib = None
 _DETERMINISTIC = os.environ.get("GSPLAT_MI355X_DETERMINISTIC", "0") not in ("", "0")

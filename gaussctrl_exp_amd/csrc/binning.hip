@@ -297,14 +297,39 @@ __global__ __launch_bounds__(1024) void rts_rowscan_kernel(uint32_t *__restrict_
 
 template <typename K, int ITEMS>
 struct OsSmem {
-  K keys[TPB * ITEMS];
-  uint32_t vals[TPB * ITEMS];
-  uint32_t wcnt[4][256];   // per-wave digit counters, then per-wave digit offsets
-  uint32_t loc_off[256];   // tile-local exclusive offset of each digit
-  uint32_t gofs[256];      // global output offset of each digit, minus loc_off
-  uint32_t hscan[256];     // exclusive scan of this pass's global histogram
+  // the tile's (key, value) pairs in digit order: 32-bit keys interleaved with their values (one
+  // 8-B LDS access per pair) in the small tiles, two arrays otherwise (16 keys per thread: the
+  // pairs' extra registers would spill)
+  static constexpr bool PAIR = sizeof(K) == 4 && ITEMS <= 8;
+  static constexpr int N = TPB * ITEMS;
+  __attribute__((aligned(16))) uint32_t raw[PAIR ? 2 * N : N * (sizeof(K) / 4 + 1)];
+  uint32_t wcnt[4][256];   // per-wave digit counters, then per-wave digit offsets in the tile
+  uint32_t gofs[256];      // global output offset of each digit, minus its tile offset
+  uint32_t hscan[256];     // exclusive scan of this pass's digit totals (large tiles)
   uint32_t scan_tmp[4];
   uint32_t tile_n;         // keys this tile writes (all valid ones; fewer when dropping)
+  __device__ __forceinline__ void put(uint32_t i, K k, uint32_t v) {
+    if constexpr (PAIR) {
+      reinterpret_cast<uint2 *>(raw)[i] = make_uint2((uint32_t)k, v);
+    } else {
+      reinterpret_cast<K *>(raw)[i] = k;
+      raw[N * (sizeof(K) / 4) + i] = v;
+    }
+  }
+  __device__ __forceinline__ void get(uint32_t i, K &k, uint32_t &v) const {
+    if constexpr (PAIR) {
+      const uint2 e = reinterpret_cast<const uint2 *>(raw)[i];
+      k = (K)e.x;
+      v = e.y;
+    } else {
+      k = reinterpret_cast<const K *>(raw)[i];
+      v = raw[N * (sizeof(K) / 4) + i];
+    }
+  }
+  __device__ __forceinline__ K key(uint32_t i) const {
+    if constexpr (PAIR) return (K)raw[2 * i];
+    else return reinterpret_cast<const K *>(raw)[i];
+  }
 };
 
 // Reduce-then-scan pass, part 3: each workgroup ranks its tile of TPB * ITEMS keys stably in
@@ -355,8 +380,11 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
   K key[ITEMS];
   uint32_t val[ITEMS], rank[ITEMS];
   bool ok[ITEMS];
-  // the digit total first: vmcnt retires in issue order, so the scan below waits for it alone
+  // the digit total (and in small tiles this tile's row offset) first: vmcnt retires in issue
+  // order, so the scans below wait for them alone
+  constexpr bool SMALL = ITEMS <= 8;
   const uint32_t hval = rowtot[min(tid, R - 1)];
+  const uint32_t oval = SMALL ? offs[(size_t)min(tid, R - 1) * nblocks + t] : 0u;
   {  // (indices clamped into [0, n): no per-element branch, so all 2 x ITEMS loads are in
      // flight together; the validity mask is applied once they are consumed)
     const long long sg = (long long)t * TPB * ITEMS + (long long)wave * (ITEMS * 64);
@@ -369,9 +397,11 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
   }
 #pragma unroll
   for (int w = 0; w < 4; ++w) sm.wcnt[w][tid] = 0;
-  {  // digit bases: exclusive scan of the digit row totals
+  uint32_t hs;  // digit base: exclusive scan of the digit row totals (thread tid: digit tid)
+  {
     uint32_t h = tid < R ? hval : 0u, tot;
-    sm.hscan[tid] = block_exclusive_scan<TPB>(h, tot, sm.scan_tmp);  // contains barriers
+    hs = block_exclusive_scan<TPB>(h, tot, sm.scan_tmp);  // contains barriers
+    if (!SMALL) sm.hscan[tid] = hs;  // (registers are tight with 16 keys per thread)
     if (n_out && blockIdx.x == 0 && tid == 0) *n_out = tot;
   }
   const long long base = (long long)t * TPB * ITEMS;
@@ -408,34 +438,33 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     }
   }
   __syncthreads();
-  uint32_t local_count = 0;
   {
-    uint32_t s = 0;
+    // digit tid's column: the waves' exclusive prefix, then the tile's exclusive digit offset
+    // added in place, so a key's tile position is wcnt[wave][digit] + its rank (one LDS read)
+    uint32_t cw[4], s = 0;
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
-      uint32_t c = sm.wcnt[w][tid];
-      sm.wcnt[w][tid] = s;
-      s += c;
+      cw[w] = s;
+      s += sm.wcnt[w][tid];
     }
-    local_count = s;  // digit tid's count in this tile (0 for tid >= R)
-  }
-  {
     uint32_t tot;
-    sm.loc_off[tid] = block_exclusive_scan<TPB>(local_count, tot, sm.scan_tmp);
-    if (tid == 0) sm.tile_n = tot;
-  }
-  __syncthreads();  // loc_off[d] is read by every thread below
-  // stable local sort into LDS
+    const uint32_t lo = block_exclusive_scan<TPB>(s, tot, sm.scan_tmp);  // (barriers)
 #pragma unroll
-  for (int r = 0; r < ITEMS; ++r) {
-    if (ok[r]) {
-      const uint32_t d = (uint32_t)(key[r] >> shift) & dmask;
-      const uint32_t lp = sm.loc_off[d] + sm.wcnt[wave][d] + rank[r];
-      sm.keys[lp] = key[r];
-      sm.vals[lp] = val[r];
+    for (int w = 0; w < 4; ++w) sm.wcnt[w][tid] = lo + cw[w];
+    if (SMALL && tid < R) sm.gofs[tid] = hs + oval - lo;
+    if (tid == 0) sm.tile_n = tot;
+    __syncthreads();  // every column is read below
+    // stable local sort into LDS
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) {
+      if (ok[r]) {
+        const uint32_t d = (uint32_t)(key[r] >> shift) & dmask;
+        sm.put(sm.wcnt[wave][d] + rank[r], key[r], val[r]);
+      }
     }
+    // large tiles: the row offset's load overlaps the scatter
+    if (!SMALL && tid < R) sm.gofs[tid] = sm.hscan[tid] + offs[(size_t)tid * nblocks + t] - lo;
   }
-  if (tid < R) sm.gofs[tid] = sm.hscan[tid] + offs[(size_t)tid * nblocks + t] - sm.loc_off[tid];
   __syncthreads();
   const long long cnt = sm.tile_n;
   if (bins) {
@@ -448,12 +477,26 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
 #pragma unroll
     for (int r = 0; r < ITEMS; ++r) {
       const int i = r * TPB + tid;
+      K k = (K)0;
+      uint32_t v = 0;
+      if (i < cnt) sm.get(i, k, v);
+      K kp, kn;
+      if constexpr (OsSmem<K, ITEMS>::PAIR) {
+        // the neighbours' keys from the adjacent lanes (a strided LDS read of the interleaved
+        // pairs would conflict); a wave's first and last lane read theirs from LDS
+        kp = __shfl_up(k, 1, 64);
+        kn = __shfl_down(k, 1, 64);
+        if (lane == 0 && i > 0 && i < cnt) kp = sm.key(i - 1);
+        if (lane == 63 && i + 1 < cnt) kn = sm.key(i + 1);
+      } else {
+        kp = i > 0 && i < cnt ? sm.key(i - 1) : k;
+        kn = i + 1 < cnt ? sm.key(i + 1) : k;
+      }
       if (i < cnt) {
-        const K k = sm.keys[i];
         const uint32_t pos = sm.gofs[(uint32_t)(k >> shift) & dmask] + (uint32_t)i;
-        vout[pos] = sm.vals[i];
-        if (i == 0 || sm.keys[i - 1] != k) atomicMax(&bins[2 * (size_t)k], (int32_t)(n - pos));
-        if (i == cnt - 1 || sm.keys[i + 1] != k) atomicMax(&bins[2 * (size_t)k + 1], (int32_t)pos + 1);
+        vout[pos] = v;
+        if (i == 0 || kp != k) atomicMax(&bins[2 * (size_t)k], (int32_t)(n - pos));
+        if (i == cnt - 1 || kn != k) atomicMax(&bins[2 * (size_t)k + 1], (int32_t)pos + 1);
       }
     }
   } else {
@@ -461,11 +504,12 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     for (int r = 0; r < ITEMS; ++r) {
       const int i = r * TPB + tid;
       if (i < cnt) {
-        const K k = sm.keys[i];
-        const uint32_t d = (uint32_t)(k >> shift) & dmask;
-        const uint32_t pos = sm.gofs[d] + (uint32_t)i;
+        K k;
+        uint32_t v;
+        sm.get(i, k, v);
+        const uint32_t pos = sm.gofs[(uint32_t)(k >> shift) & dmask] + (uint32_t)i;
         if (kout) kout[pos] = k;  // null: only the values are wanted (compacted depth sort)
-        vout[pos] = sm.vals[i];
+        vout[pos] = v;
       }
     }
   }

@@ -43,6 +43,7 @@ constexpr float ALPHA_MIN = 1.f / 255.f;
 // The backward's record atomics use 32-bit element offsets (id * REC + slot < 2^31).
 constexpr int MAX_BWD_POINTS = 1 << 27;
 constexpr int REC = 16;  // floats per gradient record: x y a b c r g b o + pad = 64 B
+constexpr int SPLIT_WAVES = 4;  // walk-table entries per tile (list-split plan; split_work_kernel)
 
 // Deterministic backward (gsplat_set_deterministic): every wave's per-Gaussian totals
 // (reduce18 / reduce9: a fixed reduction order, so run-independent) are added as exact
@@ -524,7 +525,8 @@ __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
     float *__restrict__ final_Ts, int *__restrict__ final_idx,
     const float *__restrict__ depths = nullptr, float *__restrict__ out_depth = nullptr,
     float4 *__restrict__ zero = nullptr,
-    long long zero_n = 0, const int *__restrict__ zero_radii = nullptr) {
+    long long zero_n = 0, const int *__restrict__ zero_radii = nullptr,
+    int *__restrict__ tile_last = nullptr) {
   // Side job: clear a buffer (the fused path's gradient records) with the memory bandwidth the
   // VALU-bound blend leaves idle -- a grid-stride sweep of coalesced 16-B stores, issued by each
   // wave as it finishes (issued first, the blend's first load wait would also wait for them:
@@ -537,7 +539,14 @@ __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
   };
   const WaveLog wlog;
   const WaveRect R = wave_rect<PXL, COLS>(tbx, tby, H, W);
+  // tile_last (the list-split plan's walk table, see split_work_kernel): per wave of a tile,
+  // the largest final index of its pixels (-1: none in the image)
+  constexpr int WPT = (GS_BLOCK / COLS) * (GS_BLOCK / ((64 / COLS) * PXL));
+  static_assert(WPT == SPLIT_WAVES, "one walk-table entry per wave of a tile");
+  const int wt = (threadIdx.x >> 6) % WPT;
   if (!R.live) {  // wave-uniform
+    if (tile_last && R.tile < tbx * tby && (threadIdx.x & 63) == 0)
+      tile_last[WPT * R.tile + wt] = -1;
     clear_side_job();
     return;
   }
@@ -652,6 +661,14 @@ __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
       out_img[3 * pix + 2] = cb[k] + T[k] * bg2;
       if (DEPTH) out_depth[pix] = cd[k] + T[k] * 0.f;  // the depth render's zero background
     }
+  }
+  if (tile_last) {
+    int m = -1;
+#pragma unroll
+    for (int k = 0; k < PXL; ++k)
+      if (i0 + LROWS * k < H && j < W) m = max(m, cur[k]);
+    m = wave_max_int(m);
+    if (lane == 0) tile_last[WPT * tile + wt] = m;
   }
   if constexpr (CNT) pair_count_flush(3, c_slots, c_live, c_valid);
   wlog.done(tile);
@@ -1073,28 +1090,26 @@ __global__ __launch_bounds__(256) void raster_bwd8_kernel(
 }
 
 // ---- list-split plan of the backward (SPLIT kernels) -------------------------------------
-// split_work_kernel (one workgroup per tile): the tile's backward walk length -- list positions
-// from range.x up to the last one any of its pixels composites (max final_idx; 0 when no pixel
-// composites anything: the tile has no backward work at all).
+// The walk table: per tile, 4 entries (one per wave of its pixels) holding the largest final
+// index of those pixels (-1 when none lies in the image).  The forward fills it as its waves
+// finish (raster_fwd3u_kernel's tile_last) when given the plan; otherwise split_work_kernel
+// (one workgroup per tile, from final_idx) does.  The tile's backward walk covers list positions
+// range.x .. min(max of the 4, range.y - 1): none when that max lies before range.x (no pixel
+// composited anything: final_idx 0 outside the list).
 __global__ __launch_bounds__(256) void split_work_kernel(int tbx, int tby, int H, int W,
-                                                         const int2 *__restrict__ bins,
                                                          const int *__restrict__ final_idx,
                                                          int *__restrict__ work) {
   const int t = blockIdx.x;
   const int i = (t / tbx) * GS_BLOCK + (threadIdx.x >> 4), j = (t % tbx) * GS_BLOCK + (threadIdx.x & 15);
-  const int2 r = bins[t];
   int m = -1;
   if (i < H && j < W) m = final_idx[i * W + j];
-  // a pixel that composited nothing has final_idx 0: count it only when 0 lies in the list
-  if (m < r.x) m = -1;
   m = wave_max_int(m);
-  __shared__ int wm[4];
-  if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const int mm = max(max(wm[0], wm[1]), max(wm[2], wm[3]));
-    work[t] = mm < r.x ? 0 : min(mm, r.y - 1) - r.x + 1;
-  }
+  if ((threadIdx.x & 63) == 0) work[SPLIT_WAVES * t + (threadIdx.x >> 6)] = m;
+}
+__device__ __forceinline__ int split_walk_length(const int *__restrict__ work, int2 r, int t) {
+  const int *w = work + SPLIT_WAVES * t;
+  const int m = max(max(w[0], w[1]), max(w[2], w[3]));
+  return m < r.x ? 0 : min(m, r.y - 1) - r.x + 1;
 }
 
 // split_plan_kernel (one workgroup): the backward's work items, longest first.  A tile with
@@ -1116,6 +1131,7 @@ __device__ __forceinline__ int split_cost_bucket(int L, int k, int chunk, bool s
 }
 
 __global__ __launch_bounds__(1024) void split_plan_kernel(int T, int chunk,
+                                                          const int2 *__restrict__ bins,
                                                           const int *__restrict__ work,
                                                           int2 *__restrict__ items,
                                                           int *__restrict__ n_items) {
@@ -1124,7 +1140,7 @@ __global__ __launch_bounds__(1024) void split_plan_kernel(int T, int chunk,
   if (tid < 64) hist[tid] = 0;
   __syncthreads();
   for (int t = tid; t < T; t += 1024) {
-    const int L = work[t];
+    const int L = split_walk_length(work, bins[t], t);
     if (L <= 0) continue;
     const bool split = L > chunk;
     const int m = split ? (L + chunk - 1) / chunk : 1;
@@ -1144,7 +1160,7 @@ __global__ __launch_bounds__(1024) void split_plan_kernel(int T, int chunk,
   }
   __syncthreads();
   for (int t = tid; t < T; t += 1024) {
-    const int L = work[t];
+    const int L = split_walk_length(work, bins[t], t);
     if (L <= 0) continue;
     const bool split = L > chunk;
     const int m = split ? (L + chunk - 1) / chunk : 1;
@@ -1406,8 +1422,9 @@ using namespace gs;
   } while (0)
 
 // ---- list-split backward ------------------------------------------------------------------
-// Plan workspace (gsplat_rasterize_split_bytes): work[T] int, items[T + ceil(I/chunk)] int2,
-// n_items int, filled by split_work_kernel / split_plan_kernel at the start of the backward.
+// Plan workspace (gsplat_rasterize_split_bytes): the walk table work[4 T] int (filled by the
+// forward or split_work_kernel), items[T + ceil(I/chunk)] int2 and n_items int (filled by
+// split_plan_kernel at the start of the backward).
 int g_chunk_override = 0;  // gsplat_debug_set_chunk: 0 auto, > 0 forced, < 0 off
 constexpr double SPLIT_MEANS = 0.6;
 constexpr long long SPLIT_MAX_TILES = 12288;
@@ -1427,7 +1444,7 @@ static SplitWs carve_split_ws(void *base, long long T, long long I, int chunk) {
     off += (bytes + 255) & ~(size_t)255;
     return (char *)base + o;
   };
-  w.work = (int *)take((size_t)T * sizeof(int));
+  w.work = (int *)take((size_t)T * SPLIT_WAVES * sizeof(int));
   w.items = (int2 *)take((size_t)w.items_bound * sizeof(int2));
   w.n_items = (int *)take(sizeof(int));
   w.bytes = off;
@@ -1479,13 +1496,14 @@ static void launch_fwd(hipStream_t st, int tbx, int tby, int H, int W, const int
                        const int32_t *bins, const float *xys, const float *conics,
                        const float *colors, const float *opacity, const float *background,
                        float *out_img, float *final_Ts, int32_t *final_idx, const float *depths,
-                       float *out_depth, float4 *zero, long long zn, const int32_t *zero_radii) {
+                       float *out_depth, float4 *zero, long long zn, const int32_t *zero_radii,
+                       int *tile_last = nullptr) {
   const unsigned grid = cdiv((long long)tbx * tby, (tiles_per_block<1, 8>()));
 #define FWDK(CNT, PF)                                                                      \
   hipLaunchKernelGGL((raster_fwd3u_kernel<1, 8, DEPTH, CNT, PF>), dim3(grid), dim3(256), 0, st, \
                      tbx, tby, H, W, gids, (const int2 *)bins, (const float2 *)xys, conics,     \
                      colors, opacity, background, out_img, final_Ts, final_idx, depths,         \
-                     out_depth, zero, zn, zero_radii)
+                     out_depth, zero, zn, zero_radii, tile_last)
   const bool pf = pipelined_staging(tbx, tby);
   if (!DEPTH && g_pair_count_on) {
     if (pf) FWDK(true, true); else FWDK(true, false);
@@ -1613,16 +1631,18 @@ static void launch_bwd(hipStream_t st, int tbx, int tby, int H, int W, int n,
                        const float *conics, const float *colors, const float *opacity,
                        const float *background, const float *final_Ts, const int32_t *final_idx,
                        const float *v_output, const float *v_output_alpha, float alpha_max,
-                       float *rec, int chunk, const SplitWs *w, unsigned long long *det) {
+                       float *rec, int chunk, const SplitWs *w, unsigned long long *det,
+                       bool work_ready = false) {
   const long long slots = w ? w->items_bound : (long long)tbx * tby;
   const int2 *its = w ? w->items : nullptr;
   const int *ni = w ? w->n_items : nullptr;
   if (w) {
     const int T = tbx * tby;
-    hipLaunchKernelGGL(split_work_kernel, dim3(T), dim3(256), 0, st, tbx, tby, H, W,
-                       (const int2 *)bins, final_idx, w->work);
+    if (!work_ready)  // (the forward did not fill the walk table)
+      hipLaunchKernelGGL(split_work_kernel, dim3(T), dim3(256), 0, st, tbx, tby, H, W, final_idx,
+                         w->work);
     hipLaunchKernelGGL(split_plan_kernel, dim3(1), dim3(1024), 0, st, T, chunk,
-                       (const int *)w->work, w->items, w->n_items);
+                       (const int2 *)bins, (const int *)w->work, w->items, w->n_items);
   }
   const bool cnt = g_pair_count_on && !det;
   if (bwd_geometry(tbx, tby) == 1) {
@@ -1669,7 +1689,7 @@ static int backward_into_records(const char *who, hipStream_t st, int tbx, int t
                                  const float *final_Ts, const int32_t *final_idx,
                                  const float *v_output, const float *v_output_alpha,
                                  float alpha_max, float *rec, int64_t num_intersects, int chunk,
-                                 void *plan, size_t plan_bytes) {
+                                 void *plan, size_t plan_bytes, bool work_ready = false) {
   SplitWs w{};
   if (chunk > 0) {
     w = carve_split_ws(plan, (long long)tbx * tby, num_intersects, chunk);
@@ -1683,12 +1703,12 @@ static int backward_into_records(const char *who, hipStream_t st, int tbx, int t
     if (!lease.buf) return check_launch(who);
     launch_bwd(st, tbx, tby, H, W, n, gids, bins, xys, conics, colors, opacity, background,
                final_Ts, final_idx, v_output, v_output_alpha, alpha_max, rec, chunk,
-               chunk > 0 ? &w : nullptr, lease.buf);
+               chunk > 0 ? &w : nullptr, lease.buf, work_ready);
     lease.finish();
   } else {
     launch_bwd(st, tbx, tby, H, W, n, gids, bins, xys, conics, colors, opacity, background,
                final_Ts, final_idx, v_output, v_output_alpha, alpha_max, rec, chunk,
-               chunk > 0 ? &w : nullptr, nullptr);
+               chunk > 0 ? &w : nullptr, nullptr, work_ready);
   }
   return 0;
 }
@@ -1765,18 +1785,30 @@ extern "C" int gsplat_rasterize_forward_clearing(
     const int32_t *gaussian_ids_sorted, const int32_t *tile_bins, const float *xys,
     const float *conics, const float *colors, const float *opacity, const float *background,
     float *out_img, float *final_Ts, int32_t *final_idx, void *clear, size_t clear_bytes,
-    const int32_t *clear_radii, void *stream) {
+    const int32_t *clear_radii, int64_t num_intersects, int chunk, void *plan, size_t plan_bytes,
+    void *stream) {
   const char *who = "rasterize_forward_clearing";
   if (bad_frame(tile_bounds_x, tile_bounds_y, img_height, img_width) || clear_bytes % 16 ||
-      (clear_bytes && !clear) || (clear_radii && clear_bytes % 64)) {
-    set_error("%s: bad sizes (tiles=%dx%d H=%d W=%d clear=%zu)", who, tile_bounds_x,
-              tile_bounds_y, img_height, img_width, clear_bytes);
+      (clear_bytes && !clear) || (clear_radii && clear_bytes % 64) ||
+      (chunk > 0 && (chunk % 64 || num_intersects < 0))) {
+    set_error("%s: bad sizes (tiles=%dx%d H=%d W=%d clear=%zu chunk=%d)", who, tile_bounds_x,
+              tile_bounds_y, img_height, img_width, clear_bytes, chunk);
     return 1;
+  }
+  int *tile_last = nullptr;  // the list-split plan's walk table, filled by the blend's waves
+  if (chunk > 0) {
+    const SplitWs w =
+        carve_split_ws(plan, (long long)tile_bounds_x * tile_bounds_y, num_intersects, chunk);
+    if (!plan || plan_bytes < w.bytes) {
+      set_error("%s: split plan buffer %zu < %zu bytes", who, plan_bytes, w.bytes);
+      return 1;
+    }
+    tile_last = w.work;
   }
   launch_fwd<false>((hipStream_t)stream, tile_bounds_x, tile_bounds_y, img_height, img_width,
                     gaussian_ids_sorted, tile_bins, xys, conics, colors, opacity, background,
                     out_img, final_Ts, final_idx, nullptr, nullptr, (float4 *)clear,
-                    (long long)(clear_bytes / 16), clear_radii);
+                    (long long)(clear_bytes / 16), clear_radii, tile_last);
   return check_launch(who);
 }
 
@@ -1844,7 +1876,8 @@ extern "C" int gsplat_rasterize_backward_records(
     const float *conics, const float *colors, const float *opacity, const float *background,
     const float *final_Ts, const int32_t *final_idx, const float *v_output,
     const float *v_output_alpha, float alpha_max, int64_t num_intersects, int chunk,
-    void *plan, size_t plan_bytes, void *records, size_t records_bytes, void *stream) {
+    void *plan, size_t plan_bytes, int plan_filled, void *records, size_t records_bytes,
+    void *stream) {
   hipStream_t st = (hipStream_t)stream;
   const size_t need = gsplat_grad_records_bytes(num_points);
   if (bad_frame(tile_bounds_x, tile_bounds_y, img_height, img_width) || num_points < 0 ||
@@ -1861,7 +1894,7 @@ extern "C" int gsplat_rasterize_backward_records(
                             img_height, img_width, num_points, gaussian_ids_sorted, tile_bins, xys,
                             conics, colors, opacity, background, final_Ts, final_idx, v_output,
                             v_output_alpha, alpha_max, (float *)records, num_intersects, chunk,
-                            plan, plan_bytes))
+                            plan, plan_bytes, plan_filled != 0))
     return 1;
   return check_launch("rasterize_backward_records");
 }

@@ -102,7 +102,8 @@ class _FusedRender(Function):
                       # skip culled Gaussians' records when many are culled (real scenes);
                       # at ~all visible the radii loads cost more than the stores they save
                       P(radii) if rec is not None and last_num_visible(dev) < 0.9 * n else None,
-                      st)
+                      # the list-split plan's walk table, filled by the blend's waves
+                      num_intersects, chunk, P(plan), plan.numel() if plan is not None else 0, st)
         ctx.meta = (n, K, int(degrees_to_use), float(fx), float(fy), float(cx), float(cy), H, W,
                     tbx, tby, num_intersects, chunk)
         ctx.plan, ctx.rec = plan, rec
@@ -151,8 +152,8 @@ class _FusedRender(Function):
             _lib.call("gsplat_rasterize_backward_records", tbx, tby, H, W, n, P(gids), P(bins),
                       P(xys), P(conics), P(colors), P(opac), P(background), P(final_Ts),
                       P(final_idx), P(v_img), P(v_alpha), quirks.backward_alpha_clamp(), I, chunk,
-                      P(ctx.plan), ctx.plan.numel() if ctx.plan is not None else 0, P(rec),
-                      rec.numel(), st)
+                      P(ctx.plan), ctx.plan.numel() if ctx.plan is not None else 0,
+                      int(ctx.plan is not None), P(rec), rec.numel(), st)
         if ctx.adam is not None:
             # Adam inside the backward: parameters (and moments) updated in place, no gradients
             a = ctx.adam

@@ -391,7 +391,7 @@ class _RasterizeGaussians(Function):
                 _lib.call("gsplat_rasterize_forward_clearing", tbx, tby, H, W,
                           P(gaussian_ids_sorted), P(tile_bins), P(xys), P(conics), P(colors),
                           P(opacity), P(background), P(out_img), P(final_Ts), P(final_idx),
-                          P(rec), rec.numel(), None, _lib.stream(dev))
+                          P(rec), rec.numel(), None, 0, 0, None, 0, _lib.stream(dev))
                 ctx.rec = rec
             else:
                 out_img, final_Ts, final_idx = ops().raster_fwd(
@@ -460,7 +460,7 @@ class _RasterizeGaussians(Function):
                           P(gaussian_ids_sorted), P(tile_bins), P(xys), P(conics), P(colors),
                           P(opacity), P(background), P(final_Ts), P(final_idx), P(v_out_img),
                           P(v_out_alpha), quirks.backward_alpha_clamp(), ctx.num_intersects,
-                          chunk, P(plan), plan_bytes, P(rec), rec.numel(), st)
+                          chunk, P(plan), plan_bytes, 0, P(rec), rec.numel(), st)
                 _lib.call("gsplat_grad_records_split", num_points, P(rec), rec.numel(),
                           P(conics), P(opacity), P(v_xy), P(v_conic), P(v_colors), P(v_opacity),
                           st)

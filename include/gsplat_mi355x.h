@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define GSPLAT_MI355X_ABI_VERSION 11
+#define GSPLAT_MI355X_ABI_VERSION 12
 
 int gsplat_abi_version(void);
 const char *gsplat_last_error(void);
@@ -274,14 +274,18 @@ int gsplat_rasterize_backward_chunked(
  * fused training render hands it the per-Gaussian gradient records, which the blend kernel
  * zeroes with the memory bandwidth its VALU-bound loop leaves idle (instead of the preprocess
  * kernel spending ~18 us on it).  With clear_radii != NULL the buffer is 64-B records and
- * record g is cleared only when clear_radii[g] > 0 (the backward touches no other).  Outputs
- * equal gsplat_rasterize_forward's. */
+ * record g is cleared only when clear_radii[g] > 0 (the backward touches no other).  With
+ * chunk > 0 (gsplat_rasterize_chunk_size) and a plan buffer of gsplat_rasterize_split_bytes, the
+ * blend's waves also fill the plan's walk table (each wave's largest final index), so the list-
+ * split backward given that plan and plan_filled = 1 skips the kernel that derives it from
+ * final_idx.  chunk <= 0: no plan (may be NULL).  Outputs equal gsplat_rasterize_forward's. */
 int gsplat_rasterize_forward_clearing(
     int tile_bounds_x, int tile_bounds_y, int img_height, int img_width,
     const int32_t *gaussian_ids_sorted, const int32_t *tile_bins, const float *xys,
     const float *conics, const float *colors, const float *opacity, const float *background,
     float *out_img, float *final_Ts, int32_t *final_idx, void *clear, size_t clear_bytes,
-    const int32_t *clear_radii, void *stream);
+    const int32_t *clear_radii, int64_t num_intersects, int chunk, void *plan,
+    size_t plan_bytes, void *stream);
 /* Debug: force the list-split chunk (> 0, rounded up to 64), disable it (< 0) or restore
  * the automatic choice (0). */
 int gsplat_debug_set_chunk(int chunk);
@@ -370,7 +374,8 @@ int gsplat_fused_preprocess_backward_adam(
  * 5-7 v_colors, 8 sum w (= v_opacity), 9-15 unused; gsplat's gradients follow per Gaussian as
  * v_xy = -o (a Sx + b Sy, b Sx + c Sy), v_conic = -o/2 (Sxx, Sxy, Syy) (conic = (a, b, c),
  * o = opacity; v_conic.y doubled without GSPLAT_QUIRK_CONIC_HALF).  gsplat_rasterize_backward_records is gsplat_rasterize_backward (C = 3, default
- * variant, list-split when chunk > 0 as in the _chunked entry) without the zero fill and
+ * variant, list-split when chunk > 0 as in the _chunked entry; plan_filled = 1: the plan's walk
+ * table came from gsplat_rasterize_forward_clearing with the same plan) without the zero fill and
  * without the split into v_xy / v_conic / v_colors / v_opacity -- the records must be zeroed
  * by the caller (gsplat_fused_preprocess_forward does it for the visible Gaussians, the
  * only ones the kernel touches) and are read
@@ -382,7 +387,8 @@ int gsplat_rasterize_backward_records(
     const float *conics, const float *colors, const float *opacity, const float *background,
     const float *final_Ts, const int32_t *final_idx, const float *v_output,
     const float *v_output_alpha, float alpha_max, int64_t num_intersects, int chunk,
-    void *plan, size_t plan_bytes, void *records, size_t records_bytes, void *stream);
+    void *plan, size_t plan_bytes, int plan_filled, void *records, size_t records_bytes,
+    void *stream);
 /* The records -> gsplat's four rasterize gradients (v_xy [N,2], v_conic [N,3] in gsplat's
  * convention (GSPLAT_QUIRK_CONIC_HALF), v_colors [N,3], v_opacity [N]) -- the tail of
  * gsplat_rasterize_backward, for a caller that cleared the records in the forward blend

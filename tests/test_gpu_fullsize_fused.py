@@ -83,7 +83,7 @@ class FusedRun:
         _lib.call("gsplat_rasterize_forward_clearing", self.tb[0], self.tb[1], H, W, P(self.gids),
                   P(self.bins), P(self.xys), P(self.conics), P(self.colors), P(self.opac),
                   P(self.bg), P(img), P(fT), P(fi), P(self.rec), self.rec.numel(), P(vis_only),
-                  st)
+                  self.I, self.chunk, P(self.plan), self.plan.numel() if self.chunk > 0 else 0, st)
         self.fT, self.fi = fT, fi
         return img, fT, fi
 
@@ -97,8 +97,9 @@ class FusedRun:
                   self.n, P(self.gids), P(self.bins), P(self.xys), P(self.conics),
                   P(self.colors), P(self.opac), P(self.bg), P(fT), P(fi),
                   P(self.v_img), P(self.v_alpha), quirks.backward_alpha_clamp(), self.I,
-                  self.chunk, P(self.plan), self.plan.numel() if self.chunk > 0 else 0, P(self.rec),
-                  self.rec.numel(), st)
+                  self.chunk, P(self.plan), self.plan.numel() if self.chunk > 0 else 0,
+                  # the walk table the forward filled: only for its own final state
+                  int(final_idx is None and self.chunk > 0), P(self.rec), self.rec.numel(), st)
 
     def raster_grads(self):
         """The records (pixel moments) -> gsplat's four raster gradients (the split kernel)."""

@@ -159,7 +159,7 @@ def test_forward_clearing_equals_forward_and_clears_records(gpu, case):
                              dtype=torch.uint8)
             _lib.call("gsplat_rasterize_forward_clearing", tb[0], tb[1], H, W, P(gids), P(bins),
                       P(xys), P(conics), P(colors), P(opac), P(bg), P(img), P(fT), P(fi),
-                      P(rec), rec.numel(), None, st)
+                      P(rec), rec.numel(), None, 0, 0, None, 0, st)
             torch.cuda.synchronize()
             assert int(rec.count_nonzero()) == 0
             # visible-only clearing: culled Gaussians' records keep their bytes
@@ -167,7 +167,7 @@ def test_forward_clearing_equals_forward_and_clears_records(gpu, case):
             img2 = torch.empty_like(img)
             _lib.call("gsplat_rasterize_forward_clearing", tb[0], tb[1], H, W, P(gids), P(bins),
                       P(xys), P(conics), P(colors), P(opac), P(bg), P(img2), P(fT), P(fi),
-                      P(rec), rec.numel(), P(radii), st)
+                      P(rec), rec.numel(), P(radii), 0, 0, None, 0, st)
             r = rec.view(n, 64)
             vis = radii > 0
             assert (~vis).any() or n == int(vis.sum())
@@ -182,7 +182,65 @@ def test_forward_clearing_equals_forward_and_clears_records(gpu, case):
     with pytest.raises(RuntimeError):  # clear size must be a multiple of 16 bytes
         _lib.call("gsplat_rasterize_forward_clearing", tb[0], tb[1], H, W, P(gids), P(bins),
                   P(xys), P(conics), P(colors), P(opac), P(bg), P(img), P(fT), P(fi),
-                  P(rec), 24, None, st)
+                  P(rec), 24, None, 0, 0, None, 0, st)
+
+
+@pytest.mark.parametrize("case", [CASES[0], CASES[1], CASES[6]])
+def test_forward_filled_split_plan(gpu, case):
+    """The list-split plan's walk table filled by the clearing forward's waves
+    (gsplat_rasterize_forward_clearing with a plan) gives every tile the same walk as the
+    backward's own split_work_kernel (per-tile maxima equal), and the record backward given
+    plan_filled = 1 is bit-identical to plan_filled = 0 in the deterministic mode."""
+    from gaussctrl_exp_amd.project_gaussians import project_gaussians
+    from gaussctrl_exp_amd.rasterize import bin_gaussians
+    sc, cam = _scene_cam(case)
+    n, W, H = case[:3]
+    d, c = sc.to(gpu), cam.to(gpu)
+    tb = cam.tile_bounds
+    T = tb[0] * tb[1]
+    with torch.no_grad():
+        xys, depths, radii, conics, nth, _ = project_gaussians(
+            d.means, torch.exp(d.scales), 1, d.quats / d.quats.norm(dim=-1, keepdim=True),
+            *c.project_args())
+    I, gids, bins = bin_gaussians(xys, depths, radii, nth, H, W)
+    assert I > 0
+    g = torch.Generator().manual_seed(3)
+    colors = torch.rand(n, 3, generator=g).to(gpu)
+    opac = torch.rand(n, generator=g).to(gpu)
+    bg = torch.tensor([0.2, 0.4, 0.6], device=gpu)
+    v_img = torch.randn(H, W, 3, generator=g).to(gpu)
+    v_a = torch.randn(H, W, generator=g).to(gpu)
+    P, st = _lib.ptr, _lib.stream(gpu)
+    chunk = 64  # forced: every case splits
+    plan = torch.full((_lib.query("gsplat_rasterize_split_bytes", tb[0], tb[1], I, chunk),), 0xAB,
+                      device=gpu, dtype=torch.uint8)
+    rec_bytes = _lib.query("gsplat_grad_records_bytes", n)
+    img = torch.empty(H, W, 3, device=gpu)
+    fT = torch.empty(H, W, device=gpu)
+    fi = torch.empty(H, W, device=gpu, dtype=torch.int32)
+    prev = _lib.set_deterministic(True)
+    try:
+        recs, tables = [], []
+        for filled in (1, 0):
+            rec = torch.full((rec_bytes,), 0x7F, device=gpu, dtype=torch.uint8)
+            plan.fill_(0xAB)
+            _lib.call("gsplat_rasterize_forward_clearing", tb[0], tb[1], H, W, P(gids), P(bins),
+                      P(xys), P(conics), P(colors), P(opac), P(bg), P(img), P(fT), P(fi),
+                      P(rec), rec.numel(), None, I, chunk, P(plan), plan.numel(), st)
+            if not filled:
+                plan.fill_(0xAB)  # the backward derives the table itself
+            _lib.call("gsplat_rasterize_backward_records", tb[0], tb[1], H, W, n, P(gids),
+                      P(bins), P(xys), P(conics), P(colors), P(opac), P(bg), P(fT), P(fi),
+                      P(v_img), P(v_a), 0.99, I, chunk, P(plan), plan.numel(), filled, P(rec),
+                      rec.numel(), st)
+            torch.cuda.synchronize()
+            tables.append(plan[:16 * T].view(torch.int32).view(T, 4).max(dim=1).values.clone())
+            recs.append(rec.clone())
+    finally:
+        _lib.set_deterministic(prev)
+    assert torch.equal(tables[0], tables[1])
+    assert torch.equal(recs[0], recs[1])
+    assert int((tables[0] >= 0).sum()) > 0
 
 
 @pytest.mark.parametrize("case", [CASES[0], CASES[2], CASES[3], CASES[6]])

@@ -38,7 +38,7 @@ for v in (A, B):
     rec = torch.zeros(_lib.query("gsplat_grad_records_bytes", N), dtype=torch.uint8, device=dev)
     _lib.call("gsplat_rasterize_backward_records", tb[0], tb[1], H, W, N, P(gids), P(bins),
               P(xys), P(conics), P(colors), P(opac), P(bg), P(fT), P(fi), P(v_out), P(v_a),
-              0.99, I, 0, None, 0, P(rec), rec.numel(), st)
+              0.99, I, 0, None, 0, 0, P(rec), rec.numel(), st)
     torch.cuda.synchronize()
     recs[v] = rec.view(torch.float32).view(N, 16)[:, :9].cpu().numpy().astype(np.float64)
 _lib.call("gsplat_debug_set_raster_variant", 1, 0, 0)
