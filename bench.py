@@ -107,17 +107,23 @@ def algorithmic_bytes(N, I, P, T, K, nvis):
         # records twice (bucket counts, placement: 32 N), ids placed (4 I), then per tile the ids
         # and their depth keys read and the sorted ids written (12 I), the tile table (8 T)
         bin_count, bin_emit = 20 * N, 32 * N + 16 * I + 8 * T
+        emit_head = 32 * N + 4 * I  # pre-launched: counts, scan, placement
     else:
         # depth keys (44 N) + 4 radix passes (count 4 N, scatter 16 N each) + the depth-ordered
         # record gather (36 N) + the allotment scan (8 N); keyed: without the key pass
         # emission (records in, (tile, id) pairs out) + per tile-digit pass 20 I + bin edges
         bin_count, bin_emit = 168 * N, 20 * N + 8 * I + 20 * tile_passes * I + 4 * I + 8 * T
+        # pre-launched: the emission (none when the first tile pass is generated, I >= 2^24)
+        emit_head = 0 if I >= (1 << 24) else 20 * N + 8 * I
     return {
         "gsplat_project_gaussians_forward": 96 * N,
         "gsplat_compute_sh_forward": (24 + 12 * K) * N,
         "gsplat_bin_count": bin_count,
         "gsplat_bin_count_keyed": bin_count if bucket else bin_count - 44 * N,
         "gsplat_bin_emit": bin_emit,
+        # the emission split around the host's read of I (rasterize.bin_gaussians)
+        "gsplat_bin_emit_prelaunch": emit_head,
+        "gsplat_bin_emit_finish": bin_emit - emit_head,
         "gsplat_rasterize_forward": 40 * I + 20 * P,
         "gsplat_rasterize_backward": 40 * I + 24 * P + 36 * N,
         "gsplat_compute_sh_backward": (24 + 12 * K) * N,

@@ -31,8 +31,12 @@ for f in files:
 # kernel (emit / tc_first / ep0_count, or the tile buckets' bk_count) starts bin_emit,
 # bins_decode (the buckets: the long-list bk_sort) ends it -- and average the per-call sums of
 # every counter over the calls seen.
-EMIT_START = ("emit_kernel", "tc_first_kernel", "ep0_count_kernel", "bk_count_kernel")
+# the emission's pre-launched head (gsplat_bin_emit_prelaunch), then the rest
+# (gsplat_bin_emit_finish; all of it when the first tile pass is generated)
+EMIT_HEAD = ("emit_kernel", "bk_count_kernel", "bk_scan_kernel", "bk_place_kernel")
+EMIT_START = EMIT_HEAD + ("tc_first_kernel", "ep0_count_kernel")
 EMIT_END = ("bins_decode_kernel", "bk_sort_kernel<1024")
+PRE, FIN = "gsplat_bin_emit_prelaunch", "gsplat_bin_emit_finish"
 entries = collections.defaultdict(lambda: collections.defaultdict(float))
 calls = collections.defaultdict(set)
 for f in files:
@@ -51,7 +55,9 @@ for f in files:
             state, seg = "gsplat_bin_count_keyed", seg + 1
             continue
         if state == "gsplat_bin_count_keyed" and any(s in k for s in EMIT_START):
-            state = "gsplat_bin_emit"
+            state = PRE if any(s in k for s in EMIT_HEAD) else FIN
+        elif state == PRE and not any(s in k for s in EMIT_HEAD):
+            state = FIN
         if state is None:
             continue
         if not k.startswith("gs::") and not k.startswith("void gs::"):
@@ -59,7 +65,7 @@ for f in files:
         for c, v in disp[d].items():
             entries[state][(os.path.dirname(f), c)] += v
         calls[state].add((os.path.dirname(f), seg))
-        if state == "gsplat_bin_emit" and any(s in k for s in EMIT_END):
+        if state == FIN and any(s in k for s in EMIT_END):
             state = None
 entry_rows = {}
 for e, d in entries.items():
