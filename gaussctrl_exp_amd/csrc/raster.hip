@@ -153,6 +153,8 @@ int g_fwd_pxl = FWD_PXL, g_bwd_pxl = BWD_PXL, g_bwd_flags = 0;
 // in the 8x8 backward measured no gain: c3 0.132 -> 0.134 ms, c2 0.123 -> 0.125 ms; its
 // EAGER staging already overlaps the data loads, and its blend per batch is longer.)
 int g_pf_mode = -1;
+// the forward's culls handed to the list-split backward (KeepSrc); debug flag bit 30 turns it off
+bool g_keep_bits = true;
 static bool pipelined_staging(int tbx, int tby) {
   return g_pf_mode < 0 ? (long long)tbx * tby < 3584 : g_pf_mode > 0;
 }
@@ -167,6 +169,11 @@ struct __attribute__((aligned(16))) GStage {
 };
 
 typedef float f2 __attribute__((ext_vector_type(2)));
+
+// Staged record t of a wave's LDS slice.  The slice's base is made wave-uniform where it is
+// taken (readfirstlane of the wave index), so a blend iteration forms the address in SALU and
+// one v_mov instead of a 64-bit vector multiply-add (v_mad_u64_u32) per read.
+__device__ __forceinline__ GStage stage_at(const GStage *stage, int t) { return stage[t]; }
 
 // sigma = 0.5 (a dx^2 + c dy^2) + b dx dy, evaluated as fma(fma(c/2, dy, b dx), dy, a/2 dx^2)
 // with explicit fmas.  EVERY blend kernel below (scalar or packed, forward or backward) uses
@@ -384,6 +391,144 @@ struct StagePipe {
   RawG r_next;
 };
 
+// ---- keep bits: the forward's culls handed to the backward --------------------------------
+// Every forward wave (one 8x8 block of a tile) records the ballot of its cull per 64-position
+// batch: word k of block slot wt of tile t (positions range.x + 64 k .. + 63, bit m for
+// range.x + 64 k + m) lives at kbits[wt * kbw + (range.x >> 6) + t + k] -- collision-free
+// between tiles (a tile's last word index is below the next tile's first), kbw = I / 64 + T + 2
+// words per block slot.  Words are written for the batches the wave staged, which include the
+// one holding its pixels' largest final index (tile_last), so a backward wave reads a block's
+// words only up to that batch.  The cull is exactness-preserving (touches_rect), so the union
+// of a strip's two blocks' bits holds every Gaussian with a valid pair in the strip, and a
+// Gaussian added by the union is invalid at every pixel it was not kept for: the backward's
+// per-pixel sums are bit-identical to the ones its own cull gives.
+//
+// What it buys the backward: it visits only kept positions, 64 per staging round (the headline
+// keeps ~1 in 6 positions per strip), instead of staging and culling every position of its walk
+// 64 at a time -- a wave's staging round trips drop ~5x and the cull's VALU work is gone.
+struct KeepSrc {
+  const unsigned long long *w0, *w1;  // the two blocks' words of this tile (w1 may alias w0)
+  int kmax0, kmax1;                   // last valid word index per block (-1: none)
+  int x;                              // range.x (word 0's first position)
+};
+__device__ __forceinline__ KeepSrc keep_src(const unsigned long long *__restrict__ kbits,
+                                            long long kbw, const int *__restrict__ tile_last,
+                                            int tile, int2 range, int wt0, int wt1) {
+  KeepSrc S;
+  const long long base = (long long)(range.x >> 6) + tile;
+  S.w0 = kbits + wt0 * kbw + base;
+  S.w1 = kbits + wt1 * kbw + base;
+  const int l0 = tile_last[SPLIT_WAVES * tile + wt0], l1 = tile_last[SPLIT_WAVES * tile + wt1];
+  S.kmax0 = l0 >= range.x ? (l0 - range.x) >> 6 : -1;
+  S.kmax1 = l1 >= range.x ? (l1 - range.x) >> 6 : -1;
+  S.x = range.x;
+  return S;
+}
+// The kept positions tp - m (m = 0..63) as bit m (descending positions), positions below
+// `bottom` cleared.
+__device__ __forceinline__ unsigned long long keep_word_desc(const KeepSrc &S, int tp,
+                                                             int bottom) {
+  const int lo = tp - 63;
+  const int rel = lo - S.x;
+  const int k0 = rel >> 6, s = rel & 63;  // (arithmetic shift: floor)
+  unsigned long long a0 = 0, a1 = 0;
+  if (k0 >= 0 && k0 <= S.kmax0) a0 = S.w0[k0];
+  if (k0 >= 0 && k0 <= S.kmax1) a0 |= S.w1[k0];
+  if (k0 + 1 >= 0 && k0 + 1 <= S.kmax0) a1 = S.w0[k0 + 1];
+  if (k0 + 1 >= 0 && k0 + 1 <= S.kmax1) a1 |= S.w1[k0 + 1];
+  unsigned long long asc = s ? (a0 >> s) | (a1 << (64 - s)) : a0;  // bit j: position lo + j
+  const int cut = bottom - lo;
+  if (cut > 0) asc = cut >= 64 ? 0ull : asc & (~0ull << cut);
+  return __builtin_bitreverse64(asc);
+}
+// Bit index of the n-th (0-based) lowest set bit of w (n < popcount(w)).
+__device__ __forceinline__ int select_set_bit(unsigned long long w, int n) {
+  uint32_t x = (uint32_t)w;
+  int pos = 0, c = __popc(x);
+  if (n >= c) {
+    n -= c;
+    x = (uint32_t)(w >> 32);
+    pos = 32;
+  }
+#pragma unroll
+  for (int width = 16; width >= 1; width >>= 1) {
+    c = __popc(x & ((1u << width) - 1u));
+    if (n >= c) {
+      n -= c;
+      x >>= width;
+      pos += width;
+    }
+  }
+  return pos;
+}
+__device__ __forceinline__ int wave_incl_scan(int v) {
+  const int lane = __lane_id();
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int u = __shfl_up(v, o, 64);
+    if (lane >= o) v += u;
+  }
+  return v;
+}
+// Walk the kept positions from `top` down to `bottom` (inclusive), 64 per round: each lane
+// finds its round slot's position (the owning batch by a binary search over the batches'
+// prefix counts, then the bit within the batch word), `stage_one(pos, s)` fills its GStage,
+// the round's records land in stage[0 .. n) in descending position order and `blend(n)` runs
+// over them.  Windows of 64 batches (4,096 positions) per mask load.
+template <typename StageF, typename BlendF>
+__device__ __forceinline__ void walk_kept(const KeepSrc &S, int top, int bottom, GStage *stage,
+                                          StageF &&stage_one, BlendF &&blend) {
+  const int lane = __lane_id();
+  for (int wtop = top; wtop >= bottom; wtop -= 4096) {
+    const int tp = wtop - 64 * lane;
+    const unsigned long long dw = tp >= bottom ? keep_word_desc(S, tp, bottom) : 0ull;
+    const int cnt = __popcll(dw);
+    const int incl = wave_incl_scan(cnt);
+    const int excl = incl - cnt;
+    const int total = __builtin_amdgcn_readlane(incl, 63);
+    for (int r = 0; r < total; r += 64) {
+      const int j = r + lane;
+      const bool valid = j < total;
+      int l = 0;
+#pragma unroll
+      for (int step = 32; step >= 1; step >>= 1) {
+        const int c = l + step;
+        if (__shfl(excl, c, 64) <= j) l = c;
+      }
+      const unsigned long long w = __shfl(dw, l, 64);
+      const int m = select_set_bit(w, j - __shfl(excl, l, 64));
+      GStage s;
+      if (valid) {
+        stage_one(wtop - 64 * l - m, s);
+        stage[lane] = s;
+      }
+      wave_lds_sync();
+      blend(min(64, total - r));
+      wave_lds_sync();
+    }
+  }
+}
+// stage_gaussian<true> without the cull (the forward's keep bits already decided it)
+__device__ __forceinline__ void stage_kept(int idx, const int *__restrict__ gids,
+                                           const float2 *__restrict__ xys,
+                                           const float *__restrict__ conics,
+                                           const float *__restrict__ colors,
+                                           const float *__restrict__ opacity, GStage &s) {
+  const int g = gids[idx];
+  const float2 xy = xys[g];
+  s.x = xy.x;
+  s.y = xy.y;
+  s.ha = 0.5f * conics[3 * g];
+  s.b = conics[3 * g + 1];
+  s.hc = 0.5f * conics[3 * g + 2];
+  s.o = opacity[g];
+  s.r = colors[3 * g];
+  s.g = colors[3 * g + 1];
+  s.bl = colors[3 * g + 2];
+  s.idx = idx;
+  s.id = g;
+}
+
 // A workgroup of 4 waves covers 4 / (waves per tile) tiles.  A wave owns a COLS-wide
 // rectangle of its tile: lanes map to (column lane % COLS, row lane / COLS), and each lane
 // holds PXL pixels spaced 64 / COLS rows apart.  COLS = 16 gives full-width strips, COLS = 8
@@ -526,7 +671,8 @@ __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
     const float *__restrict__ depths = nullptr, float *__restrict__ out_depth = nullptr,
     float4 *__restrict__ zero = nullptr,
     long long zero_n = 0, const int *__restrict__ zero_radii = nullptr,
-    int *__restrict__ tile_last = nullptr) {
+    int *__restrict__ tile_last = nullptr, unsigned long long *__restrict__ kbits = nullptr,
+    long long kbw = 0) {
   // Side job: clear a buffer (the fused path's gradient records) with the memory bandwidth the
   // VALU-bound blend leaves idle -- a grid-stride sweep of coalesced 16-B stores, issued by each
   // wave as it finishes (issued first, the blend's first load wait would also wait for them:
@@ -569,7 +715,7 @@ __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
     done[k] = !(i < H && j < W);
   }
   const int2 range = bins[tile];
-  GStage *stage = lds[wave];
+  GStage *stage = lds[__builtin_amdgcn_readfirstlane(wave)];  // (uniform: SGPR address arithmetic)
   unsigned c_slots = 0, c_live = 0, c_valid = 0;  // (CNT only)
   StagePipe pipe{};  // (PF: see RawG)
   if (PF && range.x < range.y) {
@@ -577,11 +723,18 @@ __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
     pipe.r_next = raw_load(pipe.g_next, xys, conics, colors, opacity);
     pipe.g_after = gids[min(range.x + 64 + lane, range.y - 1)];
   }
+  // the backward's keep bits (see KeepSrc): one word per staged batch, each stored when the
+  // next batch's loads go out (vmcnt counts stores too, so a store issued before the blend
+  // would hold the blend's first wait; issued with loads that are waited for anyway it is free)
+  const long long kb_base = wt * kbw + (long long)(range.x >> 6) + tile;
+  long long kb_at = -1;
+  unsigned long long kb_word = 0;
   for (int b = range.x; b < range.y; b += 64) {
     bool all_done = true;
 #pragma unroll
     for (int k = 0; k < PXL; ++k) all_done = all_done && done[k];
     if (__all(all_done)) break;
+    if (kbits && kb_at >= 0 && lane == 0) kbits[kb_at] = kb_word;
     const int idx = b + lane;
     GStage s;
     bool keep;
@@ -600,12 +753,14 @@ __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
     if (DEPTH && keep) s.d = depths[s.id];
     const unsigned long long kmask = __ballot(keep);
     if (keep) stage[lanes_below(kmask)] = s;
+    kb_at = kb_base + ((b - range.x) >> 6);  // (stored with the next batch's loads, see above)
+    kb_word = kmask;
     const int n = __popcll(kmask);
     wave_lds_sync();
     for (int t = 0; t < n; t += 2) {
       GStage G[2];
-      G[0] = stage[t];
-      G[1] = stage[min(t + 1, 63)];
+      G[0] = stage_at(stage, t);
+      G[1] = stage_at(stage, min(t + 1, 63));
       const bool live1 = t + 1 < n;
       if (!live1) G[1].r = G[1].g = G[1].bl = G[1].d = 0.f;  // stale slot: keep 0 * x finite
       if constexpr (CNT) c_slots += 2 * PXL * 64;
@@ -648,6 +803,7 @@ __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
     }
     wave_lds_sync();
   }
+  if (kbits && kb_at >= 0 && lane == 0) kbits[kb_at] = kb_word;
   const float bg0 = background[0], bg1 = background[1], bg2 = background[2];
 #pragma unroll
   for (int k = 0; k < PXL; ++k) {
@@ -691,7 +847,7 @@ __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
 // walk, so the per-wave totals (and the deterministic mode's sums) are unchanged, while a
 // long list's parts run as separate, earlier-dispatched waves.
 template <int NP, bool ATOMICS, int COLS, bool SPLIT = false, typename PV = f2,
-          bool DET = false, bool CNT = false>
+          bool DET = false, bool CNT = false, bool KB = false>
 __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
     int tbx, int tby, int H, int W, const int *__restrict__ gids, const int2 *__restrict__ bins,
     const float2 *__restrict__ xys, const float *__restrict__ conics,
@@ -700,7 +856,9 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
     const int *__restrict__ final_idx, const float *__restrict__ v_out,
     const float *__restrict__ v_out_alpha, float alpha_max, float *__restrict__ rec,
     int chunk = 0, const int2 *__restrict__ items = nullptr,
-    const int *__restrict__ n_items = nullptr, unsigned long long *__restrict__ det = nullptr) {
+    const int *__restrict__ n_items = nullptr, unsigned long long *__restrict__ det = nullptr,
+    const unsigned long long *__restrict__ kbits = nullptr, long long kbw = 0,
+    const int *__restrict__ tile_last = nullptr) {
   constexpr int PXL = 2 * NP;
   constexpr int LROWS = 64 / COLS;
   int ctile = -1, part = 0;
@@ -758,19 +916,19 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
   const int slot = reduce9_slot();
   // canonical once, so fminf needs no per-iteration canonicalisation of the bound
   const float amax = __builtin_canonicalizef(alpha_max);
-  GStage *stage = lds[wave];
-  if (SPLIT) {  // the positions behind this part: T and the colour behind only
-    for (int b = min(maxbin, range.y - 1); b >= hi; b -= 64) {
-      const int idx = b - lane;
-      GStage s;
-      const bool keep = idx >= hi && stage_gaussian<true>(idx, gids, xys, conics, colors,
-                                                          opacity, rx0, rx1, ry0, ry1, s);
-      const unsigned long long kmask = __ballot(keep);
-      if (keep) stage[lanes_below(kmask)] = s;
-      const int n = __popcll(kmask);
-      wave_lds_sync();
-      for (int t = 0; t < n; ++t) {
-        const GStage G = stage[t];
+  GStage *stage = lds[__builtin_amdgcn_readfirstlane(wave)];  // (uniform: SGPR address arithmetic)
+  // KB: the kept positions from the forward's keep bits (the strip's two 8x8 blocks)
+  KeepSrc S{};
+  if constexpr (KB) {
+    const int wt = (threadIdx.x >> 6) & 1;  // the strip's row half: blocks 2 wt, 2 wt + 1
+    S = keep_src(kbits, kbw, tile_last, tile, range, 2 * wt, 2 * wt + 1);
+  }
+  auto stage1 = [&](int idx, GStage &s) {
+    stage_kept(idx, gids, xys, conics, colors, opacity, s);
+  };
+  auto pre_blend = [&](int n) {
+    for (int t = 0; t < n; ++t) {
+        const GStage G = stage_at(stage, t);
         const float dx = G.x - px;
         const float hA = G.ha * dx * dx, bdx = G.b * dx;
 #pragma unroll
@@ -790,22 +948,29 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
           const PV gv = vfma(PV(G.r), vr[p], vfma(PV(G.g), vg[p], G.bl * vb[p]));
           Sb[p] = vfma(fac, gv, Sb[p]);
         }
+    }
+  };
+  if (SPLIT) {  // the positions behind this part: T and the colour behind only
+    if constexpr (KB) {
+      walk_kept(S, min(maxbin, range.y - 1), hi, stage, stage1, pre_blend);
+    } else {
+      for (int b = min(maxbin, range.y - 1); b >= hi; b -= 64) {
+        const int idx = b - lane;
+        GStage s;
+        const bool keep = idx >= hi && stage_gaussian<true>(idx, gids, xys, conics, colors,
+                                                            opacity, rx0, rx1, ry0, ry1, s);
+        const unsigned long long kmask = __ballot(keep);
+        if (keep) stage[lanes_below(kmask)] = s;
+        const int n = __popcll(kmask);
+        wave_lds_sync();
+        pre_blend(n);
+        wave_lds_sync();
       }
-      wave_lds_sync();
     }
   }
   const int last = min(maxbin, hi - 1);
   unsigned c_slots = 0, c_live = 0, c_valid = 0;  // (CNT only)
-  for (int b = last; b >= lo; b -= 64) {
-    const int idx = b - lane;
-    GStage s;
-    const bool keep = idx >= lo &&
-                      stage_gaussian<true>(idx, gids, xys, conics, colors, opacity, rx0, rx1, ry0,
-                                     ry1, s);
-    const unsigned long long kmask = __ballot(keep);
-    if (keep) stage[lanes_below(kmask)] = s;
-    const int n = __popcll(kmask);
-    wave_lds_sync();
+  auto main_blend = [&](int n) {
     constexpr int U = 1;  // (two per iteration measured slower: register pressure)
     for (int t = 0; t < n; t += U) {
       float parts[U][9];
@@ -815,7 +980,7 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
       if constexpr (CNT) c_slots += U * PXL * 64;
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        GStage G = stage[min(t + u, 63)];
+        GStage G = stage_at(stage, min(t + u, 63));
         const bool live = t + u < n;
         if (!live) G.r = G.g = G.bl = G.o = 0.f;  // stale slot: keep T / Sb finite
         gid[u] = G.id;
@@ -914,7 +1079,22 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
         }
       }
     }
-    wave_lds_sync();
+  };
+  if constexpr (KB) {
+    walk_kept(S, last, lo, stage, stage1, main_blend);
+  } else {
+    for (int b = last; b >= lo; b -= 64) {
+      const int idx = b - lane;
+      GStage s;
+      const bool keep = idx >= lo && stage_gaussian<true>(idx, gids, xys, conics, colors, opacity,
+                                                          rx0, rx1, ry0, ry1, s);
+      const unsigned long long kmask = __ballot(keep);
+      if (keep) stage[lanes_below(kmask)] = s;
+      const int n = __popcll(kmask);
+      wave_lds_sync();
+      main_blend(n);
+      wave_lds_sync();
+    }
   }
   if constexpr (CNT) pair_count_flush(0, c_slots, c_live, c_valid);
   wlog.done(tile);
@@ -941,7 +1121,7 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
 // SPLIT: list-split items as raster_bwd3p_kernel (the four waves of a workgroup take the four
 // 8x8 blocks of one (tile, part) item, with the same pre-walk).  DET: integer accumulation
 // (det_add).  CNT: lane-slot accounting (gsplat_debug_pair_count).
-template <bool SPLIT = false, bool DET = false, bool CNT = false>
+template <bool SPLIT = false, bool DET = false, bool CNT = false, bool KB = false>
 __global__ __launch_bounds__(256) void raster_bwd8_kernel(
     int tbx, int tby, int H, int W, const int *__restrict__ gids, const int2 *__restrict__ bins,
     const float2 *__restrict__ xys, const float *__restrict__ conics,
@@ -950,7 +1130,9 @@ __global__ __launch_bounds__(256) void raster_bwd8_kernel(
     const int *__restrict__ final_idx, const float *__restrict__ v_out,
     const float *__restrict__ v_out_alpha, float alpha_max, float *__restrict__ rec,
     int chunk = 0, const int2 *__restrict__ items = nullptr,
-    const int *__restrict__ n_items = nullptr, unsigned long long *__restrict__ det = nullptr) {
+    const int *__restrict__ n_items = nullptr, unsigned long long *__restrict__ det = nullptr,
+    const unsigned long long *__restrict__ kbits = nullptr, long long kbw = 0,
+    const int *__restrict__ tile_last = nullptr) {
   int ctile = -1, part = 0;
   if (SPLIT) {
     const int slot = wave_slot<1, 8>();
@@ -992,23 +1174,26 @@ __global__ __launch_bounds__(256) void raster_bwd8_kernel(
   const bool for0 = slot >= 0 && slot < 9, for1 = slot >= 9;
   const int field = slot >= 9 ? slot - 9 : slot;
   const float amax = __builtin_canonicalizef(alpha_max);
-  GStage *stage = lds[wave];
+  GStage *stage = lds[__builtin_amdgcn_readfirstlane(wave)];  // (uniform: SGPR address arithmetic)
   // this batch's staged Gaussian (b: the batch top, bottom: the lowest position staged)
   auto stage_next = [&](int b, int bottom, GStage &s) {
     const int idx = b - (int)(threadIdx.x & 63);
     return idx >= bottom && stage_gaussian<true>(idx, gids, xys, conics, colors, opacity, R.rx0,
                                                  R.rx1, R.ry0, R.ry1, s);
   };
-  if (SPLIT) {  // the positions behind this part: T and the colour behind only
-    for (int b = min(maxbin, range.y - 1); b >= hi; b -= 64) {
-      GStage s;
-      const bool keep = stage_next(b, hi, s);
-      const unsigned long long kmask = __ballot(keep);
-      if (keep) stage[lanes_below(kmask)] = s;
-      const int n = __popcll(kmask);
-      wave_lds_sync();
-      for (int t = 0; t < n; ++t) {  // (the main loop's T / Sb operations, nothing else)
-        const GStage G = stage[t];
+  // KB: the kept positions from the forward's keep bits (this wave's own 8x8 block)
+  KeepSrc S{};
+  if constexpr (KB) {
+    const int wt = (threadIdx.x >> 6) & 3;
+    S = keep_src(kbits, kbw, tile_last, tile, range, wt, wt);
+    S.kmax1 = -1;  // one block
+  }
+  auto stage1 = [&](int idx, GStage &s) {
+    stage_kept(idx, gids, xys, conics, colors, opacity, s);
+  };
+  auto pre_blend = [&](int n) {
+    for (int t = 0; t < n; ++t) {  // (the main loop's T / Sb operations, nothing else)
+        const GStage G = stage_at(stage, t);
         const float dx = G.x - px, dy = G.y - py;
         const float sg = gs_sigma(G.hc, G.b * dx, G.ha * dx * dx, dy);
         const float al = fminf(amax, G.o * gs_vis(sg));
@@ -1017,21 +1202,29 @@ __global__ __launch_bounds__(256) void raster_bwd8_kernel(
         T = T * __builtin_amdgcn_rcpf(1.f - am);
         const float fac = am * T;
         Sb = fmaf(fac, fmaf(G.r, vr, fmaf(G.g, vg, G.bl * vb)), Sb);
+    }
+  };
+  if (SPLIT) {  // the positions behind this part: T and the colour behind only
+    if constexpr (KB) {
+      walk_kept(S, min(maxbin, range.y - 1), hi, stage, stage1, pre_blend);
+    } else {
+      for (int b = min(maxbin, range.y - 1); b >= hi; b -= 64) {
+        GStage s;
+        const bool keep = stage_next(b, hi, s);
+        const unsigned long long kmask = __ballot(keep);
+        if (keep) stage[lanes_below(kmask)] = s;
+        const int n = __popcll(kmask);
+        wave_lds_sync();
+        pre_blend(n);
+        wave_lds_sync();
       }
-      wave_lds_sync();
     }
   }
   const int last = min(maxbin, hi - 1);
   unsigned c_slots = 0, c_live = 0, c_valid = 0;  // (CNT only)
-  for (int b = last; b >= lo; b -= 64) {
-    GStage s;
-    const bool keep = stage_next(b, lo, s);
-    const unsigned long long kmask = __ballot(keep);
-    if (keep) stage[lanes_below(kmask)] = s;
-    const int n = __popcll(kmask);
-    wave_lds_sync();
+  auto main_blend = [&](int n) {
     for (int t = 0; t < n; t += 2) {
-      GStage G0 = stage[t], G1 = stage[min(t + 1, 63)];
+      GStage G0 = stage_at(stage, t), G1 = stage_at(stage, min(t + 1, 63));
       const bool live1 = t + 1 < n;
       if (!live1) G1.r = G1.g = G1.bl = G1.o = 0.f;  // stale slot: alpha 0, finite terms
       int gid0 = G0.id, gid1 = G1.id;
@@ -1083,7 +1276,20 @@ __global__ __launch_bounds__(256) void raster_bwd8_kernel(
         }
       }
     }
-    wave_lds_sync();
+  };
+  if constexpr (KB) {
+    walk_kept(S, last, lo, stage, stage1, main_blend);
+  } else {
+    for (int b = last; b >= lo; b -= 64) {
+      GStage s;
+      const bool keep = stage_next(b, lo, s);
+      const unsigned long long kmask = __ballot(keep);
+      if (keep) stage[lanes_below(kmask)] = s;
+      const int n = __popcll(kmask);
+      wave_lds_sync();
+      main_blend(n);
+      wave_lds_sync();
+    }
   }
   if constexpr (CNT) pair_count_flush(0, c_slots, c_live, c_valid);
   wlog.done(tile);
@@ -1433,6 +1639,8 @@ struct SplitWs {
   int2 *items;
   int *n_items;
   long long items_bound;
+  unsigned long long *kbits;  // the forward's keep bits (KeepSrc), SPLIT_WAVES x kbw words
+  long long kbw;
   size_t bytes;
 };
 static SplitWs carve_split_ws(void *base, long long T, long long I, int chunk) {
@@ -1447,12 +1655,14 @@ static SplitWs carve_split_ws(void *base, long long T, long long I, int chunk) {
   w.work = (int *)take((size_t)T * SPLIT_WAVES * sizeof(int));
   w.items = (int2 *)take((size_t)w.items_bound * sizeof(int2));
   w.n_items = (int *)take(sizeof(int));
+  w.kbw = I / 64 + T + 2;
+  w.kbits = (unsigned long long *)take((size_t)SPLIT_WAVES * w.kbw * sizeof(unsigned long long));
   w.bytes = off;
   return w;
 }
 static bool default_variants() {
   // (the staging pipeline bits change the schedule only)
-  return g_fwd_pxl == FWD_PXL && g_bwd_pxl == BWD_PXL && (g_bwd_flags & ~(3 << 28)) == 0;
+  return g_fwd_pxl == FWD_PXL && g_bwd_pxl == BWD_PXL && (g_bwd_flags & ~(7 << 28)) == 0;
 }
 
 extern "C" int gsplat_rasterize_chunk_size(int tile_bounds_x, int tile_bounds_y,
@@ -1497,13 +1707,14 @@ static void launch_fwd(hipStream_t st, int tbx, int tby, int H, int W, const int
                        const float *colors, const float *opacity, const float *background,
                        float *out_img, float *final_Ts, int32_t *final_idx, const float *depths,
                        float *out_depth, float4 *zero, long long zn, const int32_t *zero_radii,
-                       int *tile_last = nullptr) {
+                       int *tile_last = nullptr, unsigned long long *kbits = nullptr,
+                       long long kbw = 0) {
   const unsigned grid = cdiv((long long)tbx * tby, (tiles_per_block<1, 8>()));
 #define FWDK(CNT, PF)                                                                      \
   hipLaunchKernelGGL((raster_fwd3u_kernel<1, 8, DEPTH, CNT, PF>), dim3(grid), dim3(256), 0, st, \
                      tbx, tby, H, W, gids, (const int2 *)bins, (const float2 *)xys, conics,     \
                      colors, opacity, background, out_img, final_Ts, final_idx, depths,         \
-                     out_depth, zero, zn, zero_radii, tile_last)
+                     out_depth, zero, zn, zero_radii, tile_last, kbits, kbw)
   const bool pf = pipelined_staging(tbx, tby);
   if (!DEPTH && g_pair_count_on) {
     if (pf) FWDK(true, true); else FWDK(true, false);
@@ -1565,16 +1776,17 @@ extern "C" int gsplat_rasterize_forward_rgbd(int tile_bounds_x, int tile_bounds_
 // Measurement knob: bwd_pxl picks the backward geometry (BWD_PXL above); bits 20-27 of flags
 // the XCD chunk of the blend kernels' block order (0 the default K = 8, 255 dispatch order).
 extern "C" int gsplat_debug_set_raster_variant(int fwd_pxl, int bwd_pxl, int bwd_flags) {
-  if (fwd_pxl != 1 || bwd_pxl < 0 || bwd_pxl > 2 || (bwd_flags & ~(0x3ff << 20)) ||
+  if (fwd_pxl != 1 || bwd_pxl < 0 || bwd_pxl > 2 || (bwd_flags & ~(0x7ff << 20)) ||
       ((bwd_flags >> 28) & 3) == 3) {
     set_error("debug_set_raster_variant: fwd_pxl must be 1, bwd_pxl 0 (by frame size), 1 (8x8 "
               "blocks) or 2 (16x8 strips), flags only the XCD chunk (bits 20-27) and the "
-              "staging pipeline (bits 28-29: 0 auto, 1 off, 2 on)");
+              "staging pipeline (bits 28-29: 0 auto, 1 off, 2 on), bit 30 the forward's keep bits off");
     return 1;
   }
   g_fwd_pxl = fwd_pxl;
   g_bwd_pxl = bwd_pxl;
   g_bwd_flags = bwd_flags;
+  g_keep_bits = !(bwd_flags & (1 << 30));
   const int pfm = (bwd_flags >> 28) & 3;
   g_pf_mode = pfm == 0 ? -1 : pfm == 1 ? 0 : 1;
   const int chunk = (bwd_flags >> 20) & 0xff;
@@ -1645,35 +1857,47 @@ static void launch_bwd(hipStream_t st, int tbx, int tby, int H, int W, int n,
                        (const int2 *)bins, (const int *)w->work, w->items, w->n_items);
   }
   const bool cnt = g_pair_count_on && !det;
+  // the forward's keep bits: only when the forward filled this plan (and kept its culls)
+  const bool kb = w && work_ready && g_keep_bits;
+  const unsigned long long *kbits = kb ? w->kbits : nullptr;
+  const long long kbw = kb ? w->kbw : 0;
+  const int *tl = kb ? w->work : nullptr;
   if (bwd_geometry(tbx, tby) == 1) {
     const unsigned grid = cdiv(slots, (tiles_per_block<1, 8>()));
-#define BWD8(CH, DET, CNT)                                                                 \
-  hipLaunchKernelGGL((raster_bwd8_kernel<CH, DET, CNT>), dim3(grid), dim3(256), 0, st, tbx, tby, \
-                     H, W, gids, (const int2 *)bins, (const float2 *)xys, conics, colors,       \
+#define BWD8(CH, DET, CNT, KB)                                                             \
+  hipLaunchKernelGGL((raster_bwd8_kernel<CH, DET, CNT, KB>), dim3(grid), dim3(256), 0, st, tbx,  \
+                     tby, H, W, gids, (const int2 *)bins, (const float2 *)xys, conics, colors,  \
                      opacity, background, final_Ts, final_idx, v_output, v_output_alpha,        \
-                     alpha_max, rec, chunk, its, ni, det)
-    if (w) {
-      if (det) BWD8(true, true, false); else if (cnt) BWD8(true, false, true);
-      else BWD8(true, false, false);
+                     alpha_max, rec, chunk, its, ni, det, kbits, kbw, tl)
+    if (w && kb) {
+      if (det) BWD8(true, true, false, true); else if (cnt) BWD8(true, false, true, true);
+      else BWD8(true, false, false, true);
+    } else if (w) {
+      if (det) BWD8(true, true, false, false); else if (cnt) BWD8(true, false, true, false);
+      else BWD8(true, false, false, false);
     } else {
-      if (det) BWD8(false, true, false); else if (cnt) BWD8(false, false, true);
-      else BWD8(false, false, false);
+      if (det) BWD8(false, true, false, false); else if (cnt) BWD8(false, false, true, false);
+      else BWD8(false, false, false, false);
     }
 
 #undef BWD8
   } else {
     const unsigned grid = cdiv(slots, (tiles_per_block<2, 16>()));
-#define BWDS(CH, DET, CNT)                                                                 \
-  hipLaunchKernelGGL((raster_bwd3p_kernel<1, true, 16, CH, f2, DET, CNT>), dim3(grid), dim3(256), \
-                     0, st, tbx, tby, H, W, gids, (const int2 *)bins, (const float2 *)xys,      \
-                     conics, colors, opacity, background, final_Ts, final_idx, v_output,        \
-                     v_output_alpha, alpha_max, rec, chunk, its, ni, det)
-    if (w) {
-      if (det) BWDS(true, true, false); else if (cnt) BWDS(true, false, true);
-      else BWDS(true, false, false);
+#define BWDS(CH, DET, CNT, KB)                                                             \
+  hipLaunchKernelGGL((raster_bwd3p_kernel<1, true, 16, CH, f2, DET, CNT, KB>), dim3(grid),       \
+                     dim3(256), 0, st, tbx, tby, H, W, gids, (const int2 *)bins,                \
+                     (const float2 *)xys, conics, colors, opacity, background, final_Ts,        \
+                     final_idx, v_output, v_output_alpha, alpha_max, rec, chunk, its, ni, det,  \
+                     kbits, kbw, tl)
+    if (w && kb) {
+      if (det) BWDS(true, true, false, true); else if (cnt) BWDS(true, false, true, true);
+      else BWDS(true, false, false, true);
+    } else if (w) {
+      if (det) BWDS(true, true, false, false); else if (cnt) BWDS(true, false, true, false);
+      else BWDS(true, false, false, false);
     } else {
-      if (det) BWDS(false, true, false); else if (cnt) BWDS(false, false, true);
-      else BWDS(false, false, false);
+      if (det) BWDS(false, true, false, false); else if (cnt) BWDS(false, false, true, false);
+      else BWDS(false, false, false, false);
     }
 #undef BWDS
   }
@@ -1796,6 +2020,8 @@ extern "C" int gsplat_rasterize_forward_clearing(
     return 1;
   }
   int *tile_last = nullptr;  // the list-split plan's walk table, filled by the blend's waves
+  unsigned long long *kbits = nullptr;  // and the backward's keep bits (KeepSrc)
+  long long kbw = 0;
   if (chunk > 0) {
     const SplitWs w =
         carve_split_ws(plan, (long long)tile_bounds_x * tile_bounds_y, num_intersects, chunk);
@@ -1804,11 +2030,15 @@ extern "C" int gsplat_rasterize_forward_clearing(
       return 1;
     }
     tile_last = w.work;
+    if (g_keep_bits) {
+      kbits = w.kbits;
+      kbw = w.kbw;
+    }
   }
   launch_fwd<false>((hipStream_t)stream, tile_bounds_x, tile_bounds_y, img_height, img_width,
                     gaussian_ids_sorted, tile_bins, xys, conics, colors, opacity, background,
                     out_img, final_Ts, final_idx, nullptr, nullptr, (float4 *)clear,
-                    (long long)(clear_bytes / 16), clear_radii, tile_last);
+                    (long long)(clear_bytes / 16), clear_radii, tile_last, kbits, kbw);
   return check_launch(who);
 }
 

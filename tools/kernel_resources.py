@@ -24,7 +24,7 @@ for line in r.stderr.splitlines():
 for row in rows:
     n = subprocess.run(["c++filt", row["name"]], capture_output=True,
                        text=True).stdout.strip()
-    n = re.sub(r"\(.*$", "", n.replace("gs::(anonymous namespace)::", ""))
+    n = re.sub(r"\((?!2\)).*$", "", n.replace("gs::(anonymous namespace)::", "").replace("float __vector(2)", "f2"))
     if pats and not any(p in n for p in pats):
         continue
     print(f"{n[:70]:70s} vgpr {row.get('VGPRs')} agpr {row.get('AGPRs')} sgpr {row.get('SGPRs')} "
