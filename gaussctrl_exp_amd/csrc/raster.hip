@@ -834,7 +834,9 @@ __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
 // ---------------------------------------------------------------- backward, C = 3
 // Packed backward: 2*NP pixels per lane as float2 pairs, branch-free (an invalid pixel gets
 // alpha = vis = 0: T, the colour buffer and every partial sum are unchanged exactly).
-// Per pixel the colour buffer is carried as one dot product Sb = sum_c buf_c * v_c, and the
+// Per pixel the colour buffer enters v_alpha only through q - sum_c buf_c * v_c (q: the
+// background / alpha-output term below), carried as that one running value Qs (each Gaussian
+// behind subtracts fac * (colour . v_out) with one fma), and the
 // sigma gradient as moments V = sum v_sigma, Vy = sum v_sigma dy, Vyy = sum v_sigma dy^2
 // (dx is constant along the lane's column), from which
 //   v_conic = 0.5 (dx^2 V, dx Vy, Vyy),  v_xy = (a dx V + b Vy, b dx V + c Vy).
@@ -878,7 +880,7 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
   const float px = (float)j;
   const float rx0 = R.rx0, rx1 = R.rx1, ry0 = R.ry0, ry1 = R.ry1;
   const float bg0 = background[0], bg1 = background[1], bg2 = background[2];
-  PV py[NP], T[NP], vr[NP], vg[NP], vb[NP], q[NP], Sb[NP];
+  PV py[NP], T[NP], vr[NP], vg[NP], vb[NP], Qs[NP];
   int binf[PXL];
   int maxbin = -1;
 #pragma unroll
@@ -898,11 +900,10 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
     // v_alpha's background/alpha terms: Tf/(1-alpha) * (v_alpha_out - bg . v_out)
     const float qk = Tf * (a - (bg0 * r + bg1 * g + bg2 * bl));
     if (k & 1) {
-      py[p].y = (float)i; T[p].y = Tf; vr[p].y = r; vg[p].y = g; vb[p].y = bl; q[p].y = qk;
+      py[p].y = (float)i; T[p].y = Tf; vr[p].y = r; vg[p].y = g; vb[p].y = bl; Qs[p].y = qk;
     } else {
-      py[p].x = (float)i; T[p].x = Tf; vr[p].x = r; vg[p].x = g; vb[p].x = bl; q[p].x = qk;
+      py[p].x = (float)i; T[p].x = Tf; vr[p].x = r; vg[p].x = g; vb[p].x = bl; Qs[p].x = qk;
     }
-    Sb[p] = PV(0.f);
     binf[k] = bf;
     maxbin = max(maxbin, bf);
   }
@@ -932,7 +933,7 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
         const float dx = G.x - px;
         const float hA = G.ha * dx * dx, bdx = G.b * dx;
 #pragma unroll
-        for (int p = 0; p < NP; ++p) {  // (the main loop's T / Sb operations, nothing else)
+        for (int p = 0; p < NP; ++p) {  // (the main loop's T / Qs operations, nothing else)
           const PV dy = G.y - py[p];
           const PV sig = gs_sigma2v<PV>(G.hc, bdx, hA, dy);
           const PV vis = gs_vis2v<PV>(sig);
@@ -946,7 +947,7 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
           T[p] = T[p] * ra;
           const PV fac = am * T[p];
           const PV gv = vfma(PV(G.r), vr[p], vfma(PV(G.g), vg[p], G.bl * vb[p]));
-          Sb[p] = vfma(fac, gv, Sb[p]);
+          Qs[p] = vfma(-fac, gv, Qs[p]);
         }
     }
   };
@@ -982,7 +983,7 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
       for (int u = 0; u < U; ++u) {
         GStage G = stage_at(stage, min(t + u, 63));
         const bool live = t + u < n;
-        if (!live) G.r = G.g = G.bl = G.o = 0.f;  // stale slot: keep T / Sb finite
+        if (!live) G.r = G.g = G.bl = G.o = 0.f;  // stale slot: keep T / Qs finite
         gid[u] = G.id;
         // read with the rest of the staged record at the top of the iteration: left to the
         // compiler, the id's LDS read sank to the atomic at the end -- a second LDS round trip
@@ -1024,8 +1025,8 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
           sb = fmaf(fac.y, vb[p].y, p ? fmaf(fac.x, vb[p].x, sb) : fac.x * vb[p].x);
           const PV gv = vfma(
               PV(G.r), vr[p], vfma(PV(G.g), vg[p], G.bl * vb[p]));
-          const PV v_alpha = vfma(gv, T[p], ra * (q[p] - Sb[p]));
-          Sb[p] = vfma(fac, gv, Sb[p]);
+          const PV v_alpha = vfma(gv, T[p], ra * Qs[p]);
+          Qs[p] = vfma(-fac, gv, Qs[p]);
           const PV vva = vm * v_alpha;
           const PV vdy = vva * dy;
           sa = p ? sa + (vva.x + vva.y) : vva.x + vva.y;
@@ -1148,7 +1149,7 @@ __global__ __launch_bounds__(256) void raster_bwd8_kernel(
   const int wave = threadIdx.x >> 6;
   const int tile = R.tile, j = R.j, i = R.i0;
   const float px = (float)j, py = (float)i;
-  float T = 0.f, vr = 0.f, vg = 0.f, vb = 0.f, q = 0.f, Sb = 0.f;
+  float T = 0.f, vr = 0.f, vg = 0.f, vb = 0.f, Qs = 0.f;  // Qs: as raster_bwd3p_kernel's
   int bf = -1;
   const bool inside = i < H && j < W;
   if (inside) {
@@ -1160,7 +1161,7 @@ __global__ __launch_bounds__(256) void raster_bwd8_kernel(
     vb = v_out[3 * pix + 2];
     const float a = v_out_alpha ? v_out_alpha[pix] : 0.f;
     // v_alpha's background / alpha-output terms: T_final / (1 - alpha) * (v_alpha_out - bg . v)
-    q = T * (a - (background[0] * vr + background[1] * vg + background[2] * vb));
+    Qs = T * (a - (background[0] * vr + background[1] * vg + background[2] * vb));
   }
   const int2 range = bins[tile];
   int lo = range.x, hi = range.y;
@@ -1192,7 +1193,7 @@ __global__ __launch_bounds__(256) void raster_bwd8_kernel(
     stage_kept(idx, gids, xys, conics, colors, opacity, s);
   };
   auto pre_blend = [&](int n) {
-    for (int t = 0; t < n; ++t) {  // (the main loop's T / Sb operations, nothing else)
+    for (int t = 0; t < n; ++t) {  // (the main loop's T / Qs operations, nothing else)
         const GStage G = stage_at(stage, t);
         const float dx = G.x - px, dy = G.y - py;
         const float sg = gs_sigma(G.hc, G.b * dx, G.ha * dx * dx, dy);
@@ -1201,7 +1202,7 @@ __global__ __launch_bounds__(256) void raster_bwd8_kernel(
         const float am = v ? al : 0.f;
         T = T * __builtin_amdgcn_rcpf(1.f - am);
         const float fac = am * T;
-        Sb = fmaf(fac, fmaf(G.r, vr, fmaf(G.g, vg, G.bl * vb)), Sb);
+        Qs = fmaf(-fac, fmaf(G.r, vr, fmaf(G.g, vg, G.bl * vb)), Qs);
     }
   };
   if (SPLIT) {  // the positions behind this part: T and the colour behind only
@@ -1250,14 +1251,14 @@ __global__ __launch_bounds__(256) void raster_bwd8_kernel(
       T = T * ra0;
       const float fac0 = am0 * T;
       const float gv0 = fmaf(G0.r, vr, fmaf(G0.g, vg, G0.bl * vb));
-      const float va0 = fmaf(gv0, T, ra0 * (q - Sb));
-      Sb = fmaf(fac0, gv0, Sb);
+      const float va0 = fmaf(gv0, T, ra0 * Qs);
+      Qs = fmaf(-fac0, gv0, Qs);
       const float ra1 = __builtin_amdgcn_rcpf(1.f - am1);
       T = T * ra1;
       const float fac1 = am1 * T;
       const float gv1 = fmaf(G1.r, vr, fmaf(G1.g, vg, G1.bl * vb));
-      const float va1 = fmaf(gv1, T, ra1 * (q - Sb));
-      Sb = fmaf(fac1, gv1, Sb);
+      const float va1 = fmaf(gv1, T, ra1 * Qs);
+      Qs = fmaf(-fac1, gv1, Qs);
       if (any0 | any1) {  // (an SGPR test)
         const float w0 = (v0 ? vis0 : 0.f) * va0, w1 = (v1 ? vis1 : 0.f) * va1;
         const float sx0 = dx0 * w0, sy0 = dy0 * w0, sx1 = dx1 * w1, sy1 = dy1 * w1;

@@ -6,7 +6,7 @@ import sys
 
 src = sys.argv[1]
 pats = sys.argv[2:]
-r = subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17",
+r = subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", *(["-fno-slp-vectorize"] if "raster" in src else []),
                     "-c", src, "-o", "/tmp/_kr.o", "-Rpass-analysis=kernel-resource-usage"],
                    capture_output=True, text=True)
 cur, rows = None, []
