@@ -911,7 +911,7 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
   int lo = range.x, hi = range.y;
   if (SPLIT) {
     lo = range.x + part * chunk;
-    hi = min(lo + chunk, range.y);
+    hi = (int)min((long long)lo + chunk, (long long)range.y);  // (no int overflow)
   }
   maxbin = wave_max_int(maxbin);
   const int slot = reduce9_slot();
@@ -1167,7 +1167,7 @@ __global__ __launch_bounds__(256) void raster_bwd8_kernel(
   int lo = range.x, hi = range.y;
   if (SPLIT) {
     lo = range.x + part * chunk;
-    hi = min(lo + chunk, range.y);
+    hi = (int)min((long long)lo + chunk, (long long)range.y);  // (no int overflow)
   }
   const int maxbin = wave_max_int(bf);
   // reduce18 lane roles, learned once: value k = slot (Gaussian slot / 9, field slot % 9)
@@ -1780,8 +1780,9 @@ extern "C" int gsplat_debug_set_raster_variant(int fwd_pxl, int bwd_pxl, int bwd
   if (fwd_pxl != 1 || bwd_pxl < 0 || bwd_pxl > 2 || (bwd_flags & ~(0x7ff << 20)) ||
       ((bwd_flags >> 28) & 3) == 3) {
     set_error("debug_set_raster_variant: fwd_pxl must be 1, bwd_pxl 0 (by frame size), 1 (8x8 "
-              "blocks) or 2 (16x8 strips), flags only the XCD chunk (bits 20-27) and the "
-              "staging pipeline (bits 28-29: 0 auto, 1 off, 2 on), bit 30 the forward's keep bits off");
+              "blocks) or 2 (16x8 strips), flags only the XCD chunk "
+              "(bits 20-27), the staging pipeline (bits 28-29: 0 auto, 1 off, 2 on) and bit "
+              "30 (the forward's keep bits off)");
     return 1;
   }
   g_fwd_pxl = fwd_pxl;

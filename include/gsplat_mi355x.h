@@ -404,7 +404,8 @@ int gsplat_grad_records_split(int num_points, const void *records, size_t record
  * iteration, 2 = 16x8 strips, two pixels per lane; bwd_flags bits 20-27 = K: the block -> tile
  * order of the blend kernels, chunks of K block slots dealt round-robin over the 8 XCDs (0: the
  * shipped K = 8, 255: plain dispatch order); bits 28-29: the forward's staging pipeline (0: by
- * frame size, shipped -- on below 3,584 tiles; 1 off; 2 on).  Every variant meets the same
+ * frame size, shipped -- on below 3,584 tiles; 1 off; 2 on); bit 30: the forward's keep bits
+ * off (the list-split backward culls for itself).  Every variant meets the same
  * parity bar (none changes the arithmetic).  Process-wide; (1, 0, 0) is the shipped
  * configuration. */
 int gsplat_debug_set_raster_variant(int fwd_pxl, int bwd_pxl, int bwd_flags);
