@@ -30,7 +30,10 @@ namespace gs {
 namespace {
 
 constexpr int TPB = 256;
-constexpr int SC_ITEMS = 16;
+// Scan tile of 1,024 entries: the depth-ordered gather of the binning records (one dependent
+// load chain per item) runs in 4x as many workgroups as with 4,096 (bin_count_keyed 0.112 ->
+// 0.106 ms at the headline, c5 0.285 -> 0.264; profiles/r03_scan_tile_ab.txt).
+constexpr int SC_ITEMS = 4;
 constexpr int SC_TILE = TPB * SC_ITEMS;  // elements per scan workgroup
 // keys per thread of a sort pass (workgroup tile = TPB * items): small sorts use short tiles
 // so that more, shorter workgroups run at once (a pass is a chain of latencies per workgroup)
