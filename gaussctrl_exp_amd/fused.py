@@ -24,6 +24,7 @@ the drop-in; this is the framework's own training step (TrainStep(render_mode="f
 from __future__ import annotations
 
 import ctypes
+import weakref
 from typing import Optional
 
 import torch
@@ -216,6 +217,22 @@ def _contig_f32(t: Tensor) -> Tensor:
     return t if (t.dtype == torch.float32 and t.is_contiguous()) else t.float().contiguous()
 
 
+# The camera centre c2w[:3, 3] is a strided column: contiguous, it is a copy kernel (and ~30 us
+# of host time) per render.  One cached copy per camera pose, reused while the very same c2w
+# tensor (weak reference) is unmodified (version counter) -- as rasterize.py's binning cache.
+_CAMPOS = [None, -1, None]
+
+
+def _campos(cam: GCCamera) -> Tensor:
+    c2w = cam.c2w
+    ref, version, t = _CAMPOS
+    if ref is not None and ref() is c2w and version == c2w._version:
+        return t
+    t = _contig_f32(c2w[..., :3, 3].reshape(3))
+    _CAMPOS[:] = [weakref.ref(c2w), c2w._version, t]
+    return t
+
+
 def render_fused(scene, cam: GCCamera, sh_degree_to_use: int, background: Tensor,
                  return_alpha: bool = False, clamp: bool = True, adam=None):
     """scene.render's training output (gc_model.py:158-222) through the fused kernels.
@@ -229,11 +246,10 @@ def render_fused(scene, cam: GCCamera, sh_degree_to_use: int, background: Tensor
     that Adam step itself (gsplat_fused_preprocess_backward_adam: parameters updated in place,
     no .grad); single-GPU only."""
     aux = {}
-    campos = cam.c2w[..., :3, 3].reshape(3)
     args = [_contig_f32(scene.means), _contig_f32(scene.scales), _contig_f32(scene.quats),
             _contig_f32(scene.opacities), _contig_f32(scene.features_dc),
             _contig_f32(scene.features_rest), _contig_f32(cam.viewmat), _contig_f32(cam.projmat),
-            _contig_f32(campos), cam.fx, cam.fy, cam.cx, cam.cy, cam.height, cam.width,
+            _campos(cam), cam.fx, cam.fy, cam.cx, cam.cy, cam.height, cam.width,
             int(sh_degree_to_use), _contig_f32(background), bool(return_alpha), aux, adam]
     out = _FusedRender.apply(*args)
     img, alpha = (out if return_alpha else (out, None))
