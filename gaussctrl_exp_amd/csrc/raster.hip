@@ -34,6 +34,7 @@
 
 #include <algorithm>
 #include <mutex>
+#include <unordered_map>
 #include <type_traits>
 
 namespace gs {
@@ -1666,6 +1667,24 @@ static bool default_variants() {
   return g_fwd_pxl == FWD_PXL && g_bwd_pxl == BWD_PXL && (g_bwd_flags & ~(7 << 28)) == 0;
 }
 
+// Which list-split plans carry keep bits: the forward that fills a plan notes whether it also
+// wrote the keep bits (g_keep_bits at that time), and the backward on that plan walks them only
+// then -- a switch flipped between the two calls (debug flag bit 30) cannot make the backward
+// read words no forward wrote.  Keyed by the plan's address, which the next
+// forward on that buffer overwrites.
+static std::mutex g_plan_kb_mu;
+static std::unordered_map<const void *, bool> g_plan_kb;
+static void plan_kbits_note(const void *plan, bool written) {
+  std::lock_guard<std::mutex> lk(g_plan_kb_mu);
+  if (g_plan_kb.size() > 4096) g_plan_kb.clear();  // (stale entries of freed plans)
+  g_plan_kb[plan] = written;
+}
+static bool plan_kbits_written(const void *plan) {
+  std::lock_guard<std::mutex> lk(g_plan_kb_mu);
+  const auto it = g_plan_kb.find(plan);
+  return it != g_plan_kb.end() && it->second;
+}
+
 extern "C" int gsplat_rasterize_chunk_size(int tile_bounds_x, int tile_bounds_y,
                                            int64_t num_intersects) {
   if (g_chunk_override < 0 || num_intersects <= 0 || tile_bounds_x <= 0 || tile_bounds_y <= 0)
@@ -1846,7 +1865,7 @@ static void launch_bwd(hipStream_t st, int tbx, int tby, int H, int W, int n,
                        const float *background, const float *final_Ts, const int32_t *final_idx,
                        const float *v_output, const float *v_output_alpha, float alpha_max,
                        float *rec, int chunk, const SplitWs *w, unsigned long long *det,
-                       bool work_ready = false) {
+                       bool work_ready = false, bool kbits_ready = false) {
   const long long slots = w ? w->items_bound : (long long)tbx * tby;
   const int2 *its = w ? w->items : nullptr;
   const int *ni = w ? w->n_items : nullptr;
@@ -1859,8 +1878,9 @@ static void launch_bwd(hipStream_t st, int tbx, int tby, int H, int W, int n,
                        (const int2 *)bins, (const int *)w->work, w->items, w->n_items);
   }
   const bool cnt = g_pair_count_on && !det;
-  // the forward's keep bits: only when the forward filled this plan (and kept its culls)
-  const bool kb = w && work_ready && g_keep_bits;
+  // the forward's keep bits: only when the forward that filled this plan also wrote them
+  // (plan_kbits_written: whatever g_keep_bits says now -- ADVICE r3)
+  const bool kb = w && work_ready && kbits_ready;
   const unsigned long long *kbits = kb ? w->kbits : nullptr;
   const long long kbw = kb ? w->kbw : 0;
   const int *tl = kb ? w->work : nullptr;
@@ -1915,7 +1935,8 @@ static int backward_into_records(const char *who, hipStream_t st, int tbx, int t
                                  const float *final_Ts, const int32_t *final_idx,
                                  const float *v_output, const float *v_output_alpha,
                                  float alpha_max, float *rec, int64_t num_intersects, int chunk,
-                                 void *plan, size_t plan_bytes, bool work_ready = false) {
+                                 void *plan, size_t plan_bytes, bool work_ready = false,
+                                 bool kbits_ready = false) {
   SplitWs w{};
   if (chunk > 0) {
     w = carve_split_ws(plan, (long long)tbx * tby, num_intersects, chunk);
@@ -1929,12 +1950,12 @@ static int backward_into_records(const char *who, hipStream_t st, int tbx, int t
     if (!lease.buf) return check_launch(who);
     launch_bwd(st, tbx, tby, H, W, n, gids, bins, xys, conics, colors, opacity, background,
                final_Ts, final_idx, v_output, v_output_alpha, alpha_max, rec, chunk,
-               chunk > 0 ? &w : nullptr, lease.buf, work_ready);
+               chunk > 0 ? &w : nullptr, lease.buf, work_ready, kbits_ready);
     lease.finish();
   } else {
     launch_bwd(st, tbx, tby, H, W, n, gids, bins, xys, conics, colors, opacity, background,
                final_Ts, final_idx, v_output, v_output_alpha, alpha_max, rec, chunk,
-               chunk > 0 ? &w : nullptr, nullptr, work_ready);
+               chunk > 0 ? &w : nullptr, nullptr, work_ready, kbits_ready);
   }
   return 0;
 }
@@ -2036,6 +2057,7 @@ extern "C" int gsplat_rasterize_forward_clearing(
       kbits = w.kbits;
       kbw = w.kbw;
     }
+    plan_kbits_note(plan, kbits != nullptr);
   }
   launch_fwd<false>((hipStream_t)stream, tile_bounds_x, tile_bounds_y, img_height, img_width,
                     gaussian_ids_sorted, tile_bins, xys, conics, colors, opacity, background,
@@ -2126,7 +2148,8 @@ extern "C" int gsplat_rasterize_backward_records(
                             img_height, img_width, num_points, gaussian_ids_sorted, tile_bins, xys,
                             conics, colors, opacity, background, final_Ts, final_idx, v_output,
                             v_output_alpha, alpha_max, (float *)records, num_intersects, chunk,
-                            plan, plan_bytes, plan_filled != 0))
+                            plan, plan_bytes, plan_filled != 0,
+                            plan_filled != 0 && plan_kbits_written(plan)))
     return 1;
   return check_launch("rasterize_backward_records");
 }

@@ -187,7 +187,7 @@ def bin_gaussians(xys: Tensor, depths: Tensor, radii: Tensor, num_tiles_hit: Ten
         visible = int(host[0])
     finally:
         _COUNTS.release(dev, slot, visible)
-    _EMIT_CAP[key] = num_intersects + (num_intersects >> 3)
+    _EMIT_CAP[key] = emit_capacity(num_intersects)
     if pre is not None and num_intersects <= cap and not PRELAUNCH_EMISSION:  # (A/B runs)
         ids_buf, ws2 = pre
         _lib.call("gsplat_bin_emit", n, num_intersects, tbx, tby, P(ids_buf), P(tile_bins),
@@ -205,6 +205,15 @@ def bin_gaussians(xys: Tensor, depths: Tensor, radii: Tensor, num_tiles_hit: Ten
 
 # frame shape -> the intersection capacity to pre-allocate the emission's outputs for
 _EMIT_CAP = {}
+# the C ABI's bound on an emission capacity (bin_emit_impl rejects larger ones)
+EMIT_CAP_MAX = 0x3FFFFFFF
+
+
+def emit_capacity(num_intersects: int) -> int:
+    """The next call's pre-launch capacity after a call with `num_intersects`: 1/8 headroom,
+    clamped to what gsplat_bin_emit_prelaunch accepts (an unclamped I + I/8 above
+    the C limit made every later call of that frame shape fail)."""
+    return min(num_intersects + (num_intersects >> 3), EMIT_CAP_MAX)
 # launch the emission's first part before the host reads I (False: after it; A/B runs only)
 PRELAUNCH_EMISSION = True
 

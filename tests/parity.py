@@ -11,8 +11,9 @@ explicitly instead of by an outlier allowance:
 * Transmittance recovery.  The backward recovers each Gaussian's T by dividing T_final back
   through every later composited Gaussian of the pixel -- gsplat with fp32 division, this
   rasterizer with the hardware reciprocal (1 ulp) -- so at the n-th division the recovered T's
-  drift apart by up to ~n ulps (the list-split backward restarts T from the forward's
-  checkpoints instead, within the same bound).  Per term, not per tile: the oracle returns
+  drift apart by up to ~n ulps (the list-split backward's parts re-walk the positions behind
+  them with exactly the full walk's operations, so they add no drift of their own).  Per term,
+  not per tile: the oracle returns
   sum over the pixel-Gaussian terms of n * |term| (with v_alpha's components in absolute value,
   since their errors need not cancel when v_alpha does), and the bar adds 2^-23 times that
   (drift_slack).  Each check reports its worst |diff| / allowed ratio (worst_ratio).

@@ -157,3 +157,18 @@ def test_rasterize_validates_shapes_like_gsplat():
     with pytest.raises(ValueError, match="colors must have dimensions"):
         rasterize_gaussians(torch.zeros(n, 2), torch.zeros(n), torch.zeros(n), torch.zeros(n, 3),
                             torch.zeros(n), torch.zeros(n), torch.zeros(n, 1), 16, 16)
+
+
+def test_emit_capacity_clamped_to_the_c_limit():
+    """the pre-launch capacity is I + I/8 but never above the capacity
+    gsplat_bin_emit_prelaunch accepts (bin_emit_impl rejects > 0x3FFFFFFF), so a frame shape
+    whose I lies just under the limit keeps working on later calls."""
+    from gaussctrl_exp_amd import _lib
+    from gaussctrl_exp_amd.rasterize import EMIT_CAP_MAX, emit_capacity
+    assert EMIT_CAP_MAX == 0x3FFFFFFF
+    assert emit_capacity(0) == 0
+    assert emit_capacity(8_000_000) == 9_000_000
+    for I in (955_000_000, 1_000_000_000, 0x3FFFFFFF):
+        assert emit_capacity(I) == EMIT_CAP_MAX
+    # the C ABI sizes a workspace for that capacity (a pure host query, no GPU)
+    assert _lib.query("gsplat_bin_emit_workspace_size_for", 1000, EMIT_CAP_MAX, 68, 68) > 0
