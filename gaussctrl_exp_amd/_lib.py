@@ -58,6 +58,7 @@ SIGNATURES = {
     "gsplat_bin_emit": (_I, [_I, _I64, _I, _I, _P, _P, _P, _SZ, _P, _SZ, _P]),
     "gsplat_bin_emit_prelaunch": (_I, [_I, _I64, _I, _I, _P, _P, _SZ, _P, _SZ, _P]),
     "gsplat_bin_emit_finish": (_I, [_I, _I64, _I64, _I, _I, _P, _P, _P, _SZ, _P, _SZ, _P]),
+    "gsplat_bin_emit_speculative": (_I, [_I, _I64, _I, _I, _P, _P, _P, _SZ, _P, _SZ, _P]),
     "gsplat_rasterize_forward": (_I, [_I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                                       _P, _P]),
     "gsplat_rasterize_forward_rgbd": (_I, [_I, _I, _I, _I] + [_P] * 13),
@@ -96,7 +97,7 @@ SIGNATURES = {
                                                                        _I, _P, _SZ, _P]),
 }
 
-ABI_VERSION = 12  # include/gsplat_mi355x.h GSPLAT_MI355X_ABI_VERSION
+ABI_VERSION = 13  # include/gsplat_mi355x.h GSPLAT_MI355X_ABI_VERSION
 
 _lib = None
 _DETERMINISTIC = os.environ.get("GSPLAT_MI355X_DETERMINISTIC", "0") not in ("", "0")
@@ -145,6 +146,8 @@ def lib():
             raise RuntimeError(L.gsplat_last_error().decode(errors="replace"))
         if os.environ.get("GSPLAT_MI355X_CHUNK"):
             L.gsplat_debug_set_chunk(int(os.environ["GSPLAT_MI355X_CHUNK"]))
+        if os.environ.get("GSPLAT_MI355X_DEPTH_KEY_RANGE"):  # 0 off, 1 from 2^22 keys, 2 always
+            L.gsplat_debug_depth_key_range(int(os.environ["GSPLAT_MI355X_DEPTH_KEY_RANGE"]))
         _lib = L
     return _lib
 

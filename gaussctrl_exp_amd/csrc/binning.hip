@@ -207,6 +207,49 @@ __device__ __forceinline__ bool digit_constant(const uint32_t *fin, int shift, i
   return fin && ((((fin[0] ^ fin[1]) >> shift) & ((1u << width) - 1u)) == 0u);
 }
 
+// Device-selected ping-pong of the compacting depth sort (KeyRange on): a pass whose digit is
+// constant over the kept keys does nothing at all -- its three launches return at once, no copy
+// -- so where the data sits before pass q and whether pass q is the last one that moves it
+// depend on the key range, which only the device knows.  Pass 0 (the compaction) always moves
+// the data: from (ka, va) into (kb, vb), or straight into the output when no later digit varies;
+// every later moving pass flips between the two buffers, the last one writes the output.
+struct DevIO {
+  const uint32_t *fin;       // the key range (AND, OR); null: host-selected buffers
+  const void *ka, *kb;       // key ping-pong buffers
+  const uint32_t *va, *vb;   // value ping-pong buffers
+  void *kout;                // sorted keys (may be null)
+  uint32_t *vout;            // sorted values
+  int begin, width, passes;
+};
+__device__ __forceinline__ bool pass_moves(const DevIO &io, int q) {
+  return q == 0 || !digit_constant(io.fin, io.begin + q * io.width, io.width);
+}
+// (ka, va) or (kb, vb): the buffers holding the data before pass q >= 1
+__device__ __forceinline__ bool data_in_b(const DevIO &io, int q) {
+  int m = 0;
+  for (int j = 1; j < q; ++j) m += pass_moves(io, j) ? 1 : 0;
+  return (m & 1) == 0;
+}
+__device__ __forceinline__ bool last_move(const DevIO &io, int q) {
+  for (int j = q + 1; j < io.passes; ++j)
+    if (pass_moves(io, j)) return false;
+  return true;
+}
+template <typename K>
+__device__ __forceinline__ void dev_io(const DevIO &io, int q, const K *&kin, const uint32_t *&vin,
+                                       K *&kout, uint32_t *&vout) {
+  const bool src_b = q > 0 && data_in_b(io, q);  // pass 0 reads (ka, va)
+  kin = (const K *)(src_b ? io.kb : io.ka);
+  vin = src_b ? io.vb : io.va;
+  if (last_move(io, q)) {
+    kout = (K *)io.kout;
+    vout = io.vout;
+  } else {  // the other buffer
+    kout = (K *)(src_b ? io.ka : io.kb);
+    vout = (uint32_t *)(src_b ? io.va : io.vb);
+  }
+}
+
 // Reduce-then-scan pass, part 1: the digit histogram of every tile of TPB*ITEMS keys, stored
 // digit-major (counts[d * nblocks + tile]) so one exclusive scan yields every tile's global
 // offset for every digit.  drop: all-ones keys (culled Gaussians' depth keys) are not counted
@@ -218,12 +261,19 @@ __global__ __launch_bounds__(TPB) void rts_count_kernel(const K *__restrict__ ke
                                                         uint32_t *__restrict__ counts,
                                                         bool drop = false,
                                                         const uint32_t *__restrict__ n_dev = nullptr,
-                                                        KeyRange kr = {}, int pass = 0) {
+                                                        KeyRange kr = {}, int pass = 0,
+                                                        DevIO io = {}) {
   __shared__ uint32_t h[256];
   __shared__ uint32_t kand, kor;
   const int tid = threadIdx.x;
   if (pass > 0 && digit_constant(kr.fin, shift, width)) return;  // identity pass
-  if (n_dev) n = min(n, (long long)*n_dev);
+  if (io.fin && pass > 0) keys = (const K *)(data_in_b(io, pass) ? io.kb : io.ka);
+  if (n_dev) {
+    // *n_dev > n: a capacity-launched tile sort whose intersections overflowed the capacity
+    // (bin_emit_impl, EMIT_SPEC): the emission wrote nothing, so nothing is sorted
+    if (*n_dev > (unsigned long long)n) return;
+    n = *n_dev;
+  }
   const int R = 1 << width;
   const uint32_t dmask = (uint32_t)(R - 1);
   h[tid] = 0;
@@ -244,9 +294,16 @@ __global__ __launch_bounds__(TPB) void rts_count_kernel(const K *__restrict__ ke
       a &= (uint32_t)k[r];
       o |= (uint32_t)k[r];
     }
-  if (pass == 0 && kr.blk) {
-    atomicAnd(&kand, a);
-    atomicOr(&kor, o);
+  if (pass == 0 && kr.blk) {  // one LDS atomic per wave
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      a &= __shfl_xor(a, off, 64);
+      o |= __shfl_xor(o, off, 64);
+    }
+    if ((tid & 63) == 0) {
+      atomicAnd(&kand, a);
+      atomicOr(&kor, o);
+    }
   }
   __syncthreads();
   if (tid < R) counts[(size_t)tid * nblocks + blockIdx.x] = h[tid];
@@ -346,12 +403,25 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     const uint32_t *__restrict__ rowtot, const uint32_t *__restrict__ offs, long long nblocks,
     int32_t *__restrict__ bins = nullptr, bool drop = false,
     const uint32_t *__restrict__ n_dev = nullptr, uint32_t *__restrict__ n_out = nullptr,
-    const uint32_t *__restrict__ kfin = nullptr) {
+    const uint32_t *__restrict__ kfin = nullptr, DevIO io = {}, int q = 0) {
+  if (io.fin) {  // device-selected buffers (DevIO): a constant digit moves nothing
+    if (q > 0 && digit_constant(io.fin, shift, width)) return;
+    const K *ki;
+    const uint32_t *vi;
+    K *ko;
+    uint32_t *vo;
+    dev_io<K>(io, q, ki, vi, ko, vo);
+    kin = ki;
+    vin = vi;
+    kout = ko;
+    vout = vo;
+  }
   // compacting sort: with drop, all-ones keys are left out (pass 0 of the depth sort: culled
   // Gaussians), and block 0 stores the kept count to n_out; later passes sort min(n, *n_dev)
   // keys and the workgroups past them exit at once.
   if (n_dev) {
-    n = min(n, (long long)*n_dev);
+    if (*n_dev > (unsigned long long)n) return;  // capacity overflow (see rts_count_kernel)
+    n = *n_dev;
     if ((long long)blockIdx.x * TPB * ITEMS >= n) return;  // whole workgroup
   }
   if (digit_constant(kfin, shift, width)) {  // every key has the same digit: a stable copy
@@ -518,11 +588,13 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
   }
 }
 
-// constant-digit depth passes only copy (gsplat_debug_depth_key_range: 0 off, 1 from 2^22 keys,
-// 2 always).  The range costs ~8 us (the AND / OR in the first count and a reduction block in
-// its row scan) and a skipped pass saves its ranking, worth it for large sorts only: c5 (4.8M
-// keys) -25 us, c4 (1.1M, no constant digit) +10 us (tools/exp_binning.py, RANGE_LIST).
-int g_key_range = 1;
+// Constant-digit depth passes (gsplat_debug_depth_key_range: 0 off, 1 from 2^22 keys, 2 always,
+// the default).  Round 3 copied the data in such a pass (~8 us of range bookkeeping and copy
+// against a skipped ranking: a loss below 2^22 keys); with the device-selected buffers (DevIO)
+// a constant digit costs its three launches returning at once, and the AND / OR is reduced
+// per wave before its LDS atomics.  The headline's visible depths (2.5-5.5) share their top
+// byte, so one of its four passes drops out.
+int g_key_range = 2;
 bool use_key_range(long long n) { return g_key_range == 2 || (g_key_range == 1 && n >= (1LL << 22)); }
 
 uint32_t *rts_tile_counts(void *ws) { return (uint32_t *)ws + OS_HEAD_WORDS; }
@@ -539,9 +611,15 @@ uint32_t *sort_kept_word(void *ws) { return (uint32_t *)ws + 1; }
 // drop (first_counts_ready then means counts without the all-ones keys): the first pass leaves out all-ones keys, so the sort orders only the kept keys, whose
 // count it stores to sort_kept_word(ws) (the sorted output holds that many; kout may be null).
 __global__ __launch_bounds__(TPB) void bins_decode_kernel(long long T, long long n,
-                                                          int32_t *__restrict__ bins) {
+                                                          int32_t *__restrict__ bins,
+                                                          const uint32_t *__restrict__ n_dev =
+                                                              nullptr) {
   const long long t = (long long)blockIdx.x * TPB + threadIdx.x;
   if (t >= T) return;
+  if (n_dev) {  // the device count of a capacity-launched sort (n: the capacity)
+    if (*n_dev > (unsigned long long)n) return;  // overflow: the table stays cleared
+    n = *n_dev;
+  }
   const int32_t x = bins[2 * t];
   if (x > 0) bins[2 * t] = (int32_t)(n - x);
 }
@@ -550,7 +628,10 @@ template <typename K>
 int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t *vout,
                      long long n, int begin_bit, int end_bit, void *ws, hipStream_t st,
                      bool first_counts_ready = false, int32_t *tile_bins = nullptr,
-                     long long num_tiles = 0, bool drop = false, int first_pass = 0) {
+                     long long num_tiles = 0, bool drop = false, int first_pass = 0,
+                     const uint32_t *n_dev_all = nullptr) {
+  // n_dev_all (not with drop): the key count lives on the device (<= n, the launch capacity;
+  // more than n: overflow, every kernel returns at once) -- the capacity-launched tile sort
   if (n <= 0) return 0;
   const SortPlan p = sort_plan(n, begin_bit, end_bit);
   if (p.passes == 0) {
@@ -571,24 +652,29 @@ int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t
   // first_pass = 1: the caller ran pass 0 itself, into (kb, vb)
   K *kin = first_pass ? kb : ka, *kalt = first_pass ? ka : kb;
   uint32_t *vin = first_pass ? vb : va, *valt = first_pass ? va : vb;
+  // with the key range, the device picks every pass's buffers (DevIO) and constant digits move
+  // nothing (no copy)
+  DevIO io{};
+  if (kr.fin && first_pass == 0)
+    io = DevIO{kr.fin, ka, kb, va, vb, kout, vout, begin_bit, p.width, p.passes};
   for (int q = first_pass; q < p.passes; ++q) {
     const bool last = q == p.passes - 1;
     K *ko = last ? kout : kalt;
     uint32_t *vo = last ? vout : valt;
     // tile digit counts -> row scans -> offsets
     const int sh = begin_bit + q * p.width;
-    const uint32_t *ndev = drop && q > 0 ? kept : nullptr;
+    const uint32_t *ndev = drop ? (q > 0 ? kept : nullptr) : n_dev_all;
     // first_counts_ready: the key kernel wrote pass 0's counts and key ranges (kr.blk)
     if (q == 0 && first_counts_ready) {
     } else if (p.items == 16)
       hipLaunchKernelGGL((rts_count_kernel<K, 16>), dim3((unsigned)p.nblocks), dim3(TPB), 0, st,
-                         kin, n, sh, p.width, p.nblocks, counts, drop && q == 0, ndev, kr, q);
+                         kin, n, sh, p.width, p.nblocks, counts, drop && q == 0, ndev, kr, q, io);
     else if (p.items == 8)
       hipLaunchKernelGGL((rts_count_kernel<K, 8>), dim3((unsigned)p.nblocks), dim3(TPB), 0, st,
-                         kin, n, sh, p.width, p.nblocks, counts, drop && q == 0, ndev, kr, q);
+                         kin, n, sh, p.width, p.nblocks, counts, drop && q == 0, ndev, kr, q, io);
     else
       hipLaunchKernelGGL((rts_count_kernel<K, 4>), dim3((unsigned)p.nblocks), dim3(TPB), 0, st,
-                         kin, n, sh, p.width, p.nblocks, counts, drop && q == 0, ndev, kr, q);
+                         kin, n, sh, p.width, p.nblocks, counts, drop && q == 0, ndev, kr, q, io);
     hipLaunchKernelGGL(rts_rowscan_kernel,
                        dim3((unsigned)p.radix + (q == 0 && kr.blk ? 1u : 0u)), dim3(1024), 0,
                        st, counts, p.nblocks, rowtot, kr, q, sh, p.width);
@@ -596,8 +682,8 @@ int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t
   hipLaunchKernelGGL((os_pass_kernel<K, Wd, It>), dim3((unsigned)p.nblocks), dim3(TPB), 0, st,   \
                      kin, vin, ko, vo, n, sh, p.width, rowtot, counts, p.nblocks,              \
                      last ? tile_bins : nullptr, drop && q == 0,                               \
-                     drop && q > 0 ? kept : nullptr, drop && q == 0 ? kept : nullptr,          \
-                     q > 0 ? kr.fin : nullptr)
+                     ndev, drop && q == 0 ? kept : nullptr,                                    \
+                     q > 0 && !io.fin ? kr.fin : nullptr, io, q)
 #define OS_PASS_W(Wd)                                                                       \
   do {                                                                                      \
     if (p.items == 16) OS_PASS(Wd, 16); else if (p.items == 8) OS_PASS(Wd, 8);             \
@@ -624,7 +710,7 @@ int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t
   }
   if (tile_bins)
     hipLaunchKernelGGL(bins_decode_kernel, dim3(cdiv(num_tiles, TPB)), dim3(TPB), 0, st,
-                       num_tiles, n, tile_bins);
+                       num_tiles, n, tile_bins, n_dev_all);
   return 0;
 }
 
@@ -785,14 +871,16 @@ __global__ __launch_bounds__(TPB) void emit_kernel(int n, const uint32_t *__rest
                                                    int *__restrict__ tile_bins,
                                                    const uint32_t *__restrict__ i_dev = nullptr,
                                                    uint32_t cap = 0) {
-  // pre-launched before the host knows I (gsplat_bin_emit_prelaunch): outputs hold cap slots;
-  // a larger I writes nothing (the host then re-runs the emission into larger buffers)
-  if (i_dev && *i_dev > cap) return;
   // tile_bins starts zeroed for bin_edges_kernel (empty tiles stay (0, 0)): cleared here
-  // instead of by a separate fill launch
+  // instead of by a separate fill launch -- also on an overflow below, so that a blend launched
+  // behind a capacity overflow reads empty tiles, not a stale table
   for (long long i = (long long)blockIdx.x * TPB + threadIdx.x; i < 2LL * tbx * tby;
        i += (long long)gridDim.x * TPB)
     tile_bins[i] = 0;
+  // pre-launched before the host knows I (gsplat_bin_emit_prelaunch / _speculative): outputs
+  // hold cap slots; a larger I writes nothing (the host then re-runs the emission into larger
+  // buffers)
+  if (i_dev && *i_dev > cap) return;
   const int lane = threadIdx.x & 63;
   const long long p0 = ((long long)blockIdx.x * TPB + threadIdx.x) - lane;
   if (p0 >= n) return;  // wave-uniform
@@ -2033,7 +2121,7 @@ extern "C" int gsplat_bin_count_keyed(int num_points, int tile_bounds_x, int til
 // unless the generated first pass is chosen; bucket scheme: count, scan and placement), each
 // checking the device copy of I against cap; TAIL = the rest (the tile sort / the per-tile
 // sorts).  EMIT_ALL = both, with cap = I (gsplat_bin_emit).
-enum { EMIT_HEAD = 1, EMIT_TAIL = 2, EMIT_ALL = 3 };
+enum { EMIT_HEAD = 1, EMIT_TAIL = 2, EMIT_ALL = 3, EMIT_SPEC = 4 };
 
 static bool emit_head_splits(int n, long long cap, long long T) {
   if (use_bucket(n, T)) return true;
@@ -2103,7 +2191,7 @@ static int bin_emit_impl(int num_points, int64_t num_intersects, int64_t capacit
               workspace2_bytes, p1.bytes, p2.bytes);
     return 1;
   }
-  if (num_points == 0 || (phase != EMIT_HEAD && num_intersects == 0)) {
+  if (num_points == 0 || (phase != EMIT_HEAD && phase != EMIT_SPEC && num_intersects == 0)) {
     if (tail)
       note(hipMemsetAsync(tile_bins, 0, (size_t)T * 2 * sizeof(int32_t), st), "hipMemsetAsync");
     return check_launch("bin_emit");
@@ -2132,6 +2220,17 @@ static int bin_emit_impl(int num_points, int64_t num_intersects, int64_t capacit
                                (uint32_t *)gaussian_ids_sorted, I, 0, bits_for(T), p2.rs_ws, st,
                                false, tile_bins, T, false, 1);
     return check_launch("bin_emit");
+  }
+  if (phase == EMIT_SPEC) {
+    // the whole emission and tile sort at the capacity, I read on the device (p1.dcount): no
+    // host read of I before the blend is launched behind it (rasterize.SpeculativeBinning)
+    hipLaunchKernelGGL(emit_kernel, dim3(cdiv(n, TPB)), dim3(TPB), 0, st, n, p1.order, p1.cnt,
+                       p1.off, p1.box, tile_bounds_x, tile_bounds_y, p2.tk_a, p2.tv_a, tile_bins,
+                       p1.dcount, (uint32_t)cap);
+    radix_sort_pairs<uint32_t>(p2.tk_a, p2.tv_a, p2.tk_b, p2.tv_b, nullptr,
+                               (uint32_t *)gaussian_ids_sorted, cap, 0, bits_for(T), p2.rs_ws,
+                               st, false, tile_bins, T, false, 0, p1.dcount);
+    return check_launch("bin_emit_speculative");
   }
   if (head)
     hipLaunchKernelGGL(emit_kernel, dim3(cdiv(n, TPB)), dim3(TPB), 0, st, n, p1.order, p1.cnt,
@@ -2174,6 +2273,28 @@ extern "C" int gsplat_bin_emit_finish(int num_points, int64_t num_intersects, in
   return bin_emit_impl(num_points, num_intersects, capacity, tile_bounds_x, tile_bounds_y,
                        gaussian_ids_sorted, tile_bins, workspace1, workspace1_bytes, workspace2,
                        workspace2_bytes, stream, EMIT_TAIL);
+}
+
+// The emission and the whole tile sort launched at a capacity before the host knows I (the
+// device count decides; I > capacity leaves the table cleared and the ids unwritten, and the
+// caller re-bins).  Returns 2 without launching anything where the scheme needs I on the host
+// (tile buckets; the generated first tile pass, I >= 2^24): use prelaunch / finish there.
+extern "C" int gsplat_bin_emit_speculative(int num_points, int64_t capacity, int tile_bounds_x,
+                                           int tile_bounds_y, int32_t *gaussian_ids_sorted,
+                                           int32_t *tile_bins, const void *workspace1,
+                                           size_t workspace1_bytes, void *workspace2,
+                                           size_t workspace2_bytes, void *stream) {
+  const long long T = (long long)tile_bounds_x * tile_bounds_y;
+  if (num_points > 0 && T > 0 && capacity > 0 &&
+      (use_bucket(num_points, T) || use_emit_pass0(capacity)))
+    return 2;
+  if (capacity <= 0) {
+    set_error("bin_emit_speculative: capacity must be positive");
+    return 1;
+  }
+  return bin_emit_impl(num_points, 0, capacity, tile_bounds_x, tile_bounds_y,
+                       gaussian_ids_sorted, tile_bins, workspace1, workspace1_bytes, workspace2,
+                       workspace2_bytes, stream, EMIT_SPEC);
 }
 
 extern "C" int gsplat_map_gaussian_to_intersects(int num_points, const float *xys,

@@ -33,7 +33,8 @@ from torch.autograd import Function
 
 from . import _lib, exchange, quirks
 from .camera import GCCamera
-from .rasterize import BLOCK_X, BLOCK_Y, bin_gaussians, last_num_visible
+from .rasterize import (BLOCK_X, BLOCK_Y, bin_gaussians, bin_gaussians_speculative,
+                        last_num_visible)
 
 _DEG_OF_BASES = {1: 0, 4: 1, 9: 2, 16: 3, 25: 4}
 
@@ -75,9 +76,52 @@ class _FusedRender(Function):
                   float(fx), float(fy), float(cx), float(cy), H, W, tbx, tby, 0.01, P(xys),
                   P(depths), P(radii), P(conics), P(nth), P(colors), P(opac), P(ws1),
                   ws1.numel(), st)
-        num_intersects, gids, bins = bin_gaussians(xys, depths, radii, nth, H, W,
-                                                   keyed_workspace=ws1)
+        # The binning's emission and tile sort are launched at this frame shape's capacity
+        # without the host read of I (rasterize.SpeculativeBinning), the blend right behind
+        # them; the host reads I only then, while the GPU works, and re-bins on an overflow.
+        spec = bin_gaussians_speculative(xys, depths, radii, nth, H, W, keyed_workspace=ws1)
+        if spec is None:  # first call of this frame shape (or nothing to bin)
+            num_intersects, gids, bins = bin_gaussians(xys, depths, radii, nth, H, W,
+                                                       keyed_workspace=ws1)
+            layout_i = num_intersects
+        else:
+            num_intersects, gids, bins = None, spec.ids, spec.tile_bins
+            layout_i = spec.layout_intersects
+        visible_hint = last_num_visible(dev)
         chunk, plan = 0, None
+
+        def blend(gids, bins, layout_i):
+            """The blend (it also clears the gradient records the backward accumulates into and
+            fills the list-split plan, whose layout follows layout_i)."""
+            nonlocal chunk, plan
+            chunk = _lib.query("gsplat_rasterize_chunk_size", tbx, tby, layout_i) \
+                if need_grad else 0
+            plan = None
+            if chunk > 0:  # the list-split backward's plan (filled by the blend's waves)
+                plan = torch.empty((_lib.query("gsplat_rasterize_split_bytes", tbx, tby,
+                                               layout_i, chunk),),
+                                   device=dev, dtype=torch.uint8)
+            _lib.call("gsplat_rasterize_forward_clearing", tbx, tby, H, W, P(gids), P(bins),
+                      P(xys), P(conics), P(colors), P(opac), P(background), P(out_img),
+                      P(final_Ts), P(final_idx), P(rec), rec.numel() if rec is not None else 0,
+                      # skip culled Gaussians' records when many are culled (real scenes);
+                      # at ~all visible the radii loads cost more than the stores they save
+                      P(radii) if rec is not None and visible_hint < 0.9 * n else None,
+                      layout_i, chunk, P(plan), plan.numel() if plan is not None else 0, st)
+
+        out_img = torch.empty((H, W, 3), **f32)
+        final_Ts = torch.empty((H, W), **f32)
+        final_idx = torch.empty((H, W), device=dev, dtype=torch.int32)
+        if spec is not None:
+            blend(gids, bins, layout_i)
+            if not spec.finish():  # I > capacity: the blend saw empty tiles; bin and blend again
+                gids, bins = spec.rebin()
+                layout_i = spec.layout_intersects
+                blend(gids, bins, layout_i)
+            num_intersects = spec.num_intersects
+            gids = gids[:num_intersects]
+        elif num_intersects >= 1:
+            blend(gids, bins, layout_i)
         if num_intersects < 1:
             # nothing visible: the background (the caller returns it at gc_model.py:189-190),
             # and every gradient is zero
@@ -86,27 +130,9 @@ class _FusedRender(Function):
             final_idx = torch.zeros(H, W, device=dev, dtype=torch.int32)
             if rec is not None:
                 rec.zero_()
-        else:
-            out_img = torch.empty((H, W, 3), **f32)
-            final_Ts = torch.empty((H, W), **f32)
-            final_idx = torch.empty((H, W), device=dev, dtype=torch.int32)
-            chunk = _lib.query("gsplat_rasterize_chunk_size", tbx, tby, num_intersects) \
-                if need_grad else 0
-            if chunk > 0:  # the list-split backward's plan (filled at the backward's start)
-                plan = torch.empty((_lib.query("gsplat_rasterize_split_bytes", tbx, tby,
-                                               num_intersects, chunk),),
-                                   device=dev, dtype=torch.uint8)
-            # the blend kernel also clears the gradient records the backward accumulates into
-            _lib.call("gsplat_rasterize_forward_clearing", tbx, tby, H, W, P(gids), P(bins),
-                      P(xys), P(conics), P(colors), P(opac), P(background), P(out_img),
-                      P(final_Ts), P(final_idx), P(rec), rec.numel() if rec is not None else 0,
-                      # skip culled Gaussians' records when many are culled (real scenes);
-                      # at ~all visible the radii loads cost more than the stores they save
-                      P(radii) if rec is not None and last_num_visible(dev) < 0.9 * n else None,
-                      # the list-split plan's walk table, filled by the blend's waves
-                      num_intersects, chunk, P(plan), plan.numel() if plan is not None else 0, st)
+            chunk, plan = 0, None
         ctx.meta = (n, K, int(degrees_to_use), float(fx), float(fy), float(cx), float(cy), H, W,
-                    tbx, tby, num_intersects, chunk)
+                    tbx, tby, num_intersects, chunk, layout_i)
         ctx.plan, ctx.rec = plan, rec
         ctx.opac_shape = opacities.shape
         ctx.exchange = exchange.active() if K > 1 else None
@@ -141,7 +167,7 @@ class _FusedRender(Function):
         (means, scales, quats, opacities, features_dc, features_rest, viewmat, projmat, campos,
          background, xys, radii, conics, colors, opac, gids, bins, final_Ts,
          final_idx) = ctx.saved_tensors
-        n, K, dtu, fx, fy, cx, cy, H, W, tbx, tby, I, chunk = ctx.meta
+        n, K, dtu, fx, fy, cx, cy, H, W, tbx, tby, I, chunk, layout_i = ctx.meta
         dev = means.device
         P, st = _lib.ptr, _lib.stream(dev)
         rec = ctx.rec
@@ -152,7 +178,8 @@ class _FusedRender(Function):
                 v_alpha = v_alpha.float().contiguous()
             _lib.call("gsplat_rasterize_backward_records", tbx, tby, H, W, n, P(gids), P(bins),
                       P(xys), P(conics), P(colors), P(opac), P(background), P(final_Ts),
-                      P(final_idx), P(v_img), P(v_alpha), quirks.backward_alpha_clamp(), I, chunk,
+                      P(final_idx), P(v_img), P(v_alpha), quirks.backward_alpha_clamp(),
+                      layout_i if chunk > 0 else I, chunk,
                       P(ctx.plan), ctx.plan.numel() if ctx.plan is not None else 0,
                       int(ctx.plan is not None), P(rec), rec.numel(), st)
         if ctx.adam is not None:

@@ -14,6 +14,7 @@ RGB, depth and alpha from one binning and one traversal.
 """
 from __future__ import annotations
 
+import os
 import time
 import weakref
 from typing import Optional
@@ -203,8 +204,114 @@ def bin_gaussians(xys: Tensor, depths: Tensor, radii: Tensor, num_tiles_hit: Ten
     return num_intersects, ids_buf[:max(num_intersects, 0)], tile_bins
 
 
+class SpeculativeBinning:
+    """A binning whose emission and tile sort were launched at a capacity before the host knew
+    the intersection count I (gsplat_bin_emit_speculative): the caller launches the blend right
+    behind it and calls finish() only then, so the GPU never idles at the host's read of I.
+
+    ids (capacity slots; [0, I) valid) and tile_bins are the binning's outputs once finish()
+    returns True; False means I exceeded the capacity -- the table was left all-zero (the blend
+    behind it rendered the background) and the caller re-bins with rebin() and re-launches.
+    `layout_intersects` is the count the list-split plan layout must use (both the forward that
+    fills a plan and its backward): the capacity, known before I."""
+
+    def __init__(self, dev, n, tbx, tby, ws1, slot, counts, host, key, cap, ids, ws2,
+                 tile_bins):
+        self.dev, self.n, self.tbx, self.tby = dev, n, tbx, tby
+        self.ws1, self.slot, self.counts, self.host, self.key = ws1, slot, counts, host, key
+        self.cap, self.ids, self.ws2, self.tile_bins = cap, ids, ws2, tile_bins
+        self.layout_intersects = cap
+        self.num_intersects = None
+
+    def finish(self) -> bool:
+        visible = None
+        try:
+            I = _wait_count(self.host, torch.cuda.current_stream(self.dev))
+            visible = int(self.host[0])
+        finally:
+            _COUNTS.release(self.dev, self.slot, visible)
+        self.num_intersects = I
+        _EMIT_CAP[self.key] = emit_capacity(I)
+        return I <= self.cap
+
+    def rebin(self):
+        """After an overflow: the emission and tile sort for the exact I (phase 1's workspace is
+        untouched by the speculative launch) -> (ids [I], tile_bins)."""
+        I = self.num_intersects
+        P, st = _lib.ptr, _lib.stream(self.dev)
+        ids_buf, ws2 = _emit_buffers(self.dev, self.n, I, self.tbx, self.tby)
+        _lib.call("gsplat_bin_emit", self.n, I, self.tbx, self.tby, P(ids_buf),
+                  P(self.tile_bins), P(self.ws1), self.ws1.numel(), P(ws2), ws2.numel(), st)
+        self.ids, self.ws2, self.cap = ids_buf, ws2, I
+        self.layout_intersects = I
+        return ids_buf[:I], self.tile_bins
+
+
+def bin_gaussians_speculative(xys: Tensor, depths: Tensor, radii: Tensor, num_tiles_hit: Tensor,
+                              img_height: int, img_width: int,
+                              keyed_workspace: Optional[Tensor] = None):
+    """bin_gaussians without the host read of I in the middle: the count phase, then -- when
+    this frame shape's capacity is known from an earlier call and the binning scheme allows it
+    -- the emission and the whole tile sort at that capacity (gsplat_bin_emit_speculative).
+    Returns a SpeculativeBinning (finish() before using I), or None when the capacity is not
+    known yet or the scheme needs I on the host (the caller then uses bin_gaussians)."""
+    n = xys.shape[0]
+    tbx = (img_width + BLOCK_X - 1) // BLOCK_X
+    tby = (img_height + BLOCK_Y - 1) // BLOCK_Y
+    dev = xys.device
+    key = (dev, n, tbx, tby)
+    cap = _EMIT_CAP.get(key, 0)
+    if n == 0 or cap <= 0 or keyed_workspace is None or not SPECULATIVE_BINNING:
+        return None
+    _lib.check_device("bin_gaussians_speculative", xys, depths, radii, num_tiles_hit)
+    P, st = _lib.ptr, _lib.stream(dev)
+    ws1 = keyed_workspace
+    tile_bins = torch.empty((tbx * tby, 2), device=dev, dtype=torch.int32)
+    ids_buf, ws2 = _emit_buffers(dev, n, cap, tbx, tby)
+    slot, counts, host = _COUNTS.acquire(dev)
+    try:
+        _lib.call("gsplat_bin_count_keyed", n, tbx, tby, P(counts), P(ws1), ws1.numel(), st)
+        rc = _lib.lib().gsplat_bin_emit_speculative(n, cap, tbx, tby, P(ids_buf), P(tile_bins),
+                                                    P(ws1), ws1.numel(), P(ws2), ws2.numel(), st)
+        if rc == 2:  # the scheme needs I on the host: finish as bin_gaussians does
+            pre = (ids_buf, ws2)
+            if PRELAUNCH_EMISSION:
+                _lib.call("gsplat_bin_emit_prelaunch", n, cap, tbx, tby, P(tile_bins), P(ws1),
+                          ws1.numel(), P(ws2), ws2.numel(), st)
+            I = _wait_count(host, torch.cuda.current_stream(dev))
+            _COUNTS.release(dev, slot, int(host[0]))
+            slot = None
+            _EMIT_CAP[key] = emit_capacity(I)
+            if I <= cap:
+                _lib.call("gsplat_bin_emit_finish", n, I, cap, tbx, tby, P(pre[0]), P(tile_bins),
+                          P(ws1), ws1.numel(), P(pre[1]), pre[1].numel(), st)
+                ids_buf, ws2 = pre
+            else:
+                ids_buf, ws2 = _emit_buffers(dev, n, I, tbx, tby)
+                _lib.call("gsplat_bin_emit", n, I, tbx, tby, P(ids_buf), P(tile_bins), P(ws1),
+                          ws1.numel(), P(ws2), ws2.numel(), st)
+            done = SpeculativeBinning(dev, n, tbx, tby, ws1, None, None, None, key,
+                                      max(I, cap), ids_buf, ws2, tile_bins)
+            done.num_intersects = I
+            done.layout_intersects = I
+            done.finish = lambda: True
+            return done
+        if rc != 0:
+            raise RuntimeError("gsplat_bin_emit_speculative failed: " +
+                               _lib.lib().gsplat_last_error().decode(errors="replace"))
+    except BaseException:
+        if slot is not None:
+            _COUNTS.release(dev, slot)
+        raise
+    return SpeculativeBinning(dev, n, tbx, tby, ws1, slot, counts, host, key, cap, ids_buf, ws2,
+                              tile_bins)
+
+
 # frame shape -> the intersection capacity to pre-allocate the emission's outputs for
 _EMIT_CAP = {}
+# the fused render bins speculatively (bin_gaussians_speculative); GSPLAT_MI355X_SPECULATIVE=0
+# turns it off (A/B runs)
+SPECULATIVE_BINNING = os.environ.get("GSPLAT_MI355X_SPECULATIVE", "1") != "0"
 # the C ABI's bound on an emission capacity (bin_emit_impl rejects larger ones)
 EMIT_CAP_MAX = 0x3FFFFFFF
 

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define GSPLAT_MI355X_ABI_VERSION 12
+#define GSPLAT_MI355X_ABI_VERSION 13
 
 int gsplat_abi_version(void);
 const char *gsplat_last_error(void);
@@ -218,6 +218,21 @@ int gsplat_bin_emit_finish(int num_points, int64_t num_intersects, int64_t capac
                            int tile_bounds_x, int tile_bounds_y, int32_t *gaussian_ids_sorted,
                            int32_t *tile_bins, const void *workspace1, size_t workspace1_bytes,
                            void *workspace2, size_t workspace2_bytes, void *stream);
+/* The whole of phase 2 before the host knows I: the emission AND the tile sort launched for
+ * `capacity` intersections, each kernel reading the device-side I (phase 1's) -- so the blend
+ * can be launched right behind it and the host reads I (d_counts[1]) only afterwards, while the
+ * GPU works.  I <= capacity: gaussian_ids_sorted[0, I) and tile_bins are gsplat_bin_emit's
+ * exactly.  I > capacity: nothing is emitted or sorted and tile_bins is left all-zero (a blend
+ * behind it renders the background and touches no id); the caller re-bins into buffers sized
+ * for I.  Buffers as for gsplat_bin_emit_prelaunch.  Returns 2 (nothing launched) when the
+ * binning scheme for (num_points, tiles, capacity) needs I on the host -- the small-scene tile
+ * buckets or the generated first tile pass (capacity >= 2^24): use prelaunch + finish there.
+ * Replaces, like gsplat_bin_emit, gsplat 0.1.2.1 rasterize.py's map / sort / bin edges. */
+int gsplat_bin_emit_speculative(int num_points, int64_t capacity, int tile_bounds_x,
+                                int tile_bounds_y, int32_t *gaussian_ids_sorted,
+                                int32_t *tile_bins, const void *workspace1,
+                                size_t workspace1_bytes, void *workspace2, size_t workspace2_bytes,
+                                void *stream);
 
 /* ---- rasterization (forward.cu rasterize_forward, backward.cu rasterize_backward) -----
  * colors [N,C], opacity [N] (or [N,1]), background [C]; out_img [H,W,C], final_Ts [H,W],

@@ -51,7 +51,8 @@ def headline(request, gpu, oracle_lib):
                 colors=colors, opac=opac, config=request.param)
 
 
-@pytest.mark.parametrize("scheme", ["shipped", "norange", "range", "gen", "emit", "bucket"])
+@pytest.mark.parametrize("scheme", ["shipped", "norange", "range22", "gen", "emit",
+                                    "bucket"])
 def test_headline_binning_bitexact(gpu, headline, scheme):
     """Binning bit-exact at full size: the shipped dispatch (for these scenes the depth sort of
     8-bit reduce-then-scan passes compacting the culled Gaussians away, constant-digit passes
@@ -65,16 +66,18 @@ def test_headline_binning_bitexact(gpu, headline, scheme):
     if scheme != "shipped" and h["config"] in ("c4", "c5"):
         pytest.skip("the other dispatches: headline and c3 only")
     L = _lib.lib()
-    L.gsplat_debug_binning_scheme(1 if scheme == "bucket" else -1)
-    L.gsplat_debug_emit_pass0({"emit": 0, "gen": 2}.get(scheme, 1))
-    L.gsplat_debug_depth_key_range({"norange": 0, "range": 2}.get(scheme, 1))
+    # (-1: leave the shipped setting; each call returns the previous one)
+    prev = (L.gsplat_debug_binning_scheme(1 if scheme == "bucket" else -1),
+            L.gsplat_debug_emit_pass0({"emit": 0, "gen": 2}.get(scheme, -1)),
+            L.gsplat_debug_depth_key_range({"norange": 0, "range": 2, "range22": 1}
+                                           .get(scheme, -1)))
     try:
         I, gids, bins = bin_gaussians(h["xys"], h["depths"], h["radii"], h["nth"], cam.height,
                                       cam.width)
     finally:
-        L.gsplat_debug_binning_scheme(-1)
-        L.gsplat_debug_emit_pass0(1)
-        L.gsplat_debug_depth_key_range(1)
+        L.gsplat_debug_binning_scheme(prev[0])
+        L.gsplat_debug_emit_pass0(prev[1])
+        L.gsplat_debug_depth_key_range(prev[2])
     assert I == h["ref"]["num_intersects"]
     np.testing.assert_array_equal(_np(gids), h["ref"]["gaussian_ids_sorted"])
     np.testing.assert_array_equal(_np(bins), h["ref"]["tile_bins"])

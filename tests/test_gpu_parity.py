@@ -242,11 +242,14 @@ def test_binning_prelaunched_emission(gpu, scheme):
         R._EMIT_CAP.pop(key, None)
 
 
-@pytest.mark.parametrize("fixed", [(0x5A00, 0xFF00), (0x5A5A00, 0xFFFF00), (0x0, 0x0)])
+@pytest.mark.parametrize("fixed", [(0x5A00, 0xFF00), (0x5A0000, 0xFF0000),
+                                   (0x5A5A00, 0xFFFF00), (0x0, 0x0)])
 def test_binning_depth_key_range(gpu, fixed):
-    """Depth keys whose bytes 1 (and 2) are the same for every visible Gaussian: those LSD
-    passes are identities and only copy (gsplat_debug_depth_key_range), also in the middle of
-    the pass sequence -- bit-exact vs the oracle with and without the shortcut."""
+    """Depth keys whose bytes 1 (and 2) are the same for every visible Gaussian (byte 3 always
+    is here): those LSD passes move nothing (gsplat_debug_depth_key_range; the device picks
+    every pass's buffers, DevIO), also in the middle of the pass sequence, and with only pass 0
+    moving (it then writes the sorted output itself) -- bit-exact vs the oracle with and without
+    the shortcut.  The sorted scheme is forced (20k Gaussians would take the tile buckets)."""
     sc, cam, scales, quats = _inputs(20000, 512, 512, 2, 0.003, 0.03, 1.5)
     g, o = _project_both(gpu, sc, cam, scales, quats)
     xys, depths, radii, conics, nth, cov3d = [t.detach() for t in g]
@@ -258,11 +261,13 @@ def test_binning_depth_key_range(gpu, fixed):
     L = _lib.lib()
     for on in (2, 0):
         prev = L.gsplat_debug_depth_key_range(on)
+        prev_s = L.gsplat_debug_binning_scheme(0)
         try:
             I, gids, bins = bin_gaussians(xys, torch.from_numpy(d).to(gpu), radii, nth,
                                           cam.height, cam.width)
         finally:
             L.gsplat_debug_depth_key_range(prev)
+            L.gsplat_debug_binning_scheme(prev_s)
         assert I == ref["num_intersects"]
         np.testing.assert_array_equal(_np(gids), ref["gaussian_ids_sorted"])
         np.testing.assert_array_equal(_np(bins), ref["tile_bins"])
