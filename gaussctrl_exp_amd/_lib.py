@@ -95,6 +95,12 @@ SIGNATURES = {
     "gsplat_grad_records_split": (_I, [_I, _P, _SZ, _P, _P, _P, _P, _P, _P, _P]),
     "gsplat_rasterize_backward_records": (_I, [_I] * 5 + [_P] * 11 + [_F, _I64, _I, _P, _SZ,
                                                                        _I, _P, _SZ, _P]),
+    "gsplat_rasterize_l1_partials_bytes": (_SZ, [_I, _I]),
+    "gsplat_rasterize_forward_clearing_l1": (_I, [_I, _I, _I, _I] + [_P] * 10 +
+                                             [_P, _SZ, _P, _I64, _I, _P, _SZ] +
+                                             [_P, _I, _P, _SZ, _P, _P]),
+    "gsplat_rasterize_backward_records_l1": (_I, [_I] * 5 + [_P] * 9 + [_P, _P, _I, _P] +
+                                             [_F, _I64, _I, _P, _SZ, _I, _P, _SZ, _P]),
 }
 
 ABI_VERSION = 13  # include/gsplat_mi355x.h GSPLAT_MI355X_ABI_VERSION

@@ -356,6 +356,15 @@ __global__ __launch_bounds__(256) void l1_ssim_bwd_kernel(
 }
 
 }  // namespace
+
+// The loss of per-wave / per-block L1 partials (two floats each, the second zero) written by
+// another kernel -- the fused-L1 blend (raster.hip): loss = inv_n * sum, summed in double.
+void launch_l1_finalize(hipStream_t st, int nparts, const float *partials, double inv_n,
+                        float *loss) {
+  hipLaunchKernelGGL(l1_ssim_finalize_kernel, dim3(1), dim3(256), 0, st, nparts, partials, inv_n,
+                     0.0, 0.f, loss);
+}
+
 }  // namespace gs
 
 using namespace gs;

@@ -652,6 +652,40 @@ constexpr int tiles_per_block() {
   return 4 / ((GS_BLOCK / COLS) * (GS_BLOCK / ((64 / COLS) * PXL)));
 }
 
+// ---- the fused L1 loss (gsplat_rasterize_forward_clearing_l1 / _backward_records_l1) ----
+// The training step's photometric loss mean |clamp(pred, max=1) - gt| (gc_model.py:222's clamp,
+// splatfacto's L1 with ssim_lambda = 0) folded into the blend kernels: the forward's waves sum
+// |clamp(pred) - gt| over their pixels into per-wave partials (the loss is their double sum,
+// loss.hip's finalize), and the backward forms each pixel's upstream gradient itself instead
+// of reading v_out -- exactly loss.hip l1_only_bwd_kernel's arithmetic, so the gradients equal
+// the unfused step's bit for bit: gl = grad_loss * (1/n), v = gl * sign(clamp(p) - g) * mask,
+// mask = (p <= 1) (torch's clamp backward; clamp keeps a NaN, the mask drops it).
+struct L1Grad {
+  const float *pred, *gt, *grad_loss;  // pred: the forward's raw image; null: read v_out
+  float scale;                         // 1 / (3 H W)
+  int clamp;
+};
+__device__ __forceinline__ float l1_clampv(float x, int clamp) { return clamp && x > 1.f ? 1.f : x; }
+__device__ __forceinline__ float l1_grad1(float gl, float p, float g, int clamp) {
+  const float d = l1_clampv(p, clamp) - g;
+  const float m = clamp ? (p <= 1.f ? 1.f : 0.f) : 1.f;
+  return gl * (d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f)) * m;
+}
+// pixel pix's upstream colour gradient: v_out's, or the fused L1 loss's
+__device__ __forceinline__ void upstream_rgb(const L1Grad &l1, const float *__restrict__ v_out,
+                                             int pix, float &r, float &g, float &b) {
+  if (l1.pred) {
+    const float gl = l1.grad_loss[0] * l1.scale;
+    r = l1_grad1(gl, l1.pred[3 * pix], l1.gt[3 * pix], l1.clamp);
+    g = l1_grad1(gl, l1.pred[3 * pix + 1], l1.gt[3 * pix + 1], l1.clamp);
+    b = l1_grad1(gl, l1.pred[3 * pix + 2], l1.gt[3 * pix + 2], l1.clamp);
+  } else {
+    r = v_out[3 * pix];
+    g = v_out[3 * pix + 1];
+    b = v_out[3 * pix + 2];
+  }
+}
+
 // ---------------------------------------------------------------- forward, C = 3
 // Two staged Gaussians per iteration (PXL pixels per lane, branch-free): both Gaussians'
 // sigma / exp / alpha are independent and evaluated together; only the transmittance
@@ -673,7 +707,8 @@ __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
     float4 *__restrict__ zero = nullptr,
     long long zero_n = 0, const int *__restrict__ zero_radii = nullptr,
     int *__restrict__ tile_last = nullptr, unsigned long long *__restrict__ kbits = nullptr,
-    long long kbw = 0) {
+    long long kbw = 0, const float *__restrict__ l1_gt = nullptr,
+    float *__restrict__ l1_part = nullptr, int l1_clamp = 0) {
   // Side job: clear a buffer (the fused path's gradient records) with the memory bandwidth the
   // VALU-bound blend leaves idle -- a grid-stride sweep of coalesced 16-B stores, issued by each
   // wave as it finishes (issued first, the blend's first load wait would also wait for them:
@@ -691,9 +726,15 @@ __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
   constexpr int WPT = (GS_BLOCK / COLS) * (GS_BLOCK / ((64 / COLS) * PXL));
   static_assert(WPT == SPLIT_WAVES, "one walk-table entry per wave of a tile");
   const int wt = (threadIdx.x >> 6) % WPT;
+  // the fused L1 loss's per-wave partial (l1_part[2 w], l1_part[2 w + 1] = 0: loss.hip's layout)
+  const long long l1_w = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (!R.live) {  // wave-uniform
     if (tile_last && R.tile < tbx * tby && (threadIdx.x & 63) == 0)
       tile_last[WPT * R.tile + wt] = -1;
+    if (l1_part && (threadIdx.x & 63) == 0) {
+      l1_part[2 * l1_w] = 0.f;
+      l1_part[2 * l1_w + 1] = 0.f;
+    }
     clear_side_job();
     return;
   }
@@ -819,6 +860,24 @@ __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
       if (DEPTH) out_depth[pix] = cd[k] + T[k] * 0.f;  // the depth render's zero background
     }
   }
+  if (l1_part) {  // sum |clamp(pred) - gt| over the wave's pixels (fixed order: deterministic)
+    float acc = 0.f;
+#pragma unroll
+    for (int k = 0; k < PXL; ++k) {
+      const int i = i0 + LROWS * k;
+      if (i < H && j < W) {
+        const int pix = i * W + j;
+        acc += fabsf(l1_gt[3 * pix] - l1_clampv(cr[k] + T[k] * bg0, l1_clamp)) +
+               fabsf(l1_gt[3 * pix + 1] - l1_clampv(cg[k] + T[k] * bg1, l1_clamp)) +
+               fabsf(l1_gt[3 * pix + 2] - l1_clampv(cb[k] + T[k] * bg2, l1_clamp));
+      }
+    }
+    acc = wave_sum(acc);
+    if (lane == 0) {
+      l1_part[2 * l1_w] = acc;
+      l1_part[2 * l1_w + 1] = 0.f;
+    }
+  }
   if (tile_last) {
     int m = -1;
 #pragma unroll
@@ -861,7 +920,7 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
     int chunk = 0, const int2 *__restrict__ items = nullptr,
     const int *__restrict__ n_items = nullptr, unsigned long long *__restrict__ det = nullptr,
     const unsigned long long *__restrict__ kbits = nullptr, long long kbw = 0,
-    const int *__restrict__ tile_last = nullptr) {
+    const int *__restrict__ tile_last = nullptr, L1Grad l1 = {}) {
   constexpr int PXL = 2 * NP;
   constexpr int LROWS = 64 / COLS;
   int ctile = -1, part = 0;
@@ -893,9 +952,7 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
       const int pix = i * W + j;
       Tf = final_Ts[pix];
       bf = final_idx[pix];
-      r = v_out[3 * pix];
-      g = v_out[3 * pix + 1];
-      bl = v_out[3 * pix + 2];
+      upstream_rgb(l1, v_out, pix, r, g, bl);
       a = v_out_alpha ? v_out_alpha[pix] : 0.f;
     }
     // v_alpha's background/alpha terms: Tf/(1-alpha) * (v_alpha_out - bg . v_out)
@@ -1134,7 +1191,7 @@ __global__ __launch_bounds__(256) void raster_bwd8_kernel(
     int chunk = 0, const int2 *__restrict__ items = nullptr,
     const int *__restrict__ n_items = nullptr, unsigned long long *__restrict__ det = nullptr,
     const unsigned long long *__restrict__ kbits = nullptr, long long kbw = 0,
-    const int *__restrict__ tile_last = nullptr) {
+    const int *__restrict__ tile_last = nullptr, L1Grad l1 = {}) {
   int ctile = -1, part = 0;
   if (SPLIT) {
     const int slot = wave_slot<1, 8>();
@@ -1157,9 +1214,7 @@ __global__ __launch_bounds__(256) void raster_bwd8_kernel(
     const int pix = i * W + j;
     T = final_Ts[pix];
     bf = final_idx[pix];
-    vr = v_out[3 * pix];
-    vg = v_out[3 * pix + 1];
-    vb = v_out[3 * pix + 2];
+    upstream_rgb(l1, v_out, pix, vr, vg, vb);
     const float a = v_out_alpha ? v_out_alpha[pix] : 0.f;
     // v_alpha's background / alpha-output terms: T_final / (1 - alpha) * (v_alpha_out - bg . v)
     Qs = T * (a - (background[0] * vr + background[1] * vg + background[2] * vb));
@@ -1728,13 +1783,15 @@ static void launch_fwd(hipStream_t st, int tbx, int tby, int H, int W, const int
                        float *out_img, float *final_Ts, int32_t *final_idx, const float *depths,
                        float *out_depth, float4 *zero, long long zn, const int32_t *zero_radii,
                        int *tile_last = nullptr, unsigned long long *kbits = nullptr,
-                       long long kbw = 0) {
+                       long long kbw = 0, const float *l1_gt = nullptr, float *l1_part = nullptr,
+                       int l1_clamp = 0) {
   const unsigned grid = cdiv((long long)tbx * tby, (tiles_per_block<1, 8>()));
 #define FWDK(CNT, PF)                                                                      \
   hipLaunchKernelGGL((raster_fwd3u_kernel<1, 8, DEPTH, CNT, PF>), dim3(grid), dim3(256), 0, st, \
                      tbx, tby, H, W, gids, (const int2 *)bins, (const float2 *)xys, conics,     \
                      colors, opacity, background, out_img, final_Ts, final_idx, depths,         \
-                     out_depth, zero, zn, zero_radii, tile_last, kbits, kbw)
+                     out_depth, zero, zn, zero_radii, tile_last, kbits, kbw, l1_gt, l1_part,    \
+                     l1_clamp)
   const bool pf = pipelined_staging(tbx, tby);
   if (!DEPTH && g_pair_count_on) {
     if (pf) FWDK(true, true); else FWDK(true, false);
@@ -1865,7 +1922,7 @@ static void launch_bwd(hipStream_t st, int tbx, int tby, int H, int W, int n,
                        const float *background, const float *final_Ts, const int32_t *final_idx,
                        const float *v_output, const float *v_output_alpha, float alpha_max,
                        float *rec, int chunk, const SplitWs *w, unsigned long long *det,
-                       bool work_ready = false, bool kbits_ready = false) {
+                       bool work_ready = false, bool kbits_ready = false, L1Grad l1 = {}) {
   const long long slots = w ? w->items_bound : (long long)tbx * tby;
   const int2 *its = w ? w->items : nullptr;
   const int *ni = w ? w->n_items : nullptr;
@@ -1890,7 +1947,7 @@ static void launch_bwd(hipStream_t st, int tbx, int tby, int H, int W, int n,
   hipLaunchKernelGGL((raster_bwd8_kernel<CH, DET, CNT, KB>), dim3(grid), dim3(256), 0, st, tbx,  \
                      tby, H, W, gids, (const int2 *)bins, (const float2 *)xys, conics, colors,  \
                      opacity, background, final_Ts, final_idx, v_output, v_output_alpha,        \
-                     alpha_max, rec, chunk, its, ni, det, kbits, kbw, tl)
+                     alpha_max, rec, chunk, its, ni, det, kbits, kbw, tl, l1)
     if (w && kb) {
       if (det) BWD8(true, true, false, true); else if (cnt) BWD8(true, false, true, true);
       else BWD8(true, false, false, true);
@@ -1910,7 +1967,7 @@ static void launch_bwd(hipStream_t st, int tbx, int tby, int H, int W, int n,
                      dim3(256), 0, st, tbx, tby, H, W, gids, (const int2 *)bins,                \
                      (const float2 *)xys, conics, colors, opacity, background, final_Ts,        \
                      final_idx, v_output, v_output_alpha, alpha_max, rec, chunk, its, ni, det,  \
-                     kbits, kbw, tl)
+                     kbits, kbw, tl, l1)
     if (w && kb) {
       if (det) BWDS(true, true, false, true); else if (cnt) BWDS(true, false, true, true);
       else BWDS(true, false, false, true);
@@ -1936,7 +1993,7 @@ static int backward_into_records(const char *who, hipStream_t st, int tbx, int t
                                  const float *v_output, const float *v_output_alpha,
                                  float alpha_max, float *rec, int64_t num_intersects, int chunk,
                                  void *plan, size_t plan_bytes, bool work_ready = false,
-                                 bool kbits_ready = false) {
+                                 bool kbits_ready = false, L1Grad l1 = {}) {
   SplitWs w{};
   if (chunk > 0) {
     w = carve_split_ws(plan, (long long)tbx * tby, num_intersects, chunk);
@@ -1950,12 +2007,12 @@ static int backward_into_records(const char *who, hipStream_t st, int tbx, int t
     if (!lease.buf) return check_launch(who);
     launch_bwd(st, tbx, tby, H, W, n, gids, bins, xys, conics, colors, opacity, background,
                final_Ts, final_idx, v_output, v_output_alpha, alpha_max, rec, chunk,
-               chunk > 0 ? &w : nullptr, lease.buf, work_ready, kbits_ready);
+               chunk > 0 ? &w : nullptr, lease.buf, work_ready, kbits_ready, l1);
     lease.finish();
   } else {
     launch_bwd(st, tbx, tby, H, W, n, gids, bins, xys, conics, colors, opacity, background,
                final_Ts, final_idx, v_output, v_output_alpha, alpha_max, rec, chunk,
-               chunk > 0 ? &w : nullptr, nullptr, work_ready, kbits_ready);
+               chunk > 0 ? &w : nullptr, nullptr, work_ready, kbits_ready, l1);
   }
   return 0;
 }
@@ -2025,16 +2082,13 @@ extern "C" int gsplat_rasterize_backward(int tile_bounds_x, int tile_bounds_y, i
   return check_launch("rasterize_backward");
 }
 
-// The RGB forward that also clears the gradient records of the Gaussians the backward will
-// accumulate into (all records, or those with radii > 0 when clear_radii is given).
-extern "C" int gsplat_rasterize_forward_clearing(
-    int tile_bounds_x, int tile_bounds_y, int img_height, int img_width,
+static int forward_clearing_impl(
+    const char *who, int tile_bounds_x, int tile_bounds_y, int img_height, int img_width,
     const int32_t *gaussian_ids_sorted, const int32_t *tile_bins, const float *xys,
     const float *conics, const float *colors, const float *opacity, const float *background,
     float *out_img, float *final_Ts, int32_t *final_idx, void *clear, size_t clear_bytes,
     const int32_t *clear_radii, int64_t num_intersects, int chunk, void *plan, size_t plan_bytes,
-    void *stream) {
-  const char *who = "rasterize_forward_clearing";
+    const float *l1_gt, float *l1_part, int l1_clamp, void *stream) {
   if (bad_frame(tile_bounds_x, tile_bounds_y, img_height, img_width) || clear_bytes % 16 ||
       (clear_bytes && !clear) || (clear_radii && clear_bytes % 64) ||
       (chunk > 0 && (chunk % 64 || num_intersects < 0))) {
@@ -2062,7 +2116,58 @@ extern "C" int gsplat_rasterize_forward_clearing(
   launch_fwd<false>((hipStream_t)stream, tile_bounds_x, tile_bounds_y, img_height, img_width,
                     gaussian_ids_sorted, tile_bins, xys, conics, colors, opacity, background,
                     out_img, final_Ts, final_idx, nullptr, nullptr, (float4 *)clear,
-                    (long long)(clear_bytes / 16), clear_radii, tile_last, kbits, kbw);
+                    (long long)(clear_bytes / 16), clear_radii, tile_last, kbits, kbw, l1_gt,
+                    l1_part, l1_clamp);
+  return check_launch(who);
+}
+
+// The RGB forward that also clears the gradient records of the Gaussians the backward will
+// accumulate into (all records, or those with radii > 0 when clear_radii is given).
+extern "C" int gsplat_rasterize_forward_clearing(
+    int tile_bounds_x, int tile_bounds_y, int img_height, int img_width,
+    const int32_t *gaussian_ids_sorted, const int32_t *tile_bins, const float *xys,
+    const float *conics, const float *colors, const float *opacity, const float *background,
+    float *out_img, float *final_Ts, int32_t *final_idx, void *clear, size_t clear_bytes,
+    const int32_t *clear_radii, int64_t num_intersects, int chunk, void *plan, size_t plan_bytes,
+    void *stream) {
+  return forward_clearing_impl("rasterize_forward_clearing", tile_bounds_x, tile_bounds_y,
+                               img_height, img_width, gaussian_ids_sorted, tile_bins, xys, conics,
+                               colors, opacity, background, out_img, final_Ts, final_idx, clear,
+                               clear_bytes, clear_radii, num_intersects, chunk, plan, plan_bytes,
+                               nullptr, nullptr, 0, stream);
+}
+
+// The per-wave L1 partials of gsplat_rasterize_forward_clearing_l1 (loss.hip's layout: two
+// floats per wave).
+extern "C" size_t gsplat_rasterize_l1_partials_bytes(int tile_bounds_x, int tile_bounds_y) {
+  if (tile_bounds_x <= 0 || tile_bounds_y <= 0) return 0;
+  const long long grid = cdiv((long long)tile_bounds_x * tile_bounds_y, (tiles_per_block<1, 8>()));
+  return (size_t)grid * 4 * 2 * sizeof(float);
+}
+
+extern "C" int gsplat_rasterize_forward_clearing_l1(
+    int tile_bounds_x, int tile_bounds_y, int img_height, int img_width,
+    const int32_t *gaussian_ids_sorted, const int32_t *tile_bins, const float *xys,
+    const float *conics, const float *colors, const float *opacity, const float *background,
+    float *out_img, float *final_Ts, int32_t *final_idx, void *clear, size_t clear_bytes,
+    const int32_t *clear_radii, int64_t num_intersects, int chunk, void *plan, size_t plan_bytes,
+    const float *gt, int clamp_pred, float *partials, size_t partials_bytes, float *loss,
+    void *stream) {
+  const char *who = "rasterize_forward_clearing_l1";
+  const size_t need = gsplat_rasterize_l1_partials_bytes(tile_bounds_x, tile_bounds_y);
+  if (!gt || !partials || !loss || partials_bytes < need) {
+    set_error("%s: NULL gt / partials / loss or partials %zu < %zu bytes", who, partials_bytes,
+              need);
+    return 1;
+  }
+  if (forward_clearing_impl(who, tile_bounds_x, tile_bounds_y, img_height, img_width,
+                            gaussian_ids_sorted, tile_bins, xys, conics, colors, opacity,
+                            background, out_img, final_Ts, final_idx, clear, clear_bytes,
+                            clear_radii, num_intersects, chunk, plan, plan_bytes, gt, partials,
+                            clamp_pred ? 1 : 0, stream))
+    return 1;
+  launch_l1_finalize((hipStream_t)stream, (int)(need / (2 * sizeof(float))), partials,
+                     1.0 / (3.0 * img_height * img_width), loss);
   return check_launch(who);
 }
 
@@ -2124,6 +2229,35 @@ extern "C" size_t gsplat_grad_records_bytes(int num_points) {
   return num_points > 0 ? (size_t)num_points * REC * sizeof(float) : 0;
 }
 
+static int backward_records_impl(
+    const char *who, int tile_bounds_x, int tile_bounds_y, int img_height, int img_width,
+    int num_points, const int32_t *gaussian_ids_sorted, const int32_t *tile_bins, const float *xys,
+    const float *conics, const float *colors, const float *opacity, const float *background,
+    const float *final_Ts, const int32_t *final_idx, const float *v_output,
+    const float *v_output_alpha, float alpha_max, int64_t num_intersects, int chunk,
+    void *plan, size_t plan_bytes, int plan_filled, void *records, size_t records_bytes,
+    L1Grad l1, void *stream) {
+  hipStream_t st = (hipStream_t)stream;
+  const size_t need = gsplat_grad_records_bytes(num_points);
+  if (bad_frame(tile_bounds_x, tile_bounds_y, img_height, img_width) || num_points < 0 ||
+      num_points >= MAX_BWD_POINTS || num_intersects < 0 || (chunk > 0 && chunk % 64) ||
+      records_bytes < need || (need && !records) || (!v_output && !l1.pred)) {
+    set_error("%s: bad sizes (tiles=%dx%d H=%d W=%d N=%d chunk=%d records %zu < %zu bytes) or "
+              "no upstream gradient", who, tile_bounds_x, tile_bounds_y, img_height, img_width,
+              num_points, chunk, records_bytes, need);
+    return 1;
+  }
+  if (num_points == 0 || num_intersects == 0) return check_launch(who);
+  // deterministic mode: the records' clear by the forward is superseded by det_finish_kernel
+  if (backward_into_records(who, st, tile_bounds_x, tile_bounds_y, img_height, img_width,
+                            num_points, gaussian_ids_sorted, tile_bins, xys, conics, colors,
+                            opacity, background, final_Ts, final_idx, v_output, v_output_alpha,
+                            alpha_max, (float *)records, num_intersects, chunk, plan, plan_bytes,
+                            plan_filled != 0, plan_filled != 0 && plan_kbits_written(plan), l1))
+    return 1;
+  return check_launch(who);
+}
+
 extern "C" int gsplat_rasterize_backward_records(
     int tile_bounds_x, int tile_bounds_y, int img_height, int img_width, int num_points,
     const int32_t *gaussian_ids_sorted, const int32_t *tile_bins, const float *xys,
@@ -2132,24 +2266,30 @@ extern "C" int gsplat_rasterize_backward_records(
     const float *v_output_alpha, float alpha_max, int64_t num_intersects, int chunk,
     void *plan, size_t plan_bytes, int plan_filled, void *records, size_t records_bytes,
     void *stream) {
-  hipStream_t st = (hipStream_t)stream;
-  const size_t need = gsplat_grad_records_bytes(num_points);
-  if (bad_frame(tile_bounds_x, tile_bounds_y, img_height, img_width) || num_points < 0 ||
-      num_points >= MAX_BWD_POINTS || num_intersects < 0 || (chunk > 0 && chunk % 64) ||
-      records_bytes < need || (need && !records)) {
-    set_error("rasterize_backward_records: bad sizes (tiles=%dx%d H=%d W=%d N=%d chunk=%d "
-              "records %zu < %zu bytes)", tile_bounds_x, tile_bounds_y, img_height, img_width,
-              num_points, chunk, records_bytes, need);
+  return backward_records_impl("rasterize_backward_records", tile_bounds_x, tile_bounds_y,
+                               img_height, img_width, num_points, gaussian_ids_sorted, tile_bins,
+                               xys, conics, colors, opacity, background, final_Ts, final_idx,
+                               v_output, v_output_alpha, alpha_max, num_intersects, chunk, plan,
+                               plan_bytes, plan_filled, records, records_bytes, L1Grad{}, stream);
+}
+
+extern "C" int gsplat_rasterize_backward_records_l1(
+    int tile_bounds_x, int tile_bounds_y, int img_height, int img_width, int num_points,
+    const int32_t *gaussian_ids_sorted, const int32_t *tile_bins, const float *xys,
+    const float *conics, const float *colors, const float *opacity, const float *background,
+    const float *final_Ts, const int32_t *final_idx, const float *pred, const float *gt,
+    int clamp_pred, const float *grad_loss, float alpha_max, int64_t num_intersects, int chunk,
+    void *plan, size_t plan_bytes, int plan_filled, void *records, size_t records_bytes,
+    void *stream) {
+  if (!pred || !gt || !grad_loss) {
+    set_error("rasterize_backward_records_l1: NULL pred / gt / grad_loss");
     return 1;
   }
-  if (num_points == 0 || num_intersects == 0) return check_launch("rasterize_backward_records");
-  // deterministic mode: the records' clear by the forward is superseded by det_finish_kernel
-  if (backward_into_records("rasterize_backward_records", st, tile_bounds_x, tile_bounds_y,
-                            img_height, img_width, num_points, gaussian_ids_sorted, tile_bins, xys,
-                            conics, colors, opacity, background, final_Ts, final_idx, v_output,
-                            v_output_alpha, alpha_max, (float *)records, num_intersects, chunk,
-                            plan, plan_bytes, plan_filled != 0,
-                            plan_filled != 0 && plan_kbits_written(plan)))
-    return 1;
-  return check_launch("rasterize_backward_records");
+  const L1Grad l1{pred, gt, grad_loss, (float)(1.0 / (3.0 * img_height * img_width)),
+                  clamp_pred ? 1 : 0};
+  return backward_records_impl("rasterize_backward_records_l1", tile_bounds_x, tile_bounds_y,
+                               img_height, img_width, num_points, gaussian_ids_sorted, tile_bins,
+                               xys, conics, colors, opacity, background, final_Ts, final_idx,
+                               nullptr, nullptr, alpha_max, num_intersects, chunk, plan,
+                               plan_bytes, plan_filled, records, records_bytes, l1, stream);
 }

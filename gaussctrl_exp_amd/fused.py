@@ -43,7 +43,11 @@ class _FusedRender(Function):
     @staticmethod
     def forward(ctx, means, scales, quats, opacities, features_dc, features_rest, viewmat,
                 projmat, campos, fx, fy, cx, cy, H, W, degrees_to_use, background,
-                return_alpha, aux, adam=None):
+                return_alpha, aux, adam=None, l1_gt=None):
+        # l1_gt [H,W,3]: the render returns (loss, image) instead -- loss = mean |clamp(image,
+        # max=1) - l1_gt| (splatfacto's L1 with ssim_lambda 0 on gc_model.py:222's clamped
+        # image) computed by the blend, whose backward forms the image gradient per pixel
+        # (gsplat_rasterize_forward_clearing_l1 / _backward_records_l1): no loss kernels
         n = means.shape[0]
         K = 1 + features_rest.shape[1]
         if K not in _DEG_OF_BASES or features_dc.shape != (n, 3) or \
@@ -89,6 +93,13 @@ class _FusedRender(Function):
             layout_i = spec.layout_intersects
         visible_hint = last_num_visible(dev)
         chunk, plan = 0, None
+        if l1_gt is not None:
+            if l1_gt.shape != (H, W, 3) or return_alpha:
+                raise ValueError("render_fused: the L1 loss needs gt [H, W, 3] and no alpha")
+            l1_gt = _contig_f32(l1_gt)
+            l1_part = torch.empty((_lib.query("gsplat_rasterize_l1_partials_bytes", tbx, tby)
+                                   // 4,), **f32)
+            loss = torch.empty((), **f32)
 
         def blend(gids, bins, layout_i):
             """The blend (it also clears the gradient records the backward accumulates into and
@@ -101,13 +112,18 @@ class _FusedRender(Function):
                 plan = torch.empty((_lib.query("gsplat_rasterize_split_bytes", tbx, tby,
                                                layout_i, chunk),),
                                    device=dev, dtype=torch.uint8)
-            _lib.call("gsplat_rasterize_forward_clearing", tbx, tby, H, W, P(gids), P(bins),
-                      P(xys), P(conics), P(colors), P(opac), P(background), P(out_img),
-                      P(final_Ts), P(final_idx), P(rec), rec.numel() if rec is not None else 0,
-                      # skip culled Gaussians' records when many are culled (real scenes);
-                      # at ~all visible the radii loads cost more than the stores they save
-                      P(radii) if rec is not None and visible_hint < 0.9 * n else None,
-                      layout_i, chunk, P(plan), plan.numel() if plan is not None else 0, st)
+            args = (tbx, tby, H, W, P(gids), P(bins), P(xys), P(conics), P(colors), P(opac),
+                    P(background), P(out_img), P(final_Ts), P(final_idx), P(rec),
+                    rec.numel() if rec is not None else 0,
+                    # skip culled Gaussians' records when many are culled (real scenes);
+                    # at ~all visible the radii loads cost more than the stores they save
+                    P(radii) if rec is not None and visible_hint < 0.9 * n else None,
+                    layout_i, chunk, P(plan), plan.numel() if plan is not None else 0)
+            if l1_gt is None:
+                _lib.call("gsplat_rasterize_forward_clearing", *args, st)
+            else:
+                _lib.call("gsplat_rasterize_forward_clearing_l1", *args, P(l1_gt), 1, P(l1_part),
+                          4 * l1_part.numel(), P(loss), st)
 
         out_img = torch.empty((H, W, 3), **f32)
         final_Ts = torch.empty((H, W), **f32)
@@ -131,6 +147,10 @@ class _FusedRender(Function):
             if rec is not None:
                 rec.zero_()
             chunk, plan = 0, None
+            if l1_gt is not None:  # (the blend did not run: the background's loss)
+                from .loss import fused_splatfacto_loss
+                with torch.no_grad():
+                    loss = fused_splatfacto_loss(out_img, l1_gt, 0.0, True)
         ctx.meta = (n, K, int(degrees_to_use), float(fx), float(fy), float(cx), float(cy), H, W,
                     tbx, tby, num_intersects, chunk, layout_i)
         ctx.plan, ctx.rec = plan, rec
@@ -155,9 +175,13 @@ class _FusedRender(Function):
                               background, xys, radii, conics, colors, opac, gids, bins, final_Ts,
                               final_idx)
         ctx.set_materialize_grads(False)
+        ctx.l1 = (out_img, l1_gt) if l1_gt is not None else None
         aux.update(xys=xys, radii=radii, depths=depths, num_intersects=num_intersects,
                    records=rec, num_points=n, conics=conics, colors=colors, opacity=opac,
                    num_tiles_hit=nth)
+        if l1_gt is not None:
+            ctx.mark_non_differentiable(out_img)
+            return loss, out_img
         if return_alpha:
             return out_img, 1 - final_Ts
         return out_img
@@ -171,7 +195,18 @@ class _FusedRender(Function):
         dev = means.device
         P, st = _lib.ptr, _lib.stream(dev)
         rec = ctx.rec
-        if I >= 1 and (v_img is not None or v_alpha is not None):
+        if ctx.l1 is not None:  # (loss, image): v_img is the loss's gradient, v_alpha unused
+            g_loss, v_img, v_alpha = v_img, None, None
+            if I >= 1 and g_loss is not None:
+                pred, gt = ctx.l1
+                _lib.call("gsplat_rasterize_backward_records_l1", tbx, tby, H, W, n, P(gids),
+                          P(bins), P(xys), P(conics), P(colors), P(opac), P(background),
+                          P(final_Ts), P(final_idx), P(pred), P(gt), 1,
+                          P(g_loss.float().contiguous()), quirks.backward_alpha_clamp(),
+                          layout_i if chunk > 0 else I, chunk, P(ctx.plan),
+                          ctx.plan.numel() if ctx.plan is not None else 0,
+                          int(ctx.plan is not None), P(rec), rec.numel(), st)
+        elif I >= 1 and (v_img is not None or v_alpha is not None):
             v_img = v_img.float().contiguous() if v_img is not None else \
                 torch.zeros((H, W, 3), device=dev, dtype=torch.float32)
             if v_alpha is not None:
@@ -193,7 +228,7 @@ class _FusedRender(Function):
                       cast(a["exp_avgs"], ctypes.c_void_p), cast(a["exp_avg_sqs"], ctypes.c_void_p),
                       cast(a["lrs"], ctypes.c_void_p), int(a["step"]), float(a["betas"][0]),
                       float(a["betas"][1]), float(a["eps"]), st)
-            return (None,) * 20
+            return (None,) * 21
         f32 = dict(device=dev, dtype=torch.float32)
         xchg = ctx.exchange
         if xchg is not None and ctx.early:
@@ -221,7 +256,7 @@ class _FusedRender(Function):
                                                                    views),
                 early_flat=early["flat"], early_map=early["map"])
         return (v_means, v_scales, v_quats, v_opac.view(ctx.opac_shape), v_dc, v_rest) + \
-            (None,) * 14
+            (None,) * 15
 
 
 def sh_backward_views_split(degree: int, degrees_to_use: int, means: Tensor, views: Tensor):
@@ -261,7 +296,8 @@ def _campos(cam: GCCamera) -> Tensor:
 
 
 def render_fused(scene, cam: GCCamera, sh_degree_to_use: int, background: Tensor,
-                 return_alpha: bool = False, clamp: bool = True, adam=None):
+                 return_alpha: bool = False, clamp: bool = True, adam=None,
+                 l1_gt: Optional[Tensor] = None):
     """scene.render's training output (gc_model.py:158-222) through the fused kernels.
 
     Returns dict(rgb [H,W,3] (clamped at 1 as gc_model.py:222 -- or, clamp=False, the raw
@@ -271,16 +307,26 @@ def render_fused(scene, cam: GCCamera, sh_degree_to_use: int, background: Tensor
     backward -- what splatfacto's densification reads from `xys.grad`).
     adam: optim.FusedAdam.fused_spec(params) of the six parameters -- the backward then takes
     that Adam step itself (gsplat_fused_preprocess_backward_adam: parameters updated in place,
-    no .grad); single-GPU only."""
+    no .grad); single-GPU only.
+    l1_gt [H,W,3]: also return "loss" = mean |clamp(rgb, max=1) - l1_gt| (the training step's
+    L1, splatfacto's loss at ssim_lambda 0), computed by the blend kernel; the loss is the
+    differentiable output (its backward forms the image gradient inside the rasterizer
+    backward) and "rgb" is the detached raw image (clamp ignored)."""
     aux = {}
     args = [_contig_f32(scene.means), _contig_f32(scene.scales), _contig_f32(scene.quats),
             _contig_f32(scene.opacities), _contig_f32(scene.features_dc),
             _contig_f32(scene.features_rest), _contig_f32(cam.viewmat), _contig_f32(cam.projmat),
             _campos(cam), cam.fx, cam.fy, cam.cx, cam.cy, cam.height, cam.width,
-            int(sh_degree_to_use), _contig_f32(background), bool(return_alpha), aux, adam]
+            int(sh_degree_to_use), _contig_f32(background), bool(return_alpha), aux, adam,
+            l1_gt]
     out = _FusedRender.apply(*args)
-    img, alpha = (out if return_alpha else (out, None))
-    rgb = torch.clamp(img, max=1.0) if clamp else img
+    loss = None
+    if l1_gt is not None:
+        loss, img = out
+        alpha, rgb, clamp = None, img, False
+    else:
+        img, alpha = (out if return_alpha else (out, None))
+        rgb = torch.clamp(img, max=1.0) if clamp else img
 
     def split_records():
         """The records (pixel moments, include/gsplat_mi355x.h) -> gsplat's four rasterize
@@ -308,7 +354,7 @@ def render_fused(scene, cam: GCCamera, sh_degree_to_use: int, background: Tensor
         g = split_records()
         return None if g is None else tuple(g)
 
-    return {"rgb": rgb, "clamped": bool(clamp),
+    return {"rgb": rgb, "clamped": bool(clamp), "loss": loss,
             "accumulation": alpha[..., None] if alpha is not None else None,
             "xys": aux["xys"], "radii": aux["radii"], "xys_grad": xys_grad,
             "raster_grads": raster_grads,

@@ -16,6 +16,7 @@ every tensor instead.
 from __future__ import annotations
 
 import math
+import os
 from typing import List, Optional
 
 import torch
@@ -150,6 +151,10 @@ class TrainStep:
         # single-GPU fused steps take the Adam update inside the backward kernel
         # (gsplat_fused_preprocess_backward_adam): no gradient tensors are written or re-read
         self.fuse_adam = bool(fuse_adam) and render_mode == "fused" and world_size == 1
+        # the fused render computes an L1 loss inside its blend kernels (loss="l1"); off:
+        # the separate loss kernels (GSPLAT_MI355X_FUSE_L1=0, A/B runs)
+        self.fuse_l1 = render_mode == "fused" and os.environ.get("GSPLAT_MI355X_FUSE_L1",
+                                                                 "1") != "0"
         self.scene = scene.requires_grad_()
         self.params = scene.params()
         self.world_size = world_size
@@ -208,20 +213,25 @@ class TrainStep:
     def flat_grad(self) -> torch.Tensor:
         return torch.cat([p.grad.reshape(-1) for p in self.params])
 
-    def _render(self, cam: GCCamera, background: torch.Tensor, adam=None):
+    def _render(self, cam: GCCamera, background: torch.Tensor, adam=None, gt=None):
         if self.render_mode == "fused":  # raw image: the loss applies the clamp
+            # the L1 loss folded into the blend kernels (fused.render_fused l1_gt) unless
+            # fuse_l1 is off
+            l1 = gt if (self.loss_kind == "l1" and self.fuse_l1 and gt is not None) else None
             return render_fused(self.scene, cam, self.sh_degree, background, clamp=False,
-                                adam=adam)
+                                adam=adam, l1_gt=l1)
         return render(self.scene, cam, self.sh_degree, background, api=self.api)
 
     def forward_backward(self, cam: GCCamera, gt: torch.Tensor, background: torch.Tensor,
                          adam=None):
         if self.sh_exchange is not None:
             with self.sh_exchange.view(self.scene.means, cam.c2w[..., :3, 3]):
-                out = self._render(cam, background)
+                out = self._render(cam, background, gt=gt)
         else:
-            out = self._render(cam, background, adam=adam)
-        loss = self.loss(out["rgb"], gt, clamp_pred=not out.get("clamped", True))
+            out = self._render(cam, background, adam=adam, gt=gt)
+        loss = out.get("loss")
+        if loss is None:
+            loss = self.loss(out["rgb"], gt, clamp_pred=not out.get("clamped", True))
         if loss.requires_grad:
             # a kept ones() seed: autograd's own seed is a fill kernel per step
             seed = getattr(self, "_seed", None)

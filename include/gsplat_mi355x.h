@@ -404,6 +404,33 @@ int gsplat_rasterize_backward_records(
     const float *v_output_alpha, float alpha_max, int64_t num_intersects, int chunk,
     void *plan, size_t plan_bytes, int plan_filled, void *records, size_t records_bytes,
     void *stream);
+/* The training step's L1 photometric loss folded into the blend (no gsplat counterpart: the
+ * loss of gc_pipeline.py:477-478 with splatfacto's ssim_lambda = 0, on gc_model.py:222's
+ * clamped image when clamp_pred).  The forward is gsplat_rasterize_forward_clearing plus
+ * loss[0] = mean over the H x W x 3 image of |clamp(out_img) - gt| (gt [H,W,3]; per-wave
+ * partials of gsplat_rasterize_l1_partials_bytes, summed in double); the backward is
+ * gsplat_rasterize_backward_records whose upstream image gradient is not read but formed per
+ * pixel from (pred = that forward's out_img, gt, grad_loss [1] device scalar): grad_loss/(3HW)
+ * * sign(clamp(pred) - gt) * (pred <= 1 when clamp_pred) -- gsplat_l1_ssim_backward's
+ * lambda = 0 arithmetic, so the records equal the unfused step's bit for bit.  No alpha
+ * gradient. */
+size_t gsplat_rasterize_l1_partials_bytes(int tile_bounds_x, int tile_bounds_y);
+int gsplat_rasterize_forward_clearing_l1(
+    int tile_bounds_x, int tile_bounds_y, int img_height, int img_width,
+    const int32_t *gaussian_ids_sorted, const int32_t *tile_bins, const float *xys,
+    const float *conics, const float *colors, const float *opacity, const float *background,
+    float *out_img, float *final_Ts, int32_t *final_idx, void *clear, size_t clear_bytes,
+    const int32_t *clear_radii, int64_t num_intersects, int chunk, void *plan, size_t plan_bytes,
+    const float *gt, int clamp_pred, float *partials, size_t partials_bytes, float *loss,
+    void *stream);
+int gsplat_rasterize_backward_records_l1(
+    int tile_bounds_x, int tile_bounds_y, int img_height, int img_width, int num_points,
+    const int32_t *gaussian_ids_sorted, const int32_t *tile_bins, const float *xys,
+    const float *conics, const float *colors, const float *opacity, const float *background,
+    const float *final_Ts, const int32_t *final_idx, const float *pred, const float *gt,
+    int clamp_pred, const float *grad_loss, float alpha_max, int64_t num_intersects, int chunk,
+    void *plan, size_t plan_bytes, int plan_filled, void *records, size_t records_bytes,
+    void *stream);
 /* The records -> gsplat's four rasterize gradients (v_xy [N,2], v_conic [N,3] in gsplat's
  * convention (GSPLAT_QUIRK_CONIC_HALF), v_colors [N,3], v_opacity [N]) -- the tail of
  * gsplat_rasterize_backward, for a caller that cleared the records in the forward blend
