@@ -262,12 +262,21 @@ __global__ __launch_bounds__(TPB) void rts_count_kernel(const K *__restrict__ ke
                                                         bool drop = false,
                                                         const uint32_t *__restrict__ n_dev = nullptr,
                                                         KeyRange kr = {}, int pass = 0,
-                                                        DevIO io = {}) {
+                                                        DevIO io = {}, int cap_launch = 0) {
   __shared__ uint32_t h[256];
   __shared__ uint32_t kand, kor;
   const int tid = threadIdx.x;
   if (pass > 0 && digit_constant(kr.fin, shift, width)) return;  // identity pass
   if (io.fin && pass > 0) keys = (const K *)(data_in_b(io, pass) ? io.kb : io.ka);
+  const long long base = (long long)blockIdx.x * TPB * ITEMS;
+  K k[ITEMS];
+  // cap_launch (the capacity-launched tile sort, EMIT_SPEC: n is the capacity, ~1.125 x the
+  // device count): the keys are loaded up to the capacity before the device count arrives, so
+  // the loads do not wait for it (positions past the count are masked below)
+  if (cap_launch) {
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) k[r] = keys[min(base + r * TPB + tid, n - 1)];
+  }
   if (n_dev) {
     // *n_dev > n: a capacity-launched tile sort whose intersections overflowed the capacity
     // (bin_emit_impl, EMIT_SPEC): the emission wrote nothing, so nothing is sorted
@@ -279,12 +288,12 @@ __global__ __launch_bounds__(TPB) void rts_count_kernel(const K *__restrict__ ke
   h[tid] = 0;
   if (tid == 0) kand = ~0u, kor = 0u;
   __syncthreads();
-  const long long base = (long long)blockIdx.x * TPB * ITEMS;
-  K k[ITEMS];
+  if (!cap_launch) {
 #pragma unroll
-  for (int r = 0; r < ITEMS; ++r) {
-    const long long i = base + r * TPB + tid;
-    k[r] = i < n ? keys[i] : (K)0;
+    for (int r = 0; r < ITEMS; ++r) {
+      const long long i = base + r * TPB + tid;
+      k[r] = i < n ? keys[i] : (K)0;
+    }
   }
   uint32_t a = ~0u, o = 0u;
 #pragma unroll
@@ -403,7 +412,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     const uint32_t *__restrict__ rowtot, const uint32_t *__restrict__ offs, long long nblocks,
     int32_t *__restrict__ bins = nullptr, bool drop = false,
     const uint32_t *__restrict__ n_dev = nullptr, uint32_t *__restrict__ n_out = nullptr,
-    const uint32_t *__restrict__ kfin = nullptr, DevIO io = {}, int q = 0) {
+    const uint32_t *__restrict__ kfin = nullptr, DevIO io = {}, int q = 0, int cap_launch = 0) {
   if (io.fin) {  // device-selected buffers (DevIO): a constant digit moves nothing
     if (q > 0 && digit_constant(io.fin, shift, width)) return;
     const K *ki;
@@ -419,7 +428,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
   // compacting sort: with drop, all-ones keys are left out (pass 0 of the depth sort: culled
   // Gaussians), and block 0 stores the kept count to n_out; later passes sort min(n, *n_dev)
   // keys and the workgroups past them exit at once.
-  if (n_dev) {
+  // cap_launch (see rts_count_kernel): the count is read after the loads are issued, below
+  const long long n_cap = n;
+  if (n_dev && !cap_launch) {
     if (*n_dev > (unsigned long long)n) return;  // capacity overflow (see rts_count_kernel)
     n = *n_dev;
     if ((long long)blockIdx.x * TPB * ITEMS >= n) return;  // whole workgroup
@@ -463,10 +474,15 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     const long long sg = (long long)t * TPB * ITEMS + (long long)wave * (ITEMS * 64);
 #pragma unroll
     for (int r = 0; r < ITEMS; ++r) {
-      const long long i = min(sg + r * 64 + lane, n - 1);
+      const long long i = min(sg + r * 64 + lane, n_cap - 1);
       key[r] = kin[i];
       val[r] = vin[i];
     }
+  }
+  if (n_dev && cap_launch) {  // (workgroup-uniform exits, after the loads went out)
+    if (*n_dev > (unsigned long long)n) return;
+    n = *n_dev;
+    if ((long long)blockIdx.x * TPB * ITEMS >= n) return;
   }
 #pragma unroll
   for (int w = 0; w < 4; ++w) sm.wcnt[w][tid] = 0;
@@ -668,13 +684,16 @@ int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t
     if (q == 0 && first_counts_ready) {
     } else if (p.items == 16)
       hipLaunchKernelGGL((rts_count_kernel<K, 16>), dim3((unsigned)p.nblocks), dim3(TPB), 0, st,
-                         kin, n, sh, p.width, p.nblocks, counts, drop && q == 0, ndev, kr, q, io);
+                         kin, n, sh, p.width, p.nblocks, counts, drop && q == 0, ndev, kr, q, io,
+                         n_dev_all ? 1 : 0);
     else if (p.items == 8)
       hipLaunchKernelGGL((rts_count_kernel<K, 8>), dim3((unsigned)p.nblocks), dim3(TPB), 0, st,
-                         kin, n, sh, p.width, p.nblocks, counts, drop && q == 0, ndev, kr, q, io);
+                         kin, n, sh, p.width, p.nblocks, counts, drop && q == 0, ndev, kr, q, io,
+                         n_dev_all ? 1 : 0);
     else
       hipLaunchKernelGGL((rts_count_kernel<K, 4>), dim3((unsigned)p.nblocks), dim3(TPB), 0, st,
-                         kin, n, sh, p.width, p.nblocks, counts, drop && q == 0, ndev, kr, q, io);
+                         kin, n, sh, p.width, p.nblocks, counts, drop && q == 0, ndev, kr, q, io,
+                         n_dev_all ? 1 : 0);
     hipLaunchKernelGGL(rts_rowscan_kernel,
                        dim3((unsigned)p.radix + (q == 0 && kr.blk ? 1u : 0u)), dim3(1024), 0,
                        st, counts, p.nblocks, rowtot, kr, q, sh, p.width);
@@ -683,7 +702,7 @@ int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t
                      kin, vin, ko, vo, n, sh, p.width, rowtot, counts, p.nblocks,              \
                      last ? tile_bins : nullptr, drop && q == 0,                               \
                      ndev, drop && q == 0 ? kept : nullptr,                                    \
-                     q > 0 && !io.fin ? kr.fin : nullptr, io, q)
+                     q > 0 && !io.fin ? kr.fin : nullptr, io, q, n_dev_all ? 1 : 0)
 #define OS_PASS_W(Wd)                                                                       \
   do {                                                                                      \
     if (p.items == 16) OS_PASS(Wd, 16); else if (p.items == 8) OS_PASS(Wd, 8);             \

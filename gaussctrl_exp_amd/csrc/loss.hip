@@ -240,19 +240,31 @@ __global__ __launch_bounds__(256) void l1_only_bwd_kernel(long long n, const flo
 
 // loss = (1 - lambda) * L1 / (C H W) + lambda * (1 - SSIM_sum / (C Ho Wo)); one workgroup,
 // double accumulation in a fixed order (deterministic).
-__global__ __launch_bounds__(256) void l1_ssim_finalize_kernel(int nblocks, const float *partials,
-                                                               double inv_l1, double inv_ssim,
-                                                               float lambda, float *loss) {
-  __shared__ double ra[256], rb[256];
+__global__ __launch_bounds__(1024) void l1_ssim_finalize_kernel(int nblocks, const float *partials,
+                                                                double inv_l1, double inv_ssim,
+                                                                float lambda, float *loss) {
+  // (1,024 threads, every load of a round issued before the first add: a loop waiting for each
+  // load in turn is a chain of L2 latencies)
+  constexpr int NT = 1024, U = 4;
+  __shared__ double ra[NT], rb[NT];
   double a = 0.0, b = 0.0;
-  for (int k = threadIdx.x; k < nblocks; k += 256) {
-    a += partials[2 * k];
-    b += partials[2 * k + 1];
+  for (int base = 0; base < nblocks; base += NT * U) {
+    float2 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = base + u * NT + threadIdx.x;
+      v[u] = k < nblocks ? reinterpret_cast<const float2 *>(partials)[k] : make_float2(0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      a += v[u].x;
+      b += v[u].y;
+    }
   }
   ra[threadIdx.x] = a;
   rb[threadIdx.x] = b;
   __syncthreads();
-  for (int s = 128; s > 0; s >>= 1) {
+  for (int s = NT / 2; s > 0; s >>= 1) {
     if ((int)threadIdx.x < s) {
       ra[threadIdx.x] += ra[threadIdx.x + s];
       rb[threadIdx.x] += rb[threadIdx.x + s];
@@ -355,14 +367,44 @@ __global__ __launch_bounds__(256) void l1_ssim_bwd_kernel(
   }
 }
 
+// loss = inv_n * sum of n partials (one float each), in double and a fixed order.  One
+// workgroup of 1,024 threads whose loads are all in flight together (16 per round, unrolled):
+// the fused-L1 blend writes one partial per wave (~18.5k at 1080^2), and a loop that waits for
+// each load in turn took ~30 us.
+constexpr int FIN_NT = 1024, FIN_U = 16;
+__global__ __launch_bounds__(FIN_NT) void partials_finalize_kernel(int n,
+                                                                   const float *__restrict__ p,
+                                                                   double inv_n,
+                                                                   float *__restrict__ loss) {
+  __shared__ double red[FIN_NT];
+  double a = 0.0;
+  for (int base = 0; base < n; base += FIN_NT * FIN_U) {
+    float v[FIN_U];
+#pragma unroll
+    for (int u = 0; u < FIN_U; ++u) {
+      const int k = base + u * FIN_NT + threadIdx.x;
+      v[u] = k < n ? p[k] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < FIN_U; ++u) a += (double)v[u];
+  }
+  red[threadIdx.x] = a;
+  __syncthreads();
+  for (int s = FIN_NT / 2; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) loss[0] = (float)(red[0] * inv_n);
+}
+
 }  // namespace
 
-// The loss of per-wave / per-block L1 partials (two floats each, the second zero) written by
-// another kernel -- the fused-L1 blend (raster.hip): loss = inv_n * sum, summed in double.
+// The loss of one-float-per-wave L1 partials written by another kernel -- the fused-L1 blend
+// (raster.hip): loss = inv_n * sum, summed in double.
 void launch_l1_finalize(hipStream_t st, int nparts, const float *partials, double inv_n,
                         float *loss) {
-  hipLaunchKernelGGL(l1_ssim_finalize_kernel, dim3(1), dim3(256), 0, st, nparts, partials, inv_n,
-                     0.0, 0.f, loss);
+  hipLaunchKernelGGL(partials_finalize_kernel, dim3(1), dim3(FIN_NT), 0, st, nparts, partials,
+                     inv_n, loss);
 }
 
 }  // namespace gs
@@ -414,7 +456,7 @@ extern "C" int gsplat_l1_ssim_forward(int img_height, int img_width, int channel
   }
   const double n1 = (double)channels * img_height * img_width;
   const double n2 = (double)channels * (img_height - WIN + 1) * (img_width - WIN + 1);
-  hipLaunchKernelGGL(l1_ssim_finalize_kernel, dim3(1), dim3(256), 0, st, nb, partials,
+  hipLaunchKernelGGL(l1_ssim_finalize_kernel, dim3(1), dim3(1024), 0, st, nb, partials,
                      1.0 / n1, 1.0 / n2, ssim_lambda, loss);
   return check_launch("l1_ssim_forward");
 }

@@ -161,12 +161,17 @@ static bool pipelined_staging(int tbx, int tby) {
 }
 
 struct __attribute__((aligned(16))) GStage {
+  // Field order = the order a blend iteration needs them in, one ds_read_b128 per row: the
+  // sigma / alpha / validity inputs (mean, conic, opacity, list position) in the first two
+  // rows, the Gaussian id (the backward's record atomic) with them, the colour (and depth)
+  // last -- the last row's read then overlaps the sigma / exp chain instead of being waited
+  // for right after it is issued.
   float x, y, ha, b;  // mean, 0.5*conic.a, conic.b
-  float hc, o, r, g;  // 0.5*conic.c, opacity, colour
-  float bl;
-  int idx;  // position in the tile's sorted list
-  int id;   // Gaussian id
-  float d;  // depth (fused RGB+depth forward only)
+  float hc, o;        // 0.5*conic.c, opacity
+  int idx;            // position in the tile's sorted list
+  int id;             // Gaussian id
+  float r, g, bl;     // colour
+  float d;            // depth (fused RGB+depth forward only)
 };
 
 typedef float f2 __attribute__((ext_vector_type(2)));
@@ -726,15 +731,12 @@ __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
   constexpr int WPT = (GS_BLOCK / COLS) * (GS_BLOCK / ((64 / COLS) * PXL));
   static_assert(WPT == SPLIT_WAVES, "one walk-table entry per wave of a tile");
   const int wt = (threadIdx.x >> 6) % WPT;
-  // the fused L1 loss's per-wave partial (l1_part[2 w], l1_part[2 w + 1] = 0: loss.hip's layout)
+  // the fused L1 loss's per-wave partial l1_part[w] (gsplat_rasterize_forward_clearing_l1)
   const long long l1_w = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (!R.live) {  // wave-uniform
     if (tile_last && R.tile < tbx * tby && (threadIdx.x & 63) == 0)
       tile_last[WPT * R.tile + wt] = -1;
-    if (l1_part && (threadIdx.x & 63) == 0) {
-      l1_part[2 * l1_w] = 0.f;
-      l1_part[2 * l1_w + 1] = 0.f;
-    }
+    if (l1_part && (threadIdx.x & 63) == 0) l1_part[l1_w] = 0.f;
     clear_side_job();
     return;
   }
@@ -873,10 +875,7 @@ __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
       }
     }
     acc = wave_sum(acc);
-    if (lane == 0) {
-      l1_part[2 * l1_w] = acc;
-      l1_part[2 * l1_w + 1] = 0.f;
-    }
+    if (lane == 0) l1_part[l1_w] = acc;
   }
   if (tile_last) {
     int m = -1;
@@ -2137,12 +2136,11 @@ extern "C" int gsplat_rasterize_forward_clearing(
                                nullptr, nullptr, 0, stream);
 }
 
-// The per-wave L1 partials of gsplat_rasterize_forward_clearing_l1 (loss.hip's layout: two
-// floats per wave).
+// The per-wave L1 partials of gsplat_rasterize_forward_clearing_l1 (one float per wave).
 extern "C" size_t gsplat_rasterize_l1_partials_bytes(int tile_bounds_x, int tile_bounds_y) {
   if (tile_bounds_x <= 0 || tile_bounds_y <= 0) return 0;
   const long long grid = cdiv((long long)tile_bounds_x * tile_bounds_y, (tiles_per_block<1, 8>()));
-  return (size_t)grid * 4 * 2 * sizeof(float);
+  return (size_t)grid * 4 * sizeof(float);
 }
 
 extern "C" int gsplat_rasterize_forward_clearing_l1(
@@ -2166,7 +2164,7 @@ extern "C" int gsplat_rasterize_forward_clearing_l1(
                             clear_radii, num_intersects, chunk, plan, plan_bytes, gt, partials,
                             clamp_pred ? 1 : 0, stream))
     return 1;
-  launch_l1_finalize((hipStream_t)stream, (int)(need / (2 * sizeof(float))), partials,
+  launch_l1_finalize((hipStream_t)stream, (int)(need / sizeof(float)), partials,
                      1.0 / (3.0 * img_height * img_width), loss);
   return check_launch(who);
 }

@@ -408,7 +408,8 @@ int gsplat_rasterize_backward_records(
  * loss of gc_pipeline.py:477-478 with splatfacto's ssim_lambda = 0, on gc_model.py:222's
  * clamped image when clamp_pred).  The forward is gsplat_rasterize_forward_clearing plus
  * loss[0] = mean over the H x W x 3 image of |clamp(out_img) - gt| (gt [H,W,3]; per-wave
- * partials of gsplat_rasterize_l1_partials_bytes, summed in double); the backward is
+ * partials, one float per wave, gsplat_rasterize_l1_partials_bytes; summed in double); the
+ * backward is
  * gsplat_rasterize_backward_records whose upstream image gradient is not read but formed per
  * pixel from (pred = that forward's out_img, gt, grad_loss [1] device scalar): grad_loss/(3HW)
  * * sign(clamp(pred) - gt) * (pred <= 1 when clamp_pred) -- gsplat_l1_ssim_backward's

@@ -76,7 +76,8 @@ def _fused_raster_level(gpu, sc, cam, loss="sum"):
     out["accumulation"].register_hook(
         lambda g: up.__setitem__("v_alpha", g.detach().cpu().numpy()[..., 0]))
     d = (out["rgb"] - gt.to(gpu)).abs()
-    ((d.sum() if loss == "sum" else d.mean()) + 0.1 * out["accumulation"].sum()).backward()
+    a = out["accumulation"]
+    ((d.sum() + 0.1 * a.sum()) if loss == "sum" else (d.mean() + 0.1 * a.mean())).backward()
     r = {k: v.detach().cpu().numpy() for k, v in out["raster_inputs"].items()}
     return [g.detach().cpu().numpy() for g in out["raster_grads"]()], r, up, bg.cpu().numpy()
 
