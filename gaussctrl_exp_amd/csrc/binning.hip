@@ -202,6 +202,11 @@ struct KeyRange {
   uint32_t *blk = nullptr;
   uint32_t *fin = nullptr;
   long long nblk = 0;
+  // Passes the host did not launch at all (gsplat_bin_count_keyed_ex): the key bits assumed
+  // constant from an earlier call's range; out[0] = 1 if this call's keys vary in any of them
+  // (the sort is then wrong and the caller re-bins), out[1] = the bits that vary.
+  uint32_t assume = 0;
+  int32_t *out = nullptr;
 };
 __device__ __forceinline__ bool digit_constant(const uint32_t *fin, int shift, int width) {
   return fin && ((((fin[0] ^ fin[1]) >> shift) & ((1u << width) - 1u)) == 0u);
@@ -348,6 +353,10 @@ __global__ __launch_bounds__(1024) void rts_rowscan_kernel(uint32_t *__restrict_
     if (threadIdx.x == 0) {
       kr.fin[0] = kand;
       kr.fin[1] = kor;
+      if (kr.out) {
+        kr.out[0] = ((kand ^ kor) & kr.assume) ? 1 : 0;
+        kr.out[1] = (int32_t)(kand ^ kor);
+      }
     }
     return;
   }
@@ -645,7 +654,8 @@ int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t
                      long long n, int begin_bit, int end_bit, void *ws, hipStream_t st,
                      bool first_counts_ready = false, int32_t *tile_bins = nullptr,
                      long long num_tiles = 0, bool drop = false, int first_pass = 0,
-                     const uint32_t *n_dev_all = nullptr) {
+                     const uint32_t *n_dev_all = nullptr, uint32_t assume_const = 0,
+                     int32_t *range_out = nullptr) {
   // n_dev_all (not with drop): the key count lives on the device (<= n, the launch capacity;
   // more than n: overflow, every kernel returns at once) -- the capacity-launched tile sort
   if (n <= 0) return 0;
@@ -664,6 +674,8 @@ int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t
     kr.blk = (uint32_t *)((char *)ws + radix_main_bytes(p));
     kr.fin = sort_kept_word(ws) + 1;
     kr.nblk = p.nblocks;
+    kr.assume = assume_const;
+    kr.out = range_out;
   }
   // first_pass = 1: the caller ran pass 0 itself, into (kb, vb)
   K *kin = first_pass ? kb : ka, *kalt = first_pass ? ka : kb;
@@ -674,6 +686,11 @@ int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t
   if (kr.fin && first_pass == 0)
     io = DevIO{kr.fin, ka, kb, va, vb, kout, vout, begin_bit, p.width, p.passes};
   for (int q = first_pass; q < p.passes; ++q) {
+    // a digit the caller's earlier range says is constant: not launched at all (its three
+    // launches cost ~14 us at the headline even when they return at once); the pass-0 range
+    // reduction checks the assumption (kr.out)
+    const uint32_t qmask = (p.width >= 32 ? ~0u : ((1u << p.width) - 1u)) << (begin_bit + q * p.width);
+    if (q > 0 && kr.fin && kr.out && (kr.assume & qmask) == qmask) continue;
     const bool last = q == p.passes - 1;
     K *ko = last ? kout : kalt;
     uint32_t *vo = last ? vout : valt;
@@ -2048,7 +2065,8 @@ extern "C" size_t gsplat_bin_emit_workspace_size(int64_t num_intersects) {
 static int bin_count_impl(int num_points, const float *xys, const float *depths,
                           const int32_t *radii, const int32_t *num_tiles_hit, int tile_bounds_x,
                           int tile_bounds_y, int32_t *d_counts, void *workspace1,
-                          size_t workspace1_bytes, bool keyed, void *stream) {
+                          size_t workspace1_bytes, bool keyed, void *stream,
+                          uint32_t assume_const = 0, bool range_out = false) {
   hipStream_t st = (hipStream_t)stream;
   const long long T = (long long)tile_bounds_x * tile_bounds_y;
   if (num_points < 0 || tile_bounds_x <= 0 || tile_bounds_y <= 0 || tile_bounds_x > 65535 ||
@@ -2104,8 +2122,12 @@ static int bin_count_impl(int num_points, const float *xys, const float *depths,
   else if (sp.items == 8) DEPTH_KEYS(8);
   else DEPTH_KEYS(4);
 #undef DEPTH_KEYS
+  // range_out: d_counts[2..3] are written only when the key range is computed (the caller
+  // zeroes them: without a range nothing is assumed and nothing reported)
   radix_sort_pairs<uint32_t>(p.dkeys_a, p.dvals_a, p.dkeys_b, p.dvals_b, nullptr, p.order, n, 0,
-                             32, p.rs_ws, st, pre, nullptr, 0, true);
+                             32, p.rs_ws, st, pre, nullptr, 0, true, 0, nullptr,
+                             use_key_range(n) ? assume_const : 0u,
+                             range_out ? d_counts + 2 : nullptr);
   // depth-ordered allotments (+ per-tile sums) -> scan -> offsets and I = d_counts[1]
   const int nb = (int)cdiv(n, SC_TILE);
   // the kept count sits in the sort workspace's head, before the tile counts reused below
@@ -2133,6 +2155,19 @@ extern "C" int gsplat_bin_count_keyed(int num_points, int tile_bounds_x, int til
                                       size_t workspace1_bytes, void *stream) {
   return bin_count_impl(num_points, nullptr, nullptr, nullptr, nullptr, tile_bounds_x,
                         tile_bounds_y, d_counts, workspace1, workspace1_bytes, true, stream);
+}
+
+// gsplat_bin_count_keyed plus the depth-key range across calls: depth-sort passes whose digit
+// `assume_const` covers are not launched; d_counts[2] = 1 if this call's kept keys vary in an
+// assumed-constant bit (the order is then wrong: re-bin), d_counts[3] = the bits that vary --
+// both left as the caller set them (zero) when the sort computes no key range.
+extern "C" int gsplat_bin_count_keyed_ex(int num_points, int tile_bounds_x, int tile_bounds_y,
+                                         int32_t *d_counts, void *workspace1,
+                                         size_t workspace1_bytes, uint32_t assume_const,
+                                         void *stream) {
+  return bin_count_impl(num_points, nullptr, nullptr, nullptr, nullptr, tile_bounds_x,
+                        tile_bounds_y, d_counts, workspace1, workspace1_bytes, true, stream,
+                        assume_const, true);
 }
 
 // The emission in two halves around the host's read of I: HEAD = the launches that need only

@@ -74,12 +74,14 @@ class _FusedRender(Function):
         # the preprocess kernel also writes the binning's depth-sort inputs into its workspace
         ws1 = torch.empty((max(_lib.query("gsplat_bin_count_workspace_size", n), 1),),
                           device=dev, dtype=torch.uint8)
-        _lib.call("gsplat_fused_preprocess_forward_binned", n, K, int(degrees_to_use), P(means),
-                  P(scales), P(quats), P(opacities), P(features_dc),
-                  P(features_rest) if K > 1 else None, P(viewmat), P(projmat), P(campos),
-                  float(fx), float(fy), float(cx), float(cy), H, W, tbx, tby, 0.01, P(xys),
-                  P(depths), P(radii), P(conics), P(nth), P(colors), P(opac), P(ws1),
-                  ws1.numel(), st)
+        def preprocess():
+            _lib.call("gsplat_fused_preprocess_forward_binned", n, K, int(degrees_to_use),
+                      P(means), P(scales), P(quats), P(opacities), P(features_dc),
+                      P(features_rest) if K > 1 else None, P(viewmat), P(projmat), P(campos),
+                      float(fx), float(fy), float(cx), float(cy), H, W, tbx, tby, 0.01, P(xys),
+                      P(depths), P(radii), P(conics), P(nth), P(colors), P(opac), P(ws1),
+                      ws1.numel(), st)
+        preprocess()
         # The binning's emission and tile sort are launched at this frame shape's capacity
         # without the host read of I (rasterize.SpeculativeBinning), the blend right behind
         # them; the host reads I only then, while the GPU works, and re-bins on an overflow.
@@ -130,12 +132,23 @@ class _FusedRender(Function):
         final_idx = torch.empty((H, W), device=dev, dtype=torch.int32)
         if spec is not None:
             blend(gids, bins, layout_i)
-            if not spec.finish():  # I > capacity: the blend saw empty tiles; bin and blend again
-                gids, bins = spec.rebin()
-                layout_i = spec.layout_intersects
-                blend(gids, bins, layout_i)
-            num_intersects = spec.num_intersects
-            gids = gids[:num_intersects]
+            if not spec.finish():
+                if spec.range_violated:
+                    # a depth digit the sort assumed constant varied: the sort consumed its
+                    # keys, so the (deterministic) preprocess writes them again; full binning
+                    preprocess()
+                    num_intersects, gids, bins = bin_gaussians(xys, depths, radii, nth, H, W,
+                                                               keyed_workspace=ws1)
+                    layout_i = num_intersects
+                else:  # I > capacity: the blend saw empty tiles; bin and blend again
+                    gids, bins = spec.rebin()
+                    layout_i = spec.layout_intersects
+                    num_intersects = spec.num_intersects
+                if num_intersects >= 1:
+                    blend(gids, bins, layout_i)
+            else:
+                num_intersects = spec.num_intersects
+                gids = gids[:num_intersects]
         elif num_intersects >= 1:
             blend(gids, bins, layout_i)
         if num_intersects < 1:

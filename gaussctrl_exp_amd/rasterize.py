@@ -102,6 +102,7 @@ class _CountSlots:
             busy.add(free)
             buf, host = self.bufs[dev]
             host[free, :2] = -1
+            host[free, 2:] = 0  # (gsplat_bin_count_keyed_ex: violation flag, varying key bits)
             return free, buf[free], host[free]
 
     def release(self, dev, slot, visible=None):
@@ -166,7 +167,9 @@ def bin_gaussians(xys: Tensor, depths: Tensor, radii: Tensor, num_tiles_hit: Ten
     try:
         if keyed_workspace is not None:
             ws1 = keyed_workspace
-            _lib.call("gsplat_bin_count_keyed", n, tbx, tby, P(counts), P(ws1), ws1.numel(), st)
+            # (no pass skipped: learns the depth keys' varying bits for the speculative calls)
+            _lib.call("gsplat_bin_count_keyed_ex", n, tbx, tby, P(counts), P(ws1), ws1.numel(),
+                      0, st)
         else:
             ws1 = torch.empty((_lib.query("gsplat_bin_count_workspace_size", n),), device=dev,
                               dtype=torch.uint8)
@@ -186,6 +189,8 @@ def bin_gaussians(xys: Tensor, depths: Tensor, radii: Tensor, num_tiles_hit: Ten
                       ws1.numel(), P(pre[1]), pre[1].numel(), st)
         num_intersects = _wait_count(host, torch.cuda.current_stream(dev))
         visible = int(host[0])
+        if keyed_workspace is not None:
+            _note_key_range(key, host)
     finally:
         _COUNTS.release(dev, slot, visible)
     _EMIT_CAP[key] = emit_capacity(num_intersects)
@@ -222,21 +227,27 @@ class SpeculativeBinning:
         self.cap, self.ids, self.ws2, self.tile_bins = cap, ids, ws2, tile_bins
         self.layout_intersects = cap
         self.num_intersects = None
+        self.range_violated = False
 
     def finish(self) -> bool:
         visible = None
         try:
             I = _wait_count(self.host, torch.cuda.current_stream(self.dev))
             visible = int(self.host[0])
+            # a depth-sort digit assumed constant from earlier calls varied: the order is wrong
+            # (the caller re-runs the preprocess -- the sort consumed its keys -- and re-bins)
+            self.range_violated = int(self.host[2]) != 0
+            _note_key_range(self.key, self.host)
         finally:
             _COUNTS.release(self.dev, self.slot, visible)
         self.num_intersects = I
         _EMIT_CAP[self.key] = emit_capacity(I)
-        return I <= self.cap
+        return I <= self.cap and not self.range_violated
 
     def rebin(self):
-        """After an overflow: the emission and tile sort for the exact I (phase 1's workspace is
-        untouched by the speculative launch) -> (ids [I], tile_bins)."""
+        """After an overflow (not a range violation): the emission and tile sort for the exact I
+        (phase 1's workspace is untouched by the speculative launch) -> (ids [I], tile_bins)."""
+        assert not self.range_violated
         I = self.num_intersects
         P, st = _lib.ptr, _lib.stream(self.dev)
         ids_buf, ws2 = _emit_buffers(self.dev, self.n, I, self.tbx, self.tby)
@@ -270,7 +281,8 @@ def bin_gaussians_speculative(xys: Tensor, depths: Tensor, radii: Tensor, num_ti
     ids_buf, ws2 = _emit_buffers(dev, n, cap, tbx, tby)
     slot, counts, host = _COUNTS.acquire(dev)
     try:
-        _lib.call("gsplat_bin_count_keyed", n, tbx, tby, P(counts), P(ws1), ws1.numel(), st)
+        _lib.call("gsplat_bin_count_keyed_ex", n, tbx, tby, P(counts), P(ws1), ws1.numel(),
+                  _assumed_constant(key), st)
         rc = _lib.lib().gsplat_bin_emit_speculative(n, cap, tbx, tby, P(ids_buf), P(tile_bins),
                                                     P(ws1), ws1.numel(), P(ws2), ws2.numel(), st)
         if rc == 2:  # the scheme needs I on the host: finish as bin_gaussians does
@@ -279,8 +291,16 @@ def bin_gaussians_speculative(xys: Tensor, depths: Tensor, radii: Tensor, num_ti
                 _lib.call("gsplat_bin_emit_prelaunch", n, cap, tbx, tby, P(tile_bins), P(ws1),
                           ws1.numel(), P(ws2), ws2.numel(), st)
             I = _wait_count(host, torch.cuda.current_stream(dev))
+            violated = int(host[2]) != 0
+            _note_key_range(key, host)
             _COUNTS.release(dev, slot, int(host[0]))
             slot = None
+            if violated:  # (an assumed-constant depth digit varied: the caller starts over)
+                done = SpeculativeBinning(dev, n, tbx, tby, ws1, None, None, None, key, cap,
+                                          ids_buf, ws2, tile_bins)
+                done.num_intersects, done.range_violated = I, True
+                done.finish = lambda: False
+                return done
             _EMIT_CAP[key] = emit_capacity(I)
             if I <= cap:
                 _lib.call("gsplat_bin_emit_finish", n, I, cap, tbx, tby, P(pre[0]), P(tile_bins),
@@ -309,6 +329,20 @@ def bin_gaussians_speculative(xys: Tensor, depths: Tensor, radii: Tensor, num_ti
 
 # frame shape -> the intersection capacity to pre-allocate the emission's outputs for
 _EMIT_CAP = {}
+# frame shape -> the depth-key bits seen varying over the visible Gaussians (the union over
+# calls, from gsplat_bin_count_keyed_ex's d_counts[3]); the speculative binning skips the
+# depth-sort passes whose digit lies in the complement (GSPLAT_MI355X_ASSUME_RANGE=0: never)
+_KEY_VARY = {}
+ASSUME_KEY_RANGE = os.environ.get("GSPLAT_MI355X_ASSUME_RANGE", "1") != "0"
+
+
+def _note_key_range(key, host):
+    _KEY_VARY[key] = _KEY_VARY.get(key, 0) | (int(host[3]) & 0xFFFFFFFF)
+
+
+def _assumed_constant(key) -> int:
+    v = _KEY_VARY.get(key)
+    return 0 if v is None or not ASSUME_KEY_RANGE else (~v) & 0xFFFFFFFF
 # the fused render bins speculatively (bin_gaussians_speculative); GSPLAT_MI355X_SPECULATIVE=0
 # turns it off (A/B runs)
 SPECULATIVE_BINNING = os.environ.get("GSPLAT_MI355X_SPECULATIVE", "1") != "0"

@@ -196,6 +196,16 @@ int gsplat_bin_count(int num_points, const float *xys, const float *depths,
 int gsplat_bin_count_keyed(int num_points, int tile_bounds_x, int tile_bounds_y,
                            int32_t *d_counts, void *workspace1, size_t workspace1_bytes,
                            void *stream);
+/* gsplat_bin_count_keyed with the depth-key range carried across calls (d_counts: int32[4],
+ * [2] and [3] zeroed by the caller): depth-sort passes over key bits `assume_const` covers --
+ * bits an earlier call found constant over the visible depths, e.g. the shared exponent byte --
+ * are not launched.  Afterwards d_counts[2] = 1 if this call's visible depth keys do vary in an
+ * assumed-constant bit (the order, and every binning output after it, is then wrong: re-bin
+ * with assume_const = 0), d_counts[3] = the key bits that vary (the next call's assumption is
+ * its complement).  assume_const = 0: gsplat_bin_count_keyed's results. */
+int gsplat_bin_count_keyed_ex(int num_points, int tile_bounds_x, int tile_bounds_y,
+                              int32_t *d_counts, void *workspace1, size_t workspace1_bytes,
+                              uint32_t assume_const, void *stream);
 int gsplat_bin_emit(int num_points, int64_t num_intersects, int tile_bounds_x,
                     int tile_bounds_y, int32_t *gaussian_ids_sorted, int32_t *tile_bins,
                     const void *workspace1, size_t workspace1_bytes, void *workspace2,

@@ -45,6 +45,27 @@
 
 #define BLOCK 16
 
+/* The oracle's arithmetic type: float (gsplat's fp32, liboracle.so -- the GPU's checker), or
+ * double (-DORACLE_F64, liboracle64.so): the SAME algorithm in double precision, which pins the
+ * hand-written VJPs against float64 autograd far below the parity bar and, compared with the
+ * float build, bounds what fp32 rounding alone contributes (tests/test_oracle_autograd.py).
+ * Constants keep gsplat's float values (their f suffixes) in both builds. */
+#ifdef ORACLE_F64
+typedef double real;
+#define RSQRT sqrt
+#define RMAX fmax
+#define RMIN fmin
+#define REXP exp
+#define RCEIL ceil
+#else
+typedef float real;
+#define RSQRT sqrtf
+#define RMAX fmaxf
+#define RMIN fminf
+#define REXP expf
+#define RCEIL ceilf
+#endif
+
 /* gsplat 0.1.2.1 behaviours recalled but unverified (SURVEY.md Appendix A [VERIFY]), the same
  * bits as include/gsplat_mi355x.h GSPLAT_QUIRK_* (the HIP library's gsplat_set_quirks):
  *   1 ALPHA_099      A10 backward alpha clamp 0.99 -- applied by the callers' alpha_max
@@ -62,7 +83,7 @@ int oracle_get_quirks(void) { return g_quirks; }
 /* float->int conversion with the GPU's saturating semantics (v_cvt_i32_f32 / PTX
  * cvt.rzi.s32.f32): truncate toward zero, clamp to the int32 range, NaN -> 0.  A plain C
  * cast is undefined out of range (x86 returns INT_MIN). */
-static int f2i_sat(float x) {
+static int f2i_sat(real x) {
     if (x != x) return 0;
     if (x >= 2147483648.0f) return 2147483647;
     if (x <= -2147483648.0f) return (-2147483647 - 1);
@@ -71,8 +92,8 @@ static int f2i_sat(float x) {
 
 /* 3x3 matrices are row-major m[r*3+c].  mul() sums k = 0,1,2 left to right, the order
  * glm's mat3*mat3 uses. */
-static void mat3_mul(const float *a, const float *b, float *out) {
-    float t[9];
+static void mat3_mul(const real *a, const real *b, real *out) {
+    real t[9];
     for (int r = 0; r < 3; ++r)
         for (int c = 0; c < 3; ++c)
             t[r * 3 + c] = a[r * 3 + 0] * b[0 * 3 + c] + a[r * 3 + 1] * b[1 * 3 + c] +
@@ -80,8 +101,8 @@ static void mat3_mul(const float *a, const float *b, float *out) {
     memcpy(out, t, sizeof(t));
 }
 
-static void mat3_transpose(const float *a, float *out) {
-    float t[9];
+static void mat3_transpose(const real *a, real *out) {
+    real t[9];
     for (int r = 0; r < 3; ++r)
         for (int c = 0; c < 3; ++c) t[c * 3 + r] = a[r * 3 + c];
     memcpy(out, t, sizeof(t));
@@ -89,9 +110,9 @@ static void mat3_transpose(const float *a, float *out) {
 
 /* quat_to_rotmat (helpers.cuh): q = (w,x,y,z), normalised internally.  gsplat uses
  * rsqrtf; both sides here use the correctly rounded 1/sqrtf so they agree bit for bit. */
-static void quat_to_rotmat(const float *q, float *R) {
-    float s = 1.f / sqrtf(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
-    float w = q[0] * s, x = q[1] * s, y = q[2] * s, z = q[3] * s;
+static void quat_to_rotmat(const real *q, real *R) {
+    real s = 1.f / RSQRT(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+    real w = q[0] * s, x = q[1] * s, y = q[2] * s, z = q[3] * s;
     R[0] = 1.f - 2.f * (y * y + z * z);
     R[1] = 2.f * (x * y - w * z);
     R[2] = 2.f * (x * z + w * y);
@@ -104,9 +125,9 @@ static void quat_to_rotmat(const float *q, float *R) {
 }
 
 /* scale_rot_to_cov3d (helpers.cuh): M = R*S, Sigma = M*M^T, upper triangle stored. */
-static void scale_rot_to_cov3d(const float *scale, float glob_scale, const float *q,
-                               float *cov3d) {
-    float R[9], S[9] = {0}, M[9], Mt[9], V[9];
+static void scale_rot_to_cov3d(const real *scale, real glob_scale, const real *q,
+                               real *cov3d) {
+    real R[9], S[9] = {0}, M[9], Mt[9], V[9];
     quat_to_rotmat(q, R);
     S[0] = glob_scale * scale[0];
     S[4] = glob_scale * scale[1];
@@ -127,22 +148,22 @@ static void scale_rot_to_cov3d(const float *scale, float glob_scale, const float
 /* project_cov3d_ewa (helpers.cuh).  W = viewmat[:3,:3] (row-major input),
  * t = W*mean + viewmat[:3,3], clamp x/z,y/z to +-1.3*tan_fov, J as in SURVEY a1,
  * cov = (J*W) * V * (J*W)^T, +0.3 on the diagonal. */
-static void project_cov3d_ewa(const float *mean, const float *cov3d, const float *vm,
-                              float fx, float fy, float tan_fovx, float tan_fovy,
-                              float *cov2d) {
-    float tx = vm[0] * mean[0] + vm[1] * mean[1] + vm[2] * mean[2] + vm[3];
-    float ty = vm[4] * mean[0] + vm[5] * mean[1] + vm[6] * mean[2] + vm[7];
-    float tz = vm[8] * mean[0] + vm[9] * mean[1] + vm[10] * mean[2] + vm[11];
-    float lim_x = 1.3f * tan_fovx, lim_y = 1.3f * tan_fovy;
-    tx = tz * fminf(lim_x, fmaxf(-lim_x, tx / tz));
-    ty = tz * fminf(lim_y, fmaxf(-lim_y, ty / tz));
-    float rz = 1.f / tz;
-    float rz2 = rz * rz;
-    float J[9] = {fx * rz, 0.f, -fx * tx * rz2, 0.f, fy * rz, -fy * ty * rz2, 0.f, 0.f, 0.f};
-    float W[9] = {vm[0], vm[1], vm[2], vm[4], vm[5], vm[6], vm[8], vm[9], vm[10]};
-    float V[9] = {cov3d[0], cov3d[1], cov3d[2], cov3d[1], cov3d[3],
+static void project_cov3d_ewa(const real *mean, const real *cov3d, const real *vm,
+                              real fx, real fy, real tan_fovx, real tan_fovy,
+                              real *cov2d) {
+    real tx = vm[0] * mean[0] + vm[1] * mean[1] + vm[2] * mean[2] + vm[3];
+    real ty = vm[4] * mean[0] + vm[5] * mean[1] + vm[6] * mean[2] + vm[7];
+    real tz = vm[8] * mean[0] + vm[9] * mean[1] + vm[10] * mean[2] + vm[11];
+    real lim_x = 1.3f * tan_fovx, lim_y = 1.3f * tan_fovy;
+    tx = tz * RMIN(lim_x, RMAX(-lim_x, tx / tz));
+    ty = tz * RMIN(lim_y, RMAX(-lim_y, ty / tz));
+    real rz = 1.f / tz;
+    real rz2 = rz * rz;
+    real J[9] = {fx * rz, 0.f, -fx * tx * rz2, 0.f, fy * rz, -fy * ty * rz2, 0.f, 0.f, 0.f};
+    real W[9] = {vm[0], vm[1], vm[2], vm[4], vm[5], vm[6], vm[8], vm[9], vm[10]};
+    real V[9] = {cov3d[0], cov3d[1], cov3d[2], cov3d[1], cov3d[3],
                   cov3d[4], cov3d[2], cov3d[4], cov3d[5]};
-    float T[9], TV[9], Tt[9], C[9];
+    real T[9], TV[9], Tt[9], C[9];
     mat3_mul(J, W, T);
     mat3_mul(T, V, TV);
     mat3_transpose(T, Tt);
@@ -154,37 +175,37 @@ static void project_cov3d_ewa(const float *mean, const float *cov3d, const float
 }
 
 /* compute_cov2d_bounds (helpers.cuh). */
-static int compute_cov2d_bounds(const float *cov2d, float *conic, float *radius) {
-    float det = cov2d[0] * cov2d[2] - cov2d[1] * cov2d[1];
+static int compute_cov2d_bounds(const real *cov2d, real *conic, real *radius) {
+    real det = cov2d[0] * cov2d[2] - cov2d[1] * cov2d[1];
     if (det == 0.f) return 0;
-    float inv_det = 1.f / det;
+    real inv_det = 1.f / det;
     conic[0] = cov2d[2] * inv_det;
     conic[1] = -cov2d[1] * inv_det;
     conic[2] = cov2d[0] * inv_det;
-    float b = 0.5f * (cov2d[0] + cov2d[2]);
-    float v1 = b + sqrtf(fmaxf(0.1f, b * b - det));
-    float v2 = b - sqrtf(fmaxf(0.1f, b * b - det));
+    real b = 0.5f * (cov2d[0] + cov2d[2]);
+    real v1 = b + RSQRT(RMAX(0.1f, b * b - det));
+    real v2 = b - RSQRT(RMAX(0.1f, b * b - det));
     *radius = ceilf(3.f * sqrtf(fmaxf(v1, v2)));
     return 1;
 }
 
 /* project_pix + ndc2pix (helpers.cuh). */
-static void project_pix(const float *P, const float *p, int W, int H, float cx, float cy,
-                        float *xy) {
-    float hx = P[0] * p[0] + P[1] * p[1] + P[2] * p[2] + P[3];
-    float hy = P[4] * p[0] + P[5] * p[1] + P[6] * p[2] + P[7];
-    float hw = P[12] * p[0] + P[13] * p[1] + P[14] * p[2] + P[15];
-    float rw = 1.f / (hw + 1e-6f);
-    float nx = hx * rw, ny = hy * rw;
-    xy[0] = 0.5f * (float)W * nx + cx - 0.5f;
-    xy[1] = 0.5f * (float)H * ny + cy - 0.5f;
+static void project_pix(const real *P, const real *p, int W, int H, real cx, real cy,
+                        real *xy) {
+    real hx = P[0] * p[0] + P[1] * p[1] + P[2] * p[2] + P[3];
+    real hy = P[4] * p[0] + P[5] * p[1] + P[6] * p[2] + P[7];
+    real hw = P[12] * p[0] + P[13] * p[1] + P[14] * p[2] + P[15];
+    real rw = 1.f / (hw + 1e-6f);
+    real nx = hx * rw, ny = hy * rw;
+    xy[0] = 0.5f * (real)W * nx + cx - 0.5f;
+    xy[1] = 0.5f * (real)H * ny + cy - 0.5f;
 }
 
 /* get_tile_bbox / get_bbox (helpers.cuh): inclusive min, exclusive max, in tiles. */
-static void get_tile_bbox(const float *xy, float radius, int tbx, int tby, int *tmin,
+static void get_tile_bbox(const real *xy, real radius, int tbx, int tby, int *tmin,
                           int *tmax) {
-    float cx = xy[0] / (float)BLOCK, cy = xy[1] / (float)BLOCK;
-    float rx = radius / (float)BLOCK, ry = radius / (float)BLOCK;
+    real cx = xy[0] / (real)BLOCK, cy = xy[1] / (real)BLOCK;
+    real rx = radius / (real)BLOCK, ry = radius / (real)BLOCK;
     int a;
     a = f2i_sat(cx - rx); a = a < 0 ? 0 : a; tmin[0] = a < tbx ? a : tbx;
     a = f2i_sat(cx + rx + 1.f); a = a < 0 ? 0 : a; tmax[0] = a < tbx ? a : tbx;
@@ -194,30 +215,30 @@ static void get_tile_bbox(const float *xy, float radius, int tbx, int tby, int *
 
 /* ------------------------------------------------------- projection forward */
 
-void oracle_project_forward(int n, const float *means, const float *scales, float glob_scale,
-                            const float *quats, const float *viewmat, const float *projmat,
-                            float fx, float fy, float cx, float cy, int H, int W, int tbx,
-                            int tby, float clip_thresh, float *cov3d, float *xys,
-                            float *depths, int *radii, float *conics, int *num_tiles_hit) {
+void oracle_project_forward(int n, const real *means, const real *scales, real glob_scale,
+                            const real *quats, const real *viewmat, const real *projmat,
+                            real fx, real fy, real cx, real cy, int H, int W, int tbx,
+                            int tby, real clip_thresh, real *cov3d, real *xys,
+                            real *depths, int *radii, real *conics, int *num_tiles_hit) {
     /* tan_fov is computed in double in gsplat (0.5 is a double literal). */
-    float tan_fovx = (float)(0.5 * (double)W / (double)fx);
-    float tan_fovy = (float)(0.5 * (double)H / (double)fy);
+    real tan_fovx = (real)(0.5 * (double)W / (double)fx);
+    real tan_fovy = (real)(0.5 * (double)H / (double)fy);
     for (int i = 0; i < n; ++i) {
-        const float *p = means + 3 * i;
+        const real *p = means + 3 * i;
         radii[i] = 0;
         num_tiles_hit[i] = 0;
         /* clip_near_plane: p_view = viewmat * p, cull if z <= clip_thresh */
-        float pz = viewmat[8] * p[0] + viewmat[9] * p[1] + viewmat[10] * p[2] + viewmat[11];
+        real pz = viewmat[8] * p[0] + viewmat[9] * p[1] + viewmat[10] * p[2] + viewmat[11];
         if (pz <= clip_thresh) continue;
-        float *c3 = cov3d + 6 * i;
+        real *c3 = cov3d + 6 * i;
         scale_rot_to_cov3d(scales + 3 * i, glob_scale, quats + 4 * i, c3);
-        float cov2d[3], conic[3], radius;
+        real cov2d[3], conic[3], radius;
         project_cov3d_ewa(p, c3, viewmat, fx, fy, tan_fovx, tan_fovy, cov2d);
         if (!compute_cov2d_bounds(cov2d, conic, &radius)) continue;
         conics[3 * i + 0] = conic[0]; /* written before the tile-area cull */
         conics[3 * i + 1] = conic[1];
         conics[3 * i + 2] = conic[2];
-        float xy[2];
+        real xy[2];
         project_pix(projmat, p, W, H, cx, cy, xy);
         int tmin[2], tmax[2];
         get_tile_bbox(xy, radius, tbx, tby, tmin, tmax);
@@ -234,19 +255,19 @@ void oracle_project_forward(int n, const float *means, const float *scales, floa
 /* ------------------------------------------------------ projection backward */
 
 /* cov2d_to_conic_vjp (helpers.cuh) */
-static void cov2d_to_conic_vjp(const float *conic, const float *v_conic, float *v_cov2d) {
+static void cov2d_to_conic_vjp(const real *conic, const real *v_conic, real *v_cov2d) {
     /* X = [[a,b],[b,c]], G = [[va,vb],[vb,vc]], v_Sigma = -X G X.  G holds the gradient of
      * each symmetric entry: gsplat's halved v_conic.y as is (CONIC_HALF), else half of
      * d loss / d conic.y. */
-    float a = conic[0], b = conic[1], c = conic[2];
-    float ga = v_conic[0], gb = v_conic[1], gc = v_conic[2];
+    real a = conic[0], b = conic[1], c = conic[2];
+    real ga = v_conic[0], gb = v_conic[1], gc = v_conic[2];
     if (!(g_quirks & Q_CONIC_HALF)) gb = 0.5f * gb;
     /* XG */
-    float xg00 = a * ga + b * gb, xg01 = a * gb + b * gc;
-    float xg10 = b * ga + c * gb, xg11 = b * gb + c * gc;
+    real xg00 = a * ga + b * gb, xg01 = a * gb + b * gc;
+    real xg10 = b * ga + c * gb, xg11 = b * gb + c * gc;
     /* (XG)X */
-    float s00 = xg00 * a + xg01 * b, s01 = xg00 * b + xg01 * c;
-    float s10 = xg10 * a + xg11 * b, s11 = xg10 * b + xg11 * c;
+    real s00 = xg00 * a + xg01 * b, s01 = xg00 * b + xg01 * c;
+    real s10 = xg10 * a + xg11 * b, s11 = xg10 * b + xg11 * c;
     v_cov2d[0] = -s00;
     v_cov2d[1] = -s10 + -s01;
     v_cov2d[2] = -s11;
@@ -254,13 +275,13 @@ static void cov2d_to_conic_vjp(const float *conic, const float *v_conic, float *
 
 /* project_pix_vjp (helpers.cuh): the w-derivative of the perspective divide is
  * computed but dropped by gsplat 0.1.x; only P[:3,:3]^T (v_ndc*rw, 0) is returned. */
-static void project_pix_vjp(const float *P, const float *p, int W, int H, const float *v_xy,
-                            float *v_mean) {
-    float hw = P[12] * p[0] + P[13] * p[1] + P[14] * p[2] + P[15];
-    float rw = 1.f / (hw + 1e-6f);
-    float vnx = 0.5f * (float)W * v_xy[0];
-    float vny = 0.5f * (float)H * v_xy[1];
-    float vpx = vnx * rw, vpy = vny * rw, vpz = 0.f;
+static void project_pix_vjp(const real *P, const real *p, int W, int H, const real *v_xy,
+                            real *v_mean) {
+    real hw = P[12] * p[0] + P[13] * p[1] + P[14] * p[2] + P[15];
+    real rw = 1.f / (hw + 1e-6f);
+    real vnx = 0.5f * (real)W * v_xy[0];
+    real vny = 0.5f * (real)H * v_xy[1];
+    real vpx = vnx * rw, vpy = vny * rw, vpz = 0.f;
     v_mean[0] = P[0] * vpx + P[4] * vpy + P[8] * vpz;
     v_mean[1] = P[1] * vpx + P[5] * vpy + P[9] * vpz;
     v_mean[2] = P[2] * vpx + P[6] * vpy + P[10] * vpz;
@@ -269,31 +290,31 @@ static void project_pix_vjp(const float *P, const float *p, int W, int H, const 
 /* project_cov3d_ewa_vjp (helpers.cuh): t is recomputed WITHOUT the fov clamp
  * (EWA_UNCLAMPED); otherwise the derivative of the clamped forward: t_x = t_z clamp(t_x/t_z)
  * passes d/dt_x inside the clamp and +-lim d/dt_z outside it. */
-static void project_cov3d_ewa_vjp(const float *mean, const float *cov3d, const float *vm,
-                                  float fx, float fy, float tan_fovx, float tan_fovy,
-                                  const float *v_cov2d, float *v_mean, float *v_cov3d) {
-    float W[9] = {vm[0], vm[1], vm[2], vm[4], vm[5], vm[6], vm[8], vm[9], vm[10]};
-    float tx = vm[0] * mean[0] + vm[1] * mean[1] + vm[2] * mean[2] + vm[3];
-    float ty = vm[4] * mean[0] + vm[5] * mean[1] + vm[6] * mean[2] + vm[7];
-    float tz = vm[8] * mean[0] + vm[9] * mean[1] + vm[10] * mean[2] + vm[11];
+static void project_cov3d_ewa_vjp(const real *mean, const real *cov3d, const real *vm,
+                                  real fx, real fy, real tan_fovx, real tan_fovy,
+                                  const real *v_cov2d, real *v_mean, real *v_cov3d) {
+    real W[9] = {vm[0], vm[1], vm[2], vm[4], vm[5], vm[6], vm[8], vm[9], vm[10]};
+    real tx = vm[0] * mean[0] + vm[1] * mean[1] + vm[2] * mean[2] + vm[3];
+    real ty = vm[4] * mean[0] + vm[5] * mean[1] + vm[6] * mean[2] + vm[7];
+    real tz = vm[8] * mean[0] + vm[9] * mean[1] + vm[10] * mean[2] + vm[11];
     int clamped = !(g_quirks & Q_EWA_UNCLAMPED);
-    float limx = 1.3f * tan_fovx, limy = 1.3f * tan_fovy, sx = 0.f, sy = 0.f;
+    real limx = 1.3f * tan_fovx, limy = 1.3f * tan_fovy, sx = 0.f, sy = 0.f;
     if (clamped) {
-        float ux = tx / tz, uy = ty / tz;
+        real ux = tx / tz, uy = ty / tz;
         sx = ux < -limx ? -limx : (ux > limx ? limx : 0.f);
         sy = uy < -limy ? -limy : (uy > limy ? limy : 0.f);
-        tx = tz * fminf(limx, fmaxf(-limx, ux));
-        ty = tz * fminf(limy, fmaxf(-limy, uy));
+        tx = tz * RMIN(limx, RMAX(-limx, ux));
+        ty = tz * RMIN(limy, RMAX(-limy, uy));
     }
-    float rz = 1.f / tz;
-    float rz2 = rz * rz;
-    float rz3 = rz2 * rz;
-    float J[9] = {fx * rz, 0.f, -fx * tx * rz2, 0.f, fy * rz, -fy * ty * rz2, 0.f, 0.f, 0.f};
-    float V[9] = {cov3d[0], cov3d[1], cov3d[2], cov3d[1], cov3d[3],
+    real rz = 1.f / tz;
+    real rz2 = rz * rz;
+    real rz3 = rz2 * rz;
+    real J[9] = {fx * rz, 0.f, -fx * tx * rz2, 0.f, fy * rz, -fy * ty * rz2, 0.f, 0.f, 0.f};
+    real V[9] = {cov3d[0], cov3d[1], cov3d[2], cov3d[1], cov3d[3],
                   cov3d[4], cov3d[2], cov3d[4], cov3d[5]};
-    float G[9] = {v_cov2d[0], 0.5f * v_cov2d[1], 0.f, 0.5f * v_cov2d[1], v_cov2d[2], 0.f,
+    real G[9] = {v_cov2d[0], 0.5f * v_cov2d[1], 0.f, 0.5f * v_cov2d[1], v_cov2d[2], 0.f,
                   0.f, 0.f, 0.f};
-    float T[9], Tt[9], Vt[9], Gt[9], tmp[9], vV[9], vT1[9], vT2[9], vT[9], Wt[9], vJ[9];
+    real T[9], Tt[9], Vt[9], Gt[9], tmp[9], vV[9], vT1[9], vT2[9], vT[9], Wt[9], vJ[9];
     mat3_mul(J, W, T);
     mat3_transpose(T, Tt);
     mat3_transpose(V, Vt);
@@ -317,13 +338,13 @@ static void project_cov3d_ewa_vjp(const float *mean, const float *cov3d, const f
     /* v_J = v_T * W^T; glm v_J[c][r] = vJ(r,c) */
     mat3_transpose(W, Wt);
     mat3_mul(vT, Wt, vJ);
-    float vJ20 = vJ[0 * 3 + 2]; /* glm v_J[2][0] = row 0, col 2 */
-    float vJ21 = vJ[1 * 3 + 2]; /* glm v_J[2][1] = row 1, col 2 */
-    float vJ00 = vJ[0];
-    float vJ11 = vJ[4];
-    float vt0 = -fx * rz2 * vJ20;
-    float vt1 = -fy * rz2 * vJ21;
-    float vt2 = -fx * rz2 * vJ00 + 2.f * fx * tx * rz3 * vJ20 - fy * rz2 * vJ11 +
+    real vJ20 = vJ[0 * 3 + 2]; /* glm v_J[2][0] = row 0, col 2 */
+    real vJ21 = vJ[1 * 3 + 2]; /* glm v_J[2][1] = row 1, col 2 */
+    real vJ00 = vJ[0];
+    real vJ11 = vJ[4];
+    real vt0 = -fx * rz2 * vJ20;
+    real vt1 = -fy * rz2 * vJ21;
+    real vt2 = -fx * rz2 * vJ00 + 2.f * fx * tx * rz3 * vJ20 - fy * rz2 * vJ11 +
                 2.f * fy * ty * rz3 * vJ21;
     if (clamped) {
         if (sx != 0.f) { vt2 += sx * vt0; vt0 = 0.f; }
@@ -337,9 +358,9 @@ static void project_cov3d_ewa_vjp(const float *mean, const float *cov3d, const f
 
 /* quat_to_rotmat_vjp (helpers.cuh): w.r.t. the normalised quaternion
  * components, no normalisation Jacobian.  vR is row-major; glm v_R[c][r] = vR(r,c). */
-static void quat_to_rotmat_vjp(const float *q, const float *vR, float *v_quat) {
-    float s = 1.f / sqrtf(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
-    float w = q[0] * s, x = q[1] * s, y = q[2] * s, z = q[3] * s;
+static void quat_to_rotmat_vjp(const real *q, const real *vR, real *v_quat) {
+    real s = 1.f / RSQRT(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+    real w = q[0] * s, x = q[1] * s, y = q[2] * s, z = q[3] * s;
 #define GR(c, r) vR[(r) * 3 + (c)]
     v_quat[0] = 2.f * (x * (GR(1, 2) - GR(2, 1)) + y * (GR(2, 0) - GR(0, 2)) +
                        z * (GR(0, 1) - GR(1, 0)));
@@ -353,12 +374,12 @@ static void quat_to_rotmat_vjp(const float *q, const float *vR, float *v_quat) {
 }
 
 /* scale_rot_to_cov3d_vjp (helpers.cuh) */
-static void scale_rot_to_cov3d_vjp(const float *scale, float glob_scale, const float *q,
-                                   const float *v_cov3d, float *v_scale, float *v_quat) {
-    float vV[9] = {v_cov3d[0],        0.5f * v_cov3d[1], 0.5f * v_cov3d[2],
+static void scale_rot_to_cov3d_vjp(const real *scale, real glob_scale, const real *q,
+                                   const real *v_cov3d, real *v_scale, real *v_quat) {
+    real vV[9] = {v_cov3d[0],        0.5f * v_cov3d[1], 0.5f * v_cov3d[2],
                    0.5f * v_cov3d[1], v_cov3d[3],        0.5f * v_cov3d[4],
                    0.5f * v_cov3d[2], 0.5f * v_cov3d[4], v_cov3d[5]};
-    float R[9], S[9] = {0}, M[9], vM[9], vR[9];
+    real R[9], S[9] = {0}, M[9], vM[9], vR[9];
     quat_to_rotmat(q, R);
     S[0] = glob_scale * scale[0];
     S[4] = glob_scale * scale[1];
@@ -375,23 +396,23 @@ static void scale_rot_to_cov3d_vjp(const float *scale, float glob_scale, const f
     quat_to_rotmat_vjp(q, vR, v_quat);
 }
 
-void oracle_project_backward(int n, const float *means, const float *scales, float glob_scale,
-                             const float *quats, const float *viewmat, const float *projmat,
-                             float fx, float fy, float cx, float cy, int H, int W,
-                             const float *cov3d, const int *radii, const float *conics,
-                             const float *v_xy, const float *v_depth, const float *v_conic,
-                             float *v_cov2d, float *v_cov3d, float *v_mean, float *v_scale,
-                             float *v_quat) {
+void oracle_project_backward(int n, const real *means, const real *scales, real glob_scale,
+                             const real *quats, const real *viewmat, const real *projmat,
+                             real fx, real fy, real cx, real cy, int H, int W,
+                             const real *cov3d, const int *radii, const real *conics,
+                             const real *v_xy, const real *v_depth, const real *v_conic,
+                             real *v_cov2d, real *v_cov3d, real *v_mean, real *v_scale,
+                             real *v_quat) {
     (void)cx;
     (void)cy;
-    float tan_fovx = (float)(0.5 * (double)W / (double)fx);
-    float tan_fovy = (float)(0.5 * (double)H / (double)fy);
+    real tan_fovx = (real)(0.5 * (double)W / (double)fx);
+    real tan_fovy = (real)(0.5 * (double)H / (double)fy);
     for (int i = 0; i < n; ++i) {
         if (radii[i] <= 0) continue;
-        const float *p = means + 3 * i;
-        float *vm = v_mean + 3 * i;
+        const real *p = means + 3 * i;
+        real *vm = v_mean + 3 * i;
         project_pix_vjp(projmat, p, W, H, v_xy + 2 * i, vm);
-        float vz = v_depth[i];
+        real vz = v_depth[i];
         vm[0] += viewmat[8] * vz;
         vm[1] += viewmat[9] * vz;
         vm[2] += viewmat[10] * vz;
@@ -405,14 +426,14 @@ void oracle_project_backward(int n, const float *means, const float *scales, flo
 
 /* ---------------------------------------------------------------------- SH */
 
-static const float SH_C0 = 0.28209479177387814f;
-static const float SH_C1 = 0.4886025119029199f;
-static const float SH_C2[5] = {1.0925484305920792f, -1.0925484305920792f, 0.31539156525252005f,
+static const real SH_C0 = 0.28209479177387814f;
+static const real SH_C1 = 0.4886025119029199f;
+static const real SH_C2[5] = {1.0925484305920792f, -1.0925484305920792f, 0.31539156525252005f,
                                -1.0925484305920792f, 0.5462742152960396f};
-static const float SH_C3[7] = {-0.5900435899266435f, 2.890611442640554f, -0.4570457994644658f,
+static const real SH_C3[7] = {-0.5900435899266435f, 2.890611442640554f, -0.4570457994644658f,
                                0.3731763325901154f,  -0.4570457994644658f, 1.445305721320277f,
                                -0.5900435899266435f};
-static const float SH_C4[9] = {2.5033429417967046f,  -1.7701307697799304f, 0.9461746957575601f,
+static const real SH_C4[9] = {2.5033429417967046f,  -1.7701307697799304f, 0.9461746957575601f,
                                -0.6690465435572892f, 0.10578554691520431f, -0.6690465435572892f,
                                0.47308734787878004f, -1.7701307697799304f, 0.6258357354491761f};
 
@@ -425,12 +446,12 @@ int oracle_num_sh_bases(int degree) {
 }
 
 /* SH basis values b_k(dir) in the order sh_coeffs_to_color consumes them (sh.cuh). */
-static int sh_basis(int degree, const float *dir, float *b) {
+static int sh_basis(int degree, const real *dir, real *b) {
     b[0] = SH_C0;
     if (degree < 1) return 1;
-    float norm = sqrtf(dir[0] * dir[0] + dir[1] * dir[1] + dir[2] * dir[2]);
-    float x = dir[0] / norm, y = dir[1] / norm, z = dir[2] / norm;
-    float xx = x * x, xy = x * y, xz = x * z, yy = y * y, yz = y * z, zz = z * z;
+    real norm = RSQRT(dir[0] * dir[0] + dir[1] * dir[1] + dir[2] * dir[2]);
+    real x = dir[0] / norm, y = dir[1] / norm, z = dir[2] / norm;
+    real xx = x * x, xy = x * y, xz = x * z, yy = y * y, yz = y * z, zz = z * z;
     b[1] = -SH_C1 * y;
     b[2] = SH_C1 * z;
     b[3] = -SH_C1 * x;
@@ -464,17 +485,17 @@ static int sh_basis(int degree, const float *dir, float *b) {
 /* compute_sh_forward_kernel: colors[c] = sum_k b_k * coeffs[k][c], k < num_sh_bases(
  * degrees_to_use); the coefficient stride is num_sh_bases(degree).  Sums
  * are accumulated degree band by degree band like sh_coeffs_to_color. */
-void oracle_sh_forward(int n, int degree, int degrees_to_use, const float *viewdirs,
-                       const float *coeffs, float *colors) {
+void oracle_sh_forward(int n, int degree, int degrees_to_use, const real *viewdirs,
+                       const real *coeffs, real *colors) {
     int K = oracle_num_sh_bases(degree);
-    float b[25];
+    real b[25];
     for (int i = 0; i < n; ++i) {
         int nb = sh_basis(degrees_to_use, viewdirs + 3 * i, b);
-        const float *co = coeffs + (size_t)i * K * 3;
+        const real *co = coeffs + (size_t)i * K * 3;
         for (int c = 0; c < 3; ++c) {
-            float acc = b[0] * co[c];
+            real acc = b[0] * co[c];
             for (int band = 1; (band + 1) * (band + 1) <= nb; ++band) {
-                float s = 0.f;
+                real s = 0.f;
                 for (int k = band * band; k < (band + 1) * (band + 1); ++k)
                     s += b[k] * co[k * 3 + c];
                 acc += s;
@@ -484,13 +505,13 @@ void oracle_sh_forward(int n, int degree, int degrees_to_use, const float *viewd
     }
 }
 
-void oracle_sh_backward(int n, int degree, int degrees_to_use, const float *viewdirs,
-                        const float *v_colors, float *v_coeffs) {
+void oracle_sh_backward(int n, int degree, int degrees_to_use, const real *viewdirs,
+                        const real *v_colors, real *v_coeffs) {
     int K = oracle_num_sh_bases(degree);
-    float b[25];
+    real b[25];
     for (int i = 0; i < n; ++i) {
         int nb = sh_basis(degrees_to_use, viewdirs + 3 * i, b);
-        float *vc = v_coeffs + (size_t)i * K * 3;
+        real *vc = v_coeffs + (size_t)i * K * 3;
         for (int k = 0; k < K; ++k)
             for (int c = 0; c < 3; ++c)
                 vc[k * 3 + c] = k < nb ? b[k] * v_colors[3 * i + c] : 0.f;
@@ -499,9 +520,9 @@ void oracle_sh_backward(int n, int degree, int degrees_to_use, const float *view
 
 /* compute_cov2d_bounds_kernel.  gsplat writes uninitialised locals when det == 0; this
  * restatement (and the HIP kernel) write zeros there. */
-void oracle_cov2d_bounds(int n, const float *cov2d, float *conics, float *radii) {
+void oracle_cov2d_bounds(int n, const real *cov2d, real *conics, real *radii) {
     for (int i = 0; i < n; ++i) {
-        float conic[3] = {0.f, 0.f, 0.f}, radius = 0.f;
+        real conic[3] = {0.f, 0.f, 0.f}, radius = 0.f;
         if (!compute_cov2d_bounds(cov2d + 3 * i, conic, &radius)) {
             conic[0] = conic[1] = conic[2] = 0.f;
             radius = 0.f;
@@ -516,13 +537,13 @@ void oracle_cov2d_bounds(int n, const float *cov2d, float *conics, float *radii)
 /* ----------------------------------------------------------------- binning */
 
 /* map_gaussian_to_intersects (forward.cu) */
-void oracle_map_intersects(int n, const float *xys, const float *depths, const int *radii,
+void oracle_map_intersects(int n, const real *xys, const real *depths, const int *radii,
                            const int *cum_tiles_hit, int tbx, int tby, int64_t *isect_ids,
                            int *gaussian_ids) {
     for (int i = 0; i < n; ++i) {
         if (radii[i] <= 0) continue;
         int tmin[2], tmax[2];
-        get_tile_bbox(xys + 2 * i, (float)radii[i], tbx, tby, tmin, tmax);
+        get_tile_bbox(xys + 2 * i, (real)radii[i], tbx, tby, tmin, tmax);
         int cur = i == 0 ? 0 : cum_tiles_hit[i - 1];
         int32_t dbits;
         memcpy(&dbits, depths + i, 4);
@@ -592,12 +613,12 @@ void oracle_tile_bin_edges(int64_t num_isects, const int64_t *isect_sorted, int 
  * transmittance.  tile_list (may be NULL) restricts the work to a subset of tiles (CPU
  * baseline sampling). */
 void oracle_rasterize_forward(int tbx, int tby, int H, int W, int C, const int *gids_sorted,
-                              const int *tile_bins, const float *xys, const float *conics,
-                              const float *colors, const float *opacity, const float *bg,
-                              const int *tile_list, int num_tile_list, float *out_img,
-                              float *final_Ts, int *final_idx) {
+                              const int *tile_bins, const real *xys, const real *conics,
+                              const real *colors, const real *opacity, const real *bg,
+                              const int *tile_list, int num_tile_list, real *out_img,
+                              real *final_Ts, int *final_idx) {
     int ntiles = tile_list ? num_tile_list : tbx * tby;
-    float acc[64];
+    real acc[64];
     for (int tt = 0; tt < ntiles; ++tt) {
         int t = tile_list ? tile_list[tt] : tt;
         int tx = t % tbx, ty = t / tbx;
@@ -606,20 +627,20 @@ void oracle_rasterize_forward(int tbx, int tby, int H, int W, int C, const int *
             for (int lj = 0; lj < BLOCK; ++lj) {
                 int i = ty * BLOCK + li, j = tx * BLOCK + lj;
                 if (i >= H || j >= W) continue;
-                float px = (float)j, py = (float)i;
-                float T = 1.f;
+                real px = (real)j, py = (real)i;
+                real T = 1.f;
                 int cur = 0;
                 for (int c = 0; c < C; ++c) acc[c] = 0.f;
                 for (int k = start; k < end; ++k) {
                     int g = gids_sorted[k];
-                    const float *cn = conics + 3 * g;
-                    float dx = xys[2 * g] - px, dy = xys[2 * g + 1] - py;
-                    float sigma = 0.5f * (cn[0] * dx * dx + cn[2] * dy * dy) + cn[1] * dx * dy;
-                    float alpha = fminf(0.999f, opacity[g] * expf(-sigma));
+                    const real *cn = conics + 3 * g;
+                    real dx = xys[2 * g] - px, dy = xys[2 * g + 1] - py;
+                    real sigma = 0.5f * (cn[0] * dx * dx + cn[2] * dy * dy) + cn[1] * dx * dy;
+                    real alpha = RMIN(0.999f, opacity[g] * REXP(-sigma));
                     if (sigma < 0.f || alpha < 1.f / 255.f) continue;
-                    float next_T = T * (1.f - alpha);
+                    real next_T = T * (1.f - alpha);
                     if (next_T <= 1e-4f) break;
-                    float vis = alpha * T;
+                    real vis = alpha * T;
                     for (int c = 0; c < C; ++c) acc[c] = acc[c] + colors[(size_t)C * g + c] * vis;
                     T = next_T;
                     cur = k;
@@ -636,13 +657,13 @@ void oracle_rasterize_forward(int tbx, int tby, int H, int W, int C, const int *
  * each pixel's final_idx, recovering T by division; alpha clamp alpha_max (gsplat 0.1.x:
  * 0.99 in backward vs 0.999 in forward); per-Gaussian sums accumulated in double. */
 void oracle_rasterize_backward(int tbx, int tby, int H, int W, int C, int num_points,
-                               const int *gids_sorted, const int *tile_bins, const float *xys,
-                               const float *conics, const float *colors, const float *opacity,
-                               const float *bg, const float *final_Ts, const int *final_idx,
-                               const float *v_out, const float *v_out_alpha, float alpha_max,
-                               const int *tile_list, int num_tile_list, float *v_xy,
-                               float *v_conic, float *v_colors, float *v_opacity,
-                               float *abs_sum, float *drift_sum, float *flip_sum) {
+                               const int *gids_sorted, const int *tile_bins, const real *xys,
+                               const real *conics, const real *colors, const real *opacity,
+                               const real *bg, const real *final_Ts, const int *final_idx,
+                               const real *v_out, const real *v_out_alpha, real alpha_max,
+                               const int *tile_list, int num_tile_list, real *v_xy,
+                               real *v_conic, real *v_colors, real *v_opacity,
+                               real *abs_sum, real *drift_sum, real *flip_sum) {
     /* abs_sum (optional, [num_points, 6+C] in the order xy0 xy1 con0 con1 con2 opac colors):
      * the sum of |term| over the per-pixel contributions of each gradient element -- the
      * scale of the fp32 summation error any implementation accumulating in fp32 incurs.
@@ -659,7 +680,7 @@ void oracle_rasterize_backward(int tbx, int tby, int H, int W, int C, int num_po
      * Accumulates 1.1 * (|own term|' + rel * |term|'), rel = the sum over the flippable
      * Gaussians already passed of 1/(1 - alpha) - 1. */
     /* gsplat's v_conic.y carries 1/2 (CONIC_HALF); else d sigma / d conic.y = dx dy */
-    const float hb = (g_quirks & Q_CONIC_HALF) ? 0.5f : 1.0f;
+    const real hb = (g_quirks & Q_CONIC_HALF) ? 0.5f : 1.0f;
     double *acc = (double *)calloc((size_t)num_points * (9 + (size_t)C), sizeof(double));
     double *aacc = abs_sum ? (double *)calloc((size_t)num_points * (9 + (size_t)C),
                                               sizeof(double))
@@ -673,7 +694,7 @@ void oracle_rasterize_backward(int tbx, int tby, int H, int W, int C, int num_po
     /* per Gaussian: [xy0 xy1 con0 con1 con2 opac | C colors] */
     const int S = 6 + C;
     int ntiles = tile_list ? num_tile_list : tbx * tby;
-    float buf[64];
+    real buf[64];
     for (int tt = 0; tt < ntiles; ++tt) {
         int t = tile_list ? tile_list[tt] : tt;
         int tx = t % tbx, ty = t / tbx;
@@ -683,31 +704,31 @@ void oracle_rasterize_backward(int tbx, int tby, int H, int W, int C, int num_po
                 int i = ty * BLOCK + li, j = tx * BLOCK + lj;
                 if (i >= H || j >= W) continue;
                 int pix = i * W + j;
-                float px = (float)j, py = (float)i;
-                float T_final = final_Ts[pix];
-                float T = T_final;
+                real px = (real)j, py = (real)i;
+                real T_final = final_Ts[pix];
+                real T = T_final;
                 int bin_final = final_idx[pix];
-                const float *vo = v_out + (size_t)C * pix;
-                float va_out = v_out_alpha[pix];
+                const real *vo = v_out + (size_t)C * pix;
+                real va_out = v_out_alpha[pix];
                 for (int c = 0; c < C; ++c) buf[c] = 0.f;
                 int ndiv = 0; /* divisions T /= (1 - alpha) so far on this pixel */
                 double flip_rel = 0.0; /* relative T change from flippable decisions passed */
                 int kstart = bin_final < end - 1 ? bin_final : end - 1;
                 for (int k = kstart; k >= start; --k) {
                     int g = gids_sorted[k];
-                    const float *cn = conics + 3 * g;
-                    float dx = xys[2 * g] - px, dy = xys[2 * g + 1] - py;
-                    float sigma = 0.5f * (cn[0] * dx * dx + cn[2] * dy * dy) + cn[1] * dx * dy;
-                    float opac = opacity[g];
-                    float vis = expf(-sigma);
-                    float alpha = fminf(alpha_max, opac * vis);
+                    const real *cn = conics + 3 * g;
+                    real dx = xys[2 * g] - px, dy = xys[2 * g + 1] - py;
+                    real sigma = 0.5f * (cn[0] * dx * dx + cn[2] * dy * dy) + cn[1] * dx * dy;
+                    real opac = opacity[g];
+                    real vis = REXP(-sigma);
+                    real alpha = RMIN(alpha_max, opac * vis);
                     const int near = facc && ((fabs((double)alpha * 255.0 - 1.0) <= 1e-5) ||
                                               (fabs((double)sigma) <= 1e-6 &&
                                                alpha >= 1.f / 255.f));
                     const int skip = sigma < 0.f || alpha < 1.f / 255.f;
                     if (facc && (near || (!skip && flip_rel > 0.0))) {
                         /* |term|' of this Gaussian at this pixel (as if composited) */
-                        const float ra_ = 1.f / (1.f - alpha), T_ = T * ra_, fac_ = alpha * T_;
+                        const real ra_ = 1.f / (1.f - alpha), T_ = T * ra_, fac_ = alpha * T_;
                         double vabs = fabs((double)T_final * ra_ * va_out);
                         for (int c = 0; c < C; ++c)
                             vabs += fabs((double)colors[(size_t)C * g + c] * T_ * vo[c]) +
@@ -726,13 +747,13 @@ void oracle_rasterize_backward(int tbx, int tby, int H, int W, int C, int num_po
                     }
                     if (near) flip_rel += 1.0 / (1.0 - (double)alpha) - 1.0;
                     if (skip) continue;
-                    float ra = 1.f / (1.f - alpha);
+                    real ra = 1.f / (1.f - alpha);
                     T *= ra;
                     ++ndiv;
-                    float fac = alpha * T;
-                    float v_alpha = 0.f;
+                    real fac = alpha * T;
+                    real v_alpha = 0.f;
                     double va_abs = 0.0; /* sum of |components| of v_alpha */
-                    const float *rgb = colors + (size_t)C * g;
+                    const real *rgb = colors + (size_t)C * g;
                     double *a = acc + (size_t)g * S;
                     double *aa = aacc ? aacc + (size_t)g * S : NULL;
                     double *da = dacc ? dacc + (size_t)g * S : NULL;
@@ -748,7 +769,7 @@ void oracle_rasterize_backward(int tbx, int tby, int H, int W, int C, int num_po
                     v_alpha += T_final * ra * va_out;
                     for (int c = 0; c < C; ++c) v_alpha += -T_final * ra * bg[c] * vo[c];
                     for (int c = 0; c < C; ++c) buf[c] += rgb[c] * fac;
-                    float v_sigma = -opac * vis * v_alpha;
+                    real v_sigma = -opac * vis * v_alpha;
                     a[0] += (double)(v_sigma * (cn[0] * dx + cn[1] * dy));
                     a[1] += (double)(v_sigma * (cn[1] * dx + cn[2] * dy));
                     a[2] += (double)(0.5f * v_sigma * dx * dx);
@@ -777,21 +798,21 @@ void oracle_rasterize_backward(int tbx, int tby, int H, int W, int C, int num_po
     }
     for (int g = 0; g < num_points; ++g) {
         const double *a = acc + (size_t)g * S;
-        v_xy[2 * g + 0] = (float)a[0];
-        v_xy[2 * g + 1] = (float)a[1];
-        v_conic[3 * g + 0] = (float)a[2];
-        v_conic[3 * g + 1] = (float)a[3];
-        v_conic[3 * g + 2] = (float)a[4];
-        v_opacity[g] = (float)a[5];
-        for (int c = 0; c < C; ++c) v_colors[(size_t)C * g + c] = (float)a[6 + c];
+        v_xy[2 * g + 0] = (real)a[0];
+        v_xy[2 * g + 1] = (real)a[1];
+        v_conic[3 * g + 0] = (real)a[2];
+        v_conic[3 * g + 1] = (real)a[3];
+        v_conic[3 * g + 2] = (real)a[4];
+        v_opacity[g] = (real)a[5];
+        for (int c = 0; c < C; ++c) v_colors[(size_t)C * g + c] = (real)a[6 + c];
         if (aacc)
-            for (int k = 0; k < S; ++k) abs_sum[(size_t)g * S + k] = (float)aacc[(size_t)g * S + k];
+            for (int k = 0; k < S; ++k) abs_sum[(size_t)g * S + k] = (real)aacc[(size_t)g * S + k];
         if (dacc)
             for (int k = 0; k < S; ++k)
-                drift_sum[(size_t)g * S + k] = (float)dacc[(size_t)g * S + k];
+                drift_sum[(size_t)g * S + k] = (real)dacc[(size_t)g * S + k];
         if (facc)
             for (int k = 0; k < S; ++k)
-                flip_sum[(size_t)g * S + k] = (float)facc[(size_t)g * S + k];
+                flip_sum[(size_t)g * S + k] = (real)facc[(size_t)g * S + k];
     }
     free(acc);
     free(aacc);

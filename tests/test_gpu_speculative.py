@@ -91,11 +91,15 @@ def _fused(gpu, sc, cam, gt, bg):
 
 
 @pytest.mark.parametrize("W,H,n", [(512, 384, 200_000), (1080, 1080, 400_000)])
-@pytest.mark.parametrize("overflow", [False, True])
-def test_fused_render_speculative_bit_identical(gpu, W, H, n, overflow):
-    """First call of the frame shape: synchronous binning; the next: speculative (blend launched
-    before the host reads I); with `overflow`, a capacity below I forces the re-bin and the
-    second blend.  Bit-identical outputs and gradients (deterministic mode)."""
+@pytest.mark.parametrize("mode", ["plain", "overflow", "range"])
+def test_fused_render_speculative_bit_identical(gpu, W, H, n, mode):
+    """First call of the frame shape: synchronous binning (it learns the capacity and the depth
+    keys' varying bits); the next: speculative (blend launched before the host reads I, the
+    depth-sort passes over constant key bytes not launched).  `overflow`: a capacity below I
+    forces the re-bin and the second blend; `range`: a depth-key range claimed narrower than it
+    is makes the sort skip passes it needs -- the violation is detected on the device and the
+    render redoes the preprocess and a full binning.  Bit-identical outputs and gradients
+    (deterministic mode)."""
     sc = synthetic_scene(n, 3, seed=17, scale_lo=0.004, scale_hi=0.03)
     cam = synthetic_camera(W, H)
     bg = torch.tensor([0.2, 0.4, 0.6], device=gpu)
@@ -104,11 +108,18 @@ def test_fused_render_speculative_bit_identical(gpu, W, H, n, overflow):
     prev = _lib.set_deterministic(True)
     try:
         R._EMIT_CAP.pop(key, None)
+        R._KEY_VARY.pop(key, None)
         ref, I = _fused(gpu, sc, cam, gt, bg)
         assert key in R._EMIT_CAP and I > 0
-        if overflow:
+        vary = R._KEY_VARY[key]
+        assert vary and (vary >> 24) == 0  # depths 2.5-5.5: the top key byte is constant
+        if mode == "overflow":
             R._EMIT_CAP[key] = I // 3
+        if mode == "range":
+            R._KEY_VARY[key] = 0xFF  # "only the low byte varies": passes 1-3 not launched
         got, I2 = _fused(gpu, sc, cam, gt, bg)
+        if mode == "range":
+            assert R._KEY_VARY[key] == 0xFF | vary  # the violation taught the real range
     finally:
         _lib.set_deterministic(prev)
     assert I2 == I
