@@ -972,6 +972,103 @@ __global__ __launch_bounds__(TPB) void emit_kernel(int n, const uint32_t *__rest
   }
 }
 
+// The speculative binning's emission (gsplat_bin_speculative) with the allotment scan folded
+// in: one workgroup per scan tile of SC_TILE depth-ordered Gaussians (gather_counts' tiles) takes
+// its base offset and the total I straight from gather_counts' per-tile sums (at most a few
+// thousand words, summed in fixed order), scans its own allotments in four rounds of 256 and
+// emits each round wave by wave exactly as emit_kernel does -- the scan_partials and
+// scan_downsweep launches (and the off[] array) are gone.  Workgroup 0 publishes I to the
+// device word the tile sort reads and to the host's pinned slot.  I > cap: the table is
+// cleared and nothing is emitted (the caller re-bins).
+__global__ __launch_bounds__(TPB) void emit_scan_kernel(int n, int nb,
+                                                        const uint32_t *__restrict__ order,
+                                                        const uint32_t *__restrict__ cnt,
+                                                        const uint32_t *__restrict__ partial,
+                                                        const uint2 *__restrict__ box, int tbx,
+                                                        int tby, uint32_t *__restrict__ tkeys,
+                                                        uint32_t *__restrict__ tvals,
+                                                        int *__restrict__ tile_bins,
+                                                        uint32_t *__restrict__ i_dev,
+                                                        int32_t *__restrict__ i_host, uint32_t cap) {
+  __shared__ uint32_t lds[TPB / 64];
+  for (long long i = (long long)blockIdx.x * TPB + threadIdx.x; i < 2LL * tbx * tby;
+       i += (long long)gridDim.x * TPB)
+    tile_bins[i] = 0;
+  const int tid = threadIdx.x, lane = tid & 63;
+  // this tile's allotments, loaded with the partial sums (clamped: no branch between them)
+  const long long b0 = (long long)blockIdx.x * SC_TILE;
+  uint32_t c[SC_ITEMS];
+#pragma unroll
+  for (int r = 0; r < SC_ITEMS; ++r) {
+    const long long p = b0 + r * TPB + tid;
+    c[r] = p < n ? cnt[p] : 0u;
+  }
+  uint32_t pre = 0, tot = 0;
+  for (int k = tid; k < nb; k += TPB) {
+    const uint32_t v = partial[k];
+    tot += v;
+    pre += k < (int)blockIdx.x ? v : 0u;
+  }
+  uint32_t bpre, btot;
+  block_exclusive_scan<TPB>(pre, bpre, lds);  // (only the totals are used)
+  block_exclusive_scan<TPB>(tot, btot, lds);
+  if (blockIdx.x == 0 && tid == 0) {
+    *i_dev = btot;
+    if (i_host) *i_host = (int32_t)btot;
+  }
+  if (btot > cap) return;  // workgroup-uniform
+  uint32_t run = bpre;
+#pragma unroll
+  for (int r = 0; r < SC_ITEMS; ++r) {
+    const long long p = b0 + r * TPB + tid;
+    uint32_t rtot;
+    const uint32_t start = run + block_exclusive_scan<TPB>(c[r], rtot, lds);
+    run += rtot;
+    const long long p0 = p - lane;
+    if (p0 >= n) continue;  // wave-uniform (no barrier below)
+    const bool in = p < n;
+    uint32_t g = 0;
+    uint2 bx = make_uint2(0u, 0u);
+    if (in && c[r]) {
+      g = order[p];
+      bx = box[p];
+    }
+    const uint32_t base = __shfl(start, 0, 64);
+    const int last_lane = (int)min(63LL, (long long)n - 1 - p0);
+    const uint32_t total = __shfl(start + c[r], last_lane, 64) - base;
+    const uint32_t rel = in ? start - base : total;
+    for (uint32_t j0 = 0; j0 < total; j0 += 64) {
+      const uint32_t j = j0 + lane;
+      int q = 0;
+#pragma unroll
+      for (int step = 32; step >= 1; step >>= 1) {
+        const uint32_t rq = __shfl(rel, (q + step) & 63, 64);
+        if (q + step <= 63 && rq <= j) q += step;
+      }
+      const uint32_t li = j - __shfl(rel, q, 64);
+      const uint32_t q0 = __shfl(bx.x, q, 64), q1 = __shfl(bx.y, q, 64);
+      const uint32_t qg = __shfl(g, q, 64);
+      const int qx0 = (int)(q0 & 0xFFFFu), qy0 = (int)(q0 >> 16);
+      const int qx1 = (int)(q1 & 0xFFFFu), qy1 = (int)(q1 >> 16);
+      const int qbw = max(qx1 - qx0, 1);
+      const int qarea = max(qx1 - qx0, 0) * max(qy1 - qy0, 0);
+      uint32_t tile;
+      if ((int)li < qarea) {
+        const int ly = li < (1u << 20)
+                           ? (int)(((float)li + 0.5f) * __builtin_amdgcn_rcpf((float)qbw))
+                           : (int)li / qbw;
+        tile = (uint32_t)((qy0 + ly) * tbx + qx0 + ((int)li - ly * qbw));
+      } else {
+        tile = (uint32_t)(tbx * tby);
+      }
+      if (j < total) {
+        tkeys[base + j] = tile;
+        tvals[base + j] = qg;
+      }
+    }
+  }
+}
+
 // tile_bins[t] = [first, last+1) of tile t in the tile-sorted keys (tile_bins pre-zeroed).
 template <typename K, int SHIFT>
 __global__ __launch_bounds__(TPB) void bin_edges_kernel(long long n, const K *__restrict__ keys,
@@ -2066,7 +2163,8 @@ static int bin_count_impl(int num_points, const float *xys, const float *depths,
                           const int32_t *radii, const int32_t *num_tiles_hit, int tile_bounds_x,
                           int tile_bounds_y, int32_t *d_counts, void *workspace1,
                           size_t workspace1_bytes, bool keyed, void *stream,
-                          uint32_t assume_const = 0, bool range_out = false) {
+                          uint32_t assume_const = 0, bool range_out = false,
+                          bool no_scan = false) {
   hipStream_t st = (hipStream_t)stream;
   const long long T = (long long)tile_bounds_x * tile_bounds_y;
   if (num_points < 0 || tile_bounds_x <= 0 || tile_bounds_y <= 0 || tile_bounds_x > 65535 ||
@@ -2135,6 +2233,7 @@ static int bin_count_impl(int num_points, const float *xys, const float *depths,
   uint32_t *partial = rts_tile_counts(p.rs_ws);  // the sort is done with its tile counts
   hipLaunchKernelGGL(gather_counts_kernel, dim3(nb), dim3(TPB), 0, st, n, p.order, kept, p.rec,
                      p.cnt, p.box, d_counts, partial);
+  if (no_scan) return check_launch("bin_count");  // (emit_scan_kernel scans, EMIT_SPEC)
   hipLaunchKernelGGL(scan_partials_kernel, dim3(1), dim3(1024), 0, st, partial, nb,
                      (uint32_t *)(d_counts + 1), p.dcount);
   hipLaunchKernelGGL(scan_downsweep_kernel, dim3(nb), dim3(TPB), 0, st, p.cnt, (long long)n,
@@ -2168,6 +2267,46 @@ extern "C" int gsplat_bin_count_keyed_ex(int num_points, int tile_bounds_x, int 
   return bin_count_impl(num_points, nullptr, nullptr, nullptr, nullptr, tile_bounds_x,
                         tile_bounds_y, d_counts, workspace1, workspace1_bytes, true, stream,
                         assume_const, true);
+}
+
+// The whole binning before the host knows I: the count phase (depth sort with the key-range
+// assumption, gather_counts), emit_scan_kernel (the allotment scan folded into the emission, I
+// published from the device) and the capacity-launched tile sort.  2 = the scheme needs I on
+// the host (nothing launched).
+extern "C" int gsplat_bin_speculative(int num_points, int64_t capacity, int tile_bounds_x,
+                                      int tile_bounds_y, int32_t *d_counts, void *workspace1,
+                                      size_t workspace1_bytes, uint32_t assume_const,
+                                      int32_t *gaussian_ids_sorted, int32_t *tile_bins,
+                                      void *workspace2, size_t workspace2_bytes, void *stream) {
+  hipStream_t st = (hipStream_t)stream;
+  const long long T = (long long)tile_bounds_x * tile_bounds_y;
+  if (num_points <= 0 || capacity <= 0 || capacity > 0x3FFFFFFFLL || tile_bounds_x <= 0 ||
+      tile_bounds_y <= 0 || tile_bounds_x > 65535 || tile_bounds_y > 65535 || T >= (1LL << 31)) {
+    set_error("bin_speculative: bad sizes (N=%d capacity=%lld tiles=%dx%d)", num_points,
+              (long long)capacity, tile_bounds_x, tile_bounds_y);
+    return 1;
+  }
+  if (use_bucket(num_points, T) || use_emit_pass0(capacity)) return 2;
+  Phase1 p1 = carve_phase1(workspace1, num_points);
+  Phase2 p2 = carve_phase2(workspace2, capacity);
+  if (workspace1_bytes < p1.bytes || workspace2_bytes < p2.bytes) {
+    set_error("bin_speculative: workspaces %zu/%zu < %zu/%zu bytes", workspace1_bytes,
+              workspace2_bytes, p1.bytes, p2.bytes);
+    return 1;
+  }
+  if (bin_count_impl(num_points, nullptr, nullptr, nullptr, nullptr, tile_bounds_x,
+                     tile_bounds_y, d_counts, workspace1, workspace1_bytes, true, stream,
+                     assume_const, true, true))
+    return 1;
+  const int n = num_points;
+  const int nb = (int)cdiv(n, SC_TILE);
+  hipLaunchKernelGGL(emit_scan_kernel, dim3(nb), dim3(TPB), 0, st, n, nb, p1.order, p1.cnt,
+                     rts_tile_counts(p1.rs_ws), p1.box, tile_bounds_x, tile_bounds_y, p2.tk_a,
+                     p2.tv_a, tile_bins, p1.dcount, d_counts + 1, (uint32_t)capacity);
+  radix_sort_pairs<uint32_t>(p2.tk_a, p2.tv_a, p2.tk_b, p2.tv_b, nullptr,
+                             (uint32_t *)gaussian_ids_sorted, capacity, 0, bits_for(T), p2.rs_ws,
+                             st, false, tile_bins, T, false, 0, p1.dcount);
+  return check_launch("bin_speculative");
 }
 
 // The emission in two halves around the host's read of I: HEAD = the launches that need only

@@ -18,9 +18,7 @@ void set_error(const char *fmt, ...);
 // reports it (or any pending launch error) and resets the record.
 void note(hipError_t e, const char *what);
 int check_launch(const char *what);
-// loss.hip: loss = inv_n * (double) sum of partials[k], k < nparts (the fused-L1 blend's)
-void launch_l1_finalize(hipStream_t st, int nparts, const float *partials, double inv_n,
-                        float *loss);
+
 
 // gsplat 0.1.2.1 behaviours recalled but unverified (SURVEY.md Appendix A [VERIFY]); each is a
 // bit of the process-wide quirk mask (gsplat_set_quirks, default GSPLAT_QUIRKS_ALL):

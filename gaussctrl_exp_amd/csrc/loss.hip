@@ -367,45 +367,8 @@ __global__ __launch_bounds__(256) void l1_ssim_bwd_kernel(
   }
 }
 
-// loss = inv_n * sum of n partials (one float each), in double and a fixed order.  One
-// workgroup of 1,024 threads whose loads are all in flight together (16 per round, unrolled):
-// the fused-L1 blend writes one partial per wave (~18.5k at 1080^2), and a loop that waits for
-// each load in turn took ~30 us.
-constexpr int FIN_NT = 1024, FIN_U = 16;
-__global__ __launch_bounds__(FIN_NT) void partials_finalize_kernel(int n,
-                                                                   const float *__restrict__ p,
-                                                                   double inv_n,
-                                                                   float *__restrict__ loss) {
-  __shared__ double red[FIN_NT];
-  double a = 0.0;
-  for (int base = 0; base < n; base += FIN_NT * FIN_U) {
-    float v[FIN_U];
-#pragma unroll
-    for (int u = 0; u < FIN_U; ++u) {
-      const int k = base + u * FIN_NT + threadIdx.x;
-      v[u] = k < n ? p[k] : 0.f;
-    }
-#pragma unroll
-    for (int u = 0; u < FIN_U; ++u) a += (double)v[u];
-  }
-  red[threadIdx.x] = a;
-  __syncthreads();
-  for (int s = FIN_NT / 2; s > 0; s >>= 1) {
-    if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) loss[0] = (float)(red[0] * inv_n);
-}
-
 }  // namespace
 
-// The loss of one-float-per-wave L1 partials written by another kernel -- the fused-L1 blend
-// (raster.hip): loss = inv_n * sum, summed in double.
-void launch_l1_finalize(hipStream_t st, int nparts, const float *partials, double inv_n,
-                        float *loss) {
-  hipLaunchKernelGGL(partials_finalize_kernel, dim3(1), dim3(FIN_NT), 0, st, nparts, partials,
-                     inv_n, loss);
-}
 
 }  // namespace gs
 

@@ -1390,12 +1390,10 @@ __device__ __forceinline__ int split_cost_bucket(int L, int k, int chunk, bool s
   return 63 - min(63, 4 * oct + q);  // bucket 0: the costliest
 }
 
-__global__ __launch_bounds__(1024) void split_plan_kernel(int T, int chunk,
-                                                          const int2 *__restrict__ bins,
-                                                          const int *__restrict__ work,
-                                                          int2 *__restrict__ items,
-                                                          int *__restrict__ n_items) {
-  __shared__ int hist[64], cur[64];
+__device__ __forceinline__ void split_plan_body(int T, int chunk, const int2 *__restrict__ bins,
+                                                const int *__restrict__ work,
+                                                int2 *__restrict__ items,
+                                                int *__restrict__ n_items, int *hist, int *cur) {
   const int tid = threadIdx.x;
   if (tid < 64) hist[tid] = 0;
   __syncthreads();
@@ -1427,6 +1425,55 @@ __global__ __launch_bounds__(1024) void split_plan_kernel(int T, int chunk,
     for (int k = 0; k < m; ++k)
       items[atomicAdd(&cur[split_cost_bucket(L, k, chunk, split)], 1)] = make_int2(t, k);
   }
+}
+__global__ __launch_bounds__(1024) void split_plan_kernel(int T, int chunk,
+                                                          const int2 *__restrict__ bins,
+                                                          const int *__restrict__ work,
+                                                          int2 *__restrict__ items,
+                                                          int *__restrict__ n_items) {
+  __shared__ int hist[64], cur[64];
+  split_plan_body(T, chunk, bins, work, items, n_items, hist, cur);
+}
+
+// One launch behind a plan-filling or loss-computing blend (forward_clearing_impl): workgroup
+// 0 sums the fused L1 loss's per-wave partials (loss = inv_n * the double sum, every load of a
+// round in flight before the adds), workgroup 1 orders the list-split plan from the walk table
+// the blend just filled -- two one-workgroup jobs that were a launch each (the plan at the
+// start of the backward: ~7 us of the headline step apiece).  Either may be absent (part or
+// items null); the grid is then one workgroup.
+__global__ __launch_bounds__(1024) void post_forward_kernel(int n_part, const float *__restrict__ part,
+                                                            double inv_n, float *__restrict__ loss,
+                                                            int T, int chunk,
+                                                            const int2 *__restrict__ bins,
+                                                            const int *__restrict__ work,
+                                                            int2 *__restrict__ items,
+                                                            int *__restrict__ n_items) {
+  __shared__ double red[1024];
+  __shared__ int hist[64], cur[64];
+  const bool loss_job = part && (blockIdx.x == 0 || !items);
+  if (!loss_job) {
+    split_plan_body(T, chunk, bins, work, items, n_items, hist, cur);
+    return;
+  }
+  constexpr int U = 16;
+  double a = 0.0;
+  for (int base = 0; base < n_part; base += 1024 * U) {
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = base + u * 1024 + threadIdx.x;
+      v[u] = k < n_part ? part[k] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) a += (double)v[u];
+  }
+  red[threadIdx.x] = a;
+  __syncthreads();
+  for (int st = 512; st > 0; st >>= 1) {
+    if ((int)threadIdx.x < st) red[threadIdx.x] += red[threadIdx.x + st];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) loss[0] = (float)(red[0] * inv_n);
 }
 
 // Gradient records (moments, common.h record_grads) -> gsplat's v_xy [N,2], v_conic [N,3],
@@ -1724,18 +1771,22 @@ static bool default_variants() {
 // then -- a switch flipped between the two calls (debug flag bit 30) cannot make the backward
 // read words no forward wrote.  Keyed by the plan's address, which the next
 // forward on that buffer overwrites.
+// The same note records whether the forward also ordered the plan (post_forward_kernel), so
+// the backward skips its split_plan_kernel.
 static std::mutex g_plan_kb_mu;
-static std::unordered_map<const void *, bool> g_plan_kb;
-static void plan_kbits_note(const void *plan, bool written) {
+static std::unordered_map<const void *, int> g_plan_kb;  // bit 0 keep bits, bit 1 plan ordered
+static void plan_kbits_note(const void *plan, bool written, bool planned = false) {
   std::lock_guard<std::mutex> lk(g_plan_kb_mu);
   if (g_plan_kb.size() > 4096) g_plan_kb.clear();  // (stale entries of freed plans)
-  g_plan_kb[plan] = written;
+  g_plan_kb[plan] = (written ? 1 : 0) | (planned ? 2 : 0);
 }
-static bool plan_kbits_written(const void *plan) {
+static int plan_note(const void *plan) {
   std::lock_guard<std::mutex> lk(g_plan_kb_mu);
   const auto it = g_plan_kb.find(plan);
-  return it != g_plan_kb.end() && it->second;
+  return it != g_plan_kb.end() ? it->second : 0;
 }
+static bool plan_kbits_written(const void *plan) { return plan_note(plan) & 1; }
+static bool plan_ordered(const void *plan) { return plan_note(plan) & 2; }
 
 extern "C" int gsplat_rasterize_chunk_size(int tile_bounds_x, int tile_bounds_y,
                                            int64_t num_intersects) {
@@ -1919,7 +1970,8 @@ static void launch_bwd(hipStream_t st, int tbx, int tby, int H, int W, int n,
                        const float *background, const float *final_Ts, const int32_t *final_idx,
                        const float *v_output, const float *v_output_alpha, float alpha_max,
                        float *rec, int chunk, const SplitWs *w, unsigned long long *det,
-                       bool work_ready = false, bool kbits_ready = false, L1Grad l1 = {}) {
+                       bool work_ready = false, bool kbits_ready = false, L1Grad l1 = {},
+                       bool plan_ready = false) {
   const long long slots = w ? w->items_bound : (long long)tbx * tby;
   const int2 *its = w ? w->items : nullptr;
   const int *ni = w ? w->n_items : nullptr;
@@ -1928,8 +1980,9 @@ static void launch_bwd(hipStream_t st, int tbx, int tby, int H, int W, int n,
     if (!work_ready)  // (the forward did not fill the walk table)
       hipLaunchKernelGGL(split_work_kernel, dim3(T), dim3(256), 0, st, tbx, tby, H, W, final_idx,
                          w->work);
-    hipLaunchKernelGGL(split_plan_kernel, dim3(1), dim3(1024), 0, st, T, chunk,
-                       (const int2 *)bins, (const int *)w->work, w->items, w->n_items);
+    if (!(work_ready && plan_ready))  // (the forward's post_forward_kernel ordered it)
+      hipLaunchKernelGGL(split_plan_kernel, dim3(1), dim3(1024), 0, st, T, chunk,
+                         (const int2 *)bins, (const int *)w->work, w->items, w->n_items);
   }
   const bool cnt = g_pair_count_on && !det;
   // the forward's keep bits: only when the forward that filled this plan also wrote them
@@ -1990,7 +2043,8 @@ static int backward_into_records(const char *who, hipStream_t st, int tbx, int t
                                  const float *v_output, const float *v_output_alpha,
                                  float alpha_max, float *rec, int64_t num_intersects, int chunk,
                                  void *plan, size_t plan_bytes, bool work_ready = false,
-                                 bool kbits_ready = false, L1Grad l1 = {}) {
+                                 bool kbits_ready = false, L1Grad l1 = {},
+                                 bool plan_ready = false) {
   SplitWs w{};
   if (chunk > 0) {
     w = carve_split_ws(plan, (long long)tbx * tby, num_intersects, chunk);
@@ -2004,12 +2058,12 @@ static int backward_into_records(const char *who, hipStream_t st, int tbx, int t
     if (!lease.buf) return check_launch(who);
     launch_bwd(st, tbx, tby, H, W, n, gids, bins, xys, conics, colors, opacity, background,
                final_Ts, final_idx, v_output, v_output_alpha, alpha_max, rec, chunk,
-               chunk > 0 ? &w : nullptr, lease.buf, work_ready, kbits_ready, l1);
+               chunk > 0 ? &w : nullptr, lease.buf, work_ready, kbits_ready, l1, plan_ready);
     lease.finish();
   } else {
     launch_bwd(st, tbx, tby, H, W, n, gids, bins, xys, conics, colors, opacity, background,
                final_Ts, final_idx, v_output, v_output_alpha, alpha_max, rec, chunk,
-               chunk > 0 ? &w : nullptr, nullptr, work_ready, kbits_ready, l1);
+               chunk > 0 ? &w : nullptr, nullptr, work_ready, kbits_ready, l1, plan_ready);
   }
   return 0;
 }
@@ -2085,7 +2139,7 @@ static int forward_clearing_impl(
     const float *conics, const float *colors, const float *opacity, const float *background,
     float *out_img, float *final_Ts, int32_t *final_idx, void *clear, size_t clear_bytes,
     const int32_t *clear_radii, int64_t num_intersects, int chunk, void *plan, size_t plan_bytes,
-    const float *l1_gt, float *l1_part, int l1_clamp, void *stream) {
+    const float *l1_gt, float *l1_part, int l1_clamp, float *l1_loss, void *stream) {
   if (bad_frame(tile_bounds_x, tile_bounds_y, img_height, img_width) || clear_bytes % 16 ||
       (clear_bytes && !clear) || (clear_radii && clear_bytes % 64) ||
       (chunk > 0 && (chunk % 64 || num_intersects < 0))) {
@@ -2108,13 +2162,28 @@ static int forward_clearing_impl(
       kbits = w.kbits;
       kbw = w.kbw;
     }
-    plan_kbits_note(plan, kbits != nullptr);
+    plan_kbits_note(plan, kbits != nullptr, true);
   }
   launch_fwd<false>((hipStream_t)stream, tile_bounds_x, tile_bounds_y, img_height, img_width,
                     gaussian_ids_sorted, tile_bins, xys, conics, colors, opacity, background,
                     out_img, final_Ts, final_idx, nullptr, nullptr, (float4 *)clear,
                     (long long)(clear_bytes / 16), clear_radii, tile_last, kbits, kbw, l1_gt,
                     l1_part, l1_clamp);
+  // the loss of the partials and the list-split plan, one launch (post_forward_kernel)
+  const bool plan_job = chunk > 0, loss_job = l1_part != nullptr;
+  if (plan_job || loss_job) {
+    const long long T = (long long)tile_bounds_x * tile_bounds_y;
+    SplitWs w{};
+    if (plan_job) w = carve_split_ws(plan, T, num_intersects, chunk);
+    const int n_part = loss_job ? (int)(gsplat_rasterize_l1_partials_bytes(tile_bounds_x,
+                                                                          tile_bounds_y) / 4)
+                                : 0;
+    hipLaunchKernelGGL(post_forward_kernel, dim3((plan_job ? 1 : 0) + (loss_job ? 1 : 0)),
+                       dim3(1024), 0, (hipStream_t)stream, n_part, l1_part,
+                       1.0 / (3.0 * img_height * img_width), l1_loss, (int)T, chunk,
+                       (const int2 *)tile_bins, (const int *)w.work, plan_job ? w.items : nullptr,
+                       w.n_items);
+  }
   return check_launch(who);
 }
 
@@ -2131,7 +2200,7 @@ extern "C" int gsplat_rasterize_forward_clearing(
                                img_height, img_width, gaussian_ids_sorted, tile_bins, xys, conics,
                                colors, opacity, background, out_img, final_Ts, final_idx, clear,
                                clear_bytes, clear_radii, num_intersects, chunk, plan, plan_bytes,
-                               nullptr, nullptr, 0, stream);
+                               nullptr, nullptr, 0, nullptr, stream);
 }
 
 // The per-wave L1 partials of gsplat_rasterize_forward_clearing_l1 (one float per wave).
@@ -2160,10 +2229,8 @@ extern "C" int gsplat_rasterize_forward_clearing_l1(
                             gaussian_ids_sorted, tile_bins, xys, conics, colors, opacity,
                             background, out_img, final_Ts, final_idx, clear, clear_bytes,
                             clear_radii, num_intersects, chunk, plan, plan_bytes, gt, partials,
-                            clamp_pred ? 1 : 0, stream))
+                            clamp_pred ? 1 : 0, loss, stream))
     return 1;
-  launch_l1_finalize((hipStream_t)stream, (int)(need / sizeof(float)), partials,
-                     1.0 / (3.0 * img_height * img_width), loss);
   return check_launch(who);
 }
 
@@ -2249,7 +2316,8 @@ static int backward_records_impl(
                             num_points, gaussian_ids_sorted, tile_bins, xys, conics, colors,
                             opacity, background, final_Ts, final_idx, v_output, v_output_alpha,
                             alpha_max, (float *)records, num_intersects, chunk, plan, plan_bytes,
-                            plan_filled != 0, plan_filled != 0 && plan_kbits_written(plan), l1))
+                            plan_filled != 0, plan_filled != 0 && plan_kbits_written(plan), l1,
+                            plan_filled != 0 && plan_ordered(plan)))
     return 1;
   return check_launch(who);
 }

@@ -281,11 +281,13 @@ def bin_gaussians_speculative(xys: Tensor, depths: Tensor, radii: Tensor, num_ti
     ids_buf, ws2 = _emit_buffers(dev, n, cap, tbx, tby)
     slot, counts, host = _COUNTS.acquire(dev)
     try:
-        _lib.call("gsplat_bin_count_keyed_ex", n, tbx, tby, P(counts), P(ws1), ws1.numel(),
-                  _assumed_constant(key), st)
-        rc = _lib.lib().gsplat_bin_emit_speculative(n, cap, tbx, tby, P(ids_buf), P(tile_bins),
-                                                    P(ws1), ws1.numel(), P(ws2), ws2.numel(), st)
-        if rc == 2:  # the scheme needs I on the host: finish as bin_gaussians does
+        # count phase, emission (with the allotment scan) and tile sort in one call
+        rc = _lib.lib().gsplat_bin_speculative(n, cap, tbx, tby, P(counts), P(ws1), ws1.numel(),
+                                               _assumed_constant(key), P(ids_buf), P(tile_bins),
+                                               P(ws2), ws2.numel(), st)
+        if rc == 2:  # the scheme needs I on the host: count, then finish as bin_gaussians does
+            _lib.call("gsplat_bin_count_keyed_ex", n, tbx, tby, P(counts), P(ws1), ws1.numel(),
+                      _assumed_constant(key), st)
             pre = (ids_buf, ws2)
             if PRELAUNCH_EMISSION:
                 _lib.call("gsplat_bin_emit_prelaunch", n, cap, tbx, tby, P(tile_bins), P(ws1),
@@ -317,7 +319,7 @@ def bin_gaussians_speculative(xys: Tensor, depths: Tensor, radii: Tensor, num_ti
             done.finish = lambda: True
             return done
         if rc != 0:
-            raise RuntimeError("gsplat_bin_emit_speculative failed: " +
+            raise RuntimeError("gsplat_bin_speculative failed: " +
                                _lib.lib().gsplat_last_error().decode(errors="replace"))
     except BaseException:
         if slot is not None:

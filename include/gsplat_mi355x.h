@@ -238,6 +238,14 @@ int gsplat_bin_emit_finish(int num_points, int64_t num_intersects, int64_t capac
  * binning scheme for (num_points, tiles, capacity) needs I on the host -- the small-scene tile
  * buckets or the generated first tile pass (capacity >= 2^24): use prelaunch + finish there.
  * Replaces, like gsplat_bin_emit, gsplat 0.1.2.1 rasterize.py's map / sort / bin edges. */
+/* gsplat_bin_count_keyed_ex + gsplat_bin_emit_speculative in one call, two launches fewer: the
+ * allotment scan is folded into the emission (the emission publishes I to d_counts[1] from the
+ * device).  Same outputs, overflow and range-violation semantics and return code 2 as the two
+ * calls; d_counts int32[4] as gsplat_bin_count_keyed_ex's. */
+int gsplat_bin_speculative(int num_points, int64_t capacity, int tile_bounds_x, int tile_bounds_y,
+                           int32_t *d_counts, void *workspace1, size_t workspace1_bytes,
+                           uint32_t assume_const, int32_t *gaussian_ids_sorted, int32_t *tile_bins,
+                           void *workspace2, size_t workspace2_bytes, void *stream);
 int gsplat_bin_emit_speculative(int num_points, int64_t capacity, int tile_bounds_x,
                                 int tile_bounds_y, int32_t *gaussian_ids_sorted,
                                 int32_t *tile_bins, const void *workspace1,
