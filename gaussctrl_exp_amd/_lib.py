@@ -94,6 +94,7 @@ SIGNATURES = {
                                          [_P] * 13),
     "gsplat_fused_preprocess_backward_adam": (_I, [_I, _I, _I] + [_P] * 9 + [_F] * 4 +
                                               [_I, _I] + [_P] * 8 + [_I, _F, _F, _F, _P]),
+    "gsplat_exchange_pack_colors": (_I, [_I, _P, _SZ, _P, _P, _P, _P, _P]),
     "gsplat_grad_records_bytes": (_SZ, [_I]),
     "gsplat_grad_records_split": (_I, [_I, _P, _SZ, _P, _P, _P, _P, _P, _P, _P]),
     "gsplat_rasterize_backward_records": (_I, [_I] * 5 + [_P] * 11 + [_F, _I64, _I, _P, _SZ,

@@ -581,6 +581,48 @@ extern "C" int gsplat_fused_preprocess_backward(
   return check_launch("fused_preprocess_backward");
 }
 
+// The data-parallel view exchange's record (exchange.ShViewExchange), straight from the raster
+// backward's gradient records: send[0, 3N) = the SH-output colour gradient exactly as
+// fused_bwd_kernel<K > 1> writes v_colors (record colour sums through the clamp mask kept in
+// the colours' sign bit; zero for culled Gaussians), send[3N, 3N + 3) = the camera centre,
+// send[3N + 3] = 0.  It exists as soon as the raster backward is done, so its all-gather
+// overlaps fused_bwd_kernel and the geometry all-reduce instead of following them.
+__global__ __launch_bounds__(256) void exchange_pack_kernel(int n, const float *__restrict__ rec,
+                                                            const int *__restrict__ radii,
+                                                            const float *__restrict__ colors,
+                                                            const float *__restrict__ campos,
+                                                            float *__restrict__ send) {
+  const long long g = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (g < 3 && blockIdx.x == 0) send[3LL * n + g] = campos[g];
+  if (g == 3) send[3LL * n + 3] = 0.f;
+  if (g >= n) return;
+  float v[3] = {0.f, 0.f, 0.f};
+  if (radii[g] > 0) {
+    const float4 r1 = reinterpret_cast<const float4 *>(rec + g * RECF)[1];
+    const float rgb[3] = {r1.y, r1.z, r1.w};  // REC_R, REC_G, REC_B (record_grads' vrgb)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) v[c] = clamp0_passes(colors[3 * g + c]) ? rgb[c] : 0.f;
+  }
+#pragma unroll
+  for (int c = 0; c < 3; ++c) send[3 * g + c] = v[c];
+}
+
+extern "C" int gsplat_exchange_pack_colors(int num_points, const void *grad_records,
+                                           size_t records_bytes, const int32_t *radii,
+                                           const float *colors, const float *campos, float *send,
+                                           void *stream) {
+  if (num_points < 0 || (size_t)num_points * RECF * sizeof(float) > records_bytes ||
+      !campos || !send || (num_points > 0 && (!grad_records || !radii || !colors))) {
+    set_error("exchange_pack_colors: bad args (N=%d records %zu bytes)", num_points,
+              records_bytes);
+    return 1;
+  }
+  hipLaunchKernelGGL(exchange_pack_kernel, dim3(cdiv(num_points + 4, 256)), dim3(256), 0,
+                     (hipStream_t)stream, num_points, (const float *)grad_records, radii, colors,
+                     campos, send);
+  return check_launch("exchange_pack_colors");
+}
+
 extern "C" int gsplat_fused_preprocess_backward_adam(
     int num_points, int sh_bases, int degrees_to_use, float *means3d, float *log_scales,
     float *quats, float *opacity_logits, float *features_dc, float *features_rest,

@@ -80,9 +80,19 @@ class ShViewExchange:
         dist.all_gather_into_tensor(out, rec, group=self.group)
         return out.view(world, 3 * n + 4)
 
-    def reduce(self, v_colors: torch.Tensor,
+    def start_gather(self, send: torch.Tensor):
+        """Issue (async) the all-gather of this rank's packed record send [3N + 4] (v_colors |
+        campos | 0: gsplat_exchange_pack_colors, right after the raster backward) and return
+        the pending (work, out) for reduce(gathered=...): the gather then overlaps the rest of
+        the backward instead of following it."""
+        world = dist.get_world_size(self.group)
+        out = torch.empty((world * send.numel(),), device=send.device, dtype=torch.float32)
+        work = dist.all_gather_into_tensor(out, send, group=self.group, async_op=True)
+        return work, out
+
+    def reduce(self, v_colors: Optional[torch.Tensor],
                views_backward: Callable[[torch.Tensor, torch.Tensor], torch.Tensor],
-               early_flat: Optional[torch.Tensor] = None, early_map=None):
+               early_flat: Optional[torch.Tensor] = None, early_map=None, gathered=None):
         """Summed coefficient gradient of all ranks' views.  `views_backward(means, views)`
         evaluates sum_r Y(means - campos_r) (x) v_colors_r from the gathered records.
 
@@ -91,10 +101,15 @@ class ShViewExchange:
         kernel runs while RCCL moves those 44 B per Gaussian; train.GradExchange then skips
         the four parameters (early_map: which gradient storage each parameter must hold) and
         waits for it."""
-        views = self.gather(v_colors)
+        if gathered is None:
+            views = self.gather(v_colors)
         self.handled = True
         if early_flat is not None:
             self.early = (dist.all_reduce(early_flat, op=dist.ReduceOp.SUM, group=self.group,
                                           async_op=True), dict(early_map))
             self.early_steps += 1
+        if gathered is not None:  # (start_gather: in flight since the raster backward)
+            work, out = gathered
+            work.wait()
+            views = out.view(dist.get_world_size(self.group), -1)
         return views_backward(self.means, views)

@@ -244,6 +244,14 @@ class _FusedRender(Function):
             return (None,) * 21
         f32 = dict(device=dev, dtype=torch.float32)
         xchg = ctx.exchange
+        gathered = None
+        if xchg is not None and rec is not None:
+            # the view record straight from the raster records, its all-gather issued now: it
+            # overlaps the geometry backward below and the geometry all-reduce
+            send = torch.empty((3 * n + 4,), **f32)
+            _lib.call("gsplat_exchange_pack_colors", n, P(rec), rec.numel(), P(radii),
+                      P(colors), P(xchg.campos.to(dev).contiguous()), P(send), st)
+            gathered = xchg.start_gather(send)
         if xchg is not None and ctx.early:
             flat = torch.empty((11 * n,), **f32)
             v_means, v_scales = flat[:3 * n].view(n, 3), flat[3 * n:6 * n].view(n, 3)
@@ -267,7 +275,7 @@ class _FusedRender(Function):
             v_dc, v_rest = xchg.reduce(
                 v_colors, lambda m, views: sh_backward_views_split(_DEG_OF_BASES[K], dtu, m,
                                                                    views),
-                early_flat=early["flat"], early_map=early["map"])
+                early_flat=early["flat"], early_map=early["map"], gathered=gathered)
         return (v_means, v_scales, v_quats, v_opac.view(ctx.opac_shape), v_dc, v_rest) + \
             (None,) * 15
 

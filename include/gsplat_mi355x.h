@@ -385,6 +385,15 @@ int gsplat_fused_preprocess_backward(
     float *v_opacity_logits, float *v_features_dc, float *v_features_rest, float *v_colors,
     void *stream);
 
+/* The data-parallel view exchange's send record (no gsplat counterpart), packed
+ * straight from the raster backward's gradient records: send [3N + 4] = the SH-output colour
+ * gradient v_colors [N,3] exactly as gsplat_fused_preprocess_backward writes it (zero for
+ * radii <= 0), then the camera centre campos [3], then 0.  Ready right after the raster
+ * backward, so the all-gather overlaps the rest of the backward. */
+int gsplat_exchange_pack_colors(int num_points, const void *grad_records, size_t records_bytes,
+                                const int32_t *radii, const float *colors, const float *campos,
+                                float *send, void *stream);
+
 /* Single-GPU training step: gsplat_fused_preprocess_backward with the Adam step of the six
  * parameter groups fused in (torch.optim.Adam foreach semantics, exactly gsplat_adam_step's
  * arithmetic).  The gradients stay in registers; means3d, log_scales, quats, opacity_logits,

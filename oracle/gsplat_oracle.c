@@ -546,7 +546,8 @@ void oracle_map_intersects(int n, const real *xys, const real *depths, const int
         get_tile_bbox(xys + 2 * i, (real)radii[i], tbx, tby, tmin, tmax);
         int cur = i == 0 ? 0 : cum_tiles_hit[i - 1];
         int32_t dbits;
-        memcpy(&dbits, depths + i, 4);
+        const float dk = (float)depths[i]; /* the key holds the float32 depth in both builds */
+        memcpy(&dbits, &dk, 4);
         int64_t depth_id = (int64_t)dbits; /* sign-extended like gsplat */
         for (int y = tmin[1]; y < tmax[1]; ++y)
             for (int x = tmin[0]; x < tmax[0]; ++x) {

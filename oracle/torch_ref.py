@@ -28,6 +28,16 @@ import torch
 BLOCK = 16
 
 
+def _f32(x):
+    """gsplat's float literal (0.3f, 1e-6f, SH_C1 ...) as the double it converts to: the
+    float64 restatement then differs from the float64 oracle by rounding only."""
+    return float(torch.tensor(x, dtype=torch.float32))
+
+
+_EWA, _LIM, _EIG, _EPS_W = _f32(0.3), _f32(1.3), _f32(0.1), _f32(1e-6)
+_AMAX, _AMIN, _TMIN = _f32(0.999), _f32(1.0 / 255.0), _f32(1e-4)
+
+
 def _quirk_flags(quirks):
     """(A5, A6, A8) straight-throughs from quirks: a bool switches all three; an int is the
     library's GSPLAT_QUIRK_* mask, whose EWA_UNCLAMPED bit (4) selects A6 (A5 and A8 are not
@@ -70,7 +80,7 @@ def project(means, scales, glob_scale, quats, viewmat, projmat, fx, fy, cx, cy, 
     V = cov3d_full(scales, glob_scale, quats, q8)
     tan_fovx = 0.5 * W / fx
     tan_fovy = 0.5 * H / fy
-    lim_x, lim_y = 1.3 * tan_fovx, 1.3 * tan_fovy
+    lim_x, lim_y = _LIM * tan_fovx, _LIM * tan_fovy
     tz = t[:, 2]
     txc = tz * torch.clamp(t[:, 0] / tz, -lim_x, lim_x)
     tyc = tz * torch.clamp(t[:, 1] / tz, -lim_y, lim_y)
@@ -89,18 +99,18 @@ def project(means, scales, glob_scale, quats, viewmat, projmat, fx, fy, cx, cy, 
         J = Jc
     T = J @ Wr
     cov2 = T @ V @ T.transpose(-1, -2)
-    a = cov2[:, 0, 0] + 0.3
+    a = cov2[:, 0, 0] + _EWA
     b = cov2[:, 1, 0]
-    c = cov2[:, 1, 1] + 0.3
+    c = cov2[:, 1, 1] + _EWA
     det = a * c - b * b
     conic = torch.stack([c / det, -b / det, a / det], -1)
     with torch.no_grad():
         bb = 0.5 * (a + c)
-        v1 = bb + torch.sqrt(torch.clamp(bb * bb - det, min=0.1))
-        v2 = bb - torch.sqrt(torch.clamp(bb * bb - det, min=0.1))
+        v1 = bb + torch.sqrt(torch.clamp(bb * bb - det, min=_EIG))
+        v2 = bb - torch.sqrt(torch.clamp(bb * bb - det, min=_EIG))
         radius = torch.ceil(3 * torch.sqrt(torch.maximum(v1, v2)))
     ph = torch.cat([means, torch.ones_like(means[:, :1])], -1) @ Pm.T
-    rw = 1.0 / (ph[:, 3] + 1e-6)
+    rw = 1.0 / (ph[:, 3] + _EPS_W)
     if q5:
         rw = rw.detach()
     xy = torch.stack([0.5 * W * ph[:, 0] * rw + cx - 0.5, 0.5 * H * ph[:, 1] * rw + cy - 0.5],
@@ -126,15 +136,15 @@ def project(means, scales, glob_scale, quats, viewmat, projmat, fx, fy, cx, cy, 
                 tile_min=(tminx, tminy), tile_max=(tmaxx, tmaxy))
 
 
-SH_C0 = 0.28209479177387814
-SH_C1 = 0.4886025119029199
-SH_C2 = [1.0925484305920792, -1.0925484305920792, 0.31539156525252005, -1.0925484305920792,
-         0.5462742152960396]
-SH_C3 = [-0.5900435899266435, 2.890611442640554, -0.4570457994644658, 0.3731763325901154,
-         -0.4570457994644658, 1.445305721320277, -0.5900435899266435]
-SH_C4 = [2.5033429417967046, -1.7701307697799304, 0.9461746957575601, -0.6690465435572892,
+SH_C0 = _f32(0.28209479177387814)
+SH_C1 = _f32(0.4886025119029199)
+SH_C2 = [_f32(c) for c in [1.0925484305920792, -1.0925484305920792, 0.31539156525252005, -1.0925484305920792,
+         0.5462742152960396]]
+SH_C3 = [_f32(c) for c in [-0.5900435899266435, 2.890611442640554, -0.4570457994644658, 0.3731763325901154,
+         -0.4570457994644658, 1.445305721320277, -0.5900435899266435]]
+SH_C4 = [_f32(c) for c in [2.5033429417967046, -1.7701307697799304, 0.9461746957575601, -0.6690465435572892,
          0.10578554691520431, -0.6690465435572892, 0.47308734787878004, -1.7701307697799304,
-         0.6258357354491761]
+         0.6258357354491761]]
 
 
 def sh_basis(degree, dirs):
@@ -206,10 +216,10 @@ def rasterize(xys, depths, radii, conics, num_tiles_hit, colors, opacity, H, W, 
         dy = xys[g, 1] - py
         cn = conics[g]
         sigma = 0.5 * (cn[0] * dx * dx + cn[2] * dy * dy) + cn[1] * dx * dy
-        alpha = torch.clamp(opacity.reshape(-1)[g] * torch.exp(-sigma), max=0.999)
-        ok = inb & ~(sigma < 0) & ~(alpha < 1.0 / 255.0)
+        alpha = torch.clamp(opacity.reshape(-1)[g] * torch.exp(-sigma), max=_AMAX)
+        ok = inb & ~(sigma < 0) & ~(alpha < _AMIN)
         next_T = T * (1 - alpha)
-        term = ok & (next_T <= 1e-4)
+        term = ok & (next_T <= _TMIN)
         done = done | term
         ok = ok & ~term
         okf = ok.to(dt)
@@ -280,12 +290,12 @@ def rasterize_tiles(xys, conics, colors, opacity, background, gids_sorted, tile_
         dx = g[:, :1] - px[None, :]
         dy = g[:, 1:2] - py[None, :]
         sigma = 0.5 * (cn[:, :1] * dx * dx + cn[:, 2:3] * dy * dy) + cn[:, 1:2] * dx * dy
-        alpha = torch.clamp(op_all[ids][:, None] * torch.exp(-sigma), max=0.999)
-        ok = (sigma >= 0) & (alpha >= 1.0 / 255.0)
+        alpha = torch.clamp(op_all[ids][:, None] * torch.exp(-sigma), max=_AMAX)
+        ok = (sigma >= 0) & (alpha >= _AMIN)
         a = torch.where(ok, alpha, torch.zeros_like(alpha))
         T_after = torch.cumprod(1 - a, 0)
         T_before = torch.cat([torch.ones_like(T_after[:1]), T_after[:-1]], 0)
-        term = ok & (T_after <= 1e-4)
+        term = ok & (T_after <= _TMIN)
         alive = torch.cumsum(term.to(torch.int32), 0) == 0
         w = a * T_before * alive
         T_fin = torch.prod(torch.where(alive, 1 - a, torch.ones_like(a)), 0)

@@ -5,6 +5,19 @@ CPU only.  These pin the oracle before it is trusted as the GPU kernels' checker
 has no offline fixtures, so calculus is the independent reference; the
 documented gsplat 0.1.x deviations are reproduced in torch_ref with
 straight-through constructions and exercised here both ways.
+
+Two legs per function, so neither tolerance has to absorb the other's error:
+
+* the oracle's DOUBLE build (liboracle64.so: the same C source, real = double, gsplat's float
+  constants) against float64 autograd: the same mathematics evaluated twice in double, so the
+  bound is double rounding -- rtol 1e-9 (observed <= 3e-11); integer outputs (radii,
+  num_tiles_hit, final_idx) identical;
+* the FLOAT build (the checker the GPU tests use) against the double build at the parity bar
+  the GPU kernels are held to, |f32 - f64| <= 1e-5 + 1e-4 |f64| element by element, with no
+  slack on these sizes except where a sum cancels: v_scale / v_quat are sums over the six
+  v_cov3d entries, and where those terms cancel the rounding of the sum itself is the floor
+  (slack 8 eps32 x sum |term|, _cov3d_abs_terms; one element of the 39 cases needs it);
+  integer outputs identical.
 """
 import numpy as np
 import pytest
@@ -13,6 +26,41 @@ import torch
 import torch_ref as TR
 from gaussctrl_exp_amd.camera import synthetic_camera
 from gaussctrl_exp_amd.scene import synthetic_scene
+
+RTOL64, ATOL64 = 1e-9, 1e-11  # double build vs float64 autograd
+
+
+def _d(a):
+    return np.asarray(a, np.float64)
+
+
+def _at_bar(got32, ref64, name="", slack=0.0):
+    """The GPU parity bar, elementwise: |f32 - f64| <= 1e-5 + 1e-4 |f64| (+ slack)."""
+    got32, ref64 = np.asarray(got32, np.float64), np.asarray(ref64, np.float64)
+    err = np.abs(got32 - ref64) - (1e-5 + 1e-4 * np.abs(ref64) + slack)
+    assert (err <= 0).all(), (name, float(err.max()), np.unravel_index(err.argmax(), err.shape))
+
+
+def _cov3d_abs_terms(scales, quats, v_cov3d):
+    """Per Gaussian, sum_ij |v_cov3d_ij| |d cov3d_ij / d scale_k| (and / d quat_k): the scale
+    of the sum v_scale / v_quat are formed from.  When its terms cancel (v_cov3d in the
+    thousands, the result ~1e-2) float32 rounding of that sum alone reaches ~eps32 times it,
+    past the bar's 1e-5 absolute floor: that is the per-element slack, 8 eps32 x this."""
+    from torch.func import jacrev, vmap
+
+    def cov6(s, q):
+        V = TR.cov3d_full(s[None], 1.0, q[None])[0]
+        return torch.stack([V[0, 0], V[1, 0], V[2, 0], V[1, 1], V[2, 1], V[2, 2]])
+    js, jq = vmap(jacrev(cov6, argnums=(0, 1)))(scales.double(), quats.double())
+    w = torch.from_numpy(np.abs(_d(v_cov3d)))[..., None]
+    return (w * js.abs()).sum(1).numpy(), (w * jq.abs()).sum(1).numpy()
+
+
+def _proj_args(sc, scales, quats, cam, f64=False):
+    cv = _d if f64 else (lambda a: np.asarray(a, np.float32))
+    return (cv(sc.means.numpy()), cv(scales.numpy()), 1.0, cv(quats.numpy()),
+            cv(cam.viewmat.numpy()), cv(cam.projmat.numpy()), cam.fx, cam.fy, cam.cx, cam.cy,
+            cam.height, cam.width)
 
 
 def _setup(n=300, W=64, H=48, seed=0, scale_lo=0.02, scale_hi=0.12, max_opac=0.95):
@@ -27,24 +75,25 @@ def _setup(n=300, W=64, H=48, seed=0, scale_lo=0.02, scale_hi=0.12, max_opac=0.9
 def test_project_forward_matches_torch(oracle_lib):
     O = oracle_lib
     sc, cam, scales, quats, _ = _setup()
-    xys, depths, radii, conics, nth, cov3d = O.project_forward(
-        sc.means.numpy(), scales.numpy(), 1.0, quats.numpy(), cam.viewmat.numpy(),
-        cam.projmat.numpy(), cam.fx, cam.fy, cam.cx, cam.cy, cam.height, cam.width,
-        cam.tile_bounds)
-    r = TR.project(sc.means, scales, 1.0, quats, cam.viewmat, cam.projmat, cam.fx, cam.fy, cam.cx,
-                   cam.cy, cam.height, cam.width, cam.tile_bounds)
+    with O.float64():
+        xys, depths, radii, conics, nth, cov3d = O.project_forward(
+            *_proj_args(sc, scales, quats, cam, True), cam.tile_bounds)
+    r = TR.project(sc.means.double(), scales.double(), 1.0, quats.double(), cam.viewmat.double(),
+                   cam.projmat.double(), cam.fx, cam.fy, cam.cx, cam.cy, cam.height, cam.width,
+                   cam.tile_bounds)
     vis = radii > 0
     assert vis.sum() > 50
-    # integer outputs: identical except where float32 rounding differs at a tile boundary
-    assert (radii == r["radii"].numpy()).mean() > 0.99
-    assert (nth == r["num_tiles_hit"].numpy()).mean() > 0.99
-    both = vis & (r["radii"].numpy() > 0)
-    np.testing.assert_allclose(xys[both], r["xys"].detach().numpy()[both], rtol=1e-5, atol=1e-3)
-    np.testing.assert_allclose(depths[both], r["depths"].detach().numpy()[both], rtol=1e-6)
-    np.testing.assert_allclose(conics[both], r["conics"].detach().numpy()[both], rtol=2e-4,
-                               atol=1e-6)
-    np.testing.assert_allclose(cov3d[both], r["cov3d"].detach().numpy()[both], rtol=1e-4,
-                               atol=1e-8)
+    np.testing.assert_array_equal(radii, r["radii"].numpy())
+    np.testing.assert_array_equal(nth, r["num_tiles_hit"].numpy())
+    for name, got in (("xys", xys), ("depths", depths), ("conics", conics), ("cov3d", cov3d)):
+        np.testing.assert_allclose(got, r[name].numpy(), rtol=RTOL64, atol=ATOL64, err_msg=name)
+    # the float build (the GPU tests' checker) against the double build
+    f32 = O.project_forward(*_proj_args(sc, scales, quats, cam), cam.tile_bounds)
+    np.testing.assert_array_equal(f32[2], radii)
+    np.testing.assert_array_equal(f32[4], nth)
+    for name, a, b in zip(("xys", "depths", "conics", "cov3d"), [f32[k] for k in (0, 1, 3, 5)],
+                          (xys, depths, conics, cov3d)):
+        _at_bar(a, b, name)
 
 
 def _wide(sc, scales):
@@ -72,22 +121,27 @@ def test_project_backward_matches_autograd(oracle_lib, seed, quirk_mask):
     sc, cam, scales, quats, _ = _setup(seed=seed, n=600 if seed == 2 else 300)
     if seed == 2:
         sc, scales = _wide(sc, scales)
-    xys, depths, radii, conics, nth, cov3d = O.project_forward(
-        sc.means.numpy(), scales.numpy(), 1.0, quats.numpy(), cam.viewmat.numpy(),
-        cam.projmat.numpy(), cam.fx, cam.fy, cam.cx, cam.cy, cam.height, cam.width,
-        cam.tile_bounds)
     g = torch.Generator().manual_seed(100 + seed)
     n = sc.num_points
     v_xys = torch.randn(n, 2, generator=g)
     v_depths = torch.randn(n, generator=g)
     v_conics = torch.randn(n, 3, generator=g) * 10
-    _, _, v_mean, v_scale, v_quat = O.project_backward(
-        sc.means.numpy(), scales.numpy(), 1.0, quats.numpy(), cam.viewmat.numpy(),
-        cam.projmat.numpy(), cam.fx, cam.fy, cam.cx, cam.cy, cam.height, cam.width, cov3d,
-        radii, conics, v_xys.numpy(), v_depths.numpy(), v_conics.numpy())
+    vs = (v_xys.numpy(), v_depths.numpy(), v_conics.numpy())
+    # float build (the checker) on the float inputs
+    a32 = _proj_args(sc, scales, quats, cam)
+    f32 = O.project_forward(*a32, cam.tile_bounds)
+    b32 = O.project_backward(*a32, f32[5], f32[2], f32[3], *vs)
+    # double build: the quaternions renormalised in double (gsplat's VJP is that of the unit
+    # quaternion; a float-normalised one is 1e-7 off unit length, which autograd sees)
+    q64 = quats.double() / quats.double().norm(dim=-1, keepdim=True)
+    a64 = _proj_args(sc, scales, q64, cam, True)
+    with O.float64():
+        xys, depths, radii, conics, nth, cov3d = O.project_forward(*a64, cam.tile_bounds)
+        _, _, v_mean, v_scale, v_quat = O.project_backward(*a64, cov3d, radii, conics,
+                                                           *[_d(v) for v in vs])
     m = sc.means.double().requires_grad_()
     s = scales.double().requires_grad_()
-    q = quats.double().requires_grad_()
+    q = q64.clone().requires_grad_()
     r = TR.project(m, s, 1.0, q, cam.viewmat.double(), cam.projmat.double(), cam.fx, cam.fy,
                    cam.cx, cam.cy, cam.height, cam.width, cam.tile_bounds, quirks=quirk_mask)
     # gsplat's v_conic.y is the gradient w.r.t. one off-diagonal of the symmetric conic
@@ -107,9 +161,22 @@ def test_project_backward_matches_autograd(oracle_lib, seed, quirk_mask):
         rows = np.abs(t[:, 0] / t[:, 2]) <= lim
         lim = 1.3 * 0.5 * cam.height / cam.fy
         rows &= np.abs(t[:, 1] / t[:, 2]) <= lim
-    np.testing.assert_allclose(v_mean[rows], m.grad.numpy()[rows], rtol=2e-3, atol=2e-3)
-    np.testing.assert_allclose(v_scale[rows], s.grad.numpy()[rows], rtol=2e-3, atol=2e-3)
-    np.testing.assert_allclose(v_quat[rows], q.grad.numpy()[rows], rtol=2e-3, atol=2e-3)
+    for name, got, ref in (("v_mean", v_mean, m.grad), ("v_scale", v_scale, s.grad),
+                           ("v_quat", v_quat, q.grad)):
+        np.testing.assert_allclose(got[rows], ref.numpy()[rows], rtol=RTOL64, atol=ATOL64,
+                                   err_msg=name)
+    # float build vs double build on the same (float) inputs, every row (the A6 rows
+    # included: same algorithm)
+    a64 = _proj_args(sc, scales, quats, cam, True)
+    with O.float64():
+        f64 = O.project_forward(*a64, cam.tile_bounds)
+        b64 = O.project_backward(*a64, f64[5], f64[2], f64[3], *[_d(v) for v in vs])
+    np.testing.assert_array_equal(f32[2], f64[2])
+    eps = np.finfo(np.float32).eps
+    abs_s, abs_q = _cov3d_abs_terms(scales, quats, b64[1])
+    _at_bar(b32[2], b64[2], "v_mean")
+    _at_bar(b32[3], b64[3], "v_scale", 8 * eps * abs_s)
+    _at_bar(b32[4], b64[4], "v_quat", 8 * eps * abs_q)
 
 
 def test_project_quirk_A6_is_real(oracle_lib):
@@ -170,16 +237,20 @@ def test_sh_matches_autograd(oracle_lib, degree, use):
     O = oracle_lib
     g = torch.Generator().manual_seed(degree * 10 + use)
     n, K = 200, (degree + 1) ** 2
-    dirs = torch.randn(n, 3, generator=g)
-    coeffs = torch.randn(n, K, 3, generator=g)
-    v = torch.randn(n, 3, generator=g)
-    out = O.sh_forward(use, dirs.numpy(), coeffs.numpy())
-    c = coeffs.double().requires_grad_()
-    ref = TR.spherical_harmonics(use, dirs.double(), c)
-    np.testing.assert_allclose(out, ref.detach().numpy(), rtol=1e-5, atol=1e-5)
-    (ref * v.double()).sum().backward()
-    vc = O.sh_backward(use, dirs.numpy(), v.numpy(), K)
-    np.testing.assert_allclose(vc, c.grad.numpy(), rtol=1e-5, atol=1e-6)
+    dirs = torch.randn(n, 3, generator=g).double()
+    coeffs = torch.randn(n, K, 3, generator=g).double()
+    v = torch.randn(n, 3, generator=g).double()
+    with O.float64():
+        out = O.sh_forward(use, dirs.numpy(), coeffs.numpy())
+        vc = O.sh_backward(use, dirs.numpy(), v.numpy(), K)
+    c = coeffs.clone().requires_grad_()
+    ref = TR.spherical_harmonics(use, dirs, c)
+    np.testing.assert_allclose(out, ref.detach().numpy(), rtol=RTOL64, atol=ATOL64)
+    (ref * v).sum().backward()
+    np.testing.assert_allclose(vc, c.grad.numpy(), rtol=RTOL64, atol=ATOL64)
+    f = lambda t: t.float().numpy()
+    _at_bar(O.sh_forward(use, f(dirs), f(coeffs)), out, "colors")
+    _at_bar(O.sh_backward(use, f(dirs), f(v), K), vc, "v_coeffs")
 
 
 def _raster_inputs(O, seed=0, n=300, W=64, H=48, **kw):
@@ -195,21 +266,35 @@ def _raster_inputs(O, seed=0, n=300, W=64, H=48, **kw):
                 opac=opac.numpy(), bg=bg, H=H, W=W)
 
 
+def _render64(O, d):
+    with O.float64():
+        return O.render_forward(_d(d["xys"]), _d(d["depths"]), d["radii"], _d(d["conics"]),
+                                d["nth"], _d(d["colors"]), _d(d["opac"]), d["H"], d["W"],
+                                _d(d["bg"]))
+
+
+def _torch_raster(d, xy=None, cn=None, col=None, op=None):
+    t = lambda k: torch.from_numpy(_d(d[k]))
+    return TR.rasterize(t("xys") if xy is None else xy, torch.from_numpy(d["depths"]),
+                        torch.from_numpy(d["radii"]), t("conics") if cn is None else cn, None,
+                        t("colors") if col is None else col, t("opac") if op is None else op,
+                        d["H"], d["W"], t("bg"))
+
+
 @pytest.mark.parametrize("seed", [0, 1, 2])
 def test_raster_forward_matches_torch(oracle_lib, seed):
     O = oracle_lib
     d = _raster_inputs(O, seed)
+    f64 = _render64(O, d)
+    img, alpha = _torch_raster(d)
+    assert f64["num_intersects"] > 100
+    np.testing.assert_allclose(f64["img"], img.numpy(), rtol=RTOL64, atol=ATOL64)
+    np.testing.assert_allclose(f64["alpha"], alpha.numpy(), rtol=RTOL64, atol=ATOL64)
     f = O.render_forward(d["xys"], d["depths"], d["radii"], d["conics"], d["nth"], d["colors"],
                          d["opac"], d["H"], d["W"], d["bg"])
-    img, alpha = TR.rasterize(torch.from_numpy(d["xys"]).double(), torch.from_numpy(d["depths"]),
-                              torch.from_numpy(d["radii"]),
-                              torch.from_numpy(d["conics"]).double(), None,
-                              torch.from_numpy(d["colors"]).double(),
-                              torch.from_numpy(d["opac"]).double(), d["H"], d["W"],
-                              torch.from_numpy(d["bg"]).double())
-    assert f["num_intersects"] > 100
-    np.testing.assert_allclose(f["img"], img.numpy(), rtol=1e-4, atol=1e-4)
-    np.testing.assert_allclose(f["alpha"], alpha.numpy(), rtol=1e-4, atol=1e-4)
+    np.testing.assert_array_equal(f["final_idx"], f64["final_idx"])
+    _at_bar(f["img"], f64["img"], "img")
+    _at_bar(f["alpha"], f64["alpha"], "alpha")
 
 
 @pytest.mark.parametrize("seed", [0, 1, 2])
@@ -218,25 +303,27 @@ def test_raster_backward_matches_autograd(oracle_lib, seed):
     d = _raster_inputs(O, seed)
     f = O.render_forward(d["xys"], d["depths"], d["radii"], d["conics"], d["nth"], d["colors"],
                          d["opac"], d["H"], d["W"], d["bg"])
+    f64 = _render64(O, d)
     g = torch.Generator().manual_seed(99 + seed)
     v_img = torch.randn(d["H"], d["W"], 3, generator=g)
     v_alpha = torch.randn(d["H"], d["W"], generator=g)
-    v_xy, v_conic, v_col, v_op = O.render_backward(f, d["xys"], d["conics"], d["colors"],
-                                                   d["opac"], d["bg"], v_img.numpy(),
-                                                   v_alpha.numpy())
-    xy = torch.from_numpy(d["xys"]).double().requires_grad_()
-    cn = torch.from_numpy(d["conics"]).double().requires_grad_()
-    col = torch.from_numpy(d["colors"]).double().requires_grad_()
-    op = torch.from_numpy(d["opac"]).double().requires_grad_()
-    img, alpha = TR.rasterize(xy, torch.from_numpy(d["depths"]), torch.from_numpy(d["radii"]),
-                              cn, None, col, op, d["H"], d["W"],
-                              torch.from_numpy(d["bg"]).double())
+    got32 = O.render_backward(f, d["xys"], d["conics"], d["colors"], d["opac"], d["bg"],
+                              v_img.numpy(), v_alpha.numpy())
+    with O.float64():
+        got64 = O.render_backward(f64, _d(d["xys"]), _d(d["conics"]), _d(d["colors"]),
+                                  _d(d["opac"]), _d(d["bg"]), _d(v_img), _d(v_alpha))
+    xy = torch.from_numpy(_d(d["xys"])).requires_grad_()
+    cn = torch.from_numpy(_d(d["conics"])).requires_grad_()
+    col = torch.from_numpy(_d(d["colors"])).requires_grad_()
+    op = torch.from_numpy(_d(d["opac"])).requires_grad_()
+    img, alpha = _torch_raster(d, xy, cn, col, op)
     ((img * v_img.double()).sum() + (alpha * v_alpha.double()).sum()).backward()
     half = np.array([1.0, 0.5, 1.0])  # gsplat v_conic.y = half the parameter gradient
-    np.testing.assert_allclose(v_col, col.grad.numpy(), rtol=1e-3, atol=1e-3)
-    np.testing.assert_allclose(v_op, op.grad.numpy(), rtol=1e-3, atol=2e-3)
-    np.testing.assert_allclose(v_xy, xy.grad.numpy(), rtol=1e-3, atol=2e-3)
-    np.testing.assert_allclose(v_conic, cn.grad.numpy() * half, rtol=1e-3, atol=2e-3)
+    refs = (xy.grad.numpy(), cn.grad.numpy() * half, col.grad.numpy(), op.grad.numpy())
+    for name, a64, a32, ref in zip(("v_xy", "v_conic", "v_colors", "v_opacity"), got64, got32,
+                                   refs):
+        np.testing.assert_allclose(a64, ref, rtol=RTOL64, atol=ATOL64, err_msg=name)
+        _at_bar(a32, a64, name)
 
 
 def test_binning_matches_stable_sort(oracle_lib):
