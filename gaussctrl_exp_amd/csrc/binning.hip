@@ -225,6 +225,8 @@ struct DevIO {
   void *kout;                // sorted keys (may be null)
   uint32_t *vout;            // sorted values
   int begin, width, passes;
+  const uint2 *pa, *pb;      // payload ping-pong buffers (the depth sort's tile boxes, PL)
+  uint2 *pout;               // sorted payload
 };
 __device__ __forceinline__ bool pass_moves(const DevIO &io, int q) {
   return q == 0 || !digit_constant(io.fin, io.begin + q * io.width, io.width);
@@ -242,16 +244,20 @@ __device__ __forceinline__ bool last_move(const DevIO &io, int q) {
 }
 template <typename K>
 __device__ __forceinline__ void dev_io(const DevIO &io, int q, const K *&kin, const uint32_t *&vin,
-                                       K *&kout, uint32_t *&vout) {
+                                       K *&kout, uint32_t *&vout, const uint2 *&pin,
+                                       uint2 *&pout) {
   const bool src_b = q > 0 && data_in_b(io, q);  // pass 0 reads (ka, va)
   kin = (const K *)(src_b ? io.kb : io.ka);
   vin = src_b ? io.vb : io.va;
+  pin = src_b ? io.pb : io.pa;
   if (last_move(io, q)) {
     kout = (K *)io.kout;
     vout = io.vout;
+    pout = io.pout;
   } else {  // the other buffer
     kout = (K *)(src_b ? io.ka : io.kb);
     vout = (uint32_t *)(src_b ? io.va : io.vb);
+    pout = (uint2 *)(src_b ? io.pa : io.pb);
   }
 }
 
@@ -373,7 +379,7 @@ __global__ __launch_bounds__(1024) void rts_rowscan_kernel(uint32_t *__restrict_
   if (threadIdx.x == 0) rowtot[blockIdx.x] = running;
 }
 
-template <typename K, int ITEMS>
+template <typename K, int ITEMS, bool PAY = false>
 struct OsSmem {
   // the tile's (key, value) pairs in digit order: 32-bit keys interleaved with their values (one
   // 8-B LDS access per pair) in the small tiles, two arrays otherwise (16 keys per thread: the
@@ -386,6 +392,7 @@ struct OsSmem {
   uint32_t hscan[256];     // exclusive scan of this pass's digit totals (large tiles)
   uint32_t scan_tmp[4];
   uint32_t tile_n;         // keys this tile writes (all valid ones; fewer when dropping)
+  uint2 pay[PAY ? N : 1];  // the payload in the same order (PL)
   __device__ __forceinline__ void put(uint32_t i, K k, uint32_t v) {
     if constexpr (PAIR) {
       reinterpret_cast<uint2 *>(raw)[i] = make_uint2((uint32_t)k, v);
@@ -414,26 +421,60 @@ struct OsSmem {
 // LDS, takes its digits' global offsets from the row-scanned tile counts plus the digit bases
 // (the exclusive scan of the row totals), and writes the tile out in digit order, so each
 // digit's run is written by consecutive lanes.
-template <typename K, int WIDTH, int ITEMS>
+// tile count of a packed box {x0 | y0 << 16, x1 | y1 << 16}
+__device__ __forceinline__ uint32_t box_area(uint2 b) {
+  const int w = (int)(b.y & 0xFFFFu) - (int)(b.x & 0xFFFFu);
+  const int h = (int)(b.y >> 16) - (int)(b.x >> 16);
+  return (uint32_t)(max(w, 0) * max(h, 0));
+}
+constexpr uint32_t BOX_GATHER = 0xFFFFFFFFu;
+
+// PL (the compacting depth sort): each key also carries an 8-B payload -- the Gaussian's tile box
+// -- so the sorted output holds the boxes in depth order and the binning needs no random gather
+// of the records afterwards.  PL 1 (pass 0): the payload is read from the Gaussian-order records
+// prec[i].{y, z} (coalesced); PL 2: from pin.  Written to pout in the keys' sorted order.
+template <typename K, int WIDTH, int ITEMS, int PL = 0>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) void os_pass_kernel(
     const K *__restrict__ kin, const uint32_t *__restrict__ vin, K *__restrict__ kout,
     uint32_t *__restrict__ vout, long long n, int shift, int width,
     const uint32_t *__restrict__ rowtot, const uint32_t *__restrict__ offs, long long nblocks,
     int32_t *__restrict__ bins = nullptr, bool drop = false,
     const uint32_t *__restrict__ n_dev = nullptr, uint32_t *__restrict__ n_out = nullptr,
-    const uint32_t *__restrict__ kfin = nullptr, DevIO io = {}, int q = 0, int cap_launch = 0) {
+    const uint32_t *__restrict__ kfin = nullptr, DevIO io = {}, int q = 0, int cap_launch = 0,
+    const uint4 *__restrict__ prec = nullptr, const uint2 *__restrict__ pin = nullptr,
+    uint2 *__restrict__ pout = nullptr) {
   if (io.fin) {  // device-selected buffers (DevIO): a constant digit moves nothing
     if (q > 0 && digit_constant(io.fin, shift, width)) return;
     const K *ki;
     const uint32_t *vi;
     K *ko;
     uint32_t *vo;
-    dev_io<K>(io, q, ki, vi, ko, vo);
+    const uint2 *pi;
+    uint2 *po;
+    dev_io<K>(io, q, ki, vi, ko, vo, pi, po);
     kin = ki;
     vin = vi;
     kout = ko;
     vout = vo;
+    if (PL) {
+      pin = pi;
+      pout = po;
+    }
   }
+  auto load_pay = [&](long long i) -> uint2 {
+    if constexpr (PL == 1) {
+      // an allotment that is not the box's tile count (caller-supplied num_tiles_hit
+      // disagreeing with the box) travels as the marker BOX_GATHER: box_counts_kernel then
+      // reads that Gaussian's record itself
+      const uint4 r = prec[i];
+      return r.x == box_area(make_uint2(r.y, r.z)) ? make_uint2(r.y, r.z)
+                                                   : make_uint2(BOX_GATHER, 0u);
+    } else if constexpr (PL == 2) {
+      return pin[i];
+    } else {
+      return make_uint2(0u, 0u);
+    }
+  };
   // compacting sort: with drop, all-ones keys are left out (pass 0 of the depth sort: culled
   // Gaussians), and block 0 stores the kept count to n_out; later passes sort min(n, *n_dev)
   // keys and the workgroups past them exit at once.
@@ -448,11 +489,13 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     const long long b0 = (long long)blockIdx.x * TPB * ITEMS;
     K ck[ITEMS];
     uint32_t cv[ITEMS];
+    uint2 cp[PL ? ITEMS : 1];
 #pragma unroll
     for (int r = 0; r < ITEMS; ++r) {  // all loads in flight before the first store
       const long long i = min(b0 + r * TPB + threadIdx.x, n - 1);
       if (kout) ck[r] = kin[i];
       cv[r] = vin[i];
+      if constexpr (PL != 0) cp[r] = load_pay(i);
     }
 #pragma unroll
     for (int r = 0; r < ITEMS; ++r) {
@@ -460,11 +503,12 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
       if (i < n) {
         if (kout) kout[i] = ck[r];
         vout[i] = cv[r];
+        if constexpr (PL != 0) pout[i] = cp[r];
       }
     }
     return;
   }
-  __shared__ OsSmem<K, ITEMS> sm;
+  __shared__ OsSmem<K, ITEMS, PL != 0> sm;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int R = 1 << width;
   const uint32_t dmask = (uint32_t)(R - 1);
@@ -472,6 +516,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
   const unsigned long long lt = (1ull << lane) - 1ull;
   K key[ITEMS];
   uint32_t val[ITEMS], rank[ITEMS];
+  uint2 pay[PL ? ITEMS : 1];
   bool ok[ITEMS];
   // the digit total (and in small tiles this tile's row offset) first: vmcnt retires in issue
   // order, so the scans below wait for them alone
@@ -486,6 +531,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
       const long long i = min(sg + r * 64 + lane, n_cap - 1);
       key[r] = kin[i];
       val[r] = vin[i];
+      if constexpr (PL != 0) pay[r] = load_pay(i);
     }
   }
   if (n_dev && cap_launch) {  // (workgroup-uniform exits, after the loads went out)
@@ -558,6 +604,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
       if (ok[r]) {
         const uint32_t d = (uint32_t)(key[r] >> shift) & dmask;
         sm.put(sm.wcnt[wave][d] + rank[r], key[r], val[r]);
+        if constexpr (PL != 0) sm.pay[sm.wcnt[wave][d] + rank[r]] = pay[r];
       }
     }
     // large tiles: the row offset's load overlaps the scatter
@@ -608,6 +655,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
         const uint32_t pos = sm.gofs[(uint32_t)(k >> shift) & dmask] + (uint32_t)i;
         if (kout) kout[pos] = k;  // null: only the values are wanted (compacted depth sort)
         vout[pos] = v;
+        if constexpr (PL != 0) pout[pos] = sm.pay[i];
       }
     }
   }
@@ -655,11 +703,19 @@ int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t
                      bool first_counts_ready = false, int32_t *tile_bins = nullptr,
                      long long num_tiles = 0, bool drop = false, int first_pass = 0,
                      const uint32_t *n_dev_all = nullptr, uint32_t assume_const = 0,
-                     int32_t *range_out = nullptr) {
+                     int32_t *range_out = nullptr, const uint4 *prec = nullptr,
+                     uint2 *pa = nullptr, uint2 *pb = nullptr, uint2 *pout = nullptr) {
   // n_dev_all (not with drop): the key count lives on the device (<= n, the launch capacity;
   // more than n: overflow, every kernel returns at once) -- the capacity-launched tile sort
+  // prec (the compacting depth sort, drop and first_pass 0 only): every key carries the 8-B
+  // payload prec[i].{y, z} to pout (ping-pong through pa / pb), see os_pass_kernel's PL
   if (n <= 0) return 0;
   const SortPlan p = sort_plan(n, begin_bit, end_bit);
+  const bool pay = prec != nullptr;
+  if (pay && (!drop || first_pass != 0 || p.width != 8 || p.items > 8 || !pa || !pb || !pout)) {
+    set_error("radix_sort_pairs: payload needs the compacting 8-bit depth sort");
+    return 1;
+  }
   if (p.passes == 0) {
     note(hipMemcpyAsync(kout, ka, n * sizeof(K), hipMemcpyDeviceToDevice, st), "hipMemcpyAsync");
     note(hipMemcpyAsync(vout, va, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, st),
@@ -684,7 +740,8 @@ int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t
   // nothing (no copy)
   DevIO io{};
   if (kr.fin && first_pass == 0)
-    io = DevIO{kr.fin, ka, kb, va, vb, kout, vout, begin_bit, p.width, p.passes};
+    io = DevIO{kr.fin, ka, kb, va, vb, kout, vout, begin_bit, p.width, p.passes, pa, pb, pout};
+  uint2 *pin = nullptr, *palt = pb;  // host-selected payload buffers (pass 0 reads prec)
   for (int q = first_pass; q < p.passes; ++q) {
     // a digit the caller's earlier range says is constant: not launched at all (its three
     // launches cost ~14 us at the headline even when they return at once); the pass-0 range
@@ -694,6 +751,7 @@ int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t
     const bool last = q == p.passes - 1;
     K *ko = last ? kout : kalt;
     uint32_t *vo = last ? vout : valt;
+    uint2 *po = last ? pout : palt;
     // tile digit counts -> row scans -> offsets
     const int sh = begin_bit + q * p.width;
     const uint32_t *ndev = drop ? (q > 0 ? kept : nullptr) : n_dev_all;
@@ -714,17 +772,28 @@ int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t
     hipLaunchKernelGGL(rts_rowscan_kernel,
                        dim3((unsigned)p.radix + (q == 0 && kr.blk ? 1u : 0u)), dim3(1024), 0,
                        st, counts, p.nblocks, rowtot, kr, q, sh, p.width);
-#define OS_PASS(Wd, It)                                                                     \
-  hipLaunchKernelGGL((os_pass_kernel<K, Wd, It>), dim3((unsigned)p.nblocks), dim3(TPB), 0, st,   \
-                     kin, vin, ko, vo, n, sh, p.width, rowtot, counts, p.nblocks,              \
+#define OS_PASS_PL(Wd, It, PLv)                                                             \
+  hipLaunchKernelGGL((os_pass_kernel<K, Wd, It, PLv>), dim3((unsigned)p.nblocks), dim3(TPB), 0,  \
+                     st, kin, vin, ko, vo, n, sh, p.width, rowtot, counts, p.nblocks,          \
                      last ? tile_bins : nullptr, drop && q == 0,                               \
                      ndev, drop && q == 0 ? kept : nullptr,                                    \
-                     q > 0 && !io.fin ? kr.fin : nullptr, io, q, n_dev_all ? 1 : 0)
+                     q > 0 && !io.fin ? kr.fin : nullptr, io, q, n_dev_all ? 1 : 0, prec,      \
+                     pin, po)
+#define OS_PASS(Wd, It) OS_PASS_PL(Wd, It, 0)
 #define OS_PASS_W(Wd)                                                                       \
   do {                                                                                      \
     if (p.items == 16) OS_PASS(Wd, 16); else if (p.items == 8) OS_PASS(Wd, 8);             \
     else OS_PASS(Wd, 4);                                                                    \
   } while (0)
+#define OS_PASS_P(PLv)                                                                      \
+  do {                                                                                      \
+    if (p.items == 8) OS_PASS_PL(8, 8, PLv); else OS_PASS_PL(8, 4, PLv);                    \
+  } while (0)
+    if (sizeof(K) == 4 && pay) {
+      if constexpr (sizeof(K) == 4) {
+        if (q == 0) OS_PASS_P(1); else OS_PASS_P(2);
+      }
+    } else
     switch (p.width) {
       case 1: OS_PASS_W(1); break;
       case 2: OS_PASS_W(2); break;
@@ -735,14 +804,19 @@ int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t
       case 7: OS_PASS_W(7); break;
       default: OS_PASS_W(8); break;
     }
+#undef OS_PASS_P
 #undef OS_PASS_W
 #undef OS_PASS
+#undef OS_PASS_PL
     K *kfree = (kin == ka || kin == kb) ? kin : kalt;
     uint32_t *vfree = (vin == va || vin == vb) ? vin : valt;
+    uint2 *pfree = (pin == pa || pin == pb) ? pin : (q == 0 ? pa : palt);
     kin = ko;
     vin = vo;
     kalt = kfree;
     valt = vfree;
+    pin = po;
+    palt = pfree;
   }
   if (tile_bins)
     hipLaunchKernelGGL(bins_decode_kernel, dim3(cdiv(num_tiles, TPB)), dim3(TPB), 0, st,
@@ -886,6 +960,51 @@ __global__ __launch_bounds__(TPB) void gather_counts_kernel(int n, const uint32_
     for (int k = 0; k < SC_ITEMS; ++k) {
       const long long p = base + k * TPB + threadIdx.x;
       if (p < n) cnt[p] = 0u;
+    }
+  }
+  uint32_t total;
+  block_exclusive_scan<TPB>(sum, total, lds);
+  if (threadIdx.x == 0) partial[blockIdx.x] = total;
+}
+
+// Depth-ordered allotments from the boxes the depth sort carried (box[p], p < kept): cnt[p] =
+// the box's tile count, which is the record's allotment (the fused preprocess writes allotment
+// = box area; a caller's num_tiles_hit that disagrees arrives as BOX_GATHER and is read from
+// the record), zero past the visible count.  One workgroup per scan tile
+// (SC_TILE entries), whose allotment sum it writes (the first step of the device scan).  Reads
+// only coalesced words: the records' random gather by depth order (gather_counts_kernel,
+// ~18 us at the headline) is gone.
+__global__ __launch_bounds__(TPB) void box_counts_kernel(int n, const uint32_t *__restrict__ kept,
+                                                         uint2 *__restrict__ box,
+                                                         const uint32_t *__restrict__ order,
+                                                         const uint4 *__restrict__ rec,
+                                                         uint32_t *__restrict__ cnt,
+                                                         int *__restrict__ num_visible,
+                                                         uint32_t *__restrict__ partial) {
+  __shared__ uint32_t lds[TPB / 64];
+  const long long base = (long long)blockIdx.x * SC_TILE;
+  const long long nv = min((long long)n, (long long)*kept);
+  if (blockIdx.x == 0 && threadIdx.x == 0) *num_visible = (int)nv;
+  uint2 b[SC_ITEMS];
+#pragma unroll
+  for (int k = 0; k < SC_ITEMS; ++k) b[k] = box[min(base + k * TPB + threadIdx.x, max(nv - 1, 0LL))];
+  uint32_t sum = 0;
+#pragma unroll
+  for (int k = 0; k < SC_ITEMS; ++k) {
+    const long long p = base + k * TPB + threadIdx.x;
+    if (p < n) {
+      uint32_t c = 0u;
+      if (p < nv) {
+        if (b[k].x == BOX_GATHER) {  // an inconsistent allotment (see os_pass_kernel's PL)
+          const uint4 r = rec[order[p]];
+          box[p] = make_uint2(r.y, r.z);
+          c = r.x;
+        } else {
+          c = box_area(b[k]);
+        }
+      }
+      cnt[p] = c;
+      sum += c;
     }
   }
   uint32_t total;
@@ -2007,7 +2126,8 @@ struct Carver {
 struct Phase1 {
   uint32_t *dkeys_a, *dvals_a, *dkeys_b, *dvals_b, *order, *cnt, *off;
   uint4 *rec;  // per-Gaussian binning record (Gaussian order)
-  uint2 *box;  // tile bbox in depth order
+  uint2 *box;  // tile bbox in depth order (the depth sort's sorted payload)
+  uint2 *pay_a, *pay_b;  // the depth sort's payload ping-pong buffers
   uint32_t *dcount;  // I on the device (the pre-launched emission's bound check)
   void *rs_ws;
   size_t bytes;
@@ -2026,6 +2146,8 @@ Phase1 carve_phase1(void *base, int n) {
   p.off = c.take<uint32_t>(nn);
   p.rec = c.take<uint4>(nn * 4);
   p.box = c.take<uint2>(nn * 2);
+  p.pay_a = c.take<uint2>(nn * 2);
+  p.pay_b = c.take<uint2>(nn * 2);
   p.dcount = c.take<uint32_t>(4 * sizeof(uint32_t));
   size_t rs = radix_ws_bytes(n, 0, 32);
   size_t sc = scan_ws_bytes(n);
@@ -2222,17 +2344,27 @@ static int bin_count_impl(int num_points, const float *xys, const float *depths,
 #undef DEPTH_KEYS
   // range_out: d_counts[2..3] are written only when the key range is computed (the caller
   // zeroes them: without a range nothing is assumed and nothing reported)
-  radix_sort_pairs<uint32_t>(p.dkeys_a, p.dvals_a, p.dkeys_b, p.dvals_b, nullptr, p.order, n, 0,
-                             32, p.rs_ws, st, pre, nullptr, 0, true, 0, nullptr,
-                             use_key_range(n) ? assume_const : 0u,
-                             range_out ? d_counts + 2 : nullptr);
+  // below 4M keys (4 keys per thread) the sort carries each Gaussian's tile box (its record's
+  // y, z) to p.box in depth order; above, the payload's registers and LDS (16 keys per thread:
+  // occupancy 4 -> 2) cost more than the records' gather by depth order
+  const bool carry = sp.items <= 8;
+  if (radix_sort_pairs<uint32_t>(p.dkeys_a, p.dvals_a, p.dkeys_b, p.dvals_b, nullptr, p.order, n,
+                                 0, 32, p.rs_ws, st, pre, nullptr, 0, true, 0, nullptr,
+                                 use_key_range(n) ? assume_const : 0u,
+                                 range_out ? d_counts + 2 : nullptr, carry ? p.rec : nullptr,
+                                 p.pay_a, p.pay_b, p.box))
+    return 1;
   // depth-ordered allotments (+ per-tile sums) -> scan -> offsets and I = d_counts[1]
   const int nb = (int)cdiv(n, SC_TILE);
   // the kept count sits in the sort workspace's head, before the tile counts reused below
   const uint32_t *kept = sort_kept_word(p.rs_ws);
   uint32_t *partial = rts_tile_counts(p.rs_ws);  // the sort is done with its tile counts
-  hipLaunchKernelGGL(gather_counts_kernel, dim3(nb), dim3(TPB), 0, st, n, p.order, kept, p.rec,
-                     p.cnt, p.box, d_counts, partial);
+  if (carry)
+    hipLaunchKernelGGL(box_counts_kernel, dim3(nb), dim3(TPB), 0, st, n, kept, p.box, p.order,
+                       p.rec, p.cnt, d_counts, partial);
+  else
+    hipLaunchKernelGGL(gather_counts_kernel, dim3(nb), dim3(TPB), 0, st, n, p.order, kept, p.rec,
+                       p.cnt, p.box, d_counts, partial);
   if (no_scan) return check_launch("bin_count");  // (emit_scan_kernel scans, EMIT_SPEC)
   hipLaunchKernelGGL(scan_partials_kernel, dim3(1), dim3(1024), 0, st, partial, nb,
                      (uint32_t *)(d_counts + 1), p.dcount);
