@@ -479,8 +479,15 @@ __device__ __forceinline__ int wave_incl_scan(int v) {
 // prefix counts, then the bit within the batch word), `stage_one(pos, s)` fills its GStage,
 // the round's records land in stage[0 .. n) in descending position order and `blend(n)` runs
 // over them.  Windows of 64 batches (4,096 positions) per mask load.
+// GS_STAGE_AHEAD: the next round's positions are found and their ids loaded before this round
+// is blended, so a round's staging waits for one dependent load (the records) instead of two
+// (ids, then records).  stage_one(pos, id, s) fills the record of position pos, id = gids[pos].
+#ifndef GS_STAGE_AHEAD
+#define GS_STAGE_AHEAD 1
+#endif
 template <typename StageF, typename BlendF>
 __device__ __forceinline__ void walk_kept(const KeepSrc &S, int top, int bottom, GStage *stage,
+                                          int2 *ahead, const int *__restrict__ gids,
                                           StageF &&stage_one, BlendF &&blend) {
   const int lane = __lane_id();
   for (int wtop = top; wtop >= bottom; wtop -= 4096) {
@@ -490,9 +497,9 @@ __device__ __forceinline__ void walk_kept(const KeepSrc &S, int top, int bottom,
     const int incl = wave_incl_scan(cnt);
     const int excl = incl - cnt;
     const int total = __builtin_amdgcn_readlane(incl, 63);
-    for (int r = 0; r < total; r += 64) {
+    // the position of this lane's slot of the round starting at r (-1 past the window's total)
+    auto pos_of = [&](int r) -> int {
       const int j = r + lane;
-      const bool valid = j < total;
       int l = 0;
 #pragma unroll
       for (int step = 32; step >= 1; step >>= 1) {
@@ -501,11 +508,40 @@ __device__ __forceinline__ void walk_kept(const KeepSrc &S, int top, int bottom,
       }
       const unsigned long long w = __shfl(dw, l, 64);
       const int m = select_set_bit(w, j - __shfl(excl, l, 64));
-      GStage s;
-      if (valid) {
-        stage_one(wtop - 64 * l - m, s);
+      return j < total ? wtop - 64 * l - m : -1;
+    };
+    if (total <= 0) continue;
+#if GS_STAGE_AHEAD
+    {
+      const int p0 = pos_of(0);
+      ahead[lane] = make_int2(p0, p0 >= 0 ? gids[p0] : 0);
+    }
+#endif
+    for (int r = 0; r < total; r += 64) {
+#if GS_STAGE_AHEAD
+      // (position, id) of this lane's slot, found and loaded during the previous round; kept in
+      // LDS across the blend (no VGPRs held through it).  The next round's id load goes out with
+      // this round's record loads: both latencies overlap, the records' wait covers it.
+      const int2 cur = ahead[lane];
+      int2 nxt = make_int2(-1, 0);
+      if (r + 64 < total) {
+        nxt.x = pos_of(r + 64);
+        if (nxt.x >= 0) nxt.y = gids[nxt.x];
+      }
+      if (cur.x >= 0) {
+        GStage s;
+        stage_one(cur.x, cur.y, s);
         stage[lane] = s;
       }
+      ahead[lane] = nxt;
+#else
+      const int pcur = pos_of(r);
+      GStage s;
+      if (pcur >= 0) {
+        stage_one(pcur, gids[pcur], s);
+        stage[lane] = s;
+      }
+#endif
       wave_lds_sync();
       blend(min(64, total - r));
       wave_lds_sync();
@@ -513,12 +549,10 @@ __device__ __forceinline__ void walk_kept(const KeepSrc &S, int top, int bottom,
   }
 }
 // stage_gaussian<true> without the cull (the forward's keep bits already decided it)
-__device__ __forceinline__ void stage_kept(int idx, const int *__restrict__ gids,
-                                           const float2 *__restrict__ xys,
+__device__ __forceinline__ void stage_kept(int idx, int g, const float2 *__restrict__ xys,
                                            const float *__restrict__ conics,
                                            const float *__restrict__ colors,
                                            const float *__restrict__ opacity, GStage &s) {
-  const int g = gids[idx];
   const float2 xy = xys[g];
   s.x = xy.x;
   s.y = xy.y;
@@ -973,14 +1007,16 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
   // canonical once, so fminf needs no per-iteration canonicalisation of the bound
   const float amax = __builtin_canonicalizef(alpha_max);
   GStage *stage = lds[__builtin_amdgcn_readfirstlane(wave)];  // (uniform: SGPR address arithmetic)
+  __shared__ int2 ahead_lds[4][64];  // (KB: walk_kept's next-round ids)
+  int2 *ahead = ahead_lds[__builtin_amdgcn_readfirstlane(wave)];
   // KB: the kept positions from the forward's keep bits (the strip's two 8x8 blocks)
   KeepSrc S{};
   if constexpr (KB) {
     const int wt = (threadIdx.x >> 6) & 1;  // the strip's row half: blocks 2 wt, 2 wt + 1
     S = keep_src(kbits, kbw, tile_last, tile, range, 2 * wt, 2 * wt + 1);
   }
-  auto stage1 = [&](int idx, GStage &s) {
-    stage_kept(idx, gids, xys, conics, colors, opacity, s);
+  auto stage1 = [&](int idx, int g, GStage &s) {
+    stage_kept(idx, g, xys, conics, colors, opacity, s);
   };
   auto pre_blend = [&](int n) {
     for (int t = 0; t < n; ++t) {
@@ -1008,7 +1044,7 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
   };
   if (SPLIT) {  // the positions behind this part: T and the colour behind only
     if constexpr (KB) {
-      walk_kept(S, min(maxbin, range.y - 1), hi, stage, stage1, pre_blend);
+      walk_kept(S, min(maxbin, range.y - 1), hi, stage, ahead, gids, stage1, pre_blend);
     } else {
       for (int b = min(maxbin, range.y - 1); b >= hi; b -= 64) {
         const int idx = b - lane;
@@ -1137,7 +1173,7 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
     }
   };
   if constexpr (KB) {
-    walk_kept(S, last, lo, stage, stage1, main_blend);
+    walk_kept(S, last, lo, stage, ahead, gids, stage1, main_blend);
   } else {
     for (int b = last; b >= lo; b -= 64) {
       const int idx = b - lane;
@@ -1229,6 +1265,8 @@ __global__ __launch_bounds__(256) void raster_bwd8_kernel(
   const int field = slot >= 9 ? slot - 9 : slot;
   const float amax = __builtin_canonicalizef(alpha_max);
   GStage *stage = lds[__builtin_amdgcn_readfirstlane(wave)];  // (uniform: SGPR address arithmetic)
+  __shared__ int2 ahead_lds[4][64];  // (KB: walk_kept's next-round ids)
+  int2 *ahead = ahead_lds[__builtin_amdgcn_readfirstlane(wave)];
   // this batch's staged Gaussian (b: the batch top, bottom: the lowest position staged)
   auto stage_next = [&](int b, int bottom, GStage &s) {
     const int idx = b - (int)(threadIdx.x & 63);
@@ -1242,8 +1280,8 @@ __global__ __launch_bounds__(256) void raster_bwd8_kernel(
     S = keep_src(kbits, kbw, tile_last, tile, range, wt, wt);
     S.kmax1 = -1;  // one block
   }
-  auto stage1 = [&](int idx, GStage &s) {
-    stage_kept(idx, gids, xys, conics, colors, opacity, s);
+  auto stage1 = [&](int idx, int g, GStage &s) {
+    stage_kept(idx, g, xys, conics, colors, opacity, s);
   };
   auto pre_blend = [&](int n) {
     for (int t = 0; t < n; ++t) {  // (the main loop's T / Qs operations, nothing else)
@@ -1260,7 +1298,7 @@ __global__ __launch_bounds__(256) void raster_bwd8_kernel(
   };
   if (SPLIT) {  // the positions behind this part: T and the colour behind only
     if constexpr (KB) {
-      walk_kept(S, min(maxbin, range.y - 1), hi, stage, stage1, pre_blend);
+      walk_kept(S, min(maxbin, range.y - 1), hi, stage, ahead, gids, stage1, pre_blend);
     } else {
       for (int b = min(maxbin, range.y - 1); b >= hi; b -= 64) {
         GStage s;
@@ -1332,7 +1370,7 @@ __global__ __launch_bounds__(256) void raster_bwd8_kernel(
     }
   };
   if constexpr (KB) {
-    walk_kept(S, last, lo, stage, stage1, main_blend);
+    walk_kept(S, last, lo, stage, ahead, gids, stage1, main_blend);
   } else {
     for (int b = last; b >= lo; b -= 64) {
       GStage s;

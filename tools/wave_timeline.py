@@ -47,7 +47,7 @@ def bwd():
               *[P(x) for x in g], P(ws), wsz, st)
 
 log = torch.zeros(4 * T * 5, dtype=torch.int64, device=dev)
-runs = [("bwd", int(x)) for x in os.environ.get("BWD", "2,1").split(",")]
+runs = [("bwd", int(x)) for x in os.environ.get("BWD", "2,1").split(",") if x]
 if os.environ.get("FWD", "1") == "1":
     runs.append(("fwd", 0))
 for kind, f in runs:
