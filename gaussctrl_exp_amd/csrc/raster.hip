@@ -922,6 +922,402 @@ __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
   clear_side_job();
 }
 
+// ---------------------------------------------------------------- list-split forward (C = 3)
+// Small frames (below FWD_SPLIT_MAX_TILES tiles: c2 / c3 at 512^2 have 1,024) put every wave of
+// the forward on the chip at once, so the launch lasts as long as its longest list.  The split
+// forward cuts each tile's list into parts of `chunk` positions (the list-split plan's chunk):
+//  * fwd_plan_kernel: the parts, ordered by part index (earlier parts dispatched first), each
+//    tile's first part record index fbase[t], and the termination masks cleared;
+//  * raster_fwd_part_kernel: each part blended by its own 4 waves (one 8x8 block each) from
+//    T = 1 -- colour C_p, transmittance T_p, last composited position, and "terminated here"
+//    when the local T reaches 1e-4 (the true T, which starts at or below 1, is then at or below
+//    it too: fp32 multiplication is monotone, so the true chain has ended by that position).
+//    A tile of one part is the plain forward, bit for bit, and writes the outputs itself;
+//  * raster_fwd_combine_kernel: per pixel, the parts in list order: C += T C_p, T *= T_p while
+//    the running T stays clearly above the termination threshold; a part where it may reach it
+//    is re-walked from the running T to find the exact stop.  Part 0 starts from the true T = 1,
+//    so its record is exact.  The running T of later parts differs from the sequential product
+//    by rounding only, at most gamma(2K + j + 8) relatively after K factors and j parts (each
+//    product of n fp32 factors is within (1 +- 2^-24)^n of the exact one); a termination test
+//    that close to the threshold sends the pixel to an exact sequential walk of its list.  So
+//    final_idx -- the integer state the backward walks from -- is exactly the unsplit forward's,
+//    and the image / final T differ from it by fp32 rounding of the product's grouping only.
+// Later parts skip their remaining batches once earlier parts have terminated every pixel of
+// their block (ftmask: per part and block, the ballot of locally terminated pixels).
+constexpr long long FWD_SPLIT_MAX_TILES = 3584;
+int g_fwd_split = -1;  // gsplat_debug_forward_split: -1 / 1 on, 0 off, 2 exact walks only
+constexpr int FPR = 6;  // part record words per pixel: C (3), T, last | lterm << 31, factors
+
+__global__ __launch_bounds__(1024) void fwd_plan_kernel(int T, int chunk,
+                                                        const int2 *__restrict__ bins,
+                                                        int2 *__restrict__ items,
+                                                        int *__restrict__ n_items,
+                                                        int *__restrict__ fbase,
+                                                        unsigned long long *__restrict__ ftmask) {
+  __shared__ int hist[64], cur[64], lds[16];
+  const int tid = threadIdx.x;
+  if (tid < 64) hist[tid] = 0;
+  __syncthreads();
+  // tiles [t0, t1) of this thread (consecutive, for the prefix of part counts)
+  const int per = (T + 1023) / 1024, t0 = min(T, tid * per), t1 = min(T, t0 + per);
+  int local = 0;
+  for (int t = t0; t < t1; ++t) {
+    const int L = max(0, bins[t].y - bins[t].x);
+    const int m = max(1, (L + chunk - 1) / chunk);
+    local += m;
+    for (int j = 0; j < m; ++j) atomicAdd(&hist[min(j, 63)], 1);
+  }
+  // exclusive scan of the per-thread part counts -> fbase
+  int x = local;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int y = __shfl_up(x, d, 64);
+    if ((tid & 63) >= d) x += y;
+  }
+  if ((tid & 63) == 63) lds[tid >> 6] = x;
+  __syncthreads();
+  if (tid < 64) {
+    int w = tid < 16 ? lds[tid] : 0;
+#pragma unroll
+    for (int d = 1; d < 16; d <<= 1) {
+      const int y = __shfl_up(w, d, 64);
+      if (tid >= d) w += y;
+    }
+    if (tid < 16) lds[tid] = w;  // inclusive wave totals
+    const int h = hist[tid];
+    int c = h;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int y = __shfl_up(c, d, 64);
+      if (tid >= d) c += y;
+    }
+    cur[tid] = c - h;
+    if (tid == 63) *n_items = c;
+  }
+  __syncthreads();
+  int run = x - local + ((tid >> 6) ? lds[(tid >> 6) - 1] : 0);
+  for (int t = t0; t < t1; ++t) {
+    fbase[t] = run;
+    const int L = max(0, bins[t].y - bins[t].x);
+    const int m = max(1, (L + chunk - 1) / chunk);
+    for (int j = 0; j < m; ++j) items[atomicAdd(&cur[min(j, 63)], 1)] = make_int2(t, j);
+    run += m;
+  }
+  if (tid == 1023) fbase[T] = run;
+  __syncthreads();
+  const int total = lds[15];
+  for (int k = tid; k < SPLIT_WAVES * total; k += 1024) ftmask[k] = 0ull;
+}
+
+// One staged batch of the forward's walk (64 list positions from b, within [b, end)): the
+// 8x8-block cull (touches_rect, as raster_fwd3u_kernel) and the kept records into the wave's
+// LDS stage; returns the kept count and the batch's keep ballot.
+__device__ __forceinline__ int fwd_stage_batch(int b, int end, const int *__restrict__ gids,
+                                               const float2 *__restrict__ xys,
+                                               const float *__restrict__ conics,
+                                               const float *__restrict__ colors,
+                                               const float *__restrict__ opacity,
+                                               const WaveRect &R, GStage *stage,
+                                               unsigned long long &kmask) {
+  const int idx = b + __lane_id();
+  GStage s;
+  const bool keep = idx < end && stage_gaussian(idx, gids, xys, conics, colors, opacity, R.rx0,
+                                                R.rx1, R.ry0, R.ry1, s);
+  kmask = __ballot(keep);
+  if (keep) stage[lanes_below(kmask)] = s;
+  wave_lds_sync();
+  return __popcll(kmask);
+}
+
+template <bool CNT = false>
+__global__ __launch_bounds__(256) void raster_fwd_part_kernel(
+    int tbx, int tby, int H, int W, const int *__restrict__ gids, const int2 *__restrict__ bins,
+    const float2 *__restrict__ xys, const float *__restrict__ conics,
+    const float *__restrict__ colors, const float *__restrict__ opacity,
+    const float *__restrict__ background, float *__restrict__ out_img,
+    float *__restrict__ final_Ts, int *__restrict__ final_idx, float4 *__restrict__ zero,
+    long long zero_n, const int *__restrict__ zero_radii, int *__restrict__ tile_last,
+    unsigned long long *__restrict__ kbits, long long kbw, const float *__restrict__ l1_gt,
+    float *__restrict__ l1_part, int l1_clamp, int chunk, const int2 *__restrict__ items,
+    const int *__restrict__ n_items, const int *__restrict__ fbase, float *__restrict__ fprec,
+    unsigned long long *__restrict__ ftmask) {
+  auto clear_side_job = [&]() {  // (as raster_fwd3u_kernel)
+    for (long long k = (long long)blockIdx.x * 256 + threadIdx.x; k < zero_n;
+         k += (long long)gridDim.x * 256)
+      if (!zero_radii || zero_radii[k >> 2] > 0) zero[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  const int slot = block_slot();
+  if (slot >= *n_items) {  // workgroup-uniform: past the last item
+    clear_side_job();
+    return;
+  }
+  const int2 it = items[slot];
+  const int tile = it.x, part = it.y;
+  const WaveRect R = wave_rect<1, 8>(tbx, tby, H, W, tile);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, wt = wave;
+  const int2 range = bins[tile];
+  const int L = max(0, range.y - range.x);
+  const int m = max(1, (L + chunk - 1) / chunk);
+  if (!R.live) {
+    if (m == 1 && lane == 0) {
+      if (tile_last) tile_last[SPLIT_WAVES * tile + wt] = -1;
+      if (l1_part) l1_part[SPLIT_WAVES * tile + wt] = 0.f;
+    }
+    clear_side_job();
+    return;
+  }
+  __shared__ GStage lds[4][64];
+  GStage *stage = lds[__builtin_amdgcn_readfirstlane(wave)];
+  const int j = R.j, i = R.i0;
+  const float px = (float)j, py = (float)i;
+  const bool inimg = i < H && j < W;
+  const int lo = range.x + part * chunk, hi = min(lo + chunk, range.y);
+  float T = 1.f, cr = 0.f, cg = 0.f, cb = 0.f, nfac = 0.f;
+  int cur = -1;
+  bool done = !inimg, lterm = false;
+  const unsigned long long live = __ballot(inimg);
+  const int p = fbase[tile] + part;
+  const long long kb_base = wt * kbw + (long long)(range.x >> 6) + tile;
+  for (int b = lo; b < hi; b += 64) {
+    if (__all(done)) break;
+    if (part > 0) {  // every live pixel terminated by an earlier part: nothing left to do here
+      unsigned long long t = 0;
+      for (int k = lane; k < part; k += 64)
+        t |= __hip_atomic_load(&ftmask[(size_t)(fbase[tile] + k) * SPLIT_WAVES + wt],
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) t |= __shfl_xor(t, o, 64);
+      if ((t & live) == live) break;
+    }
+    unsigned long long kmask;
+    const int n = fwd_stage_batch(b, hi, gids, xys, conics, colors, opacity, R, stage, kmask);
+    if (kbits && lane == 0) kbits[kb_base + ((b - range.x) >> 6)] = kmask;
+    for (int t = 0; t < n; ++t) {
+      const GStage G = stage_at(stage, t);
+      const float dx = G.x - px;
+      const float sg = gs_sigma(G.hc, G.b * dx, G.ha * dx * dx, G.y - py);
+      const float al = fminf(0.999f, G.o * gs_vis(sg));
+      const bool v = !done && sg >= 0.f && al >= ALPHA_MIN;
+      const float nT = T * (1.f - al);
+      const bool term = v && nT <= 1e-4f, comp = v && !term;
+      done = done || term;
+      lterm = lterm || term;
+      const float w = comp ? al * T : 0.f;
+      cr += G.r * w;
+      cg += G.g * w;
+      cb += G.bl * w;
+      T = comp ? nT : T;
+      cur = comp ? G.idx : cur;
+      nfac += comp ? 1.f : 0.f;
+      if (__all(done)) break;
+    }
+    wave_lds_sync();
+  }
+  if (m == 1) {  // the whole list: the plain forward's outputs (the same per-pixel operations)
+    const int ci = cur < 0 ? 0 : cur;
+    const float bg0 = background[0], bg1 = background[1], bg2 = background[2];
+    float acc = 0.f;
+    if (inimg) {
+      const int pix = i * W + j;
+      final_Ts[pix] = T;
+      final_idx[pix] = ci;
+      out_img[3 * pix] = cr + T * bg0;
+      out_img[3 * pix + 1] = cg + T * bg1;
+      out_img[3 * pix + 2] = cb + T * bg2;
+      if (l1_part)
+        acc = fabsf(l1_gt[3 * pix] - l1_clampv(cr + T * bg0, l1_clamp)) +
+              fabsf(l1_gt[3 * pix + 1] - l1_clampv(cg + T * bg1, l1_clamp)) +
+              fabsf(l1_gt[3 * pix + 2] - l1_clampv(cb + T * bg2, l1_clamp));
+    }
+    if (l1_part) {
+      acc = wave_sum(acc);
+      if (lane == 0) l1_part[SPLIT_WAVES * tile + wt] = acc;
+    }
+    if (tile_last) {
+      const int mx = wave_max_int(inimg ? ci : -1);
+      if (lane == 0) tile_last[SPLIT_WAVES * tile + wt] = mx;
+    }
+  } else {
+    float *r = fprec + ((size_t)p * SPLIT_WAVES + wt) * FPR * 64 + lane;
+    r[0] = cr;
+    r[64] = cg;
+    r[128] = cb;
+    r[192] = T;
+    reinterpret_cast<int *>(r)[256] = (int)((uint32_t)cur & 0x7FFFFFFFu) | (lterm ? (int)0x80000000u : 0);
+    r[320] = nfac;
+    const unsigned long long tm = __ballot(lterm);
+    if (tm && lane == 0)
+      __hip_atomic_fetch_or(&ftmask[(size_t)p * SPLIT_WAVES + wt], tm, __ATOMIC_RELAXED,
+                            __HIP_MEMORY_SCOPE_AGENT);
+  }
+  clear_side_job();
+}
+
+// The parts of a split tile in list order (see the section head).  One workgroup per tile, one
+// wave per 8x8 block; tiles of one part return at once (their outputs are written).
+__global__ __launch_bounds__(256) void raster_fwd_combine_kernel(
+    int tbx, int tby, int H, int W, const int *__restrict__ gids, const int2 *__restrict__ bins,
+    const float2 *__restrict__ xys, const float *__restrict__ conics,
+    const float *__restrict__ colors, const float *__restrict__ opacity,
+    const float *__restrict__ background, float *__restrict__ out_img,
+    float *__restrict__ final_Ts, int *__restrict__ final_idx, int *__restrict__ tile_last,
+    const float *__restrict__ l1_gt, float *__restrict__ l1_part, int l1_clamp, int chunk,
+    const int *__restrict__ fbase, const float *__restrict__ fprec, float U) {
+  const int tile = blockIdx.x;
+  const int2 range = bins[tile];
+  const int L = max(0, range.y - range.x);
+  const int m = max(1, (L + chunk - 1) / chunk);
+  if (m == 1) return;  // workgroup-uniform
+  const WaveRect R = wave_rect<1, 8>(tbx, tby, H, W, tile);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, wt = wave;
+  if (!R.live) {
+    if (lane == 0) {
+      if (tile_last) tile_last[SPLIT_WAVES * tile + wt] = -1;
+      if (l1_part) l1_part[SPLIT_WAVES * tile + wt] = 0.f;
+    }
+    return;
+  }
+  __shared__ GStage lds[4][64];
+  GStage *stage = lds[__builtin_amdgcn_readfirstlane(wave)];
+  const int j = R.j, i = R.i0;
+  const float px = (float)j, py = (float)i;
+  const bool inimg = i < H && j < W;
+  // U: the unit roundoff with a margin (0x1p-24 * 1.01); a huge U (gsplat_debug_forward_split
+  // mode 2) sends every pixel of a split tile to the exact walk -- the test of that path
+  float T = 1.f, cr = 0.f, cg = 0.f, cb = 0.f, K = 0.f;
+  int cur = 0;
+  bool done = !inimg, amb = false;
+  const int p0 = fbase[tile];
+  for (int q = 0; q < m; ++q) {
+    if (__all(done)) break;
+    const float *r = fprec + ((size_t)(p0 + q) * SPLIT_WAVES + wt) * FPR * 64 + lane;
+    const float pr = r[0], pg = r[64], pb = r[128], pT = r[192], pk = r[320];
+    const int lw = reinterpret_cast<const int *>(r)[256];
+    const bool plt = lw < 0;
+    const int plast = (int)((uint32_t)lw & 0x7FFFFFFFu) == 0x7FFFFFFF ? -1 : lw & 0x7FFFFFFF;
+    if (q == 0) {  // from the true T = 1: the part's own chain is the exact one
+      if (!done) {
+        cr = pr;
+        cg = pg;
+        cb = pb;
+        T = pT;
+        K = pk;
+        cur = plast >= 0 ? plast : 0;
+        done = plt;
+      }
+      continue;
+    }
+    const float d = (2.f * (K + pk) + (float)q + 8.f) * U;
+    const float Tend = T * pT;
+    const bool skip = !done && !plt && Tend > 1e-4f * (1.f + d);
+    if (skip) {
+      cr += T * pr;
+      cg += T * pg;
+      cb += T * pb;
+      T = Tend;
+      K += pk;
+      if (plast >= 0) cur = plast;
+    }
+    const bool need = !done && !skip;
+    if (!__any(need)) continue;
+    // re-walk part q from the running T for the pixels that may stop in it
+    bool act = need;
+    const int lo = range.x + q * chunk, hi = min(lo + chunk, range.y);
+    for (int b = lo; b < hi; b += 64) {
+      if (!__any(act)) break;
+      unsigned long long km;
+      const int n = fwd_stage_batch(b, hi, gids, xys, conics, colors, opacity, R, stage, km);
+      for (int t = 0; t < n; ++t) {
+        const GStage G = stage_at(stage, t);
+        const float dx = G.x - px;
+        const float sg = gs_sigma(G.hc, G.b * dx, G.ha * dx * dx, G.y - py);
+        const float al = fminf(0.999f, G.o * gs_vis(sg));
+        const bool v = act && sg >= 0.f && al >= ALPHA_MIN;
+        if (v) {
+          const float nT = T * (1.f - al);
+          const float dd = (2.f * K + (float)q + 10.f) * U;
+          if (nT <= 1e-4f * (1.f - dd)) {  // stops here for certain
+            act = false;
+            done = true;
+          } else if (nT > 1e-4f * (1.f + dd)) {  // composited for certain
+            const float w = al * T;
+            cr += G.r * w;
+            cg += G.g * w;
+            cb += G.bl * w;
+            T = nT;
+            cur = G.idx;
+            K += 1.f;
+          } else {  // too close to call from the regrouped product: exact walk below
+            amb = true;
+            act = false;
+            done = true;
+          }
+        }
+        if (!__any(act)) break;
+      }
+      wave_lds_sync();
+    }
+  }
+  if (__any(amb)) {
+    // the plain forward's sequential walk from the list start for the undecided pixels
+    float eT = 1.f, er = 0.f, eg = 0.f, eb = 0.f;
+    int ecur = 0;
+    bool edone = !amb;
+    for (int b = range.x; b < range.y; b += 64) {
+      if (__all(edone)) break;
+      unsigned long long km;
+      const int n = fwd_stage_batch(b, range.y, gids, xys, conics, colors, opacity, R, stage, km);
+      for (int t = 0; t < n; ++t) {
+        const GStage G = stage_at(stage, t);
+        const float dx = G.x - px;
+        const float sg = gs_sigma(G.hc, G.b * dx, G.ha * dx * dx, G.y - py);
+        const float al = fminf(0.999f, G.o * gs_vis(sg));
+        const bool v = !edone && sg >= 0.f && al >= ALPHA_MIN;
+        const float nT = eT * (1.f - al);
+        const bool term = v && nT <= 1e-4f, comp = v && !term;
+        edone = edone || term;
+        const float w = comp ? al * eT : 0.f;
+        er += G.r * w;
+        eg += G.g * w;
+        eb += G.bl * w;
+        eT = comp ? nT : eT;
+        ecur = comp ? G.idx : ecur;
+        if (__all(edone)) break;
+      }
+      wave_lds_sync();
+    }
+    if (amb) {
+      T = eT;
+      cr = er;
+      cg = eg;
+      cb = eb;
+      cur = ecur;
+    }
+  }
+  const float bg0 = background[0], bg1 = background[1], bg2 = background[2];
+  float acc = 0.f;
+  if (inimg) {
+    const int pix = i * W + j;
+    final_Ts[pix] = T;
+    final_idx[pix] = cur;
+    out_img[3 * pix] = cr + T * bg0;
+    out_img[3 * pix + 1] = cg + T * bg1;
+    out_img[3 * pix + 2] = cb + T * bg2;
+    if (l1_part)
+      acc = fabsf(l1_gt[3 * pix] - l1_clampv(cr + T * bg0, l1_clamp)) +
+            fabsf(l1_gt[3 * pix + 1] - l1_clampv(cg + T * bg1, l1_clamp)) +
+            fabsf(l1_gt[3 * pix + 2] - l1_clampv(cb + T * bg2, l1_clamp));
+  }
+  if (l1_part) {
+    acc = wave_sum(acc);
+    if (lane == 0) l1_part[SPLIT_WAVES * tile + wt] = acc;
+  }
+  if (tile_last) {
+    const int mx = wave_max_int(inimg ? cur : -1);
+    if (lane == 0) tile_last[SPLIT_WAVES * tile + wt] = mx;
+  }
+}
+
 // ---------------------------------------------------------------- backward, C = 3
 // Packed backward: 2*NP pixels per lane as float2 pairs, branch-free (an invalid pixel gets
 // alpha = vis = 0: T, the colour buffer and every partial sum are unchanged exactly).
@@ -1780,6 +2176,11 @@ struct SplitWs {
   long long items_bound;
   unsigned long long *kbits;  // the forward's keep bits (KeepSrc), SPLIT_WAVES x kbw words
   long long kbw;
+  // the list-split forward (frames below FWD_SPLIT_MAX_TILES tiles; null otherwise): each
+  // tile's first part index fbase[T + 1], the part records and termination masks
+  int *fbase;
+  float *fprec;
+  unsigned long long *ftmask;
   size_t bytes;
 };
 static SplitWs carve_split_ws(void *base, long long T, long long I, int chunk) {
@@ -1796,9 +2197,16 @@ static SplitWs carve_split_ws(void *base, long long T, long long I, int chunk) {
   w.n_items = (int *)take(sizeof(int));
   w.kbw = I / 64 + T + 2;
   w.kbits = (unsigned long long *)take((size_t)SPLIT_WAVES * w.kbw * sizeof(unsigned long long));
+  if (T < FWD_SPLIT_MAX_TILES) {
+    w.fbase = (int *)take((size_t)(T + 1) * sizeof(int));
+    w.fprec = (float *)take((size_t)w.items_bound * SPLIT_WAVES * FPR * 64 * sizeof(float));
+    w.ftmask = (unsigned long long *)take((size_t)w.items_bound * SPLIT_WAVES *
+                                          sizeof(unsigned long long));
+  }
   w.bytes = off;
   return w;
 }
+static bool forward_split_on(long long T) { return g_fwd_split != 0 && T < FWD_SPLIT_MAX_TILES; }
 static bool default_variants() {
   // (the staging pipeline bits change the schedule only)
   return g_fwd_pxl == FWD_PXL && g_bwd_pxl == BWD_PXL && (g_bwd_flags & ~(7 << 28)) == 0;
@@ -1853,6 +2261,16 @@ extern "C" size_t gsplat_rasterize_split_bytes(int tile_bounds_x, int tile_bound
 extern "C" int gsplat_debug_set_chunk(int chunk) {
   g_chunk_override = chunk;
   return 0;
+}
+
+// The list-split forward (raster_fwd_part_kernel), below 3,584 tiles (the plan workspace holds
+// its records there): -1 / 1 on (the default), 0 off, 2 on with every pixel of a split tile
+// resolved by the exact sequential walk (tests: then bit-identical to the unsplit forward).
+// Returns the previous setting.
+extern "C" int gsplat_debug_forward_split(int mode) {
+  const int prev = g_fwd_split;
+  if (mode >= -1 && mode <= 2) g_fwd_split = mode;
+  return prev;
 }
 
 static bool bad_frame(int tbx, int tby, int H, int W) {
@@ -2202,11 +2620,33 @@ static int forward_clearing_impl(
     }
     plan_kbits_note(plan, kbits != nullptr, true);
   }
-  launch_fwd<false>((hipStream_t)stream, tile_bounds_x, tile_bounds_y, img_height, img_width,
-                    gaussian_ids_sorted, tile_bins, xys, conics, colors, opacity, background,
-                    out_img, final_Ts, final_idx, nullptr, nullptr, (float4 *)clear,
-                    (long long)(clear_bytes / 16), clear_radii, tile_last, kbits, kbw, l1_gt,
-                    l1_part, l1_clamp);
+  const long long Tt = (long long)tile_bounds_x * tile_bounds_y;
+  if (chunk > 0 && forward_split_on(Tt) && !g_pair_count_on && default_variants()) {
+    // the list-split forward: plan, parts, combine (see fwd_plan_kernel)
+    const SplitWs w = carve_split_ws(plan, Tt, num_intersects, chunk);
+    hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(fwd_plan_kernel, dim3(1), dim3(1024), 0, st, (int)Tt, chunk,
+                       (const int2 *)tile_bins, w.items, w.n_items, w.fbase, w.ftmask);
+    hipLaunchKernelGGL(raster_fwd_part_kernel<false>, dim3((unsigned)w.items_bound), dim3(256), 0,
+                       st, tile_bounds_x, tile_bounds_y, img_height, img_width,
+                       gaussian_ids_sorted, (const int2 *)tile_bins, (const float2 *)xys, conics,
+                       colors, opacity, background, out_img, final_Ts, final_idx,
+                       (float4 *)clear, (long long)(clear_bytes / 16), clear_radii, tile_last,
+                       kbits, kbw, l1_gt, l1_part, l1_clamp, chunk, (const int2 *)w.items,
+                       (const int *)w.n_items, (const int *)w.fbase, w.fprec, w.ftmask);
+    hipLaunchKernelGGL(raster_fwd_combine_kernel, dim3((unsigned)Tt), dim3(256), 0, st,
+                       tile_bounds_x, tile_bounds_y, img_height, img_width, gaussian_ids_sorted,
+                       (const int2 *)tile_bins, (const float2 *)xys, conics, colors, opacity,
+                       background, out_img, final_Ts, final_idx, tile_last, l1_gt, l1_part,
+                       l1_clamp, chunk, (const int *)w.fbase, (const float *)w.fprec,
+                       g_fwd_split == 2 ? 1e30f : 0x1p-24f * 1.01f);
+  } else {
+    launch_fwd<false>((hipStream_t)stream, tile_bounds_x, tile_bounds_y, img_height, img_width,
+                      gaussian_ids_sorted, tile_bins, xys, conics, colors, opacity, background,
+                      out_img, final_Ts, final_idx, nullptr, nullptr, (float4 *)clear,
+                      (long long)(clear_bytes / 16), clear_radii, tile_last, kbits, kbw, l1_gt,
+                      l1_part, l1_clamp);
+  }
   // the loss of the partials and the list-split plan, one launch (post_forward_kernel)
   const bool plan_job = chunk > 0, loss_job = l1_part != nullptr;
   if (plan_job || loss_job) {

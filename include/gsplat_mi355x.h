@@ -322,6 +322,11 @@ int gsplat_rasterize_forward_clearing(
 /* Debug: force the list-split chunk (> 0, rounded up to 64), disable it (< 0) or restore
  * the automatic choice (0). */
 int gsplat_debug_set_chunk(int chunk);
+/* The list-split forward of small frames (below 3,584 tiles; gsplat_rasterize_forward_clearing*
+ * with a plan): -1 or 1 on (default), 0 off, 2 on with every pixel of a split tile resolved by
+ * the exact sequential walk (bit-identical to the unsplit forward; tests).  Returns the
+ * previous setting. */
+int gsplat_debug_forward_split(int mode);
 
 size_t gsplat_rasterize_backward_workspace_size(int num_points, int channels);
 int gsplat_rasterize_backward(int tile_bounds_x, int tile_bounds_y, int img_height,
