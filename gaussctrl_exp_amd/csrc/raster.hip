@@ -2596,12 +2596,23 @@ static int forward_clearing_impl(
     float *out_img, float *final_Ts, int32_t *final_idx, void *clear, size_t clear_bytes,
     const int32_t *clear_radii, int64_t num_intersects, int chunk, void *plan, size_t plan_bytes,
     const float *l1_gt, float *l1_part, int l1_clamp, float *l1_loss, void *stream) {
+  // chunk < 0: the list-split forward of parts of -chunk positions only (a render without a
+  // backward: no walk table, keep bits or backward plan)
+  const int fchunk = chunk < 0 ? -chunk : chunk;
   if (bad_frame(tile_bounds_x, tile_bounds_y, img_height, img_width) || clear_bytes % 16 ||
       (clear_bytes && !clear) || (clear_radii && clear_bytes % 64) ||
-      (chunk > 0 && (chunk % 64 || num_intersects < 0))) {
+      (fchunk > 0 && (fchunk % 64 || num_intersects < 0))) {
     set_error("%s: bad sizes (tiles=%dx%d H=%d W=%d clear=%zu chunk=%d)", who, tile_bounds_x,
               tile_bounds_y, img_height, img_width, clear_bytes, chunk);
     return 1;
+  }
+  if (chunk < 0) {
+    const SplitWs w =
+        carve_split_ws(plan, (long long)tile_bounds_x * tile_bounds_y, num_intersects, fchunk);
+    if (!plan || plan_bytes < w.bytes) {
+      set_error("%s: split plan buffer %zu < %zu bytes", who, plan_bytes, w.bytes);
+      return 1;
+    }
   }
   int *tile_last = nullptr;  // the list-split plan's walk table, filled by the blend's waves
   unsigned long long *kbits = nullptr;  // and the backward's keep bits (KeepSrc)
@@ -2621,8 +2632,9 @@ static int forward_clearing_impl(
     plan_kbits_note(plan, kbits != nullptr, true);
   }
   const long long Tt = (long long)tile_bounds_x * tile_bounds_y;
-  if (chunk > 0 && forward_split_on(Tt) && !g_pair_count_on && default_variants()) {
+  if (fchunk > 0 && forward_split_on(Tt) && !g_pair_count_on && default_variants()) {
     // the list-split forward: plan, parts, combine (see fwd_plan_kernel)
+    const int chunk = fchunk;
     const SplitWs w = carve_split_ws(plan, Tt, num_intersects, chunk);
     hipStream_t st = (hipStream_t)stream;
     hipLaunchKernelGGL(fwd_plan_kernel, dim3(1), dim3(1024), 0, st, (int)Tt, chunk,

@@ -37,6 +37,8 @@ from .rasterize import (BLOCK_X, BLOCK_Y, bin_gaussians, bin_gaussians_speculati
                         last_num_visible)
 
 _DEG_OF_BASES = {1: 0, 4: 1, 9: 2, 16: 3, 25: 4}
+# frames below this many tiles get the list-split forward (raster.hip FWD_SPLIT_MAX_TILES)
+FWD_SPLIT_TILES = 3584
 
 
 class _FusedRender(Function):
@@ -107,12 +109,15 @@ class _FusedRender(Function):
             """The blend (it also clears the gradient records the backward accumulates into and
             fills the list-split plan, whose layout follows layout_i)."""
             nonlocal chunk, plan
-            chunk = _lib.query("gsplat_rasterize_chunk_size", tbx, tby, layout_i) \
-                if need_grad else 0
+            chunk = _lib.query("gsplat_rasterize_chunk_size", tbx, tby, layout_i)
+            if not need_grad:
+                # no backward: the plan only for the list-split forward of small frames
+                # (below FWD_SPLIT_TILES tiles), signalled by a negative chunk
+                chunk = -chunk if tbx * tby < FWD_SPLIT_TILES else 0
             plan = None
-            if chunk > 0:  # the list-split backward's plan (filled by the blend's waves)
+            if chunk != 0:  # the list-split plan (filled by the blend's waves)
                 plan = torch.empty((_lib.query("gsplat_rasterize_split_bytes", tbx, tby,
-                                               layout_i, chunk),),
+                                               layout_i, abs(chunk)),),
                                    device=dev, dtype=torch.uint8)
             args = (tbx, tby, H, W, P(gids), P(bins), P(xys), P(conics), P(colors), P(opac),
                     P(background), P(out_img), P(final_Ts), P(final_idx), P(rec),

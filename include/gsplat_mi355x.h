@@ -311,7 +311,13 @@ int gsplat_rasterize_backward_chunked(
  * chunk > 0 (gsplat_rasterize_chunk_size) and a plan buffer of gsplat_rasterize_split_bytes, the
  * blend's waves also fill the plan's walk table (each wave's largest final index), so the list-
  * split backward given that plan and plan_filled = 1 skips the kernel that derives it from
- * final_idx.  chunk <= 0: no plan (may be NULL).  Outputs equal gsplat_rasterize_forward's. */
+ * final_idx.  Below 3,584 tiles the plan also carries the list-split forward (parts of chunk
+ * positions blended in their own waves and combined in list order): final_idx equals
+ * gsplat_rasterize_forward's bit for bit, final_T and the image within fp32 rounding of the
+ * regrouped transmittance product.  chunk < 0: that split forward alone with parts of -chunk
+ * positions (a render with no backward: no walk table), plan of
+ * gsplat_rasterize_split_bytes(.., -chunk).  chunk == 0: no plan (may be NULL); outputs equal
+ * gsplat_rasterize_forward's. */
 int gsplat_rasterize_forward_clearing(
     int tile_bounds_x, int tile_bounds_y, int img_height, int img_width,
     const int32_t *gaussian_ids_sorted, const int32_t *tile_bins, const float *xys,

@@ -137,3 +137,26 @@ def test_split_forward_training_step(gpu):
         assert scale > 0, name
         d = np.abs(a - b)
         assert (d <= 1e-5 * scale + 1e-4 * np.abs(b)).all(), (name, float(d.max()), scale)
+
+
+def test_split_forward_without_backward(gpu):
+    """A render with no backward (torch.no_grad: the c2 forward-only bench) takes the split
+    forward alone (negative chunk: no walk table, no backward plan): image and alpha within the
+    bar of the unsplit render, the mode-2 exact walks bit-identical."""
+    from gaussctrl_exp_amd.fused import render_fused
+    sc = synthetic_scene(100000, 0, seed=13, scale_lo=0.004, scale_hi=0.05).to(gpu)
+    cam = synthetic_camera(512, 512).to(gpu)
+    bg = torch.tensor([0.0, 0.0, 0.0], device=gpu)
+    outs = {}
+    for mode in (0, 1, 2):
+        prev = _lib.query("gsplat_debug_forward_split", mode)
+        try:
+            with torch.no_grad():
+                r = render_fused(sc, cam, 0, bg, return_alpha=True)
+            outs[mode] = (r["rgb"].cpu().numpy(), r["accumulation"].cpu().numpy())
+        finally:
+            _lib.query("gsplat_debug_forward_split", prev)
+    for k, name in enumerate(("rgb", "alpha")):
+        ref, got = outs[0][k].astype(np.float64), outs[1][k]
+        assert (np.abs(got - ref) <= 1e-5 + 1e-4 * np.abs(ref)).all(), name
+        np.testing.assert_array_equal(outs[2][k], outs[0][k], err_msg=name)
