@@ -89,6 +89,7 @@ SIGNATURES = {
                                                [_I] * 4 + [_F] + [_P] * 8 + [_SZ, _P]),
     "gsplat_bin_count_keyed": (_I, [_I, _I, _I, _P, _P, _SZ, _P]),
     "gsplat_bin_count_keyed_ex": (_I, [_I, _I, _I, _P, _P, _SZ, _c.c_uint32, _P]),
+    "gsplat_bin_rescan": (_I, [_I, _P, _SZ, _P]),
     "gsplat_bin_speculative": (_I, [_I, _I64, _I, _I, _P, _P, _SZ, _c.c_uint32, _P, _P, _P, _SZ,
                                     _P]),
     "gsplat_fused_preprocess_backward": (_I, [_I, _I, _I] + [_P] * 6 + [_F] * 4 + [_I, _I] +
@@ -141,8 +142,9 @@ def lib():
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             # (an older build loaded for a same-box A/B run, GSPLAT_MI355X_LIB, may lack a
-            # newer debug switch; every product entry must be there)
-            if name.startswith("gsplat_debug_") and not hasattr(L, name):
+            # newer entry; the shipped library must have every one)
+            if not hasattr(L, name) and (name.startswith("gsplat_debug_") or
+                                         os.environ.get("GSPLAT_MI355X_LIB")):
                 continue
             fn = getattr(L, name)
             fn.restype = res

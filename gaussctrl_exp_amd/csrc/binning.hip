@@ -2570,6 +2570,32 @@ static int bin_emit_impl(int num_points, int64_t num_intersects, int64_t capacit
   return check_launch("bin_emit");
 }
 
+// After a capacity overflow of gsplat_bin_speculative (which scans the allotments inside its
+// emission and leaves the offsets unwritten): the allotment scan into workspace1's offsets,
+// from the per-block sums its count phase left there, so gsplat_bin_emit can run for the exact
+// I (rasterize.SpeculativeBinning.rebin).  Sorted scheme only (the bucket scheme needs none).
+extern "C" int gsplat_bin_rescan(int num_points, void *workspace1, size_t workspace1_bytes,
+                                 void *stream) {
+  if (num_points < 0) {
+    set_error("bin_rescan: bad N=%d", num_points);
+    return 1;
+  }
+  Phase1 p = carve_phase1(workspace1, num_points);
+  if (workspace1_bytes < p.bytes) {
+    set_error("bin_rescan: workspace %zu < %zu bytes", workspace1_bytes, p.bytes);
+    return 1;
+  }
+  if (num_points == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  const int nb = (int)cdiv(num_points, SC_TILE);
+  uint32_t *partial = rts_tile_counts(p.rs_ws);  // box_counts / gather_counts' block sums
+  hipLaunchKernelGGL(scan_partials_kernel, dim3(1), dim3(1024), 0, st, partial, nb,
+                     (uint32_t *)nullptr, p.dcount);
+  hipLaunchKernelGGL(scan_downsweep_kernel, dim3(nb), dim3(TPB), 0, st, p.cnt,
+                     (long long)num_points, partial, p.off);
+  return check_launch("bin_rescan");
+}
+
 extern "C" int gsplat_bin_emit(int num_points, int64_t num_intersects, int tile_bounds_x,
                                int tile_bounds_y, int32_t *gaussian_ids_sorted,
                                int32_t *tile_bins, const void *workspace1,

@@ -246,6 +246,10 @@ int gsplat_bin_speculative(int num_points, int64_t capacity, int tile_bounds_x, 
                            int32_t *d_counts, void *workspace1, size_t workspace1_bytes,
                            uint32_t assume_const, int32_t *gaussian_ids_sorted, int32_t *tile_bins,
                            void *workspace2, size_t workspace2_bytes, void *stream);
+/* After gsplat_bin_speculative overflowed its capacity (returned 0, I > capacity): the
+ * allotment scan it folded into its emission, written to workspace1, so that gsplat_bin_emit
+ * can then bin the exact I from the same workspace1. */
+int gsplat_bin_rescan(int num_points, void *workspace1, size_t workspace1_bytes, void *stream);
 int gsplat_bin_emit_speculative(int num_points, int64_t capacity, int tile_bounds_x,
                                 int tile_bounds_y, int32_t *gaussian_ids_sorted,
                                 int32_t *tile_bins, const void *workspace1,
