@@ -1092,23 +1092,36 @@ __global__ __launch_bounds__(256) void raster_fwd_part_kernel(
     unsigned long long kmask;
     const int n = fwd_stage_batch(b, hi, gids, xys, conics, colors, opacity, R, stage, kmask);
     if (kbits && lane == 0) kbits[kb_base + ((b - range.x) >> 6)] = kmask;
-    for (int t = 0; t < n; ++t) {
-      const GStage G = stage_at(stage, t);
-      const float dx = G.x - px;
-      const float sg = gs_sigma(G.hc, G.b * dx, G.ha * dx * dx, G.y - py);
-      const float al = fminf(0.999f, G.o * gs_vis(sg));
-      const bool v = !done && sg >= 0.f && al >= ALPHA_MIN;
-      const float nT = T * (1.f - al);
-      const bool term = v && nT <= 1e-4f, comp = v && !term;
-      done = done || term;
-      lterm = lterm || term;
-      const float w = comp ? al * T : 0.f;
-      cr += G.r * w;
-      cg += G.g * w;
-      cb += G.bl * w;
-      T = comp ? nT : T;
-      cur = comp ? G.idx : cur;
-      nfac += comp ? 1.f : 0.f;
+    // two staged Gaussians per iteration, as raster_fwd3u_kernel: both sigma / exp / alpha
+    // chains independent, the transmittance update in list order
+    for (int t = 0; t < n; t += 2) {
+      GStage G[2];
+      G[0] = stage_at(stage, t);
+      G[1] = stage_at(stage, min(t + 1, 63));
+      const bool live1 = t + 1 < n;
+      if (!live1) G[1].r = G[1].g = G[1].bl = 0.f;  // stale slot: keep 0 * x finite
+      float sg[2], al[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const float dx = G[u].x - px;
+        sg[u] = gs_sigma(G[u].hc, G[u].b * dx, G[u].ha * dx * dx, G[u].y - py);
+        al[u] = fminf(0.999f, G[u].o * gs_vis(sg[u]));
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const bool v = !done && (u == 0 || live1) && sg[u] >= 0.f && al[u] >= ALPHA_MIN;
+        const float nT = T * (1.f - al[u]);
+        const bool term = v && nT <= 1e-4f, comp = v && !term;
+        done = done || term;
+        lterm = lterm || term;
+        const float w = comp ? al[u] * T : 0.f;
+        cr += G[u].r * w;
+        cg += G[u].g * w;
+        cb += G[u].bl * w;
+        T = comp ? nT : T;
+        cur = comp ? G[u].idx : cur;
+        nfac += comp ? 1.f : 0.f;
+      }
       if (__all(done)) break;
     }
     wave_lds_sync();

@@ -5,6 +5,7 @@
 #   CFGS="headline c3" AB="base:VAR=1 new:VAR=2,VAR2=3" REPS=2
 #                                      bench lines per config x env setting x repetition
 #                                      (STEPS, TRAIN_STEPS), one summary line each in the log
+#   GLOO2=1 (GLOO2_CFG)               bench.py at --gpus 2 over gloo, both ranks on the one GPU
 #   TIMELINE="headline c3"            rocprofv3 kernel trace -> per-step launch timeline
 # Output under gpurun_out/$ROUND/ (default "iter"): iter.log, b_<cfg>_<name>_<rep>.json,
 # timeline_<cfg>.txt.
@@ -36,6 +37,14 @@ PY
   done
 done
 done
+if [ -n "$GLOO2" ]; then
+  # the N > 1 bench path rehearsed on one GPU: two ranks, gloo carrying the collectives
+  BENCH_DIST_BACKEND=gloo timeout -k 10 600 python3 -m torch.distributed.run --nnodes=1 \
+    --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 \
+    --config ${GLOO2_CFG:-headline} --steps 10 --warmup 3 --no-cpu-baseline --no-lane-occupancy \
+    --train-steps 2 > $O/gloo2_${GLOO2_CFG:-headline}.json 2>> $L || exit $?
+  tail -n 1 $O/gloo2_${GLOO2_CFG:-headline}.json >> $L
+fi
 if [ -n "$TIMELINE" ]; then
   for c in $TIMELINE; do
     timeout -k 10 240 rocprofv3 --kernel-trace -d gpurun_out/tl_$c -o run -- python3 bench.py --config $c --steps 6 --warmup 3 --no-cpu-baseline --no-lane-occupancy --train-steps 0 > $O/tl_bench_$c.log 2>&1 || exit $?
