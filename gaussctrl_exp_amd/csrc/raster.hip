@@ -2194,8 +2194,19 @@ struct SplitWs {
   int *fbase;
   float *fprec;
   unsigned long long *ftmask;
+  int fchunk;               // the split forward's part length (fwd_chunk_of(chunk))
+  long long fitems_bound;   // its parts' bound, T + ceil(I / fchunk)
+  int2 *fitems;             // its parts in dispatch order (fwd_plan_kernel)
+  int *n_fitems;
   size_t bytes;
 };
+// The split forward's part length from the plan's chunk: chunk / g_fwd_chunk_div, rounded up
+// to 64 (gsplat_debug_forward_chunk_div; 1 = the backward's chunk).
+int g_fwd_chunk_div = 1;
+static int fwd_chunk_of(int chunk) {
+  const int c = chunk / (g_fwd_chunk_div > 0 ? g_fwd_chunk_div : 1);
+  return std::max(64, (c + 63) / 64 * 64);
+}
 static SplitWs carve_split_ws(void *base, long long T, long long I, int chunk) {
   SplitWs w{};
   w.items_bound = T + (I + chunk - 1) / chunk;
@@ -2211,10 +2222,14 @@ static SplitWs carve_split_ws(void *base, long long T, long long I, int chunk) {
   w.kbw = I / 64 + T + 2;
   w.kbits = (unsigned long long *)take((size_t)SPLIT_WAVES * w.kbw * sizeof(unsigned long long));
   if (T < FWD_SPLIT_MAX_TILES) {
+    w.fchunk = fwd_chunk_of(chunk);
+    w.fitems_bound = T + (I + w.fchunk - 1) / w.fchunk;
     w.fbase = (int *)take((size_t)(T + 1) * sizeof(int));
-    w.fprec = (float *)take((size_t)w.items_bound * SPLIT_WAVES * FPR * 64 * sizeof(float));
-    w.ftmask = (unsigned long long *)take((size_t)w.items_bound * SPLIT_WAVES *
+    w.fprec = (float *)take((size_t)w.fitems_bound * SPLIT_WAVES * FPR * 64 * sizeof(float));
+    w.ftmask = (unsigned long long *)take((size_t)w.fitems_bound * SPLIT_WAVES *
                                           sizeof(unsigned long long));
+    w.fitems = (int2 *)take((size_t)w.fitems_bound * sizeof(int2));
+    w.n_fitems = (int *)take(sizeof(int));
   }
   w.bytes = off;
   return w;
@@ -2280,6 +2295,13 @@ extern "C" int gsplat_debug_set_chunk(int chunk) {
 // its records there): -1 / 1 on (the default), 0 off, 2 on with every pixel of a split tile
 // resolved by the exact sequential walk (tests: then bit-identical to the unsplit forward).
 // Returns the previous setting.
+// The split forward's part length as the plan's chunk / div (rounded up to 64; 1 the default).
+extern "C" int gsplat_debug_forward_chunk_div(int div) {
+  const int prev = g_fwd_chunk_div;
+  if (div >= 1 && div <= 64) g_fwd_chunk_div = div;
+  return prev;
+}
+
 extern "C" int gsplat_debug_forward_split(int mode) {
   const int prev = g_fwd_split;
   if (mode >= -1 && mode <= 2) g_fwd_split = mode;
@@ -2647,18 +2669,18 @@ static int forward_clearing_impl(
   const long long Tt = (long long)tile_bounds_x * tile_bounds_y;
   if (fchunk > 0 && forward_split_on(Tt) && !g_pair_count_on && default_variants()) {
     // the list-split forward: plan, parts, combine (see fwd_plan_kernel)
-    const int chunk = fchunk;
-    const SplitWs w = carve_split_ws(plan, Tt, num_intersects, chunk);
+    const SplitWs w = carve_split_ws(plan, Tt, num_intersects, fchunk);
+    const int chunk = w.fchunk;
     hipStream_t st = (hipStream_t)stream;
     hipLaunchKernelGGL(fwd_plan_kernel, dim3(1), dim3(1024), 0, st, (int)Tt, chunk,
-                       (const int2 *)tile_bins, w.items, w.n_items, w.fbase, w.ftmask);
-    hipLaunchKernelGGL(raster_fwd_part_kernel<false>, dim3((unsigned)w.items_bound), dim3(256), 0,
+                       (const int2 *)tile_bins, w.fitems, w.n_fitems, w.fbase, w.ftmask);
+    hipLaunchKernelGGL(raster_fwd_part_kernel<false>, dim3((unsigned)w.fitems_bound), dim3(256), 0,
                        st, tile_bounds_x, tile_bounds_y, img_height, img_width,
                        gaussian_ids_sorted, (const int2 *)tile_bins, (const float2 *)xys, conics,
                        colors, opacity, background, out_img, final_Ts, final_idx,
                        (float4 *)clear, (long long)(clear_bytes / 16), clear_radii, tile_last,
-                       kbits, kbw, l1_gt, l1_part, l1_clamp, chunk, (const int2 *)w.items,
-                       (const int *)w.n_items, (const int *)w.fbase, w.fprec, w.ftmask);
+                       kbits, kbw, l1_gt, l1_part, l1_clamp, chunk, (const int2 *)w.fitems,
+                       (const int *)w.n_fitems, (const int *)w.fbase, w.fprec, w.ftmask);
     hipLaunchKernelGGL(raster_fwd_combine_kernel, dim3((unsigned)Tt), dim3(256), 0, st,
                        tile_bounds_x, tile_bounds_y, img_height, img_width, gaussian_ids_sorted,
                        (const int2 *)tile_bins, (const float2 *)xys, conics, colors, opacity,

@@ -337,6 +337,10 @@ int gsplat_debug_set_chunk(int chunk);
  * the exact sequential walk (bit-identical to the unsplit forward; tests).  Returns the
  * previous setting. */
 int gsplat_debug_forward_split(int mode);
+/* The split forward's part length: the plan's chunk / div, rounded up to 64 (div 1..64; 1 the
+ * default).  Returns the previous div.  Plans must be sized after setting it
+ * (gsplat_rasterize_split_bytes). */
+int gsplat_debug_forward_chunk_div(int div);
 
 size_t gsplat_rasterize_backward_workspace_size(int num_points, int channels);
 int gsplat_rasterize_backward(int tile_bounds_x, int tile_bounds_y, int img_height,

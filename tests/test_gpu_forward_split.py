@@ -160,3 +160,22 @@ def test_split_forward_without_backward(gpu):
         ref, got = outs[0][k].astype(np.float64), outs[1][k]
         assert (np.abs(got - ref) <= 1e-5 + 1e-4 * np.abs(ref)).all(), name
         np.testing.assert_array_equal(outs[2][k], outs[0][k], err_msg=name)
+
+
+@pytest.mark.parametrize("div", [2, 4])
+def test_split_forward_shorter_parts(gpu, div):
+    """Parts shorter than the plan's chunk (gsplat_debug_forward_chunk_div): the forward's own
+    part bound and records, same guarantees."""
+    s = _state(gpu, 30000, 512, 512, 3)
+    prev = _lib.query("gsplat_debug_forward_chunk_div", div)
+    try:
+        ref = _forward(gpu, s, 256, 0)
+        got = _forward(gpu, s, 256, 1)
+        exact = _forward(gpu, s, 256, 2)
+    finally:
+        _lib.query("gsplat_debug_forward_chunk_div", prev)
+    np.testing.assert_array_equal(got[2], ref[2], err_msg="final_idx")
+    dI = np.abs(got[0].astype(np.float64) - ref[0])
+    assert (dI <= 1e-5 + 1e-4 * np.abs(ref[0])).all(), float(dI.max())
+    for name, a, b in zip(("img", "final_T", "final_idx", "tile_last"), exact, ref):
+        np.testing.assert_array_equal(a, b, err_msg=name)
