@@ -184,6 +184,13 @@ def call(name: str, *args) -> int:
     return rc
 
 
+def call_status(name: str, *args) -> int:
+    """Call an entry point whose non-zero statuses include expected outcomes (e.g.
+    gsplat_bin_speculative's 2 = "needs I on the host"): the status is returned, not raised.
+    (A separate function from call() so bench.py's per-entry timing sees it too.)"""
+    return int(getattr(lib(), name)(*args))
+
+
 def query(name: str, *args) -> int:
     """Call a size query (`*_workspace_size`)."""
     return int(getattr(lib(), name)(*args))

@@ -285,9 +285,9 @@ def bin_gaussians_speculative(xys: Tensor, depths: Tensor, radii: Tensor, num_ti
     slot, counts, host = _COUNTS.acquire(dev)
     try:
         # count phase, emission (with the allotment scan) and tile sort in one call
-        rc = _lib.lib().gsplat_bin_speculative(n, cap, tbx, tby, P(counts), P(ws1), ws1.numel(),
-                                               _assumed_constant(key), P(ids_buf), P(tile_bins),
-                                               P(ws2), ws2.numel(), st)
+        rc = _lib.call_status("gsplat_bin_speculative", n, cap, tbx, tby, P(counts), P(ws1),
+                              ws1.numel(), _assumed_constant(key), P(ids_buf), P(tile_bins),
+                              P(ws2), ws2.numel(), st)
         if rc == 2:  # the scheme needs I on the host: count, then finish as bin_gaussians does
             _lib.call("gsplat_bin_count_keyed_ex", n, tbx, tby, P(counts), P(ws1), ws1.numel(),
                       _assumed_constant(key), st)

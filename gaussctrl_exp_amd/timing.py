@@ -14,17 +14,18 @@ import torch
 from . import _lib
 
 _orig_call = _lib.call
+_orig_call_status = _lib.call_status
 
 
 class CallTimer:
     def __init__(self):
         self.events = collections.defaultdict(list)
 
-    def _call(self, name, *args):
+    def _call(self, name, *args, _fn=None):
         s = torch.cuda.Event(enable_timing=True)
         e = torch.cuda.Event(enable_timing=True)
         s.record()
-        rc = _orig_call(name, *args)
+        rc = (_fn or _orig_call)(name, *args)
         e.record()
         # the list-split variants are the same entry (gsplat_rasterize_forward/_backward)
         key = name[:-len("_chunked")] if name.endswith("_chunked") else name
@@ -45,7 +46,9 @@ class CallTimer:
 def timed_calls():
     t = CallTimer()
     _lib.call = t._call
+    _lib.call_status = lambda name, *a: t._call(name, *a, _fn=_orig_call_status)
     try:
         yield t
     finally:
         _lib.call = _orig_call
+        _lib.call_status = _orig_call_status
