@@ -943,7 +943,7 @@ __global__ __launch_bounds__(TPB) void gather_counts_kernel(int n, const uint32_
     for (int k = 0; k < SC_ITEMS; ++k)
       ord[k] = order[min(base + k * TPB + threadIdx.x, nv - 1)];
 #pragma unroll
-    for (int k = 0; k < SC_ITEMS; ++k) q[k] = rec[ord[k]];
+    for (int k = 0; k < SC_ITEMS; ++k) q[k] = rec[min(ord[k], (uint32_t)n - 1u)];  // (see box_counts)
 #pragma unroll
     for (int k = 0; k < SC_ITEMS; ++k) {
       const long long p = base + k * TPB + threadIdx.x;
@@ -996,7 +996,9 @@ __global__ __launch_bounds__(TPB) void box_counts_kernel(int n, const uint32_t *
       uint32_t c = 0u;
       if (p < nv) {
         if (b[k].x == BOX_GATHER) {  // an inconsistent allotment (see os_pass_kernel's PL)
-          const uint4 r = rec[order[p]];
+          // (clamped: after a depth-key range violation the order is garbage; the caller
+          // discards that binning, but no read may leave the records)
+          const uint4 r = rec[min(order[p], (uint32_t)n - 1u)];
           box[p] = make_uint2(r.y, r.z);
           c = r.x;
         } else {
@@ -1108,7 +1110,9 @@ __global__ __launch_bounds__(TPB) void emit_scan_kernel(int n, int nb,
                                                         uint32_t *__restrict__ tvals,
                                                         int *__restrict__ tile_bins,
                                                         uint32_t *__restrict__ i_dev,
-                                                        int32_t *__restrict__ i_host, uint32_t cap) {
+                                                        int32_t *__restrict__ i_host, uint32_t cap,
+                                                        const uint32_t *__restrict__ kfin = nullptr,
+                                                        uint32_t assume = 0u) {
   __shared__ uint32_t lds[TPB / 64];
   for (long long i = (long long)blockIdx.x * TPB + threadIdx.x; i < 2LL * tbx * tby;
        i += (long long)gridDim.x * TPB)
@@ -1131,11 +1135,15 @@ __global__ __launch_bounds__(TPB) void emit_scan_kernel(int n, int nb,
   uint32_t bpre, btot;
   block_exclusive_scan<TPB>(pre, bpre, lds);  // (only the totals are used)
   block_exclusive_scan<TPB>(tot, btot, lds);
+  // a depth-key digit the sort assumed constant varied (KeyRange): the depth order, and with
+  // it every id and box, is wrong -- treated as an overflow, so nothing is emitted or sorted
+  // and the blend behind reads an empty table (the host sees the violation and starts over)
+  const bool violated = assume && (((kfin[0] ^ kfin[1]) & assume) != 0u);
   if (blockIdx.x == 0 && tid == 0) {
-    *i_dev = btot;
+    *i_dev = violated ? 0xFFFFFFFFu : btot;
     if (i_host) *i_host = (int32_t)btot;
   }
-  if (btot > cap) return;  // workgroup-uniform
+  if (violated || btot > cap) return;  // workgroup-uniform
   uint32_t run = bpre;
 #pragma unroll
   for (int r = 0; r < SC_ITEMS; ++r) {
@@ -2434,7 +2442,8 @@ extern "C" int gsplat_bin_speculative(int num_points, int64_t capacity, int tile
   const int nb = (int)cdiv(n, SC_TILE);
   hipLaunchKernelGGL(emit_scan_kernel, dim3(nb), dim3(TPB), 0, st, n, nb, p1.order, p1.cnt,
                      rts_tile_counts(p1.rs_ws), p1.box, tile_bounds_x, tile_bounds_y, p2.tk_a,
-                     p2.tv_a, tile_bins, p1.dcount, d_counts + 1, (uint32_t)capacity);
+                     p2.tv_a, tile_bins, p1.dcount, d_counts + 1, (uint32_t)capacity,
+                     sort_kept_word(p1.rs_ws) + 1, use_key_range(n) ? assume_const : 0u);
   radix_sort_pairs<uint32_t>(p2.tk_a, p2.tv_a, p2.tk_b, p2.tv_b, nullptr,
                              (uint32_t *)gaussian_ids_sorted, capacity, 0, bits_for(T), p2.rs_ws,
                              st, false, tile_bins, T, false, 0, p1.dcount);

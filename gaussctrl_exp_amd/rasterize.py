@@ -242,7 +242,8 @@ class SpeculativeBinning:
         finally:
             _COUNTS.release(self.dev, self.slot, visible)
         self.num_intersects = I
-        _EMIT_CAP[self.key] = emit_capacity(I)
+        if not self.range_violated:  # (a violated sort's I is meaningless: the caller re-bins)
+            _EMIT_CAP[self.key] = emit_capacity(I)
         return I <= self.cap and not self.range_violated
 
     def rebin(self):
@@ -361,7 +362,7 @@ def emit_capacity(num_intersects: int) -> int:
     """The next call's pre-launch capacity after a call with `num_intersects`: 1/8 headroom,
     clamped to what gsplat_bin_emit_prelaunch accepts (an unclamped I + I/8 above
     the C limit made every later call of that frame shape fail)."""
-    return min(num_intersects + (num_intersects >> 3), EMIT_CAP_MAX)
+    return max(0, min(num_intersects + (num_intersects >> 3), EMIT_CAP_MAX))
 # launch the emission's first part before the host reads I (False: after it; A/B runs only)
 PRELAUNCH_EMISSION = True
 
