@@ -90,7 +90,7 @@ SIGNATURES = {
                                                [_I] * 4 + [_F] + [_P] * 8 + [_SZ, _P]),
     "gsplat_bin_count_keyed": (_I, [_I, _I, _I, _P, _P, _SZ, _P]),
     "gsplat_bin_count_keyed_ex": (_I, [_I, _I, _I, _P, _P, _SZ, _c.c_uint32, _P]),
-    "gsplat_bin_rescan": (_I, [_I, _P, _SZ, _P]),
+    "gsplat_bin_rescan": (_I, [_I, _I, _I, _P, _SZ, _P]),
     "gsplat_bin_speculative": (_I, [_I, _I64, _I, _I, _P, _P, _SZ, _c.c_uint32, _P, _P, _P, _SZ,
                                     _P]),
     "gsplat_fused_preprocess_backward": (_I, [_I, _I, _I] + [_P] * 6 + [_F] * 4 + [_I, _I] +

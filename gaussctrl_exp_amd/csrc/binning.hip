@@ -1378,7 +1378,9 @@ __global__ __launch_bounds__(BK_NT) void bk_scan_kernel(int nbk, int nwg, uint32
                                                         uint32_t *__restrict__ tot,
                                                         uint32_t *__restrict__ start,
                                                         uint32_t *__restrict__ ctr, int T,
-                                                        int *__restrict__ tile_bins) {
+                                                        int *__restrict__ tile_bins,
+                                                        const uint32_t *__restrict__ i_dev = nullptr,
+                                                        uint32_t cap = 0) {
   constexpr int NW = BK_NT / 64;
   __shared__ uint32_t seg[NW][64];
   __shared__ uint32_t lds[NW];
@@ -1437,6 +1439,10 @@ __global__ __launch_bounds__(BK_NT) void bk_scan_kernel(int nbk, int nwg, uint32
   }
   __syncthreads();
   if (!last) return;
+  if (i_dev && *i_dev > cap) {  // capacity-launched (EMIT_SPEC) and overflowed: an empty table
+    for (int i = threadIdx.x; i < 2 * T; i += BK_NT) tile_bins[i] = 0;
+    return;
+  }
   uint32_t running = 0;
   for (int c0 = 0; c0 < nbk; c0 += BK_NT) {
     const int i = c0 + threadIdx.x;
@@ -1912,8 +1918,11 @@ __global__ __launch_bounds__(NT) void bk_msd_kernel(int nbk, const uint32_t *__r
                                                     const uint32_t *__restrict__ ids,
                                                     const uint32_t *__restrict__ dkeys,
                                                     uint32_t *__restrict__ out,
-                                                    uint32_t *__restrict__ fail) {
+                                                    uint32_t *__restrict__ fail,
+                                                    const uint32_t *__restrict__ i_dev = nullptr,
+                                                    uint32_t cap = 0) {
   __shared__ BsSmem<NT, 0> sm;
+  if (i_dev && *i_dev > cap) return;  // capacity overflow (EMIT_SPEC): nothing was placed
   const int b = blockIdx.x;
   const uint32_t s0 = start[b], L = tot[b];
   bool ok = true;
@@ -1939,11 +1948,14 @@ __global__ __launch_bounds__(NT) void bk_sort_kernel(int nbk, uint32_t lo, uint3
                                                      const uint32_t *__restrict__ dkeys,
                                                      uint32_t *__restrict__ out, uint32_t *ka,
                                                      uint32_t *va, uint32_t *kb, uint32_t *vb,
-                                                     const uint32_t *__restrict__ fail) {
+                                                     const uint32_t *__restrict__ fail,
+                                                     const uint32_t *__restrict__ i_dev = nullptr,
+                                                     uint32_t cap = 0) {
   constexpr int CAP = NT * ITEMS;
   __shared__ BsSmem<NT, ITEMS> sm;
   const int b = blockIdx.x;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  if (i_dev && *i_dev > cap) return;  // capacity overflow (EMIT_SPEC)
   if (fail && !fail[b]) return;  // sorted by bk_msd_kernel
   const uint32_t s0 = start[b], L = tot[b];
   if (L < lo || L > hi || L == 0) return;
@@ -2413,6 +2425,12 @@ extern "C" int gsplat_bin_count_keyed_ex(int num_points, int tile_bounds_x, int 
 // assumption, gather_counts), emit_scan_kernel (the allotment scan folded into the emission, I
 // published from the device) and the capacity-launched tile sort.  2 = the scheme needs I on
 // the host (nothing launched).
+enum { EMIT_HEAD = 1, EMIT_TAIL = 2, EMIT_ALL = 3, EMIT_SPEC = 4 };
+static int bin_emit_impl(int num_points, int64_t num_intersects, int64_t capacity,
+                         int tile_bounds_x, int tile_bounds_y, int32_t *gaussian_ids_sorted,
+                         int32_t *tile_bins, const void *workspace1, size_t workspace1_bytes,
+                         void *workspace2, size_t workspace2_bytes, void *stream, int phase);
+
 extern "C" int gsplat_bin_speculative(int num_points, int64_t capacity, int tile_bounds_x,
                                       int tile_bounds_y, int32_t *d_counts, void *workspace1,
                                       size_t workspace1_bytes, uint32_t assume_const,
@@ -2426,7 +2444,17 @@ extern "C" int gsplat_bin_speculative(int num_points, int64_t capacity, int tile
               (long long)capacity, tile_bounds_x, tile_bounds_y);
     return 1;
   }
-  if (use_bucket(num_points, T) || use_emit_pass0(capacity)) return 2;
+  if (use_emit_pass0(capacity)) return 2;
+  if (use_bucket(num_points, T)) {
+    // tile buckets: the count phase (I on the device), then every bucket launch at the
+    // capacity, each returning at once on an overflow (the table cleared by bk_scan_kernel)
+    if (bin_count_impl(num_points, nullptr, nullptr, nullptr, nullptr, tile_bounds_x,
+                       tile_bounds_y, d_counts, workspace1, workspace1_bytes, true, stream))
+      return 1;
+    return bin_emit_impl(num_points, 0, capacity, tile_bounds_x, tile_bounds_y,
+                         gaussian_ids_sorted, tile_bins, workspace1, workspace1_bytes,
+                         workspace2, workspace2_bytes, stream, EMIT_SPEC);
+  }
   Phase1 p1 = carve_phase1(workspace1, num_points);
   Phase2 p2 = carve_phase2(workspace2, capacity);
   if (workspace1_bytes < p1.bytes || workspace2_bytes < p2.bytes) {
@@ -2455,7 +2483,7 @@ extern "C" int gsplat_bin_speculative(int num_points, int64_t capacity, int tile
 // unless the generated first pass is chosen; bucket scheme: count, scan and placement), each
 // checking the device copy of I against cap; TAIL = the rest (the tile sort / the per-tile
 // sorts).  EMIT_ALL = both, with cap = I (gsplat_bin_emit).
-enum { EMIT_HEAD = 1, EMIT_TAIL = 2, EMIT_ALL = 3, EMIT_SPEC = 4 };
+// (EMIT_* : declared with gsplat_bin_speculative, above)
 
 static bool emit_head_splits(int n, long long cap, long long T) {
   if (use_bucket(n, T)) return true;
@@ -2479,7 +2507,8 @@ static int bin_emit_impl(int num_points, int64_t num_intersects, int64_t capacit
   const long long cap = capacity;
   // the head's launches run here unless they were pre-launched for this capacity
   const bool split = phase != EMIT_ALL && emit_head_splits(num_points, cap, T);
-  const bool head = phase == EMIT_ALL || (phase == EMIT_HEAD && split) || (phase == EMIT_TAIL && !split);
+  const bool head = phase == EMIT_ALL || phase == EMIT_SPEC || (phase == EMIT_HEAD && split) ||
+                    (phase == EMIT_TAIL && !split);
   const bool tail = phase != EMIT_HEAD;
   const uint32_t *idev = phase == EMIT_HEAD ? p1.dcount : nullptr;  // bound check when pre-launched
   if (use_bucket(num_points, T)) {
@@ -2490,17 +2519,20 @@ static int bin_emit_impl(int num_points, int64_t num_intersects, int64_t capacit
                 p1.bytes, w.bytes);
       return 1;
     }
-    if (num_points == 0 || (phase != EMIT_HEAD && num_intersects == 0)) {
+    if (num_points == 0 || (phase != EMIT_HEAD && phase != EMIT_SPEC && num_intersects == 0)) {
       if (tail)
         note(hipMemsetAsync(tile_bins, 0, (size_t)T * 2 * sizeof(int32_t), st), "hipMemsetAsync");
       return check_launch("bin_emit");
     }
     const int n = num_points;
+    // EMIT_SPEC (gsplat_bin_speculative): every launch at the capacity, I read on the device
+    const uint32_t *sdev = phase == EMIT_SPEC ? p1.dcount : nullptr;
+    if (phase == EMIT_SPEC) idev = p1.dcount;
     if (head) {
       hipLaunchKernelGGL(bk_count_kernel, dim3(w.nwg), dim3(BK_NT), 0, st, n, p1.rec, tile_bounds_x,
                          tile_bounds_y, w.nbk, w.M, w.ctr);
       hipLaunchKernelGGL(bk_scan_kernel, dim3(cdiv(w.nbk, 64)), dim3(BK_NT), 0, st, w.nbk, w.nwg,
-                         w.M, w.tot, w.start, w.ctr, (int)T, tile_bins);
+                         w.M, w.tot, w.start, w.ctr, (int)T, tile_bins, sdev, (uint32_t)cap);
       hipLaunchKernelGGL(bk_place_kernel, dim3(w.nwg), dim3(BK_NT), 0, st, n, p1.rec,
                          tile_bounds_x, tile_bounds_y, w.nbk, w.M, w.start, w.ids, idev,
                          (uint32_t)cap);
@@ -2510,13 +2542,16 @@ static int bin_emit_impl(int num_points, int64_t num_intersects, int64_t capacit
     // 4,096: 256 threads; longer: 1,024 threads, in LDS up to 14,336, then through the
     // ping-pong buffers)
     hipLaunchKernelGGL((bk_msd_kernel<TPB, 16>), dim3(w.nbk), dim3(TPB), 0, st, w.nbk, w.start,
-                       w.tot, w.ids, p1.dkeys_a, (uint32_t *)gaussian_ids_sorted, w.fail);
+                       w.tot, w.ids, p1.dkeys_a, (uint32_t *)gaussian_ids_sorted, w.fail, sdev,
+                       (uint32_t)cap);
     hipLaunchKernelGGL((bk_sort_kernel<TPB, 16>), dim3(w.nbk), dim3(TPB), 0, st, w.nbk, 0u,
                        (uint32_t)(TPB * 16), w.start, w.tot, w.ids, p1.dkeys_a,
-                       (uint32_t *)gaussian_ids_sorted, w.ka, w.va, w.kb, w.vb, w.fail);
+                       (uint32_t *)gaussian_ids_sorted, w.ka, w.va, w.kb, w.vb, w.fail, sdev,
+                       (uint32_t)cap);
     hipLaunchKernelGGL((bk_sort_kernel<1024, 14>), dim3(w.nbk), dim3(1024), 0, st, w.nbk,
                        (uint32_t)(TPB * 16 + 1), 0xFFFFFFFFu, w.start, w.tot, w.ids, p1.dkeys_a,
-                       (uint32_t *)gaussian_ids_sorted, w.ka, w.va, w.kb, w.vb, w.fail);
+                       (uint32_t *)gaussian_ids_sorted, w.ka, w.va, w.kb, w.vb, w.fail, sdev,
+                       (uint32_t)cap);
     return check_launch("bin_emit");
   }
   Phase2 p2 = carve_phase2(workspace2, cap);
@@ -2583,12 +2618,14 @@ static int bin_emit_impl(int num_points, int64_t num_intersects, int64_t capacit
 // emission and leaves the offsets unwritten): the allotment scan into workspace1's offsets,
 // from the per-block sums its count phase left there, so gsplat_bin_emit can run for the exact
 // I (rasterize.SpeculativeBinning.rebin).  Sorted scheme only (the bucket scheme needs none).
-extern "C" int gsplat_bin_rescan(int num_points, void *workspace1, size_t workspace1_bytes,
-                                 void *stream) {
-  if (num_points < 0) {
-    set_error("bin_rescan: bad N=%d", num_points);
+extern "C" int gsplat_bin_rescan(int num_points, int tile_bounds_x, int tile_bounds_y,
+                                 void *workspace1, size_t workspace1_bytes, void *stream) {
+  if (num_points < 0 || tile_bounds_x <= 0 || tile_bounds_y <= 0) {
+    set_error("bin_rescan: bad sizes (N=%d tiles=%dx%d)", num_points, tile_bounds_x,
+              tile_bounds_y);
     return 1;
   }
+  if (use_bucket(num_points, (long long)tile_bounds_x * tile_bounds_y)) return 0;  // (none)
   Phase1 p = carve_phase1(workspace1, num_points);
   if (workspace1_bytes < p.bytes) {
     set_error("bin_rescan: workspace %zu < %zu bytes", workspace1_bytes, p.bytes);

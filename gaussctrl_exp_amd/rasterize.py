@@ -254,7 +254,8 @@ class SpeculativeBinning:
         P, st = _lib.ptr, _lib.stream(self.dev)
         ids_buf, ws2 = _emit_buffers(self.dev, self.n, I, self.tbx, self.tby)
         if self.rescan:  # gsplat_bin_speculative scanned inside its emission: offsets first
-            _lib.call("gsplat_bin_rescan", self.n, P(self.ws1), self.ws1.numel(), st)
+            _lib.call("gsplat_bin_rescan", self.n, self.tbx, self.tby, P(self.ws1),
+                      self.ws1.numel(), st)
         _lib.call("gsplat_bin_emit", self.n, I, self.tbx, self.tby, P(ids_buf),
                   P(self.tile_bins), P(self.ws1), self.ws1.numel(), P(ws2), ws2.numel(), st)
         self.ids, self.ws2, self.cap = ids_buf, ws2, I

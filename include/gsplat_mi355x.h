@@ -240,8 +240,10 @@ int gsplat_bin_emit_finish(int num_points, int64_t num_intersects, int64_t capac
  * Replaces, like gsplat_bin_emit, gsplat 0.1.2.1 rasterize.py's map / sort / bin edges. */
 /* gsplat_bin_count_keyed_ex + gsplat_bin_emit_speculative in one call, two launches fewer: the
  * allotment scan is folded into the emission (the emission publishes I to d_counts[1] from the
- * device).  Same outputs, overflow and range-violation semantics and return code 2 as the two
- * calls; d_counts int32[4] as gsplat_bin_count_keyed_ex's. */
+ * device).  Same outputs and overflow / range-violation semantics as the two calls; also the
+ * small-scene tile buckets run capacity-launched here (each bucket kernel returns at once on an
+ * overflow, the table cleared), so it returns 2 only for the generated first tile pass
+ * (capacity >= 2^24).  d_counts int32[4] as gsplat_bin_count_keyed_ex's. */
 int gsplat_bin_speculative(int num_points, int64_t capacity, int tile_bounds_x, int tile_bounds_y,
                            int32_t *d_counts, void *workspace1, size_t workspace1_bytes,
                            uint32_t assume_const, int32_t *gaussian_ids_sorted, int32_t *tile_bins,
@@ -249,7 +251,8 @@ int gsplat_bin_speculative(int num_points, int64_t capacity, int tile_bounds_x, 
 /* After gsplat_bin_speculative overflowed its capacity (returned 0, I > capacity): the
  * allotment scan it folded into its emission, written to workspace1, so that gsplat_bin_emit
  * can then bin the exact I from the same workspace1. */
-int gsplat_bin_rescan(int num_points, void *workspace1, size_t workspace1_bytes, void *stream);
+int gsplat_bin_rescan(int num_points, int tile_bounds_x, int tile_bounds_y, void *workspace1,
+                      size_t workspace1_bytes, void *stream);
 int gsplat_bin_emit_speculative(int num_points, int64_t capacity, int tile_bounds_x,
                                 int tile_bounds_y, int32_t *gaussian_ids_sorted,
                                 int32_t *tile_bins, const void *workspace1,

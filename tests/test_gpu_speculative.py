@@ -6,8 +6,8 @@ the blend right behind them.  Checks:
   capacity a little above I (the steady state), far above it, and BELOW it (overflow: the
   table is left all-zero, nothing is written past the capacity, rebin() then gives the exact
   result);
-* scenes the sorted scheme handles and small ones whose scheme needs I on the host (the tile
-  buckets: the speculative call falls back to prelaunch + finish inside);
+* scenes the sorted scheme handles and small ones binned by tile buckets (also launched at the
+  capacity: each bucket kernel returns at once on an overflow and the table is cleared);
 * the fused render through it (second call of a frame shape) equals the first call's
   synchronous path: image, alpha and all six gradients bit-identical (deterministic mode), also
   when the capacity overflows and the render re-bins and re-blends.
