@@ -120,6 +120,9 @@ def algorithmic_bytes(N, I, P, T, K, nvis):
         "gsplat_compute_sh_forward": (24 + 12 * K) * N,
         "gsplat_bin_count": bin_count,
         "gsplat_bin_count_keyed": bin_count if bucket else bin_count - 44 * N,
+        "gsplat_bin_count_keyed_ex": bin_count if bucket else bin_count - 44 * N,
+        # count + emission + tile sort in one call (the speculative binning)
+        "gsplat_bin_speculative": (bin_count if bucket else bin_count - 44 * N) + bin_emit,
         "gsplat_bin_emit": bin_emit,
         # the emission split around the host's read of I (rasterize.bin_gaussians)
         "gsplat_bin_emit_prelaunch": emit_head,
@@ -136,6 +139,10 @@ def algorithmic_bytes(N, I, P, T, K, nvis):
         # its blend also zeroes the 48-B gradient record of every visible Gaussian
         "gsplat_rasterize_forward_clearing": 40 * I + 20 * P + 48 * nvis,
         "gsplat_rasterize_backward_records": 40 * I + 24 * P,
+        # the fused L1 loss (round 4): the forward also reads gt (12 P); the backward reads the
+        # image and gt (24 P) in place of v_out / v_alpha (16 P), + final T and index (8 P)
+        "gsplat_rasterize_forward_clearing_l1": 40 * I + 32 * P + 48 * nvis,
+        "gsplat_rasterize_backward_records_l1": 40 * I + 32 * P,
         # params + saved forward outputs (72 B) and the 48 B record in, 6 gradients out
         "gsplat_fused_preprocess_backward": (116 + 12 * K) * N + 48 * nvis,
     }
@@ -148,6 +155,8 @@ def algorithmic_bytes(N, I, P, T, K, nvis):
 ENTRY_KERNELS = {
     "gsplat_rasterize_backward": (("raster_bwd", "split_grads_kernel"), False),
     "gsplat_rasterize_backward_records": (("raster_bwd",), False),
+    "gsplat_rasterize_backward_records_l1": (("raster_bwd",), False),
+    "gsplat_rasterize_forward_clearing_l1": (("raster_fwd", "post_forward"), False),
     "gsplat_fused_preprocess_forward": (("fused_fwd_kernel",), True),
     "gsplat_fused_preprocess_forward_binned": (("fused_fwd_kernel",), True),
     "gsplat_fused_preprocess_backward": (("fused_bwd_kernel",), True),
