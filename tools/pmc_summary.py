@@ -37,6 +37,7 @@ EMIT_HEAD = ("emit_kernel", "bk_count_kernel", "bk_scan_kernel", "bk_place_kerne
 EMIT_START = EMIT_HEAD + ("tc_first_kernel", "ep0_count_kernel")
 EMIT_END = ("bins_decode_kernel", "bk_sort_kernel<1024")
 PRE, FIN = "gsplat_bin_emit_prelaunch", "gsplat_bin_emit_finish"
+SPEC = "gsplat_bin_speculative"
 entries = collections.defaultdict(lambda: collections.defaultdict(float))
 calls = collections.defaultdict(set)
 for f in files:
@@ -49,12 +50,20 @@ for f in files:
         names[d] = r["Kernel_Name"]
         disp[d][r["Counter_Name"]] = disp[d].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
     state, seg = None, 0
+    count_part = []  # this segment's count-phase dispatches (re-labelled for the one-call binning)
     for d in sorted(disp):
         k = names[d]
         if "fused_fwd_kernel" in k or "project_fwd_kernel" in k:
-            state, seg = "gsplat_bin_count_keyed", seg + 1
+            state, seg, count_part = "gsplat_bin_count_keyed_ex", seg + 1, []
             continue
-        if state == "gsplat_bin_count_keyed" and any(s in k for s in EMIT_START):
+        if state == "gsplat_bin_count_keyed_ex" and "emit_scan_kernel" in k:
+            # round 4's gsplat_bin_speculative: count, emission and tile sort in one entry
+            for dd in count_part:
+                for c, v in disp[dd].items():
+                    entries[state][(os.path.dirname(f), c)] -= v
+                    entries[SPEC][(os.path.dirname(f), c)] += v
+            state = SPEC
+        elif state == "gsplat_bin_count_keyed_ex" and any(s in k for s in EMIT_START):
             state = PRE if any(s in k for s in EMIT_HEAD) else FIN
         elif state == PRE and not any(s in k for s in EMIT_HEAD):
             state = FIN
@@ -65,7 +74,9 @@ for f in files:
         for c, v in disp[d].items():
             entries[state][(os.path.dirname(f), c)] += v
         calls[state].add((os.path.dirname(f), seg))
-        if state == FIN and any(s in k for s in EMIT_END):
+        if state == "gsplat_bin_count_keyed_ex":
+            count_part.append(d)
+        if state in (FIN, SPEC) and any(s in k for s in EMIT_END):
             state = None
 entry_rows = {}
 for e, d in entries.items():
