@@ -95,8 +95,9 @@ def test_split_forward_against_unsplit(gpu, W, H, n, seed, chunk, shift):
     assert (dT <= 2e-4 * np.abs(ref[1]) + 1e-9).all(), float((dT / (np.abs(ref[1]) + 1e-9)).max())
     dI = np.abs(got[0].astype(np.float64) - ref[0])
     assert (dI <= 1e-5 + 1e-4 * np.abs(ref[0])).all(), float(dI.max())
-    # a real share of pixels terminates (the termination fix-up is exercised)
-    assert (ref[1] <= 1e-4).mean() > 0.01 or shift == 0.0
+    # a real share of pixels saturates (a stopped pixel keeps the T before its stop, > 1e-4:
+    # below 1e-3 it is within a few Gaussians of it), so the termination fix-up is exercised
+    assert (ref[1] < 1e-3).mean() > 0.01 or shift == 0.0
 
 
 @pytest.mark.parametrize("W,H,n,seed,chunk,shift", CASES[::2])
