@@ -668,6 +668,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
 // per wave before its LDS atomics.  The headline's visible depths (2.5-5.5) share their top
 // byte, so one of its four passes drops out.
 int g_key_range = 2;
+bool g_depth_payload = false;  // see bin_count_impl
 bool use_key_range(long long n) { return g_key_range == 2 || (g_key_range == 1 && n >= (1LL << 22)); }
 
 uint32_t *rts_tile_counts(void *ws) { return (uint32_t *)ws + OS_HEAD_WORDS; }
@@ -2271,6 +2272,12 @@ extern "C" int gsplat_debug_emit_pass0(int on) {
   return prev;
 }
 
+extern "C" int gsplat_debug_depth_payload(int on) {
+  const int prev = g_depth_payload ? 1 : 0;
+  if (on >= 0) g_depth_payload = on != 0;
+  return prev;
+}
+
 extern "C" int gsplat_debug_depth_key_range(int on) {
   const int prev = g_key_range;
   if (on >= 0) g_key_range = on > 2 ? 2 : on;
@@ -2364,10 +2371,14 @@ static int bin_count_impl(int num_points, const float *xys, const float *depths,
 #undef DEPTH_KEYS
   // range_out: d_counts[2..3] are written only when the key range is computed (the caller
   // zeroes them: without a range nothing is assumed and nothing reported)
-  // below 4M keys (4 keys per thread) the sort carries each Gaussian's tile box (its record's
-  // y, z) to p.box in depth order; above, the payload's registers and LDS (16 keys per thread:
-  // occupancy 4 -> 2) cost more than the records' gather by depth order
-  const bool carry = sp.items <= 8;
+  // g_depth_payload (gsplat_debug_depth_payload, off by default): below 4M keys the sort carries
+  // each Gaussian's tile box (its record's y, z) to p.box in depth order and box_counts_kernel
+  // reads it coalesced, instead of gather_counts_kernel's random gather of the records by
+  // depth order.  Measured slower (round 4, same-box A/B, 2 reps: headline binning 0.2244 /
+  // 0.2278 -> 0.2302 / 0.2305 ms, c3 0.1406 / 0.1409 -> 0.1412 / 0.1417): the payload's extra
+  // 16 B per key and pass and its registers (occupancy 7 -> 6) cost the passes more than the
+  // gather's random reads.  Above 4M keys (16 keys per thread) never (occupancy 4 -> 2).
+  const bool carry = g_depth_payload && sp.items <= 8;
   if (radix_sort_pairs<uint32_t>(p.dkeys_a, p.dvals_a, p.dkeys_b, p.dvals_b, nullptr, p.order, n,
                                  0, 32, p.rs_ws, st, pre, nullptr, 0, true, 0, nullptr,
                                  use_key_range(n) ? assume_const : 0u,

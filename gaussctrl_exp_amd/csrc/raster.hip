@@ -1040,14 +1040,17 @@ __global__ __launch_bounds__(256) void raster_fwd_part_kernel(
     unsigned long long *__restrict__ kbits, long long kbw, const float *__restrict__ l1_gt,
     float *__restrict__ l1_part, int l1_clamp, int chunk, const int2 *__restrict__ items,
     const int *__restrict__ n_items, const int *__restrict__ fbase, float *__restrict__ fprec,
-    unsigned long long *__restrict__ ftmask) {
+    unsigned long long *__restrict__ ftmask, int slot0 = 0, int slot_end = 0x7FFFFFFF) {
   auto clear_side_job = [&]() {  // (as raster_fwd3u_kernel)
     for (long long k = (long long)blockIdx.x * 256 + threadIdx.x; k < zero_n;
          k += (long long)gridDim.x * 256)
       if (!zero_radii || zero_radii[k >> 2] > 0) zero[k] = make_float4(0.f, 0.f, 0.f, 0.f);
   };
-  const int slot = block_slot();
-  if (slot >= *n_items) {  // workgroup-uniform: past the last item
+  // two launches (see forward_clearing_impl): the first parts of all tiles (slots [0, T): the
+  // plan puts every tile's part 0 first), then the later parts, which then know exactly which
+  // pixels the first parts stopped
+  const int slot = block_slot() + slot0;
+  if (slot >= min(*n_items, slot_end)) {  // workgroup-uniform: past the last item
     clear_side_job();
     return;
   }
@@ -1078,6 +1081,15 @@ __global__ __launch_bounds__(256) void raster_fwd_part_kernel(
   const unsigned long long live = __ballot(inimg);
   const int p = fbase[tile] + part;
   const long long kb_base = wt * kbw + (long long)(range.x >> 6) + tile;
+  if (part > 0) {  // pixels an earlier part stopped take no part here
+    unsigned long long t = 0;
+    for (int k = lane; k < part; k += 64)
+      t |= __hip_atomic_load(&ftmask[(size_t)(fbase[tile] + k) * SPLIT_WAVES + wt],
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) t |= __shfl_xor(t, o, 64);
+    done = done || ((t >> lane) & 1ull);
+  }
   for (int b = lo; b < hi; b += 64) {
     if (__all(done)) break;
     if (part > 0) {  // every live pixel terminated by an earlier part: nothing left to do here
@@ -2674,13 +2686,25 @@ static int forward_clearing_impl(
     hipStream_t st = (hipStream_t)stream;
     hipLaunchKernelGGL(fwd_plan_kernel, dim3(1), dim3(1024), 0, st, (int)Tt, chunk,
                        (const int2 *)tile_bins, w.fitems, w.n_fitems, w.fbase, w.ftmask);
-    hipLaunchKernelGGL(raster_fwd_part_kernel<false>, dim3((unsigned)w.fitems_bound), dim3(256), 0,
-                       st, tile_bounds_x, tile_bounds_y, img_height, img_width,
-                       gaussian_ids_sorted, (const int2 *)tile_bins, (const float2 *)xys, conics,
-                       colors, opacity, background, out_img, final_Ts, final_idx,
-                       (float4 *)clear, (long long)(clear_bytes / 16), clear_radii, tile_last,
-                       kbits, kbw, l1_gt, l1_part, l1_clamp, chunk, (const int2 *)w.fitems,
-                       (const int *)w.n_fitems, (const int *)w.fbase, w.fprec, w.ftmask);
+    // every tile's first part (the plain forward for a tile of one part), then the later parts:
+    // a dense tile's pixels mostly stop in its first part, and the later parts skip them
+    // (launched together, the later parts would blend every position of every list)
+    hipLaunchKernelGGL(raster_fwd_part_kernel<false>, dim3((unsigned)Tt), dim3(256), 0, st,
+                       tile_bounds_x, tile_bounds_y, img_height, img_width, gaussian_ids_sorted,
+                       (const int2 *)tile_bins, (const float2 *)xys, conics, colors, opacity,
+                       background, out_img, final_Ts, final_idx, (float4 *)clear,
+                       (long long)(clear_bytes / 16), clear_radii, tile_last, kbits, kbw, l1_gt,
+                       l1_part, l1_clamp, chunk, (const int2 *)w.fitems, (const int *)w.n_fitems,
+                       (const int *)w.fbase, w.fprec, w.ftmask, 0, (int)Tt);
+    if (w.fitems_bound > Tt)
+      hipLaunchKernelGGL(raster_fwd_part_kernel<false>, dim3((unsigned)(w.fitems_bound - Tt)),
+                         dim3(256), 0, st, tile_bounds_x, tile_bounds_y, img_height, img_width,
+                         gaussian_ids_sorted, (const int2 *)tile_bins, (const float2 *)xys,
+                         conics, colors, opacity, background, out_img, final_Ts, final_idx,
+                         (float4 *)nullptr, 0LL, (const int *)nullptr, tile_last, kbits, kbw,
+                         l1_gt, l1_part, l1_clamp, chunk, (const int2 *)w.fitems,
+                         (const int *)w.n_fitems, (const int *)w.fbase, w.fprec, w.ftmask,
+                         (int)Tt);
     hipLaunchKernelGGL(raster_fwd_combine_kernel, dim3((unsigned)Tt), dim3(256), 0, st,
                        tile_bounds_x, tile_bounds_y, img_height, img_width, gaussian_ids_sorted,
                        (const int2 *)tile_bins, (const float2 *)xys, conics, colors, opacity,

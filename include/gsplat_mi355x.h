@@ -518,6 +518,9 @@ int gsplat_debug_raster_variant_is_default(void);
  *   tile sort), 0 depth sort + tile sort, 1 tile buckets.  Must not change between a
  *   gsplat_bin_count and its gsplat_bin_emit. */
 int gsplat_debug_emit_pass0(int on);
+/* Debug: the depth sort carries each Gaussian's tile box as a payload (1) instead of the
+ * records' gather by depth order (0, the default: measured faster).  Returns the previous. */
+int gsplat_debug_depth_payload(int on);
 int gsplat_debug_depth_key_range(int on);
 int gsplat_debug_binning_scheme(int scheme);
 /* Profiling hook: the backward blend kernels record per wave {start, end (s_memrealtime,
