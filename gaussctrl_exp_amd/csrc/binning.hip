@@ -1095,11 +1095,12 @@ __global__ __launch_bounds__(TPB) void emit_kernel(int n, const uint32_t *__rest
 }
 
 // The speculative binning's emission (gsplat_bin_speculative) with the allotment scan folded
-// in: one workgroup per scan tile of SC_TILE depth-ordered Gaussians (gather_counts' tiles) takes
-// its base offset and the total I straight from gather_counts' per-tile sums (at most a few
-// thousand words, summed in fixed order), scans its own allotments in four rounds of 256 and
-// emits each round wave by wave exactly as emit_kernel does -- the scan_partials and
-// scan_downsweep launches (and the off[] array) are gone.  Workgroup 0 publishes I to the
+// in: one workgroup per round of 256 depth-ordered Gaussians (a quarter of a gather_counts scan
+// tile) takes its base offset and the total I straight from gather_counts' per-tile sums (at
+// most a few thousand words, summed in fixed order) plus the allotments of the rounds before it
+// in its tile, scans its own allotments and emits them wave by wave exactly as emit_kernel does
+// -- the scan_partials and scan_downsweep launches (and the off[] array) are gone.  (One
+// workgroup per whole tile, four rounds each, left c3's 300 workgroups ~1 per CU: 28 us.)  Workgroup 0 publishes I to the
 // device word the tile sort reads and to the host's pinned slot.  I > cap: the table is
 // cleared and nothing is emitted (the caller re-bins).
 __global__ __launch_bounds__(TPB) void emit_scan_kernel(int n, int nb,
@@ -1119,19 +1120,28 @@ __global__ __launch_bounds__(TPB) void emit_scan_kernel(int n, int nb,
        i += (long long)gridDim.x * TPB)
     tile_bins[i] = 0;
   const int tid = threadIdx.x, lane = tid & 63;
-  // this tile's allotments, loaded with the partial sums (clamped: no branch between them)
-  const long long b0 = (long long)blockIdx.x * SC_TILE;
-  uint32_t c[SC_ITEMS];
+  // one round of TPB depth-ordered Gaussians per workgroup: round rr of scan tile t (the
+  // partial sums are per scan tile; the rounds before this one in the tile are summed here)
+  const int t = (int)(blockIdx.x / SC_ITEMS), rr = (int)(blockIdx.x % SC_ITEMS);
+  const long long b0 = (long long)t * SC_TILE;
+  const long long p = b0 + (long long)rr * TPB + tid;
+  uint32_t cr[SC_ITEMS];  // (all loads in flight together: clamped, no branch)
 #pragma unroll
   for (int r = 0; r < SC_ITEMS; ++r) {
-    const long long p = b0 + r * TPB + tid;
-    c[r] = p < n ? cnt[p] : 0u;
+    const long long pr = b0 + r * TPB + tid;
+    cr[r] = (r <= rr && pr < n) ? cnt[pr] : 0u;
   }
   uint32_t pre = 0, tot = 0;
   for (int k = tid; k < nb; k += TPB) {
     const uint32_t v = partial[k];
     tot += v;
-    pre += k < (int)blockIdx.x ? v : 0u;
+    pre += k < t ? v : 0u;
+  }
+  uint32_t c = 0;
+#pragma unroll
+  for (int r = 0; r < SC_ITEMS; ++r) {
+    if (r < rr) pre += cr[r];
+    if (r == rr) c = cr[r];
   }
   uint32_t bpre, btot;
   block_exclusive_scan<TPB>(pre, bpre, lds);  // (only the totals are used)
@@ -1145,25 +1155,21 @@ __global__ __launch_bounds__(TPB) void emit_scan_kernel(int n, int nb,
     if (i_host) *i_host = (int32_t)btot;
   }
   if (violated || btot > cap) return;  // workgroup-uniform
-  uint32_t run = bpre;
-#pragma unroll
-  for (int r = 0; r < SC_ITEMS; ++r) {
-    const long long p = b0 + r * TPB + tid;
+  {
     uint32_t rtot;
-    const uint32_t start = run + block_exclusive_scan<TPB>(c[r], rtot, lds);
-    run += rtot;
+    const uint32_t start = bpre + block_exclusive_scan<TPB>(c, rtot, lds);
     const long long p0 = p - lane;
-    if (p0 >= n) continue;  // wave-uniform (no barrier below)
+    if (p0 >= n) return;  // wave-uniform (no barrier below)
     const bool in = p < n;
     uint32_t g = 0;
     uint2 bx = make_uint2(0u, 0u);
-    if (in && c[r]) {
+    if (in && c) {
       g = order[p];
       bx = box[p];
     }
     const uint32_t base = __shfl(start, 0, 64);
     const int last_lane = (int)min(63LL, (long long)n - 1 - p0);
-    const uint32_t total = __shfl(start + c[r], last_lane, 64) - base;
+    const uint32_t total = __shfl(start + c, last_lane, 64) - base;
     const uint32_t rel = in ? start - base : total;
     for (uint32_t j0 = 0; j0 < total; j0 += 64) {
       const uint32_t j = j0 + lane;
@@ -2479,7 +2485,8 @@ extern "C" int gsplat_bin_speculative(int num_points, int64_t capacity, int tile
     return 1;
   const int n = num_points;
   const int nb = (int)cdiv(n, SC_TILE);
-  hipLaunchKernelGGL(emit_scan_kernel, dim3(nb), dim3(TPB), 0, st, n, nb, p1.order, p1.cnt,
+  hipLaunchKernelGGL(emit_scan_kernel, dim3(nb * SC_ITEMS), dim3(TPB), 0, st, n, nb, p1.order,
+                     p1.cnt,
                      rts_tile_counts(p1.rs_ws), p1.box, tile_bounds_x, tile_bounds_y, p2.tk_a,
                      p2.tv_a, tile_bins, p1.dcount, d_counts + 1, (uint32_t)capacity,
                      sort_kept_word(p1.rs_ws) + 1, use_key_range(n) ? assume_const : 0u);

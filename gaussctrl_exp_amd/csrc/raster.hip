@@ -945,7 +945,13 @@ __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
 // Later parts skip their remaining batches once earlier parts have terminated every pixel of
 // their block (ftmask: per part and block, the ballot of locally terminated pixels).
 constexpr long long FWD_SPLIT_MAX_TILES = 3584;
-int g_fwd_split = -1;  // gsplat_debug_forward_split: -1 / 1 on, 0 off, 2 exact walks only
+// gsplat_debug_forward_split: 0 off (the default), 1 on, 2 on with exact walks only.  Measured
+// slower on c3 (bear, 1,024 tiles; round 4 same-box A/B, 2 reps: forward 0.099 -> 0.28-0.29 ms,
+// step 0.387 -> 0.57-0.59 ms; parts of 1/2 and 1/4 the chunk alike): the first parts alone took
+// as long as the whole unsplit forward (its longest waves are dense tiles saturating within
+// their first chunk, not long unsaturated lists), the later parts 81 us and the combine 95 us
+// of re-walks (profiles/r04_ab_split_forward_c3.txt).
+int g_fwd_split = 0;
 constexpr int FPR = 6;  // part record words per pixel: C (3), T, last | lterm << 31, factors
 
 __global__ __launch_bounds__(1024) void fwd_plan_kernel(int T, int chunk,
@@ -2304,8 +2310,9 @@ extern "C" int gsplat_debug_set_chunk(int chunk) {
 }
 
 // The list-split forward (raster_fwd_part_kernel), below 3,584 tiles (the plan workspace holds
-// its records there): -1 / 1 on (the default), 0 off, 2 on with every pixel of a split tile
-// resolved by the exact sequential walk (tests: then bit-identical to the unsplit forward).
+// its records there): 0 off (the default, see g_fwd_split), 1 / -1 on, 2 on with every pixel of
+// a split tile resolved by the exact sequential walk (tests: then bit-identical to the unsplit
+// forward); other values leave the setting (a query).
 // Returns the previous setting.
 // The split forward's part length as the plan's chunk / div (rounded up to 64; 1 the default).
 extern "C" int gsplat_debug_forward_chunk_div(int div) {

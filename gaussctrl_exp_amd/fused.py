@@ -112,8 +112,10 @@ class _FusedRender(Function):
             chunk = _lib.query("gsplat_rasterize_chunk_size", tbx, tby, layout_i)
             if not need_grad:
                 # no backward: the plan only for the list-split forward of small frames
-                # (below FWD_SPLIT_TILES tiles), signalled by a negative chunk
-                chunk = -chunk if tbx * tby < FWD_SPLIT_TILES else 0
+                # (below FWD_SPLIT_TILES tiles, when switched on), signalled by a negative chunk
+                split = tbx * tby < FWD_SPLIT_TILES and \
+                    _lib.query("gsplat_debug_forward_split", -9) != 0
+                chunk = -chunk if split else 0
             plan = None
             if chunk != 0:  # the list-split plan (filled by the blend's waves)
                 plan = torch.empty((_lib.query("gsplat_rasterize_split_bytes", tbx, tby,

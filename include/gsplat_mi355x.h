@@ -336,9 +336,9 @@ int gsplat_rasterize_forward_clearing(
  * the automatic choice (0). */
 int gsplat_debug_set_chunk(int chunk);
 /* The list-split forward of small frames (below 3,584 tiles; gsplat_rasterize_forward_clearing*
- * with a plan): -1 or 1 on (default), 0 off, 2 on with every pixel of a split tile resolved by
- * the exact sequential walk (bit-identical to the unsplit forward; tests).  Returns the
- * previous setting. */
+ * with a plan): 0 off (default: measured slower on c3), -1 or 1 on, 2 on with every pixel of a
+ * split tile resolved by the exact sequential walk (bit-identical to the unsplit forward;
+ * tests); any other value only queries.  Returns the previous setting. */
 int gsplat_debug_forward_split(int mode);
 /* The split forward's part length: the plan's chunk / div, rounded up to 64 (div 1..64; 1 the
  * default).  Returns the previous div.  Plans must be sized after setting it
