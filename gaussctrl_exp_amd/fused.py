@@ -34,6 +34,7 @@ from torch.autograd import Function
 from . import _lib, exchange, quirks
 from .camera import GCCamera
 from .rasterize import (BLOCK_X, BLOCK_Y, bin_gaussians, bin_gaussians_speculative,
+                        speculative_capacity,
                         last_num_visible)
 
 _DEG_OF_BASES = {1: 0, 4: 1, 9: 2, 16: 3, 25: 4}
@@ -83,6 +84,39 @@ class _FusedRender(Function):
                       float(fx), float(fy), float(cx), float(cy), H, W, tbx, tby, 0.01, P(xys),
                       P(depths), P(radii), P(conics), P(nth), P(colors), P(opac), P(ws1),
                       ws1.numel(), st)
+        # every output and scratch buffer of the forward is allocated before the first launch,
+        # so the preprocess, the binning and the blend go out back to back (the host's work
+        # between them left the GPU idle: ~24 us before the blend at c3)
+        visible_hint = last_num_visible(dev)
+        chunk, plan = 0, None
+        if l1_gt is not None:
+            if l1_gt.shape != (H, W, 3) or return_alpha:
+                raise ValueError("render_fused: the L1 loss needs gt [H, W, 3] and no alpha")
+            l1_gt = _contig_f32(l1_gt)
+            l1_part = torch.empty((_lib.query("gsplat_rasterize_l1_partials_bytes", tbx, tby)
+                                   // 4,), **f32)
+            loss = torch.empty((), **f32)
+        out_img = torch.empty((H, W, 3), **f32)
+        final_Ts = torch.empty((H, W), **f32)
+        final_idx = torch.empty((H, W), device=dev, dtype=torch.int32)
+
+        def plan_for(layout_i):
+            """(chunk, plan buffer) of the list-split plan laid out for layout_i intersections."""
+            c = _lib.query("gsplat_rasterize_chunk_size", tbx, tby, layout_i)
+            if not need_grad:
+                # no backward: the plan only for the list-split forward of small frames
+                # (below FWD_SPLIT_TILES tiles, when switched on), signalled by a negative chunk
+                split = tbx * tby < FWD_SPLIT_TILES and \
+                    _lib.query("gsplat_debug_forward_split", -9) != 0
+                c = -c if split else 0
+            if c == 0:
+                return 0, None
+            return c, torch.empty((_lib.query("gsplat_rasterize_split_bytes", tbx, tby,
+                                              layout_i, abs(c)),), device=dev, dtype=torch.uint8)
+        # the speculative binning's layout is its capacity, known now
+        spec_cap = speculative_capacity(n, H, W, dev)
+        prepared = (spec_cap, plan_for(spec_cap)) if spec_cap > 0 else None
+
         preprocess()
         # The binning's emission and tile sort are launched at this frame shape's capacity
         # without the host read of I (rasterize.SpeculativeBinning), the blend right behind
@@ -95,32 +129,15 @@ class _FusedRender(Function):
         else:
             num_intersects, gids, bins = None, spec.ids, spec.tile_bins
             layout_i = spec.layout_intersects
-        visible_hint = last_num_visible(dev)
-        chunk, plan = 0, None
-        if l1_gt is not None:
-            if l1_gt.shape != (H, W, 3) or return_alpha:
-                raise ValueError("render_fused: the L1 loss needs gt [H, W, 3] and no alpha")
-            l1_gt = _contig_f32(l1_gt)
-            l1_part = torch.empty((_lib.query("gsplat_rasterize_l1_partials_bytes", tbx, tby)
-                                   // 4,), **f32)
-            loss = torch.empty((), **f32)
 
         def blend(gids, bins, layout_i):
             """The blend (it also clears the gradient records the backward accumulates into and
             fills the list-split plan, whose layout follows layout_i)."""
             nonlocal chunk, plan
-            chunk = _lib.query("gsplat_rasterize_chunk_size", tbx, tby, layout_i)
-            if not need_grad:
-                # no backward: the plan only for the list-split forward of small frames
-                # (below FWD_SPLIT_TILES tiles, when switched on), signalled by a negative chunk
-                split = tbx * tby < FWD_SPLIT_TILES and \
-                    _lib.query("gsplat_debug_forward_split", -9) != 0
-                chunk = -chunk if split else 0
-            plan = None
-            if chunk != 0:  # the list-split plan (filled by the blend's waves)
-                plan = torch.empty((_lib.query("gsplat_rasterize_split_bytes", tbx, tby,
-                                               layout_i, abs(chunk)),),
-                                   device=dev, dtype=torch.uint8)
+            if prepared is not None and prepared[0] == layout_i:
+                chunk, plan = prepared[1]
+            else:
+                chunk, plan = plan_for(layout_i)
             args = (tbx, tby, H, W, P(gids), P(bins), P(xys), P(conics), P(colors), P(opac),
                     P(background), P(out_img), P(final_Ts), P(final_idx), P(rec),
                     rec.numel() if rec is not None else 0,
@@ -134,9 +151,6 @@ class _FusedRender(Function):
                 _lib.call("gsplat_rasterize_forward_clearing_l1", *args, P(l1_gt), 1, P(l1_part),
                           4 * l1_part.numel(), P(loss), st)
 
-        out_img = torch.empty((H, W, 3), **f32)
-        final_Ts = torch.empty((H, W), **f32)
-        final_idx = torch.empty((H, W), device=dev, dtype=torch.int32)
         if spec is not None:
             blend(gids, bins, layout_i)
             if not spec.finish():

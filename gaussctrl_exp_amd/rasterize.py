@@ -263,6 +263,16 @@ class SpeculativeBinning:
         return ids_buf[:I], self.tile_bins
 
 
+def speculative_capacity(n: int, img_height: int, img_width: int, dev) -> int:
+    """The capacity (intersection layout) bin_gaussians_speculative will use for this frame
+    shape, or 0 when it will not run speculatively (first call of the shape, switched off)."""
+    if n == 0 or not SPECULATIVE_BINNING:
+        return 0
+    tbx = (img_width + BLOCK_X - 1) // BLOCK_X
+    tby = (img_height + BLOCK_Y - 1) // BLOCK_Y
+    return _EMIT_CAP.get((dev, n, tbx, tby), 0)
+
+
 def bin_gaussians_speculative(xys: Tensor, depths: Tensor, radii: Tensor, num_tiles_hit: Tensor,
                               img_height: int, img_width: int,
                               keyed_workspace: Optional[Tensor] = None):
