@@ -35,6 +35,7 @@ sys.path.insert(0, ROOT)
 from gaussctrl_exp_amd import _lib, timing  # noqa: E402
 from gaussctrl_exp_amd.camera import gc_camera, look_at_c2w  # noqa: E402
 from gaussctrl_exp_amd.fused import render_fused  # noqa: E402
+from gaussctrl_exp_amd.graphs import StepGraph  # noqa: E402
 from gaussctrl_exp_amd.rasterize import bin_gaussians  # noqa: E402
 from gaussctrl_exp_amd.scene import render, synthetic_scene  # noqa: E402
 from gaussctrl_exp_amd.sh import num_sh_bases  # noqa: E402
@@ -136,6 +137,10 @@ def algorithmic_bytes(N, I, P, T, K, nvis):
         "gsplat_fused_preprocess_forward": (92 + 12 * K) * N,
         # + the binning's depth key, id and 16-B record per Gaussian
         "gsplat_fused_preprocess_forward_binned": (116 + 12 * K) * N,
+        # its two parts (round 4: the colours on a second stream): params + projection outputs
+        # + binning inputs; means, features and colours
+        "gsplat_fused_preprocess_forward_part[1]": 104 * N,
+        "gsplat_fused_preprocess_forward_part[2] (side stream)": (24 + 12 * K) * N,
         # its blend also zeroes the 48-B gradient record of every visible Gaussian
         "gsplat_rasterize_forward_clearing": 40 * I + 20 * P + 48 * nvis,
         "gsplat_rasterize_backward_records": 40 * I + 24 * P,
@@ -159,6 +164,7 @@ ENTRY_KERNELS = {
     "gsplat_rasterize_forward_clearing_l1": (("raster_fwd", "post_forward"), False),
     "gsplat_fused_preprocess_forward": (("fused_fwd_kernel",), True),
     "gsplat_fused_preprocess_forward_binned": (("fused_fwd_kernel",), True),
+    "gsplat_fused_preprocess_forward_part[1]": (("fused_fwd_proj_kernel",), True),
     "gsplat_fused_preprocess_backward": (("fused_bwd_kernel",), True),
     "gsplat_rasterize_forward": (("raster_fwd",), False),
     "gsplat_rasterize_forward_clearing": (("raster_fwd",), False),
@@ -460,6 +466,9 @@ def main():
                          "kernels out of the PMC and kernel-trace summaries)")
     ap.add_argument("--forward-only", action="store_true",
                     help="time the render without backward (default for config c2)")
+    ap.add_argument("--graph", default="auto", choices=("auto", "off"),
+                    help="auto: one GPU replays the fused step as a HIP graph (graphs.py); "
+                         "off: every step issued eagerly")
     ap.add_argument("--render", default="fused", choices=("fused", "caller"),
                     help="fused: the caller's activations inside the HIP kernels (default); "
                          "caller: gc_model.py's torch glue around the gsplat API")
@@ -495,7 +504,7 @@ def main():
 
     fwd_only = args.forward_only or args.config in FORWARD_ONLY
 
-    def step(t=trainer):
+    def step_eager(t=trainer):
         if fwd_only:
             with torch.no_grad():
                 if t.render_mode == "fused":
@@ -506,6 +515,19 @@ def main():
         t.zero_grad()
         t.forward_backward(cam, gt, bg)
         t.sync_grads()
+
+    # the fused step replayed as one HIP graph (graphs.StepGraph: captured after eager warm-up
+    # steps; every replay's binning counts checked on the host, an overflow re-run eagerly).
+    # One GPU only: the N > 1 step's collectives stay eager.
+    graph = None
+    if args.graph == "auto" and world == 1 and args.render == "fused":
+        graph = StepGraph(step_eager, dev, params=() if fwd_only else trainer.params)
+
+    def step(t=trainer):
+        if graph is not None and t is trainer:
+            graph.step()
+        else:
+            step_eager(t)
 
     def timed(fn, steps):
         barrier()
@@ -539,6 +561,10 @@ def main():
         dt = float(t.item())
     ms_per_step = dt / args.steps * 1e3
     value = world * H * W * args.steps / dt / 1e6
+    eager_value = None
+    if graph is not None:
+        # the same step issued eagerly (kernel launches from Python each step), for comparison
+        eager_value = world * H * W * args.steps / timed(step_eager, args.steps) / 1e6
     exch = None
     if world > 1 and not fwd_only:
         exch = exchange_profile(scene, cam, gt, bg, deg, world, dev, args.steps, timed)
@@ -560,7 +586,7 @@ def main():
         ev1 = torch.cuda.Event(enable_timing=True)
         ev0.record()
         for _ in range(args.steps):
-            step()
+            step_eager()
         ev1.record()
         per_call = tm.summary()
         events_step_ms = ev0.elapsed_time(ev1) / args.steps
@@ -586,7 +612,8 @@ def main():
     # the entries' device time per step against the same loop's device time per step: the
     # remainder is torch work outside the C ABI (loss glue, zero_grad, all-reduce) and device
     # idle between calls, so the block sums to the step
-    attributed = sum(v[2] for v in per_call.values()) / args.steps
+    # (entries on a second stream overlap the others: not part of the sum)
+    attributed = sum(v[2] for k, v in per_call.items() if "(side stream)" not in k) / args.steps
     kernels["(outside the C-ABI calls)"] = {
         "ms_per_call": round(events_step_ms - attributed, 4), "calls_per_step": 1.0,
         "GBps": None}
@@ -622,7 +649,7 @@ def main():
         "roofline_mpix_s": round(P / (step_bytes / (HBM_PEAK_GBS * 1e9)) / 1e6, 1),
     }
 
-    lanes = None if args.no_lane_occupancy else lane_occupancy(step, dev, args.config)
+    lanes = None if args.no_lane_occupancy else lane_occupancy(step_eager, dev, args.config)
 
     # full train step: splatfacto loss + backward + all-reduce + Adam
     tsteps = args.train_steps if args.train_steps is not None else args.steps
@@ -677,6 +704,10 @@ def main():
             },
             "render": args.render,
             "exchange": exch,
+            "step_issue": "hip_graph" if graph is not None and graph.graph is not None
+                          else "eager",
+            "graph": graph.stats() if graph is not None else None,
+            "value_eager_launches": round(eager_value, 2) if eager_value else None,
             "value_unchanged_caller": round(caller_value, 2),
             "train_iters_per_s": round(tsteps / tdt, 2),
             "train_views_per_s": round(world * tsteps / tdt, 2),

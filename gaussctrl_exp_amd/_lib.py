@@ -89,6 +89,8 @@ SIGNATURES = {
                                         [_I] * 4 + [_F] + [_P] * 11),
     "gsplat_fused_preprocess_forward_binned": (_I, [_I, _I, _I] + [_P] * 9 + [_F] * 4 +
                                                [_I] * 4 + [_F] + [_P] * 8 + [_SZ, _P]),
+    "gsplat_fused_preprocess_forward_part": (_I, [_I, _I, _I, _I] + [_P] * 9 + [_F] * 4 +
+                                             [_I] * 4 + [_F] + [_P] * 8 + [_SZ, _P]),
     "gsplat_bin_count_keyed": (_I, [_I, _I, _I, _P, _P, _SZ, _P]),
     "gsplat_bin_count_keyed_ex": (_I, [_I, _I, _I, _P, _P, _SZ, _c.c_uint32, _P]),
     "gsplat_bin_rescan": (_I, [_I, _I, _I, _P, _SZ, _P]),

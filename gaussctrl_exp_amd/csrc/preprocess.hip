@@ -135,7 +135,12 @@ __device__ __forceinline__ void load_cam_scalar(Cam &c, const float *viewmat,
 // waits only for its own inputs (vmcnt counts in issue order and a branch in between makes the
 // compiler drain the counter) while the features_rest slab stays in flight; the slab lands in
 // LDS after the projection.  Otherwise: guarded loads and stage_rows.
-template <int K, bool FULL>
+// PART: 0 the whole forward; 1 the projection part (activations, projection, opacity, the
+// binning's inputs) without the SH colours; 2 the SH colours alone (gsplat_fused_preprocess_
+// forward_part: the two parts on two streams, the colours' 216 B per Gaussian overlapping the
+// binning's latency-bound sort passes).  Each part's outputs are the whole forward's, bit for bit
+// (the same code; a part only leaves out the other's loads and stores).
+template <int K, bool FULL, int PART = 0>
 __device__ __forceinline__ void fused_fwd_body(const FusedFwdArgs &a, const ProjParams &pp,
                                                float *smem, long long g0, int cnt) {
   constexpr int RROW = (K - 1) * 3;  // features_rest floats per Gaussian
@@ -146,27 +151,33 @@ __device__ __forceinline__ void fused_fwd_body(const FusedFwdArgs &a, const Proj
   const int t = threadIdx.x;
   const bool live = FULL || t < cnt;
   const long long g = g0 + (live ? t : 0);
+  constexpr bool PROJ = PART != 2, COLOURS = PART != 1;
   Cam cam;
-  load_cam_scalar(cam, a.viewmat, a.projmat);
-  float p0, p1, p2, dc[3], lsv[3], qv[4], ologit;
+  if constexpr (PROJ) load_cam_scalar(cam, a.viewmat, a.projmat);
+  float p0, p1, p2, dc[3] = {0.f, 0.f, 0.f}, lsv[3] = {0.f, 0.f, 0.f},
+                    qv[4] = {0.f, 0.f, 0.f, 0.f}, ologit = 0.f;
   p0 = a.means[3 * g];
   p1 = a.means[3 * g + 1];
   p2 = a.means[3 * g + 2];
+  if constexpr (PROJ) {
 #pragma unroll
-  for (int k = 0; k < 3; ++k) lsv[k] = a.log_scales[3 * g + k];
+    for (int k = 0; k < 3; ++k) lsv[k] = a.log_scales[3 * g + k];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) qv[k] = a.quats[4 * g + k];
-  ologit = a.opacity_logits[g];
+    for (int k = 0; k < 4; ++k) qv[k] = a.quats[4 * g + k];
+    ologit = a.opacity_logits[g];
+  }
+  if constexpr (COLOURS) {
 #pragma unroll
-  for (int c = 0; c < 3; ++c) dc[c] = a.features_dc[3 * g + c];
+    for (int c = 0; c < 3; ++c) dc[c] = a.features_dc[3 * g + c];
+  }
   const float *rest_src = K > 1 ? a.features_rest + g0 * RROW : nullptr;
-  float4 slab[FULL && K > 1 ? PER : 1];
-  if constexpr (FULL && K > 1) {
+  float4 slab[FULL && K > 1 && COLOURS ? PER : 1];
+  if constexpr (FULL && K > 1 && COLOURS) {
     const float4 *s4 = reinterpret_cast<const float4 *>(rest_src);
 #pragma unroll
     for (int u = 0; u < PER; ++u) slab[u] = s4[min(u * THR + t, NV - 1)];  // clamped: no branch
   }
-  if (live) {
+  if (PROJ && live) {
     float s[3], qr[4], qn[4], norm;
     activate_vals(lsv, qv, s, qr, qn, norm);
     ProjOut o;
@@ -212,7 +223,9 @@ __device__ __forceinline__ void fused_fwd_body(const FusedFwdArgs &a, const Proj
       for (int k = 0; k < 4; ++k) a.quats_out[4 * g + k] = qn[k];
     }
   }
-  if constexpr (K == 1) {  // sh_degree 0: sigmoid(features_dc) (gc_model.py:203)
+  if constexpr (!COLOURS) {
+    return;
+  } else if constexpr (K == 1) {  // sh_degree 0: sigmoid(features_dc) (gc_model.py:203)
     if (live) {
 #pragma unroll
       for (int c = 0; c < 3; ++c) a.colors[3 * g + c] = sigmoidf(dc[c]);
@@ -260,6 +273,35 @@ __global__ __launch_bounds__(sh_threads(K)) void fused_fwd_kernel(FusedFwdArgs a
     fused_fwd_body<K, true>(a, pp, smem, g0, cnt);
   else
     fused_fwd_body<K, false>(a, pp, smem, g0, cnt);
+}
+
+// the two parts of fused_fwd_kernel (PART 1 / 2 of fused_fwd_body)
+template <int K>
+__global__ __launch_bounds__(sh_threads(K)) void fused_fwd_proj_kernel(FusedFwdArgs a,
+                                                                       ProjParams pp) {
+  constexpr int THR = sh_threads(K);
+  const long long g0 = (long long)blockIdx.x * THR;
+  const int cnt = (int)min((long long)THR, (long long)a.n - g0);
+  if (cnt == THR)
+    fused_fwd_body<K, true, 1>(a, pp, nullptr, g0, cnt);
+  else
+    fused_fwd_body<K, false, 1>(a, pp, nullptr, g0, cnt);
+}
+
+template <int K>
+__global__ __launch_bounds__(sh_threads(K)) void fused_fwd_sh_kernel(FusedFwdArgs a,
+                                                                     ProjParams pp) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int THR = sh_threads(K);
+  const long long g0 = (long long)blockIdx.x * THR;
+  const int cnt = (int)min((long long)THR, (long long)a.n - g0);
+  const bool aligned =
+      K == 1 || ((((uintptr_t)(a.features_rest + g0 * (K - 1) * 3)) & 15) == 0 &&
+                 (THR * (K - 1) * 3) % 4 == 0);
+  if (cnt == THR && aligned)
+    fused_fwd_body<K, true, 2>(a, pp, smem, g0, cnt);
+  else
+    fused_fwd_body<K, false, 2>(a, pp, smem, g0, cnt);
 }
 
 template <int K, bool ADAM = false>
@@ -478,7 +520,7 @@ static int fused_forward_impl(
     int img_height, int img_width, int tile_bounds_x, int tile_bounds_y, float clip_thresh,
     float *xys, float *depths, int32_t *radii, float *conics, int32_t *num_tiles_hit,
     float *colors, float *opacity, void *grad_records, float *scales_out, float *quats_out,
-    void *bin_workspace, size_t bin_workspace_bytes, void *stream) {
+    void *bin_workspace, size_t bin_workspace_bytes, void *stream, int part = 0) {
   const int K = sh_bases;
   if (num_points < 0 || !valid_bases(K) || degrees_to_use < 0 || degrees_to_use > degree_of(K) ||
       img_height <= 0 || img_width <= 0 || tile_bounds_x <= 0 || tile_bounds_y <= 0 ||
@@ -507,7 +549,14 @@ static int fused_forward_impl(
   const dim3 grid(cdiv(num_points, thr));
   const size_t smem = K > 1 ? (size_t)thr * (((K - 1) * 3) | 1) * sizeof(float) : 0;
   hipStream_t st = (hipStream_t)stream;
-  FUSED_DISPATCH(fused_fwd_kernel, args);
+  if (part == 1) {
+    const size_t smem = 0;  // (no features_rest slab)
+    FUSED_DISPATCH(fused_fwd_proj_kernel, args);
+  } else if (part == 2) {
+    FUSED_DISPATCH(fused_fwd_sh_kernel, args);
+  } else {
+    FUSED_DISPATCH(fused_fwd_kernel, args);
+  }
   return check_launch("fused_preprocess_forward");
 }
 
@@ -546,6 +595,38 @@ extern "C" int gsplat_fused_preprocess_forward_binned(
                             clip_thresh, xys, depths, radii, conics, num_tiles_hit, colors,
                             opacity, nullptr, nullptr, nullptr, bin_workspace,
                             bin_workspace_bytes, stream);
+}
+
+extern "C" int gsplat_fused_preprocess_forward_part(
+    int part, int num_points, int sh_bases, int degrees_to_use, const float *means3d,
+    const float *log_scales, const float *quats, const float *opacity_logits,
+    const float *features_dc, const float *features_rest, const float *viewmat,
+    const float *projmat, const float *campos, float fx, float fy, float cx, float cy,
+    int img_height, int img_width, int tile_bounds_x, int tile_bounds_y, float clip_thresh,
+    float *xys, float *depths, int32_t *radii, float *conics, int32_t *num_tiles_hit,
+    float *colors, float *opacity, void *bin_workspace, size_t bin_workspace_bytes,
+    void *stream) {
+  if (part != 1 && part != 2) {
+    set_error("fused_preprocess_forward_part: part %d (1 = projection, 2 = colours)", part);
+    return 1;
+  }
+  if (part == 1 && !bin_workspace) {
+    set_error("fused_preprocess_forward_part: no binning workspace");
+    return 1;
+  }
+  if (num_points > 0 && (part == 2 ? !colors || !means3d || !features_dc
+                                   : !xys || !depths || !radii || !conics || !num_tiles_hit ||
+                                         !opacity || !means3d || !log_scales || !quats ||
+                                         !opacity_logits || !viewmat || !projmat)) {
+    set_error("fused_preprocess_forward_part: missing tensors for part %d", part);
+    return 1;
+  }
+  return fused_forward_impl(num_points, sh_bases, degrees_to_use, means3d, log_scales, quats,
+                            opacity_logits, features_dc, features_rest, viewmat, projmat, campos,
+                            fx, fy, cx, cy, img_height, img_width, tile_bounds_x, tile_bounds_y,
+                            clip_thresh, xys, depths, radii, conics, num_tiles_hit, colors,
+                            opacity, nullptr, nullptr, nullptr, part == 1 ? bin_workspace : nullptr,
+                            bin_workspace_bytes, stream, part);
 }
 
 extern "C" int gsplat_fused_preprocess_backward(

@@ -24,6 +24,7 @@ the drop-in; this is the framework's own training step (TrainStep(render_mode="f
 from __future__ import annotations
 
 import ctypes
+import os
 import weakref
 from typing import Optional
 
@@ -33,13 +34,31 @@ from torch.autograd import Function
 
 from . import _lib, exchange, quirks
 from .camera import GCCamera
-from .rasterize import (BLOCK_X, BLOCK_Y, bin_gaussians, bin_gaussians_speculative,
-                        speculative_capacity,
-                        last_num_visible)
+from .rasterize import (BLOCK_X, BLOCK_Y, GraphCaptureUnsupported, bin_gaussians,
+                        bin_gaussians_speculative, speculative_capacity, last_num_visible)
 
 _DEG_OF_BASES = {1: 0, 4: 1, 9: 2, 16: 3, 25: 4}
 # frames below this many tiles get the list-split forward (raster.hip FWD_SPLIT_MAX_TILES)
 FWD_SPLIT_TILES = 3584
+
+# While a step is captured into a HIP graph (graphs.StepGraph): the speculative binnings the
+# captured forwards launched, whose pinned count words the graph's owner checks after every
+# replay instead of the forward's own finish() (a capture runs no kernel: nothing to wait for).
+_CAPTURE_SPECS: Optional[list] = None
+# How the last forward binned: "speculative" (capacity-launched, no host read: capturable),
+# "host" (the scheme needs I on the host first) or "sync" (first call of the frame shape)
+LAST_BINNING = {"mode": None}
+# the preprocess's SH-colour part on a second stream, overlapping the binning
+# (gsplat_fused_preprocess_forward_part); GSPLAT_MI355X_SPLIT_COLOURS=0: one kernel (A/B runs)
+SPLIT_COLOURS = os.environ.get("GSPLAT_MI355X_SPLIT_COLOURS", "1") != "0"
+_SIDE = {}
+
+
+def _side_stream(dev) -> torch.cuda.Stream:
+    s = _SIDE.get(dev)
+    if s is None:
+        s = _SIDE[dev] = torch.cuda.Stream(device=dev)
+    return s
 
 
 class _FusedRender(Function):
@@ -77,13 +96,34 @@ class _FusedRender(Function):
         # the preprocess kernel also writes the binning's depth-sort inputs into its workspace
         ws1 = torch.empty((max(_lib.query("gsplat_bin_count_workspace_size", n), 1),),
                           device=dev, dtype=torch.uint8)
+        cam_args = (P(viewmat), P(projmat), P(campos), float(fx), float(fy), float(cx),
+                    float(cy), H, W, tbx, tby, 0.01)
+        split_colours = K > 1 and SPLIT_COLOURS
+
         def preprocess():
-            _lib.call("gsplat_fused_preprocess_forward_binned", n, K, int(degrees_to_use),
+            """The preprocess; with split_colours its SH-colour part goes out on a second
+            stream (joined before the blend, join_colours) and overlaps the binning."""
+            if not split_colours:
+                _lib.call("gsplat_fused_preprocess_forward_binned", n, K, int(degrees_to_use),
+                          P(means), P(scales), P(quats), P(opacities), P(features_dc),
+                          P(features_rest) if K > 1 else None, *cam_args, P(xys), P(depths),
+                          P(radii), P(conics), P(nth), P(colors), P(opac), P(ws1), ws1.numel(),
+                          st)
+                return
+            cur = torch.cuda.current_stream(dev)
+            side = _side_stream(dev)
+            side.wait_stream(cur)
+            _lib.call("gsplat_fused_preprocess_forward_part", 2, n, K, int(degrees_to_use),
+                      P(means), None, None, None, P(features_dc), P(features_rest), *cam_args,
+                      None, None, None, None, None, P(colors), None, None, 0, side.cuda_stream)
+            _lib.call("gsplat_fused_preprocess_forward_part", 1, n, K, int(degrees_to_use),
                       P(means), P(scales), P(quats), P(opacities), P(features_dc),
-                      P(features_rest) if K > 1 else None, P(viewmat), P(projmat), P(campos),
-                      float(fx), float(fy), float(cx), float(cy), H, W, tbx, tby, 0.01, P(xys),
-                      P(depths), P(radii), P(conics), P(nth), P(colors), P(opac), P(ws1),
-                      ws1.numel(), st)
+                      P(features_rest), *cam_args, P(xys), P(depths), P(radii), P(conics),
+                      P(nth), None, P(opac), P(ws1), ws1.numel(), st)
+
+        def join_colours():
+            if split_colours:
+                torch.cuda.current_stream(dev).wait_stream(_side_stream(dev))
         # every output and scratch buffer of the forward is allocated before the first launch,
         # so the preprocess, the binning and the blend go out back to back (the host's work
         # between them left the GPU idle: ~24 us before the blend at c3)
@@ -117,11 +157,25 @@ class _FusedRender(Function):
         spec_cap = speculative_capacity(n, H, W, dev)
         prepared = (spec_cap, plan_for(spec_cap)) if spec_cap > 0 else None
 
+        capturing = _CAPTURE_SPECS is not None
+        if capturing and prepared is None:
+            raise GraphCaptureUnsupported("render_fused: no intersection capacity for this "
+                                          "frame shape yet (run it eagerly first)")
         preprocess()
         # The binning's emission and tile sort are launched at this frame shape's capacity
         # without the host read of I (rasterize.SpeculativeBinning), the blend right behind
         # them; the host reads I only then, while the GPU works, and re-bins on an overflow.
-        spec = bin_gaussians_speculative(xys, depths, radii, nth, H, W, keyed_workspace=ws1)
+        spec = bin_gaussians_speculative(xys, depths, radii, nth, H, W, keyed_workspace=ws1,
+                                         host_wait=not capturing)
+        LAST_BINNING["mode"] = "sync" if spec is None else (
+            "speculative" if spec.slot is not None else "host")
+        if capturing:
+            # a captured forward: the replay's owner checks the count words (graphs.StepGraph);
+            # the layout and the backward's intersection count are the capacity
+            if spec is None or spec.slot is None:
+                raise GraphCaptureUnsupported("render_fused: this frame's binning reads I on "
+                                              "the host")
+            _CAPTURE_SPECS.append(spec)
         if spec is None:  # first call of this frame shape (or nothing to bin)
             num_intersects, gids, bins = bin_gaussians(xys, depths, radii, nth, H, W,
                                                        keyed_workspace=ws1)
@@ -134,6 +188,7 @@ class _FusedRender(Function):
             """The blend (it also clears the gradient records the backward accumulates into and
             fills the list-split plan, whose layout follows layout_i)."""
             nonlocal chunk, plan
+            join_colours()
             if prepared is not None and prepared[0] == layout_i:
                 chunk, plan = prepared[1]
             else:
@@ -151,7 +206,10 @@ class _FusedRender(Function):
                 _lib.call("gsplat_rasterize_forward_clearing_l1", *args, P(l1_gt), 1, P(l1_part),
                           4 * l1_part.numel(), P(loss), st)
 
-        if spec is not None:
+        if capturing:
+            blend(gids, bins, layout_i)
+            num_intersects = spec.cap
+        elif spec is not None:
             blend(gids, bins, layout_i)
             if not spec.finish():
                 if spec.range_violated:

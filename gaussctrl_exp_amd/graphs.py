@@ -1,0 +1,134 @@
+"""One training (or render) step of the fused path captured as a HIP graph and replayed.
+
+The fused step issues ~25 kernels through ~10 C-ABI calls plus torch's autograd between them;
+on small frames (c3: 512x512, ~0.3 ms of kernels) the host's Python/ctypes work per step is
+as long as the GPU's, so the GPU idles between launches.  Since the speculative binning
+(rasterize.SpeculativeBinning) took the host read of I out of the step, the whole step -- the
+fused preprocess, the binning, the blend with the L1 loss, the raster backward and the fused
+preprocess backward -- is a fixed launch sequence on one stream for a given frame shape and
+capacity, so it is captured once (torch.cuda.graph: every launch our C-ABI issues goes to the
+capturing stream) and replayed as one graph launch per step.
+
+What stays on the host per replay: the check of the binning's pinned count words
+(SpeculativeBinning.check_replay), written by the emission kernel early in the step while the
+GPU carries on.  A replay whose intersection count exceeded the captured capacity, or whose
+depth keys varied in a digit the capture assumed constant, produced an empty or wrong table;
+replay() then returns False, the owner re-runs the step eagerly (which re-bins) and the graph
+is captured again at the new capacity on the next call.  Replays read the step's inputs from
+the tensors they were captured with (parameters, camera, ground truth, background): update
+those in place.
+
+Single GPU only (the N > 1 step's collectives stay eager).  Reference step:
+gaussctrl/gc_pipeline.py:469-480 (loss, backward per view) around gc_model.py:158-222.
+"""
+from __future__ import annotations
+
+from typing import Callable, List, Optional, Sequence
+
+import torch
+
+from . import fused
+from .rasterize import GraphCaptureUnsupported
+
+
+class StepGraph:
+    """fn() -- one step on the current device -- as a replayable HIP graph.
+
+    params: tensors whose .grad the step assigns (autograd leaves); after each replay their
+    .grad are the graph's gradient tensors again (an eager fallback replaces them)."""
+
+    def __init__(self, fn: Callable[[], object], device, params: Sequence[torch.Tensor] = (),
+                 warmup: int = 2):
+        self.fn = fn
+        self.dev = torch.device(device)
+        self.params = list(params)
+        self.warmup = warmup
+        self.graph: Optional[torch.cuda.CUDAGraph] = None
+        self.specs: List = []
+        self.grads: List[Optional[torch.Tensor]] = []
+        self.result = None
+        self.replays = 0
+        self.fallbacks = 0
+        self.captures = 0
+        self.unsupported: Optional[str] = None
+
+    # ------------------------------------------------------------------ capture
+    def capture(self) -> bool:
+        """Warm up eagerly (capacity, key range, autograd and allocator state), then capture.
+        False (and the reason in .unsupported) when the step needs a host read of I."""
+        self.close()
+        cur = torch.cuda.current_stream(self.dev)
+        side = torch.cuda.Stream(self.dev)
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            for _ in range(self.warmup):
+                self.fn()
+        cur.wait_stream(side)
+        if fused.LAST_BINNING["mode"] != "speculative":
+            self.unsupported = f"binning mode {fused.LAST_BINNING['mode']!r}"
+            return False
+        for p in self.params:
+            p.grad = None
+        g = torch.cuda.CUDAGraph()
+        specs: list = []
+        fused._CAPTURE_SPECS = specs
+        try:
+            with torch.cuda.graph(g):
+                result = self.fn()
+        except GraphCaptureUnsupported as e:
+            for s in specs:
+                s.release()
+            self.unsupported = str(e)
+            return False
+        finally:
+            fused._CAPTURE_SPECS = None
+        if not specs:
+            self.unsupported = "the step launched no speculative binning"
+            return False
+        self.graph, self.specs, self.result = g, specs, result
+        self.grads = [p.grad for p in self.params]
+        self.captures += 1
+        self.unsupported = None
+        return True
+
+    def close(self):
+        for s in self.specs:
+            s.release()
+        self.specs, self.graph, self.result, self.grads = [], None, None, []
+
+    # ------------------------------------------------------------------ replay
+    def replay(self) -> bool:
+        """One step.  True: the replay's outputs (.result, the params' .grad) are valid.
+        False: they are not (capacity overflow / depth-range violation); run the step eagerly
+        -- step() does -- and the next call captures again."""
+        if self.graph is None:
+            raise RuntimeError("StepGraph.replay: nothing captured")
+        self.graph.replay()
+        stream = torch.cuda.current_stream(self.dev)
+        ok = True
+        for s in self.specs:
+            ok = s.check_replay(stream) and ok
+        self.replays += 1
+        if ok:
+            for p, g in zip(self.params, self.grads):
+                p.grad = g
+        return ok
+
+    def step(self):
+        """Replay (capturing first when needed); an invalid replay is redone eagerly and the
+        graph dropped so the next step captures again.  Returns the step's result."""
+        if self.graph is None and self.unsupported is None:
+            self.capture()
+        if self.graph is None:
+            return self.fn()
+        if self.replay():
+            return self.result
+        self.fallbacks += 1
+        self.close()
+        for p in self.params:
+            p.grad = None
+        return self.fn()
+
+    def stats(self) -> dict:
+        return {"replays": self.replays, "fallbacks": self.fallbacks,
+                "captures": self.captures, "unsupported": self.unsupported}

@@ -246,6 +246,33 @@ class SpeculativeBinning:
             _EMIT_CAP[self.key] = emit_capacity(I)
         return I <= self.cap and not self.range_violated
 
+    def check_replay(self, stream) -> bool:
+        """After a HIP-graph replay of the forward that launched this binning (graphs.StepGraph:
+        the captured forward skipped finish()): wait for the replay's count words, re-arm them
+        for the next replay.  False: I exceeded the capacity the graph was captured with, or a
+        depth digit assumed constant varied -- the replay's binning (and everything behind it)
+        is invalid, and the owner runs the step eagerly and captures it again."""
+        I = _wait_count(self.host, stream)
+        visible = int(self.host[0])
+        violated = int(self.host[2]) != 0
+        _note_key_range(self.key, self.host)
+        self.host[:2] = -1
+        self.host[2:] = 0
+        _COUNTS.last_visible[self.dev] = visible
+        self.num_intersects = I
+        if violated:
+            return False
+        if I > self.cap:  # the eager re-run starts from a capacity that holds this frame
+            _EMIT_CAP[self.key] = emit_capacity(I)
+            return False
+        return True
+
+    def release(self):
+        """Give the pinned count slot back (a graph holding this binning was dropped)."""
+        if self.slot is not None:
+            _COUNTS.release(self.dev, self.slot)
+            self.slot = None
+
     def rebin(self):
         """After an overflow (not a range violation): the emission and tile sort for the exact I
         (phase 1's workspace is untouched by the speculative launch) -> (ids [I], tile_bins)."""
@@ -273,14 +300,22 @@ def speculative_capacity(n: int, img_height: int, img_width: int, dev) -> int:
     return _EMIT_CAP.get((dev, n, tbx, tby), 0)
 
 
+class GraphCaptureUnsupported(RuntimeError):
+    """A binning that needs the host read of I (the first frame of a shape, or a scheme that
+    reads I before its emission) was asked for inside a HIP-graph capture: the step stays
+    eager (graphs.StepGraph)."""
+
+
 def bin_gaussians_speculative(xys: Tensor, depths: Tensor, radii: Tensor, num_tiles_hit: Tensor,
                               img_height: int, img_width: int,
-                              keyed_workspace: Optional[Tensor] = None):
+                              keyed_workspace: Optional[Tensor] = None, host_wait: bool = True):
     """bin_gaussians without the host read of I in the middle: the count phase, then -- when
     this frame shape's capacity is known from an earlier call and the binning scheme allows it
     -- the emission and the whole tile sort at that capacity (gsplat_bin_emit_speculative).
     Returns a SpeculativeBinning (finish() before using I), or None when the capacity is not
-    known yet or the scheme needs I on the host (the caller then uses bin_gaussians)."""
+    known yet or the scheme needs I on the host (the caller then uses bin_gaussians).
+    host_wait=False (a HIP-graph capture): a scheme that needs I on the host raises
+    GraphCaptureUnsupported before anything is launched."""
     n = xys.shape[0]
     tbx = (img_width + BLOCK_X - 1) // BLOCK_X
     tby = (img_height + BLOCK_Y - 1) // BLOCK_Y
@@ -300,6 +335,9 @@ def bin_gaussians_speculative(xys: Tensor, depths: Tensor, radii: Tensor, num_ti
         rc = _lib.call_status("gsplat_bin_speculative", n, cap, tbx, tby, P(counts), P(ws1),
                               ws1.numel(), _assumed_constant(key), P(ids_buf), P(tile_bins),
                               P(ws2), ws2.numel(), st)
+        if rc == 2 and not host_wait:  # (nothing was launched)
+            raise GraphCaptureUnsupported("bin_gaussians_speculative: the binning scheme of "
+                                          f"{cap} intersections reads I on the host")
         if rc == 2:  # the scheme needs I on the host: count, then finish as bin_gaussians does
             _lib.call("gsplat_bin_count_keyed_ex", n, tbx, tby, P(counts), P(ws1), ws1.numel(),
                       _assumed_constant(key), st)

@@ -24,11 +24,20 @@ class CallTimer:
     def _call(self, name, *args, _fn=None):
         s = torch.cuda.Event(enable_timing=True)
         e = torch.cuda.Event(enable_timing=True)
-        s.record()
+        # a call issued on another stream than the current one (the fused forward's colour
+        # part, concurrent with the binning): bracketed on that stream, and keyed apart
+        st = args[-1] if args and isinstance(args[-1], int) else None
+        side = st is not None and st != torch.cuda.current_stream().cuda_stream
+        ext = torch.cuda.ExternalStream(st) if side else None
+        s.record(ext)
         rc = (_fn or _orig_call)(name, *args)
-        e.record()
+        e.record(ext)
         # the list-split variants are the same entry (gsplat_rasterize_forward/_backward)
         key = name[:-len("_chunked")] if name.endswith("_chunked") else name
+        if name == "gsplat_fused_preprocess_forward_part":
+            key = f"{name}[{args[0]}]"
+        if side:
+            key += " (side stream)"
         self.events[key].append((s, e))
         return rc
 

@@ -398,6 +398,22 @@ int gsplat_fused_preprocess_forward_binned(
     float *xys, float *depths, int32_t *radii, float *conics, int32_t *num_tiles_hit,
     float *colors, float *opacity, void *bin_workspace, size_t bin_workspace_bytes,
     void *stream);
+/* gsplat_fused_preprocess_forward_binned in two parts for two streams: part 1 = the
+ * activations, projection, opacity and the binning's inputs (colors may be NULL); part 2 = the
+ * SH colours alone (reads means3d, features_dc, features_rest, campos; writes colors; every
+ * projection output and the workspace may be NULL).  Outputs equal the one-kernel forward's
+ * bit for bit.  The fused render issues part 2 on a second stream, where the colours' loads
+ * (12 K + 24 B per Gaussian) overlap the binning's latency-bound sort passes, joining before
+ * the blend.  (Same reference rows as the forward above: gc_model.py:172-215.) */
+int gsplat_fused_preprocess_forward_part(
+    int part, int num_points, int sh_bases, int degrees_to_use, const float *means3d,
+    const float *log_scales, const float *quats, const float *opacity_logits,
+    const float *features_dc, const float *features_rest, const float *viewmat,
+    const float *projmat, const float *campos, float fx, float fy, float cx, float cy,
+    int img_height, int img_width, int tile_bounds_x, int tile_bounds_y, float clip_thresh,
+    float *xys, float *depths, int32_t *radii, float *conics, int32_t *num_tiles_hit,
+    float *colors, float *opacity, void *bin_workspace, size_t bin_workspace_bytes,
+    void *stream);
 int gsplat_fused_preprocess_backward(
     int num_points, int sh_bases, int degrees_to_use, const float *means3d,
     const float *log_scales, const float *quats, const float *viewmat, const float *projmat,
