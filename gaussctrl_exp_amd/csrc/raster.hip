@@ -388,6 +388,35 @@ __device__ __forceinline__ bool stage_raw(const RawG &q, bool live, int idx, int
   }
   return keep;
 }
+// The forward's staging layout (one pixel per lane, no depth): two consecutive staged
+// Gaussians interleaved field by field, so an iteration reads both with five 16-B LDS reads and
+// evaluates their sigma / exp argument / alpha / 1 - alpha as packed pairs (v_pk_fma_f32 and
+// friends: the same IEEE operations as the scalar ones, so bit-identical) -- 54 -> ~38 VALU per
+// iteration of the VALU-issue-bound forward.  The colour of Gaussian u sits at rg[u] / bl[u] so
+// the red-green accumulation is one packed fma per Gaussian.
+struct __attribute__((aligned(16))) FPair {
+  f2 x, y, ha, b;
+  f2 hc, o, rg0, rg1;
+  f2 bl;
+  int idx[2];
+};
+static_assert(sizeof(FPair) == 80, "FPair layout");
+// the staged Gaussian s at rank q of the wave's batch
+__device__ __forceinline__ void fpair_put(FPair *pairs, int q, const GStage &s) {
+  FPair &P = pairs[q >> 1];
+  const int h = q & 1;
+  P.x[h] = s.x;
+  P.y[h] = s.y;
+  P.ha[h] = s.ha;
+  P.b[h] = s.b;
+  P.hc[h] = s.hc;
+  P.o[h] = s.o;
+  if (h) P.rg1 = f2{s.r, s.g};
+  else P.rg0 = f2{s.r, s.g};
+  P.bl[h] = s.bl;
+  P.idx[h] = s.idx;
+}
+
 // The pipeline state: ids of batch k+1 (loaded) and k+2 (in flight), data of batch k+1 (in
 // flight).
 struct StagePipe {
@@ -485,10 +514,12 @@ __device__ __forceinline__ int wave_incl_scan(int v) {
 #ifndef GS_STAGE_AHEAD
 #define GS_STAGE_AHEAD 1
 #endif
-template <typename StageF, typename BlendF>
-__device__ __forceinline__ void walk_kept(const KeepSrc &S, int top, int bottom, GStage *stage,
-                                          int2 *ahead, const int *__restrict__ gids,
-                                          StageF &&stage_one, BlendF &&blend) {
+// put(slot, s): where slot `slot`'s record goes (s == nullptr: the slot is past the round's
+// count); walk_kept stores GStage records at stage[slot].
+template <typename StageF, typename BlendF, typename PutF>
+__device__ __forceinline__ void walk_kept_put(const KeepSrc &S, int top, int bottom,
+                                              int2 *ahead, const int *__restrict__ gids,
+                                              StageF &&stage_one, BlendF &&blend, PutF &&put) {
   const int lane = __lane_id();
   for (int wtop = top; wtop >= bottom; wtop -= 4096) {
     const int tp = wtop - 64 * lane;
@@ -531,7 +562,9 @@ __device__ __forceinline__ void walk_kept(const KeepSrc &S, int top, int bottom,
       if (cur.x >= 0) {
         GStage s;
         stage_one(cur.x, cur.y, s);
-        stage[lane] = s;
+        put(lane, &s);
+      } else {
+        put(lane, (const GStage *)nullptr);
       }
       ahead[lane] = nxt;
 #else
@@ -539,13 +572,62 @@ __device__ __forceinline__ void walk_kept(const KeepSrc &S, int top, int bottom,
       GStage s;
       if (pcur >= 0) {
         stage_one(pcur, gids[pcur], s);
-        stage[lane] = s;
+        put(lane, &s);
+      } else {
+        put(lane, (const GStage *)nullptr);
       }
 #endif
       wave_lds_sync();
       blend(min(64, total - r));
       wave_lds_sync();
     }
+  }
+}
+template <typename StageF, typename BlendF>
+__device__ __forceinline__ void walk_kept(const KeepSrc &S, int top, int bottom, GStage *stage,
+                                          int2 *ahead, const int *__restrict__ gids,
+                                          StageF &&stage_one, BlendF &&blend) {
+  walk_kept_put(S, top, bottom, ahead, gids, stage_one, blend,
+                [&](int l, const GStage *s) {
+                  if (s) stage[l] = *s;
+                });
+}
+
+// The 8x8 backward's staging layout: two consecutive records interleaved field by field
+// (as FPair for the forward), so both Gaussians' sigma, exp argument, alpha, colour dot
+// product and moments are packed pairs.  A slot past the round's count holds a null record
+// (zero opacity and colour, finite geometry): alpha 0, never valid, finite terms.
+#ifndef GS_BWD8_PACKED
+#define GS_BWD8_PACKED 1
+#endif
+struct __attribute__((aligned(16))) BPair {
+  f2 x, y, ha, b;
+  f2 hc, o, r, g;
+  f2 bl;
+  int idx[2], id[2];
+  int pad[2];
+};
+static_assert(sizeof(BPair) == 96, "BPair layout");
+__device__ __forceinline__ void bpair_put(BPair *pairs, int q, const GStage *s) {
+  BPair &P = pairs[q >> 1];
+  const int h = q & 1;
+  if (s) {
+    P.x[h] = s->x;
+    P.y[h] = s->y;
+    P.ha[h] = s->ha;
+    P.b[h] = s->b;
+    P.hc[h] = s->hc;
+    P.o[h] = s->o;
+    P.r[h] = s->r;
+    P.g[h] = s->g;
+    P.bl[h] = s->bl;
+    P.idx[h] = s->idx;
+    P.id[h] = s->id;
+  } else {
+    P.x[h] = P.y[h] = P.ha[h] = P.b[h] = P.hc[h] = 0.f;
+    P.o[h] = P.r[h] = P.g[h] = P.bl[h] = 0.f;
+    P.idx[h] = 0x7FFFFFFF;
+    P.id[h] = 0;
   }
 }
 // stage_gaussian<true> without the cull (the forward's keep bits already decided it)
@@ -778,6 +860,10 @@ __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
   const float px = (float)j;
   const float rx0 = R.rx0, rx1 = R.rx1, ry0 = R.ry0, ry1 = R.ry1;
   constexpr int LROWS = 64 / COLS;
+  // one pixel per lane, no depth: the packed-pair blend (FPair)
+  constexpr bool PACKED = PXL == 1 && !DEPTH;
+  static_assert(sizeof(FPair) * 32 <= sizeof(GStage) * 64, "FPair slice fits the wave's slice");
+  f2 crg = {0.f, 0.f};  // (PACKED: red, green)
   float py[PXL], T[PXL], cr[PXL], cg[PXL], cb[PXL], cd[PXL];
   int cur[PXL];
   bool done[PXL];
@@ -792,6 +878,7 @@ __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
   }
   const int2 range = bins[tile];
   GStage *stage = lds[__builtin_amdgcn_readfirstlane(wave)];  // (uniform: SGPR address arithmetic)
+  FPair *pairs = reinterpret_cast<FPair *>(stage);
   unsigned c_slots = 0, c_live = 0, c_valid = 0;  // (CNT only)
   StagePipe pipe{};  // (PF: see RawG)
   if (PF && range.x < range.y) {
@@ -828,11 +915,71 @@ __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
     }
     if (DEPTH && keep) s.d = depths[s.id];
     const unsigned long long kmask = __ballot(keep);
-    if (keep) stage[lanes_below(kmask)] = s;
+    const int n = __popcll(kmask);
+    if constexpr (PACKED) {
+      if (keep) fpair_put(pairs, lanes_below(kmask), s);
+      // an odd batch leaves slot n unwritten: a zero colour there keeps 0 * colour finite
+      if ((n & 1) && lane == 0) {
+        pairs[n >> 1].rg1 = f2{0.f, 0.f};
+        pairs[n >> 1].bl[1] = 0.f;
+      }
+    } else {
+      if (keep) stage[lanes_below(kmask)] = s;
+    }
     kb_at = kb_base + ((b - range.x) >> 6);  // (stored with the next batch's loads, see above)
     kb_word = kmask;
-    const int n = __popcll(kmask);
     wave_lds_sync();
+    if constexpr (PACKED) {
+      // two staged Gaussians per iteration, their per-pixel terms as packed pairs; the
+      // transmittance / colour updates in list order exactly as the scalar loop below
+      const float px1 = px, py1 = py[0];
+      for (int t = 0; t < n; t += 2) {
+        const FPair P = pairs[t >> 1];
+        const bool live1 = t + 1 < n;
+        if constexpr (CNT) c_slots += 2 * 64;
+        const f2 dx = P.x - px1;
+        const f2 hA = P.ha * dx * dx, bdx = P.b * dx;
+        const f2 dy = P.y - py1;
+        const f2 sg = vfma(vfma(P.hc, dy, bdx), dy, hA);
+        const f2 e = sg * NEG_LOG2E;
+        const f2 ov = P.o * f2{__builtin_amdgcn_exp2f(e.x), __builtin_amdgcn_exp2f(e.y)};
+        const f2 al = f2{fminf(0.999f, ov.x), fminf(0.999f, ov.y)};
+        const f2 om = 1.f - al;
+        {
+          const bool v = !done[0] && sg.x >= 0.f && al.x >= ALPHA_MIN;
+          if constexpr (CNT) {
+            c_live += !done[0] ? 1u : 0u;
+            c_valid += v ? 1u : 0u;
+          }
+          const float nT = T[0] * om.x;
+          const bool term = v && nT <= 1e-4f, comp = v && !term;
+          done[0] = done[0] || term;
+          const float w = comp ? al.x * T[0] : 0.f;
+          crg = vfma(P.rg0, f2{w, w}, crg);
+          cb[0] += P.bl.x * w;
+          T[0] = comp ? nT : T[0];
+          cur[0] = comp ? P.idx[0] : cur[0];
+        }
+        {
+          const bool v = !done[0] && live1 && sg.y >= 0.f && al.y >= ALPHA_MIN;
+          if constexpr (CNT) {
+            c_live += (!done[0] && live1) ? 1u : 0u;
+            c_valid += v ? 1u : 0u;
+          }
+          const float nT = T[0] * om.y;
+          const bool term = v && nT <= 1e-4f, comp = v && !term;
+          done[0] = done[0] || term;
+          const float w = comp ? al.y * T[0] : 0.f;
+          crg = vfma(P.rg1, f2{w, w}, crg);
+          cb[0] += P.bl.y * w;
+          T[0] = comp ? nT : T[0];
+          cur[0] = comp ? P.idx[1] : cur[0];
+        }
+        if (__all(done[0])) break;
+      }
+      wave_lds_sync();
+      continue;
+    }
     for (int t = 0; t < n; t += 2) {
       GStage G[2];
       G[0] = stage_at(stage, t);
@@ -880,6 +1027,10 @@ __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
     wave_lds_sync();
   }
   if (kbits && kb_at >= 0 && lane == 0) kbits[kb_at] = kb_word;
+  if constexpr (PACKED) {
+    cr[0] = crg.x;
+    cg[0] = crg.y;
+  }
   const float bg0 = background[0], bg1 = background[1], bg2 = background[2];
 #pragma unroll
   for (int k = 0; k < PXL; ++k) {
@@ -1692,6 +1843,17 @@ __global__ __launch_bounds__(256) void raster_bwd8_kernel(
   const int field = slot >= 9 ? slot - 9 : slot;
   const float amax = __builtin_canonicalizef(alpha_max);
   GStage *stage = lds[__builtin_amdgcn_readfirstlane(wave)];  // (uniform: SGPR address arithmetic)
+  // the records as interleaved pairs (BPair): the two Gaussians of an iteration packed
+  static_assert(sizeof(BPair) * 32 <= sizeof(GStage) * 64, "BPair slice fits the wave's slice");
+  constexpr bool BP = GS_BWD8_PACKED;
+  BPair *pairs = reinterpret_cast<BPair *>(stage);
+  auto put = [&](int q, const GStage *sp) {
+    if constexpr (BP) {
+        bpair_put(pairs, q, sp);
+    } else {
+        if (sp) stage[q] = *sp;
+    }
+  };
   __shared__ int2 ahead_lds[4][64];  // (KB: walk_kept's next-round ids)
   int2 *ahead = ahead_lds[__builtin_amdgcn_readfirstlane(wave)];
   // this batch's staged Gaussian (b: the batch top, bottom: the lowest position staged)
@@ -1710,8 +1872,39 @@ __global__ __launch_bounds__(256) void raster_bwd8_kernel(
   auto stage1 = [&](int idx, int g, GStage &s) {
     stage_kept(idx, g, xys, conics, colors, opacity, s);
   };
+  // both Gaussians' per-pixel terms of pair t / 2 as packed pairs: sigma, alpha (masked by
+  // validity), the colour dot product gv; dx, dy and vis kept for the moments
+  struct PairTerms {
+    f2 dx, dy, vis, am, gv;
+    bool v0, v1;
+  };
+  auto pair_terms = [&](const BPair &P, bool live1) {
+    PairTerms q;
+    q.dx = P.x - px;
+    q.dy = P.y - py;
+    const f2 sg = vfma(vfma(P.hc, q.dy, P.b * q.dx), q.dy, P.ha * q.dx * q.dx);
+    const f2 e = sg * NEG_LOG2E;
+    q.vis = f2{__builtin_amdgcn_exp2f(e.x), __builtin_amdgcn_exp2f(e.y)};
+    const f2 ov = P.o * q.vis;
+    const f2 al = f2{fminf(amax, ov.x), fminf(amax, ov.y)};
+    q.v0 = P.idx[0] <= bf && sg.x >= 0.f && al.x >= ALPHA_MIN;
+    q.v1 = live1 && P.idx[1] <= bf && sg.y >= 0.f && al.y >= ALPHA_MIN;
+    q.am = f2{q.v0 ? al.x : 0.f, q.v1 ? al.y : 0.f};
+    q.gv = vfma(P.r, f2{vr, vr}, vfma(P.g, f2{vg, vg}, P.bl * f2{vb, vb}));
+    return q;
+  };
   auto pre_blend = [&](int n) {
-    for (int t = 0; t < n; ++t) {  // (the main loop's T / Qs operations, nothing else)
+    if constexpr (BP) {
+      for (int t = 0; t < n; t += 2) {  // (the main loop's T / Qs operations, nothing else)
+        const PairTerms q = pair_terms(pairs[t >> 1], t + 1 < n);
+        const f2 ra = f2{__builtin_amdgcn_rcpf(1.f - q.am.x), __builtin_amdgcn_rcpf(1.f - q.am.y)};
+        T = T * ra.x;
+        Qs = fmaf(-(q.am.x * T), q.gv.x, Qs);
+        T = T * ra.y;
+        Qs = fmaf(-(q.am.y * T), q.gv.y, Qs);
+      }
+    } else {
+      for (int t = 0; t < n; ++t) {  // (the main loop's T / Qs operations, nothing else)
         const GStage G = stage_at(stage, t);
         const float dx = G.x - px, dy = G.y - py;
         const float sg = gs_sigma(G.hc, G.b * dx, G.ha * dx * dx, dy);
@@ -1721,18 +1914,20 @@ __global__ __launch_bounds__(256) void raster_bwd8_kernel(
         T = T * __builtin_amdgcn_rcpf(1.f - am);
         const float fac = am * T;
         Qs = fmaf(-fac, fmaf(G.r, vr, fmaf(G.g, vg, G.bl * vb)), Qs);
+      }
     }
   };
   if (SPLIT) {  // the positions behind this part: T and the colour behind only
     if constexpr (KB) {
-      walk_kept(S, min(maxbin, range.y - 1), hi, stage, ahead, gids, stage1, pre_blend);
+      walk_kept_put(S, min(maxbin, range.y - 1), hi, ahead, gids, stage1, pre_blend, put);
     } else {
       for (int b = min(maxbin, range.y - 1); b >= hi; b -= 64) {
         GStage s;
         const bool keep = stage_next(b, hi, s);
         const unsigned long long kmask = __ballot(keep);
-        if (keep) stage[lanes_below(kmask)] = s;
         const int n = __popcll(kmask);
+        if (keep) put(lanes_below(kmask), &s);
+        if ((n & 1) && (threadIdx.x & 63) == 0) put(n, nullptr);
         wave_lds_sync();
         pre_blend(n);
         wave_lds_sync();
@@ -1742,69 +1937,116 @@ __global__ __launch_bounds__(256) void raster_bwd8_kernel(
   const int last = min(maxbin, hi - 1);
   unsigned c_slots = 0, c_live = 0, c_valid = 0;  // (CNT only)
   auto main_blend = [&](int n) {
-    for (int t = 0; t < n; t += 2) {
-      GStage G0 = stage_at(stage, t), G1 = stage_at(stage, min(t + 1, 63));
-      const bool live1 = t + 1 < n;
-      if (!live1) G1.r = G1.g = G1.bl = G1.o = 0.f;  // stale slot: alpha 0, finite terms
-      int gid0 = G0.id, gid1 = G1.id;
-      asm volatile("" : "+v"(gid0), "+v"(gid1));  // read with the records, not at the atomic
-      // the two Gaussians' per-pixel terms (independent)
-      const float dx0 = G0.x - px, dy0 = G0.y - py, dx1 = G1.x - px, dy1 = G1.y - py;
-      const float sg0 = gs_sigma(G0.hc, G0.b * dx0, G0.ha * dx0 * dx0, dy0);
-      const float sg1 = gs_sigma(G1.hc, G1.b * dx1, G1.ha * dx1 * dx1, dy1);
-      const float vis0 = gs_vis(sg0), vis1 = gs_vis(sg1);
-      const float al0 = fminf(amax, G0.o * vis0), al1 = fminf(amax, G1.o * vis1);
-      const bool v0 = G0.idx <= bf && sg0 >= 0.f && al0 >= ALPHA_MIN;
-      const bool v1 = live1 && G1.idx <= bf && sg1 >= 0.f && al1 >= ALPHA_MIN;
-      const unsigned long long any0 = __builtin_amdgcn_ballot_w64(v0),
-                               any1 = __builtin_amdgcn_ballot_w64(v1);
-      if constexpr (CNT) {
-        c_slots += 2 * 64;
-        c_live += (G0.idx <= bf ? 1u : 0u) + (live1 && G1.idx <= bf ? 1u : 0u);
-        c_valid += (v0 ? 1u : 0u) + (v1 ? 1u : 0u);
+    if constexpr (BP) {
+      for (int t = 0; t < n; t += 2) {
+        const BPair &P = pairs[t >> 1];
+        const bool live1 = t + 1 < n;
+        int gid0 = P.id[0], gid1 = P.id[1];
+        asm volatile("" : "+v"(gid0), "+v"(gid1));  // read with the records, not at the atomic
+        // the two Gaussians' per-pixel terms (independent), packed
+        const PairTerms q = pair_terms(P, live1);
+        const unsigned long long any0 = __builtin_amdgcn_ballot_w64(q.v0),
+                                 any1 = __builtin_amdgcn_ballot_w64(q.v1);
+        if constexpr (CNT) {
+          c_slots += 2 * 64;
+          c_live += (P.idx[0] <= bf ? 1u : 0u) + (live1 && P.idx[1] <= bf ? 1u : 0u);
+          c_valid += (q.v0 ? 1u : 0u) + (q.v1 ? 1u : 0u);
+        }
+        // list order (back to front): G0 then G1 -- T and the colour behind are sequential
+        const f2 ra = f2{__builtin_amdgcn_rcpf(1.f - q.am.x), __builtin_amdgcn_rcpf(1.f - q.am.y)};
+        T = T * ra.x;
+        const float fac0 = q.am.x * T;
+        const float va0 = fmaf(q.gv.x, T, ra.x * Qs);
+        Qs = fmaf(-fac0, q.gv.x, Qs);
+        T = T * ra.y;
+        const float fac1 = q.am.y * T;
+        const float va1 = fmaf(q.gv.y, T, ra.y * Qs);
+        Qs = fmaf(-fac1, q.gv.y, Qs);
+        if (any0 | any1) {  // (an SGPR test)
+          const f2 w = f2{q.v0 ? q.vis.x : 0.f, q.v1 ? q.vis.y : 0.f} * f2{va0, va1};
+          const f2 sx = q.dx * w, sy = q.dy * w;
+          const f2 xx = q.dx * sx, yx = q.dy * sx, yy = q.dy * sy;
+          const f2 fac = f2{fac0, fac1};
+          const f2 fr = fac * vr, fg = fac * vg, fb = fac * vb;
+          const float m[18] = {sx.x, sy.x, xx.x, yx.x, yy.x, fr.x, fg.x, fb.x, w.x,
+                               sx.y, sy.y, xx.y, yx.y, yy.y, fr.y, fg.y, fb.y, w.y};
+          const float v = reduce18(m);
+          const bool act = (for0 && any0) || (for1 && any1);
+          const int g = for1 ? gid1 : gid0;
+          if constexpr (DET) {
+            if (act) det_add(det + ((size_t)g * REC_FIELDS + field) * DET_LIMBS, v);
+          } else {
+            // 32-bit element offset (the entry points reject N >= 2^27)
+            if (act) atomicAdd(rec + (uint32_t)(g * REC + field), v);
+          }
+        }
       }
-      // list order (back to front): G0 then G1 -- T and the colour behind are sequential
-      const float am0 = v0 ? al0 : 0.f, am1 = v1 ? al1 : 0.f;
-      const float ra0 = __builtin_amdgcn_rcpf(1.f - am0);
-      T = T * ra0;
-      const float fac0 = am0 * T;
-      const float gv0 = fmaf(G0.r, vr, fmaf(G0.g, vg, G0.bl * vb));
-      const float va0 = fmaf(gv0, T, ra0 * Qs);
-      Qs = fmaf(-fac0, gv0, Qs);
-      const float ra1 = __builtin_amdgcn_rcpf(1.f - am1);
-      T = T * ra1;
-      const float fac1 = am1 * T;
-      const float gv1 = fmaf(G1.r, vr, fmaf(G1.g, vg, G1.bl * vb));
-      const float va1 = fmaf(gv1, T, ra1 * Qs);
-      Qs = fmaf(-fac1, gv1, Qs);
-      if (any0 | any1) {  // (an SGPR test)
-        const float w0 = (v0 ? vis0 : 0.f) * va0, w1 = (v1 ? vis1 : 0.f) * va1;
-        const float sx0 = dx0 * w0, sy0 = dy0 * w0, sx1 = dx1 * w1, sy1 = dy1 * w1;
-        const float m[18] = {sx0, sy0, dx0 * sx0, dy0 * sx0, dy0 * sy0,
-                             fac0 * vr, fac0 * vg, fac0 * vb, w0,
-                             sx1, sy1, dx1 * sx1, dy1 * sx1, dy1 * sy1,
-                             fac1 * vr, fac1 * vg, fac1 * vb, w1};
-        const float v = reduce18(m);
-        const bool act = (for0 && any0) || (for1 && any1);
-        const int g = for1 ? gid1 : gid0;
-        if constexpr (DET) {
-          if (act) det_add(det + ((size_t)g * REC_FIELDS + field) * DET_LIMBS, v);
-        } else {
-          // 32-bit element offset (the entry points reject N >= 2^27)
-          if (act) atomicAdd(rec + (uint32_t)(g * REC + field), v);
+    } else {
+      for (int t = 0; t < n; t += 2) {
+        GStage G0 = stage_at(stage, t), G1 = stage_at(stage, min(t + 1, 63));
+        const bool live1 = t + 1 < n;
+        if (!live1) G1.r = G1.g = G1.bl = G1.o = 0.f;  // stale slot: alpha 0, finite terms
+        int gid0 = G0.id, gid1 = G1.id;
+        asm volatile("" : "+v"(gid0), "+v"(gid1));  // read with the records, not at the atomic
+        // the two Gaussians' per-pixel terms (independent)
+        const float dx0 = G0.x - px, dy0 = G0.y - py, dx1 = G1.x - px, dy1 = G1.y - py;
+        const float sg0 = gs_sigma(G0.hc, G0.b * dx0, G0.ha * dx0 * dx0, dy0);
+        const float sg1 = gs_sigma(G1.hc, G1.b * dx1, G1.ha * dx1 * dx1, dy1);
+        const float vis0 = gs_vis(sg0), vis1 = gs_vis(sg1);
+        const float al0 = fminf(amax, G0.o * vis0), al1 = fminf(amax, G1.o * vis1);
+        const bool v0 = G0.idx <= bf && sg0 >= 0.f && al0 >= ALPHA_MIN;
+        const bool v1 = live1 && G1.idx <= bf && sg1 >= 0.f && al1 >= ALPHA_MIN;
+        const unsigned long long any0 = __builtin_amdgcn_ballot_w64(v0),
+                                 any1 = __builtin_amdgcn_ballot_w64(v1);
+        if constexpr (CNT) {
+          c_slots += 2 * 64;
+          c_live += (G0.idx <= bf ? 1u : 0u) + (live1 && G1.idx <= bf ? 1u : 0u);
+          c_valid += (v0 ? 1u : 0u) + (v1 ? 1u : 0u);
+        }
+        // list order (back to front): G0 then G1 -- T and the colour behind are sequential
+        const float am0 = v0 ? al0 : 0.f, am1 = v1 ? al1 : 0.f;
+        const float ra0 = __builtin_amdgcn_rcpf(1.f - am0);
+        T = T * ra0;
+        const float fac0 = am0 * T;
+        const float gv0 = fmaf(G0.r, vr, fmaf(G0.g, vg, G0.bl * vb));
+        const float va0 = fmaf(gv0, T, ra0 * Qs);
+        Qs = fmaf(-fac0, gv0, Qs);
+        const float ra1 = __builtin_amdgcn_rcpf(1.f - am1);
+        T = T * ra1;
+        const float fac1 = am1 * T;
+        const float gv1 = fmaf(G1.r, vr, fmaf(G1.g, vg, G1.bl * vb));
+        const float va1 = fmaf(gv1, T, ra1 * Qs);
+        Qs = fmaf(-fac1, gv1, Qs);
+        if (any0 | any1) {  // (an SGPR test)
+          const float w0 = (v0 ? vis0 : 0.f) * va0, w1 = (v1 ? vis1 : 0.f) * va1;
+          const float sx0 = dx0 * w0, sy0 = dy0 * w0, sx1 = dx1 * w1, sy1 = dy1 * w1;
+          const float m[18] = {sx0, sy0, dx0 * sx0, dy0 * sx0, dy0 * sy0,
+                               fac0 * vr, fac0 * vg, fac0 * vb, w0,
+                               sx1, sy1, dx1 * sx1, dy1 * sx1, dy1 * sy1,
+                               fac1 * vr, fac1 * vg, fac1 * vb, w1};
+          const float v = reduce18(m);
+          const bool act = (for0 && any0) || (for1 && any1);
+          const int g = for1 ? gid1 : gid0;
+          if constexpr (DET) {
+            if (act) det_add(det + ((size_t)g * REC_FIELDS + field) * DET_LIMBS, v);
+          } else {
+            // 32-bit element offset (the entry points reject N >= 2^27)
+            if (act) atomicAdd(rec + (uint32_t)(g * REC + field), v);
+          }
         }
       }
     }
   };
   if constexpr (KB) {
-    walk_kept(S, last, lo, stage, ahead, gids, stage1, main_blend);
+    walk_kept_put(S, last, lo, ahead, gids, stage1, main_blend, put);
   } else {
     for (int b = last; b >= lo; b -= 64) {
       GStage s;
       const bool keep = stage_next(b, lo, s);
       const unsigned long long kmask = __ballot(keep);
-      if (keep) stage[lanes_below(kmask)] = s;
       const int n = __popcll(kmask);
+      if (keep) put(lanes_below(kmask), &s);
+      if ((n & 1) && (threadIdx.x & 63) == 0) put(n, nullptr);
       wave_lds_sync();
       main_blend(n);
       wave_lds_sync();
