@@ -654,18 +654,35 @@ def main():
     # full train step: splatfacto loss + backward + all-reduce + Adam
     tsteps = args.train_steps if args.train_steps is not None else args.steps
     trainer.loss_kind = "splatfacto"
-    for _ in range(2):
-        trainer.step(cam, gt)
-    barrier()
-    t0 = time.perf_counter()
-    for _ in range(tsteps):
-        trainer.step(cam, gt)
-    barrier()
-    tdt = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([tdt], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        tdt = float(t.item())
+    # one GPU: the train step replayed as a HIP graph too (its Adam schedule on the device)
+    tgraph = None
+    if graph is not None:
+        tgraph = StepGraph(lambda: trainer.step(cam, gt, device_schedule=True), dev,
+                           after_capture=lambda: trainer.advance_step_count(-1),
+                           after_replay=trainer.advance_step_count)
+
+    def train_step():
+        if tgraph is not None:
+            tgraph.step()
+        else:
+            trainer.step(cam, gt)
+
+    def train_time(fn):
+        for _ in range(2):
+            fn()
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(tsteps):
+            fn()
+        barrier()
+        tdt = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([tdt], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            tdt = float(t.item())
+        return tdt
+    tdt = train_time(train_step)
+    tdt_eager = train_time(lambda: trainer.step(cam, gt)) if tgraph is not None else None
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -710,6 +727,9 @@ def main():
             "value_eager_launches": round(eager_value, 2) if eager_value else None,
             "value_unchanged_caller": round(caller_value, 2),
             "train_iters_per_s": round(tsteps / tdt, 2),
+            "train_iters_per_s_eager_launches": round(tsteps / tdt_eager, 2) if tdt_eager
+                                                else None,
+            "train_graph": tgraph.stats() if tgraph is not None else None,
             "train_views_per_s": round(world * tsteps / tdt, 2),
             "roofline": roofline,
             "lane_occupancy": lanes,

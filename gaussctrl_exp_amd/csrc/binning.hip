@@ -2310,6 +2310,13 @@ extern "C" size_t gsplat_bin_count_workspace_size(int num_points) {
   return carve_phase1(nullptr, num_points).bytes;
 }
 
+// Byte offset, in a gsplat_bin_count workspace, of the device word holding the speculative
+// binning's intersection count (0xFFFFFFFF after a depth-range violation): the scheduled Adam
+// step's validity check (gsplat_fused_preprocess_backward_adam_sched).
+extern "C" size_t gsplat_bin_device_count_offset(int num_points) {
+  return (size_t)((const char *)carve_phase1(nullptr, num_points).dcount - (const char *)nullptr);
+}
+
 extern "C" size_t gsplat_bin_emit_workspace_size(int64_t num_intersects) {
   return carve_phase2(nullptr, num_intersects).bytes;
 }

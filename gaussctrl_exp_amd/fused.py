@@ -262,6 +262,14 @@ class _FusedRender(Function):
                     raise ValueError("render_fused: in-backward Adam needs the parameters "
                                      "themselves (contiguous fp32), not copies")
         ctx.adam = adam
+        # a captured step's device-scheduled Adam checks the binning's device count word itself
+        # (a replay whose binning overflowed must not move the parameters): the word lives in
+        # ws1, kept alive for the backward
+        ctx.bin_word = None
+        if capturing and adam is not None and "sched" in adam:
+            ctx.ws1 = ws1
+            ctx.bin_word = (ws1.data_ptr() + _lib.query("gsplat_bin_device_count_offset", n),
+                            int(spec.cap))
         ctx.save_for_backward(means, scales, quats, opacities, features_dc, features_rest,
                               viewmat, projmat, campos,
                               background, xys, radii, conics, colors, opac, gids, bins, final_Ts,
@@ -313,13 +321,18 @@ class _FusedRender(Function):
             # Adam inside the backward: parameters (and moments) updated in place, no gradients
             a = ctx.adam
             cast = ctypes.cast
-            _lib.call("gsplat_fused_preprocess_backward_adam", n, K, dtu, P(means), P(scales),
-                      P(quats), P(opacities), P(features_dc),
-                      P(features_rest) if K > 1 else None, P(viewmat), P(projmat), P(campos),
-                      fx, fy, cx, cy, H, W, P(radii), P(conics), P(colors), P(opac), P(rec),
-                      cast(a["exp_avgs"], ctypes.c_void_p), cast(a["exp_avg_sqs"], ctypes.c_void_p),
-                      cast(a["lrs"], ctypes.c_void_p), int(a["step"]), float(a["betas"][0]),
-                      float(a["betas"][1]), float(a["eps"]), st)
+            head = (n, K, dtu, P(means), P(scales), P(quats), P(opacities), P(features_dc),
+                    P(features_rest) if K > 1 else None, P(viewmat), P(projmat), P(campos),
+                    fx, fy, cx, cy, H, W, P(radii), P(conics), P(colors), P(opac), P(rec),
+                    cast(a["exp_avgs"], ctypes.c_void_p), cast(a["exp_avg_sqs"], ctypes.c_void_p))
+            tail = (float(a["betas"][0]), float(a["betas"][1]), float(a["eps"]), st)
+            if "sched" in a:  # the device schedule (a replayable step: TrainStep.device_schedule)
+                word, cap = ctx.bin_word if ctx.bin_word is not None else (None, 0)
+                _lib.call("gsplat_fused_preprocess_backward_adam_sched", *head, P(a["sched"]),
+                          int(a["sched_len"]), P(a["counter"]), word, cap, *tail)
+            else:
+                _lib.call("gsplat_fused_preprocess_backward_adam", *head,
+                          cast(a["lrs"], ctypes.c_void_p), int(a["step"]), *tail)
             return (None,) * 21
         f32 = dict(device=dev, dtype=torch.float32)
         xchg = ctx.exchange

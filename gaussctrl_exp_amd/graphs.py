@@ -18,6 +18,12 @@ is captured again at the new capacity on the next call.  Replays read the step's
 the tensors they were captured with (parameters, camera, ground truth, background): update
 those in place.
 
+A training step with the in-backward Adam is replayable too when its schedule lives on the
+device (TrainStep.step(device_schedule=True): the learning rates and bias corrections from a
+table indexed by a device step counter, and the Adam kernel itself skips the update when the
+binning's device count word says the replay overflowed), with after_capture / after_replay
+keeping the host's step count in step.
+
 Single GPU only (the N > 1 step's collectives stay eager).  Reference step:
 gaussctrl/gc_pipeline.py:469-480 (loss, backward per view) around gc_model.py:158-222.
 """
@@ -38,8 +44,14 @@ class StepGraph:
     .grad are the graph's gradient tensors again (an eager fallback replaces them)."""
 
     def __init__(self, fn: Callable[[], object], device, params: Sequence[torch.Tensor] = (),
-                 warmup: int = 2):
+                 warmup: int = 2, after_capture: Optional[Callable[[], None]] = None,
+                 after_replay: Optional[Callable[[], None]] = None):
         self.fn = fn
+        # host bookkeeping of a step whose effects live on the device (a training step's step
+        # count: TrainStep.advance_step_count): undone after the capture (which ran nothing),
+        # redone after each valid replay
+        self.after_capture = after_capture
+        self.after_replay = after_replay
         self.dev = torch.device(device)
         self.params = list(params)
         self.warmup = warmup
@@ -82,6 +94,8 @@ class StepGraph:
             return False
         finally:
             fused._CAPTURE_SPECS = None
+        if self.after_capture is not None:
+            self.after_capture()
         if not specs:
             self.unsupported = "the step launched no speculative binning"
             return False
@@ -112,6 +126,8 @@ class StepGraph:
         if ok:
             for p, g in zip(self.params, self.grads):
                 p.grad = g
+            if self.after_replay is not None:
+                self.after_replay()
         return ok
 
     def step(self):
