@@ -466,9 +466,10 @@ def main():
                          "kernels out of the PMC and kernel-trace summaries)")
     ap.add_argument("--forward-only", action="store_true",
                     help="time the render without backward (default for config c2)")
-    ap.add_argument("--graph", default="auto", choices=("auto", "off"),
-                    help="auto: one GPU replays the fused step as a HIP graph (graphs.py); "
-                         "off: every step issued eagerly")
+    ap.add_argument("--graph", default=os.environ.get("BENCH_GRAPH", "off"),
+                    choices=("on", "off"),
+                    help="on: one GPU replays the fused step (and the train step) as a HIP "
+                         "graph (graphs.py); off (default, measured faster): issued eagerly")
     ap.add_argument("--render", default="fused", choices=("fused", "caller"),
                     help="fused: the caller's activations inside the HIP kernels (default); "
                          "caller: gc_model.py's torch glue around the gsplat API")
@@ -519,8 +520,12 @@ def main():
     # the fused step replayed as one HIP graph (graphs.StepGraph: captured after eager warm-up
     # steps; every replay's binning counts checked on the host, an overflow re-run eagerly).
     # One GPU only: the N > 1 step's collectives stay eager.
+    # --graph on: the step replayed as a HIP graph (graphs.StepGraph).  Off by default: on ROCm
+    # 7 a replayed graph of this step runs slower than the same launches issued from the stream
+    # (round 4, same box: headline 0.761 vs 0.748 ms/step, c3 0.403 vs 0.392 ms; the eager c3
+    # step is already within ~5 % of its kernel time)
     graph = None
-    if args.graph == "auto" and world == 1 and args.render == "fused":
+    if world == 1 and args.render == "fused" and args.graph == "on":
         graph = StepGraph(step_eager, dev, params=() if fwd_only else trainer.params)
 
     def step(t=trainer):

@@ -394,6 +394,13 @@ __device__ __forceinline__ bool stage_raw(const RawG &q, bool live, int idx, int
 // friends: the same IEEE operations as the scalar ones, so bit-identical) -- 54 -> ~38 VALU per
 // iteration of the VALU-issue-bound forward.  The colour of Gaussian u sits at rg[u] / bl[u] so
 // the red-green accumulation is one packed fma per Gaussian.
+// The packed-pair forward (FPair) is off: measured slower than the scalar two-Gaussian loop
+// despite 54 -> 39 VALU per iteration (round 4, same-box A/B: headline forward 0.1461 ->
+// 0.1486-0.1506 ms, c3 0.0975 -> 0.1018-0.1021 ms) -- the five 16-B LDS reads of an iteration
+// and the longer dependent chain of the packed operations cost more than the issue slots saved.
+#ifndef GS_FWD_PACKED
+#define GS_FWD_PACKED 0
+#endif
 struct __attribute__((aligned(16))) FPair {
   f2 x, y, ha, b;
   f2 hc, o, rg0, rg1;
@@ -597,8 +604,11 @@ __device__ __forceinline__ void walk_kept(const KeepSrc &S, int top, int bottom,
 // (as FPair for the forward), so both Gaussians' sigma, exp argument, alpha, colour dot
 // product and moments are packed pairs.  A slot past the round's count holds a null record
 // (zero opacity and colour, finite geometry): alpha 0, never valid, finite terms.
+// The packed-pair 8x8 backward (BPair) is off: 132 -> 117 VALU per iteration but 62 -> 72 VGPRs
+// (occupancy 8 -> 7), measured slower (round 4, same-box A/B: c3 record backward 0.1083 ->
+// 0.1106 ms).
 #ifndef GS_BWD8_PACKED
-#define GS_BWD8_PACKED 1
+#define GS_BWD8_PACKED 0
 #endif
 struct __attribute__((aligned(16))) BPair {
   f2 x, y, ha, b;
@@ -861,7 +871,7 @@ __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
   const float rx0 = R.rx0, rx1 = R.rx1, ry0 = R.ry0, ry1 = R.ry1;
   constexpr int LROWS = 64 / COLS;
   // one pixel per lane, no depth: the packed-pair blend (FPair)
-  constexpr bool PACKED = PXL == 1 && !DEPTH;
+  constexpr bool PACKED = GS_FWD_PACKED && PXL == 1 && !DEPTH;
   static_assert(sizeof(FPair) * 32 <= sizeof(GStage) * 64, "FPair slice fits the wave's slice");
   f2 crg = {0.f, 0.f};  // (PACKED: red, green)
   float py[PXL], T[PXL], cr[PXL], cg[PXL], cb[PXL], cd[PXL];

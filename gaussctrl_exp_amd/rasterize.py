@@ -332,8 +332,12 @@ def bin_gaussians_speculative(xys: Tensor, depths: Tensor, radii: Tensor, num_ti
     slot, counts, host = _COUNTS.acquire(dev)
     try:
         # count phase, emission (with the allotment scan) and tile sort in one call
+        # a captured binning (host_wait False) assumes no constant depth digit: every later
+        # replay sorts all four passes, so a depth range that changes between replays can never
+        # invalidate it (the capacity is the only thing a replay checks)
+        assume = _assumed_constant(key) if host_wait else 0
         rc = _lib.call_status("gsplat_bin_speculative", n, cap, tbx, tby, P(counts), P(ws1),
-                              ws1.numel(), _assumed_constant(key), P(ids_buf), P(tile_bins),
+                              ws1.numel(), assume, P(ids_buf), P(tile_bins),
                               P(ws2), ws2.numel(), st)
         if rc == 2 and not host_wait:  # (nothing was launched)
             raise GraphCaptureUnsupported("bin_gaussians_speculative: the binning scheme of "
