@@ -51,6 +51,7 @@ LAST_BINNING = {"mode": None}
 # the preprocess's SH-colour part on a second stream, overlapping the binning
 # (gsplat_fused_preprocess_forward_part); GSPLAT_MI355X_SPLIT_COLOURS=0: one kernel (A/B runs)
 SPLIT_COLOURS = os.environ.get("GSPLAT_MI355X_SPLIT_COLOURS", "1") != "0"
+SPLIT_COLOURS_MIN_TILES = 3584  # (the blend kernels' small-frame threshold as well)
 _SIDE = {}
 
 
@@ -98,7 +99,9 @@ class _FusedRender(Function):
                           device=dev, dtype=torch.uint8)
         cam_args = (P(viewmat), P(projmat), P(campos), float(fx), float(fy), float(cx),
                     float(cy), H, W, tbx, tby, 0.01)
-        split_colours = K > 1 and SPLIT_COLOURS
+        # (frames from SPLIT_COLOURS_MIN_TILES tiles: on small frames the second stream's
+        # event work costs the host more than the overlap saves -- c3 step 0.371 -> 0.402 ms)
+        split_colours = K > 1 and SPLIT_COLOURS and tbx * tby >= SPLIT_COLOURS_MIN_TILES
 
         def preprocess():
             """The preprocess; with split_colours its SH-colour part goes out on a second

@@ -44,7 +44,7 @@ class StepGraph:
     .grad are the graph's gradient tensors again (an eager fallback replaces them)."""
 
     def __init__(self, fn: Callable[[], object], device, params: Sequence[torch.Tensor] = (),
-                 warmup: int = 2, after_capture: Optional[Callable[[], None]] = None,
+                 warmup: int = 1, after_capture: Optional[Callable[[], None]] = None,
                  after_replay: Optional[Callable[[], None]] = None):
         self.fn = fn
         # host bookkeeping of a step whose effects live on the device (a training step's step
@@ -63,18 +63,20 @@ class StepGraph:
         self.fallbacks = 0
         self.captures = 0
         self.unsupported: Optional[str] = None
+        self.warm_result = None
 
     # ------------------------------------------------------------------ capture
     def capture(self) -> bool:
-        """Warm up eagerly (capacity, key range, autograd and allocator state), then capture.
+        """Warm up eagerly (capacity, key range, autograd and allocator state: `warmup` real
+        steps, the last one's result kept in .warm_result), then capture (which runs nothing).
         False (and the reason in .unsupported) when the step needs a host read of I."""
         self.close()
         cur = torch.cuda.current_stream(self.dev)
         side = torch.cuda.Stream(self.dev)
         side.wait_stream(cur)
         with torch.cuda.stream(side):
-            for _ in range(self.warmup):
-                self.fn()
+            for _ in range(max(self.warmup, 1)):
+                self.warm_result = self.fn()
         cur.wait_stream(side)
         if fused.LAST_BINNING["mode"] != "speculative":
             self.unsupported = f"binning mode {fused.LAST_BINNING['mode']!r}"
@@ -131,10 +133,15 @@ class StepGraph:
         return ok
 
     def step(self):
-        """Replay (capturing first when needed); an invalid replay is redone eagerly and the
-        graph dropped so the next step captures again.  Returns the step's result."""
+        """One step: a replay, or -- when nothing is captured yet -- the warm-up (its last eager
+        step is this call's step) and the capture; an invalid replay is redone eagerly and the
+        graph dropped so the next step captures again.  Returns the step's result.  With
+        warmup = 1 every call is exactly one step (a training loop's step count holds)."""
         if self.graph is None and self.unsupported is None:
             self.capture()
+            if self.warmup <= 1:
+                return self.warm_result
+            # (more warm-up steps than one: the calls before the capture were extra steps)
         if self.graph is None:
             return self.fn()
         if self.replay():

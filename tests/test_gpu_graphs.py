@@ -73,8 +73,8 @@ def test_graphed_step_equals_eager(gpu):
     sg = StepGraph(_stepper(tr, cam, gt, bg), gpu, params=tr.params)
     for k in range(3):
         _close(_graphed(sg, tr), ref, f"replay {k}")
-    st = sg.stats()
-    assert st["captures"] == 1 and st["fallbacks"] == 0 and st["replays"] == 3, st
+    st = sg.stats()  # (the first call: the warm-up step and the capture, then two replays)
+    assert st["captures"] == 1 and st["fallbacks"] == 0 and st["replays"] == 2, st
     # an in-place parameter update is seen by the next replay
     with torch.no_grad():
         sc.opacities.add_(0.25)

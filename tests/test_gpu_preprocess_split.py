@@ -71,7 +71,8 @@ def test_split_render_bit_identical(gpu):
     v_img = torch.rand(384, 512, 3, generator=g).to(gpu)
     outs = {}
     prev_det = _lib.set_deterministic(True)
-    prev = fused.SPLIT_COLOURS
+    prev = fused.SPLIT_COLOURS, fused.SPLIT_COLOURS_MIN_TILES
+    fused.SPLIT_COLOURS_MIN_TILES = 0  # (a small frame: split regardless of its size)
     try:
         for split in (False, True, False, True):  # (second round: capacity-launched binning)
             fused.SPLIT_COLOURS = split
@@ -82,7 +83,7 @@ def test_split_render_bit_identical(gpu):
                            r["accumulation"].detach().cpu().numpy()] + \
                 [t.grad.cpu().numpy() for t in s.params()]
     finally:
-        fused.SPLIT_COLOURS = prev
+        fused.SPLIT_COLOURS, fused.SPLIT_COLOURS_MIN_TILES = prev
         _lib.set_deterministic(prev_det)
     for name, x, y in zip(("rgb", "alpha", "means", "scales", "quats", "opacities", "dc", "rest"),
                           outs[True], outs[False]):
