@@ -64,6 +64,7 @@ class StepGraph:
         self.captures = 0
         self.unsupported: Optional[str] = None
         self.warm_result = None
+        self.warm_grads: List[Optional[torch.Tensor]] = []
 
     # ------------------------------------------------------------------ capture
     def capture(self) -> bool:
@@ -78,6 +79,8 @@ class StepGraph:
             for _ in range(max(self.warmup, 1)):
                 self.warm_result = self.fn()
         cur.wait_stream(side)
+        # the warm-up step's gradients (the capture below assigns the graph's own, unexecuted)
+        self.warm_grads = [p.grad for p in self.params]
         if fused.LAST_BINNING["mode"] != "speculative":
             self.unsupported = f"binning mode {fused.LAST_BINNING['mode']!r}"
             return False
@@ -140,6 +143,8 @@ class StepGraph:
         if self.graph is None and self.unsupported is None:
             self.capture()
             if self.warmup <= 1:
+                for p, g in zip(self.params, self.warm_grads):
+                    p.grad = g
                 return self.warm_result
             # (more warm-up steps than one: the calls before the capture were extra steps)
         if self.graph is None:
