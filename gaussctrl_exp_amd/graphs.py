@@ -81,8 +81,12 @@ class StepGraph:
         cur.wait_stream(side)
         # the warm-up step's gradients (the capture below assigns the graph's own, unexecuted)
         self.warm_grads = [p.grad for p in self.params]
-        if fused.LAST_BINNING["mode"] != "speculative":
-            self.unsupported = f"binning mode {fused.LAST_BINNING['mode']!r}"
+        mode = fused.LAST_BINNING["mode"]
+        if mode != "speculative":
+            # "sync": the frame shape's first binning (no capacity known yet) -- the next call
+            # tries again; "host": a scheme that reads I on the host -- never capturable
+            if mode == "host":
+                self.unsupported = "binning mode 'host'"
             return False
         for p in self.params:
             p.grad = None
@@ -142,7 +146,7 @@ class StepGraph:
         warmup = 1 every call is exactly one step (a training loop's step count holds)."""
         if self.graph is None and self.unsupported is None:
             self.capture()
-            if self.warmup <= 1:
+            if self.warmup <= 1 or self.graph is None:
                 for p, g in zip(self.params, self.warm_grads):
                     p.grad = g
                 return self.warm_result
