@@ -1015,6 +1015,37 @@ __global__ __launch_bounds__(TPB) void box_counts_kernel(int n, const uint32_t *
   if (threadIdx.x == 0) partial[blockIdx.x] = total;
 }
 
+// Inclusive max-scan over the wave (DPP row shifts, then the row broadcasts; no LDS).
+__device__ __forceinline__ int wave_incl_max(int v) {
+  constexpr int NONE = -2147483647 - 1;
+  v = max(v, __builtin_amdgcn_update_dpp(NONE, v, 0x111, 0xF, 0xF, false));  // row_shr:1
+  v = max(v, __builtin_amdgcn_update_dpp(NONE, v, 0x112, 0xF, 0xF, false));  // row_shr:2
+  v = max(v, __builtin_amdgcn_update_dpp(NONE, v, 0x114, 0xF, 0xF, false));  // row_shr:4
+  v = max(v, __builtin_amdgcn_update_dpp(NONE, v, 0x118, 0xF, 0xF, false));  // row_shr:8
+  v = max(v, __builtin_amdgcn_update_dpp(NONE, v, 0x142, 0xA, 0xF, false));  // row_bcast:15
+  v = max(v, __builtin_amdgcn_update_dpp(NONE, v, 0x143, 0xC, 0xF, false));  // row_bcast:31
+  return v;
+}
+
+// The owner of slot j0 + lane of a wave's combined slot range -- the last lane q with
+// rel[q] <= j and an allotment (has) -- without a search: every owner starting in the 64-slot
+// chunk marks its start offset with j0 + q (LDS max into the wave's 64 marks `mk`, set to -1
+// once before the first chunk), and an inclusive max-scan over the chunk's slots, with the
+// previous chunk's last owner as carry, gives every slot's owner.  Marks are never cleared: a
+// stale mark from an earlier chunk encodes a smaller j0 + q than any owner it could shadow
+// (owners start in lane order and their slot ranges do not overlap), so the max is still the
+// owner.  (Replaces a 6-step shuffle search: six dependent ds_bpermute round trips per chunk.)
+__device__ __forceinline__ int slot_owner(int *mk, uint32_t j0, uint32_t rel, bool has,
+                                          int &carry) {
+  const int lane = threadIdx.x & 63;
+  wave_lds_sync();
+  if (has && rel >= j0 && rel < j0 + 64u) atomicMax(&mk[rel - j0], (int)j0 + lane);
+  wave_lds_sync();
+  const int own = max(wave_incl_max(mk[lane]), carry);
+  carry = __builtin_amdgcn_readlane(own, 63);
+  return own & 63;
+}
+
 // One wave per 64 depth-ordered Gaussians: the wave fills their combined slot range
 // [off[p0], off[p0] + total) with lanes striding over it, so stores are coalesced.  Slot j
 // belongs to the lane q with start[q] <= j < start[q+1] (6-step shuffle search); its tile
@@ -1060,14 +1091,13 @@ __global__ __launch_bounds__(TPB) void emit_kernel(int n, const uint32_t *__rest
   const uint32_t rel = in ? start - base : total;  // lanes past n are never chosen
   // wave-uniform trip count: every lane stays active for the shuffles (a shuffle reading an
   // inactive lane is undefined); only the stores are predicated.
+  __shared__ int emit_marks[TPB];
+  int *mk = emit_marks + (threadIdx.x & ~63);  // (slot owners: slot_owner)
+  mk[lane] = -1;
+  int carry = -1;
   for (uint32_t j0 = 0; j0 < total; j0 += 64) {
     const uint32_t j = j0 + lane;
-    int q = 0;  // largest q with rel[q] <= j
-#pragma unroll
-    for (int step = 32; step >= 1; step >>= 1) {
-      const uint32_t rq = __shfl(rel, (q + step) & 63, 64);
-      if (q + step <= 63 && rq <= j) q += step;
-    }
+    const int q = slot_owner(mk, j0, rel, c != 0u, carry);  // the last q with rel[q] <= j
     const uint32_t li = j - __shfl(rel, q, 64);
     // the owner's box (two shuffles of the packed corners) and id
     const uint32_t b0 = __shfl(b.x, q, 64), b1 = __shfl(b.y, q, 64);
@@ -1116,6 +1146,7 @@ __global__ __launch_bounds__(TPB) void emit_scan_kernel(int n, int nb,
                                                         const uint32_t *__restrict__ kfin = nullptr,
                                                         uint32_t assume = 0u) {
   __shared__ uint32_t lds[TPB / 64];
+  __shared__ int emit_marks[TPB];  // (per wave: the slot-owner marks)
   for (long long i = (long long)blockIdx.x * TPB + threadIdx.x; i < 2LL * tbx * tby;
        i += (long long)gridDim.x * TPB)
     tile_bins[i] = 0;
@@ -1171,14 +1202,12 @@ __global__ __launch_bounds__(TPB) void emit_scan_kernel(int n, int nb,
     const int last_lane = (int)min(63LL, (long long)n - 1 - p0);
     const uint32_t total = __shfl(start + c, last_lane, 64) - base;
     const uint32_t rel = in ? start - base : total;
+    int *mk = emit_marks + (threadIdx.x & ~63);  // (slot owners: slot_owner)
+    mk[lane] = -1;
+    int carry = -1;
     for (uint32_t j0 = 0; j0 < total; j0 += 64) {
       const uint32_t j = j0 + lane;
-      int q = 0;
-#pragma unroll
-      for (int step = 32; step >= 1; step >>= 1) {
-        const uint32_t rq = __shfl(rel, (q + step) & 63, 64);
-        if (q + step <= 63 && rq <= j) q += step;
-      }
+      const int q = slot_owner(mk, j0, rel, c != 0u, carry);
       const uint32_t li = j - __shfl(rel, q, 64);
       const uint32_t q0 = __shfl(bx.x, q, 64), q1 = __shfl(bx.y, q, 64);
       const uint32_t qg = __shfl(g, q, 64);
@@ -1311,7 +1340,7 @@ __global__ __launch_bounds__(1024) void bk_finalize_kernel(int nb, const uint32_
 // each slot (tile = T for the padding of an allotment larger than its box, as emit_kernel).
 template <typename F>
 __device__ __forceinline__ void expand_wave(long long p, long long n, const uint4 *__restrict__ rec,
-                                            int tbx, int tby, F &&f) {
+                                            int tbx, int tby, int *marks, F &&f) {
   const int lane = threadIdx.x & 63;
   uint32_t c = 0;
   uint4 q = make_uint4(0u, 0u, 0u, 0u);
@@ -1329,16 +1358,13 @@ __device__ __forceinline__ void expand_wave(long long p, long long n, const uint
   const uint32_t total = __shfl(inc, 63, 64);
   const uint32_t rel = inc - c;  // exclusive start of this lane's slots
   const uint32_t g = (uint32_t)p;
+  int *mk = marks + (threadIdx.x & ~63);  // (slot owners: slot_owner)
+  mk[lane] = -1;
+  int carry = -1;
   for (uint32_t j0 = 0; j0 < total; j0 += 64) {
     const uint32_t j = j0 + lane;
-    // owner = the largest lane o with rel[o] <= j (a zero allotment after the owner starts past
-    // j; lanes past n start at total)
-    int o = 0;
-#pragma unroll
-    for (int step = 32; step >= 1; step >>= 1) {
-      const uint32_t ro = __shfl(rel, (o + step) & 63, 64);
-      if (o + step <= 63 && ro <= j) o += step;
-    }
+    // owner = the last lane o with rel[o] <= j and an allotment (lanes past n start at total)
+    const int o = slot_owner(mk, j0, rel, c != 0u, carry);
     const uint32_t li = j - __shfl(rel, o, 64);
     const uint32_t b0 = __shfl(q.y, o, 64), b1 = __shfl(q.z, o, 64);
     const uint32_t og = __shfl(g, o, 64);
@@ -1364,6 +1390,7 @@ __global__ __launch_bounds__(BK_NT) void bk_count_kernel(int n, const uint4 *__r
                                                          uint32_t *__restrict__ ctr) {
   constexpr int NW = BK_NT / 64;
   __shared__ uint32_t hist[BK_MAX_BUCKETS];
+  __shared__ int marks[BK_NT];  // (expand_wave's slot owners)
   for (int i = threadIdx.x; i < nbk; i += BK_NT) hist[i] = 0;
   if (blockIdx.x == 0 && threadIdx.x == 0) *ctr = 0u;  // bk_scan's last-block counter
   __syncthreads();
@@ -1372,7 +1399,7 @@ __global__ __launch_bounds__(BK_NT) void bk_count_kernel(int n, const uint4 *__r
   for (int r = 0; r < BK_CHUNK / (64 * NW); ++r) {
     const long long p0 = base + (long long)(r * NW + wave) * 64;
     if (p0 >= n) break;  // wave-uniform
-    expand_wave(p0 + lane, n, rec, tbx, tby,
+    expand_wave(p0 + lane, n, rec, tbx, tby, marks,
                 [&](uint32_t tile, uint32_t) { atomicAdd(&hist[tile], 1u); });
   }
   __syncthreads();
@@ -1478,6 +1505,7 @@ __global__ __launch_bounds__(BK_NT) void bk_place_kernel(int n, const uint4 *__r
                                                          uint32_t cap = 0) {
   constexpr int NW = BK_NT / 64;
   __shared__ uint32_t cur[BK_MAX_BUCKETS];
+  __shared__ int marks[BK_NT];  // (expand_wave's slot owners)
   if (i_dev && *i_dev > cap) return;  // pre-launched: as emit_kernel
   const uint32_t *col = M + (size_t)blockIdx.x * nbk;
   for (int i = threadIdx.x; i < nbk; i += BK_NT) cur[i] = start[i] + col[i];
@@ -1487,7 +1515,7 @@ __global__ __launch_bounds__(BK_NT) void bk_place_kernel(int n, const uint4 *__r
   for (int r = 0; r < BK_CHUNK / (64 * NW); ++r) {
     const long long p0 = base + (long long)(r * NW + wave) * 64;
     if (p0 >= n) break;  // wave-uniform
-    expand_wave(p0 + lane, n, rec, tbx, tby, [&](uint32_t tile, uint32_t g) {
+    expand_wave(p0 + lane, n, rec, tbx, tby, marks, [&](uint32_t tile, uint32_t g) {
       ids[atomicAdd(&cur[tile], 1u)] = g;
     });
   }
