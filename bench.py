@@ -35,7 +35,7 @@ sys.path.insert(0, ROOT)
 from gaussctrl_exp_amd import _lib, timing  # noqa: E402
 from gaussctrl_exp_amd.camera import gc_camera, look_at_c2w  # noqa: E402
 from gaussctrl_exp_amd.fused import render_fused  # noqa: E402
-from gaussctrl_exp_amd.graphs import StepGraph  # noqa: E402
+from gaussctrl_exp_amd import rasterize  # noqa: E402
 from gaussctrl_exp_amd.rasterize import bin_gaussians  # noqa: E402
 from gaussctrl_exp_amd.scene import render, synthetic_scene  # noqa: E402
 from gaussctrl_exp_amd.sh import num_sh_bases  # noqa: E402
@@ -417,6 +417,53 @@ def c_oracle_baseline(scene, cam, sh_degree, budget_tiles=64, seed=0):
     }
 
 
+def view_cameras(config: str, rank: int, dev, count: int = 16):
+    """The cameras a training loop would draw for `config`, in the order it would draw them:
+    synthetic configs cycle the 8-view orbit from view `rank`; real configs draw the scene's own
+    training cameras at random (gc_datamanager.py:218: a random camera each step; seeded per
+    rank), rescaled to the config's width."""
+    N, W, H, deg, lo, hi, seed, real, _ = CONFIGS[config]
+    if real is None:
+        return [view_camera(W, H, (rank + k) % 8).to(dev) for k in range(count)]
+    import random
+    from gaussctrl_exp_amd.formats import load_transforms, rescale_cameras
+    d = load_transforms(os.path.join(ROOT, "tests", "golden", f"{real}_transforms.json"))
+    rng = random.Random(1234 + rank)
+    cams = []
+    for _ in range(count):
+        c = d.cameras[rng.randrange(len(d.cameras))]
+        if c.width != W:
+            c = rescale_cameras([c], W / c.width)[0]
+        cams.append(c.to(dev))
+    return cams
+
+
+def rotating_cameras(config, rank, dev, step, timed, steps, world):
+    """The timed step under the reference's camera pattern: the same step with
+    a different camera each step (view_cameras), after one warm-up pass over them.  A camera
+    change can defeat what the speculative binning learns from earlier frames (the capacity:
+    a running maximum over the shape's recent intersection counts; the depth-key bits seen
+    varying): speculative_misses counts the steps that had to re-bin."""
+    cams = view_cameras(config, rank, dev)
+    state = {"i": 0}
+
+    def rot():
+        step(c=cams[state["i"] % len(cams)])
+        state["i"] += 1
+    for _ in range(len(cams)):
+        rot()
+    torch.cuda.synchronize()
+    s0 = dict(rasterize.SPEC_STATS)
+    dt = timed(rot, steps)
+    H, W = cams[0].height, cams[0].width
+    s1 = rasterize.SPEC_STATS
+    return {"value": round(world * H * W * steps / dt / 1e6, 2),
+            "misses": {k: s1[k] - s0[k] for k in s1},
+            "desc": (f"{len(cams)} cameras cycled: " +
+                     ("the 8-view orbit" if CONFIGS[config][7] is None else
+                      f"random draws from the {CONFIGS[config][7]} training cameras"))}
+
+
 def exchange_profile(scene, cam, gt, bg, deg, world, dev, steps, timed):
     """N > 1 only: what the data-parallel exchange costs this rank and how much of it the step
     hides.  Times (max over ranks, same `steps`): the step's compute alone (the
@@ -466,10 +513,6 @@ def main():
                          "kernels out of the PMC and kernel-trace summaries)")
     ap.add_argument("--forward-only", action="store_true",
                     help="time the render without backward (default for config c2)")
-    ap.add_argument("--graph", default=os.environ.get("BENCH_GRAPH", "off"),
-                    choices=("on", "off"),
-                    help="on: one GPU replays the fused step (and the train step) as a HIP "
-                         "graph (graphs.py); off (default, measured faster): issued eagerly")
     ap.add_argument("--render", default="fused", choices=("fused", "caller"),
                     help="fused: the caller's activations inside the HIP kernels (default); "
                          "caller: gc_model.py's torch glue around the gsplat API")
@@ -505,34 +548,20 @@ def main():
 
     fwd_only = args.forward_only or args.config in FORWARD_ONLY
 
-    def step_eager(t=trainer):
+    def step_eager(t=trainer, c=None):
+        c = cam if c is None else c
         if fwd_only:
             with torch.no_grad():
                 if t.render_mode == "fused":
-                    render_fused(scene, cam, deg, bg)
+                    render_fused(scene, c, deg, bg)
                 else:
-                    render(scene, cam, deg, bg)
+                    render(scene, c, deg, bg)
             return
         t.zero_grad()
-        t.forward_backward(cam, gt, bg)
+        t.forward_backward(c, gt, bg)
         t.sync_grads()
 
-    # the fused step replayed as one HIP graph (graphs.StepGraph: captured after eager warm-up
-    # steps; every replay's binning counts checked on the host, an overflow re-run eagerly).
-    # One GPU only: the N > 1 step's collectives stay eager.
-    # --graph on: the step replayed as a HIP graph (graphs.StepGraph).  Off by default: on ROCm
-    # 7 a replayed graph of this step runs slower than the same launches issued from the stream
-    # (round 4, same box: headline 0.761 vs 0.748 ms/step, c3 0.403 vs 0.392 ms; the eager c3
-    # step is already within ~5 % of its kernel time)
-    graph = None
-    if world == 1 and args.render == "fused" and args.graph == "on":
-        graph = StepGraph(step_eager, dev, params=() if fwd_only else trainer.params)
-
-    def step(t=trainer):
-        if graph is not None and t is trainer:
-            graph.step()
-        else:
-            step_eager(t)
+    step = step_eager
 
     def timed(fn, steps):
         barrier()
@@ -566,10 +595,7 @@ def main():
         dt = float(t.item())
     ms_per_step = dt / args.steps * 1e3
     value = world * H * W * args.steps / dt / 1e6
-    eager_value = None
-    if graph is not None:
-        # the same step issued eagerly (kernel launches from Python each step), for comparison
-        eager_value = world * H * W * args.steps / timed(step_eager, args.steps) / 1e6
+    rotating = rotating_cameras(args.config, rank, dev, step_eager, timed, args.steps, world)
     exch = None
     if world > 1 and not fwd_only:
         exch = exchange_profile(scene, cam, gt, bg, deg, world, dev, args.steps, timed)
@@ -659,18 +685,9 @@ def main():
     # full train step: splatfacto loss + backward + all-reduce + Adam
     tsteps = args.train_steps if args.train_steps is not None else args.steps
     trainer.loss_kind = "splatfacto"
-    # one GPU: the train step replayed as a HIP graph too (its Adam schedule on the device)
-    tgraph = None
-    if graph is not None:
-        tgraph = StepGraph(lambda: trainer.step(cam, gt, device_schedule=True), dev,
-                           after_capture=lambda: trainer.advance_step_count(-1),
-                           after_replay=trainer.advance_step_count)
 
     def train_step():
-        if tgraph is not None:
-            tgraph.step()
-        else:
-            trainer.step(cam, gt)
+        trainer.step(cam, gt)
 
     def train_time(fn):
         for _ in range(2):
@@ -687,7 +704,6 @@ def main():
             tdt = float(t.item())
         return tdt
     tdt = train_time(train_step)
-    tdt_eager = train_time(lambda: trainer.step(cam, gt)) if tgraph is not None else None
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -726,15 +742,11 @@ def main():
             },
             "render": args.render,
             "exchange": exch,
-            "step_issue": "hip_graph" if graph is not None and graph.graph is not None
-                          else "eager",
-            "graph": graph.stats() if graph is not None else None,
-            "value_eager_launches": round(eager_value, 2) if eager_value else None,
+            "value_rotating_cameras": rotating["value"],
+            "speculative_misses": rotating["misses"],
+            "rotating_cameras": rotating["desc"],
             "value_unchanged_caller": round(caller_value, 2),
             "train_iters_per_s": round(tsteps / tdt, 2),
-            "train_iters_per_s_eager_launches": round(tsteps / tdt_eager, 2) if tdt_eager
-                                                else None,
-            "train_graph": tgraph.stats() if tgraph is not None else None,
             "train_views_per_s": round(world * tsteps / tdt, 2),
             "roofline": roofline,
             "lane_occupancy": lanes,

@@ -100,10 +100,6 @@ SIGNATURES = {
                                          [_P] * 13),
     "gsplat_fused_preprocess_backward_adam": (_I, [_I, _I, _I] + [_P] * 9 + [_F] * 4 +
                                               [_I, _I] + [_P] * 8 + [_I, _F, _F, _F, _P]),
-    "gsplat_fused_preprocess_backward_adam_sched": (
-        _I, [_I, _I, _I] + [_P] * 9 + [_F] * 4 + [_I, _I] + [_P] * 7 +
-        [_P, _I, _P, _P, _c.c_uint32, _F, _F, _F, _P]),
-    "gsplat_bin_device_count_offset": (_SZ, [_I]),
     "gsplat_exchange_pack_colors": (_I, [_I, _P, _SZ, _P, _P, _P, _P, _P]),
     "gsplat_grad_records_bytes": (_SZ, [_I]),
     "gsplat_grad_records_split": (_I, [_I, _P, _SZ, _P, _P, _P, _P, _P, _P, _P]),

@@ -73,15 +73,6 @@ struct FusedAdamArgs {
   float *p[6], *m[6], *v[6];
   float ss[6], bc2s[6];  // lr / (1 - beta1^t), sqrt(1 - beta2^t) (host, double -> float)
   float beta1, beta2, eps;
-  // device schedule (gsplat_fused_preprocess_backward_adam_sched; NULL: ss / bc2s above): the
-  // step's ss / bc2s from a table indexed by the device step counter (completed steps, clamped
-  // to the table), and no step at all when the binning's device count word exceeds the capacity
-  // it was launched at (an overflowed or range-violated capacity-launched binning)
-  const float *sched;
-  int sched_len;
-  const int *counter;
-  const uint32_t *valid_word;
-  uint32_t valid_cap;
 };
 
 // The caller's activations (gc_model.py:177-178): exp(scales), quats / |quats|.
@@ -324,17 +315,6 @@ __global__ __launch_bounds__(sh_threads(K)) void fused_bwd_kernel(FusedBwdArgs a
   const int cnt = (int)min((long long)THR, (long long)a.n - g0);
   const bool rest_out = K > 1 && a.v_colors == nullptr;
   const int t = threadIdx.x;
-  if constexpr (ADAM) {
-    if (o.sched) {  // (grid-uniform: every workgroup returns or none does)
-      if (o.valid_word && *o.valid_word > o.valid_cap) return;
-      const int c = min(max(*o.counter, 0), o.sched_len - 1);
-#pragma unroll
-      for (int k = 0; k < 6; ++k) {
-        o.ss[k] = o.sched[k * o.sched_len + c];
-        o.bc2s[k] = o.sched[6 * o.sched_len + c];
-      }
-    }
-  }
   if (t < cnt) {
     const long long g = g0 + t;
     float vmean[3] = {0.f, 0.f, 0.f}, vls[3] = {0.f, 0.f, 0.f}, vq[4] = {0.f, 0.f, 0.f, 0.f};
@@ -724,17 +704,6 @@ extern "C" int gsplat_exchange_pack_colors(int num_points, const void *grad_reco
   return check_launch("exchange_pack_colors");
 }
 
-namespace gs {
-namespace {
-// The device step counter of the scheduled Adam: one more completed step, unless the step's
-// binning overflowed its capacity (then the Adam kernel skipped it as well).
-__global__ void adam_step_advance_kernel(int *counter, const uint32_t *valid_word,
-                                         uint32_t valid_cap) {
-  if (threadIdx.x == 0 && !(valid_word && *valid_word > valid_cap)) *counter += 1;
-}
-}  // namespace
-}  // namespace gs
-
 extern "C" int gsplat_fused_preprocess_backward_adam(
     int num_points, int sh_bases, int degrees_to_use, float *means3d, float *log_scales,
     float *quats, float *opacity_logits, float *features_dc, float *features_rest,
@@ -790,70 +759,3 @@ extern "C" int gsplat_fused_preprocess_backward_adam(
   return check_launch("fused_preprocess_backward_adam");
 }
 
-// The in-backward Adam step with its schedule on the device (a step captured in a HIP graph and
-// replayed: graphs.StepGraph): sched = 7 rows of sched_len floats -- rows 0-5 the groups' lr /
-// (1 - beta1^(c+1)), row 6 sqrt(1 - beta2^(c+1)), each rounded to float exactly as the host
-// computes them for gsplat_fused_preprocess_backward_adam -- indexed by the device counter c of
-// completed steps (clamped to the last row); then the counter advances.  bin_count (may be NULL):
-// the capacity-launched binning's device count word; above bin_cap (overflow or depth-range
-// violation) neither the update nor the advance happens.
-extern "C" int gsplat_fused_preprocess_backward_adam_sched(
-    int num_points, int sh_bases, int degrees_to_use, float *means3d, float *log_scales,
-    float *quats, float *opacity_logits, float *features_dc, float *features_rest,
-    const float *viewmat, const float *projmat, const float *campos, float fx, float fy,
-    float cx, float cy, int img_height, int img_width, const int32_t *radii, const float *conics,
-    const float *colors, const float *opacity, const void *grad_records, float *const *exp_avgs,
-    float *const *exp_avg_sqs, const float *sched, int sched_len, int *step_counter,
-    const uint32_t *bin_count, uint32_t bin_cap, float beta1, float beta2, float eps,
-    void *stream) {
-  const int K = sh_bases;
-  if (num_points < 0 || !valid_bases(K) || degrees_to_use < 0 || degrees_to_use > degree_of(K) ||
-      img_height <= 0 || img_width <= 0 || !sched || sched_len < 1 || !step_counter ||
-      !(beta1 > 0.5f && beta1 < 1.f) || !(beta2 >= 0.f && beta2 < 1.f) || !exp_avgs ||
-      !exp_avg_sqs ||
-      (num_points > 0 && (!grad_records || (K > 1 && (!campos || !features_rest))))) {
-    set_error("fused_preprocess_backward_adam_sched: bad args (N=%d sh_bases=%d "
-              "degrees_to_use=%d sched_len=%d)", num_points, sh_bases, degrees_to_use, sched_len);
-    return 1;
-  }
-  hipStream_t st = (hipStream_t)stream;
-  if (num_points > 0) {
-    FusedBwdArgs args{num_points, degrees_to_use, means3d, log_scales, quats, viewmat, projmat,
-                      campos, radii, conics, colors, opacity, (const float *)grad_records,
-                      nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
-    FusedAdamArgs o{};
-    float *params[6] = {means3d, log_scales, quats, opacity_logits, features_dc, features_rest};
-    for (int k = 0; k < 6; ++k) {
-      o.p[k] = params[k];
-      o.m[k] = exp_avgs[k];
-      o.v[k] = exp_avg_sqs[k];
-    }
-    o.beta1 = beta1;
-    o.beta2 = beta2;
-    o.eps = eps;
-    o.sched = sched;
-    o.sched_len = sched_len;
-    o.counter = step_counter;
-    o.valid_word = bin_count;
-    o.valid_cap = bin_cap;
-    const ProjParams pp = make_proj_params(fx, fy, cx, cy, 1.f, 0.f, img_height, img_width, 1, 1);
-    const int thr = sh_threads(K);
-    const dim3 grid(cdiv(num_points, thr));
-    const size_t smem = K > 1 ? (size_t)thr * (((K - 1) * 3) | 1) * sizeof(float) : 0;
-    switch (K) {
-#define ADAM_CASE(KK)                                                                      \
-  case KK:                                                                                 \
-    hipLaunchKernelGGL((fused_bwd_kernel<KK, true>), grid, dim3(thr), smem, st, args, pp, o); \
-    break;
-      ADAM_CASE(1)
-      ADAM_CASE(4)
-      ADAM_CASE(9)
-      ADAM_CASE(16)
-      ADAM_CASE(25)
-#undef ADAM_CASE
-    }
-  }
-  hipLaunchKernelGGL(adam_step_advance_kernel, dim3(1), dim3(64), 0, st, step_counter, bin_count,
-                     bin_cap);
-  return check_launch("fused_preprocess_backward_adam_sched");
-}

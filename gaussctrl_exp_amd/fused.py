@@ -34,19 +34,15 @@ from torch.autograd import Function
 
 from . import _lib, exchange, quirks
 from .camera import GCCamera
-from .rasterize import (BLOCK_X, BLOCK_Y, GraphCaptureUnsupported, bin_gaussians,
-                        bin_gaussians_speculative, speculative_capacity, last_num_visible)
+from .rasterize import (BLOCK_X, BLOCK_Y, SPEC_STATS, bin_gaussians, bin_gaussians_speculative,
+                        speculative_capacity, last_num_visible)
 
 _DEG_OF_BASES = {1: 0, 4: 1, 9: 2, 16: 3, 25: 4}
 # frames below this many tiles get the list-split forward (raster.hip FWD_SPLIT_MAX_TILES)
 FWD_SPLIT_TILES = 3584
 
-# While a step is captured into a HIP graph (graphs.StepGraph): the speculative binnings the
-# captured forwards launched, whose pinned count words the graph's owner checks after every
-# replay instead of the forward's own finish() (a capture runs no kernel: nothing to wait for).
-_CAPTURE_SPECS: Optional[list] = None
-# How the last forward binned: "speculative" (capacity-launched, no host read: capturable),
-# "host" (the scheme needs I on the host first) or "sync" (first call of the frame shape)
+# How the last forward binned: "speculative" (capacity-launched, no host read), "host" (the
+# scheme needs I on the host first) or "sync" (first call of the frame shape)
 LAST_BINNING = {"mode": None}
 # the preprocess's SH-colour part on a second stream, overlapping the binning
 # (gsplat_fused_preprocess_forward_part); GSPLAT_MI355X_SPLIT_COLOURS=0: one kernel (A/B runs)
@@ -160,25 +156,14 @@ class _FusedRender(Function):
         spec_cap = speculative_capacity(n, H, W, dev)
         prepared = (spec_cap, plan_for(spec_cap)) if spec_cap > 0 else None
 
-        capturing = _CAPTURE_SPECS is not None
-        if capturing and prepared is None:
-            raise GraphCaptureUnsupported("render_fused: no intersection capacity for this "
-                                          "frame shape yet (run it eagerly first)")
         preprocess()
         # The binning's emission and tile sort are launched at this frame shape's capacity
         # without the host read of I (rasterize.SpeculativeBinning), the blend right behind
         # them; the host reads I only then, while the GPU works, and re-bins on an overflow.
-        spec = bin_gaussians_speculative(xys, depths, radii, nth, H, W, keyed_workspace=ws1,
-                                         host_wait=not capturing)
+        spec = bin_gaussians_speculative(xys, depths, radii, nth, H, W, keyed_workspace=ws1)
         LAST_BINNING["mode"] = "sync" if spec is None else (
             "speculative" if spec.slot is not None else "host")
-        if capturing:
-            # a captured forward: the replay's owner checks the count words (graphs.StepGraph);
-            # the layout and the backward's intersection count are the capacity
-            if spec is None or spec.slot is None:
-                raise GraphCaptureUnsupported("render_fused: this frame's binning reads I on "
-                                              "the host")
-            _CAPTURE_SPECS.append(spec)
+        SPEC_STATS["sync" if spec is None else "speculative"] += 1
         if spec is None:  # first call of this frame shape (or nothing to bin)
             num_intersects, gids, bins = bin_gaussians(xys, depths, radii, nth, H, W,
                                                        keyed_workspace=ws1)
@@ -209,12 +194,10 @@ class _FusedRender(Function):
                 _lib.call("gsplat_rasterize_forward_clearing_l1", *args, P(l1_gt), 1, P(l1_part),
                           4 * l1_part.numel(), P(loss), st)
 
-        if capturing:
-            blend(gids, bins, layout_i)
-            num_intersects = spec.cap
-        elif spec is not None:
+        if spec is not None:
             blend(gids, bins, layout_i)
             if not spec.finish():
+                SPEC_STATS["range" if spec.range_violated else "overflow"] += 1
                 if spec.range_violated:
                     # a depth digit the sort assumed constant varied: the sort consumed its
                     # keys, so the (deterministic) preprocess writes them again; full binning
@@ -233,6 +216,9 @@ class _FusedRender(Function):
                 gids = gids[:num_intersects]
         elif num_intersects >= 1:
             blend(gids, bins, layout_i)
+        # the colours are saved for the backward and returned in aux: the side-stream kernel
+        # must have finished even when no blend ran (nothing visible) to join it
+        join_colours()
         if num_intersects < 1:
             # nothing visible: the background (the caller returns it at gc_model.py:189-190),
             # and every gradient is zero
@@ -265,14 +251,6 @@ class _FusedRender(Function):
                     raise ValueError("render_fused: in-backward Adam needs the parameters "
                                      "themselves (contiguous fp32), not copies")
         ctx.adam = adam
-        # a captured step's device-scheduled Adam checks the binning's device count word itself
-        # (a replay whose binning overflowed must not move the parameters): the word lives in
-        # ws1, kept alive for the backward
-        ctx.bin_word = None
-        if capturing and adam is not None and "sched" in adam:
-            ctx.ws1 = ws1
-            ctx.bin_word = (ws1.data_ptr() + _lib.query("gsplat_bin_device_count_offset", n),
-                            int(spec.cap))
         ctx.save_for_backward(means, scales, quats, opacities, features_dc, features_rest,
                               viewmat, projmat, campos,
                               background, xys, radii, conics, colors, opac, gids, bins, final_Ts,
@@ -329,13 +307,8 @@ class _FusedRender(Function):
                     fx, fy, cx, cy, H, W, P(radii), P(conics), P(colors), P(opac), P(rec),
                     cast(a["exp_avgs"], ctypes.c_void_p), cast(a["exp_avg_sqs"], ctypes.c_void_p))
             tail = (float(a["betas"][0]), float(a["betas"][1]), float(a["eps"]), st)
-            if "sched" in a:  # the device schedule (a replayable step: TrainStep.device_schedule)
-                word, cap = ctx.bin_word if ctx.bin_word is not None else (None, 0)
-                _lib.call("gsplat_fused_preprocess_backward_adam_sched", *head, P(a["sched"]),
-                          int(a["sched_len"]), P(a["counter"]), word, cap, *tail)
-            else:
-                _lib.call("gsplat_fused_preprocess_backward_adam", *head,
-                          cast(a["lrs"], ctypes.c_void_p), int(a["step"]), *tail)
+            _lib.call("gsplat_fused_preprocess_backward_adam", *head,
+                      cast(a["lrs"], ctypes.c_void_p), int(a["step"]), *tail)
             return (None,) * 21
         f32 = dict(device=dev, dtype=torch.float32)
         xchg = ctx.exchange

@@ -10,10 +10,7 @@ passes.  Semantics: torch.optim.Adam(foreach=True), no weight decay, no amsgrad.
 from __future__ import annotations
 
 import ctypes
-import math
-from typing import Callable, Dict, List, Sequence
-
-import numpy as np
+from typing import Dict, List
 
 import torch
 
@@ -100,17 +97,6 @@ class FusedAdam:
         return {"exp_avgs": M, "exp_avg_sqs": V, "lrs": lrs, "step": self.step_count,
                 "betas": self.betas, "eps": self.eps, "params": list(params)}
 
-    def sched_spec(self, params, sched: Dict):
-        """fused_spec for gsplat_fused_preprocess_backward_adam_sched: the moments' pointers
-        plus the device schedule `sched` (adam_schedule_table on the device and the device
-        counter of completed steps, see TrainStep); the kernel reads the step's learning rates
-        and bias corrections there, so the same launch can be replayed step after step.
-        Advances the host mirror of the step count, as fused_spec does."""
-        spec = self.fused_spec(params)
-        spec.update(sched=sched["table"], sched_len=int(sched["table"].shape[1]),
-                    counter=sched["counter"])
-        return spec
-
     def zero_grad(self, set_to_none: bool = True):
         for g in self.param_groups:
             p = g["params"][0]
@@ -118,24 +104,3 @@ class FusedAdam:
                 p.grad = None
             elif p.grad is not None:
                 p.grad.zero_()
-
-
-def adam_schedule_table(lrs_of_step: Callable[[int], Sequence[float]], betas, length: int):
-    """[7, length] float32: for c completed steps (the step t = c + 1), rows 0-5 the groups'
-    float(lr) / (1 - beta1^t) and row 6 sqrt(1 - beta2^t), rounded to float -- exactly the
-    values gsplat_fused_preprocess_backward_adam computes on the host from a float lr and float
-    betas (C double pow / division / sqrt; Python's math functions are the same libm calls), so
-    a device-scheduled step is bit-identical to the host-scheduled one.  Past the table the last
-    row is used: with lr schedules that end within it, and t large enough that both corrections
-    round to their limits, the values no longer change."""
-    b1 = float(np.float32(betas[0]))
-    b2 = float(np.float32(betas[1]))
-    out = np.empty((7, length), dtype=np.float32)
-    for c in range(length):
-        t = c + 1
-        bc1 = 1.0 - math.pow(b1, t)
-        bc2 = 1.0 - math.pow(b2, t)
-        for k, lr in enumerate(lrs_of_step(c)):
-            out[k, c] = np.float32(float(np.float32(lr)) / bc1)
-        out[6, c] = np.float32(math.sqrt(bc2))
-    return out

@@ -14,6 +14,7 @@ RGB, depth and alpha from one binning and one traversal.
 """
 from __future__ import annotations
 
+import collections
 import os
 import time
 import weakref
@@ -193,7 +194,7 @@ def bin_gaussians(xys: Tensor, depths: Tensor, radii: Tensor, num_tiles_hit: Ten
             _note_key_range(key, host)
     finally:
         _COUNTS.release(dev, slot, visible)
-    _EMIT_CAP[key] = emit_capacity(num_intersects)
+    _note_capacity(key, num_intersects)
     if pre is not None and num_intersects <= cap and not PRELAUNCH_EMISSION:  # (A/B runs)
         ids_buf, ws2 = pre
         _lib.call("gsplat_bin_emit", n, num_intersects, tbx, tby, P(ids_buf), P(tile_bins),
@@ -243,35 +244,8 @@ class SpeculativeBinning:
             _COUNTS.release(self.dev, self.slot, visible)
         self.num_intersects = I
         if not self.range_violated:  # (a violated sort's I is meaningless: the caller re-bins)
-            _EMIT_CAP[self.key] = emit_capacity(I)
+            _note_capacity(self.key, I)
         return I <= self.cap and not self.range_violated
-
-    def check_replay(self, stream) -> bool:
-        """After a HIP-graph replay of the forward that launched this binning (graphs.StepGraph:
-        the captured forward skipped finish()): wait for the replay's count words, re-arm them
-        for the next replay.  False: I exceeded the capacity the graph was captured with, or a
-        depth digit assumed constant varied -- the replay's binning (and everything behind it)
-        is invalid, and the owner runs the step eagerly and captures it again."""
-        I = _wait_count(self.host, stream)
-        visible = int(self.host[0])
-        violated = int(self.host[2]) != 0
-        _note_key_range(self.key, self.host)
-        self.host[:2] = -1
-        self.host[2:] = 0
-        _COUNTS.last_visible[self.dev] = visible
-        self.num_intersects = I
-        if violated:
-            return False
-        if I > self.cap:  # the eager re-run starts from a capacity that holds this frame
-            _EMIT_CAP[self.key] = emit_capacity(I)
-            return False
-        return True
-
-    def release(self):
-        """Give the pinned count slot back (a graph holding this binning was dropped)."""
-        if self.slot is not None:
-            _COUNTS.release(self.dev, self.slot)
-            self.slot = None
 
     def rebin(self):
         """After an overflow (not a range violation): the emission and tile sort for the exact I
@@ -300,22 +274,14 @@ def speculative_capacity(n: int, img_height: int, img_width: int, dev) -> int:
     return _EMIT_CAP.get((dev, n, tbx, tby), 0)
 
 
-class GraphCaptureUnsupported(RuntimeError):
-    """A binning that needs the host read of I (the first frame of a shape, or a scheme that
-    reads I before its emission) was asked for inside a HIP-graph capture: the step stays
-    eager (graphs.StepGraph)."""
-
-
 def bin_gaussians_speculative(xys: Tensor, depths: Tensor, radii: Tensor, num_tiles_hit: Tensor,
                               img_height: int, img_width: int,
-                              keyed_workspace: Optional[Tensor] = None, host_wait: bool = True):
+                              keyed_workspace: Optional[Tensor] = None):
     """bin_gaussians without the host read of I in the middle: the count phase, then -- when
     this frame shape's capacity is known from an earlier call and the binning scheme allows it
     -- the emission and the whole tile sort at that capacity (gsplat_bin_emit_speculative).
     Returns a SpeculativeBinning (finish() before using I), or None when the capacity is not
-    known yet or the scheme needs I on the host (the caller then uses bin_gaussians).
-    host_wait=False (a HIP-graph capture): a scheme that needs I on the host raises
-    GraphCaptureUnsupported before anything is launched."""
+    known yet or the scheme needs I on the host (the caller then uses bin_gaussians)."""
     n = xys.shape[0]
     tbx = (img_width + BLOCK_X - 1) // BLOCK_X
     tby = (img_height + BLOCK_Y - 1) // BLOCK_Y
@@ -331,17 +297,11 @@ def bin_gaussians_speculative(xys: Tensor, depths: Tensor, radii: Tensor, num_ti
     ids_buf, ws2 = _emit_buffers(dev, n, cap, tbx, tby)
     slot, counts, host = _COUNTS.acquire(dev)
     try:
-        # count phase, emission (with the allotment scan) and tile sort in one call
-        # a captured binning (host_wait False) assumes no constant depth digit: every later
-        # replay sorts all four passes, so a depth range that changes between replays can never
-        # invalidate it (the capacity is the only thing a replay checks)
-        assume = _assumed_constant(key) if host_wait else 0
+        # the count phase and the region binning in one call
+        assume = _assumed_constant(key)
         rc = _lib.call_status("gsplat_bin_speculative", n, cap, tbx, tby, P(counts), P(ws1),
                               ws1.numel(), assume, P(ids_buf), P(tile_bins),
                               P(ws2), ws2.numel(), st)
-        if rc == 2 and not host_wait:  # (nothing was launched)
-            raise GraphCaptureUnsupported("bin_gaussians_speculative: the binning scheme of "
-                                          f"{cap} intersections reads I on the host")
         if rc == 2:  # the scheme needs I on the host: count, then finish as bin_gaussians does
             _lib.call("gsplat_bin_count_keyed_ex", n, tbx, tby, P(counts), P(ws1), ws1.numel(),
                       _assumed_constant(key), st)
@@ -355,12 +315,15 @@ def bin_gaussians_speculative(xys: Tensor, depths: Tensor, radii: Tensor, num_ti
             _COUNTS.release(dev, slot, int(host[0]))
             slot = None
             if violated:  # (an assumed-constant depth digit varied: the caller starts over)
+                # the caller may blend before it calls finish(): nothing was emitted, so the
+                # table must read as empty (it was uninitialised here)
+                tile_bins.zero_()
                 done = SpeculativeBinning(dev, n, tbx, tby, ws1, None, None, None, key, cap,
                                           ids_buf, ws2, tile_bins)
                 done.num_intersects, done.range_violated = I, True
                 done.finish = lambda: False
                 return done
-            _EMIT_CAP[key] = emit_capacity(I)
+            _note_capacity(key, I)
             if I <= cap:
                 _lib.call("gsplat_bin_emit_finish", n, I, cap, tbx, tby, P(pre[0]), P(tile_bins),
                           P(ws1), ws1.numel(), P(pre[1]), pre[1].numel(), st)
@@ -390,6 +353,23 @@ def bin_gaussians_speculative(xys: Tensor, depths: Tensor, radii: Tensor, num_ti
 
 # frame shape -> the intersection capacity to pre-allocate the emission's outputs for
 _EMIT_CAP = {}
+# frame shape -> the intersection counts of its last CAP_WINDOW binnings: the capacity is 1/8
+# above their maximum, so a training loop that draws a random camera each step
+# (gc_datamanager.py:218) overflows only on a view with more intersections than any of the last
+# CAP_WINDOW (round 4 sized it from the previous frame alone: every larger view re-binned)
+_CAP_WINDOW = {}
+CAP_WINDOW = 64
+# speculative binnings of the fused render: calls, and those that had to re-bin (capacity
+# overflow / a depth digit assumed constant that varied) -- bench.py's speculative_misses
+SPEC_STATS = {"speculative": 0, "overflow": 0, "range": 0, "sync": 0}
+
+
+def _note_capacity(key, num_intersects: int):
+    w = _CAP_WINDOW.get(key)
+    if w is None:
+        w = _CAP_WINDOW[key] = collections.deque(maxlen=CAP_WINDOW)
+    w.append(int(num_intersects))
+    _EMIT_CAP[key] = emit_capacity(max(w))
 # frame shape -> the depth-key bits seen varying over the visible Gaussians (the union over
 # calls, from gsplat_bin_count_keyed_ex's d_counts[3]); the speculative binning skips the
 # depth-sort passes whose digit lies in the complement (GSPLAT_MI355X_ASSUME_RANGE=0: never)

@@ -260,48 +260,10 @@ class TrainStep:
         sc.features_dc.grad = v[:, 0, :].contiguous()
         sc.features_rest.grad = v[:, 1:, :].contiguous()
 
-    def _lrs_of_step(self, c: int):
-        """The six groups' learning rates after c completed steps (splatfacto's schedule:
-        means decays exponentially, the rest constant)."""
-        lr = {n: GROUP_LR[n] for n in PARAM_NAMES}
-        t = min(c / XYZ_MAX_STEPS, 1.0)
-        lr["means"] = math.exp(math.log(GROUP_LR["means"]) * (1 - t) + math.log(XYZ_LR_FINAL) * t)
-        return [lr[g["name"]] for g in self.opt.param_groups]
-
-    def device_schedule(self):
-        """The in-backward Adam's schedule on the device (graphs.StepGraph replays of step():
-        a replayed launch cannot take new host arguments): the [7, XYZ_MAX_STEPS + 1] table of
-        optim.adam_schedule_table and the device counter of completed steps, re-synchronised
-        with the host count whenever they were stepped apart."""
-        from .optim import adam_schedule_table
-        dev = self.scene.means.device
-        sc = getattr(self, "_sched", None)
-        if sc is None or sc["table"].device != dev:
-            table = adam_schedule_table(self._lrs_of_step, self.opt.betas, XYZ_MAX_STEPS + 1)
-            sc = self._sched = {"table": torch.from_numpy(table).to(dev),
-                                "counter": torch.zeros(1, dtype=torch.int32, device=dev),
-                                "believed": None}
-        if sc["believed"] != self.step_count:
-            sc["counter"].fill_(self.step_count)
-            sc["believed"] = self.step_count
-        return sc
-
-    def advance_step_count(self, k: int = 1):
-        """Host mirrors of a device-scheduled step taken (k = 1) or of a captured one that never
-        ran (k = -1): the step count, the optimiser's, and the schedule's belief of the device
-        counter move together."""
-        self.step_count += k
-        self.opt.step_count += k
-        sc = getattr(self, "_sched", None)
-        if sc is not None and sc["believed"] is not None:
-            sc["believed"] += k
-
     def step(self, cam: GCCamera, gt: torch.Tensor, background: Optional[torch.Tensor] = None,
-             optimizer: bool = True, device_schedule: bool = False):
-        """One training step.  device_schedule (single GPU, in-backward Adam): the step's
-        learning rates and bias corrections come from the device schedule, so the step can be
-        captured and replayed (graphs.StepGraph with after_capture / after_replay =
-        advance_step_count(-1) / advance_step_count())."""
+             optimizer: bool = True):
+        """One training step (gc_trainer.py:258-301 / gc_pipeline.py:469-480): render, the
+        splatfacto loss, backward, gradient exchange (N > 1) and Adam."""
         if background is None:
             background = torch.rand(3, device=gt.device)
         if optimizer:
@@ -312,18 +274,8 @@ class TrainStep:
                 all(p.dtype == torch.float32 and p.is_contiguous() for p in self.params):
             # the backward takes the Adam step (one kernel instead of gradient tensors + step)
             self.zero_grad()
-            if device_schedule:
-                sched = self.device_schedule()
-                spec = self.opt.sched_spec(self.params, sched)
-                try:
-                    loss, out = self.forward_backward(cam, gt, background, adam=spec)
-                except BaseException:  # (nothing launched the update: the counts stay)
-                    self.opt.step_count -= 1
-                    raise
-                sched["believed"] += 1
-            else:
-                spec = self.opt.fused_spec(self.params)
-                loss, out = self.forward_backward(cam, gt, background, adam=spec)
+            spec = self.opt.fused_spec(self.params)
+            loss, out = self.forward_backward(cam, gt, background, adam=spec)
             self.step_count += 1
             return loss
         self.zero_grad()

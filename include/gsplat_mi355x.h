@@ -447,24 +447,6 @@ int gsplat_fused_preprocess_backward_adam(
     const float *colors, const float *opacity, const void *grad_records, float *const *exp_avgs,
     float *const *exp_avg_sqs, const float *lrs, int step, float beta1, float beta2, float eps,
     void *stream);
-/* gsplat_fused_preprocess_backward_adam with its schedule on the device, for a training step
- * captured in a HIP graph (graphs.StepGraph): `sched` holds 7 rows of sched_len floats -- rows
- * 0-5 each group's lr / (1 - beta1^(c+1)), row 6 sqrt(1 - beta2^(c+1)), rounded to float as the
- * host rounds them for gsplat_fused_preprocess_backward_adam -- indexed by the device counter c
- * of completed steps (clamped to the last row), which then advances by one.  bin_count (may be
- * NULL): the speculative binning's device count word (gsplat_bin_device_count_offset); above
- * bin_cap (capacity overflow, depth-range violation) no parameter moves and the counter stays. */
-int gsplat_fused_preprocess_backward_adam_sched(
-    int num_points, int sh_bases, int degrees_to_use, float *means3d, float *log_scales,
-    float *quats, float *opacity_logits, float *features_dc, float *features_rest,
-    const float *viewmat, const float *projmat, const float *campos, float fx, float fy,
-    float cx, float cy, int img_height, int img_width, const int32_t *radii, const float *conics,
-    const float *colors, const float *opacity, const void *grad_records, float *const *exp_avgs,
-    float *const *exp_avg_sqs, const float *sched, int sched_len, int *step_counter,
-    const uint32_t *bin_count, uint32_t bin_cap, float beta1, float beta2, float eps,
-    void *stream);
-/* Byte offset of that device count word inside a gsplat_bin_count workspace of num_points. */
-size_t gsplat_bin_device_count_offset(int num_points);
 
 /* Per-Gaussian gradient records (64 B each) the fused path's rasterize backward accumulates
  * into, as pixel moments over every pixel the Gaussian is composited at (d = xy - pixel,
