@@ -51,7 +51,6 @@ SIGNATURES = {
     "gsplat_sort_isect_pairs": (_I, [_I64, _I, _P, _P, _P, _P, _P, _SZ, _P]),
     "gsplat_get_tile_bin_edges": (_I, [_I64, _P, _P, _I64, _P]),
     "gsplat_bin_count_workspace_size": (_SZ, [_I]),
-    "gsplat_bin_emit_workspace_size": (_SZ, [_I64]),
     "gsplat_bin_emit_workspace_size_for": (_SZ, [_I, _I64, _I, _I]),
     "gsplat_debug_binning_scheme": (_I, [_I]),
     "gsplat_bin_count": (_I, [_I, _P, _P, _P, _P, _I, _I, _P, _P, _SZ, _P]),
@@ -71,12 +70,10 @@ SIGNATURES = {
                                           [_P] * 4 + [_I64, _I, _P, _SZ, _P, _SZ, _P]),
     "gsplat_debug_set_chunk": (_I, [_I]),
     "gsplat_debug_forward_split": (_I, [_I]),
-    "gsplat_debug_depth_payload": (_I, [_I]),
     "gsplat_debug_forward_chunk_div": (_I, [_I]),
     "gsplat_debug_set_raster_variant": (_I, [_I, _I, _I]),
     "gsplat_debug_raster_variant_is_default": (_I, []),
     "gsplat_debug_depth_key_range": (_I, [_I]),
-    "gsplat_debug_emit_pass0": (_I, [_I]),
     "gsplat_debug_wave_log": (_I, [_P]),
     "gsplat_debug_pair_count": (_I, [_P]),
     "gsplat_l1_ssim_num_blocks": (_I, [_I, _I]),
@@ -93,7 +90,6 @@ SIGNATURES = {
                                              [_I] * 4 + [_F] + [_P] * 8 + [_SZ, _P]),
     "gsplat_bin_count_keyed": (_I, [_I, _I, _I, _P, _P, _SZ, _P]),
     "gsplat_bin_count_keyed_ex": (_I, [_I, _I, _I, _P, _P, _SZ, _c.c_uint32, _P]),
-    "gsplat_bin_rescan": (_I, [_I, _I, _I, _P, _SZ, _P]),
     "gsplat_bin_speculative": (_I, [_I, _I64, _I, _I, _P, _P, _SZ, _c.c_uint32, _P, _P, _P, _SZ,
                                     _P]),
     "gsplat_fused_preprocess_backward": (_I, [_I, _I, _I] + [_P] * 6 + [_F] * 4 + [_I, _I] +
@@ -113,7 +109,7 @@ SIGNATURES = {
                                              [_F, _I64, _I, _P, _SZ, _I, _P, _SZ, _P]),
 }
 
-ABI_VERSION = 13  # include/gsplat_mi355x.h GSPLAT_MI355X_ABI_VERSION
+ABI_VERSION = 14  # include/gsplat_mi355x.h GSPLAT_MI355X_ABI_VERSION
 
 _lib = None
 _DETERMINISTIC = os.environ.get("GSPLAT_MI355X_DETERMINISTIC", "0") not in ("", "0")
@@ -172,9 +168,6 @@ def lib():
             L.gsplat_debug_forward_chunk_div(int(os.environ["GSPLAT_MI355X_FWD_CHUNK_DIV"]))
         if os.environ.get("GSPLAT_MI355X_FWD_SPLIT") and hasattr(L, "gsplat_debug_forward_split"):
             L.gsplat_debug_forward_split(int(os.environ["GSPLAT_MI355X_FWD_SPLIT"]))
-        if os.environ.get("GSPLAT_MI355X_DEPTH_PAYLOAD") and \
-                hasattr(L, "gsplat_debug_depth_payload"):
-            L.gsplat_debug_depth_payload(int(os.environ["GSPLAT_MI355X_DEPTH_PAYLOAD"]))
         if os.environ.get("GSPLAT_MI355X_DEPTH_KEY_RANGE"):  # 0 off, 1 from 2^22 keys, 2 always
             L.gsplat_debug_depth_key_range(int(os.environ["GSPLAT_MI355X_DEPTH_KEY_RANGE"]))
         _lib = L

@@ -84,22 +84,6 @@ __device__ __forceinline__ unsigned long long digit_peers(uint32_t d, int width,
   return ((unsigned long long)hi << 32) | lo;
 }
 
-__global__ __launch_bounds__(TPB) void scan_reduce_kernel(const uint32_t *__restrict__ in,
-                                                          long long m,
-                                                          uint32_t *__restrict__ partial) {
-  __shared__ uint32_t lds[TPB / 64];
-  const long long base = (long long)blockIdx.x * SC_TILE;
-  uint32_t s = 0;
-#pragma unroll
-  for (int r = 0; r < SC_ITEMS; ++r) {
-    long long i = base + r * TPB + threadIdx.x;
-    if (i < m) s += in[i];
-  }
-  uint32_t total;
-  block_exclusive_scan<TPB>(s, total, lds);
-  if (threadIdx.x == 0) partial[blockIdx.x] = total;
-}
-
 // Single workgroup: exclusive scan of partial[0..nb) in place; grand total -> *total.
 __global__ __launch_bounds__(1024) void scan_partials_kernel(uint32_t *__restrict__ partial,
                                                              int nb, uint32_t *__restrict__ total_out,
@@ -120,44 +104,7 @@ __global__ __launch_bounds__(1024) void scan_partials_kernel(uint32_t *__restric
   }
 }
 
-// out[i] = partial[block] + exclusive prefix inside the block's tile.  In place is allowed.
-__global__ __launch_bounds__(TPB) void scan_downsweep_kernel(const uint32_t *in, long long m,
-                                                             const uint32_t *__restrict__ partial,
-                                                             uint32_t *out) {
-  __shared__ uint32_t lds[TPB / 64];
-  const long long base = (long long)blockIdx.x * SC_TILE + (long long)threadIdx.x * SC_ITEMS;
-  uint32_t v[SC_ITEMS];
-  uint32_t s = 0;
-#pragma unroll
-  for (int j = 0; j < SC_ITEMS; ++j) {
-    long long i = base + j;
-    v[j] = i < m ? in[i] : 0u;
-    s += v[j];
-  }
-  uint32_t total;
-  uint32_t run = partial[blockIdx.x] + block_exclusive_scan<TPB>(s, total, lds);
-#pragma unroll
-  for (int j = 0; j < SC_ITEMS; ++j) {
-    long long i = base + j;
-    if (i < m) out[i] = run;
-    run += v[j];
-  }
-}
-
 size_t scan_ws_bytes(long long m) { return (size_t)(cdiv(m, SC_TILE) + 1) * sizeof(uint32_t); }
-
-// Exclusive scan of in[0..m) into out (in place allowed); total (device) optional.
-void device_exclusive_scan(const uint32_t *in, uint32_t *out, long long m, uint32_t *total,
-                           uint32_t *partial, hipStream_t st) {
-  if (m <= 0) {
-    if (total) note(hipMemsetAsync(total, 0, sizeof(uint32_t), st), "hipMemsetAsync");
-    return;
-  }
-  int nb = (int)cdiv(m, SC_TILE);
-  hipLaunchKernelGGL(scan_reduce_kernel, dim3(nb), dim3(TPB), 0, st, in, m, partial);
-  hipLaunchKernelGGL(scan_partials_kernel, dim3(1), dim3(1024), 0, st, partial, nb, total);
-  hipLaunchKernelGGL(scan_downsweep_kernel, dim3(nb), dim3(TPB), 0, st, in, m, partial, out);
-}
 
 // ------------------------------------------------------------ one-sweep radix sort
 
@@ -225,8 +172,6 @@ struct DevIO {
   void *kout;                // sorted keys (may be null)
   uint32_t *vout;            // sorted values
   int begin, width, passes;
-  const uint2 *pa, *pb;      // payload ping-pong buffers (the depth sort's tile boxes, PL)
-  uint2 *pout;               // sorted payload
 };
 __device__ __forceinline__ bool pass_moves(const DevIO &io, int q) {
   return q == 0 || !digit_constant(io.fin, io.begin + q * io.width, io.width);
@@ -244,20 +189,16 @@ __device__ __forceinline__ bool last_move(const DevIO &io, int q) {
 }
 template <typename K>
 __device__ __forceinline__ void dev_io(const DevIO &io, int q, const K *&kin, const uint32_t *&vin,
-                                       K *&kout, uint32_t *&vout, const uint2 *&pin,
-                                       uint2 *&pout) {
+                                       K *&kout, uint32_t *&vout) {
   const bool src_b = q > 0 && data_in_b(io, q);  // pass 0 reads (ka, va)
   kin = (const K *)(src_b ? io.kb : io.ka);
   vin = src_b ? io.vb : io.va;
-  pin = src_b ? io.pb : io.pa;
   if (last_move(io, q)) {
     kout = (K *)io.kout;
     vout = io.vout;
-    pout = io.pout;
   } else {  // the other buffer
     kout = (K *)(src_b ? io.ka : io.kb);
     vout = (uint32_t *)(src_b ? io.va : io.vb);
-    pout = (uint2 *)(src_b ? io.pa : io.pb);
   }
 }
 
@@ -273,7 +214,7 @@ __global__ __launch_bounds__(TPB) void rts_count_kernel(const K *__restrict__ ke
                                                         bool drop = false,
                                                         const uint32_t *__restrict__ n_dev = nullptr,
                                                         KeyRange kr = {}, int pass = 0,
-                                                        DevIO io = {}, int cap_launch = 0) {
+                                                        DevIO io = {}) {
   __shared__ uint32_t h[256];
   __shared__ uint32_t kand, kor;
   const int tid = threadIdx.x;
@@ -281,30 +222,16 @@ __global__ __launch_bounds__(TPB) void rts_count_kernel(const K *__restrict__ ke
   if (io.fin && pass > 0) keys = (const K *)(data_in_b(io, pass) ? io.kb : io.ka);
   const long long base = (long long)blockIdx.x * TPB * ITEMS;
   K k[ITEMS];
-  // cap_launch (the capacity-launched tile sort, EMIT_SPEC: n is the capacity, ~1.125 x the
-  // device count): the keys are loaded up to the capacity before the device count arrives, so
-  // the loads do not wait for it (positions past the count are masked below)
-  if (cap_launch) {
-#pragma unroll
-    for (int r = 0; r < ITEMS; ++r) k[r] = keys[min(base + r * TPB + tid, n - 1)];
-  }
-  if (n_dev) {
-    // *n_dev > n: a capacity-launched tile sort whose intersections overflowed the capacity
-    // (bin_emit_impl, EMIT_SPEC): the emission wrote nothing, so nothing is sorted
-    if (*n_dev > (unsigned long long)n) return;
-    n = *n_dev;
-  }
+  if (n_dev) n = min(n, (long long)*n_dev);  // (the compacted length)
   const int R = 1 << width;
   const uint32_t dmask = (uint32_t)(R - 1);
   h[tid] = 0;
   if (tid == 0) kand = ~0u, kor = 0u;
   __syncthreads();
-  if (!cap_launch) {
 #pragma unroll
-    for (int r = 0; r < ITEMS; ++r) {
-      const long long i = base + r * TPB + tid;
-      k[r] = i < n ? keys[i] : (K)0;
-    }
+  for (int r = 0; r < ITEMS; ++r) {
+    const long long i = base + r * TPB + tid;
+    k[r] = i < n ? keys[i] : (K)0;
   }
   uint32_t a = ~0u, o = 0u;
 #pragma unroll
@@ -379,7 +306,7 @@ __global__ __launch_bounds__(1024) void rts_rowscan_kernel(uint32_t *__restrict_
   if (threadIdx.x == 0) rowtot[blockIdx.x] = running;
 }
 
-template <typename K, int ITEMS, bool PAY = false>
+template <typename K, int ITEMS>
 struct OsSmem {
   // the tile's (key, value) pairs in digit order: 32-bit keys interleaved with their values (one
   // 8-B LDS access per pair) in the small tiles, two arrays otherwise (16 keys per thread: the
@@ -392,7 +319,6 @@ struct OsSmem {
   uint32_t hscan[256];     // exclusive scan of this pass's digit totals (large tiles)
   uint32_t scan_tmp[4];
   uint32_t tile_n;         // keys this tile writes (all valid ones; fewer when dropping)
-  uint2 pay[PAY ? N : 1];  // the payload in the same order (PL)
   __device__ __forceinline__ void put(uint32_t i, K k, uint32_t v) {
     if constexpr (PAIR) {
       reinterpret_cast<uint2 *>(raw)[i] = make_uint2((uint32_t)k, v);
@@ -421,81 +347,42 @@ struct OsSmem {
 // LDS, takes its digits' global offsets from the row-scanned tile counts plus the digit bases
 // (the exclusive scan of the row totals), and writes the tile out in digit order, so each
 // digit's run is written by consecutive lanes.
-// tile count of a packed box {x0 | y0 << 16, x1 | y1 << 16}
-__device__ __forceinline__ uint32_t box_area(uint2 b) {
-  const int w = (int)(b.y & 0xFFFFu) - (int)(b.x & 0xFFFFu);
-  const int h = (int)(b.y >> 16) - (int)(b.x >> 16);
-  return (uint32_t)(max(w, 0) * max(h, 0));
-}
-constexpr uint32_t BOX_GATHER = 0xFFFFFFFFu;
-
-// PL (the compacting depth sort): each key also carries an 8-B payload -- the Gaussian's tile box
-// -- so the sorted output holds the boxes in depth order and the binning needs no random gather
-// of the records afterwards.  PL 1 (pass 0): the payload is read from the Gaussian-order records
-// prec[i].{y, z} (coalesced); PL 2: from pin.  Written to pout in the keys' sorted order.
-template <typename K, int WIDTH, int ITEMS, int PL = 0>
+template <typename K, int WIDTH, int ITEMS>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) void os_pass_kernel(
     const K *__restrict__ kin, const uint32_t *__restrict__ vin, K *__restrict__ kout,
     uint32_t *__restrict__ vout, long long n, int shift, int width,
     const uint32_t *__restrict__ rowtot, const uint32_t *__restrict__ offs, long long nblocks,
-    int32_t *__restrict__ bins = nullptr, bool drop = false,
-    const uint32_t *__restrict__ n_dev = nullptr, uint32_t *__restrict__ n_out = nullptr,
-    const uint32_t *__restrict__ kfin = nullptr, DevIO io = {}, int q = 0, int cap_launch = 0,
-    const uint4 *__restrict__ prec = nullptr, const uint2 *__restrict__ pin = nullptr,
-    uint2 *__restrict__ pout = nullptr) {
+    bool drop = false, const uint32_t *__restrict__ n_dev = nullptr,
+    uint32_t *__restrict__ n_out = nullptr, const uint32_t *__restrict__ kfin = nullptr,
+    DevIO io = {}, int q = 0) {
   if (io.fin) {  // device-selected buffers (DevIO): a constant digit moves nothing
     if (q > 0 && digit_constant(io.fin, shift, width)) return;
     const K *ki;
     const uint32_t *vi;
     K *ko;
     uint32_t *vo;
-    const uint2 *pi;
-    uint2 *po;
-    dev_io<K>(io, q, ki, vi, ko, vo, pi, po);
+    dev_io<K>(io, q, ki, vi, ko, vo);
     kin = ki;
     vin = vi;
     kout = ko;
     vout = vo;
-    if (PL) {
-      pin = pi;
-      pout = po;
-    }
   }
-  auto load_pay = [&](long long i) -> uint2 {
-    if constexpr (PL == 1) {
-      // an allotment that is not the box's tile count (caller-supplied num_tiles_hit
-      // disagreeing with the box) travels as the marker BOX_GATHER: box_counts_kernel then
-      // reads that Gaussian's record itself
-      const uint4 r = prec[i];
-      return r.x == box_area(make_uint2(r.y, r.z)) ? make_uint2(r.y, r.z)
-                                                   : make_uint2(BOX_GATHER, 0u);
-    } else if constexpr (PL == 2) {
-      return pin[i];
-    } else {
-      return make_uint2(0u, 0u);
-    }
-  };
   // compacting sort: with drop, all-ones keys are left out (pass 0 of the depth sort: culled
   // Gaussians), and block 0 stores the kept count to n_out; later passes sort min(n, *n_dev)
   // keys and the workgroups past them exit at once.
-  // cap_launch (see rts_count_kernel): the count is read after the loads are issued, below
-  const long long n_cap = n;
-  if (n_dev && !cap_launch) {
-    if (*n_dev > (unsigned long long)n) return;  // capacity overflow (see rts_count_kernel)
-    n = *n_dev;
+  if (n_dev) {
+    n = min(n, (long long)*n_dev);
     if ((long long)blockIdx.x * TPB * ITEMS >= n) return;  // whole workgroup
   }
   if (digit_constant(kfin, shift, width)) {  // every key has the same digit: a stable copy
     const long long b0 = (long long)blockIdx.x * TPB * ITEMS;
     K ck[ITEMS];
     uint32_t cv[ITEMS];
-    uint2 cp[PL ? ITEMS : 1];
 #pragma unroll
     for (int r = 0; r < ITEMS; ++r) {  // all loads in flight before the first store
       const long long i = min(b0 + r * TPB + threadIdx.x, n - 1);
       if (kout) ck[r] = kin[i];
       cv[r] = vin[i];
-      if constexpr (PL != 0) cp[r] = load_pay(i);
     }
 #pragma unroll
     for (int r = 0; r < ITEMS; ++r) {
@@ -503,12 +390,11 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
       if (i < n) {
         if (kout) kout[i] = ck[r];
         vout[i] = cv[r];
-        if constexpr (PL != 0) pout[i] = cp[r];
       }
     }
     return;
   }
-  __shared__ OsSmem<K, ITEMS, PL != 0> sm;
+  __shared__ OsSmem<K, ITEMS> sm;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int R = 1 << width;
   const uint32_t dmask = (uint32_t)(R - 1);
@@ -516,7 +402,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
   const unsigned long long lt = (1ull << lane) - 1ull;
   K key[ITEMS];
   uint32_t val[ITEMS], rank[ITEMS];
-  uint2 pay[PL ? ITEMS : 1];
   bool ok[ITEMS];
   // the digit total (and in small tiles this tile's row offset) first: vmcnt retires in issue
   // order, so the scans below wait for them alone
@@ -528,16 +413,10 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     const long long sg = (long long)t * TPB * ITEMS + (long long)wave * (ITEMS * 64);
 #pragma unroll
     for (int r = 0; r < ITEMS; ++r) {
-      const long long i = min(sg + r * 64 + lane, n_cap - 1);
+      const long long i = min(sg + r * 64 + lane, n - 1);
       key[r] = kin[i];
       val[r] = vin[i];
-      if constexpr (PL != 0) pay[r] = load_pay(i);
     }
-  }
-  if (n_dev && cap_launch) {  // (workgroup-uniform exits, after the loads went out)
-    if (*n_dev > (unsigned long long)n) return;
-    n = *n_dev;
-    if ((long long)blockIdx.x * TPB * ITEMS >= n) return;
   }
 #pragma unroll
   for (int w = 0; w < 4; ++w) sm.wcnt[w][tid] = 0;
@@ -604,7 +483,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
       if (ok[r]) {
         const uint32_t d = (uint32_t)(key[r] >> shift) & dmask;
         sm.put(sm.wcnt[wave][d] + rank[r], key[r], val[r]);
-        if constexpr (PL != 0) sm.pay[sm.wcnt[wave][d] + rank[r]] = pay[r];
       }
     }
     // large tiles: the row offset's load overlaps the scatter
@@ -612,39 +490,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
   }
   __syncthreads();
   const long long cnt = sm.tile_n;
-  if (bins) {
-    // last pass of the tile sort: the keys (tile ids) are not written; the tile table comes from
-    // the runs of equal keys instead.  This tile's LDS array is sorted by the whole key (this
-    // digit, then the previous passes' order of its contiguous input), and each run is one
-    // contiguous range of the output, so its ends are range ends unless a neighbouring tile
-    // continues the run: the start as I - pos (atomicMax, 0 = empty) and the end, both decoded
-    // by bins_decode_kernel.
-#pragma unroll
-    for (int r = 0; r < ITEMS; ++r) {
-      const int i = r * TPB + tid;
-      K k = (K)0;
-      uint32_t v = 0;
-      if (i < cnt) sm.get(i, k, v);
-      K kp, kn;
-      if constexpr (OsSmem<K, ITEMS>::PAIR) {
-        // the neighbours' keys from the adjacent lanes (a strided LDS read of the interleaved
-        // pairs would conflict); a wave's first and last lane read theirs from LDS
-        kp = __shfl_up(k, 1, 64);
-        kn = __shfl_down(k, 1, 64);
-        if (lane == 0 && i > 0 && i < cnt) kp = sm.key(i - 1);
-        if (lane == 63 && i + 1 < cnt) kn = sm.key(i + 1);
-      } else {
-        kp = i > 0 && i < cnt ? sm.key(i - 1) : k;
-        kn = i + 1 < cnt ? sm.key(i + 1) : k;
-      }
-      if (i < cnt) {
-        const uint32_t pos = sm.gofs[(uint32_t)(k >> shift) & dmask] + (uint32_t)i;
-        vout[pos] = v;
-        if (i == 0 || kp != k) atomicMax(&bins[2 * (size_t)k], (int32_t)(n - pos));
-        if (i == cnt - 1 || kn != k) atomicMax(&bins[2 * (size_t)k + 1], (int32_t)pos + 1);
-      }
-    }
-  } else {
+  {
 #pragma unroll
     for (int r = 0; r < ITEMS; ++r) {
       const int i = r * TPB + tid;
@@ -655,7 +501,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
         const uint32_t pos = sm.gofs[(uint32_t)(k >> shift) & dmask] + (uint32_t)i;
         if (kout) kout[pos] = k;  // null: only the values are wanted (compacted depth sort)
         vout[pos] = v;
-        if constexpr (PL != 0) pout[pos] = sm.pay[i];
       }
     }
   }
@@ -668,7 +513,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
 // per wave before its LDS atomics.  The headline's visible depths (2.5-5.5) share their top
 // byte, so one of its four passes drops out.
 int g_key_range = 2;
-bool g_depth_payload = false;  // see bin_count_impl
 bool use_key_range(long long n) { return g_key_range == 2 || (g_key_range == 1 && n >= (1LL << 22)); }
 
 uint32_t *rts_tile_counts(void *ws) { return (uint32_t *)ws + OS_HEAD_WORDS; }
@@ -680,43 +524,17 @@ uint32_t *sort_kept_word(void *ws) { return (uint32_t *)ws + 1; }
 // there are more than two passes.  ws must hold radix_ws_bytes(n, begin_bit, end_bit).
 // first_counts_ready: the caller's key kernel already wrote pass 0's tile digit counts to
 // rts_tile_counts(ws).
-// tile_bins (uint32 tile-id keys only): the last pass writes no keys but the tile table --
-// zeroed by the caller, [first, last+1) per tile afterwards (bins_decode_kernel).
-// drop (first_counts_ready then means counts without the all-ones keys): the first pass leaves out all-ones keys, so the sort orders only the kept keys, whose
-// count it stores to sort_kept_word(ws) (the sorted output holds that many; kout may be null).
-__global__ __launch_bounds__(TPB) void bins_decode_kernel(long long T, long long n,
-                                                          int32_t *__restrict__ bins,
-                                                          const uint32_t *__restrict__ n_dev =
-                                                              nullptr) {
-  const long long t = (long long)blockIdx.x * TPB + threadIdx.x;
-  if (t >= T) return;
-  if (n_dev) {  // the device count of a capacity-launched sort (n: the capacity)
-    if (*n_dev > (unsigned long long)n) return;  // overflow: the table stays cleared
-    n = *n_dev;
-  }
-  const int32_t x = bins[2 * t];
-  if (x > 0) bins[2 * t] = (int32_t)(n - x);
-}
-
+// drop (first_counts_ready then means counts without the all-ones keys): the first pass leaves
+// out all-ones keys, so the sort orders only the kept keys, whose count it stores to
+// sort_kept_word(ws) (the sorted output holds that many; kout may be null).
+// assume_const / range_out (drop only): gsplat_bin_count_keyed_ex's depth-key range.
 template <typename K>
 int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t *vout,
                      long long n, int begin_bit, int end_bit, void *ws, hipStream_t st,
-                     bool first_counts_ready = false, int32_t *tile_bins = nullptr,
-                     long long num_tiles = 0, bool drop = false, int first_pass = 0,
-                     const uint32_t *n_dev_all = nullptr, uint32_t assume_const = 0,
-                     int32_t *range_out = nullptr, const uint4 *prec = nullptr,
-                     uint2 *pa = nullptr, uint2 *pb = nullptr, uint2 *pout = nullptr) {
-  // n_dev_all (not with drop): the key count lives on the device (<= n, the launch capacity;
-  // more than n: overflow, every kernel returns at once) -- the capacity-launched tile sort
-  // prec (the compacting depth sort, drop and first_pass 0 only): every key carries the 8-B
-  // payload prec[i].{y, z} to pout (ping-pong through pa / pb), see os_pass_kernel's PL
+                     bool first_counts_ready = false, bool drop = false,
+                     uint32_t assume_const = 0, int32_t *range_out = nullptr) {
   if (n <= 0) return 0;
   const SortPlan p = sort_plan(n, begin_bit, end_bit);
-  const bool pay = prec != nullptr;
-  if (pay && (!drop || first_pass != 0 || p.width != 8 || p.items > 8 || !pa || !pb || !pout)) {
-    set_error("radix_sort_pairs: payload needs the compacting 8-bit depth sort");
-    return 1;
-  }
   if (p.passes == 0) {
     note(hipMemcpyAsync(kout, ka, n * sizeof(K), hipMemcpyDeviceToDevice, st), "hipMemcpyAsync");
     note(hipMemcpyAsync(vout, va, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, st),
@@ -734,16 +552,13 @@ int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t
     kr.assume = assume_const;
     kr.out = range_out;
   }
-  // first_pass = 1: the caller ran pass 0 itself, into (kb, vb)
-  K *kin = first_pass ? kb : ka, *kalt = first_pass ? ka : kb;
-  uint32_t *vin = first_pass ? vb : va, *valt = first_pass ? va : vb;
+  K *kin = ka, *kalt = kb;
+  uint32_t *vin = va, *valt = vb;
   // with the key range, the device picks every pass's buffers (DevIO) and constant digits move
   // nothing (no copy)
   DevIO io{};
-  if (kr.fin && first_pass == 0)
-    io = DevIO{kr.fin, ka, kb, va, vb, kout, vout, begin_bit, p.width, p.passes, pa, pb, pout};
-  uint2 *pin = nullptr, *palt = pb;  // host-selected payload buffers (pass 0 reads prec)
-  for (int q = first_pass; q < p.passes; ++q) {
+  if (kr.fin) io = DevIO{kr.fin, ka, kb, va, vb, kout, vout, begin_bit, p.width, p.passes};
+  for (int q = 0; q < p.passes; ++q) {
     // a digit the caller's earlier range says is constant: not launched at all (its three
     // launches cost ~14 us at the headline even when they return at once); the pass-0 range
     // reduction checks the assumption (kr.out)
@@ -752,49 +567,29 @@ int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t
     const bool last = q == p.passes - 1;
     K *ko = last ? kout : kalt;
     uint32_t *vo = last ? vout : valt;
-    uint2 *po = last ? pout : palt;
     // tile digit counts -> row scans -> offsets
     const int sh = begin_bit + q * p.width;
-    const uint32_t *ndev = drop ? (q > 0 ? kept : nullptr) : n_dev_all;
+    const uint32_t *ndev = drop && q > 0 ? kept : nullptr;
     // first_counts_ready: the key kernel wrote pass 0's counts and key ranges (kr.blk)
     if (q == 0 && first_counts_ready) {
     } else if (p.items == 16)
       hipLaunchKernelGGL((rts_count_kernel<K, 16>), dim3((unsigned)p.nblocks), dim3(TPB), 0, st,
-                         kin, n, sh, p.width, p.nblocks, counts, drop && q == 0, ndev, kr, q, io,
-                         n_dev_all ? 1 : 0);
-    else if (p.items == 8)
-      hipLaunchKernelGGL((rts_count_kernel<K, 8>), dim3((unsigned)p.nblocks), dim3(TPB), 0, st,
-                         kin, n, sh, p.width, p.nblocks, counts, drop && q == 0, ndev, kr, q, io,
-                         n_dev_all ? 1 : 0);
+                         kin, n, sh, p.width, p.nblocks, counts, drop && q == 0, ndev, kr, q, io);
     else
       hipLaunchKernelGGL((rts_count_kernel<K, 4>), dim3((unsigned)p.nblocks), dim3(TPB), 0, st,
-                         kin, n, sh, p.width, p.nblocks, counts, drop && q == 0, ndev, kr, q, io,
-                         n_dev_all ? 1 : 0);
+                         kin, n, sh, p.width, p.nblocks, counts, drop && q == 0, ndev, kr, q, io);
     hipLaunchKernelGGL(rts_rowscan_kernel,
                        dim3((unsigned)p.radix + (q == 0 && kr.blk ? 1u : 0u)), dim3(1024), 0,
                        st, counts, p.nblocks, rowtot, kr, q, sh, p.width);
-#define OS_PASS_PL(Wd, It, PLv)                                                             \
-  hipLaunchKernelGGL((os_pass_kernel<K, Wd, It, PLv>), dim3((unsigned)p.nblocks), dim3(TPB), 0,  \
-                     st, kin, vin, ko, vo, n, sh, p.width, rowtot, counts, p.nblocks,          \
-                     last ? tile_bins : nullptr, drop && q == 0,                               \
-                     ndev, drop && q == 0 ? kept : nullptr,                                    \
-                     q > 0 && !io.fin ? kr.fin : nullptr, io, q, n_dev_all ? 1 : 0, prec,      \
-                     pin, po)
-#define OS_PASS(Wd, It) OS_PASS_PL(Wd, It, 0)
+#define OS_PASS(Wd, It)                                                                     \
+  hipLaunchKernelGGL((os_pass_kernel<K, Wd, It>), dim3((unsigned)p.nblocks), dim3(TPB), 0, st, \
+                     kin, vin, ko, vo, n, sh, p.width, rowtot, counts, p.nblocks,              \
+                     drop && q == 0, ndev, drop && q == 0 ? kept : nullptr,                    \
+                     q > 0 && !io.fin ? kr.fin : nullptr, io, q)
 #define OS_PASS_W(Wd)                                                                       \
   do {                                                                                      \
-    if (p.items == 16) OS_PASS(Wd, 16); else if (p.items == 8) OS_PASS(Wd, 8);             \
-    else OS_PASS(Wd, 4);                                                                    \
+    if (p.items == 16) OS_PASS(Wd, 16); else OS_PASS(Wd, 4);                                \
   } while (0)
-#define OS_PASS_P(PLv)                                                                      \
-  do {                                                                                      \
-    if (p.items == 8) OS_PASS_PL(8, 8, PLv); else OS_PASS_PL(8, 4, PLv);                    \
-  } while (0)
-    if (sizeof(K) == 4 && pay) {
-      if constexpr (sizeof(K) == 4) {
-        if (q == 0) OS_PASS_P(1); else OS_PASS_P(2);
-      }
-    } else
     switch (p.width) {
       case 1: OS_PASS_W(1); break;
       case 2: OS_PASS_W(2); break;
@@ -805,23 +600,15 @@ int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t
       case 7: OS_PASS_W(7); break;
       default: OS_PASS_W(8); break;
     }
-#undef OS_PASS_P
 #undef OS_PASS_W
 #undef OS_PASS
-#undef OS_PASS_PL
     K *kfree = (kin == ka || kin == kb) ? kin : kalt;
     uint32_t *vfree = (vin == va || vin == vb) ? vin : valt;
-    uint2 *pfree = (pin == pa || pin == pb) ? pin : (q == 0 ? pa : palt);
     kin = ko;
     vin = vo;
     kalt = kfree;
     valt = vfree;
-    pin = po;
-    palt = pfree;
   }
-  if (tile_bins)
-    hipLaunchKernelGGL(bins_decode_kernel, dim3(cdiv(num_tiles, TPB)), dim3(TPB), 0, st,
-                       num_tiles, n, tile_bins, n_dev_all);
   return 0;
 }
 
@@ -987,53 +774,6 @@ __global__ __launch_bounds__(TPB) void gather_counts_kernel(int n, const uint32_
   if (threadIdx.x == 0) partial[blockIdx.x] = total;
 }
 
-// Depth-ordered allotments from the boxes the depth sort carried (box[p], p < kept): cnt[p] =
-// the box's tile count, which is the record's allotment (the fused preprocess writes allotment
-// = box area; a caller's num_tiles_hit that disagrees arrives as BOX_GATHER and is read from
-// the record), zero past the visible count.  One workgroup per scan tile
-// (SC_TILE entries), whose allotment sum it writes (the first step of the device scan).  Reads
-// only coalesced words: the records' random gather by depth order (gather_counts_kernel,
-// ~18 us at the headline) is gone.
-__global__ __launch_bounds__(TPB) void box_counts_kernel(int n, const uint32_t *__restrict__ kept,
-                                                         uint2 *__restrict__ box,
-                                                         const uint32_t *__restrict__ order,
-                                                         const uint4 *__restrict__ rec,
-                                                         uint32_t *__restrict__ cnt,
-                                                         int *__restrict__ num_visible,
-                                                         uint32_t *__restrict__ partial) {
-  __shared__ uint32_t lds[TPB / 64];
-  const long long base = (long long)blockIdx.x * SC_TILE;
-  const long long nv = min((long long)n, (long long)*kept);
-  if (blockIdx.x == 0 && threadIdx.x == 0) *num_visible = (int)nv;
-  uint2 b[SC_ITEMS];
-#pragma unroll
-  for (int k = 0; k < SC_ITEMS; ++k) b[k] = box[min(base + k * TPB + threadIdx.x, max(nv - 1, 0LL))];
-  uint32_t sum = 0;
-#pragma unroll
-  for (int k = 0; k < SC_ITEMS; ++k) {
-    const long long p = base + k * TPB + threadIdx.x;
-    if (p < n) {
-      uint32_t c = 0u;
-      if (p < nv) {
-        if (b[k].x == BOX_GATHER) {  // an inconsistent allotment (see os_pass_kernel's PL)
-          // (clamped: after a depth-key range violation the order is garbage; the caller
-          // discards that binning, but no read may leave the records)
-          const uint4 r = rec[min(order[p], (uint32_t)n - 1u)];
-          box[p] = make_uint2(r.y, r.z);
-          c = r.x;
-        } else {
-          c = box_area(b[k]);
-        }
-      }
-      cnt[p] = c;
-      sum += c;
-    }
-  }
-  uint32_t total;
-  block_exclusive_scan<TPB>(sum, total, lds);
-  if (threadIdx.x == 0) partial[blockIdx.x] = total;
-}
-
 // Inclusive max-scan over the wave (DPP row shifts, then the row broadcasts; no LDS).
 __device__ __forceinline__ int wave_incl_max(int v) {
   constexpr int NONE = -2147483647 - 1;
@@ -1063,192 +803,6 @@ __device__ __forceinline__ int slot_owner(int *mk, uint32_t j0, uint32_t rel, bo
   const int own = max(wave_incl_max(mk[lane]), carry);
   carry = __builtin_amdgcn_readlane(own, 63);
   return own & 63;
-}
-
-// One wave per 64 depth-ordered Gaussians: the wave fills their combined slot range
-// [off[p0], off[p0] + total) with lanes striding over it, so stores are coalesced.  Slot j
-// belongs to the lane q with start[q] <= j < start[q+1] (6-step shuffle search); its tile
-// is the (j - start[q])-th tile of q's bbox in row-major order.  An allotment larger than
-// the bbox (inconsistent caller inputs) is padded with the sentinel tile id T.
-__global__ __launch_bounds__(TPB) void emit_kernel(int n, const uint32_t *__restrict__ order,
-                                                   const uint32_t *__restrict__ cnt,
-                                                   const uint32_t *__restrict__ off,
-                                                   const uint2 *__restrict__ box, int tbx,
-                                                   int tby, uint32_t *__restrict__ tkeys,
-                                                   uint32_t *__restrict__ tvals,
-                                                   int *__restrict__ tile_bins,
-                                                   const uint32_t *__restrict__ i_dev = nullptr,
-                                                   uint32_t cap = 0) {
-  // tile_bins starts zeroed for bin_edges_kernel (empty tiles stay (0, 0)): cleared here
-  // instead of by a separate fill launch -- also on an overflow below, so that a blend launched
-  // behind a capacity overflow reads empty tiles, not a stale table
-  for (long long i = (long long)blockIdx.x * TPB + threadIdx.x; i < 2LL * tbx * tby;
-       i += (long long)gridDim.x * TPB)
-    tile_bins[i] = 0;
-  // pre-launched before the host knows I (gsplat_bin_emit_prelaunch / _speculative): outputs
-  // hold cap slots; a larger I writes nothing (the host then re-runs the emission into larger
-  // buffers)
-  if (i_dev && *i_dev > cap) return;
-  const int lane = threadIdx.x & 63;
-  const long long p0 = ((long long)blockIdx.x * TPB + threadIdx.x) - lane;
-  if (p0 >= n) return;  // wave-uniform
-  const long long p = p0 + lane;
-  const bool in = p < n;
-  uint32_t c = 0, g = 0, start = 0;
-  uint2 b = make_uint2(0u, 0u);  // {x0 | y0 << 16, x1 | y1 << 16}: an empty box
-  if (in) {
-    c = cnt[p];
-    start = off[p];
-    if (c) {
-      g = order[p];
-      b = box[p];
-    }
-  }
-  const uint32_t base = __shfl(start, 0, 64);
-  const int last_lane = (int)min(63LL, (long long)n - 1 - p0);
-  const uint32_t total = __shfl(start + c, last_lane, 64) - base;
-  const uint32_t rel = in ? start - base : total;  // lanes past n are never chosen
-  // wave-uniform trip count: every lane stays active for the shuffles (a shuffle reading an
-  // inactive lane is undefined); only the stores are predicated.
-  __shared__ int emit_marks[TPB];
-  int *mk = emit_marks + (threadIdx.x & ~63);  // (slot owners: slot_owner)
-  mk[lane] = -1;
-  int carry = -1;
-  for (uint32_t j0 = 0; j0 < total; j0 += 64) {
-    const uint32_t j = j0 + lane;
-    const int q = slot_owner(mk, j0, rel, c != 0u, carry);  // the last q with rel[q] <= j
-    const uint32_t li = j - __shfl(rel, q, 64);
-    // the owner's box (two shuffles of the packed corners) and id
-    const uint32_t b0 = __shfl(b.x, q, 64), b1 = __shfl(b.y, q, 64);
-    const uint32_t qg = __shfl(g, q, 64);
-    const int qx0 = (int)(b0 & 0xFFFFu), qy0 = (int)(b0 >> 16);
-    const int qx1 = (int)(b1 & 0xFFFFu), qy1 = (int)(b1 >> 16);
-    const int qbw = max(qx1 - qx0, 1);
-    const int qarea = max(qx1 - qx0, 0) * max(qy1 - qy0, 0);
-    uint32_t tile;
-    if ((int)li < qarea) {
-      // row = li / bw: (li + 0.5) / bw is at least 0.5 / bw from an integer, far more than
-      // the float quotient's error while li < 2^20; exact integer division beyond
-      const int ly = li < (1u << 20)
-                         ? (int)(((float)li + 0.5f) * __builtin_amdgcn_rcpf((float)qbw))
-                         : (int)li / qbw;
-      tile = (uint32_t)((qy0 + ly) * tbx + qx0 + ((int)li - ly * qbw));
-    } else {
-      tile = (uint32_t)(tbx * tby);
-    }
-    if (j < total) {
-      tkeys[base + j] = tile;
-      tvals[base + j] = qg;
-    }
-  }
-}
-
-// The speculative binning's emission (gsplat_bin_speculative) with the allotment scan folded
-// in: one workgroup per round of 256 depth-ordered Gaussians (a quarter of a gather_counts scan
-// tile) takes its base offset and the total I straight from gather_counts' per-tile sums (at
-// most a few thousand words, summed in fixed order) plus the allotments of the rounds before it
-// in its tile, scans its own allotments and emits them wave by wave exactly as emit_kernel does
-// -- the scan_partials and scan_downsweep launches (and the off[] array) are gone.  (One
-// workgroup per whole tile, four rounds each, left c3's 300 workgroups ~1 per CU: 28 us.)  Workgroup 0 publishes I to the
-// device word the tile sort reads and to the host's pinned slot.  I > cap: the table is
-// cleared and nothing is emitted (the caller re-bins).
-__global__ __launch_bounds__(TPB) void emit_scan_kernel(int n, int nb,
-                                                        const uint32_t *__restrict__ order,
-                                                        const uint32_t *__restrict__ cnt,
-                                                        const uint32_t *__restrict__ partial,
-                                                        const uint2 *__restrict__ box, int tbx,
-                                                        int tby, uint32_t *__restrict__ tkeys,
-                                                        uint32_t *__restrict__ tvals,
-                                                        int *__restrict__ tile_bins,
-                                                        uint32_t *__restrict__ i_dev,
-                                                        int32_t *__restrict__ i_host, uint32_t cap,
-                                                        const uint32_t *__restrict__ kfin = nullptr,
-                                                        uint32_t assume = 0u) {
-  __shared__ uint32_t lds[TPB / 64];
-  __shared__ int emit_marks[TPB];  // (per wave: the slot-owner marks)
-  for (long long i = (long long)blockIdx.x * TPB + threadIdx.x; i < 2LL * tbx * tby;
-       i += (long long)gridDim.x * TPB)
-    tile_bins[i] = 0;
-  const int tid = threadIdx.x, lane = tid & 63;
-  // one round of TPB depth-ordered Gaussians per workgroup: round rr of scan tile t (the
-  // partial sums are per scan tile; the rounds before this one in the tile are summed here)
-  const int t = (int)(blockIdx.x / SC_ITEMS), rr = (int)(blockIdx.x % SC_ITEMS);
-  const long long b0 = (long long)t * SC_TILE;
-  const long long p = b0 + (long long)rr * TPB + tid;
-  uint32_t cr[SC_ITEMS];  // (all loads in flight together: clamped, no branch)
-#pragma unroll
-  for (int r = 0; r < SC_ITEMS; ++r) {
-    const long long pr = b0 + r * TPB + tid;
-    cr[r] = (r <= rr && pr < n) ? cnt[pr] : 0u;
-  }
-  uint32_t pre = 0, tot = 0;
-  for (int k = tid; k < nb; k += TPB) {
-    const uint32_t v = partial[k];
-    tot += v;
-    pre += k < t ? v : 0u;
-  }
-  uint32_t c = 0;
-#pragma unroll
-  for (int r = 0; r < SC_ITEMS; ++r) {
-    if (r < rr) pre += cr[r];
-    if (r == rr) c = cr[r];
-  }
-  uint32_t bpre, btot;
-  block_exclusive_scan<TPB>(pre, bpre, lds);  // (only the totals are used)
-  block_exclusive_scan<TPB>(tot, btot, lds);
-  // a depth-key digit the sort assumed constant varied (KeyRange): the depth order, and with
-  // it every id and box, is wrong -- treated as an overflow, so nothing is emitted or sorted
-  // and the blend behind reads an empty table (the host sees the violation and starts over)
-  const bool violated = assume && (((kfin[0] ^ kfin[1]) & assume) != 0u);
-  if (blockIdx.x == 0 && tid == 0) {
-    *i_dev = violated ? 0xFFFFFFFFu : btot;
-    if (i_host) *i_host = (int32_t)btot;
-  }
-  if (violated || btot > cap) return;  // workgroup-uniform
-  {
-    uint32_t rtot;
-    const uint32_t start = bpre + block_exclusive_scan<TPB>(c, rtot, lds);
-    const long long p0 = p - lane;
-    if (p0 >= n) return;  // wave-uniform (no barrier below)
-    const bool in = p < n;
-    uint32_t g = 0;
-    uint2 bx = make_uint2(0u, 0u);
-    if (in && c) {
-      g = order[p];
-      bx = box[p];
-    }
-    const uint32_t base = __shfl(start, 0, 64);
-    const int last_lane = (int)min(63LL, (long long)n - 1 - p0);
-    const uint32_t total = __shfl(start + c, last_lane, 64) - base;
-    const uint32_t rel = in ? start - base : total;
-    int *mk = emit_marks + (threadIdx.x & ~63);  // (slot owners: slot_owner)
-    mk[lane] = -1;
-    int carry = -1;
-    for (uint32_t j0 = 0; j0 < total; j0 += 64) {
-      const uint32_t j = j0 + lane;
-      const int q = slot_owner(mk, j0, rel, c != 0u, carry);
-      const uint32_t li = j - __shfl(rel, q, 64);
-      const uint32_t q0 = __shfl(bx.x, q, 64), q1 = __shfl(bx.y, q, 64);
-      const uint32_t qg = __shfl(g, q, 64);
-      const int qx0 = (int)(q0 & 0xFFFFu), qy0 = (int)(q0 >> 16);
-      const int qx1 = (int)(q1 & 0xFFFFu), qy1 = (int)(q1 >> 16);
-      const int qbw = max(qx1 - qx0, 1);
-      const int qarea = max(qx1 - qx0, 0) * max(qy1 - qy0, 0);
-      uint32_t tile;
-      if ((int)li < qarea) {
-        const int ly = li < (1u << 20)
-                           ? (int)(((float)li + 0.5f) * __builtin_amdgcn_rcpf((float)qbw))
-                           : (int)li / qbw;
-        tile = (uint32_t)((qy0 + ly) * tbx + qx0 + ((int)li - ly * qbw));
-      } else {
-        tile = (uint32_t)(tbx * tby);
-      }
-      if (j < total) {
-        tkeys[base + j] = tile;
-        tvals[base + j] = qg;
-      }
-    }
-  }
 }
 
 // ------------------------------------------------------------------ region binning
@@ -1540,7 +1094,7 @@ __global__ __launch_bounds__(RB_NT) void rb_count_kernel(RbPlan p, int n,
   rb_region(p, g, rx0, ry0, rx1, ry1, tg);
   const int rw = rx1 - rx0;
   const bool sentinel = g >= p.G;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int tid = threadIdx.x, wave = tid >> 6;
   for (int i = tid; i < RB_NW * RB_TG_MAX; i += RB_NT) (&cw[0][0])[i] = 0u;
   __syncthreads();
   const long long nv = min((long long)n, (long long)*kept);
@@ -2035,236 +1589,6 @@ __global__ __launch_bounds__(BK_NT) void bk_place_kernel(int n, const uint4 *__r
   }
 }
 
-// ---- intersection generation from the depth-ordered allotments (large frames) ----
-// The intersections in depth order (slot j of the exclusive scan `off` of the depth-ordered
-// allotments), generated on the fly without an emitted (tile, id) array: slots are cut into
-// wave segments of 256 (4 per lane); tc_first_kernel records the owner of every segment's
-// first slot, and tc_gen regenerates a segment's (tile, id) pairs from it (ep0_* below).  (A
-// counting sort placing them straight into their tile buckets was measured slower at every
-// size: a (chunk, tile) cell holds ~3.5 ids at the headline, so its placement writes are runs
-// of 4-14 bytes; headline 0.267 vs 0.255 ms, c5 2.35 vs 1.93 ms.)
-constexpr int TC_NT = 1024;
-constexpr int TC_NW = TC_NT / 64;
-constexpr int TC_SEG = 256;                 // slots per wave segment (4 per lane)
-constexpr int TC_ROUND = TC_SEG * TC_NW;    // slots per workgroup round
-
-struct TcSrc {
-  const uint32_t *first, *off, *cnt, *order;
-  const uint2 *box;
-  int n;
-  uint32_t I;
-  int tbx, tby;
-};
-
-__global__ __launch_bounds__(TPB) void tc_first_kernel(int n, const uint32_t *__restrict__ cnt,
-                                                       const uint32_t *__restrict__ off,
-                                                       uint32_t *__restrict__ first) {
-  const long long p = (long long)blockIdx.x * TPB + threadIdx.x;
-  if (p >= n) return;
-  const uint32_t c = cnt[p];
-  if (!c) return;
-  const uint32_t o = off[p];
-  for (uint32_t s = (o + TC_SEG - 1) / TC_SEG; s <= (o + c - 1) / TC_SEG; ++s) first[s] = (uint32_t)p;
-}
-
-// Slots seg * 256 + k * 64 + lane (k < 4) of the depth-ordered intersection list: tile (T for
-// an allotment's padding past its box, as emit_kernel; ~0 past I) and Gaussian id.  The wave
-// holds a window of 64 consecutive depth-ordered Gaussians starting at the segment's first
-// owner; a slot's owner is the largest window lane whose slot range starts at or before it (a
-// six-step shuffle search); the window moves on by 64 while slots lie past its end.
-__device__ __forceinline__ void tc_gen(const TcSrc &S, long long seg, uint32_t (&tile)[4],
-                                       uint32_t (&gid)[4]) {
-  const int lane = threadIdx.x & 63;
-  long long p0 = S.first[seg];
-  uint32_t o, c, b0, b1, g;
-  auto load = [&]() {
-    const long long p = p0 + lane;
-    o = S.I;
-    c = b0 = b1 = g = 0u;
-    if (p < S.n) {
-      o = S.off[p];
-      c = S.cnt[p];
-      if (c) {
-        const uint2 bb = S.box[p];
-        b0 = bb.x;
-        b1 = bb.y;
-        g = S.order[p];
-      }
-    }
-  };
-  load();
-  uint32_t wend = __shfl(o + c, 63, 64);
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const uint32_t j = (uint32_t)(seg * TC_SEG) + (uint32_t)(k * 64 + lane);
-    bool todo = j < S.I;
-    tile[k] = ~0u;
-    gid[k] = 0u;
-    while (true) {
-      const bool here = todo && j < wend;
-      int q = 0;
-#pragma unroll
-      for (int step = 32; step >= 1; step >>= 1) {
-        const uint32_t oq = __shfl(o, (q + step) & 63, 64);
-        if (q + step <= 63 && oq <= j) q += step;
-      }
-      const uint32_t li = j - __shfl(o, q, 64);
-      const uint32_t q0 = __shfl(b0, q, 64), q1 = __shfl(b1, q, 64), qg = __shfl(g, q, 64);
-      if (here) {
-        const int qx0 = (int)(q0 & 0xFFFFu), qy0 = (int)(q0 >> 16);
-        const int qx1 = (int)(q1 & 0xFFFFu), qy1 = (int)(q1 >> 16);
-        const int qbw = max(qx1 - qx0, 1);
-        const int qarea = max(qx1 - qx0, 0) * max(qy1 - qy0, 0);
-        uint32_t t;
-        if ((int)li < qarea) {
-          const int ly = li < (1u << 20)
-                             ? (int)(((float)li + 0.5f) * __builtin_amdgcn_rcpf((float)qbw))
-                             : (int)li / qbw;
-          t = (uint32_t)((qy0 + ly) * S.tbx + qx0 + ((int)li - ly * qbw));
-        } else {
-          t = (uint32_t)(S.tbx * S.tby);
-        }
-        tile[k] = t;
-        gid[k] = qg;
-        todo = false;
-      }
-      if (!__any(todo)) break;
-      p0 += 64;  // wave-uniform
-      load();
-      wend = __shfl(o + c, 63, 64);
-    }
-  }
-}
-
-// One stable LDS radix pass over the workgroup's 4,096 16-bit keys (item order: wave, k,
-// lane): digit (key >> shift) & 255 ranked by ballot match with per-wave counters, then
-// offset by the digit's exclusive count over earlier waves and earlier digits.
-__device__ __forceinline__ void tc_rank_pass(const uint32_t (&key)[4], int shift,
-                                             uint32_t (&pos)[4], uint32_t *wcnt /*[16][256]*/,
-                                             uint32_t *dofs /*[256]*/, uint32_t *tmp,
-                                             int width = 8) {
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const unsigned long long lt = (1ull << lane) - 1ull;
-#pragma unroll
-  for (int u = 0; u < 4; ++u) wcnt[wave * 256 + u * 64 + lane] = 0u;
-  wave_lds_sync();
-  uint32_t rank[4], dig[4], old[4];
-  unsigned long long pr[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    dig[k] = (key[k] >> shift) & ((1u << width) - 1u);
-    pr[k] = digit_peers<8>(dig[k], width, true);
-  }
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    old[k] = 0u;
-    if ((int)__builtin_ctzll(pr[k]) == lane)
-      old[k] = atomicAdd(&wcnt[wave * 256 + dig[k]], (uint32_t)__popcll(pr[k]));
-  }
-#pragma unroll
-  for (int k = 0; k < 4; ++k)
-    rank[k] = __shfl(old[k], (int)__builtin_ctzll(pr[k]), 64) + (uint32_t)__popcll(pr[k] & lt);
-  __syncthreads();
-  uint32_t s = 0;
-  if (tid < 256) {
-#pragma unroll
-    for (int w = 0; w < TC_NW; ++w) {
-      const uint32_t c = wcnt[w * 256 + tid];
-      wcnt[w * 256 + tid] = s;
-      s += c;
-    }
-  }
-  uint32_t tot;
-  const uint32_t ex = block_exclusive_scan<TC_NT>(tid < 256 ? s : 0u, tot, tmp);
-  if (tid < 256) dofs[tid] = ex;
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < 4; ++k) pos[k] = dofs[dig[k]] + wcnt[wave * 256 + dig[k]] + rank[k];
-  __syncthreads();  // wcnt / dofs are reused by the next pass
-}
-
-// ---- the tile sort's first LSD pass, generated (shipped) ----
-// Pass 0 of the tile-id radix sort takes its (tile, id) pairs straight from the depth-ordered
-// allotments (tc_gen) instead of from an emitted key array: ep0_count_kernel histograms each
-// 4,096-slot round's low tile digit (digit-major counts, the reduce-then-scan layout), the row
-// scan makes them offsets, and ep0_place_kernel regenerates the round, ranks it stably by the
-// digit in LDS and writes it out in digit order (runs of ~32 per digit, as an os_pass tile).
-// Saves the emission's 8 I-byte write and pass 0's re-read of it (used for I >= 2^24: see
-// use_emit_pass0).
-__global__ __launch_bounds__(TC_NT) void ep0_count_kernel(TcSrc S, int width, long long nrounds,
-                                                          uint32_t *__restrict__ counts,
-                                                          int *__restrict__ tile_bins) {
-  __shared__ uint32_t h[256];
-  const int tid = threadIdx.x, wave = tid >> 6;
-  // the tile table starts zeroed for the last pass's run ends (emit_kernel's job before)
-  for (long long i = (long long)blockIdx.x * TC_NT + tid; i < 2LL * S.tbx * S.tby;
-       i += (long long)gridDim.x * TC_NT)
-    tile_bins[i] = 0;
-  if (tid < 256) h[tid] = 0u;
-  __syncthreads();
-  const uint32_t mask = (1u << width) - 1u;
-  const long long seg = (long long)blockIdx.x * TC_NW + wave;
-  if (seg * TC_SEG < (long long)S.I) {
-    uint32_t tile[4], gid[4];
-    tc_gen(S, seg, tile, gid);
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (tile[k] != ~0u) atomicAdd(&h[tile[k] & mask], 1u);
-  }
-  __syncthreads();
-  if (tid < (1 << width)) counts[(size_t)tid * nrounds + blockIdx.x] = h[tid];
-}
-
-__global__ __launch_bounds__(TC_NT) void ep0_place_kernel(TcSrc S, int width, long long nrounds,
-                                                          const uint32_t *__restrict__ rowtot,
-                                                          const uint32_t *__restrict__ offs,
-                                                          uint32_t *__restrict__ kout,
-                                                          uint32_t *__restrict__ vout) {
-  __shared__ uint32_t keys[TC_ROUND], vals[TC_ROUND];
-  __shared__ uint32_t wcnt[TC_NW * 256], dofs[256], gofs[256], tmp[16];
-  const int tid = threadIdx.x, wave = tid >> 6;
-  const int R = 1 << width;
-  const uint32_t mask = (uint32_t)(R - 1);
-  const long long rbase = (long long)blockIdx.x * TC_ROUND;
-  const uint32_t nvalid = (uint32_t)min((long long)TC_ROUND, (long long)S.I - rbase);
-  {  // digit bases: exclusive scan of the row totals
-    uint32_t tot;
-    const uint32_t hs = block_exclusive_scan<TC_NT>(tid < R ? rowtot[tid] : 0u, tot, tmp);
-    if (tid < R) gofs[tid] = hs + offs[(size_t)tid * nrounds + blockIdx.x];
-  }
-  const long long seg = rbase / TC_SEG + wave;
-  uint32_t key[4], gid[4], pos[4];
-  if (seg * TC_SEG < (long long)S.I) {
-    tc_gen(S, seg, key, gid);
-  } else {
-#pragma unroll
-    for (int k = 0; k < 4; ++k) key[k] = ~0u, gid[k] = 0u;
-  }
-  // slots past I (last round only): the largest digit, so they rank after every valid key
-  uint32_t rk[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) rk[k] = key[k] == ~0u ? mask : key[k];
-  tc_rank_pass(rk, 0, pos, wcnt, dofs, tmp, width);
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    keys[pos[k]] = key[k];
-    vals[pos[k]] = gid[k];
-  }
-  __syncthreads();
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const uint32_t i = (uint32_t)(u * TC_NT + tid);
-    if (i < nvalid) {
-      const uint32_t k = keys[i];
-      const uint32_t d = k & mask;
-      const uint32_t g = gofs[d] + (i - dofs[d]);
-      kout[g] = k;
-      vout[g] = vals[i];
-    }
-  }
-}
-
-
 // ---- per-tile LSD radix sort (bk_sort_kernel) ----
 // ITEMS = 0: the MSD kernel's layout (key/val arrays of CAPX entries)
 template <int NT, int ITEMS>
@@ -2693,11 +2017,10 @@ struct Carver {
 };
 
 struct Phase1 {
-  uint32_t *dkeys_a, *dvals_a, *dkeys_b, *dvals_b, *order, *cnt, *off;
+  uint32_t *dkeys_a, *dvals_a, *dkeys_b, *dvals_b, *order, *cnt;
   uint4 *rec;  // per-Gaussian binning record (Gaussian order)
-  uint2 *box;  // tile bbox in depth order (the depth sort's sorted payload)
-  uint2 *pay_a, *pay_b;  // the depth sort's payload ping-pong buffers
-  uint32_t *dcount;  // I on the device (the pre-launched emission's bound check)
+  uint2 *box;  // tile bbox in depth order (gather_counts_kernel)
+  uint32_t *dcount;  // I on the device (the capacity-launched placement's bound check)
   uint32_t *rmask;   // region-membership filter per depth position (rb_mask)
   void *rs_ws;
   size_t bytes;
@@ -2713,11 +2036,8 @@ Phase1 carve_phase1(void *base, int n) {
   p.dvals_b = c.take<uint32_t>(nn);
   p.order = c.take<uint32_t>(nn);
   p.cnt = c.take<uint32_t>(nn);
-  p.off = c.take<uint32_t>(nn);
   p.rec = c.take<uint4>(nn * 4);
   p.box = c.take<uint2>(nn * 2);
-  p.pay_a = c.take<uint2>(nn * 2);
-  p.pay_b = c.take<uint2>(nn * 2);
   p.dcount = c.take<uint32_t>(4 * sizeof(uint32_t));
   p.rmask = c.take<uint32_t>(nn);
   size_t rs = radix_ws_bytes(n, 0, 32);
@@ -2731,27 +2051,6 @@ int bits_for(long long v) {  // smallest b with (1 << b) > v
   int b = 0;
   while (b < 62 && (1LL << b) <= v) ++b;
   return b;
-}
-
-struct Phase2 {
-  uint32_t *tk_a, *tv_a, *tk_b, *tv_b;
-  uint32_t *first;  // segment owners of the generated first tile pass (tc_first_kernel)
-  void *rs_ws;
-  size_t bytes;
-};
-
-Phase2 carve_phase2(void *base, long long I) {
-  Phase2 p;
-  Carver c(base);
-  size_t ii = (size_t)(I > 0 ? I : 1) * 4;
-  p.tk_a = c.take<uint32_t>(ii);
-  p.tv_a = c.take<uint32_t>(ii);
-  p.tk_b = c.take<uint32_t>(ii);
-  p.tv_b = c.take<uint32_t>(ii);
-  p.first = c.take<uint32_t>((size_t)(I > 0 ? cdiv(I, (long long)TC_SEG) : 1) * 4);
-  p.rs_ws = c.take<char>(radix_ws_bytes(I, 0, 32));  // >= any tile-key width
-  p.bytes = c.off;
-  return p;
 }
 
 // bucket scheme, phase 2: M [nwg][nbk], tot/start [nbk], last-block counter, the grouped ids
@@ -2782,17 +2081,6 @@ BkWs carve_bk(void *base, int n, long long I, long long T) {
   return w;
 }
 
-// tile counting sort, phase 2: segment owners, the chunk x bucket matrix, bucket totals /
-// starts, the scan's last-block counter
-// gsplat_debug_emit_pass0: 0 = emit_kernel + a plain first pass, 1 = generated first pass when
-// the emitted pairs (8 I bytes) would not stay in the 256 MB MALL (I >= 2^24), 2 = always.
-// Measured (tools/exp_binning.py): c5 (83M) 1.93 -> 1.78 ms; headline (7.7M) 0.256 -> 0.268 ms
-// and c4 (8.7M) 0.333 -> 0.338 ms, where the emitted pairs are re-read from the MALL cheaply and
-// the generation's dependent loads (segment owner, then its window) cost more.
-int g_emit_pass0 = 1;
-bool use_emit_pass0(long long I) {
-  return g_emit_pass0 == 2 || (g_emit_pass0 == 1 && I >= (1LL << 24));
-}
 // Binning scheme (gsplat_debug_binning_scheme): -1 by size (shipped), 0 depth sort + tile sort,
 // 1 tile buckets + per-tile sorts.  The buckets need far fewer launches (8 against ~23), which
 // wins where every launch is short: small scenes, whose tile lists are short too (c2, 100k
@@ -2848,18 +2136,6 @@ extern "C" void gsplat_tune_rb(int wgs, int regs, int map) {
   g_rb_knobs[2] = map;
 }
 
-extern "C" int gsplat_debug_emit_pass0(int on) {
-  const int prev = g_emit_pass0;
-  if (on >= 0) g_emit_pass0 = on > 2 ? 2 : on;
-  return prev;
-}
-
-extern "C" int gsplat_debug_depth_payload(int on) {
-  const int prev = g_depth_payload ? 1 : 0;
-  if (on >= 0) g_depth_payload = on != 0;
-  return prev;
-}
-
 extern "C" int gsplat_debug_depth_key_range(int on) {
   const int prev = g_key_range;
   if (on >= 0) g_key_range = on > 2 ? 2 : on;
@@ -2875,8 +2151,7 @@ extern "C" int gsplat_debug_binning_scheme(int scheme) {
 extern "C" size_t gsplat_bin_emit_workspace_size_for(int num_points, int64_t num_intersects,
                                                      int tile_bounds_x, int tile_bounds_y) {
   const long long T = (long long)tile_bounds_x * tile_bounds_y;
-  if (num_points < 0 || num_intersects < 0 || tile_bounds_x <= 0 || tile_bounds_y <= 0)
-    return carve_phase2(nullptr, num_intersects).bytes;
+  if (num_points < 0 || num_intersects < 0 || tile_bounds_x <= 0 || tile_bounds_y <= 0) return 0;
   const size_t sorted = rb_ws_bytes(rb_plan(num_points, tile_bounds_x, tile_bounds_y));
   if (!use_bucket(num_points, T)) return sorted;
   const size_t bk = carve_bk(nullptr, num_points, num_intersects, T).bytes;
@@ -2885,10 +2160,6 @@ extern "C" size_t gsplat_bin_emit_workspace_size_for(int num_points, int64_t num
 
 extern "C" size_t gsplat_bin_count_workspace_size(int num_points) {
   return carve_phase1(nullptr, num_points).bytes;
-}
-
-extern "C" size_t gsplat_bin_emit_workspace_size(int64_t num_intersects) {
-  return carve_phase2(nullptr, num_intersects).bytes;
 }
 
 static int bin_count_impl(int num_points, const float *xys, const float *depths,
@@ -2954,35 +2225,20 @@ static int bin_count_impl(int num_points, const float *xys, const float *depths,
 #undef DEPTH_KEYS
   // range_out: d_counts[2..3] are written only when the key range is computed (the caller
   // zeroes them: without a range nothing is assumed and nothing reported)
-  // g_depth_payload (gsplat_debug_depth_payload, off by default): below 4M keys the sort carries
-  // each Gaussian's tile box (its record's y, z) to p.box in depth order and box_counts_kernel
-  // reads it coalesced, instead of gather_counts_kernel's random gather of the records by
-  // depth order.  Measured slower (round 4, same-box A/B, 2 reps: headline binning 0.2244 /
-  // 0.2278 -> 0.2302 / 0.2305 ms, c3 0.1406 / 0.1409 -> 0.1412 / 0.1417): the payload's extra
-  // 16 B per key and pass and its registers (occupancy 7 -> 6) cost the passes more than the
-  // gather's random reads.  Above 4M keys (16 keys per thread) never (occupancy 4 -> 2).
-  const bool carry = g_depth_payload && sp.items <= 8;
   if (radix_sort_pairs<uint32_t>(p.dkeys_a, p.dvals_a, p.dkeys_b, p.dvals_b, nullptr, p.order, n,
-                                 0, 32, p.rs_ws, st, pre, nullptr, 0, true, 0, nullptr,
+                                 0, 32, p.rs_ws, st, pre, true,
                                  use_key_range(n) ? assume_const : 0u,
-                                 range_out ? d_counts + 2 : nullptr, carry ? p.rec : nullptr,
-                                 p.pay_a, p.pay_b, p.box))
+                                 range_out ? d_counts + 2 : nullptr))
     return 1;
-  // depth-ordered allotments (+ per-tile sums) -> scan -> offsets and I = d_counts[1]
+  // depth-ordered allotments, boxes and region filter (+ per-block allotment sums) -> I
   const int nb = (int)cdiv(n, SC_TILE);
   // the kept count sits in the sort workspace's head, before the tile counts reused below
   const uint32_t *kept = sort_kept_word(p.rs_ws);
   uint32_t *partial = rts_tile_counts(p.rs_ws);  // the sort is done with its tile counts
-  if (carry)
-    hipLaunchKernelGGL(box_counts_kernel, dim3(nb), dim3(TPB), 0, st, n, kept, p.box, p.order,
-                       p.rec, p.cnt, d_counts, partial);
-  else
-  {
-    const RbPlan rp = rb_plan(n, tile_bounds_x, tile_bounds_y);
-    hipLaunchKernelGGL(gather_counts_kernel, dim3(nb), dim3(TPB), 0, st, n, p.order, kept, p.rec,
-                       p.cnt, p.box, d_counts, partial, p.rmask, rp.gw, rp.gh, rp.gxn);
-  }
-  if (no_scan) return check_launch("bin_count");  // (emit_scan_kernel scans, EMIT_SPEC)
+  const RbPlan rp = rb_plan(n, tile_bounds_x, tile_bounds_y);
+  hipLaunchKernelGGL(gather_counts_kernel, dim3(nb), dim3(TPB), 0, st, n, p.order, kept, p.rec,
+                     p.cnt, p.box, d_counts, partial, p.rmask, rp.gw, rp.gh, rp.gxn);
+  if (no_scan) return check_launch("bin_count");  // (the speculative binning: I from rb_tiles)
   // I = the sum of the allotments (the region binning needs no per-Gaussian offsets)
   hipLaunchKernelGGL(scan_partials_kernel, dim3(1), dim3(1024), 0, st, partial, nb,
                      (uint32_t *)(d_counts + 1), p.dcount);
@@ -3018,9 +2274,8 @@ extern "C" int gsplat_bin_count_keyed_ex(int num_points, int tile_bounds_x, int 
 }
 
 // The whole binning before the host knows I: the count phase (depth sort with the key-range
-// assumption, gather_counts), emit_scan_kernel (the allotment scan folded into the emission, I
-// published from the device) and the capacity-launched tile sort.  2 = the scheme needs I on
-// the host (nothing launched).
+// assumption, gather_counts) and the region binning with its placement launched at the
+// capacity (I published from the device, rb_tiles_kernel).
 enum { EMIT_HEAD = 1, EMIT_TAIL = 2, EMIT_ALL = 3, EMIT_SPEC = 4 };
 static int bin_emit_impl(int num_points, int64_t num_intersects, int64_t capacity,
                          int tile_bounds_x, int tile_bounds_y, int32_t *gaussian_ids_sorted,
@@ -3074,8 +2329,6 @@ extern "C" int gsplat_bin_speculative(int num_points, int64_t capacity, int tile
 // sorts).  EMIT_ALL = both, with cap = I (gsplat_bin_emit).
 // (EMIT_* : declared with gsplat_bin_speculative, above)
 
-static bool emit_head_splits(int, long long, long long) { return true; }
-
 static int bin_emit_impl(int num_points, int64_t num_intersects, int64_t capacity,
                          int tile_bounds_x, int tile_bounds_y, int32_t *gaussian_ids_sorted,
                          int32_t *tile_bins, const void *workspace1, size_t workspace1_bytes,
@@ -3091,10 +2344,8 @@ static int bin_emit_impl(int num_points, int64_t num_intersects, int64_t capacit
   }
   Phase1 p1 = carve_phase1(const_cast<void *>(workspace1), num_points);
   const long long cap = capacity;
-  // the head's launches run here unless they were pre-launched for this capacity
-  const bool split = phase != EMIT_ALL && emit_head_splits(num_points, cap, T);
-  const bool head = phase == EMIT_ALL || phase == EMIT_SPEC || (phase == EMIT_HEAD && split) ||
-                    (phase == EMIT_TAIL && !split);
+  // HEAD (pre-launched before the host read of I) needs no I-sized buffer; TAIL the rest
+  const bool head = phase != EMIT_TAIL;
   const bool tail = phase != EMIT_HEAD;
   const uint32_t *idev = phase == EMIT_HEAD ? p1.dcount : nullptr;  // bound check when pre-launched
   if (use_bucket(num_points, T)) {
@@ -3158,27 +2409,6 @@ static int bin_emit_impl(int num_points, int64_t num_intersects, int64_t capacit
   return check_launch("bin_emit");
 }
 
-// After a capacity overflow of gsplat_bin_speculative (which scans the allotments inside its
-// emission and leaves the offsets unwritten): the allotment scan into workspace1's offsets,
-// from the per-block sums its count phase left there, so gsplat_bin_emit can run for the exact
-// I (rasterize.SpeculativeBinning.rebin).  Sorted scheme only (the bucket scheme needs none).
-extern "C" int gsplat_bin_rescan(int num_points, int tile_bounds_x, int tile_bounds_y,
-                                 void *workspace1, size_t workspace1_bytes, void *stream) {
-  if (num_points < 0 || tile_bounds_x <= 0 || tile_bounds_y <= 0) {
-    set_error("bin_rescan: bad sizes (N=%d tiles=%dx%d)", num_points, tile_bounds_x,
-              tile_bounds_y);
-    return 1;
-  }
-  if (use_bucket(num_points, (long long)tile_bounds_x * tile_bounds_y)) return 0;  // (none)
-  Phase1 p = carve_phase1(workspace1, num_points);
-  if (workspace1_bytes < p.bytes) {
-    set_error("bin_rescan: workspace %zu < %zu bytes", workspace1_bytes, p.bytes);
-    return 1;
-  }
-  (void)stream;
-  return 0;  // the region binning reads no offsets: nothing to rescan
-}
-
 extern "C" int gsplat_bin_emit(int num_points, int64_t num_intersects, int tile_bounds_x,
                                int tile_bounds_y, int32_t *gaussian_ids_sorted,
                                int32_t *tile_bins, const void *workspace1,
@@ -3209,10 +2439,10 @@ extern "C" int gsplat_bin_emit_finish(int num_points, int64_t num_intersects, in
                        workspace2_bytes, stream, EMIT_TAIL);
 }
 
-// The emission and the whole tile sort launched at a capacity before the host knows I (the
-// device count decides; I > capacity leaves the table cleared and the ids unwritten, and the
-// caller re-bins).  Returns 2 without launching anything where the scheme needs I on the host
-// (tile buckets; the generated first tile pass, I >= 2^24): use prelaunch / finish there.
+// The region binning launched at a capacity before the host knows I (the device count decides;
+// I > capacity leaves the table cleared and the ids unwritten, and the caller re-bins).  Returns
+// 2 without launching anything where the scheme needs I on the host (tile buckets): use
+// prelaunch / finish there.
 extern "C" int gsplat_bin_emit_speculative(int num_points, int64_t capacity, int tile_bounds_x,
                                            int tile_bounds_y, int32_t *gaussian_ids_sorted,
                                            int32_t *tile_bins, const void *workspace1,
@@ -3220,7 +2450,7 @@ extern "C" int gsplat_bin_emit_speculative(int num_points, int64_t capacity, int
                                            size_t workspace2_bytes, void *stream) {
   const long long T = (long long)tile_bounds_x * tile_bounds_y;
   if (num_points > 0 && T > 0 && capacity > 0 &&
-      (use_bucket(num_points, T) || use_emit_pass0(capacity)))
+      use_bucket(num_points, T))
     return 2;
   if (capacity <= 0) {
     set_error("bin_emit_speculative: capacity must be positive");

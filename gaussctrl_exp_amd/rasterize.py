@@ -229,7 +229,6 @@ class SpeculativeBinning:
         self.layout_intersects = cap
         self.num_intersects = None
         self.range_violated = False
-        self.rescan = False  # rebin() must scan the allotments first (gsplat_bin_speculative)
 
     def finish(self) -> bool:
         visible = None
@@ -254,9 +253,6 @@ class SpeculativeBinning:
         I = self.num_intersects
         P, st = _lib.ptr, _lib.stream(self.dev)
         ids_buf, ws2 = _emit_buffers(self.dev, self.n, I, self.tbx, self.tby)
-        if self.rescan:  # gsplat_bin_speculative scanned inside its emission: offsets first
-            _lib.call("gsplat_bin_rescan", self.n, self.tbx, self.tby, P(self.ws1),
-                      self.ws1.numel(), st)
         _lib.call("gsplat_bin_emit", self.n, I, self.tbx, self.tby, P(ids_buf),
                   P(self.tile_bins), P(self.ws1), self.ws1.numel(), P(ws2), ws2.numel(), st)
         self.ids, self.ws2, self.cap = ids_buf, ws2, I
@@ -347,7 +343,6 @@ def bin_gaussians_speculative(xys: Tensor, depths: Tensor, radii: Tensor, num_ti
         raise
     sb = SpeculativeBinning(dev, n, tbx, tby, ws1, slot, counts, host, key, cap, ids_buf, ws2,
                             tile_bins)
-    sb.rescan = True  # (its emission scanned the allotments itself: no offsets in ws1)
     return sb
 
 

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define GSPLAT_MI355X_ABI_VERSION 13
+#define GSPLAT_MI355X_ABI_VERSION 14
 
 int gsplat_abi_version(void);
 const char *gsplat_last_error(void);
@@ -176,14 +176,14 @@ int gsplat_get_tile_bin_edges(int64_t num_intersects, const int64_t *isect_ids_s
  * Phase 1 (gsplat_bin_count) orders the visible Gaussians (radii > 0) front to back
  * (stable on the depth bits, ties by Gaussian id) and writes d_counts[0] = visible count,
  * d_counts[1] = total intersections I (device int32[2]).  The caller reads d_counts -- the
- * one host sync, like gsplat's cum_tiles_hit[-1].item() -- sizes phase 2's workspace from
- * I, and calls gsplat_bin_emit with BOTH workspaces (phase 1's must be left untouched in
- * between).  Phase 2 writes gaussian_ids_sorted [I] and tile_bins [tbx*tby, 2]; the order is
+ * one host sync, like gsplat's cum_tiles_hit[-1].item() -- sizes gaussian_ids_sorted from I,
+ * and calls gsplat_bin_emit with BOTH workspaces (phase 1's must be left untouched in
+ * between).  Phase 2 (the region binning: each depth-ordered intersection placed straight into
+ * its tile's list) writes gaussian_ids_sorted [I] and tile_bins [tbx*tby, 2]; the order is
  * identical to a stable sort of gsplat's 64-bit isect_ids. */
 size_t gsplat_bin_count_workspace_size(int num_points);
-size_t gsplat_bin_emit_workspace_size(int64_t num_intersects);
-/* Phase-2 workspace for the binning scheme in use (tile bucketing needs N and the tile
- * count; callers should size gsplat_bin_emit's workspace2 with this query). */
+/* Phase-2 workspace for the binning scheme in use (it depends on N and the tile grid; the
+ * small-scene tile buckets also on I). */
 size_t gsplat_bin_emit_workspace_size_for(int num_points, int64_t num_intersects,
                                           int tile_bounds_x, int tile_bounds_y);
 int gsplat_bin_count(int num_points, const float *xys, const float *depths,
@@ -212,9 +212,9 @@ int gsplat_bin_emit(int num_points, int64_t num_intersects, int tile_bounds_x,
                     size_t workspace2_bytes, void *stream);
 /* Phase 2 split around the host's read of I, so that the GPU is not idle while the host
  * waits for it: gsplat_bin_emit_prelaunch, issued right after phase 1 with buffers sized for
- * `capacity` intersections (e.g. the last call's I plus a margin), launches the part of the
- * emission that needs only phase 1's results -- each of its kernels compares the device-side
- * I with capacity and writes nothing when I > capacity.  Then, with the host's I:
+ * `capacity` intersections (e.g. the last call's I plus a margin), launches the part of
+ * phase 2 that needs only phase 1's results (the region binning's counts and tile table;
+ * I > capacity leaves the table all-zero).  Then, with the host's I:
  *   I <= capacity: gsplat_bin_emit_finish(..., I, capacity, ...) with the SAME buffers, stream
  *                  and capacity (the workspace layout follows capacity);
  *   I >  capacity: gsplat_bin_emit (or a new prelaunch + finish) into buffers sized for I.
@@ -228,31 +228,25 @@ int gsplat_bin_emit_finish(int num_points, int64_t num_intersects, int64_t capac
                            int tile_bounds_x, int tile_bounds_y, int32_t *gaussian_ids_sorted,
                            int32_t *tile_bins, const void *workspace1, size_t workspace1_bytes,
                            void *workspace2, size_t workspace2_bytes, void *stream);
-/* The whole of phase 2 before the host knows I: the emission AND the tile sort launched for
- * `capacity` intersections, each kernel reading the device-side I (phase 1's) -- so the blend
- * can be launched right behind it and the host reads I (d_counts[1]) only afterwards, while the
- * GPU works.  I <= capacity: gaussian_ids_sorted[0, I) and tile_bins are gsplat_bin_emit's
- * exactly.  I > capacity: nothing is emitted or sorted and tile_bins is left all-zero (a blend
- * behind it renders the background and touches no id); the caller re-bins into buffers sized
- * for I.  Buffers as for gsplat_bin_emit_prelaunch.  Returns 2 (nothing launched) when the
- * binning scheme for (num_points, tiles, capacity) needs I on the host -- the small-scene tile
- * buckets or the generated first tile pass (capacity >= 2^24): use prelaunch + finish there.
+/* The whole of phase 2 before the host knows I: the region binning launched for `capacity`
+ * intersections, its placement reading the device-side I -- so the blend can be launched right
+ * behind it and the host reads I (d_counts[1]) only afterwards, while the GPU works.
+ * I <= capacity: gaussian_ids_sorted[0, I) and tile_bins are gsplat_bin_emit's exactly.
+ * I > capacity: nothing is placed and tile_bins is left all-zero (a blend behind it renders the
+ * background and touches no id); the caller re-bins into buffers sized for I (gsplat_bin_emit
+ * from the same workspace1).  Buffers as for gsplat_bin_emit_prelaunch.  Returns 2 (nothing
+ * launched) when the binning scheme for (num_points, tiles) needs I on the host -- the
+ * small-scene tile buckets: use prelaunch + finish there.
  * Replaces, like gsplat_bin_emit, gsplat 0.1.2.1 rasterize.py's map / sort / bin edges. */
-/* gsplat_bin_count_keyed_ex + gsplat_bin_emit_speculative in one call, two launches fewer: the
- * allotment scan is folded into the emission (the emission publishes I to d_counts[1] from the
- * device).  Same outputs and overflow / range-violation semantics as the two calls; also the
- * small-scene tile buckets run capacity-launched here (each bucket kernel returns at once on an
- * overflow, the table cleared), so it returns 2 only for the generated first tile pass
- * (capacity >= 2^24).  d_counts int32[4] as gsplat_bin_count_keyed_ex's. */
+/* gsplat_bin_count_keyed_ex + gsplat_bin_emit_speculative in one call (I published to
+ * d_counts[1] from the device).  Same outputs and overflow / range-violation semantics as the
+ * two calls; the small-scene tile buckets also run capacity-launched here (each bucket kernel
+ * returns at once on an overflow, the table cleared).  d_counts int32[4] as
+ * gsplat_bin_count_keyed_ex's. */
 int gsplat_bin_speculative(int num_points, int64_t capacity, int tile_bounds_x, int tile_bounds_y,
                            int32_t *d_counts, void *workspace1, size_t workspace1_bytes,
                            uint32_t assume_const, int32_t *gaussian_ids_sorted, int32_t *tile_bins,
                            void *workspace2, size_t workspace2_bytes, void *stream);
-/* After gsplat_bin_speculative overflowed its capacity (returned 0, I > capacity): the
- * allotment scan it folded into its emission, written to workspace1, so that gsplat_bin_emit
- * can then bin the exact I from the same workspace1. */
-int gsplat_bin_rescan(int num_points, int tile_bounds_x, int tile_bounds_y, void *workspace1,
-                      size_t workspace1_bytes, void *stream);
 int gsplat_bin_emit_speculative(int num_points, int64_t capacity, int tile_bounds_x,
                                 int tile_bounds_y, int32_t *gaussian_ids_sorted,
                                 int32_t *tile_bins, const void *workspace1,
@@ -523,9 +517,6 @@ int gsplat_debug_raster_variant_is_default(void);
 /* Binning dispatch switches (not part of the gsplat surface; every setting gives the identical
  * output, tests cover each).  Each returns the previous setting; -1 (or, for the scheme, -2)
  * only queries.
- * gsplat_debug_emit_pass0: the tile sort's first pass run over emitted (tile, id) pairs (0),
- *   generated from the depth-ordered allotments without an emitted key array when I >= 2^24
- *   (1, shipped: the pairs would not stay in the MALL), or always generated (2).
  * gsplat_debug_depth_key_range: depth-sort passes whose digit is the same for every kept key
  *   (from the keys' AND / OR, found during the first pass) only copy -- from 2^22 keys (1,
  *   shipped), always (2) -- or rank as any pass (0).
@@ -533,10 +524,6 @@ int gsplat_debug_raster_variant_is_default(void);
  *   scenes of <= 131,072 Gaussians on frames up to 16,447 tiles, else the depth sort + stable
  *   tile sort), 0 depth sort + tile sort, 1 tile buckets.  Must not change between a
  *   gsplat_bin_count and its gsplat_bin_emit. */
-int gsplat_debug_emit_pass0(int on);
-/* Debug: the depth sort carries each Gaussian's tile box as a payload (1) instead of the
- * records' gather by depth order (0, the default: measured faster).  Returns the previous. */
-int gsplat_debug_depth_payload(int on);
 int gsplat_debug_depth_key_range(int on);
 int gsplat_debug_binning_scheme(int scheme);
 /* Profiling hook: the backward blend kernels record per wave {start, end (s_memrealtime,

@@ -51,16 +51,14 @@ def headline(request, gpu, oracle_lib):
                 colors=colors, opac=opac, config=request.param)
 
 
-@pytest.mark.parametrize("scheme", ["shipped", "norange", "range22", "gen", "emit",
-                                    "bucket"])
+@pytest.mark.parametrize("scheme", ["shipped", "norange", "range22", "bucket"])
 def test_headline_binning_bitexact(gpu, headline, scheme):
     """Binning bit-exact at full size: the shipped dispatch (for these scenes the depth sort of
     8-bit reduce-then-scan passes compacting the culled Gaussians away, constant-digit passes
-    copying from 2^22 keys; then two LSD tile passes, the first generated from the depth-ordered
-    allotments at I >= 2^24 (c5) and over emitted pairs below, the last writing the tile table);
-    and every other setting a shipped dispatch takes elsewhere: the key-range shortcut off or
-    always on, the first tile pass always generated or always over emitted pairs, and the tile
-    buckets with per-tile LDS sorts (shipped for small scenes)."""
+    skipped, then the region binning placing each depth-ordered intersection into its tile
+    list); and every other setting a shipped dispatch takes elsewhere: the key-range shortcut
+    off or from 2^22 keys only, and the tile buckets with per-tile LDS sorts (shipped for small
+    scenes)."""
     h, cam = headline, headline["cam"]
     assert h["ref"]["num_intersects"] > 1 << 20
     if scheme != "shipped" and h["config"] in ("c4", "c5"):
@@ -68,16 +66,13 @@ def test_headline_binning_bitexact(gpu, headline, scheme):
     L = _lib.lib()
     # (-1: leave the shipped setting; each call returns the previous one)
     prev = (L.gsplat_debug_binning_scheme(1 if scheme == "bucket" else -1),
-            L.gsplat_debug_emit_pass0({"emit": 0, "gen": 2}.get(scheme, -1)),
-            L.gsplat_debug_depth_key_range({"norange": 0, "range": 2, "range22": 1}
-                                           .get(scheme, -1)))
+            L.gsplat_debug_depth_key_range({"norange": 0, "range22": 1}.get(scheme, -1)))
     try:
         I, gids, bins = bin_gaussians(h["xys"], h["depths"], h["radii"], h["nth"], cam.height,
                                       cam.width)
     finally:
         L.gsplat_debug_binning_scheme(prev[0])
-        L.gsplat_debug_emit_pass0(prev[1])
-        L.gsplat_debug_depth_key_range(prev[2])
+        L.gsplat_debug_depth_key_range(prev[1])
     assert I == h["ref"]["num_intersects"]
     np.testing.assert_array_equal(_np(gids), h["ref"]["gaussian_ids_sorted"])
     np.testing.assert_array_equal(_np(bins), h["ref"]["tile_bins"])

@@ -151,28 +151,26 @@ def test_sh_unaligned_slab(gpu):
                                rtol=RTOL, atol=ATOL)
 
 
-# binning dispatch settings: (gsplat_debug_binning_scheme, gsplat_debug_emit_pass0)
-BIN_SETTINGS = {"shipped": (-1, 1), "gen": (0, 2), "emit": (0, 0), "bucket": (1, 1)}
+# binning dispatch settings (gsplat_debug_binning_scheme): as shipped (by size), the depth sort +
+# region binning, the small-scene tile buckets
+BIN_SETTINGS = {"shipped": -1, "region": 0, "bucket": 1}
 
 
 @pytest.mark.parametrize("scheme", list(BIN_SETTINGS))
 @pytest.mark.parametrize("case", CASES)
 def test_binning_fused_bitexact(gpu, case, scheme):
-    """The binning as dispatched for each case, the depth sort + tile sort with the first LSD
-    tile pass generated from the depth-ordered allotments or run over emitted (tile, id) pairs,
-    and the tile buckets with per-tile LDS sorts: bit-exact against the oracle's stable sort of
-    gsplat's keys."""
+    """The binning as dispatched for each case, the depth sort + region binning (each
+    depth-ordered intersection placed into its tile list) and the tile buckets with per-tile LDS
+    sorts: bit-exact against the oracle's stable sort of gsplat's keys."""
     sc, cam, scales, quats = _inputs(*case)
     g, o = _project_both(gpu, sc, cam, scales, quats)
     xys, depths, radii, conics, nth, cov3d = g
     L = _lib.lib()
-    b, e = BIN_SETTINGS[scheme]
-    prev, prev_e = L.gsplat_debug_binning_scheme(b), L.gsplat_debug_emit_pass0(e)
+    prev = L.gsplat_debug_binning_scheme(BIN_SETTINGS[scheme])
     try:
         I, gids, bins = bin_gaussians(xys, depths, radii, nth, cam.height, cam.width)
     finally:
         L.gsplat_debug_binning_scheme(prev)
-        L.gsplat_debug_emit_pass0(prev_e)
     ref = O.bin_and_sort(o[0], o[1], o[2], o[4], cam.tile_bounds)
     assert I == ref["num_intersects"]
     np.testing.assert_array_equal(_np(gids), ref["gaussian_ids_sorted"])
@@ -181,9 +179,9 @@ def test_binning_fused_bitexact(gpu, case, scheme):
 
 def test_binning_inconsistent_allotments(gpu):
     """Caller-supplied num_tiles_hit that disagree with the tile boxes (allotments larger than
-    the box are padded with the sentinel tile, smaller ones truncate the box): the generated
-    first LSD tile pass and the tile buckets place exactly what emission + LSD does, including
-    Gaussians whose allotment spans several rounds (one Gaussian over 600 tiles)."""
+    the box are padded with the sentinel tile, smaller ones truncate the box): the region
+    binning (its sentinel region) and the tile buckets place the same ids, including Gaussians
+    whose allotment spans several expansion rounds (one Gaussian over 600 tiles)."""
     sc, cam, scales, quats = _inputs(20000, 512, 512, 2, 0.003, 0.03, 1.5)
     g, _ = _project_both(gpu, sc, cam, scales, quats)
     xys, depths, radii, conics, nth, cov3d = [t.detach() for t in g]
@@ -194,15 +192,15 @@ def test_binning_inconsistent_allotments(gpu):
     nth[vis[5]] = 600
     out = []
     L = _lib.lib()
-    for scheme in ("emit", "gen", "bucket"):
-        b, e = BIN_SETTINGS[scheme]
-        prev, prev_e = L.gsplat_debug_binning_scheme(b), L.gsplat_debug_emit_pass0(e)
+    for scheme in ("region", "bucket"):
+        prev = L.gsplat_debug_binning_scheme(BIN_SETTINGS[scheme])
         try:
             I, gids, bins = bin_gaussians(xys, depths, radii, nth, cam.height, cam.width)
         finally:
             L.gsplat_debug_binning_scheme(prev)
-            L.gsplat_debug_emit_pass0(prev_e)
         out.append((I, _np(gids), _np(bins)))
+    # (gsplat leaves such slots unwritten, so no oracle output exists for them: the two
+    # independent implementations of the padding semantics must agree)
     for o in out[1:]:
         assert o[0] == out[0][0] == int(nth[radii > 0].sum())
         np.testing.assert_array_equal(o[1], out[0][1])
@@ -224,8 +222,7 @@ def test_binning_prelaunched_emission(gpu, scheme):
     n_ref = ref["num_intersects"]
     key = (xys.device, xys.shape[0], cam.tile_bounds[0], cam.tile_bounds[1])
     L = _lib.lib()
-    b, e = BIN_SETTINGS[scheme]
-    prev, prev_e = L.gsplat_debug_binning_scheme(b), L.gsplat_debug_emit_pass0(e)
+    prev = L.gsplat_debug_binning_scheme(BIN_SETTINGS[scheme])
     try:
         for cap in (None, n_ref, n_ref + 1000, n_ref - 1, n_ref):
             if cap is None:
@@ -238,7 +235,6 @@ def test_binning_prelaunched_emission(gpu, scheme):
             np.testing.assert_array_equal(_np(bins), ref["tile_bins"])
     finally:
         L.gsplat_debug_binning_scheme(prev)
-        L.gsplat_debug_emit_pass0(prev_e)
         R._EMIT_CAP.pop(key, None)
 
 

@@ -126,19 +126,3 @@ def test_fused_render_speculative_bit_identical(gpu, W, H, n, mode):
     names = ("rgb", "alpha", "means", "scales", "quats", "opacities", "dc", "rest")
     for name, x, y in zip(names, got, ref):
         np.testing.assert_array_equal(x, y, err_msg=name)
-
-
-def test_depth_payload_option_bit_identical(gpu):
-    """gsplat_debug_depth_payload (the depth sort carrying the tile boxes; off by default):
-    ids and tile table bit-identical to the records' gather (the default)."""
-    sc = synthetic_scene(200_000, 3, seed=11, scale_lo=0.004, scale_hi=0.03)
-    xys, depths, radii, nth, ws1, cam = _keyed(gpu, sc, synthetic_camera(640, 480))
-    ref = R.bin_gaussians(xys, depths, radii, nth, 480, 640, keyed_workspace=_fresh_ws(ws1))
-    prev = _lib.query("gsplat_debug_depth_payload", 1)
-    try:
-        got = R.bin_gaussians(xys, depths, radii, nth, 480, 640, keyed_workspace=_fresh_ws(ws1))
-    finally:
-        _lib.query("gsplat_debug_depth_payload", prev)
-    assert got[0] == ref[0] > 0
-    np.testing.assert_array_equal(got[1].cpu().numpy(), ref[1].cpu().numpy())
-    np.testing.assert_array_equal(got[2].cpu().numpy(), ref[2].cpu().numpy())
