@@ -69,8 +69,6 @@ SIGNATURES = {
     "gsplat_rasterize_backward_chunked": (_I, [_I, _I, _I, _I, _I] + [_P] * 11 + [_F] +
                                           [_P] * 4 + [_I64, _I, _P, _SZ, _P, _SZ, _P]),
     "gsplat_debug_set_chunk": (_I, [_I]),
-    "gsplat_debug_forward_split": (_I, [_I]),
-    "gsplat_debug_forward_chunk_div": (_I, [_I]),
     "gsplat_debug_set_raster_variant": (_I, [_I, _I, _I]),
     "gsplat_debug_raster_variant_is_default": (_I, []),
     "gsplat_debug_depth_key_range": (_I, [_I]),
@@ -163,11 +161,6 @@ def lib():
             raise RuntimeError(L.gsplat_last_error().decode(errors="replace"))
         if os.environ.get("GSPLAT_MI355X_CHUNK"):
             L.gsplat_debug_set_chunk(int(os.environ["GSPLAT_MI355X_CHUNK"]))
-        if os.environ.get("GSPLAT_MI355X_FWD_CHUNK_DIV") and \
-                hasattr(L, "gsplat_debug_forward_chunk_div"):
-            L.gsplat_debug_forward_chunk_div(int(os.environ["GSPLAT_MI355X_FWD_CHUNK_DIV"]))
-        if os.environ.get("GSPLAT_MI355X_FWD_SPLIT") and hasattr(L, "gsplat_debug_forward_split"):
-            L.gsplat_debug_forward_split(int(os.environ["GSPLAT_MI355X_FWD_SPLIT"]))
         if os.environ.get("GSPLAT_MI355X_DEPTH_KEY_RANGE"):  # 0 off, 1 from 2^22 keys, 2 always
             L.gsplat_debug_depth_key_range(int(os.environ["GSPLAT_MI355X_DEPTH_KEY_RANGE"]))
         _lib = L

@@ -388,42 +388,6 @@ __device__ __forceinline__ bool stage_raw(const RawG &q, bool live, int idx, int
   }
   return keep;
 }
-// The forward's staging layout (one pixel per lane, no depth): two consecutive staged
-// Gaussians interleaved field by field, so an iteration reads both with five 16-B LDS reads and
-// evaluates their sigma / exp argument / alpha / 1 - alpha as packed pairs (v_pk_fma_f32 and
-// friends: the same IEEE operations as the scalar ones, so bit-identical) -- 54 -> ~38 VALU per
-// iteration of the VALU-issue-bound forward.  The colour of Gaussian u sits at rg[u] / bl[u] so
-// the red-green accumulation is one packed fma per Gaussian.
-// The packed-pair forward (FPair) is off: measured slower than the scalar two-Gaussian loop
-// despite 54 -> 39 VALU per iteration (round 4, same-box A/B: headline forward 0.1461 ->
-// 0.1486-0.1506 ms, c3 0.0975 -> 0.1018-0.1021 ms) -- the five 16-B LDS reads of an iteration
-// and the longer dependent chain of the packed operations cost more than the issue slots saved.
-#ifndef GS_FWD_PACKED
-#define GS_FWD_PACKED 0
-#endif
-struct __attribute__((aligned(16))) FPair {
-  f2 x, y, ha, b;
-  f2 hc, o, rg0, rg1;
-  f2 bl;
-  int idx[2];
-};
-static_assert(sizeof(FPair) == 80, "FPair layout");
-// the staged Gaussian s at rank q of the wave's batch
-__device__ __forceinline__ void fpair_put(FPair *pairs, int q, const GStage &s) {
-  FPair &P = pairs[q >> 1];
-  const int h = q & 1;
-  P.x[h] = s.x;
-  P.y[h] = s.y;
-  P.ha[h] = s.ha;
-  P.b[h] = s.b;
-  P.hc[h] = s.hc;
-  P.o[h] = s.o;
-  if (h) P.rg1 = f2{s.r, s.g};
-  else P.rg0 = f2{s.r, s.g};
-  P.bl[h] = s.bl;
-  P.idx[h] = s.idx;
-}
-
 // The pipeline state: ids of batch k+1 (loaded) and k+2 (in flight), data of batch k+1 (in
 // flight).
 struct StagePipe {
@@ -600,46 +564,6 @@ __device__ __forceinline__ void walk_kept(const KeepSrc &S, int top, int bottom,
                 });
 }
 
-// The 8x8 backward's staging layout: two consecutive records interleaved field by field
-// (as FPair for the forward), so both Gaussians' sigma, exp argument, alpha, colour dot
-// product and moments are packed pairs.  A slot past the round's count holds a null record
-// (zero opacity and colour, finite geometry): alpha 0, never valid, finite terms.
-// The packed-pair 8x8 backward (BPair) is off: 132 -> 117 VALU per iteration but 62 -> 72 VGPRs
-// (occupancy 8 -> 7), measured slower (round 4, same-box A/B: c3 record backward 0.1083 ->
-// 0.1106 ms).
-#ifndef GS_BWD8_PACKED
-#define GS_BWD8_PACKED 0
-#endif
-struct __attribute__((aligned(16))) BPair {
-  f2 x, y, ha, b;
-  f2 hc, o, r, g;
-  f2 bl;
-  int idx[2], id[2];
-  int pad[2];
-};
-static_assert(sizeof(BPair) == 96, "BPair layout");
-__device__ __forceinline__ void bpair_put(BPair *pairs, int q, const GStage *s) {
-  BPair &P = pairs[q >> 1];
-  const int h = q & 1;
-  if (s) {
-    P.x[h] = s->x;
-    P.y[h] = s->y;
-    P.ha[h] = s->ha;
-    P.b[h] = s->b;
-    P.hc[h] = s->hc;
-    P.o[h] = s->o;
-    P.r[h] = s->r;
-    P.g[h] = s->g;
-    P.bl[h] = s->bl;
-    P.idx[h] = s->idx;
-    P.id[h] = s->id;
-  } else {
-    P.x[h] = P.y[h] = P.ha[h] = P.b[h] = P.hc[h] = 0.f;
-    P.o[h] = P.r[h] = P.g[h] = P.bl[h] = 0.f;
-    P.idx[h] = 0x7FFFFFFF;
-    P.id[h] = 0;
-  }
-}
 // stage_gaussian<true> without the cull (the forward's keep bits already decided it)
 __device__ __forceinline__ void stage_kept(int idx, int g, const float2 *__restrict__ xys,
                                            const float *__restrict__ conics,
@@ -870,10 +794,6 @@ __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
   const float px = (float)j;
   const float rx0 = R.rx0, rx1 = R.rx1, ry0 = R.ry0, ry1 = R.ry1;
   constexpr int LROWS = 64 / COLS;
-  // one pixel per lane, no depth: the packed-pair blend (FPair)
-  constexpr bool PACKED = GS_FWD_PACKED && PXL == 1 && !DEPTH;
-  static_assert(sizeof(FPair) * 32 <= sizeof(GStage) * 64, "FPair slice fits the wave's slice");
-  f2 crg = {0.f, 0.f};  // (PACKED: red, green)
   float py[PXL], T[PXL], cr[PXL], cg[PXL], cb[PXL], cd[PXL];
   int cur[PXL];
   bool done[PXL];
@@ -888,7 +808,6 @@ __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
   }
   const int2 range = bins[tile];
   GStage *stage = lds[__builtin_amdgcn_readfirstlane(wave)];  // (uniform: SGPR address arithmetic)
-  FPair *pairs = reinterpret_cast<FPair *>(stage);
   unsigned c_slots = 0, c_live = 0, c_valid = 0;  // (CNT only)
   StagePipe pipe{};  // (PF: see RawG)
   if (PF && range.x < range.y) {
@@ -926,70 +845,10 @@ __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
     if (DEPTH && keep) s.d = depths[s.id];
     const unsigned long long kmask = __ballot(keep);
     const int n = __popcll(kmask);
-    if constexpr (PACKED) {
-      if (keep) fpair_put(pairs, lanes_below(kmask), s);
-      // an odd batch leaves slot n unwritten: a zero colour there keeps 0 * colour finite
-      if ((n & 1) && lane == 0) {
-        pairs[n >> 1].rg1 = f2{0.f, 0.f};
-        pairs[n >> 1].bl[1] = 0.f;
-      }
-    } else {
-      if (keep) stage[lanes_below(kmask)] = s;
-    }
+    if (keep) stage[lanes_below(kmask)] = s;
     kb_at = kb_base + ((b - range.x) >> 6);  // (stored with the next batch's loads, see above)
     kb_word = kmask;
     wave_lds_sync();
-    if constexpr (PACKED) {
-      // two staged Gaussians per iteration, their per-pixel terms as packed pairs; the
-      // transmittance / colour updates in list order exactly as the scalar loop below
-      const float px1 = px, py1 = py[0];
-      for (int t = 0; t < n; t += 2) {
-        const FPair P = pairs[t >> 1];
-        const bool live1 = t + 1 < n;
-        if constexpr (CNT) c_slots += 2 * 64;
-        const f2 dx = P.x - px1;
-        const f2 hA = P.ha * dx * dx, bdx = P.b * dx;
-        const f2 dy = P.y - py1;
-        const f2 sg = vfma(vfma(P.hc, dy, bdx), dy, hA);
-        const f2 e = sg * NEG_LOG2E;
-        const f2 ov = P.o * f2{__builtin_amdgcn_exp2f(e.x), __builtin_amdgcn_exp2f(e.y)};
-        const f2 al = f2{fminf(0.999f, ov.x), fminf(0.999f, ov.y)};
-        const f2 om = 1.f - al;
-        {
-          const bool v = !done[0] && sg.x >= 0.f && al.x >= ALPHA_MIN;
-          if constexpr (CNT) {
-            c_live += !done[0] ? 1u : 0u;
-            c_valid += v ? 1u : 0u;
-          }
-          const float nT = T[0] * om.x;
-          const bool term = v && nT <= 1e-4f, comp = v && !term;
-          done[0] = done[0] || term;
-          const float w = comp ? al.x * T[0] : 0.f;
-          crg = vfma(P.rg0, f2{w, w}, crg);
-          cb[0] += P.bl.x * w;
-          T[0] = comp ? nT : T[0];
-          cur[0] = comp ? P.idx[0] : cur[0];
-        }
-        {
-          const bool v = !done[0] && live1 && sg.y >= 0.f && al.y >= ALPHA_MIN;
-          if constexpr (CNT) {
-            c_live += (!done[0] && live1) ? 1u : 0u;
-            c_valid += v ? 1u : 0u;
-          }
-          const float nT = T[0] * om.y;
-          const bool term = v && nT <= 1e-4f, comp = v && !term;
-          done[0] = done[0] || term;
-          const float w = comp ? al.y * T[0] : 0.f;
-          crg = vfma(P.rg1, f2{w, w}, crg);
-          cb[0] += P.bl.y * w;
-          T[0] = comp ? nT : T[0];
-          cur[0] = comp ? P.idx[1] : cur[0];
-        }
-        if (__all(done[0])) break;
-      }
-      wave_lds_sync();
-      continue;
-    }
     for (int t = 0; t < n; t += 2) {
       GStage G[2];
       G[0] = stage_at(stage, t);
@@ -1037,10 +896,6 @@ __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
     wave_lds_sync();
   }
   if (kbits && kb_at >= 0 && lane == 0) kbits[kb_at] = kb_word;
-  if constexpr (PACKED) {
-    cr[0] = crg.x;
-    cg[0] = crg.y;
-  }
   const float bg0 = background[0], bg1 = background[1], bg2 = background[2];
 #pragma unroll
   for (int k = 0; k < PXL; ++k) {
@@ -1081,433 +936,6 @@ __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
   if constexpr (CNT) pair_count_flush(3, c_slots, c_live, c_valid);
   wlog.done(tile);
   clear_side_job();
-}
-
-// ---------------------------------------------------------------- list-split forward (C = 3)
-// Small frames (below FWD_SPLIT_MAX_TILES tiles: c2 / c3 at 512^2 have 1,024) put every wave of
-// the forward on the chip at once, so the launch lasts as long as its longest list.  The split
-// forward cuts each tile's list into parts of `chunk` positions (the list-split plan's chunk):
-//  * fwd_plan_kernel: the parts, ordered by part index (earlier parts dispatched first), each
-//    tile's first part record index fbase[t], and the termination masks cleared;
-//  * raster_fwd_part_kernel: each part blended by its own 4 waves (one 8x8 block each) from
-//    T = 1 -- colour C_p, transmittance T_p, last composited position, and "terminated here"
-//    when the local T reaches 1e-4 (the true T, which starts at or below 1, is then at or below
-//    it too: fp32 multiplication is monotone, so the true chain has ended by that position).
-//    A tile of one part is the plain forward, bit for bit, and writes the outputs itself;
-//  * raster_fwd_combine_kernel: per pixel, the parts in list order: C += T C_p, T *= T_p while
-//    the running T stays clearly above the termination threshold; a part where it may reach it
-//    is re-walked from the running T to find the exact stop.  Part 0 starts from the true T = 1,
-//    so its record is exact.  The running T of later parts differs from the sequential product
-//    by rounding only, at most gamma(2K + j + 8) relatively after K factors and j parts (each
-//    product of n fp32 factors is within (1 +- 2^-24)^n of the exact one); a termination test
-//    that close to the threshold sends the pixel to an exact sequential walk of its list.  So
-//    final_idx -- the integer state the backward walks from -- is exactly the unsplit forward's,
-//    and the image / final T differ from it by fp32 rounding of the product's grouping only.
-// Later parts skip their remaining batches once earlier parts have terminated every pixel of
-// their block (ftmask: per part and block, the ballot of locally terminated pixels).
-constexpr long long FWD_SPLIT_MAX_TILES = 3584;
-// gsplat_debug_forward_split: 0 off (the default), 1 on, 2 on with exact walks only.  Measured
-// slower on c3 (bear, 1,024 tiles; round 4 same-box A/B, 2 reps: forward 0.099 -> 0.28-0.29 ms,
-// step 0.387 -> 0.57-0.59 ms; parts of 1/2 and 1/4 the chunk alike): the first parts alone took
-// as long as the whole unsplit forward (its longest waves are dense tiles saturating within
-// their first chunk, not long unsaturated lists), the later parts 81 us and the combine 95 us
-// of re-walks (profiles/r04_ab_split_forward_c3.txt).
-int g_fwd_split = 0;
-constexpr int FPR = 6;  // part record words per pixel: C (3), T, last | lterm << 31, factors
-
-__global__ __launch_bounds__(1024) void fwd_plan_kernel(int T, int chunk,
-                                                        const int2 *__restrict__ bins,
-                                                        int2 *__restrict__ items,
-                                                        int *__restrict__ n_items,
-                                                        int *__restrict__ fbase,
-                                                        unsigned long long *__restrict__ ftmask) {
-  __shared__ int hist[64], cur[64], lds[16];
-  const int tid = threadIdx.x;
-  if (tid < 64) hist[tid] = 0;
-  __syncthreads();
-  // tiles [t0, t1) of this thread (consecutive, for the prefix of part counts)
-  const int per = (T + 1023) / 1024, t0 = min(T, tid * per), t1 = min(T, t0 + per);
-  int local = 0;
-  for (int t = t0; t < t1; ++t) {
-    const int L = max(0, bins[t].y - bins[t].x);
-    const int m = max(1, (L + chunk - 1) / chunk);
-    local += m;
-    for (int j = 0; j < m; ++j) atomicAdd(&hist[min(j, 63)], 1);
-  }
-  // exclusive scan of the per-thread part counts -> fbase
-  int x = local;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const int y = __shfl_up(x, d, 64);
-    if ((tid & 63) >= d) x += y;
-  }
-  if ((tid & 63) == 63) lds[tid >> 6] = x;
-  __syncthreads();
-  if (tid < 64) {
-    int w = tid < 16 ? lds[tid] : 0;
-#pragma unroll
-    for (int d = 1; d < 16; d <<= 1) {
-      const int y = __shfl_up(w, d, 64);
-      if (tid >= d) w += y;
-    }
-    if (tid < 16) lds[tid] = w;  // inclusive wave totals
-    const int h = hist[tid];
-    int c = h;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const int y = __shfl_up(c, d, 64);
-      if (tid >= d) c += y;
-    }
-    cur[tid] = c - h;
-    if (tid == 63) *n_items = c;
-  }
-  __syncthreads();
-  int run = x - local + ((tid >> 6) ? lds[(tid >> 6) - 1] : 0);
-  for (int t = t0; t < t1; ++t) {
-    fbase[t] = run;
-    const int L = max(0, bins[t].y - bins[t].x);
-    const int m = max(1, (L + chunk - 1) / chunk);
-    for (int j = 0; j < m; ++j) items[atomicAdd(&cur[min(j, 63)], 1)] = make_int2(t, j);
-    run += m;
-  }
-  if (tid == 1023) fbase[T] = run;
-  __syncthreads();
-  const int total = lds[15];
-  for (int k = tid; k < SPLIT_WAVES * total; k += 1024) ftmask[k] = 0ull;
-}
-
-// One staged batch of the forward's walk (64 list positions from b, within [b, end)): the
-// 8x8-block cull (touches_rect, as raster_fwd3u_kernel) and the kept records into the wave's
-// LDS stage; returns the kept count and the batch's keep ballot.
-__device__ __forceinline__ int fwd_stage_batch(int b, int end, const int *__restrict__ gids,
-                                               const float2 *__restrict__ xys,
-                                               const float *__restrict__ conics,
-                                               const float *__restrict__ colors,
-                                               const float *__restrict__ opacity,
-                                               const WaveRect &R, GStage *stage,
-                                               unsigned long long &kmask) {
-  const int idx = b + __lane_id();
-  GStage s;
-  const bool keep = idx < end && stage_gaussian(idx, gids, xys, conics, colors, opacity, R.rx0,
-                                                R.rx1, R.ry0, R.ry1, s);
-  kmask = __ballot(keep);
-  if (keep) stage[lanes_below(kmask)] = s;
-  wave_lds_sync();
-  return __popcll(kmask);
-}
-
-template <bool CNT = false>
-__global__ __launch_bounds__(256) void raster_fwd_part_kernel(
-    int tbx, int tby, int H, int W, const int *__restrict__ gids, const int2 *__restrict__ bins,
-    const float2 *__restrict__ xys, const float *__restrict__ conics,
-    const float *__restrict__ colors, const float *__restrict__ opacity,
-    const float *__restrict__ background, float *__restrict__ out_img,
-    float *__restrict__ final_Ts, int *__restrict__ final_idx, float4 *__restrict__ zero,
-    long long zero_n, const int *__restrict__ zero_radii, int *__restrict__ tile_last,
-    unsigned long long *__restrict__ kbits, long long kbw, const float *__restrict__ l1_gt,
-    float *__restrict__ l1_part, int l1_clamp, int chunk, const int2 *__restrict__ items,
-    const int *__restrict__ n_items, const int *__restrict__ fbase, float *__restrict__ fprec,
-    unsigned long long *__restrict__ ftmask, int slot0 = 0, int slot_end = 0x7FFFFFFF) {
-  auto clear_side_job = [&]() {  // (as raster_fwd3u_kernel)
-    for (long long k = (long long)blockIdx.x * 256 + threadIdx.x; k < zero_n;
-         k += (long long)gridDim.x * 256)
-      if (!zero_radii || zero_radii[k >> 2] > 0) zero[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-  };
-  // two launches (see forward_clearing_impl): the first parts of all tiles (slots [0, T): the
-  // plan puts every tile's part 0 first), then the later parts, which then know exactly which
-  // pixels the first parts stopped
-  const int slot = block_slot() + slot0;
-  if (slot >= min(*n_items, slot_end)) {  // workgroup-uniform: past the last item
-    clear_side_job();
-    return;
-  }
-  const int2 it = items[slot];
-  const int tile = it.x, part = it.y;
-  const WaveRect R = wave_rect<1, 8>(tbx, tby, H, W, tile);
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, wt = wave;
-  const int2 range = bins[tile];
-  const int L = max(0, range.y - range.x);
-  const int m = max(1, (L + chunk - 1) / chunk);
-  if (!R.live) {
-    if (m == 1 && lane == 0) {
-      if (tile_last) tile_last[SPLIT_WAVES * tile + wt] = -1;
-      if (l1_part) l1_part[SPLIT_WAVES * tile + wt] = 0.f;
-    }
-    clear_side_job();
-    return;
-  }
-  __shared__ GStage lds[4][64];
-  GStage *stage = lds[__builtin_amdgcn_readfirstlane(wave)];
-  const int j = R.j, i = R.i0;
-  const float px = (float)j, py = (float)i;
-  const bool inimg = i < H && j < W;
-  const int lo = range.x + part * chunk, hi = min(lo + chunk, range.y);
-  float T = 1.f, cr = 0.f, cg = 0.f, cb = 0.f, nfac = 0.f;
-  int cur = -1;
-  bool done = !inimg, lterm = false;
-  const unsigned long long live = __ballot(inimg);
-  const int p = fbase[tile] + part;
-  const long long kb_base = wt * kbw + (long long)(range.x >> 6) + tile;
-  if (part > 0) {  // pixels an earlier part stopped take no part here
-    unsigned long long t = 0;
-    for (int k = lane; k < part; k += 64)
-      t |= __hip_atomic_load(&ftmask[(size_t)(fbase[tile] + k) * SPLIT_WAVES + wt],
-                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) t |= __shfl_xor(t, o, 64);
-    done = done || ((t >> lane) & 1ull);
-  }
-  for (int b = lo; b < hi; b += 64) {
-    if (__all(done)) break;
-    if (part > 0) {  // every live pixel terminated by an earlier part: nothing left to do here
-      unsigned long long t = 0;
-      for (int k = lane; k < part; k += 64)
-        t |= __hip_atomic_load(&ftmask[(size_t)(fbase[tile] + k) * SPLIT_WAVES + wt],
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) t |= __shfl_xor(t, o, 64);
-      if ((t & live) == live) break;
-    }
-    unsigned long long kmask;
-    const int n = fwd_stage_batch(b, hi, gids, xys, conics, colors, opacity, R, stage, kmask);
-    if (kbits && lane == 0) kbits[kb_base + ((b - range.x) >> 6)] = kmask;
-    // two staged Gaussians per iteration, as raster_fwd3u_kernel: both sigma / exp / alpha
-    // chains independent, the transmittance update in list order
-    for (int t = 0; t < n; t += 2) {
-      GStage G[2];
-      G[0] = stage_at(stage, t);
-      G[1] = stage_at(stage, min(t + 1, 63));
-      const bool live1 = t + 1 < n;
-      if (!live1) G[1].r = G[1].g = G[1].bl = 0.f;  // stale slot: keep 0 * x finite
-      float sg[2], al[2];
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const float dx = G[u].x - px;
-        sg[u] = gs_sigma(G[u].hc, G[u].b * dx, G[u].ha * dx * dx, G[u].y - py);
-        al[u] = fminf(0.999f, G[u].o * gs_vis(sg[u]));
-      }
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const bool v = !done && (u == 0 || live1) && sg[u] >= 0.f && al[u] >= ALPHA_MIN;
-        const float nT = T * (1.f - al[u]);
-        const bool term = v && nT <= 1e-4f, comp = v && !term;
-        done = done || term;
-        lterm = lterm || term;
-        const float w = comp ? al[u] * T : 0.f;
-        cr += G[u].r * w;
-        cg += G[u].g * w;
-        cb += G[u].bl * w;
-        T = comp ? nT : T;
-        cur = comp ? G[u].idx : cur;
-        nfac += comp ? 1.f : 0.f;
-      }
-      if (__all(done)) break;
-    }
-    wave_lds_sync();
-  }
-  if (m == 1) {  // the whole list: the plain forward's outputs (the same per-pixel operations)
-    const int ci = cur < 0 ? 0 : cur;
-    const float bg0 = background[0], bg1 = background[1], bg2 = background[2];
-    float acc = 0.f;
-    if (inimg) {
-      const int pix = i * W + j;
-      final_Ts[pix] = T;
-      final_idx[pix] = ci;
-      out_img[3 * pix] = cr + T * bg0;
-      out_img[3 * pix + 1] = cg + T * bg1;
-      out_img[3 * pix + 2] = cb + T * bg2;
-      if (l1_part)
-        acc = fabsf(l1_gt[3 * pix] - l1_clampv(cr + T * bg0, l1_clamp)) +
-              fabsf(l1_gt[3 * pix + 1] - l1_clampv(cg + T * bg1, l1_clamp)) +
-              fabsf(l1_gt[3 * pix + 2] - l1_clampv(cb + T * bg2, l1_clamp));
-    }
-    if (l1_part) {
-      acc = wave_sum(acc);
-      if (lane == 0) l1_part[SPLIT_WAVES * tile + wt] = acc;
-    }
-    if (tile_last) {
-      const int mx = wave_max_int(inimg ? ci : -1);
-      if (lane == 0) tile_last[SPLIT_WAVES * tile + wt] = mx;
-    }
-  } else {
-    float *r = fprec + ((size_t)p * SPLIT_WAVES + wt) * FPR * 64 + lane;
-    r[0] = cr;
-    r[64] = cg;
-    r[128] = cb;
-    r[192] = T;
-    reinterpret_cast<int *>(r)[256] = (int)((uint32_t)cur & 0x7FFFFFFFu) | (lterm ? (int)0x80000000u : 0);
-    r[320] = nfac;
-    const unsigned long long tm = __ballot(lterm);
-    if (tm && lane == 0)
-      __hip_atomic_fetch_or(&ftmask[(size_t)p * SPLIT_WAVES + wt], tm, __ATOMIC_RELAXED,
-                            __HIP_MEMORY_SCOPE_AGENT);
-  }
-  clear_side_job();
-}
-
-// The parts of a split tile in list order (see the section head).  One workgroup per tile, one
-// wave per 8x8 block; tiles of one part return at once (their outputs are written).
-__global__ __launch_bounds__(256) void raster_fwd_combine_kernel(
-    int tbx, int tby, int H, int W, const int *__restrict__ gids, const int2 *__restrict__ bins,
-    const float2 *__restrict__ xys, const float *__restrict__ conics,
-    const float *__restrict__ colors, const float *__restrict__ opacity,
-    const float *__restrict__ background, float *__restrict__ out_img,
-    float *__restrict__ final_Ts, int *__restrict__ final_idx, int *__restrict__ tile_last,
-    const float *__restrict__ l1_gt, float *__restrict__ l1_part, int l1_clamp, int chunk,
-    const int *__restrict__ fbase, const float *__restrict__ fprec, float U) {
-  const int tile = blockIdx.x;
-  const int2 range = bins[tile];
-  const int L = max(0, range.y - range.x);
-  const int m = max(1, (L + chunk - 1) / chunk);
-  if (m == 1) return;  // workgroup-uniform
-  const WaveRect R = wave_rect<1, 8>(tbx, tby, H, W, tile);
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, wt = wave;
-  if (!R.live) {
-    if (lane == 0) {
-      if (tile_last) tile_last[SPLIT_WAVES * tile + wt] = -1;
-      if (l1_part) l1_part[SPLIT_WAVES * tile + wt] = 0.f;
-    }
-    return;
-  }
-  __shared__ GStage lds[4][64];
-  GStage *stage = lds[__builtin_amdgcn_readfirstlane(wave)];
-  const int j = R.j, i = R.i0;
-  const float px = (float)j, py = (float)i;
-  const bool inimg = i < H && j < W;
-  // U: the unit roundoff with a margin (0x1p-24 * 1.01); a huge U (gsplat_debug_forward_split
-  // mode 2) sends every pixel of a split tile to the exact walk -- the test of that path
-  float T = 1.f, cr = 0.f, cg = 0.f, cb = 0.f, K = 0.f;
-  int cur = 0;
-  bool done = !inimg, amb = false;
-  const int p0 = fbase[tile];
-  for (int q = 0; q < m; ++q) {
-    if (__all(done)) break;
-    const float *r = fprec + ((size_t)(p0 + q) * SPLIT_WAVES + wt) * FPR * 64 + lane;
-    const float pr = r[0], pg = r[64], pb = r[128], pT = r[192], pk = r[320];
-    const int lw = reinterpret_cast<const int *>(r)[256];
-    const bool plt = lw < 0;
-    const int plast = (int)((uint32_t)lw & 0x7FFFFFFFu) == 0x7FFFFFFF ? -1 : lw & 0x7FFFFFFF;
-    if (q == 0) {  // from the true T = 1: the part's own chain is the exact one
-      if (!done) {
-        cr = pr;
-        cg = pg;
-        cb = pb;
-        T = pT;
-        K = pk;
-        cur = plast >= 0 ? plast : 0;
-        done = plt;
-      }
-      continue;
-    }
-    const float d = (2.f * (K + pk) + (float)q + 8.f) * U;
-    const float Tend = T * pT;
-    const bool skip = !done && !plt && Tend > 1e-4f * (1.f + d);
-    if (skip) {
-      cr += T * pr;
-      cg += T * pg;
-      cb += T * pb;
-      T = Tend;
-      K += pk;
-      if (plast >= 0) cur = plast;
-    }
-    const bool need = !done && !skip;
-    if (!__any(need)) continue;
-    // re-walk part q from the running T for the pixels that may stop in it
-    bool act = need;
-    const int lo = range.x + q * chunk, hi = min(lo + chunk, range.y);
-    for (int b = lo; b < hi; b += 64) {
-      if (!__any(act)) break;
-      unsigned long long km;
-      const int n = fwd_stage_batch(b, hi, gids, xys, conics, colors, opacity, R, stage, km);
-      for (int t = 0; t < n; ++t) {
-        const GStage G = stage_at(stage, t);
-        const float dx = G.x - px;
-        const float sg = gs_sigma(G.hc, G.b * dx, G.ha * dx * dx, G.y - py);
-        const float al = fminf(0.999f, G.o * gs_vis(sg));
-        const bool v = act && sg >= 0.f && al >= ALPHA_MIN;
-        if (v) {
-          const float nT = T * (1.f - al);
-          const float dd = (2.f * K + (float)q + 10.f) * U;
-          if (nT <= 1e-4f * (1.f - dd)) {  // stops here for certain
-            act = false;
-            done = true;
-          } else if (nT > 1e-4f * (1.f + dd)) {  // composited for certain
-            const float w = al * T;
-            cr += G.r * w;
-            cg += G.g * w;
-            cb += G.bl * w;
-            T = nT;
-            cur = G.idx;
-            K += 1.f;
-          } else {  // too close to call from the regrouped product: exact walk below
-            amb = true;
-            act = false;
-            done = true;
-          }
-        }
-        if (!__any(act)) break;
-      }
-      wave_lds_sync();
-    }
-  }
-  if (__any(amb)) {
-    // the plain forward's sequential walk from the list start for the undecided pixels
-    float eT = 1.f, er = 0.f, eg = 0.f, eb = 0.f;
-    int ecur = 0;
-    bool edone = !amb;
-    for (int b = range.x; b < range.y; b += 64) {
-      if (__all(edone)) break;
-      unsigned long long km;
-      const int n = fwd_stage_batch(b, range.y, gids, xys, conics, colors, opacity, R, stage, km);
-      for (int t = 0; t < n; ++t) {
-        const GStage G = stage_at(stage, t);
-        const float dx = G.x - px;
-        const float sg = gs_sigma(G.hc, G.b * dx, G.ha * dx * dx, G.y - py);
-        const float al = fminf(0.999f, G.o * gs_vis(sg));
-        const bool v = !edone && sg >= 0.f && al >= ALPHA_MIN;
-        const float nT = eT * (1.f - al);
-        const bool term = v && nT <= 1e-4f, comp = v && !term;
-        edone = edone || term;
-        const float w = comp ? al * eT : 0.f;
-        er += G.r * w;
-        eg += G.g * w;
-        eb += G.bl * w;
-        eT = comp ? nT : eT;
-        ecur = comp ? G.idx : ecur;
-        if (__all(edone)) break;
-      }
-      wave_lds_sync();
-    }
-    if (amb) {
-      T = eT;
-      cr = er;
-      cg = eg;
-      cb = eb;
-      cur = ecur;
-    }
-  }
-  const float bg0 = background[0], bg1 = background[1], bg2 = background[2];
-  float acc = 0.f;
-  if (inimg) {
-    const int pix = i * W + j;
-    final_Ts[pix] = T;
-    final_idx[pix] = cur;
-    out_img[3 * pix] = cr + T * bg0;
-    out_img[3 * pix + 1] = cg + T * bg1;
-    out_img[3 * pix + 2] = cb + T * bg2;
-    if (l1_part)
-      acc = fabsf(l1_gt[3 * pix] - l1_clampv(cr + T * bg0, l1_clamp)) +
-            fabsf(l1_gt[3 * pix + 1] - l1_clampv(cg + T * bg1, l1_clamp)) +
-            fabsf(l1_gt[3 * pix + 2] - l1_clampv(cb + T * bg2, l1_clamp));
-  }
-  if (l1_part) {
-    acc = wave_sum(acc);
-    if (lane == 0) l1_part[SPLIT_WAVES * tile + wt] = acc;
-  }
-  if (tile_last) {
-    const int mx = wave_max_int(inimg ? cur : -1);
-    if (lane == 0) tile_last[SPLIT_WAVES * tile + wt] = mx;
-  }
 }
 
 // ---------------------------------------------------------------- backward, C = 3
@@ -1853,16 +1281,8 @@ __global__ __launch_bounds__(256) void raster_bwd8_kernel(
   const int field = slot >= 9 ? slot - 9 : slot;
   const float amax = __builtin_canonicalizef(alpha_max);
   GStage *stage = lds[__builtin_amdgcn_readfirstlane(wave)];  // (uniform: SGPR address arithmetic)
-  // the records as interleaved pairs (BPair): the two Gaussians of an iteration packed
-  static_assert(sizeof(BPair) * 32 <= sizeof(GStage) * 64, "BPair slice fits the wave's slice");
-  constexpr bool BP = GS_BWD8_PACKED;
-  BPair *pairs = reinterpret_cast<BPair *>(stage);
   auto put = [&](int q, const GStage *sp) {
-    if constexpr (BP) {
-        bpair_put(pairs, q, sp);
-    } else {
-        if (sp) stage[q] = *sp;
-    }
+    if (sp) stage[q] = *sp;
   };
   __shared__ int2 ahead_lds[4][64];  // (KB: walk_kept's next-round ids)
   int2 *ahead = ahead_lds[__builtin_amdgcn_readfirstlane(wave)];
@@ -1882,49 +1302,17 @@ __global__ __launch_bounds__(256) void raster_bwd8_kernel(
   auto stage1 = [&](int idx, int g, GStage &s) {
     stage_kept(idx, g, xys, conics, colors, opacity, s);
   };
-  // both Gaussians' per-pixel terms of pair t / 2 as packed pairs: sigma, alpha (masked by
-  // validity), the colour dot product gv; dx, dy and vis kept for the moments
-  struct PairTerms {
-    f2 dx, dy, vis, am, gv;
-    bool v0, v1;
-  };
-  auto pair_terms = [&](const BPair &P, bool live1) {
-    PairTerms q;
-    q.dx = P.x - px;
-    q.dy = P.y - py;
-    const f2 sg = vfma(vfma(P.hc, q.dy, P.b * q.dx), q.dy, P.ha * q.dx * q.dx);
-    const f2 e = sg * NEG_LOG2E;
-    q.vis = f2{__builtin_amdgcn_exp2f(e.x), __builtin_amdgcn_exp2f(e.y)};
-    const f2 ov = P.o * q.vis;
-    const f2 al = f2{fminf(amax, ov.x), fminf(amax, ov.y)};
-    q.v0 = P.idx[0] <= bf && sg.x >= 0.f && al.x >= ALPHA_MIN;
-    q.v1 = live1 && P.idx[1] <= bf && sg.y >= 0.f && al.y >= ALPHA_MIN;
-    q.am = f2{q.v0 ? al.x : 0.f, q.v1 ? al.y : 0.f};
-    q.gv = vfma(P.r, f2{vr, vr}, vfma(P.g, f2{vg, vg}, P.bl * f2{vb, vb}));
-    return q;
-  };
   auto pre_blend = [&](int n) {
-    if constexpr (BP) {
-      for (int t = 0; t < n; t += 2) {  // (the main loop's T / Qs operations, nothing else)
-        const PairTerms q = pair_terms(pairs[t >> 1], t + 1 < n);
-        const f2 ra = f2{__builtin_amdgcn_rcpf(1.f - q.am.x), __builtin_amdgcn_rcpf(1.f - q.am.y)};
-        T = T * ra.x;
-        Qs = fmaf(-(q.am.x * T), q.gv.x, Qs);
-        T = T * ra.y;
-        Qs = fmaf(-(q.am.y * T), q.gv.y, Qs);
-      }
-    } else {
-      for (int t = 0; t < n; ++t) {  // (the main loop's T / Qs operations, nothing else)
-        const GStage G = stage_at(stage, t);
-        const float dx = G.x - px, dy = G.y - py;
-        const float sg = gs_sigma(G.hc, G.b * dx, G.ha * dx * dx, dy);
-        const float al = fminf(amax, G.o * gs_vis(sg));
-        const bool v = G.idx <= bf && sg >= 0.f && al >= ALPHA_MIN;
-        const float am = v ? al : 0.f;
-        T = T * __builtin_amdgcn_rcpf(1.f - am);
-        const float fac = am * T;
-        Qs = fmaf(-fac, fmaf(G.r, vr, fmaf(G.g, vg, G.bl * vb)), Qs);
-      }
+    for (int t = 0; t < n; ++t) {  // (the main loop's T / Qs operations, nothing else)
+      const GStage G = stage_at(stage, t);
+      const float dx = G.x - px, dy = G.y - py;
+      const float sg = gs_sigma(G.hc, G.b * dx, G.ha * dx * dx, dy);
+      const float al = fminf(amax, G.o * gs_vis(sg));
+      const bool v = G.idx <= bf && sg >= 0.f && al >= ALPHA_MIN;
+      const float am = v ? al : 0.f;
+      T = T * __builtin_amdgcn_rcpf(1.f - am);
+      const float fac = am * T;
+      Qs = fmaf(-fac, fmaf(G.r, vr, fmaf(G.g, vg, G.bl * vb)), Qs);
     }
   };
   if (SPLIT) {  // the positions behind this part: T and the colour behind only
@@ -1947,102 +1335,56 @@ __global__ __launch_bounds__(256) void raster_bwd8_kernel(
   const int last = min(maxbin, hi - 1);
   unsigned c_slots = 0, c_live = 0, c_valid = 0;  // (CNT only)
   auto main_blend = [&](int n) {
-    if constexpr (BP) {
-      for (int t = 0; t < n; t += 2) {
-        const BPair &P = pairs[t >> 1];
-        const bool live1 = t + 1 < n;
-        int gid0 = P.id[0], gid1 = P.id[1];
-        asm volatile("" : "+v"(gid0), "+v"(gid1));  // read with the records, not at the atomic
-        // the two Gaussians' per-pixel terms (independent), packed
-        const PairTerms q = pair_terms(P, live1);
-        const unsigned long long any0 = __builtin_amdgcn_ballot_w64(q.v0),
-                                 any1 = __builtin_amdgcn_ballot_w64(q.v1);
-        if constexpr (CNT) {
-          c_slots += 2 * 64;
-          c_live += (P.idx[0] <= bf ? 1u : 0u) + (live1 && P.idx[1] <= bf ? 1u : 0u);
-          c_valid += (q.v0 ? 1u : 0u) + (q.v1 ? 1u : 0u);
-        }
-        // list order (back to front): G0 then G1 -- T and the colour behind are sequential
-        const f2 ra = f2{__builtin_amdgcn_rcpf(1.f - q.am.x), __builtin_amdgcn_rcpf(1.f - q.am.y)};
-        T = T * ra.x;
-        const float fac0 = q.am.x * T;
-        const float va0 = fmaf(q.gv.x, T, ra.x * Qs);
-        Qs = fmaf(-fac0, q.gv.x, Qs);
-        T = T * ra.y;
-        const float fac1 = q.am.y * T;
-        const float va1 = fmaf(q.gv.y, T, ra.y * Qs);
-        Qs = fmaf(-fac1, q.gv.y, Qs);
-        if (any0 | any1) {  // (an SGPR test)
-          const f2 w = f2{q.v0 ? q.vis.x : 0.f, q.v1 ? q.vis.y : 0.f} * f2{va0, va1};
-          const f2 sx = q.dx * w, sy = q.dy * w;
-          const f2 xx = q.dx * sx, yx = q.dy * sx, yy = q.dy * sy;
-          const f2 fac = f2{fac0, fac1};
-          const f2 fr = fac * vr, fg = fac * vg, fb = fac * vb;
-          const float m[18] = {sx.x, sy.x, xx.x, yx.x, yy.x, fr.x, fg.x, fb.x, w.x,
-                               sx.y, sy.y, xx.y, yx.y, yy.y, fr.y, fg.y, fb.y, w.y};
-          const float v = reduce18(m);
-          const bool act = (for0 && any0) || (for1 && any1);
-          const int g = for1 ? gid1 : gid0;
-          if constexpr (DET) {
-            if (act) det_add(det + ((size_t)g * REC_FIELDS + field) * DET_LIMBS, v);
-          } else {
-            // 32-bit element offset (the entry points reject N >= 2^27)
-            if (act) atomicAdd(rec + (uint32_t)(g * REC + field), v);
-          }
-        }
+    for (int t = 0; t < n; t += 2) {
+      GStage G0 = stage_at(stage, t), G1 = stage_at(stage, min(t + 1, 63));
+      const bool live1 = t + 1 < n;
+      if (!live1) G1.r = G1.g = G1.bl = G1.o = 0.f;  // stale slot: alpha 0, finite terms
+      int gid0 = G0.id, gid1 = G1.id;
+      asm volatile("" : "+v"(gid0), "+v"(gid1));  // read with the records, not at the atomic
+      // the two Gaussians' per-pixel terms (independent)
+      const float dx0 = G0.x - px, dy0 = G0.y - py, dx1 = G1.x - px, dy1 = G1.y - py;
+      const float sg0 = gs_sigma(G0.hc, G0.b * dx0, G0.ha * dx0 * dx0, dy0);
+      const float sg1 = gs_sigma(G1.hc, G1.b * dx1, G1.ha * dx1 * dx1, dy1);
+      const float vis0 = gs_vis(sg0), vis1 = gs_vis(sg1);
+      const float al0 = fminf(amax, G0.o * vis0), al1 = fminf(amax, G1.o * vis1);
+      const bool v0 = G0.idx <= bf && sg0 >= 0.f && al0 >= ALPHA_MIN;
+      const bool v1 = live1 && G1.idx <= bf && sg1 >= 0.f && al1 >= ALPHA_MIN;
+      const unsigned long long any0 = __builtin_amdgcn_ballot_w64(v0),
+                               any1 = __builtin_amdgcn_ballot_w64(v1);
+      if constexpr (CNT) {
+        c_slots += 2 * 64;
+        c_live += (G0.idx <= bf ? 1u : 0u) + (live1 && G1.idx <= bf ? 1u : 0u);
+        c_valid += (v0 ? 1u : 0u) + (v1 ? 1u : 0u);
       }
-    } else {
-      for (int t = 0; t < n; t += 2) {
-        GStage G0 = stage_at(stage, t), G1 = stage_at(stage, min(t + 1, 63));
-        const bool live1 = t + 1 < n;
-        if (!live1) G1.r = G1.g = G1.bl = G1.o = 0.f;  // stale slot: alpha 0, finite terms
-        int gid0 = G0.id, gid1 = G1.id;
-        asm volatile("" : "+v"(gid0), "+v"(gid1));  // read with the records, not at the atomic
-        // the two Gaussians' per-pixel terms (independent)
-        const float dx0 = G0.x - px, dy0 = G0.y - py, dx1 = G1.x - px, dy1 = G1.y - py;
-        const float sg0 = gs_sigma(G0.hc, G0.b * dx0, G0.ha * dx0 * dx0, dy0);
-        const float sg1 = gs_sigma(G1.hc, G1.b * dx1, G1.ha * dx1 * dx1, dy1);
-        const float vis0 = gs_vis(sg0), vis1 = gs_vis(sg1);
-        const float al0 = fminf(amax, G0.o * vis0), al1 = fminf(amax, G1.o * vis1);
-        const bool v0 = G0.idx <= bf && sg0 >= 0.f && al0 >= ALPHA_MIN;
-        const bool v1 = live1 && G1.idx <= bf && sg1 >= 0.f && al1 >= ALPHA_MIN;
-        const unsigned long long any0 = __builtin_amdgcn_ballot_w64(v0),
-                                 any1 = __builtin_amdgcn_ballot_w64(v1);
-        if constexpr (CNT) {
-          c_slots += 2 * 64;
-          c_live += (G0.idx <= bf ? 1u : 0u) + (live1 && G1.idx <= bf ? 1u : 0u);
-          c_valid += (v0 ? 1u : 0u) + (v1 ? 1u : 0u);
-        }
-        // list order (back to front): G0 then G1 -- T and the colour behind are sequential
-        const float am0 = v0 ? al0 : 0.f, am1 = v1 ? al1 : 0.f;
-        const float ra0 = __builtin_amdgcn_rcpf(1.f - am0);
-        T = T * ra0;
-        const float fac0 = am0 * T;
-        const float gv0 = fmaf(G0.r, vr, fmaf(G0.g, vg, G0.bl * vb));
-        const float va0 = fmaf(gv0, T, ra0 * Qs);
-        Qs = fmaf(-fac0, gv0, Qs);
-        const float ra1 = __builtin_amdgcn_rcpf(1.f - am1);
-        T = T * ra1;
-        const float fac1 = am1 * T;
-        const float gv1 = fmaf(G1.r, vr, fmaf(G1.g, vg, G1.bl * vb));
-        const float va1 = fmaf(gv1, T, ra1 * Qs);
-        Qs = fmaf(-fac1, gv1, Qs);
-        if (any0 | any1) {  // (an SGPR test)
-          const float w0 = (v0 ? vis0 : 0.f) * va0, w1 = (v1 ? vis1 : 0.f) * va1;
-          const float sx0 = dx0 * w0, sy0 = dy0 * w0, sx1 = dx1 * w1, sy1 = dy1 * w1;
-          const float m[18] = {sx0, sy0, dx0 * sx0, dy0 * sx0, dy0 * sy0,
-                               fac0 * vr, fac0 * vg, fac0 * vb, w0,
-                               sx1, sy1, dx1 * sx1, dy1 * sx1, dy1 * sy1,
-                               fac1 * vr, fac1 * vg, fac1 * vb, w1};
-          const float v = reduce18(m);
-          const bool act = (for0 && any0) || (for1 && any1);
-          const int g = for1 ? gid1 : gid0;
-          if constexpr (DET) {
-            if (act) det_add(det + ((size_t)g * REC_FIELDS + field) * DET_LIMBS, v);
-          } else {
-            // 32-bit element offset (the entry points reject N >= 2^27)
-            if (act) atomicAdd(rec + (uint32_t)(g * REC + field), v);
-          }
+      // list order (back to front): G0 then G1 -- T and the colour behind are sequential
+      const float am0 = v0 ? al0 : 0.f, am1 = v1 ? al1 : 0.f;
+      const float ra0 = __builtin_amdgcn_rcpf(1.f - am0);
+      T = T * ra0;
+      const float fac0 = am0 * T;
+      const float gv0 = fmaf(G0.r, vr, fmaf(G0.g, vg, G0.bl * vb));
+      const float va0 = fmaf(gv0, T, ra0 * Qs);
+      Qs = fmaf(-fac0, gv0, Qs);
+      const float ra1 = __builtin_amdgcn_rcpf(1.f - am1);
+      T = T * ra1;
+      const float fac1 = am1 * T;
+      const float gv1 = fmaf(G1.r, vr, fmaf(G1.g, vg, G1.bl * vb));
+      const float va1 = fmaf(gv1, T, ra1 * Qs);
+      Qs = fmaf(-fac1, gv1, Qs);
+      if (any0 | any1) {  // (an SGPR test)
+        const float w0 = (v0 ? vis0 : 0.f) * va0, w1 = (v1 ? vis1 : 0.f) * va1;
+        const float sx0 = dx0 * w0, sy0 = dy0 * w0, sx1 = dx1 * w1, sy1 = dy1 * w1;
+        const float m[18] = {sx0, sy0, dx0 * sx0, dy0 * sx0, dy0 * sy0,
+                             fac0 * vr, fac0 * vg, fac0 * vb, w0,
+                             sx1, sy1, dx1 * sx1, dy1 * sx1, dy1 * sy1,
+                             fac1 * vr, fac1 * vg, fac1 * vb, w1};
+        const float v = reduce18(m);
+        const bool act = (for0 && any0) || (for1 && any1);
+        const int g = for1 ? gid1 : gid0;
+        if constexpr (DET) {
+          if (act) det_add(det + ((size_t)g * REC_FIELDS + field) * DET_LIMBS, v);
+        } else {
+          // 32-bit element offset (the entry points reject N >= 2^27)
+          if (act) atomicAdd(rec + (uint32_t)(g * REC + field), v);
         }
       }
     }
@@ -2459,24 +1801,8 @@ struct SplitWs {
   long long items_bound;
   unsigned long long *kbits;  // the forward's keep bits (KeepSrc), SPLIT_WAVES x kbw words
   long long kbw;
-  // the list-split forward (frames below FWD_SPLIT_MAX_TILES tiles; null otherwise): each
-  // tile's first part index fbase[T + 1], the part records and termination masks
-  int *fbase;
-  float *fprec;
-  unsigned long long *ftmask;
-  int fchunk;               // the split forward's part length (fwd_chunk_of(chunk))
-  long long fitems_bound;   // its parts' bound, T + ceil(I / fchunk)
-  int2 *fitems;             // its parts in dispatch order (fwd_plan_kernel)
-  int *n_fitems;
   size_t bytes;
 };
-// The split forward's part length from the plan's chunk: chunk / g_fwd_chunk_div, rounded up
-// to 64 (gsplat_debug_forward_chunk_div; 1 = the backward's chunk).
-int g_fwd_chunk_div = 1;
-static int fwd_chunk_of(int chunk) {
-  const int c = chunk / (g_fwd_chunk_div > 0 ? g_fwd_chunk_div : 1);
-  return std::max(64, (c + 63) / 64 * 64);
-}
 static SplitWs carve_split_ws(void *base, long long T, long long I, int chunk) {
   SplitWs w{};
   w.items_bound = T + (I + chunk - 1) / chunk;
@@ -2491,20 +1817,9 @@ static SplitWs carve_split_ws(void *base, long long T, long long I, int chunk) {
   w.n_items = (int *)take(sizeof(int));
   w.kbw = I / 64 + T + 2;
   w.kbits = (unsigned long long *)take((size_t)SPLIT_WAVES * w.kbw * sizeof(unsigned long long));
-  if (T < FWD_SPLIT_MAX_TILES) {
-    w.fchunk = fwd_chunk_of(chunk);
-    w.fitems_bound = T + (I + w.fchunk - 1) / w.fchunk;
-    w.fbase = (int *)take((size_t)(T + 1) * sizeof(int));
-    w.fprec = (float *)take((size_t)w.fitems_bound * SPLIT_WAVES * FPR * 64 * sizeof(float));
-    w.ftmask = (unsigned long long *)take((size_t)w.fitems_bound * SPLIT_WAVES *
-                                          sizeof(unsigned long long));
-    w.fitems = (int2 *)take((size_t)w.fitems_bound * sizeof(int2));
-    w.n_fitems = (int *)take(sizeof(int));
-  }
   w.bytes = off;
   return w;
 }
-static bool forward_split_on(long long T) { return g_fwd_split != 0 && T < FWD_SPLIT_MAX_TILES; }
 static bool default_variants() {
   // (the staging pipeline bits change the schedule only)
   return g_fwd_pxl == FWD_PXL && g_bwd_pxl == BWD_PXL && (g_bwd_flags & ~(7 << 28)) == 0;
@@ -2559,24 +1874,6 @@ extern "C" size_t gsplat_rasterize_split_bytes(int tile_bounds_x, int tile_bound
 extern "C" int gsplat_debug_set_chunk(int chunk) {
   g_chunk_override = chunk;
   return 0;
-}
-
-// The list-split forward (raster_fwd_part_kernel), below 3,584 tiles (the plan workspace holds
-// its records there): 0 off (the default, see g_fwd_split), 1 / -1 on, 2 on with every pixel of
-// a split tile resolved by the exact sequential walk (tests: then bit-identical to the unsplit
-// forward); other values leave the setting (a query).
-// Returns the previous setting.
-// The split forward's part length as the plan's chunk / div (rounded up to 64; 1 the default).
-extern "C" int gsplat_debug_forward_chunk_div(int div) {
-  const int prev = g_fwd_chunk_div;
-  if (div >= 1 && div <= 64) g_fwd_chunk_div = div;
-  return prev;
-}
-
-extern "C" int gsplat_debug_forward_split(int mode) {
-  const int prev = g_fwd_split;
-  if (mode >= -1 && mode <= 2) g_fwd_split = mode;
-  return prev;
 }
 
 static bool bad_frame(int tbx, int tby, int H, int W) {
@@ -2902,23 +2199,12 @@ static int forward_clearing_impl(
     float *out_img, float *final_Ts, int32_t *final_idx, void *clear, size_t clear_bytes,
     const int32_t *clear_radii, int64_t num_intersects, int chunk, void *plan, size_t plan_bytes,
     const float *l1_gt, float *l1_part, int l1_clamp, float *l1_loss, void *stream) {
-  // chunk < 0: the list-split forward of parts of -chunk positions only (a render without a
-  // backward: no walk table, keep bits or backward plan)
-  const int fchunk = chunk < 0 ? -chunk : chunk;
   if (bad_frame(tile_bounds_x, tile_bounds_y, img_height, img_width) || clear_bytes % 16 ||
-      (clear_bytes && !clear) || (clear_radii && clear_bytes % 64) ||
-      (fchunk > 0 && (fchunk % 64 || num_intersects < 0))) {
+      (clear_bytes && !clear) || (clear_radii && clear_bytes % 64) || chunk < 0 ||
+      (chunk > 0 && (chunk % 64 || num_intersects < 0))) {
     set_error("%s: bad sizes (tiles=%dx%d H=%d W=%d clear=%zu chunk=%d)", who, tile_bounds_x,
               tile_bounds_y, img_height, img_width, clear_bytes, chunk);
     return 1;
-  }
-  if (chunk < 0) {
-    const SplitWs w =
-        carve_split_ws(plan, (long long)tile_bounds_x * tile_bounds_y, num_intersects, fchunk);
-    if (!plan || plan_bytes < w.bytes) {
-      set_error("%s: split plan buffer %zu < %zu bytes", who, plan_bytes, w.bytes);
-      return 1;
-    }
   }
   int *tile_last = nullptr;  // the list-split plan's walk table, filled by the blend's waves
   unsigned long long *kbits = nullptr;  // and the backward's keep bits (KeepSrc)
@@ -2937,46 +2223,11 @@ static int forward_clearing_impl(
     }
     plan_kbits_note(plan, kbits != nullptr, true);
   }
-  const long long Tt = (long long)tile_bounds_x * tile_bounds_y;
-  if (fchunk > 0 && forward_split_on(Tt) && !g_pair_count_on && default_variants()) {
-    // the list-split forward: plan, parts, combine (see fwd_plan_kernel)
-    const SplitWs w = carve_split_ws(plan, Tt, num_intersects, fchunk);
-    const int chunk = w.fchunk;
-    hipStream_t st = (hipStream_t)stream;
-    hipLaunchKernelGGL(fwd_plan_kernel, dim3(1), dim3(1024), 0, st, (int)Tt, chunk,
-                       (const int2 *)tile_bins, w.fitems, w.n_fitems, w.fbase, w.ftmask);
-    // every tile's first part (the plain forward for a tile of one part), then the later parts:
-    // a dense tile's pixels mostly stop in its first part, and the later parts skip them
-    // (launched together, the later parts would blend every position of every list)
-    hipLaunchKernelGGL(raster_fwd_part_kernel<false>, dim3((unsigned)Tt), dim3(256), 0, st,
-                       tile_bounds_x, tile_bounds_y, img_height, img_width, gaussian_ids_sorted,
-                       (const int2 *)tile_bins, (const float2 *)xys, conics, colors, opacity,
-                       background, out_img, final_Ts, final_idx, (float4 *)clear,
-                       (long long)(clear_bytes / 16), clear_radii, tile_last, kbits, kbw, l1_gt,
-                       l1_part, l1_clamp, chunk, (const int2 *)w.fitems, (const int *)w.n_fitems,
-                       (const int *)w.fbase, w.fprec, w.ftmask, 0, (int)Tt);
-    if (w.fitems_bound > Tt)
-      hipLaunchKernelGGL(raster_fwd_part_kernel<false>, dim3((unsigned)(w.fitems_bound - Tt)),
-                         dim3(256), 0, st, tile_bounds_x, tile_bounds_y, img_height, img_width,
-                         gaussian_ids_sorted, (const int2 *)tile_bins, (const float2 *)xys,
-                         conics, colors, opacity, background, out_img, final_Ts, final_idx,
-                         (float4 *)nullptr, 0LL, (const int *)nullptr, tile_last, kbits, kbw,
-                         l1_gt, l1_part, l1_clamp, chunk, (const int2 *)w.fitems,
-                         (const int *)w.n_fitems, (const int *)w.fbase, w.fprec, w.ftmask,
-                         (int)Tt);
-    hipLaunchKernelGGL(raster_fwd_combine_kernel, dim3((unsigned)Tt), dim3(256), 0, st,
-                       tile_bounds_x, tile_bounds_y, img_height, img_width, gaussian_ids_sorted,
-                       (const int2 *)tile_bins, (const float2 *)xys, conics, colors, opacity,
-                       background, out_img, final_Ts, final_idx, tile_last, l1_gt, l1_part,
-                       l1_clamp, chunk, (const int *)w.fbase, (const float *)w.fprec,
-                       g_fwd_split == 2 ? 1e30f : 0x1p-24f * 1.01f);
-  } else {
-    launch_fwd<false>((hipStream_t)stream, tile_bounds_x, tile_bounds_y, img_height, img_width,
-                      gaussian_ids_sorted, tile_bins, xys, conics, colors, opacity, background,
-                      out_img, final_Ts, final_idx, nullptr, nullptr, (float4 *)clear,
-                      (long long)(clear_bytes / 16), clear_radii, tile_last, kbits, kbw, l1_gt,
-                      l1_part, l1_clamp);
-  }
+  launch_fwd<false>((hipStream_t)stream, tile_bounds_x, tile_bounds_y, img_height, img_width,
+                    gaussian_ids_sorted, tile_bins, xys, conics, colors, opacity, background,
+                    out_img, final_Ts, final_idx, nullptr, nullptr, (float4 *)clear,
+                    (long long)(clear_bytes / 16), clear_radii, tile_last, kbits, kbw, l1_gt,
+                    l1_part, l1_clamp);
   // the loss of the partials and the list-split plan, one launch (post_forward_kernel)
   const bool plan_job = chunk > 0, loss_job = l1_part != nullptr;
   if (plan_job || loss_job) {

@@ -38,8 +38,6 @@ from .rasterize import (BLOCK_X, BLOCK_Y, SPEC_STATS, bin_gaussians, bin_gaussia
                         speculative_capacity, last_num_visible)
 
 _DEG_OF_BASES = {1: 0, 4: 1, 9: 2, 16: 3, 25: 4}
-# frames below this many tiles get the list-split forward (raster.hip FWD_SPLIT_MAX_TILES)
-FWD_SPLIT_TILES = 3584
 
 # How the last forward binned: "speculative" (capacity-launched, no host read), "host" (the
 # scheme needs I on the host first) or "sync" (first call of the frame shape)
@@ -142,16 +140,10 @@ class _FusedRender(Function):
         def plan_for(layout_i):
             """(chunk, plan buffer) of the list-split plan laid out for layout_i intersections."""
             c = _lib.query("gsplat_rasterize_chunk_size", tbx, tby, layout_i)
-            if not need_grad:
-                # no backward: the plan only for the list-split forward of small frames
-                # (below FWD_SPLIT_TILES tiles, when switched on), signalled by a negative chunk
-                split = tbx * tby < FWD_SPLIT_TILES and \
-                    _lib.query("gsplat_debug_forward_split", -9) != 0
-                c = -c if split else 0
-            if c == 0:
+            if not need_grad or c == 0:  # (the plan is the backward's)
                 return 0, None
             return c, torch.empty((_lib.query("gsplat_rasterize_split_bytes", tbx, tby,
-                                              layout_i, abs(c)),), device=dev, dtype=torch.uint8)
+                                              layout_i, c),), device=dev, dtype=torch.uint8)
         # the speculative binning's layout is its capacity, known now
         spec_cap = speculative_capacity(n, H, W, dev)
         prepared = (spec_cap, plan_for(spec_cap)) if spec_cap > 0 else None

@@ -329,15 +329,6 @@ int gsplat_rasterize_forward_clearing(
 /* Debug: force the list-split chunk (> 0, rounded up to 64), disable it (< 0) or restore
  * the automatic choice (0). */
 int gsplat_debug_set_chunk(int chunk);
-/* The list-split forward of small frames (below 3,584 tiles; gsplat_rasterize_forward_clearing*
- * with a plan): 0 off (default: measured slower on c3), -1 or 1 on, 2 on with every pixel of a
- * split tile resolved by the exact sequential walk (bit-identical to the unsplit forward;
- * tests); any other value only queries.  Returns the previous setting. */
-int gsplat_debug_forward_split(int mode);
-/* The split forward's part length: the plan's chunk / div, rounded up to 64 (div 1..64; 1 the
- * default).  Returns the previous div.  Plans must be sized after setting it
- * (gsplat_rasterize_split_bytes). */
-int gsplat_debug_forward_chunk_div(int div);
 
 size_t gsplat_rasterize_backward_workspace_size(int num_points, int channels);
 int gsplat_rasterize_backward(int tile_bounds_x, int tile_bounds_y, int img_height,

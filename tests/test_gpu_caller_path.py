@@ -31,10 +31,6 @@ def test_caller_path_fusions_are_exact(gpu, size, monkeypatch):
     sc = synthetic_scene(n, max(deg, 0), seed=5, scale_lo=0.005, scale_hi=0.05)
     cam = synthetic_camera(W, H)
     prev = _lib.set_deterministic(True)
-    # the caller path's forward is the unsplit one (no list-split plan): the fused path's split
-    # forward of small frames regroups the transmittance product (test_gpu_forward_split), so it
-    # is pinned off for this bit-identity check
-    prev_fs = _lib.query("gsplat_debug_forward_split", 0)
     try:
         hits0 = R.keyed_workspaces.cache.hits
         fused = [t.detach().cpu() for t in _run(gpu, sc, cam, deg)]
@@ -45,7 +41,6 @@ def test_caller_path_fusions_are_exact(gpu, size, monkeypatch):
         plain = [t.detach().cpu() for t in _run(gpu, sc, cam, deg)]
     finally:
         _lib.set_deterministic(prev)
-        _lib.query("gsplat_debug_forward_split", prev_fs)
     names = ["rgb", "alpha", "depth", "means", "scales", "quats", "opacities", "dc", "rest"]
     for name, a, b in zip(names, fused, plain):
         assert a.shape == b.shape, name

@@ -141,9 +141,6 @@ def test_list_split_bit_identical_to_the_full_walk(gpu, deterministic, bwd, mode
     sc = synthetic_scene(30000, 3, seed=5, scale_lo=0.005, scale_hi=0.06)
     cam = synthetic_camera(512, 384)
     _lib.call("gsplat_debug_set_raster_variant", 1, bwd, 0)
-    # (the forward split regroups the forward's transmittance product, so it is pinned off here:
-    # this test is about the backward's split; test_gpu_forward_split covers the forward's)
-    prev_fs = _lib.query("gsplat_debug_forward_split", 0)
     try:
         _lib.call("gsplat_debug_set_chunk", -1)
         full = _grads(gpu, mode, sc, cam)
@@ -152,7 +149,6 @@ def test_list_split_bit_identical_to_the_full_walk(gpu, deterministic, bwd, mode
     finally:
         _lib.call("gsplat_debug_set_chunk", 0)
         _lib.call("gsplat_debug_set_raster_variant", 1, 0, 0)
-        _lib.query("gsplat_debug_forward_split", prev_fs)
     for name, x, y in zip(("means", "scales", "quats", "opacities", "dc", "rest"), full, split):
         assert np.abs(x).max() > 0, name
         np.testing.assert_array_equal(y, x, err_msg=name)
