@@ -251,7 +251,8 @@ class _FusedRender(Function):
         ctx.l1 = (out_img, l1_gt) if l1_gt is not None else None
         aux.update(xys=xys, radii=radii, depths=depths, num_intersects=num_intersects,
                    records=rec, num_points=n, conics=conics, colors=colors, opacity=opac,
-                   num_tiles_hit=nth)
+                   num_tiles_hit=nth, gaussian_ids_sorted=gids, tile_bins=bins,
+                   final_Ts=final_Ts, final_idx=final_idx, binning=LAST_BINNING["mode"])
         if l1_gt is not None:
             ctx.mark_non_differentiable(out_img)
             return loss, out_img
@@ -443,6 +444,9 @@ def render_fused(scene, cam: GCCamera, sh_degree_to_use: int, background: Tensor
             # the clamp mask in their sign bit: -0.0, which no rasterizer sum can see)
             "raster_inputs": {k: aux[k] for k in ("xys", "depths", "radii", "conics",
                                                    "num_tiles_hit", "colors", "opacity")},
+            # the binning and the blend's final state, as the backward consumes them (tests)
+            "raster_state": {k: aux[k] for k in ("gaussian_ids_sorted", "tile_bins", "final_Ts",
+                                                  "final_idx", "binning")},
             "num_intersects": aux["num_intersects"]}
 
 

@@ -1,21 +1,25 @@
-"""The kernels bench.py times, at BASELINE.json's full sizes (headline 1M @ 1080², c3 bear,
-c4 garden 2M @ 1080², c5 5M @ 2048²; c2 forward only), driven through the C ABI in exactly
-the fused training render's sequence (gaussctrl_exp_amd/fused.py):
+"""The step bench.py times, at BASELINE.json's full sizes (headline 1M @ 1080², c3 bear, c4
+garden 2M @ 1080², c5 5M @ 2048²; c2 forward only), through exactly the code bench.py runs:
+TrainStep(loss="l1", render_mode="fused").forward_backward (fused.render_fused with the L1 loss
+inside the blend), i.e. the kernels of the bench line's `kernels` block:
 
-  gsplat_fused_preprocess_forward_binned -> gsplat_bin_count_keyed -> gsplat_bin_emit ->
-  gsplat_rasterize_forward_clearing -> gsplat_rasterize_backward_records ->
-  gsplat_fused_preprocess_backward
+  gsplat_fused_preprocess_forward_part [2] (SH colours, second stream) + [1] (projection, keys)
+  gsplat_bin_speculative       (depth sort + region binning at the learned capacity: the second
+                                call of the frame shape -- the first one bins synchronously)
+  gsplat_rasterize_forward_clearing_l1   (blend + L1 partials + records cleared)
+  gsplat_rasterize_backward_records_l1   (L1 upstream formed per pixel, record backward; strip
+                                          geometry from 3,584 tiles, 8x8 blocks + list split below)
+  gsplat_fused_preprocess_backward       (projection / SH / activation chain rule)
 
-Checked, with zero outliers:
-* projection outputs bit-exact vs the oracle on torch's activations of the parameters;
-* the keyed binning identical to the plain binning of the same outputs (which
-  test_gpu_fullsize checks bit-exact against the oracle at these sizes);
-* the blend on sampled tiles vs the oracle (image, alpha), and the gradient records cleared;
-* the backward's records (raster-level gradients, upstream gradient on the sampled tiles only)
-  vs the oracle's rasterize backward on the same forward state (fp32 summation slack);
-* with a dense upstream gradient, the fused backward's six parameter gradients over ALL N vs
-  the oracle chain (projection + SH VJPs, torch's activation derivatives in float64) fed the
-  same records.
+Checked, with zero outliers (tests/parity.py bars):
+* projection outputs bit-exact vs the oracle on torch's activations; SH colours vs the oracle;
+* the speculative binning bit-exact vs the oracle's stable sort of gsplat's keys;
+* the image on sampled tiles vs the oracle's forward, final_idx bit-exact, the loss vs float64;
+* the records (raster-level gradients) vs the oracle's rasterize backward on the sampled tiles:
+  the ground truth equals the clamped image everywhere else, so the L1 upstream gradient
+  sign(clamp(img) - gt) is zero there and the records hold the sampled tiles' sums only;
+* the six parameter gradients over ALL N vs the oracle chain (projection + SH VJPs, torch's
+  activation derivatives in float64) fed the same raster-level gradients.
 """
 import numpy as np
 import pytest
@@ -23,8 +27,9 @@ import torch
 
 import bench
 import oracle as O
-from gaussctrl_exp_amd import _lib, quirks
-from gaussctrl_exp_amd.rasterize import bin_gaussians
+from gaussctrl_exp_amd import quirks
+from gaussctrl_exp_amd.fused import render_fused
+from gaussctrl_exp_amd.train import TrainStep
 from parity import assert_close, assert_raster_close, close_frac
 
 pytestmark = pytest.mark.gpu
@@ -34,98 +39,55 @@ def _np(t):
     return t.detach().cpu().numpy()
 
 
-class FusedRun:
-    """One view of a bench config through the fused C-ABI sequence, intermediates kept."""
+class BenchStep:
+    """One view of a bench config stepped as bench.py steps it, intermediates kept."""
 
     def __init__(self, config, gpu):
         sc, cam = bench.make_workload(config, 0, gpu)
-        self.sc, self.cam, self.gpu, self.config = sc, cam.to(gpu), gpu, config
+        self.config, self.gpu, self.sc, self.cam = config, gpu, sc, cam.to(gpu)
         c = self.cam
-        n = sc.means.shape[0]
-        K = 1 + sc.features_rest.shape[1]
-        self.n, self.K, self.dtu = n, K, {1: 0, 4: 1, 9: 2, 16: 3, 25: 4}[K]
-        H, W = c.height, c.width
-        self.H, self.W = H, W
-        self.tb = c.tile_bounds
-        f = lambda *s: torch.empty(*s, device=gpu)
-        self.xys, self.depths, self.conics = f(n, 2), f(n), f(n, 3)
-        self.colors, self.opac = f(n, 3), f(n)
-        self.radii = torch.empty(n, device=gpu, dtype=torch.int32)
-        self.nth = torch.empty(n, device=gpu, dtype=torch.int32)
-        self.campos = c.c2w[:3, 3].contiguous()
-        P, st = _lib.ptr, _lib.stream(gpu)
-        ws1 = torch.empty((_lib.query("gsplat_bin_count_workspace_size", n),), device=gpu,
-                          dtype=torch.uint8)
-        _lib.call("gsplat_fused_preprocess_forward_binned", n, K, self.dtu, P(sc.means),
-                  P(sc.scales), P(sc.quats), P(sc.opacities), P(sc.features_dc),
-                  P(sc.features_rest) if K > 1 else None, P(c.viewmat), P(c.projmat),
-                  P(self.campos), c.fx, c.fy, c.cx, c.cy, H, W, self.tb[0], self.tb[1], 0.01,
-                  P(self.xys), P(self.depths), P(self.radii), P(self.conics), P(self.nth),
-                  P(self.colors), P(self.opac), P(ws1), ws1.numel(), st)
-        self.I, self.gids, self.bins = bin_gaussians(self.xys, self.depths, self.radii, self.nth,
-                                                     H, W, keyed_workspace=ws1)
-        self.rec = torch.full((_lib.query("gsplat_grad_records_bytes", n),), 0x7F, device=gpu,
-                              dtype=torch.uint8)
-        self.chunk = _lib.query("gsplat_rasterize_chunk_size", self.tb[0], self.tb[1], self.I)
-        self.plan = torch.empty((max(_lib.query("gsplat_rasterize_split_bytes", self.tb[0],
-                                                self.tb[1], self.I, self.chunk), 1),),
-                                device=gpu, dtype=torch.uint8)
+        self.H, self.W, self.tb = c.height, c.width, c.tile_bounds
+        self.n = sc.means.shape[0]
+        self.K = 1 + sc.features_rest.shape[1]
+        self.dtu = {1: 0, 4: 1, 9: 2, 16: 3, 25: 4}[self.K]
         self.bg = torch.tensor([0.3, 0.2, 0.1], device=gpu)
-
-    def forward(self):
-        """The clearing blend; returns (img, final_Ts, final_idx)."""
-        P, st, gpu = _lib.ptr, _lib.stream(self.gpu), self.gpu
-        H, W = self.H, self.W
-        img = torch.empty(H, W, 3, device=gpu)
-        fT = torch.empty(H, W, device=gpu)
-        fi = torch.empty(H, W, device=gpu, dtype=torch.int32)
-        vis_only = self.radii if int((self.radii > 0).sum()) < 0.9 * self.n else None
-        _lib.call("gsplat_rasterize_forward_clearing", self.tb[0], self.tb[1], H, W, P(self.gids),
-                  P(self.bins), P(self.xys), P(self.conics), P(self.colors), P(self.opac),
-                  P(self.bg), P(img), P(fT), P(fi), P(self.rec), self.rec.numel(), P(vis_only),
-                  self.I, self.chunk, P(self.plan), self.plan.numel() if self.chunk > 0 else 0, st)
-        self.fT, self.fi = fT, fi
-        return img, fT, fi
-
-    def backward(self, v_img, v_alpha, final_Ts=None, final_idx=None):
-        """The record backward from the forward's state (or the given final_Ts / final_idx)."""
-        P, st = _lib.ptr, _lib.stream(self.gpu)
-        self.v_img, self.v_alpha = v_img.to(self.gpu).contiguous(), v_alpha.to(self.gpu).contiguous()
-        fT = self.fT if final_Ts is None else final_Ts
-        fi = self.fi if final_idx is None else final_idx
-        _lib.call("gsplat_rasterize_backward_records", self.tb[0], self.tb[1], self.H, self.W,
-                  self.n, P(self.gids), P(self.bins), P(self.xys), P(self.conics),
-                  P(self.colors), P(self.opac), P(self.bg), P(fT), P(fi),
-                  P(self.v_img), P(self.v_alpha), quirks.backward_alpha_clamp(), self.I,
-                  self.chunk, P(self.plan), self.plan.numel() if self.chunk > 0 else 0,
-                  # the walk table the forward filled: only for its own final state
-                  int(final_idx is None and self.chunk > 0), P(self.rec), self.rec.numel(), st)
-
-    def raster_grads(self):
-        """The records (pixel moments) -> gsplat's four raster gradients (the split kernel)."""
-        P, n = _lib.ptr, self.n
-        out = [torch.empty(n, k, device=self.gpu) for k in (2, 3, 3, 1)]
-        _lib.call("gsplat_grad_records_split", n, P(self.rec), self.rec.numel(), P(self.conics),
-                  P(self.opac), *[P(t) for t in out], _lib.stream(self.gpu))
-        vis = self.radii[:, None] > 0
-        return tuple(_np(torch.where(vis, t, torch.zeros_like(t))) for t in out)
-
-    def param_grads(self):
-        P, st, gpu, n, K, sc, c = _lib.ptr, _lib.stream(self.gpu), self.gpu, self.n, self.K, \
-            self.sc, self.cam
-        f = lambda *s: torch.empty(*s, device=gpu)
-        out = [f(n, 3), f(n, 3), f(n, 4), f(n, 1), f(n, 3), f(n, K - 1, 3)]
-        _lib.call("gsplat_fused_preprocess_backward", n, K, self.dtu, P(sc.means), P(sc.scales),
-                  P(sc.quats), P(c.viewmat), P(c.projmat), P(self.campos), c.fx, c.fy, c.cx,
-                  c.cy, self.H, self.W, P(self.radii), P(self.conics), P(self.colors),
-                  P(self.opac), P(self.rec), *[P(t) for t in out[:5]],
-                  P(out[5]) if K > 1 else None, None, st)
-        return [_np(t) for t in out]
+        self.trainer = TrainStep(sc, sh_degree=self.dtu, world_size=1, loss="l1",
+                                 render_mode="fused")
+        # first call of the frame shape: synchronous binning (learns the capacity / key range)
+        gt0 = torch.rand(self.H, self.W, 3, generator=torch.Generator().manual_seed(4)).to(gpu)
+        self.trainer.zero_grad()
+        _, out0 = self.trainer.forward_backward(c, gt0, self.bg)
+        assert out0["raster_state"]["binning"] == "sync"
+        self.img0 = out0["rgb"].detach().clone()
+        T = self.tb[0] * self.tb[1]
+        self.tiles = np.random.default_rng(3).choice(
+            T, size=min(24 if self.n > 3_000_000 else 48, T), replace=False).astype(np.int32)
+        m = np.zeros((self.H, self.W), bool)
+        for t in self.tiles:
+            y0, x0 = (t // self.tb[0]) * 16, (t % self.tb[0]) * 16
+            m[y0:y0 + 16, x0:x0 + 16] = True
+        self.mask = m
+        # the ground truth: random on the sampled tiles, the clamped image elsewhere (zero L1
+        # gradient there)
+        gt = torch.clamp(self.img0, max=1.0)
+        r = torch.rand(self.H, self.W, 3, generator=torch.Generator().manual_seed(9)).to(gpu)
+        mt = torch.from_numpy(m).to(gpu)[..., None]
+        self.gt = torch.where(mt, r, gt).contiguous()
+        self.trainer.zero_grad()
+        self.loss, self.out = self.trainer.forward_backward(c, self.gt, self.bg)
+        self.param_grads = [_np(p.grad) for p in sc.params()]
+        self.raster_grads = [_np(g) for g in self.out["raster_grads"]()]
+        self.inp = {k: _np(v) for k, v in self.out["raster_inputs"].items()}
+        st = self.out["raster_state"]
+        self.gids, self.bins = _np(st["gaussian_ids_sorted"]), _np(st["tile_bins"])
+        self.fT, self.fi = _np(st["final_Ts"]), _np(st["final_idx"])
+        self.binning = st["binning"]
+        self.img = _np(self.out["rgb"])
 
 
 @pytest.fixture(scope="module", params=["headline", "c3", "c4", "c5"])
 def run(request, gpu, oracle_lib):
-    return FusedRun(request.param, gpu)
+    return BenchStep(request.param, gpu)
 
 
 def _activated(sc):
@@ -134,83 +96,68 @@ def _activated(sc):
     return (_np(torch.exp(sc.scales)), _np(sc.quats / sc.quats.norm(dim=-1, keepdim=True)))
 
 
-def _tiles(run, count, seed=3):
-    T = run.tb[0] * run.tb[1]
-    return np.random.default_rng(seed).choice(T, size=min(count, T), replace=False).astype(np.int32)
-
-
-def _mask(run, tiles):
-    m = np.zeros((run.H, run.W), bool)
-    for t in tiles:
-        y0, x0 = (t // run.tb[0]) * 16, (t % run.tb[0]) * 16
-        m[y0:y0 + 16, x0:x0 + 16] = True
-    return m
-
-
-def test_preprocess_and_keyed_binning(gpu, run):
+def test_preprocess_outputs(gpu, run):
     c, sc = run.cam, run.sc
     s_act, q_act = _activated(sc)
     o = O.project_forward(_np(sc.means), s_act, 1.0, q_act, _np(c.viewmat), _np(c.projmat),
                           c.fx, c.fy, c.cx, c.cy, run.H, run.W, run.tb)
-    for name, g, r in zip(["xys", "depths", "radii", "conics", "num_tiles_hit"],
-                          [run.xys, run.depths, run.radii, run.conics, run.nth], o[:5]):
-        np.testing.assert_array_equal(_np(g), r, err_msg=name)
-    I, gids, bins = bin_gaussians(run.xys, run.depths, run.radii, run.nth, run.H, run.W)
-    assert I == run.I == int(o[4].astype(np.int64).sum()) > 1 << 20
-    assert torch.equal(gids, run.gids) and torch.equal(bins, run.bins)
+    for name, r in zip(["xys", "depths", "radii", "conics", "num_tiles_hit"], o[:5]):
+        np.testing.assert_array_equal(run.inp[name], r, err_msg=name)
+    # SH colours (gc_model.py:196-201): clamp(SH(dirs) + 0.5, min=0), the clamp mask in the sign
+    d = _np(sc.means) - _np(c.c2w[:3, 3])
+    dirs = (d / np.linalg.norm(d, axis=1, keepdims=True)).astype(np.float32)
+    coeffs = np.concatenate([_np(sc.features_dc)[:, None], _np(sc.features_rest)], 1)
+    ref = np.maximum(O.sh_forward(run.dtu, dirs, coeffs) + 0.5, 0.0)
+    vis = o[2] > 0
+    assert_close("colours (visible)", np.abs(run.inp["colors"][vis]), ref[vis])
 
 
-def test_blend_and_records_on_sampled_tiles(gpu, run):
-    tiles = _tiles(run, 24 if run.n > 3_000_000 else 48)
-    mask = _mask(run, tiles)
-    img, fT, fi = run.forward()
-    assert int(run.rec.view(-1, 64)[run.radii > 0].count_nonzero()) == 0  # records cleared
-    xys, conics, colors, opac = (_np(t) for t in (run.xys, run.conics, run.colors, run.opac))
-    bg = _np(run.bg)
-    rimg, rT, ridx = O.rasterize_forward(run.tb, run.H, run.W, _np(run.gids), _np(run.bins), xys,
-                                         conics, colors, opac, bg, tile_list=tiles)
-    assert_close("image (sampled tiles)", _np(img)[mask], rimg[mask])
-    assert_close("alpha (sampled tiles)", 1 - _np(fT)[mask], 1 - rT[mask])
-    # final_idx: the integer forward state the backward walks from, bit-exact
-    np.testing.assert_array_equal(_np(fi)[mask], ridx[mask], err_msg="final_idx")
-    gen = torch.Generator().manual_seed(9)
-    m = torch.from_numpy(mask)
-    v_img = torch.randn(run.H, run.W, 3, generator=gen) * m[..., None]
-    v_alpha = torch.randn(run.H, run.W, generator=gen) * m
-    run.backward(v_img, v_alpha)
-    got = run.raster_grads()
+def test_speculative_binning_bitexact(gpu, run):
+    assert run.binning == "speculative"
+    ref = O.bin_and_sort(run.inp["xys"], run.inp["depths"], run.inp["radii"],
+                         run.inp["num_tiles_hit"], run.tb)
+    assert run.out["num_intersects"] == ref["num_intersects"] > 1 << 20
+    np.testing.assert_array_equal(run.gids, ref["gaussian_ids_sorted"])
+    np.testing.assert_array_equal(run.bins, ref["tile_bins"])
+
+
+def test_blend_loss_and_records_on_sampled_tiles(gpu, run):
+    inp, bg, mask = run.inp, _np(run.bg), run.mask
+    # the same forward as the first (synchronously binned) step: deterministic, bit-identical
+    np.testing.assert_array_equal(run.img, _np(run.img0))
+    rimg, rT, ridx = O.rasterize_forward(run.tb, run.H, run.W, run.gids, run.bins, inp["xys"],
+                                         inp["conics"], np.abs(inp["colors"]), inp["opacity"], bg,
+                                         tile_list=run.tiles)
+    assert_close("image (sampled tiles)", run.img[mask], rimg[mask])
+    assert_close("alpha (sampled tiles)", 1 - run.fT[mask], 1 - rT[mask])
+    np.testing.assert_array_equal(run.fi[mask], ridx[mask], err_msg="final_idx")
+    gt = _np(run.gt)
+    ref_loss = np.abs(np.minimum(run.img.astype(np.float64), 1.0) - gt).mean()
+    assert abs(float(run.loss) - ref_loss) <= 1e-6 * ref_loss, (float(run.loss), ref_loss)
+    # the L1 loss's upstream gradient (l1_grad1 in raster.hip: sign(clamp(p) - g), masked where
+    # the clamp saturates, times d loss / d loss = 1 over 3 H W); zero off the sampled tiles
+    p = run.img
+    s = np.sign(np.minimum(p, 1.0) - gt) * (p <= 1.0)
+    v_img = (np.float32(1.0 / (3.0 * run.H * run.W)) * s).astype(np.float32)
+    assert not v_img[~mask].any()
+    v_alpha = np.zeros((run.H, run.W), np.float32)
+    # (the backward walks from the GPU forward's final state, which matched the oracle's above)
     ref, absum, drift, flip = O.rasterize_backward(
-        run.tb, run.H, run.W, _np(run.gids), _np(run.bins), xys, conics, colors, opac, bg,
-        _np(fT), _np(fi), v_img.numpy(), v_alpha.numpy(), alpha_max=quirks.backward_alpha_clamp(),
-        tile_list=tiles, return_abs=True, return_drift=True, return_flip=True)
+        run.tb, run.H, run.W, run.gids, run.bins, inp["xys"], inp["conics"],
+        np.abs(inp["colors"]), inp["opacity"], bg, run.fT, run.fi, v_img, v_alpha,
+        alpha_max=quirks.backward_alpha_clamp(), tile_list=run.tiles, return_abs=True,
+        return_drift=True, return_flip=True)
     for k, name in enumerate(("v_xy", "v_conic", "v_colors", "v_opacity")):
-        assert np.abs(ref[k]).max() > 0
-        assert_raster_close(f"{run.config} {name}", got[k], ref[k], absum[k], drift[k], flip[k])
-    # the same backward fed the ORACLE's forward state (its final_Ts / final_idx; zero outside the
-    # sampled tiles, where the upstream gradient is zero too) instead of the GPU's
-    run.rec.fill_(0)
-    fT_o = torch.from_numpy(np.ascontiguousarray(rT)).to(gpu)
-    fi_o = torch.from_numpy(np.ascontiguousarray(ridx)).to(gpu)
-    run.backward(v_img, v_alpha, final_Ts=fT_o, final_idx=fi_o)
-    got_o = run.raster_grads()
-    ref_o, absum_o, drift_o, flip_o = O.rasterize_backward(
-        run.tb, run.H, run.W, _np(run.gids), _np(run.bins), xys, conics, colors, opac, bg, rT,
-        ridx, v_img.numpy(), v_alpha.numpy(), alpha_max=quirks.backward_alpha_clamp(),
-        tile_list=tiles, return_abs=True, return_drift=True, return_flip=True)
-    for k, name in enumerate(("v_xy", "v_conic", "v_colors", "v_opacity")):
-        assert_raster_close(f"{run.config} {name} (oracle forward state)", got_o[k], ref_o[k],
-                            absum_o[k], drift_o[k], flip_o[k])
+        assert np.abs(ref[k]).max() > 0, name
+        assert_raster_close(f"{run.config} {name}", run.raster_grads[k], ref[k], absum[k],
+                            drift[k], flip[k])
 
 
 def test_fused_backward_chain_all_gaussians(gpu, run):
-    """Dense upstream gradient; the fused backward's six gradients (all N) vs the oracle chain
-    on the same raster-level gradients."""
-    run.forward()
-    gen = torch.Generator().manual_seed(11)
-    run.backward(torch.randn(run.H, run.W, 3, generator=gen) * 0.1,
-                 torch.randn(run.H, run.W, generator=gen) * 0.1)
-    v_xy, v_conic, v_colors, v_opac = run.raster_grads()
-    got = run.param_grads()
+    """The six parameter gradients of the bench step (all N) vs the oracle chain on the same
+    raster-level gradients."""
+    v_xy, v_conic, v_colors, v_opac = run.raster_grads
+    got = run.param_grads
     sc, c = run.sc, run.cam
     means = _np(sc.means)
     s_act, q_act = _activated(sc)
@@ -221,16 +168,14 @@ def test_fused_backward_chain_all_gaussians(gpu, run):
         means, s_act, 1.0, q_act, vm, pm, c.fx, c.fy, c.cx, c.cy, run.H, run.W, o[5], o[2],
         o[3], v_xy, np.zeros(run.n, np.float32), v_conic)
     vis = o[2] > 0
-    # SH (gc_model.py:196-201): colours = clamp(SH(dirs) + 0.5, min=0); no viewdir gradient
-    d = means - _np(run.campos)
+    d = means - _np(c.c2w[:3, 3])
     dirs = (d / np.linalg.norm(d, axis=1, keepdims=True)).astype(np.float32)
     coeffs = np.concatenate([_np(sc.features_dc)[:, None], _np(sc.features_rest)], 1)
     # the clamp's backward mask: the kernel keeps it in the colour's sign bit (-0.0 = clamped),
     # which is exactly torch's clamp decision on its SH value (test_gpu_fused: bit-identical)
-    passed = ~np.signbit(_np(run.colors))
+    passed = ~np.signbit(run.inp["colors"])
     v_sh = np.where(passed & vis[:, None], v_colors, 0).astype(np.float32)
     v_coeffs = O.sh_backward(run.dtu, dirs, v_sh, run.K)
-    # activation derivatives (torch's formulas), float64
     f64 = lambda a: np.asarray(a, np.float64)
     q = f64(_np(sc.quats))
     qn_norm = np.linalg.norm(q, axis=1, keepdims=True)
@@ -248,23 +193,30 @@ def test_fused_backward_chain_all_gaussians(gpu, run):
         assert np.isfinite(a).all(), name
         assert np.abs(b).max() > 0, name
         mx = assert_close(name, a, b, extra=q_slack if name == "quats" else None)
-        print(f"{run.n}: {name} max |diff| {mx:.3e}")
+        print(f"{run.config} {run.n}: {name} max |diff| {mx:.3e}")
 
 
 def test_c2_forward_full_image(gpu, oracle_lib):
-    """c2 (100k @ 512², SH degree 0: sigmoid colours, forward only): the full image and alpha
-    of the fused forward vs the oracle, zero outliers."""
-    run = FusedRun("c2", gpu)
-    img, fT, fi = run.forward()
-    r = O.render_forward(_np(run.xys), _np(run.depths), _np(run.radii), _np(run.conics),
-                         _np(run.nth), _np(run.colors), _np(run.opac), run.H, run.W,
-                         _np(run.bg))
-    assert r["num_intersects"] == run.I > 0
-    np.testing.assert_array_equal(_np(run.gids), r["gaussian_ids_sorted"])
-    np.testing.assert_array_equal(_np(run.bins), r["tile_bins"])
-    frac, mx = close_frac(_np(img), r["img"])
+    """c2 (100k @ 512², SH degree 0: sigmoid colours, forward only -- bench.py renders it under
+    no_grad): the full image and alpha of the fused forward vs the oracle, zero outliers; the
+    second call (speculative binning) included."""
+    sc, cam = bench.make_workload("c2", 0, gpu)
+    cam = cam.to(gpu)
+    bg = torch.tensor([0.3, 0.2, 0.1], device=gpu)
+    with torch.no_grad():
+        for _ in range(2):
+            out = render_fused(sc, cam, 0, bg, return_alpha=True, clamp=False)
+    inp = {k: _np(v) for k, v in out["raster_inputs"].items()}
+    st = out["raster_state"]
+    r = O.render_forward(inp["xys"], inp["depths"], inp["radii"], inp["conics"],
+                         inp["num_tiles_hit"], inp["colors"], inp["opacity"], cam.height,
+                         cam.width, _np(bg))
+    assert r["num_intersects"] == out["num_intersects"] > 0
+    np.testing.assert_array_equal(_np(st["gaussian_ids_sorted"]), r["gaussian_ids_sorted"])
+    np.testing.assert_array_equal(_np(st["tile_bins"]), r["tile_bins"])
+    frac, mx = close_frac(_np(out["rgb"]), r["img"])
     assert frac == 0, (frac, mx)
-    assert_close("alpha", 1 - _np(fT), r["alpha"])
-    np.testing.assert_array_equal(_np(fi), r["final_idx"], err_msg="final_idx")
+    assert_close("alpha", 1 - _np(st["final_Ts"]), r["alpha"])
+    np.testing.assert_array_equal(_np(st["final_idx"]), r["final_idx"], err_msg="final_idx")
     # colours are sigmoid(features_dc) (gc_model.py:203)
-    np.testing.assert_array_equal(_np(run.colors), _np(torch.sigmoid(run.sc.features_dc)))
+    np.testing.assert_array_equal(inp["colors"], _np(torch.sigmoid(sc.features_dc)))

@@ -4,10 +4,12 @@
 Against the same step with the separate loss kernels (csrc/loss.hip, lambda = 0, clamp_pred):
 the backward forms each pixel's upstream gradient with exactly l1_only_bwd_kernel's arithmetic,
 so every parameter gradient -- and the parameters after the in-backward Adam step -- are
-bit-identical (deterministic accumulation); the loss value is the same sum in a different
-order (per-wave partials instead of grid-stride blocks, both finished in double): within
-1e-6 relative.  Frame sizes cover the strip backward (1080x720, 4,050 tiles), the 8x8-block
-list-split backward (512x384) and a ragged frame (333x201)."""
+bit-identical under deterministic accumulation, and within the atomic summation order's
+rounding with the shipped atomic records; the loss value is the same sum in a different order
+(per-wave partials instead of grid-stride blocks, both finished in double): within 1e-6
+relative.  Frame sizes cover the strip backward (1080x1080: 4,624 tiles, from 3,584 the
+shipped geometry, as at the headline), the 8x8-block backward without (1080x720: 3,060 tiles)
+and with the list split (512x384), and a ragged frame (333x201)."""
 import numpy as np
 import pytest
 import torch
@@ -32,15 +34,19 @@ def _step(gpu, sc, cam, gt, bg, fuse_l1, adam):
     return float(loss), [p.grad.detach().cpu().numpy() for p in s.params()]
 
 
-@pytest.mark.parametrize("W,H,n", [(1080, 720, 300_000), (512, 384, 60_000), (333, 201, 20_000)])
+@pytest.mark.parametrize("W,H,n", [(1080, 1080, 400_000), (1080, 720, 300_000),
+                                   (512, 384, 60_000), (333, 201, 20_000)])
 @pytest.mark.parametrize("adam", [False, True])
-def test_fused_l1_equals_loss_kernels(gpu, W, H, n, adam):
+@pytest.mark.parametrize("det", [True, False])
+def test_fused_l1_equals_loss_kernels(gpu, W, H, n, adam, det):
+    if adam and not det:
+        pytest.skip("the in-backward Adam is compared bit for bit (deterministic) only")
     sc = synthetic_scene(n, 3, seed=23, scale_lo=0.004, scale_hi=0.03)
     cam = synthetic_camera(W, H).to(gpu)
     gt = torch.rand(H, W, 3, generator=torch.Generator().manual_seed(6)).to(gpu)
     gt[: H // 4] = 1.5  # targets above the clamp: the clamp's gradient mask matters
     bg = torch.tensor([0.9, 1.2, 0.3], device=gpu)  # a background above 1 as well
-    prev = _lib.set_deterministic(True)
+    prev = _lib.set_deterministic(det)
     try:
         l_ref, ref = _step(gpu, sc, cam, gt, bg, False, adam)
         l_got, got = _step(gpu, sc, cam, gt, bg, True, adam)
@@ -50,7 +56,11 @@ def test_fused_l1_equals_loss_kernels(gpu, W, H, n, adam):
     for name, x, y in zip(("means", "scales", "quats", "opacities", "dc", "rest"), got, ref):
         if not adam:
             assert np.abs(y).max() > 0, name
-        np.testing.assert_array_equal(x, y, err_msg=name)
+        if det:
+            np.testing.assert_array_equal(x, y, err_msg=name)
+        else:  # atomic records: the same terms summed in another order
+            np.testing.assert_allclose(x, y, rtol=1e-4, atol=1e-5 * np.abs(y).max(),
+                                       err_msg=name)
 
 
 def test_fused_l1_loss_value(gpu):
