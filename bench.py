@@ -195,19 +195,36 @@ def _pmc_kernels(config):
         return None
 
 
+def _entry_kernel_rows(entry, config):
+    """The PMC rows of an entry's kernels on `config`: per kernel pattern of ENTRY_KERNELS, the
+    most-dispatched instantiation matching it (the one the timed step launches; the bench's
+    other legs -- deterministic, unchanged-caller, warm-up variants -- run other instantiations
+    far fewer times), keyed by the full instantiation name (tools/kname.py).  [] without that
+    config's counters."""
+    kern = _pmc_kernels(config)
+    pats, _ = ENTRY_KERNELS.get(entry, ((), False))
+    if not kern or not pats:
+        return []
+    out = []
+    for p in pats:
+        cand = [(v.get("dispatches") or 0.0, name) for name, v in kern.items() if p in name]
+        if cand:
+            name = max(cand)[1]
+            if all(name != n for n, _ in out):
+                out.append((name, kern[name]))
+    return out
+
+
 def pmc_traffic(entry, config):
     """HBM bytes per call of a C-ABI entry on `config`: FETCH_SIZE (x2 only for streaming
     16-B-per-lane kernels, see ENTRY_KERNELS) + WRITE_SIZE; None without counters."""
     e = _pmc_entry(entry, config)
     if e and e.get("fetch_kb") is not None:  # binning entries: raw FETCH_SIZE (gathers)
         return int((e["fetch_kb"] + (e.get("write_kb") or 0.0)) * 1024.0)
-    kern = _pmc_kernels(config)
-    pats, streaming = ENTRY_KERNELS.get(entry, ((), False))
-    if not kern or not pats:
-        return None
+    _, streaming = ENTRY_KERNELS.get(entry, ((), False))
     tot, hit = 0.0, False
-    for name, v in kern.items():
-        if any(p in name for p in pats) and v.get("fetch_kb") is not None:
+    for name, v in _entry_kernel_rows(entry, config):
+        if v.get("fetch_kb") is not None:
             tot += ((2.0 if streaming else 1.0) * v["fetch_kb"] + (v.get("write_kb") or 0.0)) \
                 * 1024.0
             hit = True
@@ -223,13 +240,11 @@ def pmc_valu_busy(entry, config, ms_per_call, n_simd=256 * 4, clock_hz=2.4e9):
     e = _pmc_entry(entry, config)
     if e and e.get("valu_quad_cycles") is not None and ms_per_call:
         return round(e["valu_quad_cycles"] / (n_simd * ms_per_call * 1e-3 * clock_hz / 4.0), 3)
-    kern = _pmc_kernels(config)
-    pats, _ = ENTRY_KERNELS.get(entry, ((), False))
-    if not kern or not pats or not ms_per_call:
+    if not ms_per_call:
         return None
     tot, hit = 0.0, False
-    for name, v in kern.items():
-        if any(p in name for p in pats) and v.get("valu_quad_cycles") is not None:
+    for name, v in _entry_kernel_rows(entry, config):
+        if v.get("valu_quad_cycles") is not None:
             tot += v["valu_quad_cycles"]
             hit = True
     return round(tot / (n_simd * ms_per_call * 1e-3 * clock_hz / 4.0), 3) if hit else None
@@ -248,12 +263,7 @@ def pmc_issue_and_wait(entry, config, ms_per_call, n_simd=256 * 4, clock_hz=2.4e
     if e and e.get("insts_valu") is not None:
         rows = [e]
     else:
-        kern = _pmc_kernels(config)
-        pats, _ = ENTRY_KERNELS.get(entry, ((), False))
-        if not kern or not pats:
-            return None, None, None
-        rows = [v for name, v in kern.items()
-                if any(p in name for p in pats) and v.get("insts_valu") is not None]
+        rows = [v for _, v in _entry_kernel_rows(entry, config) if v.get("insts_valu") is not None]
     if not rows or not ms_per_call:
         return None, None, None
     iv = sum(v["insts_valu"] for v in rows)
@@ -268,14 +278,11 @@ def pmc_issue_and_wait(entry, config, ms_per_call, n_simd=256 * 4, clock_hz=2.4e
 
 
 def pmc_insts_valu(entry, config):
-    """SQ_INSTS_VALU (wave64 VALU instructions) per call of the entry's kernels on `config`, or
-    None without that config's counters."""
-    kern = _pmc_kernels(config)
-    pats, _ = ENTRY_KERNELS.get(entry, ((), False))
-    if not kern or not pats:
-        return None
-    vals = [v["insts_valu"] for name, v in kern.items()
-            if any(p in name for p in pats) and v.get("insts_valu") is not None]
+    """SQ_INSTS_VALU (wave64 VALU instructions) per call of the entry's kernels on `config` -- the
+    instantiations the timed step ran (_entry_kernel_rows) -- or None without that config's
+    counters."""
+    vals = [v["insts_valu"] for _, v in _entry_kernel_rows(entry, config)
+            if v.get("insts_valu") is not None]
     return sum(vals) if vals else None
 
 

@@ -9,22 +9,25 @@ import collections
 import csv
 import glob
 import os
-import re
 import sys
+
+from kname import short_name
 
 root = sys.argv[1]
 acc = collections.defaultdict(lambda: collections.defaultdict(list))
+# dispatches of each instantiation per pass (file): the bench picks the most-dispatched
+# instantiation of an entry's kernel -- the one its timed step ran -- for per-step figures
+ndisp = collections.defaultdict(lambda: collections.defaultdict(set))
 cfg_arg = sys.argv[4] if len(sys.argv) > 4 else "headline"
 files = glob.glob(os.path.join(root, "pmc", cfg_arg + "_*", "**", "*counter_collection.csv"),
                   recursive=True)
 for f in files:
     for r in csv.DictReader(open(f)):
-        name = r["Kernel_Name"].replace("(anonymous namespace)::", "")
-        if name.startswith("void gs::") or name.startswith("gs::"):
-            name = re.sub(r"\(.*$", "", name)
-        else:
+        name = short_name(r["Kernel_Name"])
+        if not name.startswith(("void gs::", "gs::")):
             continue
         acc[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        ndisp[name][f].add(r.get("Dispatch_Id"))
 # Per C-ABI entry of the binning, whose kernels (radix passes, scans) are shared between the
 # depth sort (gsplat_bin_count_keyed) and the tile sort (gsplat_bin_emit): segment each pass's
 # dispatch sequence -- a fused forward kernel starts a step's binning, the emission's first
@@ -87,11 +90,11 @@ for e, d in entries.items():
     entry_rows[e] = {c: sum(v) / len(v) for c, v in per.items()}
 rows = []
 for k, d in sorted(acc.items()):
-    row = {"kernel": k}
+    row = {"kernel": k, "dispatches": sum(len(v) for v in ndisp[k].values()) / max(len(ndisp[k]), 1)}
     for c, v in sorted(d.items()):
         row[c] = sum(v) / len(v)
     rows.append(row)
-cols = sorted({c for r in rows for c in r if c != "kernel"})
+cols = sorted({c for r in rows for c in r if c not in ("kernel", "dispatches")})
 if len(sys.argv) > 3:
     def pick(r):
         return {"fetch_kb": r.get("FETCH_SIZE"), "write_kb": r.get("WRITE_SIZE"),
@@ -100,7 +103,8 @@ if len(sys.argv) > 3:
                 "insts_trans": r.get("SQ_INSTS_VALU_TRANS_F32"),
                 "wait_any": r.get("SQ_WAIT_ANY"),
                 "wait_inst_any": r.get("SQ_WAIT_INST_ANY"),
-                "wave_cycles": r.get("SQ_WAVE_CYCLES")}
+                "wave_cycles": r.get("SQ_WAVE_CYCLES"),
+                "dispatches": r.get("dispatches")}
     tj = {r["kernel"]: pick(r) for r in rows if "FETCH_SIZE" in r and "WRITE_SIZE" in r}
     ej = {e: pick(r) for e, r in entry_rows.items() if "FETCH_SIZE" in r and "WRITE_SIZE" in r}
     cfg = cfg_arg
@@ -116,6 +120,6 @@ if len(sys.argv) > 3:
         json.dump(doc, f, indent=1)
 out = sys.argv[2] if len(sys.argv) > 2 else None
 w = csv.writer(open(out, "w", newline="") if out else sys.stdout)
-w.writerow(["kernel"] + cols)
+w.writerow(["kernel", "dispatches"] + cols)
 for r in rows:
-    w.writerow([r["kernel"]] + [f"{r.get(c, float('nan')):.4g}" for c in cols])
+    w.writerow([r["kernel"], f"{r['dispatches']:.0f}"] + [f"{r.get(c, float('nan')):.4g}" for c in cols])

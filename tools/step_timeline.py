@@ -3,9 +3,10 @@ steps at each launch of MARK (default: the fused forward kernel), and for the fi
 steps it prints the step span, the summed kernel time, the idle time, and the largest gaps
 between consecutive kernels (with the kernels on either side) -- where the GPU waits for the
 host.  Usage: step_timeline.py run_results.db [MARK] [STEPS]"""
-import re
 import sqlite3
 import sys
+
+from kname import short_name
 
 db = sqlite3.connect(sys.argv[1])
 mark = sys.argv[2] if len(sys.argv) > 2 else "fused_fwd_kernel"
@@ -14,9 +15,7 @@ rows = db.execute("select name, start, end from kernels order by start").fetchal
 
 
 def short(n):
-    n = n.replace("(anonymous namespace)::", "")
-    n = re.sub(r"\(.*$", "", n) if n.startswith(("void gs::", "gs::")) else n
-    return n[:70]
+    return short_name(n)[:90]
 
 
 cuts = [i for i, r in enumerate(rows) if mark in r[0]]
