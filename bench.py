@@ -74,7 +74,7 @@ def make_workload(config: str, rank: int, dev):
         return synthetic_scene(N, deg, seed=seed, scale_lo=lo, scale_hi=hi, device=dev), \
             view_camera(W, H, rank)
     import numpy as np
-    from gaussctrl_exp_amd.formats import load_transforms, rescale_cameras, transform_points
+    from gaussctrl_exp_amd.formats import load_transforms, transform_points
     from gaussctrl_exp_amd.scene import scene_from_points
     golden = os.path.join(ROOT, "tests", "golden")
     d = load_transforms(os.path.join(golden, f"{real}_transforms.json"))
@@ -82,10 +82,21 @@ def make_workload(config: str, rank: int, dev):
     pts = transform_points(torch.from_numpy(pc["xyz"]), d.transform_matrix, d.points_scale)
     scene = scene_from_points(pts, torch.from_numpy(pc["rgb"]), N, deg, seed=seed,
                               scale_lo=lo, scale_hi=hi, device=dev)
-    cam = d.cameras[rank % len(d.cameras)]
+    return scene, config_camera(config, rank)
+
+
+def config_camera(config: str, index: int):
+    """Camera `index` of `config`: the synthetic orbit's view, or the real scene's own camera
+    (dataparser coordinates, rescaled to the config's width)."""
+    N, W, H, deg, lo, hi, seed, real, _ = CONFIGS[config]
+    if real is None:
+        return view_camera(W, H, index)
+    from gaussctrl_exp_amd.formats import load_transforms, rescale_cameras
+    d = load_transforms(os.path.join(ROOT, "tests", "golden", f"{real}_transforms.json"))
+    cam = d.cameras[index % len(d.cameras)]
     if cam.width != W:
         cam = rescale_cameras([cam], W / cam.width)[0]
-    return scene, cam
+    return cam
 
 
 def view_camera(W, H, view: int):
@@ -471,7 +482,7 @@ def rotating_cameras(config, rank, dev, step, timed, steps, world):
                       f"random draws from the {CONFIGS[config][7]} training cameras"))}
 
 
-def exchange_profile(scene, cam, gt, bg, deg, world, dev, steps, timed):
+def exchange_profile(scene, cam, gt, bg, deg, world, dev, steps, timed, record_floats=None):
     """N > 1 only: what the data-parallel exchange costs this rank and how much of it the step
     hides.  Times (max over ranks, same `steps`): the step's compute alone (the
     same render + loss + backward on a world-size-1 TrainStep: no collectives), the SH record
@@ -487,8 +498,9 @@ def exchange_profile(scene, cam, gt, bg, deg, world, dev, steps, timed):
     for _ in range(3):
         compute_only()
     t_comp = timed(compute_only, steps) / steps * 1e3
-    rec = torch.zeros(3 * n + 4, device=dev)
-    gathered = torch.empty(world * (3 * n + 4), device=dev)
+    rlen = record_floats or 3 * n + 4  # the record the step sent (sparse or dense)
+    rec = torch.zeros(rlen, device=dev)
+    gathered = torch.empty(world * rlen, device=dev)
     flat = torch.zeros(11 * n, device=dev)  # means 3 + scales 3 + quats 4 + opacity 1 floats
     for _ in range(3):
         dist.all_gather_into_tensor(gathered, rec)
@@ -501,7 +513,8 @@ def exchange_profile(scene, cam, gt, bg, deg, world, dev, steps, timed):
         "t_compute_only_ms": round(t_comp, 4),
         "t_allgather_ms": round(t_ag, 4),
         "t_allreduce_ms": round(t_ar, 4),
-        "bytes_allgather_recv_per_rank": (world - 1) * (3 * n + 4) * 4,
+        "record": "dense" if rlen == 3 * n + 4 else "sparse",
+        "bytes_allgather_recv_per_rank": (world - 1) * rlen * 4,
         "bytes_allreduce_per_rank": int(2 * (world - 1) / world * 11 * n * 4),  # ring send+recv
         "collectives_per_step": 2,
     }
@@ -520,6 +533,10 @@ def main():
                          "kernels out of the PMC and kernel-trace summaries)")
     ap.add_argument("--forward-only", action="store_true",
                     help="time the render without backward (default for config c2)")
+    ap.add_argument("--views-per-gpu", type=int, default=1,
+                    help="views each rank renders per step (gradients summed over all; N > 1: "
+                         "the record all-gathers of a rank's earlier views overlap its later "
+                         "views, exchange.py)")
     ap.add_argument("--render", default="fused", choices=("fused", "caller"),
                     help="fused: the caller's activations inside the HIP kernels (default); "
                          "caller: gc_model.py's torch glue around the gsplat API")
@@ -555,8 +572,21 @@ def main():
 
     fwd_only = args.forward_only or args.config in FORWARD_ONLY
 
+    V = max(args.views_per_gpu, 1)
+    # several views per rank: rank r renders views r, r + N, r + 2N, ... of the config's set
+    extra = [config_camera(args.config, rank + k * world).to(dev) for k in range(1, V)]
+    gts = [gt] + [torch.rand(H, W, 3, generator=g).to(dev) for _ in range(1, V)]
+
+    def step_views(t, cams):
+        t.zero_grad()
+        t.forward_backward_views(cams, gts[:len(cams)], bg)
+        t.sync_grads()
+
     def step_eager(t=trainer, c=None):
         c = cam if c is None else c
+        if V > 1 and not fwd_only and t.render_mode == "fused":
+            step_views(t, [c] + extra)
+            return
         if fwd_only:
             with torch.no_grad():
                 if t.render_mode == "fused":
@@ -601,11 +631,28 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     ms_per_step = dt / args.steps * 1e3
-    value = world * H * W * args.steps / dt / 1e6
-    rotating = rotating_cameras(args.config, rank, dev, step_eager, timed, args.steps, world)
+    value = world * V * H * W * args.steps / dt / 1e6
+    value_2v = None
+    if world > 1 and V == 1 and not fwd_only and args.render == "fused":
+        # the same job with two views per rank per step (exchange.py: the first view's record
+        # all-gather overlaps the second view's render): the step's per-view throughput
+        cams2 = [cam, config_camera(args.config, rank + world).to(dev)]
+        gts2 = [gt, torch.rand(H, W, 3, generator=torch.Generator().manual_seed(77 + rank)).to(dev)]
+
+        def two():
+            trainer.zero_grad()
+            trainer.forward_backward_views(cams2, gts2, bg)
+            trainer.sync_grads()
+        for _ in range(3):
+            two()
+        value_2v = round(world * 2 * H * W * args.steps / timed(two, args.steps) / 1e6, 2)
+    rotating = rotating_cameras(args.config, rank, dev, step_eager, timed, args.steps,
+                                world * V)
     exch = None
     if world > 1 and not fwd_only:
-        exch = exchange_profile(scene, cam, gt, bg, deg, world, dev, args.steps, timed)
+        xc = trainer.sh_exchange
+        exch = exchange_profile(scene, cam, gt, bg, deg, world, dev, args.steps, timed,
+                                xc.last_record_floats if xc is not None else None)
         comm = exch["t_allgather_ms"] + exch["t_allreduce_ms"]
         exch["t_step_ms"] = round(ms_per_step, 4)
         exch["exposed_ms"] = round(ms_per_step - exch["t_compute_only_ms"], 4)
@@ -741,14 +788,16 @@ def main():
                 "tiles": T,
                 "image": [H, W],
                 "sh_degree": deg,
-                "views_per_gpu_per_step": 1,
-                "parallelism": f"dp{world} (1 view/GPU; SH-coefficient grads by RCCL all-gather "
-                               f"of {N * 12 + 16} B/rank + multi-view SH backward, other "
-                               f"{N * 11 * 4} B of grads RCCL all-reduced)" if world > 1
+                "views_per_gpu_per_step": V,
+                "parallelism": f"dp{world} ({V} view/GPU; SH-coefficient grads by RCCL "
+                               f"all-gather of each view's colour-gradient record (sparse: "
+                               f"visible Gaussians only, when smaller) + multi-view SH backward, "
+                               f"other {N * 11 * 4} B of grads RCCL all-reduced)" if world > 1
                                else "dp1",
             },
             "render": args.render,
             "exchange": exch,
+            "value_2_views_per_gpu": value_2v,
             "value_rotating_cameras": rotating["value"],
             "speculative_misses": rotating["misses"],
             "rotating_cameras": rotating["desc"],

@@ -95,6 +95,12 @@ SIGNATURES = {
     "gsplat_fused_preprocess_backward_adam": (_I, [_I, _I, _I] + [_P] * 9 + [_F] * 4 +
                                               [_I, _I] + [_P] * 8 + [_I, _F, _F, _F, _P]),
     "gsplat_exchange_pack_colors": (_I, [_I, _P, _SZ, _P, _P, _P, _P, _P]),
+    "gsplat_exchange_sparse_floats": (_I64, [_I, _I64]),
+    "gsplat_exchange_sparse_plan": (_I, [_I, _P, _P, _P]),
+    "gsplat_exchange_pack_sparse": (_I, [_I, _P, _SZ, _P, _P, _P, _P, _I64, _P]),
+    "gsplat_fused_preprocess_backward_accumulate": (_I, [_I, _I, _I] + [_P] * 6 + [_F] * 4 +
+                                                    [_I, _I] + [_P] * 11),
+    "gsplat_compute_sh_backward_view_table": (_I, [_I, _I, _I, _I, _P, _P, _P, _P, _P, _P]),
     "gsplat_grad_records_bytes": (_SZ, [_I]),
     "gsplat_grad_records_split": (_I, [_I, _P, _SZ, _P, _P, _P, _P, _P, _P, _P]),
     "gsplat_rasterize_backward_records": (_I, [_I] * 5 + [_P] * 11 + [_F, _I64, _I, _P, _SZ,
@@ -107,7 +113,7 @@ SIGNATURES = {
                                              [_F, _I64, _I, _P, _SZ, _I, _P, _SZ, _P]),
 }
 
-ABI_VERSION = 14  # include/gsplat_mi355x.h GSPLAT_MI355X_ABI_VERSION
+ABI_VERSION = 15  # include/gsplat_mi355x.h GSPLAT_MI355X_ABI_VERSION
 
 _lib = None
 _DETERMINISTIC = os.environ.get("GSPLAT_MI355X_DETERMINISTIC", "0") not in ("", "0")

@@ -25,6 +25,7 @@
 #include "adam_math.h"
 #include "project_math.h"
 #include "sh_math.h"
+#include "exchange_layout.h"
 
 namespace gs {
 namespace {
@@ -64,6 +65,7 @@ struct FusedBwdArgs {
   const float *conics, *colors, *opacity, *records;
   float *v_means, *v_log_scales, *v_quats, *v_opacity_logits, *v_dc, *v_rest;
   float *v_colors;  // non-NULL: write the SH-output gradient here instead of v_dc / v_rest
+  int accumulate;   // add the four geometry gradients to the outputs' values (v_colors mode)
 };
 
 // Adam fused into the backward (single-GPU training step): the six parameter tensors are
@@ -418,6 +420,15 @@ __global__ __launch_bounds__(sh_threads(K)) void fused_bwd_kernel(FusedBwdArgs a
       upd(3, g, vlogit);
       upd3(4, vdc);
     } else {
+      if (a.accumulate) {  // a further view of this rank's step (exchange multi-view mode)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) vmean[k] += a.v_means[3 * g + k];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) vls[k] += a.v_log_scales[3 * g + k];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) vq[k] += a.v_quats[4 * g + k];
+        vlogit += a.v_opacity_logits[g];
+      }
 #pragma unroll
       for (int k = 0; k < 3; ++k) a.v_means[3 * g + k] = vmean[k];
 #pragma unroll
@@ -629,14 +640,14 @@ extern "C" int gsplat_fused_preprocess_forward_part(
                             bin_workspace_bytes, stream, part);
 }
 
-extern "C" int gsplat_fused_preprocess_backward(
+static int fused_backward_impl(
     int num_points, int sh_bases, int degrees_to_use, const float *means3d,
     const float *log_scales, const float *quats, const float *viewmat, const float *projmat,
     const float *campos, float fx, float fy, float cx, float cy, int img_height, int img_width,
     const int32_t *radii, const float *conics, const float *colors, const float *opacity,
     const void *grad_records, float *v_means3d, float *v_log_scales, float *v_quats,
     float *v_opacity_logits, float *v_features_dc, float *v_features_rest, float *v_colors,
-    void *stream) {
+    int accumulate, void *stream) {
   const int K = sh_bases;
   if (num_points < 0 || !valid_bases(K) || degrees_to_use < 0 || degrees_to_use > degree_of(K) ||
       img_height <= 0 || img_width <= 0 ||
@@ -651,7 +662,7 @@ extern "C" int gsplat_fused_preprocess_backward(
   FusedBwdArgs args{num_points, degrees_to_use, means3d, log_scales, quats, viewmat, projmat,
                     campos, radii, conics, colors, opacity, (const float *)grad_records,
                     v_means3d, v_log_scales, v_quats, v_opacity_logits, v_features_dc,
-                    v_features_rest, K > 1 ? v_colors : nullptr};
+                    v_features_rest, K > 1 ? v_colors : nullptr, accumulate};
   const ProjParams pp = make_proj_params(fx, fy, cx, cy, 1.f, 0.f, img_height, img_width, 1, 1);
   const int thr = sh_threads(K);
   const dim3 grid(cdiv(num_points, thr));
@@ -660,6 +671,41 @@ extern "C" int gsplat_fused_preprocess_backward(
   hipStream_t st = (hipStream_t)stream;
   FUSED_DISPATCH(fused_bwd_kernel, args);
   return check_launch("fused_preprocess_backward");
+}
+
+extern "C" int gsplat_fused_preprocess_backward(
+    int num_points, int sh_bases, int degrees_to_use, const float *means3d,
+    const float *log_scales, const float *quats, const float *viewmat, const float *projmat,
+    const float *campos, float fx, float fy, float cx, float cy, int img_height, int img_width,
+    const int32_t *radii, const float *conics, const float *colors, const float *opacity,
+    const void *grad_records, float *v_means3d, float *v_log_scales, float *v_quats,
+    float *v_opacity_logits, float *v_features_dc, float *v_features_rest, float *v_colors,
+    void *stream) {
+  return fused_backward_impl(num_points, sh_bases, degrees_to_use, means3d, log_scales, quats,
+                             viewmat, projmat, campos, fx, fy, cx, cy, img_height, img_width,
+                             radii, conics, colors, opacity, grad_records, v_means3d,
+                             v_log_scales, v_quats, v_opacity_logits, v_features_dc,
+                             v_features_rest, v_colors, 0, stream);
+}
+
+extern "C" int gsplat_fused_preprocess_backward_accumulate(
+    int num_points, int sh_bases, int degrees_to_use, const float *means3d,
+    const float *log_scales, const float *quats, const float *viewmat, const float *projmat,
+    const float *campos, float fx, float fy, float cx, float cy, int img_height, int img_width,
+    const int32_t *radii, const float *conics, const float *colors, const float *opacity,
+    const void *grad_records, float *v_means3d, float *v_log_scales, float *v_quats,
+    float *v_opacity_logits, float *v_colors, void *stream) {
+  if (sh_bases <= 1 || (num_points > 0 && (!v_colors || !v_means3d || !v_log_scales ||
+                                           !v_quats || !v_opacity_logits))) {
+    set_error("fused_preprocess_backward_accumulate: needs sh_bases > 1 and v_colors (the view "
+              "exchange), N=%d sh_bases=%d", num_points, sh_bases);
+    return 1;
+  }
+  return fused_backward_impl(num_points, sh_bases, degrees_to_use, means3d, log_scales, quats,
+                             viewmat, projmat, campos, fx, fy, cx, cy, img_height, img_width,
+                             radii, conics, colors, opacity, grad_records, v_means3d,
+                             v_log_scales, v_quats, v_opacity_logits, nullptr, nullptr, v_colors,
+                             1, stream);
 }
 
 // The data-parallel view exchange's record (exchange.ShViewExchange), straight from the raster
@@ -702,6 +748,132 @@ extern "C" int gsplat_exchange_pack_colors(int num_points, const void *grad_reco
                      (hipStream_t)stream, num_points, (const float *)grad_records, radii, colors,
                      campos, send);
   return check_launch("exchange_pack_colors");
+}
+
+// The sparse view record (exchange_layout.h), for views that see a fraction of the scene
+// (c4 garden: 55 % visible): the masks, their prefix and the count depend only on radii, so
+// gsplat_exchange_sparse_plan runs in the forward and the count's all-gather (the ranks
+// agree on the capacity) completes long before the backward packs the values.
+// xs_mask_kernel: one wave per 64 Gaussians -- the ballot is the mask word, its popcount goes
+// to the prefix slot (scanned in place by xs_scan_kernel).
+__global__ __launch_bounds__(256) void xs_mask_kernel(int n, const int *__restrict__ radii,
+                                                      float *__restrict__ send) {
+  const long long W = xs_words(n);
+  const long long w = ((long long)blockIdx.x * 256 + threadIdx.x) >> 6;
+  if (w >= W) return;  // (uniform per wave)
+  const long long g = (long long)blockIdx.x * 256 + threadIdx.x;
+  const unsigned long long m = __ballot(g < n && radii[g] > 0);
+  if ((threadIdx.x & 63) == 0) {
+    reinterpret_cast<unsigned long long *>(send + XS_HDR)[w] = m;
+    reinterpret_cast<uint32_t *>(send + XS_HDR + 2 * W)[w] = (uint32_t)__popcll(m);
+  }
+}
+
+__device__ __forceinline__ uint32_t xs_wave_incl_scan(uint32_t v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t o = __shfl_up(v, d, 64);
+    if (lane >= d) v += o;
+  }
+  return v;
+}
+
+// One workgroup: the exclusive scan of the W per-word counts, 16 consecutive words per thread
+// per round (W = 31,250 at 2M Gaussians: two rounds), and the total into the header.
+__global__ __launch_bounds__(1024) void xs_scan_kernel(long long W, float *__restrict__ send) {
+  constexpr int PER = 16;
+  uint32_t *c = reinterpret_cast<uint32_t *>(send + XS_HDR + 2 * W);
+  __shared__ uint32_t wsum[16];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  uint32_t carry = 0;
+  for (long long base = 0; base < W; base += 1024LL * PER) {
+    const long long s0 = base + (long long)threadIdx.x * PER;
+    uint32_t v[PER], tot = 0;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      v[k] = s0 + k < W ? c[s0 + k] : 0u;
+      tot += v[k];
+    }
+    const uint32_t inc = xs_wave_incl_scan(tot);
+    if (lane == 63) wsum[wv] = inc;
+    __syncthreads();
+    uint32_t before = 0, all = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const uint32_t x = wsum[j];
+      before += j < wv ? x : 0u;
+      all += x;
+    }
+    __syncthreads();  // wsum is rewritten next round
+    uint32_t run = carry + before + inc - tot;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      if (s0 + k < W) c[s0 + k] = run;
+      run += v[k];
+    }
+    carry += all;
+  }
+  if (threadIdx.x == 0) reinterpret_cast<uint32_t *>(send)[3] = carry;
+}
+
+// The values: each visible Gaussian's colour gradient (as exchange_pack_kernel computes it) at
+// its row; the camera centre into the header.
+__global__ __launch_bounds__(256) void xs_pack_kernel(int n, const float *__restrict__ rec,
+                                                      const int *__restrict__ radii,
+                                                      const float *__restrict__ colors,
+                                                      const float *__restrict__ campos,
+                                                      float *__restrict__ send, long long cap) {
+  const long long g = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (blockIdx.x == 0 && threadIdx.x < 3) send[threadIdx.x] = campos[threadIdx.x];
+  if (g >= n || radii[g] <= 0) return;
+  const long long W = xs_words(n);
+  const unsigned long long m = reinterpret_cast<const unsigned long long *>(send + XS_HDR)[g >> 6];
+  const long long pos = (long long)reinterpret_cast<const uint32_t *>(send + XS_HDR + 2 * W)[g >> 6] +
+                        __popcll(m & ((1ull << (g & 63)) - 1ull));
+  if (pos >= cap) return;
+  const float4 r1 = reinterpret_cast<const float4 *>(rec + g * RECF)[1];
+  const float rgb[3] = {r1.y, r1.z, r1.w};
+  float *vals = send + xs_values_at(n);
+#pragma unroll
+  for (int c = 0; c < 3; ++c) vals[3 * pos + c] = clamp0_passes(colors[3 * g + c]) ? rgb[c] : 0.f;
+}
+
+extern "C" long long gsplat_exchange_sparse_floats(int num_points, long long capacity) {
+  if (num_points < 0 || capacity < 0 || capacity > num_points) return -1;
+  return xs_values_at(num_points) + 3 * capacity;
+}
+
+extern "C" int gsplat_exchange_sparse_plan(int num_points, const int32_t *radii, float *send,
+                                           void *stream) {
+  if (num_points < 0 || !send || (num_points > 0 && !radii)) {
+    set_error("exchange_sparse_plan: bad args (N=%d)", num_points);
+    return 1;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  const long long W = xs_words(num_points);
+  if (W > 0)
+    hipLaunchKernelGGL(xs_mask_kernel, dim3((unsigned)cdiv(W * 64, 256)), dim3(256), 0, st,
+                       num_points, radii, send);
+  hipLaunchKernelGGL(xs_scan_kernel, dim3(1), dim3(1024), 0, st, W, send);
+  return check_launch("exchange_sparse_plan");
+}
+
+extern "C" int gsplat_exchange_pack_sparse(int num_points, const void *grad_records,
+                                           size_t records_bytes, const int32_t *radii,
+                                           const float *colors, const float *campos,
+                                           float *send, long long capacity, void *stream) {
+  if (num_points < 0 || (size_t)num_points * RECF * sizeof(float) > records_bytes ||
+      !campos || !send || capacity < 0 || capacity > num_points ||
+      (num_points > 0 && (!grad_records || !radii || !colors))) {
+    set_error("exchange_pack_sparse: bad args (N=%d records %zu bytes capacity %lld)",
+              num_points, records_bytes, capacity);
+    return 1;
+  }
+  hipLaunchKernelGGL(xs_pack_kernel, dim3(cdiv(num_points + 3, 256)), dim3(256), 0,
+                     (hipStream_t)stream, num_points, (const float *)grad_records, radii, colors,
+                     campos, send, capacity);
+  return check_launch("exchange_pack_sparse");
 }
 
 extern "C" int gsplat_fused_preprocess_backward_adam(

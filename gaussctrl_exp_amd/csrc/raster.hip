@@ -593,21 +593,38 @@ struct WaveRect {
   float rx0, rx1, ry0, ry1;
 };
 // Debug hook (gsplat_debug_wave_log): when set, the backward blend kernels record per wave
-// {start, end (s_memrealtime, 100 MHz), HW_ID, XCC_ID, work slot} into [waves][5] u64.
+// {start, end (s_memrealtime, 100 MHz), HW_ID, XCC_ID, work slot} into [waves][WAVE_LOG_F] u64.
+// Attribution build (-DGS_BWD_ATTR, tools/bwd_attr.sh; never the shipped library): the strip
+// backward also sums s_memtime cycles per wave -- [5] its blend rounds, [6] their reduce9 +
+// record-atomic tails, [7] the walk before its first round, [8] rounds << 32 | iterations,
+// [9] tail iterations, [10] its whole life -- so a wave's time splits into staging (life - blend
+// - prologue), blend math (blend - tail) and tail; the end times give the launch's imbalance.
+#ifdef GS_BWD_ATTR
+#define GS_ATTR 1
+#define WAVE_LOG_F 11
+#else
+#define GS_ATTR 0
+#define WAVE_LOG_F 5
+#endif
 __device__ unsigned long long *g_wave_log = nullptr;
 struct WaveLog {
   unsigned long long t0;
   __device__ __forceinline__ WaveLog() : t0(__builtin_amdgcn_s_memrealtime()) {}
-  __device__ __forceinline__ void done(int slot) const {
+  __device__ __forceinline__ void done(int slot, const unsigned long long *attr = nullptr) const {
     unsigned long long *log = g_wave_log;
+    if (GS_ATTR && !attr) return;  // (attribution build: only the strip backward logs)
     if (log && (threadIdx.x & 63) == 0) {
       const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
       const int w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-      log[5 * w + 0] = t0;
-      log[5 * w + 1] = t1;
-      log[5 * w + 2] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
-      log[5 * w + 3] = (unsigned)__builtin_amdgcn_s_getreg((15 << 11) | 20);  // XCC_ID
-      log[5 * w + 4] = (unsigned)slot;
+      unsigned long long *e = log + (size_t)WAVE_LOG_F * w;
+      e[0] = t0;
+      e[1] = t1;
+      e[2] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+      e[3] = (unsigned)__builtin_amdgcn_s_getreg((15 << 11) | 20);  // XCC_ID
+      e[4] = (unsigned)slot;
+#if GS_ATTR
+      for (int k = 0; k < 6; ++k) e[5 + k] = attr ? attr[k] : 0ull;
+#endif
     }
   }
 };
@@ -979,6 +996,7 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
     part = it.y;
   }
   const WaveLog wlog;
+  const unsigned long long at_t0 = GS_ATTR ? __builtin_amdgcn_s_memtime() : 0ull;
   const WaveRect R = wave_rect<PXL, COLS>(tbx, tby, H, W, ctile);
   if (!R.live) return;  // wave-uniform
   __shared__ GStage lds[4][64];
@@ -1078,8 +1096,17 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
   }
   const int last = min(maxbin, hi - 1);
   unsigned c_slots = 0, c_live = 0, c_valid = 0;  // (CNT only)
+  // (GS_ATTR: [0] blend, [1] tail, [2] prologue cycles, [3] rounds << 32 | iterations,
+  //  [4] tail iterations, [5] life; cycles by s_memtime)
+  unsigned long long at[6] = {0ull, 0ull, 0ull, 0ull, 0ull, 0ull};
   auto main_blend = [&](int n) {
     constexpr int U = 1;  // (two per iteration measured slower: register pressure)
+    unsigned long long at_b0 = 0;
+    if constexpr (GS_ATTR) {
+      at_b0 = __builtin_amdgcn_s_memtime();
+      if (at[3] == 0) at[2] = at_b0 - at_t0;  // (the prologue: kernel start to first round)
+      at[3] += (1ull << 32) + (unsigned long long)n;
+    }
     for (int t = 0; t < n; t += U) {
       float parts[U][9];
       bool anyv[U];
@@ -1158,6 +1185,8 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
 #pragma unroll
       for (int u = 0; u < U; ++u) any_all |= anyw[u];
       if (any_all) {  // (an SGPR test, no VGPR round trip)
+        unsigned long long at_t = 0;
+        if constexpr (GS_ATTR) at_t = __builtin_amdgcn_s_memtime();
         float v[U];
 #ifdef GS_ABLATE_NO_REDUCE  // attribution build (tools/attr_bwd.sh): a lane-local sum instead
 #pragma unroll
@@ -1185,8 +1214,13 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
             asm volatile("" ::"v"(v[u]));
           }
         }
+        if constexpr (GS_ATTR) {
+          at[1] += __builtin_amdgcn_s_memtime() - at_t;
+          at[4] += 1;
+        }
       }
     }
+    if constexpr (GS_ATTR) at[0] += __builtin_amdgcn_s_memtime() - at_b0;
   };
   if constexpr (KB) {
     walk_kept(S, last, lo, stage, ahead, gids, stage1, main_blend);
@@ -1205,7 +1239,11 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
     }
   }
   if constexpr (CNT) pair_count_flush(0, c_slots, c_live, c_valid);
-  wlog.done(tile);
+  if constexpr (GS_ATTR) {
+    at[5] = __builtin_amdgcn_s_memtime() - at_t0;
+    if (at[3] == 0) at[2] = at[5];
+  }
+  wlog.done(tile, GS_ATTR ? at : nullptr);
 }
 
 // ---------------------------------------------------------------- block backward (shipped)

@@ -8,6 +8,7 @@
 // LDS with 16-byte, fully coalesced loads (forward) / stores (backward); the per-Gaussian
 // arithmetic then reads its own row from LDS.
 #include "sh_math.h"
+#include "exchange_layout.h"
 
 namespace gs {
 namespace {
@@ -151,6 +152,99 @@ __global__ __launch_bounds__(256) void sh_bwd_views_kernel(int n, int degrees_to
   }
 }
 
+// sh_bwd_views_kernel<K, true> over a table of dense and sparse view records
+// (exchange_layout.h): the sum runs in table order, skipping a sparse record's absent
+// Gaussians -- exactly zero colour gradients, whose products would add +-0 to an accumulator
+// that is never -0 -- so a table of sparse records gives the dense sum bit for bit.  Views
+// go in groups of XV: every group's mask / prefix loads are issued together, then its
+// value loads, so a wave waits two round trips per group instead of two per view.
+template <int K>
+__global__ __launch_bounds__(256) void sh_bwd_table_kernel(int n, int degrees_to_use,
+                                                           int num_views,
+                                                           const float *__restrict__ means,
+                                                           const ViewTable tab,
+                                                           float *__restrict__ v_dc,
+                                                           float *__restrict__ v_rest) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int ROW = K * 3;
+  constexpr int ROWP = sh_row_pitch(K);
+  constexpr int SH_THREADS = sh_threads(K);
+  constexpr int XV = 8;
+  const long long g0 = (long long)blockIdx.x * SH_THREADS;
+  const int cnt = (int)min((long long)SH_THREADS, (long long)n - g0);
+  const int t = threadIdx.x;
+  if (t < cnt) {
+    const long long g = g0 + t;
+    const long long W = xs_words(n), w = g >> 6;
+    const unsigned long long below = (1ull << (g & 63)) - 1ull;
+    const float mx = means[3 * g], my = means[3 * g + 1], mz = means[3 * g + 2];
+    float acc[ROW];
+#pragma unroll
+    for (int k = 0; k < ROW; ++k) acc[k] = 0.f;
+    for (int r0 = 0; r0 < num_views; r0 += XV) {
+      const int nv = min(XV, num_views - r0);
+      float u[XV][3], cp[XV][3];
+      bool has[XV];
+      long long row[XV];
+#pragma unroll
+      for (int j = 0; j < XV; ++j) {  // masks + prefixes (sparse), or the dense row index
+        has[j] = false;
+        row[j] = -1;
+        if (j < nv) {
+          const float *p = tab.rec[r0 + j];
+          const long long cap = tab.cap[r0 + j];
+          if (cap < 0) {
+            has[j] = true;
+            row[j] = g;
+            cp[j][0] = p[3LL * n];
+            cp[j][1] = p[3LL * n + 1];
+            cp[j][2] = p[3LL * n + 2];
+          } else {
+            const unsigned long long m = reinterpret_cast<const unsigned long long *>(p + XS_HDR)[w];
+            const uint32_t pre = reinterpret_cast<const uint32_t *>(p + XS_HDR + 2 * W)[w];
+            const long long pos = (long long)pre + __popcll(m & below);
+            has[j] = ((m >> (g & 63)) & 1ull) && pos < cap;
+            row[j] = pos;
+            cp[j][0] = p[0];
+            cp[j][1] = p[1];
+            cp[j][2] = p[2];
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < XV; ++j) {  // the colour gradients
+        u[j][0] = u[j][1] = u[j][2] = 0.f;
+        if (has[j]) {
+          const float *p = tab.rec[r0 + j];
+          const float *vals = tab.cap[r0 + j] < 0 ? p : p + xs_values_at(n);
+          u[j][0] = vals[3 * row[j]];
+          u[j][1] = vals[3 * row[j] + 1];
+          u[j][2] = vals[3 * row[j] + 2];
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < XV; ++j) {
+        if (!has[j]) continue;
+        float b[25];
+        const int nb = sh_basis(degrees_to_use, mx - cp[j][0], my - cp[j][1], mz - cp[j][2], b);
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          const float bk = k < nb ? b[k] : 0.f;
+          acc[k * 3 + 0] += bk * u[j][0];
+          acc[k * 3 + 1] += bk * u[j][1];
+          acc[k * 3 + 2] += bk * u[j][2];
+        }
+      }
+    }
+    float *rowp = smem + t * ROWP;
+#pragma unroll
+    for (int k = 0; k < ROW; ++k) rowp[k] = acc[k];
+  }
+  __syncthreads();
+  store_cols<3, 0, ROWP, SH_THREADS>(smem, cnt, v_dc + g0 * 3);
+  if constexpr (K > 1) store_cols<ROW - 3, 3, ROWP, SH_THREADS>(smem, cnt, v_rest + g0 * (ROW - 3));
+}
+
 }  // namespace
 }  // namespace gs
 
@@ -287,4 +381,39 @@ extern "C" int gsplat_compute_sh_backward_split(int num_points, int degree, int 
 #undef SPLIT_CASE
   }
   return check_launch("compute_sh_backward_split");
+}
+
+extern "C" int gsplat_compute_sh_backward_view_table(int num_points, int degree,
+                                                     int degrees_to_use, int num_views,
+                                                     const float *means3d,
+                                                     const float *const *records,
+                                                     const long long *capacities, float *v_dc,
+                                                     float *v_rest, void *stream) {
+  if (num_points < 0 || degree < 0 || degree > 4 || degrees_to_use < 0 ||
+      degrees_to_use > degree || num_views < 1 || num_views > XS_MAX_VIEWS || !records ||
+      !capacities || (num_points > 0 && (!means3d || !v_dc || (degree > 0 && !v_rest)))) {
+    set_error("compute_sh_backward_view_table: bad args (N=%d degree=%d degrees_to_use=%d "
+              "views=%d, at most %d)", num_points, degree, degrees_to_use, num_views,
+              XS_MAX_VIEWS);
+    return 1;
+  }
+  ViewTable tab{};
+  for (int r = 0; r < num_views; ++r) {
+    if (!records[r] || capacities[r] > num_points) {
+      set_error("compute_sh_backward_view_table: record %d is NULL or its capacity %lld exceeds "
+                "N=%d", r, capacities[r], num_points);
+      return 1;
+    }
+    tab.rec[r] = records[r];
+    tab.cap[r] = capacities[r];
+  }
+  if (num_points == 0) return 0;
+  const int K = num_bases(degree);
+  const int thr = sh_threads(K);
+  dim3 grid(cdiv(num_points, thr)), block(thr);
+  size_t smem = (size_t)thr * sh_row_pitch(K) * sizeof(float);
+  hipStream_t st = (hipStream_t)stream;
+  SH_DISPATCH(sh_bwd_table_kernel, num_points, degrees_to_use, num_views, means3d, tab, v_dc,
+              v_rest);
+  return check_launch("compute_sh_backward_view_table");
 }

@@ -149,6 +149,11 @@ class _FusedRender(Function):
         prepared = (spec_cap, plan_for(spec_cap)) if spec_cap > 0 else None
 
         preprocess()
+        # data-parallel view exchange: this view's sparse-record bitmap and the ranks' visible
+        # counts (async all-gather), as soon as radii exist (exchange.ShViewExchange.plan)
+        xchg = exchange.active() if K > 1 and need_grad and adam is None else None
+        if xchg is not None:
+            xchg.plan(n, radii, st)
         # The binning's emission and tile sort are launched at this frame shape's capacity
         # without the host read of I (rasterize.SpeculativeBinning), the blend right behind
         # them; the host reads I only then, while the GPU works, and re-bins on an overflow.
@@ -228,7 +233,7 @@ class _FusedRender(Function):
                     tbx, tby, num_intersects, chunk, layout_i)
         ctx.plan, ctx.rec = plan, rec
         ctx.opac_shape = opacities.shape
-        ctx.exchange = exchange.active() if K > 1 else None
+        ctx.exchange = xchg
         # data-parallel: all-reduce the four non-SH gradients from inside the backward (one flat
         # buffer, overlapping the SH views kernel) when autograd will hand them over as the
         # parameters' .grad (no gradient to accumulate into)
@@ -305,40 +310,63 @@ class _FusedRender(Function):
             return (None,) * 21
         f32 = dict(device=dev, dtype=torch.float32)
         xchg = ctx.exchange
-        gathered = None
         if xchg is not None and rec is not None:
-            # the view record straight from the raster records, its all-gather issued now: it
-            # overlaps the geometry backward below and the geometry all-reduce
-            send = torch.empty((3 * n + 4,), **f32)
-            _lib.call("gsplat_exchange_pack_colors", n, P(rec), rec.numel(), P(radii),
-                      P(colors), P(xchg.campos.to(dev).contiguous()), P(send), st)
-            gathered = xchg.start_gather(send)
-        if xchg is not None and ctx.early:
-            flat = torch.empty((11 * n,), **f32)
-            v_means, v_scales = flat[:3 * n].view(n, 3), flat[3 * n:6 * n].view(n, 3)
-            v_quats, v_opac = flat[6 * n:10 * n].view(n, 4), flat[10 * n:].view(n, 1)
-            early = dict(flat=flat, map={p.data_ptr(): g.data_ptr() for p, g in zip(
-                (means, scales, quats, opacities), (v_means, v_scales, v_quats, v_opac))})
-        else:
-            v_means = torch.empty((n, 3), **f32)
-            v_scales = torch.empty((n, 3), **f32)
-            v_quats = torch.empty((n, 4), **f32)
-            v_opac = torch.empty((n, 1), **f32)
-            early = dict(flat=None, map=None)
+            return _exchange_backward(ctx, xchg, rec, st)
+        v_means = torch.empty((n, 3), **f32)
+        v_scales = torch.empty((n, 3), **f32)
+        v_quats = torch.empty((n, 4), **f32)
+        v_opac = torch.empty((n, 1), **f32)
         v_dc = torch.empty((n, 3), **f32)
         v_rest = torch.empty((n, K - 1, 3), **f32)
-        v_colors = torch.empty((n, 3), **f32) if xchg is not None else None
         _lib.call("gsplat_fused_preprocess_backward", n, K, dtu, P(means), P(scales), P(quats),
                   P(viewmat), P(projmat), P(campos), fx, fy, cx, cy, H, W, P(radii), P(conics),
                   P(colors), P(opac), P(rec), P(v_means), P(v_scales), P(v_quats), P(v_opac),
-                  P(v_dc), P(v_rest) if K > 1 else None, P(v_colors), st)
-        if xchg is not None:
-            v_dc, v_rest = xchg.reduce(
-                v_colors, lambda m, views: sh_backward_views_split(_DEG_OF_BASES[K], dtu, m,
-                                                                   views),
-                early_flat=early["flat"], early_map=early["map"], gathered=gathered)
+                  P(v_dc), P(v_rest) if K > 1 else None, None, st)
         return (v_means, v_scales, v_quats, v_opac.view(ctx.opac_shape), v_dc, v_rest) + \
             (None,) * 15
+
+
+def _exchange_backward(ctx, xchg, rec, st):
+    """The fused backward under the data-parallel view exchange (exchange.ShViewExchange).  Right
+    after the raster backward this view's colour-gradient record is packed from the records and
+    its all-gather issued (it overlaps the geometry backward, and -- several views per rank --
+    the rank's next views).  The geometry gradients go to one flat buffer [11 N] (summed over
+    the rank's views: gsplat_fused_preprocess_backward_accumulate).  The last view of the step
+    issues the flat all-reduce (async: it overlaps the views kernel; train.GradExchange waits)
+    and evaluates every gathered record; earlier views return no gradient."""
+    (means, scales, quats, opacities, features_dc, features_rest, viewmat, projmat, campos,
+     background, xys, radii, conics, colors, opac, gids, bins, final_Ts,
+     final_idx) = ctx.saved_tensors
+    n, K, dtu, fx, fy, cx, cy, H, W = ctx.meta[:9]
+    P = _lib.ptr
+    dev = means.device
+    if not ctx.early and xchg.views_per_step > 1:
+        raise RuntimeError("render_fused: several views per rank need the four geometry "
+                           "parameters without a .grad (zero_grad before the step's first view)")
+    xchg.send_view(n, rec, radii, colors, st)
+    first = xchg.geo is None
+    if first:
+        xchg.geo = torch.empty((11 * n,), device=dev, dtype=torch.float32)
+    flat = xchg.geo
+    v_means, v_scales = flat[:3 * n].view(n, 3), flat[3 * n:6 * n].view(n, 3)
+    v_quats, v_opac = flat[6 * n:10 * n].view(n, 4), flat[10 * n:].view(n, 1)
+    v_colors = torch.empty((n, 3), device=dev, dtype=torch.float32)
+    head = (n, K, dtu, P(means), P(scales), P(quats), P(viewmat), P(projmat), P(campos), fx, fy,
+            cx, cy, H, W, P(radii), P(conics), P(colors), P(opac), P(rec), P(v_means),
+            P(v_scales), P(v_quats), P(v_opac))
+    if first:
+        _lib.call("gsplat_fused_preprocess_backward", *head, None, None, P(v_colors), st)
+    else:
+        _lib.call("gsplat_fused_preprocess_backward_accumulate", *head, P(v_colors), st)
+    if not xchg.last_view:
+        return (None,) * 21
+    xchg.geo = None
+    if ctx.early:  # (else autograd accumulates into existing grads: GradExchange reduces them)
+        xchg.all_reduce_early(flat, {p.data_ptr(): g.data_ptr() for p, g in zip(
+            (means, scales, quats, opacities), (v_means, v_scales, v_quats, v_opac))})
+    v_dc, v_rest = xchg.reduce_views(_DEG_OF_BASES[K], dtu)
+    return (v_means, v_scales, v_quats, v_opac.view(ctx.opac_shape), v_dc, v_rest) + \
+        (None,) * 15
 
 
 def sh_backward_views_split(degree: int, degrees_to_use: int, means: Tensor, views: Tensor):

@@ -138,7 +138,7 @@ class TrainStep:
     def __init__(self, scene: GaussianScene, sh_degree: int = 3, world_size: int = 1,
                  loss: str = "splatfacto", group=None, api=None,
                  grad_exchange: str = "sh_views", render_mode: str = "caller",
-                 fuse_adam: bool = True):
+                 fuse_adam: bool = True, sparse_exchange: str = "auto"):
         if render_mode not in ("caller", "fused"):
             raise ValueError(f"render_mode must be 'caller' or 'fused', not {render_mode}")
         if render_mode == "fused" and (api is not None or not scene.means.is_cuda):
@@ -160,7 +160,9 @@ class TrainStep:
         self.world_size = world_size
         if grad_exchange not in ("sh_views", "allreduce"):
             raise ValueError(f"grad_exchange must be 'sh_views' or 'allreduce', not {grad_exchange}")
-        self.sh_exchange = ShViewExchange(group) if world_size > 1 and \
+        # sparse_exchange: "auto" sends only the visible Gaussians' colour gradients when that
+        # record is clearly smaller (exchange.py); "on" / "off" force it (tests)
+        self.sh_exchange = ShViewExchange(group, sparse=sparse_exchange) if world_size > 1 and \
             grad_exchange == "sh_views" else None
         self.grad_sync = GradExchange(
             self.params, group, sh=self.sh_exchange,
@@ -223,9 +225,11 @@ class TrainStep:
         return render(self.scene, cam, self.sh_degree, background, api=self.api)
 
     def forward_backward(self, cam: GCCamera, gt: torch.Tensor, background: torch.Tensor,
-                         adam=None):
+                         adam=None, view: int = 0, of: int = 1):
+        """Render, loss and backward of one view -- view `view` of this rank's `of` views this
+        step (forward_backward_views)."""
         if self.sh_exchange is not None:
-            with self.sh_exchange.view(self.scene.means, cam.c2w[..., :3, 3]):
+            with self.sh_exchange.view(self.scene.means, cam.c2w[..., :3, 3], view, of):
                 out = self._render(cam, background, gt=gt)
         else:
             out = self._render(cam, background, adam=adam, gt=gt)
@@ -245,6 +249,23 @@ class TrainStep:
             self._null_sh_exchange()
         return loss, out
 
+    def forward_backward_views(self, cams: List[GCCamera], gts: List[torch.Tensor],
+                               background: torch.Tensor):
+        """Several views per rank in one step (gradients summed over this rank's views and
+        all ranks'): with the fused render under the view exchange, each view's record
+        all-gather stays in flight while the next view renders, and only the last view's
+        exchange is exposed (exchange.py).  Returns the summed loss."""
+        if len(cams) != len(gts) or not cams:
+            raise ValueError("forward_backward_views: one ground truth per camera")
+        if len(cams) > 1 and self.sh_exchange is not None and self.render_mode != "fused":
+            raise ValueError("forward_backward_views: several views per rank under the view "
+                             "exchange need render_mode='fused'")
+        total = 0.0
+        for k, (cam, gt) in enumerate(zip(cams, gts)):
+            loss, _ = self.forward_backward(cam, gt, background, view=k, of=len(cams))
+            total = total + loss.detach()
+        return total
+
     def _null_sh_exchange(self):
         sc = self.scene
         n, K = sc.num_points, sc.features_rest.shape[1] + 1
@@ -260,17 +281,19 @@ class TrainStep:
         sc.features_dc.grad = v[:, 0, :].contiguous()
         sc.features_rest.grad = v[:, 1:, :].contiguous()
 
-    def step(self, cam: GCCamera, gt: torch.Tensor, background: Optional[torch.Tensor] = None,
+    def step(self, cam, gt, background: Optional[torch.Tensor] = None,
              optimizer: bool = True):
         """One training step (gc_trainer.py:258-301 / gc_pipeline.py:469-480): render, the
-        splatfacto loss, backward, gradient exchange (N > 1) and Adam."""
+        splatfacto loss, backward, gradient exchange (N > 1) and Adam.  cam / gt may be lists:
+        several views per rank, their gradients summed (forward_backward_views)."""
+        multi = isinstance(cam, (list, tuple))
         if background is None:
-            background = torch.rand(3, device=gt.device)
+            background = torch.rand(3, device=(gt[0] if multi else gt).device)
         if optimizer:
             for g in self.opt.param_groups:
                 if g["name"] == "means":
                     g["lr"] = self._xyz_lr()
-        if optimizer and self.fuse_adam and isinstance(self.opt, FusedAdamType()) and \
+        if optimizer and not multi and self.fuse_adam and isinstance(self.opt, FusedAdamType()) and \
                 all(p.dtype == torch.float32 and p.is_contiguous() for p in self.params):
             # the backward takes the Adam step (one kernel instead of gradient tensors + step)
             self.zero_grad()
@@ -279,7 +302,10 @@ class TrainStep:
             self.step_count += 1
             return loss
         self.zero_grad()
-        loss, out = self.forward_backward(cam, gt, background)
+        if multi:
+            loss = self.forward_backward_views(list(cam), list(gt), background)
+        else:
+            loss, out = self.forward_backward(cam, gt, background)
         if not optimizer:
             self.sync_grads()
             return loss

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define GSPLAT_MI355X_ABI_VERSION 14
+#define GSPLAT_MI355X_ABI_VERSION 15
 
 int gsplat_abi_version(void);
 const char *gsplat_last_error(void);
@@ -147,6 +147,16 @@ int gsplat_compute_sh_backward_views_split(int num_points, int degree, int degre
                                            int num_views, const float *means3d,
                                            const float *views, long long view_stride,
                                            float *v_dc, float *v_rest, void *stream);
+/* gsplat_compute_sh_backward_views_split over a table of records (HOST arrays of num_views <=
+ * 64 device pointers and capacities): capacities[r] < 0 -> records[r] is a dense record
+ * (v_colors [3N] | camera centre | pad), else a sparse one of that capacity
+ * (gsplat_exchange_pack_sparse).  Sums in table order; sparse and dense records of the same
+ * views give bit-identical results. */
+int gsplat_compute_sh_backward_view_table(int num_points, int degree, int degrees_to_use,
+                                          int num_views, const float *means3d,
+                                          const float *const *records,
+                                          const long long *capacities, float *v_dc,
+                                          float *v_rest, void *stream);
 
 /* covs2d [N,3] -> conics [N,3], radii [N] (float).  det == 0 rows get zeros. */
 int gsplat_compute_cov2d_bounds(int num_points, const float *covs2d, float *conics,
@@ -416,6 +426,35 @@ int gsplat_fused_preprocess_backward(
 int gsplat_exchange_pack_colors(int num_points, const void *grad_records, size_t records_bytes,
                                 const int32_t *radii, const float *colors, const float *campos,
                                 float *send, void *stream);
+
+/* The sparse view record (no gsplat counterpart): only the visible Gaussians'
+ * colour gradients travel, after a visibility bitmap and its prefix -- 12 B per visible
+ * Gaussian + 0.19 B per Gaussian instead of 12 B per Gaussian (c4 garden, 55 % visible: 6.8
+ * B).  Layout in floats, W = ceil(N/64): [0,3) camera centre, [3] visible count (uint32
+ * bits), [4, 4+2W) uint64 masks (bit b of word w <=> radii[64w+b] > 0), [4+2W, 4+3W) uint32
+ * exclusive prefix of their popcounts, [4+3W, 4+3W+3C) the visible Gaussians' v_colors in
+ * index order, C >= the count (the capacity the ranks agreed on).
+ * gsplat_exchange_sparse_floats: the record's length in floats for capacity C (-1: bad args).
+ * gsplat_exchange_sparse_plan: writes the count, masks and prefix from radii (the forward,
+ * once radii exist), into send's first 4 + 3W floats.
+ * gsplat_exchange_pack_sparse: after the raster backward, the camera centre and the values
+ * (as gsplat_exchange_pack_colors computes them) into a planned send of >= that length. */
+long long gsplat_exchange_sparse_floats(int num_points, long long capacity);
+int gsplat_exchange_sparse_plan(int num_points, const int32_t *radii, float *send, void *stream);
+int gsplat_exchange_pack_sparse(int num_points, const void *grad_records, size_t records_bytes,
+                                const int32_t *radii, const float *colors, const float *campos,
+                                float *send, long long capacity, void *stream);
+/* gsplat_fused_preprocess_backward in the view-exchange mode (v_colors written, sh_bases > 1)
+ * for a rank that renders several views per step: the four geometry gradients are ADDED to
+ * v_means3d, v_log_scales, v_quats, v_opacity_logits (the earlier views' sum); v_colors is
+ * this view's. */
+int gsplat_fused_preprocess_backward_accumulate(
+    int num_points, int sh_bases, int degrees_to_use, const float *means3d,
+    const float *log_scales, const float *quats, const float *viewmat, const float *projmat,
+    const float *campos, float fx, float fy, float cx, float cy, int img_height, int img_width,
+    const int32_t *radii, const float *conics, const float *colors, const float *opacity,
+    const void *grad_records, float *v_means3d, float *v_log_scales, float *v_quats,
+    float *v_opacity_logits, float *v_colors, void *stream);
 
 /* Single-GPU training step: gsplat_fused_preprocess_backward with the Adam step of the six
  * parameter groups fused in (torch.optim.Adam foreach semantics, exactly gsplat_adam_step's

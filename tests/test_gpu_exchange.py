@@ -184,3 +184,127 @@ def test_trainstep_multirank_path_over_rccl_world1(gpu):
     finally:
         _lib.set_deterministic(prev)
         dist.destroy_process_group()
+
+
+def _sparse_inputs(n, frac, seed, gpu):
+    """radii with about `frac` visible (plus whole 64-blocks culled / visible), random gradient
+    records, colours with some clamp-raised (-0.0) entries."""
+    g = torch.Generator().manual_seed(seed)
+    vis = torch.rand(n, generator=g) < frac
+    if n >= 256:
+        vis[64:128] = False
+        vis[128:192] = True
+    radii = torch.where(vis, torch.randint(1, 9, (n,), generator=g), torch.zeros(n, dtype=torch.int64))
+    recf = 16  # floats per gradient record (gsplat_grad_records_bytes / N / 4)
+    rec = torch.randn(n, recf, generator=g)
+    colors = torch.rand(n, 3, generator=g)
+    colors[torch.rand(n, 3, generator=g) < 0.1] = -0.0
+    campos = torch.randn(3, generator=g)
+    return (radii.to(torch.int32), rec, colors, campos,
+            [t.to(gpu) for t in (radii.to(torch.int32), rec, colors, campos)])
+
+
+def _expected_sparse(radii, rec, colors, campos, cap):
+    """The sparse record (exchange_layout.h) restated in numpy."""
+    n = radii.shape[0]
+    W = (n + 63) // 64
+    vis = (radii.numpy() > 0)
+    pad = np.zeros(W * 64, dtype=bool)
+    pad[:n] = vis
+    bits = pad.reshape(W, 64)
+    words = (bits.astype(np.uint64) << np.arange(64, dtype=np.uint64)).sum(axis=1, dtype=np.uint64)
+    pop = bits.sum(axis=1).astype(np.uint32)
+    prefix = np.concatenate([[0], np.cumsum(pop)[:-1]]).astype(np.uint32)
+    c = colors.numpy()
+    passes = (c >= 0) & ~np.signbit(c)
+    v = np.where(passes, rec.numpy()[:, 5:8], 0.0).astype(np.float32)
+    out = np.zeros(4 + 3 * W + 3 * cap, dtype=np.float32)
+    out[:3] = campos.numpy()
+    out[3:4] = np.array([vis.sum()], dtype=np.uint32).view(np.float32)
+    out[4:4 + 2 * W] = words.view(np.float32)
+    out[4 + 2 * W:4 + 3 * W] = prefix.view(np.float32)
+    vals = v[vis]
+    out[4 + 3 * W:4 + 3 * W + vals.size] = vals.reshape(-1)
+    return out, int(vis.sum())
+
+
+@pytest.mark.parametrize("n,frac", [(1, 1.0), (63, 0.5), (1037, 0.55), (4101, 0.3),
+                                    (130_000, 0.55), (70_000, 0.0)])
+def test_sparse_record_matches_restatement(gpu, n, frac):
+    """gsplat_exchange_sparse_plan + _pack_sparse write exactly the layout exchange_layout.h
+    states (bitmap, prefix, count, values in index order, camera centre), and the dense pack of
+    the same inputs holds the same values at the visible rows and zeros elsewhere."""
+    from gaussctrl_exp_amd import _lib
+    from gaussctrl_exp_amd.exchange import sparse_floats
+    radii, rec, colors, campos, (d_radii, d_rec, d_colors, d_campos) = _sparse_inputs(n, frac, n, gpu)
+    rec_bytes = d_rec.numel() * 4
+    exp_full, count = _expected_sparse(radii, rec, colors, campos, n)
+    for cap in sorted({count, n}):
+        send = torch.full((sparse_floats(n, n),), float("nan"), device=gpu)
+        st = _lib.stream(gpu)
+        _lib.call("gsplat_exchange_sparse_plan", n, _lib.ptr(d_radii), _lib.ptr(send), st)
+        _lib.call("gsplat_exchange_pack_sparse", n, _lib.ptr(d_rec), rec_bytes, _lib.ptr(d_radii),
+                  _lib.ptr(d_colors), _lib.ptr(d_campos), _lib.ptr(send), cap, st)
+        L = sparse_floats(n, cap)
+        assert _lib.query("gsplat_exchange_sparse_floats", n, cap) == L
+        got = send[:L].cpu().numpy()
+        exp = exp_full[:L]
+        head = 4 + 3 * ((n + 63) // 64) + 3 * count
+        np.testing.assert_array_equal(got[:head].view(np.uint32), exp[:head].view(np.uint32))
+    dense = torch.empty(3 * n + 4, device=gpu)
+    _lib.call("gsplat_exchange_pack_colors", n, _lib.ptr(d_rec), rec_bytes, _lib.ptr(d_radii),
+              _lib.ptr(d_colors), _lib.ptr(d_campos), _lib.ptr(dense), _lib.stream(gpu))
+    dv = dense[:3 * n].view(n, 3).cpu().numpy()
+    vis = radii.numpy() > 0
+    W = (n + 63) // 64
+    np.testing.assert_array_equal(dv[vis].reshape(-1), exp_full[4 + 3 * W:4 + 3 * W + 3 * count])
+    assert not dv[~vis].any()
+
+
+@pytest.mark.parametrize("degree,dtu", [(3, 3), (3, 1), (1, 1), (0, 0)])
+def test_view_table_sparse_equals_dense_bitwise(gpu, degree, dtu):
+    """gsplat_compute_sh_backward_view_table over sparse records, dense records and a mix gives
+    the dense multi-view kernel's result bit for bit (absent rows are exact zeros)."""
+    import ctypes
+    from gaussctrl_exp_amd import _lib
+    from gaussctrl_exp_amd.exchange import sparse_floats
+    from gaussctrl_exp_amd.fused import sh_backward_views_split
+    n, R = 50_021, 11  # two groups of 8 views in the kernel, one partial
+    g = torch.Generator().manual_seed(9)
+    means = ((torch.rand(n, 3, generator=g) * 2 - 1) * 1.5).to(gpu)
+    dense, sparse = [], []
+    st = _lib.stream(gpu)
+    for r in range(R):
+        radii, rec, colors, campos, (d_radii, d_rec, d_colors, d_campos) = \
+            _sparse_inputs(n, 0.2 + 0.07 * r, 100 + r, gpu)
+        d = torch.empty(3 * n + 4, device=gpu)
+        _lib.call("gsplat_exchange_pack_colors", n, _lib.ptr(d_rec), d_rec.numel() * 4,
+                  _lib.ptr(d_radii), _lib.ptr(d_colors), _lib.ptr(d_campos), _lib.ptr(d), st)
+        cap = int((radii > 0).sum()) + r  # capacities above the count are allowed
+        s = torch.empty(sparse_floats(n, n), device=gpu)
+        _lib.call("gsplat_exchange_sparse_plan", n, _lib.ptr(d_radii), _lib.ptr(s), st)
+        _lib.call("gsplat_exchange_pack_sparse", n, _lib.ptr(d_rec), d_rec.numel() * 4,
+                  _lib.ptr(d_radii), _lib.ptr(d_colors), _lib.ptr(d_campos), _lib.ptr(s), cap, st)
+        dense.append(d)
+        sparse.append((s, cap))
+    ref_dc, ref_rest = sh_backward_views_split(degree, dtu, means, torch.stack(dense))
+    K = num_sh_bases(degree)
+    for mode in ("sparse", "dense", "mix"):
+        ptrs, caps = [], []
+        for r in range(R):
+            use_sparse = mode == "sparse" or (mode == "mix" and r % 2 == 0)
+            ptrs.append(sparse[r][0].data_ptr() if use_sparse else dense[r].data_ptr())
+            caps.append(sparse[r][1] if use_sparse else -1)
+        v_dc = torch.empty(n, 3, device=gpu)
+        v_rest = torch.empty(n, K - 1, 3, device=gpu)
+        _lib.call("gsplat_compute_sh_backward_view_table", n, degree, dtu, R, _lib.ptr(means),
+                  ctypes.cast((ctypes.c_void_p * R)(*ptrs), ctypes.c_void_p),
+                  ctypes.cast((ctypes.c_longlong * R)(*caps), ctypes.c_void_p), _lib.ptr(v_dc),
+                  _lib.ptr(v_rest) if K > 1 else None, st)
+        np.testing.assert_array_equal(v_dc.cpu().numpy(), ref_dc.cpu().numpy())
+        np.testing.assert_array_equal(v_rest.cpu().numpy(), ref_rest.cpu().numpy())
+    with pytest.raises(RuntimeError, match="capacity"):
+        _lib.call("gsplat_compute_sh_backward_view_table", n, degree, dtu, 1, _lib.ptr(means),
+                  ctypes.cast((ctypes.c_void_p * 1)(dense[0].data_ptr()), ctypes.c_void_p),
+                  ctypes.cast((ctypes.c_longlong * 1)(n + 1), ctypes.c_void_p), _lib.ptr(v_dc),
+                  _lib.ptr(v_rest) if K > 1 else None, st)

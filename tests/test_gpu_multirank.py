@@ -46,7 +46,7 @@ def _gt(rank, dev):
 BG = (0.3, 0.5, 0.7)
 
 
-def _worker(rank, world, port, out_dir, mode):
+def _worker(rank, world, port, out_dir, mode, sparse="auto", per_rank=1):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
@@ -54,22 +54,33 @@ def _worker(rank, world, port, out_dir, mode):
     from gaussctrl_exp_amd.train import TrainStep
     bg = torch.tensor(BG, device=dev)
     t = TrainStep(_scene(dev), sh_degree=3, world_size=world, loss="l1", render_mode="fused",
-                  grad_exchange=mode)
+                  grad_exchange=mode, sparse_exchange=sparse)
     assert not t.fuse_adam  # multi-rank: the gradients must be summed before Adam
-    t.step(_views(dev)[rank], _gt(rank, dev), background=bg, optimizer=False)
+    # rank r renders views r*per_rank ... (several per rank: one step sums them all)
+    mine = list(range(rank * per_rank, (rank + 1) * per_rank))
+    cams = [_views(dev)[v] for v in mine] if per_rank > 1 else _views(dev)[rank]
+    gts = [_gt(v, dev) for v in mine] if per_rank > 1 else _gt(rank, dev)
+    t.step(cams, gts, background=bg, optimizer=False)
     np.save(os.path.join(out_dir, f"grad{rank}.npy"), t.flat_grad().cpu().numpy())
     if mode == "sh_views":  # the four non-SH gradients went out early, from the fused backward
         assert t.sh_exchange.early_steps == 1
+        kinds = t.sh_exchange.record_kinds
+        assert kinds["sparse" if sparse == "on" else "dense"] == per_rank if sparse != "auto" \
+            else sum(kinds.values()) == per_rank
     for _ in range(2):
-        t.step(_views(dev)[rank], _gt(rank, dev), background=bg)
+        t.step(cams, gts, background=bg)
     np.save(os.path.join(out_dir, f"params{rank}.npy"),
             torch.cat([p.detach().reshape(-1) for p in t.params]).cpu().numpy())
     torch.cuda.synchronize()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode,world", [("sh_views", 2), ("allreduce", 2), ("sh_views", 4)])
-def test_fused_ranks_sum_the_view_gradients(tmp_path, mode, world):
+@pytest.mark.parametrize("mode,world,sparse,per_rank", [
+    ("sh_views", 2, "auto", 1), ("sh_views", 2, "on", 1), ("sh_views", 2, "off", 1),
+    ("allreduce", 2, "auto", 1), ("sh_views", 4, "auto", 1),
+    ("sh_views", 2, "on", 2),  # two views per rank: records in flight across the rank's views
+])
+def test_fused_ranks_sum_the_view_gradients(tmp_path, mode, world, sparse, per_rank):
     from gaussctrl_exp_amd import _lib
     from parity import assert_close
     port = _free_port()
@@ -77,7 +88,8 @@ def test_fused_ranks_sum_the_view_gradients(tmp_path, mode, world):
     # has the very raster gradients the ranks summed, and the bar needs no outlier allowance
     os.environ["GSPLAT_MI355X_DETERMINISTIC"] = "1"
     try:
-        mp.spawn(_worker, args=(world, port, str(tmp_path), mode), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, port, str(tmp_path), mode, sparse, per_rank),
+                 nprocs=world, join=True)
     finally:
         os.environ.pop("GSPLAT_MI355X_DETERMINISTIC", None)
     g0 = np.load(tmp_path / "grad0.npy")
@@ -90,7 +102,7 @@ def test_fused_ranks_sum_the_view_gradients(tmp_path, mode, world):
     ref = 0
     prev = _lib.set_deterministic(True)
     try:
-        for r in range(world):
+        for r in range(world * per_rank):
             t = TrainStep(_scene(dev), sh_degree=3, world_size=1, loss="l1", render_mode="fused")
             t.step(_views(dev)[r], _gt(r, dev), background=torch.tensor(BG, device=dev),
                    optimizer=False)
@@ -117,6 +129,8 @@ def _garden_worker(rank, world, port, out_dir):
     t.step(cam, gt, background=torch.tensor(BG, device=dev), optimizer=False)
     np.save(os.path.join(out_dir, f"grad{rank}.npy"), t.flat_grad().cpu().numpy())
     assert t.sh_exchange.early_steps == 1
+    # the garden views see ~55 % of the Gaussians: the colour gradients travel as sparse records
+    assert t.sh_exchange.record_kinds == {"sparse": 1, "dense": 0}
     t.step(cam, gt, background=torch.tensor(BG, device=dev))
     np.save(os.path.join(out_dir, f"params{rank}.npy"),
             torch.cat([p.detach().reshape(-1) for p in t.params]).cpu().numpy())
