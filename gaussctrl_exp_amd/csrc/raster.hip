@@ -691,7 +691,8 @@ __device__ __forceinline__ int wave_slot() {
   return block_slot() * (4 / WPT) + (threadIdx.x >> 6) / WPT;
 }
 template <int PXL, int COLS>
-__device__ __forceinline__ WaveRect wave_rect(int tbx, int tby, int H, int W, int tile = -1) {
+__device__ __forceinline__ WaveRect wave_rect(int tbx, int tby, int H, int W, int tile = -1,
+                                              int wt_item = -1) {
   constexpr int LROWS = 64 / COLS;      // rows per lane pass
   constexpr int WROWS = LROWS * PXL;    // rows per wave
   constexpr int WX = GS_BLOCK / COLS, WY = GS_BLOCK / WROWS;
@@ -705,7 +706,7 @@ __device__ __forceinline__ WaveRect wave_rect(int tbx, int tby, int H, int W, in
     const int slot = wave_slot<PXL, COLS>();
     r.tile = slot;
   }
-  const int wt = wave % WPT;
+  const int wt = wt_item >= 0 ? wt_item : wave % WPT;
   const int tx = r.tile % tbx, ty = r.tile / tbx;
   const int c0 = tx * GS_BLOCK + (wt % WX) * COLS, r0 = ty * GS_BLOCK + (wt / WX) * WROWS;
   r.live = r.tile < tbx * tby && c0 < W && r0 < H;
@@ -972,32 +973,28 @@ __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
 // blend the part itself -- per pixel the same arithmetic in the same order as the unsplit
 // walk, so the per-wave totals (and the deterministic mode's sums) are unchanged, while a
 // long list's parts run as separate, earlier-dispatched waves.
-template <int NP, bool ATOMICS, int COLS, bool SPLIT = false, typename PV = f2,
-          bool DET = false, bool CNT = false, bool KB = false>
-__global__ __launch_bounds__(256) void raster_bwd3p_kernel(
-    int tbx, int tby, int H, int W, const int *__restrict__ gids, const int2 *__restrict__ bins,
-    const float2 *__restrict__ xys, const float *__restrict__ conics,
-    const float *__restrict__ colors, const float *__restrict__ opacity,
-    const float *__restrict__ background, const float *__restrict__ final_Ts,
-    const int *__restrict__ final_idx, const float *__restrict__ v_out,
-    const float *__restrict__ v_out_alpha, float alpha_max, float *__restrict__ rec,
-    int chunk = 0, const int2 *__restrict__ items = nullptr,
-    const int *__restrict__ n_items = nullptr, unsigned long long *__restrict__ det = nullptr,
-    const unsigned long long *__restrict__ kbits = nullptr, long long kbw = 0,
-    const int *__restrict__ tile_last = nullptr, L1Grad l1 = {}) {
+#define BWD3P_PARAMS                                                                         \
+    int tbx, int tby, int H, int W, const int *__restrict__ gids, const int2 *__restrict__ bins, \
+    const float2 *__restrict__ xys, const float *__restrict__ conics,                            \
+    const float *__restrict__ colors, const float *__restrict__ opacity,                         \
+    const float *__restrict__ background, const float *__restrict__ final_Ts,                    \
+    const int *__restrict__ final_idx, const float *__restrict__ v_out,                          \
+    const float *__restrict__ v_out_alpha, float alpha_max, float *__restrict__ rec, int chunk,  \
+    const int2 *__restrict__ items, const int *__restrict__ n_items,                             \
+    unsigned long long *__restrict__ det, const unsigned long long *__restrict__ kbits,          \
+    long long kbw, const int *__restrict__ tile_last, L1Grad l1
+#define BWD3P_ARGS                                                                           \
+  tbx, tby, H, W, gids, bins, xys, conics, colors, opacity, background, final_Ts, final_idx,  \
+      v_out, v_out_alpha, alpha_max, rec, chunk, items, n_items, det, kbits, kbw, tile_last, l1
+// One work item of the strip backward: tile `ctile` (-1: the wave's own slot), list part `part`
+// (SPLIT), strip `wt` of the tile (-1: by the wave's index in its workgroup).
+template <int NP, bool ATOMICS, int COLS, bool SPLIT, typename PV, bool DET, bool CNT, bool KB>
+__device__ __forceinline__ void bwd3p_item(BWD3P_PARAMS, int ctile, int part, int wt_item) {
   constexpr int PXL = 2 * NP;
   constexpr int LROWS = 64 / COLS;
-  int ctile = -1, part = 0;
-  if (SPLIT) {
-    const int slot = wave_slot<PXL, COLS>();
-    if (slot >= *n_items) return;  // wave-uniform: past the last item
-    const int2 it = items[slot];
-    ctile = it.x;
-    part = it.y;
-  }
   const WaveLog wlog;
   const unsigned long long at_t0 = GS_ATTR ? __builtin_amdgcn_s_memtime() : 0ull;
-  const WaveRect R = wave_rect<PXL, COLS>(tbx, tby, H, W, ctile);
+  const WaveRect R = wave_rect<PXL, COLS>(tbx, tby, H, W, ctile, wt_item);
   if (!R.live) return;  // wave-uniform
   __shared__ GStage lds[4][64];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1046,7 +1043,8 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
   // KB: the kept positions from the forward's keep bits (the strip's two 8x8 blocks)
   KeepSrc S{};
   if constexpr (KB) {
-    const int wt = (threadIdx.x >> 6) & 1;  // the strip's row half: blocks 2 wt, 2 wt + 1
+    // the strip's row half: blocks 2 wt, 2 wt + 1
+    const int wt = wt_item >= 0 ? wt_item : (threadIdx.x >> 6) & 1;
     S = keep_src(kbits, kbw, tile_last, tile, range, 2 * wt, 2 * wt + 1);
   }
   auto stage1 = [&](int idx, int g, GStage &s) {
@@ -1244,6 +1242,51 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(
     if (at[3] == 0) at[2] = at[5];
   }
   wlog.done(tile, GS_ATTR ? at : nullptr);
+}
+
+template <int NP, bool ATOMICS, int COLS, bool SPLIT = false, typename PV = f2,
+          bool DET = false, bool CNT = false, bool KB = false>
+__global__ __launch_bounds__(256) void raster_bwd3p_kernel(BWD3P_PARAMS) {
+  int ctile = -1, part = 0;
+  if (SPLIT) {
+    const int slot = wave_slot<2 * NP, COLS>();
+    if (slot >= *n_items) return;  // wave-uniform: past the last item
+    const int2 it = items[slot];
+    ctile = it.x;
+    part = it.y;
+  }
+  bwd3p_item<NP, ATOMICS, COLS, SPLIT, PV, DET, CNT, KB>(BWD3P_ARGS, ctile, part, -1);
+}
+
+// The list-split strip backward as resident waves taking work from a queue: entry s of the
+// queue is strip s & 1 of item s >> 1 (the items longest first), fetched by one atomic per
+// wave as the wave finishes its last.  Against one item pair per workgroup dispatched by the
+// hardware, a wave never idles for its workgroup's slowest wave, and no second, partly filled
+// generation of workgroups runs after the first (profiles/r05_bwd_attribution.txt).  The grid
+// is at most the resident capacity; every wave exits once the queue is empty, and the last to
+// exit resets the two counters (n_items[1], n_items[2]: zeroed by the plan as well) for the
+// next launch on this plan.
+// (7 waves per SIMD as the one-item kernel: inlined into the loop the item takes 93 VGPRs)
+template <int NP, bool KB>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) void
+raster_bwd3p_queue_kernel(BWD3P_PARAMS) {
+  int *q = const_cast<int *>(n_items) + 1;
+  const int total = 2 * *n_items;
+  for (;;) {
+    int s = 0;
+    if ((threadIdx.x & 63) == 0) s = atomicAdd(q, 1);
+    s = __builtin_amdgcn_readfirstlane(s);  // (lane 0's: the wave's entry, in an SGPR)
+    if (s >= total) break;
+    const int2 it = items[s >> 1];
+    bwd3p_item<NP, true, 16, true, f2, false, false, KB>(BWD3P_ARGS, it.x, it.y, s & 1);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    const int waves = (int)gridDim.x * (int)(blockDim.x >> 6);
+    if (atomicAdd(q + 1, 1) == waves - 1) {  // every wave has fetched past the end
+      atomicExch(q, 0);
+      atomicExch(q + 1, 0);
+    }
+  }
 }
 
 // ---------------------------------------------------------------- block backward (shipped)
@@ -1511,7 +1554,11 @@ __device__ __forceinline__ void split_plan_body(int T, int chunk, const int2 *__
       if (tid >= d) x += y;
     }
     cur[tid] = x - h;
-    if (tid == 63) *n_items = x;
+    if (tid == 63) {
+      n_items[0] = x;
+      n_items[1] = 0;  // the queue backward's counters (raster_bwd3p_queue_kernel)
+      n_items[2] = 0;
+    }
   }
   __syncthreads();
   for (int t = tid; t < T; t += 1024) {
@@ -2058,6 +2105,33 @@ static int bwd_geometry(int tbx, int tby) {
   return (long long)tbx * tby < 3584 ? 1 : 2;
 }
 
+// The queue backward (raster_bwd3p_queue_kernel) when GSPLAT_MI355X_BWD_QUEUE=1 (A/B runs),
+// and its grid: the workgroups the device holds resident at once (occupancy x CUs).
+static bool bwd_queue_on() {
+  static const bool on = [] {
+    const char *e = getenv("GSPLAT_MI355X_BWD_QUEUE");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+static unsigned bwd_queue_grid(bool kb) {
+  static unsigned cached[2] = {0, 0};
+  unsigned &g = cached[kb ? 1 : 0];
+  if (g == 0) {
+    int dev = 0, cus = 0, per_cu = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (kb)
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
+          &per_cu, reinterpret_cast<const void *>(&raster_bwd3p_queue_kernel<1, true>), 256, 0);
+    else
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
+          &per_cu, reinterpret_cast<const void *>(&raster_bwd3p_queue_kernel<1, false>), 256, 0);
+    g = (unsigned)std::max(1, cus * std::max(per_cu, 1));
+  }
+  return g;
+}
+
 // The C = 3 backward into the records `rec` (which the caller cleared), with the list split
 // when w != NULL, the integer accumulators when det != NULL (then det_finish_kernel writes the
 // records), the lane-slot counting instantiation when the pair-count hook is on.
@@ -2107,6 +2181,22 @@ static void launch_bwd(hipStream_t st, int tbx, int tby, int H, int W, int n,
     }
 
 #undef BWD8
+  } else if (w && !det && !cnt && bwd_queue_on()) {
+    // resident waves on a work queue (raster_bwd3p_queue_kernel)
+    const unsigned need = cdiv(2 * w->items_bound, 4);
+    if (kb) {
+      const unsigned grid = std::min(need, bwd_queue_grid(kb));
+      hipLaunchKernelGGL((raster_bwd3p_queue_kernel<1, true>), dim3(grid), dim3(256), 0, st, tbx,
+                         tby, H, W, gids, (const int2 *)bins, (const float2 *)xys, conics,
+                         colors, opacity, background, final_Ts, final_idx, v_output,
+                         v_output_alpha, alpha_max, rec, chunk, its, ni, det, kbits, kbw, tl, l1);
+    } else {
+      const unsigned grid = std::min(need, bwd_queue_grid(kb));
+      hipLaunchKernelGGL((raster_bwd3p_queue_kernel<1, false>), dim3(grid), dim3(256), 0, st,
+                         tbx, tby, H, W, gids, (const int2 *)bins, (const float2 *)xys, conics,
+                         colors, opacity, background, final_Ts, final_idx, v_output,
+                         v_output_alpha, alpha_max, rec, chunk, its, ni, det, kbits, kbw, tl, l1);
+    }
   } else {
     const unsigned grid = cdiv(slots, (tiles_per_block<2, 16>()));
 #define BWDS(CH, DET, CNT, KB)                                                             \

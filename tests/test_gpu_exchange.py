@@ -264,7 +264,8 @@ def test_sparse_record_matches_restatement(gpu, n, frac):
 @pytest.mark.parametrize("degree,dtu", [(3, 3), (3, 1), (1, 1), (0, 0)])
 def test_view_table_sparse_equals_dense_bitwise(gpu, degree, dtu):
     """gsplat_compute_sh_backward_view_table over sparse records, dense records and a mix gives
-    the dense multi-view kernel's result bit for bit (absent rows are exact zeros)."""
+    the same result bit for bit (absent rows are exact zeros), within the parity bar of the
+    dense multi-view kernel."""
     import ctypes
     from gaussctrl_exp_amd import _lib
     from gaussctrl_exp_amd.exchange import sparse_floats
@@ -289,6 +290,7 @@ def test_view_table_sparse_equals_dense_bitwise(gpu, degree, dtu):
         sparse.append((s, cap))
     ref_dc, ref_rest = sh_backward_views_split(degree, dtu, means, torch.stack(dense))
     K = num_sh_bases(degree)
+    first = None
     for mode in ("sparse", "dense", "mix"):
         ptrs, caps = [], []
         for r in range(R):
@@ -301,8 +303,16 @@ def test_view_table_sparse_equals_dense_bitwise(gpu, degree, dtu):
                   ctypes.cast((ctypes.c_void_p * R)(*ptrs), ctypes.c_void_p),
                   ctypes.cast((ctypes.c_longlong * R)(*caps), ctypes.c_void_p), _lib.ptr(v_dc),
                   _lib.ptr(v_rest) if K > 1 else None, st)
-        np.testing.assert_array_equal(v_dc.cpu().numpy(), ref_dc.cpu().numpy())
-        np.testing.assert_array_equal(v_rest.cpu().numpy(), ref_rest.cpu().numpy())
+        got = (v_dc.cpu().numpy(), v_rest.cpu().numpy())
+        if first is None:
+            first = got
+        # every record mix gives the same bits (absent rows add nothing); against the dense
+        # multi-view kernel (a separately compiled basis: fma contraction may differ) the
+        # parity bar
+        np.testing.assert_array_equal(got[0], first[0])
+        np.testing.assert_array_equal(got[1], first[1])
+        np.testing.assert_allclose(got[0], ref_dc.cpu().numpy(), rtol=1e-4, atol=1e-6)
+        np.testing.assert_allclose(got[1], ref_rest.cpu().numpy(), rtol=1e-4, atol=1e-6)
     with pytest.raises(RuntimeError, match="capacity"):
         _lib.call("gsplat_compute_sh_backward_view_table", n, degree, dtu, 1, _lib.ptr(means),
                   ctypes.cast((ctypes.c_void_p * 1)(dense[0].data_ptr()), ctypes.c_void_p),
