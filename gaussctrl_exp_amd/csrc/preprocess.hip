@@ -779,42 +779,50 @@ __device__ __forceinline__ uint32_t xs_wave_incl_scan(uint32_t v) {
   return v;
 }
 
-// One workgroup: the exclusive scan of the W per-word counts, 16 consecutive words per thread
-// per round (W = 31,250 at 2M Gaussians: two rounds), and the total into the header.
+// The exclusive scan of the W per-word counts, in place, XS_CHUNK words per workgroup: each
+// workgroup first sums the counts of every word before its chunk (L2-resident; the last one of
+// a 5M-Gaussian record reads ~78K words), then scans its chunk; the last workgroup writes the
+// total into the header.
+constexpr int XS_CHUNK = 4096;
 __global__ __launch_bounds__(1024) void xs_scan_kernel(long long W, float *__restrict__ send) {
-  constexpr int PER = 16;
+  constexpr int PER = XS_CHUNK / 1024;
   uint32_t *c = reinterpret_cast<uint32_t *>(send + XS_HDR + 2 * W);
   __shared__ uint32_t wsum[16];
+  __shared__ uint32_t base_s;
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  uint32_t carry = 0;
-  for (long long base = 0; base < W; base += 1024LL * PER) {
-    const long long s0 = base + (long long)threadIdx.x * PER;
-    uint32_t v[PER], tot = 0;
+  const long long c0 = (long long)blockIdx.x * XS_CHUNK;
+  uint32_t before = 0;
+  for (long long k = threadIdx.x; k < c0; k += 1024) before += c[k];
 #pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      v[k] = s0 + k < W ? c[s0 + k] : 0u;
-      tot += v[k];
-    }
-    const uint32_t inc = xs_wave_incl_scan(tot);
-    if (lane == 63) wsum[wv] = inc;
-    __syncthreads();
-    uint32_t before = 0, all = 0;
+  for (int o = 32; o >= 1; o >>= 1) before += __shfl_xor(before, o, 64);
+  if (threadIdx.x == 0) base_s = 0;
+  __syncthreads();
+  if (lane == 0) atomicAdd(&base_s, before);
+  const long long s0 = c0 + (long long)threadIdx.x * PER;
+  uint32_t v[PER], tot = 0;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const uint32_t x = wsum[j];
-      before += j < wv ? x : 0u;
-      all += x;
-    }
-    __syncthreads();  // wsum is rewritten next round
-    uint32_t run = carry + before + inc - tot;
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      if (s0 + k < W) c[s0 + k] = run;
-      run += v[k];
-    }
-    carry += all;
+  for (int k = 0; k < PER; ++k) {
+    v[k] = s0 + k < W ? c[s0 + k] : 0u;
+    tot += v[k];
   }
-  if (threadIdx.x == 0) reinterpret_cast<uint32_t *>(send)[3] = carry;
+  const uint32_t inc = xs_wave_incl_scan(tot);
+  if (lane == 63) wsum[wv] = inc;
+  __syncthreads();  // (also: every wave has read its counts and added to base_s)
+  uint32_t wpre = 0, all = 0;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const uint32_t x = wsum[j];
+    wpre += j < wv ? x : 0u;
+    all += x;
+  }
+  uint32_t run = base_s + wpre + inc - tot;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    if (s0 + k < W) c[s0 + k] = run;
+    run += v[k];
+  }
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0)
+    reinterpret_cast<uint32_t *>(send)[3] = base_s + all;
 }
 
 // The values: each visible Gaussian's colour gradient (as exchange_pack_kernel computes it) at
@@ -855,7 +863,8 @@ extern "C" int gsplat_exchange_sparse_plan(int num_points, const int32_t *radii,
   if (W > 0)
     hipLaunchKernelGGL(xs_mask_kernel, dim3((unsigned)cdiv(W * 64, 256)), dim3(256), 0, st,
                        num_points, radii, send);
-  hipLaunchKernelGGL(xs_scan_kernel, dim3(1), dim3(1024), 0, st, W, send);
+  hipLaunchKernelGGL(xs_scan_kernel, dim3((unsigned)max(1LL, (W + XS_CHUNK - 1) / XS_CHUNK)),
+                     dim3(1024), 0, st, W, send);
   return check_launch("exchange_sparse_plan");
 }
 

@@ -1258,37 +1258,6 @@ __global__ __launch_bounds__(256) void raster_bwd3p_kernel(BWD3P_PARAMS) {
   bwd3p_item<NP, ATOMICS, COLS, SPLIT, PV, DET, CNT, KB>(BWD3P_ARGS, ctile, part, -1);
 }
 
-// The list-split strip backward as resident waves taking work from a queue: entry s of the
-// queue is strip s & 1 of item s >> 1 (the items longest first), fetched by one atomic per
-// wave as the wave finishes its last.  Against one item pair per workgroup dispatched by the
-// hardware, a wave never idles for its workgroup's slowest wave, and no second, partly filled
-// generation of workgroups runs after the first (profiles/r05_bwd_attribution.txt).  The grid
-// is at most the resident capacity; every wave exits once the queue is empty, and the last to
-// exit resets the two counters (n_items[1], n_items[2]: zeroed by the plan as well) for the
-// next launch on this plan.
-// (7 waves per SIMD as the one-item kernel: inlined into the loop the item takes 93 VGPRs)
-template <int NP, bool KB>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) void
-raster_bwd3p_queue_kernel(BWD3P_PARAMS) {
-  int *q = const_cast<int *>(n_items) + 1;
-  const int total = 2 * *n_items;
-  for (;;) {
-    int s = 0;
-    if ((threadIdx.x & 63) == 0) s = atomicAdd(q, 1);
-    s = __builtin_amdgcn_readfirstlane(s);  // (lane 0's: the wave's entry, in an SGPR)
-    if (s >= total) break;
-    const int2 it = items[s >> 1];
-    bwd3p_item<NP, true, 16, true, f2, false, false, KB>(BWD3P_ARGS, it.x, it.y, s & 1);
-  }
-  if ((threadIdx.x & 63) == 0) {
-    const int waves = (int)gridDim.x * (int)(blockDim.x >> 6);
-    if (atomicAdd(q + 1, 1) == waves - 1) {  // every wave has fetched past the end
-      atomicExch(q, 0);
-      atomicExch(q + 1, 0);
-    }
-  }
-}
-
 // ---------------------------------------------------------------- block backward (shipped)
 // The forward's geometry: a wave owns an 8x8 block of its tile (4 waves per tile, one pixel
 // per lane) and walks the block's culled list back to front two staged Gaussians per
@@ -1554,11 +1523,7 @@ __device__ __forceinline__ void split_plan_body(int T, int chunk, const int2 *__
       if (tid >= d) x += y;
     }
     cur[tid] = x - h;
-    if (tid == 63) {
-      n_items[0] = x;
-      n_items[1] = 0;  // the queue backward's counters (raster_bwd3p_queue_kernel)
-      n_items[2] = 0;
-    }
+    if (tid == 63) *n_items = x;
   }
   __syncthreads();
   for (int t = tid; t < T; t += 1024) {
@@ -2105,33 +2070,6 @@ static int bwd_geometry(int tbx, int tby) {
   return (long long)tbx * tby < 3584 ? 1 : 2;
 }
 
-// The queue backward (raster_bwd3p_queue_kernel) when GSPLAT_MI355X_BWD_QUEUE=1 (A/B runs),
-// and its grid: the workgroups the device holds resident at once (occupancy x CUs).
-static bool bwd_queue_on() {
-  static const bool on = [] {
-    const char *e = getenv("GSPLAT_MI355X_BWD_QUEUE");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
-static unsigned bwd_queue_grid(bool kb) {
-  static unsigned cached[2] = {0, 0};
-  unsigned &g = cached[kb ? 1 : 0];
-  if (g == 0) {
-    int dev = 0, cus = 0, per_cu = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (kb)
-      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
-          &per_cu, reinterpret_cast<const void *>(&raster_bwd3p_queue_kernel<1, true>), 256, 0);
-    else
-      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
-          &per_cu, reinterpret_cast<const void *>(&raster_bwd3p_queue_kernel<1, false>), 256, 0);
-    g = (unsigned)std::max(1, cus * std::max(per_cu, 1));
-  }
-  return g;
-}
-
 // The C = 3 backward into the records `rec` (which the caller cleared), with the list split
 // when w != NULL, the integer accumulators when det != NULL (then det_finish_kernel writes the
 // records), the lane-slot counting instantiation when the pair-count hook is on.
@@ -2181,22 +2119,6 @@ static void launch_bwd(hipStream_t st, int tbx, int tby, int H, int W, int n,
     }
 
 #undef BWD8
-  } else if (w && !det && !cnt && bwd_queue_on()) {
-    // resident waves on a work queue (raster_bwd3p_queue_kernel)
-    const unsigned need = cdiv(2 * w->items_bound, 4);
-    if (kb) {
-      const unsigned grid = std::min(need, bwd_queue_grid(kb));
-      hipLaunchKernelGGL((raster_bwd3p_queue_kernel<1, true>), dim3(grid), dim3(256), 0, st, tbx,
-                         tby, H, W, gids, (const int2 *)bins, (const float2 *)xys, conics,
-                         colors, opacity, background, final_Ts, final_idx, v_output,
-                         v_output_alpha, alpha_max, rec, chunk, its, ni, det, kbits, kbw, tl, l1);
-    } else {
-      const unsigned grid = std::min(need, bwd_queue_grid(kb));
-      hipLaunchKernelGGL((raster_bwd3p_queue_kernel<1, false>), dim3(grid), dim3(256), 0, st,
-                         tbx, tby, H, W, gids, (const int2 *)bins, (const float2 *)xys, conics,
-                         colors, opacity, background, final_Ts, final_idx, v_output,
-                         v_output_alpha, alpha_max, rec, chunk, its, ni, det, kbits, kbw, tl, l1);
-    }
   } else {
     const unsigned grid = cdiv(slots, (tiles_per_block<2, 16>()));
 #define BWDS(CH, DET, CNT, KB)                                                             \

@@ -155,9 +155,52 @@ __global__ __launch_bounds__(256) void sh_bwd_views_kernel(int n, int degrees_to
 // sh_bwd_views_kernel<K, true> over a table of dense and sparse view records
 // (exchange_layout.h): the sum runs in table order, skipping a sparse record's absent
 // Gaussians -- exactly zero colour gradients, whose products would add +-0 to an accumulator
-// that is never -0 -- so a table of sparse records gives the dense sum bit for bit.  Views
-// go in groups of XV: every group's mask / prefix loads are issued together, then its
-// value loads, so a wave waits two round trips per group instead of two per view.
+// that is never -0 -- so sparse and dense records of the same views give the same bits.
+// Software-pipelined two views deep: view r + 2's mask word, prefix and camera centre (dense:
+// its colour gradient) are loaded while view r + 1's row is resolved and its colour gradient
+// loaded, while view r's basis and outer product are computed.
+struct XsAhead {  // a view's first-stage loads
+  unsigned long long m;
+  uint32_t pre;
+  float c[3], u[3];
+};
+__device__ __forceinline__ void xs_load_a(const ViewTable &tab, int r, long long n, long long g,
+                                          long long W, XsAhead &a) {
+  const float *p = tab.rec[r];
+  if (tab.cap[r] < 0) {
+    a.c[0] = p[3 * n];
+    a.c[1] = p[3 * n + 1];
+    a.c[2] = p[3 * n + 2];
+    a.u[0] = p[3 * g];
+    a.u[1] = p[3 * g + 1];
+    a.u[2] = p[3 * g + 2];
+    a.m = ~0ull;
+    a.pre = 0u;
+  } else {
+    a.c[0] = p[0];
+    a.c[1] = p[1];
+    a.c[2] = p[2];
+    a.m = reinterpret_cast<const unsigned long long *>(p + XS_HDR)[g >> 6];
+    a.pre = reinterpret_cast<const uint32_t *>(p + XS_HDR + 2 * W)[g >> 6];
+  }
+}
+// second stage: the row of a sparse view and its colour gradient (0 when absent)
+__device__ __forceinline__ bool xs_resolve(const ViewTable &tab, int r, long long n, long long g,
+                                           XsAhead &a) {
+  if (tab.cap[r] < 0) return true;
+  const int b = (int)(g & 63);
+  const bool has = (a.m >> b) & 1ull;
+  const long long pos = (long long)a.pre + __popcll(a.m & ((1ull << b) - 1ull));
+  a.u[0] = a.u[1] = a.u[2] = 0.f;
+  if (has && pos < tab.cap[r]) {
+    const float *vals = tab.rec[r] + xs_values_at(n);
+    a.u[0] = vals[3 * pos];
+    a.u[1] = vals[3 * pos + 1];
+    a.u[2] = vals[3 * pos + 2];
+    return true;
+  }
+  return false;
+}
 template <int K>
 __global__ __launch_bounds__(256) void sh_bwd_table_kernel(int n, int degrees_to_use,
                                                            int num_views,
@@ -169,71 +212,38 @@ __global__ __launch_bounds__(256) void sh_bwd_table_kernel(int n, int degrees_to
   constexpr int ROW = K * 3;
   constexpr int ROWP = sh_row_pitch(K);
   constexpr int SH_THREADS = sh_threads(K);
-  constexpr int XV = 8;
   const long long g0 = (long long)blockIdx.x * SH_THREADS;
   const int cnt = (int)min((long long)SH_THREADS, (long long)n - g0);
   const int t = threadIdx.x;
   if (t < cnt) {
     const long long g = g0 + t;
-    const long long W = xs_words(n), w = g >> 6;
-    const unsigned long long below = (1ull << (g & 63)) - 1ull;
+    const long long W = xs_words(n);
     const float mx = means[3 * g], my = means[3 * g + 1], mz = means[3 * g + 2];
     float acc[ROW];
 #pragma unroll
     for (int k = 0; k < ROW; ++k) acc[k] = 0.f;
-    for (int r0 = 0; r0 < num_views; r0 += XV) {
-      const int nv = min(XV, num_views - r0);
-      float u[XV][3], cp[XV][3];
-      bool has[XV];
-      long long row[XV];
-#pragma unroll
-      for (int j = 0; j < XV; ++j) {  // masks + prefixes (sparse), or the dense row index
-        has[j] = false;
-        row[j] = -1;
-        if (j < nv) {
-          const float *p = tab.rec[r0 + j];
-          const long long cap = tab.cap[r0 + j];
-          if (cap < 0) {
-            has[j] = true;
-            row[j] = g;
-            cp[j][0] = p[3LL * n];
-            cp[j][1] = p[3LL * n + 1];
-            cp[j][2] = p[3LL * n + 2];
-          } else {
-            const unsigned long long m = reinterpret_cast<const unsigned long long *>(p + XS_HDR)[w];
-            const uint32_t pre = reinterpret_cast<const uint32_t *>(p + XS_HDR + 2 * W)[w];
-            const long long pos = (long long)pre + __popcll(m & below);
-            has[j] = ((m >> (g & 63)) & 1ull) && pos < cap;
-            row[j] = pos;
-            cp[j][0] = p[0];
-            cp[j][1] = p[1];
-            cp[j][2] = p[2];
-          }
-        }
+    XsAhead b, a;  // b: view r + 1 (resolved), a: view r + 2 (first stage)
+    xs_load_a(tab, 0, n, g, W, b);
+    bool hb = xs_resolve(tab, 0, n, g, b);
+    if (num_views > 1) xs_load_a(tab, 1, n, g, W, a);
+    for (int r = 0; r < num_views; ++r) {
+      const float c0 = b.c[0], c1 = b.c[1], c2 = b.c[2];
+      const float u0 = b.u[0], u1 = b.u[1], u2 = b.u[2];
+      const bool has = hb;
+      if (r + 1 < num_views) {
+        b = a;
+        hb = xs_resolve(tab, r + 1, n, g, b);
+        if (r + 2 < num_views) xs_load_a(tab, r + 2, n, g, W, a);
       }
+      if (!has) continue;
+      float bs[25];
+      const int nb = sh_basis(degrees_to_use, mx - c0, my - c1, mz - c2, bs);
 #pragma unroll
-      for (int j = 0; j < XV; ++j) {  // the colour gradients
-        u[j][0] = u[j][1] = u[j][2] = 0.f;
-        if (has[j]) {
-          const float *p = tab.rec[r0 + j];
-          const float *vals = tab.cap[r0 + j] < 0 ? p : p + xs_values_at(n);
-          u[j][0] = vals[3 * row[j]];
-          u[j][1] = vals[3 * row[j] + 1];
-          u[j][2] = vals[3 * row[j] + 2];
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < XV; ++j) {
-        if (!has[j]) continue;
-        float b[25];
-        const int nb = sh_basis(degrees_to_use, mx - cp[j][0], my - cp[j][1], mz - cp[j][2], b);
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-          const float bk = k < nb ? b[k] : 0.f;
-          acc[k * 3 + 0] += bk * u[j][0];
-          acc[k * 3 + 1] += bk * u[j][1];
-          acc[k * 3 + 2] += bk * u[j][2];
-        }
+      for (int k = 0; k < K; ++k) {
+        const float bk = k < nb ? bs[k] : 0.f;
+        acc[k * 3 + 0] += bk * u0;
+        acc[k * 3 + 1] += bk * u1;
+        acc[k * 3 + 2] += bk * u2;
       }
     }
     float *rowp = smem + t * ROWP;

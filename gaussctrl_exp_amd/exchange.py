@@ -54,6 +54,11 @@ _ACTIVE: Optional["ShViewExchange"] = None
 
 # a sparse record is used when it is at most this fraction of the dense one
 SPARSE_MAX_FRAC = 0.9
+# after a view whose agreed capacity leaves the sparse record above this fraction of the dense
+# one, the next DENSE_SKIP views skip the plan and the count gather (dense records): the ranks
+# share that history, so they skip together
+DENSE_HOPELESS_FRAC = 0.95
+DENSE_SKIP = 32
 MAX_TABLE = 64  # exchange_layout.h XS_MAX_VIEWS: records per views kernel
 
 
@@ -87,6 +92,7 @@ class ShViewExchange:
         self.geo = None  # multi-view step: the flat geometry gradient summed over this rank's views
         self.record_kinds = {"sparse": 0, "dense": 0}  # views exchanged per record kind (tests)
         self.last_record_floats = None  # length of the last record sent (bench)
+        self._skip = 0  # views left to exchange dense without planning (DENSE_SKIP)
         self._buffers = {}
         self._host_counts = None
 
@@ -149,6 +155,10 @@ class ShViewExchange:
         """Forward, once radii exist: the visibility bitmap of this view's sparse record and the
         async all-gather of every rank's visible count."""
         dev = radii.device
+        if self.sparse != "on" and (self.sparse == "off" or self._skip > 0):
+            self._skip = max(self._skip - 1, 0)
+            self.planned[self.view_index] = None  # dense record, no count gather
+            return
         key = ("send", self.view_index)
         send = self._buffer(key, sparse_floats(n, n), dev)
         _lib.call("gsplat_exchange_sparse_plan", n, _lib.ptr(radii), _lib.ptr(send), stream)
@@ -181,11 +191,16 @@ class ShViewExchange:
         dense) and issue its all-gather (async); reduce_views waits for it."""
         dev = rec.device
         campos = self.campos.to(dev).contiguous()
-        send, _, _ = self.planned[self.view_index]
-        cap = self._capacity(dev)
+        planned = self.planned[self.view_index]
         dense_len = 3 * n + 4
-        use_sparse = self.sparse == "on" or (
-            self.sparse == "auto" and sparse_floats(n, cap) <= SPARSE_MAX_FRAC * dense_len)
+        use_sparse = False
+        if planned is not None:
+            send = planned[0]
+            cap = self._capacity(dev)
+            use_sparse = self.sparse == "on" or (
+                self.sparse == "auto" and sparse_floats(n, cap) <= SPARSE_MAX_FRAC * dense_len)
+            if not use_sparse and sparse_floats(n, cap) > DENSE_HOPELESS_FRAC * dense_len:
+                self._skip = DENSE_SKIP
         if use_sparse:
             length = sparse_floats(n, cap)
             _lib.call("gsplat_exchange_pack_sparse", n, _lib.ptr(rec), rec.numel(),
