@@ -897,7 +897,7 @@ RbPlan rb_plan(int n, int tbx, int tby) {
 // for speed only) and so read that range's depth-ordered boxes through one L2.
 __device__ __forceinline__ void rb_wg(const RbPlan &p, int b, int &r, int &g) {
   const int nreg = p.G + 1;
-  if (p.map == 0 && p.R % 8 == 0) {
+  if (p.map % 10 == 0 && p.R % 8 == 0) {
     const int k = b >> 3;
     r = (b & 7) + 8 * (k / nreg);
     g = k % nreg;
@@ -962,6 +962,12 @@ __device__ __forceinline__ RbSlots rb_slots(uint2 bx, uint32_t c, int rx0, int r
 template <typename F>
 __device__ __forceinline__ void rb_expand(const RbSlots &s, int gw, bool sentinel, int *mk,
                                          F &&f) {
+  rb_expand(s, gw, sentinel, mk, f, [] {});
+}
+// (fin() runs once after the last round: rb_place_kernel completes its pipelined round there)
+template <typename F, typename Fin>
+__device__ __forceinline__ void rb_expand(const RbSlots &s, int gw, bool sentinel, int *mk,
+                                         F &&f, Fin &&fin) {
   const int lane = threadIdx.x & 63;
   uint32_t inc = s.k;
 #pragma unroll
@@ -992,6 +998,7 @@ __device__ __forceinline__ void rb_expand(const RbSlots &s, int gw, bool sentine
     }
     f(j < total, tl, q);
   }
+  fin();
 }
 
 // A wave's depth-ordered walk over [w0, w1): the region filter bit of RB_M x 64 positions is
@@ -1021,7 +1028,7 @@ __device__ __forceinline__ void rb_walk(long long w0, long long w1, const uint32
     uint32_t g = 0u;
     if (q != 0xFFFFFFFFu) {
       s = rb_slots(box[q], cnt[q], rx0, ry0, rx1, ry1, sentinel);
-      if (ORDER) g = order[q];
+      if (ORDER) g = order ? order[q] : q;
     }
     f(s, g);
     return rest;
@@ -1272,19 +1279,43 @@ __global__ __launch_bounds__(RB_NT) void rb_place_kernel(RbPlan p, int n,
   const int width = sentinel ? 0 : 32 - __builtin_clz((uint32_t)max(tg - 1, 1));
   const unsigned long long lt = (1ull << lane) - 1ull;
   const uint32_t bit = sentinel ? 0x80000000u : 1u << (g % 31);
-  rb_walk<true>(w0, w1, rmask, bit, box, cnt, order, rx0, ry0, rx1, ry1, sentinel, queue[wave],
-                [&](const RbSlots &s, uint32_t gid) {
+  // (tuning ablations, p.map / 10 -- timing only, wrong output: 1 no id stores, 2 no ranking,
+  //  3 no id loads, 4 none of the three; tools/exp_rb.py)
+  const int abl = p.map / 10;
+  rb_walk<true>(w0, w1, rmask, bit, box, cnt, abl >= 3 ? nullptr : order, rx0, ry0, rx1, ry1,
+                sentinel, queue[wave], [&](const RbSlots &s, uint32_t gid) {
+    // Software-pipelined one round deep: a round's counter atomics (the leaders of each tile's
+    // lanes reserve their run of the wave's tile counter) go out, then the PREVIOUS round's
+    // returned values are spread to its lanes and its ids stored -- the atomic's LDS round trip
+    // overlaps the next round's owner search, expansion and match instead of stalling the wave.
+    bool pv = false;                  // the pending round: its lane's slot is valid
+    uint32_t pog = 0u, pold = 0u, pbelow = 0u;
+    int pleader = lane;
+    bool pending = false;             // (wave-uniform)
+    auto complete = [&]() {
+      if (!pending) return;
+      const uint32_t pos = __shfl(pold, pleader, 64) + pbelow;
+      if (pv && pos < cap && abl != 1 && abl != 4) ids[pos] = pog;  // (pos < I <= cap always)
+      pending = false;
+    };
     rb_expand(s, rw, sentinel, mk, [&](bool valid, uint32_t tl, int owner) {
       const uint32_t og = __shfl(gid, owner, 64);
+      if (abl == 2 || abl == 4) {
+        if (valid) atomicAdd(&mine[tl], 1u);
+        complete();
+        pv = valid, pog = og, pold = tl, pleader = lane, pbelow = lane, pending = true;
+        return;
+      }
       // the lanes of this round with the same tile, in lane (= list) order
       const unsigned long long peers = digit_peers<RB_TL_BITS>(tl, width, valid);
       const int leader = valid ? (int)__builtin_ctzll(peers) : lane;
       uint32_t old = 0u;
       if (valid && leader == lane) old = atomicAdd(&mine[tl], (uint32_t)__popcll(peers));
-      old = __shfl(old, leader, 64);
-      const uint32_t pos = old + (uint32_t)__popcll(peers & lt);
-      if (valid && pos < cap && p.map != 9) ids[pos] = og;  // (pos < I <= cap always)
-    });
+      complete();
+      pv = valid, pog = og, pold = old, pleader = leader;
+      pbelow = (uint32_t)__popcll(peers & lt);
+      pending = true;
+    }, complete);
   });
 }
 

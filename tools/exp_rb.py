@@ -57,7 +57,7 @@ def main():
             assert ok
             if it >= 5:
                 times.append(e0.elapsed_time(e1))
-            if it == 0 and s[2] != 9:  # (map 9: a timing-only mode without the id stores)
+            if it == 0 and s[2] < 10:  # (map >= 10: timing-only ablations, wrong output)
                 assert torch.equal(spec.ids[:I].cpu(), ref_ids) and \
                     torch.equal(spec.tile_bins.cpu(), ref_bins), s
         times.sort()
