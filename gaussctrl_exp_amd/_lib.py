@@ -6,6 +6,7 @@ something else.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 import subprocess
@@ -14,6 +15,15 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GSPLAT_MI355X_LIB") or os.path.join(_HERE, "libgsplat_mi355x.so")
+# the test library (the same sources built with the gsplat_debug_* switches: hooks())
+HOOKS_PATH = os.environ.get("GSPLAT_MI355X_HOOKS_LIB") or \
+    os.path.join(_HERE, "libgsplat_mi355x_hooks.so")
+# measurement switches for A/B runs of bench.py / tools (applied at load): they exist in the
+# test library only, so setting one loads that library in place of the shipped one
+_SWITCH_ENV = ("GSPLAT_MI355X_RASTER_VARIANT", "GSPLAT_MI355X_CHUNK",
+               "GSPLAT_MI355X_DEPTH_KEY_RANGE")
+if any(os.environ.get(k) for k in _SWITCH_ENV) and not os.environ.get("GSPLAT_MI355X_LIB"):
+    LIB_PATH = HOOKS_PATH
 CSRC = os.path.join(_HERE, "csrc")
 
 _c = ctypes
@@ -52,7 +62,6 @@ SIGNATURES = {
     "gsplat_get_tile_bin_edges": (_I, [_I64, _P, _P, _I64, _P]),
     "gsplat_bin_count_workspace_size": (_SZ, [_I]),
     "gsplat_bin_emit_workspace_size_for": (_SZ, [_I, _I64, _I, _I]),
-    "gsplat_debug_binning_scheme": (_I, [_I]),
     "gsplat_bin_count": (_I, [_I, _P, _P, _P, _P, _I, _I, _P, _P, _SZ, _P]),
     "gsplat_bin_emit": (_I, [_I, _I64, _I, _I, _P, _P, _P, _SZ, _P, _SZ, _P]),
     "gsplat_bin_emit_prelaunch": (_I, [_I, _I64, _I, _I, _P, _P, _SZ, _P, _SZ, _P]),
@@ -68,11 +77,6 @@ SIGNATURES = {
                                           [_P, _SZ, _P, _I64, _I, _P, _SZ, _P]),
     "gsplat_rasterize_backward_chunked": (_I, [_I, _I, _I, _I, _I] + [_P] * 11 + [_F] +
                                           [_P] * 4 + [_I64, _I, _P, _SZ, _P, _SZ, _P]),
-    "gsplat_debug_set_chunk": (_I, [_I]),
-    "gsplat_debug_set_raster_variant": (_I, [_I, _I, _I]),
-    "gsplat_debug_raster_variant_is_default": (_I, []),
-    "gsplat_debug_depth_key_range": (_I, [_I]),
-    "gsplat_debug_wave_log": (_I, [_P]),
     "gsplat_debug_pair_count": (_I, [_P]),
     "gsplat_l1_ssim_num_blocks": (_I, [_I, _I]),
     "gsplat_l1_ssim_forward": (_I, [_I, _I, _I, _P, _P, _P, _F, _I, _P, _P, _P, _P]),
@@ -113,6 +117,16 @@ SIGNATURES = {
                                              [_F, _I64, _I, _P, _SZ, _I, _P, _SZ, _P]),
 }
 
+# the test library's extra entries (include/gsplat_mi355x.h "test hooks", GSPLAT_TEST_HOOKS)
+HOOK_SIGNATURES = {
+    "gsplat_debug_binning_scheme": (_I, [_I]),
+    "gsplat_debug_set_chunk": (_I, [_I]),
+    "gsplat_debug_set_raster_variant": (_I, [_I, _I, _I]),
+    "gsplat_debug_raster_variant_is_default": (_I, []),
+    "gsplat_debug_depth_key_range": (_I, [_I]),
+    "gsplat_debug_wave_log": (_I, [_P]),
+}
+
 ABI_VERSION = 15  # include/gsplat_mi355x.h GSPLAT_MI355X_ABI_VERSION
 
 _lib = None
@@ -136,32 +150,40 @@ def build(jobs: int = 8) -> str:
     return LIB_PATH
 
 
-def lib():
-    global _lib
-    if _lib is None:
-        if not os.path.exists(LIB_PATH):
-            raise RuntimeError(
-                f"gsplat MI355X library not built: {LIB_PATH} is missing "
-                "(run `python -c 'import __graft_entry__ as g; g.build()'`)")
-        L = ctypes.CDLL(LIB_PATH)
-        for name, (res, args) in SIGNATURES.items():
-            # (an older build loaded for a same-box A/B run, GSPLAT_MI355X_LIB, may lack a
-            # newer entry; the shipped library must have every one)
-            if not hasattr(L, name) and (name.startswith("gsplat_debug_") or
-                                         os.environ.get("GSPLAT_MI355X_LIB")):
+def _load(path):
+    """Load and bind a build of the library (shipped or test), apply the quirks and the
+    deterministic setting."""
+    if not os.path.exists(path):
+        raise RuntimeError(
+            f"gsplat MI355X library not built: {path} is missing "
+            "(run `python -c 'import __graft_entry__ as g; g.build()'`)")
+    L = ctypes.CDLL(path)
+    for table in (SIGNATURES, HOOK_SIGNATURES):
+        for name, (res, args) in table.items():
+            # (an older build loaded for a same-box A/B run, GSPLAT_MI355X_LIB, may lack a newer
+            # entry; the shipped library must have every SIGNATURES one)
+            if not hasattr(L, name) and (table is HOOK_SIGNATURES or name.startswith(
+                    "gsplat_debug_") or os.environ.get("GSPLAT_MI355X_LIB")):
                 continue
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
-        if L.gsplat_abi_version() != ABI_VERSION:
-            raise RuntimeError("libgsplat_mi355x.so ABI version mismatch")
-        from . import quirks
-        if L.gsplat_set_quirks(quirks.get()) != 0:
-            raise RuntimeError(L.gsplat_last_error().decode(errors="replace"))
-        L.gsplat_set_deterministic(int(_DETERMINISTIC))
-        # measurement hooks (A/B runs of bench.py / tools): GSPLAT_MI355X_RASTER_VARIANT =
-        # "fwd_pxl,bwd_pxl,flags" (gsplat_debug_set_raster_variant), GSPLAT_MI355X_CHUNK = the
-        # list-split chunk override (gsplat_debug_set_chunk)
+    if L.gsplat_abi_version() != ABI_VERSION:
+        raise RuntimeError(f"{os.path.basename(path)} ABI version mismatch")
+    from . import quirks
+    if L.gsplat_set_quirks(quirks.get()) != 0:
+        raise RuntimeError(L.gsplat_last_error().decode(errors="replace"))
+    L.gsplat_set_deterministic(int(_DETERMINISTIC))
+    return L
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        L = _load(LIB_PATH)
+        # measurement switches (A/B runs; LIB_PATH is then the test library):
+        # GSPLAT_MI355X_RASTER_VARIANT = "fwd_pxl,bwd_pxl,flags" (gsplat_debug_set_raster_variant),
+        # GSPLAT_MI355X_CHUNK = the list-split chunk override (gsplat_debug_set_chunk)
         var = os.environ.get("GSPLAT_MI355X_RASTER_VARIANT")
         if var and L.gsplat_debug_set_raster_variant(*[int(x) for x in var.split(",")]) != 0:
             raise RuntimeError(L.gsplat_last_error().decode(errors="replace"))
@@ -171,6 +193,35 @@ def lib():
             L.gsplat_debug_depth_key_range(int(os.environ["GSPLAT_MI355X_DEPTH_KEY_RANGE"]))
         _lib = L
     return _lib
+
+
+_hooks_lib = None
+
+
+@contextlib.contextmanager
+def hooks():
+    """Run the C ABI through the test library (libgsplat_mi355x_hooks.so: the shipped kernels
+    plus the gsplat_debug_* switches) for the duration: tests that select non-default paths.
+    Yields that library; the switches must be restored before leaving (each test does)."""
+    global _lib, _hooks_lib
+    prev = lib()
+    if _hooks_lib is None:
+        _hooks_lib = _load(HOOKS_PATH)
+    from . import quirks
+    _hooks_lib.gsplat_set_quirks(quirks.get())
+    _hooks_lib.gsplat_set_deterministic(int(_DETERMINISTIC))
+    _lib = _hooks_lib
+    try:
+        yield _hooks_lib
+    finally:
+        _lib = prev
+
+
+def variant_is_default() -> bool:
+    """True while the shipped raster variants are selected (always in the shipped library)."""
+    L = lib()
+    return not hasattr(L, "gsplat_debug_raster_variant_is_default") or \
+        bool(L.gsplat_debug_raster_variant_is_default())
 
 
 def call(name: str, *args) -> int:

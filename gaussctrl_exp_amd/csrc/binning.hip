@@ -2160,6 +2160,7 @@ BinKeys bin_keys_view(void *workspace1, int n) {
 
 using namespace gs;
 
+#ifdef GSPLAT_TEST_HOOKS  // the test library only (libgsplat_mi355x_hooks.so, Makefile)
 // (tuning only, not in the public header) the region binning's plan knobs; -1 = default
 extern "C" void gsplat_tune_rb(int wgs, int regs, int map) {
   g_rb_knobs[0] = wgs;
@@ -2178,6 +2179,7 @@ extern "C" int gsplat_debug_binning_scheme(int scheme) {
   if (scheme >= -1 && scheme <= 1) g_bin_scheme = scheme;
   return prev;
 }
+#endif
 
 extern "C" size_t gsplat_bin_emit_workspace_size_for(int num_points, int64_t num_intersects,
                                                      int tile_bounds_x, int tile_bounds_y) {

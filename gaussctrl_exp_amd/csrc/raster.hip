@@ -611,6 +611,9 @@ struct WaveLog {
   unsigned long long t0;
   __device__ __forceinline__ WaveLog() : t0(__builtin_amdgcn_s_memrealtime()) {}
   __device__ __forceinline__ void done(int slot, const unsigned long long *attr = nullptr) const {
+#ifndef GSPLAT_TEST_HOOKS
+    return;  // (the shipped library has no wave log: gsplat_debug_wave_log is a test hook)
+#endif
     unsigned long long *log = g_wave_log;
     if (GS_ATTR && !attr) return;  // (attribution build: only the strip backward logs)
     if (log && (threadIdx.x & 63) == 0) {
@@ -1921,10 +1924,12 @@ extern "C" size_t gsplat_rasterize_split_bytes(int tile_bounds_x, int tile_bound
       .bytes;
 }
 
+#ifdef GSPLAT_TEST_HOOKS  // the test library only
 extern "C" int gsplat_debug_set_chunk(int chunk) {
   g_chunk_override = chunk;
   return 0;
 }
+#endif
 
 static bool bad_frame(int tbx, int tby, int H, int W) {
   return tbx <= 0 || tby <= 0 || H <= 0 || W <= 0 || (long long)tbx * GS_BLOCK < W ||
@@ -2007,6 +2012,7 @@ extern "C" int gsplat_rasterize_forward_rgbd(int tile_bounds_x, int tile_bounds_
   return check_launch("rasterize_forward_rgbd");
 }
 
+#ifdef GSPLAT_TEST_HOOKS  // the test library only
 // Measurement knob: bwd_pxl picks the backward geometry (BWD_PXL above); bits 20-27 of flags
 // the XCD chunk of the blend kernels' block order (0 the default K = 8, 255 dispatch order).
 extern "C" int gsplat_debug_set_raster_variant(int fwd_pxl, int bwd_pxl, int bwd_flags) {
@@ -2034,6 +2040,7 @@ extern "C" int gsplat_debug_set_raster_variant(int fwd_pxl, int bwd_pxl, int bwd
 }
 
 extern "C" int gsplat_debug_raster_variant_is_default(void) { return default_variants() ? 1 : 0; }
+#endif
 
 extern "C" int gsplat_set_deterministic(int on) {
   g_det = on != 0;
@@ -2041,6 +2048,7 @@ extern "C" int gsplat_set_deterministic(int on) {
 }
 extern "C" int gsplat_get_deterministic(void) { return g_det ? 1 : 0; }
 
+#ifdef GSPLAT_TEST_HOOKS  // the test library only (tools/wave_timeline.py, tools/bwd_attr.py)
 extern "C" int gsplat_debug_wave_log(void *buffer) {
   unsigned long long *p = (unsigned long long *)buffer;
   if (hipMemcpyToSymbol(HIP_SYMBOL(g_wave_log), &p, sizeof(p)) != hipSuccess) {
@@ -2049,6 +2057,7 @@ extern "C" int gsplat_debug_wave_log(void *buffer) {
   }
   return 0;
 }
+#endif
 
 extern "C" int gsplat_debug_pair_count(void *buffer) {
   unsigned long long *p = (unsigned long long *)buffer;

@@ -565,7 +565,7 @@ class _RasterizeGaussians(Function):
         else:
             P = _lib.ptr
             if C == 3 and any(ctx.needs_input_grad) and \
-                    _lib.lib().gsplat_debug_raster_variant_is_default():
+                    _lib.variant_is_default():
                 # the backward accumulates into per-Gaussian gradient records that this blend
                 # zeroes as its waves finish (no memset in the backward; every record, since
                 # gsplat_grad_records_split reads the culled Gaussians' zeros too)

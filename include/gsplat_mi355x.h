@@ -336,9 +336,11 @@ int gsplat_rasterize_forward_clearing(
     float *out_img, float *final_Ts, int32_t *final_idx, void *clear, size_t clear_bytes,
     const int32_t *clear_radii, int64_t num_intersects, int chunk, void *plan,
     size_t plan_bytes, void *stream);
-/* Debug: force the list-split chunk (> 0, rounded up to 64), disable it (< 0) or restore
- * the automatic choice (0). */
+#ifdef GSPLAT_TEST_HOOKS
+/* Test library only: force the list-split chunk (> 0, rounded up to 64), disable it (< 0) or
+ * restore the automatic choice (0). */
 int gsplat_debug_set_chunk(int chunk);
+#endif
 
 size_t gsplat_rasterize_backward_workspace_size(int num_points, int channels);
 int gsplat_rasterize_backward(int tile_bounds_x, int tile_bounds_y, int img_height,
@@ -530,6 +532,13 @@ int gsplat_grad_records_split(int num_points, const void *records, size_t record
                               const float *conics, const float *opacity, float *v_xy,
                               float *v_conic, float *v_colors, float *v_opacity, void *stream);
 
+/* ---- test hooks (not part of the gsplat surface) ------------------------------------------
+ * Exported only by the test library libgsplat_mi355x_hooks.so (the same sources built with
+ * -DGSPLAT_TEST_HOOKS: identical kernels, plus these switches, which select the non-default
+ * paths the parity tests cover and the profiling tools' wave log); the shipped
+ * libgsplat_mi355x.so runs the shipped configuration only.  (gaussctrl_exp_amd/_lib.py
+ * hooks() runs a test against the test library.) */
+#ifdef GSPLAT_TEST_HOOKS
 /* Measurement hook (not part of the gsplat surface): fwd_pxl must be 1 (the forward's 8x8
  * blocks); bwd_pxl selects the C = 3 backward's geometry: 0 = by frame size (shipped: blocks
  * below 3,584 tiles, strips above), 1 = 8x8 blocks, one pixel per lane, two Gaussians per
@@ -560,7 +569,8 @@ int gsplat_debug_binning_scheme(int scheme);
  * 100 MHz), HW_ID, XCC_ID, work slot} as [waves][5] uint64 into the device buffer (NULL
  * disables); the buffer needs 5 entries per launched wave. */
 int gsplat_debug_wave_log(void *buffer);
-/* Debug: lane-slot accounting of the shipped blend kernels (separate counting instantiations,
+#endif  /* GSPLAT_TEST_HOOKS */
+/* Measurement hook (shipped: bench.py's lane_occupancy): lane-slot accounting of the shipped blend kernels (separate counting instantiations,
  * the shipped code is unchanged).  buffer = device u64[6], accumulated by every later forward
  * (clearing) and record backward launch until called again with NULL:
  * [0] backward lane slots (wave iterations x 128 pixel slots), [1] slots whose pixel is live for

@@ -53,3 +53,12 @@ def quirk_mask(request, oracle_lib):
     yield mask
     quirks.set(prev)
     oracle_lib.set_quirks(prev_o)
+
+
+@pytest.fixture
+def hooks():
+    """The test's C-ABI calls go to the test library (libgsplat_mi355x_hooks.so: the shipped
+    kernels plus the gsplat_debug_* switches, include/gsplat_mi355x.h "test hooks")."""
+    from gaussctrl_exp_amd import _lib
+    with _lib.hooks() as L:
+        yield L

@@ -13,21 +13,36 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "gsplat_mi355x.h")
 
 
-def _declared():
-    src = open(HEADER).read()
-    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(gsplat_[a-z0-9_]+)\s*\(", src)))
+def _header_parts():
+    """(shipped text, test-hook text) of the header: the declarations inside the
+    `#ifdef GSPLAT_TEST_HOOKS` sections are the test library's only."""
+    src = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    hooks = "".join(re.findall(r"#ifdef GSPLAT_TEST_HOOKS(.*?)#endif", src, flags=re.S))
+    shipped = re.sub(r"#ifdef GSPLAT_TEST_HOOKS.*?#endif", "", src, flags=re.S)
+    return shipped, hooks
+
+
+def _names(text):
+    return sorted(set(re.findall(r"\b(gsplat_[a-z0-9_]+)\s*\(", text)))
 
 
 def test_library_exports_every_declared_symbol():
+    """The shipped library exports every declared entry point and none of the test hooks; the
+    test library (GSPLAT_TEST_HOOKS) exports both; every declaration has a binding."""
     from gaussctrl_exp_amd import _lib
-    lib = ctypes.CDLL(_lib.LIB_PATH)
-    names = _declared()
-    assert len(names) >= 18
+    shipped, hooks = _header_parts()
+    names, hook_names = _names(shipped), _names(hooks)
+    assert len(names) >= 18 and len(hook_names) >= 5
+    lib = ctypes.CDLL(os.path.join(ROOT, "gaussctrl_exp_amd", "libgsplat_mi355x.so"))
     missing = [n for n in names if not hasattr(lib, n)]
     assert not missing, missing
-    # every declared symbol has a binding signature and vice versa
+    leaked = [n for n in hook_names if hasattr(lib, n)]
+    assert not leaked, leaked
+    hl = ctypes.CDLL(_lib.HOOKS_PATH)
+    missing = [n for n in names + hook_names if not hasattr(hl, n)]
+    assert not missing, missing
     assert set(names) == set(_lib.SIGNATURES)
+    assert set(hook_names) == set(_lib.HOOK_SIGNATURES)
 
 
 def _prototypes():
@@ -44,9 +59,9 @@ def test_binding_arities_match_the_header():
     """ctypes argtypes have exactly as many entries as the C prototypes have parameters."""
     from gaussctrl_exp_amd import _lib
     protos = _prototypes()
-    assert set(protos) == set(_lib.SIGNATURES)
-    wrong = {n: (len(_lib.SIGNATURES[n][1]), k) for n, k in protos.items()
-             if len(_lib.SIGNATURES[n][1]) != k}
+    sigs = {**_lib.SIGNATURES, **_lib.HOOK_SIGNATURES}
+    assert set(protos) == set(sigs)
+    wrong = {n: (len(sigs[n][1]), k) for n, k in protos.items() if len(sigs[n][1]) != k}
     assert not wrong, wrong
 
 
@@ -57,7 +72,7 @@ def test_host_queries_without_gpu():
     assert _lib.query("gsplat_sort_isect_pairs_workspace_size", 0) > 0
 
 
-def test_list_split_policy_without_gpu():
+def test_list_split_policy_without_gpu(hooks):
     """gsplat_rasterize_chunk_size: parts of ~0.6 mean list lengths (a multiple of 64, at least
     256) below 12,288 tiles, no split above (c5's 16,384 tiles) or without intersections; the
     debug override forces / disables it; the plan buffer grows with the part count."""
@@ -71,7 +86,7 @@ def test_list_split_policy_without_gpu():
     for t, i in ((68, 7_717_748), (32, 1_686_461), (50, 123_457)):
         c = q(t, t, i)
         assert c % 64 == 0 and c >= 256
-    L = _lib.lib()
+    L = hooks
     try:
         L.gsplat_debug_set_chunk(100)
         assert q(68, 68, 7_717_748) == 128  # forced, rounded up to 64

@@ -26,7 +26,7 @@ def _run(gpu, sc, cam, deg):
 
 
 @pytest.mark.parametrize("size", [(128, 96, 4000, 3), (512, 512, 30000, 3), (96, 64, 3000, 0)])
-def test_caller_path_fusions_are_exact(gpu, size, monkeypatch):
+def test_caller_path_fusions_are_exact(gpu, size, monkeypatch, hooks):
     W, H, n, deg = size
     sc = synthetic_scene(n, max(deg, 0), seed=5, scale_lo=0.005, scale_hi=0.05)
     cam = synthetic_camera(W, H)

@@ -133,7 +133,7 @@ def test_deterministic_and_atomic_agree(gpu, loss):
 @pytest.mark.parametrize("bwd,mode", [(0, "fused"), (1, "caller"), (2, "caller"),
                                       (1, "fused"), (2, "fused")])
 @pytest.mark.parametrize("chunk", [64, 192])
-def test_list_split_bit_identical_to_the_full_walk(gpu, deterministic, bwd, mode, chunk):
+def test_list_split_bit_identical_to_the_full_walk(gpu, deterministic, bwd, mode, chunk, hooks):
     """The list-split backward re-walks the positions behind each part with the full walk's
     operations, so every wave's per-Gaussian totals -- and the deterministic mode's exact sums of
     them -- equal the unsplit walk's bit for bit (8x8 blocks, 16x8 strips, and the frame-size
@@ -156,7 +156,7 @@ def test_list_split_bit_identical_to_the_full_walk(gpu, deterministic, bwd, mode
 
 @pytest.mark.parametrize("bwd", [1, 2])
 @pytest.mark.parametrize("chunk", [64, 0])
-def test_keep_bits_on_off_bit_identical(gpu, deterministic, bwd, chunk):
+def test_keep_bits_on_off_bit_identical(gpu, deterministic, bwd, chunk, hooks):
     """the list-split backward after a plan-filling forward walks only the positions
     the forward's culls kept (keep bits); the cull is exactness-preserving, so with the keep
     bits off (debug flag bit 30: the backward re-stages and culls every position) the six
@@ -180,7 +180,7 @@ def test_keep_bits_on_off_bit_identical(gpu, deterministic, bwd, chunk):
         np.testing.assert_array_equal(y, x, err_msg=name)
 
 
-def test_keep_bits_switch_between_forward_and_backward(gpu, deterministic):
+def test_keep_bits_switch_between_forward_and_backward(gpu, deterministic, hooks):
     """keep bits switched ON between a forward that did not write them and its
     backward: the backward must not walk the never-written words (it re-stages instead), so the
     gradients equal a run with keep bits off throughout."""

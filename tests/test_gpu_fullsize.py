@@ -52,7 +52,7 @@ def headline(request, gpu, oracle_lib):
 
 
 @pytest.mark.parametrize("scheme", ["shipped", "norange", "range22", "bucket"])
-def test_headline_binning_bitexact(gpu, headline, scheme):
+def test_headline_binning_bitexact(gpu, headline, scheme, hooks):
     """Binning bit-exact at full size: the shipped dispatch (for these scenes the depth sort of
     8-bit reduce-then-scan passes compacting the culled Gaussians away, constant-digit passes
     skipped, then the region binning placing each depth-ordered intersection into its tile

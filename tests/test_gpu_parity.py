@@ -158,7 +158,7 @@ BIN_SETTINGS = {"shipped": -1, "region": 0, "bucket": 1}
 
 @pytest.mark.parametrize("scheme", list(BIN_SETTINGS))
 @pytest.mark.parametrize("case", CASES)
-def test_binning_fused_bitexact(gpu, case, scheme):
+def test_binning_fused_bitexact(gpu, case, scheme, hooks):
     """The binning as dispatched for each case, the depth sort + region binning (each
     depth-ordered intersection placed into its tile list) and the tile buckets with per-tile LDS
     sorts: bit-exact against the oracle's stable sort of gsplat's keys."""
@@ -177,7 +177,7 @@ def test_binning_fused_bitexact(gpu, case, scheme):
     np.testing.assert_array_equal(_np(bins), ref["tile_bins"])
 
 
-def test_binning_inconsistent_allotments(gpu):
+def test_binning_inconsistent_allotments(gpu, hooks):
     """Caller-supplied num_tiles_hit that disagree with the tile boxes (allotments larger than
     the box are padded with the sentinel tile, smaller ones truncate the box): the region
     binning (its sentinel region) and the tile buckets place the same ids, including Gaussians
@@ -208,7 +208,7 @@ def test_binning_inconsistent_allotments(gpu):
 
 
 @pytest.mark.parametrize("scheme", list(BIN_SETTINGS))
-def test_binning_prelaunched_emission(gpu, scheme):
+def test_binning_prelaunched_emission(gpu, scheme, hooks):
     """The emission pre-launched before the host reads I (gsplat_bin_emit_prelaunch into
     buffers of the last call's capacity, then gsplat_bin_emit_finish): bit-exact vs the oracle
     with no capacity (first call: gsplat_bin_emit), a capacity of exactly I, a larger one, and
@@ -240,7 +240,7 @@ def test_binning_prelaunched_emission(gpu, scheme):
 
 @pytest.mark.parametrize("fixed", [(0x5A00, 0xFF00), (0x5A0000, 0xFF0000),
                                    (0x5A5A00, 0xFFFF00), (0x0, 0x0)])
-def test_binning_depth_key_range(gpu, fixed):
+def test_binning_depth_key_range(gpu, fixed, hooks):
     """Depth keys whose bytes 1 (and 2) are the same for every visible Gaussian (byte 3 always
     is here): those LSD passes move nothing (gsplat_debug_depth_key_range; the device picks
     every pass's buffers, DevIO), also in the middle of the pass sequence, and with only pass 0
@@ -360,7 +360,7 @@ def test_raster_backward(gpu, case, quirk_mask):
 @pytest.mark.parametrize("quirk_mask", [7, 0], indirect=True)
 @pytest.mark.parametrize("bwd", [1, 2])
 @pytest.mark.parametrize("case", CASES)
-def test_raster_backward_geometries(gpu, case, bwd, quirk_mask):
+def test_raster_backward_geometries(gpu, case, bwd, quirk_mask, hooks):
     """Both shipped backward geometries on every case, whatever the frame size picks: 8x8 blocks
     (bwd 1, small frames) and 16x8 strips (bwd 2, from 3,584 tiles)."""
     _lib.call("gsplat_debug_set_raster_variant", 1, bwd, 0)
@@ -379,7 +379,7 @@ RASTER_VARIANTS = [(1, 0, 255 << 20), (1, 0, 1 << 20), (1, 0, 3 << 20)]
 @pytest.mark.ablation
 @pytest.mark.parametrize("variant", RASTER_VARIANTS)
 @pytest.mark.parametrize("case", [CASES[0], CASES[1], CASES[3]])
-def test_raster_variants(gpu, case, variant):
+def test_raster_variants(gpu, case, variant, hooks):
     """Every blend-kernel block order reachable through gsplat_debug_set_raster_variant meets the
     same bar as the shipped one."""
     _lib.call("gsplat_debug_set_raster_variant", *variant)
@@ -430,7 +430,7 @@ def _check_raster_backward(gpu, case):
 @pytest.mark.parametrize("bwd", [1, 2])
 @pytest.mark.parametrize("chunk", [64, 128, 256])
 @pytest.mark.parametrize("case", CASES[1:3])
-def test_raster_backward_list_split(gpu, case, chunk, bwd):
+def test_raster_backward_list_split(gpu, case, chunk, bwd, hooks):
     """The list-split backward (parts of a forced chunk size, each re-walking the positions
     behind it; 8x8 block waves or, bwd 2, 16x8 strips): identical forward, gradients within the
     same bar vs the oracle."""

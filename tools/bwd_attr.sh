@@ -8,7 +8,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 if [ "$1" = build ]; then
   mkdir -p ab/attr
   make -s -C gaussctrl_exp_amd/csrc BUILD=../../ab/attr OUT=../../ab/libattr.so \
-    EXTRA=-DGS_BWD_ATTR ../../ab/libattr.so
+    EXTRA="-DGS_BWD_ATTR -DGSPLAT_TEST_HOOKS" ../../ab/libattr.so
   exit 0
 fi
 mkdir -p gpurun_out

@@ -3,6 +3,10 @@
 fraction of Gaussians whose records differ beyond 1e-4 relative, and a few examples."""
 import os, sys
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+# the gsplat_debug_* switches live in the test library (include/gsplat_mi355x.h "test hooks")
+os.environ.setdefault("GSPLAT_MI355X_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                        "..", "gaussctrl_exp_amd",
+                                                        "libgsplat_mi355x_hooks.so"))
 import numpy as np
 import torch
 import bench

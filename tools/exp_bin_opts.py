@@ -4,6 +4,10 @@ forced (gsplat_debug_binning_scheme -1 / 0 / 1); outputs must stay identical.  C
 (default "c2 c3 headline")."""
 import os, sys
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+# the gsplat_debug_* switches live in the test library (include/gsplat_mi355x.h "test hooks")
+os.environ.setdefault("GSPLAT_MI355X_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                        "..", "gaussctrl_exp_amd",
+                                                        "libgsplat_mi355x_hooks.so"))
 import torch
 import bench
 from gaussctrl_exp_amd import _lib

@@ -3,6 +3,10 @@ block backward vs the 16x8-strip kernel): gradient agreement and interleaved tim
 bench config (CFG)."""
 import os, sys
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+# the gsplat_debug_* switches live in the test library (include/gsplat_mi355x.h "test hooks")
+os.environ.setdefault("GSPLAT_MI355X_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                        "..", "gaussctrl_exp_amd",
+                                                        "libgsplat_mi355x_hooks.so"))
 import numpy as np
 import torch
 import bench

@@ -9,6 +9,10 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+# the gsplat_debug_* switches live in the test library (include/gsplat_mi355x.h "test hooks")
+os.environ.setdefault("GSPLAT_MI355X_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                        "..", "gaussctrl_exp_amd",
+                                                        "libgsplat_mi355x_hooks.so"))
 import bench  # noqa: E402
 from gaussctrl_exp_amd import _lib, timing  # noqa: E402
 from gaussctrl_exp_amd.project_gaussians import project_gaussians  # noqa: E402

@@ -67,4 +67,5 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    with _lib.hooks():  # (gsplat_tune_rb: the test library)
+        main()

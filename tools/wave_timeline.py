@@ -4,6 +4,10 @@ geometries (gsplat_debug_set_raster_variant bwd_pxl: 1 blocks, 2 strips), CFG th
 config."""
 import os, sys
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+# the gsplat_debug_* switches live in the test library (include/gsplat_mi355x.h "test hooks")
+os.environ.setdefault("GSPLAT_MI355X_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                        "..", "gaussctrl_exp_amd",
+                                                        "libgsplat_mi355x_hooks.so"))
 import numpy as np
 import torch
 import bench
