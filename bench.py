@@ -111,8 +111,11 @@ def algorithmic_bytes(N, I, P, T, K, nvis):
     """Per-view algorithmic HBM bytes of each C-ABI entry point (SURVEY.md §8d model; the
     binning entries count every radix pass's key/value reads and writes)."""
     tile_passes = max(1, -(-max(1, (T - 1).bit_length()) // 8))  # 8-bit digits of the tile id
-    # the tile buckets (gsplat_debug_binning_scheme; shipped for N <= 2^17 on <= 16,447 tiles)
-    setting = int(_lib.lib().gsplat_debug_binning_scheme(-2))
+    # the tile buckets (shipped for N <= 2^17 on <= 16,447 tiles; the test library's
+    # gsplat_debug_binning_scheme can force either scheme)
+    L = _lib.lib()
+    setting = int(L.gsplat_debug_binning_scheme(-2)) if \
+        hasattr(L, "gsplat_debug_binning_scheme") else -1
     bucket = setting == 1 or (setting == -1 and N <= (1 << 17) and T + 1 <= 16448)
     if bucket:
         # count: allotment + visibility sums over the records and keys (20 N); emit: the

@@ -215,6 +215,14 @@ def hooks():
         yield _hooks_lib
     finally:
         _lib = prev
+        # (settings changed meanwhile reached the test library only)
+        prev.gsplat_set_quirks(quirks.get())
+        prev.gsplat_set_deterministic(int(_DETERMINISTIC))
+
+
+def hooks_active() -> bool:
+    """True inside hooks(): the C ABI (and the torch op layer) run on the test library."""
+    return _lib is not None and _lib is _hooks_lib
 
 
 def variant_is_default() -> bool:

@@ -23,6 +23,14 @@
 
 #include "../../include/gsplat_mi355x.h"
 
+// The op namespace: gsplat_mi355x, or gsplat_mi355x_hooks for the copy linked against the test
+// library (Makefile: libgsplat_torch_ops_hooks.so; gaussctrl_exp_amd/ops.py under _lib.hooks()).
+#ifndef GSPLAT_OPS_NS
+#define GSPLAT_OPS_NS gsplat_mi355x
+#endif
+#define GS_TORCH_LIBRARY(ns, m) TORCH_LIBRARY(ns, m)
+#define GS_TORCH_LIBRARY_IMPL(ns, k, m) TORCH_LIBRARY_IMPL(ns, k, m)
+
 namespace {
 
 using at::Tensor;
@@ -375,7 +383,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> raster_bwd_meta(
 
 }  // namespace
 
-TORCH_LIBRARY(gsplat_mi355x, m) {
+GS_TORCH_LIBRARY(GSPLAT_OPS_NS, m) {
   m.def("project_fwd(Tensor means3d, Tensor scales, float glob_scale, Tensor quats, "
         "Tensor viewmat, Tensor projmat, float fx, float fy, float cx, float cy, int img_height, "
         "int img_width, int tile_bounds_x, int tile_bounds_y, float clip_thresh) -> "
@@ -403,7 +411,7 @@ TORCH_LIBRARY(gsplat_mi355x, m) {
         "(Tensor v_xy, Tensor v_conic, Tensor v_colors, Tensor v_opacity)");
 }
 
-TORCH_LIBRARY_IMPL(gsplat_mi355x, CUDA, m) {  // the ROCm device dispatch key
+GS_TORCH_LIBRARY_IMPL(GSPLAT_OPS_NS, CUDA, m) {  // the ROCm device dispatch key
   m.impl("project_fwd", &project_fwd);
   m.impl("project_bwd", &project_bwd);
   m.impl("sh_fwd", &sh_fwd);
@@ -415,7 +423,7 @@ TORCH_LIBRARY_IMPL(gsplat_mi355x, CUDA, m) {  // the ROCm device dispatch key
   m.impl("raster_bwd", &raster_bwd);
 }
 
-TORCH_LIBRARY_IMPL(gsplat_mi355x, Meta, m) {
+GS_TORCH_LIBRARY_IMPL(GSPLAT_OPS_NS, Meta, m) {
   m.impl("project_fwd", &project_fwd_meta);
   m.impl("project_bwd", &project_bwd_meta);
   m.impl("sh_fwd", &sh_fwd_meta);
