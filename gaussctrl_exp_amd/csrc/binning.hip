@@ -85,9 +85,11 @@ __device__ __forceinline__ unsigned long long digit_peers(uint32_t d, int width,
 }
 
 // Single workgroup: exclusive scan of partial[0..nb) in place; grand total -> *total.
+// (in_place false: only the total, partial[] left as the block sums)
 __global__ __launch_bounds__(1024) void scan_partials_kernel(uint32_t *__restrict__ partial,
                                                              int nb, uint32_t *__restrict__ total_out,
-                                                             uint32_t *__restrict__ total_dev = nullptr) {
+                                                             uint32_t *__restrict__ total_dev = nullptr,
+                                                             bool in_place = true) {
   __shared__ uint32_t lds[16];
   uint32_t running = 0;
   for (int c = 0; c < nb; c += 1024) {
@@ -95,7 +97,7 @@ __global__ __launch_bounds__(1024) void scan_partials_kernel(uint32_t *__restric
     uint32_t v = i < nb ? partial[i] : 0u;
     uint32_t tot;
     uint32_t ex = block_exclusive_scan<1024>(v, tot, lds);
-    if (i < nb) partial[i] = running + ex;
+    if (in_place && i < nb) partial[i] = running + ex;
     running += tot;
   }
   if (threadIdx.x == 0) {
@@ -222,7 +224,9 @@ __global__ __launch_bounds__(TPB) void rts_count_kernel(const K *__restrict__ ke
   if (io.fin && pass > 0) keys = (const K *)(data_in_b(io, pass) ? io.kb : io.ka);
   const long long base = (long long)blockIdx.x * TPB * ITEMS;
   K k[ITEMS];
-  if (n_dev) n = min(n, (long long)*n_dev);  // (the compacted length)
+  // (the compacted length; above the launch length n: an overflowed capacity launch, which
+  // sorts nothing)
+  if (n_dev) n = (long long)*n_dev > n ? 0 : (long long)*n_dev;
   const int R = 1 << width;
   const uint32_t dmask = (uint32_t)(R - 1);
   h[tid] = 0;
@@ -371,7 +375,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
   // Gaussians), and block 0 stores the kept count to n_out; later passes sort min(n, *n_dev)
   // keys and the workgroups past them exit at once.
   if (n_dev) {
-    n = min(n, (long long)*n_dev);
+    n = (long long)*n_dev > n ? 0 : (long long)*n_dev;  // (see rts_count_kernel)
     if ((long long)blockIdx.x * TPB * ITEMS >= n) return;  // whole workgroup
   }
   if (digit_constant(kfin, shift, width)) {  // every key has the same digit: a stable copy
@@ -528,11 +532,14 @@ uint32_t *sort_kept_word(void *ws) { return (uint32_t *)ws + 1; }
 // out all-ones keys, so the sort orders only the kept keys, whose count it stores to
 // sort_kept_word(ws) (the sorted output holds that many; kout may be null).
 // assume_const / range_out (drop only): gsplat_bin_count_keyed_ex's depth-key range.
+// n_dev_all (no drop): the key count on the device, n the launch length (a capacity): every pass
+// sorts *n_dev_all keys, none when it exceeds n.
 template <typename K>
 int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t *vout,
                      long long n, int begin_bit, int end_bit, void *ws, hipStream_t st,
                      bool first_counts_ready = false, bool drop = false,
-                     uint32_t assume_const = 0, int32_t *range_out = nullptr) {
+                     uint32_t assume_const = 0, int32_t *range_out = nullptr,
+                     const uint32_t *n_dev_all = nullptr) {
   if (n <= 0) return 0;
   const SortPlan p = sort_plan(n, begin_bit, end_bit);
   if (p.passes == 0) {
@@ -569,7 +576,7 @@ int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t
     uint32_t *vo = last ? vout : valt;
     // tile digit counts -> row scans -> offsets
     const int sh = begin_bit + q * p.width;
-    const uint32_t *ndev = drop && q > 0 ? kept : nullptr;
+    const uint32_t *ndev = drop ? (q > 0 ? kept : nullptr) : n_dev_all;
     // first_counts_ready: the key kernel wrote pass 0's counts and key ranges (kr.blk)
     if (q == 0 && first_counts_ready) {
     } else if (p.items == 16)
@@ -803,6 +810,144 @@ __device__ __forceinline__ int slot_owner(int *mk, uint32_t j0, uint32_t rel, bo
   const int own = max(wave_incl_max(mk[lane]), carry);
   carry = __builtin_amdgcn_readlane(own, 63);
   return own & 63;
+}
+
+// ------------------------------------------------------------------ tile sort (shipped)
+// The depth-ordered Gaussians -> gsplat's tile lists by emitting every intersection as a
+// (tile, id) pair in depth order and sorting the pairs stably by tile:
+//   ts_emit_kernel   one workgroup per 256 depth-ordered Gaussians: their intersection offsets
+//                    (the per-1,024-block allotment sums of gather_counts_kernel plus a block
+//                    scan -- no separate scan launches), then each wave fills its 64 Gaussians'
+//                    combined slot range with lanes striding over it (slot owners from
+//                    slot_owner), so the pair stores are coalesced; the tile table is cleared
+//                    on the way; workgroup 0 publishes I.
+//   radix_sort_pairs the stable LSD sort of the pairs by tile id (ceil(log2(T + 1)) bits: two
+//                    passes up to 16,383 tiles), launched at the capacity with the device count
+//                    as its length (n_dev_all): no host read of I before it.
+//   ts_bins_kernel   the tile table from the runs of equal sorted keys.
+// Stable sort of depth-ordered pairs by tile = gsplat's order (ties by Gaussian id), bit for
+// bit.  Against the region binning below (measured round 5, same box, tools/exp_rb.py): the
+// headline 0.22 vs 0.24 ms, c4 garden ~0.30 vs 0.39 ms -- the region binning's per-(depth
+// range, region) workgroups are imbalanced on real scenes and its in-order ranking costs a
+// returning LDS atomic per round; the sort's passes are coalesced and balanced by construction.
+// partial[]: gather_counts_kernel's per-1,024-Gaussian block sums, scanned here by every
+// workgroup (<= a few loads per thread); workgroup 0 publishes their total I to i_dev and
+// i_host (the speculative binning; after a count phase that found I already, the same value).  i_dev > cap (an overflow, or a
+// depth-key digit the sort assumed constant that varied: i_dev = ~0): nothing is emitted.
+__global__ __launch_bounds__(TPB) void ts_emit_kernel(int n, int nb,
+                                                      const uint32_t *__restrict__ order,
+                                                      const uint32_t *__restrict__ cnt,
+                                                      const uint32_t *__restrict__ partial,
+                                                      const uint2 *__restrict__ box, int tbx,
+                                                      int tby, uint32_t *__restrict__ tkeys,
+                                                      uint32_t *__restrict__ tvals,
+                                                      int *__restrict__ tile_bins,
+                                                      uint32_t *__restrict__ i_dev,
+                                                      int32_t *__restrict__ i_host, uint32_t cap,
+                                                      const uint32_t *__restrict__ kfin,
+                                                      uint32_t assume) {
+  __shared__ uint32_t lds[TPB / 64];
+  __shared__ int marks[TPB];
+  for (long long i = (long long)blockIdx.x * TPB + threadIdx.x; i < 2LL * tbx * tby;
+       i += (long long)gridDim.x * TPB)
+    tile_bins[i] = 0;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int t = (int)(blockIdx.x / SC_ITEMS), rr = (int)(blockIdx.x % SC_ITEMS);
+  const long long b0 = (long long)t * SC_TILE;
+  const long long p = b0 + (long long)rr * TPB + tid;
+  uint32_t cr[SC_ITEMS];  // this 1,024-block's allotments up to this round (all loads at once)
+#pragma unroll
+  for (int r = 0; r < SC_ITEMS; ++r) {
+    const long long pr = b0 + r * TPB + tid;
+    cr[r] = (r <= rr && pr < n) ? cnt[pr] : 0u;
+  }
+  uint32_t pre = 0, tot = 0;
+  for (int k = tid; k < nb; k += TPB) {
+    const uint32_t v = partial[k];
+    tot += v;
+    pre += k < t ? v : 0u;
+  }
+  uint32_t c = 0;
+#pragma unroll
+  for (int r = 0; r < SC_ITEMS; ++r) {
+    if (r < rr) pre += cr[r];
+    if (r == rr) c = cr[r];
+  }
+  uint32_t bpre, btot;
+  block_exclusive_scan<TPB>(pre, bpre, lds);  // (only the totals are used)
+  block_exclusive_scan<TPB>(tot, btot, lds);
+  const bool violated = assume && kfin && (((kfin[0] ^ kfin[1]) & assume) != 0u);
+  if (blockIdx.x == 0 && tid == 0) {
+    *i_dev = violated ? 0xFFFFFFFFu : btot;
+    if (i_host) *i_host = (int32_t)btot;
+  }
+  if (violated || btot > cap) return;  // workgroup-uniform
+  uint32_t rtot;
+  const uint32_t start = bpre + block_exclusive_scan<TPB>(c, rtot, lds);
+  const long long p0 = p - lane;
+  if (p0 >= n) return;  // wave-uniform (no barrier below)
+  const bool in = p < n;
+  uint32_t g = 0;
+  uint2 bx = make_uint2(0u, 0u);
+  if (in && c) {
+    g = order[p];
+    bx = box[p];
+  }
+  const uint32_t base = __shfl(start, 0, 64);
+  const int last_lane = (int)min(63LL, (long long)n - 1 - p0);
+  const uint32_t total = __shfl(start + c, last_lane, 64) - base;
+  const uint32_t rel = in ? start - base : total;
+  int *mk = marks + (threadIdx.x & ~63);
+  mk[lane] = -1;
+  int carry = -1;
+  for (uint32_t j0 = 0; j0 < total; j0 += 64) {
+    const uint32_t j = j0 + lane;
+    const int q = slot_owner(mk, j0, rel, c != 0u, carry);
+    const uint32_t li = j - __shfl(rel, q, 64);
+    const uint32_t q0 = __shfl(bx.x, q, 64), q1 = __shfl(bx.y, q, 64);
+    const uint32_t qg = __shfl(g, q, 64);
+    const int qx0 = (int)(q0 & 0xFFFFu), qy0 = (int)(q0 >> 16);
+    const int qx1 = (int)(q1 & 0xFFFFu), qy1 = (int)(q1 >> 16);
+    const int qbw = max(qx1 - qx0, 1);
+    const int qarea = max(qx1 - qx0, 0) * max(qy1 - qy0, 0);
+    uint32_t tile;
+    if ((int)li < qarea) {  // li / qbw as in rb_slots (exact below 2^20)
+      const int ly = li < (1u << 20)
+                         ? (int)(((float)li + 0.5f) * __builtin_amdgcn_rcpf((float)qbw))
+                         : (int)li / qbw;
+      tile = (uint32_t)((qy0 + ly) * tbx + qx0 + ((int)li - ly * qbw));
+    } else {
+      tile = (uint32_t)(tbx * tby);  // an allotment past its box: the sentinel tile
+    }
+    if (j < total) {
+      tkeys[base + j] = tile;
+      tvals[base + j] = qg;
+    }
+  }
+}
+
+// The tile table from the sorted keys (tile ids; the sentinel T has no row): [first, last + 1)
+// per non-empty tile, the cleared (0, 0) elsewhere.  n_dev: the device count of a
+// capacity-launched sort (cap the launch length; above it the table stays cleared).
+__global__ __launch_bounds__(TPB) void ts_bins_kernel(long long cap, const uint32_t *__restrict__ keys,
+                                                      int *__restrict__ bins, long long T,
+                                                      const uint32_t *__restrict__ n_dev) {
+  long long n = cap;
+  if (n_dev) {
+    if ((long long)*n_dev > cap) return;
+    n = *n_dev;
+  }
+  const long long k = (long long)blockIdx.x * TPB + threadIdx.x;
+  if (k >= n) return;
+  const long long cur = keys[k];
+  if (k == 0 && cur < T) bins[2 * cur] = 0;
+  if (k == n - 1 && cur < T) bins[2 * cur + 1] = (int)n;
+  if (k == 0) return;
+  const long long prev = keys[k - 1];
+  if (prev != cur) {
+    if (prev < T) bins[2 * prev + 1] = (int)k;
+    if (cur < T) bins[2 * cur] = (int)k;
+  }
 }
 
 // ------------------------------------------------------------------ region binning
@@ -2112,17 +2257,65 @@ BkWs carve_bk(void *base, int n, long long I, long long T) {
   return w;
 }
 
+struct TsWs {
+  uint32_t *ka, *va, *kb, *vb, *kout;
+  void *rs;
+  size_t bytes;
+};
+TsWs carve_ts(void *base, long long cap, long long T) {
+  TsWs w;
+  Carver c(base);
+  const size_t ii = (size_t)(cap > 0 ? cap : 1) * sizeof(uint32_t);
+  w.ka = c.take<uint32_t>(ii);
+  w.va = c.take<uint32_t>(ii);
+  w.kb = c.take<uint32_t>(ii);
+  w.vb = c.take<uint32_t>(ii);
+  w.kout = c.take<uint32_t>(ii);
+  // (any sort length up to cap: the short-tile plan below 2^22 keys has more tiles)
+  const long long c1 = cap > 0 ? cap : 1, c0 = c1 < (4LL << 20) ? c1 : (4LL << 20) - 1;
+  const size_t r0 = radix_ws_bytes(c0, 0, bits_for(T)), r1 = radix_ws_bytes(c1, 0, bits_for(T));
+  w.rs = c.take<char>(r0 > r1 ? r0 : r1);
+  w.bytes = c.off;
+  return w;
+}
+
+// The tile sort (ts_*) over phase 1's depth-ordered allotments into workspace2 (carve_ts at the
+// capacity).  HEAD: the emission (I published to p1.dcount and i_host); TAIL: the
+// sort and the tile table over m pairs: with n_dev, *n_dev of them (I on the device; m = cap,
+// the launch length), else exactly m = I.
+void ts_launch(int n, const Phase1 &p1, void *ws2, int32_t *ids, int32_t *tile_bins, int tbx,
+               int tby, long long cap, long long m, int32_t *i_host, uint32_t assume,
+               bool head, bool tail, const uint32_t *n_dev, hipStream_t st) {
+  const long long T = (long long)tbx * tby;
+  const TsWs w = carve_ts(ws2, cap, T);
+  const int nb = (int)cdiv(n, SC_TILE);
+  if (head)
+    hipLaunchKernelGGL(ts_emit_kernel, dim3((unsigned)nb * SC_ITEMS), dim3(TPB), 0, st, n, nb,
+                       p1.order, p1.cnt, rts_tile_counts(p1.rs_ws), p1.box,
+                       tbx, tby, w.ka, w.va, tile_bins, p1.dcount, i_host,
+                       (uint32_t)(cap > 0xFFFFFFFELL ? 0xFFFFFFFELL : cap),
+                       assume ? sort_kept_word(p1.rs_ws) + 1 : nullptr, assume);
+  if (!tail || m <= 0) return;
+  radix_sort_pairs<uint32_t>(w.ka, w.va, w.kb, w.vb, w.kout, (uint32_t *)ids, m, 0, bits_for(T),
+                             w.rs, st, false, false, 0u, nullptr, n_dev);
+  hipLaunchKernelGGL(ts_bins_kernel, dim3((unsigned)cdiv(m, TPB)), dim3(TPB), 0, st, m, w.kout,
+                     tile_bins, T, n_dev);
+}
+
 // Binning scheme (gsplat_debug_binning_scheme): -1 by size (shipped), 0 depth sort + tile sort,
 // 1 tile buckets + per-tile sorts.  The buckets need far fewer launches (8 against ~23), which
 // wins where every launch is short: small scenes, whose tile lists are short too (c2, 100k
 // Gaussians @ 512^2, max list 837: 0.100 vs 0.112 ms).  A long list is sorted by one
 // workgroup, so real scenes lose (c3 bear, 300k, max list 7,984: 0.365 vs 0.144 ms; headline
 // 1M: 0.287 vs 0.243); the cut is on N, which the count phase must know before I exists.
+// 2: the region binning in place of the tile sort (kept for A/B: slower on every config, see
+// ts_emit_kernel).
 int g_bin_scheme = -1;
 bool use_bucket(long long n, long long T) {
   if (T + 1 > BK_MAX_BUCKETS) return false;
   return g_bin_scheme < 0 ? n <= (1LL << 17) : g_bin_scheme == 1;
 }
+bool use_region(long long n, long long T) { return g_bin_scheme == 2 && !use_bucket(n, T); }
 
 // The region binning (rb_*) over phase 1's depth-ordered records into workspace2
 // (rb_ws_bytes): head = count, column scan, tile table (no I-sized buffer: they can run before
@@ -2176,7 +2369,7 @@ extern "C" int gsplat_debug_depth_key_range(int on) {
 
 extern "C" int gsplat_debug_binning_scheme(int scheme) {
   const int prev = g_bin_scheme;
-  if (scheme >= -1 && scheme <= 1) g_bin_scheme = scheme;
+  if (scheme >= -1 && scheme <= 2) g_bin_scheme = scheme;
   return prev;
 }
 #endif
@@ -2185,7 +2378,9 @@ extern "C" size_t gsplat_bin_emit_workspace_size_for(int num_points, int64_t num
                                                      int tile_bounds_x, int tile_bounds_y) {
   const long long T = (long long)tile_bounds_x * tile_bounds_y;
   if (num_points < 0 || num_intersects < 0 || tile_bounds_x <= 0 || tile_bounds_y <= 0) return 0;
-  const size_t sorted = rb_ws_bytes(rb_plan(num_points, tile_bounds_x, tile_bounds_y));
+  const size_t rb = rb_ws_bytes(rb_plan(num_points, tile_bounds_x, tile_bounds_y));
+  const size_t ts = carve_ts(nullptr, num_intersects, T).bytes;
+  const size_t sorted = rb > ts ? rb : ts;  // (either may run: the scheme is a test-hooks switch)
   if (!use_bucket(num_points, T)) return sorted;
   const size_t bk = carve_bk(nullptr, num_points, num_intersects, T).bytes;
   return bk > sorted ? bk : sorted;
@@ -2270,11 +2465,14 @@ static int bin_count_impl(int num_points, const float *xys, const float *depths,
   uint32_t *partial = rts_tile_counts(p.rs_ws);  // the sort is done with its tile counts
   const RbPlan rp = rb_plan(n, tile_bounds_x, tile_bounds_y);
   hipLaunchKernelGGL(gather_counts_kernel, dim3(nb), dim3(TPB), 0, st, n, p.order, kept, p.rec,
-                     p.cnt, p.box, d_counts, partial, p.rmask, rp.gw, rp.gh, rp.gxn);
-  if (no_scan) return check_launch("bin_count");  // (the speculative binning: I from rb_tiles)
-  // I = the sum of the allotments (the region binning needs no per-Gaussian offsets)
+                     p.cnt, p.box, d_counts, partial, use_region(n, T) ? p.rmask : nullptr, rp.gw,
+                     rp.gh, rp.gxn);
+  // (the speculative binning: I from ts_emit_kernel / rb_tiles_kernel)
+  if (no_scan) return check_launch("bin_count");
+  // I = the sum of the block sums, which stay as they are: the emission (ts_emit_kernel)
+  // scans them itself, so a speculative count phase (no_scan) and this one leave the same state
   hipLaunchKernelGGL(scan_partials_kernel, dim3(1), dim3(1024), 0, st, partial, nb,
-                     (uint32_t *)(d_counts + 1), p.dcount);
+                     (uint32_t *)(d_counts + 1), p.dcount, false);
   return check_launch("bin_count");
 }
 
@@ -2339,19 +2537,26 @@ extern "C" int gsplat_bin_speculative(int num_points, int64_t capacity, int tile
                          workspace2, workspace2_bytes, stream, EMIT_SPEC);
   }
   Phase1 p1 = carve_phase1(workspace1, num_points);
+  const bool region = use_region(num_points, T);
   const RbPlan rp = rb_plan(num_points, tile_bounds_x, tile_bounds_y);
-  if (workspace1_bytes < p1.bytes || workspace2_bytes < rb_ws_bytes(rp)) {
+  const size_t need2 = region ? rb_ws_bytes(rp) : carve_ts(nullptr, capacity, T).bytes;
+  if (workspace1_bytes < p1.bytes || workspace2_bytes < need2) {
     set_error("bin_speculative: workspaces %zu/%zu < %zu/%zu bytes", workspace1_bytes,
-              workspace2_bytes, p1.bytes, rb_ws_bytes(rp));
+              workspace2_bytes, p1.bytes, need2);
     return 1;
   }
   if (bin_count_impl(num_points, nullptr, nullptr, nullptr, nullptr, tile_bounds_x,
                      tile_bounds_y, d_counts, workspace1, workspace1_bytes, true, stream,
                      assume_const, true, true))
     return 1;
-  rb_launch(rp, num_points, p1, workspace2, gaussian_ids_sorted, tile_bins,
-            (unsigned long long)capacity, d_counts + 1,
-            use_key_range(num_points) ? assume_const : 0u, true, true, st);
+  const uint32_t assume = use_key_range(num_points) ? assume_const : 0u;
+  if (region)
+    rb_launch(rp, num_points, p1, workspace2, gaussian_ids_sorted, tile_bins,
+              (unsigned long long)capacity, d_counts + 1, assume, true, true, st);
+  else
+    ts_launch(num_points, p1, workspace2, gaussian_ids_sorted, tile_bins, tile_bounds_x,
+              tile_bounds_y, capacity, capacity, d_counts + 1, assume, true, true,
+              p1.dcount, st);
   return check_launch("bin_speculative");
 }
 
@@ -2424,10 +2629,12 @@ static int bin_emit_impl(int num_points, int64_t num_intersects, int64_t capacit
                        (uint32_t)cap);
     return check_launch("bin_emit");
   }
+  const bool region = use_region(num_points, T);
   const RbPlan rp = rb_plan(num_points, tile_bounds_x, tile_bounds_y);
-  if (workspace1_bytes < p1.bytes || workspace2_bytes < rb_ws_bytes(rp)) {
+  const size_t need2 = region ? rb_ws_bytes(rp) : carve_ts(nullptr, cap, T).bytes;
+  if (workspace1_bytes < p1.bytes || workspace2_bytes < need2) {
     set_error("bin_emit: workspaces %zu/%zu < %zu/%zu bytes", workspace1_bytes,
-              workspace2_bytes, p1.bytes, rb_ws_bytes(rp));
+              workspace2_bytes, p1.bytes, need2);
     return 1;
   }
   if (num_points == 0 || (phase != EMIT_HEAD && phase != EMIT_SPEC && num_intersects == 0)) {
@@ -2435,10 +2642,18 @@ static int bin_emit_impl(int num_points, int64_t num_intersects, int64_t capacit
       note(hipMemsetAsync(tile_bins, 0, (size_t)T * 2 * sizeof(int32_t), st), "hipMemsetAsync");
     return check_launch("bin_emit");
   }
-  // the region binning: its head needs no I-sized buffer, so HEAD (pre-launched before the
-  // host read of I) is the count, scan and tile table at the capacity, TAIL the placement
-  rb_launch(rp, num_points, p1, workspace2, gaussian_ids_sorted, tile_bins,
-            (unsigned long long)cap, nullptr, 0u, head, tail, st);
+  if (region) {
+    // the region binning: its head needs no I-sized buffer, so HEAD (pre-launched before the
+    // host read of I) is the count, scan and tile table at the capacity, TAIL the placement
+    rb_launch(rp, num_points, p1, workspace2, gaussian_ids_sorted, tile_bins,
+              (unsigned long long)cap, nullptr, 0u, head, tail, st);
+    return check_launch("bin_emit");
+  }
+  // the tile sort: HEAD = the emission at the capacity (nothing when the device's I exceeds
+  // it), TAIL = the sort and table over I (EMIT_SPEC: I on the device, launched at the capacity)
+  ts_launch(num_points, p1, workspace2, gaussian_ids_sorted, tile_bins, tile_bounds_x,
+            tile_bounds_y, cap, phase == EMIT_SPEC ? cap : num_intersects, nullptr, 0u, head,
+            tail, phase == EMIT_SPEC ? p1.dcount : nullptr, st);
   return check_launch("bin_emit");
 }
 

@@ -1,6 +1,7 @@
 """Region-binning plan sweep (gsplat_tune_rb: target workgroups, regions per axis, mapping):
 times the whole speculative binning (gsplat_bin_speculative, HIP events) per setting on a
-bench config's first view.  Usage: exp_rb.py <config> [wgs,regs,map ...]"""
+bench config's first view.  Usage: exp_rb.py <config> [wgs,regs,map | scheme=S ...]
+(scheme=S: gsplat_debug_binning_scheme -- -1 shipped (tile sort), 2 region binning)"""
 import os
 import sys
 
@@ -16,7 +17,8 @@ from gaussctrl_exp_amd import rasterize as R  # noqa: E402
 
 def main():
     cfg = sys.argv[1]
-    settings = [tuple(int(x) for x in s.split(",")) for s in sys.argv[2:]] or [(-1, -1, -1)]
+    settings = [s if s.startswith("scheme=") else tuple(int(x) for x in s.split(","))
+                for s in sys.argv[2:]] or [(-1, -1, -1)]
     dev = torch.device("cuda:0")
     sc, cam = bench.make_workload(cfg, 0, dev)
     cam = cam.to(dev)
@@ -43,7 +45,12 @@ def main():
     ref_ids, ref_bins = ids.cpu(), bins.cpu()
     L = _lib.lib()
     for s in settings:
-        L.gsplat_tune_rb(*s)
+        if isinstance(s, str):
+            L.gsplat_debug_binning_scheme(int(s.split("=")[1]))
+            L.gsplat_tune_rb(-1, -1, -1)
+        else:
+            L.gsplat_debug_binning_scheme(2)  # (the plan knobs are the region binning's)
+            L.gsplat_tune_rb(*s)
         times = []
         for it in range(25):
             w = ws1.clone()
@@ -57,13 +64,14 @@ def main():
             assert ok
             if it >= 5:
                 times.append(e0.elapsed_time(e1))
-            if it == 0 and s[2] < 10:  # (map >= 10: timing-only ablations, wrong output)
+            if it == 0 and (isinstance(s, str) or s[2] < 10):  # (map >= 10: timing-only ablations, wrong output)
                 assert torch.equal(spec.ids[:I].cpu(), ref_ids) and \
                     torch.equal(spec.tile_bins.cpu(), ref_bins), s
         times.sort()
-        print(f"{cfg} wgs,regs,map={s}: bin_speculative median {times[len(times) // 2]:.4f} "
+        print(f"{cfg} {s}: bin_speculative median {times[len(times) // 2]:.4f} "
               f"min {times[0]:.4f} ms (I={I})", flush=True)
     L.gsplat_tune_rb(-1, -1, -1)
+    L.gsplat_debug_binning_scheme(-1)
 
 
 if __name__ == "__main__":
