@@ -959,188 +959,6 @@ __global__ __launch_bounds__(256) void raster_fwd3u_kernel(
   clear_side_job();
 }
 
-// Small-frame forward (frames below SMALL_FWD_TILES tiles): S lanes per pixel.  A workgroup is
-// one 8x8 block of a tile, its S waves each a sub-block of 64 / S pixels (S = 4: 4x4, S = 2:
-// 8x4); the S lanes of a pixel take S consecutive staged Gaussians at once.  Every lane
-// evaluates its Gaussian's sigma and alpha; then the pixel's transmittance runs through the S
-// lanes in list order (a DPP broadcast from lane k of the group after step k), so every pixel
-// sees exactly gsplat's sequence of operations: T <- T * (1 - alpha) per composited Gaussian,
-// termination when that product drops to 1e-4 (the Gaussian not composited), final_idx the
-// last composited.  Each lane sums its own Gaussians' alpha * T-weighted colours; the S
-// partial sums are added at the end (colour sums associate differently from the one-lane
-// walk: within the parity bar; T, final_Ts and final_idx are bit-identical).  Against the
-// 8x8-block forward: S x the waves per tile (a long tile list is walked by 4 S waves instead of
-// 4), each culling against a smaller rectangle -- on small frames the forward's time is the
-// longest tiles' walk (bear c3: max / mean list length ~5).  Writes what the 8x8 forward
-// writes, the list-split walk table (tile_last, one per 8x8 block) and the L1 partials (one
-// per block) included; no keep bits (the backward then culls for itself).
-template <int S>
-__device__ __forceinline__ float grp_bcast(float x, int k) {
-  // lane k of each S-lane group (S = 4: the quad; S = 2: each half of the quad)
-  const int ctrl = S == 4 ? (k | (k << 2) | (k << 4) | (k << 6))
-                          : (k | (k << 2) | ((2 + k) << 4) | ((2 + k) << 6));
-  int v = __float_as_int(x);
-  switch (ctrl) {  // (the DPP control must be a constant)
-#define GB(C) case C: v = __builtin_amdgcn_mov_dpp(v, C, 0xF, 0xF, false); break;
-    GB(0x00) GB(0x55) GB(0xAA) GB(0xFF) GB(0xA0) GB(0xF5)
-#undef GB
-    default: break;
-  }
-  return __int_as_float(v);
-}
-template <int S>
-__device__ __forceinline__ float grp_sum(float x) {
-  x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), S == 4 ? 0xB1 : 0xB1, 0xF, 0xF,
-                                               false));  // quad_perm [1,0,3,2]: pairs
-  if (S == 4)
-    x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x4E, 0xF, 0xF,
-                                                 false));  // quad_perm [2,3,0,1]
-  return x;
-}
-template <int S>
-__device__ __forceinline__ int grp_max(int x) {
-  x = max(x, __builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, false));
-  if (S == 4) x = max(x, __builtin_amdgcn_mov_dpp(x, 0x4E, 0xF, 0xF, false));
-  return x;
-}
-constexpr long long SMALL_FWD_TILES = 3584;
-template <int S, bool DEPTH>
-__global__ __launch_bounds__(64 * S) void raster_fwdq_kernel(
-    int tbx, int tby, int H, int W, const int *__restrict__ gids, const int2 *__restrict__ bins,
-    const float2 *__restrict__ xys, const float *__restrict__ conics,
-    const float *__restrict__ colors, const float *__restrict__ opacity,
-    const float *__restrict__ background, float *__restrict__ out_img,
-    float *__restrict__ final_Ts, int *__restrict__ final_idx,
-    const float *__restrict__ depths, float *__restrict__ out_depth,
-    float4 *__restrict__ zero, long long zero_n, const int *__restrict__ zero_radii,
-    int *__restrict__ tile_last, const float *__restrict__ l1_gt,
-    float *__restrict__ l1_part, int l1_clamp) {
-  static_assert(S == 2 || S == 4, "2 or 4 lanes per pixel");
-  constexpr int NT = 64 * S;
-  auto clear_side_job = [&]() {
-    for (long long k = (long long)blockIdx.x * NT + threadIdx.x; k < zero_n;
-         k += (long long)gridDim.x * NT)
-      if (!zero_radii || zero_radii[k >> 2] > 0)
-        zero[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-  };
-  const int slot = block_slot();
-  const int tile = slot >> 2, wt = slot & 3;  // 8x8 block wt of the tile (row-major)
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int tx = tile % tbx, ty = tile / tbx;
-  const int bx = tx * GS_BLOCK + (wt & 1) * 8, by = ty * GS_BLOCK + (wt >> 1) * 8;
-  const bool block_live = tile < tbx * tby && bx < W && by < H;  // (workgroup-uniform)
-  __shared__ GStage lds[S][64];
-  __shared__ float part_s[S];
-  __shared__ int last_s[S];
-  // this wave's sub-block and this lane's pixel / group member
-  constexpr int SW = S == 4 ? 4 : 8;  // sub-block width
-  const int sx0 = bx + (S == 4 ? (wave & 1) * 4 : 0);
-  const int sy0 = by + (S == 4 ? (wave >> 1) * 4 : wave * 4);
-  const int p = lane / S, q = lane % S;
-  const int j = sx0 + p % SW, i = sy0 + p / SW;
-  const bool in_img = block_live && i < H && j < W;
-  const float px = (float)j, py = (float)i;
-  const float rx0 = (float)sx0, rx1 = (float)min(sx0 + SW - 1, W - 1);
-  const float ry0 = (float)sy0, ry1 = (float)min(sy0 + 3, H - 1);
-  float T = 1.f, cr = 0.f, cg = 0.f, cb = 0.f, cd = 0.f;
-  int cur = 0;
-  bool done = !in_img;
-  const bool wave_live = block_live && sx0 < W && sy0 < H;  // (wave-uniform)
-  if (wave_live) {
-    GStage *stage = lds[__builtin_amdgcn_readfirstlane(wave)];
-    const int2 range = bins[tile];
-    for (int b = range.x; b < range.y; b += 64) {
-      if (__all(done)) break;
-      const int idx = b + lane;
-      GStage sg;
-      const bool keep = idx < range.y &&
-                        stage_gaussian(idx, gids, xys, conics, colors, opacity, rx0, rx1, ry0,
-                                       ry1, sg);
-      if (DEPTH && keep) sg.d = depths[sg.id];
-      const unsigned long long kmask = __ballot(keep);
-      const int n = __popcll(kmask);
-      if (keep) stage[lanes_below(kmask)] = sg;
-      wave_lds_sync();
-      for (int t = 0; t < n; t += S) {
-        const bool live = t + q < n;
-        GStage G = stage_at(stage, min(t + q, 63));
-        if (!live) G.r = G.g = G.bl = G.d = 0.f;  // stale slot: keep 0 * x finite
-        const float dx = G.x - px;
-        const float hA = G.ha * dx * dx, bdx = G.b * dx;
-        const float sgm = gs_sigma(G.hc, bdx, hA, G.y - py);
-        const float al = fminf(0.999f, G.o * gs_vis(sgm));
-        const bool v = live && sgm >= 0.f && al >= ALPHA_MIN;
-        const float om = 1.f - al;
-        float w = 0.f;
-#pragma unroll
-        for (int k = 0; k < S; ++k) {  // the group's transmittance, in list order
-          const float nT = T * om;
-          const bool term = v && !done && nT <= 1e-4f, comp = v && !done && !term;
-          if (q == k) {
-            w = comp ? al * T : 0.f;
-            cur = comp ? G.idx : cur;
-          }
-          T = grp_bcast<S>(comp ? nT : T, k);
-          done = grp_bcast<S>((done || term) ? 1.f : 0.f, k) != 0.f;
-        }
-        cr += G.r * w;
-        cg += G.g * w;
-        cb += G.bl * w;
-        if (DEPTH) cd += G.d * w;
-        if (__all(done)) break;
-      }
-      wave_lds_sync();
-    }
-  }
-  // the group's colour sums; its last composited index
-  cr = grp_sum<S>(cr);
-  cg = grp_sum<S>(cg);
-  cb = grp_sum<S>(cb);
-  if (DEPTH) cd = grp_sum<S>(cd);
-  cur = grp_max<S>(cur);
-  const float bg0 = background[0], bg1 = background[1], bg2 = background[2];
-  float l1 = 0.f;
-  if (in_img && q == 0) {
-    const int pix = i * W + j;
-    final_Ts[pix] = T;
-    final_idx[pix] = cur;
-    out_img[3 * pix] = cr + T * bg0;
-    out_img[3 * pix + 1] = cg + T * bg1;
-    out_img[3 * pix + 2] = cb + T * bg2;
-    if (DEPTH) out_depth[pix] = cd + T * 0.f;
-    if (l1_part)
-      l1 = fabsf(l1_gt[3 * pix] - l1_clampv(cr + T * bg0, l1_clamp)) +
-           fabsf(l1_gt[3 * pix + 1] - l1_clampv(cg + T * bg1, l1_clamp)) +
-           fabsf(l1_gt[3 * pix + 2] - l1_clampv(cb + T * bg2, l1_clamp));
-  }
-  // per 8x8 block: the L1 partial (waves in order: deterministic) and the walk-table entry
-  if (l1_part) {
-    l1 = wave_sum(l1);
-    if (lane == 0) part_s[wave] = l1;
-  }
-  if (tile_last) {
-    int m = (in_img && q == 0) ? cur : -1;
-    m = wave_max_int(m);
-    if (lane == 0) last_s[wave] = m;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    if (l1_part) {
-      float a = 0.f;
-#pragma unroll
-      for (int w2 = 0; w2 < S; ++w2) a += part_s[w2];
-      l1_part[blockIdx.x] = a;
-    }
-    if (tile_last && tile < tbx * tby) {
-      int m = -1;
-#pragma unroll
-      for (int w2 = 0; w2 < S; ++w2) m = max(m, last_s[w2]);
-      tile_last[SPLIT_WAVES * tile + wt] = m;
-    }
-  }
-  clear_side_job();
-}
-
 // ---------------------------------------------------------------- backward, C = 3
 // Packed backward: 2*NP pixels per lane as float2 pairs, branch-free (an invalid pixel gets
 // alpha = vis = 0: T, the colour buffer and every partial sum are unchanged exactly).
@@ -2118,20 +1936,8 @@ static bool bad_frame(int tbx, int tby, int H, int W) {
          (long long)tby * GS_BLOCK < H;
 }
 
-// The small-frame forward (raster_fwdq_kernel, S lanes per pixel) below SMALL_FWD_TILES tiles:
-// GSPLAT_MI355X_FWD_LANES = 2 or 4 selects it (A/B runs), 0 / unset the 8x8 forward everywhere.
-static int fwd_lanes(int tbx, int tby) {
-  static const int mode = [] {
-    const char *e = getenv("GSPLAT_MI355X_FWD_LANES");
-    const int v = e ? atoi(e) : 0;
-    return v == 2 || v == 4 ? v : 0;
-  }();
-  return (long long)tbx * tby < SMALL_FWD_TILES ? mode : 0;
-}
-
 // The shipped C = 3 forward: 8x8 blocks, two Gaussians per iteration (CNT: the lane-slot
-// counting instantiation, same arithmetic), optional record clear; on small frames the
-// S-lanes-per-pixel forward when selected (fwd_lanes; no keep bits: kbits must be null then).
+// counting instantiation, same arithmetic), optional record clear.
 template <bool DEPTH>
 static void launch_fwd(hipStream_t st, int tbx, int tby, int H, int W, const int32_t *gids,
                        const int32_t *bins, const float *xys, const float *conics,
@@ -2148,21 +1954,6 @@ static void launch_fwd(hipStream_t st, int tbx, int tby, int H, int W, const int
                      colors, opacity, background, out_img, final_Ts, final_idx, depths,         \
                      out_depth, zero, zn, zero_radii, tile_last, kbits, kbw, l1_gt, l1_part,    \
                      l1_clamp)
-  const int lanes = (!DEPTH && g_pair_count_on) ? 0 : fwd_lanes(tbx, tby);
-  if (lanes) {
-    const unsigned qgrid = (unsigned)((long long)tbx * tby * 4);  // one workgroup per 8x8 block
-    if (lanes == 4)
-      hipLaunchKernelGGL((raster_fwdq_kernel<4, DEPTH>), dim3(qgrid), dim3(256), 0, st, tbx, tby,
-                         H, W, gids, (const int2 *)bins, (const float2 *)xys, conics, colors,
-                         opacity, background, out_img, final_Ts, final_idx, depths, out_depth,
-                         zero, zn, zero_radii, tile_last, l1_gt, l1_part, l1_clamp);
-    else
-      hipLaunchKernelGGL((raster_fwdq_kernel<2, DEPTH>), dim3(qgrid), dim3(128), 0, st, tbx, tby,
-                         H, W, gids, (const int2 *)bins, (const float2 *)xys, conics, colors,
-                         opacity, background, out_img, final_Ts, final_idx, depths, out_depth,
-                         zero, zn, zero_radii, tile_last, l1_gt, l1_part, l1_clamp);
-    return;
-  }
   const bool pf = pipelined_staging(tbx, tby);
   if (!DEPTH && g_pair_count_on) {
     if (pf) FWDK(true, true); else FWDK(true, false);
@@ -2485,8 +2276,7 @@ static int forward_clearing_impl(
       return 1;
     }
     tile_last = w.work;
-    // (the small-frame forward writes no keep bits: the backward then culls for itself)
-    if (g_keep_bits && !(fwd_lanes(tile_bounds_x, tile_bounds_y) && !g_pair_count_on)) {
+    if (g_keep_bits) {
       kbits = w.kbits;
       kbw = w.kbw;
     }
