@@ -2308,8 +2308,8 @@ void ts_launch(int n, const Phase1 &p1, void *ws2, int32_t *ids, int32_t *tile_b
 // Gaussians @ 512^2, max list 837: 0.100 vs 0.112 ms).  A long list is sorted by one
 // workgroup, so real scenes lose (c3 bear, 300k, max list 7,984: 0.365 vs 0.144 ms; headline
 // 1M: 0.287 vs 0.243); the cut is on N, which the count phase must know before I exists.
-// 2: the region binning in place of the tile sort (kept for A/B: slower on every config, see
-// ts_emit_kernel).
+// Within the sorted family (depth sort first): 0 = the shipped tile sort, 2 = the region
+// binning (kept for A/B: measured slower, see ts_emit_kernel).
 int g_bin_scheme = -1;
 bool use_bucket(long long n, long long T) {
   if (T + 1 > BK_MAX_BUCKETS) return false;

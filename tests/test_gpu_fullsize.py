@@ -51,21 +51,20 @@ def headline(request, gpu, oracle_lib):
                 colors=colors, opac=opac, config=request.param)
 
 
-@pytest.mark.parametrize("scheme", ["shipped", "norange", "range22", "bucket"])
+@pytest.mark.parametrize("scheme", ["shipped", "norange", "range22", "bucket", "region"])
 def test_headline_binning_bitexact(gpu, headline, scheme, hooks):
     """Binning bit-exact at full size: the shipped dispatch (for these scenes the depth sort of
     8-bit reduce-then-scan passes compacting the culled Gaussians away, constant-digit passes
-    skipped, then the region binning placing each depth-ordered intersection into its tile
-    list); and every other setting a shipped dispatch takes elsewhere: the key-range shortcut
-    off or from 2^22 keys only, and the tile buckets with per-tile LDS sorts (shipped for small
-    scenes)."""
+    skipped, then the depth-ordered (tile, id) pairs sorted stably by tile); and every other
+    setting a dispatch takes: the key-range shortcut off or from 2^22 keys only, the tile
+    buckets with per-tile LDS sorts (shipped for small scenes) and the region binning (A/B)."""
     h, cam = headline, headline["cam"]
     assert h["ref"]["num_intersects"] > 1 << 20
     if scheme != "shipped" and h["config"] in ("c4", "c5"):
         pytest.skip("the other dispatches: headline and c3 only")
     L = _lib.lib()
     # (-1: leave the shipped setting; each call returns the previous one)
-    prev = (L.gsplat_debug_binning_scheme(1 if scheme == "bucket" else -1),
+    prev = (L.gsplat_debug_binning_scheme({"bucket": 1, "region": 2}.get(scheme, -1)),
             L.gsplat_debug_depth_key_range({"norange": 0, "range22": 1}.get(scheme, -1)))
     try:
         I, gids, bins = bin_gaussians(h["xys"], h["depths"], h["radii"], h["nth"], cam.height,

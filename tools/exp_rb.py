@@ -1,7 +1,7 @@
 """Region-binning plan sweep (gsplat_tune_rb: target workgroups, regions per axis, mapping):
 times the whole speculative binning (gsplat_bin_speculative, HIP events) per setting on a
 bench config's first view.  Usage: exp_rb.py <config> [wgs,regs,map | scheme=S ...]
-(scheme=S: gsplat_debug_binning_scheme -- -1 shipped (tile sort), 2 region binning)"""
+(scheme=S: gsplat_debug_binning_scheme -- -1 shipped, 0 tile sort, 2 region binning)"""
 import os
 import sys
 
