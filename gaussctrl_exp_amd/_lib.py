@@ -182,10 +182,11 @@ def lib():
     if _lib is None:
         L = _load(LIB_PATH)
         # measurement switches (A/B runs; LIB_PATH is then the test library):
-        # GSPLAT_MI355X_RASTER_VARIANT = "fwd_pxl,bwd_pxl,flags" (gsplat_debug_set_raster_variant),
+        # GSPLAT_MI355X_RASTER_VARIANT = "fwd_pxl,bwd_pxl,flags" (gsplat_debug_set_raster_variant;
+        # "/" separates as well, for tools/gpu_iter.sh's comma-separated env lists),
         # GSPLAT_MI355X_CHUNK = the list-split chunk override (gsplat_debug_set_chunk)
         var = os.environ.get("GSPLAT_MI355X_RASTER_VARIANT")
-        if var and L.gsplat_debug_set_raster_variant(*[int(x) for x in var.split(",")]) != 0:
+        if var and L.gsplat_debug_set_raster_variant(*[int(x) for x in var.replace("/", ",").split(",")]) != 0:
             raise RuntimeError(L.gsplat_last_error().decode(errors="replace"))
         if os.environ.get("GSPLAT_MI355X_CHUNK"):
             L.gsplat_debug_set_chunk(int(os.environ["GSPLAT_MI355X_CHUNK"]))
