@@ -358,7 +358,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     const uint32_t *__restrict__ rowtot, const uint32_t *__restrict__ offs, long long nblocks,
     bool drop = false, const uint32_t *__restrict__ n_dev = nullptr,
     uint32_t *__restrict__ n_out = nullptr, const uint32_t *__restrict__ kfin = nullptr,
-    DevIO io = {}, int q = 0) {
+    DevIO io = {}, int q = 0, int *__restrict__ tbins = nullptr, uint32_t tcount = 0) {
   if (io.fin) {  // device-selected buffers (DevIO): a constant digit moves nothing
     if (q > 0 && digit_constant(io.fin, shift, width)) return;
     const K *ki;
@@ -505,6 +505,14 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
         const uint32_t pos = sm.gofs[(uint32_t)(k >> shift) & dmask] + (uint32_t)i;
         if (kout) kout[pos] = k;  // null: only the values are wanted (compacted depth sort)
         vout[pos] = v;
+        // the tile sort's last pass (tbins): the tile table from this tile's runs of equal keys
+        // (equal keys sit at consecutive positions): a run's first position -> max(n - pos),
+        // its end -> max(pos + 1); over all runs of a tile, the list's first and end
+        // (ts_decode_kernel turns n - first back); keys >= tcount (the sentinel) have no row
+        if (tbins && (uint32_t)k < tcount) {
+          if (i == 0 || sm.key(i - 1) != k) atomicMax(&tbins[2 * (uint32_t)k], (int)(n - pos));
+          if (i + 1 == cnt || sm.key(i + 1) != k) atomicMax(&tbins[2 * (uint32_t)k + 1], (int)(pos + 1));
+        }
       }
     }
   }
@@ -533,13 +541,15 @@ uint32_t *sort_kept_word(void *ws) { return (uint32_t *)ws + 1; }
 // sort_kept_word(ws) (the sorted output holds that many; kout may be null).
 // assume_const / range_out (drop only): gsplat_bin_count_keyed_ex's depth-key range.
 // n_dev_all (no drop): the key count on the device, n the launch length (a capacity): every pass
-// sorts *n_dev_all keys, none when it exceeds n.
+// sorts *n_dev_all keys, none when it exceeds n.  tbins (the tile sort, no KeyRange): the last
+// pass also accumulates the tile table of keys < tcount (os_pass_kernel; ts_decode_kernel).
 template <typename K>
 int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t *vout,
                      long long n, int begin_bit, int end_bit, void *ws, hipStream_t st,
                      bool first_counts_ready = false, bool drop = false,
                      uint32_t assume_const = 0, int32_t *range_out = nullptr,
-                     const uint32_t *n_dev_all = nullptr) {
+                     const uint32_t *n_dev_all = nullptr, int *tbins = nullptr,
+                     uint32_t tcount = 0) {
   if (n <= 0) return 0;
   const SortPlan p = sort_plan(n, begin_bit, end_bit);
   if (p.passes == 0) {
@@ -592,7 +602,7 @@ int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t
   hipLaunchKernelGGL((os_pass_kernel<K, Wd, It>), dim3((unsigned)p.nblocks), dim3(TPB), 0, st, \
                      kin, vin, ko, vo, n, sh, p.width, rowtot, counts, p.nblocks,              \
                      drop && q == 0, ndev, drop && q == 0 ? kept : nullptr,                    \
-                     q > 0 && !io.fin ? kr.fin : nullptr, io, q)
+                     q > 0 && !io.fin ? kr.fin : nullptr, io, q, last ? tbins : nullptr, tcount)
 #define OS_PASS_W(Wd)                                                                       \
   do {                                                                                      \
     if (p.items == 16) OS_PASS(Wd, 16); else OS_PASS(Wd, 4);                                \
@@ -824,7 +834,10 @@ __device__ __forceinline__ int slot_owner(int *mk, uint32_t j0, uint32_t rel, bo
 //   radix_sort_pairs the stable LSD sort of the pairs by tile id (ceil(log2(T + 1)) bits: two
 //                    passes up to 16,383 tiles), launched at the capacity with the device count
 //                    as its length (n_dev_all): no host read of I before it.
-//   ts_bins_kernel   the tile table from the runs of equal sorted keys.
+//                    Its last pass writes only the ids and accumulates the tile table from
+//                    its LDS-sorted runs of equal tile ids (atomicMax of n - first and of end);
+//   ts_decode_kernel turns each row back into gsplat's (first, end) -- no sorted keys are
+//                    written or re-read.
 // Stable sort of depth-ordered pairs by tile = gsplat's order (ties by Gaussian id), bit for
 // bit.  Against the region binning below (measured round 5, same box, tools/exp_rb.py): the
 // headline 0.22 vs 0.24 ms, c4 garden ~0.30 vs 0.39 ms -- the region binning's per-(depth
@@ -832,8 +845,9 @@ __device__ __forceinline__ int slot_owner(int *mk, uint32_t j0, uint32_t rel, bo
 // returning LDS atomic per round; the sort's passes are coalesced and balanced by construction.
 // partial[]: gather_counts_kernel's per-1,024-Gaussian block sums, scanned here by every
 // workgroup (<= a few loads per thread); workgroup 0 publishes their total I to i_dev and
-// i_host (the speculative binning; after a count phase that found I already, the same value).  i_dev > cap (an overflow, or a
-// depth-key digit the sort assumed constant that varied: i_dev = ~0): nothing is emitted.
+// i_host (the speculative binning; after a count phase that found I already, the same value).
+// i_dev > cap (an overflow, or a depth-key digit the sort assumed constant that varied: i_dev =
+// ~0): nothing is emitted.
 __global__ __launch_bounds__(TPB) void ts_emit_kernel(int n, int nb,
                                                       const uint32_t *__restrict__ order,
                                                       const uint32_t *__restrict__ cnt,
@@ -926,47 +940,23 @@ __global__ __launch_bounds__(TPB) void ts_emit_kernel(int n, int nb,
   }
 }
 
-// The tile table from the sorted keys (tile ids; the sentinel T has no row): [first, last + 1)
-// per non-empty tile, the cleared (0, 0) elsewhere.  n_dev: the device count of a
-// capacity-launched sort (cap the launch length; above it the table stays cleared).  Eight keys
-// per thread from two 16-B loads (one key per thread: 14.4 us at the headline's 7.7M keys, the
-// dispatch of 30k workgroups rather than the 31 MB read).
-constexpr int TS_BINS_KEYS = 8;
-__global__ __launch_bounds__(TPB) void ts_bins_kernel(long long cap, const uint32_t *__restrict__ keys,
-                                                      int *__restrict__ bins, long long T,
-                                                      const uint32_t *__restrict__ n_dev) {
+// The tile table from the last sort pass's run bounds (os_pass_kernel tbins): row t holds
+// (max(n - first), max(end)) over the runs of tile t, or (0, 0) when no run (the emission
+// cleared it) -> gsplat's (first, end).  n_dev: the device count of a capacity-launched sort
+// (above cap the sort did nothing and the table stays cleared).  Replaces writing the sorted
+// keys and a pass over them (8 B per intersection).
+__global__ __launch_bounds__(TPB) void ts_decode_kernel(long long T, long long cap,
+                                                        int *__restrict__ bins,
+                                                        const uint32_t *__restrict__ n_dev) {
   long long n = cap;
   if (n_dev) {
     if ((long long)*n_dev > cap) return;
     n = *n_dev;
   }
-  const long long k0 = ((long long)blockIdx.x * TPB + threadIdx.x) * TS_BINS_KEYS;
-  if (k0 >= n) return;
-  uint32_t v[TS_BINS_KEYS];
-  if (k0 + TS_BINS_KEYS <= n) {  // (keys is 256-B aligned, k0 a multiple of 8)
-    const uint4 a = *reinterpret_cast<const uint4 *>(keys + k0);
-    const uint4 c = *reinterpret_cast<const uint4 *>(keys + k0 + 4);
-    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
-    v[4] = c.x; v[5] = c.y; v[6] = c.z; v[7] = c.w;
-  } else {
-#pragma unroll
-    for (int j = 0; j < TS_BINS_KEYS; ++j) v[j] = k0 + j < n ? keys[k0 + j] : 0u;
-  }
-  uint32_t prev = k0 > 0 ? keys[k0 - 1] : 0u;
-#pragma unroll
-  for (int j = 0; j < TS_BINS_KEYS; ++j) {
-    const long long k = k0 + j;
-    if (k >= n) break;
-    const uint32_t cur = v[j];
-    if (k == 0) {
-      if (cur < T) bins[2 * cur] = 0;
-    } else if (prev != cur) {
-      if (prev < T) bins[2 * prev + 1] = (int)k;
-      if (cur < T) bins[2 * cur] = (int)k;
-    }
-    if (k == n - 1 && cur < T) bins[2 * cur + 1] = (int)n;
-    prev = cur;
-  }
+  const long long t = (long long)blockIdx.x * TPB + threadIdx.x;
+  if (t >= T) return;
+  const int2 r = reinterpret_cast<int2 *>(bins)[t];
+  if (r.y > 0) reinterpret_cast<int2 *>(bins)[t] = make_int2((int)(n - r.x), r.y);
 }
 
 // ------------------------------------------------------------------ region binning
@@ -2277,7 +2267,7 @@ BkWs carve_bk(void *base, int n, long long I, long long T) {
 }
 
 struct TsWs {
-  uint32_t *ka, *va, *kb, *vb, *kout;
+  uint32_t *ka, *va, *kb, *vb;
   void *rs;
   size_t bytes;
 };
@@ -2289,7 +2279,6 @@ TsWs carve_ts(void *base, long long cap, long long T) {
   w.va = c.take<uint32_t>(ii);
   w.kb = c.take<uint32_t>(ii);
   w.vb = c.take<uint32_t>(ii);
-  w.kout = c.take<uint32_t>(ii);
   // (any sort length up to cap: the short-tile plan below 2^22 keys has more tiles)
   const long long c1 = cap > 0 ? cap : 1, c0 = c1 < (4LL << 20) ? c1 : (4LL << 20) - 1;
   const size_t r0 = radix_ws_bytes(c0, 0, bits_for(T)), r1 = radix_ws_bytes(c1, 0, bits_for(T));
@@ -2315,10 +2304,10 @@ void ts_launch(int n, const Phase1 &p1, void *ws2, int32_t *ids, int32_t *tile_b
                        (uint32_t)(cap > 0xFFFFFFFELL ? 0xFFFFFFFELL : cap),
                        assume ? sort_kept_word(p1.rs_ws) + 1 : nullptr, assume);
   if (!tail || m <= 0) return;
-  radix_sort_pairs<uint32_t>(w.ka, w.va, w.kb, w.vb, w.kout, (uint32_t *)ids, m, 0, bits_for(T),
-                             w.rs, st, false, false, 0u, nullptr, n_dev);
-  hipLaunchKernelGGL(ts_bins_kernel, dim3((unsigned)cdiv(m, (long long)TPB * TS_BINS_KEYS)),
-                     dim3(TPB), 0, st, m, w.kout, tile_bins, T, n_dev);
+  radix_sort_pairs<uint32_t>(w.ka, w.va, w.kb, w.vb, nullptr, (uint32_t *)ids, m, 0, bits_for(T),
+                             w.rs, st, false, false, 0u, nullptr, n_dev, tile_bins, (uint32_t)T);
+  hipLaunchKernelGGL(ts_decode_kernel, dim3(cdiv(T, TPB)), dim3(TPB), 0, st, T, m, tile_bins,
+                     n_dev);
 }
 
 // Binning scheme (gsplat_debug_binning_scheme): -1 by size (shipped), 0 depth sort + tile sort,

@@ -48,7 +48,7 @@ fi
 if [ -n "$TIMELINE" ]; then
   for c in $TIMELINE; do
     timeout -k 10 240 rocprofv3 --kernel-trace -d gpurun_out/tl_$c -o run -- python3 bench.py --config $c --steps 6 --warmup 3 --no-cpu-baseline --no-lane-occupancy --train-steps 0 > $O/tl_bench_$c.log 2>&1 || exit $?
-    python3 tools/step_timeline.py gpurun_out/tl_$c/run_results.db fused_fwd_kernel 5 > $O/timeline_$c.txt || exit $?
+    python3 tools/step_timeline.py gpurun_out/tl_$c/run_results.db ${TL_MARK:-fused_fwd_proj_kernel} 5 > $O/timeline_$c.txt || exit $?
     rm -rf gpurun_out/tl_$c
   done
 fi
