@@ -125,6 +125,7 @@ HOOK_SIGNATURES = {
     "gsplat_debug_raster_variant_is_default": (_I, []),
     "gsplat_debug_depth_key_range": (_I, [_I]),
     "gsplat_debug_wave_log": (_I, [_P]),
+    "gsplat_debug_tile_sort_gen": (_I64, [_I64]),
 }
 
 ABI_VERSION = 15  # include/gsplat_mi355x.h GSPLAT_MI355X_ABI_VERSION

@@ -347,18 +347,157 @@ struct OsSmem {
   }
 };
 
+// Inclusive max-scan over the wave (DPP row shifts, then the row broadcasts; no LDS).
+__device__ __forceinline__ int wave_incl_max(int v) {
+  constexpr int NONE = -2147483647 - 1;
+  v = max(v, __builtin_amdgcn_update_dpp(NONE, v, 0x111, 0xF, 0xF, false));  // row_shr:1
+  v = max(v, __builtin_amdgcn_update_dpp(NONE, v, 0x112, 0xF, 0xF, false));  // row_shr:2
+  v = max(v, __builtin_amdgcn_update_dpp(NONE, v, 0x114, 0xF, 0xF, false));  // row_shr:4
+  v = max(v, __builtin_amdgcn_update_dpp(NONE, v, 0x118, 0xF, 0xF, false));  // row_shr:8
+  v = max(v, __builtin_amdgcn_update_dpp(NONE, v, 0x142, 0xA, 0xF, false));  // row_bcast:15
+  v = max(v, __builtin_amdgcn_update_dpp(NONE, v, 0x143, 0xC, 0xF, false));  // row_bcast:31
+  return v;
+}
+
+// The tile sort's first pass generated instead of loaded (GenSrc; intersection counts from
+// 2^24, where the emitted pair array would not stay in the 256 MB MALL and writing it and
+// reading it back costs more than generating each slot twice): slot s of the depth-ordered
+// intersection list belongs to the last depth position p with start[p] <= s (start = the
+// exclusive scan of the allotments; a zero allotment shares its start with the next position,
+// so the last such p always owns s), and its tile is the (s - start[p])-th of p's box in gsplat's
+// row order (the sentinel T past the box, as the emission).  seg[k] = the owner of slot 64 k,
+// so a wave finds a round's owners from a window of the 64 positions from seg[k] on.
+struct GenSrc {
+  const uint32_t *start, *cnt, *order, *seg;
+  const uint2 *box;
+  int tbx, tby;
+  long long n;  // depth positions
+};
+// Slots s0 + 64 u + lane (u < G; s0 a multiple of 64) of the list of n_slots -> (tile, id);
+// every lane of the wave calls it (wave-uniform s0).  The G rounds' loads are issued together,
+// level by level (owners' windows, window starts, then the owners' boxes and ids), so a wave
+// waits for three load latencies per G rounds instead of per round.  mk: the wave's G x 64 LDS
+// ints.
+constexpr int GEN_G = 4;
+template <int G>
+__device__ __forceinline__ void gen_rounds(const GenSrc &g, long long s0, long long n_slots,
+                                           int *mk, uint32_t (&key)[G], uint32_t (&val)[G]) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t T = (uint32_t)(g.tbx * g.tby);
+  long long pa[G];
+  uint32_t st[G];
+#pragma unroll
+  for (int u = 0; u < G; ++u) {
+    const long long su = s0 + 64 * u;
+    pa[u] = su < n_slots ? (long long)g.seg[su >> 6] : 0;
+  }
+#pragma unroll
+  for (int u = 0; u < G; ++u) {
+    const long long p = pa[u] + lane;
+    st[u] = (s0 + 64 * u < n_slots && p < g.n) ? g.start[p] : 0xFFFFFFFFu;
+  }
+  // owner = the last window lane q with start[q] <= s: lane 0 owns the round's first slot; a
+  // later lane starting inside the round marks its first slot (several with one start: the
+  // last of them wins)
+  wave_lds_sync();
+#pragma unroll
+  for (int u = 0; u < G; ++u) mk[u * 64 + lane] = 0;
+  wave_lds_sync();
+#pragma unroll
+  for (int u = 0; u < G; ++u) {
+    const uint64_t su = (uint64_t)(s0 + 64 * u);
+    if (lane > 0 && (uint64_t)st[u] < su + 64u) atomicMax(&mk[u * 64 + (int)(st[u] - (uint32_t)su)], lane);
+  }
+  wave_lds_sync();
+  long long own[G];
+  uint32_t ost[G];
+#pragma unroll
+  for (int u = 0; u < G; ++u) {
+    const long long s = s0 + 64 * u + lane;
+    const int q = wave_incl_max(mk[u * 64 + lane]);
+    const uint32_t sq = __shfl(st[u], q, 64);
+    const uint32_t st63 = __shfl(st[u], 63, 64);
+    own[u] = pa[u] + q;
+    ost[u] = sq;
+    // past the window (only with zero allotments in it): the owner by binary search
+    if (q == 63 && s < n_slots && st63 != 0xFFFFFFFFu &&
+        (uint64_t)s >= (uint64_t)st63 + (uint64_t)g.cnt[min(pa[u] + 63, g.n - 1)]) {
+      long long lo = pa[u] + 63, hi = g.n - 1;  // start[lo] <= s; the last such position
+      while (lo < hi) {
+        const long long mid = (lo + hi + 1) >> 1;
+        if ((uint64_t)g.start[mid] <= (uint64_t)s) lo = mid;
+        else hi = mid - 1;
+      }
+      own[u] = lo;
+      ost[u] = g.start[lo];
+    }
+  }
+  uint2 bx[G];
+#pragma unroll
+  for (int u = 0; u < G; ++u) {
+    const bool valid = s0 + 64 * u + lane < n_slots;
+    bx[u] = valid ? g.box[own[u]] : make_uint2(0u, 0u);
+    val[u] = valid ? g.order[own[u]] : 0u;
+  }
+#pragma unroll
+  for (int u = 0; u < G; ++u) {
+    const uint32_t li = (uint32_t)(s0 + 64 * u + lane) - ost[u];
+    const int qx0 = (int)(bx[u].x & 0xFFFFu), qy0 = (int)(bx[u].x >> 16);
+    const int qx1 = (int)(bx[u].y & 0xFFFFu), qy1 = (int)(bx[u].y >> 16);
+    const int qbw = max(qx1 - qx0, 1);
+    const int qarea = max(qx1 - qx0, 0) * max(qy1 - qy0, 0);
+    key[u] = T;
+    if ((int)li < qarea) {  // li / qbw as in the emission (exact below 2^20)
+      const int ly = li < (1u << 20)
+                         ? (int)(((float)li + 0.5f) * __builtin_amdgcn_rcpf((float)qbw))
+                         : (int)li / qbw;
+      key[u] = (uint32_t)((qy0 + ly) * g.tbx + qx0 + ((int)li - ly * qbw));
+    }
+  }
+}
+
+// The generated first pass's digit counts (rts_count_kernel's layout): one workgroup per sort
+// tile of TPB * ITEMS slots, each wave its ITEMS rounds.
+template <int ITEMS>
+__global__ __launch_bounds__(TPB) void gen_count_kernel(GenSrc g, long long cap,
+                                                        const uint32_t *__restrict__ n_dev,
+                                                        int width, long long nblocks,
+                                                        uint32_t *__restrict__ counts) {
+  __shared__ uint32_t h[256];
+  __shared__ int marks[TPB * GEN_G];
+  const int tid = threadIdx.x, wave = tid >> 6;
+  long long n = cap;
+  if (n_dev) n = (long long)*n_dev > cap ? 0 : (long long)*n_dev;
+  const int R = 1 << width;
+  h[tid] = 0;
+  __syncthreads();
+  const long long sg = (long long)blockIdx.x * TPB * ITEMS + (long long)wave * (ITEMS * 64);
+  static_assert(ITEMS % GEN_G == 0, "rounds in groups of GEN_G");
+  for (int r = 0; r < ITEMS; r += GEN_G) {
+    if (sg + r * 64 >= n) break;  // wave-uniform
+    uint32_t k[GEN_G], v[GEN_G];
+    gen_rounds<GEN_G>(g, sg + r * 64, n, marks + wave * 64 * GEN_G, k, v);
+#pragma unroll
+    for (int u = 0; u < GEN_G; ++u)
+      if (sg + (r + u) * 64 + (tid & 63) < n) atomicAdd(&h[k[u] & (uint32_t)(R - 1)], 1u);
+  }
+  __syncthreads();
+  if (tid < R) counts[(size_t)tid * nblocks + blockIdx.x] = h[tid];
+}
+
 // Reduce-then-scan pass, part 3: each workgroup ranks its tile of TPB * ITEMS keys stably in
 // LDS, takes its digits' global offsets from the row-scanned tile counts plus the digit bases
 // (the exclusive scan of the row totals), and writes the tile out in digit order, so each
 // digit's run is written by consecutive lanes.
-template <typename K, int WIDTH, int ITEMS>
+template <typename K, int WIDTH, int ITEMS, bool GEN = false>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) void os_pass_kernel(
     const K *__restrict__ kin, const uint32_t *__restrict__ vin, K *__restrict__ kout,
     uint32_t *__restrict__ vout, long long n, int shift, int width,
     const uint32_t *__restrict__ rowtot, const uint32_t *__restrict__ offs, long long nblocks,
     bool drop = false, const uint32_t *__restrict__ n_dev = nullptr,
     uint32_t *__restrict__ n_out = nullptr, const uint32_t *__restrict__ kfin = nullptr,
-    DevIO io = {}, int q = 0, int *__restrict__ tbins = nullptr, uint32_t tcount = 0) {
+    DevIO io = {}, int q = 0, int *__restrict__ tbins = nullptr, uint32_t tcount = 0,
+    GenSrc gen = {}) {
   if (io.fin) {  // device-selected buffers (DevIO): a constant digit moves nothing
     if (q > 0 && digit_constant(io.fin, shift, width)) return;
     const K *ki;
@@ -412,8 +551,24 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
   constexpr bool SMALL = ITEMS <= 8;
   const uint32_t hval = rowtot[min(tid, R - 1)];
   const uint32_t oval = SMALL ? offs[(size_t)min(tid, R - 1) * nblocks + t] : 0u;
-  {  // (indices clamped into [0, n): no per-element branch, so all 2 x ITEMS loads are in
-     // flight together; the validity mask is applied once they are consumed)
+  if constexpr (GEN) {  // the generated first pass of the tile sort (gen_rounds)
+    // (the marks live in the tile's pair buffer, which is written only after the barriers of
+    // the digit-base scan below)
+    int *gmarks = reinterpret_cast<int *>(sm.raw);
+    static_assert(sizeof(sm.raw) >= sizeof(int) * TPB * GEN_G, "marks fit the pair buffer");
+    const long long sg = (long long)t * TPB * ITEMS + (long long)wave * (ITEMS * 64);
+#pragma unroll
+    for (int r = 0; r < ITEMS; r += GEN_G) {
+      uint32_t k[GEN_G], v[GEN_G];
+      gen_rounds<GEN_G>(gen, sg + r * 64, n, gmarks + wave * 64 * GEN_G, k, v);
+#pragma unroll
+      for (int u = 0; u < GEN_G; ++u) {
+        key[r + u] = (K)k[u];
+        val[r + u] = v[u];
+      }
+    }
+  } else {  // (indices clamped into [0, n): no per-element branch, so all 2 x ITEMS loads are
+            // in flight together; the validity mask is applied once they are consumed)
     const long long sg = (long long)t * TPB * ITEMS + (long long)wave * (ITEMS * 64);
 #pragma unroll
     for (int r = 0; r < ITEMS; ++r) {
@@ -549,7 +704,7 @@ int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t
                      bool first_counts_ready = false, bool drop = false,
                      uint32_t assume_const = 0, int32_t *range_out = nullptr,
                      const uint32_t *n_dev_all = nullptr, int *tbins = nullptr,
-                     uint32_t tcount = 0) {
+                     uint32_t tcount = 0, const GenSrc *gen = nullptr) {
   if (n <= 0) return 0;
   const SortPlan p = sort_plan(n, begin_bit, end_bit);
   if (p.passes == 0) {
@@ -588,7 +743,14 @@ int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t
     const int sh = begin_bit + q * p.width;
     const uint32_t *ndev = drop ? (q > 0 ? kept : nullptr) : n_dev_all;
     // first_counts_ready: the key kernel wrote pass 0's counts and key ranges (kr.blk)
-    if (q == 0 && first_counts_ready) {
+    if (q == 0 && gen) {
+      if (p.items == 16)
+        hipLaunchKernelGGL(gen_count_kernel<16>, dim3((unsigned)p.nblocks), dim3(TPB), 0, st, *gen,
+                           n, ndev, p.width, p.nblocks, counts);
+      else
+        hipLaunchKernelGGL(gen_count_kernel<4>, dim3((unsigned)p.nblocks), dim3(TPB), 0, st, *gen,
+                           n, ndev, p.width, p.nblocks, counts);
+    } else if (q == 0 && first_counts_ready) {
     } else if (p.items == 16)
       hipLaunchKernelGGL((rts_count_kernel<K, 16>), dim3((unsigned)p.nblocks), dim3(TPB), 0, st,
                          kin, n, sh, p.width, p.nblocks, counts, drop && q == 0, ndev, kr, q, io);
@@ -599,10 +761,19 @@ int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t
                        dim3((unsigned)p.radix + (q == 0 && kr.blk ? 1u : 0u)), dim3(1024), 0,
                        st, counts, p.nblocks, rowtot, kr, q, sh, p.width);
 #define OS_PASS(Wd, It)                                                                     \
-  hipLaunchKernelGGL((os_pass_kernel<K, Wd, It>), dim3((unsigned)p.nblocks), dim3(TPB), 0, st, \
-                     kin, vin, ko, vo, n, sh, p.width, rowtot, counts, p.nblocks,              \
-                     drop && q == 0, ndev, drop && q == 0 ? kept : nullptr,                    \
-                     q > 0 && !io.fin ? kr.fin : nullptr, io, q, last ? tbins : nullptr, tcount)
+  do {                                                                                      \
+    if (q == 0 && gen)                                                                      \
+      hipLaunchKernelGGL((os_pass_kernel<K, Wd, It, true>), dim3((unsigned)p.nblocks),      \
+                         dim3(TPB), 0, st, kin, vin, ko, vo, n, sh, p.width, rowtot, counts, \
+                         p.nblocks, false, ndev, nullptr, nullptr, io, q,                   \
+                         last ? tbins : nullptr, tcount, *gen);                             \
+    else                                                                                    \
+      hipLaunchKernelGGL((os_pass_kernel<K, Wd, It>), dim3((unsigned)p.nblocks), dim3(TPB), \
+                         0, st, kin, vin, ko, vo, n, sh, p.width, rowtot, counts, p.nblocks, \
+                         drop && q == 0, ndev, drop && q == 0 ? kept : nullptr,            \
+                         q > 0 && !io.fin ? kr.fin : nullptr, io, q,                        \
+                         last ? tbins : nullptr, tcount);                                   \
+  } while (0)
 #define OS_PASS_W(Wd)                                                                       \
   do {                                                                                      \
     if (p.items == 16) OS_PASS(Wd, 16); else OS_PASS(Wd, 4);                                \
@@ -791,18 +962,6 @@ __global__ __launch_bounds__(TPB) void gather_counts_kernel(int n, const uint32_
   if (threadIdx.x == 0) partial[blockIdx.x] = total;
 }
 
-// Inclusive max-scan over the wave (DPP row shifts, then the row broadcasts; no LDS).
-__device__ __forceinline__ int wave_incl_max(int v) {
-  constexpr int NONE = -2147483647 - 1;
-  v = max(v, __builtin_amdgcn_update_dpp(NONE, v, 0x111, 0xF, 0xF, false));  // row_shr:1
-  v = max(v, __builtin_amdgcn_update_dpp(NONE, v, 0x112, 0xF, 0xF, false));  // row_shr:2
-  v = max(v, __builtin_amdgcn_update_dpp(NONE, v, 0x114, 0xF, 0xF, false));  // row_shr:4
-  v = max(v, __builtin_amdgcn_update_dpp(NONE, v, 0x118, 0xF, 0xF, false));  // row_shr:8
-  v = max(v, __builtin_amdgcn_update_dpp(NONE, v, 0x142, 0xA, 0xF, false));  // row_bcast:15
-  v = max(v, __builtin_amdgcn_update_dpp(NONE, v, 0x143, 0xC, 0xF, false));  // row_bcast:31
-  return v;
-}
-
 // The owner of slot j0 + lane of a wave's combined slot range -- the last lane q with
 // rel[q] <= j and an allotment (has) -- without a search: every owner starting in the 64-slot
 // chunk marks its start offset with j0 + q (LDS max into the wave's 64 marks `mk`, set to -1
@@ -859,7 +1018,9 @@ __global__ __launch_bounds__(TPB) void ts_emit_kernel(int n, int nb,
                                                       uint32_t *__restrict__ i_dev,
                                                       int32_t *__restrict__ i_host, uint32_t cap,
                                                       const uint32_t *__restrict__ kfin,
-                                                      uint32_t assume) {
+                                                      uint32_t assume,
+                                                      uint32_t *__restrict__ gstart = nullptr,
+                                                      uint32_t *__restrict__ gseg = nullptr) {
   __shared__ uint32_t lds[TPB / 64];
   __shared__ int marks[TPB];
   for (long long i = (long long)blockIdx.x * TPB + threadIdx.x; i < 2LL * tbx * tby;
@@ -898,6 +1059,13 @@ __global__ __launch_bounds__(TPB) void ts_emit_kernel(int n, int nb,
   if (violated || btot > cap) return;  // workgroup-uniform
   uint32_t rtot;
   const uint32_t start = bpre + block_exclusive_scan<TPB>(c, rtot, lds);
+  if (gstart) {  // the generated first pass (GenSrc): start offsets and the 64-slot owners
+    if (p < n) {
+      gstart[p] = start;
+      for (uint32_t k = (start + 63u) >> 6; c && (k << 6) < start + c; ++k) gseg[k] = (uint32_t)p;
+    }
+    return;
+  }
   const long long p0 = p - lane;
   if (p0 >= n) return;  // wave-uniform (no barrier below)
   const bool in = p < n;
@@ -2268,10 +2436,14 @@ BkWs carve_bk(void *base, int n, long long I, long long T) {
 
 struct TsWs {
   uint32_t *ka, *va, *kb, *vb;
+  uint32_t *gstart, *gseg;  // the generated first pass (cap >= GEN_MIN_I)
   void *rs;
   size_t bytes;
 };
-TsWs carve_ts(void *base, long long cap, long long T) {
+// gen (from GEN_MIN_I intersections): + the start offsets (n) and the 64-slot owners
+constexpr long long GEN_MIN_I = 1LL << 24;
+long long g_gen_min_i = GEN_MIN_I;  // (gsplat_debug_tile_sort_gen: tests force it lower)
+TsWs carve_ts(void *base, long long cap, long long T, int n) {
   TsWs w;
   Carver c(base);
   const size_t ii = (size_t)(cap > 0 ? cap : 1) * sizeof(uint32_t);
@@ -2283,6 +2455,11 @@ TsWs carve_ts(void *base, long long cap, long long T) {
   const long long c1 = cap > 0 ? cap : 1, c0 = c1 < (4LL << 20) ? c1 : (4LL << 20) - 1;
   const size_t r0 = radix_ws_bytes(c0, 0, bits_for(T)), r1 = radix_ws_bytes(c1, 0, bits_for(T));
   w.rs = c.take<char>(r0 > r1 ? r0 : r1);
+  w.gstart = w.gseg = nullptr;
+  if (cap >= g_gen_min_i) {
+    w.gstart = c.take<uint32_t>((size_t)(n > 0 ? n : 1) * 4);
+    w.gseg = c.take<uint32_t>((size_t)cdiv(cap, 64) * 4 + 4);
+  }
   w.bytes = c.off;
   return w;
 }
@@ -2295,17 +2472,19 @@ void ts_launch(int n, const Phase1 &p1, void *ws2, int32_t *ids, int32_t *tile_b
                int tby, long long cap, long long m, int32_t *i_host, uint32_t assume,
                bool head, bool tail, const uint32_t *n_dev, hipStream_t st) {
   const long long T = (long long)tbx * tby;
-  const TsWs w = carve_ts(ws2, cap, T);
+  const TsWs w = carve_ts(ws2, cap, T, n);
   const int nb = (int)cdiv(n, SC_TILE);
   if (head)
     hipLaunchKernelGGL(ts_emit_kernel, dim3((unsigned)nb * SC_ITEMS), dim3(TPB), 0, st, n, nb,
                        p1.order, p1.cnt, rts_tile_counts(p1.rs_ws), p1.box,
                        tbx, tby, w.ka, w.va, tile_bins, p1.dcount, i_host,
                        (uint32_t)(cap > 0xFFFFFFFELL ? 0xFFFFFFFELL : cap),
-                       assume ? sort_kept_word(p1.rs_ws) + 1 : nullptr, assume);
+                       assume ? sort_kept_word(p1.rs_ws) + 1 : nullptr, assume, w.gstart, w.gseg);
   if (!tail || m <= 0) return;
+  GenSrc g{w.gstart, p1.cnt, p1.order, w.gseg, p1.box, tbx, tby, (long long)n};
   radix_sort_pairs<uint32_t>(w.ka, w.va, w.kb, w.vb, nullptr, (uint32_t *)ids, m, 0, bits_for(T),
-                             w.rs, st, false, false, 0u, nullptr, n_dev, tile_bins, (uint32_t)T);
+                             w.rs, st, false, false, 0u, nullptr, n_dev, tile_bins, (uint32_t)T,
+                             w.gstart ? &g : nullptr);
   hipLaunchKernelGGL(ts_decode_kernel, dim3(cdiv(T, TPB)), dim3(TPB), 0, st, T, m, tile_bins,
                      n_dev);
 }
@@ -2369,6 +2548,14 @@ extern "C" void gsplat_tune_rb(int wgs, int regs, int map) {
   g_rb_knobs[2] = map;
 }
 
+// The tile sort's generated first pass from min_i intersections (capacity; < 0: leave);
+// returns the previous threshold.  Set it only between binnings: the workspace layout follows it.
+extern "C" long long gsplat_debug_tile_sort_gen(long long min_i) {
+  const long long prev = g_gen_min_i;
+  if (min_i >= 0) g_gen_min_i = min_i;
+  return prev;
+}
+
 extern "C" int gsplat_debug_depth_key_range(int on) {
   const int prev = g_key_range;
   if (on >= 0) g_key_range = on > 2 ? 2 : on;
@@ -2387,7 +2574,7 @@ extern "C" size_t gsplat_bin_emit_workspace_size_for(int num_points, int64_t num
   const long long T = (long long)tile_bounds_x * tile_bounds_y;
   if (num_points < 0 || num_intersects < 0 || tile_bounds_x <= 0 || tile_bounds_y <= 0) return 0;
   const size_t rb = rb_ws_bytes(rb_plan(num_points, tile_bounds_x, tile_bounds_y));
-  const size_t ts = carve_ts(nullptr, num_intersects, T).bytes;
+  const size_t ts = carve_ts(nullptr, num_intersects, T, num_points).bytes;
   const size_t sorted = rb > ts ? rb : ts;  // (either may run: the scheme is a test-hooks switch)
   if (!use_bucket(num_points, T)) return sorted;
   const size_t bk = carve_bk(nullptr, num_points, num_intersects, T).bytes;
@@ -2547,7 +2734,7 @@ extern "C" int gsplat_bin_speculative(int num_points, int64_t capacity, int tile
   Phase1 p1 = carve_phase1(workspace1, num_points);
   const bool region = use_region(num_points, T);
   const RbPlan rp = rb_plan(num_points, tile_bounds_x, tile_bounds_y);
-  const size_t need2 = region ? rb_ws_bytes(rp) : carve_ts(nullptr, capacity, T).bytes;
+  const size_t need2 = region ? rb_ws_bytes(rp) : carve_ts(nullptr, capacity, T, num_points).bytes;
   if (workspace1_bytes < p1.bytes || workspace2_bytes < need2) {
     set_error("bin_speculative: workspaces %zu/%zu < %zu/%zu bytes", workspace1_bytes,
               workspace2_bytes, p1.bytes, need2);
@@ -2639,7 +2826,7 @@ static int bin_emit_impl(int num_points, int64_t num_intersects, int64_t capacit
   }
   const bool region = use_region(num_points, T);
   const RbPlan rp = rb_plan(num_points, tile_bounds_x, tile_bounds_y);
-  const size_t need2 = region ? rb_ws_bytes(rp) : carve_ts(nullptr, cap, T).bytes;
+  const size_t need2 = region ? rb_ws_bytes(rp) : carve_ts(nullptr, cap, T, num_points).bytes;
   if (workspace1_bytes < p1.bytes || workspace2_bytes < need2) {
     set_error("bin_emit: workspaces %zu/%zu < %zu/%zu bytes", workspace1_bytes,
               workspace2_bytes, p1.bytes, need2);

@@ -240,6 +240,51 @@ def test_binning_prelaunched_emission(gpu, scheme, hooks):
         R._EMIT_CAP.pop(key, None)
 
 
+@pytest.mark.parametrize("scheme", ["shipped", "tilesort"])
+def test_binning_generated_first_pass(gpu, scheme, hooks):
+    """The tile sort's first pass generated from the depth-ordered allotments (shipped from 2^24
+    intersections, forced here from 1): bit-exact vs the oracle for the synchronous binning, a
+    pre-launched capacity above I and one below it, a speculative binning, and allotments that
+    disagree with the boxes (the sentinel slots, a Gaussian over 600 tiles)."""
+    from gaussctrl_exp_amd import rasterize as R
+    sc, cam, scales, quats = _inputs(150000, 640, 480, 2, 0.003, 0.03, 1.5)
+    g, o = _project_both(gpu, sc, cam, scales, quats)
+    xys, depths, radii, conics, nth, cov3d = [t.detach() for t in g]
+    ref = O.bin_and_sort(o[0], o[1], o[2], o[4], cam.tile_bounds)
+    n_ref = ref["num_intersects"]
+    key = (xys.device, xys.shape[0], cam.tile_bounds[0], cam.tile_bounds[1])
+    L = _lib.lib()
+    prev = (L.gsplat_debug_tile_sort_gen(1),
+            L.gsplat_debug_binning_scheme(BIN_SETTINGS[scheme]))
+    try:
+        for cap in (None, n_ref + 777, n_ref - 1, n_ref):
+            if cap is None:
+                R._EMIT_CAP.pop(key, None)
+            else:
+                R._EMIT_CAP[key] = cap
+            I, gids, bins = bin_gaussians(xys, depths, radii, nth, cam.height, cam.width)
+            assert I == n_ref, cap
+            np.testing.assert_array_equal(_np(gids), ref["gaussian_ids_sorted"])
+            np.testing.assert_array_equal(_np(bins), ref["tile_bins"])
+        # the padding semantics: the generated pass against the emitted one
+        nth2 = nth.clone()
+        vis = torch.nonzero(radii > 0).flatten()
+        nth2[vis[::7]] += 3
+        nth2[vis[5]] = 600
+        R._EMIT_CAP.pop(key, None)
+        got = bin_gaussians(xys, depths, radii, nth2, cam.height, cam.width)
+        L.gsplat_debug_tile_sort_gen(1 << 40)
+        R._EMIT_CAP.pop(key, None)
+        want = bin_gaussians(xys, depths, radii, nth2, cam.height, cam.width)
+        assert got[0] == want[0] == int(nth2[radii > 0].sum())
+        np.testing.assert_array_equal(_np(got[1]), _np(want[1]))
+        np.testing.assert_array_equal(_np(got[2]), _np(want[2]))
+    finally:
+        L.gsplat_debug_tile_sort_gen(prev[0])
+        L.gsplat_debug_binning_scheme(prev[1])
+        R._EMIT_CAP.pop(key, None)
+
+
 @pytest.mark.parametrize("fixed", [(0x5A00, 0xFF00), (0x5A0000, 0xFF0000),
                                    (0x5A5A00, 0xFFFF00), (0x0, 0x0)])
 def test_binning_depth_key_range(gpu, fixed, hooks):
