@@ -378,7 +378,7 @@ struct GenSrc {
 // level by level (owners' windows, window starts, then the owners' boxes and ids), so a wave
 // waits for three load latencies per G rounds instead of per round.  mk: the wave's G x 64 LDS
 // ints.
-constexpr int GEN_G = 4;
+constexpr int GEN_G = 16;
 template <int G>
 __device__ __forceinline__ void gen_rounds(const GenSrc &g, long long s0, long long n_slots,
                                            int *mk, uint32_t (&key)[G], uint32_t (&val)[G]) {
@@ -472,13 +472,14 @@ __global__ __launch_bounds__(TPB) void gen_count_kernel(GenSrc g, long long cap,
   h[tid] = 0;
   __syncthreads();
   const long long sg = (long long)blockIdx.x * TPB * ITEMS + (long long)wave * (ITEMS * 64);
-  static_assert(ITEMS % GEN_G == 0, "rounds in groups of GEN_G");
-  for (int r = 0; r < ITEMS; r += GEN_G) {
+  constexpr int GG = ITEMS < GEN_G ? ITEMS : GEN_G;
+  static_assert(ITEMS % GG == 0, "rounds in groups of GG");
+  for (int r = 0; r < ITEMS; r += GG) {
     if (sg + r * 64 >= n) break;  // wave-uniform
-    uint32_t k[GEN_G], v[GEN_G];
-    gen_rounds<GEN_G>(g, sg + r * 64, n, marks + wave * 64 * GEN_G, k, v);
+    uint32_t k[GG], v[GG];
+    gen_rounds<GG>(g, sg + r * 64, n, marks + wave * 64 * GG, k, v);
 #pragma unroll
-    for (int u = 0; u < GEN_G; ++u)
+    for (int u = 0; u < GG; ++u)
       if (sg + (r + u) * 64 + (tid & 63) < n) atomicAdd(&h[k[u] & (uint32_t)(R - 1)], 1u);
   }
   __syncthreads();
@@ -555,14 +556,15 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     // (the marks live in the tile's pair buffer, which is written only after the barriers of
     // the digit-base scan below)
     int *gmarks = reinterpret_cast<int *>(sm.raw);
-    static_assert(sizeof(sm.raw) >= sizeof(int) * TPB * GEN_G, "marks fit the pair buffer");
+    constexpr int GG = ITEMS < GEN_G ? ITEMS : GEN_G;
+    static_assert(sizeof(sm.raw) >= sizeof(int) * TPB * GG, "marks fit the pair buffer");
     const long long sg = (long long)t * TPB * ITEMS + (long long)wave * (ITEMS * 64);
 #pragma unroll
-    for (int r = 0; r < ITEMS; r += GEN_G) {
-      uint32_t k[GEN_G], v[GEN_G];
-      gen_rounds<GEN_G>(gen, sg + r * 64, n, gmarks + wave * 64 * GEN_G, k, v);
+    for (int r = 0; r < ITEMS; r += GG) {
+      uint32_t k[GG], v[GG];
+      gen_rounds<GG>(gen, sg + r * 64, n, gmarks + wave * 64 * GG, k, v);
 #pragma unroll
-      for (int u = 0; u < GEN_G; ++u) {
+      for (int u = 0; u < GG; ++u) {
         key[r + u] = (K)k[u];
         val[r + u] = v[u];
       }
