@@ -38,7 +38,7 @@ for f in files:
 # (gsplat_bin_emit_finish; all of it when the first tile pass is generated)
 EMIT_HEAD = ("emit_kernel", "bk_count_kernel", "bk_scan_kernel", "bk_place_kernel")
 EMIT_START = EMIT_HEAD + ("tc_first_kernel", "ep0_count_kernel")
-EMIT_END = ("bins_decode_kernel", "bk_sort_kernel<1024")
+EMIT_END = ("bins_decode_kernel", "ts_decode_kernel", "bk_sort_kernel<1024")
 PRE, FIN = "gsplat_bin_emit_prelaunch", "gsplat_bin_emit_finish"
 SPEC = "gsplat_bin_speculative"
 entries = collections.defaultdict(lambda: collections.defaultdict(float))
@@ -56,11 +56,12 @@ for f in files:
     count_part = []  # this segment's count-phase dispatches (re-labelled for the one-call binning)
     for d in sorted(disp):
         k = names[d]
-        if "fused_fwd_kernel" in k or "project_fwd_kernel" in k:
+        if "fused_fwd_kernel" in k or "fused_fwd_proj_kernel" in k or "project_fwd_kernel" in k:
             state, seg, count_part = "gsplat_bin_count_keyed_ex", seg + 1, []
             continue
-        if state == "gsplat_bin_count_keyed_ex" and "emit_scan_kernel" in k:
-            # round 4's gsplat_bin_speculative: count, emission and tile sort in one entry
+        if state == "gsplat_bin_count_keyed_ex" and ("emit_scan_kernel" in k or
+                                                      "ts_emit_kernel" in k):
+            # gsplat_bin_speculative (rounds 4 and 5): count, emission and tile sort in one entry
             for dd in count_part:
                 for c, v in disp[dd].items():
                     entries[state][(os.path.dirname(f), c)] -= v
@@ -73,6 +74,8 @@ for f in files:
         if state is None:
             continue
         if not k.startswith("gs::") and not k.startswith("void gs::"):
+            continue
+        if "fused_fwd_sh_kernel" in k:  # (the preprocess's colour part, on its own stream)
             continue
         for c, v in disp[d].items():
             entries[state][(os.path.dirname(f), c)] += v
