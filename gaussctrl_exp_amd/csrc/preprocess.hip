@@ -755,7 +755,10 @@ extern "C" int gsplat_exchange_pack_colors(int num_points, const void *grad_reco
 // gsplat_exchange_sparse_plan runs in the forward and the count's all-gather (the ranks
 // agree on the capacity) completes long before the backward packs the values.
 // xs_mask_kernel: one wave per 64 Gaussians -- the ballot is the mask word, its popcount goes
-// to the prefix slot (scanned in place by xs_scan_kernel).
+// to a scratch word in the (not yet written) values area, which xs_scan_kernel scans into the
+// prefix slots.  (Round 5 first scanned the prefix slots in place: a workgroup summing the
+// words before its chunk then raced the earlier workgroups rewriting theirs -- wrong prefixes
+// and a wrong total, seen as garbage capacities from the third step of a gloo rehearsal.)
 __global__ __launch_bounds__(256) void xs_mask_kernel(int n, const int *__restrict__ radii,
                                                       float *__restrict__ send) {
   const long long W = xs_words(n);
@@ -765,7 +768,7 @@ __global__ __launch_bounds__(256) void xs_mask_kernel(int n, const int *__restri
   const unsigned long long m = __ballot(g < n && radii[g] > 0);
   if ((threadIdx.x & 63) == 0) {
     reinterpret_cast<unsigned long long *>(send + XS_HDR)[w] = m;
-    reinterpret_cast<uint32_t *>(send + XS_HDR + 2 * W)[w] = (uint32_t)__popcll(m);
+    reinterpret_cast<uint32_t *>(send + XS_HDR + 3 * W)[w] = (uint32_t)__popcll(m);
   }
 }
 
@@ -779,20 +782,21 @@ __device__ __forceinline__ uint32_t xs_wave_incl_scan(uint32_t v) {
   return v;
 }
 
-// The exclusive scan of the W per-word counts, in place, XS_CHUNK words per workgroup: each
-// workgroup first sums the counts of every word before its chunk (L2-resident; the last one of
-// a 5M-Gaussian record reads ~78K words), then scans its chunk; the last workgroup writes the
-// total into the header.
+// The exclusive scan of the W per-word counts (the scratch words) into the prefix slots,
+// XS_CHUNK words per workgroup: each workgroup first sums the counts of every word before its
+// chunk (L2-resident; the last one of a 5M-Gaussian record reads ~78K words), then scans its
+// chunk; the last workgroup writes the total into the header.
 constexpr int XS_CHUNK = 4096;
 __global__ __launch_bounds__(1024) void xs_scan_kernel(long long W, float *__restrict__ send) {
   constexpr int PER = XS_CHUNK / 1024;
-  uint32_t *c = reinterpret_cast<uint32_t *>(send + XS_HDR + 2 * W);
+  uint32_t *c = reinterpret_cast<uint32_t *>(send + XS_HDR + 2 * W);           // prefix slots
+  const uint32_t *cnt = reinterpret_cast<const uint32_t *>(send + XS_HDR + 3 * W);  // counts
   __shared__ uint32_t wsum[16];
   __shared__ uint32_t base_s;
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const long long c0 = (long long)blockIdx.x * XS_CHUNK;
   uint32_t before = 0;
-  for (long long k = threadIdx.x; k < c0; k += 1024) before += c[k];
+  for (long long k = threadIdx.x; k < c0; k += 1024) before += cnt[k];
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) before += __shfl_xor(before, o, 64);
   if (threadIdx.x == 0) base_s = 0;
@@ -802,7 +806,7 @@ __global__ __launch_bounds__(1024) void xs_scan_kernel(long long W, float *__res
   uint32_t v[PER], tot = 0;
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
-    v[k] = s0 + k < W ? c[s0 + k] : 0u;
+    v[k] = s0 + k < W ? cnt[s0 + k] : 0u;
     tot += v[k];
   }
   const uint32_t inc = xs_wave_incl_scan(tot);

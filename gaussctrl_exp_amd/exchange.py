@@ -92,6 +92,7 @@ class ShViewExchange:
         self.geo = None  # multi-view step: the flat geometry gradient summed over this rank's views
         self.record_kinds = {"sparse": 0, "dense": 0}  # views exchanged per record kind (tests)
         self.last_record_floats = None  # length of the last record sent (bench)
+        self.last_capacity = None  # the agreed sparse capacity of the last planned view (bench)
         self._skip = 0  # views left to exchange dense without planning (DENSE_SKIP)
         self._buffers = {}
         self._host_counts = None
@@ -197,6 +198,7 @@ class ShViewExchange:
         if planned is not None:
             send = planned[0]
             cap = self._capacity(dev)
+            self.last_capacity = cap
             use_sparse = self.sparse == "on" or (
                 self.sparse == "auto" and sparse_floats(n, cap) <= SPARSE_MAX_FRAC * dense_len)
             if not use_sparse and sparse_floats(n, cap) > DENSE_HOPELESS_FRAC * dense_len:

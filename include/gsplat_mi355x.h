@@ -438,7 +438,8 @@ int gsplat_exchange_pack_colors(int num_points, const void *grad_records, size_t
  * index order, C >= the count (the capacity the ranks agreed on).
  * gsplat_exchange_sparse_floats: the record's length in floats for capacity C (-1: bad args).
  * gsplat_exchange_sparse_plan: writes the count, masks and prefix from radii (the forward,
- * once radii exist), into send's first 4 + 3W floats.
+ * once radii exist), into send's first 4 + 3W floats; send must hold 4 + 4W floats (the
+ * popcounts are staged in the values area, which pack overwrites).
  * gsplat_exchange_pack_sparse: after the raster backward, the camera centre and the values
  * (as gsplat_exchange_pack_colors computes them) into a planned send of >= that length. */
 long long gsplat_exchange_sparse_floats(int num_points, long long capacity);

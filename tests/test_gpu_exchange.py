@@ -229,11 +229,13 @@ def _expected_sparse(radii, rec, colors, campos, cap):
 
 
 @pytest.mark.parametrize("n,frac", [(1, 1.0), (63, 0.5), (1037, 0.55), (4101, 0.3),
-                                    (130_000, 0.55), (70_000, 0.0)])
+                                    (130_000, 0.55), (70_000, 0.0), (1_500_000, 0.55),
+                                    (700_000, 0.97)])
 def test_sparse_record_matches_restatement(gpu, n, frac):
     """gsplat_exchange_sparse_plan + _pack_sparse write exactly the layout exchange_layout.h
     states (bitmap, prefix, count, values in index order, camera centre), and the dense pack of
-    the same inputs holds the same values at the visible rows and zeros elsewhere."""
+    the same inputs holds the same values at the visible rows and zeros elsewhere.  (The two
+    largest cases span several scan workgroups: XS_CHUNK = 4,096 words each.)"""
     from gaussctrl_exp_amd import _lib
     from gaussctrl_exp_amd.exchange import sparse_floats
     radii, rec, colors, campos, (d_radii, d_rec, d_colors, d_campos) = _sparse_inputs(n, frac, n, gpu)
