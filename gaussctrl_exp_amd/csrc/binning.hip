@@ -1129,6 +1129,7 @@ __global__ __launch_bounds__(TPB) void ts_decode_kernel(long long T, long long c
   if (r.y > 0) reinterpret_cast<int2 *>(bins)[t] = make_int2((int)(n - r.x), r.y);
 }
 
+#ifdef GSPLAT_TEST_HOOKS  // A/B only (gsplat_debug_binning_scheme 2): measured slower
 // ------------------------------------------------------------------ region binning
 // The depth-ordered Gaussians -> gsplat's tile lists (gaussian_ids_sorted, tile_bins) without
 // emitting (tile, id) pairs or sorting them by tile.  A tile's list is the depth-ordered
@@ -1654,6 +1655,14 @@ RbWs rb_ws(const RbPlan &p, void *base) {
 size_t rb_ws_bytes(const RbPlan &p) {
   return (size_t)(p.rows + p.R + 2) * (size_t)p.TS * sizeof(uint32_t) + 256;
 }
+
+#else  // the shipped library: no region binning (use_region() is false there)
+struct RbPlan {
+  int gw = 1, gh = 1, gxn = 1;
+};
+RbPlan rb_plan(int, int, int) { return RbPlan{}; }
+size_t rb_ws_bytes(const RbPlan &) { return 0; }
+#endif  // GSPLAT_TEST_HOOKS
 
 // tile_bins[t] = [first, last+1) of tile t in the tile-sorted keys (tile_bins pre-zeroed).
 template <typename K, int SHIFT>
@@ -2504,8 +2513,13 @@ bool use_bucket(long long n, long long T) {
   if (T + 1 > BK_MAX_BUCKETS) return false;
   return g_bin_scheme < 0 ? n <= (1LL << 17) : g_bin_scheme == 1;
 }
+#ifdef GSPLAT_TEST_HOOKS
 bool use_region(long long n, long long T) { return g_bin_scheme == 2 && !use_bucket(n, T); }
+#else
+bool use_region(long long, long long) { return false; }
+#endif
 
+#ifdef GSPLAT_TEST_HOOKS
 // The region binning (rb_*) over phase 1's depth-ordered records into workspace2
 // (rb_ws_bytes): head = count, column scan, tile table (no I-sized buffer: they can run before
 // the host knows I), tail = the placement into gaussian_ids_sorted (cap slots).  i_host: the
@@ -2530,6 +2544,11 @@ void rb_launch(const RbPlan &rp, int n, const Phase1 &p1, void *ws2, int32_t *id
                        p1.cnt, p1.box, w.cw, w.cr, w.tstart, (uint32_t *)ids, p1.dcount,
                        cap > 0xFFFFFFFEull ? 0xFFFFFFFEu : (uint32_t)cap);
 }
+
+#else
+void rb_launch(const RbPlan &, int, const Phase1 &, void *, int32_t *, int32_t *,
+               unsigned long long, int32_t *, uint32_t, bool, bool, hipStream_t) {}
+#endif
 
 }  // namespace
 

@@ -293,7 +293,7 @@ def bin_gaussians_speculative(xys: Tensor, depths: Tensor, radii: Tensor, num_ti
     ids_buf, ws2 = _emit_buffers(dev, n, cap, tbx, tby)
     slot, counts, host = _COUNTS.acquire(dev)
     try:
-        # the count phase and the region binning in one call
+        # the count phase and the tile sort in one call
         assume = _assumed_constant(key)
         rc = _lib.call_status("gsplat_bin_speculative", n, cap, tbx, tby, P(counts), P(ws1),
                               ws1.numel(), assume, P(ids_buf), P(tile_bins),

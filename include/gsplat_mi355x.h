@@ -188,9 +188,10 @@ int gsplat_get_tile_bin_edges(int64_t num_intersects, const int64_t *isect_ids_s
  * d_counts[1] = total intersections I (device int32[2]).  The caller reads d_counts -- the
  * one host sync, like gsplat's cum_tiles_hit[-1].item() -- sizes gaussian_ids_sorted from I,
  * and calls gsplat_bin_emit with BOTH workspaces (phase 1's must be left untouched in
- * between).  Phase 2 (the region binning: each depth-ordered intersection placed straight into
- * its tile's list) writes gaussian_ids_sorted [I] and tile_bins [tbx*tby, 2]; the order is
- * identical to a stable sort of gsplat's 64-bit isect_ids. */
+ * between).  Phase 2 (the tile sort: the depth-ordered intersections emitted as (tile, id)
+ * pairs -- or, from 2^24 of them, generated inside the first pass -- and sorted stably by tile;
+ * small scenes: tile buckets with per-tile sorts) writes gaussian_ids_sorted [I] and tile_bins
+ * [tbx*tby, 2]; the order is identical to a stable sort of gsplat's 64-bit isect_ids. */
 size_t gsplat_bin_count_workspace_size(int num_points);
 /* Phase-2 workspace for the binning scheme in use (it depends on N and the tile grid; the
  * small-scene tile buckets also on I). */
@@ -223,8 +224,8 @@ int gsplat_bin_emit(int num_points, int64_t num_intersects, int tile_bounds_x,
 /* Phase 2 split around the host's read of I, so that the GPU is not idle while the host
  * waits for it: gsplat_bin_emit_prelaunch, issued right after phase 1 with buffers sized for
  * `capacity` intersections (e.g. the last call's I plus a margin), launches the part of
- * phase 2 that needs only phase 1's results (the region binning's counts and tile table;
- * I > capacity leaves the table all-zero).  Then, with the host's I:
+ * phase 2 that needs only phase 1's results (the emission into capacity slots, the table
+ * cleared; I > capacity emits nothing and leaves the table all-zero).  Then, with the host's I:
  *   I <= capacity: gsplat_bin_emit_finish(..., I, capacity, ...) with the SAME buffers, stream
  *                  and capacity (the workspace layout follows capacity);
  *   I >  capacity: gsplat_bin_emit (or a new prelaunch + finish) into buffers sized for I.
@@ -238,8 +239,8 @@ int gsplat_bin_emit_finish(int num_points, int64_t num_intersects, int64_t capac
                            int tile_bounds_x, int tile_bounds_y, int32_t *gaussian_ids_sorted,
                            int32_t *tile_bins, const void *workspace1, size_t workspace1_bytes,
                            void *workspace2, size_t workspace2_bytes, void *stream);
-/* The whole of phase 2 before the host knows I: the region binning launched for `capacity`
- * intersections, its placement reading the device-side I -- so the blend can be launched right
+/* The whole of phase 2 before the host knows I: the emission and tile sort launched for
+ * `capacity` intersections, sorting the device-side I -- so the blend can be launched right
  * behind it and the host reads I (d_counts[1]) only afterwards, while the GPU works.
  * I <= capacity: gaussian_ids_sorted[0, I) and tile_bins are gsplat_bin_emit's exactly.
  * I > capacity: nothing is placed and tile_bins is left all-zero (a blend behind it renders the

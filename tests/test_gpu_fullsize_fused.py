@@ -4,8 +4,9 @@ TrainStep(loss="l1", render_mode="fused").forward_backward (fused.render_fused w
 inside the blend), i.e. the kernels of the bench line's `kernels` block:
 
   gsplat_fused_preprocess_forward_part [2] (SH colours, second stream) + [1] (projection, keys)
-  gsplat_bin_speculative       (depth sort + region binning at the learned capacity: the second
-                                call of the frame shape -- the first one bins synchronously)
+  gsplat_bin_speculative       (depth sort + tile sort at the learned capacity, its first pass
+                                generated at c5: the second call of the frame shape -- the
+                                first one bins synchronously)
   gsplat_rasterize_forward_clearing_l1   (blend + L1 partials + records cleared)
   gsplat_rasterize_backward_records_l1   (L1 upstream formed per pixel, record backward; strip
                                           geometry from 3,584 tiles, 8x8 blocks + list split below)
