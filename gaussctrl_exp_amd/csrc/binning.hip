@@ -86,10 +86,15 @@ __device__ __forceinline__ unsigned long long digit_peers(uint32_t d, int width,
 
 // Single workgroup: exclusive scan of partial[0..nb) in place; grand total -> *total.
 // (in_place false: only the total, partial[] left as the block sums)
+// kfin / assume / vflag: the count phase's depth-key range check for a later emission call
+// (gsplat_bin_emit_speculative): vflag = 1 when a digit the sort assumed constant varied.
 __global__ __launch_bounds__(1024) void scan_partials_kernel(uint32_t *__restrict__ partial,
                                                              int nb, uint32_t *__restrict__ total_out,
                                                              uint32_t *__restrict__ total_dev = nullptr,
-                                                             bool in_place = true) {
+                                                             bool in_place = true,
+                                                             const uint32_t *__restrict__ kfin = nullptr,
+                                                             uint32_t assume = 0,
+                                                             uint32_t *__restrict__ vflag = nullptr) {
   __shared__ uint32_t lds[16];
   uint32_t running = 0;
   for (int c = 0; c < nb; c += 1024) {
@@ -103,6 +108,7 @@ __global__ __launch_bounds__(1024) void scan_partials_kernel(uint32_t *__restric
   if (threadIdx.x == 0) {
     if (total_dev) *total_dev = running;  // device copy (read by the pre-launched emission)
     if (total_out) *total_out = running;
+    if (vflag) *vflag = (assume && kfin && ((kfin[0] ^ kfin[1]) & assume)) ? 1u : 0u;
   }
 }
 
@@ -924,12 +930,16 @@ __global__ __launch_bounds__(TPB) void gather_counts_kernel(int n, const uint32_
                                                             int *__restrict__ num_visible,
                                                             uint32_t *__restrict__ partial,
                                                             uint32_t *__restrict__ rmask = nullptr,
-                                                            int gw = 1, int gh = 1, int gxn = 1) {
+                                                            int gw = 1, int gh = 1, int gxn = 1,
+                                                            uint32_t *__restrict__ vflag = nullptr) {
   __shared__ uint32_t lds[TPB / 64];
   const long long base = (long long)blockIdx.x * SC_TILE;
   uint32_t sum = 0;
   const long long nv = min((long long)n, (long long)*kept);
-  if (blockIdx.x == 0 && threadIdx.x == 0) *num_visible = (int)nv;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    *num_visible = (int)nv;
+    if (vflag) *vflag = 0u;  // (set by scan_partials_kernel when it checks the key range)
+  }
   if (base < nv) {  // workgroup-uniform
     // all ids, then all records, with clamped indices and no per-item branch, so each level
     // of the gather has its 16 loads in flight together
@@ -1022,7 +1032,8 @@ __global__ __launch_bounds__(TPB) void ts_emit_kernel(int n, int nb,
                                                       const uint32_t *__restrict__ kfin,
                                                       uint32_t assume,
                                                       uint32_t *__restrict__ gstart = nullptr,
-                                                      uint32_t *__restrict__ gseg = nullptr) {
+                                                      uint32_t *__restrict__ gseg = nullptr,
+                                                      const uint32_t *__restrict__ vflag = nullptr) {
   __shared__ uint32_t lds[TPB / 64];
   __shared__ int marks[TPB];
   for (long long i = (long long)blockIdx.x * TPB + threadIdx.x; i < 2LL * tbx * tby;
@@ -1053,7 +1064,9 @@ __global__ __launch_bounds__(TPB) void ts_emit_kernel(int n, int nb,
   uint32_t bpre, btot;
   block_exclusive_scan<TPB>(pre, bpre, lds);  // (only the totals are used)
   block_exclusive_scan<TPB>(tot, btot, lds);
-  const bool violated = assume && kfin && (((kfin[0] ^ kfin[1]) & assume) != 0u);
+  // (vflag: the count phase found the range violated -- a separate count call)
+  const bool violated =
+      (assume && kfin && (((kfin[0] ^ kfin[1]) & assume) != 0u)) || (vflag && *vflag);
   if (blockIdx.x == 0 && tid == 0) {
     *i_dev = violated ? 0xFFFFFFFFu : btot;
     if (i_host) *i_host = (int32_t)btot;
@@ -2490,7 +2503,8 @@ void ts_launch(int n, const Phase1 &p1, void *ws2, int32_t *ids, int32_t *tile_b
                        p1.order, p1.cnt, rts_tile_counts(p1.rs_ws), p1.box,
                        tbx, tby, w.ka, w.va, tile_bins, p1.dcount, i_host,
                        (uint32_t)(cap > 0xFFFFFFFELL ? 0xFFFFFFFELL : cap),
-                       assume ? sort_kept_word(p1.rs_ws) + 1 : nullptr, assume, w.gstart, w.gseg);
+                       assume ? sort_kept_word(p1.rs_ws) + 1 : nullptr, assume, w.gstart, w.gseg,
+                       p1.dcount + 2);
   if (!tail || m <= 0) return;
   GenSrc g{w.gstart, p1.cnt, p1.order, w.gseg, p1.box, tbx, tby, (long long)n};
   radix_sort_pairs<uint32_t>(w.ka, w.va, w.kb, w.vb, nullptr, (uint32_t *)ids, m, 0, bits_for(T),
@@ -2682,13 +2696,15 @@ static int bin_count_impl(int num_points, const float *xys, const float *depths,
   const RbPlan rp = rb_plan(n, tile_bounds_x, tile_bounds_y);
   hipLaunchKernelGGL(gather_counts_kernel, dim3(nb), dim3(TPB), 0, st, n, p.order, kept, p.rec,
                      p.cnt, p.box, d_counts, partial, use_region(n, T) ? p.rmask : nullptr, rp.gw,
-                     rp.gh, rp.gxn);
+                     rp.gh, rp.gxn, p.dcount + 2);
   // (the speculative binning: I from ts_emit_kernel / rb_tiles_kernel)
   if (no_scan) return check_launch("bin_count");
   // I = the sum of the block sums, which stay as they are: the emission (ts_emit_kernel)
   // scans them itself, so a speculative count phase (no_scan) and this one leave the same state
+  const uint32_t chk = range_out && use_key_range(n) ? assume_const : 0u;
   hipLaunchKernelGGL(scan_partials_kernel, dim3(1), dim3(1024), 0, st, partial, nb,
-                     (uint32_t *)(d_counts + 1), p.dcount, false);
+                     (uint32_t *)(d_counts + 1), p.dcount, false, chk ? kept + 1 : nullptr, chk,
+                     p.dcount + 2);
   return check_launch("bin_count");
 }
 

@@ -107,16 +107,19 @@ class _FusedRender(Function):
                           P(radii), P(conics), P(nth), P(colors), P(opac), P(ws1), ws1.numel(),
                           st)
                 return
+            colours_part()
+            _lib.call("gsplat_fused_preprocess_forward_part", 1, n, K, int(degrees_to_use),
+                      P(means), P(scales), P(quats), P(opacities), P(features_dc),
+                      P(features_rest), *cam_args, P(xys), P(depths), P(radii), P(conics),
+                      P(nth), None, P(opac), P(ws1), ws1.numel(), st)
+
+        def colours_part():
             cur = torch.cuda.current_stream(dev)
             side = _side_stream(dev)
             side.wait_stream(cur)
             _lib.call("gsplat_fused_preprocess_forward_part", 2, n, K, int(degrees_to_use),
                       P(means), None, None, None, P(features_dc), P(features_rest), *cam_args,
                       None, None, None, None, None, P(colors), None, None, 0, side.cuda_stream)
-            _lib.call("gsplat_fused_preprocess_forward_part", 1, n, K, int(degrees_to_use),
-                      P(means), P(scales), P(quats), P(opacities), P(features_dc),
-                      P(features_rest), *cam_args, P(xys), P(depths), P(radii), P(conics),
-                      P(nth), None, P(opac), P(ws1), ws1.numel(), st)
 
         def join_colours():
             if split_colours:

@@ -272,12 +272,14 @@ def speculative_capacity(n: int, img_height: int, img_width: int, dev) -> int:
 
 def bin_gaussians_speculative(xys: Tensor, depths: Tensor, radii: Tensor, num_tiles_hit: Tensor,
                               img_height: int, img_width: int,
-                              keyed_workspace: Optional[Tensor] = None):
+                              keyed_workspace: Optional[Tensor] = None, between=None):
     """bin_gaussians without the host read of I in the middle: the count phase, then -- when
     this frame shape's capacity is known from an earlier call and the binning scheme allows it
     -- the emission and the whole tile sort at that capacity (gsplat_bin_emit_speculative).
     Returns a SpeculativeBinning (finish() before using I), or None when the capacity is not
-    known yet or the scheme needs I on the host (the caller then uses bin_gaussians)."""
+    known yet or the scheme needs I on the host (the caller then uses bin_gaussians).
+    between: called between the count phase (the depth sort) and the emission + tile sort,
+    which then go out as two C-ABI calls (the sorted scheme only); None: one call."""
     n = xys.shape[0]
     tbx = (img_width + BLOCK_X - 1) // BLOCK_X
     tby = (img_height + BLOCK_Y - 1) // BLOCK_Y
@@ -295,9 +297,19 @@ def bin_gaussians_speculative(xys: Tensor, depths: Tensor, radii: Tensor, num_ti
     try:
         # the count phase and the tile sort in one call
         assume = _assumed_constant(key)
-        rc = _lib.call_status("gsplat_bin_speculative", n, cap, tbx, tby, P(counts), P(ws1),
-                              ws1.numel(), assume, P(ids_buf), P(tile_bins),
-                              P(ws2), ws2.numel(), st)
+        if between is not None and n > BUCKET_MAX_N:
+            _lib.call("gsplat_bin_count_keyed_ex", n, tbx, tby, P(counts), P(ws1), ws1.numel(),
+                      assume, st)
+            between()
+            rc = _lib.call_status("gsplat_bin_emit_speculative", n, cap, tbx, tby, P(ids_buf),
+                                  P(tile_bins), P(ws1), ws1.numel(), P(ws2), ws2.numel(), st)
+            if rc != 0:
+                raise RuntimeError("gsplat_bin_emit_speculative failed (" + str(rc) + "): " +
+                                   _lib.lib().gsplat_last_error().decode(errors="replace"))
+        else:
+            rc = _lib.call_status("gsplat_bin_speculative", n, cap, tbx, tby, P(counts), P(ws1),
+                                  ws1.numel(), assume, P(ids_buf), P(tile_bins),
+                                  P(ws2), ws2.numel(), st)
         if rc == 2:  # the scheme needs I on the host: count, then finish as bin_gaussians does
             _lib.call("gsplat_bin_count_keyed_ex", n, tbx, tby, P(counts), P(ws1), ws1.numel(),
                       _assumed_constant(key), st)
@@ -346,6 +358,8 @@ def bin_gaussians_speculative(xys: Tensor, depths: Tensor, radii: Tensor, num_ti
     return sb
 
 
+# the tile buckets' size limit (binning.hip use_bucket: N <= 2^17 takes them)
+BUCKET_MAX_N = 1 << 17
 # frame shape -> the intersection capacity to pre-allocate the emission's outputs for
 _EMIT_CAP = {}
 # frame shape -> the intersection counts of its last CAP_WINDOW binnings: the capacity is 1/8

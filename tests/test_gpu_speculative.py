@@ -82,6 +82,42 @@ def test_speculative_binning_equals_sync(gpu, n, W, H, cap_scale):
     assert R._EMIT_CAP[key] == R.emit_capacity(I)
 
 
+@pytest.mark.parametrize("case", ["plain", "overflow", "range"])
+def test_split_speculative_binning(gpu, case):
+    """The speculative binning as two calls (the count phase, a callback, then
+    gsplat_bin_emit_speculative -- the fused render's colour part goes out in between): equal
+    to the synchronous binning; an overflow and a depth-key range violation found by the count
+    call leave the table all-zero and write no id (the emission call checks the count phase's
+    violation flag on the device)."""
+    n, W, H = 200_000, 640, 480
+    sc = synthetic_scene(n, 3, seed=11, scale_lo=0.004, scale_hi=0.03)
+    xys, depths, radii, nth, ws1, cam = _keyed(gpu, sc, synthetic_camera(W, H))
+    key = (gpu, n, (W + 15) // 16, (H + 15) // 16)
+    R._EMIT_CAP.pop(key, None)
+    R._KEY_VARY.pop(key, None)
+    I, ids, bins = R.bin_gaussians(xys, depths, radii, nth, H, W, keyed_workspace=_fresh_ws(ws1))
+    if case == "overflow":
+        R._EMIT_CAP[key] = I // 2
+    if case == "range":
+        R._KEY_VARY[key] = 0xFF  # "only the low byte varies": the upper passes are skipped
+    called = []
+    spec = R.bin_gaussians_speculative(xys, depths, radii, nth, H, W,
+                                       keyed_workspace=_fresh_ws(ws1),
+                                       between=lambda: called.append(1))
+    assert called == [1]
+    ok = spec.finish()
+    torch.cuda.synchronize()
+    if case == "plain":
+        assert ok and spec.num_intersects == I
+        np.testing.assert_array_equal(spec.ids[:I].cpu().numpy(), ids.cpu().numpy())
+        np.testing.assert_array_equal(spec.tile_bins.cpu().numpy(), bins.cpu().numpy())
+    else:
+        assert not ok and spec.range_violated == (case == "range")
+        assert int(spec.tile_bins.abs().sum()) == 0
+    R._EMIT_CAP.pop(key, None)
+    R._KEY_VARY.pop(key, None)
+
+
 def _fused(gpu, sc, cam, gt, bg):
     s = sc.to(gpu).requires_grad_()
     out = render_fused(s, cam.to(gpu), 3, bg, return_alpha=True)
