@@ -128,7 +128,7 @@ HOOK_SIGNATURES = {
     "gsplat_debug_tile_sort_gen": (_I64, [_I64]),
 }
 
-ABI_VERSION = 15  # include/gsplat_mi355x.h GSPLAT_MI355X_ABI_VERSION
+ABI_VERSION = 16  # include/gsplat_mi355x.h GSPLAT_MI355X_ABI_VERSION
 
 _lib = None
 _DETERMINISTIC = os.environ.get("GSPLAT_MI355X_DETERMINISTIC", "0") not in ("", "0")

@@ -41,7 +41,9 @@
 extern "C" {
 #endif
 
-#define GSPLAT_MI355X_ABI_VERSION 15
+/* 16: gsplat_exchange_sparse_plan needs a send buffer of 4 + 4W floats (its popcounts are staged
+ * in the values area); the binning's phase-2 workspace layout follows the tile sort. */
+#define GSPLAT_MI355X_ABI_VERSION 16
 
 int gsplat_abi_version(void);
 const char *gsplat_last_error(void);
