@@ -8,12 +8,16 @@ or sigmoid(dc) (:203), sigmoid(opacities) (:215) -- then calls project_gaussians
 spherical_harmonics (:200) and rasterize_gaussians (:208) and clamps the image (:222).
 `render_fused` computes the same image and the same six parameter gradients with
 
-  forward:  gsplat_fused_preprocess_forward_binned (activations + projection + SH + clamp
-            + the binning's depth keys, one kernel) -> gsplat_bin_count_keyed /
-            gsplat_bin_emit -> gsplat_rasterize_forward_clearing
-            (the blend, which also zeroes the backward's per-Gaussian gradient records)
-  backward: gsplat_rasterize_backward_records -> gsplat_fused_preprocess_backward (projection
-            VJP + SH backward + the activations' chain rule, one kernel)
+  forward:  gsplat_fused_preprocess_forward_part [1] (activations + projection + the
+            binning's depth keys and records) with [2] (SH + clamp) on a second stream from
+            3,584 tiles (else gsplat_fused_preprocess_forward_binned, one kernel) ->
+            gsplat_bin_speculative (depth sort + tile sort launched at the capacity learned
+            from the frame shape's earlier calls: no host read of the intersection count before
+            the blend; the first call: gsplat_bin_count_keyed_ex / gsplat_bin_emit) ->
+            gsplat_rasterize_forward_clearing(_l1) (the blend, which also zeroes the
+            backward's per-Gaussian gradient records and, with the L1 loss, sums it)
+  backward: gsplat_rasterize_backward_records(_l1) -> gsplat_fused_preprocess_backward(_adam)
+            (projection VJP + SH backward + the activations' chain rule, one kernel)
 
 so none of the glue's elementwise kernels, reductions, the cat, its backward's strided copies
 or the caller's `radii.sum() == 0` host sync remain.  Results equal the unchanged-caller path
