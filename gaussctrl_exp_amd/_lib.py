@@ -261,8 +261,18 @@ def ptr(t):
     return None if t is None else t.data_ptr()
 
 
+_RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def stream(device) -> int:
-    """The current HIP stream of `device`, as the `void *stream` argument."""
+    """The current HIP stream of `device`, as the `void *stream` argument (the raw handle
+    straight from the stream registry: ~0.3 us instead of ~2.5 us for a torch.cuda.Stream
+    object per call, tools/host_timeline.py)."""
+    if _RAW_STREAM is not None:
+        if not isinstance(device, (torch.device, int)):
+            device = torch.device(device)
+        idx = device.index if isinstance(device, torch.device) else device
+        return _RAW_STREAM(torch.cuda.current_device() if idx is None else int(idx))
     return torch.cuda.current_stream(device).cuda_stream
 
 

@@ -412,9 +412,54 @@ def _campos(cam: GCCamera) -> Tensor:
     return t
 
 
+class _DirectCtx:
+    """The context _FusedRender.forward / backward read and write, for a training step that
+    calls the two back to back without an autograd graph (render_fused(direct=True)): the same
+    kernels and gradients, without Function.apply, the saved-tensor bookkeeping, the engine's
+    hand-off to its device thread and AccumulateGrad -- ~100 us of host time per step, which is
+    what bounds the small frames' step (c3: host 0.41 ms per step against 0.26 ms of kernels,
+    tools/host_timeline.py)."""
+
+    def __init__(self, needs_input_grad):
+        self.needs_input_grad = needs_input_grad
+        self.saved_tensors = ()
+
+    def save_for_backward(self, *tensors):
+        self.saved_tensors = tensors
+
+    def set_materialize_grads(self, value):
+        pass
+
+    def mark_non_differentiable(self, *tensors):
+        pass
+
+
+# the training step calls the fused forward and backward directly (TrainStep); "0": through
+# autograd (A/B runs)
+DIRECT_STEP = os.environ.get("GSPLAT_MI355X_DIRECT_STEP", "1") != "0"
+_UNIT = {}
+
+
+def _unit_grad(dev) -> Tensor:
+    """A kept scalar 1.0: the loss's own gradient (autograd's seed is a fill kernel per step)."""
+    t = _UNIT.get(dev)
+    if t is None:
+        t = _UNIT[dev] = torch.ones((), device=dev, dtype=torch.float32)
+    return t
+
+
+def direct_step_ok(scene) -> bool:
+    """render_fused(direct=True) takes the parameters' gradients itself: it needs them as the
+    contiguous fp32 leaves the kernels read (no copy for autograd to route a gradient through)."""
+    return DIRECT_STEP and all(
+        t.is_leaf and t.dtype == torch.float32 and t.is_contiguous()
+        for t in (scene.means, scene.scales, scene.quats, scene.opacities, scene.features_dc,
+                  scene.features_rest))
+
+
 def render_fused(scene, cam: GCCamera, sh_degree_to_use: int, background: Tensor,
                  return_alpha: bool = False, clamp: bool = True, adam=None,
-                 l1_gt: Optional[Tensor] = None):
+                 l1_gt: Optional[Tensor] = None, direct: bool = False):
     """scene.render's training output (gc_model.py:158-222) through the fused kernels.
 
     Returns dict(rgb [H,W,3] (clamped at 1 as gc_model.py:222 -- or, clamp=False, the raw
@@ -428,7 +473,11 @@ def render_fused(scene, cam: GCCamera, sh_degree_to_use: int, background: Tensor
     l1_gt [H,W,3]: also return "loss" = mean |clamp(rgb, max=1) - l1_gt| (the training step's
     L1, splatfacto's loss at ssim_lambda 0), computed by the blend kernel; the loss is the
     differentiable output (its backward forms the image gradient inside the rasterizer
-    backward) and "rgb" is the detached raw image (clamp ignored)."""
+    backward) and "rgb" is the detached raw image (clamp ignored).
+    direct (with l1_gt; direct_step_ok(scene)): no autograd graph -- "loss" is detached and
+    "backward" is a callable that runs the fused backward of d loss / d loss = 1 (or its
+    argument) and accumulates the six gradients into the parameters' .grad as autograd's
+    loss.backward() would (TrainStep's step)."""
     aux = {}
     args = [_contig_f32(scene.means), _contig_f32(scene.scales), _contig_f32(scene.quats),
             _contig_f32(scene.opacities), _contig_f32(scene.features_dc),
@@ -436,7 +485,36 @@ def render_fused(scene, cam: GCCamera, sh_degree_to_use: int, background: Tensor
             _campos(cam), cam.fx, cam.fy, cam.cx, cam.cy, cam.height, cam.width,
             int(sh_degree_to_use), _contig_f32(background), bool(return_alpha), aux, adam,
             l1_gt]
-    out = _FusedRender.apply(*args)
+    backward = None
+    if direct:
+        if l1_gt is None or not direct_step_ok(scene):
+            raise ValueError("render_fused(direct=True) needs l1_gt and contiguous fp32 leaf "
+                             "parameters (direct_step_ok)")
+        params = args[:6]
+        ctx = _DirectCtx(tuple(t.requires_grad for t in params) + (False,) * 15)
+        with torch.no_grad():
+            out = _FusedRender.forward(ctx, *args)
+
+        def backward(grad: Optional[Tensor] = None):
+            """The step's backward (once): d loss -> the parameters' .grad (accumulated)."""
+            nonlocal ctx
+            if ctx is None:
+                raise RuntimeError("render_fused(direct=True): backward already ran")
+            c, ctx = ctx, None
+            if not any(c.needs_input_grad[:6]):
+                return
+            g = _unit_grad(out[0].device) if grad is None else grad
+            with torch.no_grad():
+                grads = _FusedRender.backward(c, g, None)
+                for p, gp in zip(params, grads[:6]):
+                    if gp is None or not p.requires_grad:
+                        continue
+                    if p.grad is None:
+                        p.grad = gp
+                    else:
+                        p.grad += gp
+    else:
+        out = _FusedRender.apply(*args)
     loss = None
     if l1_gt is not None:
         loss, img = out
@@ -471,7 +549,7 @@ def render_fused(scene, cam: GCCamera, sh_degree_to_use: int, background: Tensor
         g = split_records()
         return None if g is None else tuple(g)
 
-    return {"rgb": rgb, "clamped": bool(clamp), "loss": loss,
+    return {"rgb": rgb, "clamped": bool(clamp), "loss": loss, "backward": backward,
             "accumulation": alpha[..., None] if alpha is not None else None,
             "xys": aux["xys"], "radii": aux["radii"], "xys_grad": xys_grad,
             "raster_grads": raster_grads,

@@ -122,12 +122,13 @@ def last_num_visible(dev) -> int:
     return int(_COUNTS.last_visible.get(dev, 0))
 
 
-def _wait_count(host, stream, spin_s: float = 2.0) -> int:
+def _wait_count(host, dev, spin_s: float = 2.0) -> int:
     """The single host sync of the binning (gsplat: cum_tiles_hit[-1].item()): the scan kernel
     writes the intersection count once, straight into this call's pinned slot, so the host
     polls that word (about a microsecond from the write to the read) instead of a copy kernel
     plus a stream synchronisation (tens of microseconds of wake-up latency).  Falls back to
-    synchronising the stream the binning was issued on if nothing arrives within spin_s."""
+    synchronising the stream the binning was issued on (dev's current stream) if nothing
+    arrives within spin_s."""
     t_end = None
     while True:
         v = int(host[1])
@@ -136,7 +137,7 @@ def _wait_count(host, stream, spin_s: float = 2.0) -> int:
         if t_end is None:
             t_end = time.perf_counter() + spin_s
         elif time.perf_counter() > t_end:
-            stream.synchronize()
+            torch.cuda.current_stream(dev).synchronize()
             v = int(host[1])
             if v == -1:
                 raise RuntimeError("bin_gaussians: the intersection count was never written")
@@ -188,7 +189,7 @@ def bin_gaussians(xys: Tensor, depths: Tensor, radii: Tensor, num_tiles_hit: Ten
         if cap and PRELAUNCH_EMISSION:
             _lib.call("gsplat_bin_emit_prelaunch", n, cap, tbx, tby, P(tile_bins), P(ws1),
                       ws1.numel(), P(pre[1]), pre[1].numel(), st)
-        num_intersects = _wait_count(host, torch.cuda.current_stream(dev))
+        num_intersects = _wait_count(host, dev)
         visible = int(host[0])
         if keyed_workspace is not None:
             _note_key_range(key, host)
@@ -233,7 +234,7 @@ class SpeculativeBinning:
     def finish(self) -> bool:
         visible = None
         try:
-            I = _wait_count(self.host, torch.cuda.current_stream(self.dev))
+            I = _wait_count(self.host, self.dev)
             visible = int(self.host[0])
             # a depth-sort digit assumed constant from earlier calls varied: the order is wrong
             # (the caller re-runs the preprocess -- the sort consumed its keys -- and re-bins)
@@ -317,7 +318,7 @@ def bin_gaussians_speculative(xys: Tensor, depths: Tensor, radii: Tensor, num_ti
             if PRELAUNCH_EMISSION:
                 _lib.call("gsplat_bin_emit_prelaunch", n, cap, tbx, tby, P(tile_bins), P(ws1),
                           ws1.numel(), P(ws2), ws2.numel(), st)
-            I = _wait_count(host, torch.cuda.current_stream(dev))
+            I = _wait_count(host, dev)
             violated = int(host[2]) != 0
             _note_key_range(key, host)
             _COUNTS.release(dev, slot, int(host[0]))

@@ -25,7 +25,7 @@ import torch.nn.functional as F
 
 from .camera import GCCamera
 from .exchange import ShViewExchange
-from .fused import render_fused
+from .fused import direct_step_ok, render_fused
 from .scene import PARAM_NAMES, GaussianScene, render
 
 # gc_config.py:58-87 (Adam, eps 1e-15); xyz decays 1.6e-4 -> 1.6e-6 over 30k steps.
@@ -218,10 +218,12 @@ class TrainStep:
     def _render(self, cam: GCCamera, background: torch.Tensor, adam=None, gt=None):
         if self.render_mode == "fused":  # raw image: the loss applies the clamp
             # the L1 loss folded into the blend kernels (fused.render_fused l1_gt) unless
-            # fuse_l1 is off
+            # fuse_l1 is off; with it, the forward and backward are called directly (no
+            # autograd graph: out["backward"], fused.direct_step_ok)
             l1 = gt if (self.loss_kind == "l1" and self.fuse_l1 and gt is not None) else None
             return render_fused(self.scene, cam, self.sh_degree, background, clamp=False,
-                                adam=adam, l1_gt=l1)
+                                adam=adam, l1_gt=l1,
+                                direct=l1 is not None and direct_step_ok(self.scene))
         return render(self.scene, cam, self.sh_degree, background, api=self.api)
 
     def forward_backward(self, cam: GCCamera, gt: torch.Tensor, background: torch.Tensor,
@@ -236,7 +238,9 @@ class TrainStep:
         loss = out.get("loss")
         if loss is None:
             loss = self.loss(out["rgb"], gt, clamp_pred=not out.get("clamped", True))
-        if loss.requires_grad:
+        if out.get("backward") is not None:  # the fused render's direct step
+            out["backward"]()
+        elif loss.requires_grad:
             # a kept ones() seed: autograd's own seed is a fill kernel per step
             seed = getattr(self, "_seed", None)
             if seed is None or seed.device != loss.device or seed.dtype != loss.dtype or \

@@ -75,3 +75,46 @@ def test_fused_l1_loss_value(gpu):
         ref = (torch.clamp(out["rgb"].double(), max=1.0) - gt.double()).abs().mean()
         assert abs(float(out["loss"]) - float(ref)) <= 1e-6 * float(ref)
         assert out["loss"].requires_grad and not out["rgb"].requires_grad
+
+
+@pytest.mark.parametrize("W,H,n", [(1080, 1080, 400_000), (512, 384, 60_000)])
+def test_direct_step_equals_autograd(gpu, W, H, n):
+    """TrainStep's direct fused step (render_fused(direct=True): forward and backward called
+    without an autograd graph) against the same step through autograd: the same loss and, under
+    deterministic accumulation, bit-identical gradients -- also when they accumulate into
+    existing .grad (two steps without zero_grad) and with the in-backward Adam step."""
+    from gaussctrl_exp_amd import fused
+    sc = synthetic_scene(n, 3, seed=21, scale_lo=0.004, scale_hi=0.03)
+    cam = synthetic_camera(W, H).to(gpu)
+    gt = torch.rand(H, W, 3, generator=torch.Generator().manual_seed(4)).to(gpu)
+    bg = torch.tensor([0.1, 0.7, 0.3], device=gpu)
+    prev, prev_direct = _lib.set_deterministic(True), fused.DIRECT_STEP
+    res = {}
+    try:
+        for direct in (True, False):
+            fused.DIRECT_STEP = direct
+            s = sc.to(gpu)
+            t = TrainStep(s, sh_degree=3, loss="l1", render_mode="fused")
+            t.zero_grad()
+            l1, out = t.forward_backward(cam, gt, bg)
+            assert (out["backward"] is not None) == direct
+            assert l1.requires_grad != direct
+            g1 = [p.grad.detach().clone() for p in s.params()]
+            l2, _ = t.forward_backward(cam, gt, bg)  # accumulates
+            g2 = [p.grad.detach().cpu().numpy() for p in s.params()]
+            t2 = TrainStep(sc.to(gpu), sh_degree=3, loss="l1", render_mode="fused")
+            for _ in range(2):
+                t2.step(cam, gt, bg)
+            res[direct] = (float(l1), [g.cpu().numpy() for g in g1], g2,
+                           [p.detach().cpu().numpy() for p in t2.params])
+            if direct:  # the direct step's backward runs once
+                with pytest.raises(RuntimeError, match="already ran"):
+                    out["backward"]()
+    finally:
+        _lib.set_deterministic(prev)
+        fused.DIRECT_STEP = prev_direct
+    a, b = res[True], res[False]
+    assert a[0] == b[0]
+    for x, y in zip(a[1] + a[2] + a[3], b[1] + b[2] + b[3]):
+        np.testing.assert_array_equal(x, y)
+    assert np.abs(a[1][0]).max() > 0
