@@ -474,10 +474,11 @@ def render_fused(scene, cam: GCCamera, sh_degree_to_use: int, background: Tensor
     L1, splatfacto's loss at ssim_lambda 0), computed by the blend kernel; the loss is the
     differentiable output (its backward forms the image gradient inside the rasterizer
     backward) and "rgb" is the detached raw image (clamp ignored).
-    direct (with l1_gt; direct_step_ok(scene)): no autograd graph -- "loss" is detached and
-    "backward" is a callable that runs the fused backward of d loss / d loss = 1 (or its
-    argument) and accumulates the six gradients into the parameters' .grad as autograd's
-    loss.backward() would (TrainStep's step)."""
+    direct (direct_step_ok(scene), no alpha): no autograd graph -- the outputs are detached and
+    "backward" is a callable that runs the fused backward once and accumulates the six
+    gradients into the parameters' .grad as autograd's backward would (TrainStep's step): of
+    d loss / d loss = 1 (or its argument) with l1_gt, else of its argument, d image [H,W,3]
+    (loss.fused_splatfacto_loss_and_grad)."""
     aux = {}
     args = [_contig_f32(scene.means), _contig_f32(scene.scales), _contig_f32(scene.quats),
             _contig_f32(scene.opacities), _contig_f32(scene.features_dc),
@@ -487,9 +488,9 @@ def render_fused(scene, cam: GCCamera, sh_degree_to_use: int, background: Tensor
             l1_gt]
     backward = None
     if direct:
-        if l1_gt is None or not direct_step_ok(scene):
-            raise ValueError("render_fused(direct=True) needs l1_gt and contiguous fp32 leaf "
-                             "parameters (direct_step_ok)")
+        if return_alpha or not direct_step_ok(scene):
+            raise ValueError("render_fused(direct=True) needs contiguous fp32 leaf parameters "
+                             "(direct_step_ok) and no alpha output")
         params = args[:6]
         ctx = _DirectCtx(tuple(t.requires_grad for t in params) + (False,) * 15)
         with torch.no_grad():
@@ -503,7 +504,13 @@ def render_fused(scene, cam: GCCamera, sh_degree_to_use: int, background: Tensor
             c, ctx = ctx, None
             if not any(c.needs_input_grad[:6]):
                 return
-            g = _unit_grad(out[0].device) if grad is None else grad
+            if l1_gt is not None:  # d loss: 1 unless given
+                g = _unit_grad(out[0].device) if grad is None else grad
+            elif grad is None:
+                raise ValueError("render_fused(direct=True) without l1_gt: backward needs the "
+                                 "image gradient")
+            else:  # d image
+                g = grad
             with torch.no_grad():
                 grads = _FusedRender.backward(c, g, None)
                 for p, gp in zip(params, grads[:6]):

@@ -77,3 +77,16 @@ def fused_splatfacto_loss(pred: Tensor, gt: Tensor, ssim_lambda: float = 0.2,
     clamp_pred: the loss of torch.clamp(pred, max=1.0) (gc_model.py:222) without materialising
     the clamped image (its forward and backward kernels fold into the loss kernels)."""
     return _FusedL1SSIM.apply(pred, gt, ssim_lambda, clamp_pred)
+
+
+def fused_splatfacto_loss_and_grad(pred: Tensor, gt: Tensor, ssim_lambda: float = 0.2,
+                                   clamp_pred: bool = False):
+    """(loss, d loss / d pred) of fused_splatfacto_loss in one call, without an autograd graph
+    (the direct training step, fused.render_fused(direct=True)): the same two kernels, the
+    backward of a unit loss gradient."""
+    from .fused import _DirectCtx, _unit_grad
+    ctx = _DirectCtx((True, False, False, False))
+    with torch.no_grad():
+        loss = _FusedL1SSIM.forward(ctx, pred, gt, ssim_lambda, clamp_pred)
+        v_pred = _FusedL1SSIM.backward(ctx, _unit_grad(loss.device))[0]
+    return loss, v_pred

@@ -221,9 +221,12 @@ class TrainStep:
             # fuse_l1 is off; with it, the forward and backward are called directly (no
             # autograd graph: out["backward"], fused.direct_step_ok)
             l1 = gt if (self.loss_kind == "l1" and self.fuse_l1 and gt is not None) else None
+            # (the direct step's loss: the fused L1 in the blend, or the fused L1 + SSIM kernels
+            # called directly as well, forward_backward)
+            direct = gt is not None and (l1 is not None or self.loss_kind == "splatfacto") and \
+                direct_step_ok(self.scene)
             return render_fused(self.scene, cam, self.sh_degree, background, clamp=False,
-                                adam=adam, l1_gt=l1,
-                                direct=l1 is not None and direct_step_ok(self.scene))
+                                adam=adam, l1_gt=l1, direct=direct)
         return render(self.scene, cam, self.sh_degree, background, api=self.api)
 
     def forward_backward(self, cam: GCCamera, gt: torch.Tensor, background: torch.Tensor,
@@ -236,11 +239,19 @@ class TrainStep:
         else:
             out = self._render(cam, background, adam=adam, gt=gt)
         loss = out.get("loss")
+        direct = out.get("backward")
+        if direct is not None:  # the fused render's direct step (no autograd graph)
+            if loss is None:  # the L1 + SSIM loss kernels, called directly as well
+                from .loss import fused_splatfacto_loss_and_grad
+                loss, v_img = fused_splatfacto_loss_and_grad(out["rgb"], gt, SSIM_LAMBDA,
+                                                             not out.get("clamped", True))
+                direct(v_img)
+            else:  # the L1 loss inside the blend
+                direct()
+            return loss, out
         if loss is None:
             loss = self.loss(out["rgb"], gt, clamp_pred=not out.get("clamped", True))
-        if out.get("backward") is not None:  # the fused render's direct step
-            out["backward"]()
-        elif loss.requires_grad:
+        if loss.requires_grad:
             # a kept ones() seed: autograd's own seed is a fill kernel per step
             seed = getattr(self, "_seed", None)
             if seed is None or seed.device != loss.device or seed.dtype != loss.dtype or \

@@ -2,7 +2,7 @@
 _FusedRender.forward / backward without an autograd graph).  The numerics -- bit-identical
 gradients against the autograd step -- are tests/test_gpu_fused_l1.py's
 test_direct_step_equals_autograd; these CPU tests cover when the step is taken and the
-context object the two static methods share."""
+context object the static methods share."""
 import pytest
 import torch
 
@@ -42,18 +42,21 @@ def test_direct_ctx_mirrors_the_autograd_context():
     assert ctx.meta == (1, 2)
 
 
-def test_direct_render_rejects_unsupported_calls():
+def test_direct_render_rejects_unsupported_calls(monkeypatch):
     sc = synthetic_scene(16, 3, seed=2).requires_grad_()
+    with pytest.raises(ValueError, match="direct"):  # the alpha output has no direct backward
+        _render(sc, return_alpha=True)
+    monkeypatch.setattr(fused, "DIRECT_STEP", False)  # not eligible: autograd's step only
     with pytest.raises(ValueError, match="direct"):
-        _render_without_camera(sc)
+        _render(sc)
 
 
-def _render_without_camera(sc):
-    """render_fused with a stand-in CPU camera: direct without l1_gt is refused before any
-    kernel call (the direct backward differentiates the loss output)."""
+def _render(sc, **kw):
+    """render_fused(direct=True) with a stand-in CPU camera: the refusals come before any
+    kernel call."""
     class Cam:
         viewmat = projmat = torch.eye(4)[:3]
         c2w = torch.eye(4)[:3]
         fx = fy = cx = cy = 1.0
         height = width = 8
-    fused.render_fused(sc, Cam(), 3, torch.zeros(3), direct=True)
+    fused.render_fused(sc, Cam(), 3, torch.zeros(3), direct=True, **kw)

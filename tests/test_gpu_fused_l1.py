@@ -77,12 +77,14 @@ def test_fused_l1_loss_value(gpu):
         assert out["loss"].requires_grad and not out["rgb"].requires_grad
 
 
+@pytest.mark.parametrize("loss_kind", ["l1", "splatfacto"])
 @pytest.mark.parametrize("W,H,n", [(1080, 1080, 400_000), (512, 384, 60_000)])
-def test_direct_step_equals_autograd(gpu, W, H, n):
+def test_direct_step_equals_autograd(gpu, W, H, n, loss_kind):
     """TrainStep's direct fused step (render_fused(direct=True): forward and backward called
-    without an autograd graph) against the same step through autograd: the same loss and, under
-    deterministic accumulation, bit-identical gradients -- also when they accumulate into
-    existing .grad (two steps without zero_grad) and with the in-backward Adam step."""
+    without an autograd graph; with the L1 + SSIM loss its kernels are called directly too,
+    loss.fused_splatfacto_loss_and_grad) against the same step through autograd: the same loss
+    and, under deterministic accumulation, bit-identical gradients -- also when they accumulate
+    into existing .grad (two steps without zero_grad) and with the in-backward Adam step."""
     from gaussctrl_exp_amd import fused
     sc = synthetic_scene(n, 3, seed=21, scale_lo=0.004, scale_hi=0.03)
     cam = synthetic_camera(W, H).to(gpu)
@@ -94,7 +96,7 @@ def test_direct_step_equals_autograd(gpu, W, H, n):
         for direct in (True, False):
             fused.DIRECT_STEP = direct
             s = sc.to(gpu)
-            t = TrainStep(s, sh_degree=3, loss="l1", render_mode="fused")
+            t = TrainStep(s, sh_degree=3, loss=loss_kind, render_mode="fused")
             t.zero_grad()
             l1, out = t.forward_backward(cam, gt, bg)
             assert (out["backward"] is not None) == direct
@@ -102,7 +104,7 @@ def test_direct_step_equals_autograd(gpu, W, H, n):
             g1 = [p.grad.detach().clone() for p in s.params()]
             l2, _ = t.forward_backward(cam, gt, bg)  # accumulates
             g2 = [p.grad.detach().cpu().numpy() for p in s.params()]
-            t2 = TrainStep(sc.to(gpu), sh_degree=3, loss="l1", render_mode="fused")
+            t2 = TrainStep(sc.to(gpu), sh_degree=3, loss=loss_kind, render_mode="fused")
             for _ in range(2):
                 t2.step(cam, gt, bg)
             res[direct] = (float(l1), [g.cpu().numpy() for g in g1], g2,
