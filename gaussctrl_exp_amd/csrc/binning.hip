@@ -909,22 +909,6 @@ __global__ __launch_bounds__(TPB) void depth_keys_kernel(int n, const float *__r
 // visible count): order holds only the visible Gaussians and the positions past them get zero
 // allotments.  One workgroup per scan tile (SC_TILE entries): it also writes the tile's
 // allotment sum, the first step of the device scan of cnt.
-// The region binning's membership filter (rb_*): bit (g % 31) for every region g of the
-// gw x gh-tile region grid (gxn regions per row) that the Gaussian's tile box overlaps, bit 31
-// when its allotment exceeds the box (sentinel slots).  A superset: the workgroups of a region
-// test only that bit before reading the Gaussian (a region sharing the bit, or a box row past a
-// truncated allotment, just yields no slots).
-__device__ __forceinline__ uint32_t rb_mask(uint4 q, int gw, int gh, int gxn) {
-  const int x0 = (int)(q.y & 0xFFFFu), y0 = (int)(q.y >> 16);
-  const int x1 = (int)(q.z & 0xFFFFu), y1 = (int)(q.z >> 16);
-  const uint32_t area = (uint32_t)max(x1 - x0, 0) * (uint32_t)max(y1 - y0, 0);
-  uint32_t m = q.x > area ? 0x80000000u : 0u;
-  if (q.x == 0u || area == 0u) return m;
-  for (int gy = y0 / gh; gy <= (y1 - 1) / gh; ++gy)
-    for (int gx = x0 / gw; gx <= (x1 - 1) / gw; ++gx) m |= 1u << ((gy * gxn + gx) % 31);
-  return m;
-}
-
 __global__ __launch_bounds__(TPB) void gather_counts_kernel(int n, const uint32_t *__restrict__ order,
                                                             const uint32_t *__restrict__ kept,
                                                             const uint4 *__restrict__ rec,
@@ -932,8 +916,6 @@ __global__ __launch_bounds__(TPB) void gather_counts_kernel(int n, const uint32_
                                                             uint2 *__restrict__ box,
                                                             int *__restrict__ num_visible,
                                                             uint32_t *__restrict__ partial,
-                                                            uint32_t *__restrict__ rmask = nullptr,
-                                                            int gw = 1, int gh = 1, int gxn = 1,
                                                             uint32_t *__restrict__ vflag = nullptr) {
   __shared__ uint32_t lds[TPB / 64];
   const long long base = (long long)blockIdx.x * SC_TILE;
@@ -959,7 +941,6 @@ __global__ __launch_bounds__(TPB) void gather_counts_kernel(int n, const uint32_
       if (p < nv) {
         cnt[p] = q[k].x;
         box[p] = make_uint2(q[k].y, q[k].z);
-        if (rmask) rmask[p] = rb_mask(q[k], gw, gh, gxn);
         sum += q[k].x;
       } else if (p < n) {
         cnt[p] = 0u;
@@ -1013,10 +994,10 @@ __device__ __forceinline__ int slot_owner(int *mk, uint32_t j0, uint32_t rel, bo
 //   ts_decode_kernel turns each row back into gsplat's (first, end) -- no sorted keys are
 //                    written or re-read.
 // Stable sort of depth-ordered pairs by tile = gsplat's order (ties by Gaussian id), bit for
-// bit.  Against the region binning below (measured round 5, same box, tools/exp_rb.py): the
-// headline 0.22 vs 0.24 ms, c4 garden ~0.30 vs 0.39 ms -- the region binning's per-(depth
-// range, region) workgroups are imbalanced on real scenes and its in-order ranking costs a
-// returning LDS atomic per round; the sort's passes are coalesced and balanced by construction.
+// bit.  Against the region binning of round 5 (removed in round 6; measured on one box: the
+// headline 0.22 vs 0.24 ms, c4 garden ~0.30 vs 0.39 ms, profiles/r05_region_binning_sweep.txt)
+// the sort's passes are coalesced and balanced by construction, where the region binning's
+// per-(depth range, region) workgroups were imbalanced on real scenes.
 // partial[]: gather_counts_kernel's per-1,024-Gaussian block sums, scanned here by every
 // workgroup (<= a few loads per thread); workgroup 0 publishes their total I to i_dev and
 // i_host (the speculative binning; after a count phase that found I already, the same value).
@@ -1119,7 +1100,7 @@ __global__ __launch_bounds__(TPB) void ts_emit_kernel(int n, int nb,
     const int qbw = max(qx1 - qx0, 1);
     const int qarea = max(qx1 - qx0, 0) * max(qy1 - qy0, 0);
     uint32_t tile;
-    if ((int)li < qarea) {  // li / qbw as in rb_slots (exact below 2^20)
+    if ((int)li < qarea) {  // li / qbw (exact below 2^20: the float estimate rounds to the floor)
       const int ly = li < (1u << 20)
                          ? (int)(((float)li + 0.5f) * __builtin_amdgcn_rcpf((float)qbw))
                          : (int)li / qbw;
@@ -1153,540 +1134,6 @@ __global__ __launch_bounds__(TPB) void ts_decode_kernel(long long T, long long c
   if (r.y > 0) reinterpret_cast<int2 *>(bins)[t] = make_int2((int)(n - r.x), r.y);
 }
 
-#ifdef GSPLAT_TEST_HOOKS  // A/B only (gsplat_debug_binning_scheme 2): measured slower
-// ------------------------------------------------------------------ region binning
-// The depth-ordered Gaussians -> gsplat's tile lists (gaussian_ids_sorted, tile_bins) without
-// emitting (tile, id) pairs or sorting them by tile.  A tile's list is the depth-ordered
-// Gaussians whose intersections include the tile, so a counting sort by tile in depth order
-// gives it directly -- what it needs is each intersection's rank among the earlier (deeper in
-// the list) intersections of its tile.  The image is cut into G rectangular regions of <= 1,024
-// tiles and the visible Gaussians (depth order) into R contiguous depth ranges; workgroup
-// (r, g) takes range r clipped to region g, its 16 waves one contiguous sub-range each:
-//   rb_count_kernel  per wave and tile, the wave's intersections (LDS counters)
-//                    -> cw[r * 16 + w][t], and their sum over the workgroup's waves cr[r][t]
-//   rb_scan_kernel   per tile, the exclusive prefix of its cr column over the ranges (in
-//                    place; tile-minor rows: coalesced) and its total
-//   rb_tiles_kernel  one workgroup: tile starts = exclusive scan of the totals -> tile_bins, I
-//   rb_place_kernel  each wave regenerates its intersections in order and writes each id to
-//                    start[t] + cr[r][t] + sum over w' < w of cw[r * 16 + w'][t] + (its rank
-//                    in the wave so far), ranks within a
-//                    64-slot round by a ballot match of the region-local tile index
-// The order inside a tile is (range, wave, round, lane) = depth order, with the depth sort's
-// ties (Gaussian id) kept: gsplat's stable order, bit for bit.  A workgroup writes each tile's
-// ids as one run of ~I / (R T) (the headline: ~100 ids) instead of the ~3.5-id cells that made a
-// chunk-wise counting sort lose (see the note at tc_first_kernel).  An allotment that is not the
-// box's tile count (inconsistent caller inputs) keeps emit_kernel's semantics: the first
-// min(c, area) tiles of the box in row-major order, and c - area padding slots of the sentinel
-// tile T, which region G (the extra one) lists after every real tile.
-// Replaces the emission and the two LSD passes of the tile sort (~8 dependent launches and
-// 2 x 16 I bytes of pass traffic) with 4 launches and one 4 I-byte write of the ids.
-constexpr int RB_NW = 16;             // waves per workgroup
-constexpr int RB_NT = RB_NW * 64;
-constexpr int RB_TG_MAX = 1024;       // tiles per region (LDS counters: RB_NW x RB_TG_MAX words)
-constexpr int RB_TL_BITS = 10;        // bits of a region-local tile index
-
-struct RbPlan {
-  int tbx, tby;
-  int gw, gh;      // region size in tiles
-  int gxn, gyn;    // regions per axis
-  int G;           // real regions (region G is the sentinel region)
-  int R;           // depth ranges
-  int map;         // workgroup -> (range, region) mapping (rb_wg)
-  long long T, TS; // tiles, tiles + the sentinel tile
-  long long rows;  // R * RB_NW rows of per-wave counts
-};
-// workspace2 of the region binning: per-wave counts cw [rows][TS], per-range counts cr [R][TS]
-// (column-scanned in place), tile totals [TS], tile starts [TS]
-struct RbWs {
-  uint32_t *cw, *cr, *tot, *tstart;
-};
-
-// tuning knobs (environment, read once): target workgroups, regions per axis, mapping
-static int rb_env(const char *name, int dflt) {
-  const char *s = getenv(name);
-  return s ? atoi(s) : dflt;
-}
-
-int g_rb_knobs[3] = {-1, -1, -1};  // (tuning runs: tools/exp_rb.py) wgs, regs per axis, map
-RbPlan rb_plan(int n, int tbx, int tby) {
-  static const int wg_env = rb_env("GSPLAT_MI355X_RB_WGS", 512);
-  static const int axis_env = rb_env("GSPLAT_MI355X_RB_REGS", 4);
-  static const int map_env = rb_env("GSPLAT_MI355X_RB_MAP", 0);
-  const int wg_target = g_rb_knobs[0] > 0 ? g_rb_knobs[0] : wg_env;
-  const int per_axis = g_rb_knobs[1] > 0 ? g_rb_knobs[1] : axis_env;
-  const int map = g_rb_knobs[2] >= 0 ? g_rb_knobs[2] : map_env;
-  RbPlan p;
-  p.tbx = tbx;
-  p.tby = tby;
-  p.T = (long long)tbx * tby;
-  p.TS = p.T + 1;
-  int gxn = max(1, min(per_axis, tbx)), gyn = max(1, min(per_axis, tby));
-  while ((long long)cdiv(tbx, gxn) * cdiv(tby, gyn) > RB_TG_MAX) {
-    if (cdiv(tbx, gxn) >= cdiv(tby, gyn)) ++gxn; else ++gyn;
-  }
-  p.gw = (int)cdiv(tbx, gxn);
-  p.gh = (int)cdiv(tby, gyn);
-  p.gxn = (int)cdiv(tbx, p.gw);  // (no empty regions)
-  p.gyn = (int)cdiv(tby, p.gh);
-  p.G = p.gxn * p.gyn;
-  // ranges: ~wg_target workgroups over all regions, a multiple of 8 (one XCD per range under
-  // the range-major mapping), and at least ~4 chunks of 64 Gaussians per wave
-  int R = max(1, wg_target / p.G);
-  R = R >= 8 ? R / 8 * 8 : R;
-  const int rmax = max(1, (int)(((long long)n + RB_NW * 256 - 1) / (RB_NW * 256)));
-  if (R > rmax) R = rmax >= 8 ? rmax / 8 * 8 : rmax;
-  p.R = max(1, min(R, 256));
-  p.map = map;
-  p.rows = (long long)p.R * RB_NW;
-  return p;
-}
-
-// workgroup b -> (range r, region g); r >= R: nothing to do.  Range-major mapping (map 0): the
-// G + 1 workgroups of one range share an XCD (b % 8; the observed round-robin placement, used
-// for speed only) and so read that range's depth-ordered boxes through one L2.
-__device__ __forceinline__ void rb_wg(const RbPlan &p, int b, int &r, int &g) {
-  const int nreg = p.G + 1;
-  if (p.map % 10 == 0 && p.R % 8 == 0) {
-    const int k = b >> 3;
-    r = (b & 7) + 8 * (k / nreg);
-    g = k % nreg;
-  } else {
-    r = b / nreg;
-    g = b % nreg;
-  }
-}
-
-// One lane's Gaussian clipped to a region: k slots, slot li -> region-local tile index.
-//   li < nf: the full rows of the box's first min(c, area) tiles (row-major) inside the
-//            region: local (fy0 + li / cf, fx0 + li % cf);
-//   else   : the partial last row: local (yp, px0 + li - nf).
-// The sentinel region: k = max(c - area, 0) slots of local tile 0.
-struct RbSlots {
-  uint32_t k;
-  uint32_t a;  // fy0 | fx0 << 16 (region-local)
-  uint32_t b;  // cf | yp << 16   (region-local; yp = 0xFFFF: no partial row here)
-  uint32_t c;  // nf | px0 << 16
-};
-
-__device__ __forceinline__ RbSlots rb_slots(uint2 bx, uint32_t c, int rx0, int ry0, int rx1,
-                                            int ry1, bool sentinel) {
-  RbSlots s{0u, 0u, 0u, 0u};
-  const int x0 = (int)(bx.x & 0xFFFFu), y0 = (int)(bx.x >> 16);
-  const int x1 = (int)(bx.y & 0xFFFFu), y1 = (int)(bx.y >> 16);
-  const int bw = max(x1 - x0, 0), bh = max(y1 - y0, 0);
-  const uint32_t area = (uint32_t)bw * (uint32_t)bh;
-  if (sentinel) {
-    s.k = c > area ? c - area : 0u;
-    return s;
-  }
-  const uint32_t m = min(c, area);
-  if (m == 0u) return s;
-  // full rows fr = m / bw (exact: the float quotient's error is far below 0.5 / bw for m < 2^20)
-  const uint32_t fr = m < (1u << 20)
-                          ? (uint32_t)(((float)m + 0.5f) * __builtin_amdgcn_rcpf((float)bw))
-                          : m / (uint32_t)bw;
-  const uint32_t rem = m - fr * (uint32_t)bw;
-  const int fy0 = max(y0, ry0), fy1 = min(y0 + (int)fr, ry1);
-  const int fx0 = max(x0, rx0), fx1 = min(x1, rx1);
-  const int nrow = max(fy1 - fy0, 0), ncol = max(fx1 - fx0, 0);
-  const uint32_t nf = (uint32_t)(nrow * ncol);
-  const int yp = y0 + (int)fr;
-  uint32_t np = 0u;
-  int px0 = 0;
-  if (rem && yp >= ry0 && yp < ry1) {
-    px0 = max(x0, rx0);
-    const int px1 = min(x0 + (int)rem, rx1);
-    np = (uint32_t)max(px1 - px0, 0);
-  }
-  s.k = nf + np;
-  s.a = (uint32_t)(fy0 - ry0) | ((uint32_t)(fx0 - rx0) << 16);
-  s.b = (uint32_t)max(ncol, 1) | ((uint32_t)(np ? yp - ry0 : 0xFFFF) << 16);
-  s.c = nf | ((uint32_t)(np ? px0 - rx0 : 0) << 16);
-  return s;
-}
-
-// Walks the slots of one wave's 64 Gaussians (slot order = the lanes' order, then li), 64 slots
-// per round; f(valid, local tile, owner lane) is called by every lane each round (wave-uniform
-// trip count: the ballots and shuffles inside f need every lane).
-template <typename F>
-__device__ __forceinline__ void rb_expand(const RbSlots &s, int gw, bool sentinel, int *mk,
-                                         F &&f) {
-  rb_expand(s, gw, sentinel, mk, f, [] {});
-}
-// (fin() runs once after the last round: rb_place_kernel completes its pipelined round there)
-template <typename F, typename Fin>
-__device__ __forceinline__ void rb_expand(const RbSlots &s, int gw, bool sentinel, int *mk,
-                                         F &&f, Fin &&fin) {
-  const int lane = threadIdx.x & 63;
-  uint32_t inc = s.k;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const uint32_t o = __shfl_up(inc, off, 64);
-    if (lane >= off) inc += o;
-  }
-  const uint32_t total = __shfl(inc, 63, 64);
-  if (total == 0u) return;
-  const uint32_t rel = inc - s.k;
-  mk[lane] = -1;
-  int carry = -1;
-  for (uint32_t j0 = 0; j0 < total; j0 += 64) {
-    const uint32_t j = j0 + lane;
-    const int q = slot_owner(mk, j0, rel, s.k != 0u, carry);
-    const uint32_t li = j - __shfl(rel, q, 64);
-    uint32_t tl = 0u;
-    if (!sentinel) {
-      const uint32_t qa = __shfl(s.a, q, 64), qb = __shfl(s.b, q, 64), qc = __shfl(s.c, q, 64);
-      const uint32_t nf = qc & 0xFFFFu;
-      if (li < nf) {
-        const uint32_t cf = qb & 0xFFFFu;
-        const uint32_t ly = (uint32_t)(((float)li + 0.5f) * __builtin_amdgcn_rcpf((float)cf));
-        tl = ((qa & 0xFFFFu) + ly) * (uint32_t)gw + (qa >> 16) + (li - ly * cf);
-      } else {
-        tl = (qb >> 16) * (uint32_t)gw + (qc >> 16) + (li - nf);
-      }
-    }
-    f(j < total, tl, q);
-  }
-  fin();
-}
-
-// A wave's depth-ordered walk over [w0, w1): the region filter bit of RB_M x 64 positions is
-// tested per step (one 4-B load per position, all in flight together), the positions that pass
-// are queued in order in LDS, and every 64 queued ones are read (box, allotment, id) and
-// expanded -- most positions of a range miss a given region, so the expansion rounds stay dense
-// and only members are read.  f(slots, gid) expands 64 Gaussians (gid: ORDER only).
-constexpr int RB_M = 8;
-template <bool ORDER, typename F>
-__device__ __forceinline__ void rb_walk(long long w0, long long w1, const uint32_t *__restrict__ rmask,
-                                        uint32_t bit, const uint2 *__restrict__ box,
-                                        const uint32_t *__restrict__ cnt,
-                                        const uint32_t *__restrict__ order, int rx0, int ry0,
-                                        int rx1, int ry1, bool sentinel, uint32_t *Q /*[128]*/,
-                                        F &&f) {
-  const int lane = threadIdx.x & 63;
-  const unsigned long long lt = (1ull << lane) - 1ull;
-  int qn = 0;  // wave-uniform
-  auto drain = [&](int m) {  // expand the first min(m, 64) queued positions, shift the rest
-    wave_lds_sync();
-    const uint32_t q = lane < m ? Q[lane] : 0xFFFFFFFFu;
-    const int rest = m > 64 ? m - 64 : 0;
-    const uint32_t q2 = lane < rest ? Q[64 + lane] : 0u;
-    wave_lds_sync();
-    if (lane < rest) Q[lane] = q2;
-    RbSlots s{0u, 0u, 0u, 0u};
-    uint32_t g = 0u;
-    if (q != 0xFFFFFFFFu) {
-      s = rb_slots(box[q], cnt[q], rx0, ry0, rx1, ry1, sentinel);
-      if (ORDER) g = order ? order[q] : q;
-    }
-    f(s, g);
-    return rest;
-  };
-  for (long long base = w0; base < w1; base += 64 * RB_M) {  // wave-uniform
-    uint32_t mk[RB_M];
-#pragma unroll
-    for (int j = 0; j < RB_M; ++j) mk[j] = rmask[min(base + j * 64 + lane, w1 - 1)];
-#pragma unroll
-    for (int j = 0; j < RB_M; ++j) {
-      const long long q = base + j * 64 + lane;
-      const bool hit = q < w1 && (mk[j] & bit) != 0u;
-      const unsigned long long m = __ballot(hit);
-      if (m == 0ull) continue;  // wave-uniform
-      if (hit) Q[qn + __popcll(m & lt)] = (uint32_t)q;
-      qn += __popcll(m);
-      if (qn >= 64) qn = drain(qn);
-    }
-  }
-  if (qn > 0) drain(qn);
-}
-
-// Region g's rectangle (tiles) and local tile count; the sentinel region is one tile.
-__device__ __forceinline__ void rb_region(const RbPlan &p, int g, int &rx0, int &ry0, int &rx1,
-                                          int &ry1, int &tg) {
-  if (g >= p.G) {
-    rx0 = ry0 = 0;
-    rx1 = ry1 = 1;
-    tg = 1;
-    return;
-  }
-  const int gx = g % p.gxn, gy = g / p.gxn;
-  rx0 = gx * p.gw;
-  ry0 = gy * p.gh;
-  rx1 = min(rx0 + p.gw, p.tbx);
-  ry1 = min(ry0 + p.gh, p.tby);
-  tg = (rx1 - rx0) * (ry1 - ry0);
-}
-
-// local tile index -> global tile id (sentinel: T)
-__device__ __forceinline__ long long rb_global(const RbPlan &p, int g, int rx0, int ry0, int rw,
-                                               int tl) {
-  if (g >= p.G) return p.T;
-  return (long long)(ry0 + tl / rw) * p.tbx + rx0 + tl % rw;
-}
-
-// [p0, p1): the depth positions of workgroup (r, *)'s wave w (nv visible Gaussians)
-__device__ __forceinline__ void rb_wave_range(const RbPlan &p, long long nv, int r, int w,
-                                              long long &p0, long long &p1) {
-  const long long lo = nv * r / p.R, hi = nv * (r + 1) / p.R;
-  const long long q = (hi - lo + RB_NW - 1) / RB_NW;
-  p0 = min(lo + q * w, hi);
-  p1 = min(p0 + q, hi);
-}
-
-__global__ __launch_bounds__(RB_NT) void rb_count_kernel(RbPlan p, int n,
-                                                         const uint32_t *__restrict__ kept,
-                                                         const uint32_t *__restrict__ rmask,
-                                                         const uint32_t *__restrict__ cnt,
-                                                         const uint2 *__restrict__ box,
-                                                         uint32_t *__restrict__ cw_out,
-                                                         uint32_t *__restrict__ cr_out) {
-  __shared__ uint32_t cw[RB_NW][RB_TG_MAX];
-  __shared__ int marks[RB_NT];
-  __shared__ uint32_t queue[RB_NW][128];
-  int r, g;
-  rb_wg(p, blockIdx.x, r, g);
-  if (r >= p.R) return;  // workgroup-uniform
-  int rx0, ry0, rx1, ry1, tg;
-  rb_region(p, g, rx0, ry0, rx1, ry1, tg);
-  const int rw = rx1 - rx0;
-  const bool sentinel = g >= p.G;
-  const int tid = threadIdx.x, wave = tid >> 6;
-  for (int i = tid; i < RB_NW * RB_TG_MAX; i += RB_NT) (&cw[0][0])[i] = 0u;
-  __syncthreads();
-  const long long nv = min((long long)n, (long long)*kept);
-  long long w0, w1;
-  rb_wave_range(p, nv, r, wave, w0, w1);
-  int *mk = marks + wave * 64;
-  uint32_t *mine = cw[wave];
-  const uint32_t bit = sentinel ? 0x80000000u : 1u << (g % 31);
-  rb_walk<false>(w0, w1, rmask, bit, box, cnt, nullptr, rx0, ry0, rx1, ry1, sentinel, queue[wave],
-                 [&](const RbSlots &s, uint32_t) {
-                   rb_expand(s, rw, sentinel, mk, [&](bool valid, uint32_t tl, int) {
-                     if (valid) atomicAdd(&mine[tl], 1u);
-                   });
-                 });
-  __syncthreads();
-  for (int tl = tid; tl < tg; tl += RB_NT) {
-    const long long t = rb_global(p, g, rx0, ry0, rw, tl);
-    uint32_t s = 0;
-#pragma unroll 4
-    for (int w = 0; w < RB_NW; ++w) {
-      const uint32_t c = cw[w][tl];
-      cw_out[((long long)r * RB_NW + w) * p.TS + t] = c;
-      s += c;
-    }
-    cr_out[(long long)r * p.TS + t] = s;
-  }
-}
-
-// Per tile t = blockIdx.x * 64 + lane: the exclusive prefix of its column over the rows (in
-// place) and its total; wave v scans rows [v * rq, (v + 1) * rq).
-__global__ __launch_bounds__(256) void rb_scan_kernel(long long TS, long long rows,
-                                                      uint32_t *__restrict__ cw,
-                                                      uint32_t *__restrict__ tot) {
-  __shared__ uint32_t seg[4][64];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const long long t = (long long)blockIdx.x * 64 + lane;
-  const long long rq = (rows + 3) / 4;
-  const long long r0 = min(wave * rq, rows), r1 = min(r0 + rq, rows);
-  uint32_t s = 0;
-  if (t < TS) {
-    long long r = r0;
-    for (; r + 8 <= r1; r += 8) {
-      uint32_t v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = cw[(r + u) * TS + t];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) s += v[u];
-    }
-    for (; r < r1; ++r) s += cw[r * TS + t];
-  }
-  seg[wave][lane] = s;
-  __syncthreads();
-  uint32_t run = 0, total = 0;
-#pragma unroll
-  for (int v = 0; v < 4; ++v) {
-    const uint32_t x = seg[v][lane];
-    if (v < wave) run += x;
-    total += x;
-  }
-  if (t >= TS) return;
-  long long r = r0;
-  for (; r + 8 <= r1; r += 8) {
-    uint32_t v[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = cw[(r + u) * TS + t];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      cw[(r + u) * TS + t] = run;
-      run += v[u];
-    }
-  }
-  for (; r < r1; ++r) {
-    const uint32_t v = cw[r * TS + t];
-    cw[r * TS + t] = run;
-    run += v;
-  }
-  if (wave == 0) tot[t] = total;
-}
-
-// One workgroup: I = the sum of the tile totals (with the sentinel tile); tile starts = their
-// exclusive scan -> tstart[t] and gsplat's tile_bins ((0, 0) for an empty tile).  The count goes
-// to the device word the placement checks (i_dev) and to the host's pinned slot (i_host).
-// I > cap, or a depth-key digit the sort assumed constant varied (kfin / assume: the depth
-// order is wrong; I_dev = ~0): an all-zero table and nothing placed.
-__global__ __launch_bounds__(1024) void rb_tiles_kernel(long long T, long long TS,
-                                                        const uint32_t *__restrict__ tot,
-                                                        uint32_t *__restrict__ tstart,
-                                                        int32_t *__restrict__ tile_bins,
-                                                        uint32_t *__restrict__ i_dev,
-                                                        int32_t *__restrict__ i_host,
-                                                        unsigned long long cap,
-                                                        const uint32_t *__restrict__ kfin,
-                                                        uint32_t assume) {
-  __shared__ uint32_t lds[16];
-  __shared__ unsigned long long all;
-  const int tid = threadIdx.x;
-  unsigned long long s = 0;
-  for (long long i = tid; i < TS; i += 1024) s += tot[i];
-  if (tid == 0) all = 0ull;
-  __syncthreads();
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off, 64);
-  if ((tid & 63) == 0) atomicAdd(&all, s);
-  __syncthreads();
-  const unsigned long long I = all;
-  const bool violated = assume && kfin && (((kfin[0] ^ kfin[1]) & assume) != 0u);
-  const bool ok = !violated && I <= cap;
-  if (tid == 0) {
-    *i_dev = violated ? 0xFFFFFFFFu : I > 0xFFFFFFFEull ? 0xFFFFFFFEu : (uint32_t)I;
-    if (i_host) *i_host = I > 0x7FFFFFFFull ? 0x7FFFFFFF : (int32_t)I;
-  }
-  if (!ok) {
-    for (long long i = tid; i < 2 * T; i += 1024) tile_bins[i] = 0;
-    return;
-  }
-  uint32_t running = 0;
-  for (long long c0 = 0; c0 < TS; c0 += 1024) {
-    const long long i = c0 + tid;
-    const uint32_t v = i < TS ? tot[i] : 0u;
-    uint32_t t;
-    const uint32_t ex = running + block_exclusive_scan<1024>(v, t, lds);
-    if (i < TS) {
-      tstart[i] = ex;
-      if (i < T) {
-        tile_bins[2 * i] = v ? (int32_t)ex : 0;
-        tile_bins[2 * i + 1] = v ? (int32_t)(ex + v) : 0;
-      }
-    }
-    running += t;
-  }
-}
-
-__global__ __launch_bounds__(RB_NT) void rb_place_kernel(RbPlan p, int n,
-                                                         const uint32_t *__restrict__ kept,
-                                                         const uint32_t *__restrict__ rmask,
-                                                         const uint32_t *__restrict__ order,
-                                                         const uint32_t *__restrict__ cnt,
-                                                         const uint2 *__restrict__ box,
-                                                         const uint32_t *__restrict__ cw_in,
-                                                         const uint32_t *__restrict__ cr_in,
-                                                         const uint32_t *__restrict__ tstart,
-                                                         uint32_t *__restrict__ ids,
-                                                         const uint32_t *__restrict__ i_dev,
-                                                         uint32_t cap) {
-  __shared__ uint32_t cw[RB_NW][RB_TG_MAX];
-  __shared__ int marks[RB_NT];
-  __shared__ uint32_t queue[RB_NW][128];
-  int r, g;
-  rb_wg(p, blockIdx.x, r, g);
-  if (r >= p.R) return;         // workgroup-uniform
-  if (*i_dev > cap) return;     // overflow / depth-range violation: nothing is placed
-  int rx0, ry0, rx1, ry1, tg;
-  rb_region(p, g, rx0, ry0, rx1, ry1, tg);
-  const int rw = rx1 - rx0;
-  const bool sentinel = g >= p.G;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  for (int tl = tid; tl < tg; tl += RB_NT) {
-    const long long t = rb_global(p, g, rx0, ry0, rw, tl);
-    uint32_t c[RB_NW];
-#pragma unroll
-    for (int w = 0; w < RB_NW; ++w) c[w] = cw_in[((long long)r * RB_NW + w) * p.TS + t];
-    uint32_t base = tstart[t] + cr_in[(long long)r * p.TS + t];
-#pragma unroll
-    for (int w = 0; w < RB_NW; ++w) {
-      cw[w][tl] = base;
-      base += c[w];
-    }
-  }
-  __syncthreads();
-  const long long nv = min((long long)n, (long long)*kept);
-  long long w0, w1;
-  rb_wave_range(p, nv, r, wave, w0, w1);
-  int *mk = marks + wave * 64;
-  uint32_t *mine = cw[wave];
-  const int width = sentinel ? 0 : 32 - __builtin_clz((uint32_t)max(tg - 1, 1));
-  const unsigned long long lt = (1ull << lane) - 1ull;
-  const uint32_t bit = sentinel ? 0x80000000u : 1u << (g % 31);
-  // (tuning ablations, p.map / 10 -- timing only, wrong output: 1 no id stores, 2 no ranking,
-  //  3 no id loads, 4 none of the three; tools/exp_rb.py)
-  const int abl = p.map / 10;
-  rb_walk<true>(w0, w1, rmask, bit, box, cnt, abl >= 3 ? nullptr : order, rx0, ry0, rx1, ry1,
-                sentinel, queue[wave], [&](const RbSlots &s, uint32_t gid) {
-    // Software-pipelined one round deep: a round's counter atomics (the leaders of each tile's
-    // lanes reserve their run of the wave's tile counter) go out, then the PREVIOUS round's
-    // returned values are spread to its lanes and its ids stored -- the atomic's LDS round trip
-    // overlaps the next round's owner search, expansion and match instead of stalling the wave.
-    bool pv = false;                  // the pending round: its lane's slot is valid
-    uint32_t pog = 0u, pold = 0u, pbelow = 0u;
-    int pleader = lane;
-    bool pending = false;             // (wave-uniform)
-    auto complete = [&]() {
-      if (!pending) return;
-      const uint32_t pos = __shfl(pold, pleader, 64) + pbelow;
-      if (pv && pos < cap && abl != 1 && abl != 4) ids[pos] = pog;  // (pos < I <= cap always)
-      pending = false;
-    };
-    rb_expand(s, rw, sentinel, mk, [&](bool valid, uint32_t tl, int owner) {
-      const uint32_t og = __shfl(gid, owner, 64);
-      if (abl == 2 || abl == 4) {
-        if (valid) atomicAdd(&mine[tl], 1u);
-        complete();
-        pv = valid, pog = og, pold = tl, pleader = lane, pbelow = lane, pending = true;
-        return;
-      }
-      // the lanes of this round with the same tile, in lane (= list) order
-      const unsigned long long peers = digit_peers<RB_TL_BITS>(tl, width, valid);
-      const int leader = valid ? (int)__builtin_ctzll(peers) : lane;
-      uint32_t old = 0u;
-      if (valid && leader == lane) old = atomicAdd(&mine[tl], (uint32_t)__popcll(peers));
-      complete();
-      pv = valid, pog = og, pold = old, pleader = leader;
-      pbelow = (uint32_t)__popcll(peers & lt);
-      pending = true;
-    }, complete);
-  });
-}
-
-RbWs rb_ws(const RbPlan &p, void *base) {
-  RbWs w;
-  w.cw = (uint32_t *)base;
-  w.cr = w.cw + p.rows * p.TS;
-  w.tot = w.cr + (long long)p.R * p.TS;
-  w.tstart = w.tot + p.TS;
-  return w;
-}
-size_t rb_ws_bytes(const RbPlan &p) {
-  return (size_t)(p.rows + p.R + 2) * (size_t)p.TS * sizeof(uint32_t) + 256;
-}
-
-#else  // the shipped library: no region binning (use_region() is false there)
-struct RbPlan {
-  int gw = 1, gh = 1, gxn = 1;
-};
-RbPlan rb_plan(int, int, int) { return RbPlan{}; }
-size_t rb_ws_bytes(const RbPlan &) { return 0; }
-#endif  // GSPLAT_TEST_HOOKS
 
 // tile_bins[t] = [first, last+1) of tile t in the tile-sorted keys (tile_bins pre-zeroed).
 template <typename K, int SHIFT>
@@ -2408,8 +1855,7 @@ struct Phase1 {
   uint32_t *dkeys_a, *dvals_a, *dkeys_b, *dvals_b, *order, *cnt;
   uint4 *rec;  // per-Gaussian binning record (Gaussian order)
   uint2 *box;  // tile bbox in depth order (gather_counts_kernel)
-  uint32_t *dcount;  // I on the device (the capacity-launched placement's bound check)
-  uint32_t *rmask;   // region-membership filter per depth position (rb_mask)
+  uint32_t *dcount;  // I on the device (the capacity-launched sort's bound check)
   void *rs_ws;
   size_t bytes;
 };
@@ -2427,7 +1873,6 @@ Phase1 carve_phase1(void *base, int n) {
   p.rec = c.take<uint4>(nn * 4);
   p.box = c.take<uint2>(nn * 2);
   p.dcount = c.take<uint32_t>(4 * sizeof(uint32_t));
-  p.rmask = c.take<uint32_t>(nn);
   size_t rs = radix_ws_bytes(n, 0, 32);
   size_t sc = scan_ws_bytes(n);
   p.rs_ws = c.take<char>(rs > sc ? rs : sc);
@@ -2541,49 +1986,11 @@ void ts_launch(int n, const Phase1 &p1, void *ws2, int32_t *ids, int32_t *tile_b
 // Gaussians @ 512^2, max list 837: 0.100 vs 0.112 ms).  A long list is sorted by one
 // workgroup, so real scenes lose (c3 bear, 300k, max list 7,984: 0.365 vs 0.144 ms; headline
 // 1M: 0.287 vs 0.243); the cut is on N, which the count phase must know before I exists.
-// Within the sorted family (depth sort first): 0 = the shipped tile sort, 2 = the region
-// binning (kept for A/B: measured slower, see ts_emit_kernel).
 int g_bin_scheme = -1;
 bool use_bucket(long long n, long long T) {
   if (T + 1 > BK_MAX_BUCKETS) return false;
   return g_bin_scheme < 0 ? n <= (1LL << 17) : g_bin_scheme == 1;
 }
-#ifdef GSPLAT_TEST_HOOKS
-bool use_region(long long n, long long T) { return g_bin_scheme == 2 && !use_bucket(n, T); }
-#else
-bool use_region(long long, long long) { return false; }
-#endif
-
-#ifdef GSPLAT_TEST_HOOKS
-// The region binning (rb_*) over phase 1's depth-ordered records into workspace2
-// (rb_ws_bytes): head = count, column scan, tile table (no I-sized buffer: they can run before
-// the host knows I), tail = the placement into gaussian_ids_sorted (cap slots).  i_host: the
-// host's pinned count word (or null); assume: the depth-key bits the sort took as constant.
-void rb_launch(const RbPlan &rp, int n, const Phase1 &p1, void *ws2, int32_t *ids,
-               int32_t *tile_bins, unsigned long long cap, int32_t *i_host, uint32_t assume,
-               bool head, bool tail, hipStream_t st) {
-  const RbWs w = rb_ws(rp, ws2);
-  const uint32_t *kept = sort_kept_word(p1.rs_ws);
-  const unsigned nwg = (unsigned)(rp.R * (rp.G + 1));
-  if (head) {
-    hipLaunchKernelGGL(rb_count_kernel, dim3(nwg), dim3(RB_NT), 0, st, rp, n, kept, p1.rmask,
-                       p1.cnt, p1.box, w.cw, w.cr);
-    hipLaunchKernelGGL(rb_scan_kernel, dim3(cdiv(rp.TS, 64)), dim3(256), 0, st, rp.TS,
-                       (long long)rp.R, w.cr, w.tot);
-    hipLaunchKernelGGL(rb_tiles_kernel, dim3(1), dim3(1024), 0, st, rp.T, rp.TS, w.tot, w.tstart,
-                       tile_bins, p1.dcount, i_host, cap, kept + 1, assume);
-  }
-  if (tail)
-    hipLaunchKernelGGL(rb_place_kernel, dim3(nwg), dim3(RB_NT), 0, st, rp, n, kept, p1.rmask,
-                       p1.order,
-                       p1.cnt, p1.box, w.cw, w.cr, w.tstart, (uint32_t *)ids, p1.dcount,
-                       cap > 0xFFFFFFFEull ? 0xFFFFFFFEu : (uint32_t)cap);
-}
-
-#else
-void rb_launch(const RbPlan &, int, const Phase1 &, void *, int32_t *, int32_t *,
-               unsigned long long, int32_t *, uint32_t, bool, bool, hipStream_t) {}
-#endif
 
 }  // namespace
 
@@ -2597,13 +2004,6 @@ BinKeys bin_keys_view(void *workspace1, int n) {
 using namespace gs;
 
 #ifdef GSPLAT_TEST_HOOKS  // the test library only (libgsplat_mi355x_hooks.so, Makefile)
-// (tuning only, not in the public header) the region binning's plan knobs; -1 = default
-extern "C" void gsplat_tune_rb(int wgs, int regs, int map) {
-  g_rb_knobs[0] = wgs;
-  g_rb_knobs[1] = regs;
-  g_rb_knobs[2] = map;
-}
-
 // The tile sort's generated first pass from min_i intersections (capacity; < 0: leave);
 // returns the previous threshold.  Set it only between binnings: the workspace layout follows it.
 extern "C" long long gsplat_debug_tile_sort_gen(long long min_i) {
@@ -2620,7 +2020,7 @@ extern "C" int gsplat_debug_depth_key_range(int on) {
 
 extern "C" int gsplat_debug_binning_scheme(int scheme) {
   const int prev = g_bin_scheme;
-  if (scheme >= -1 && scheme <= 2) g_bin_scheme = scheme;
+  if (scheme >= -1 && scheme <= 1) g_bin_scheme = scheme;
   return prev;
 }
 #endif
@@ -2629,9 +2029,7 @@ extern "C" size_t gsplat_bin_emit_workspace_size_for(int num_points, int64_t num
                                                      int tile_bounds_x, int tile_bounds_y) {
   const long long T = (long long)tile_bounds_x * tile_bounds_y;
   if (num_points < 0 || num_intersects < 0 || tile_bounds_x <= 0 || tile_bounds_y <= 0) return 0;
-  const size_t rb = rb_ws_bytes(rb_plan(num_points, tile_bounds_x, tile_bounds_y));
-  const size_t ts = carve_ts(nullptr, num_intersects, T, num_points).bytes;
-  const size_t sorted = rb > ts ? rb : ts;  // (either may run: the scheme is a test-hooks switch)
+  const size_t sorted = carve_ts(nullptr, num_intersects, T, num_points).bytes;
   if (!use_bucket(num_points, T)) return sorted;
   const size_t bk = carve_bk(nullptr, num_points, num_intersects, T).bytes;
   return bk > sorted ? bk : sorted;
@@ -2709,16 +2107,14 @@ static int bin_count_impl(int num_points, const float *xys, const float *depths,
                                  use_key_range(n) ? assume_const : 0u,
                                  range_out ? d_counts + 2 : nullptr))
     return 1;
-  // depth-ordered allotments, boxes and region filter (+ per-block allotment sums) -> I
+  // depth-ordered allotments and boxes (+ per-block allotment sums) -> I
   const int nb = (int)cdiv(n, SC_TILE);
   // the kept count sits in the sort workspace's head, before the tile counts reused below
   const uint32_t *kept = sort_kept_word(p.rs_ws);
   uint32_t *partial = rts_tile_counts(p.rs_ws);  // the sort is done with its tile counts
-  const RbPlan rp = rb_plan(n, tile_bounds_x, tile_bounds_y);
   hipLaunchKernelGGL(gather_counts_kernel, dim3(nb), dim3(TPB), 0, st, n, p.order, kept, p.rec,
-                     p.cnt, p.box, d_counts, partial, use_region(n, T) ? p.rmask : nullptr, rp.gw,
-                     rp.gh, rp.gxn, p.dcount + 2);
-  // (the speculative binning: I from ts_emit_kernel / rb_tiles_kernel)
+                     p.cnt, p.box, d_counts, partial, p.dcount + 2);
+  // (the speculative binning: I from ts_emit_kernel)
   if (no_scan) return check_launch("bin_count");
   // I = the sum of the block sums, which stay as they are: the emission (ts_emit_kernel)
   // scans them itself, so a speculative count phase (no_scan) and this one leave the same state
@@ -2758,8 +2154,8 @@ extern "C" int gsplat_bin_count_keyed_ex(int num_points, int tile_bounds_x, int 
 }
 
 // The whole binning before the host knows I: the count phase (depth sort with the key-range
-// assumption, gather_counts) and the region binning with its placement launched at the
-// capacity (I published from the device, rb_tiles_kernel).
+// assumption, gather_counts) and the tile sort launched at the capacity (I published from the
+// device by ts_emit_kernel).
 enum { EMIT_HEAD = 1, EMIT_TAIL = 2, EMIT_ALL = 3, EMIT_SPEC = 4 };
 static int bin_emit_impl(int num_points, int64_t num_intersects, int64_t capacity,
                          int tile_bounds_x, int tile_bounds_y, int32_t *gaussian_ids_sorted,
@@ -2790,9 +2186,7 @@ extern "C" int gsplat_bin_speculative(int num_points, int64_t capacity, int tile
                          workspace2, workspace2_bytes, stream, EMIT_SPEC);
   }
   Phase1 p1 = carve_phase1(workspace1, num_points);
-  const bool region = use_region(num_points, T);
-  const RbPlan rp = rb_plan(num_points, tile_bounds_x, tile_bounds_y);
-  const size_t need2 = region ? rb_ws_bytes(rp) : carve_ts(nullptr, capacity, T, num_points).bytes;
+  const size_t need2 = carve_ts(nullptr, capacity, T, num_points).bytes;
   if (workspace1_bytes < p1.bytes || workspace2_bytes < need2) {
     set_error("bin_speculative: workspaces %zu/%zu < %zu/%zu bytes", workspace1_bytes,
               workspace2_bytes, p1.bytes, need2);
@@ -2803,13 +2197,8 @@ extern "C" int gsplat_bin_speculative(int num_points, int64_t capacity, int tile
                      assume_const, true, true))
     return 1;
   const uint32_t assume = use_key_range(num_points) ? assume_const : 0u;
-  if (region)
-    rb_launch(rp, num_points, p1, workspace2, gaussian_ids_sorted, tile_bins,
-              (unsigned long long)capacity, d_counts + 1, assume, true, true, st);
-  else
-    ts_launch(num_points, p1, workspace2, gaussian_ids_sorted, tile_bins, tile_bounds_x,
-              tile_bounds_y, capacity, capacity, d_counts + 1, assume, true, true,
-              p1.dcount, st);
+  ts_launch(num_points, p1, workspace2, gaussian_ids_sorted, tile_bins, tile_bounds_x,
+            tile_bounds_y, capacity, capacity, d_counts + 1, assume, true, true, p1.dcount, st);
   return check_launch("bin_speculative");
 }
 
@@ -2882,9 +2271,7 @@ static int bin_emit_impl(int num_points, int64_t num_intersects, int64_t capacit
                        (uint32_t)cap);
     return check_launch("bin_emit");
   }
-  const bool region = use_region(num_points, T);
-  const RbPlan rp = rb_plan(num_points, tile_bounds_x, tile_bounds_y);
-  const size_t need2 = region ? rb_ws_bytes(rp) : carve_ts(nullptr, cap, T, num_points).bytes;
+  const size_t need2 = carve_ts(nullptr, cap, T, num_points).bytes;
   if (workspace1_bytes < p1.bytes || workspace2_bytes < need2) {
     set_error("bin_emit: workspaces %zu/%zu < %zu/%zu bytes", workspace1_bytes,
               workspace2_bytes, p1.bytes, need2);
@@ -2893,13 +2280,6 @@ static int bin_emit_impl(int num_points, int64_t num_intersects, int64_t capacit
   if (num_points == 0 || (phase != EMIT_HEAD && phase != EMIT_SPEC && num_intersects == 0)) {
     if (tail)
       note(hipMemsetAsync(tile_bins, 0, (size_t)T * 2 * sizeof(int32_t), st), "hipMemsetAsync");
-    return check_launch("bin_emit");
-  }
-  if (region) {
-    // the region binning: its head needs no I-sized buffer, so HEAD (pre-launched before the
-    // host read of I) is the count, scan and tile table at the capacity, TAIL the placement
-    rb_launch(rp, num_points, p1, workspace2, gaussian_ids_sorted, tile_bins,
-              (unsigned long long)cap, nullptr, 0u, head, tail, st);
     return check_launch("bin_emit");
   }
   // the tile sort: HEAD = the emission at the capacity (nothing when the device's I exceeds
@@ -2940,7 +2320,7 @@ extern "C" int gsplat_bin_emit_finish(int num_points, int64_t num_intersects, in
                        workspace2_bytes, stream, EMIT_TAIL);
 }
 
-// The region binning launched at a capacity before the host knows I (the device count decides;
+// The tile sort launched at a capacity before the host knows I (the device count decides;
 // I > capacity leaves the table cleared and the ids unwritten, and the caller re-bins).  Returns
 // 2 without launching anything where the scheme needs I on the host (tile buckets): use
 // prelaunch / finish there.

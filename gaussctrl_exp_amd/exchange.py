@@ -104,6 +104,13 @@ class ShViewExchange:
         """Scope of one rank's render of view `index` of its `of` views this step: SH calls
         inside it exchange their gradients."""
         global _ACTIVE
+        # every rank gathers world * of records into one table kernel: refuse a step that could
+        # not be evaluated before any of its collectives is issued (not at the last view's
+        # reduce_views, with the gathers and the geometry all-reduce already in flight)
+        world = dist.get_world_size(self.group) if dist.is_initialized() else 1
+        if int(of) < 1 or world * int(of) > MAX_TABLE:
+            raise ValueError(f"ShViewExchange: {world} ranks x {int(of)} views per step = "
+                             f"{world * int(of)} records; the views kernel takes 1..{MAX_TABLE}")
         prev = _ACTIVE
         self.means = means.detach()
         self.campos = campos.detach().reshape(3).to(torch.float32)

@@ -448,11 +448,20 @@ def _unit_grad(dev) -> Tensor:
     return t
 
 
+def _has_grad_hooks(t: Tensor) -> bool:
+    """A gradient hook a caller registered on the parameter (register_hook /
+    register_post_accumulate_grad_hook): autograd runs it, the direct step would not."""
+    return bool(getattr(t, "_backward_hooks", None)) or \
+        bool(getattr(t, "_post_accumulate_grad_hooks", None))
+
+
 def direct_step_ok(scene) -> bool:
     """render_fused(direct=True) takes the parameters' gradients itself: it needs them as the
-    contiguous fp32 leaves the kernels read (no copy for autograd to route a gradient through)."""
+    contiguous fp32 leaves the kernels read (no copy for autograd to route a gradient through),
+    and no gradient hooks on them (the direct step assigns .grad without running hooks, so a
+    hooked parameter takes the autograd path)."""
     return DIRECT_STEP and all(
-        t.is_leaf and t.dtype == torch.float32 and t.is_contiguous()
+        t.is_leaf and t.dtype == torch.float32 and t.is_contiguous() and not _has_grad_hooks(t)
         for t in (scene.means, scene.scales, scene.quats, scene.opacities, scene.features_dc,
                   scene.features_rest))
 
@@ -490,7 +499,12 @@ def render_fused(scene, cam: GCCamera, sh_degree_to_use: int, background: Tensor
     if direct:
         if return_alpha or not direct_step_ok(scene):
             raise ValueError("render_fused(direct=True) needs contiguous fp32 leaf parameters "
-                             "(direct_step_ok) and no alpha output")
+                             "without gradient hooks (direct_step_ok) and no alpha output")
+        if l1_gt is None and clamp:
+            # the returned image would be clamp(rgb, max=1) while backward(grad) feeds grad to the
+            # rasterizer as the raw image's gradient, dropping the clamp's zero-gradient mask
+            raise ValueError("render_fused(direct=True) without l1_gt returns the raw image: "
+                             "pass clamp=False (and apply the clamp in the loss)")
         params = args[:6]
         ctx = _DirectCtx(tuple(t.requires_grad for t in params) + (False,) * 15)
         with torch.no_grad():

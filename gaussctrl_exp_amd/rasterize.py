@@ -280,7 +280,9 @@ def bin_gaussians_speculative(xys: Tensor, depths: Tensor, radii: Tensor, num_ti
     Returns a SpeculativeBinning (finish() before using I), or None when the capacity is not
     known yet or the scheme needs I on the host (the caller then uses bin_gaussians).
     between: called between the count phase (the depth sort) and the emission + tile sort,
-    which then go out as two C-ABI calls (the sorted scheme only); None: one call."""
+    which then go out as two C-ABI calls (the sorted scheme, uses_tile_sort); with the tile
+    buckets, or on the fallback paths, it is called once after the binning's launches instead
+    -- always before this function returns, so work it issues precedes any blend."""
     n = xys.shape[0]
     tbx = (img_width + BLOCK_X - 1) // BLOCK_X
     tby = (img_height + BLOCK_Y - 1) // BLOCK_Y
@@ -298,10 +300,11 @@ def bin_gaussians_speculative(xys: Tensor, depths: Tensor, radii: Tensor, num_ti
     try:
         # the count phase and the tile sort in one call
         assume = _assumed_constant(key)
-        if between is not None and n > BUCKET_MAX_N:
+        if between is not None and uses_tile_sort(n, tbx * tby):
             _lib.call("gsplat_bin_count_keyed_ex", n, tbx, tby, P(counts), P(ws1), ws1.numel(),
                       assume, st)
             between()
+            between = None
             rc = _lib.call_status("gsplat_bin_emit_speculative", n, cap, tbx, tby, P(ids_buf),
                                   P(tile_bins), P(ws1), ws1.numel(), P(ws2), ws2.numel(), st)
             if rc != 0:
@@ -331,6 +334,8 @@ def bin_gaussians_speculative(xys: Tensor, depths: Tensor, radii: Tensor, num_ti
                                           ids_buf, ws2, tile_bins)
                 done.num_intersects, done.range_violated = I, True
                 done.finish = lambda: False
+                if between is not None:
+                    between()
                 return done
             _note_capacity(key, I)
             if I <= cap:
@@ -346,6 +351,8 @@ def bin_gaussians_speculative(xys: Tensor, depths: Tensor, radii: Tensor, num_ti
             done.num_intersects = I
             done.layout_intersects = I
             done.finish = lambda: True
+            if between is not None:
+                between()
             return done
         if rc != 0:
             raise RuntimeError("gsplat_bin_speculative failed: " +
@@ -356,11 +363,21 @@ def bin_gaussians_speculative(xys: Tensor, depths: Tensor, radii: Tensor, num_ti
         raise
     sb = SpeculativeBinning(dev, n, tbx, tby, ws1, slot, counts, host, key, cap, ids_buf, ws2,
                             tile_bins)
+    if between is not None:  # (one call: the work goes after the binning's launches)
+        between()
     return sb
 
 
-# the tile buckets' size limit (binning.hip use_bucket: N <= 2^17 takes them)
+# the tile buckets' size limit (binning.hip use_bucket: N <= 2^17 takes them, on at most
+# BK_MAX_BUCKETS - 1 tiles)
 BUCKET_MAX_N = 1 << 17
+BK_MAX_BUCKETS = 16448
+
+
+def uses_tile_sort(n: int, tiles: int) -> bool:
+    """binning.hip use_bucket's complement for the shipped dispatch: the depth sort + tile sort
+    (two-call speculative binning possible) rather than the tile buckets."""
+    return n > BUCKET_MAX_N or tiles + 1 > BK_MAX_BUCKETS
 # frame shape -> the intersection capacity to pre-allocate the emission's outputs for
 _EMIT_CAP = {}
 # frame shape -> the intersection counts of its last CAP_WINDOW binnings: the capacity is 1/8

@@ -25,8 +25,20 @@ def test_direct_step_ok_needs_contiguous_fp32_leaves(monkeypatch):
     assert not fused.direct_step_ok(sc)
     sc.quats = q
     # a non-leaf (e.g. a view of a larger parameter)
+    m = sc.means
     sc.means = sc.means * 1.0
     assert not fused.direct_step_ok(sc)
+    sc.means = m
+    # gradient hooks a caller registered: autograd runs them, the direct step would not
+    assert fused.direct_step_ok(sc)
+    h = sc.scales.register_hook(lambda g: g)
+    assert not fused.direct_step_ok(sc)
+    h.remove()
+    assert fused.direct_step_ok(sc)
+    h = sc.opacities.register_post_accumulate_grad_hook(lambda p: None)
+    assert not fused.direct_step_ok(sc)
+    h.remove()
+    assert fused.direct_step_ok(sc)
 
 
 def test_direct_ctx_mirrors_the_autograd_context():
@@ -46,6 +58,9 @@ def test_direct_render_rejects_unsupported_calls(monkeypatch):
     sc = synthetic_scene(16, 3, seed=2).requires_grad_()
     with pytest.raises(ValueError, match="direct"):  # the alpha output has no direct backward
         _render(sc, return_alpha=True)
+    # without l1_gt the returned image must be the raw one its backward(grad) differentiates
+    with pytest.raises(ValueError, match="clamp=False"):
+        _render(sc, clamp=True)
     monkeypatch.setattr(fused, "DIRECT_STEP", False)  # not eligible: autograd's step only
     with pytest.raises(ValueError, match="direct"):
         _render(sc)
@@ -60,3 +75,21 @@ def _render(sc, **kw):
         fx = fy = cx = cy = 1.0
         height = width = 8
     fused.render_fused(sc, Cam(), 3, torch.zeros(3), direct=True, **kw)
+
+
+def test_view_exchange_refuses_an_oversized_table_before_any_collective():
+    """ShViewExchange.view checks world x views-per-step against the views kernel's record table
+    (exchange.MAX_TABLE) on entry, before the render issues a gather."""
+    from gaussctrl_exp_amd import exchange
+    x = exchange.ShViewExchange()
+    means, campos = torch.zeros(4, 3), torch.zeros(3)
+    with x.view(means, campos, 0, exchange.MAX_TABLE):  # world 1: at the limit
+        assert exchange.active() is x
+    assert exchange.active() is None
+    with pytest.raises(ValueError, match="records"):
+        with x.view(means, campos, 0, exchange.MAX_TABLE + 1):
+            pass
+    with pytest.raises(ValueError, match="records"):
+        with x.view(means, campos, 0, 0):
+            pass
+    assert exchange.active() is None

@@ -2,8 +2,9 @@
 MI355X -- the sizes where the sort switches to 16 keys per thread and the blend kernels see
 ~1,700 Gaussians per tile -- against the CPU oracle:
 
-* binning (fused depth + tile radix sorts) bit-exact against the oracle's map + numpy stable
-  sort of the 64-bit keys, under both sort schemes (reduce-then-scan, one-sweep);
+* binning (the compacting depth sort, then the stable tile sort of the depth-ordered pairs)
+  bit-exact against the oracle's map + numpy stable sort of the 64-bit keys, as shipped and
+  under every other dispatch setting (key-range shortcut off / from 2^22 keys, tile buckets);
 * forward blend on 48 random tiles within the parity tolerance, and bit-identical when run
   twice (no atomics in the forward);
 * backward on the same tiles (upstream gradient zero elsewhere, so only those tiles
@@ -51,20 +52,20 @@ def headline(request, gpu, oracle_lib):
                 colors=colors, opac=opac, config=request.param)
 
 
-@pytest.mark.parametrize("scheme", ["shipped", "norange", "range22", "bucket", "region"])
+@pytest.mark.parametrize("scheme", ["shipped", "norange", "range22", "bucket"])
 def test_headline_binning_bitexact(gpu, headline, scheme, hooks):
     """Binning bit-exact at full size: the shipped dispatch (for these scenes the depth sort of
     8-bit reduce-then-scan passes compacting the culled Gaussians away, constant-digit passes
     skipped, then the depth-ordered (tile, id) pairs sorted stably by tile); and every other
-    setting a dispatch takes: the key-range shortcut off or from 2^22 keys only, the tile
-    buckets with per-tile LDS sorts (shipped for small scenes) and the region binning (A/B)."""
+    setting a dispatch takes: the key-range shortcut off or from 2^22 keys only and the tile
+    buckets with per-tile LDS sorts (shipped for small scenes)."""
     h, cam = headline, headline["cam"]
     assert h["ref"]["num_intersects"] > 1 << 20
     if scheme != "shipped" and h["config"] in ("c4", "c5"):
         pytest.skip("the other dispatches: headline and c3 only")
     L = _lib.lib()
     # (-1: leave the shipped setting; each call returns the previous one)
-    prev = (L.gsplat_debug_binning_scheme({"bucket": 1, "region": 2}.get(scheme, -1)),
+    prev = (L.gsplat_debug_binning_scheme({"bucket": 1}.get(scheme, -1)),
             L.gsplat_debug_depth_key_range({"norange": 0, "range22": 1}.get(scheme, -1)))
     try:
         I, gids, bins = bin_gaussians(h["xys"], h["depths"], h["radii"], h["nth"], cam.height,

@@ -152,18 +152,16 @@ def test_sh_unaligned_slab(gpu):
 
 
 # binning dispatch settings (gsplat_debug_binning_scheme): as shipped (by size), the depth sort +
-# tile sort (the shipped scheme above 2^17 Gaussians), the depth sort + region binning (A/B
-# only), the small-scene tile buckets
-BIN_SETTINGS = {"shipped": -1, "tilesort": 0, "region": 2, "bucket": 1}
+# tile sort (the shipped scheme above 2^17 Gaussians), the small-scene tile buckets
+BIN_SETTINGS = {"shipped": -1, "tilesort": 0, "bucket": 1}
 
 
 @pytest.mark.parametrize("scheme", list(BIN_SETTINGS))
 @pytest.mark.parametrize("case", CASES)
 def test_binning_fused_bitexact(gpu, case, scheme, hooks):
     """The binning as dispatched for each case and every scheme (after the depth sort: the
-    tile sort of depth-ordered pairs, the region binning; without it:
-    the tile buckets with per-tile LDS sorts): bit-exact against the oracle's stable sort of
-    gsplat's keys."""
+    tile sort of depth-ordered pairs; without it: the tile buckets with per-tile LDS sorts):
+    bit-exact against the oracle's stable sort of gsplat's keys."""
     sc, cam, scales, quats = _inputs(*case)
     g, o = _project_both(gpu, sc, cam, scales, quats)
     xys, depths, radii, conics, nth, cov3d = g
@@ -182,7 +180,7 @@ def test_binning_fused_bitexact(gpu, case, scheme, hooks):
 def test_binning_inconsistent_allotments(gpu, hooks):
     """Caller-supplied num_tiles_hit that disagree with the tile boxes (allotments larger than
     the box are padded with the sentinel tile, smaller ones truncate the box): every scheme
-    places the same ids (the sentinel bucket / sort key / region last), including Gaussians
+    places the same ids (the sentinel bucket / sort key last), including Gaussians
     whose allotment spans several expansion rounds (one Gaussian over 600 tiles)."""
     sc, cam, scales, quats = _inputs(20000, 512, 512, 2, 0.003, 0.03, 1.5)
     g, _ = _project_both(gpu, sc, cam, scales, quats)
@@ -194,7 +192,7 @@ def test_binning_inconsistent_allotments(gpu, hooks):
     nth[vis[5]] = 600
     out = []
     L = _lib.lib()
-    for scheme in ("tilesort", "region", "bucket"):
+    for scheme in ("tilesort", "bucket"):
         prev = L.gsplat_debug_binning_scheme(BIN_SETTINGS[scheme])
         try:
             I, gids, bins = bin_gaussians(xys, depths, radii, nth, cam.height, cam.width)
