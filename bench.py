@@ -164,7 +164,30 @@ def algorithmic_bytes(N, I, P, T, K, nvis):
         "gsplat_rasterize_backward_records_l1": 40 * I + 32 * P,
         # params + saved forward outputs (72 B) and the 48 B record in, 6 gradients out
         "gsplat_fused_preprocess_backward": (116 + 12 * K) * N + 48 * nvis,
+        # the same with the Adam step inside (one GPU): no gradients written; every parameter
+        # and its two moments read and written (24 B per parameter, 11 + 3 K per Gaussian)
+        "gsplat_fused_preprocess_backward_adam": (72 + 24 * (11 + 3 * K)) * N + 48 * nvis,
+        # the splatfacto loss (loss.hip): forward reads pred + gt and writes the three SSIM
+        # derivative maps (60 P); backward reads the maps, pred and gt, writes v_pred (72 P)
+        "gsplat_l1_ssim_forward": 60 * P,
+        "gsplat_l1_ssim_backward": 72 * P,
+        # standalone multi-tensor Adam (N > 1): param, grad, m, v in; param, m, v out
+        "gsplat_adam_step": 28 * (11 + 3 * K) * N,
     }
+
+
+# train_roofline: which part of the train step each C-ABI entry belongs to (SURVEY.md §8d asks
+# for the step's byte split: render vs loss vs Adam vs the exchange)
+def train_part(entry: str) -> str:
+    if entry.startswith("gsplat_l1_ssim"):
+        return "loss"
+    if entry == "gsplat_adam_step":
+        return "adam"
+    if entry == "gsplat_fused_preprocess_backward_adam":
+        return "geometry backward + adam (one kernel)"
+    if entry.startswith("gsplat_exchange") or "views" in entry or "view_table" in entry:
+        return "exchange (pack / multi-view SH backward)"
+    return "render"
 
 
 # Device kernels behind each C-ABI entry (for the PMC counters of the dominant entry), and
@@ -179,7 +202,12 @@ ENTRY_KERNELS = {
     "gsplat_fused_preprocess_forward": (("fused_fwd_kernel",), True),
     "gsplat_fused_preprocess_forward_binned": (("fused_fwd_kernel",), True),
     "gsplat_fused_preprocess_forward_part[1]": (("fused_fwd_proj_kernel",), True),
-    "gsplat_fused_preprocess_backward": (("fused_bwd_kernel",), True),
+    "gsplat_fused_preprocess_forward_part[2] (side stream)": (("fused_fwd_sh_kernel",), True),
+    # (a pattern's '&'-separated parts must all occur in the instantiation's name)
+    "gsplat_fused_preprocess_backward": (("fused_bwd_kernel&, false>",), True),
+    "gsplat_fused_preprocess_backward_adam": (("fused_bwd_kernel&, true>",), True),
+    "gsplat_l1_ssim_forward": (("l1_ssim_fwd_kernel", "l1_ssim_finalize"), False),
+    "gsplat_l1_ssim_backward": (("l1_ssim_bwd_kernel",), False),
     "gsplat_rasterize_forward": (("raster_fwd",), False),
     "gsplat_rasterize_forward_clearing": (("raster_fwd",), False),
     "gsplat_compute_sh_forward": (("sh_fwd_kernel",), True),
@@ -221,7 +249,9 @@ def _entry_kernel_rows(entry, config):
         return []
     out = []
     for p in pats:
-        cand = [(v.get("dispatches") or 0.0, name) for name, v in kern.items() if p in name]
+        parts = p.split("&")
+        cand = [(v.get("dispatches") or 0.0, name) for name, v in kern.items()
+                if all(q in name for q in parts)]
         if cand:
             name = max(cand)[1]
             if all(name != n for n, _ in out):
@@ -523,6 +553,64 @@ def exchange_profile(scene, cam, gt, bg, deg, world, dev, steps, timed, record_f
     }
 
 
+def train_roofline(train_step, steps, barrier, ab, N, I, P, T, K, world, trainer, iters_per_s):
+    """The train step's byte split (render vs loss vs Adam vs the exchange) and
+    its time split, measured with HIP events around every C-ABI call over `steps` train steps
+    (the step is re-run for this; the timed train_iters_per_s loop runs without events).
+    Bytes: the render's §8d fwd+bwd model, the loss kernels' 132 P, Adam 24 B per parameter
+    inside the fused backward (one GPU) or 28 B standalone (gsplat_adam_step), the exchange
+    kernels' records; link bytes (N > 1) apart: per rank, the record all-gather receives
+    (N - 1) records and the flat ring all-reduce moves 2 (N - 1) / N x 44 B per Gaussian."""
+    if steps <= 0:
+        return None
+    with timing.timed_calls() as tm:
+        barrier()
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record()
+        for _ in range(steps):
+            train_step()
+        ev1.record()
+        calls = tm.summary()
+        step_ms_events = ev0.elapsed_time(ev1) / steps
+    params = (11 + 3 * K) * N
+    render_bytes = (388 + 24 * K) * N + 124 * I + 44 * P + 8 * T
+    parts_ms, parts_bytes = {}, {"render": render_bytes}
+    for name, (ncalls, mean_ms, tot_ms) in calls.items():
+        if "(side stream)" in name:
+            continue  # (overlaps the step's own stream)
+        part = train_part(name)
+        parts_ms[part] = parts_ms.get(part, 0.0) + tot_ms / steps
+        if part != "render":
+            parts_bytes[part] = parts_bytes.get(part, 0) + int(ab.get(name, 0) * ncalls / steps)
+    if "geometry backward + adam (one kernel)" in parts_bytes:
+        # the render model counts the geometry backward's gradient traffic; the fused kernel's
+        # bytes beyond it are the Adam update's (24 B per parameter)
+        parts_bytes.pop("geometry backward + adam (one kernel)")
+        parts_bytes["adam (inside the geometry backward)"] = 24 * params
+    attributed = sum(parts_ms.values())
+    parts_ms["(outside the C-ABI calls)"] = step_ms_events - attributed
+    hbm = sum(parts_bytes.values())
+    step_ms = 1e3 / iters_per_s
+    out = {
+        "step_ms": round(step_ms, 4),
+        "step_ms_events": round(step_ms_events, 4),
+        "time_ms_per_step": {k: round(v, 4) for k, v in parts_ms.items()},
+        "algorithmic_bytes_per_step": parts_bytes,
+        "algorithmic_bytes_total": hbm,
+        "frac": round(hbm / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+        "adam_bytes_per_gaussian": 28 * (11 + 3 * K),
+    }
+    if world > 1:
+        xc = trainer.sh_exchange
+        rec = xc.last_record_floats if xc is not None and xc.last_record_floats else 3 * N
+        out["link_bytes_per_rank"] = {
+            "record_all_gather_in": 4 * rec * (world - 1),
+            "geometry_all_reduce": int(2 * (world - 1) / world * 44 * N),
+        }
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -692,10 +780,18 @@ def main():
     for name, (calls, mean_ms, tot_ms) in per_call.items():
         per_step = calls / args.steps
         b = ab.get(name)
+        hb = pmc_traffic(name, args.config)
         kernels[name] = {
             "ms_per_call": round(mean_ms, 4),
             "calls_per_step": per_step,
-            "GBps": round(b / (mean_ms * 1e-3) / 1e9, 1) if b else None,
+            # algorithmic bytes (SURVEY.md §8d model) / time: bytes the L2 / MALL serve count
+            # too, so this can exceed the 8 TB/s HBM peak (c5's forward); hbm_GBps is the
+            # rocprofv3 PMC HBM traffic (FETCH_SIZE + WRITE_SIZE, profiles/pmc_traffic.json) of
+            # this config / time, null without counters
+            "alg_bytes": b,
+            "alg_GBps": round(b / (mean_ms * 1e-3) / 1e9, 1) if b else None,
+            "hbm_bytes": hb,
+            "hbm_GBps": round(hb / (mean_ms * 1e-3) / 1e9, 1) if hb else None,
         }
     # the entries' device time per step against the same loop's device time per step: the
     # remainder is torch work outside the C ABI (loss glue, zero_grad, all-reduce) and device
@@ -704,7 +800,7 @@ def main():
     attributed = sum(v[2] for k, v in per_call.items() if "(side stream)" not in k) / args.steps
     kernels["(outside the C-ABI calls)"] = {
         "ms_per_call": round(events_step_ms - attributed, 4), "calls_per_step": 1.0,
-        "GBps": None}
+        "alg_bytes": None, "alg_GBps": None, "hbm_bytes": None, "hbm_GBps": None}
     kernels_timing = {
         "method": "HIP events recorded on the launch stream before and after each C-ABI call "
                   "(device timestamps; an entry's time includes device idle while the host "
@@ -712,6 +808,13 @@ def main():
         "step_ms_events": round(events_step_ms, 4),
         "sum_entries_ms_per_step": round(attributed, 4),
     }
+    step_hbm = 0
+    for name, (calls, mean_ms, tot_ms) in per_call.items():
+        hb = kernels[name]["hbm_bytes"]
+        if hb is None:
+            step_hbm = None
+            break
+        step_hbm += int(hb * calls / args.steps)
     dom = max(per_call, key=lambda k: per_call[k][2])
     dom_ms = per_call[dom][1]
     dom_bytes = ab.get(dom)
@@ -734,6 +837,11 @@ def main():
         "issue_stall_frac": pmc_issue_and_wait(dom, args.config, dom_ms)[2],
         "step_algorithmic_bytes": step_bytes,
         "step_frac": round(step_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+        # the step's HBM bytes as the PMC counters saw them (sum over the entries on the step's
+        # stream of hbm_bytes x calls; null when an entry has no counters for this config)
+        "step_hbm_bytes_pmc": step_hbm,
+        "step_hbm_frac_pmc": (round(step_hbm / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                              if step_hbm else None),
         "roofline_mpix_s": round(P / (step_bytes / (HBM_PEAK_GBS * 1e9)) / 1e6, 1),
     }
 
@@ -761,6 +869,8 @@ def main():
             tdt = float(t.item())
         return tdt
     tdt = train_time(train_step)
+    train_rl = train_roofline(train_step, tsteps, barrier, ab, N, I, P, T, K, world,
+                              trainer, tsteps / tdt)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -808,6 +918,7 @@ def main():
             "train_iters_per_s": round(tsteps / tdt, 2),
             "train_views_per_s": round(world * tsteps / tdt, 2),
             "roofline": roofline,
+            "train_roofline": train_rl,
             "lane_occupancy": lanes,
             "kernels": kernels,
             "kernels_timing": kernels_timing,

@@ -105,6 +105,8 @@ SIGNATURES = {
     "gsplat_fused_preprocess_backward_accumulate": (_I, [_I, _I, _I] + [_P] * 6 + [_F] * 4 +
                                                     [_I, _I] + [_P] * 11),
     "gsplat_compute_sh_backward_view_table": (_I, [_I, _I, _I, _I, _P, _P, _P, _P, _P, _P]),
+    "gsplat_compute_sh_backward_view_table_adam": (
+        _I, [_I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _F, _F, _I, _F, _F, _F, _P]),
     "gsplat_grad_records_bytes": (_SZ, [_I]),
     "gsplat_grad_records_split": (_I, [_I, _P, _SZ, _P, _P, _P, _P, _P, _P, _P]),
     "gsplat_rasterize_backward_records": (_I, [_I] * 5 + [_P] * 11 + [_F, _I64, _I, _P, _SZ,
@@ -128,7 +130,7 @@ HOOK_SIGNATURES = {
     "gsplat_debug_tile_sort_gen": (_I64, [_I64]),
 }
 
-ABI_VERSION = 16  # include/gsplat_mi355x.h GSPLAT_MI355X_ABI_VERSION
+ABI_VERSION = 17  # include/gsplat_mi355x.h GSPLAT_MI355X_ABI_VERSION
 
 _lib = None
 _DETERMINISTIC = os.environ.get("GSPLAT_MI355X_DETERMINISTIC", "0") not in ("", "0")

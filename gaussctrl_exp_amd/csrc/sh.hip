@@ -8,6 +8,7 @@
 // LDS with 16-byte, fully coalesced loads (forward) / stores (backward); the per-Gaussian
 // arithmetic then reads its own row from LDS.
 #include "sh_math.h"
+#include "adam_math.h"
 #include "exchange_layout.h"
 
 namespace gs {
@@ -201,13 +202,69 @@ __device__ __forceinline__ bool xs_resolve(const ViewTable &tab, int r, long lon
   }
   return false;
 }
-template <int K>
+// The Adam step of the two SH-feature groups fused into the multi-view table kernel (N > 1
+// training step, TrainStep): the summed coefficient gradient never leaves the workgroup -- each
+// parameter element is updated from its LDS gradient row with adam_math.h's element update (the
+// arithmetic of gsplat_adam_step), so the 2 x 192 B per Gaussian of gradient write + re-read
+// of the unfused table kernel + multi-tensor Adam disappear.  Group 0 = features_dc [N,3],
+// group 1 = features_rest [N,K-1,3]; ss / bc2s as the host computes them for gsplat_adam_step.
+struct ShAdam {
+  float *p[2], *m[2], *v[2];
+  float ss[2], bc2s;
+  float beta1, beta2, eps;
+};
+
+// Columns [C0, C0 + WIDTH) of the block's cnt LDS gradient rows (pitch ROWP) applied to the
+// contiguous parameter slab p/m/v[base : base + cnt * WIDTH] (one group): 16-B accesses when
+// the three slabs are 16-B aligned, else dwords -- every element through adam_elem either way.
+template <int WIDTH, int C0, int ROWP, int THREADS>
+__device__ __forceinline__ void adam_cols(const float *smem, int cnt, const ShAdam &o, int grp,
+                                          long long base) {
+  const int total = cnt * WIDTH;
+  const float w1 = 1.f - o.beta1, w2 = 1.f - o.beta2;
+  const float ss = o.ss[grp], bc2s = o.bc2s;
+  float *__restrict__ P = o.p[grp] + base;
+  float *__restrict__ M = o.m[grp] + base;
+  float *__restrict__ V = o.v[grp] + base;
+  auto at = [&](int k) {
+    const int r = k / WIDTH;
+    return smem[r * ROWP + C0 + (k - r * WIDTH)];
+  };
+  const bool vec = ((((uintptr_t)P) | ((uintptr_t)M) | ((uintptr_t)V)) & 15) == 0;
+  int k0 = 0;
+  if (vec) {
+    const int nv = total >> 2;
+    float4 *P4 = reinterpret_cast<float4 *>(P), *M4 = reinterpret_cast<float4 *>(M),
+           *V4 = reinterpret_cast<float4 *>(V);
+    for (int k = threadIdx.x; k < nv; k += THREADS) {
+      float4 pv = P4[k], mv = M4[k], vv = V4[k];
+      adam_elem(pv.x, at(4 * k), mv.x, vv.x, w1, o.beta2, w2, ss, bc2s, o.eps);
+      adam_elem(pv.y, at(4 * k + 1), mv.y, vv.y, w1, o.beta2, w2, ss, bc2s, o.eps);
+      adam_elem(pv.z, at(4 * k + 2), mv.z, vv.z, w1, o.beta2, w2, ss, bc2s, o.eps);
+      adam_elem(pv.w, at(4 * k + 3), mv.w, vv.w, w1, o.beta2, w2, ss, bc2s, o.eps);
+      P4[k] = pv;
+      M4[k] = mv;
+      V4[k] = vv;
+    }
+    k0 = nv << 2;
+  }
+  for (int k = k0 + threadIdx.x; k < total; k += THREADS) {
+    float pv = P[k], mv = M[k], vv = V[k];
+    adam_elem(pv, at(k), mv, vv, w1, o.beta2, w2, ss, bc2s, o.eps);
+    P[k] = pv;
+    M[k] = mv;
+    V[k] = vv;
+  }
+}
+
+template <int K, bool ADAM = false>
 __global__ __launch_bounds__(256) void sh_bwd_table_kernel(int n, int degrees_to_use,
                                                            int num_views,
                                                            const float *__restrict__ means,
                                                            const ViewTable tab,
                                                            float *__restrict__ v_dc,
-                                                           float *__restrict__ v_rest) {
+                                                           float *__restrict__ v_rest,
+                                                           const ShAdam adam = {}) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int ROW = K * 3;
   constexpr int ROWP = sh_row_pitch(K);
@@ -251,8 +308,14 @@ __global__ __launch_bounds__(256) void sh_bwd_table_kernel(int n, int degrees_to
     for (int k = 0; k < ROW; ++k) rowp[k] = acc[k];
   }
   __syncthreads();
-  store_cols<3, 0, ROWP, SH_THREADS>(smem, cnt, v_dc + g0 * 3);
-  if constexpr (K > 1) store_cols<ROW - 3, 3, ROWP, SH_THREADS>(smem, cnt, v_rest + g0 * (ROW - 3));
+  if constexpr (ADAM) {
+    adam_cols<3, 0, ROWP, SH_THREADS>(smem, cnt, adam, 0, g0 * 3);
+    if constexpr (K > 1) adam_cols<ROW - 3, 3, ROWP, SH_THREADS>(smem, cnt, adam, 1, g0 * (ROW - 3));
+  } else {
+    store_cols<3, 0, ROWP, SH_THREADS>(smem, cnt, v_dc + g0 * 3);
+    if constexpr (K > 1)
+      store_cols<ROW - 3, 3, ROWP, SH_THREADS>(smem, cnt, v_rest + g0 * (ROW - 3));
+  }
 }
 
 }  // namespace
@@ -426,4 +489,67 @@ extern "C" int gsplat_compute_sh_backward_view_table(int num_points, int degree,
   SH_DISPATCH(sh_bwd_table_kernel, num_points, degrees_to_use, num_views, means3d, tab, v_dc,
               v_rest);
   return check_launch("compute_sh_backward_view_table");
+}
+
+extern "C" int gsplat_compute_sh_backward_view_table_adam(
+    int num_points, int degree, int degrees_to_use, int num_views, const float *means3d,
+    const float *const *records, const long long *capacities, float *features_dc,
+    float *features_rest, float *exp_avg_dc, float *exp_avg_sq_dc, float *exp_avg_rest,
+    float *exp_avg_sq_rest, float lr_dc, float lr_rest, int step, float beta1, float beta2,
+    float eps, void *stream) {
+  if (num_points < 0 || degree < 0 || degree > 4 || degrees_to_use < 0 ||
+      degrees_to_use > degree || num_views < 1 || num_views > XS_MAX_VIEWS || !records ||
+      !capacities || step < 1 || !(beta1 > 0.5f && beta1 < 1.f) || !(beta2 >= 0.f && beta2 < 1.f) ||
+      (num_points > 0 && (!means3d || !features_dc || !exp_avg_dc || !exp_avg_sq_dc ||
+                          (degree > 0 && (!features_rest || !exp_avg_rest || !exp_avg_sq_rest))))) {
+    set_error("compute_sh_backward_view_table_adam: bad args (N=%d degree=%d degrees_to_use=%d "
+              "views=%d, at most %d, step=%d beta1=%g beta2=%g)", num_points, degree,
+              degrees_to_use, num_views, XS_MAX_VIEWS, step, (double)beta1, (double)beta2);
+    return 1;
+  }
+  ViewTable tab{};
+  for (int r = 0; r < num_views; ++r) {
+    if (!records[r] || capacities[r] > num_points) {
+      set_error("compute_sh_backward_view_table_adam: record %d is NULL or its capacity %lld "
+                "exceeds N=%d", r, capacities[r], num_points);
+      return 1;
+    }
+    tab.rec[r] = records[r];
+    tab.cap[r] = capacities[r];
+  }
+  if (num_points == 0) return 0;
+  // torch non-capturable Adam: bias corrections in double on the host (as gsplat_adam_step)
+  const double bc1 = 1.0 - pow((double)beta1, step), bc2 = 1.0 - pow((double)beta2, step);
+  ShAdam o{};
+  o.p[0] = features_dc;
+  o.m[0] = exp_avg_dc;
+  o.v[0] = exp_avg_sq_dc;
+  o.p[1] = features_rest;
+  o.m[1] = exp_avg_rest;
+  o.v[1] = exp_avg_sq_rest;
+  o.ss[0] = (float)(lr_dc / bc1);
+  o.ss[1] = (float)(lr_rest / bc1);
+  o.bc2s = (float)sqrt(bc2);
+  o.beta1 = beta1;
+  o.beta2 = beta2;
+  o.eps = eps;
+  const int K = num_bases(degree);
+  const int thr = sh_threads(K);
+  dim3 grid(cdiv(num_points, thr)), block(thr);
+  size_t smem = (size_t)thr * sh_row_pitch(K) * sizeof(float);
+  hipStream_t st = (hipStream_t)stream;
+  switch (K) {
+#define ADAM_CASE(KK)                                                                        \
+  case KK:                                                                                   \
+    hipLaunchKernelGGL((sh_bwd_table_kernel<KK, true>), grid, block, smem, st, num_points,    \
+                       degrees_to_use, num_views, means3d, tab, nullptr, nullptr, o);        \
+    break;
+    ADAM_CASE(1)
+    ADAM_CASE(4)
+    ADAM_CASE(9)
+    ADAM_CASE(16)
+    ADAM_CASE(25)
+#undef ADAM_CASE
+  }
+  return check_launch("compute_sh_backward_view_table_adam");
 }

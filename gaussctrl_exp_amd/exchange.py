@@ -94,6 +94,11 @@ class ShViewExchange:
         self.last_record_floats = None  # length of the last record sent (bench)
         self.last_capacity = None  # the agreed sparse capacity of the last planned view (bench)
         self._skip = 0  # views left to exchange dense without planning (DENSE_SKIP)
+        # the SH-feature groups' Adam step fused into the views kernel (TrainStep sets it for
+        # the step, reduce_views consumes it): dict(groups=[(param, exp_avg, exp_avg_sq, lr)] x 2
+        # (features_dc, features_rest), step, betas, eps); adam_applied once the kernel ran
+        self.adam = None
+        self.adam_applied = False
         self._buffers = {}
         self._host_counts = None
 
@@ -127,6 +132,8 @@ class ShViewExchange:
 
     def reset(self):
         self.handled = False
+        self.adam = None
+        self.adam_applied = False
         self.early = None
         self.pending = []
         self.planned = {}
@@ -240,7 +247,9 @@ class ShViewExchange:
 
     def reduce_views(self, degree: int, degrees_to_use: int):
         """(v_features_dc [N,3], v_features_rest [N,K-1,3]): the sum over every rank's views
-        of this step, from the gathered records (view-major, rank order), in one kernel."""
+        of this step, from the gathered records (view-major, rank order), in one kernel.  With
+        `adam` set (TrainStep), that kernel applies the SH-feature groups' Adam step instead
+        and (None, None) is returned."""
         means = self.means
         n = means.shape[0]
         dev = means.device
@@ -253,13 +262,31 @@ class ShViewExchange:
         if not ptrs or len(ptrs) > MAX_TABLE:
             raise RuntimeError(f"ShViewExchange: {len(ptrs)} gathered view records (1..{MAX_TABLE})")
         K = (degree + 1) ** 2
-        v_dc = torch.empty((n, 3), device=dev, dtype=torch.float32)
-        v_rest = torch.empty((n, K - 1, 3), device=dev, dtype=torch.float32)
         R = len(ptrs)
         tab = (ctypes.c_void_p * R)(*ptrs)
         cap_arr = (ctypes.c_longlong * R)(*caps)
+        means_c = means.float().contiguous()
+        if self.adam is not None:
+            # the SH-feature groups' Adam step inside the table kernel: parameters and moments
+            # updated in place, no gradient tensors (gsplat_compute_sh_backward_view_table_adam)
+            (pd, md, vd, lr_d), (pr, mr, vr, lr_r) = self.adam["groups"]
+            b1, b2 = self.adam["betas"]
+            P = _lib.ptr
+            _lib.call("gsplat_compute_sh_backward_view_table_adam", n, degree,
+                      int(degrees_to_use), R, P(means_c), ctypes.cast(tab, ctypes.c_void_p),
+                      ctypes.cast(cap_arr, ctypes.c_void_p), P(pd), P(pr) if K > 1 else None,
+                      P(md), P(vd), P(mr) if K > 1 else None, P(vr) if K > 1 else None,
+                      float(lr_d), float(lr_r), int(self.adam["step"]), float(b1), float(b2),
+                      float(self.adam["eps"]), _lib.stream(dev))
+            self._last_gathered = [p[1] for p in self.pending]
+            self.pending = []
+            self.handled = True
+            self.adam_applied = True
+            return None, None
+        v_dc = torch.empty((n, 3), device=dev, dtype=torch.float32)
+        v_rest = torch.empty((n, K - 1, 3), device=dev, dtype=torch.float32)
         _lib.call("gsplat_compute_sh_backward_view_table", n, degree, int(degrees_to_use), R,
-                  _lib.ptr(means.float().contiguous()), ctypes.cast(tab, ctypes.c_void_p),
+                  _lib.ptr(means_c), ctypes.cast(tab, ctypes.c_void_p),
                   ctypes.cast(cap_arr, ctypes.c_void_p), _lib.ptr(v_dc),
                   _lib.ptr(v_rest) if K > 1 else None, _lib.stream(dev))
         # (the gathered buffers must outlive the kernel: keep them until the next step)

@@ -97,6 +97,22 @@ class FusedAdam:
         return {"exp_avgs": M, "exp_avg_sqs": V, "lrs": lrs, "step": self.step_count,
                 "betas": self.betas, "eps": self.eps, "params": list(params)}
 
+    def next_step_groups(self, params):
+        """[(param, exp_avg, exp_avg_sq, lr)] of `params` for the NEXT step, whose number is
+        step_count + 1, without advancing the count: for a kernel that updates these groups
+        itself inside this step (exchange.ShViewExchange: the SH-feature groups inside the
+        multi-view table kernel) while step(names=<the others>) then advances to the same step
+        number for the rest."""
+        by_param = {id(g["params"][0]): g for g in self.param_groups}
+        out = []
+        for p in params:
+            g = by_param.get(id(p))
+            if g is None:
+                raise ValueError("next_step_groups: parameter not managed by this optimiser")
+            st = self._buffers(p)
+            out.append((p, st["exp_avg"], st["exp_avg_sq"], float(g["lr"])))
+        return out
+
     def zero_grad(self, set_to_none: bool = True):
         for g in self.param_groups:
             p = g["params"][0]

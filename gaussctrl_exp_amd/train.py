@@ -151,6 +151,10 @@ class TrainStep:
         # single-GPU fused steps take the Adam update inside the backward kernel
         # (gsplat_fused_preprocess_backward_adam): no gradient tensors are written or re-read
         self.fuse_adam = bool(fuse_adam) and render_mode == "fused" and world_size == 1
+        # N > 1: the SH-feature groups' Adam step fused into the multi-view SH table kernel
+        # (GSPLAT_MI355X_FUSE_SH_ADAM=0: the table kernel's gradients + the multi-tensor Adam)
+        self.fuse_sh_adam = bool(fuse_adam) and world_size > 1 and os.environ.get(
+            "GSPLAT_MI355X_FUSE_SH_ADAM", "1") != "0"
         # the fused render computes an L1 loss inside its blend kernels (loss="l1"); off:
         # the separate loss kernels (GSPLAT_MI355X_FUSE_L1=0, A/B runs)
         self.fuse_l1 = render_mode == "fused" and os.environ.get("GSPLAT_MI355X_FUSE_L1",
@@ -317,6 +321,15 @@ class TrainStep:
             self.step_count += 1
             return loss
         self.zero_grad()
+        xc = self.sh_exchange
+        if optimizer and xc is not None and self.fuse_sh_adam and \
+                isinstance(self.opt, FusedAdamType()):
+            # N > 1: the SH-feature groups' Adam step inside the multi-view table kernel
+            # (exchange.reduce_views; gsplat_compute_sh_backward_view_table_adam) at the step
+            # number the other groups' step below advances to
+            xc.adam = {"groups": self.opt.next_step_groups(
+                [self.scene.features_dc, self.scene.features_rest]),
+                "step": self.opt.step_count + 1, "betas": self.opt.betas, "eps": self.opt.eps}
         if multi:
             loss = self.forward_backward_views(list(cam), list(gt), background)
         else:
@@ -325,6 +338,14 @@ class TrainStep:
             self.sync_grads()
             return loss
         gs = self.grad_sync
+        if gs is not None and xc is not None and xc.adam_applied:
+            # the SH groups are updated; the geometry all-reduce overlapped the table kernel
+            gs.wait()
+            self.opt.step(names=[n for n in PARAM_NAMES if n not in SH_GROUPS])
+            self.step_count += 1
+            return loss
+        if xc is not None:
+            xc.adam = None  # (not consumed: the caller path / degree-0 steps sum gradients)
         if gs is not None and gs.sh_done() and isinstance(self.opt, FusedAdamType()):
             # the SH-feature gradients (81 % of the update's bytes) are final: update them
             # while the other groups' all-reduces are in flight, then the rest

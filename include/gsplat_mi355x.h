@@ -42,8 +42,9 @@ extern "C" {
 #endif
 
 /* 16: gsplat_exchange_sparse_plan needs a send buffer of 4 + 4W floats (its popcounts are staged
- * in the values area); the binning's phase-2 workspace layout follows the tile sort. */
-#define GSPLAT_MI355X_ABI_VERSION 16
+ * in the values area); the binning's phase-2 workspace layout follows the tile sort.
+ * 17: gsplat_compute_sh_backward_view_table_adam; the region binning (test hooks) is gone. */
+#define GSPLAT_MI355X_ABI_VERSION 17
 
 int gsplat_abi_version(void);
 const char *gsplat_last_error(void);
@@ -159,6 +160,18 @@ int gsplat_compute_sh_backward_view_table(int num_points, int degree, int degree
                                           const float *const *records,
                                           const long long *capacities, float *v_dc,
                                           float *v_rest, void *stream);
+/* gsplat_compute_sh_backward_view_table with the Adam step of the two SH-feature groups fused
+ * in (the N > 1 training step; replaces the table kernel + gsplat_adam_step over features_dc /
+ * features_rest at gc_trainer.py:281): the summed gradient is applied in place to features_dc
+ * [N,3] / features_rest [N, num_sh_bases(degree) - 1, 3] and their exp_avg / exp_avg_sq
+ * moments, with gsplat_adam_step's element arithmetic and bias corrections (lr_dc / lr_rest,
+ * step >= 1, beta1 in (0.5, 1)) -- bit-identical to the two calls.  No gradient is written. */
+int gsplat_compute_sh_backward_view_table_adam(
+    int num_points, int degree, int degrees_to_use, int num_views, const float *means3d,
+    const float *const *records, const long long *capacities, float *features_dc,
+    float *features_rest, float *exp_avg_dc, float *exp_avg_sq_dc, float *exp_avg_rest,
+    float *exp_avg_sq_rest, float lr_dc, float lr_rest, int step, float beta1, float beta2,
+    float eps, void *stream);
 
 /* covs2d [N,3] -> conics [N,3], radii [N] (float).  det == 0 rows get zeros. */
 int gsplat_compute_cov2d_bounds(int num_points, const float *covs2d, float *conics,

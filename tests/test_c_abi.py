@@ -67,7 +67,7 @@ def test_binding_arities_match_the_header():
 
 def test_host_queries_without_gpu():
     from gaussctrl_exp_amd import _lib
-    assert _lib.lib().gsplat_abi_version() == _lib.ABI_VERSION == 16
+    assert _lib.lib().gsplat_abi_version() == _lib.ABI_VERSION == 17
     assert _lib.query("gsplat_bin_count_workspace_size", 1000) > 1000 * 16
     assert _lib.query("gsplat_sort_isect_pairs_workspace_size", 0) > 0
 

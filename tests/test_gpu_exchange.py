@@ -320,3 +320,93 @@ def test_view_table_sparse_equals_dense_bitwise(gpu, degree, dtu):
                   ctypes.cast((ctypes.c_void_p * 1)(dense[0].data_ptr()), ctypes.c_void_p),
                   ctypes.cast((ctypes.c_longlong * 1)(n + 1), ctypes.c_void_p), _lib.ptr(v_dc),
                   _lib.ptr(v_rest) if K > 1 else None, st)
+
+
+@pytest.mark.parametrize("degree,dtu", [(3, 3), (3, 1), (1, 1), (0, 0)])
+@pytest.mark.parametrize("n", [50_021, 4096])
+def test_view_table_adam_equals_table_then_adam(gpu, degree, dtu, n):
+    """gsplat_compute_sh_backward_view_table_adam (the N > 1 train step's SH-feature Adam fused
+    into the multi-view table kernel) leaves features_dc / features_rest and both moments
+    bit-identical to the table kernel's gradients followed by gsplat_adam_step (FusedAdam) --
+    over two consecutive steps (moments non-zero), sparse and dense records mixed, ragged N
+    (dword tail) and an unaligned slab start (4096 + 1 rows into a larger buffer)."""
+    import ctypes
+    from gaussctrl_exp_amd import _lib
+    from gaussctrl_exp_amd.exchange import sparse_floats
+    from gaussctrl_exp_amd.optim import FusedAdam
+    R = 5
+    g = torch.Generator().manual_seed(19)
+    means = ((torch.rand(n, 3, generator=g) * 2 - 1) * 1.5).to(gpu)
+    st = _lib.stream(gpu)
+    ptrs, caps, keep = [], [], []
+    for r in range(R):
+        radii, rec, colors, campos, (d_radii, d_rec, d_colors, d_campos) = \
+            _sparse_inputs(n, 0.3 + 0.1 * r, 200 + r, gpu)
+        if r % 2:
+            d = torch.empty(3 * n + 4, device=gpu)
+            _lib.call("gsplat_exchange_pack_colors", n, _lib.ptr(d_rec), d_rec.numel() * 4,
+                      _lib.ptr(d_radii), _lib.ptr(d_colors), _lib.ptr(d_campos), _lib.ptr(d), st)
+            ptrs.append(d.data_ptr())
+            caps.append(-1)
+            keep.append(d)
+        else:
+            cap = int((radii > 0).sum())
+            s = torch.empty(sparse_floats(n, n), device=gpu)
+            _lib.call("gsplat_exchange_sparse_plan", n, _lib.ptr(d_radii), _lib.ptr(s), st)
+            _lib.call("gsplat_exchange_pack_sparse", n, _lib.ptr(d_rec), d_rec.numel() * 4,
+                      _lib.ptr(d_radii), _lib.ptr(d_colors), _lib.ptr(d_campos), _lib.ptr(s),
+                      cap, st)
+            ptrs.append(s.data_ptr())
+            caps.append(cap)
+            keep.append(s)
+    K = num_sh_bases(degree)
+    tab = ctypes.cast((ctypes.c_void_p * R)(*ptrs), ctypes.c_void_p)
+    cap_arr = ctypes.cast((ctypes.c_longlong * R)(*caps), ctypes.c_void_p)
+    # the rest slab starts one row into its storage when n is a multiple of 4 (unaligned path)
+    off = 1 if n % 4 == 0 else 0
+    base_dc = torch.randn(n, 3, generator=g).to(gpu)
+    store = torch.randn(n + off, max(K - 1, 1), 3, generator=g).to(gpu)
+    base_rest = store[off:off + n, :K - 1]
+
+    def params():
+        dc = torch.nn.Parameter(base_dc.clone())
+        buf = store.clone()
+        rest = torch.nn.Parameter(buf[off:off + n, :K - 1])
+        return dc, rest, buf
+    # reference: table kernel -> gradients -> FusedAdam.step (gsplat_adam_step)
+    dc_a, rest_a, buf_a = params()
+    opt_a = FusedAdam([{"params": [dc_a], "lr": 2.5e-3, "name": "features_dc"},
+                       {"params": [rest_a], "lr": 1.25e-4, "name": "features_rest"}], eps=1e-15)
+    dc_b, rest_b, buf_b = params()
+    opt_b = FusedAdam([{"params": [dc_b], "lr": 2.5e-3, "name": "features_dc"},
+                       {"params": [rest_b], "lr": 1.25e-4, "name": "features_rest"}], eps=1e-15)
+    if K > 1:
+        assert rest_a.is_contiguous() and (rest_a.data_ptr() % 16 != 0) == (off == 1)
+    for it in range(2):
+        v_dc = torch.empty(n, 3, device=gpu)
+        v_rest = torch.empty(n, K - 1, 3, device=gpu)
+        _lib.call("gsplat_compute_sh_backward_view_table", n, degree, dtu, R, _lib.ptr(means),
+                  tab, cap_arr, _lib.ptr(v_dc), _lib.ptr(v_rest) if K > 1 else None, st)
+        dc_a.grad = v_dc
+        rest_a.grad = v_rest if K > 1 else None
+        opt_a.step()
+        (pd, md, vd, lr_d), (pr, mr, vr, lr_r) = opt_b.next_step_groups([dc_b, rest_b])
+        P = _lib.ptr
+        _lib.call("gsplat_compute_sh_backward_view_table_adam", n, degree, dtu, R, P(means), tab,
+                  cap_arr, P(pd), P(pr) if K > 1 else None, P(md), P(vd),
+                  P(mr) if K > 1 else None, P(vr) if K > 1 else None, lr_d, lr_r,
+                  opt_b.step_count + 1, opt_b.betas[0], opt_b.betas[1], opt_b.eps, st)
+        opt_b.step_count += 1
+        torch.cuda.synchronize()
+        assert torch.equal(dc_a, dc_b), it
+        assert torch.equal(opt_a.state[dc_a]["exp_avg"], opt_b.state[dc_b]["exp_avg"])
+        assert torch.equal(opt_a.state[dc_a]["exp_avg_sq"], opt_b.state[dc_b]["exp_avg_sq"])
+        if K > 1:
+            assert torch.equal(rest_a, rest_b), it
+            assert torch.equal(opt_a.state[rest_a]["exp_avg"], opt_b.state[rest_b]["exp_avg"])
+            assert torch.equal(opt_a.state[rest_a]["exp_avg_sq"],
+                               opt_b.state[rest_b]["exp_avg_sq"])
+            # the rows around the slab were not touched
+            assert torch.equal(buf_b[:off], store[:off]) and torch.equal(buf_b[off + n:],
+                                                                           store[off + n:])
+        assert not torch.equal(dc_b, base_dc)

@@ -69,6 +69,8 @@ def _worker(rank, world, port, out_dir, mode, sparse="auto", per_rank=1):
             else sum(kinds.values()) == per_rank
     for _ in range(2):
         t.step(cams, gts, background=bg)
+    # (the SH-feature Adam ran inside the table kernel unless GSPLAT_MI355X_FUSE_SH_ADAM=0)
+    assert t.fuse_sh_adam == (os.environ.get("GSPLAT_MI355X_FUSE_SH_ADAM", "1") != "0")
     np.save(os.path.join(out_dir, f"params{rank}.npy"),
             torch.cat([p.detach().reshape(-1) for p in t.params]).cpu().numpy())
     torch.cuda.synchronize()
@@ -111,6 +113,30 @@ def test_fused_ranks_sum_the_view_gradients(tmp_path, mode, world, sparse, per_r
         _lib.set_deterministic(prev)
     assert np.abs(ref).max() > 0
     assert_close("summed view gradients", g0, ref, atol=1e-6, rtol=1e-4)
+
+
+@pytest.mark.parametrize("sparse,per_rank", [("on", 1), ("off", 2)])
+def test_fused_sh_adam_equals_unfused(tmp_path, sparse, per_rank):
+    """The N > 1 train step with the SH-feature Adam inside the multi-view table kernel
+    (GSPLAT_MI355X_FUSE_SH_ADAM, default on) leaves every parameter bit-identical to the same
+    steps with the table kernel's gradients and the multi-tensor Adam (deterministic raster
+    backward, so both runs sum the same gradients)."""
+    world = 2
+    out = {}
+    os.environ["GSPLAT_MI355X_DETERMINISTIC"] = "1"
+    try:
+        for fuse in ("1", "0"):
+            d = tmp_path / f"fuse{fuse}"
+            d.mkdir()
+            os.environ["GSPLAT_MI355X_FUSE_SH_ADAM"] = fuse
+            mp.spawn(_worker, args=(world, _free_port(), str(d), "sh_views", sparse, per_rank),
+                     nprocs=world, join=True)
+            out[fuse] = [np.load(d / f"params{r}.npy") for r in range(world)]
+    finally:
+        os.environ.pop("GSPLAT_MI355X_DETERMINISTIC", None)
+        os.environ.pop("GSPLAT_MI355X_FUSE_SH_ADAM", None)
+    for r in range(world):
+        np.testing.assert_array_equal(out["1"][r], out["0"][r])
 
 
 def _garden_worker(rank, world, port, out_dir):
