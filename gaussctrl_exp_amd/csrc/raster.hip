@@ -1207,10 +1207,14 @@ __device__ __forceinline__ void bwd3p_item(BWD3P_PARAMS, int ctile, int part, in
             if (__any(anyv[u]) && slot >= 0)
               det_add(det + ((size_t)gid[u] * REC_FIELDS + slot) * DET_LIMBS, v[u]);
           } else if constexpr (ATOMICS) {
+#ifdef GS_ABLATE_NO_ATOMIC  // attribution build (tools/attr_bwd.sh): the total consumed, no add
+            asm volatile("" ::"v"(v[u]), "v"(gid[u]));
+#else
             // 32-bit element offset (the entry points reject N >= 2^27): the atomic takes the
             // SGPR base + a VGPR offset, no 64-bit address arithmetic per iteration
             if (anyw[u] && slot >= 0)
               atomicAdd(rec + (uint32_t)(gid[u] * REC + slot), v[u]);
+#endif
           } else {
             asm volatile("" ::"v"(v[u]));
           }

@@ -50,10 +50,6 @@ LAST_BINNING = {"mode": None}
 # (gsplat_fused_preprocess_forward_part); GSPLAT_MI355X_SPLIT_COLOURS=0: one kernel (A/B runs)
 SPLIT_COLOURS = os.environ.get("GSPLAT_MI355X_SPLIT_COLOURS", "1") != "0"
 SPLIT_COLOURS_MIN_TILES = 3584  # (the blend kernels' small-frame threshold as well)
-# the colour part's start: 0 beside the projection part (both from the step's start), 1 behind
-# it (the side stream waits for the projection part: the projection runs alone, the colours
-# beside the depth sort only) -- GSPLAT_MI355X_COLOURS_AFTER_PROJ, A/B runs
-COLOURS_AFTER_PROJ = os.environ.get("GSPLAT_MI355X_COLOURS_AFTER_PROJ", "0") != "0"
 _SIDE = {}
 
 
@@ -115,14 +111,11 @@ class _FusedRender(Function):
                           P(radii), P(conics), P(nth), P(colors), P(opac), P(ws1), ws1.numel(),
                           st)
                 return
-            if not COLOURS_AFTER_PROJ:
-                colours_part()
+            colours_part()
             _lib.call("gsplat_fused_preprocess_forward_part", 1, n, K, int(degrees_to_use),
                       P(means), P(scales), P(quats), P(opacities), P(features_dc),
                       P(features_rest), *cam_args, P(xys), P(depths), P(radii), P(conics),
                       P(nth), None, P(opac), P(ws1), ws1.numel(), st)
-            if COLOURS_AFTER_PROJ:
-                colours_part()
 
         def colours_part():
             cur = torch.cuda.current_stream(dev)

@@ -1,22 +1,24 @@
 #!/bin/bash
-# Attribution of the shipped strip backward's time: the same kernel with
-# staging only (flag 64), without the record atomics (flag 1), and with the nine-value
-# reduce-scatter replaced by a lane-local sum (a separate library built with
-# -DGS_ABLATE_NO_REDUCE).  Interleaved timing by tools/exp_bwd.py on each CONFIGS entry.
+# Attribution of the shipped strip backward's reduce + atomic tail: the record
+# backward timed in the bench step (tools/gpu_iter.sh AB over GSPLAT_MI355X_LIB) with three
+# ablation builds of the library beside the shipped one:
+#   ablib/libNR.so  -DGS_ABLATE_NO_REDUCE  the nine-value reduce-scatter replaced by a lane-local sum
+#   ablib/libNA.so  -DGS_ABLATE_NO_ATOMIC  the record atomics replaced by an empty consumer
+#   ablib/libNN.so  both
+# (results are wrong numerically in the ablations; only their time is read).  The libraries
+# go to ablib/ (git-ignored, not gpurun-ignored: they travel to the box).
 # Build (here, CPU): tools/attr_bwd.sh build ; run (GPU box): tools/attr_bwd.sh run
 set -e
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 if [ "$1" = build ]; then
-  mkdir -p ab/nored
-  make -s -C gaussctrl_exp_amd/csrc BUILD=../../ab/nored OUT=../../ab/libNR.so \
-    COMMON="--offload-arch=gfx950 -O3 -fPIC -std=c++17 -Wall -Wno-unused-function -DGS_ABLATE_NO_REDUCE" \
-    ../../ab/libNR.so
+  for v in "NR:-DGS_ABLATE_NO_REDUCE" "NA:-DGS_ABLATE_NO_ATOMIC" "NN:-DGS_ABLATE_NO_REDUCE -DGS_ABLATE_NO_ATOMIC"; do
+    name=${v%%:*}; defs=${v#*:}
+    mkdir -p ablib/$name
+    make -s -C gaussctrl_exp_amd/csrc BUILD=../../ablib/$name OUT=../../ablib/lib$name.so \
+      EXTRA="$defs" ../../ablib/lib$name.so
+  done
   exit 0
 fi
-mkdir -p gpurun_out
-for cfg in ${CONFIGS:-headline c4 c3}; do
-  echo "== $cfg shipped library: flags 0 (shipped), 64 (staging only), 1 (no atomics)"
-  CFG=$cfg FLAGS=0,64,1 timeout -k 10 240 python3 tools/exp_bwd.py
-  echo "== $cfg no-reduce library: flags 0, 1 (no reduce, no atomics)"
-  CFG=$cfg FLAGS=0,1 GSPLAT_MI355X_LIB=ab/libNR.so timeout -k 10 240 python3 tools/exp_bwd.py
-done
+ROUND=${ROUND:-attr} CFGS="${CFGS:-headline c4}" REPS=${REPS:-2} \
+  AB="ship:X=0 NR:GSPLAT_MI355X_LIB=ablib/libNR.so NA:GSPLAT_MI355X_LIB=ablib/libNA.so NN:GSPLAT_MI355X_LIB=ablib/libNN.so" \
+  bash tools/gpu_iter.sh
