@@ -185,6 +185,8 @@ def train_part(entry: str) -> str:
         return "adam"
     if entry == "gsplat_fused_preprocess_backward_adam":
         return "geometry backward + adam (one kernel)"
+    if entry == "gsplat_compute_sh_backward_view_table_adam":
+        return "exchange: multi-view SH backward + SH-feature Adam (one kernel)"
     if entry.startswith("gsplat_exchange") or "views" in entry or "view_table" in entry:
         return "exchange (pack / multi-view SH backward)"
     return "render"
@@ -574,6 +576,12 @@ def train_roofline(train_step, steps, barrier, ab, N, I, P, T, K, world, trainer
         calls = tm.summary()
         step_ms_events = ev0.elapsed_time(ev1) / steps
     params = (11 + 3 * K) * N
+    if world > 1:  # the multi-view table kernels over R = world x views records (12 B each)
+        R = world * getattr(trainer.sh_exchange, "views_per_step", 1) if trainer.sh_exchange \
+            else world
+        ab = dict(ab)
+        ab["gsplat_compute_sh_backward_view_table"] = (12 + 12 * R + 12 * K) * N
+        ab["gsplat_compute_sh_backward_view_table_adam"] = (12 + 12 * R + 24 * 3 * K) * N
     render_bytes = (388 + 24 * K) * N + 124 * I + 44 * P + 8 * T
     parts_ms, parts_bytes = {}, {"render": render_bytes}
     for name, (ncalls, mean_ms, tot_ms) in calls.items():
@@ -709,6 +717,15 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
+    # the same step through the unchanged caller's torch glue (gc_model.py as it runs on the
+    # gsplat drop-in), for comparison -- measured first: its steps also bring the GPU to its
+    # steady-state clocks before the headline's warm-up and timed steps (with the driver's 5
+    # warm-up steps alone the first timed steps still ran below them: 1,549 vs 1,606 Mpix/s on
+    # one box, profiles/r06_warmup_sensitivity.txt)
+    for _ in range(max(args.warmup // 2, 1)):
+        step(caller)
+    caller_value = world * H * W * args.steps / timed(lambda: step(caller), args.steps) / 1e6
+
     for _ in range(args.warmup):
         step()
     barrier()
@@ -749,12 +766,6 @@ def main():
         exch["exposed_ms"] = round(ms_per_step - exch["t_compute_only_ms"], 4)
         exch["hidden_frac"] = round(1 - exch["exposed_ms"] / comm, 3) if comm > 0 else None
         exch["backend"] = backend
-    # the same step through the unchanged caller's torch glue (gc_model.py as it runs on the
-    # gsplat drop-in), for comparison
-    for _ in range(max(args.warmup // 2, 1)):
-        step(caller)
-    caller_value = world * H * W * args.steps / timed(lambda: step(caller), args.steps) / 1e6
-
     # per-entry-point device time (HIP events on the launch stream), same step, K steps
     with timing.timed_calls() as tm:
         barrier()

@@ -128,6 +128,7 @@ HOOK_SIGNATURES = {
     "gsplat_debug_depth_key_range": (_I, [_I]),
     "gsplat_debug_wave_log": (_I, [_P]),
     "gsplat_debug_tile_sort_gen": (_I64, [_I64]),
+    "gsplat_debug_emit_counts": (_I, [_I]),
 }
 
 ABI_VERSION = 17  # include/gsplat_mi355x.h GSPLAT_MI355X_ABI_VERSION

@@ -276,11 +276,14 @@ __global__ __launch_bounds__(TPB) void rts_count_kernel(const K *__restrict__ ke
 // Reduce-then-scan pass, part 2: one workgroup per digit scans that digit's row of tile
 // counts in place (exclusive) and writes the row total; the pass kernel turns the <= 256 row
 // totals into digit bases itself.  (One launch instead of a three-kernel device scan.)
+// tmaj: the counts are tile-major (counts[t * R + d], R = 1 << width: the tile sort's first pass
+// as the emission accumulates it, EmitCounts) -- scanned in place in that layout.
 __global__ __launch_bounds__(1024) void rts_rowscan_kernel(uint32_t *__restrict__ counts,
                                                            long long nblocks,
                                                            uint32_t *__restrict__ rowtot,
                                                            KeyRange kr = {}, int pass = 0,
-                                                           int shift = 0, int width = 8) {
+                                                           int shift = 0, int width = 8,
+                                                           bool tmaj = false) {
   __shared__ uint32_t lds[16];
   __shared__ uint32_t kand, kor;
   if (pass > 0 && digit_constant(kr.fin, shift, width)) return;  // identity pass
@@ -306,14 +309,15 @@ __global__ __launch_bounds__(1024) void rts_rowscan_kernel(uint32_t *__restrict_
     }
     return;
   }
-  uint32_t *row = counts + (size_t)blockIdx.x * nblocks;
+  const size_t es = tmaj ? ((size_t)1 << width) : 1;  // element stride of the row
+  uint32_t *row = counts + (tmaj ? (size_t)blockIdx.x : (size_t)blockIdx.x * nblocks);
   uint32_t running = 0;
   for (long long c0 = 0; c0 < nblocks; c0 += 1024) {
     const long long i = c0 + threadIdx.x;
-    const uint32_t v = i < nblocks ? row[i] : 0u;
+    const uint32_t v = i < nblocks ? row[i * es] : 0u;
     uint32_t tot;
     const uint32_t ex = block_exclusive_scan<1024>(v, tot, lds);
-    if (i < nblocks) row[i] = running + ex;
+    if (i < nblocks) row[i * es] = running + ex;
     running += tot;
   }
   if (threadIdx.x == 0) rowtot[blockIdx.x] = running;
@@ -507,7 +511,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     bool drop = false, const uint32_t *__restrict__ n_dev = nullptr,
     uint32_t *__restrict__ n_out = nullptr, const uint32_t *__restrict__ kfin = nullptr,
     DevIO io = {}, int q = 0, int *__restrict__ tbins = nullptr, uint32_t tcount = 0,
-    GenSrc gen = {}) {
+    GenSrc gen = {}, bool tmaj = false) {
   if (io.fin) {  // device-selected buffers (DevIO): a constant digit moves nothing
     if (q > 0 && digit_constant(io.fin, shift, width)) return;
     const K *ki;
@@ -560,7 +564,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
   // order, so the scans below wait for them alone
   constexpr bool SMALL = ITEMS <= 8;
   const uint32_t hval = rowtot[min(tid, R - 1)];
-  const uint32_t oval = SMALL ? offs[(size_t)min(tid, R - 1) * nblocks + t] : 0u;
+  // (tmaj: tile-major offsets, rts_rowscan_kernel)
+  const size_t oidx = tmaj ? (size_t)t * R + min(tid, R - 1) : (size_t)min(tid, R - 1) * nblocks + t;
+  const uint32_t oval = SMALL ? offs[oidx] : 0u;
   if constexpr (GEN) {  // the generated first pass of the tile sort (gen_rounds)
     // (the marks live in the tile's pair buffer, which is written only after the barriers of
     // the digit-base scan below)
@@ -656,7 +662,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
       }
     }
     // large tiles: the row offset's load overlaps the scatter
-    if (!SMALL && tid < R) sm.gofs[tid] = sm.hscan[tid] + offs[(size_t)tid * nblocks + t] - lo;
+    if (!SMALL && tid < R) sm.gofs[tid] = sm.hscan[tid] + offs[oidx] - lo;
   }
   __syncthreads();
   const long long cnt = sm.tile_n;
@@ -709,13 +715,16 @@ uint32_t *sort_kept_word(void *ws) { return (uint32_t *)ws + 1; }
 // n_dev_all (no drop): the key count on the device, n the launch length (a capacity): every pass
 // sorts *n_dev_all keys, none when it exceeds n.  tbins (the tile sort, no KeyRange): the last
 // pass also accumulates the tile table of keys < tcount (os_pass_kernel; ts_decode_kernel).
+// first_tmaj (with first_counts_ready): pass 0's counts are tile-major (the emission's,
+// EmitCounts) -- its row scan and pass kernel read them in that layout.
 template <typename K>
 int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t *vout,
                      long long n, int begin_bit, int end_bit, void *ws, hipStream_t st,
                      bool first_counts_ready = false, bool drop = false,
                      uint32_t assume_const = 0, int32_t *range_out = nullptr,
                      const uint32_t *n_dev_all = nullptr, int *tbins = nullptr,
-                     uint32_t tcount = 0, const GenSrc *gen = nullptr) {
+                     uint32_t tcount = 0, const GenSrc *gen = nullptr,
+                     bool first_tmaj = false) {
   if (n <= 0) return 0;
   const SortPlan p = sort_plan(n, begin_bit, end_bit);
   if (p.passes == 0) {
@@ -768,9 +777,10 @@ int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t
     else
       hipLaunchKernelGGL((rts_count_kernel<K, 4>), dim3((unsigned)p.nblocks), dim3(TPB), 0, st,
                          kin, n, sh, p.width, p.nblocks, counts, drop && q == 0, ndev, kr, q, io);
+    const bool tmaj = q == 0 && first_tmaj;
     hipLaunchKernelGGL(rts_rowscan_kernel,
                        dim3((unsigned)p.radix + (q == 0 && kr.blk ? 1u : 0u)), dim3(1024), 0,
-                       st, counts, p.nblocks, rowtot, kr, q, sh, p.width);
+                       st, counts, p.nblocks, rowtot, kr, q, sh, p.width, tmaj);
 #define OS_PASS(Wd, It)                                                                     \
   do {                                                                                      \
     if (q == 0 && gen)                                                                      \
@@ -783,7 +793,7 @@ int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t
                          0, st, kin, vin, ko, vo, n, sh, p.width, rowtot, counts, p.nblocks, \
                          drop && q == 0, ndev, drop && q == 0 ? kept : nullptr,            \
                          q > 0 && !io.fin ? kr.fin : nullptr, io, q,                        \
-                         last ? tbins : nullptr, tcount);                                   \
+                         last ? tbins : nullptr, tcount, GenSrc{}, tmaj);                   \
   } while (0)
 #define OS_PASS_W(Wd)                                                                       \
   do {                                                                                      \
@@ -916,8 +926,14 @@ __global__ __launch_bounds__(TPB) void gather_counts_kernel(int n, const uint32_
                                                             uint2 *__restrict__ box,
                                                             int *__restrict__ num_visible,
                                                             uint32_t *__restrict__ partial,
-                                                            uint32_t *__restrict__ vflag = nullptr) {
+                                                            uint32_t *__restrict__ vflag = nullptr,
+                                                            uint32_t *__restrict__ zero = nullptr,
+                                                            long long zero_words = 0) {
   __shared__ uint32_t lds[TPB / 64];
+  // (zero: the emission's first-pass count matrix, EmitCounts -- cleared before the emission)
+  for (long long i = (long long)blockIdx.x * TPB + threadIdx.x; zero && i < zero_words;
+       i += (long long)gridDim.x * TPB)
+    zero[i] = 0u;
   const long long base = (long long)blockIdx.x * SC_TILE;
   uint32_t sum = 0;
   const long long nv = min((long long)n, (long long)*kept);
@@ -1003,6 +1019,18 @@ __device__ __forceinline__ int slot_owner(int *mk, uint32_t j0, uint32_t rel, bo
 // i_host (the speculative binning; after a count phase that found I already, the same value).
 // i_dev > cap (an overflow, or a depth-key digit the sort assumed constant that varied: i_dev =
 // ~0): nothing is emitted.
+// EmitCounts (the speculative binning, round 6): the tile sort's first digit counts come from
+// the emission itself instead of a count launch over the emitted pairs.  A workgroup's slots
+// are one contiguous range, so they fall in a few consecutive sort tiles (2^shift slots each):
+// the first EC_LT of them are counted in an LDS histogram and added once per (tile, digit) at
+// the end, the rest (a very large allotment) straight into the tile-major matrix
+// counts[tile * 2^width + digit], which gather_counts_kernel zeroed.
+constexpr int EC_LT = 4;
+struct EmitCounts {
+  uint32_t *counts = nullptr;  // null: the sort counts its first pass itself
+  int shift = 0, width = 0;
+  long long nblocks = 0;
+};
 __global__ __launch_bounds__(TPB) void ts_emit_kernel(int n, int nb,
                                                       const uint32_t *__restrict__ order,
                                                       const uint32_t *__restrict__ cnt,
@@ -1018,13 +1046,18 @@ __global__ __launch_bounds__(TPB) void ts_emit_kernel(int n, int nb,
                                                       uint32_t *__restrict__ gstart = nullptr,
                                                       uint32_t *__restrict__ gseg = nullptr,
                                                       const uint32_t *__restrict__ vflag = nullptr,
-                                                      const uint32_t *__restrict__ pscan = nullptr) {
+                                                      const uint32_t *__restrict__ pscan = nullptr,
+                                                      const EmitCounts ec = {}) {
   __shared__ uint32_t lds[TPB / 64];
   __shared__ int marks[TPB];
+  __shared__ uint32_t ech[EC_LT * 256];
   for (long long i = (long long)blockIdx.x * TPB + threadIdx.x; i < 2LL * tbx * tby;
        i += (long long)gridDim.x * TPB)
     tile_bins[i] = 0;
   const int tid = threadIdx.x, lane = tid & 63;
+  const uint32_t ecr = 1u << ec.width;  // (the first pass's digits)
+  if (ec.counts)
+    for (int i = tid; i < EC_LT * (int)ecr; i += TPB) ech[i] = 0u;  // (barriers below)
   const int t = (int)(blockIdx.x / SC_ITEMS), rr = (int)(blockIdx.x % SC_ITEMS);
   const long long b0 = (long long)t * SC_TILE;
   const long long p = b0 + (long long)rr * TPB + tid;
@@ -1074,7 +1107,9 @@ __global__ __launch_bounds__(TPB) void ts_emit_kernel(int n, int nb,
     return;
   }
   const long long p0 = p - lane;
-  if (p0 >= n) return;  // wave-uniform (no barrier below)
+  if (p0 >= n) {  // wave-uniform
+    if (!ec.counts) return;  // (no barrier below)
+  } else {
   const bool in = p < n;
   uint32_t g = 0;
   uint2 bx = make_uint2(0u, 0u);
@@ -1111,6 +1146,22 @@ __global__ __launch_bounds__(TPB) void ts_emit_kernel(int n, int nb,
     if (j < total) {
       tkeys[base + j] = tile;
       tvals[base + j] = qg;
+      if (ec.counts) {  // the first sort pass's digit count (EmitCounts)
+        const uint32_t st = (base + j) >> ec.shift, lt = st - (bpre >> ec.shift);
+        const uint32_t d = tile & (ecr - 1u);
+        if (lt < (uint32_t)EC_LT) atomicAdd(&ech[lt * ecr + d], 1u);
+        else atomicAdd(&ec.counts[(size_t)st * ecr + d], 1u);
+      }
+    }
+  }
+  }
+  if (ec.counts) {  // every wave of the workgroup reaches this barrier
+    __syncthreads();
+    const uint32_t ft = bpre >> ec.shift;
+    for (int i = tid; i < EC_LT * (int)ecr; i += TPB) {
+      const uint32_t v = ech[i];
+      const long long st = (long long)ft + (i >> ec.width);
+      if (v && st < ec.nblocks) atomicAdd(&ec.counts[(size_t)st * ecr + (i & (ecr - 1u))], v);
     }
   }
 }
@@ -1951,11 +2002,36 @@ TsWs carve_ts(void *base, long long cap, long long T, int n) {
 // capacity).  HEAD: the emission (I published to p1.dcount and i_host); TAIL: the
 // sort and the tile table over m pairs: with n_dev, *n_dev of them (I on the device; m = cap,
 // the launch length), else exactly m = I.
+// ec_zeroed: the caller cleared ec_matrix(ws2, cap, T, n) (gather_counts_kernel), so the
+// emission counts the sort's first pass (EmitCounts; one call: HEAD and TAIL, m = cap, not the
+// generated first pass).
+struct EcMatrix {
+  uint32_t *counts;
+  long long words;
+  SortPlan plan;
+};
+EcMatrix ec_matrix(void *ws2, long long cap, long long T, int n) {
+  const TsWs w = carve_ts(ws2, cap, T, n);
+  const SortPlan sp = sort_plan(cap, 0, bits_for(T));
+  return EcMatrix{rts_tile_counts(w.rs), sp.nblocks * sp.radix, sp};
+}
+bool ec_applies(long long cap) { return cap > 0 && cap < g_gen_min_i; }
+
 void ts_launch(int n, const Phase1 &p1, void *ws2, int32_t *ids, int32_t *tile_bins, int tbx,
                int tby, long long cap, long long m, int32_t *i_host, uint32_t assume,
-               bool head, bool tail, const uint32_t *n_dev, hipStream_t st) {
+               bool head, bool tail, const uint32_t *n_dev, hipStream_t st,
+               bool ec_zeroed = false) {
   const long long T = (long long)tbx * tby;
   const TsWs w = carve_ts(ws2, cap, T, n);
+  EmitCounts ec{};
+  const bool use_ec = ec_zeroed && head && tail && m == cap && !w.gstart;
+  if (use_ec) {
+    const EcMatrix em = ec_matrix(ws2, cap, T, n);
+    ec.counts = em.counts;
+    ec.width = em.plan.width;
+    ec.shift = em.plan.items == 16 ? 12 : 10;  // (TPB * items slots per sort tile)
+    ec.nblocks = em.plan.nblocks;
+  }
   const int nb = (int)cdiv(n, SC_TILE);
   // every emission workgroup sums the block sums before it: quadratic in N, so from
   // TS_SCAN_NB blocks (1M Gaussians) one workgroup scans them first (c5: ~95M L2 reads saved)
@@ -1970,12 +2046,12 @@ void ts_launch(int n, const Phase1 &p1, void *ws2, int32_t *ids, int32_t *tile_b
                        tbx, tby, w.ka, w.va, tile_bins, p1.dcount, i_host,
                        (uint32_t)(cap > 0xFFFFFFFELL ? 0xFFFFFFFELL : cap),
                        assume ? sort_kept_word(p1.rs_ws) + 1 : nullptr, assume, w.gstart, w.gseg,
-                       p1.dcount + 2, scan ? w.pscan : nullptr);
+                       p1.dcount + 2, scan ? w.pscan : nullptr, ec);
   if (!tail || m <= 0) return;
   GenSrc g{w.gstart, p1.cnt, p1.order, w.gseg, p1.box, tbx, tby, (long long)n};
   radix_sort_pairs<uint32_t>(w.ka, w.va, w.kb, w.vb, nullptr, (uint32_t *)ids, m, 0, bits_for(T),
-                             w.rs, st, false, false, 0u, nullptr, n_dev, tile_bins, (uint32_t)T,
-                             w.gstart ? &g : nullptr);
+                             w.rs, st, use_ec, false, 0u, nullptr, n_dev, tile_bins, (uint32_t)T,
+                             w.gstart ? &g : nullptr, use_ec);
   hipLaunchKernelGGL(ts_decode_kernel, dim3(cdiv(T, TPB)), dim3(TPB), 0, st, T, m, tile_bins,
                      n_dev);
 }
@@ -1987,6 +2063,13 @@ void ts_launch(int n, const Phase1 &p1, void *ws2, int32_t *ids, int32_t *tile_b
 // workgroup, so real scenes lose (c3 bear, 300k, max list 7,984: 0.365 vs 0.144 ms; headline
 // 1M: 0.287 vs 0.243); the cut is on N, which the count phase must know before I exists.
 int g_bin_scheme = -1;
+// the emission counts the tile sort's first pass (speculative binning; gsplat_debug_emit_counts;
+// -DGS_NO_EMIT_COUNTS: an A/B build with the count launch)
+#ifdef GS_NO_EMIT_COUNTS
+bool g_emit_counts = false;
+#else
+bool g_emit_counts = true;
+#endif
 bool use_bucket(long long n, long long T) {
   if (T + 1 > BK_MAX_BUCKETS) return false;
   return g_bin_scheme < 0 ? n <= (1LL << 17) : g_bin_scheme == 1;
@@ -2018,6 +2101,14 @@ extern "C" int gsplat_debug_depth_key_range(int on) {
   return prev;
 }
 
+// The speculative binning's first tile-sort pass counted by the emission (1, shipped) or by its
+// own count launch (0); < 0 leaves it.  Returns the previous setting.
+extern "C" int gsplat_debug_emit_counts(int on) {
+  const int prev = g_emit_counts ? 1 : 0;
+  if (on >= 0) g_emit_counts = on != 0;
+  return prev;
+}
+
 extern "C" int gsplat_debug_binning_scheme(int scheme) {
   const int prev = g_bin_scheme;
   if (scheme >= -1 && scheme <= 1) g_bin_scheme = scheme;
@@ -2044,7 +2135,8 @@ static int bin_count_impl(int num_points, const float *xys, const float *depths,
                           int tile_bounds_y, int32_t *d_counts, void *workspace1,
                           size_t workspace1_bytes, bool keyed, void *stream,
                           uint32_t assume_const = 0, bool range_out = false,
-                          bool no_scan = false) {
+                          bool no_scan = false, uint32_t *zero = nullptr,
+                          long long zero_words = 0) {
   hipStream_t st = (hipStream_t)stream;
   const long long T = (long long)tile_bounds_x * tile_bounds_y;
   if (num_points < 0 || tile_bounds_x <= 0 || tile_bounds_y <= 0 || tile_bounds_x > 65535 ||
@@ -2113,7 +2205,7 @@ static int bin_count_impl(int num_points, const float *xys, const float *depths,
   const uint32_t *kept = sort_kept_word(p.rs_ws);
   uint32_t *partial = rts_tile_counts(p.rs_ws);  // the sort is done with its tile counts
   hipLaunchKernelGGL(gather_counts_kernel, dim3(nb), dim3(TPB), 0, st, n, p.order, kept, p.rec,
-                     p.cnt, p.box, d_counts, partial, p.dcount + 2);
+                     p.cnt, p.box, d_counts, partial, p.dcount + 2, zero, zero_words);
   // (the speculative binning: I from ts_emit_kernel)
   if (no_scan) return check_launch("bin_count");
   // I = the sum of the block sums, which stay as they are: the emission (ts_emit_kernel)
@@ -2192,13 +2284,18 @@ extern "C" int gsplat_bin_speculative(int num_points, int64_t capacity, int tile
               workspace2_bytes, p1.bytes, need2);
     return 1;
   }
+  // the emission counts the tile sort's first pass (EmitCounts): its matrix is cleared by the
+  // count phase's gather kernel
+  const bool ec = g_emit_counts && ec_applies(capacity);
+  const EcMatrix em = ec_matrix(workspace2, capacity, T, num_points);
   if (bin_count_impl(num_points, nullptr, nullptr, nullptr, nullptr, tile_bounds_x,
                      tile_bounds_y, d_counts, workspace1, workspace1_bytes, true, stream,
-                     assume_const, true, true))
+                     assume_const, true, true, ec ? em.counts : nullptr, ec ? em.words : 0))
     return 1;
   const uint32_t assume = use_key_range(num_points) ? assume_const : 0u;
   ts_launch(num_points, p1, workspace2, gaussian_ids_sorted, tile_bins, tile_bounds_x,
-            tile_bounds_y, capacity, capacity, d_counts + 1, assume, true, true, p1.dcount, st);
+            tile_bounds_y, capacity, capacity, d_counts + 1, assume, true, true, p1.dcount, st,
+            ec);
   return check_launch("bin_speculative");
 }
 

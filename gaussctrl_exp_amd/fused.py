@@ -117,17 +117,23 @@ class _FusedRender(Function):
                       P(features_rest), *cam_args, P(xys), P(depths), P(radii), P(conics),
                       P(nth), None, P(opac), P(ws1), ws1.numel(), st)
 
+        joined = [True]  # the step's stream has waited for the latest colour part
+
         def colours_part():
             cur = torch.cuda.current_stream(dev)
             side = _side_stream(dev)
             side.wait_stream(cur)
+            joined[0] = False
             _lib.call("gsplat_fused_preprocess_forward_part", 2, n, K, int(degrees_to_use),
                       P(means), None, None, None, P(features_dc), P(features_rest), *cam_args,
                       None, None, None, None, None, P(colors), None, None, 0, side.cuda_stream)
 
         def join_colours():
-            if split_colours:
+            # once per colour part: a second cross-stream wait (the blend joins, then the end of
+            # the forward would again) costs the device a barrier packet for nothing
+            if split_colours and not joined[0]:
                 torch.cuda.current_stream(dev).wait_stream(_side_stream(dev))
+                joined[0] = True
         # every output and scratch buffer of the forward is allocated before the first launch,
         # so the preprocess, the binning and the blend go out back to back (the host's work
         # between them left the GPU idle: ~24 us before the blend at c3)

@@ -578,14 +578,17 @@ int gsplat_debug_raster_variant_is_default(void);
  *   shipped), always (2) -- or rank as any pass (0).
  * gsplat_debug_binning_scheme: -1 by size (shipped: tile buckets + per-tile LDS sorts for
  *   scenes of <= 131,072 Gaussians on frames up to 16,447 tiles, else the depth sort + stable
- *   tile sort), 0 depth sort + tile sort, 1 tile buckets, 2 depth sort + region binning (A/B).
+ *   tile sort), 0 depth sort + tile sort, 1 tile buckets.
  *   Must not change between a gsplat_bin_count and its gsplat_bin_emit.
  * gsplat_debug_tile_sort_gen: the tile sort's first pass is generated from the depth-ordered
  *   allotments instead of emitted and re-read from capacities of min_i intersections (shipped
- *   2^24); < 0 only queries.  Must not change between a workspace-size query and its use. */
+ *   2^24); < 0 only queries.  Must not change between a workspace-size query and its use.
+ * gsplat_debug_emit_counts: gsplat_bin_speculative's tile sort takes its first digit counts
+ *   from the emission (1, shipped) or from a count launch over the emitted pairs (0). */
 int gsplat_debug_depth_key_range(int on);
 int gsplat_debug_binning_scheme(int scheme);
 long long gsplat_debug_tile_sort_gen(long long min_i);
+int gsplat_debug_emit_counts(int on);
 /* Profiling hook: the backward blend kernels record per wave {start, end (s_memrealtime,
  * 100 MHz), HW_ID, XCC_ID, work slot} as [waves][5] uint64 into the device buffer (NULL
  * disables); the buffer needs 5 entries per launched wave. */

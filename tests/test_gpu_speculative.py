@@ -82,6 +82,54 @@ def test_speculative_binning_equals_sync(gpu, n, W, H, cap_scale):
     assert R._EMIT_CAP[key] == R.emit_capacity(I)
 
 
+@pytest.mark.parametrize("n,W,H,scale,big,cap_scale", [
+    (200_000, 640, 480, 0.03, 0, 1.125),      # 1,024-slot sort tiles
+    (200_000, 640, 480, 0.03, 512, 1.125),    # + 512 frame-sized Gaussians at one depth
+    (700_000, 1080, 1080, 0.02, 300, 1.125),  # > 4M intersections: 4,096-slot sort tiles
+    (700_000, 1080, 1080, 0.02, 300, 0.5),    # overflow: nothing counted, table all-zero
+])
+def test_emission_counted_first_pass(gpu, hooks, n, W, H, scale, big, cap_scale):
+    """The speculative binning's tile sort with its first digit counts accumulated by the
+    emission (EmitCounts: LDS histograms of each workgroup's first EC_LT sort tiles, the rest
+    straight into the tile-major matrix) equals the same binning with the first pass counted by
+    its own launch, and the synchronous binning, bit for bit.  `big` Gaussians as large as the
+    frame, all at the same depth, sit next to each other in depth order: their workgroups' slot
+    ranges span hundreds of sort tiles, so most of their counts take the global path."""
+    sc = synthetic_scene(n, 3, seed=13, scale_lo=0.004, scale_hi=scale)
+    if big:
+        sc.scales.data[:big] = float(np.log(0.9))  # radius ~ the frame: every tile
+        sc.means.data[:big] = 0.0  # one depth, centred (the camera looks down -z from z = 4)
+    xys, depths, radii, nth, ws1, cam = _keyed(gpu, sc, synthetic_camera(W, H))
+    I, ids, bins = R.bin_gaussians(xys, depths, radii, nth, H, W, keyed_workspace=_fresh_ws(ws1))
+    assert I > 0
+    T = ((W + 15) // 16) * ((H + 15) // 16)
+    if big:
+        assert int((nth[:big] == T).sum()) > big // 2  # (most cover the whole frame)
+    # the two sort-tile plans, both below the generated first pass (2^24)
+    assert (I < (4 << 20)) if n == 200_000 else ((4 << 20) <= I < (1 << 24))
+    key = (gpu, n, (W + 15) // 16, (H + 15) // 16)
+    got = {}
+    for on in (1, 0):
+        prev = hooks.gsplat_debug_emit_counts(on)
+        try:
+            R._EMIT_CAP[key] = max(1, int(I * cap_scale))
+            spec = R.bin_gaussians_speculative(xys, depths, radii, nth, H, W,
+                                               keyed_workspace=_fresh_ws(ws1))
+            ok = spec.finish()
+            assert spec.num_intersects == I
+            if not ok:
+                assert cap_scale < 1 and int(spec.tile_bins.abs().sum()) == 0
+                continue
+            got[on] = (spec.ids[:I].cpu().numpy(), spec.tile_bins.cpu().numpy())
+        finally:
+            hooks.gsplat_debug_emit_counts(prev)
+    if cap_scale < 1:
+        return
+    for on in (1, 0):
+        np.testing.assert_array_equal(got[on][0], ids.cpu().numpy())
+        np.testing.assert_array_equal(got[on][1], bins.cpu().numpy())
+
+
 @pytest.mark.parametrize("case", ["plain", "overflow", "range"])
 def test_split_speculative_binning(gpu, case):
     """The speculative binning as two calls (the count phase, a callback, then

@@ -35,3 +35,27 @@ def test_entry_uses_the_step_instantiation(monkeypatch):
     # an entry with two kernels takes one instantiation of each
     kern["void gs::split_grads_kernel"] = {"insts_valu": 5.0, "dispatches": 52}
     assert bench.pmc_insts_valu("gsplat_rasterize_backward", "headline") == 105.0
+
+
+def test_entry_pattern_parts_select_the_adam_instantiation(monkeypatch):
+    """'&'-separated pattern parts must all match: the in-backward Adam entry takes the
+    <K, true> fused backward, the plain one the <K, false> one, even when the other is
+    dispatched more often."""
+    kern = {
+        "void gs::fused_bwd_kernel<16, false>": {"fetch_kb": 1.0, "write_kb": 0.0, "dispatches": 80},
+        "void gs::fused_bwd_kernel<16, true>": {"fetch_kb": 7.0, "write_kb": 0.0, "dispatches": 7},
+    }
+    monkeypatch.setattr(bench, "_pmc_kernels", lambda config: kern)
+    monkeypatch.setattr(bench, "_pmc_entry", lambda entry, config: None)
+    # (streaming kernels: FETCH_SIZE x 2, MI355X_MICROARCH.md)
+    assert bench.pmc_traffic("gsplat_fused_preprocess_backward", "headline") == 2 * 1024
+    assert bench.pmc_traffic("gsplat_fused_preprocess_backward_adam", "headline") == 14 * 1024
+
+
+def test_train_parts():
+    assert bench.train_part("gsplat_l1_ssim_forward") == "loss"
+    assert bench.train_part("gsplat_adam_step") == "adam"
+    assert bench.train_part("gsplat_compute_sh_backward_view_table_adam").startswith("exchange")
+    assert bench.train_part("gsplat_exchange_pack_sparse").startswith("exchange")
+    assert bench.train_part("gsplat_bin_speculative") == "render"
+    assert bench.train_part("gsplat_fused_preprocess_backward_adam").startswith("geometry")
