@@ -290,27 +290,20 @@ __global__ __launch_bounds__(sh_threads(K)) void fused_fwd_proj_kernel(FusedFwdA
     fused_fwd_body<K, false, 1>(a, pp, nullptr, g0, cnt);
 }
 
-// The colour part walks the blocks grid-stride: launched with a bounded grid (sh_part_grid) it
-// occupies a fraction of the chip beside the projection part and the depth sort, which are on
-// the step's critical path, instead of competing with them for every CU.
 template <int K>
 __global__ __launch_bounds__(sh_threads(K)) void fused_fwd_sh_kernel(FusedFwdArgs a,
                                                                      ProjParams pp) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int THR = sh_threads(K);
-  const long long nblk = ((long long)a.n + THR - 1) / THR;
-  for (long long b = blockIdx.x; b < nblk; b += gridDim.x) {
-    const long long g0 = b * THR;
-    const int cnt = (int)min((long long)THR, (long long)a.n - g0);
-    const bool aligned =
-        K == 1 || ((((uintptr_t)(a.features_rest + g0 * (K - 1) * 3)) & 15) == 0 &&
-                   (THR * (K - 1) * 3) % 4 == 0);
-    if (b != blockIdx.x) __syncthreads();  // (the previous block's LDS slab reads are done)
-    if (cnt == THR && aligned)
-      fused_fwd_body<K, true, 2>(a, pp, smem, g0, cnt);
-    else
-      fused_fwd_body<K, false, 2>(a, pp, smem, g0, cnt);
-  }
+  const long long g0 = (long long)blockIdx.x * THR;
+  const int cnt = (int)min((long long)THR, (long long)a.n - g0);
+  const bool aligned =
+      K == 1 || ((((uintptr_t)(a.features_rest + g0 * (K - 1) * 3)) & 15) == 0 &&
+                 (THR * (K - 1) * 3) % 4 == 0);
+  if (cnt == THR && aligned)
+    fused_fwd_body<K, true, 2>(a, pp, smem, g0, cnt);
+  else
+    fused_fwd_body<K, false, 2>(a, pp, smem, g0, cnt);
 }
 
 template <int K, bool ADAM = false>
@@ -521,21 +514,6 @@ int degree_of(int K) { return K == 1 ? 0 : K == 4 ? 1 : K == 9 ? 2 : K == 16 ? 3
 
 using namespace gs;
 
-// Workgroups of the colour part (gsplat_fused_preprocess_forward_part 2; 0: one per block).
-// The test library reads GSPLAT_MI355X_SH_PART_WGS (A/B runs).
-constexpr int SH_PART_WGS = 0;
-static int sh_part_grid() {
-#ifdef GSPLAT_TEST_HOOKS
-  static const int v = [] {
-    const char *e = getenv("GSPLAT_MI355X_SH_PART_WGS");
-    return e ? atoi(e) : SH_PART_WGS;
-  }();
-  return v;
-#else
-  return SH_PART_WGS;
-#endif
-}
-
 #define FUSED_DISPATCH(KERNEL, ARGS)                                                       \
   switch (K) {                                                                            \
     case 1: hipLaunchKernelGGL(KERNEL<1>, grid, dim3(thr), smem, st, ARGS, pp); break;    \
@@ -586,9 +564,6 @@ static int fused_forward_impl(
     const size_t smem = 0;  // (no features_rest slab)
     FUSED_DISPATCH(fused_fwd_proj_kernel, args);
   } else if (part == 2) {
-    const long long blocks = cdiv(num_points, thr);
-    const int cap = sh_part_grid();
-    const dim3 grid((unsigned)(cap > 0 && blocks > cap ? cap : blocks));
     FUSED_DISPATCH(fused_fwd_sh_kernel, args);
   } else {
     FUSED_DISPATCH(fused_fwd_kernel, args);
