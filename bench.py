@@ -582,6 +582,13 @@ def train_roofline(train_step, steps, barrier, ab, N, I, P, T, K, world, trainer
         ab = dict(ab)
         ab["gsplat_compute_sh_backward_view_table"] = (12 + 12 * R + 12 * K) * N
         ab["gsplat_compute_sh_backward_view_table_adam"] = (12 + 12 * R + 24 * 3 * K) * N
+        # the record packing: gradient record (64 B), radii and colours in, 12 B out (dense; a
+        # sparse record writes only the visible rows); the visibility plan reads radii
+        ab["gsplat_exchange_pack_colors"] = 92 * N
+        ab["gsplat_exchange_pack_sparse"] = 92 * N
+        ab["gsplat_exchange_sparse_plan"] = 4 * N
+        if getattr(trainer, "fuse_sh_adam", False):  # the standalone Adam: geometry groups only
+            ab["gsplat_adam_step"] = 28 * 11 * N
     render_bytes = (388 + 24 * K) * N + 124 * I + 44 * P + 8 * T
     parts_ms, parts_bytes = {}, {"render": render_bytes}
     for name, (ncalls, mean_ms, tot_ms) in calls.items():

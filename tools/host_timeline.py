@@ -71,8 +71,17 @@ _lib.check_device = wrap_small(_lib.check_device, "_lib.check_device")
 _lib.stream = wrap_small(_lib.stream, "_lib.stream")
 
 
+FWD_ONLY = cfg in bench.FORWARD_ONLY or os.environ.get("FWD_ONLY") == "1"
+
+
 def step():
     t0 = clock()
+    if FWD_ONLY:  # bench.py's forward-only step (c2): the fused render without gradients
+        with torch.no_grad():
+            from gaussctrl_exp_amd.fused import render_fused
+            render_fused(scene, cam, deg, bg)
+        events.append(("phase forward", t0, clock()))
+        return t0
     tr.zero_grad()
     t1 = clock()
     out = tr._render(cam, bg, gt=gt)
