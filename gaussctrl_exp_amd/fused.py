@@ -81,14 +81,18 @@ class _FusedRender(Function):
         H, W = int(H), int(W)
         tbx, tby = (W + BLOCK_X - 1) // BLOCK_X, (H + BLOCK_Y - 1) // BLOCK_Y
         f32 = dict(device=dev, dtype=torch.float32)
-        xys = torch.empty((n, 2), **f32)
-        depths = torch.empty((n,), **f32)
-        radii = torch.empty((n,), device=dev, dtype=torch.int32)
-        conics = torch.empty((n, 3), **f32)
-        nth = torch.empty((n,), device=dev, dtype=torch.int32)
-        colors = torch.empty((n, 3), **f32)
-        opac = torch.empty((n,), **f32)
-        need_grad = any(ctx.needs_input_grad[:6])
+        # the seven per-Gaussian outputs carved from one allocation (12 words per Gaussian: one
+        # caching-allocator call instead of seven, ~1.5 us of host time each -- the small frames'
+        # step is bound by the host path)
+        slab = torch.empty((12 * n,), **f32)
+        xys, depths = slab[:2 * n].view(n, 2), slab[2 * n:3 * n]
+        radii = slab[3 * n:4 * n].view(torch.int32)
+        conics = slab[4 * n:7 * n].view(n, 3)
+        nth = slab[7 * n:8 * n].view(torch.int32)
+        colors, opac = slab[8 * n:11 * n].view(n, 3), slab[11 * n:12 * n]
+        # (needs_input_grad ignores the caller's grad mode: a render under torch.no_grad -- the
+        # forward-only bench step, an eval render -- keeps no records, plan or walk table)
+        need_grad = any(ctx.needs_input_grad[:6]) and aux.get("grad_mode", True)
         rec = torch.empty((max(_lib.query("gsplat_grad_records_bytes", n), 1),), device=dev,
                           dtype=torch.uint8) if need_grad else None
         P, st = _lib.ptr, _lib.stream(dev)
@@ -146,9 +150,11 @@ class _FusedRender(Function):
             l1_part = torch.empty((_lib.query("gsplat_rasterize_l1_partials_bytes", tbx, tby)
                                    // 4,), **f32)
             loss = torch.empty((), **f32)
-        out_img = torch.empty((H, W, 3), **f32)
-        final_Ts = torch.empty((H, W), **f32)
-        final_idx = torch.empty((H, W), device=dev, dtype=torch.int32)
+        # (image, final T and final index: one allocation too)
+        pix = torch.empty((5 * H * W,), **f32)
+        out_img = pix[:3 * H * W].view(H, W, 3)
+        final_Ts = pix[3 * H * W:4 * H * W].view(H, W)
+        final_idx = pix[4 * H * W:].view(torch.int32).view(H, W)
 
         def plan_for(layout_i):
             """(chunk, plan buffer) of the list-split plan laid out for layout_i intersections."""
@@ -494,7 +500,9 @@ def render_fused(scene, cam: GCCamera, sh_degree_to_use: int, background: Tensor
     gradients into the parameters' .grad as autograd's backward would (TrainStep's step): of
     d loss / d loss = 1 (or its argument) with l1_gt, else of its argument, d image [H,W,3]
     (loss.fused_splatfacto_loss_and_grad)."""
-    aux = {}
+    # the caller's grad mode (inside Function.forward it is always off); the direct step runs
+    # its forward under no_grad but does take a backward
+    aux = {"grad_mode": bool(direct) or torch.is_grad_enabled()}
     args = [_contig_f32(scene.means), _contig_f32(scene.scales), _contig_f32(scene.quats),
             _contig_f32(scene.opacities), _contig_f32(scene.features_dc),
             _contig_f32(scene.features_rest), _contig_f32(cam.viewmat), _contig_f32(cam.projmat),
@@ -540,6 +548,10 @@ def render_fused(scene, cam: GCCamera, sh_degree_to_use: int, background: Tensor
                         p.grad = gp
                     else:
                         p.grad += gp
+    elif not torch.is_grad_enabled():
+        # no graph is recorded anyway: the forward without Function.apply's bookkeeping (~10 us
+        # of host time; the forward-only bench step and eval renders are host-bound at c2)
+        out = _FusedRender.forward(_DirectCtx((False,) * 21), *args)
     else:
         out = _FusedRender.apply(*args)
     loss = None

@@ -381,6 +381,27 @@ def test_fused_empty_view_gives_background_and_zero_grads(gpu):
     assert all(p.grad is not None and not p.grad.any() for p in sc.params())
 
 
+@pytest.mark.parametrize("case", [CASES[0], CASES[6]])
+def test_fused_render_under_no_grad_keeps_no_backward_state(gpu, case):
+    """A render under torch.no_grad (the forward-only bench step, an eval render) gives the same
+    image and alpha bit for bit as one that keeps the backward's state, and keeps none: no
+    gradient records, no list-split plan (needs_input_grad alone ignores the grad mode)."""
+    n, W, H, deg, dtu, *_ = case
+    sc, cam = _scene_cam(case)
+    sc = sc.to(gpu).requires_grad_()
+    cam = cam.to(gpu)
+    bg = torch.tensor([0.1, 0.2, 0.3], device=gpu)
+    with torch.no_grad():
+        a = render_fused(sc, cam, dtu, bg, return_alpha=True)
+    b = render_fused(sc, cam, dtu, bg, return_alpha=True)
+    assert torch.equal(a["rgb"], b["rgb"].detach())
+    assert torch.equal(a["accumulation"], b["accumulation"].detach())
+    assert a["raster_grads"]() is None
+    (b["rgb"].sum() + b["accumulation"].sum()).backward()
+    assert all(p.grad is not None for p in sc.params())
+    assert b["raster_grads"]() is not None
+
+
 def test_fused_rejects_cpu_tensors():
     sc = synthetic_scene(10)
     with pytest.raises(RuntimeError, match="ROCm device"):
