@@ -564,9 +564,11 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
   // order, so the scans below wait for them alone
   constexpr bool SMALL = ITEMS <= 8;
   const uint32_t hval = rowtot[min(tid, R - 1)];
-  // (tmaj: tile-major offsets, rts_rowscan_kernel)
-  const size_t oidx = tmaj ? (size_t)t * R + min(tid, R - 1) : (size_t)min(tid, R - 1) * nblocks + t;
-  const uint32_t oval = SMALL ? offs[oidx] : 0u;
+  // (tmaj: tile-major offsets, rts_rowscan_kernel; the index is formed where it is used: held
+  // across the ranking it cost the 16-keys-per-thread plan two registers and a spill)
+  const uint32_t oval =
+      SMALL ? offs[tmaj ? (size_t)t * R + min(tid, R - 1) : (size_t)min(tid, R - 1) * nblocks + t]
+            : 0u;
   if constexpr (GEN) {  // the generated first pass of the tile sort (gen_rounds)
     // (the marks live in the tile's pair buffer, which is written only after the barriers of
     // the digit-base scan below)
@@ -662,7 +664,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
       }
     }
     // large tiles: the row offset's load overlaps the scatter
-    if (!SMALL && tid < R) sm.gofs[tid] = sm.hscan[tid] + offs[oidx] - lo;
+    if (!SMALL && tid < R)
+      sm.gofs[tid] = sm.hscan[tid] + offs[tmaj ? (size_t)t * R + tid : (size_t)tid * nblocks + t] - lo;
   }
   __syncthreads();
   const long long cnt = sm.tile_n;
