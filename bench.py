@@ -42,6 +42,8 @@ from gaussctrl_exp_amd.sh import num_sh_bases  # noqa: E402
 from gaussctrl_exp_amd.train import TrainStep  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
+# untimed steps before the first timed leg (clock settle, see main); reported as settle_steps
+SETTLE_STEPS = 40
 
 CONFIGS = {
     # name: (N, W, H, sh_degree, scale_lo, scale_hi, seed, real scene or None, description)
@@ -724,11 +726,16 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
+    # settle: a fixed number of untimed steps before anything is timed, so that every leg
+    # starts at the GPU's steady-state clocks -- with the driver's --steps 20 --warmup 5 and
+    # the caller leg alone in front, the headline still read 1,567-1,568 against 1,604 at
+    # steady state (profiles/r06_warmup_sensitivity.txt).  A step count, not a time, so every
+    # rank runs the same collectives at N > 1.
+    for _ in range(SETTLE_STEPS):
+        step()
+    barrier()
     # the same step through the unchanged caller's torch glue (gc_model.py as it runs on the
-    # gsplat drop-in), for comparison -- measured first: its steps also bring the GPU to its
-    # steady-state clocks before the headline's warm-up and timed steps (with the driver's 5
-    # warm-up steps alone the first timed steps still ran below them: 1,549 vs 1,606 Mpix/s on
-    # one box, profiles/r06_warmup_sensitivity.txt)
+    # gsplat drop-in), for comparison
     for _ in range(max(args.warmup // 2, 1)):
         step(caller)
     caller_value = world * H * W * args.steps / timed(lambda: step(caller), args.steps) / 1e6
@@ -903,6 +910,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "settle_steps": SETTLE_STEPS,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
             "scaling": "weak",
