@@ -1,5 +1,6 @@
 """VGPRs / SGPRs / scratch / occupancy per kernel of one HIP source, from the compiler's
-kernel-resource-usage remarks.  Usage: kernel_resources.py file.hip [name-substring ...]"""
+kernel-resource-usage remarks.  Usage: kernel_resources.py file.hip [name-substring ...]
+(KR_EXTRA: extra compiler flags, e.g. -D defines of an A/B build)"""
 import re
 import subprocess
 import sys
@@ -7,6 +8,7 @@ import sys
 src = sys.argv[1]
 pats = sys.argv[2:]
 r = subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", *(["-fno-slp-vectorize"] if "raster" in src else []),
+                    *[a for a in __import__("os").environ.get("KR_EXTRA", "").split() if a],
                     "-c", src, "-o", "/tmp/_kr.o", "-Rpass-analysis=kernel-resource-usage"],
                    capture_output=True, text=True)
 cur, rows = None, []
