@@ -276,14 +276,17 @@ __global__ __launch_bounds__(TPB) void rts_count_kernel(const K *__restrict__ ke
 // Reduce-then-scan pass, part 2: one workgroup per digit scans that digit's row of tile
 // counts in place (exclusive) and writes the row total; the pass kernel turns the <= 256 row
 // totals into digit bases itself.  (One launch instead of a three-kernel device scan.)
-// tmaj: the counts are tile-major (counts[t * R + d], R = 1 << width: the tile sort's first pass
-// as the emission accumulates it, EmitCounts) -- scanned in place in that layout.
+// tsrc: the counts come tile-major from there (tsrc[t * R + d], R = 1 << width: the tile sort's
+// first pass as the emission accumulates it, EmitCounts) and the scanned rows go digit-major
+// into counts -- the matrix lines each hold one tile's counts of 32 digits, so scanning them in
+// place would have 32 workgroups writing words of every line (0.010 vs 0.005 ms at the
+// headline); read-only, those lines are shared from L2.
 __global__ __launch_bounds__(1024) void rts_rowscan_kernel(uint32_t *__restrict__ counts,
                                                            long long nblocks,
                                                            uint32_t *__restrict__ rowtot,
                                                            KeyRange kr = {}, int pass = 0,
                                                            int shift = 0, int width = 8,
-                                                           bool tmaj = false) {
+                                                           const uint32_t *__restrict__ tsrc = nullptr) {
   __shared__ uint32_t lds[16];
   __shared__ uint32_t kand, kor;
   if (pass > 0 && digit_constant(kr.fin, shift, width)) return;  // identity pass
@@ -309,15 +312,15 @@ __global__ __launch_bounds__(1024) void rts_rowscan_kernel(uint32_t *__restrict_
     }
     return;
   }
-  const size_t es = tmaj ? ((size_t)1 << width) : 1;  // element stride of the row
-  uint32_t *row = counts + (tmaj ? (size_t)blockIdx.x : (size_t)blockIdx.x * nblocks);
+  uint32_t *row = counts + (size_t)blockIdx.x * nblocks;
+  const size_t R = (size_t)1 << width;
   uint32_t running = 0;
   for (long long c0 = 0; c0 < nblocks; c0 += 1024) {
     const long long i = c0 + threadIdx.x;
-    const uint32_t v = i < nblocks ? row[i * es] : 0u;
+    const uint32_t v = i < nblocks ? (tsrc ? tsrc[(size_t)i * R + blockIdx.x] : row[i]) : 0u;
     uint32_t tot;
     const uint32_t ex = block_exclusive_scan<1024>(v, tot, lds);
-    if (i < nblocks) row[i * es] = running + ex;
+    if (i < nblocks) row[i] = running + ex;
     running += tot;
   }
   if (threadIdx.x == 0) rowtot[blockIdx.x] = running;
@@ -511,7 +514,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     bool drop = false, const uint32_t *__restrict__ n_dev = nullptr,
     uint32_t *__restrict__ n_out = nullptr, const uint32_t *__restrict__ kfin = nullptr,
     DevIO io = {}, int q = 0, int *__restrict__ tbins = nullptr, uint32_t tcount = 0,
-    GenSrc gen = {}, bool tmaj = false) {
+    GenSrc gen = {}) {
   if (io.fin) {  // device-selected buffers (DevIO): a constant digit moves nothing
     if (q > 0 && digit_constant(io.fin, shift, width)) return;
     const K *ki;
@@ -564,11 +567,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
   // order, so the scans below wait for them alone
   constexpr bool SMALL = ITEMS <= 8;
   const uint32_t hval = rowtot[min(tid, R - 1)];
-  // (tmaj: tile-major offsets, rts_rowscan_kernel; the index is formed where it is used: held
-  // across the ranking it cost the 16-keys-per-thread plan two registers and a spill)
-  const uint32_t oval =
-      SMALL ? offs[tmaj ? (size_t)t * R + min(tid, R - 1) : (size_t)min(tid, R - 1) * nblocks + t]
-            : 0u;
+  const uint32_t oval = SMALL ? offs[(size_t)min(tid, R - 1) * nblocks + t] : 0u;
   if constexpr (GEN) {  // the generated first pass of the tile sort (gen_rounds)
     // (the marks live in the tile's pair buffer, which is written only after the barriers of
     // the digit-base scan below)
@@ -665,7 +664,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     }
     // large tiles: the row offset's load overlaps the scatter
     if (!SMALL && tid < R)
-      sm.gofs[tid] = sm.hscan[tid] + offs[tmaj ? (size_t)t * R + tid : (size_t)tid * nblocks + t] - lo;
+      sm.gofs[tid] = sm.hscan[tid] + offs[(size_t)tid * nblocks + t] - lo;
   }
   __syncthreads();
   const long long cnt = sm.tile_n;
@@ -718,8 +717,8 @@ uint32_t *sort_kept_word(void *ws) { return (uint32_t *)ws + 1; }
 // n_dev_all (no drop): the key count on the device, n the launch length (a capacity): every pass
 // sorts *n_dev_all keys, none when it exceeds n.  tbins (the tile sort, no KeyRange): the last
 // pass also accumulates the tile table of keys < tcount (os_pass_kernel; ts_decode_kernel).
-// first_tmaj (with first_counts_ready): pass 0's counts are tile-major (the emission's,
-// EmitCounts) -- its row scan and pass kernel read them in that layout.
+// first_tsrc (with first_counts_ready): pass 0's counts are tile-major there (the emission's,
+// EmitCounts, in the kb buffer the pass writes later) -- its row scan reads them from there.
 template <typename K>
 int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t *vout,
                      long long n, int begin_bit, int end_bit, void *ws, hipStream_t st,
@@ -727,7 +726,7 @@ int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t
                      uint32_t assume_const = 0, int32_t *range_out = nullptr,
                      const uint32_t *n_dev_all = nullptr, int *tbins = nullptr,
                      uint32_t tcount = 0, const GenSrc *gen = nullptr,
-                     bool first_tmaj = false) {
+                     const uint32_t *first_tsrc = nullptr) {
   if (n <= 0) return 0;
   const SortPlan p = sort_plan(n, begin_bit, end_bit);
   if (p.passes == 0) {
@@ -780,10 +779,10 @@ int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t
     else
       hipLaunchKernelGGL((rts_count_kernel<K, 4>), dim3((unsigned)p.nblocks), dim3(TPB), 0, st,
                          kin, n, sh, p.width, p.nblocks, counts, drop && q == 0, ndev, kr, q, io);
-    const bool tmaj = q == 0 && first_tmaj;
     hipLaunchKernelGGL(rts_rowscan_kernel,
                        dim3((unsigned)p.radix + (q == 0 && kr.blk ? 1u : 0u)), dim3(1024), 0,
-                       st, counts, p.nblocks, rowtot, kr, q, sh, p.width, tmaj);
+                       st, counts, p.nblocks, rowtot, kr, q, sh, p.width,
+                       q == 0 ? first_tsrc : nullptr);
 #define OS_PASS(Wd, It)                                                                     \
   do {                                                                                      \
     if (q == 0 && gen)                                                                      \
@@ -796,7 +795,7 @@ int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t
                          0, st, kin, vin, ko, vo, n, sh, p.width, rowtot, counts, p.nblocks, \
                          drop && q == 0, ndev, drop && q == 0 ? kept : nullptr,            \
                          q > 0 && !io.fin ? kr.fin : nullptr, io, q,                        \
-                         last ? tbins : nullptr, tcount, GenSrc{}, tmaj);                   \
+                         last ? tbins : nullptr, tcount, GenSrc{});                         \
   } while (0)
 #define OS_PASS_W(Wd)                                                                       \
   do {                                                                                      \
@@ -2016,9 +2015,16 @@ struct EcMatrix {
 EcMatrix ec_matrix(void *ws2, long long cap, long long T, int n) {
   const TsWs w = carve_ts(ws2, cap, T, n);
   const SortPlan sp = sort_plan(cap, 0, bits_for(T));
-  return EcMatrix{rts_tile_counts(w.rs), sp.nblocks * sp.radix, sp};
+  // (in kb: free until the first pass writes it, after its row scan has read the counts;
+  // nblocks x radix <= cap / 4 words)
+  return EcMatrix{w.kb, sp.nblocks * sp.radix, sp};
 }
-bool ec_applies(long long cap) { return cap > 0 && cap < g_gen_min_i; }
+// (the matrix must fit the kb buffer of cap words: always beyond a few thousand slots)
+bool ec_applies(long long cap, long long T) {
+  if (!(cap > 0 && cap < g_gen_min_i)) return false;
+  const SortPlan sp = sort_plan(cap, 0, bits_for(T));
+  return sp.nblocks * sp.radix <= cap;
+}
 
 void ts_launch(int n, const Phase1 &p1, void *ws2, int32_t *ids, int32_t *tile_bins, int tbx,
                int tby, long long cap, long long m, int32_t *i_host, uint32_t assume,
@@ -2054,7 +2060,7 @@ void ts_launch(int n, const Phase1 &p1, void *ws2, int32_t *ids, int32_t *tile_b
   GenSrc g{w.gstart, p1.cnt, p1.order, w.gseg, p1.box, tbx, tby, (long long)n};
   radix_sort_pairs<uint32_t>(w.ka, w.va, w.kb, w.vb, nullptr, (uint32_t *)ids, m, 0, bits_for(T),
                              w.rs, st, use_ec, false, 0u, nullptr, n_dev, tile_bins, (uint32_t)T,
-                             w.gstart ? &g : nullptr, use_ec);
+                             w.gstart ? &g : nullptr, use_ec ? ec.counts : nullptr);
   hipLaunchKernelGGL(ts_decode_kernel, dim3(cdiv(T, TPB)), dim3(TPB), 0, st, T, m, tile_bins,
                      n_dev);
 }
@@ -2289,7 +2295,7 @@ extern "C" int gsplat_bin_speculative(int num_points, int64_t capacity, int tile
   }
   // the emission counts the tile sort's first pass (EmitCounts): its matrix is cleared by the
   // count phase's gather kernel
-  const bool ec = g_emit_counts && ec_applies(capacity);
+  const bool ec = g_emit_counts && ec_applies(capacity, T);
   const EcMatrix em = ec_matrix(workspace2, capacity, T, num_points);
   if (bin_count_impl(num_points, nullptr, nullptr, nullptr, nullptr, tile_bounds_x,
                      tile_bounds_y, d_counts, workspace1, workspace1_bytes, true, stream,
