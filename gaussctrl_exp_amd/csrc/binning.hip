@@ -213,6 +213,22 @@ __device__ __forceinline__ void dev_io(const DevIO &io, int q, const K *&kin, co
   }
 }
 
+// The sort tile of workgroup b among G: workgroups are dealt round-robin to the 8 XCDs
+// (b % 8), so tile = b makes neighbouring tiles -- whose digit runs share output lines, and
+// whose counts share count-matrix lines -- write from different XCDs' L2s.  Each XCD instead
+// takes a contiguous range of tiles, in its dispatch order (a bijection on [0, G)): headline
+// 1,625 -> 1,650 Mpix/s, c4 1,153 -> 1,161 (profiles/r06_sort_xcd_ab.txt; -DGS_SORT_NO_XCD: the
+// round-robin order, for A/B builds).
+__device__ __forceinline__ uint32_t sort_tile(uint32_t b, uint32_t G) {
+#ifdef GS_SORT_NO_XCD
+  (void)G;
+  return b;
+#else
+  const uint32_t x = b & 7u, k = b >> 3, q = G >> 3, r = G & 7u;
+  return x * q + min(x, r) + k;
+#endif
+}
+
 // Reduce-then-scan pass, part 1: the digit histogram of every tile of TPB*ITEMS keys, stored
 // digit-major (counts[d * nblocks + tile]) so one exclusive scan yields every tile's global
 // offset for every digit.  drop: all-ones keys (culled Gaussians' depth keys) are not counted
@@ -231,7 +247,8 @@ __global__ __launch_bounds__(TPB) void rts_count_kernel(const K *__restrict__ ke
   const int tid = threadIdx.x;
   if (pass > 0 && digit_constant(kr.fin, shift, width)) return;  // identity pass
   if (io.fin && pass > 0) keys = (const K *)(data_in_b(io, pass) ? io.kb : io.ka);
-  const long long base = (long long)blockIdx.x * TPB * ITEMS;
+  const uint32_t tile = sort_tile(blockIdx.x, gridDim.x);
+  const long long base = (long long)tile * TPB * ITEMS;
   K k[ITEMS];
   // (the compacted length; above the launch length n: an overflowed capacity launch, which
   // sorts nothing)
@@ -266,10 +283,10 @@ __global__ __launch_bounds__(TPB) void rts_count_kernel(const K *__restrict__ ke
     }
   }
   __syncthreads();
-  if (tid < R) counts[(size_t)tid * nblocks + blockIdx.x] = h[tid];
+  if (tid < R) counts[(size_t)tid * nblocks + tile] = h[tid];
   if (pass == 0 && kr.blk && tid == 0) {
-    kr.blk[2 * blockIdx.x] = kand;
-    kr.blk[2 * blockIdx.x + 1] = kor;
+    kr.blk[2 * tile] = kand;
+    kr.blk[2 * tile + 1] = kor;
   }
 }
 
@@ -487,7 +504,8 @@ __global__ __launch_bounds__(TPB) void gen_count_kernel(GenSrc g, long long cap,
   const int R = 1 << width;
   h[tid] = 0;
   __syncthreads();
-  const long long sg = (long long)blockIdx.x * TPB * ITEMS + (long long)wave * (ITEMS * 64);
+  const uint32_t tile = sort_tile(blockIdx.x, gridDim.x);
+  const long long sg = (long long)tile * TPB * ITEMS + (long long)wave * (ITEMS * 64);
   constexpr int GG = ITEMS < GEN_G ? ITEMS : GEN_G;
   static_assert(ITEMS % GG == 0, "rounds in groups of GG");
   for (int r = 0; r < ITEMS; r += GG) {
@@ -499,7 +517,7 @@ __global__ __launch_bounds__(TPB) void gen_count_kernel(GenSrc g, long long cap,
       if (sg + (r + u) * 64 + (tid & 63) < n) atomicAdd(&h[k[u] & (uint32_t)(R - 1)], 1u);
   }
   __syncthreads();
-  if (tid < R) counts[(size_t)tid * nblocks + blockIdx.x] = h[tid];
+  if (tid < R) counts[(size_t)tid * nblocks + tile] = h[tid];
 }
 
 // Reduce-then-scan pass, part 3: each workgroup ranks its tile of TPB * ITEMS keys stably in
@@ -532,10 +550,10 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
   // keys and the workgroups past them exit at once.
   if (n_dev) {
     n = (long long)*n_dev > n ? 0 : (long long)*n_dev;  // (see rts_count_kernel)
-    if ((long long)blockIdx.x * TPB * ITEMS >= n) return;  // whole workgroup
+    if ((long long)sort_tile(blockIdx.x, gridDim.x) * TPB * ITEMS >= n) return;  // whole workgroup
   }
   if (digit_constant(kfin, shift, width)) {  // every key has the same digit: a stable copy
-    const long long b0 = (long long)blockIdx.x * TPB * ITEMS;
+    const long long b0 = (long long)sort_tile(blockIdx.x, gridDim.x) * TPB * ITEMS;
     K ck[ITEMS];
     uint32_t cv[ITEMS];
 #pragma unroll
@@ -558,7 +576,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int R = 1 << width;
   const uint32_t dmask = (uint32_t)(R - 1);
-  const uint32_t t = blockIdx.x;
+  const uint32_t t = sort_tile(blockIdx.x, gridDim.x);
   const unsigned long long lt = (1ull << lane) - 1ull;
   K key[ITEMS];
   uint32_t val[ITEMS], rank[ITEMS];
