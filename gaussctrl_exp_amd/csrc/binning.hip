@@ -37,7 +37,20 @@ constexpr int SC_ITEMS = 4;
 constexpr int SC_TILE = TPB * SC_ITEMS;  // elements per scan workgroup
 // keys per thread of a sort pass (workgroup tile = TPB * items): small sorts use short tiles
 // so that more, shorter workgroups run at once (a pass is a chain of latencies per workgroup)
-int os_items_for(long long n) { return n >= (4LL << 20) ? 16 : 4; }
+// Keys per thread of a sort pass: 16 (4,096-key tiles) from 4M keys, and for the 32-bit depth
+// sort from 448 such tiles; else 4.  Measured with the XCD-chunked tiles
+// (profiles/r06_sort_items_ab.txt): c4's 2M depth keys prefer 16 (binning 0.301 -> 0.291 ms),
+// the headline's 1M depth keys 4 (244 tiles of 16 leave CUs idle), and c3's tile sort at its
+// 1.9M capacity 4 (0.123 -> 0.126 ms with 16).  (Until round 6: 16 from 4M keys for all.)
+#ifndef GS_ITEMS16_FROM  // (A/B builds)
+#define GS_ITEMS16_FROM (4LL << 20)
+#endif
+#ifndef GS_ITEMS16_DEPTH_FROM
+#define GS_ITEMS16_DEPTH_FROM (448LL * 4096)
+#endif
+int os_items_for(long long n, int bits) {
+  return n >= (long long)(bits == 32 ? GS_ITEMS16_DEPTH_FROM : GS_ITEMS16_FROM) ? 16 : 4;
+}
 
 // ------------------------------------------------------------------ block scan helpers
 
@@ -130,7 +143,7 @@ SortPlan sort_plan(long long n, int begin_bit, int end_bit) {
   p.passes = bits <= 0 ? 0 : (bits + 7) / 8;
   p.width = p.passes ? (bits + p.passes - 1) / p.passes : 0;
   p.radix = 1 << p.width;
-  p.items = os_items_for(n);
+  p.items = os_items_for(n, bits);
   p.nblocks = n > 0 ? cdiv(n, (long long)TPB * p.items) : 0;
   return p;
 }
@@ -2004,8 +2017,10 @@ TsWs carve_ts(void *base, long long cap, long long T, int n) {
   w.va = c.take<uint32_t>(ii);
   w.kb = c.take<uint32_t>(ii);
   w.vb = c.take<uint32_t>(ii);
-  // (any sort length up to cap: the short-tile plan below 2^22 keys has more tiles)
-  const long long c1 = cap > 0 ? cap : 1, c0 = c1 < (4LL << 20) ? c1 : (4LL << 20) - 1;
+  // (any sort length up to cap: the short-tile plan below GS_ITEMS16_FROM keys -- the tile
+  // sort's keys are never 32 bits -- has more tiles)
+  const long long c1 = cap > 0 ? cap : 1,
+                  c0 = c1 < (long long)(GS_ITEMS16_FROM) ? c1 : (long long)(GS_ITEMS16_FROM) - 1;
   const size_t r0 = radix_ws_bytes(c0, 0, bits_for(T)), r1 = radix_ws_bytes(c1, 0, bits_for(T));
   w.rs = c.take<char>(r0 > r1 ? r0 : r1);
   w.pscan = c.take<uint32_t>((size_t)(cdiv(n > 0 ? n : 1, SC_TILE) + 1) * 4);
