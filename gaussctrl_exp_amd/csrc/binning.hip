@@ -311,13 +311,14 @@ __global__ __launch_bounds__(TPB) void rts_count_kernel(const K *__restrict__ ke
 // into counts -- the matrix lines each hold one tile's counts of 32 digits, so scanning them in
 // place would have 32 workgroups writing words of every line (0.010 vs 0.005 ms at the
 // headline); read-only, those lines are shared from L2.
-__global__ __launch_bounds__(1024) void rts_rowscan_kernel(uint32_t *__restrict__ counts,
-                                                           long long nblocks,
-                                                           uint32_t *__restrict__ rowtot,
-                                                           KeyRange kr = {}, int pass = 0,
-                                                           int shift = 0, int width = 8,
-                                                           const uint32_t *__restrict__ tsrc = nullptr) {
-  __shared__ uint32_t lds[16];
+constexpr int RS_NT = 256, RS_PER = 4;  // row scan: 256 threads x 4 counts per chunk
+__global__ __launch_bounds__(RS_NT) void rts_rowscan_kernel(uint32_t *__restrict__ counts,
+                                                            long long nblocks,
+                                                            uint32_t *__restrict__ rowtot,
+                                                            KeyRange kr = {}, int pass = 0,
+                                                            int shift = 0, int width = 8,
+                                                            const uint32_t *__restrict__ tsrc = nullptr) {
+  __shared__ uint32_t lds[RS_NT / 64];
   __shared__ uint32_t kand, kor;
   if (pass > 0 && digit_constant(kr.fin, shift, width)) return;  // identity pass
   if (blockIdx.x == gridDim.x - 1 && pass == 0 && kr.blk) {
@@ -325,7 +326,7 @@ __global__ __launch_bounds__(1024) void rts_rowscan_kernel(uint32_t *__restrict_
     if (threadIdx.x == 0) kand = ~0u, kor = 0u;
     __syncthreads();
     uint32_t a = ~0u, o = 0u;
-    for (long long i = threadIdx.x; i < kr.nblk; i += 1024) {
+    for (long long i = threadIdx.x; i < kr.nblk; i += RS_NT) {
       a &= kr.blk[2 * i];
       o |= kr.blk[2 * i + 1];
     }
@@ -342,15 +343,32 @@ __global__ __launch_bounds__(1024) void rts_rowscan_kernel(uint32_t *__restrict_
     }
     return;
   }
+  // chunks of RS_NT x RS_PER counts, each thread RS_PER consecutive ones (all loads of a chunk
+  // in flight together), a per-thread scan, then one block scan of the thread totals: a quarter
+  // of the waves and barriers of one count per thread of a 1,024-thread workgroup
   uint32_t *row = counts + (size_t)blockIdx.x * nblocks;
   const size_t R = (size_t)1 << width;
   uint32_t running = 0;
-  for (long long c0 = 0; c0 < nblocks; c0 += 1024) {
-    const long long i = c0 + threadIdx.x;
-    const uint32_t v = i < nblocks ? (tsrc ? tsrc[(size_t)i * R + blockIdx.x] : row[i]) : 0u;
+  for (long long c0 = 0; c0 < nblocks; c0 += RS_NT * RS_PER) {
+    const long long i0 = c0 + (long long)threadIdx.x * RS_PER;
+    uint32_t v[RS_PER];
+#pragma unroll
+    for (int u = 0; u < RS_PER; ++u) {
+      const long long i = i0 + u;
+      v[u] = i < nblocks ? (tsrc ? tsrc[(size_t)i * R + blockIdx.x] : row[i]) : 0u;
+    }
+    uint32_t s = 0;
+#pragma unroll
+    for (int u = 0; u < RS_PER; ++u) {
+      const uint32_t x = v[u];
+      v[u] = s;
+      s += x;
+    }
     uint32_t tot;
-    const uint32_t ex = block_exclusive_scan<1024>(v, tot, lds);
-    if (i < nblocks) row[i] = running + ex;
+    const uint32_t ex = block_exclusive_scan<RS_NT>(s, tot, lds);
+#pragma unroll
+    for (int u = 0; u < RS_PER; ++u)
+      if (i0 + u < nblocks) row[i0 + u] = running + ex + v[u];
     running += tot;
   }
   if (threadIdx.x == 0) rowtot[blockIdx.x] = running;
@@ -811,7 +829,7 @@ int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t
       hipLaunchKernelGGL((rts_count_kernel<K, 4>), dim3((unsigned)p.nblocks), dim3(TPB), 0, st,
                          kin, n, sh, p.width, p.nblocks, counts, drop && q == 0, ndev, kr, q, io);
     hipLaunchKernelGGL(rts_rowscan_kernel,
-                       dim3((unsigned)p.radix + (q == 0 && kr.blk ? 1u : 0u)), dim3(1024), 0,
+                       dim3((unsigned)p.radix + (q == 0 && kr.blk ? 1u : 0u)), dim3(RS_NT), 0,
                        st, counts, p.nblocks, rowtot, kr, q, sh, p.width,
                        q == 0 ? first_tsrc : nullptr);
 #define OS_PASS(Wd, It)                                                                     \
