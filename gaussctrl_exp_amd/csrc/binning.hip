@@ -311,7 +311,12 @@ __global__ __launch_bounds__(TPB) void rts_count_kernel(const K *__restrict__ ke
 // into counts -- the matrix lines each hold one tile's counts of 32 digits, so scanning them in
 // place would have 32 workgroups writing words of every line (0.010 vs 0.005 ms at the
 // headline); read-only, those lines are shared from L2.
-constexpr int RS_NT = 256, RS_PER = 4;  // row scan: 256 threads x 4 counts per chunk
+#ifndef GS_RS_NT  // (A/B builds)
+#define GS_RS_NT 256
+#endif
+// row scan: 256 threads x 4 counts per chunk (1,024 x 1 slower by 3 us, 128 x 8 by 2-4 us,
+// 64 x 16 by 4-6 us: profiles/r06_rowscan_ab.txt)
+constexpr int RS_NT = GS_RS_NT, RS_PER = 1024 / RS_NT;
 __global__ __launch_bounds__(RS_NT) void rts_rowscan_kernel(uint32_t *__restrict__ counts,
                                                             long long nblocks,
                                                             uint32_t *__restrict__ rowtot,
