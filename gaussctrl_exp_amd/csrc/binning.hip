@@ -38,18 +38,23 @@ constexpr int SC_TILE = TPB * SC_ITEMS;  // elements per scan workgroup
 // keys per thread of a sort pass (workgroup tile = TPB * items): small sorts use short tiles
 // so that more, shorter workgroups run at once (a pass is a chain of latencies per workgroup)
 // Keys per thread of a sort pass: 16 (4,096-key tiles) from 4M keys, and for the 32-bit depth
-// sort from 448 such tiles; else 4.  Measured with the XCD-chunked tiles
-// (profiles/r06_sort_items_ab.txt): c4's 2M depth keys prefer 16 (binning 0.301 -> 0.291 ms),
-// the headline's 1M depth keys 4 (244 tiles of 16 leave CUs idle), and c3's tile sort at its
-// 1.9M capacity 4 (0.123 -> 0.126 ms with 16).  (Until round 6: 16 from 4M keys for all.)
+// sort from 448 such tiles, 8 from 256 tiles of 2,048; else 4.  Measured with the XCD-chunked
+// tiles (profiles/r06_sort_items_ab.txt): c4's 2M depth keys prefer 16 (binning 0.301 -> 0.291
+// ms), the headline's 1M depth keys 8 (-2 to -4 us against 4; 244 tiles of 16 leave CUs idle),
+// and c3's tile sort at its 1.9M capacity 4 (0.123 -> 0.126 ms with 16).  (Until round 6: 16
+// from 4M keys for all, else 4.)
 #ifndef GS_ITEMS16_FROM  // (A/B builds)
 #define GS_ITEMS16_FROM (4LL << 20)
 #endif
 #ifndef GS_ITEMS16_DEPTH_FROM
 #define GS_ITEMS16_DEPTH_FROM (448LL * 4096)
 #endif
+#ifndef GS_ITEMS8_DEPTH_FROM  // (A/B builds)
+#define GS_ITEMS8_DEPTH_FROM (256LL * 2048)
+#endif
 int os_items_for(long long n, int bits) {
-  return n >= (long long)(bits == 32 ? GS_ITEMS16_DEPTH_FROM : GS_ITEMS16_FROM) ? 16 : 4;
+  if (n >= (long long)(bits == 32 ? GS_ITEMS16_DEPTH_FROM : GS_ITEMS16_FROM)) return 16;
+  return bits == 32 && n >= (long long)(GS_ITEMS8_DEPTH_FROM) ? 8 : 4;
 }
 
 // ------------------------------------------------------------------ block scan helpers
@@ -830,6 +835,9 @@ int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t
     } else if (p.items == 16)
       hipLaunchKernelGGL((rts_count_kernel<K, 16>), dim3((unsigned)p.nblocks), dim3(TPB), 0, st,
                          kin, n, sh, p.width, p.nblocks, counts, drop && q == 0, ndev, kr, q, io);
+    else if (p.items == 8)
+      hipLaunchKernelGGL((rts_count_kernel<K, 8>), dim3((unsigned)p.nblocks), dim3(TPB), 0, st,
+                         kin, n, sh, p.width, p.nblocks, counts, drop && q == 0, ndev, kr, q, io);
     else
       hipLaunchKernelGGL((rts_count_kernel<K, 4>), dim3((unsigned)p.nblocks), dim3(TPB), 0, st,
                          kin, n, sh, p.width, p.nblocks, counts, drop && q == 0, ndev, kr, q, io);
@@ -853,7 +861,9 @@ int radix_sort_pairs(K *ka, uint32_t *va, K *kb, uint32_t *vb, K *kout, uint32_t
   } while (0)
 #define OS_PASS_W(Wd)                                                                       \
   do {                                                                                      \
-    if (p.items == 16) OS_PASS(Wd, 16); else OS_PASS(Wd, 4);                                \
+    if (p.items == 16) OS_PASS(Wd, 16);                                                     \
+    else if (p.items == 8) { if constexpr (Wd == 8) OS_PASS(Wd, 8); }                       \
+    else OS_PASS(Wd, 4);                                                                    \
   } while (0)
     switch (p.width) {
       case 1: OS_PASS_W(1); break;
