@@ -119,25 +119,31 @@ __device__ __forceinline__ float reduce9(const float (&v)[9]) {
               a4 = swap32_sum(v[4], 0.f);
   // 5 -> 3 (lanes l, l^16)
   const float b0 = swap16_sum(a0, a2), b1 = swap16_sum(a1, a3), b2 = swap16_sum(a4, 0.f);
-  // 3 -> 2 (lanes l, l^8: row_ror:8)
+  // 3 -> 2 (lanes l, l^8: row_ror:8).  The odd slot b2 is summed in both lanes of the pair
+  // (one fused DPP add instead of a zero-padded pair: two selects fewer); its total then also
+  // reaches the quad 12-15, which reduce9_slot() drops as a duplicate.
   const bool h8 = lane & 8, h4 = lane & 4;
-  const float c0 = dpp_pair_sum<0x128>(b0, b1, h8), c1 = dpp_pair_sum<0x128>(b2, 0.f, h8);
+  const float c0 = dpp_pair_sum<0x128>(b0, b1, h8), c1 = b2 + dpp_f<0x128>(b2);
   // 2 -> 1 (lanes l, 7-l within eight: row_half_mirror pairs opposite bit-2 halves)
   float d = dpp_pair_sum<0x141>(c0, c1, h4);
   d += dpp_f<0xB1>(d);  // quad_perm [1,0,3,2]
   d += dpp_f<0x4E>(d);  // quad_perm [2,3,0,1]
+  // kept ahead of the caller's atomic branch: sunk into it, the last add lost its DPP fusion
+  // (a zeroed move + a DPP move + an add per iteration instead of one v_add_f32_dpp)
+  asm volatile("" : "+v"(d));
   return d;
 }
 
 // Which of the nine values reduce9() leaves in this lane: 0..8 for one lane per quad
-// (lane % 4 == 0), -1 elsewhere.  Found by reducing a probe where lane 0 holds k+1.
+// (lane % 4 == 0), -1 elsewhere.  Found by reducing a probe where lane 0 holds k+1; value
+// 4's total, also left in the quad 12-15 (see reduce9), is taken from lanes 4-7 only.
 __device__ __forceinline__ int reduce9_slot() {
   const int lane = __lane_id();
   float p[9];
 #pragma unroll
   for (int k = 0; k < 9; ++k) p[k] = lane == 0 ? (float)(k + 1) : 0.f;
   const int s = (int)reduce9(p) - 1;
-  return (lane & 3) == 0 ? s : -1;
+  return (lane & 3) == 0 && !(s == 4 && lane >= 8) ? s : -1;
 }
 
 // ---- wave64 reduce-scatter of eighteen values (two Gaussians' nine record moments) -------
