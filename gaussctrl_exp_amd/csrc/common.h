@@ -77,13 +77,13 @@ __device__ __forceinline__ float wave_sum(float v) {
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, r), 63));
 }
 
-// ---- wave64 reduce-scatter of nine values --------------------------------------------
+// ---- wave64 reduce-scatters ----------------------------------------------------------
 // Summing nine per-lane values with nine independent wave_sum()s costs ~9x18 serialised
 // DPP slots.  Instead every exchange step halves the number of live slots per lane:
 // lanes l / l^32 (v_permlane32_swap), l / l^16 (v_permlane16_swap), l / l^8 (row_ror:8),
 // l / 7-l within 8 (row_half_mirror), then a quad sum.  Afterwards each quad of lanes holds
-// the full wave sum of ONE of the nine values (27 VALU ops, no serial chain).  Which value
-// a lane holds is learned once per wave with reduce9_slot().
+// the full wave sum of ONE of the values (no serial chain).  Which value a lane holds is
+// learned once per wave with a probe (reduce_rec_slot, reduce18_slot).
 
 template <int CTRL>
 __device__ __forceinline__ float dpp_f(float v) {
@@ -111,46 +111,53 @@ __device__ __forceinline__ float dpp_pair_sum(float x, float y, bool hi) {
   return keep + dpp_f<CTRL>(send);
 }
 
-__device__ __forceinline__ float reduce9(const float (&v)[9]) {
+// ---- the record moments' reduce-scatter with the column factor applied mid-ladder --------
+// Of the nine record sums of a strip-backward iteration, three are dx times another (sx = dx
+// sa, sxx = dx sx, sxy = dx my; dx = G.x - px), and dx is constant along a lane's column
+// (lane % 16: the 16-column strips), while the ladder's first two rungs (l^32, l^16) only add
+// lanes of one column.  So only the six plain sums (sa, my, myy, r, g, b) take the l^32 rung
+// (three swaps, no zero pad); lanes 0-31 then form the three products from their column sums,
+// and the l^16 rung carries them beside the colours: 21 VALU ops against 25 for the plain
+// ladder over the nine per-lane values (the zero-padded odd value at l^32 and l^16), with the
+// products' three multiplies in both (profiles/r06_reduce9_fusion_ab.txt).  The odd slot at
+// the l^8 rung is summed in both lanes of the pair (one fused DPP add instead of two selects).
+// Afterwards lanes 0-15 hold sa / my / myy totals, 16-31 sx / sxx / sxy, 32-47 r / g / b
+// (quads 0, 2, 1 of each sixteen; quad 3 a duplicate), lanes 48-63 products of the colour
+// sums (unused).
+__device__ __forceinline__ float reduce_rec(float sa, float my, float myy, float r, float g,
+                                            float b, float dx) {
   const int lane = __lane_id();
-  // 9 slots -> 5 (lanes l, l^32)
-  const float a0 = swap32_sum(v[0], v[5]), a1 = swap32_sum(v[1], v[6]),
-              a2 = swap32_sum(v[2], v[7]), a3 = swap32_sum(v[3], v[8]),
-              a4 = swap32_sum(v[4], 0.f);
-  // 5 -> 3 (lanes l, l^16)
-  const float b0 = swap16_sum(a0, a2), b1 = swap16_sum(a1, a3), b2 = swap16_sum(a4, 0.f);
-  // 3 -> 2 (lanes l, l^8: row_ror:8).  The odd slot b2 is summed in both lanes of the pair
-  // (one fused DPP add instead of a zero-padded pair: two selects fewer); its total then also
-  // reaches the quad 12-15, which reduce9_slot() drops as a duplicate.
+  const float a0 = swap32_sum(sa, r), a1 = swap32_sum(my, g), a2 = swap32_sum(myy, b);
+  const float e0 = dx * a0, e1 = dx * e0, e2 = dx * a1;
+  const float b0 = swap16_sum(a0, e0), b1 = swap16_sum(a1, e1), b2 = swap16_sum(a2, e2);
   const bool h8 = lane & 8, h4 = lane & 4;
   const float c0 = dpp_pair_sum<0x128>(b0, b1, h8), c1 = b2 + dpp_f<0x128>(b2);
-  // 2 -> 1 (lanes l, 7-l within eight: row_half_mirror pairs opposite bit-2 halves)
   float d = dpp_pair_sum<0x141>(c0, c1, h4);
-  d += dpp_f<0xB1>(d);  // quad_perm [1,0,3,2]
-  d += dpp_f<0x4E>(d);  // quad_perm [2,3,0,1]
+  d += dpp_f<0xB1>(d);
+  d += dpp_f<0x4E>(d);
   // kept ahead of the caller's atomic branch: sunk into it, the last add lost its DPP fusion
   // (a zeroed move + a DPP move + an add per iteration instead of one v_add_f32_dpp)
   asm volatile("" : "+v"(d));
   return d;
 }
-
-// Which of the nine values reduce9() leaves in this lane: 0..8 for one lane per quad
-// (lane % 4 == 0), -1 elsewhere.  Found by reducing a probe where lane 0 holds k+1; value
-// 4's total, also left in the quad 12-15 (see reduce9), is taken from lanes 4-7 only.
-__device__ __forceinline__ int reduce9_slot() {
+// The record field reduce_rec() leaves in this lane (one lane per quad), -1 elsewhere: found
+// by reducing a probe (lane 0 holds 1..6, dx = 16 in every lane) and decoding the totals.
+__device__ __forceinline__ int reduce_rec_slot(int sx, int sy, int sxx, int sxy, int syy, int r,
+                                               int g, int b, int s0) {
   const int lane = __lane_id();
-  float p[9];
-#pragma unroll
-  for (int k = 0; k < 9; ++k) p[k] = lane == 0 ? (float)(k + 1) : 0.f;
-  const int s = (int)reduce9(p) - 1;
-  return (lane & 3) == 0 && !(s == 4 && lane >= 8) ? s : -1;
+  const bool l0 = lane == 0;
+  const float v = reduce_rec(l0 ? 1.f : 0.f, l0 ? 2.f : 0.f, l0 ? 3.f : 0.f, l0 ? 4.f : 0.f,
+                             l0 ? 5.f : 0.f, l0 ? 6.f : 0.f, 16.f);
+  if ((lane & 3) || (lane & 12) == 12 || lane >= 48) return -1;
+  return v == 1.f ? s0 : v == 2.f ? sy : v == 3.f ? syy : v == 4.f ? r : v == 5.f ? g
+       : v == 6.f ? b : v == 16.f ? sx : v == 256.f ? sxx : v == 32.f ? sxy : -1;
 }
 
 // ---- wave64 reduce-scatter of eighteen values (two Gaussians' nine record moments) -------
-// The same halving ladder as reduce9 with one more rung: l^32 (18 -> 9: lanes 0-31 keep the
+// The halving ladder (above) over eighteen values, one rung more: l^32 (18 -> 9: lanes 0-31 keep the
 // first nine, 32-63 the second nine), l^16 (9 -> 5), l^8 (5 -> 3), 7-l within eight (3 -> 2),
 // l^1 (2 -> 1), and a final sum with l^2.  Each value's total ends in two lanes (l, l^2) of
-// one quad: 47 VALU ops for 18 values (two reduce9s: 54).
+// one quad: 47 VALU ops for 18 values (two nine-value ladders: 54).
 __device__ __forceinline__ float reduce18(const float (&v)[18]) {
   const int lane = __lane_id();
   float a[9];
@@ -170,7 +177,7 @@ __device__ __forceinline__ float reduce18(const float (&v)[18]) {
 }
 
 // Which of the eighteen values reduce18() leaves in this lane: 0..17 for one lane of each
-// holding pair (lane bit 1 clear), -1 elsewhere (found by a probe, like reduce9_slot).
+// holding pair (lane bit 1 clear), -1 elsewhere (found by a probe, like reduce_rec_slot).
 __device__ __forceinline__ int reduce18_slot() {
   const int lane = __lane_id();
   float p[18];

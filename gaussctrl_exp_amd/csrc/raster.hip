@@ -22,7 +22,7 @@
 //  * Backward (shipped: raster_bwd3p_kernel<1>, 16x8 strips, 2 pixels per lane): the lane's
 //    two pixels are a float2 pair blended branch-free; per Gaussian the lane folds them into
 //    9 partial sums (sigma-gradient moments, colour and opacity terms), the wave
-//    reduce-scatters the 9 sums (common.h reduce9: permlane32/16 swaps + 3 DPP steps) so
+//    reduce-scatters the 9 sums (common.h reduce_rec: permlane32/16 swaps + 3 DPP steps) so
 //    that 9 lanes each hold one total, and ONE 9-lane atomic instruction adds them to the
 //    Gaussian's 64-byte gradient record; a split kernel then writes gsplat's
 //    v_xy / v_conic / v_colors / v_opacity tensors.
@@ -47,7 +47,7 @@ constexpr int REC = 16;  // floats per gradient record: x y a b c r g b o + pad 
 constexpr int SPLIT_WAVES = 4;  // walk-table entries per tile (list-split plan; split_work_kernel)
 
 // Deterministic backward (gsplat_set_deterministic): every wave's per-Gaussian totals
-// (reduce18 / reduce9: a fixed reduction order, so run-independent) are added as exact
+// (reduce18 / reduce_rec: a fixed reduction order, so run-independent) are added as exact
 // integers instead of fp32 atomics.  A total v is quantised to X = trunc(v * 2^80), split into
 // three signed 40-bit limbs (v ~ l0 2^-80 + l1 2^-40 + l2), and each limb is added to a 64-bit
 // integer accumulator; integer addition is associative, so the sums -- and every gradient
@@ -595,7 +595,7 @@ struct WaveRect {
 // Debug hook (gsplat_debug_wave_log): when set, the backward blend kernels record per wave
 // {start, end (s_memrealtime, 100 MHz), HW_ID, XCC_ID, work slot} into [waves][WAVE_LOG_F] u64.
 // Attribution build (-DGS_BWD_ATTR, tools/bwd_attr.sh; never the shipped library): the strip
-// backward also sums s_memtime cycles per wave -- [5] its blend rounds, [6] their reduce9 +
+// backward also sums s_memtime cycles per wave -- [5] its blend rounds, [6] their reduce_rec +
 // record-atomic tails, [7] the walk before its first round, [8] rounds << 32 | iterations,
 // [9] tail iterations, [10] its whole life -- so a wave's time splits into staging (life - blend
 // - prologue), blend math (blend - tail) and tail; the end times give the launch's imbalance.
@@ -1037,7 +1037,8 @@ __device__ __forceinline__ void bwd3p_item(BWD3P_PARAMS, int ctile, int part, in
     hi = (int)min((long long)lo + chunk, (long long)range.y);  // (no int overflow)
   }
   maxbin = wave_max_int(maxbin);
-  const int slot = reduce9_slot();
+  const int slot = reduce_rec_slot(REC_SX, REC_SY, REC_SXX, REC_SXY, REC_SYY, REC_R, REC_G, REC_B,
+                                   REC_S0);
   // canonical once, so fminf needs no per-iteration canonicalisation of the bound
   const float amax = __builtin_canonicalizef(alpha_max);
   GStage *stage = lds[__builtin_amdgcn_readfirstlane(wave)];  // (uniform: SGPR address arithmetic)
@@ -1109,7 +1110,7 @@ __device__ __forceinline__ void bwd3p_item(BWD3P_PARAMS, int ctile, int part, in
       at[3] += (1ull << 32) + (unsigned long long)n;
     }
     for (int t = 0; t < n; t += U) {
-      float parts[U][9];
+      float rsum[U][7];  // sa, my, myy, r, g, b and dx: reduce_rec's inputs
       bool anyv[U];
       int gid[U];
       unsigned long long anyw[U];
@@ -1170,17 +1171,10 @@ __device__ __forceinline__ void bwd3p_item(BWD3P_PARAMS, int ctile, int part, in
         }
         anyv[u] = any;
         anyw[u] = anym;
-        // the record moments (common.h record_grads), dx constant along the lane's column
-        const float sx = dx * sa;
-        parts[u][REC_SX] = sx;
-        parts[u][REC_SY] = my;
-        parts[u][REC_SXX] = dx * sx;
-        parts[u][REC_SXY] = dx * my;
-        parts[u][REC_SYY] = myy;
-        parts[u][REC_R] = sr;
-        parts[u][REC_G] = sg;
-        parts[u][REC_B] = sb;
-        parts[u][REC_S0] = sa;
+        // the record moments (common.h record_grads): the six lane sums and dx, which is
+        // constant along the lane's column -- reduce_rec forms sx, sxx, sxy from column sums
+        rsum[u][0] = sa; rsum[u][1] = my; rsum[u][2] = myy;
+        rsum[u][3] = sr; rsum[u][4] = sg; rsum[u][5] = sb; rsum[u][6] = dx;
       }
       unsigned long long any_all = 0;
 #pragma unroll
@@ -1192,14 +1186,16 @@ __device__ __forceinline__ void bwd3p_item(BWD3P_PARAMS, int ctile, int part, in
 #ifdef GS_ABLATE_NO_REDUCE  // attribution build (tools/attr_bwd.sh): a lane-local sum instead
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          float s = parts[u][0];
+          float s = rsum[u][0];
 #pragma unroll
-          for (int k = 1; k < 9; ++k) s += parts[u][k];
+          for (int k = 1; k < 7; ++k) s += rsum[u][k];
           v[u] = s;
         }
 #else
 #pragma unroll
-        for (int u = 0; u < U; ++u) v[u] = reduce9(parts[u]);
+        for (int u = 0; u < U; ++u)
+          v[u] = reduce_rec(rsum[u][0], rsum[u][1], rsum[u][2], rsum[u][3], rsum[u][4],
+                            rsum[u][5], rsum[u][6]);
 #endif
 #pragma unroll
         for (int u = 0; u < U; ++u) {
