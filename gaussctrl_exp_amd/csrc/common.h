@@ -168,23 +168,32 @@ __device__ __forceinline__ float reduce18(const float (&v)[18]) {
   for (int k = 0; k < 4; ++k) b[k] = swap16_sum(a[2 * k], a[2 * k + 1]);
   b[4] = swap16_sum(a[8], 0.f);
   const bool h8 = lane & 8, h4 = lane & 4, h1 = lane & 1;
+  // the odd slots at l^8 and 7-l are summed in both lanes of their pairs (one fused DPP add
+  // each instead of two selects and a zero-padded add); reduce18_slot drops the duplicates
   const float c0 = dpp_pair_sum<0x128>(b[0], b[1], h8), c1 = dpp_pair_sum<0x128>(b[2], b[3], h8),
-              c2 = dpp_pair_sum<0x128>(b[4], 0.f, h8);
-  const float d0 = dpp_pair_sum<0x141>(c0, c1, h4), d1 = dpp_pair_sum<0x141>(c2, 0.f, h4);
+              c2 = b[4] + dpp_f<0x128>(b[4]);
+  const float d0 = dpp_pair_sum<0x141>(c0, c1, h4), d1 = c2 + dpp_f<0x141>(c2);
   float e = dpp_pair_sum<0xB1>(d0, d1, h1);  // quad_perm [1,0,3,2]
   e += dpp_f<0x4E>(e);                        // quad_perm [2,3,0,1]
+  asm volatile("" : "+v"(e));  // (kept fused ahead of the caller's atomic branch)
   return e;
 }
 
 // Which of the eighteen values reduce18() leaves in this lane: 0..17 for one lane of each
-// holding pair (lane bit 1 clear), -1 elsewhere (found by a probe, like reduce_rec_slot).
+// holding pair (lane bit 1 clear, the lowest such lane), -1 elsewhere (found by a probe,
+// like reduce_rec_slot).
 __device__ __forceinline__ int reduce18_slot() {
   const int lane = __lane_id();
   float p[18];
 #pragma unroll
   for (int k = 0; k < 18; ++k) p[k] = lane == 0 ? (float)(k + 1) : 0.f;
   const int s = (int)reduce18(p) - 1;
-  return (lane & 2) == 0 ? s : -1;
+  const int cand = (lane & 2) == 0 ? s : -1;
+  // a value also left in other lanes (the odd slots' duplicates) is taken from its lowest lane
+  int keep = cand;
+  for (int k = 0; k < 64; ++k)
+    if (k < lane && cand >= 0 && __builtin_amdgcn_readlane(cand, k) == cand) keep = -1;
+  return keep;
 }
 
 // ---- per-Gaussian gradient records (the C=3 backward's accumulators) -----------------------
